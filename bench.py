@@ -1,0 +1,193 @@
+#!/usr/bin/env python3
+"""Benchmark: NITI int8 training images/sec (+ int8 MFMA TOPS) on VGG-11, batch 256 per GPU.
+
+A step is one full NITI_SGD training step of VGG-11 on a 3x32x32 int8 batch, entirely on
+device: 9 NITI_Conv_Int8 forwards (+relu/maxpool), NITI_LOSS_Grad, 9 weight gradients,
+8 input gradients, pool/relu gradients and the int8 weight update.  Data-parallel runs
+(torchrun, one process per GPU) shard nothing else: each rank trains its own 256 images
+and the exact-mode RCCL all-reduces (MAX of every range, SUM of every int32 weight
+gradient) keep all ranks bit-identical to one device running the global batch.
+
+Prints ONE JSON line on rank 0 (contract in the task statement).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "mandheling-dsp-training_amd"))
+
+PEAK_INT8_TOPS = 256 * 4 * 2048 * 2.4e9 / 1e12  # 256 CU x 4 SIMD x 2048 int8 op/clk x 2.4 GHz = 5033
+PEAK_HBM_GBS = 8000.0
+METRIC = "training images/sec + int8 MFMA TOPS, VGG-11 batch 256, 1/2/4/8 MI355X"
+
+
+def synth_weights(layers, seed):
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    out = []
+    for l in layers:
+        shape = (l["c_out"], l["c_in"], l["kh"], l["kw"])
+        fan_in = l["c_in"] * l["kh"] * l["kw"]
+        fan_out = l["c_out"] * l["kh"] * l["kw"]
+        t = rng.normal(0.0, (2.0 / (fan_in + fan_out)) ** 0.5, size=shape).astype(np.float32)
+        r = float(np.abs(t).max())  # nn/Distributions.cpp:26-51 with a fixed seed
+        out.append((np.round(t / r * 127).astype(np.int8), int(np.ceil(np.log2(r))) - 7))
+    return out
+
+
+def cpu_baseline(layers, sample, threads):
+    """The oracle's reference-structured restatement (C4, 16x4 GEMM unit, float32 accumulation,
+    batch-split threads) timed on this host for one VGG-11 step on `sample` images."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import niti_oracle as O
+    rng = np.random.default_rng(1)
+    t_total = 0.0
+    for i, l in enumerate(layers):
+        g = O.geom(sample, l["c_in"], l["h"], l["w"], l["c_out"], l["kh"], pad=l["pad"])
+        x = O.synth_x(rng, (sample, l["c_in"], l["h"], l["w"]))
+        w, _ = O.synth_w(rng, (l["c_out"], l["c_in"], l["kh"], l["kw"]))
+        dy = O.synth_dy(rng, (sample, l["c_out"], g.oh, g.ow))
+        t0 = time.perf_counter()
+        O.layer_step(g, x, w, dy, threads=threads, with_dgrad=i > 0)
+        t_total += time.perf_counter() - t0
+    return sample / t_total, t_total
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=256, help="images per GPU per step")
+    ap.add_argument("--arch", default="vgg11", choices=["vgg11", "lenet"])
+    ap.add_argument("--cpu-sample", type=int, default=32, help="images in the CPU baseline sample (0 = skip)")
+    ap.add_argument("--cpu-threads", type=int, default=4, help="reference default: MnistUtils.cpp:43")
+    ap.add_argument("--probe-layer", type=int, default=3, help="layer whose GEMM is timed for the roofline")
+    ap.add_argument("--probe-phase", type=int, default=2, help="0 fwd, 1 input grad, 2 weight grad")
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")  # control plane only; the data path is RCCL in C++
+
+    import niti_amd
+    from niti_amd.model import NitiModel
+
+    arch = niti_amd.ARCH_VGG11 if args.arch == "vgg11" else niti_amd.ARCH_LENET
+    model = NitiModel(arch, args.batch)
+    for i, (w, s) in enumerate(synth_weights(model.layers, seed=17)):
+        model.set_weight(i, w, s)
+    if world > 1:
+        uid = [NitiModel.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        model.attach_comm(uid[0], rank, world, exact=True)
+
+    l0 = model.layers[0]
+    rng = np.random.default_rng(100 + rank)
+    x = torch.from_numpy(rng.integers(-127, 128, (args.batch, l0["c_in"], l0["h"], l0["w"])).astype(np.int8)).cuda()
+    labels = torch.from_numpy(rng.integers(0, 10, args.batch).astype(np.int32)).cuda()
+
+    for _ in range(args.warmup):
+        model.train_step(x, -3, labels)
+    torch.cuda.synchronize()
+    probe_layer = args.probe_layer if args.probe_layer < len(model.layers) else len(model.layers) - 1
+    model.set_probe(probe_layer, args.probe_phase, args.steps)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        model.train_step(x, -3, labels)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    probe_ms, probe_n = model.probe_read()
+    model.set_probe(-1, 0, 0)
+
+    ms_per_step = elapsed / args.steps * 1e3
+    images = args.batch * world * args.steps
+    value = images / elapsed
+    step_ops = 2 * model.step_macs() * world
+    tops = step_ops * args.steps / elapsed / 1e12
+
+    pl = model.layers[probe_layer]
+    k_ops = 2 * args.batch * pl["oh"] * pl["ow"] * pl["c_out"] * pl["c_in"] * pl["kh"] * pl["kw"]
+    k_avg_s = probe_ms / max(probe_n, 1) / 1e3
+    achieved = k_ops / k_avg_s / 1e12 if probe_n else None
+    traffic = None
+    tfile = os.path.join(ROOT, "profiles", "traffic.json")
+    if os.path.exists(tfile):
+        try:
+            tr = json.load(open(tfile))
+            key = f"{args.arch}_b{args.batch}_L{probe_layer}_p{args.probe_phase}"
+            traffic = tr.get(key, {}).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_sample > 0:
+        v, secs = cpu_baseline(model.layers, args.cpu_sample, args.cpu_threads)
+        cpu = {"value": round(v, 3), "unit": "images/s", "cores": args.cpu_threads, "kind": "port",
+               "sample": f"{args.cpu_sample} images of the VGG-11 step (every conv: fwd + weight grad + input grad, "
+                         f"reference-structured C restatement, float32 accumulation), {secs:.1f} s"}
+
+    phase_name = {0: "forward conv", 1: "input-gradient conv", 2: "weight-gradient conv"}[args.probe_phase]
+    line = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "images/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int8",
+        "data": "synthetic (random int8 images, labels; seeded niti_normal_int8 weights)",
+        "config": {"workload": f"{args.arch.upper()} NITI int8 training step (fwd+relu+pool, loss grad, "
+                               f"weight grad, input grad, SGD), 3x32x32" if arch == niti_amd.ARCH_VGG11 else
+                               "LeNet NITI int8 training step, 1x28x28",
+                   "global_batch": args.batch * world, "per_gpu_batch": args.batch,
+                   "parallelism": f"dp{world} exact (RCCL all-reduce MAX ranges + SUM int32 grads)"},
+        "int8_mfma_tops": round(tops, 2),
+        "int8_mfma_frac_of_peak": round(tops / PEAK_INT8_TOPS, 4),
+        "roofline": {
+            "kernel": f"layer {probe_layer} {phase_name} GEMM (gemm_i8_kernel)",
+            "bound": "mfma",
+            "achieved": round(achieved, 2) if achieved else None,
+            "peak": round(PEAK_INT8_TOPS, 1),
+            "unit": "TFLOP/s",
+            "frac": round(achieved / PEAK_INT8_TOPS, 4) if achieved else None,
+            "traffic": traffic,
+            "avg_launch_us": round(k_avg_s * 1e6, 2) if probe_n else None,
+            "launches": probe_n,
+            "ops_per_launch": k_ops,
+        },
+        "cpu_baseline": cpu,
+    }
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

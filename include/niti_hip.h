@@ -1,0 +1,215 @@
+/*
+ * niti_hip.h -- C ABI of the MI355X (gfx950) NITI int8 training backend.
+ *
+ * This is the drop-in boundary for the reference's NITI int8 hot path.  The reference
+ * exposes that path through MNN's operator interface:
+ *
+ *   Creator  : CPUBackend::Creator::onCreate(inputs, outputs, const MNN::Op*, Backend*)
+ *              execution-engine/source/backend/cpu/CPUBackend.hpp:85-91, registered per
+ *              OpType by REGISTER_CPU_OP_CREATOR (:179-182)
+ *   Execution: onResize(inputs, outputs) / onExecute(inputs, outputs)
+ *              execution-engine/source/core/Execution.hpp:24-82
+ *   Errors   : MNN::ErrorCode, execution-engine/include/MNN/ErrorCode.hpp:17-30
+ *
+ * Section 1 mirrors that interface one to one (niti_create_execution / _resize / _execute /
+ * niti_destroy_execution), keyed by the same OpType values, taking the same input and output
+ * tensors in the same layouts; an MNN maintainer binds it with a ~40-line Creator (see
+ * INTEGRATION.md).  Section 2 is the native split interface the device-resident training
+ * driver and data parallelism use (accumulate -> [RCCL] -> requantise).  Section 3 is the
+ * whole-step driver (NITIInt8Train's step, execution-engine/tools/train/source/demo/
+ * MnistUtils.cpp:68-147, on device) with an optional RCCL communicator.
+ *
+ * All pointers are device (HBM) pointers unless stated; `stream` is a hipStream_t passed as
+ * void*.  No call synchronises the stream or allocates on the execute path.  Handles are not
+ * thread safe (as MNN Executions are not re-entrant).
+ */
+#ifndef NITI_HIP_H
+#define NITI_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- error codes: MNN::ErrorCode (include/MNN/ErrorCode.hpp:17-30) ------------------------ */
+enum niti_error_code {
+    NITI_NO_ERROR = 0,
+    NITI_OUT_OF_MEMORY = 1,
+    NITI_NOT_SUPPORT = 2,
+    NITI_COMPUTE_SIZE_ERROR = 3,
+    NITI_NO_EXECUTION = 4,
+    NITI_INVALID_VALUE = 5,
+    NITI_INPUT_DATA_ERROR = 10,
+    NITI_CALL_BACK_STOP = 11
+};
+
+/* ---- OpType keys (schema/default/MNN.fbs:189-233) ------------------------------------------ */
+enum niti_op_type {
+    NITI_OP_CONV_INT8 = 700,               /* NITI_CONV_Int8          -> NITI_Conv_Int8.cpp:162-310 */
+    NITI_OP_DECONV_INT8 = 701,             /* NITI_DeCONV_Int8        -> NITI_DeConv_Int8.cpp:187-332 */
+    NITI_OP_MATMUL_INT8 = 713,             /* NITI_MatMul_Int8        -> NITI_Matmul_Int8.cpp:140-231 */
+    NITI_OP_GRADIENT_CONV_INT8 = 715,      /* NITI_GradientCONV_Int8  -> NITI_GradientConv_Int8.cpp:165-298 */
+    NITI_OP_DSP_MATMUL_GRADIENT_INT8 = 818 /* NITI_DSP_MATMUL_GRADIENT_Int8 -> NITI_DSPMatmulGradientConv_Int8.cpp:105-553 */
+};
+
+/* ---- tensor formats: MNN_DATA_FORMAT (schema/default/Tensor.fbs:12-18) ---------------------- */
+enum niti_format { NITI_FORMAT_NCHW = 0, NITI_FORMAT_NHWC = 1, NITI_FORMAT_NC4HW4 = 2 };
+
+/* ---- pad modes: PadMode (schema/default/CaffeOp.fbs:3-7) ----------------------------------- */
+enum niti_pad_mode { NITI_PAD_CAFFE = 0, NITI_PAD_VALID = 1, NITI_PAD_SAME = 2 };
+
+/* A tensor as an Execution sees it: Tensor::host<T>() + batch/channel/height/width +
+ * TensorUtils::getDescribe()->dimensionFormat.  dims are the logical N, C, H, W in every
+ * format (for NHWC data, dims still list N, C, H, W).  2-D tensors use dims {rows, cols, 1, 1}. */
+typedef struct niti_tensor {
+    void* data;
+    int dims[4];
+    int format;
+} niti_tensor;
+
+/* The parts of Convolution2DCommon (schema/default/CaffeOp.fbs) the NITI ops read
+ * (NeuralNetWorkOp.cpp:1857-1880). pads = {top, left, bottom, right} when has_pads. */
+typedef struct niti_conv2d_common {
+    int kernel_x, kernel_y;
+    int stride_x, stride_y;
+    int dilate_x, dilate_y;
+    int pad_x, pad_y;
+    int has_pads;
+    int pads[4];
+    int pad_mode;
+    int input_count, output_count;
+    int group;
+} niti_conv2d_common;
+
+/* ============================ 1. Execution-shaped drop-in ============================== */
+typedef struct niti_execution* niti_execution_t;
+
+/* CPUBackend::Creator::onCreate for `op_type`.  common may be NULL for NITI_OP_MATMUL_INT8.
+ * Returns NITI_NOT_SUPPORT for an op type or parameter the backend does not implement
+ * (group != 1; dilation != 1 on a gradient op). */
+int niti_create_execution(int op_type, const niti_conv2d_common* common, niti_execution_t* out);
+
+/* Execution::onResize: shape checks + workspace (device memory owned by the handle).
+ *  NITI_OP_CONV_INT8          in {x NC4HW4 [N,Ci,H,W], w NCHW [Co,Ci,KH,KW], exp_in int8[1], wscale int8[1]}
+ *                             out{y NC4HW4 [N,Co,OH,OW], exp_out int8[1]}
+ *  NITI_OP_DECONV_INT8        in {dy' NC4HW4 [N,Co,H',W'] (already padded/dilated by the graph),
+ *                                 w^T NCHW [Ci,Co,KH,KW], exp int8[1]}     out{dx NC4HW4 [N,Ci,H,W]}
+ *  NITI_OP_GRADIENT_CONV_INT8 in {C4(x^T) NC4HW4 [Ci,N,H,W], dy^T NCHW [Co,N,OH',OW'], ...}
+ *                             out{dw NC4HW4 [Ci,Co,KH,KW]}
+ *  NITI_OP_MATMUL_INT8        in {B [M,K], A [Co,K]} (2-D, row major)      out{C [M,Co]}
+ *  NITI_OP_DSP_MATMUL_GRADIENT_INT8
+ *                             in {x NHWC [N,Ci,H,W], dy NHWC [N,Co,OH,OW]} out{dw HWIO [KH,KW,Ci,Co] as
+ *                                 dims {KH,KW,Ci,Co}}
+ * Output channel counts must be multiples of 4 on NC4HW4 outputs (the reference sizes its
+ * int32 accumulator N*C*H*W but its GEMM writes ceil(C/4)*4 channels): NITI_NOT_SUPPORT. */
+int niti_execution_resize(niti_execution_t e, const niti_tensor* inputs, int n_in, const niti_tensor* outputs,
+                          int n_out);
+/* Execution::onExecute on `stream` (asynchronous). */
+int niti_execution_execute(niti_execution_t e, const niti_tensor* inputs, int n_in, const niti_tensor* outputs,
+                           int n_out, void* stream);
+void niti_destroy_execution(niti_execution_t e);
+/* bytes of device workspace the handle holds after resize */
+size_t niti_execution_workspace_bytes(niti_execution_t e);
+
+/* ============================ 2. native split primitives ============================== */
+/* Native layouts (padded lanes zero): NHWC16 [N][H][W][round16(C)]; CHWN16 [round16(C)][H][W]
+ * [round16(N)]; OHWI16 weights [Co][KH][KW][round16(Ci)]; IHWO16 [Ci][KH][KW][round16(Co)]. */
+typedef struct niti_geom {
+    int n, c_in, h, w, c_out, kh, kw;
+    int stride_h, stride_w, pad_t, pad_l, pad_b, pad_r, dilate_h, dilate_w;
+    int oh, ow, cip, cop, np; /* filled by niti_geom_finalize */
+} niti_geom;
+
+int niti_geom_finalize(niti_geom* g);
+
+/* acc[n*oh*ow][cop] int32 = conv(x, w); *amax = max(*amax, max|acc|)   (caller zeroes amax) */
+int niti_conv_fwd_acc(const niti_geom* g, const int8_t* x_nhwc16, const int8_t* w_ohwi16, int32_t* acc,
+                      uint32_t* amax, void* stream);
+/* acc[n*h*w][cip] int32 = input gradient of the conv for dy (NHWC16) and w^T (IHWO16) */
+int niti_conv_dgrad_acc(const niti_geom* g, const int8_t* dy_nhwc16, const int8_t* wt_ihwo16, int32_t* acc,
+                        uint32_t* amax, void* stream);
+/* acc[co][kh][kw][cip] int32 = weight gradient for x (CHWN16) and dy (CHWN16) */
+int niti_conv_wgrad_acc(const niti_geom* g, const int8_t* x_chwn16, const int8_t* dy_chwn16, int32_t* acc,
+                        void* stream);
+/* acc[m][o] = sum_k B[m][k] A[o][k]; K padded to k16 with zero bytes, ld* in bytes/elements */
+int niti_matmul_acc(int m, int o, int k16, const int8_t* B, int64_t ldb, const int8_t* A, int64_t lda,
+                    int32_t* acc, int64_t ldc, uint32_t* amax, int split_k, void* stream);
+int niti_absmax_i32(const int32_t* acc, int64_t n, uint32_t* amax, void* stream);
+/* forward/deconv rule (NITI_Conv_Int8.cpp:260-307) on acc[rows][ldc]; exp_out = exp_in + wscale + inc
+ * (any exponent pointer may be NULL); relu fuses NITI_Relu_Int8; relu_mask (NHWC16) fuses
+ * NITI_ReluGrad_Int8.  out_nhwc16 [rows][ldc]. */
+int niti_requant_act(const int32_t* acc, int64_t rows, int ldc, const uint32_t* amax, const int8_t* exp_in,
+                     const int8_t* wscale, int8_t* exp_out, int relu, const int8_t* relu_mask, int8_t* out_nhwc16,
+                     void* stream);
+/* gradient rules: rule 2 = NITI_GradientConv_Int8 (bw-2), rule 3 = NITI_Matmul_Int8 (bw-3);
+ * g_out optional; w_update optional fused NITI_SGD step w <- clip(w - g, +-127). */
+int niti_requant_grad(const int32_t* acc, int64_t n, const uint32_t* amax, int rule, int8_t* g_out,
+                      int8_t* w_update, void* stream);
+/* layout helpers */
+int niti_nhwc16_to_chwn16(const int8_t* in, int n, int hw, int cp, int np, int8_t* out, void* stream);
+int niti_ohwi16_to_ihwo16(const int8_t* w, int co, int ci, int kk, int cip, int cop, int8_t* wt, void* stream);
+int niti_nchw_to_nhwc16(const int8_t* x, int n, int c, int hw, int cp, int8_t* out, void* stream);
+int niti_nchw_to_chwn16(const int8_t* x, int n, int c, int hw, int cp, int np, int8_t* out, void* stream);
+int niti_nhwc16_to_nchw(const int8_t* x, int n, int c, int hw, int cp, int8_t* out, void* stream);
+int niti_oihw_to_ohwi16(const int8_t* w, int co, int ci, int kk, int cip, int8_t* out, void* stream);
+int niti_ohwi16_to_oihw(const int8_t* w, int co, int ci, int kk, int cip, int8_t* out, void* stream);
+/* rest of the step, NHWC16 */
+int niti_maxpool(const int8_t* x, int n, int h, int w, int cp, int k, int s, int p, int8_t* y, int oh, int ow,
+                 void* stream);
+int niti_maxpool_grad(const int8_t* x, const int8_t* y, const int8_t* dy, int n, int h, int w, int cp, int k,
+                      int s, int p, int oh, int ow, int relu, int8_t* dx, void* stream);
+int niti_relu_grad(const int8_t* x, const int8_t* dy, int64_t n, int8_t* out, void* stream);
+int niti_loss_grad(const int8_t* logits, int batch, int classes, int ld, const int8_t* ascale,
+                   const int32_t* labels, int8_t* out, void* stream);
+
+/* ============================ 3. device-resident training step ========================= */
+enum niti_arch { NITI_ARCH_LENET = 1, NITI_ARCH_VGG11 = 2 };
+typedef struct niti_model* niti_model_t;
+
+/* batch = this rank's images per step.  Weights start zero; load them with
+ * niti_model_set_weight (OIHW int8, host memory) -- the reference initialises them with a
+ * time-seeded RNG (nn/Distributions.cpp:26-51), so callers supply their own. */
+int niti_model_create(int arch, int batch, niti_model_t* out);
+void niti_model_destroy(niti_model_t m);
+int niti_model_num_layers(niti_model_t m);
+/* per layer: {c_in, c_out, kh, kw, h_in, w_in, oh, ow, pad, stride, relu, pool} */
+int niti_model_layer_info(niti_model_t m, int layer, int info[12]);
+int niti_model_set_weight(niti_model_t m, int layer, const int8_t* w_oihw_host, int wscale);
+int niti_model_get_weight(niti_model_t m, int layer, int8_t* w_oihw_host);
+/* One NITI_SGD step: forward, NITI_LOSS_Grad, backward, w <- clip(w - g).
+ * x: NCHW int8 device [batch][C][H][W]; labels: int32 device [batch]; exp_in: input ascale.
+ * Asynchronous on `stream`. */
+int niti_model_train_step(niti_model_t m, const int8_t* x_nchw, int exp_in, const int32_t* labels, void* stream);
+/* Read back (synchronising `stream`): logits [batch][classes] int8 and their exponent. */
+int niti_model_get_logits(niti_model_t m, int8_t* logits_host, int* exp_out, void* stream);
+/* Per-layer debug taps (synchronising): which = 0 fwd output (post relu, pre pool, NCHW),
+ * 1 int8 weight gradient (OIHW), 2 dy of the layer (NCHW, post relu/pool grad). */
+int niti_model_get_tap(niti_model_t m, int layer, int which, int8_t* host, size_t bytes, void* stream);
+/* Algorithmic int8 MACs per step (unpadded channels; no zero-dilation taps). */
+int64_t niti_model_step_macs(niti_model_t m);
+
+/* Kernel probe: HIP events on the step's stream around one GEMM launch (layer, phase
+ * 0 = forward, 1 = input gradient, 2 = weight gradient) for up to max_launches steps;
+ * layer < 0 disables.  probe_read synchronises those events and returns the summed
+ * duration and the number of launches timed, then resets the count. */
+int niti_model_set_probe(niti_model_t m, int layer, int phase, int max_launches);
+int niti_model_probe_read(niti_model_t m, double* total_ms, int* count);
+
+/* ---- data parallel over RCCL (xGMI) ---------------------------------------------------- */
+#define NITI_UNIQUE_ID_BYTES 128
+/* rank 0 creates the id; every rank receives it out of band (torch.distributed store). */
+int niti_dp_get_unique_id(char id[NITI_UNIQUE_ID_BYTES]);
+/* Attach an RCCL communicator: exact mode all-reduces (MAX) every forward and input-gradient
+ * range and (SUM) every int32 weight-gradient accumulator, so N ranks of batch b are
+ * bit-identical to one device of batch N*b.  exact=0 keeps ranges shard-local (not parity). */
+int niti_model_attach_comm(niti_model_t m, const char id[NITI_UNIQUE_ID_BYTES], int rank, int world, int exact);
+
+/* library build info */
+const char* niti_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NITI_HIP_H */

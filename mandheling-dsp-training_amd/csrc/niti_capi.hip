@@ -1,0 +1,188 @@
+// niti_capi.hip -- extern "C" entry points of sections 1 and 2 of include/niti_hip.h.
+#include "../../include/niti_hip.h"
+#include "niti_internal.hpp"
+#include "niti_kernels.hpp"
+
+struct niti_execution {
+    niti::Execution* impl = nullptr;
+    ~niti_execution() { delete impl; }
+};
+
+namespace {
+int code(hipError_t e) {
+    if (e == hipSuccess) return NITI_NO_ERROR;
+    if (e == hipErrorOutOfMemory) return NITI_OUT_OF_MEMORY;
+    if (e == hipErrorInvalidValue) return NITI_INVALID_VALUE;
+    return NITI_NO_EXECUTION;
+}
+niti::ConvGeom to_geom(const niti_geom* g) {
+    niti::ConvGeom r{};
+    r.n = g->n;
+    r.c_in = g->c_in;
+    r.h = g->h;
+    r.w = g->w;
+    r.c_out = g->c_out;
+    r.kh = g->kh;
+    r.kw = g->kw;
+    r.sh = g->stride_h;
+    r.sw = g->stride_w;
+    r.pt = g->pad_t;
+    r.pl = g->pad_l;
+    r.pb = g->pad_b;
+    r.pr = g->pad_r;
+    r.dh = g->dilate_h;
+    r.dw = g->dilate_w;
+    r.finalize();
+    return r;
+}
+inline hipStream_t S(void* s) { return (hipStream_t)s; }
+}  // namespace
+
+extern "C" {
+
+const char* niti_version(void) { return "niti-mi355x 0.1 (gfx950, int8 MFMA v_mfma_i32_32x32x32_i8)"; }
+
+// ------------------------------------------------------------------ section 1
+int niti_create_execution(int op_type, const niti_conv2d_common* common, niti_execution_t* out) {
+    if (!out) return NITI_INVALID_VALUE;
+    int err = NITI_NO_ERROR;
+    niti::Execution* e = niti::create_execution(op_type, common, &err);
+    if (!e) return err;
+    auto* h = new niti_execution();
+    h->impl = e;
+    *out = h;
+    return NITI_NO_ERROR;
+}
+
+int niti_execution_resize(niti_execution_t e, const niti_tensor* in, int nin, const niti_tensor* out, int nout) {
+    if (!e || !in || !out) return NITI_INVALID_VALUE;
+    return e->impl->onResize(in, nin, out, nout);
+}
+
+int niti_execution_execute(niti_execution_t e, const niti_tensor* in, int nin, const niti_tensor* out, int nout,
+                           void* stream) {
+    if (!e || !in || !out) return NITI_INVALID_VALUE;
+    return e->impl->onExecute(in, nin, out, nout, S(stream));
+}
+
+void niti_destroy_execution(niti_execution_t e) { delete e; }
+
+size_t niti_execution_workspace_bytes(niti_execution_t e) { return e ? e->impl->workspaceBytes() : 0; }
+
+// ------------------------------------------------------------------ section 2
+int niti_geom_finalize(niti_geom* g) {
+    if (!g) return NITI_INVALID_VALUE;
+    niti::ConvGeom r{};
+    r.n = g->n;
+    r.c_in = g->c_in;
+    r.h = g->h;
+    r.w = g->w;
+    r.c_out = g->c_out;
+    r.kh = g->kh;
+    r.kw = g->kw;
+    r.sh = g->stride_h;
+    r.sw = g->stride_w;
+    r.pt = g->pad_t;
+    r.pl = g->pad_l;
+    r.pb = g->pad_b;
+    r.pr = g->pad_r;
+    r.dh = g->dilate_h;
+    r.dw = g->dilate_w;
+    if (!r.finalize()) return NITI_COMPUTE_SIZE_ERROR;
+    g->oh = r.oh;
+    g->ow = r.ow;
+    g->cip = r.cip;
+    g->cop = r.cop;
+    g->np = r.np;
+    return NITI_NO_ERROR;
+}
+
+int niti_conv_fwd_acc(const niti_geom* g, const int8_t* x, const int8_t* w, int32_t* acc, uint32_t* amax,
+                      void* stream) {
+    if (!g) return NITI_INVALID_VALUE;
+    return code(niti::conv_fwd_acc(to_geom(g), x, w, acc, amax, S(stream)));
+}
+
+int niti_conv_dgrad_acc(const niti_geom* g, const int8_t* dy, const int8_t* wt, int32_t* acc, uint32_t* amax,
+                        void* stream) {
+    if (!g) return NITI_INVALID_VALUE;
+    return code(niti::conv_dgrad_acc(to_geom(g), dy, wt, acc, amax, S(stream)));
+}
+
+int niti_conv_wgrad_acc(const niti_geom* g, const int8_t* x, const int8_t* dy, int32_t* acc, void* stream) {
+    if (!g) return NITI_INVALID_VALUE;
+    return code(niti::conv_wgrad_acc(to_geom(g), x, dy, acc, S(stream)));
+}
+
+int niti_matmul_acc(int m, int o, int k16, const int8_t* B, int64_t ldb, const int8_t* A, int64_t lda, int32_t* acc,
+                    int64_t ldc, uint32_t* amax, int split_k, void* stream) {
+    if (k16 % 16 || ldb % 16 || lda % 16 || ldc % 16) return NITI_INVALID_VALUE;
+    return code(niti::matmul_acc(m, o, k16, B, ldb, A, lda, acc, ldc, amax, split_k != 0, S(stream)));
+}
+
+int niti_absmax_i32(const int32_t* acc, int64_t n, uint32_t* amax, void* stream) {
+    return code(niti::absmax_i32(acc, n, amax, S(stream)));
+}
+
+int niti_requant_act(const int32_t* acc, int64_t rows, int ldc, const uint32_t* amax, const int8_t* exp_in,
+                     const int8_t* wscale, int8_t* exp_out, int relu, const int8_t* relu_mask, int8_t* out,
+                     void* stream) {
+    niti::ActRequant r;
+    r.acc = acc;
+    r.rows = rows;
+    r.ldc = ldc;
+    r.amax = amax;
+    r.exp_in = exp_in;
+    r.wscale = wscale;
+    r.exp_out = exp_out;
+    r.relu = relu;
+    r.relu_mask = relu_mask;
+    r.out_nhwc16 = out;
+    return code(niti::requant_act(r, S(stream)));
+}
+
+int niti_requant_grad(const int32_t* acc, int64_t n, const uint32_t* amax, int rule, int8_t* g_out, int8_t* w,
+                      void* stream) {
+    if (rule != 2 && rule != 3) return NITI_INVALID_VALUE;
+    return code(niti::requant_grad(acc, n, amax, rule, g_out, w, S(stream)));
+}
+
+int niti_nhwc16_to_chwn16(const int8_t* in, int n, int hw, int cp, int np, int8_t* out, void* stream) {
+    return code(niti::nhwc16_to_chwn16(in, n, hw, cp, np, out, S(stream)));
+}
+int niti_ohwi16_to_ihwo16(const int8_t* w, int co, int ci, int kk, int cip, int cop, int8_t* wt, void* stream) {
+    return code(niti::ohwi16_to_ihwo16(w, co, ci, kk, cip, cop, wt, S(stream)));
+}
+int niti_nchw_to_nhwc16(const int8_t* x, int n, int c, int hw, int cp, int8_t* out, void* stream) {
+    return code(niti::nchw_to_nhwc16(x, n, c, hw, cp, out, S(stream)));
+}
+int niti_nchw_to_chwn16(const int8_t* x, int n, int c, int hw, int cp, int np, int8_t* out, void* stream) {
+    return code(niti::nchw_to_chwn16(x, n, c, hw, cp, np, out, S(stream)));
+}
+int niti_nhwc16_to_nchw(const int8_t* x, int n, int c, int hw, int cp, int8_t* out, void* stream) {
+    return code(niti::nhwc16_to_nchw(x, n, c, hw, cp, out, S(stream)));
+}
+int niti_oihw_to_ohwi16(const int8_t* w, int co, int ci, int kk, int cip, int8_t* out, void* stream) {
+    return code(niti::oihw_to_ohwi16(w, co, ci, kk, cip, out, S(stream)));
+}
+int niti_ohwi16_to_oihw(const int8_t* w, int co, int ci, int kk, int cip, int8_t* out, void* stream) {
+    return code(niti::ohwi16_to_oihw(w, co, ci, kk, cip, out, S(stream)));
+}
+int niti_maxpool(const int8_t* x, int n, int h, int w, int cp, int k, int s, int p, int8_t* y, int oh, int ow,
+                 void* stream) {
+    return code(niti::maxpool_nhwc16(x, n, h, w, cp, k, s, p, y, oh, ow, S(stream)));
+}
+int niti_maxpool_grad(const int8_t* x, const int8_t* y, const int8_t* dy, int n, int h, int w, int cp, int k, int s,
+                      int p, int oh, int ow, int relu, int8_t* dx, void* stream) {
+    return code(niti::maxpool_relu_grad_nhwc16(x, y, dy, n, h, w, cp, k, s, p, oh, ow, relu, dx, S(stream)));
+}
+int niti_relu_grad(const int8_t* x, const int8_t* dy, int64_t n, int8_t* out, void* stream) {
+    if (n % 16) return NITI_INVALID_VALUE;
+    return code(niti::relu_grad_nhwc16(x, dy, n, out, S(stream)));
+}
+int niti_loss_grad(const int8_t* logits, int batch, int classes, int ld, const int8_t* ascale, const int32_t* labels,
+                   int8_t* out, void* stream) {
+    return code(niti::loss_grad(logits, batch, classes, ld, ascale, labels, out, S(stream)));
+}
+
+}  // extern "C"

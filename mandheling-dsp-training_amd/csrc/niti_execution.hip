@@ -1,0 +1,488 @@
+// niti_execution.hip -- MNN Execution-shaped drop-in for the NITI int8 GEMM-class ops.
+//
+// Each class mirrors one reference Execution: the same OpType key, the same inputs and
+// outputs in the same layouts (MNN C4 activations, OIHW / transposed weights, int8
+// exponent scalars), the same onResize/onExecute split and the same ErrorCode values.
+// Inside, the tensors are converted to the native layouts (niti_kernels.hpp) and the work
+// runs on the gfx950 kernels; nothing here computes on the host.
+//
+//   NITI_Conv_Int8            execution-engine/source/backend/cpu/NITI_Conv_Int8.cpp:78-322
+//   NITI_DeConv_Int8          execution-engine/source/backend/cpu/NITI_DeConv_Int8.cpp:80-345
+//   NITI_GradientConv_Int8    execution-engine/source/backend/cpu/NITI_GradientConv_Int8.cpp:81-310
+//   NITI_Matmul_Int8          execution-engine/source/backend/cpu/NITI_Matmul_Int8.cpp:63-243
+//   NITI_DSPMatmulGradientConv_Int8
+//                             execution-engine/source/backend/cpu/NITI_DSPMatmulGradientConv_Int8.cpp:105-553
+//                             (op slot: NHWC/HWIO tensors, CPU weight-gradient numerics)
+#include <math.h>
+
+#include <memory>
+#include <vector>
+
+#include "../../include/niti_hip.h"
+#include "niti_internal.hpp"
+#include "niti_kernels.hpp"
+#include "niti_map.hpp"
+
+namespace niti {
+
+// ------------------------------------------------------------------ boundary converters
+namespace {
+
+// C4(x^T): dims [Ci(batch), N(channel), H, W] -> x CHWN16 [Cip][H][W][Np]
+struct C4TransposedToChwn16 {
+    const int8_t* x;
+    int n, ci, hw, np;
+    int8_t* out;
+    __device__ void operator()(int64_t i) const {  // i over [cip][hw][np]
+        const int b = (int)(i % np);
+        const int64_t r = i / np;
+        const int64_t p = r % hw;
+        const int c = (int)(r / hw);
+        out[i] = (c < ci && b < n) ? x[(((int64_t)(b >> 2) * ci + c) * hw + p) * 4 + (b & 3)] : (int8_t)0;
+    }
+};
+
+// dy^T NCHW [Co][N][OHW] -> dy CHWN16 [Cop][OHW][Np]
+struct NchwTransposedToChwn16 {
+    const int8_t* d;
+    int n, co, hw, np;
+    int8_t* out;
+    __device__ void operator()(int64_t i) const {
+        const int b = (int)(i % np);
+        const int64_t r = i / np;
+        const int64_t p = r % hw;
+        const int c = (int)(r / hw);
+        out[i] = (c < co && b < n) ? d[((int64_t)c * n + b) * hw + p] : (int8_t)0;
+    }
+};
+
+// NHWC [N][HW][C] -> CHWN16 [Cp][HW][Np]
+struct NhwcToChwn16 {
+    const int8_t* x;
+    int n, c, hw, np;
+    int8_t* out;
+    __device__ void operator()(int64_t i) const {
+        const int b = (int)(i % np);
+        const int64_t r = i / np;
+        const int64_t p = r % hw;
+        const int ch = (int)(r / hw);
+        out[i] = (ch < c && b < n) ? x[((int64_t)b * hw + p) * c + ch] : (int8_t)0;
+    }
+};
+
+// g OHWI16 [Co][KK][Cip] -> C4 [ceil(Co/4)][Ci][KK][4] (the GradientConv output tensor,
+// batch = Ci, channel = Co)
+struct Ohwi16ToC4Grad {
+    const int8_t* g;
+    int co, ci, kk, cip;
+    int8_t* out;
+    __device__ void operator()(int64_t i) const {  // i over [ceil(co/4)][ci][kk][4]
+        const int j = (int)(i & 3);
+        const int64_t r = i >> 2;
+        const int k = (int)(r % kk);
+        const int64_t r2 = r / kk;
+        const int c = (int)(r2 % ci);
+        const int oq = (int)(r2 / ci);
+        const int o = oq * 4 + j;
+        out[i] = o < co ? g[((int64_t)o * kk + k) * cip + c] : (int8_t)0;
+    }
+};
+
+// g OHWI16 [Co][KK][Cip] -> HWIO [KK][Ci][Co]
+struct Ohwi16ToHwio {
+    const int8_t* g;
+    int co, ci, kk, cip;
+    int8_t* out;
+    __device__ void operator()(int64_t i) const {  // i over [kk][ci][co]
+        const int o = (int)(i % co);
+        const int64_t r = i / co;
+        const int c = (int)(r % ci);
+        const int k = (int)(r / ci);
+        out[i] = g[((int64_t)o * kk + k) * cip + c];
+    }
+};
+
+// [rows][ld] int8 -> [rows][cols]
+struct UnpadRows {
+    const int8_t* in;
+    int cols, ld;
+    int8_t* out;
+    __device__ void operator()(int64_t i) const {
+        const int64_t r = i / cols;
+        const int c = (int)(i - r * cols);
+        out[i] = in[r * ld + c];
+    }
+};
+
+int to_code(hipError_t e) {
+    if (e == hipSuccess) return NITI_NO_ERROR;
+    if (e == hipErrorOutOfMemory) return NITI_OUT_OF_MEMORY;
+    if (e == hipErrorInvalidValue) return NITI_INVALID_VALUE;
+    return NITI_NO_EXECUTION;
+}
+
+#define NITI_TRY(expr)                         \
+    do {                                       \
+        const int _c = to_code(expr);          \
+        if (_c != NITI_NO_ERROR) return _c;    \
+    } while (0)
+
+inline int64_t count4(const niti_tensor& t) { return (int64_t)t.dims[0] * t.dims[1] * t.dims[2] * t.dims[3]; }
+
+}  // namespace
+
+// ------------------------------------------------------------------ device workspace
+void* Workspace::alloc(size_t bytes) {
+    bytes = (bytes + 255) & ~(size_t)255;
+    void* p = nullptr;
+    if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+    ptrs.push_back(p);
+    total += bytes;
+    return p;
+}
+void Workspace::release() {
+    for (void* p : ptrs) (void)hipFree(p);
+    ptrs.clear();
+    total = 0;
+}
+
+// Convolution2DCommon -> geometry (ConvolutionCommon::convolutionPad,
+// source/core/ConvolutionCommon.cpp:550-569; output size ShapeNITI_Conv_Int8.cpp:41-76).
+bool geom_from_common(const niti_conv2d_common& c, int n, int ci, int h, int w, int co, int kh, int kw,
+                      ConvGeom* g) {
+    ConvGeom r{};
+    r.n = n;
+    r.c_in = ci;
+    r.h = h;
+    r.w = w;
+    r.c_out = co;
+    r.kh = kh;
+    r.kw = kw;
+    r.sh = c.stride_y > 0 ? c.stride_y : 1;
+    r.sw = c.stride_x > 0 ? c.stride_x : 1;
+    r.dh = c.dilate_y > 0 ? c.dilate_y : 1;
+    r.dw = c.dilate_x > 0 ? c.dilate_x : 1;
+    const int keh = r.dh * (kh - 1) + 1, kew = r.dw * (kw - 1) + 1;
+    int oh, ow;
+    if (c.pad_mode == NITI_PAD_SAME) {
+        oh = (h + r.sh - 1) / r.sh;
+        ow = (w + r.sw - 1) / r.sw;
+        const int pnh = (oh - 1) * r.sh + keh - h, pnw = (ow - 1) * r.sw + kew - w;
+        r.pt = pnh / 2;
+        r.pl = pnw / 2;
+    } else if (c.pad_mode == NITI_PAD_VALID) {
+        oh = (int)ceilf((float)(h - keh + 1) / (float)r.sh);
+        ow = (int)ceilf((float)(w - kew + 1) / (float)r.sw);
+        r.pt = c.has_pads ? c.pads[0] : c.pad_y;
+        r.pl = c.has_pads ? c.pads[1] : c.pad_x;
+    } else if (c.has_pads) {
+        oh = (h + c.pads[0] + c.pads[2] - keh) / r.sh + 1;
+        ow = (w + c.pads[1] + c.pads[3] - kew) / r.sw + 1;
+        r.pt = c.pads[0];
+        r.pl = c.pads[1];
+    } else {
+        oh = (h + 2 * c.pad_y - keh) / r.sh + 1;
+        ow = (w + 2 * c.pad_x - kew) / r.sw + 1;
+        r.pt = c.pad_y;
+        r.pl = c.pad_x;
+    }
+    r.pb = (oh - 1) * r.sh + keh - h - r.pt;
+    r.pr = (ow - 1) * r.sw + kew - w - r.pl;
+    if (!r.finalize()) return false;
+    r.oh = oh;
+    r.ow = ow;
+    *g = r;
+    return oh > 0 && ow > 0;
+}
+
+// ------------------------------------------------------------------ NITI_Conv_Int8 (700)
+class ConvInt8Execution : public Execution {
+   public:
+    explicit ConvInt8Execution(const niti_conv2d_common& c) : common_(c) {}
+    int onResize(const niti_tensor* in, int nin, const niti_tensor* out, int nout) override {
+        if (nin < 4 || nout < 2) return NITI_INVALID_VALUE;
+        const niti_tensor &x = in[0], &w = in[1], &y = out[0];
+        if (x.format != NITI_FORMAT_NC4HW4 || y.format != NITI_FORMAT_NC4HW4) return NITI_NOT_SUPPORT;
+        if (common_.group > 1) return NITI_NOT_SUPPORT;
+        if (w.dims[1] != x.dims[1]) return NITI_COMPUTE_SIZE_ERROR;
+        if (!geom_from_common(common_, x.dims[0], x.dims[1], x.dims[2], x.dims[3], w.dims[0], w.dims[2], w.dims[3], &g_))
+            return NITI_COMPUTE_SIZE_ERROR;
+        if (y.dims[0] != g_.n || y.dims[1] != g_.c_out || y.dims[2] != g_.oh || y.dims[3] != g_.ow)
+            return NITI_COMPUTE_SIZE_ERROR;
+        if (g_.c_out % 4) return NITI_NOT_SUPPORT;  // NITI_Conv_Int8.cpp:130 sizes acc N*C*H*W
+        ws_.release();
+        x16_ = (int8_t*)ws_.alloc((size_t)g_.n * g_.h * g_.w * g_.cip);
+        w16_ = (int8_t*)ws_.alloc((size_t)g_.c_out * g_.kh * g_.kw * g_.cip);
+        acc_ = (int32_t*)ws_.alloc((size_t)g_.n * g_.oh * g_.ow * g_.cop * 4);
+        amax_ = (uint32_t*)ws_.alloc(16);
+        return (x16_ && w16_ && acc_ && amax_) ? NITI_NO_ERROR : NITI_OUT_OF_MEMORY;
+    }
+    int onExecute(const niti_tensor* in, int nin, const niti_tensor* out, int nout, hipStream_t st) override {
+        if (!acc_) return NITI_NO_EXECUTION;
+        NITI_TRY(c4_to_nhwc16((const int8_t*)in[0].data, g_.n, g_.c_in, g_.h * g_.w, g_.cip, x16_, st));
+        // reorderWeight every call: weights change each step (NITI_Conv_Int8.cpp:177)
+        NITI_TRY(oihw_to_ohwi16((const int8_t*)in[1].data, g_.c_out, g_.c_in, g_.kh * g_.kw, g_.cip, w16_, st));
+        NITI_TRY(hipMemsetAsync(amax_, 0, 4, st));
+        NITI_TRY(conv_fwd_acc(g_, x16_, w16_, acc_, amax_, st));
+        ActRequant r;
+        r.acc = acc_;
+        r.rows = (int64_t)g_.n * g_.oh * g_.ow;
+        r.ldc = g_.cop;
+        r.amax = amax_;
+        r.exp_in = (const int8_t*)in[2].data;
+        r.wscale = (const int8_t*)in[3].data;
+        r.exp_out = nout > 1 ? (int8_t*)out[1].data : nullptr;
+        r.out_c4 = (int8_t*)out[0].data;
+        r.c_real = g_.c_out;
+        r.n = g_.n;
+        r.hw = g_.oh * g_.ow;
+        NITI_TRY(requant_act(r, st));
+        return NITI_NO_ERROR;
+    }
+
+   private:
+    niti_conv2d_common common_;
+    ConvGeom g_{};
+    int8_t *x16_ = nullptr, *w16_ = nullptr;
+    int32_t* acc_ = nullptr;
+    uint32_t* amax_ = nullptr;
+};
+
+// ------------------------------------------------------------------ NITI_DeConv_Int8 (701)
+// Receives dy already padded / dilated by the graph (NITI_Conv_Int8_Grad.cpp:86-120) and w^T;
+// rotates w^T by 180 degrees and runs a stride-1 conv with the forward shift rule (no exponent).
+class DeconvInt8Execution : public Execution {
+   public:
+    explicit DeconvInt8Execution(const niti_conv2d_common& c) : common_(c) {}
+    int onResize(const niti_tensor* in, int nin, const niti_tensor* out, int nout) override {
+        if (nin < 2 || nout < 1) return NITI_INVALID_VALUE;
+        const niti_tensor &d = in[0], &wt = in[1], &y = out[0];
+        if (d.format != NITI_FORMAT_NC4HW4 || y.format != NITI_FORMAT_NC4HW4) return NITI_NOT_SUPPORT;
+        if (common_.group > 1) return NITI_NOT_SUPPORT;
+        if (wt.dims[1] != d.dims[1]) return NITI_COMPUTE_SIZE_ERROR;
+        if (!geom_from_common(common_, d.dims[0], d.dims[1], d.dims[2], d.dims[3], wt.dims[0], wt.dims[2], wt.dims[3],
+                              &g_))
+            return NITI_COMPUTE_SIZE_ERROR;
+        if (y.dims[0] != g_.n || y.dims[1] != g_.c_out || y.dims[2] != g_.oh || y.dims[3] != g_.ow)
+            return NITI_COMPUTE_SIZE_ERROR;
+        if (g_.c_out % 4) return NITI_NOT_SUPPORT;
+        ws_.release();
+        x16_ = (int8_t*)ws_.alloc((size_t)g_.n * g_.h * g_.w * g_.cip);
+        w16_ = (int8_t*)ws_.alloc((size_t)g_.c_out * g_.kh * g_.kw * g_.cip);
+        acc_ = (int32_t*)ws_.alloc((size_t)g_.n * g_.oh * g_.ow * g_.cop * 4);
+        amax_ = (uint32_t*)ws_.alloc(16);
+        return (x16_ && w16_ && acc_ && amax_) ? NITI_NO_ERROR : NITI_OUT_OF_MEMORY;
+    }
+    int onExecute(const niti_tensor* in, int nin, const niti_tensor* out, int nout, hipStream_t st) override {
+        if (!acc_) return NITI_NO_EXECUTION;
+        NITI_TRY(c4_to_nhwc16((const int8_t*)in[0].data, g_.n, g_.c_in, g_.h * g_.w, g_.cip, x16_, st));
+        NITI_TRY(oihw_to_ohwi16((const int8_t*)in[1].data, g_.c_out, g_.c_in, g_.kh * g_.kw, g_.cip, w16_, st, true));
+        NITI_TRY(hipMemsetAsync(amax_, 0, 4, st));
+        NITI_TRY(conv_fwd_acc(g_, x16_, w16_, acc_, amax_, st));
+        ActRequant r;
+        r.acc = acc_;
+        r.rows = (int64_t)g_.n * g_.oh * g_.ow;
+        r.ldc = g_.cop;
+        r.amax = amax_;
+        r.out_c4 = (int8_t*)out[0].data;
+        r.c_real = g_.c_out;
+        r.n = g_.n;
+        r.hw = g_.oh * g_.ow;
+        NITI_TRY(requant_act(r, st));
+        return NITI_NO_ERROR;
+    }
+
+   private:
+    niti_conv2d_common common_;
+    ConvGeom g_{};
+    int8_t *x16_ = nullptr, *w16_ = nullptr;
+    int32_t* acc_ = nullptr;
+    uint32_t* amax_ = nullptr;
+};
+
+// ------------------------------------------------------------------ NITI_GradientConv_Int8 (715)
+// A conv of C4(x^T) [Ci, N, H, W] with dy^T [Co, N, OH', OW'] as its kernel; computed as the
+// native weight-gradient GEMM (K = OH'*OW'*N) followed by PSTO(bw-2).
+class GradientConvInt8Execution : public Execution {
+   public:
+    explicit GradientConvInt8Execution(const niti_conv2d_common& c) : common_(c) {}
+    int onResize(const niti_tensor* in, int nin, const niti_tensor* out, int nout) override {
+        if (nin < 2 || nout < 1) return NITI_INVALID_VALUE;
+        const niti_tensor &xt = in[0], &dyt = in[1], &o = out[0];
+        if (xt.format != NITI_FORMAT_NC4HW4 || o.format != NITI_FORMAT_NC4HW4) return NITI_NOT_SUPPORT;
+        if (common_.group > 1 || common_.dilate_x > 1 || common_.dilate_y > 1) return NITI_NOT_SUPPORT;
+        if (dyt.dims[1] != xt.dims[1]) return NITI_COMPUTE_SIZE_ERROR;
+        // the op's own view: batch Ci, channel N, kernel OH' x OW'
+        ConvGeom op{};
+        if (!geom_from_common(common_, xt.dims[0], xt.dims[1], xt.dims[2], xt.dims[3], dyt.dims[0], dyt.dims[2],
+                              dyt.dims[3], &op))
+            return NITI_COMPUTE_SIZE_ERROR;
+        if (op.sh != 1 || op.sw != 1) return NITI_NOT_SUPPORT;  // the grad graph always passes stride 1
+        if (o.dims[0] != op.n || o.dims[1] != op.c_out || o.dims[2] != op.oh || o.dims[3] != op.ow)
+            return NITI_COMPUTE_SIZE_ERROR;
+        if (op.c_out % 4) return NITI_NOT_SUPPORT;
+        // the native weight-gradient geometry: images N, channels Ci, kernel (op.oh, op.ow)
+        ConvGeom g{};
+        g.n = xt.dims[1];
+        g.c_in = xt.dims[0];
+        g.h = xt.dims[2];
+        g.w = xt.dims[3];
+        g.c_out = dyt.dims[0];
+        g.kh = op.oh;
+        g.kw = op.ow;
+        g.sh = g.sw = g.dh = g.dw = 1;
+        g.pt = op.pt;
+        g.pl = op.pl;
+        g.pb = op.pb;
+        g.pr = op.pr;
+        if (!g.finalize() || g.oh != dyt.dims[2] || g.ow != dyt.dims[3]) return NITI_COMPUTE_SIZE_ERROR;
+        g_ = g;
+        ws_.release();
+        xT_ = (int8_t*)ws_.alloc((size_t)g_.cip * g_.h * g_.w * g_.np);
+        dyT_ = (int8_t*)ws_.alloc((size_t)g_.cop * g_.oh * g_.ow * g_.np);
+        acc_ = (int32_t*)ws_.alloc((size_t)g_.c_out * g_.kh * g_.kw * g_.cip * 4);
+        g8_ = (int8_t*)ws_.alloc((size_t)g_.c_out * g_.kh * g_.kw * g_.cip);
+        amax_ = (uint32_t*)ws_.alloc(16);
+        return (xT_ && dyT_ && acc_ && g8_ && amax_) ? NITI_NO_ERROR : NITI_OUT_OF_MEMORY;
+    }
+    int onExecute(const niti_tensor* in, int nin, const niti_tensor* out, int nout, hipStream_t st) override {
+        if (!acc_) return NITI_NO_EXECUTION;
+        const int hw = g_.h * g_.w, ohw = g_.oh * g_.ow, kk = g_.kh * g_.kw;
+        NITI_TRY(launch_map((int64_t)g_.cip * hw * g_.np,
+                            C4TransposedToChwn16{(const int8_t*)in[0].data, g_.n, g_.c_in, hw, g_.np, xT_}, st));
+        NITI_TRY(launch_map((int64_t)g_.cop * ohw * g_.np,
+                            NchwTransposedToChwn16{(const int8_t*)in[1].data, g_.n, g_.c_out, ohw, g_.np, dyT_}, st));
+        NITI_TRY(conv_wgrad_acc(g_, xT_, dyT_, acc_, st));
+        const int64_t nacc = (int64_t)g_.c_out * kk * g_.cip;
+        NITI_TRY(hipMemsetAsync(amax_, 0, 4, st));
+        NITI_TRY(absmax_i32(acc_, nacc, amax_, st));
+        NITI_TRY(requant_grad(acc_, nacc, amax_, RULE_WGRAD_BW2, g8_, nullptr, st));
+        NITI_TRY(launch_map((int64_t)((g_.c_out + 3) / 4) * g_.c_in * kk * 4,
+                            Ohwi16ToC4Grad{g8_, g_.c_out, g_.c_in, kk, g_.cip, (int8_t*)out[0].data}, st));
+        return NITI_NO_ERROR;
+    }
+
+   private:
+    niti_conv2d_common common_;
+    ConvGeom g_{};
+    int8_t *xT_ = nullptr, *dyT_ = nullptr, *g8_ = nullptr;
+    int32_t* acc_ = nullptr;
+    uint32_t* amax_ = nullptr;
+};
+
+// ------------------------------------------------------------------ NITI_Matmul_Int8 (713)
+// C[m][o] = PSTO(sum_k B[m][k] A[o][k], bw-3).  Output tensor C [M, Co] row major: the
+// values the reference computes (its output region then transposes C to [Co][M],
+// NITI_GeometryConv2DBackPropFilter_Int8.cpp:105-121).
+class MatmulInt8Execution : public Execution {
+   public:
+    int onResize(const niti_tensor* in, int nin, const niti_tensor* out, int nout) override {
+        if (nin < 2 || nout < 1) return NITI_INVALID_VALUE;
+        m_ = in[0].dims[0];
+        k_ = in[0].dims[1];
+        o_ = in[1].dims[0];
+        if (in[1].dims[1] != k_ || out[0].dims[0] != m_ || out[0].dims[1] != o_) return NITI_COMPUTE_SIZE_ERROR;
+        if (m_ <= 0 || k_ <= 0 || o_ <= 0) return NITI_COMPUTE_SIZE_ERROR;
+        k16_ = round_up(k_, 16);
+        ldc_ = round_up(o_, 16);
+        ws_.release();
+        b16_ = (int8_t*)ws_.alloc((size_t)m_ * k16_);
+        a16_ = (int8_t*)ws_.alloc((size_t)o_ * k16_);
+        acc_ = (int32_t*)ws_.alloc((size_t)m_ * ldc_ * 4);
+        g8_ = (int8_t*)ws_.alloc((size_t)m_ * ldc_);
+        amax_ = (uint32_t*)ws_.alloc(16);
+        return (b16_ && a16_ && acc_ && g8_ && amax_) ? NITI_NO_ERROR : NITI_OUT_OF_MEMORY;
+    }
+    int onExecute(const niti_tensor* in, int nin, const niti_tensor* out, int nout, hipStream_t st) override {
+        if (!acc_) return NITI_NO_EXECUTION;
+        NITI_TRY(pad_rows((const int8_t*)in[0].data, m_, k_, k16_, b16_, st));
+        NITI_TRY(pad_rows((const int8_t*)in[1].data, o_, k_, k16_, a16_, st));
+        NITI_TRY(matmul_acc(m_, o_, k16_, b16_, k16_, a16_, k16_, acc_, ldc_, nullptr, true, st));
+        NITI_TRY(hipMemsetAsync(amax_, 0, 4, st));
+        NITI_TRY(absmax_i32(acc_, (int64_t)m_ * ldc_, amax_, st));
+        NITI_TRY(requant_grad(acc_, (int64_t)m_ * ldc_, amax_, RULE_MATMUL_BW3, g8_, nullptr, st));
+        NITI_TRY(launch_map((int64_t)m_ * o_, UnpadRows{g8_, o_, ldc_, (int8_t*)out[0].data}, st));
+        return NITI_NO_ERROR;
+    }
+
+   private:
+    int m_ = 0, k_ = 0, o_ = 0, k16_ = 0, ldc_ = 0;
+    int8_t *b16_ = nullptr, *a16_ = nullptr, *g8_ = nullptr;
+    int32_t* acc_ = nullptr;
+    uint32_t* amax_ = nullptr;
+};
+
+// ------------------------------------------------------------------ NITI_DSP_MATMUL_GRADIENT_Int8 (818)
+// Op slot of the DSP weight-gradient (NHWC x, NHWC dy -> HWIO dw).  The DSP build
+// requantises on the Hexagon (round-to-nearest, then /16 on the CPU,
+// NITI_DSPMatmulGradientConv_Int8.cpp:543-550); this backend gives the op the CPU path's
+// numerics (NITI_GradientConv_Int8: PSTO(bw-2)), SURVEY.md §8(a) A5.
+class DspMatmulGradientExecution : public Execution {
+   public:
+    explicit DspMatmulGradientExecution(const niti_conv2d_common& c) : common_(c) {}
+    int onResize(const niti_tensor* in, int nin, const niti_tensor* out, int nout) override {
+        if (nin < 2 || nout < 1) return NITI_INVALID_VALUE;
+        const niti_tensor &x = in[0], &dy = in[1], &o = out[0];
+        if (x.format != NITI_FORMAT_NHWC || dy.format != NITI_FORMAT_NHWC) return NITI_NOT_SUPPORT;
+        if (common_.group > 1 || common_.dilate_x > 1 || common_.dilate_y > 1) return NITI_NOT_SUPPORT;
+        const int kh = common_.kernel_y, kw = common_.kernel_x;
+        if (!geom_from_common(common_, x.dims[0], x.dims[1], x.dims[2], x.dims[3], dy.dims[1], kh, kw, &g_))
+            return NITI_COMPUTE_SIZE_ERROR;
+        if (dy.dims[0] != g_.n || dy.dims[2] != g_.oh || dy.dims[3] != g_.ow) return NITI_COMPUTE_SIZE_ERROR;
+        if (o.dims[0] != kh || o.dims[1] != kw || o.dims[2] != g_.c_in || o.dims[3] != g_.c_out)
+            return NITI_COMPUTE_SIZE_ERROR;
+        ws_.release();
+        xT_ = (int8_t*)ws_.alloc((size_t)g_.cip * g_.h * g_.w * g_.np);
+        dyT_ = (int8_t*)ws_.alloc((size_t)g_.cop * g_.oh * g_.ow * g_.np);
+        acc_ = (int32_t*)ws_.alloc((size_t)g_.c_out * kh * kw * g_.cip * 4);
+        g8_ = (int8_t*)ws_.alloc((size_t)g_.c_out * kh * kw * g_.cip);
+        amax_ = (uint32_t*)ws_.alloc(16);
+        return (xT_ && dyT_ && acc_ && g8_ && amax_) ? NITI_NO_ERROR : NITI_OUT_OF_MEMORY;
+    }
+    int onExecute(const niti_tensor* in, int nin, const niti_tensor* out, int nout, hipStream_t st) override {
+        if (!acc_) return NITI_NO_EXECUTION;
+        const int hw = g_.h * g_.w, ohw = g_.oh * g_.ow, kk = g_.kh * g_.kw;
+        NITI_TRY(launch_map((int64_t)g_.cip * hw * g_.np, NhwcToChwn16{(const int8_t*)in[0].data, g_.n, g_.c_in, hw, g_.np, xT_}, st));
+        NITI_TRY(launch_map((int64_t)g_.cop * ohw * g_.np, NhwcToChwn16{(const int8_t*)in[1].data, g_.n, g_.c_out, ohw, g_.np, dyT_}, st));
+        NITI_TRY(conv_wgrad_acc(g_, xT_, dyT_, acc_, st));
+        const int64_t nacc = (int64_t)g_.c_out * kk * g_.cip;
+        NITI_TRY(hipMemsetAsync(amax_, 0, 4, st));
+        NITI_TRY(absmax_i32(acc_, nacc, amax_, st));
+        NITI_TRY(requant_grad(acc_, nacc, amax_, RULE_WGRAD_BW2, g8_, nullptr, st));
+        NITI_TRY(launch_map((int64_t)kk * g_.c_in * g_.c_out, Ohwi16ToHwio{g8_, g_.c_out, g_.c_in, kk, g_.cip, (int8_t*)out[0].data}, st));
+        return NITI_NO_ERROR;
+    }
+
+   private:
+    niti_conv2d_common common_;
+    ConvGeom g_{};
+    int8_t *xT_ = nullptr, *dyT_ = nullptr, *g8_ = nullptr;
+    int32_t* acc_ = nullptr;
+    uint32_t* amax_ = nullptr;
+};
+
+Execution* create_execution(int op_type, const niti_conv2d_common* c, int* err) {
+    *err = NITI_NO_ERROR;
+    niti_conv2d_common dflt{};
+    dflt.kernel_x = dflt.kernel_y = dflt.stride_x = dflt.stride_y = dflt.dilate_x = dflt.dilate_y = 1;
+    dflt.group = 1;
+    const niti_conv2d_common& cc = c ? *c : dflt;
+    if (op_type != NITI_OP_MATMUL_INT8 && c == nullptr) {
+        *err = NITI_INVALID_VALUE;
+        return nullptr;
+    }
+    if (cc.group > 1) {
+        *err = NITI_NOT_SUPPORT;
+        return nullptr;
+    }
+    switch (op_type) {
+        case NITI_OP_CONV_INT8: return new ConvInt8Execution(cc);
+        case NITI_OP_DECONV_INT8: return new DeconvInt8Execution(cc);
+        case NITI_OP_GRADIENT_CONV_INT8: return new GradientConvInt8Execution(cc);
+        case NITI_OP_MATMUL_INT8: return new MatmulInt8Execution();
+        case NITI_OP_DSP_MATMUL_GRADIENT_INT8: return new DspMatmulGradientExecution(cc);
+        default: *err = NITI_NOT_SUPPORT; return nullptr;
+    }
+}
+
+}  // namespace niti

@@ -1,0 +1,997 @@
+// niti_kernels.hip -- gfx950 (MI355X / CDNA4) kernels for the NITI int8 training path.
+//
+// The three GEMM-class ops of the reference (NITI_Conv_Int8, NITI_GradientConv_Int8 /
+// NITI_Matmul_Int8 / NITI_DSPMatmulGradientConv_Int8, NITI_DeConv_Int8) are one
+// implicit-GEMM kernel template on v_mfma_i32_32x32x32_i8 with exact int32
+// accumulation; the im2col gather happens in the global->LDS staging of each operand
+// (an operand "loader" per op), never as a materialised column buffer.  The per-layer
+// power-of-two rescale (NITI_RangeEstimate + NITI_MNNPstoShiftInt32,
+// CommonOptFunction.cpp:1565-1627) is split around a grid-wide max: the GEMM epilogue
+// reduces max|acc| per workgroup and atomically max-es it into one word; the requant
+// kernel reads that word (after a kernel boundary -- or an RCCL all-reduce(MAX) in
+// data-parallel exact mode) and applies the shift.
+#include "niti_kernels.hpp"
+#include "niti_map.hpp"
+
+namespace niti {
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v16i __attribute__((ext_vector_type(16)));
+typedef signed char v16c __attribute__((ext_vector_type(16)));
+
+bool ConvGeom::finalize() {
+    if (n <= 0 || c_in <= 0 || h <= 0 || w <= 0 || c_out <= 0 || kh <= 0 || kw <= 0) return false;
+    if (sh <= 0 || sw <= 0 || dh <= 0 || dw <= 0) return false;
+    const int keh = dh * (kh - 1) + 1, kew = dw * (kw - 1) + 1;
+    oh = (h + pt + pb - keh) / sh + 1;  // ShapeNITI_Conv_Int8.cpp:58-76
+    ow = (w + pl + pr - kew) / sw + 1;
+    cip = round_up(c_in, 16);
+    cop = round_up(c_out, 16);
+    np = round_up(n, 16);
+    return oh > 0 && ow > 0;
+}
+
+__device__ __forceinline__ v4i zero4() {
+    v4i z = {0, 0, 0, 0};
+    return z;
+}
+
+// =====================================================================================
+// Operand loaders: each returns one 16-byte K-chunk of one GEMM row (zero if outside).
+// =====================================================================================
+
+// Plain row-major operand: row r at p + r*ld, K-chunks contiguous.
+struct LoadRowMajor {
+    const int8_t* p;
+    int64_t ld;
+    int rows;
+    int kc_total;
+    struct Row {
+        const int8_t* base;
+    };
+    __device__ __forceinline__ Row row(int r) const { return {r < rows ? p + (int64_t)r * ld : nullptr}; }
+    __device__ __forceinline__ v4i load(const Row& R, int kc) const {
+        if (R.base == nullptr || kc >= kc_total) return zero4();
+        return *(const v4i*)(R.base + (int64_t)kc * 16);
+    }
+};
+
+// Forward conv, A operand: row m = output pixel (n, oy, ox) of an NHWC16 input,
+// K-chunk kc = (ky, kx, cc) with cc the 16-channel group (im2col of
+// Int8FunctionsOpt.cpp:342-392, but channel-contiguous and never materialised).
+struct LoadConvFwd {
+    const int8_t* x;
+    int H, W, CPC, OH, OW, KW, sh, sw, pt, pl, dh, dw, M, kc_total;
+    int64_t img;  // bytes per image
+    struct Row {
+        const int8_t* base;
+        int iy0, ix0;
+    };
+    __device__ __forceinline__ Row row(int m) const {
+        if (m >= M) return {nullptr, 0, 0};
+        const int ox = m % OW;
+        const int t = m / OW;
+        const int oy = t % OH;
+        const int n = t / OH;
+        return {x + (int64_t)n * img, oy * sh - pt, ox * sw - pl};
+    }
+    __device__ __forceinline__ v4i load(const Row& R, int kc) const {
+        if (R.base == nullptr || kc >= kc_total) return zero4();
+        const int tap = kc / CPC;
+        const int cc = kc - tap * CPC;
+        const int ky = tap / KW;
+        const int kx = tap - ky * KW;
+        const int iy = R.iy0 + ky * dh;
+        const int ix = R.ix0 + kx * dw;
+        if ((unsigned)iy >= (unsigned)H || (unsigned)ix >= (unsigned)W) return zero4();
+        return *(const v4i*)(R.base + ((int64_t)(iy * W + ix) * CPC + cc) * 16);
+    }
+};
+
+// Input-gradient conv, A operand: row m = input pixel (n, iy, ix), K-chunk = (ky, kx, cc)
+// over the NHWC16 output gradient; oy = (iy + pt - ky*dh) / sh when divisible.  This is the
+// transposed convolution the reference builds from pad(dilate(dy)) and rot180(w^T)
+// (grad/NITI_Conv_Int8_Grad.cpp:29-122, NITI_DeConv_Int8.cpp:179-219).
+struct LoadConvDgrad {
+    const int8_t* dy;
+    int OH, OW, CPC, H, W, KW, sh, sw, pt, pl, dh, dw, M, kc_total;
+    int64_t img;
+    struct Row {
+        const int8_t* base;
+        int ty0, tx0;
+    };
+    __device__ __forceinline__ Row row(int m) const {
+        if (m >= M) return {nullptr, 0, 0};
+        const int ix = m % W;
+        const int t = m / W;
+        const int iy = t % H;
+        const int n = t / H;
+        return {dy + (int64_t)n * img, iy + pt, ix + pl};
+    }
+    __device__ __forceinline__ v4i load(const Row& R, int kc) const {
+        if (R.base == nullptr || kc >= kc_total) return zero4();
+        const int tap = kc / CPC;
+        const int cc = kc - tap * CPC;
+        const int ky = tap / KW;
+        const int kx = tap - ky * KW;
+        const int ty = R.ty0 - ky * dh;
+        const int tx = R.tx0 - kx * dw;
+        if (ty < 0 || tx < 0) return zero4();
+        const int oy = ty / sh, ox = tx / sw;
+        if (oy * sh != ty || ox * sw != tx || oy >= OH || ox >= OW) return zero4();
+        return *(const v4i*)(R.base + ((int64_t)(oy * OW + ox) * CPC + cc) * 16);
+    }
+};
+
+// Weight-gradient conv, B operand: row r = (ky, kx, ci) of the OHWI16 gradient, K-chunk =
+// (oy, ox, nc) over a CHWN16 input (16 consecutive images of one channel and pixel).
+struct LoadWgradX {
+    const int8_t* xT;
+    int H, W, NPC, OW, sh, sw, pt, pl, dh, dw, KW, CIP, rows, kc_total;
+    int64_t plane;  // bytes per channel plane (H*W*Np)
+    struct Row {
+        const int8_t* base;
+        int offy, offx;
+    };
+    __device__ __forceinline__ Row row(int r) const {
+        if (r >= rows) return {nullptr, 0, 0};
+        const int ci = r % CIP;
+        const int tap = r / CIP;
+        const int ky = tap / KW;
+        const int kx = tap - ky * KW;
+        return {xT + (int64_t)ci * plane, ky * dh - pt, kx * dw - pl};
+    }
+    __device__ __forceinline__ v4i load(const Row& R, int kc) const {
+        if (R.base == nullptr || kc >= kc_total) return zero4();
+        const int pix = kc / NPC;
+        const int nc = kc - pix * NPC;
+        const int oy = pix / OW;
+        const int ox = pix - oy * OW;
+        const int iy = oy * sh + R.offy;
+        const int ix = ox * sw + R.offx;
+        if ((unsigned)iy >= (unsigned)H || (unsigned)ix >= (unsigned)W) return zero4();
+        return *(const v4i*)(R.base + ((int64_t)(iy * W + ix) * NPC + nc) * 16);
+    }
+};
+
+// =====================================================================================
+// The GEMM: C[m][n] = sum_k A[m][k] * B[n][k], int8 x int8 -> exact int32.
+//   256 threads = 4 waves; BM x BN block tile; 64-byte K step (two 32-deep MFMAs);
+//   LDS double buffer with one barrier per step; 16-byte chunks XOR-swizzled so the
+//   ds_read_b128 fragment reads of 32 rows are bank-conflict free.
+// =====================================================================================
+constexpr int BK = 64;        // K bytes per step
+constexpr int CPS = BK / 16;  // 16-byte chunks per row per step
+
+__device__ __forceinline__ int lds_off(int r, int c) { return r * BK + ((c ^ ((r >> 2) & 3)) << 4); }
+
+__device__ __forceinline__ uint32_t uabs32(int v) { return v < 0 ? 0u - (uint32_t)v : (uint32_t)v; }
+
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint32_t t = __shfl_xor(v, o, 64);
+        v = v > t ? v : t;
+    }
+    return v;
+}
+
+template <int BM, int BN, int WM, int WN, class LA, class LB, bool ATOMIC>
+__global__ void __launch_bounds__(256) gemm_i8_kernel(LA la, LB lb, int M, int N, int tiles_n,
+                                                       int kc_total, int kc_per_split, int32_t* __restrict__ C,
+                                                       int64_t ldc, uint32_t* __restrict__ amax) {
+    static_assert(WM * WN == 4, "4 waves");
+    constexpr int TM = BM / WM / 32;
+    constexpr int TN = BN / WN / 32;
+    static_assert(TM >= 1 && TN >= 1, "tile");
+    constexpr int A_CH = BM * CPS;  // chunks per step
+    constexpr int B_CH = BN * CPS;
+    constexpr int A_LD = (A_CH + 255) / 256;
+    constexpr int B_LD = (B_CH + 255) / 256;
+    constexpr int A_BYTES = BM * BK, B_BYTES = BN * BK;
+    __shared__ __attribute__((aligned(16))) int8_t smem[2 * (A_BYTES + B_BYTES)];
+    int8_t* sA = smem;
+    int8_t* sB = smem + 2 * A_BYTES;
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wid = tid >> 6;
+    const int wm = wid / WN, wn = wid % WN;
+    const int tm_ = blockIdx.x / tiles_n, tn_ = blockIdx.x % tiles_n;
+    const int m0 = tm_ * BM, n0 = tn_ * BN;
+    const int kc_begin = blockIdx.y * kc_per_split;
+    const int kc_end = min(kc_total, kc_begin + kc_per_split);
+    const int nsteps = kc_end > kc_begin ? (kc_end - kc_begin + CPS - 1) / CPS : 0;
+
+    typename LA::Row ra[A_LD];
+    typename LB::Row rb[B_LD];
+    int ar[A_LD], ac[A_LD], br[B_LD], bc[B_LD];
+#pragma unroll
+    for (int i = 0; i < A_LD; ++i) {
+        const int id = tid + i * 256;
+        ar[i] = id / CPS;
+        ac[i] = id % CPS;
+        ra[i] = la.row(id < A_CH ? m0 + ar[i] : 0x7fffffff);
+    }
+#pragma unroll
+    for (int i = 0; i < B_LD; ++i) {
+        const int id = tid + i * 256;
+        br[i] = id / CPS;
+        bc[i] = id % CPS;
+        rb[i] = lb.row(id < B_CH ? n0 + br[i] : 0x7fffffff);
+    }
+    v4i sa[A_LD], sb[B_LD];
+    auto gload = [&](int kc0) {
+#pragma unroll
+        for (int i = 0; i < A_LD; ++i) sa[i] = la.load(ra[i], kc0 + ac[i] < kc_end ? kc0 + ac[i] : 0x7fffffff);
+#pragma unroll
+        for (int i = 0; i < B_LD; ++i) sb[i] = lb.load(rb[i], kc0 + bc[i] < kc_end ? kc0 + bc[i] : 0x7fffffff);
+    };
+    auto sstore = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < A_LD; ++i)
+            if (A_CH % 256 == 0 || tid + i * 256 < A_CH) *(v4i*)(sA + buf * A_BYTES + lds_off(ar[i], ac[i])) = sa[i];
+#pragma unroll
+        for (int i = 0; i < B_LD; ++i)
+            if (B_CH % 256 == 0 || tid + i * 256 < B_CH) *(v4i*)(sB + buf * B_BYTES + lds_off(br[i], bc[i])) = sb[i];
+    };
+
+    v16i acc[TM][TN];
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int b = 0; b < TN; ++b)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) acc[a][b][i] = 0;
+
+    if (nsteps > 0) {
+        gload(kc_begin);
+        sstore(0);
+    }
+    __syncthreads();
+    for (int s = 0; s < nsteps; ++s) {
+        const int buf = s & 1;
+        if (s + 1 < nsteps) gload(kc_begin + (s + 1) * CPS);
+        const int8_t* cA = sA + buf * A_BYTES;
+        const int8_t* cB = sB + buf * B_BYTES;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            const int c = kk * 2 + (lane >> 5);
+            v4i fa[TM], fb[TN];
+#pragma unroll
+            for (int a = 0; a < TM; ++a) fa[a] = *(const v4i*)(cA + lds_off(wm * (BM / WM) + a * 32 + (lane & 31), c));
+#pragma unroll
+            for (int b = 0; b < TN; ++b) fb[b] = *(const v4i*)(cB + lds_off(wn * (BN / WN) + b * 32 + (lane & 31), c));
+#pragma unroll
+            for (int a = 0; a < TM; ++a)
+#pragma unroll
+                for (int b = 0; b < TN; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[a], fb[b], acc[a][b], 0, 0, 0);
+        }
+        if (s + 1 < nsteps) sstore(buf ^ 1);
+        __syncthreads();
+    }
+
+    // epilogue: D[row][col], row = (i&3) + 8*(i>>2) + 4*(lane>>5), col = lane&31
+    uint32_t lmax = 0;
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int b = 0; b < TN; ++b) {
+            const int col = n0 + wn * (BN / WN) + b * 32 + (lane & 31);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int row = m0 + wm * (BM / WM) + a * 32 + (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
+                const int v = acc[a][b][i];
+                if (row < M && col < N) {
+                    if (ATOMIC) {
+                        if (v != 0) atomicAdd(C + (int64_t)row * ldc + col, v);
+                    } else {
+                        C[(int64_t)row * ldc + col] = v;
+                        const uint32_t u = uabs32(v);
+                        lmax = lmax > u ? lmax : u;
+                    }
+                }
+            }
+        }
+    if (!ATOMIC && amax != nullptr) {
+        lmax = wave_max(lmax);
+        uint32_t* red = (uint32_t*)smem;  // all LDS reads finished at the last barrier
+        if (lane == 0) red[wid] = lmax;
+        __syncthreads();
+        if (tid == 0) {
+            uint32_t m = red[0];
+            for (int i = 1; i < 4; ++i) m = m > red[i] ? m : red[i];
+            if (m) atomicMax(amax, m);
+        }
+    }
+}
+
+template <class LA, class LB, bool ATOMIC>
+static hipError_t launch_gemm(const LA& la, const LB& lb, int M, int N, int kc_total, int splits, int32_t* C,
+                              int64_t ldc, uint32_t* amax, hipStream_t st) {
+    if (M <= 0 || N <= 0) return hipSuccess;
+    if (splits < 1) splits = 1;
+    const int kc_per_split = ((kc_total + splits - 1) / splits + CPS - 1) / CPS * CPS;
+    splits = kc_per_split > 0 ? (kc_total + kc_per_split - 1) / kc_per_split : 1;
+    if (splits < 1) splits = 1;
+#define NITI_LAUNCH(BM_, BN_, WM_, WN_)                                                                   \
+    do {                                                                                                  \
+        const int tm = (M + BM_ - 1) / BM_, tn = (N + BN_ - 1) / BN_;                                     \
+        dim3 grid(tm * tn, splits);                                                                       \
+        hipLaunchKernelGGL((gemm_i8_kernel<BM_, BN_, WM_, WN_, LA, LB, ATOMIC>), grid, dim3(256), 0, st, \
+                           la, lb, M, N, tn, kc_total, kc_per_split, C, ldc, amax);                       \
+    } while (0)
+    if (N <= 32)
+        NITI_LAUNCH(128, 32, 4, 1);
+    else if (N <= 64)
+        NITI_LAUNCH(128, 64, 2, 2);
+    else
+        NITI_LAUNCH(128, 128, 2, 2);
+#undef NITI_LAUNCH
+    return hipGetLastError();
+}
+
+static int choose_splits(int M, int N, int kc_total) {
+    // enough workgroups for 256 CUs (x2), but keep >= 8 K-steps per split
+    const int tiles = ((M + 127) / 128) * ((N + 127) / 128);
+    const int steps = (kc_total + CPS - 1) / CPS;
+    int s = (512 + tiles - 1) / tiles;
+    const int max_s = steps / 8 > 1 ? steps / 8 : 1;
+    if (s > max_s) s = max_s;
+    return s < 1 ? 1 : s;
+}
+
+hipError_t conv_fwd_acc(const ConvGeom& g, const int8_t* x, const int8_t* w, int32_t* acc, uint32_t* amax,
+                        hipStream_t st) {
+    LoadConvFwd la;
+    la.x = x;
+    la.H = g.h;
+    la.W = g.w;
+    la.CPC = g.cip / 16;
+    la.OH = g.oh;
+    la.OW = g.ow;
+    la.KW = g.kw;
+    la.sh = g.sh;
+    la.sw = g.sw;
+    la.pt = g.pt;
+    la.pl = g.pl;
+    la.dh = g.dh;
+    la.dw = g.dw;
+    la.M = g.n * g.oh * g.ow;
+    la.kc_total = g.kh * g.kw * la.CPC;
+    la.img = (int64_t)g.h * g.w * g.cip;
+    LoadRowMajor lb{w, (int64_t)g.kh * g.kw * g.cip, g.c_out, la.kc_total};
+    return launch_gemm<LoadConvFwd, LoadRowMajor, false>(la, lb, la.M, g.cop, la.kc_total, 1, acc, g.cop, amax, st);
+}
+
+hipError_t conv_dgrad_acc(const ConvGeom& g, const int8_t* dy, const int8_t* wt, int32_t* acc, uint32_t* amax,
+                          hipStream_t st) {
+    LoadConvDgrad la;
+    la.dy = dy;
+    la.OH = g.oh;
+    la.OW = g.ow;
+    la.CPC = g.cop / 16;
+    la.H = g.h;
+    la.W = g.w;
+    la.KW = g.kw;
+    la.sh = g.sh;
+    la.sw = g.sw;
+    la.pt = g.pt;
+    la.pl = g.pl;
+    la.dh = g.dh;
+    la.dw = g.dw;
+    la.M = g.n * g.h * g.w;
+    la.kc_total = g.kh * g.kw * la.CPC;
+    la.img = (int64_t)g.oh * g.ow * g.cop;
+    LoadRowMajor lb{wt, (int64_t)g.kh * g.kw * g.cop, g.c_in, la.kc_total};
+    return launch_gemm<LoadConvDgrad, LoadRowMajor, false>(la, lb, la.M, g.cip, la.kc_total, 1, acc, g.cip, amax, st);
+}
+
+hipError_t conv_wgrad_acc(const ConvGeom& g, const int8_t* xT, const int8_t* dyT, int32_t* acc, hipStream_t st,
+                          bool zero) {
+    const int npc = g.np / 16;
+    const int kc_total = g.oh * g.ow * npc;
+    const int M = g.c_out, N = g.kh * g.kw * g.cip;
+    LoadRowMajor la{dyT, (int64_t)g.oh * g.ow * g.np, g.c_out, kc_total};
+    LoadWgradX lb;
+    lb.xT = xT;
+    lb.H = g.h;
+    lb.W = g.w;
+    lb.NPC = npc;
+    lb.OW = g.ow;
+    lb.sh = g.sh;
+    lb.sw = g.sw;
+    lb.pt = g.pt;
+    lb.pl = g.pl;
+    lb.dh = g.dh;
+    lb.dw = g.dw;
+    lb.KW = g.kw;
+    lb.CIP = g.cip;
+    lb.rows = N;
+    lb.kc_total = kc_total;
+    lb.plane = (int64_t)g.h * g.w * g.np;
+    if (zero) {
+        hipError_t e = hipMemsetAsync(acc, 0, (size_t)M * N * sizeof(int32_t), st);
+        if (e != hipSuccess) return e;
+    }
+    return launch_gemm<LoadRowMajor, LoadWgradX, true>(la, lb, M, N, kc_total, choose_splits(M, N, kc_total), acc, N,
+                                                       nullptr, st);
+}
+
+hipError_t matmul_acc(int M, int O, int k16, const int8_t* B, int64_t ldb, const int8_t* A, int64_t lda,
+                      int32_t* acc, int64_t ldc, uint32_t* amax, bool split_k, hipStream_t st) {
+    const int kc_total = k16 / 16;
+    LoadRowMajor la{B, ldb, M, kc_total};
+    LoadRowMajor lb{A, lda, O, kc_total};
+    if (split_k) {
+        hipError_t e = hipMemsetAsync(acc, 0, (size_t)M * ldc * sizeof(int32_t), st);
+        if (e != hipSuccess) return e;
+        return launch_gemm<LoadRowMajor, LoadRowMajor, true>(la, lb, M, O, kc_total, choose_splits(M, O, kc_total),
+                                                             acc, ldc, nullptr, st);
+    }
+    return launch_gemm<LoadRowMajor, LoadRowMajor, false>(la, lb, M, O, kc_total, 1, acc, ldc, amax, st);
+}
+
+// =====================================================================================
+// Range estimate and requantisation
+// =====================================================================================
+
+// NITI_RangeEstimate on the max word: ceil(log2(m)), 0 for m <= 1.
+__device__ __forceinline__ int bitwidth_of(uint32_t m) { return m <= 1u ? 0 : 32 - __clz((int)(m - 1u)); }
+
+__device__ __forceinline__ int32_t clip127(int32_t a) { return a > 127 ? 127 : (a < -127 ? -127 : a); }
+
+// (1 << s) as the reference's x86 build executes it for a run-time s (count & 31).
+__device__ __forceinline__ int32_t pow2_x86(int s) { return (int32_t)(1u << ((unsigned)s & 31u)); }
+
+// NITI_MNNPstoShiftInt32 (CommonOptFunction.cpp:1595-1627), exact for any shift the
+// reference can produce; the fast path covers 0 <= s <= 30.
+__device__ __forceinline__ int32_t psto_fast(int32_t a, int s) {
+    const uint32_t ua = a < 0 ? 0u - (uint32_t)a : (uint32_t)a;
+    const uint32_t q = ua >> s;
+    const uint32_t prob = ua & ((1u << s) - 1u);
+    const int h = s >> 1;
+    const uint32_t qp = prob >> h;
+    uint32_t pr = prob & ((1u << h) - 1u);
+    if (s & 1) pr <<= 1;
+    const int32_t r = (int32_t)q + (qp > pr ? 1 : 0);
+    return clip127(a < 0 ? -r : r);
+}
+
+__device__ int32_t psto_generic(int32_t a, int s) {
+    const int32_t p = pow2_x86(s);
+    const int32_t q = a / p;
+    int32_t prob = (int32_t)((uint32_t)a - (uint32_t)q * (uint32_t)p);
+    prob = prob < 0 ? -prob : prob;
+    const int32_t hp = pow2_x86(s / 2);
+    const int32_t qp = prob / hp;
+    int32_t pr = (int32_t)((uint32_t)prob - (uint32_t)qp * (uint32_t)hp);
+    if (s % 2 == 1) pr = (int32_t)((uint32_t)pr * 2u);
+    const int32_t sg = a > 0 ? 1 : (a < 0 ? -1 : 0);
+    return clip127((int32_t)((uint32_t)q + (uint32_t)((qp > pr) * sg)));
+}
+
+__device__ __forceinline__ int32_t psto_any(int32_t a, int s) {
+    return (s >= 0 && s <= 30) ? psto_fast(a, s) : psto_generic(a, s);
+}
+
+__global__ void absmax_kernel(const int32_t* __restrict__ a, int64_t n, uint32_t* __restrict__ amax) {
+    uint32_t m = 0;
+    const int64_t n4 = n / 4;
+    const v4i* a4 = (const v4i*)a;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+        const v4i v = a4[i];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t u = uabs32(v[j]);
+            m = m > u ? m : u;
+        }
+    }
+    for (int64_t i = n4 * 4 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t u = uabs32(a[i]);
+        m = m > u ? m : u;
+    }
+    m = wave_max(m);
+    __shared__ uint32_t red[16];
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int i = 1; i < (int)(blockDim.x >> 6); ++i) m = m > red[i] ? m : red[i];
+        m = m > red[0] ? m : red[0];
+        if (m) atomicMax(amax, m);
+    }
+}
+
+hipError_t absmax_i32(const int32_t* a, int64_t n, uint32_t* amax, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    int64_t blocks = (n / 4 + 255) / 256;
+    if (blocks > 2048) blocks = 2048;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(absmax_kernel, dim3((unsigned)blocks), dim3(256), 0, st, a, n, amax);
+    return hipGetLastError();
+}
+
+// forward / deconv rule, NITI_Conv_Int8.cpp:262-307: shift>1 PSTO(shift); ==1 PSTO(2); else raw cast
+__global__ void requant_act_kernel(ActRequant r) {
+    const int bw = bitwidth_of(*r.amax);
+    const int shift = bw - 7;
+    const int s = shift > 1 ? shift : 2;
+    const bool raw = shift <= 0;
+    const int groups = r.ldc / 16;
+    const int64_t total = r.rows * groups;
+    if (blockIdx.x == 0 && threadIdx.x == 0 && r.exp_out != nullptr) {
+        const int inc = shift > 1 ? shift : (shift == 1 ? 2 : 0);
+        const int ein = r.exp_in ? (int)*r.exp_in : 0;
+        const int ws = r.wscale ? (int)*r.wscale : 0;
+        *r.exp_out = (int8_t)(ein + ws + inc);
+    }
+    for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t m = t / groups;
+        const int gi = (int)(t - m * groups);
+        const v4i* src = (const v4i*)(r.acc + m * r.ldc + gi * 16);
+        v16c q;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const v4i v = src[j];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                int32_t o = raw ? (int32_t)(int8_t)v[e] : psto_any(v[e], s);
+                if (r.relu && o < 0) o = 0;
+                q[j * 4 + e] = (signed char)o;
+            }
+        }
+        if (r.relu_mask != nullptr) {
+            const v16c mk = *(const v16c*)(r.relu_mask + m * r.ldc + gi * 16);
+#pragma unroll
+            for (int j = 0; j < 16; ++j) q[j] = mk[j] > 0 ? q[j] : (signed char)0;
+        }
+        if (r.out_nhwc16 != nullptr) *(v16c*)(r.out_nhwc16 + m * r.ldc + gi * 16) = q;
+        if (r.out_c4 != nullptr) {
+            const int64_t b = m / r.hw, p = m - b * r.hw;
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const int c = gi * 16 + j;
+                if (c < r.c_real) r.out_c4[(((int64_t)(c >> 2) * r.n + b) * r.hw + p) * 4 + (c & 3)] = q[j];
+            }
+        }
+    }
+}
+
+hipError_t requant_act(const ActRequant& r, hipStream_t st) {
+    if (r.ldc % 16 != 0 || r.acc == nullptr || r.amax == nullptr) return hipErrorInvalidValue;
+    const int64_t total = r.rows * (r.ldc / 16);
+    int64_t blocks = (total + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(requant_act_kernel, dim3((unsigned)blocks), dim3(256), 0, st, r);
+    return hipGetLastError();
+}
+
+__global__ void requant_grad_kernel(const int32_t* __restrict__ acc, int64_t n, const uint32_t* __restrict__ amax,
+                                    int rule, int8_t* __restrict__ g_out, int8_t* __restrict__ w) {
+    const int bw = bitwidth_of(*amax);
+    const int s = bw - rule;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t g = bw == 0 ? 0 : psto_any(acc[i], s);
+        if (g_out) g_out[i] = (int8_t)g;
+        if (w) w[i] = (int8_t)clip127((int32_t)w[i] - g);
+    }
+}
+
+hipError_t requant_grad(const int32_t* acc, int64_t n, const uint32_t* amax, int rule, int8_t* g_out, int8_t* w,
+                        hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    int64_t blocks = (n + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(requant_grad_kernel, dim3((unsigned)blocks), dim3(256), 0, st, acc, n, amax, rule, g_out, w);
+    return hipGetLastError();
+}
+
+// =====================================================================================
+// The rest of the step: pool / relu-grad / loss-grad
+// =====================================================================================
+
+// NITI_Maxpool_Int8.cpp:24-72 (kernel clipped to the input); one thread per 16 channels.
+__global__ void maxpool_kernel(const int8_t* __restrict__ x, int n, int h, int w, int cp, int k, int s, int p,
+                               int8_t* __restrict__ y, int oh, int ow) {
+    const int groups = cp / 16;
+    const int64_t total = (int64_t)n * oh * ow * groups;
+    const int kh = k < h ? k : h, kw = k < w ? k : w;
+    for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+        int64_t r = t;
+        const int gi = (int)(r % groups);
+        r /= groups;
+        const int ox = (int)(r % ow);
+        r /= ow;
+        const int oy = (int)(r % oh);
+        const int b = (int)(r / oh);
+        const int sx0 = ox * s - p, sy0 = oy * s - p;
+        v16c m;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) m[j] = (signed char)-128;
+        for (int yy = max(0, -sy0); yy < min(kh, h - sy0); ++yy)
+            for (int xx = max(0, -sx0); xx < min(kw, w - sx0); ++xx) {
+                const v16c v = *(const v16c*)(x + (((int64_t)b * h + sy0 + yy) * w + sx0 + xx) * cp + gi * 16);
+#pragma unroll
+                for (int j = 0; j < 16; ++j) m[j] = v[j] > m[j] ? v[j] : m[j];
+            }
+        *(v16c*)(y + (((int64_t)b * oh + oy) * ow + ox) * cp + gi * 16) = m;
+    }
+}
+
+hipError_t maxpool_nhwc16(const int8_t* x, int n, int h, int w, int cp, int k, int s, int p, int8_t* y, int oh, int ow,
+                          hipStream_t st) {
+    const int64_t total = (int64_t)n * oh * ow * (cp / 16);
+    int64_t blocks = (total + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(maxpool_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, n, h, w, cp, k, s, p, y, oh, ow);
+    return hipGetLastError();
+}
+
+// NITI_CPUPoolGrad_Int8.cpp:21-77 in gather form: input pixel (iy,ix) receives, from every
+// window containing it, dy if it is that window's first (ky,kx) element with x >= max.
+// Optionally fused NITI_CPUReluGrad_Int8 (out = x > 0 ? dx : 0).
+__global__ void maxpool_grad_kernel(const int8_t* __restrict__ x, const int8_t* __restrict__ y,
+                                    const int8_t* __restrict__ dy, int n, int h, int w, int cp, int k, int s,
+                                    int p, int oh, int ow, int relu, int8_t* __restrict__ dx) {
+    const int groups = cp / 16;
+    const int64_t total = (int64_t)n * h * w * groups;
+    for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+        int64_t r = t;
+        const int gi = (int)(r % groups);
+        r /= groups;
+        const int ix = (int)(r % w);
+        r /= w;
+        const int iy = (int)(r % h);
+        const int b = (int)(r / h);
+        const v16c xv = *(const v16c*)(x + (((int64_t)b * h + iy) * w + ix) * cp + gi * 16);
+        v16c acc;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) acc[j] = 0;
+        // windows (oy, ox) with oy*s - p <= iy < oy*s - p + k
+        const int oy_lo = max(0, (iy + p - k + s) / s), oy_hi = min(oh - 1, (iy + p) / s);
+        const int ox_lo = max(0, (ix + p - k + s) / s), ox_hi = min(ow - 1, (ix + p) / s);
+        for (int oy = oy_lo; oy <= oy_hi; ++oy)
+            for (int ox = ox_lo; ox <= ox_hi; ++ox) {
+                const int sy0 = oy * s - p, sx0 = ox * s - p;
+                if (iy < sy0 || iy >= sy0 + k || ix < sx0 || ix >= sx0 + k) continue;
+                const int64_t po = (((int64_t)b * oh + oy) * ow + ox) * cp + gi * 16;
+                const v16c mv = *(const v16c*)(y + po);
+                const v16c dv = *(const v16c*)(dy + po);
+                // is (iy,ix) the first element >= max in this window, per channel?
+                unsigned first = 0xffffu;
+                for (int ky = 0; ky < k; ++ky) {
+                    const int sy = sy0 + ky;
+                    if (sy < 0 || sy >= h) continue;
+                    for (int kx = 0; kx < k; ++kx) {
+                        const int sx = sx0 + kx;
+                        if (sx < 0 || sx >= w) continue;
+                        if (sy == iy && sx == ix) goto done;
+                        {
+                            const v16c ov = *(const v16c*)(x + (((int64_t)b * h + sy) * w + sx) * cp + gi * 16);
+#pragma unroll
+                            for (int j = 0; j < 16; ++j)
+                                if (ov[j] >= mv[j]) first &= ~(1u << j);
+                        }
+                    }
+                }
+            done:
+#pragma unroll
+                for (int j = 0; j < 16; ++j)
+                    if (((first >> j) & 1u) && xv[j] >= mv[j]) acc[j] = (signed char)(acc[j] + dv[j]);
+            }
+        if (relu) {
+#pragma unroll
+            for (int j = 0; j < 16; ++j) acc[j] = xv[j] > 0 ? acc[j] : (signed char)0;
+        }
+        *(v16c*)(dx + (((int64_t)b * h + iy) * w + ix) * cp + gi * 16) = acc;
+    }
+}
+
+hipError_t maxpool_relu_grad_nhwc16(const int8_t* x, const int8_t* y, const int8_t* dy, int n, int h, int w, int cp,
+                                    int k, int s, int p, int oh, int ow, int relu, int8_t* dx, hipStream_t st) {
+    const int64_t total = (int64_t)n * h * w * (cp / 16);
+    int64_t blocks = (total + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(maxpool_grad_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, y, dy, n, h, w, cp, k, s, p,
+                       oh, ow, relu, dx);
+    return hipGetLastError();
+}
+
+__global__ void relu_grad_kernel(const int8_t* __restrict__ x, const int8_t* __restrict__ dy, int64_t n16,
+                                 int8_t* __restrict__ out) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n16; i += (int64_t)gridDim.x * blockDim.x) {
+        const v16c xv = ((const v16c*)x)[i];
+        const v16c dv = ((const v16c*)dy)[i];
+        v16c o;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) o[j] = xv[j] > 0 ? dv[j] : (signed char)0;
+        ((v16c*)out)[i] = o;
+    }
+}
+
+hipError_t relu_grad_nhwc16(const int8_t* x, const int8_t* dy, int64_t n, int8_t* out, hipStream_t st) {
+    const int64_t n16 = n / 16;
+    int64_t blocks = (n16 + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(relu_grad_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, dy, n16, out);
+    return hipGetLastError();
+}
+
+__device__ __forceinline__ int64_t ipow2_64(int64_t t) { return (int64_t)pow2_x86((int)(t & 31)); }
+
+// NITI_CPULossGrad_Int8.cpp:81-200, one thread per sample.
+__global__ void loss_grad_kernel(const int8_t* __restrict__ logits, int batch, int classes, int ld,
+                                 const int8_t* __restrict__ ascale_p, const int32_t* __restrict__ labels,
+                                 int8_t* __restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= batch) return;
+    const int as = (int)*ascale_p;
+    int64_t o[64];
+    const int8_t* L = logits + (int64_t)i * ld;
+    if (as > -7) {
+        int64_t sv[64];
+        int64_t mx = 0;
+        for (int j = 0; j < classes; ++j) {
+            int64_t t = (int64_t)L[j] * 47274;
+            t = t / (1 << 15);
+            sv[j] = as >= 0 ? t * ipow2_64(as) : t / ipow2_64(-as);
+            if (j == 0 || mx < sv[j]) mx = sv[j];
+        }
+        mx -= 10;
+        for (int j = 0; j < classes; ++j) {
+            int64_t t = sv[j] - mx;
+            t = t > 0 ? t : 0;
+            o[j] = ipow2_64(t) - 1;
+        }
+    } else {
+        const int64_t base = ipow2_64(1 - 2 * (int64_t)as);
+        const int64_t sb = ipow2_64(1 - (int64_t)as);
+        for (int j = 0; j < classes; ++j) {
+            const int64_t t = L[j];
+            o[j] = base + t * sb + t * t;
+        }
+    }
+    int64_t sum = 0;
+    for (int j = 0; j < classes; ++j) sum += o[j];
+    int64_t gs = 0;
+    for (int j = 0; j < classes; ++j) {
+        o[j] = (o[j] * (1 << 11)) / sum;
+        gs += o[j];
+    }
+    const int tgt = labels[i];
+    int8_t* O = out + (int64_t)i * ld;
+    for (int j = 0; j < ld; ++j) {
+        if (j >= classes) {
+            O[j] = 0;
+            continue;
+        }
+        const int32_t gf = (int32_t)(j == tgt ? o[j] - gs : o[j]);
+        O[j] = (int8_t)psto_any(gf, 4);
+    }
+}
+
+hipError_t loss_grad(const int8_t* logits, int batch, int classes, int ld, const int8_t* ascale, const int32_t* labels,
+                     int8_t* out, hipStream_t st) {
+    if (classes > 64 || classes > ld) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(loss_grad_kernel, dim3((batch + 63) / 64), dim3(64), 0, st, logits, batch, classes, ld, ascale,
+                       labels, out);
+    return hipGetLastError();
+}
+
+// =====================================================================================
+// Layout transforms
+// =====================================================================================
+
+// NHWC16 -> CHWN16 through an LDS tile: block = (pixel, 64 images, 64 channels).
+__global__ void nhwc16_to_chwn16_kernel(const int8_t* __restrict__ in, int n, int hw, int cp, int np,
+                                        int8_t* __restrict__ out) {
+    __shared__ int8_t tile[64][64 + 4];
+    const int pix = blockIdx.x;
+    const int n0 = blockIdx.y * 64, c0 = blockIdx.z * 64;
+    const int t = threadIdx.x;
+    {   // read: row = image, 4 x 16B chunks of channels
+        const int r = t >> 2, ch = (t & 3) * 16;
+        v16c v;
+        if (n0 + r < n && c0 + ch < cp)
+            v = *(const v16c*)(in + ((int64_t)(n0 + r) * hw + pix) * cp + c0 + ch);
+        else
+            for (int j = 0; j < 16; ++j) v[j] = 0;
+        for (int j = 0; j < 16; ++j) tile[r][ch + j] = v[j];
+    }
+    __syncthreads();
+    {   // write: row = channel, 4 x 16B chunks of images
+        const int c = t >> 2, nb = (t & 3) * 16;
+        if (c0 + c < cp && n0 + nb < np) {
+            v16c v;
+            for (int j = 0; j < 16; ++j) v[j] = tile[nb + j][c];
+            *(v16c*)(out + ((int64_t)(c0 + c) * hw + pix) * np + n0 + nb) = v;
+        }
+    }
+}
+
+hipError_t nhwc16_to_chwn16(const int8_t* in, int n, int hw, int cp, int np, int8_t* out, hipStream_t st) {
+    dim3 grid(hw, (np + 63) / 64, (cp + 63) / 64);
+    hipLaunchKernelGGL(nhwc16_to_chwn16_kernel, grid, dim3(256), 0, st, in, n, hw, cp, np, out);
+    return hipGetLastError();
+}
+
+struct OhwiToIhwo {
+    const int8_t* w;
+    int co, ci, kk, cip, cop;
+    int8_t* wt;
+    __device__ void operator()(int64_t i) const {  // i over [ci][kk][cop]
+        const int o = (int)(i % cop);
+        const int64_t r = i / cop;
+        const int k = (int)(r % kk);
+        const int c = (int)(r / kk);
+        wt[i] = o < co ? w[((int64_t)o * kk + k) * cip + c] : (int8_t)0;
+    }
+};
+hipError_t ohwi16_to_ihwo16(const int8_t* w, int co, int ci, int kk, int cip, int cop, int8_t* wt, hipStream_t st) {
+    return launch_map((int64_t)ci * kk * cop, OhwiToIhwo{w, co, ci, kk, cip, cop, wt}, st);
+}
+
+struct C4ToNhwc16 {
+    const int8_t* x;
+    int n, c, hw, cp;
+    int8_t* out;
+    __device__ void operator()(int64_t i) const {  // i over [n][hw][cp]
+        const int ch = (int)(i % cp);
+        const int64_t r = i / cp;
+        const int64_t p = r % hw;
+        const int64_t b = r / hw;
+        out[i] = ch < c ? x[(((int64_t)(ch >> 2) * n + b) * hw + p) * 4 + (ch & 3)] : (int8_t)0;
+    }
+};
+hipError_t c4_to_nhwc16(const int8_t* x, int n, int c, int hw, int cp, int8_t* out, hipStream_t st) {
+    return launch_map((int64_t)n * hw * cp, C4ToNhwc16{x, n, c, hw, cp, out}, st);
+}
+
+struct NchwToNhwc16 {
+    const int8_t* x;
+    int n, c, hw, cp;
+    int8_t* out;
+    __device__ void operator()(int64_t i) const {
+        const int ch = (int)(i % cp);
+        const int64_t r = i / cp;
+        const int64_t p = r % hw;
+        const int64_t b = r / hw;
+        out[i] = ch < c ? x[((int64_t)b * c + ch) * hw + p] : (int8_t)0;
+    }
+};
+hipError_t nchw_to_nhwc16(const int8_t* x, int n, int c, int hw, int cp, int8_t* out, hipStream_t st) {
+    return launch_map((int64_t)n * hw * cp, NchwToNhwc16{x, n, c, hw, cp, out}, st);
+}
+
+struct NchwToChwn16 {
+    const int8_t* x;
+    int n, c, hw, cp, np;
+    int8_t* out;
+    __device__ void operator()(int64_t i) const {  // i over [cp][hw][np]
+        const int b = (int)(i % np);
+        const int64_t r = i / np;
+        const int64_t p = r % hw;
+        const int ch = (int)(r / hw);
+        out[i] = (ch < c && b < n) ? x[((int64_t)b * c + ch) * hw + p] : (int8_t)0;
+    }
+};
+hipError_t nchw_to_chwn16(const int8_t* x, int n, int c, int hw, int cp, int np, int8_t* out, hipStream_t st) {
+    return launch_map((int64_t)cp * hw * np, NchwToChwn16{x, n, c, hw, cp, np, out}, st);
+}
+
+struct C4ToChwn16 {
+    const int8_t* x;
+    int n, c, hw, cp, np;
+    int8_t* out;
+    __device__ void operator()(int64_t i) const {
+        const int b = (int)(i % np);
+        const int64_t r = i / np;
+        const int64_t p = r % hw;
+        const int ch = (int)(r / hw);
+        out[i] = (ch < c && b < n) ? x[(((int64_t)(ch >> 2) * n + b) * hw + p) * 4 + (ch & 3)] : (int8_t)0;
+    }
+};
+hipError_t c4_to_chwn16(const int8_t* x, int n, int c, int hw, int cp, int np, int8_t* out, hipStream_t st) {
+    return launch_map((int64_t)cp * hw * np, C4ToChwn16{x, n, c, hw, cp, np, out}, st);
+}
+
+struct Nhwc16ToNchw {
+    const int8_t* x;
+    int n, c, hw, cp;
+    int8_t* out;
+    __device__ void operator()(int64_t i) const {  // i over [n][c][hw]
+        const int64_t p = i % hw;
+        const int64_t r = i / hw;
+        const int ch = (int)(r % c);
+        const int64_t b = r / c;
+        out[i] = x[(b * hw + p) * cp + ch];
+    }
+};
+hipError_t nhwc16_to_nchw(const int8_t* x, int n, int c, int hw, int cp, int8_t* out, hipStream_t st) {
+    return launch_map((int64_t)n * c * hw, Nhwc16ToNchw{x, n, c, hw, cp, out}, st);
+}
+
+struct OihwToOhwi16 {
+    const int8_t* w;
+    int co, ci, kk, cip, rev;
+    int8_t* out;
+    __device__ void operator()(int64_t i) const {  // i over [co][kk][cip]
+        const int c = (int)(i % cip);
+        const int64_t r = i / cip;
+        const int k = (int)(r % kk);
+        const int64_t o = r / kk;
+        const int ks = rev ? kk - 1 - k : k;  // rotate180 == reversing the KH*KW plane
+        out[i] = c < ci ? w[(o * ci + c) * kk + ks] : (int8_t)0;
+    }
+};
+hipError_t oihw_to_ohwi16(const int8_t* w, int co, int ci, int kk, int cip, int8_t* out, hipStream_t st,
+                          bool reverse_taps) {
+    return launch_map((int64_t)co * kk * cip, OihwToOhwi16{w, co, ci, kk, cip, reverse_taps ? 1 : 0, out}, st);
+}
+
+struct OihwToIhwo16 {
+    const int8_t* w;
+    int co, ci, kk, cop;
+    int8_t* out;
+    __device__ void operator()(int64_t i) const {  // i over [ci][kk][cop]
+        const int o = (int)(i % cop);
+        const int64_t r = i / cop;
+        const int k = (int)(r % kk);
+        const int64_t c = r / kk;
+        out[i] = o < co ? w[((int64_t)o * ci + c) * kk + k] : (int8_t)0;
+    }
+};
+hipError_t oihw_to_ihwo16(const int8_t* w, int co, int ci, int kk, int cop, int8_t* out, hipStream_t st) {
+    return launch_map((int64_t)ci * kk * cop, OihwToIhwo16{w, co, ci, kk, cop, out}, st);
+}
+
+struct Ohwi16ToOihw {
+    const int8_t* w;
+    int co, ci, kk, cip;
+    int8_t* out;
+    __device__ void operator()(int64_t i) const {  // i over [co][ci][kk]
+        const int k = (int)(i % kk);
+        const int64_t r = i / kk;
+        const int c = (int)(r % ci);
+        const int64_t o = r / ci;
+        out[i] = w[(o * kk + k) * cip + c];
+    }
+};
+hipError_t ohwi16_to_oihw(const int8_t* w, int co, int ci, int kk, int cip, int8_t* out, hipStream_t st) {
+    return launch_map((int64_t)co * ci * kk, Ohwi16ToOihw{w, co, ci, kk, cip, out}, st);
+}
+
+struct PadRows {
+    const int8_t* in;
+    int rows, cols, ld;
+    int8_t* out;
+    __device__ void operator()(int64_t i) const {
+        const int c = (int)(i % ld);
+        const int64_t r = i / ld;
+        out[i] = c < cols ? in[r * cols + c] : (int8_t)0;
+    }
+};
+hipError_t pad_rows(const int8_t* in, int rows, int cols, int ld, int8_t* out, hipStream_t st) {
+    return launch_map((int64_t)rows * ld, PadRows{in, rows, cols, ld, out}, st);
+}
+
+struct TransposeI32 {
+    const int32_t* in;
+    int rows, cols, ld;
+    int32_t* out;
+    __device__ void operator()(int64_t i) const {  // out [cols][rows]
+        const int r = (int)(i % rows);
+        const int64_t c = i / rows;
+        out[i] = in[(int64_t)r * ld + c];
+    }
+};
+hipError_t transpose_i32(const int32_t* in, int rows, int cols, int ld, int32_t* out, hipStream_t st) {
+    return launch_map((int64_t)rows * cols, TransposeI32{in, rows, cols, ld, out}, st);
+}
+
+}  // namespace niti

@@ -1,0 +1,118 @@
+// niti_kernels.hpp -- internal launch API of the MI355X (gfx950) NITI int8 kernels.
+//
+// Native device layouts (all int8 unless noted; padded lanes are always zero):
+//   NHWC16 activations  [N][H][W][Cp]      Cp = round_up(C, 16)     (fwd / dgrad operand)
+//   CHWN16 activations  [Cp][H][W][Np]     Np = round_up(N, 16)     (wgrad operand: K = (oy,ox,n))
+//   OHWI16 weights      [Co][KH][KW][Cip]                           (fwd B operand, wgrad output)
+//   IHWO16 weights      [Ci][KH][KW][Cop]                           (dgrad B operand)
+//   accumulators        int32 [rows][ld] with ld a multiple of 16
+// The reference's layouts (MNN C4 [C/4][N][H][W][4], NCHW, OIHW) only appear at the
+// drop-in boundary (niti_execution.hip) and are converted by the kernels declared at
+// the end of this file.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace niti {
+
+inline int round_up(int x, int m) { return (x + m - 1) / m * m; }
+
+struct ConvGeom {
+    int n, c_in, h, w;
+    int c_out, kh, kw;
+    int sh, sw, pt, pl, pb, pr, dh, dw;
+    int oh, ow;
+    int cip, cop, np;  // padded channel / batch counts (multiples of 16)
+    // fills oh/ow/cip/cop/np; returns false on an invalid geometry
+    bool finalize();
+};
+
+// Exponent rules (NITI_Conv_Int8.cpp:260-307 / NITI_GradientConv_Int8.cpp:272-296 /
+// NITI_Matmul_Int8.cpp:214-228).
+enum GradRule { RULE_WGRAD_BW2 = 2, RULE_MATMUL_BW3 = 3 };
+
+// ---- GEMM-class accumulation (int8 MFMA v_mfma_i32_32x32x32_i8, exact int32) ----------
+// acc[M = n*oh*ow][cop] = conv(x, w);  atomically max-es |acc| into *amax (caller zeroes it).
+hipError_t conv_fwd_acc(const ConvGeom& g, const int8_t* x_nhwc16, const int8_t* w_ohwi16,
+                        int32_t* acc, uint32_t* amax, hipStream_t st);
+// acc[M = n*h*w][cip] = transposed conv of dy with w (input gradient), |acc| max into *amax.
+hipError_t conv_dgrad_acc(const ConvGeom& g, const int8_t* dy_nhwc16, const int8_t* wt_ihwo16,
+                          int32_t* acc, uint32_t* amax, hipStream_t st);
+// acc[co][kh][kw][cip] = sum over (n, oy, ox) of dy * x (weight gradient).  Zeroes acc
+// (unless zero=false: the caller did), then split-K accumulates with int32 atomics (exact
+// and order independent).
+hipError_t conv_wgrad_acc(const ConvGeom& g, const int8_t* x_chwn16, const int8_t* dy_chwn16,
+                          int32_t* acc, hipStream_t st, bool zero = true);
+// acc[m][o] = sum_k B[m][k] * A[o][k] (NITI_Matmul_Int8).  k16 = K rounded up to 16 (rows are
+// zero padded), ldb/lda in bytes (multiples of 16), ldc in elements (multiple of 16).
+// accumulate=true adds with atomics into a zeroed acc (split-K), else stores and max-es |acc|.
+hipError_t matmul_acc(int M, int O, int k16, const int8_t* B, int64_t ldb, const int8_t* A,
+                      int64_t lda, int32_t* acc, int64_t ldc, uint32_t* amax, bool split_k,
+                      hipStream_t st);
+
+// ---- range estimate + requantisation ----------------------------------------------------
+hipError_t absmax_i32(const int32_t* a, int64_t n, uint32_t* amax, hipStream_t st);
+
+struct ActRequant {
+    const int32_t* acc = nullptr;  // [rows][ldc]
+    int64_t rows = 0;
+    int ldc = 0;                   // multiple of 16 (the padded channel count)
+    const uint32_t* amax = nullptr;
+    // exponent bookkeeping (device int8 scalars); exp_out = exp_in + wscale + inc
+    const int8_t* exp_in = nullptr;
+    const int8_t* wscale = nullptr;
+    int8_t* exp_out = nullptr;
+    int relu = 0;                     // fused NITI_Relu_Int8 (forward)
+    const int8_t* relu_mask = nullptr;  // fused NITI_ReluGrad_Int8: out = mask > 0 ? q : 0 (NHWC16)
+    int8_t* out_nhwc16 = nullptr;     // [rows][ldc]
+    // optional reference-layout copy: MNN C4 [ceil(C/4)][N][HW][4]; rows = N*HW
+    int8_t* out_c4 = nullptr;
+    int c_real = 0, n = 0, hw = 0;
+};
+hipError_t requant_act(const ActRequant& r, hipStream_t st);
+
+// Gradient rule: bw==0 -> 0, else PSTO(bw - rule).  Optional fused NITI_SGD update
+// w <- clip(w - g, +-127) (NITI_SGD.hpp:49-52, BinaryUtils.hpp:278-299).
+hipError_t requant_grad(const int32_t* acc, int64_t n, const uint32_t* amax, int rule, int8_t* g_out,
+                        int8_t* w_update, hipStream_t st);
+
+// ---- the rest of the NITI step -----------------------------------------
+hipError_t maxpool_nhwc16(const int8_t* x, int n, int h, int w, int cp, int k, int s, int p, int8_t* y,
+                          int oh, int ow, hipStream_t st);
+// dx = maxpool_grad(x, y, dy) then, if relu, dx = x > 0 ? dx : 0 (x is the relu output)
+hipError_t maxpool_relu_grad_nhwc16(const int8_t* x, const int8_t* y, const int8_t* dy, int n, int h,
+                                    int w, int cp, int k, int s, int p, int oh, int ow, int relu,
+                                    int8_t* dx, hipStream_t st);
+hipError_t relu_grad_nhwc16(const int8_t* x, const int8_t* dy, int64_t n, int8_t* out, hipStream_t st);
+// logits int8 [batch][ld] (first `classes` used), labels int32 [batch] (class index);
+// out int8 [batch][ld] (padded lanes zeroed).  NITI_CPULossGrad_Int8.cpp:81-200.
+hipError_t loss_grad(const int8_t* logits, int batch, int classes, int ld, const int8_t* ascale,
+                     const int32_t* labels, int8_t* out, hipStream_t st);
+
+// ---- layout transforms --------------------------------------------------------------------
+// NHWC16 [N][H][W][Cp] -> CHWN16 [Cp][H][W][Np]
+hipError_t nhwc16_to_chwn16(const int8_t* in, int n, int hw, int cp, int np, int8_t* out, hipStream_t st);
+// OHWI16 [Co][KK][Cip] -> IHWO16 [Ci][KK][Cop]
+hipError_t ohwi16_to_ihwo16(const int8_t* w, int co, int ci, int kk, int cip, int cop, int8_t* wt,
+                            hipStream_t st);
+// reference-layout conversions (drop-in boundary)
+hipError_t c4_to_nhwc16(const int8_t* x_c4, int n, int c, int hw, int cp, int8_t* out, hipStream_t st);
+hipError_t nchw_to_nhwc16(const int8_t* x, int n, int c, int hw, int cp, int8_t* out, hipStream_t st);
+hipError_t nchw_to_chwn16(const int8_t* x, int n, int c, int hw, int cp, int np, int8_t* out,
+                          hipStream_t st);
+hipError_t c4_to_chwn16(const int8_t* x_c4, int n, int c, int hw, int cp, int np, int8_t* out,
+                        hipStream_t st);
+hipError_t nhwc16_to_nchw(const int8_t* x, int n, int c, int hw, int cp, int8_t* out, hipStream_t st);
+// reverse_taps: NITI_DeConv_Int8's rotate180 (NITI_DeConv_Int8.cpp:179-184) reverses each KH*KW plane
+hipError_t oihw_to_ohwi16(const int8_t* w, int co, int ci, int kk, int cip, int8_t* out, hipStream_t st,
+                          bool reverse_taps = false);
+hipError_t oihw_to_ihwo16(const int8_t* w, int co, int ci, int kk, int cop, int8_t* out, hipStream_t st);
+// OHWI16 int8 -> OIHW (drop the channel padding)
+hipError_t ohwi16_to_oihw(const int8_t* w, int co, int ci, int kk, int cip, int8_t* out, hipStream_t st);
+// row-major [rows][cols] int8 -> zero-padded [rows][ld] (ld multiple of 16)
+hipError_t pad_rows(const int8_t* in, int rows, int cols, int ld, int8_t* out, hipStream_t st);
+// [rows][ld] int32 -> transpose [cols][rows] int32 (cols <= ld)
+hipError_t transpose_i32(const int32_t* in, int rows, int cols, int ld, int32_t* out, hipStream_t st);
+
+}  // namespace niti

@@ -1,0 +1,494 @@
+// niti_model.hip -- device-resident NITI int8 training step (+ RCCL data parallelism).
+//
+// One NITI_SGD step of the reference's NITIInt8Train (execution-engine/tools/train/source/
+// demo/MnistUtils.cpp:68-147, optimizer/NITI_SGD.hpp:20-54) executed entirely on the GPU:
+//   forward   : per layer NITI_Conv_Int8 (+ NITI_Relu_Int8, NITI_Maxpool_Int8)
+//   loss      : NITI_LOSS_Grad_Int8 (NITI_CPULossGrad_Int8.cpp:81-200)
+//   backward  : grad/NITI_Conv_Int8_Grad.cpp -- NITI_GradientCONV_Int8 (weight gradient) and
+//               NITI_DeCONV_Int8 (input gradient, skipped for the first layer exactly as the
+//               lazy reference graph skips it), pool / relu gradients
+//   update    : w <- clip(w - g, +-127)  (NITI_SGD.hpp:49-52)
+// With an RCCL communicator (exact mode) every forward / input-gradient range is
+// all-reduced with MAX and every int32 weight-gradient accumulator with SUM before it is
+// requantised, so N ranks of batch b reproduce one device of batch N*b bit for bit.
+#include <rccl/rccl.h>
+#include <string.h>
+
+#include <memory>
+#include <vector>
+
+#include "../../include/niti_hip.h"
+#include "niti_internal.hpp"
+#include "niti_kernels.hpp"
+#include "niti_map.hpp"
+
+namespace niti {
+
+namespace {
+
+// NCHW flatten of a pooled NHWC16 map: out[n][c*HW + p] = in[n][p][c] (c < C); LeNet's
+// _Reshape(x, {0, -1, 1, 1}) after _Convert(x, NCHW) (mnistTrain.cpp:175-176).
+struct FlattenFwd {
+    const int8_t* in;
+    int hw, c, cp, ldo;
+    int8_t* out;
+    __device__ void operator()(int64_t i) const {  // i over [n][ldo]
+        const int64_t b = i / ldo;
+        const int j = (int)(i - b * ldo);
+        const int ch = j / hw, p = j - ch * hw;
+        out[i] = ch < c ? in[(b * hw + p) * cp + ch] : (int8_t)0;
+    }
+};
+struct FlattenBwd {
+    const int8_t* dout;
+    int hw, c, cp, ldo;
+    int8_t* din;
+    __device__ void operator()(int64_t i) const {  // i over [n][hw][cp]
+        const int ch = (int)(i % cp);
+        const int64_t r = i / cp;
+        const int p = (int)(r % hw);
+        const int64_t b = r / hw;
+        din[i] = ch < c ? dout[b * ldo + ch * hw + p] : (int8_t)0;
+    }
+};
+
+}  // namespace
+
+struct Layer {
+    ConvGeom g{};
+    int relu = 0, pool = 0, flatten = 0;
+    int ph = 0, pw = 0;      // pooled size
+    int8_t wscale = 0;
+    // persistent
+    int8_t* w = nullptr;     // OHWI16
+    int8_t* ws_dev = nullptr;  // wscale scalar
+    // per step
+    int8_t* wT = nullptr;    // IHWO16
+    int8_t* r = nullptr;     // conv (+relu) output NHWC16 [n][oh][ow][cop]
+    int8_t* p = nullptr;     // pooled NHWC16
+    int8_t* flat = nullptr;  // flattened NHWC16 [n][1][1][c*ph*pw]
+    int8_t* xT = nullptr;    // input CHWN16
+    int8_t* dy = nullptr;    // output gradient NHWC16 [n][oh][ow][cop]
+    int8_t* dyT = nullptr;   // CHWN16
+    int8_t* dtmp = nullptr;  // gradient wrt the pooled / flattened output
+    int8_t* dflat = nullptr;
+    int32_t* dwacc = nullptr;  // [co][kk][cip]
+    int8_t* g8 = nullptr;    // int8 weight gradient OHWI16
+    int8_t* exp = nullptr;   // exponent of this layer's output
+    const int8_t* in = nullptr;  // NHWC16 input (previous output or x0)
+    int64_t w_elems() const { return (int64_t)g.c_out * g.kh * g.kw * g.cip; }
+    int64_t macs() const { return (int64_t)g.n * g.oh * g.ow * g.c_out * g.c_in * g.kh * g.kw; }
+};
+
+struct Model {
+    int arch = 0, batch = 0, in_c = 0, in_h = 0, in_w = 0, classes = 10;
+    std::vector<Layer> L;
+    Workspace ws;
+    int8_t* x0 = nullptr;   // NHWC16 input
+    int8_t* exp0 = nullptr; // input exponent
+    int32_t* acc = nullptr; // shared fwd / dgrad accumulator
+    uint32_t* amax = nullptr;
+    size_t amax_bytes = 0;
+    ncclComm_t comm = nullptr;
+    int world = 1, rank = 0, exact = 1;
+    // hipGraph of one step
+    hipGraphExec_t graph = nullptr;
+    // kernel probe: HIP events around one GEMM (layer, phase 0 fwd / 1 dgrad / 2 wgrad)
+    int probe_layer = -1, probe_phase = -1, probe_count = 0;
+    std::vector<hipEvent_t> ev0, ev1;
+    void probe(int layer, int phase, bool begin, hipStream_t st) {
+        if (layer != probe_layer || phase != probe_phase || probe_count >= (int)ev0.size()) return;
+        if (begin) {
+            (void)hipEventRecord(ev0[probe_count], st);
+        } else {
+            (void)hipEventRecord(ev1[probe_count], st);
+            ++probe_count;
+        }
+    }
+    void clear_probe() {
+        for (auto e : ev0) (void)hipEventDestroy(e);
+        for (auto e : ev1) (void)hipEventDestroy(e);
+        ev0.clear();
+        ev1.clear();
+        probe_count = 0;
+        probe_layer = probe_phase = -1;
+    }
+
+    int build(int arch_, int batch_);
+    int step(const int8_t* x_nchw, int exp_in, const int32_t* labels, hipStream_t st);
+    ~Model() {
+        clear_probe();
+        if (graph) (void)hipGraphExecDestroy(graph);
+        if (comm) (void)ncclCommDestroy(comm);
+    }
+};
+
+static void add_conv(Model& m, int ci, int co, int k, int pad, int h, int relu, int pool, int flatten = 0) {
+    Layer l;
+    l.g.n = m.batch;
+    l.g.c_in = ci;
+    l.g.h = l.g.w = h;
+    l.g.c_out = co;
+    l.g.kh = l.g.kw = k;
+    l.g.sh = l.g.sw = 1;
+    l.g.pt = l.g.pl = l.g.pb = l.g.pr = pad;
+    l.g.dh = l.g.dw = 1;
+    l.g.finalize();
+    l.relu = relu;
+    l.pool = pool;
+    l.flatten = flatten;
+    if (pool) {
+        l.ph = (l.g.oh - 2) / 2 + 1;
+        l.pw = (l.g.ow - 2) / 2 + 1;
+    }
+    m.L.push_back(l);
+}
+
+int Model::build(int arch_, int batch_) {
+    arch = arch_;
+    batch = batch_;
+    if (arch == NITI_ARCH_LENET) {  // mnistTrain.cpp:131-181
+        in_c = 1;
+        in_h = in_w = 28;
+        add_conv(*this, 1, 20, 5, 0, 28, 1, 1);
+        add_conv(*this, 20, 52, 5, 0, 12, 1, 1, /*flatten=*/1);
+        add_conv(*this, 832, 500, 1, 0, 1, 1, 0);
+        add_conv(*this, 500, 12, 1, 0, 1, 0, 0);
+    } else if (arch == NITI_ARCH_VGG11) {  // VGG-11 for 32x32 inputs, NITI layers (BASELINE cfg 3)
+        in_c = 3;
+        in_h = in_w = 32;
+        add_conv(*this, 3, 64, 3, 1, 32, 1, 1);
+        add_conv(*this, 64, 128, 3, 1, 16, 1, 1);
+        add_conv(*this, 128, 256, 3, 1, 8, 1, 0);
+        add_conv(*this, 256, 256, 3, 1, 8, 1, 1);
+        add_conv(*this, 256, 512, 3, 1, 4, 1, 0);
+        add_conv(*this, 512, 512, 3, 1, 4, 1, 1);
+        add_conv(*this, 512, 512, 3, 1, 2, 1, 0);
+        add_conv(*this, 512, 512, 3, 1, 2, 1, 1);
+        add_conv(*this, 512, 12, 1, 0, 1, 0, 0);
+    } else {
+        return NITI_NOT_SUPPORT;
+    }
+    const int n = batch;
+    x0 = (int8_t*)ws.alloc((size_t)n * in_h * in_w * round_up(in_c, 16));
+    exp0 = (int8_t*)ws.alloc(16);
+    size_t acc_elems = 0;
+    const int nl = (int)L.size();
+    for (int i = 0; i < nl; ++i) {
+        Layer& l = L[i];
+        const ConvGeom& g = l.g;
+        const size_t out_px = (size_t)n * g.oh * g.ow;
+        l.w = (int8_t*)ws.alloc(l.w_elems());
+        l.ws_dev = (int8_t*)ws.alloc(16);
+        l.wT = (int8_t*)ws.alloc((size_t)g.c_in * g.kh * g.kw * g.cop);
+        l.r = (int8_t*)ws.alloc(out_px * g.cop);
+        if (l.pool) {
+            l.p = (int8_t*)ws.alloc((size_t)n * l.ph * l.pw * g.cop);
+            l.dtmp = (int8_t*)ws.alloc((size_t)n * l.ph * l.pw * g.cop);
+        }
+        if (l.flatten) {
+            const int fc = g.c_out * l.ph * l.pw;
+            l.flat = (int8_t*)ws.alloc((size_t)n * round_up(fc, 16));
+            l.dflat = (int8_t*)ws.alloc((size_t)n * round_up(fc, 16));
+        }
+        l.xT = (int8_t*)ws.alloc((size_t)g.cip * g.h * g.w * g.np);
+        l.dy = (int8_t*)ws.alloc(out_px * g.cop);
+        l.dyT = (int8_t*)ws.alloc((size_t)g.cop * g.oh * g.ow * g.np);
+        l.dwacc = (int32_t*)ws.alloc(l.w_elems() * 4);
+        l.g8 = (int8_t*)ws.alloc(l.w_elems());
+        l.exp = (int8_t*)ws.alloc(16);
+        if (!l.w || !l.ws_dev || !l.wT || !l.r || !l.xT || !l.dy || !l.dyT || !l.dwacc || !l.g8 || !l.exp)
+            return NITI_OUT_OF_MEMORY;
+        if (hipMemset(l.w, 0, l.w_elems()) != hipSuccess) return NITI_NO_EXECUTION;
+        if (hipMemset(l.ws_dev, 0, 16) != hipSuccess) return NITI_NO_EXECUTION;
+        acc_elems = std::max(acc_elems, out_px * g.cop);
+        acc_elems = std::max(acc_elems, (size_t)n * g.h * g.w * g.cip);
+        // layer input / its C alignment with the previous output
+        if (i == 0) {
+            l.in = x0;
+        } else {
+            const Layer& pr = L[i - 1];
+            l.in = pr.flatten ? pr.flat : (pr.pool ? pr.p : pr.r);
+        }
+    }
+    acc = (int32_t*)ws.alloc(acc_elems * 4);
+    amax_bytes = (size_t)round_up(3 * nl, 4) * 4;
+    amax = (uint32_t*)ws.alloc(amax_bytes);
+    if (!x0 || !exp0 || !acc || !amax) return NITI_OUT_OF_MEMORY;
+    if (hipMemset(x0, 0, (size_t)n * in_h * in_w * round_up(in_c, 16)) != hipSuccess) return NITI_NO_EXECUTION;
+    return hipDeviceSynchronize() == hipSuccess ? NITI_NO_ERROR : NITI_NO_EXECUTION;
+}
+
+#define MTRY(expr)                                             \
+    do {                                                       \
+        if ((expr) != hipSuccess) return NITI_NO_EXECUTION;    \
+    } while (0)
+#define CTRY(expr)                                             \
+    do {                                                       \
+        if ((expr) != ncclSuccess) return NITI_NO_EXECUTION;   \
+    } while (0)
+
+int Model::step(const int8_t* x_nchw, int exp_in, const int32_t* labels, hipStream_t st) {
+    const int n = batch;
+    const int nl = (int)L.size();
+    const bool dp = comm != nullptr && world > 1;
+    MTRY(hipMemsetAsync(amax, 0, amax_bytes, st));
+    MTRY(hipMemsetAsync(exp0, exp_in, 1, st));
+    MTRY(nchw_to_nhwc16(x_nchw, n, in_c, in_h * in_w, round_up(in_c, 16), x0, st));
+    // ------------------------------------------------------------------ forward
+    for (int i = 0; i < nl; ++i) {
+        Layer& l = L[i];
+        const ConvGeom& g = l.g;
+        probe(i, 0, true, st);
+        MTRY(conv_fwd_acc(g, l.in, l.w, acc, amax + 3 * i, st));
+        probe(i, 0, false, st);
+        if (dp && exact) CTRY(ncclAllReduce(amax + 3 * i, amax + 3 * i, 1, ncclUint32, ncclMax, comm, st));
+        ActRequant r;
+        r.acc = acc;
+        r.rows = (int64_t)n * g.oh * g.ow;
+        r.ldc = g.cop;
+        r.amax = amax + 3 * i;
+        r.exp_in = i == 0 ? exp0 : L[i - 1].exp;
+        r.wscale = l.ws_dev;
+        r.exp_out = l.exp;
+        r.relu = l.relu;
+        r.out_nhwc16 = l.r;
+        MTRY(requant_act(r, st));
+        if (l.pool) MTRY(maxpool_nhwc16(l.r, n, g.oh, g.ow, g.cop, 2, 2, 0, l.p, l.ph, l.pw, st));
+        if (l.flatten) {
+            const int fc = g.c_out * l.ph * l.pw, ld = round_up(fc, 16);
+            MTRY(launch_map((int64_t)n * ld, FlattenFwd{l.p, l.ph * l.pw, g.c_out, g.cop, ld, l.flat}, st));
+        }
+    }
+    // ------------------------------------------------------------------ loss gradient
+    {
+        Layer& t = L[nl - 1];
+        MTRY(loss_grad(t.r, n, t.g.c_out, t.g.cop, t.exp, labels, t.dy, st));
+    }
+    // ------------------------------------------------------------------ backward
+    for (int i = nl - 1; i >= 0; --i) {
+        Layer& l = L[i];
+        const ConvGeom& g = l.g;
+        const int64_t we = l.w_elems();
+        MTRY(nhwc16_to_chwn16(l.in, n, g.h * g.w, g.cip, g.np, l.xT, st));
+        MTRY(nhwc16_to_chwn16(l.dy, n, g.oh * g.ow, g.cop, g.np, l.dyT, st));
+        MTRY(hipMemsetAsync(l.dwacc, 0, (size_t)we * sizeof(int32_t), st));
+        probe(i, 2, true, st);
+        MTRY(conv_wgrad_acc(g, l.xT, l.dyT, l.dwacc, st, /*zero=*/false));
+        probe(i, 2, false, st);
+        if (dp) CTRY(ncclAllReduce(l.dwacc, l.dwacc, (size_t)we, ncclInt32, ncclSum, comm, st));
+        if (i > 0) {
+            Layer& pv = L[i - 1];
+            MTRY(ohwi16_to_ihwo16(l.w, g.c_out, g.c_in, g.kh * g.kw, g.cip, g.cop, l.wT, st));
+            probe(i, 1, true, st);
+            MTRY(conv_dgrad_acc(g, l.dy, l.wT, acc, amax + 3 * i + 1, st));
+            probe(i, 1, false, st);
+            if (dp && exact) CTRY(ncclAllReduce(amax + 3 * i + 1, amax + 3 * i + 1, 1, ncclUint32, ncclMax, comm, st));
+            ActRequant r;
+            r.acc = acc;
+            r.rows = (int64_t)n * g.h * g.w;
+            r.ldc = g.cip;
+            r.amax = amax + 3 * i + 1;
+            const ConvGeom& pg = pv.g;
+            if (pv.flatten) {
+                r.out_nhwc16 = pv.dflat;
+                MTRY(requant_act(r, st));
+                const int fc = pg.c_out * pv.ph * pv.pw, ld = round_up(fc, 16);
+                MTRY(launch_map((int64_t)n * pv.ph * pv.pw * pg.cop,
+                                FlattenBwd{pv.dflat, pv.ph * pv.pw, pg.c_out, pg.cop, ld, pv.dtmp}, st));
+                MTRY(maxpool_relu_grad_nhwc16(pv.r, pv.p, pv.dtmp, n, pg.oh, pg.ow, pg.cop, 2, 2, 0, pv.ph, pv.pw,
+                                              pv.relu, pv.dy, st));
+            } else if (pv.pool) {
+                r.out_nhwc16 = pv.dtmp;
+                MTRY(requant_act(r, st));
+                MTRY(maxpool_relu_grad_nhwc16(pv.r, pv.p, pv.dtmp, n, pg.oh, pg.ow, pg.cop, 2, 2, 0, pv.ph, pv.pw,
+                                              pv.relu, pv.dy, st));
+            } else {
+                r.relu_mask = pv.relu ? pv.r : nullptr;
+                r.out_nhwc16 = pv.dy;
+                MTRY(requant_act(r, st));
+            }
+        }
+        MTRY(absmax_i32(l.dwacc, we, amax + 3 * i + 2, st));
+        MTRY(requant_grad(l.dwacc, we, amax + 3 * i + 2, RULE_WGRAD_BW2, l.g8, l.w, st));
+    }
+    return NITI_NO_ERROR;
+}
+
+}  // namespace niti
+
+// =========================================================================== C ABI (section 3)
+struct niti_model {
+    niti::Model m;
+};
+
+extern "C" {
+
+int niti_model_create(int arch, int batch, niti_model_t* out) {
+    if (!out || batch <= 0) return NITI_INVALID_VALUE;
+    auto* h = new niti_model();
+    const int rc = h->m.build(arch, batch);
+    if (rc != NITI_NO_ERROR) {
+        delete h;
+        return rc;
+    }
+    *out = h;
+    return NITI_NO_ERROR;
+}
+
+void niti_model_destroy(niti_model_t m) { delete m; }
+
+int niti_model_num_layers(niti_model_t m) { return m ? (int)m->m.L.size() : 0; }
+
+int niti_model_layer_info(niti_model_t m, int layer, int info[12]) {
+    if (!m || layer < 0 || layer >= (int)m->m.L.size()) return NITI_INVALID_VALUE;
+    const niti::Layer& l = m->m.L[layer];
+    const int v[12] = {l.g.c_in, l.g.c_out, l.g.kh, l.g.kw, l.g.h, l.g.w, l.g.oh, l.g.ow, l.g.pt, l.g.sh, l.relu, l.pool};
+    memcpy(info, v, sizeof(v));
+    return NITI_NO_ERROR;
+}
+
+int niti_model_set_weight(niti_model_t m, int layer, const int8_t* w_host, int wscale) {
+    if (!m || layer < 0 || layer >= (int)m->m.L.size() || !w_host) return NITI_INVALID_VALUE;
+    niti::Layer& l = m->m.L[layer];
+    const size_t n = (size_t)l.g.c_out * l.g.c_in * l.g.kh * l.g.kw;
+    int8_t* tmp = nullptr;
+    if (hipMalloc(&tmp, n) != hipSuccess) return NITI_OUT_OF_MEMORY;
+    int rc = NITI_NO_ERROR;
+    if (hipMemcpy(tmp, w_host, n, hipMemcpyHostToDevice) != hipSuccess ||
+        niti::oihw_to_ohwi16(tmp, l.g.c_out, l.g.c_in, l.g.kh * l.g.kw, l.g.cip, l.w, nullptr) != hipSuccess ||
+        hipMemset(l.ws_dev, (int)(int8_t)wscale, 1) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+        rc = NITI_NO_EXECUTION;
+    l.wscale = (int8_t)wscale;
+    (void)hipFree(tmp);
+    return rc;
+}
+
+int niti_model_get_weight(niti_model_t m, int layer, int8_t* w_host) {
+    if (!m || layer < 0 || layer >= (int)m->m.L.size() || !w_host) return NITI_INVALID_VALUE;
+    niti::Layer& l = m->m.L[layer];
+    const size_t n = (size_t)l.g.c_out * l.g.c_in * l.g.kh * l.g.kw;
+    int8_t* tmp = nullptr;
+    if (hipDeviceSynchronize() != hipSuccess || hipMalloc(&tmp, n) != hipSuccess) return NITI_OUT_OF_MEMORY;
+    int rc = NITI_NO_ERROR;
+    if (niti::ohwi16_to_oihw(l.w, l.g.c_out, l.g.c_in, l.g.kh * l.g.kw, l.g.cip, tmp, nullptr) != hipSuccess ||
+        hipMemcpy(w_host, tmp, n, hipMemcpyDeviceToHost) != hipSuccess)
+        rc = NITI_NO_EXECUTION;
+    (void)hipFree(tmp);
+    return rc;
+}
+
+int niti_model_train_step(niti_model_t m, const int8_t* x_nchw, int exp_in, const int32_t* labels, void* stream) {
+    if (!m || !x_nchw || !labels) return NITI_INVALID_VALUE;
+    return m->m.step(x_nchw, exp_in, labels, (hipStream_t)stream);
+}
+
+int niti_model_get_logits(niti_model_t m, int8_t* logits_host, int* exp_out, void* stream) {
+    if (!m) return NITI_INVALID_VALUE;
+    niti::Layer& t = m->m.L.back();
+    const int n = m->m.batch;
+    if (hipStreamSynchronize((hipStream_t)stream) != hipSuccess) return NITI_NO_EXECUTION;
+    std::vector<int8_t> buf((size_t)n * t.g.cop);
+    int8_t e = 0;
+    if (hipMemcpy(buf.data(), t.r, buf.size(), hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(&e, t.exp, 1, hipMemcpyDeviceToHost) != hipSuccess)
+        return NITI_NO_EXECUTION;
+    for (int i = 0; i < n; ++i) memcpy(logits_host + (size_t)i * t.g.c_out, buf.data() + (size_t)i * t.g.cop, t.g.c_out);
+    if (exp_out) *exp_out = e;
+    return NITI_NO_ERROR;
+}
+
+int niti_model_get_tap(niti_model_t m, int layer, int which, int8_t* host, size_t bytes, void* stream) {
+    if (!m || layer < 0 || layer >= (int)m->m.L.size()) return NITI_INVALID_VALUE;
+    niti::Layer& l = m->m.L[layer];
+    const niti::ConvGeom& g = l.g;
+    const int n = m->m.batch;
+    if (hipStreamSynchronize((hipStream_t)stream) != hipSuccess) return NITI_NO_EXECUTION;
+    int8_t* tmp = nullptr;
+    size_t need = 0;
+    if (which == 0 || which == 2)
+        need = (size_t)n * g.c_out * g.oh * g.ow;
+    else if (which == 1)
+        need = (size_t)g.c_out * g.c_in * g.kh * g.kw;
+    else
+        return NITI_INVALID_VALUE;
+    if (bytes < need) return NITI_INVALID_VALUE;
+    if (hipMalloc(&tmp, need) != hipSuccess) return NITI_OUT_OF_MEMORY;
+    hipError_t e;
+    if (which == 0)
+        e = niti::nhwc16_to_nchw(l.r, n, g.c_out, g.oh * g.ow, g.cop, tmp, nullptr);
+    else if (which == 2)
+        e = niti::nhwc16_to_nchw(l.dy, n, g.c_out, g.oh * g.ow, g.cop, tmp, nullptr);
+    else
+        e = niti::ohwi16_to_oihw(l.g8, g.c_out, g.c_in, g.kh * g.kw, g.cip, tmp, nullptr);
+    if (e == hipSuccess) e = hipMemcpy(host, tmp, need, hipMemcpyDeviceToHost);
+    (void)hipFree(tmp);
+    return e == hipSuccess ? NITI_NO_ERROR : NITI_NO_EXECUTION;
+}
+
+int64_t niti_model_step_macs(niti_model_t m) {
+    if (!m) return 0;
+    int64_t s = 0;
+    const int world = m->m.world > 0 ? m->m.world : 1;
+    for (size_t i = 0; i < m->m.L.size(); ++i) {
+        const int64_t f = m->m.L[i].macs();
+        s += f;            // forward
+        s += f;            // weight gradient
+        if (i > 0) s += f; // input gradient
+    }
+    (void)world;
+    return s;
+}
+
+int niti_model_set_probe(niti_model_t m, int layer, int phase, int max_launches) {
+    if (!m || max_launches < 0) return NITI_INVALID_VALUE;
+    m->m.clear_probe();
+    if (layer < 0) return NITI_NO_ERROR;
+    m->m.probe_layer = layer;
+    m->m.probe_phase = phase;
+    m->m.ev0.resize(max_launches);
+    m->m.ev1.resize(max_launches);
+    for (int i = 0; i < max_launches; ++i)
+        if (hipEventCreate(&m->m.ev0[i]) != hipSuccess || hipEventCreate(&m->m.ev1[i]) != hipSuccess)
+            return NITI_OUT_OF_MEMORY;
+    return NITI_NO_ERROR;
+}
+
+int niti_model_probe_read(niti_model_t m, double* total_ms, int* count) {
+    if (!m || !total_ms || !count) return NITI_INVALID_VALUE;
+    double t = 0;
+    for (int i = 0; i < m->m.probe_count; ++i) {
+        float ms = 0.f;
+        if (hipEventSynchronize(m->m.ev1[i]) != hipSuccess ||
+            hipEventElapsedTime(&ms, m->m.ev0[i], m->m.ev1[i]) != hipSuccess)
+            return NITI_NO_EXECUTION;
+        t += ms;
+    }
+    *total_ms = t;
+    *count = m->m.probe_count;
+    m->m.probe_count = 0;
+    return NITI_NO_ERROR;
+}
+
+int niti_dp_get_unique_id(char id[NITI_UNIQUE_ID_BYTES]) {
+    static_assert(sizeof(ncclUniqueId) == NITI_UNIQUE_ID_BYTES, "ncclUniqueId size");
+    ncclUniqueId u;
+    if (ncclGetUniqueId(&u) != ncclSuccess) return NITI_NO_EXECUTION;
+    memcpy(id, &u, sizeof(u));
+    return NITI_NO_ERROR;
+}
+
+int niti_model_attach_comm(niti_model_t m, const char id[NITI_UNIQUE_ID_BYTES], int rank, int world, int exact) {
+    if (!m || world < 1 || rank < 0 || rank >= world) return NITI_INVALID_VALUE;
+    ncclUniqueId u;
+    memcpy(&u, id, sizeof(u));
+    ncclComm_t c = nullptr;
+    if (ncclCommInitRank(&c, world, u, rank) != ncclSuccess) return NITI_NO_EXECUTION;
+    m->m.comm = c;
+    m->m.world = world;
+    m->m.rank = rank;
+    m->m.exact = exact ? 1 : 0;
+    return NITI_NO_ERROR;
+}
+
+}  // extern "C"

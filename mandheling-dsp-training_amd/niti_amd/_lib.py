@@ -1,0 +1,123 @@
+"""ctypes binding of libniti_hip.so (the C ABI declared in include/niti_hip.h).
+
+There is no fallback: if the HIP library is missing the import fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_lib", "libniti_hip.so")
+HEADER = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "include", "niti_hip.h")
+
+# MNN::ErrorCode names (include/MNN/ErrorCode.hpp:17-30)
+ERROR_NAMES = {0: "NO_ERROR", 1: "OUT_OF_MEMORY", 2: "NOT_SUPPORT", 3: "COMPUTE_SIZE_ERROR",
+               4: "NO_EXECUTION", 5: "INVALID_VALUE", 10: "INPUT_DATA_ERROR", 11: "CALL_BACK_STOP"}
+
+OP_CONV_INT8 = 700
+OP_DECONV_INT8 = 701
+OP_MATMUL_INT8 = 713
+OP_GRADIENT_CONV_INT8 = 715
+OP_DSP_MATMUL_GRADIENT_INT8 = 818
+FORMAT_NCHW, FORMAT_NHWC, FORMAT_NC4HW4 = 0, 1, 2
+PAD_CAFFE, PAD_VALID, PAD_SAME = 0, 1, 2
+ARCH_LENET, ARCH_VGG11 = 1, 2
+
+
+class NitiError(RuntimeError):
+    def __init__(self, code, what=""):
+        self.code = code
+        super().__init__(f"{what}: {ERROR_NAMES.get(code, code)}")
+
+
+class Tensor(C.Structure):
+    _fields_ = [("data", C.c_void_p), ("dims", C.c_int * 4), ("format", C.c_int)]
+
+
+class ConvCommon(C.Structure):
+    _fields_ = [("kernel_x", C.c_int), ("kernel_y", C.c_int), ("stride_x", C.c_int), ("stride_y", C.c_int),
+                ("dilate_x", C.c_int), ("dilate_y", C.c_int), ("pad_x", C.c_int), ("pad_y", C.c_int),
+                ("has_pads", C.c_int), ("pads", C.c_int * 4), ("pad_mode", C.c_int),
+                ("input_count", C.c_int), ("output_count", C.c_int), ("group", C.c_int)]
+
+
+class Geom(C.Structure):
+    _fields_ = [(n, C.c_int) for n in (
+        "n", "c_in", "h", "w", "c_out", "kh", "kw", "stride_h", "stride_w", "pad_t", "pad_l", "pad_b",
+        "pad_r", "dilate_h", "dilate_w", "oh", "ow", "cip", "cop", "np")]
+
+
+_lib = None
+
+
+def header_functions():
+    """Every function the public header declares (name -> None)."""
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\*?\s+\*?(niti_[a-z0-9_]+)\s*\(", src, flags=re.M)))
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"libniti_hip.so not built ({LIB_PATH}); run __graft_entry__.build() or "
+                          f"make -C mandheling-dsp-training_amd/csrc")
+    L = C.CDLL(LIB_PATH)
+    vp, i32, i64, ci = C.c_void_p, C.c_int32, C.c_int64, C.c_int
+    tp = C.POINTER(Tensor)
+    sig = {
+        "niti_version": (C.c_char_p, []),
+        "niti_create_execution": (ci, [ci, C.POINTER(ConvCommon), C.POINTER(vp)]),
+        "niti_execution_resize": (ci, [vp, tp, ci, tp, ci]),
+        "niti_execution_execute": (ci, [vp, tp, ci, tp, ci, vp]),
+        "niti_destroy_execution": (None, [vp]),
+        "niti_execution_workspace_bytes": (C.c_size_t, [vp]),
+        "niti_geom_finalize": (ci, [C.POINTER(Geom)]),
+        "niti_conv_fwd_acc": (ci, [C.POINTER(Geom), vp, vp, vp, vp, vp]),
+        "niti_conv_dgrad_acc": (ci, [C.POINTER(Geom), vp, vp, vp, vp, vp]),
+        "niti_conv_wgrad_acc": (ci, [C.POINTER(Geom), vp, vp, vp, vp]),
+        "niti_matmul_acc": (ci, [ci, ci, ci, vp, i64, vp, i64, vp, i64, vp, ci, vp]),
+        "niti_absmax_i32": (ci, [vp, i64, vp, vp]),
+        "niti_requant_act": (ci, [vp, i64, ci, vp, vp, vp, vp, ci, vp, vp, vp]),
+        "niti_requant_grad": (ci, [vp, i64, vp, ci, vp, vp, vp]),
+        "niti_nhwc16_to_chwn16": (ci, [vp, ci, ci, ci, ci, vp, vp]),
+        "niti_ohwi16_to_ihwo16": (ci, [vp, ci, ci, ci, ci, ci, vp, vp]),
+        "niti_nchw_to_nhwc16": (ci, [vp, ci, ci, ci, ci, vp, vp]),
+        "niti_nchw_to_chwn16": (ci, [vp, ci, ci, ci, ci, ci, vp, vp]),
+        "niti_nhwc16_to_nchw": (ci, [vp, ci, ci, ci, ci, vp, vp]),
+        "niti_oihw_to_ohwi16": (ci, [vp, ci, ci, ci, ci, vp, vp]),
+        "niti_ohwi16_to_oihw": (ci, [vp, ci, ci, ci, ci, vp, vp]),
+        "niti_maxpool": (ci, [vp] + [ci] * 7 + [vp, ci, ci, vp]),
+        "niti_maxpool_grad": (ci, [vp, vp, vp] + [ci] * 10 + [vp, vp]),
+        "niti_relu_grad": (ci, [vp, vp, i64, vp, vp]),
+        "niti_loss_grad": (ci, [vp, ci, ci, ci, vp, vp, vp, vp]),
+        "niti_model_create": (ci, [ci, ci, C.POINTER(vp)]),
+        "niti_model_destroy": (None, [vp]),
+        "niti_model_num_layers": (ci, [vp]),
+        "niti_model_layer_info": (ci, [vp, ci, C.POINTER(ci)]),
+        "niti_model_set_weight": (ci, [vp, ci, vp, ci]),
+        "niti_model_get_weight": (ci, [vp, ci, vp]),
+        "niti_model_train_step": (ci, [vp, vp, ci, vp, vp]),
+        "niti_model_get_logits": (ci, [vp, vp, C.POINTER(ci), vp]),
+        "niti_model_get_tap": (ci, [vp, ci, ci, vp, C.c_size_t, vp]),
+        "niti_model_step_macs": (i64, [vp]),
+        "niti_model_set_probe": (ci, [vp, ci, ci, ci]),
+        "niti_model_probe_read": (ci, [vp, C.POINTER(C.c_double), C.POINTER(ci)]),
+        "niti_dp_get_unique_id": (ci, [C.c_char_p]),
+        "niti_model_attach_comm": (ci, [vp, C.c_char_p, ci, ci, ci]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def check(code, what=""):
+    if code != 0:
+        raise NitiError(code, what)

@@ -1,0 +1,93 @@
+"""Device-resident NITI training step (section 3 of include/niti_hip.h)."""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+import torch
+
+from . import _lib as L
+from ._lib import check
+from .ops import _stream
+
+
+class NitiModel:
+    """NITIInt8Train's model + NITI_SGD step, on one GPU (optionally one rank of a DP group)."""
+
+    def __init__(self, arch: int, batch: int):
+        self._lib = L.lib()
+        h = C.c_void_p()
+        check(self._lib.niti_model_create(arch, batch, C.byref(h)), "model_create")
+        self._h = h
+        self.arch, self.batch = arch, batch
+        self.layers = []
+        for i in range(self._lib.niti_model_num_layers(h)):
+            info = (C.c_int * 12)()
+            check(self._lib.niti_model_layer_info(h, i, info), "layer_info")
+            keys = ("c_in", "c_out", "kh", "kw", "h", "w", "oh", "ow", "pad", "stride", "relu", "pool")
+            self.layers.append(dict(zip(keys, list(info))))
+
+    def weight_shape(self, i):
+        l = self.layers[i]
+        return (l["c_out"], l["c_in"], l["kh"], l["kw"])
+
+    def set_weight(self, i, w: np.ndarray, wscale: int):
+        w = np.ascontiguousarray(w, dtype=np.int8)
+        assert w.shape == self.weight_shape(i), (w.shape, self.weight_shape(i))
+        check(self._lib.niti_model_set_weight(self._h, i, w.ctypes.data_as(C.c_void_p), int(wscale)), "set_weight")
+
+    def get_weight(self, i) -> np.ndarray:
+        w = np.empty(self.weight_shape(i), np.int8)
+        check(self._lib.niti_model_get_weight(self._h, i, w.ctypes.data_as(C.c_void_p)), "get_weight")
+        return w
+
+    def train_step(self, x: torch.Tensor, exp_in: int, labels: torch.Tensor, stream=None):
+        assert x.dtype == torch.int8 and x.is_contiguous() and labels.dtype == torch.int32
+        check(self._lib.niti_model_train_step(self._h, C.c_void_p(x.data_ptr()), int(exp_in),
+                                              C.c_void_p(labels.data_ptr()), _stream(stream)), "train_step")
+
+    def logits(self, stream=None):
+        last = self.layers[-1]
+        out = np.empty((self.batch, last["c_out"]), np.int8)
+        e = C.c_int()
+        check(self._lib.niti_model_get_logits(self._h, out.ctypes.data_as(C.c_void_p), C.byref(e),
+                                              _stream(stream)), "get_logits")
+        return out, int(e.value)
+
+    def tap(self, i, which, stream=None):
+        l = self.layers[i]
+        if which == 1:
+            shape = (l["c_out"], l["c_in"], l["kh"], l["kw"])
+        else:
+            shape = (self.batch, l["c_out"], l["oh"], l["ow"])
+        out = np.empty(shape, np.int8)
+        check(self._lib.niti_model_get_tap(self._h, i, which, out.ctypes.data_as(C.c_void_p), out.nbytes,
+                                           _stream(stream)), "get_tap")
+        return out
+
+    def set_probe(self, layer: int, phase: int, max_launches: int = 256):
+        check(self._lib.niti_model_set_probe(self._h, layer, phase, max_launches), "set_probe")
+
+    def probe_read(self):
+        t = C.c_double()
+        n = C.c_int()
+        check(self._lib.niti_model_probe_read(self._h, C.byref(t), C.byref(n)), "probe_read")
+        return float(t.value), int(n.value)
+
+    def step_macs(self) -> int:
+        return int(self._lib.niti_model_step_macs(self._h))
+
+    def attach_comm(self, unique_id: bytes, rank: int, world: int, exact: bool = True):
+        check(self._lib.niti_model_attach_comm(self._h, unique_id, rank, world, 1 if exact else 0), "attach_comm")
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = C.create_string_buffer(128)
+        check(L.lib().niti_dp_get_unique_id(buf), "unique_id")
+        return buf.raw
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            self._lib.niti_model_destroy(h)
+            self._h = None

@@ -1,0 +1,229 @@
+"""Thin torch-facing wrappers over the C ABI (include/niti_hip.h).
+
+torch supplies device memory and the stream; every byte of compute runs in
+libniti_hip.so.  Section 1 (the MNN Execution-shaped drop-in) is exposed as
+`NITIExecution`; section 2 (native split primitives) as plain functions.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+
+from . import _lib as L
+from ._lib import check
+
+
+def _stream(stream=None):
+    if stream is not None:
+        return stream
+    return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _ptr(t):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+def tensor(t: torch.Tensor, dims, fmt=L.FORMAT_NCHW) -> L.Tensor:
+    d = list(dims) + [1] * (4 - len(dims))
+    return L.Tensor(t.data_ptr(), (C.c_int * 4)(*d), fmt)
+
+
+def conv_common(kernel, stride=1, pad=0, dilate=1, pads=None, pad_mode=L.PAD_CAFFE, input_count=0,
+                output_count=0, group=1) -> L.ConvCommon:
+    kx, ky = (kernel, kernel) if isinstance(kernel, int) else kernel
+    c = L.ConvCommon()
+    c.kernel_x, c.kernel_y = kx, ky
+    c.stride_x = c.stride_y = stride
+    c.dilate_x = c.dilate_y = dilate
+    c.pad_x = c.pad_y = pad
+    if pads is not None:
+        c.has_pads = 1
+        c.pads = (C.c_int * 4)(*pads)
+    c.pad_mode = pad_mode
+    c.input_count, c.output_count, c.group = input_count, output_count, group
+    return c
+
+
+class NITIExecution:
+    """One MNN Execution (Creator::onCreate + onResize + onExecute) for `op_type`."""
+
+    def __init__(self, op_type: int, common: L.ConvCommon | None = None):
+        self._lib = L.lib()
+        h = C.c_void_p()
+        check(self._lib.niti_create_execution(op_type, C.byref(common) if common is not None else None,
+                                              C.byref(h)), f"create op {op_type}")
+        self._h = h
+
+    @staticmethod
+    def _arr(ts):
+        arr = (L.Tensor * len(ts))(*ts)
+        return arr, len(ts)
+
+    def resize(self, inputs, outputs):
+        i, ni = self._arr(inputs)
+        o, no = self._arr(outputs)
+        return self._lib.niti_execution_resize(self._h, i, ni, o, no)
+
+    def execute(self, inputs, outputs, stream=None):
+        i, ni = self._arr(inputs)
+        o, no = self._arr(outputs)
+        return self._lib.niti_execution_execute(self._h, i, ni, o, no, _stream(stream))
+
+    @property
+    def workspace_bytes(self):
+        return int(self._lib.niti_execution_workspace_bytes(self._h))
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            self._lib.niti_destroy_execution(h)
+            self._h = None
+
+
+# ------------------------------------------------------------------------------------ native
+def geom(n, c_in, h, w, c_out, kh, kw=None, stride=1, pad=0, dilate=1, pads=None) -> L.Geom:
+    kw = kh if kw is None else kw
+    pt, pl, pb, pr = pads if pads is not None else (pad,) * 4
+    g = L.Geom(n, c_in, h, w, c_out, kh, kw, stride, stride, pt, pl, pb, pr, dilate, dilate, 0, 0, 0, 0, 0)
+    check(L.lib().niti_geom_finalize(C.byref(g)), "geometry")
+    return g
+
+
+def r16(x):
+    return (x + 15) // 16 * 16
+
+
+def nchw_to_nhwc16(x: torch.Tensor, stream=None):
+    n, c, h, w = x.shape
+    out = torch.empty((n, h, w, r16(c)), dtype=torch.int8, device=x.device)
+    check(L.lib().niti_nchw_to_nhwc16(_ptr(x), n, c, h * w, r16(c), _ptr(out), _stream(stream)), "nchw->nhwc16")
+    return out
+
+
+def nchw_to_chwn16(x: torch.Tensor, stream=None):
+    n, c, h, w = x.shape
+    out = torch.empty((r16(c), h, w, r16(n)), dtype=torch.int8, device=x.device)
+    check(L.lib().niti_nchw_to_chwn16(_ptr(x), n, c, h * w, r16(c), r16(n), _ptr(out), _stream(stream)),
+          "nchw->chwn16")
+    return out
+
+
+def nhwc16_to_nchw(x16: torch.Tensor, c: int, stream=None):
+    n, h, w, cp = x16.shape
+    out = torch.empty((n, c, h, w), dtype=torch.int8, device=x16.device)
+    check(L.lib().niti_nhwc16_to_nchw(_ptr(x16), n, c, h * w, cp, _ptr(out), _stream(stream)), "nhwc16->nchw")
+    return out
+
+
+def oihw_to_ohwi16(w: torch.Tensor, stream=None):
+    co, ci, kh, kw = w.shape
+    out = torch.empty((co, kh, kw, r16(ci)), dtype=torch.int8, device=w.device)
+    check(L.lib().niti_oihw_to_ohwi16(_ptr(w), co, ci, kh * kw, r16(ci), _ptr(out), _stream(stream)), "oihw->ohwi16")
+    return out
+
+
+def ohwi16_to_ihwo16(w16: torch.Tensor, ci: int, stream=None):
+    co, kh, kw, cip = w16.shape
+    out = torch.empty((ci, kh, kw, r16(co)), dtype=torch.int8, device=w16.device)
+    check(L.lib().niti_ohwi16_to_ihwo16(_ptr(w16), co, ci, kh * kw, cip, r16(co), _ptr(out), _stream(stream)),
+          "ohwi16->ihwo16")
+    return out
+
+
+def ohwi16_to_oihw(w16: torch.Tensor, ci: int, stream=None):
+    co, kh, kw, cip = w16.shape
+    out = torch.empty((co, ci, kh, kw), dtype=torch.int8, device=w16.device)
+    check(L.lib().niti_ohwi16_to_oihw(_ptr(w16), co, ci, kh * kw, cip, _ptr(out), _stream(stream)), "ohwi16->oihw")
+    return out
+
+
+def nhwc16_to_chwn16(x16: torch.Tensor, stream=None):
+    n, h, w, cp = x16.shape
+    out = torch.empty((cp, h, w, r16(n)), dtype=torch.int8, device=x16.device)
+    check(L.lib().niti_nhwc16_to_chwn16(_ptr(x16), n, h * w, cp, r16(n), _ptr(out), _stream(stream)),
+          "nhwc16->chwn16")
+    return out
+
+
+def conv_fwd_acc(g: L.Geom, x16, w16, amax, stream=None):
+    acc = torch.empty((g.n * g.oh * g.ow, g.cop), dtype=torch.int32, device=x16.device)
+    check(L.lib().niti_conv_fwd_acc(C.byref(g), _ptr(x16), _ptr(w16), _ptr(acc), _ptr(amax), _stream(stream)),
+          "conv_fwd_acc")
+    return acc
+
+
+def conv_dgrad_acc(g: L.Geom, dy16, wt16, amax, stream=None):
+    acc = torch.empty((g.n * g.h * g.w, g.cip), dtype=torch.int32, device=dy16.device)
+    check(L.lib().niti_conv_dgrad_acc(C.byref(g), _ptr(dy16), _ptr(wt16), _ptr(acc), _ptr(amax), _stream(stream)),
+          "conv_dgrad_acc")
+    return acc
+
+
+def conv_wgrad_acc(g: L.Geom, xT, dyT, stream=None):
+    acc = torch.empty((g.c_out, g.kh, g.kw, g.cip), dtype=torch.int32, device=xT.device)
+    check(L.lib().niti_conv_wgrad_acc(C.byref(g), _ptr(xT), _ptr(dyT), _ptr(acc), _stream(stream)),
+          "conv_wgrad_acc")
+    return acc
+
+
+def matmul_acc(B16, A16, ldc, amax=None, split_k=True, stream=None):
+    m, k16 = B16.shape
+    o = A16.shape[0]
+    acc = torch.empty((m, ldc), dtype=torch.int32, device=B16.device)
+    if split_k:
+        acc.zero_()
+    check(L.lib().niti_matmul_acc(m, o, k16, _ptr(B16), k16, _ptr(A16), k16, _ptr(acc), ldc, _ptr(amax),
+                                  1 if split_k else 0, _stream(stream)), "matmul_acc")
+    return acc
+
+
+def absmax(acc, amax, stream=None):
+    check(L.lib().niti_absmax_i32(_ptr(acc), acc.numel(), _ptr(amax), _stream(stream)), "absmax")
+
+
+def requant_act(acc, amax, exp_in=None, wscale=None, exp_out=None, relu=False, relu_mask=None, stream=None):
+    rows, ldc = acc.shape
+    out = torch.empty((rows, ldc), dtype=torch.int8, device=acc.device)
+    check(L.lib().niti_requant_act(_ptr(acc), rows, ldc, _ptr(amax), _ptr(exp_in), _ptr(wscale), _ptr(exp_out),
+                                   1 if relu else 0, _ptr(relu_mask), _ptr(out), _stream(stream)), "requant_act")
+    return out
+
+
+def requant_grad(acc, amax, rule=2, w_update=None, stream=None):
+    g = torch.empty(acc.shape, dtype=torch.int8, device=acc.device)
+    check(L.lib().niti_requant_grad(_ptr(acc), acc.numel(), _ptr(amax), rule, _ptr(g), _ptr(w_update),
+                                    _stream(stream)), "requant_grad")
+    return g
+
+
+def maxpool(x16, k=2, s=2, p=0, stream=None):
+    n, h, w, cp = x16.shape
+    oh = (h + 2 * p - min(k, h)) // s + 1
+    ow = (w + 2 * p - min(k, w)) // s + 1
+    y = torch.empty((n, oh, ow, cp), dtype=torch.int8, device=x16.device)
+    check(L.lib().niti_maxpool(_ptr(x16), n, h, w, cp, k, s, p, _ptr(y), oh, ow, _stream(stream)), "maxpool")
+    return y
+
+
+def maxpool_grad(x16, y16, dy16, k=2, s=2, p=0, relu=False, stream=None):
+    n, h, w, cp = x16.shape
+    oh, ow = y16.shape[1], y16.shape[2]
+    dx = torch.empty_like(x16)
+    check(L.lib().niti_maxpool_grad(_ptr(x16), _ptr(y16), _ptr(dy16), n, h, w, cp, k, s, p, oh, ow,
+                                    1 if relu else 0, _ptr(dx), _stream(stream)), "maxpool_grad")
+    return dx
+
+
+def relu_grad(x, dy, stream=None):
+    out = torch.empty_like(x)
+    check(L.lib().niti_relu_grad(_ptr(x), _ptr(dy), x.numel(), _ptr(out), _stream(stream)), "relu_grad")
+    return out
+
+
+def loss_grad(logits, classes, ascale_dev, labels, stream=None):
+    b, ld = logits.shape
+    out = torch.empty_like(logits)
+    check(L.lib().niti_loss_grad(_ptr(logits), b, classes, ld, _ptr(ascale_dev), _ptr(labels), _ptr(out),
+                                 _stream(stream)), "loss_grad")
+    return out

@@ -1,0 +1,100 @@
+"""One NITI_SGD training step on the CPU oracle (TEST INFRASTRUCTURE ONLY).
+
+Restates the reference's NITIInt8Train step op by op with the oracle primitives:
+  forward  NITIInt8::onForward            tools/train/source/demo/mnistTrain.cpp:159-181
+  loss     NITI_LOSS_Grad_Int8            source/backend/cpu/NITI_CPULossGrad_Int8.cpp:81-200
+  backward grad/NITI_Conv_Int8_Grad.cpp:16-197, NITI_Pool_Int8_Grad, NITI_ReluGrad_Int8
+  update   NITI_SGD::onGetNextParameter   tools/train/source/optimizer/NITI_SGD.hpp:20-54
+Parity unpinned (see niti_oracle.h).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+import niti_oracle as O
+
+
+def lenet_layers():
+    # mnistTrain.cpp:131-157 / :159-181
+    return [
+        dict(ci=1, co=20, k=5, pad=0, h=28, relu=1, pool=1, flatten=0),
+        dict(ci=20, co=52, k=5, pad=0, h=12, relu=1, pool=1, flatten=1),
+        dict(ci=832, co=500, k=1, pad=0, h=1, relu=1, pool=0, flatten=0),
+        dict(ci=500, co=12, k=1, pad=0, h=1, relu=0, pool=0, flatten=0),
+    ]
+
+
+def vgg11_layers():
+    L = []
+    for ci, co, h, pool in [(3, 64, 32, 1), (64, 128, 16, 1), (128, 256, 8, 0), (256, 256, 8, 1),
+                            (256, 512, 4, 0), (512, 512, 4, 1), (512, 512, 2, 0), (512, 512, 2, 1)]:
+        L.append(dict(ci=ci, co=co, k=3, pad=1, h=h, relu=1, pool=pool, flatten=0))
+    L.append(dict(ci=512, co=12, k=1, pad=0, h=1, relu=0, pool=0, flatten=0))
+    return L
+
+
+def init_weights(layers, seed=17):
+    rng = np.random.default_rng(seed)
+    W, S = [], []
+    for l in layers:
+        w, s = O.synth_w(rng, (l["co"], l["ci"], l["k"], l["k"]))
+        W.append(w)
+        S.append(s)
+    return W, S
+
+
+def onehot(labels, classes=10):
+    oh = np.zeros((len(labels), classes), np.int32)
+    oh[np.arange(len(labels)), labels] = 1
+    return oh
+
+
+def train_step(layers, W, S, x, exp_in, labels):
+    """Returns (new weights, record) where record holds logits, exponents and per-layer taps."""
+    n = x.shape[0]
+    rec = dict(inp=[], y=[], r=[], p=[], exp=[], dw=[], dy=[], geom=[])
+    a = x
+    exp = exp_in
+    for i, l in enumerate(layers):
+        g = O.geom(n, l["ci"], l["h"], l["h"], l["co"], l["k"], pad=l["pad"])
+        rec["geom"].append(g)
+        rec["inp"].append(a)
+        y, exp, _, st = O.conv_fwd(g, a, W[i], exp, S[i])
+        assert st.overflow == 0
+        r = O.relu(y) if l["relu"] else y
+        rec["y"].append(y)
+        rec["r"].append(r)
+        rec["exp"].append(exp)
+        if l["pool"]:
+            p = O.maxpool(r)
+            rec["p"].append(p)
+            a = p
+        else:
+            rec["p"].append(None)
+            a = r
+        if l["flatten"]:
+            a = a.reshape(n, -1, 1, 1)
+    last = layers[-1]
+    logits = rec["r"][-1].reshape(n, last["co"])
+    d = O.loss_grad(logits, rec["exp"][-1], onehot(labels)).reshape(n, last["co"], 1, 1)
+    dy = [None] * len(layers)
+    dy[-1] = d
+    newW = list(W)
+    for i in range(len(layers) - 1, -1, -1):
+        g = rec["geom"][i]
+        dw, bw, _, _ = O.conv_wgrad(g, rec["inp"][i], dy[i])
+        rec["dw"].insert(0, dw)
+        if i > 0:
+            dx, _, _, _ = O.conv_dgrad(g, dy[i], W[i])
+            pl = layers[i - 1]
+            if pl["flatten"]:
+                dx = dx.reshape(rec["p"][i - 1].shape)
+            if pl["pool"]:
+                dx = O.maxpool_grad(rec["r"][i - 1], rec["p"][i - 1], dx)
+            if pl["relu"]:
+                dx = O.relu_grad(rec["y"][i - 1], dx)
+            dy[i - 1] = dx
+        newW[i] = O.sgd_update(W[i], dw)
+    rec["dy"] = dy
+    rec["logits"] = logits
+    return newW, rec

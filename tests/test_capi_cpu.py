@@ -1,0 +1,76 @@
+"""CPU-side checks of the C-ABI library: it loads, exports every symbol include/niti_hip.h
+declares, and its host-only entry points validate arguments (no device calls here)."""
+import ctypes as C
+import subprocess
+
+import pytest
+
+
+@pytest.fixture(scope="module")
+def L():
+    from niti_amd import _lib
+    return _lib
+
+
+def test_library_loads_and_reports_version(L):
+    assert b"gfx950" in L.lib().niti_version()
+
+
+def test_every_header_symbol_is_exported(L):
+    names = L.header_functions()
+    assert len(names) >= 30
+    out = subprocess.run(["nm", "-D", "--defined-only", L.LIB_PATH], capture_output=True, text=True, check=True).stdout
+    exported = {line.split()[-1] for line in out.splitlines() if line.strip()}
+    missing = [n for n in names if n not in exported]
+    assert not missing, missing
+    for n in names:  # and ctypes resolves them
+        getattr(L.lib(), n)
+
+
+def test_code_object_targets_gfx950(L):
+    data = open(L.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in data
+    assert b"gfx942" not in data and b"gfx90a" not in data
+
+
+def test_create_execution_validation(L):
+    lib = L.lib()
+    h = C.c_void_p()
+    c = L.ConvCommon()
+    c.kernel_x = c.kernel_y = 3
+    c.stride_x = c.stride_y = c.dilate_x = c.dilate_y = 1
+    c.group = 1
+    assert lib.niti_create_execution(999, C.byref(c), C.byref(h)) == 2      # NOT_SUPPORT
+    assert lib.niti_create_execution(700, None, C.byref(h)) == 5            # INVALID_VALUE
+    c.group = 2
+    assert lib.niti_create_execution(700, C.byref(c), C.byref(h)) == 2      # grouped conv: NOT_SUPPORT
+    c.group = 1
+    for op in (700, 701, 715, 818):
+        assert lib.niti_create_execution(op, C.byref(c), C.byref(h)) == 0
+        assert lib.niti_execution_workspace_bytes(h) == 0
+        lib.niti_destroy_execution(h)
+    assert lib.niti_create_execution(713, None, C.byref(h)) == 0
+    lib.niti_destroy_execution(h)
+
+
+def test_geometry(L):
+    lib = L.lib()
+    g = L.Geom(256, 3, 32, 32, 64, 3, 3, 1, 1, 1, 1, 1, 1, 1, 1, 0, 0, 0, 0, 0)
+    assert lib.niti_geom_finalize(C.byref(g)) == 0
+    assert (g.oh, g.ow, g.cip, g.cop, g.np) == (32, 32, 16, 64, 256)
+    g = L.Geom(5, 20, 12, 12, 52, 5, 5, 1, 1, 0, 0, 0, 0, 1, 1, 0, 0, 0, 0, 0)
+    assert lib.niti_geom_finalize(C.byref(g)) == 0
+    assert (g.oh, g.ow, g.cip, g.cop, g.np) == (8, 8, 32, 64, 16)
+    g = L.Geom(1, 1, 2, 2, 1, 5, 5, 1, 1, 0, 0, 0, 0, 1, 1, 0, 0, 0, 0, 0)
+    assert lib.niti_geom_finalize(C.byref(g)) == 3  # COMPUTE_SIZE_ERROR
+
+
+def test_no_fallback_when_library_missing(tmp_path, monkeypatch):
+    import importlib
+
+    from niti_amd import _lib
+    monkeypatch.setattr(_lib, "LIB_PATH", str(tmp_path / "missing.so"))
+    monkeypatch.setattr(_lib, "_lib", None)
+    with pytest.raises(ImportError):
+        _lib.lib()
+    importlib.reload(_lib)

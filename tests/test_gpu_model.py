@@ -1,0 +1,66 @@
+"""GPU parity of the device-resident training step against the oracle's NITI_SGD step.
+
+Every forward output, exponent, input gradient, int8 weight gradient and updated weight of
+the step must equal the oracle (niti_model_ref.py) bit for bit, over two consecutive steps.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def T():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import niti_amd  # noqa: F401
+    return torch
+
+
+def _run(T, arch, layers, batch, steps=2, seed=5):
+    import niti_model_ref as R
+    from niti_amd.model import NitiModel
+    rng = np.random.default_rng(seed)
+    W, S = R.init_weights(layers, seed=seed)
+    m = NitiModel(arch, batch)
+    for i, (w, s) in enumerate(zip(W, S)):
+        m.set_weight(i, w, s)
+    for i in range(len(layers)):
+        assert np.array_equal(m.get_weight(i), W[i])
+    l0 = layers[0]
+    for step in range(steps):
+        x = rng.integers(-127, 128, (batch, l0["ci"], l0["h"], l0["h"])).astype(np.int8)
+        labels = rng.integers(0, 10, batch).astype(np.int32)
+        exp_in = -3
+        newW, rec = R.train_step(layers, W, S, x, exp_in, labels)
+        xd = T.from_numpy(x).cuda()
+        ld = T.from_numpy(labels).cuda()
+        m.train_step(xd, exp_in, ld)
+        logits, e = m.logits()
+        assert e == rec["exp"][-1], (step, e, rec["exp"][-1])
+        assert np.array_equal(logits, rec["logits"]), step
+        for i in range(len(layers)):
+            assert np.array_equal(m.tap(i, 0), rec["r"][i]), ("fwd", step, i)
+            assert np.array_equal(m.tap(i, 2), rec["dy"][i]), ("dy", step, i)
+            assert np.array_equal(m.tap(i, 1), rec["dw"][i]), ("dw", step, i)
+            assert np.array_equal(m.get_weight(i), newW[i]), ("w", step, i)
+        W = newW
+
+
+def test_lenet_step_matches_oracle(T):
+    import niti_amd
+    import niti_model_ref as R
+    _run(T, niti_amd.ARCH_LENET, R.lenet_layers(), batch=64)
+
+
+def test_vgg11_step_matches_oracle(T):
+    import niti_amd
+    import niti_model_ref as R
+    _run(T, niti_amd.ARCH_VGG11, R.vgg11_layers(), batch=8, steps=2)
+
+
+def test_vgg11_ragged_batch(T):
+    import niti_amd
+    import niti_model_ref as R
+    _run(T, niti_amd.ARCH_VGG11, R.vgg11_layers(), batch=5, steps=1, seed=9)

@@ -1,0 +1,409 @@
+"""GPU parity: every HIP kernel / C-ABI entry point against the CPU oracle, bit for bit.
+
+All calls go through libniti_hip.so (include/niti_hip.h).  The oracle is the checker only.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+GEOMS = [
+    (4, 1, 28, 28, 20, 5, 1, 0),     # LeNet conv1 (batch cut)
+    (4, 20, 12, 12, 52, 5, 1, 0),    # LeNet conv2
+    (4, 832, 1, 1, 500, 1, 1, 0),    # LeNet ip1
+    (4, 500, 1, 1, 12, 1, 1, 0),     # LeNet ip2
+    (3, 3, 16, 16, 64, 3, 1, 1),     # VGG L1 shape
+    (2, 64, 8, 8, 128, 3, 1, 1),     # VGG L2 shape
+    (17, 256, 4, 4, 256, 3, 1, 1),   # VGG mid, ragged batch
+    (5, 6, 9, 9, 8, 3, 2, 1),        # stride 2
+    (7, 5, 6, 7, 12, 3, 1, 1),       # ragged everything
+    (3, 40, 7, 5, 36, 3, 1, 0),      # non-square, no pad
+    (3, 8, 9, 9, 12, 3, 2, 1),       # stride 2, channels % 4 == 0
+]
+
+
+@pytest.fixture(scope="module")
+def T():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import niti_amd  # noqa: F401  (fails loudly without the HIP library)
+    return torch
+
+
+@pytest.fixture(scope="module")
+def ops(T):
+    from niti_amd import ops
+    return ops
+
+
+def dev(T, a, dtype=None):
+    return T.from_numpy(np.ascontiguousarray(a)).to("cuda")
+
+
+def zeros_u32(T):
+    return T.zeros(4, dtype=T.int32, device="cuda")
+
+
+def i8s(T, v):
+    return T.tensor([v], dtype=T.int8, device="cuda")
+
+
+# --------------------------------------------------------------------------- GEMM core
+@pytest.mark.parametrize("m,o,k", [(1, 1, 1), (37, 29, 100), (128, 128, 64), (300, 200, 777), (5, 700, 4100)])
+@pytest.mark.parametrize("split", [False, True])
+def test_matmul_acc_exact(T, ops, m, o, k, split):
+    rng = np.random.default_rng(m * 7 + o + k)
+    B = rng.integers(-128, 128, (m, k), dtype=np.int16).astype(np.int8)
+    A = rng.integers(-128, 128, (o, k), dtype=np.int16).astype(np.int8)
+    k16 = (k + 15) // 16 * 16
+    Bp = np.zeros((m, k16), np.int8)
+    Bp[:, :k] = B
+    Ap = np.zeros((o, k16), np.int8)
+    Ap[:, :k] = A
+    ldc = (o + 15) // 16 * 16
+    amax = zeros_u32(T)
+    acc = ops.matmul_acc(dev(T, Bp), dev(T, Ap), ldc, amax=None if split else amax, split_k=split)
+    want = B.astype(np.int64) @ A.astype(np.int64).T
+    got = acc.cpu().numpy()[:, :o]
+    assert np.array_equal(got, want)
+    if not split:
+        assert int(amax[0].item()) == int(np.abs(want).max())
+
+
+# --------------------------------------------------------------------------- native conv ops
+def nchw_to_nhwc_acc(a):
+    return np.ascontiguousarray(a.transpose(0, 2, 3, 1)).reshape(-1, a.shape[1])
+
+
+@pytest.mark.parametrize("geo", GEOMS)
+def test_conv_fwd_native(T, ops, oracle, geo):
+    n, ci, h, w, co, k, s, p = geo
+    rng = np.random.default_rng(101)
+    g = oracle.geom(n, ci, h, w, co, k, stride=s, pad=p)
+    x = oracle.synth_x(rng, (n, ci, h, w))
+    wt, ws = oracle.synth_w(rng, (co, ci, k, k))
+    y_ref, e_ref, acc_ref, _ = oracle.conv_fwd(g, x, wt, -7, ws)
+    gg = ops.geom(n, ci, h, w, co, k, stride=s, pad=p)
+    x16 = ops.nchw_to_nhwc16(dev(T, x))
+    w16 = ops.oihw_to_ohwi16(dev(T, wt))
+    amax = zeros_u32(T)
+    acc = ops.conv_fwd_acc(gg, x16, w16, amax)
+    got = acc.cpu().numpy()
+    assert np.array_equal(got[:, :co], nchw_to_nhwc_acc(acc_ref))
+    assert not got[:, co:].any()
+    assert int(amax[0].item()) == int(np.abs(acc_ref.astype(np.int64)).max())
+    e_out = i8s(T, 0)
+    y16 = ops.requant_act(acc, amax, exp_in=i8s(T, -7), wscale=i8s(T, ws), exp_out=e_out)
+    y = y16.cpu().numpy()[:, :co].reshape(n, g.oh, g.ow, co).transpose(0, 3, 1, 2)
+    assert np.array_equal(y, y_ref)
+    assert int(e_out.item()) == e_ref
+
+
+@pytest.mark.parametrize("geo", GEOMS)
+def test_conv_dgrad_native(T, ops, oracle, geo):
+    n, ci, h, w, co, k, s, p = geo
+    rng = np.random.default_rng(102)
+    g = oracle.geom(n, ci, h, w, co, k, stride=s, pad=p)
+    dy = oracle.synth_dy(rng, (n, co, g.oh, g.ow))
+    wt, _ = oracle.synth_w(rng, (co, ci, k, k))
+    dx_ref, inc_ref, acc_ref, _ = oracle.conv_dgrad(g, dy, wt)
+    gg = ops.geom(n, ci, h, w, co, k, stride=s, pad=p)
+    dy16 = ops.nchw_to_nhwc16(dev(T, dy))
+    w16 = ops.oihw_to_ohwi16(dev(T, wt))
+    wT = ops.ohwi16_to_ihwo16(w16, ci)
+    amax = zeros_u32(T)
+    acc = ops.conv_dgrad_acc(gg, dy16, wT, amax)
+    got = acc.cpu().numpy()
+    assert np.array_equal(got[:, :ci], nchw_to_nhwc_acc(acc_ref))
+    dx16 = ops.requant_act(acc, amax)
+    dx = dx16.cpu().numpy()[:, :ci].reshape(n, h, w, ci).transpose(0, 3, 1, 2)
+    assert np.array_equal(dx, dx_ref)
+
+
+@pytest.mark.parametrize("geo", GEOMS)
+def test_conv_wgrad_native(T, ops, oracle, geo):
+    n, ci, h, w, co, k, s, p = geo
+    rng = np.random.default_rng(103)
+    g = oracle.geom(n, ci, h, w, co, k, stride=s, pad=p)
+    x = oracle.synth_x(rng, (n, ci, h, w))
+    dy = oracle.synth_dy(rng, (n, co, g.oh, g.ow))
+    dw_ref, bw_ref, acc_ref, _ = oracle.conv_wgrad(g, x, dy)
+    gg = ops.geom(n, ci, h, w, co, k, stride=s, pad=p)
+    xT = ops.nchw_to_chwn16(dev(T, x))
+    dyT = ops.nchw_to_chwn16(dev(T, dy))
+    acc = ops.conv_wgrad_acc(gg, xT, dyT)
+    got = acc.cpu().numpy()  # [co][kh][kw][cip]
+    assert np.array_equal(got[..., :ci].transpose(0, 3, 1, 2), acc_ref)
+    assert not got[..., ci:].any()
+    amax = zeros_u32(T)
+    ops.absmax(acc, amax)
+    w16 = T.zeros(acc.shape, dtype=T.int8, device="cuda")
+    gq = ops.requant_grad(acc, amax, rule=2, w_update=w16)
+    assert np.array_equal(gq.cpu().numpy()[..., :ci].transpose(0, 3, 1, 2), dw_ref)
+    # fused SGD: 0 - g, clipped
+    assert np.array_equal(w16.cpu().numpy()[..., :ci].transpose(0, 3, 1, 2),
+                          oracle.sgd_update(np.zeros_like(dw_ref), dw_ref))
+
+
+# --------------------------------------------------------------------------- drop-in Executions
+def _c4_dims(a):
+    return list(a.shape)
+
+
+@pytest.mark.parametrize("geo", [gg for gg in GEOMS if gg[4] % 4 == 0])
+def test_exec_conv_int8(T, ops, oracle, geo):
+    import niti_amd
+    n, ci, h, w, co, k, s, p = geo
+    rng = np.random.default_rng(201)
+    g = oracle.geom(n, ci, h, w, co, k, stride=s, pad=p)
+    x = oracle.synth_x(rng, (n, ci, h, w))
+    wt, ws = oracle.synth_w(rng, (co, ci, k, k))
+    y_ref, e_ref, y4_ref = oracle.mnn_conv_fwd(g, x, wt, -7, ws)
+    x4 = dev(T, oracle.nchw_to_c4(x))
+    y4 = T.zeros(y4_ref.shape, dtype=T.int8, device="cuda")
+    e_in, wsc, e_out = i8s(T, -7), i8s(T, ws), i8s(T, 0)
+    wd = dev(T, wt)
+    ex = ops.NITIExecution(niti_amd.OP_CONV_INT8, ops.conv_common(k, stride=s, pad=p, input_count=ci, output_count=co))
+    ins = [ops.tensor(x4, (n, ci, h, w), niti_amd.FORMAT_NC4HW4), ops.tensor(wd, (co, ci, k, k)),
+           ops.tensor(e_in, (1, 1, 1, 1)), ops.tensor(wsc, (1, 1, 1, 1))]
+    outs = [ops.tensor(y4, (n, co, g.oh, g.ow), niti_amd.FORMAT_NC4HW4), ops.tensor(e_out, (1, 1, 1, 1))]
+    assert ex.resize(ins, outs) == 0
+    assert ex.execute(ins, outs) == 0
+    assert np.array_equal(y4.cpu().numpy(), y4_ref)
+    assert int(e_out.item()) == e_ref
+
+
+def test_exec_conv_int8_rejects_unaligned_channels(T, ops):
+    import niti_amd
+    x4 = T.zeros((1, 1, 5, 5, 4), dtype=T.int8, device="cuda")
+    w = T.zeros((6, 3, 3, 3), dtype=T.int8, device="cuda")
+    y4 = T.zeros((2, 1, 3, 3, 4), dtype=T.int8, device="cuda")
+    e = i8s(T, 0)
+    ex = ops.NITIExecution(niti_amd.OP_CONV_INT8, ops.conv_common(3))
+    ins = [ops.tensor(x4, (1, 3, 5, 5), 2), ops.tensor(w, (6, 3, 3, 3)), ops.tensor(e, (1,)), ops.tensor(e, (1,))]
+    outs = [ops.tensor(y4, (1, 6, 3, 3), 2), ops.tensor(e, (1,))]
+    assert ex.resize(ins, outs) == 2  # NOT_SUPPORT: C_out % 4 != 0 (reference acc overflow)
+
+
+@pytest.mark.parametrize("geo", [gg for gg in GEOMS if gg[2] > 1 and gg[1] % 4 == 0])
+def test_exec_deconv_int8(T, ops, oracle, geo):
+    """NITI_DeConv_Int8 on the tensors the grad graph hands it: pad(dilate(dy)) and w^T."""
+    import niti_amd
+    n, ci, h, w, co, k, s, p = geo
+    g = oracle.geom(n, ci, h, w, co, k, stride=s, pad=p)
+    if s == 2 and (w - ((w + 2 * p - k + 1) + 2 * p - k + 1)) % 2:
+        pytest.skip("reference extra-pad arithmetic undefined for this shape")
+    rng = np.random.default_rng(202)
+    dy = oracle.synth_dy(rng, (n, co, g.oh, g.ow))
+    wt, _ = oracle.synth_w(rng, (co, ci, k, k))
+    dx_ref, _, _ = oracle.mnn_conv_dgrad(g, dy, wt)
+    # build the graph-side inputs exactly as grad/NITI_Conv_Int8_Grad.cpp:86-120 does
+    d = dy
+    if s == 2:
+        ow1 = w + 2 * p - k + 1
+        dd = np.zeros((n, co, ow1, ow1), np.int8)
+        dd[:, :, ::2, ::2][:, :, :g.oh, :g.ow] = dy
+        d = dd
+    e = (w - (d.shape[3] + 2 * p - k + 1)) // 2
+    if e:
+        d = np.pad(d, ((0, 0), (0, 0), (e, e), (e, e)))
+    wT = np.ascontiguousarray(wt.transpose(1, 0, 2, 3))
+    d4 = dev(T, oracle.nchw_to_c4(d))
+    out4 = T.zeros(((ci + 3) // 4, n, h, w, 4), dtype=T.int8, device="cuda")
+    ex = ops.NITIExecution(niti_amd.OP_DECONV_INT8, ops.conv_common(k, stride=1, pad=p, input_count=co,
+                                                                     output_count=ci))
+    ins = [ops.tensor(d4, (n, co, d.shape[2], d.shape[3]), 2), ops.tensor(dev(T, wT), (ci, co, k, k))]
+    outs = [ops.tensor(out4, (n, ci, h, w), 2)]
+    assert ex.resize(ins, outs) == 0
+    assert ex.execute(ins, outs) == 0
+    assert np.array_equal(oracle.c4_to_nchw(out4.cpu().numpy(), ci), dx_ref)
+
+
+@pytest.mark.parametrize("geo", [gg for gg in GEOMS if gg[4] % 4 == 0])
+def test_exec_gradient_conv_int8(T, ops, oracle, geo):
+    import niti_amd
+    n, ci, h, w, co, k, s, p = geo
+    g = oracle.geom(n, ci, h, w, co, k, stride=s, pad=p)
+    rng = np.random.default_rng(203)
+    x = oracle.synth_x(rng, (n, ci, h, w))
+    dy = oracle.synth_dy(rng, (n, co, g.oh, g.ow))
+    dw_ref, bw_ref, _ = oracle.mnn_conv_wgrad(g, x, dy)
+    d = dy
+    if s == 2:
+        ow1 = w + 2 * p - k + 1
+        dd = np.zeros((n, co, ow1, ow1), np.int8)
+        dd[:, :, ::2, ::2][:, :, :g.oh, :g.ow] = dy
+        d = dd
+    xT4 = oracle.nchw_to_c4(np.ascontiguousarray(x.transpose(1, 0, 2, 3)))   # C4(x^T)
+    dyT = np.ascontiguousarray(d.transpose(1, 0, 2, 3))                       # dy^T NCHW
+    out4 = T.zeros(((co + 3) // 4, ci, k, k, 4), dtype=T.int8, device="cuda")
+    ex = ops.NITIExecution(niti_amd.OP_GRADIENT_CONV_INT8,
+                           ops.conv_common((d.shape[3], d.shape[2]), stride=1, pad=p, input_count=n, output_count=co))
+    ins = [ops.tensor(dev(T, xT4), (ci, n, h, w), 2), ops.tensor(dev(T, dyT), (co, n, d.shape[2], d.shape[3]))]
+    outs = [ops.tensor(out4, (ci, co, k, k), 2)]
+    assert ex.resize(ins, outs) == 0
+    assert ex.execute(ins, outs) == 0
+    got = oracle.c4_to_nchw(out4.cpu().numpy(), co)  # [ci][co][k][k]
+    assert np.array_equal(got.transpose(1, 0, 2, 3), dw_ref)
+
+
+@pytest.mark.parametrize("m,o,k", [(27, 64, 3 * 256), (500, 12, 64), (4608, 32, 70)])
+def test_exec_matmul_int8(T, ops, oracle, m, o, k):
+    import niti_amd
+    rng = np.random.default_rng(204)
+    B = oracle.synth_x(rng, (m, k))
+    A = oracle.synth_dy(rng, (o, k))
+    dwT_ref, bw, acc, _ = oracle.matmul(B, A)  # dwT_ref [o][m]
+    out = T.zeros((m, o), dtype=T.int8, device="cuda")
+    ex = ops.NITIExecution(niti_amd.OP_MATMUL_INT8, None)
+    ins = [ops.tensor(dev(T, B), (m, k)), ops.tensor(dev(T, A), (o, k))]
+    outs = [ops.tensor(out, (m, o))]
+    assert ex.resize(ins, outs) == 0
+    assert ex.execute(ins, outs) == 0
+    assert np.array_equal(out.cpu().numpy().T, dwT_ref)
+
+
+@pytest.mark.parametrize("geo", [GEOMS[1], GEOMS[4], GEOMS[7]])
+def test_exec_dsp_matmul_gradient(T, ops, oracle, geo):
+    import niti_amd
+    n, ci, h, w, co, k, s, p = geo
+    g = oracle.geom(n, ci, h, w, co, k, stride=s, pad=p)
+    rng = np.random.default_rng(205)
+    x = oracle.synth_x(rng, (n, ci, h, w))
+    dy = oracle.synth_dy(rng, (n, co, g.oh, g.ow))
+    dw_ref, _, _, _ = oracle.conv_wgrad(g, x, dy)
+    out = T.zeros((k, k, ci, co), dtype=T.int8, device="cuda")
+    ex = ops.NITIExecution(niti_amd.OP_DSP_MATMUL_GRADIENT_INT8, ops.conv_common(k, stride=s, pad=p))
+    ins = [ops.tensor(dev(T, x.transpose(0, 2, 3, 1)), (n, ci, h, w), niti_amd.FORMAT_NHWC),
+           ops.tensor(dev(T, dy.transpose(0, 2, 3, 1)), (n, co, g.oh, g.ow), niti_amd.FORMAT_NHWC)]
+    outs = [ops.tensor(out, (k, k, ci, co))]
+    assert ex.resize(ins, outs) == 0
+    assert ex.execute(ins, outs) == 0
+    assert np.array_equal(out.cpu().numpy().transpose(3, 2, 0, 1), dw_ref)
+
+
+# --------------------------------------------------------------------------- requant edge cases
+@pytest.mark.parametrize("vals", [[0, 0, 0], [128, -5, 3], [200, -103, 101], [40000, -1007, 0], [1, -1, 0],
+                                  [2**30, -(2**30) + 7, 12345], [127, -127, 64]])
+def test_requant_act_branches(T, ops, oracle, vals):
+    acc = np.zeros((1, 16), np.int32)
+    acc[0, :len(vals)] = vals
+    want, inc = oracle.requant_fwd(acc)
+    amax = zeros_u32(T)
+    a = dev(T, acc)
+    ops.absmax(a, amax)
+    e = i8s(T, 0)
+    got = ops.requant_act(a, amax, exp_in=i8s(T, 3), wscale=i8s(T, -7), exp_out=e)
+    assert np.array_equal(got.cpu().numpy(), want)
+    assert int(e.item()) == int(np.int8(3 - 7 + inc))
+
+
+@pytest.mark.parametrize("vals", [[0, 0], [1, -1], [2, -1], [3, -2, 1], [4, -3], [5, 7, -9],
+                                  [65536, -65535, 3], [2**31 - 1, 5]])
+@pytest.mark.parametrize("rule", [2, 3])
+def test_requant_grad_rules(T, ops, oracle, vals, rule):
+    acc = np.array(vals, np.int32)
+    want, bw = (oracle.requant_wgrad if rule == 2 else oracle.requant_matmul)(acc)
+    amax = zeros_u32(T)
+    a = dev(T, acc)
+    ops.absmax(a, amax)
+    assert np.array_equal(ops.requant_grad(a, amax, rule=rule).cpu().numpy(), want)
+
+
+def test_psto_all_shifts(T, ops, oracle):
+    """requant_act's PSTO against the oracle for every forward shift 2..24."""
+    rng = np.random.default_rng(7)
+    for s in range(2, 25):
+        top = 1 << (s + 7)
+        acc = rng.integers(-top, top, (64, 16)).astype(np.int32)
+        acc[0, 0] = top  # pin the range estimate
+        want, _ = oracle.requant_fwd(acc)
+        amax = zeros_u32(T)
+        a = dev(T, acc)
+        ops.absmax(a, amax)
+        assert np.array_equal(ops.requant_act(a, amax).cpu().numpy(), want), s
+
+
+# --------------------------------------------------------------------------- rest of the step
+def test_pool_relu_loss_kernels(T, ops, oracle):
+    rng = np.random.default_rng(301)
+    for (n, c, h, w) in [(3, 20, 24, 24), (2, 52, 8, 8), (4, 64, 7, 7)]:
+        y = rng.integers(-127, 128, (n, c, h, w)).astype(np.int8)
+        y[rng.random(y.shape) < 0.3] = 5  # ties
+        r = oracle.relu(y)
+        p_ref = oracle.maxpool(r)
+        r16 = ops.nchw_to_nhwc16(dev(T, r))
+        p16 = ops.maxpool(r16)
+        cp = r16.shape[3]
+        p = p16.cpu().numpy()[..., :c].transpose(0, 3, 1, 2)
+        assert np.array_equal(p, p_ref)
+        dp = oracle.synth_dy(rng, p_ref.shape)
+        dx_ref = oracle.relu_grad(y, oracle.maxpool_grad(r, p_ref, dp))
+        dx16 = ops.maxpool_grad(r16, p16, ops.nchw_to_nhwc16(dev(T, dp)), relu=True)
+        assert np.array_equal(dx16.cpu().numpy()[..., :c].transpose(0, 3, 1, 2), dx_ref)
+        assert not dx16.cpu().numpy()[..., c:].any() or cp == c
+        d = oracle.synth_dy(rng, y.shape)
+        rg = ops.relu_grad(r16, ops.nchw_to_nhwc16(dev(T, d)))
+        assert np.array_equal(rg.cpu().numpy()[..., :c].transpose(0, 3, 1, 2), oracle.relu_grad(y, d))
+    for ascale in (-12, -7, -6, -3, 0, 2):
+        logits = rng.integers(-127, 128, (33, 12)).astype(np.int8)
+        labels = rng.integers(0, 10, 33).astype(np.int32)
+        oh = np.zeros((33, 10), np.int32)
+        oh[np.arange(33), labels] = 1
+        want = oracle.loss_grad(logits, ascale, oh)
+        lg = np.zeros((33, 16), np.int8)
+        lg[:, :12] = logits
+        got = ops.loss_grad(dev(T, lg), 12, i8s(T, ascale), dev(T, labels)).cpu().numpy()
+        assert np.array_equal(got[:, :12], want), ascale
+        assert not got[:, 12:].any()
+
+
+# --------------------------------------------------------------------------- full sizes
+def _sample_check(acc_fn, n_samples, rng):
+    for _ in range(n_samples):
+        ok, got, want = acc_fn(rng)
+        assert ok, (got, want)
+
+
+def test_vgg11_batch256_layers_sampled(T, ops, oracle):
+    """BASELINE cfg 3 sizes (batch 256): every GEMM-class op checked on 512 sampled outputs
+    against exact int64 dot products, plus the split-batch linearity of the weight gradient."""
+    rng = np.random.default_rng(17)
+    for (ci, co, hh) in [(3, 64, 32), (256, 256, 8), (512, 512, 2)]:
+        n, k, p = 256, 3, 1
+        x = oracle.synth_x(rng, (n, ci, hh, hh))
+        wt, _ = oracle.synth_w(rng, (co, ci, k, k))
+        dy = oracle.synth_dy(rng, (n, co, hh, hh))
+        gg = ops.geom(n, ci, hh, hh, co, k, pad=p)
+        xp = np.pad(x, ((0, 0), (0, 0), (1, 1), (1, 1))).astype(np.int64)
+        dyp = np.pad(dy, ((0, 0), (0, 0), (1, 1), (1, 1))).astype(np.int64)
+        # forward
+        amax = zeros_u32(T)
+        acc = ops.conv_fwd_acc(gg, ops.nchw_to_nhwc16(dev(T, x)), ops.oihw_to_ohwi16(dev(T, wt)), amax).cpu().numpy()
+        for _ in range(512):
+            b, o, yy, xx = (int(rng.integers(0, v)) for v in (n, co, hh, hh))
+            want = int((xp[b, :, yy:yy + 3, xx:xx + 3] * wt[o].astype(np.int64)).sum())
+            assert acc[(b * hh + yy) * hh + xx, o] == want
+        # input gradient: dx[b,c,y,x] = sum dy[b,o,y+1-ky,x+1-kx] w[o,c,ky,kx]
+        w16 = ops.oihw_to_ohwi16(dev(T, wt))
+        accd = ops.conv_dgrad_acc(gg, ops.nchw_to_nhwc16(dev(T, dy)), ops.ohwi16_to_ihwo16(w16, ci), amax).cpu().numpy()
+        wf = wt[:, :, ::-1, ::-1].astype(np.int64)
+        for _ in range(512):
+            b, c, yy, xx = (int(rng.integers(0, v)) for v in (n, ci, hh, hh))
+            want = int((dyp[b, :, yy:yy + 3, xx:xx + 3] * wf[:, c]).sum())
+            assert accd[(b * hh + yy) * hh + xx, c] == want
+        # weight gradient + linearity over the batch split
+        xT = ops.nchw_to_chwn16(dev(T, x))
+        dyT = ops.nchw_to_chwn16(dev(T, dy))
+        accw = ops.conv_wgrad_acc(gg, xT, dyT).cpu().numpy()
+        for _ in range(128):
+            o, c, ky, kx = (int(rng.integers(0, v)) for v in (co, ci, 3, 3))
+            want = int((xp[:, c, ky:ky + hh, kx:kx + hh] * dy[:, o].astype(np.int64)).sum())
+            assert accw[o, ky, kx, c] == want
+        g1 = ops.geom(128, ci, hh, hh, co, k, pad=p)
+        a1 = ops.conv_wgrad_acc(g1, ops.nchw_to_chwn16(dev(T, x[:128])), ops.nchw_to_chwn16(dev(T, dy[:128])))
+        a2 = ops.conv_wgrad_acc(g1, ops.nchw_to_chwn16(dev(T, x[128:])), ops.nchw_to_chwn16(dev(T, dy[128:])))
+        assert np.array_equal((a1 + a2).cpu().numpy(), accw)
