@@ -124,18 +124,24 @@ typedef struct niti_geom {
 
 int niti_geom_finalize(niti_geom* g);
 
-/* acc[n*oh*ow][cop] int32 = conv(x, w); *amax = max(*amax, max|acc|)   (caller zeroes amax) */
+/* Device workspace (bytes) an op needs to split K over workgroups when its output has too
+ * few tiles for 256 CUs (op 0 forward, 1 input gradient, 2 weight gradient).  Passing less
+ * (or NULL) is allowed: the op then runs unsplit. */
+int niti_conv_workspace_bytes(const niti_geom* g, int op, size_t* bytes);
+int niti_matmul_workspace_bytes(int m, int ldc, int k16, size_t* bytes);
+/* acc[n*oh*ow][cop] int32 = conv(x, w); if amax: *amax = max(*amax, max|acc|) (caller zeroes it) */
 int niti_conv_fwd_acc(const niti_geom* g, const int8_t* x_nhwc16, const int8_t* w_ohwi16, int32_t* acc,
-                      uint32_t* amax, void* stream);
+                      uint32_t* amax, void* workspace, size_t workspace_bytes, void* stream);
 /* acc[n*h*w][cip] int32 = input gradient of the conv for dy (NHWC16) and w^T (IHWO16) */
 int niti_conv_dgrad_acc(const niti_geom* g, const int8_t* dy_nhwc16, const int8_t* wt_ihwo16, int32_t* acc,
-                        uint32_t* amax, void* stream);
+                        uint32_t* amax, void* workspace, size_t workspace_bytes, void* stream);
 /* acc[co][kh][kw][cip] int32 = weight gradient for x (CHWN16) and dy (CHWN16) */
 int niti_conv_wgrad_acc(const niti_geom* g, const int8_t* x_chwn16, const int8_t* dy_chwn16, int32_t* acc,
-                        void* stream);
-/* acc[m][o] = sum_k B[m][k] A[o][k]; K padded to k16 with zero bytes, ld* in bytes/elements */
+                        uint32_t* amax, void* workspace, size_t workspace_bytes, void* stream);
+/* acc[m][ldc] = sum_k B[m][k] A[o][k] (columns o..ldc = 0); K zero padded to k16; ldb/lda bytes */
 int niti_matmul_acc(int m, int o, int k16, const int8_t* B, int64_t ldb, const int8_t* A, int64_t lda,
-                    int32_t* acc, int64_t ldc, uint32_t* amax, int split_k, void* stream);
+                    int32_t* acc, int64_t ldc, uint32_t* amax, void* workspace, size_t workspace_bytes,
+                    void* stream);
 int niti_absmax_i32(const int32_t* acc, int64_t n, uint32_t* amax, void* stream);
 /* forward/deconv rule (NITI_Conv_Int8.cpp:260-307) on acc[rows][ldc]; exp_out = exp_in + wscale + inc
  * (any exponent pointer may be NULL); relu fuses NITI_Relu_Int8; relu_mask (NHWC16) fuses

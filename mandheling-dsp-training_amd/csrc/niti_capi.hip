@@ -97,27 +97,48 @@ int niti_geom_finalize(niti_geom* g) {
     return NITI_NO_ERROR;
 }
 
-int niti_conv_fwd_acc(const niti_geom* g, const int8_t* x, const int8_t* w, int32_t* acc, uint32_t* amax,
-                      void* stream) {
+int niti_conv_workspace_bytes(const niti_geom* g, int op, size_t* bytes) {
+    if (!g || !bytes) return NITI_INVALID_VALUE;
+    const niti::ConvGeom r = to_geom(g);
+    if (op == 0)
+        *bytes = niti::conv_fwd_workspace(r);
+    else if (op == 1)
+        *bytes = niti::conv_dgrad_workspace(r);
+    else if (op == 2)
+        *bytes = niti::conv_wgrad_workspace(r);
+    else
+        return NITI_INVALID_VALUE;
+    return NITI_NO_ERROR;
+}
+
+int niti_matmul_workspace_bytes(int m, int ldc, int k16, size_t* bytes) {
+    if (!bytes || ldc % 16 || k16 % 16) return NITI_INVALID_VALUE;
+    *bytes = niti::matmul_workspace(m, ldc, k16);
+    return NITI_NO_ERROR;
+}
+
+int niti_conv_fwd_acc(const niti_geom* g, const int8_t* x, const int8_t* w, int32_t* acc, uint32_t* amax, void* ws,
+                      size_t ws_bytes, void* stream) {
     if (!g) return NITI_INVALID_VALUE;
-    return code(niti::conv_fwd_acc(to_geom(g), x, w, acc, amax, S(stream)));
+    return code(niti::conv_fwd_acc(to_geom(g), x, w, acc, amax, ws, ws_bytes, S(stream)));
 }
 
 int niti_conv_dgrad_acc(const niti_geom* g, const int8_t* dy, const int8_t* wt, int32_t* acc, uint32_t* amax,
-                        void* stream) {
+                        void* ws, size_t ws_bytes, void* stream) {
     if (!g) return NITI_INVALID_VALUE;
-    return code(niti::conv_dgrad_acc(to_geom(g), dy, wt, acc, amax, S(stream)));
+    return code(niti::conv_dgrad_acc(to_geom(g), dy, wt, acc, amax, ws, ws_bytes, S(stream)));
 }
 
-int niti_conv_wgrad_acc(const niti_geom* g, const int8_t* x, const int8_t* dy, int32_t* acc, void* stream) {
+int niti_conv_wgrad_acc(const niti_geom* g, const int8_t* x, const int8_t* dy, int32_t* acc, uint32_t* amax,
+                        void* ws, size_t ws_bytes, void* stream) {
     if (!g) return NITI_INVALID_VALUE;
-    return code(niti::conv_wgrad_acc(to_geom(g), x, dy, acc, S(stream)));
+    return code(niti::conv_wgrad_acc(to_geom(g), x, dy, acc, amax, ws, ws_bytes, S(stream)));
 }
 
 int niti_matmul_acc(int m, int o, int k16, const int8_t* B, int64_t ldb, const int8_t* A, int64_t lda, int32_t* acc,
-                    int64_t ldc, uint32_t* amax, int split_k, void* stream) {
-    if (k16 % 16 || ldb % 16 || lda % 16 || ldc % 16) return NITI_INVALID_VALUE;
-    return code(niti::matmul_acc(m, o, k16, B, ldb, A, lda, acc, ldc, amax, split_k != 0, S(stream)));
+                    int64_t ldc, uint32_t* amax, void* ws, size_t ws_bytes, void* stream) {
+    if (k16 % 16 || ldb % 16 || lda % 16 || ldc % 16 || ldc < o) return NITI_INVALID_VALUE;
+    return code(niti::matmul_acc(m, o, k16, B, ldb, A, lda, acc, ldc, amax, ws, ws_bytes, S(stream)));
 }
 
 int niti_absmax_i32(const int32_t* acc, int64_t n, uint32_t* amax, void* stream) {

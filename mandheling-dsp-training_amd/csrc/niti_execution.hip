@@ -215,6 +215,9 @@ class ConvInt8Execution : public Execution {
         w16_ = (int8_t*)ws_.alloc((size_t)g_.c_out * g_.kh * g_.kw * g_.cip);
         acc_ = (int32_t*)ws_.alloc((size_t)g_.n * g_.oh * g_.ow * g_.cop * 4);
         amax_ = (uint32_t*)ws_.alloc(16);
+        slab_bytes_ = conv_fwd_workspace(g_);
+        slab_ = slab_bytes_ ? ws_.alloc(slab_bytes_) : nullptr;
+        if (slab_bytes_ && !slab_) return NITI_OUT_OF_MEMORY;
         return (x16_ && w16_ && acc_ && amax_) ? NITI_NO_ERROR : NITI_OUT_OF_MEMORY;
     }
     int onExecute(const niti_tensor* in, int nin, const niti_tensor* out, int nout, hipStream_t st) override {
@@ -223,7 +226,7 @@ class ConvInt8Execution : public Execution {
         // reorderWeight every call: weights change each step (NITI_Conv_Int8.cpp:177)
         NITI_TRY(oihw_to_ohwi16((const int8_t*)in[1].data, g_.c_out, g_.c_in, g_.kh * g_.kw, g_.cip, w16_, st));
         NITI_TRY(hipMemsetAsync(amax_, 0, 4, st));
-        NITI_TRY(conv_fwd_acc(g_, x16_, w16_, acc_, amax_, st));
+        NITI_TRY(conv_fwd_acc(g_, x16_, w16_, acc_, amax_, slab_, slab_bytes_, st));
         ActRequant r;
         r.acc = acc_;
         r.rows = (int64_t)g_.n * g_.oh * g_.ow;
@@ -246,6 +249,8 @@ class ConvInt8Execution : public Execution {
     int8_t *x16_ = nullptr, *w16_ = nullptr;
     int32_t* acc_ = nullptr;
     uint32_t* amax_ = nullptr;
+    void* slab_ = nullptr;
+    size_t slab_bytes_ = 0;
 };
 
 // ------------------------------------------------------------------ NITI_DeConv_Int8 (701)
@@ -271,6 +276,9 @@ class DeconvInt8Execution : public Execution {
         w16_ = (int8_t*)ws_.alloc((size_t)g_.c_out * g_.kh * g_.kw * g_.cip);
         acc_ = (int32_t*)ws_.alloc((size_t)g_.n * g_.oh * g_.ow * g_.cop * 4);
         amax_ = (uint32_t*)ws_.alloc(16);
+        slab_bytes_ = conv_fwd_workspace(g_);
+        slab_ = slab_bytes_ ? ws_.alloc(slab_bytes_) : nullptr;
+        if (slab_bytes_ && !slab_) return NITI_OUT_OF_MEMORY;
         return (x16_ && w16_ && acc_ && amax_) ? NITI_NO_ERROR : NITI_OUT_OF_MEMORY;
     }
     int onExecute(const niti_tensor* in, int nin, const niti_tensor* out, int nout, hipStream_t st) override {
@@ -278,7 +286,7 @@ class DeconvInt8Execution : public Execution {
         NITI_TRY(c4_to_nhwc16((const int8_t*)in[0].data, g_.n, g_.c_in, g_.h * g_.w, g_.cip, x16_, st));
         NITI_TRY(oihw_to_ohwi16((const int8_t*)in[1].data, g_.c_out, g_.c_in, g_.kh * g_.kw, g_.cip, w16_, st, true));
         NITI_TRY(hipMemsetAsync(amax_, 0, 4, st));
-        NITI_TRY(conv_fwd_acc(g_, x16_, w16_, acc_, amax_, st));
+        NITI_TRY(conv_fwd_acc(g_, x16_, w16_, acc_, amax_, slab_, slab_bytes_, st));
         ActRequant r;
         r.acc = acc_;
         r.rows = (int64_t)g_.n * g_.oh * g_.ow;
@@ -298,6 +306,8 @@ class DeconvInt8Execution : public Execution {
     int8_t *x16_ = nullptr, *w16_ = nullptr;
     int32_t* acc_ = nullptr;
     uint32_t* amax_ = nullptr;
+    void* slab_ = nullptr;
+    size_t slab_bytes_ = 0;
 };
 
 // ------------------------------------------------------------------ NITI_GradientConv_Int8 (715)
@@ -343,6 +353,9 @@ class GradientConvInt8Execution : public Execution {
         acc_ = (int32_t*)ws_.alloc((size_t)g_.c_out * g_.kh * g_.kw * g_.cip * 4);
         g8_ = (int8_t*)ws_.alloc((size_t)g_.c_out * g_.kh * g_.kw * g_.cip);
         amax_ = (uint32_t*)ws_.alloc(16);
+        slab_bytes_ = conv_wgrad_workspace(g_);
+        slab_ = slab_bytes_ ? ws_.alloc(slab_bytes_) : nullptr;
+        if (slab_bytes_ && !slab_) return NITI_OUT_OF_MEMORY;
         return (xT_ && dyT_ && acc_ && g8_ && amax_) ? NITI_NO_ERROR : NITI_OUT_OF_MEMORY;
     }
     int onExecute(const niti_tensor* in, int nin, const niti_tensor* out, int nout, hipStream_t st) override {
@@ -352,10 +365,9 @@ class GradientConvInt8Execution : public Execution {
                             C4TransposedToChwn16{(const int8_t*)in[0].data, g_.n, g_.c_in, hw, g_.np, xT_}, st));
         NITI_TRY(launch_map((int64_t)g_.cop * ohw * g_.np,
                             NchwTransposedToChwn16{(const int8_t*)in[1].data, g_.n, g_.c_out, ohw, g_.np, dyT_}, st));
-        NITI_TRY(conv_wgrad_acc(g_, xT_, dyT_, acc_, st));
         const int64_t nacc = (int64_t)g_.c_out * kk * g_.cip;
         NITI_TRY(hipMemsetAsync(amax_, 0, 4, st));
-        NITI_TRY(absmax_i32(acc_, nacc, amax_, st));
+        NITI_TRY(conv_wgrad_acc(g_, xT_, dyT_, acc_, amax_, slab_, slab_bytes_, st));
         NITI_TRY(requant_grad(acc_, nacc, amax_, RULE_WGRAD_BW2, g8_, nullptr, st));
         NITI_TRY(launch_map((int64_t)((g_.c_out + 3) / 4) * g_.c_in * kk * 4,
                             Ohwi16ToC4Grad{g8_, g_.c_out, g_.c_in, kk, g_.cip, (int8_t*)out[0].data}, st));
@@ -368,6 +380,8 @@ class GradientConvInt8Execution : public Execution {
     int8_t *xT_ = nullptr, *dyT_ = nullptr, *g8_ = nullptr;
     int32_t* acc_ = nullptr;
     uint32_t* amax_ = nullptr;
+    void* slab_ = nullptr;
+    size_t slab_bytes_ = 0;
 };
 
 // ------------------------------------------------------------------ NITI_Matmul_Int8 (713)
@@ -391,15 +405,17 @@ class MatmulInt8Execution : public Execution {
         acc_ = (int32_t*)ws_.alloc((size_t)m_ * ldc_ * 4);
         g8_ = (int8_t*)ws_.alloc((size_t)m_ * ldc_);
         amax_ = (uint32_t*)ws_.alloc(16);
+        slab_bytes_ = matmul_workspace(m_, ldc_, k16_);
+        slab_ = slab_bytes_ ? ws_.alloc(slab_bytes_) : nullptr;
+        if (slab_bytes_ && !slab_) return NITI_OUT_OF_MEMORY;
         return (b16_ && a16_ && acc_ && g8_ && amax_) ? NITI_NO_ERROR : NITI_OUT_OF_MEMORY;
     }
     int onExecute(const niti_tensor* in, int nin, const niti_tensor* out, int nout, hipStream_t st) override {
         if (!acc_) return NITI_NO_EXECUTION;
         NITI_TRY(pad_rows((const int8_t*)in[0].data, m_, k_, k16_, b16_, st));
         NITI_TRY(pad_rows((const int8_t*)in[1].data, o_, k_, k16_, a16_, st));
-        NITI_TRY(matmul_acc(m_, o_, k16_, b16_, k16_, a16_, k16_, acc_, ldc_, nullptr, true, st));
         NITI_TRY(hipMemsetAsync(amax_, 0, 4, st));
-        NITI_TRY(absmax_i32(acc_, (int64_t)m_ * ldc_, amax_, st));
+        NITI_TRY(matmul_acc(m_, o_, k16_, b16_, k16_, a16_, k16_, acc_, ldc_, amax_, slab_, slab_bytes_, st));
         NITI_TRY(requant_grad(acc_, (int64_t)m_ * ldc_, amax_, RULE_MATMUL_BW3, g8_, nullptr, st));
         NITI_TRY(launch_map((int64_t)m_ * o_, UnpadRows{g8_, o_, ldc_, (int8_t*)out[0].data}, st));
         return NITI_NO_ERROR;
@@ -410,6 +426,8 @@ class MatmulInt8Execution : public Execution {
     int8_t *b16_ = nullptr, *a16_ = nullptr, *g8_ = nullptr;
     int32_t* acc_ = nullptr;
     uint32_t* amax_ = nullptr;
+    void* slab_ = nullptr;
+    size_t slab_bytes_ = 0;
 };
 
 // ------------------------------------------------------------------ NITI_DSP_MATMUL_GRADIENT_Int8 (818)
@@ -437,6 +455,9 @@ class DspMatmulGradientExecution : public Execution {
         acc_ = (int32_t*)ws_.alloc((size_t)g_.c_out * kh * kw * g_.cip * 4);
         g8_ = (int8_t*)ws_.alloc((size_t)g_.c_out * kh * kw * g_.cip);
         amax_ = (uint32_t*)ws_.alloc(16);
+        slab_bytes_ = conv_wgrad_workspace(g_);
+        slab_ = slab_bytes_ ? ws_.alloc(slab_bytes_) : nullptr;
+        if (slab_bytes_ && !slab_) return NITI_OUT_OF_MEMORY;
         return (xT_ && dyT_ && acc_ && g8_ && amax_) ? NITI_NO_ERROR : NITI_OUT_OF_MEMORY;
     }
     int onExecute(const niti_tensor* in, int nin, const niti_tensor* out, int nout, hipStream_t st) override {
@@ -444,10 +465,9 @@ class DspMatmulGradientExecution : public Execution {
         const int hw = g_.h * g_.w, ohw = g_.oh * g_.ow, kk = g_.kh * g_.kw;
         NITI_TRY(launch_map((int64_t)g_.cip * hw * g_.np, NhwcToChwn16{(const int8_t*)in[0].data, g_.n, g_.c_in, hw, g_.np, xT_}, st));
         NITI_TRY(launch_map((int64_t)g_.cop * ohw * g_.np, NhwcToChwn16{(const int8_t*)in[1].data, g_.n, g_.c_out, ohw, g_.np, dyT_}, st));
-        NITI_TRY(conv_wgrad_acc(g_, xT_, dyT_, acc_, st));
         const int64_t nacc = (int64_t)g_.c_out * kk * g_.cip;
         NITI_TRY(hipMemsetAsync(amax_, 0, 4, st));
-        NITI_TRY(absmax_i32(acc_, nacc, amax_, st));
+        NITI_TRY(conv_wgrad_acc(g_, xT_, dyT_, acc_, amax_, slab_, slab_bytes_, st));
         NITI_TRY(requant_grad(acc_, nacc, amax_, RULE_WGRAD_BW2, g8_, nullptr, st));
         NITI_TRY(launch_map((int64_t)kk * g_.c_in * g_.c_out, Ohwi16ToHwio{g8_, g_.c_out, g_.c_in, kk, g_.cip, (int8_t*)out[0].data}, st));
         return NITI_NO_ERROR;
@@ -459,6 +479,8 @@ class DspMatmulGradientExecution : public Execution {
     int8_t *xT_ = nullptr, *dyT_ = nullptr, *g8_ = nullptr;
     int32_t* acc_ = nullptr;
     uint32_t* amax_ = nullptr;
+    void* slab_ = nullptr;
+    size_t slab_bytes_ = 0;
 };
 
 Execution* create_execution(int op_type, const niti_conv2d_common* c, int* err) {

@@ -155,15 +155,47 @@ struct LoadWgradX {
 };
 
 // =====================================================================================
-// The GEMM: C[m][n] = sum_k A[m][k] * B[n][k], int8 x int8 -> exact int32.
-//   256 threads = 4 waves; BM x BN block tile; 64-byte K step (two 32-deep MFMAs);
-//   LDS double buffer with one barrier per step; 16-byte chunks XOR-swizzled so the
-//   ds_read_b128 fragment reads of 32 rows are bank-conflict free.
+// Range estimate and PSTO helpers (used by the GEMM epilogue and the requant kernels)
 // =====================================================================================
-constexpr int BK = 64;        // K bytes per step
-constexpr int CPS = BK / 16;  // 16-byte chunks per row per step
 
-__device__ __forceinline__ int lds_off(int r, int c) { return r * BK + ((c ^ ((r >> 2) & 3)) << 4); }
+// NITI_RangeEstimate on the max word: ceil(log2(m)), 0 for m <= 1.
+__device__ __forceinline__ int bitwidth_of(uint32_t m) { return m <= 1u ? 0 : 32 - __clz((int)(m - 1u)); }
+
+__device__ __forceinline__ int32_t clip127(int32_t a) { return a > 127 ? 127 : (a < -127 ? -127 : a); }
+
+// (1 << s) as the reference's x86 build executes it for a run-time s (count & 31).
+__device__ __forceinline__ int32_t pow2_x86(int s) { return (int32_t)(1u << ((unsigned)s & 31u)); }
+
+// NITI_MNNPstoShiftInt32 (CommonOptFunction.cpp:1595-1627), exact for any shift the
+// reference can produce; the fast path covers 0 <= s <= 30.
+__device__ __forceinline__ int32_t psto_fast(int32_t a, int s) {
+    const uint32_t ua = a < 0 ? 0u - (uint32_t)a : (uint32_t)a;
+    const uint32_t q = ua >> s;
+    const uint32_t prob = ua & ((1u << s) - 1u);
+    const int h = s >> 1;
+    const uint32_t qp = prob >> h;
+    uint32_t pr = prob & ((1u << h) - 1u);
+    if (s & 1) pr <<= 1;
+    const int32_t r = (int32_t)q + (qp > pr ? 1 : 0);
+    return clip127(a < 0 ? -r : r);
+}
+
+__device__ int32_t psto_generic(int32_t a, int s) {
+    const int32_t p = pow2_x86(s);
+    const int32_t q = a / p;
+    int32_t prob = (int32_t)((uint32_t)a - (uint32_t)q * (uint32_t)p);
+    prob = prob < 0 ? -prob : prob;
+    const int32_t hp = pow2_x86(s / 2);
+    const int32_t qp = prob / hp;
+    int32_t pr = (int32_t)((uint32_t)prob - (uint32_t)qp * (uint32_t)hp);
+    if (s % 2 == 1) pr = (int32_t)((uint32_t)pr * 2u);
+    const int32_t sg = a > 0 ? 1 : (a < 0 ? -1 : 0);
+    return clip127((int32_t)((uint32_t)q + (uint32_t)((qp > pr) * sg)));
+}
+
+__device__ __forceinline__ int32_t psto_any(int32_t a, int s) {
+    return (s >= 0 && s <= 30) ? psto_fast(a, s) : psto_generic(a, s);
+}
 
 __device__ __forceinline__ uint32_t uabs32(int v) { return v < 0 ? 0u - (uint32_t)v : (uint32_t)v; }
 
@@ -176,10 +208,56 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
     return v;
 }
 
-template <int BM, int BN, int WM, int WN, class LA, class LB, bool ATOMIC>
-__global__ void __launch_bounds__(256) gemm_i8_kernel(LA la, LB lb, int M, int N, int tiles_n,
-                                                       int kc_total, int kc_per_split, int32_t* __restrict__ C,
-                                                       int64_t ldc, uint32_t* __restrict__ amax) {
+// One atomic per workgroup, skipped when the word already holds a larger value (the
+// single max word is otherwise a serialisation point for thousands of workgroups).
+__device__ __forceinline__ void publish_max(uint32_t* amax, uint32_t m) {
+    if (m != 0u && m > __hip_atomic_load(amax, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(amax, m);
+}
+
+// =====================================================================================
+// The GEMM: C[m][n] = sum_k A[m][k] * B[n][k], int8 x int8 -> exact int32.
+//   256 threads = 4 waves; BM x BN block tile; 64-byte K step (two 32-deep MFMAs);
+//   LDS double buffer with one barrier per step; 16-byte chunks XOR-swizzled so the
+//   ds_read_b128 fragment reads of 32 rows are bank-conflict free.  Workgroups are
+//   remapped so each XCD walks a contiguous range of tiles (A-row panels stay in one L2).
+// Epilogues:
+//   EPI_STORE    int32 C + max|C| (one word, agent-scope atomic)
+//   EPI_AMAX     max|C| only                          (first pass of the recompute strategy)
+//   EPI_REQUANT  reads the max word, applies the NITI forward shift rule, writes int8
+//                (+ fused relu / relu-grad mask, + exponent)   (second pass)
+//   EPI_SLAB     int32 partial sums of one K split -> slab[blockIdx.y] (reduced later)
+// =====================================================================================
+constexpr int BK = 64;        // K bytes per step
+constexpr int CPS = BK / 16;  // 16-byte chunks per row per step
+
+enum EpiMode { EPI_STORE = 0, EPI_AMAX = 1, EPI_REQUANT = 2, EPI_SLAB = 3 };
+
+struct Epi {
+    int32_t* C = nullptr;  // STORE: C; SLAB: slab base
+    int64_t ldc = 0;
+    int64_t slab_stride = 0;  // elements between K-split slabs
+    uint32_t* amax = nullptr;
+    int8_t* out = nullptr;  // REQUANT output [M][ldo]
+    int64_t ldo = 0;
+    int relu = 0;
+    const int8_t* relu_mask = nullptr;  // [M][ldo]
+    const int8_t* exp_in = nullptr;
+    const int8_t* wscale = nullptr;
+    int8_t* exp_out = nullptr;
+};
+
+__device__ __forceinline__ int lds_off(int r, int c) { return r * BK + ((c ^ ((r >> 2) & 3)) << 4); }
+
+// bijective XCD remap: blocks b, b+8, b+16, ... (one XCD under round-robin dispatch) get
+// consecutive tile ids.  Speed only; any placement is correct.
+__device__ __forceinline__ int xcd_remap(int b, int nwg) {
+    const int xcd = b & 7, q = nwg >> 3, r = nwg & 7;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+}
+
+template <int BM, int BN, int WM, int WN, class LA, class LB, int MODE>
+__global__ void __launch_bounds__(256) gemm_i8_kernel(LA la, LB lb, int M, int N, int tiles_n, int kc_total,
+                                                       int kc_per_split, Epi epi) {
     static_assert(WM * WN == 4, "4 waves");
     constexpr int TM = BM / WM / 32;
     constexpr int TN = BN / WN / 32;
@@ -197,7 +275,8 @@ __global__ void __launch_bounds__(256) gemm_i8_kernel(LA la, LB lb, int M, int N
     const int lane = tid & 63;
     const int wid = tid >> 6;
     const int wm = wid / WN, wn = wid % WN;
-    const int tm_ = blockIdx.x / tiles_n, tn_ = blockIdx.x % tiles_n;
+    const int tile = xcd_remap(blockIdx.x, gridDim.x);
+    const int tm_ = tile / tiles_n, tn_ = tile % tiles_n;
     const int m0 = tm_ * BM, n0 = tn_ * BN;
     const int kc_begin = blockIdx.y * kc_per_split;
     const int kc_end = min(kc_total, kc_begin + kc_per_split);
@@ -273,6 +352,20 @@ __global__ void __launch_bounds__(256) gemm_i8_kernel(LA la, LB lb, int M, int N
     }
 
     // epilogue: D[row][col], row = (i&3) + 8*(i>>2) + 4*(lane>>5), col = lane&31
+    int rq_shift = 2;
+    bool rq_raw = false;
+    if (MODE == EPI_REQUANT) {
+        const int shift = bitwidth_of(*epi.amax) - 7;  // NITI_Conv_Int8.cpp:262-307
+        rq_shift = shift > 1 ? shift : 2;
+        rq_raw = shift <= 0;
+        if (blockIdx.x == 0 && blockIdx.y == 0 && tid == 0 && epi.exp_out != nullptr) {
+            const int inc = shift > 1 ? shift : (shift == 1 ? 2 : 0);
+            const int ein = epi.exp_in ? (int)*epi.exp_in : 0;
+            const int ws = epi.wscale ? (int)*epi.wscale : 0;
+            *epi.exp_out = (int8_t)(ein + ws + inc);
+        }
+    }
+    int32_t* Cs = MODE == EPI_SLAB ? epi.C + (int64_t)blockIdx.y * epi.slab_stride : epi.C;
     uint32_t lmax = 0;
 #pragma unroll
     for (int a = 0; a < TM; ++a)
@@ -284,17 +377,21 @@ __global__ void __launch_bounds__(256) gemm_i8_kernel(LA la, LB lb, int M, int N
                 const int row = m0 + wm * (BM / WM) + a * 32 + (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
                 const int v = acc[a][b][i];
                 if (row < M && col < N) {
-                    if (ATOMIC) {
-                        if (v != 0) atomicAdd(C + (int64_t)row * ldc + col, v);
-                    } else {
-                        C[(int64_t)row * ldc + col] = v;
+                    if (MODE == EPI_STORE || MODE == EPI_SLAB) Cs[(int64_t)row * epi.ldc + col] = v;
+                    if (MODE == EPI_STORE || MODE == EPI_AMAX) {
                         const uint32_t u = uabs32(v);
                         lmax = lmax > u ? lmax : u;
+                    }
+                    if (MODE == EPI_REQUANT) {
+                        int32_t q = rq_raw ? (int32_t)(int8_t)v : psto_any(v, rq_shift);
+                        if (epi.relu && q < 0) q = 0;
+                        if (epi.relu_mask != nullptr && epi.relu_mask[(int64_t)row * epi.ldo + col] <= 0) q = 0;
+                        epi.out[(int64_t)row * epi.ldo + col] = (int8_t)q;
                     }
                 }
             }
         }
-    if (!ATOMIC && amax != nullptr) {
+    if (MODE == EPI_STORE || MODE == EPI_AMAX) {
         lmax = wave_max(lmax);
         uint32_t* red = (uint32_t*)smem;  // all LDS reads finished at the last barrier
         if (lane == 0) red[wid] = lmax;
@@ -302,48 +399,182 @@ __global__ void __launch_bounds__(256) gemm_i8_kernel(LA la, LB lb, int M, int N
         if (tid == 0) {
             uint32_t m = red[0];
             for (int i = 1; i < 4; ++i) m = m > red[i] ? m : red[i];
-            if (m) atomicMax(amax, m);
+            if (epi.amax != nullptr) publish_max(epi.amax, m);
         }
     }
 }
 
-template <class LA, class LB, bool ATOMIC>
-static hipError_t launch_gemm(const LA& la, const LB& lb, int M, int N, int kc_total, int splits, int32_t* C,
-                              int64_t ldc, uint32_t* amax, hipStream_t st) {
-    if (M <= 0 || N <= 0) return hipSuccess;
-    if (splits < 1) splits = 1;
-    const int kc_per_split = ((kc_total + splits - 1) / splits + CPS - 1) / CPS * CPS;
-    splits = kc_per_split > 0 ? (kc_total + kc_per_split - 1) / kc_per_split : 1;
-    if (splits < 1) splits = 1;
-#define NITI_LAUNCH(BM_, BN_, WM_, WN_)                                                                   \
-    do {                                                                                                  \
-        const int tm = (M + BM_ - 1) / BM_, tn = (N + BN_ - 1) / BN_;                                     \
-        dim3 grid(tm * tn, splits);                                                                       \
-        hipLaunchKernelGGL((gemm_i8_kernel<BM_, BN_, WM_, WN_, LA, LB, ATOMIC>), grid, dim3(256), 0, st, \
-                           la, lb, M, N, tn, kc_total, kc_per_split, C, ldc, amax);                       \
+// Sum of K-split slabs -> C (+ max|C|).  n = elements per slab (multiple of 4).
+__global__ void splitk_reduce_kernel(const int32_t* __restrict__ slab, int splits, int64_t stride, int64_t n4,
+                                     int32_t* __restrict__ C, uint32_t* __restrict__ amax) {
+    uint32_t m = 0;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+        v4i s = ((const v4i*)slab)[i];
+        for (int z = 1; z < splits; ++z) s += ((const v4i*)(slab + z * stride))[i];
+        ((v4i*)C)[i] = s;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t u = uabs32(s[j]);
+            m = m > u ? m : u;
+        }
+    }
+    if (amax != nullptr) {
+        m = wave_max(m);
+        __shared__ uint32_t red[4];
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            for (int i = 1; i < 4; ++i) m = m > red[i] ? m : red[i];
+            m = m > red[0] ? m : red[0];
+            publish_max(amax, m);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------ planning
+enum Strategy { STRAT_STORE = 0, STRAT_RECOMPUTE = 1, STRAT_SLAB = 2 };
+
+struct GemmPlan {
+    int bm = 128, bn = 128, tiles = 1, splits = 1, kc_per_split = 0;
+    Strategy strat = STRAT_STORE;
+};
+
+static GemmPlan plan_gemm(int M, int N, int kc_total, bool recompute_ok, size_t ws_elems) {
+    GemmPlan p;
+    p.bn = N <= 32 ? 32 : (N <= 64 ? 64 : 128);
+    p.bm = (M <= 64 && p.bn >= 64) ? 64 : 128;
+    p.tiles = ((M + p.bm - 1) / p.bm) * ((N + p.bn - 1) / p.bn);
+    const int steps = (kc_total + CPS - 1) / CPS;
+    p.kc_per_split = steps * CPS;
+    if (p.tiles >= 160 || steps < 24) {
+        // enough workgroups: one pass; small K makes recomputing cheaper than an int32 round trip
+        p.strat = (recompute_ok && kc_total * 16 <= 1152) ? STRAT_RECOMPUTE : STRAT_STORE;
+        return p;
+    }
+    int s = (320 + p.tiles - 1) / p.tiles;
+    const int max_s = steps / 8;
+    if (s > max_s) s = max_s;
+    const size_t slab = (size_t)M * N;
+    while (s > 1 && (size_t)s * slab > ws_elems) --s;
+    if (s < 2) {
+        p.strat = STRAT_STORE;
+        return p;
+    }
+    const int per = ((steps + s - 1) / s) * CPS;
+    p.splits = (kc_total + per - 1) / per;
+    p.kc_per_split = per;
+    p.strat = STRAT_SLAB;
+    return p;
+}
+
+static size_t plan_ws_elems(int M, int N, int kc_total) {
+    GemmPlan p = plan_gemm(M, N, kc_total, false, (size_t)-1);
+    return p.strat == STRAT_SLAB ? (size_t)p.splits * M * N : 0;
+}
+
+template <class LA, class LB, int MODE>
+static hipError_t launch_mode(const GemmPlan& p, const LA& la, const LB& lb, int M, int N, int kc_total,
+                              const Epi& epi, hipStream_t st) {
+    const int splits = MODE == EPI_SLAB ? p.splits : 1;
+    const int per = MODE == EPI_SLAB ? p.kc_per_split : ((kc_total + CPS - 1) / CPS) * CPS;
+#define NITI_LAUNCH(BM_, BN_, WM_, WN_)                                                                \
+    do {                                                                                               \
+        const int tm = (M + BM_ - 1) / BM_, tn = (N + BN_ - 1) / BN_;                                  \
+        dim3 grid(tm * tn, splits);                                                                    \
+        hipLaunchKernelGGL((gemm_i8_kernel<BM_, BN_, WM_, WN_, LA, LB, MODE>), grid, dim3(256), 0, st, \
+                           la, lb, M, N, tn, kc_total, per, epi);                                      \
     } while (0)
-    if (N <= 32)
+    if (p.bn == 32)
         NITI_LAUNCH(128, 32, 4, 1);
-    else if (N <= 64)
+    else if (p.bn == 64 && p.bm == 64)
+        NITI_LAUNCH(64, 64, 2, 2);
+    else if (p.bn == 64)
         NITI_LAUNCH(128, 64, 2, 2);
+    else if (p.bm == 64)
+        NITI_LAUNCH(64, 128, 1, 4);
     else
         NITI_LAUNCH(128, 128, 2, 2);
 #undef NITI_LAUNCH
     return hipGetLastError();
 }
 
-static int choose_splits(int M, int N, int kc_total) {
-    // enough workgroups for 256 CUs (x2), but keep >= 8 K-steps per split
-    const int tiles = ((M + 127) / 128) * ((N + 127) / 128);
-    const int steps = (kc_total + CPS - 1) / CPS;
-    int s = (512 + tiles - 1) / tiles;
-    const int max_s = steps / 8 > 1 ? steps / 8 : 1;
-    if (s > max_s) s = max_s;
-    return s < 1 ? 1 : s;
+static hipError_t splitk_reduce(const GemmPlan& p, const int32_t* slab, int64_t n, int32_t* C, uint32_t* amax,
+                                hipStream_t st) {
+    int64_t blocks = (n / 4 + 255) / 256;
+    if (blocks > 1024) blocks = 1024;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, st, slab, p.splits, n, n / 4, C,
+                       amax);
+    return hipGetLastError();
 }
 
-hipError_t conv_fwd_acc(const ConvGeom& g, const int8_t* x, const int8_t* w, int32_t* acc, uint32_t* amax,
-                        hipStream_t st) {
+// Materialise C [M][N] int32 (+ max|C| if amax): STORE, or SLAB + reduce.
+template <class LA, class LB>
+static hipError_t gemm_acc(const LA& la, const LB& lb, int M, int N, int kc_total, int32_t* C, uint32_t* amax,
+                           int32_t* ws, size_t ws_elems, hipStream_t st) {
+    if (M <= 0 || N <= 0) return hipSuccess;
+    GemmPlan p = plan_gemm(M, N, kc_total, false, ws ? ws_elems : 0);
+    Epi e;
+    if (p.strat == STRAT_SLAB) {
+        e.C = ws;
+        e.ldc = N;
+        e.slab_stride = (int64_t)M * N;
+        hipError_t r = launch_mode<LA, LB, EPI_SLAB>(p, la, lb, M, N, kc_total, e, st);
+        if (r != hipSuccess) return r;
+        return splitk_reduce(p, ws, (int64_t)M * N, C, amax, st);
+    }
+    e.C = C;
+    e.ldc = N;
+    e.amax = amax;
+    return launch_mode<LA, LB, EPI_STORE>(p, la, lb, M, N, kc_total, e, st);
+}
+
+// Two-phase activation GEMM (forward / input gradient): phase 1 establishes max|acc| (and
+// materialises acc unless the plan recomputes); phase 2 writes the requantised int8.
+template <class LA, class LB>
+static hipError_t act_phase1(const LA& la, const LB& lb, int M, int N, int kc_total, int32_t* acc, uint32_t* amax,
+                             int32_t* ws, size_t ws_elems, hipStream_t st) {
+    GemmPlan p = plan_gemm(M, N, kc_total, true, ws ? ws_elems : 0);
+    if (p.strat == STRAT_RECOMPUTE) {
+        Epi e;
+        e.amax = amax;
+        return launch_mode<LA, LB, EPI_AMAX>(p, la, lb, M, N, kc_total, e, st);
+    }
+    return gemm_acc(la, lb, M, N, kc_total, acc, amax, ws, ws_elems, st);
+}
+
+template <class LA, class LB>
+static hipError_t act_phase2(const LA& la, const LB& lb, int M, int N, int kc_total, const int32_t* acc,
+                             const uint32_t* amax, const ActOut& o, size_t ws_elems, hipStream_t st) {
+    GemmPlan p = plan_gemm(M, N, kc_total, true, ws_elems);
+    if (p.strat == STRAT_RECOMPUTE) {
+        Epi e;
+        e.amax = const_cast<uint32_t*>(amax);
+        e.out = o.out;
+        e.ldo = N;
+        e.relu = o.relu;
+        e.relu_mask = o.relu_mask;
+        e.exp_in = o.exp_in;
+        e.wscale = o.wscale;
+        e.exp_out = o.exp_out;
+        return launch_mode<LA, LB, EPI_REQUANT>(p, la, lb, M, N, kc_total, e, st);
+    }
+    ActRequant r;
+    r.acc = acc;
+    r.rows = M;
+    r.ldc = N;
+    r.amax = amax;
+    r.exp_in = o.exp_in;
+    r.wscale = o.wscale;
+    r.exp_out = o.exp_out;
+    r.relu = o.relu;
+    r.relu_mask = o.relu_mask;
+    r.out_nhwc16 = o.out;
+    return requant_act(r, st);
+}
+
+// ------------------------------------------------------------------------------ per-op wrappers
+static LoadConvFwd fwd_loader(const ConvGeom& g, const int8_t* x) {
     LoadConvFwd la;
     la.x = x;
     la.H = g.h;
@@ -361,12 +592,9 @@ hipError_t conv_fwd_acc(const ConvGeom& g, const int8_t* x, const int8_t* w, int
     la.M = g.n * g.oh * g.ow;
     la.kc_total = g.kh * g.kw * la.CPC;
     la.img = (int64_t)g.h * g.w * g.cip;
-    LoadRowMajor lb{w, (int64_t)g.kh * g.kw * g.cip, g.c_out, la.kc_total};
-    return launch_gemm<LoadConvFwd, LoadRowMajor, false>(la, lb, la.M, g.cop, la.kc_total, 1, acc, g.cop, amax, st);
+    return la;
 }
-
-hipError_t conv_dgrad_acc(const ConvGeom& g, const int8_t* dy, const int8_t* wt, int32_t* acc, uint32_t* amax,
-                          hipStream_t st) {
+static LoadConvDgrad dgrad_loader(const ConvGeom& g, const int8_t* dy) {
     LoadConvDgrad la;
     la.dy = dy;
     la.OH = g.oh;
@@ -384,21 +612,14 @@ hipError_t conv_dgrad_acc(const ConvGeom& g, const int8_t* dy, const int8_t* wt,
     la.M = g.n * g.h * g.w;
     la.kc_total = g.kh * g.kw * la.CPC;
     la.img = (int64_t)g.oh * g.ow * g.cop;
-    LoadRowMajor lb{wt, (int64_t)g.kh * g.kw * g.cop, g.c_in, la.kc_total};
-    return launch_gemm<LoadConvDgrad, LoadRowMajor, false>(la, lb, la.M, g.cip, la.kc_total, 1, acc, g.cip, amax, st);
+    return la;
 }
-
-hipError_t conv_wgrad_acc(const ConvGeom& g, const int8_t* xT, const int8_t* dyT, int32_t* acc, hipStream_t st,
-                          bool zero) {
-    const int npc = g.np / 16;
-    const int kc_total = g.oh * g.ow * npc;
-    const int M = g.c_out, N = g.kh * g.kw * g.cip;
-    LoadRowMajor la{dyT, (int64_t)g.oh * g.ow * g.np, g.c_out, kc_total};
+static LoadWgradX wgrad_loader(const ConvGeom& g, const int8_t* xT) {
     LoadWgradX lb;
     lb.xT = xT;
     lb.H = g.h;
     lb.W = g.w;
-    lb.NPC = npc;
+    lb.NPC = g.np / 16;
     lb.OW = g.ow;
     lb.sh = g.sh;
     lb.sw = g.sw;
@@ -408,73 +629,80 @@ hipError_t conv_wgrad_acc(const ConvGeom& g, const int8_t* xT, const int8_t* dyT
     lb.dw = g.dw;
     lb.KW = g.kw;
     lb.CIP = g.cip;
-    lb.rows = N;
-    lb.kc_total = kc_total;
+    lb.rows = g.kh * g.kw * g.cip;
+    lb.kc_total = g.oh * g.ow * lb.NPC;
     lb.plane = (int64_t)g.h * g.w * g.np;
-    if (zero) {
-        hipError_t e = hipMemsetAsync(acc, 0, (size_t)M * N * sizeof(int32_t), st);
-        if (e != hipSuccess) return e;
-    }
-    return launch_gemm<LoadRowMajor, LoadWgradX, true>(la, lb, M, N, kc_total, choose_splits(M, N, kc_total), acc, N,
-                                                       nullptr, st);
+    return lb;
 }
 
-hipError_t matmul_acc(int M, int O, int k16, const int8_t* B, int64_t ldb, const int8_t* A, int64_t lda,
-                      int32_t* acc, int64_t ldc, uint32_t* amax, bool split_k, hipStream_t st) {
+size_t conv_fwd_workspace(const ConvGeom& g) {
+    return plan_ws_elems(g.n * g.oh * g.ow, g.cop, g.kh * g.kw * g.cip / 16) * sizeof(int32_t);
+}
+size_t conv_dgrad_workspace(const ConvGeom& g) {
+    return plan_ws_elems(g.n * g.h * g.w, g.cip, g.kh * g.kw * g.cop / 16) * sizeof(int32_t);
+}
+size_t conv_wgrad_workspace(const ConvGeom& g) {
+    return plan_ws_elems(g.c_out, g.kh * g.kw * g.cip, g.oh * g.ow * g.np / 16) * sizeof(int32_t);
+}
+size_t matmul_workspace(int M, int ldc, int k16) { return plan_ws_elems(M, ldc, k16 / 16) * sizeof(int32_t); }
+
+hipError_t conv_fwd_acc(const ConvGeom& g, const int8_t* x, const int8_t* w, int32_t* acc, uint32_t* amax,
+                        void* ws, size_t ws_bytes, hipStream_t st) {
+    LoadConvFwd la = fwd_loader(g, x);
+    LoadRowMajor lb{w, (int64_t)g.kh * g.kw * g.cip, g.c_out, la.kc_total};
+    return gemm_acc(la, lb, la.M, g.cop, la.kc_total, acc, amax, (int32_t*)ws, ws_bytes / 4, st);
+}
+
+hipError_t conv_dgrad_acc(const ConvGeom& g, const int8_t* dy, const int8_t* wt, int32_t* acc, uint32_t* amax,
+                          void* ws, size_t ws_bytes, hipStream_t st) {
+    LoadConvDgrad la = dgrad_loader(g, dy);
+    LoadRowMajor lb{wt, (int64_t)g.kh * g.kw * g.cop, g.c_in, la.kc_total};
+    return gemm_acc(la, lb, la.M, g.cip, la.kc_total, acc, amax, (int32_t*)ws, ws_bytes / 4, st);
+}
+
+hipError_t conv_wgrad_acc(const ConvGeom& g, const int8_t* xT, const int8_t* dyT, int32_t* acc, uint32_t* amax,
+                          void* ws, size_t ws_bytes, hipStream_t st) {
+    LoadWgradX lb = wgrad_loader(g, xT);
+    LoadRowMajor la{dyT, (int64_t)g.oh * g.ow * g.np, g.c_out, lb.kc_total};
+    return gemm_acc(la, lb, g.c_out, lb.rows, lb.kc_total, acc, amax, (int32_t*)ws, ws_bytes / 4, st);
+}
+
+hipError_t matmul_acc(int M, int O, int k16, const int8_t* B, int64_t ldb, const int8_t* A, int64_t lda, int32_t* acc,
+                      int64_t ldc, uint32_t* amax, void* ws, size_t ws_bytes, hipStream_t st) {
     const int kc_total = k16 / 16;
     LoadRowMajor la{B, ldb, M, kc_total};
-    LoadRowMajor lb{A, lda, O, kc_total};
-    if (split_k) {
-        hipError_t e = hipMemsetAsync(acc, 0, (size_t)M * ldc * sizeof(int32_t), st);
-        if (e != hipSuccess) return e;
-        return launch_gemm<LoadRowMajor, LoadRowMajor, true>(la, lb, M, O, kc_total, choose_splits(M, O, kc_total),
-                                                             acc, ldc, nullptr, st);
-    }
-    return launch_gemm<LoadRowMajor, LoadRowMajor, false>(la, lb, M, O, kc_total, 1, acc, ldc, amax, st);
+    LoadRowMajor lb{A, lda, O, kc_total};  // rows >= O read as zero, so columns O..ldc are 0
+    return gemm_acc(la, lb, M, (int)ldc, kc_total, acc, amax, (int32_t*)ws, ws_bytes / 4, st);
+}
+
+hipError_t conv_fwd_phase1(const ConvGeom& g, const int8_t* x, const int8_t* w, int32_t* acc, uint32_t* amax,
+                           void* ws, size_t ws_bytes, hipStream_t st) {
+    LoadConvFwd la = fwd_loader(g, x);
+    LoadRowMajor lb{w, (int64_t)g.kh * g.kw * g.cip, g.c_out, la.kc_total};
+    return act_phase1(la, lb, la.M, g.cop, la.kc_total, acc, amax, (int32_t*)ws, ws_bytes / 4, st);
+}
+hipError_t conv_fwd_phase2(const ConvGeom& g, const int8_t* x, const int8_t* w, const int32_t* acc,
+                           const uint32_t* amax, const ActOut& o, size_t ws_bytes, hipStream_t st) {
+    LoadConvFwd la = fwd_loader(g, x);
+    LoadRowMajor lb{w, (int64_t)g.kh * g.kw * g.cip, g.c_out, la.kc_total};
+    return act_phase2(la, lb, la.M, g.cop, la.kc_total, acc, amax, o, ws_bytes / 4, st);
+}
+hipError_t conv_dgrad_phase1(const ConvGeom& g, const int8_t* dy, const int8_t* wt, int32_t* acc, uint32_t* amax,
+                             void* ws, size_t ws_bytes, hipStream_t st) {
+    LoadConvDgrad la = dgrad_loader(g, dy);
+    LoadRowMajor lb{wt, (int64_t)g.kh * g.kw * g.cop, g.c_in, la.kc_total};
+    return act_phase1(la, lb, la.M, g.cip, la.kc_total, acc, amax, (int32_t*)ws, ws_bytes / 4, st);
+}
+hipError_t conv_dgrad_phase2(const ConvGeom& g, const int8_t* dy, const int8_t* wt, const int32_t* acc,
+                             const uint32_t* amax, const ActOut& o, size_t ws_bytes, hipStream_t st) {
+    LoadConvDgrad la = dgrad_loader(g, dy);
+    LoadRowMajor lb{wt, (int64_t)g.kh * g.kw * g.cop, g.c_in, la.kc_total};
+    return act_phase2(la, lb, la.M, g.cip, la.kc_total, acc, amax, o, ws_bytes / 4, st);
 }
 
 // =====================================================================================
 // Range estimate and requantisation
 // =====================================================================================
-
-// NITI_RangeEstimate on the max word: ceil(log2(m)), 0 for m <= 1.
-__device__ __forceinline__ int bitwidth_of(uint32_t m) { return m <= 1u ? 0 : 32 - __clz((int)(m - 1u)); }
-
-__device__ __forceinline__ int32_t clip127(int32_t a) { return a > 127 ? 127 : (a < -127 ? -127 : a); }
-
-// (1 << s) as the reference's x86 build executes it for a run-time s (count & 31).
-__device__ __forceinline__ int32_t pow2_x86(int s) { return (int32_t)(1u << ((unsigned)s & 31u)); }
-
-// NITI_MNNPstoShiftInt32 (CommonOptFunction.cpp:1595-1627), exact for any shift the
-// reference can produce; the fast path covers 0 <= s <= 30.
-__device__ __forceinline__ int32_t psto_fast(int32_t a, int s) {
-    const uint32_t ua = a < 0 ? 0u - (uint32_t)a : (uint32_t)a;
-    const uint32_t q = ua >> s;
-    const uint32_t prob = ua & ((1u << s) - 1u);
-    const int h = s >> 1;
-    const uint32_t qp = prob >> h;
-    uint32_t pr = prob & ((1u << h) - 1u);
-    if (s & 1) pr <<= 1;
-    const int32_t r = (int32_t)q + (qp > pr ? 1 : 0);
-    return clip127(a < 0 ? -r : r);
-}
-
-__device__ int32_t psto_generic(int32_t a, int s) {
-    const int32_t p = pow2_x86(s);
-    const int32_t q = a / p;
-    int32_t prob = (int32_t)((uint32_t)a - (uint32_t)q * (uint32_t)p);
-    prob = prob < 0 ? -prob : prob;
-    const int32_t hp = pow2_x86(s / 2);
-    const int32_t qp = prob / hp;
-    int32_t pr = (int32_t)((uint32_t)prob - (uint32_t)qp * (uint32_t)hp);
-    if (s % 2 == 1) pr = (int32_t)((uint32_t)pr * 2u);
-    const int32_t sg = a > 0 ? 1 : (a < 0 ? -1 : 0);
-    return clip127((int32_t)((uint32_t)q + (uint32_t)((qp > pr) * sg)));
-}
-
-__device__ __forceinline__ int32_t psto_any(int32_t a, int s) {
-    return (s >= 0 && s <= 30) ? psto_fast(a, s) : psto_generic(a, s);
-}
 
 __global__ void absmax_kernel(const int32_t* __restrict__ a, int64_t n, uint32_t* __restrict__ amax) {
     uint32_t m = 0;
@@ -499,14 +727,14 @@ __global__ void absmax_kernel(const int32_t* __restrict__ a, int64_t n, uint32_t
     if (threadIdx.x == 0) {
         for (int i = 1; i < (int)(blockDim.x >> 6); ++i) m = m > red[i] ? m : red[i];
         m = m > red[0] ? m : red[0];
-        if (m) atomicMax(amax, m);
+        publish_max(amax, m);
     }
 }
 
 hipError_t absmax_i32(const int32_t* a, int64_t n, uint32_t* amax, hipStream_t st) {
     if (n <= 0) return hipSuccess;
     int64_t blocks = (n / 4 + 255) / 256;
-    if (blocks > 2048) blocks = 2048;
+    if (blocks > 512) blocks = 512;
     if (blocks < 1) blocks = 1;
     hipLaunchKernelGGL(absmax_kernel, dim3((unsigned)blocks), dim3(256), 0, st, a, n, amax);
     return hipGetLastError();

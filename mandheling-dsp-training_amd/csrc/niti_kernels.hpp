@@ -33,23 +33,48 @@ struct ConvGeom {
 enum GradRule { RULE_WGRAD_BW2 = 2, RULE_MATMUL_BW3 = 3 };
 
 // ---- GEMM-class accumulation (int8 MFMA v_mfma_i32_32x32x32_i8, exact int32) ----------
-// acc[M = n*oh*ow][cop] = conv(x, w);  atomically max-es |acc| into *amax (caller zeroes it).
-hipError_t conv_fwd_acc(const ConvGeom& g, const int8_t* x_nhwc16, const int8_t* w_ohwi16,
-                        int32_t* acc, uint32_t* amax, hipStream_t st);
-// acc[M = n*h*w][cip] = transposed conv of dy with w (input gradient), |acc| max into *amax.
-hipError_t conv_dgrad_acc(const ConvGeom& g, const int8_t* dy_nhwc16, const int8_t* wt_ihwo16,
-                          int32_t* acc, uint32_t* amax, hipStream_t st);
-// acc[co][kh][kw][cip] = sum over (n, oy, ox) of dy * x (weight gradient).  Zeroes acc
-// (unless zero=false: the caller did), then split-K accumulates with int32 atomics (exact
-// and order independent).
-hipError_t conv_wgrad_acc(const ConvGeom& g, const int8_t* x_chwn16, const int8_t* dy_chwn16,
-                          int32_t* acc, hipStream_t st, bool zero = true);
-// acc[m][o] = sum_k B[m][k] * A[o][k] (NITI_Matmul_Int8).  k16 = K rounded up to 16 (rows are
-// zero padded), ldb/lda in bytes (multiples of 16), ldc in elements (multiple of 16).
-// accumulate=true adds with atomics into a zeroed acc (split-K), else stores and max-es |acc|.
-hipError_t matmul_acc(int M, int O, int k16, const int8_t* B, int64_t ldb, const int8_t* A,
-                      int64_t lda, int32_t* acc, int64_t ldc, uint32_t* amax, bool split_k,
-                      hipStream_t st);
+// Every op materialises acc [rows][ld] int32 and, when amax != null, max-es |acc| into it
+// (caller zeroes it).  Shapes with too few output tiles for 256 CUs split K over workgroups
+// into int32 slabs in the caller's workspace `ws` and reduce them (exact, order independent);
+// a workspace smaller than *_workspace() just means no split.
+size_t conv_fwd_workspace(const ConvGeom& g);
+size_t conv_dgrad_workspace(const ConvGeom& g);
+size_t conv_wgrad_workspace(const ConvGeom& g);
+size_t matmul_workspace(int M, int ldc, int k16);
+// acc[M = n*oh*ow][cop] = conv(x NHWC16, w OHWI16)
+hipError_t conv_fwd_acc(const ConvGeom& g, const int8_t* x_nhwc16, const int8_t* w_ohwi16, int32_t* acc,
+                        uint32_t* amax, void* ws, size_t ws_bytes, hipStream_t st);
+// acc[M = n*h*w][cip] = transposed conv of dy (NHWC16) with w^T (IHWO16): the input gradient
+hipError_t conv_dgrad_acc(const ConvGeom& g, const int8_t* dy_nhwc16, const int8_t* wt_ihwo16, int32_t* acc,
+                          uint32_t* amax, void* ws, size_t ws_bytes, hipStream_t st);
+// acc[co][kh][kw][cip] = sum over (n, oy, ox) of dy * x (x, dy CHWN16): the weight gradient
+hipError_t conv_wgrad_acc(const ConvGeom& g, const int8_t* x_chwn16, const int8_t* dy_chwn16, int32_t* acc,
+                          uint32_t* amax, void* ws, size_t ws_bytes, hipStream_t st);
+// acc[m][o] = sum_k B[m][k] * A[o][k] (NITI_Matmul_Int8); k16 multiple of 16 (zero padded rows),
+// ldb/lda bytes, ldc elements (multiple of 16; columns o..ldc come out 0)
+hipError_t matmul_acc(int M, int O, int k16, const int8_t* B, int64_t ldb, const int8_t* A, int64_t lda,
+                      int32_t* acc, int64_t ldc, uint32_t* amax, void* ws, size_t ws_bytes, hipStream_t st);
+
+// Fused forward / input-gradient path used by the training step: phase 1 establishes the
+// tensor-wide max|acc| (either materialising acc, or -- for small K -- computing the max
+// only and recomputing the GEMM in phase 2 with the requantisation in its epilogue).
+// Between the phases a data-parallel run all-reduces *amax (MAX).
+struct ActOut {
+    int8_t* out = nullptr;             // NHWC16 [rows][ld]
+    int relu = 0;                      // fused NITI_Relu_Int8
+    const int8_t* relu_mask = nullptr; // fused NITI_ReluGrad_Int8 (out = mask > 0 ? q : 0)
+    const int8_t* exp_in = nullptr;
+    const int8_t* wscale = nullptr;
+    int8_t* exp_out = nullptr;
+};
+hipError_t conv_fwd_phase1(const ConvGeom& g, const int8_t* x, const int8_t* w, int32_t* acc, uint32_t* amax,
+                           void* ws, size_t ws_bytes, hipStream_t st);
+hipError_t conv_fwd_phase2(const ConvGeom& g, const int8_t* x, const int8_t* w, const int32_t* acc,
+                           const uint32_t* amax, const ActOut& o, size_t ws_bytes, hipStream_t st);
+hipError_t conv_dgrad_phase1(const ConvGeom& g, const int8_t* dy, const int8_t* wt, int32_t* acc, uint32_t* amax,
+                             void* ws, size_t ws_bytes, hipStream_t st);
+hipError_t conv_dgrad_phase2(const ConvGeom& g, const int8_t* dy, const int8_t* wt, const int32_t* acc,
+                             const uint32_t* amax, const ActOut& o, size_t ws_bytes, hipStream_t st);
 
 // ---- range estimate + requantisation ----------------------------------------------------
 hipError_t absmax_i32(const int32_t* a, int64_t n, uint32_t* amax, hipStream_t st);

@@ -87,6 +87,8 @@ struct Model {
     int8_t* x0 = nullptr;   // NHWC16 input
     int8_t* exp0 = nullptr; // input exponent
     int32_t* acc = nullptr; // shared fwd / dgrad accumulator
+    void* slab = nullptr;   // split-K slabs (shared, sequential on the stream)
+    size_t slab_bytes = 0;
     uint32_t* amax = nullptr;
     size_t amax_bytes = 0;
     ncclComm_t comm = nullptr;
@@ -203,6 +205,9 @@ int Model::build(int arch_, int batch_) {
         if (hipMemset(l.ws_dev, 0, 16) != hipSuccess) return NITI_NO_EXECUTION;
         acc_elems = std::max(acc_elems, out_px * g.cop);
         acc_elems = std::max(acc_elems, (size_t)n * g.h * g.w * g.cip);
+        slab_bytes = std::max(slab_bytes, conv_fwd_workspace(g));
+        slab_bytes = std::max(slab_bytes, conv_dgrad_workspace(g));
+        slab_bytes = std::max(slab_bytes, conv_wgrad_workspace(g));
         // layer input / its C alignment with the previous output
         if (i == 0) {
             l.in = x0;
@@ -212,6 +217,10 @@ int Model::build(int arch_, int batch_) {
         }
     }
     acc = (int32_t*)ws.alloc(acc_elems * 4);
+    if (slab_bytes) {
+        slab = ws.alloc(slab_bytes);
+        if (!slab) return NITI_OUT_OF_MEMORY;
+    }
     amax_bytes = (size_t)round_up(3 * nl, 4) * 4;
     amax = (uint32_t*)ws.alloc(amax_bytes);
     if (!x0 || !exp0 || !acc || !amax) return NITI_OUT_OF_MEMORY;
@@ -240,20 +249,16 @@ int Model::step(const int8_t* x_nchw, int exp_in, const int32_t* labels, hipStre
         Layer& l = L[i];
         const ConvGeom& g = l.g;
         probe(i, 0, true, st);
-        MTRY(conv_fwd_acc(g, l.in, l.w, acc, amax + 3 * i, st));
-        probe(i, 0, false, st);
+        MTRY(conv_fwd_phase1(g, l.in, l.w, acc, amax + 3 * i, slab, slab_bytes, st));
         if (dp && exact) CTRY(ncclAllReduce(amax + 3 * i, amax + 3 * i, 1, ncclUint32, ncclMax, comm, st));
-        ActRequant r;
-        r.acc = acc;
-        r.rows = (int64_t)n * g.oh * g.ow;
-        r.ldc = g.cop;
-        r.amax = amax + 3 * i;
-        r.exp_in = i == 0 ? exp0 : L[i - 1].exp;
-        r.wscale = l.ws_dev;
-        r.exp_out = l.exp;
-        r.relu = l.relu;
-        r.out_nhwc16 = l.r;
-        MTRY(requant_act(r, st));
+        ActOut o;
+        o.out = l.r;
+        o.relu = l.relu;
+        o.exp_in = i == 0 ? exp0 : L[i - 1].exp;
+        o.wscale = l.ws_dev;
+        o.exp_out = l.exp;
+        MTRY(conv_fwd_phase2(g, l.in, l.w, acc, amax + 3 * i, o, slab_bytes, st));
+        probe(i, 0, false, st);
         if (l.pool) MTRY(maxpool_nhwc16(l.r, n, g.oh, g.ow, g.cop, 2, 2, 0, l.p, l.ph, l.pw, st));
         if (l.flatten) {
             const int fc = g.c_out * l.ph * l.pw, ld = round_up(fc, 16);
@@ -272,44 +277,43 @@ int Model::step(const int8_t* x_nchw, int exp_in, const int32_t* labels, hipStre
         const int64_t we = l.w_elems();
         MTRY(nhwc16_to_chwn16(l.in, n, g.h * g.w, g.cip, g.np, l.xT, st));
         MTRY(nhwc16_to_chwn16(l.dy, n, g.oh * g.ow, g.cop, g.np, l.dyT, st));
-        MTRY(hipMemsetAsync(l.dwacc, 0, (size_t)we * sizeof(int32_t), st));
         probe(i, 2, true, st);
-        MTRY(conv_wgrad_acc(g, l.xT, l.dyT, l.dwacc, st, /*zero=*/false));
+        MTRY(conv_wgrad_acc(g, l.xT, l.dyT, l.dwacc, dp ? nullptr : amax + 3 * i + 2, slab, slab_bytes, st));
         probe(i, 2, false, st);
-        if (dp) CTRY(ncclAllReduce(l.dwacc, l.dwacc, (size_t)we, ncclInt32, ncclSum, comm, st));
+        if (dp) {
+            CTRY(ncclAllReduce(l.dwacc, l.dwacc, (size_t)we, ncclInt32, ncclSum, comm, st));
+            MTRY(absmax_i32(l.dwacc, we, amax + 3 * i + 2, st));
+        }
         if (i > 0) {
             Layer& pv = L[i - 1];
             MTRY(ohwi16_to_ihwo16(l.w, g.c_out, g.c_in, g.kh * g.kw, g.cip, g.cop, l.wT, st));
             probe(i, 1, true, st);
-            MTRY(conv_dgrad_acc(g, l.dy, l.wT, acc, amax + 3 * i + 1, st));
-            probe(i, 1, false, st);
+            MTRY(conv_dgrad_phase1(g, l.dy, l.wT, acc, amax + 3 * i + 1, slab, slab_bytes, st));
             if (dp && exact) CTRY(ncclAllReduce(amax + 3 * i + 1, amax + 3 * i + 1, 1, ncclUint32, ncclMax, comm, st));
-            ActRequant r;
-            r.acc = acc;
-            r.rows = (int64_t)n * g.h * g.w;
-            r.ldc = g.cip;
-            r.amax = amax + 3 * i + 1;
             const ConvGeom& pg = pv.g;
+            ActOut o;
             if (pv.flatten) {
-                r.out_nhwc16 = pv.dflat;
-                MTRY(requant_act(r, st));
+                o.out = pv.dflat;
+                MTRY(conv_dgrad_phase2(g, l.dy, l.wT, acc, amax + 3 * i + 1, o, slab_bytes, st));
+                probe(i, 1, false, st);
                 const int fc = pg.c_out * pv.ph * pv.pw, ld = round_up(fc, 16);
                 MTRY(launch_map((int64_t)n * pv.ph * pv.pw * pg.cop,
                                 FlattenBwd{pv.dflat, pv.ph * pv.pw, pg.c_out, pg.cop, ld, pv.dtmp}, st));
                 MTRY(maxpool_relu_grad_nhwc16(pv.r, pv.p, pv.dtmp, n, pg.oh, pg.ow, pg.cop, 2, 2, 0, pv.ph, pv.pw,
                                               pv.relu, pv.dy, st));
             } else if (pv.pool) {
-                r.out_nhwc16 = pv.dtmp;
-                MTRY(requant_act(r, st));
+                o.out = pv.dtmp;
+                MTRY(conv_dgrad_phase2(g, l.dy, l.wT, acc, amax + 3 * i + 1, o, slab_bytes, st));
+                probe(i, 1, false, st);
                 MTRY(maxpool_relu_grad_nhwc16(pv.r, pv.p, pv.dtmp, n, pg.oh, pg.ow, pg.cop, 2, 2, 0, pv.ph, pv.pw,
                                               pv.relu, pv.dy, st));
             } else {
-                r.relu_mask = pv.relu ? pv.r : nullptr;
-                r.out_nhwc16 = pv.dy;
-                MTRY(requant_act(r, st));
+                o.relu_mask = pv.relu ? pv.r : nullptr;
+                o.out = pv.dy;
+                MTRY(conv_dgrad_phase2(g, l.dy, l.wT, acc, amax + 3 * i + 1, o, slab_bytes, st));
+                probe(i, 1, false, st);
             }
         }
-        MTRY(absmax_i32(l.dwacc, we, amax + 3 * i + 2, st));
         MTRY(requant_grad(l.dwacc, we, amax + 3 * i + 2, RULE_WGRAD_BW2, l.g8, l.w, st));
     }
     return NITI_NO_ERROR;

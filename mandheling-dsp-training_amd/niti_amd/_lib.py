@@ -77,10 +77,12 @@ def lib():
         "niti_destroy_execution": (None, [vp]),
         "niti_execution_workspace_bytes": (C.c_size_t, [vp]),
         "niti_geom_finalize": (ci, [C.POINTER(Geom)]),
-        "niti_conv_fwd_acc": (ci, [C.POINTER(Geom), vp, vp, vp, vp, vp]),
-        "niti_conv_dgrad_acc": (ci, [C.POINTER(Geom), vp, vp, vp, vp, vp]),
-        "niti_conv_wgrad_acc": (ci, [C.POINTER(Geom), vp, vp, vp, vp]),
-        "niti_matmul_acc": (ci, [ci, ci, ci, vp, i64, vp, i64, vp, i64, vp, ci, vp]),
+        "niti_conv_workspace_bytes": (ci, [C.POINTER(Geom), ci, C.POINTER(C.c_size_t)]),
+        "niti_matmul_workspace_bytes": (ci, [ci, ci, ci, C.POINTER(C.c_size_t)]),
+        "niti_conv_fwd_acc": (ci, [C.POINTER(Geom), vp, vp, vp, vp, vp, C.c_size_t, vp]),
+        "niti_conv_dgrad_acc": (ci, [C.POINTER(Geom), vp, vp, vp, vp, vp, C.c_size_t, vp]),
+        "niti_conv_wgrad_acc": (ci, [C.POINTER(Geom), vp, vp, vp, vp, vp, C.c_size_t, vp]),
+        "niti_matmul_acc": (ci, [ci, ci, ci, vp, i64, vp, i64, vp, i64, vp, vp, C.c_size_t, vp]),
         "niti_absmax_i32": (ci, [vp, i64, vp, vp]),
         "niti_requant_act": (ci, [vp, i64, ci, vp, vp, vp, vp, ci, vp, vp, vp]),
         "niti_requant_grad": (ci, [vp, i64, vp, ci, vp, vp, vp]),

@@ -25,8 +25,11 @@ def _ptr(t):
 
 
 def tensor(t: torch.Tensor, dims, fmt=L.FORMAT_NCHW) -> L.Tensor:
+    """niti_tensor view of `t`; the view keeps `t` alive (the C side only holds the pointer)."""
     d = list(dims) + [1] * (4 - len(dims))
-    return L.Tensor(t.data_ptr(), (C.c_int * 4)(*d), fmt)
+    v = L.Tensor(t.data_ptr(), (C.c_int * 4)(*d), fmt)
+    v._keep = t
+    return v
 
 
 def conv_common(kernel, stride=1, pad=0, dilate=1, pads=None, pad_mode=L.PAD_CAFFE, input_count=0,
@@ -146,35 +149,46 @@ def nhwc16_to_chwn16(x16: torch.Tensor, stream=None):
     return out
 
 
+def conv_workspace(g: L.Geom, op: int, device="cuda"):
+    n = C.c_size_t()
+    check(L.lib().niti_conv_workspace_bytes(C.byref(g), op, C.byref(n)), "workspace")
+    return torch.empty(max(int(n.value), 16), dtype=torch.uint8, device=device), int(n.value)
+
+
 def conv_fwd_acc(g: L.Geom, x16, w16, amax, stream=None):
     acc = torch.empty((g.n * g.oh * g.ow, g.cop), dtype=torch.int32, device=x16.device)
-    check(L.lib().niti_conv_fwd_acc(C.byref(g), _ptr(x16), _ptr(w16), _ptr(acc), _ptr(amax), _stream(stream)),
-          "conv_fwd_acc")
+    ws, nb = conv_workspace(g, 0, x16.device)
+    check(L.lib().niti_conv_fwd_acc(C.byref(g), _ptr(x16), _ptr(w16), _ptr(acc), _ptr(amax), _ptr(ws), nb,
+                                    _stream(stream)), "conv_fwd_acc")
     return acc
 
 
 def conv_dgrad_acc(g: L.Geom, dy16, wt16, amax, stream=None):
     acc = torch.empty((g.n * g.h * g.w, g.cip), dtype=torch.int32, device=dy16.device)
-    check(L.lib().niti_conv_dgrad_acc(C.byref(g), _ptr(dy16), _ptr(wt16), _ptr(acc), _ptr(amax), _stream(stream)),
-          "conv_dgrad_acc")
+    ws, nb = conv_workspace(g, 1, dy16.device)
+    check(L.lib().niti_conv_dgrad_acc(C.byref(g), _ptr(dy16), _ptr(wt16), _ptr(acc), _ptr(amax), _ptr(ws), nb,
+                                      _stream(stream)), "conv_dgrad_acc")
     return acc
 
 
-def conv_wgrad_acc(g: L.Geom, xT, dyT, stream=None):
+def conv_wgrad_acc(g: L.Geom, xT, dyT, amax=None, stream=None):
     acc = torch.empty((g.c_out, g.kh, g.kw, g.cip), dtype=torch.int32, device=xT.device)
-    check(L.lib().niti_conv_wgrad_acc(C.byref(g), _ptr(xT), _ptr(dyT), _ptr(acc), _stream(stream)),
-          "conv_wgrad_acc")
+    ws, nb = conv_workspace(g, 2, xT.device)
+    check(L.lib().niti_conv_wgrad_acc(C.byref(g), _ptr(xT), _ptr(dyT), _ptr(acc), _ptr(amax), _ptr(ws), nb,
+                                      _stream(stream)), "conv_wgrad_acc")
     return acc
 
 
-def matmul_acc(B16, A16, ldc, amax=None, split_k=True, stream=None):
+def matmul_acc(B16, A16, ldc, amax=None, use_workspace=True, stream=None):
     m, k16 = B16.shape
     o = A16.shape[0]
     acc = torch.empty((m, ldc), dtype=torch.int32, device=B16.device)
-    if split_k:
-        acc.zero_()
-    check(L.lib().niti_matmul_acc(m, o, k16, _ptr(B16), k16, _ptr(A16), k16, _ptr(acc), ldc, _ptr(amax),
-                                  1 if split_k else 0, _stream(stream)), "matmul_acc")
+    n = C.c_size_t(0)
+    if use_workspace:
+        check(L.lib().niti_matmul_workspace_bytes(m, ldc, k16, C.byref(n)), "workspace")
+    ws = torch.empty(max(int(n.value), 16), dtype=torch.uint8, device=B16.device)
+    check(L.lib().niti_matmul_acc(m, o, k16, _ptr(B16), k16, _ptr(A16), k16, _ptr(acc), ldc, _ptr(amax), _ptr(ws),
+                                  int(n.value), _stream(stream)), "matmul_acc")
     return acc
 
 

@@ -52,7 +52,8 @@ def i8s(T, v):
 
 
 # --------------------------------------------------------------------------- GEMM core
-@pytest.mark.parametrize("m,o,k", [(1, 1, 1), (37, 29, 100), (128, 128, 64), (300, 200, 777), (5, 700, 4100)])
+@pytest.mark.parametrize("m,o,k", [(1, 1, 1), (37, 29, 100), (128, 128, 64), (300, 200, 777), (5, 700, 4100),
+                                   (64, 144, 65536), (256, 2304, 16384)])
 @pytest.mark.parametrize("split", [False, True])
 def test_matmul_acc_exact(T, ops, m, o, k, split):
     rng = np.random.default_rng(m * 7 + o + k)
@@ -65,12 +66,12 @@ def test_matmul_acc_exact(T, ops, m, o, k, split):
     Ap[:, :k] = A
     ldc = (o + 15) // 16 * 16
     amax = zeros_u32(T)
-    acc = ops.matmul_acc(dev(T, Bp), dev(T, Ap), ldc, amax=None if split else amax, split_k=split)
+    acc = ops.matmul_acc(dev(T, Bp), dev(T, Ap), ldc, amax=amax, use_workspace=split)
     want = B.astype(np.int64) @ A.astype(np.int64).T
-    got = acc.cpu().numpy()[:, :o]
-    assert np.array_equal(got, want)
-    if not split:
-        assert int(amax[0].item()) == int(np.abs(want).max())
+    got = acc.cpu().numpy()
+    assert np.array_equal(got[:, :o], want)
+    assert not got[:, o:].any()
+    assert int(amax[0].item()) == int(np.abs(want).max())
 
 
 # --------------------------------------------------------------------------- native conv ops
