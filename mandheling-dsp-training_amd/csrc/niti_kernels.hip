@@ -37,89 +37,149 @@ __device__ __forceinline__ v4i zero4() {
 }
 
 // =====================================================================================
-// Operand loaders: each returns one 16-byte K-chunk of one GEMM row (zero if outside).
+// Operand loaders.  Each GEMM row's K dimension is a sequence of 16-byte chunks; a loader
+// turns (row, chunk) into a byte offset inside one tensor, or OOB (>= 2^31) for a zero
+// chunk (padding, out-of-image taps, rows past M, chunks past the K split).  Loads are
+// raw buffer loads, so an OOB offset reads zeros without a branch.  Per-thread iterators
+// advance by CPS chunks per K step with compares instead of divisions.
 // =====================================================================================
+constexpr uint32_t OOB = 0x80000000u;
 
-// Plain row-major operand: row r at p + r*ld, K-chunks contiguous.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const int8_t* p, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ v4i buf_load16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_bit_cast(v4i, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0));
+}
+
+// Plain row-major operand: row r at r*ld, K-chunks contiguous.
 struct LoadRowMajor {
     const int8_t* p;
     int64_t ld;
     int rows;
     int kc_total;
-    struct Row {
-        const int8_t* base;
+    uint32_t bytes;
+    __device__ __forceinline__ const int8_t* ptr() const { return p; }
+    struct It {
+        uint32_t base;
+        int kc;
+        bool ok;
     };
-    __device__ __forceinline__ Row row(int r) const { return {r < rows ? p + (int64_t)r * ld : nullptr}; }
-    __device__ __forceinline__ v4i load(const Row& R, int kc) const {
-        if (R.base == nullptr || kc >= kc_total) return zero4();
-        return *(const v4i*)(R.base + (int64_t)kc * 16);
+    __device__ __forceinline__ It begin(int r, int kc) const {
+        return {r < rows ? (uint32_t)(r * ld) : 0u, kc, r < rows};
+    }
+    template <int S>
+    __device__ __forceinline__ void next(It& t) const { t.kc += S; }
+    __device__ __forceinline__ uint32_t off(const It& t, int kc_end) const {
+        return (t.ok && t.kc < kc_end && t.kc < kc_total) ? t.base + (uint32_t)t.kc * 16u : OOB;
     }
 };
 
-// Forward conv, A operand: row m = output pixel (n, oy, ox) of an NHWC16 input,
-// K-chunk kc = (ky, kx, cc) with cc the 16-channel group (im2col of
-// Int8FunctionsOpt.cpp:342-392, but channel-contiguous and never materialised).
+// Forward conv, A operand: row m = output pixel (n, oy, ox) of an NHWC16 input, K-chunk
+// kc = (ky, kx, cc) with cc the 16-channel group (the im2col of Int8FunctionsOpt.cpp:342-392,
+// channel-contiguous and never materialised).
 struct LoadConvFwd {
     const int8_t* x;
+    uint32_t bytes;
     int H, W, CPC, OH, OW, KW, sh, sw, pt, pl, dh, dw, M, kc_total;
-    int64_t img;  // bytes per image
-    struct Row {
-        const int8_t* base;
-        int iy0, ix0;
+    uint32_t img;  // bytes per image
+    __device__ __forceinline__ const int8_t* ptr() const { return x; }
+    struct It {
+        uint32_t base;
+        int iy0, ix0, ky, kx, cc, kc;
+        bool ok;
     };
-    __device__ __forceinline__ Row row(int m) const {
-        if (m >= M) return {nullptr, 0, 0};
-        const int ox = m % OW;
-        const int t = m / OW;
-        const int oy = t % OH;
-        const int n = t / OH;
-        return {x + (int64_t)n * img, oy * sh - pt, ox * sw - pl};
-    }
-    __device__ __forceinline__ v4i load(const Row& R, int kc) const {
-        if (R.base == nullptr || kc >= kc_total) return zero4();
+    __device__ __forceinline__ It begin(int m, int kc) const {
+        It t;
+        t.ok = m < M;
+        const int mm = t.ok ? m : 0;
+        const int ox = mm % OW, r = mm / OW, oy = r % OH, n = r / OH;
+        t.base = (uint32_t)n * img;
+        t.iy0 = oy * sh - pt;
+        t.ix0 = ox * sw - pl;
         const int tap = kc / CPC;
-        const int cc = kc - tap * CPC;
-        const int ky = tap / KW;
-        const int kx = tap - ky * KW;
-        const int iy = R.iy0 + ky * dh;
-        const int ix = R.ix0 + kx * dw;
-        if ((unsigned)iy >= (unsigned)H || (unsigned)ix >= (unsigned)W) return zero4();
-        return *(const v4i*)(R.base + ((int64_t)(iy * W + ix) * CPC + cc) * 16);
+        t.cc = kc - tap * CPC;
+        t.ky = tap / KW;
+        t.kx = tap - t.ky * KW;
+        t.kc = kc;
+        return t;
+    }
+    template <int S>
+    __device__ __forceinline__ void next(It& t) const {
+        t.kc += S;
+        t.cc += S;
+        while (t.cc >= CPC) {
+            t.cc -= CPC;
+            if (++t.kx == KW) {
+                t.kx = 0;
+                ++t.ky;
+            }
+        }
+    }
+    __device__ __forceinline__ uint32_t off(const It& t, int kc_end) const {
+        const int iy = t.iy0 + t.ky * dh, ix = t.ix0 + t.kx * dw;
+        const bool ok = t.ok && t.kc < kc_end && t.kc < kc_total && (unsigned)iy < (unsigned)H &&
+                        (unsigned)ix < (unsigned)W;
+        return ok ? t.base + ((uint32_t)(iy * W + ix) * CPC + t.cc) * 16u : OOB;
     }
 };
 
 // Input-gradient conv, A operand: row m = input pixel (n, iy, ix), K-chunk = (ky, kx, cc)
-// over the NHWC16 output gradient; oy = (iy + pt - ky*dh) / sh when divisible.  This is the
+// over the NHWC16 output gradient, oy = (iy + pt - ky*dh) / sh when divisible.  This is the
 // transposed convolution the reference builds from pad(dilate(dy)) and rot180(w^T)
 // (grad/NITI_Conv_Int8_Grad.cpp:29-122, NITI_DeConv_Int8.cpp:179-219).
 struct LoadConvDgrad {
     const int8_t* dy;
+    uint32_t bytes;
     int OH, OW, CPC, H, W, KW, sh, sw, pt, pl, dh, dw, M, kc_total;
-    int64_t img;
-    struct Row {
-        const int8_t* base;
-        int ty0, tx0;
+    uint32_t img;
+    __device__ __forceinline__ const int8_t* ptr() const { return dy; }
+    struct It {
+        uint32_t base;
+        int ty0, tx0, ky, kx, cc, kc;
+        bool ok;
     };
-    __device__ __forceinline__ Row row(int m) const {
-        if (m >= M) return {nullptr, 0, 0};
-        const int ix = m % W;
-        const int t = m / W;
-        const int iy = t % H;
-        const int n = t / H;
-        return {dy + (int64_t)n * img, iy + pt, ix + pl};
-    }
-    __device__ __forceinline__ v4i load(const Row& R, int kc) const {
-        if (R.base == nullptr || kc >= kc_total) return zero4();
+    __device__ __forceinline__ It begin(int m, int kc) const {
+        It t;
+        t.ok = m < M;
+        const int mm = t.ok ? m : 0;
+        const int ix = mm % W, r = mm / W, iy = r % H, n = r / H;
+        t.base = (uint32_t)n * img;
+        t.ty0 = iy + pt;
+        t.tx0 = ix + pl;
         const int tap = kc / CPC;
-        const int cc = kc - tap * CPC;
-        const int ky = tap / KW;
-        const int kx = tap - ky * KW;
-        const int ty = R.ty0 - ky * dh;
-        const int tx = R.tx0 - kx * dw;
-        if (ty < 0 || tx < 0) return zero4();
-        const int oy = ty / sh, ox = tx / sw;
-        if (oy * sh != ty || ox * sw != tx || oy >= OH || ox >= OW) return zero4();
-        return *(const v4i*)(R.base + ((int64_t)(oy * OW + ox) * CPC + cc) * 16);
+        t.cc = kc - tap * CPC;
+        t.ky = tap / KW;
+        t.kx = tap - t.ky * KW;
+        t.kc = kc;
+        return t;
+    }
+    template <int S>
+    __device__ __forceinline__ void next(It& t) const {
+        t.kc += S;
+        t.cc += S;
+        while (t.cc >= CPC) {
+            t.cc -= CPC;
+            if (++t.kx == KW) {
+                t.kx = 0;
+                ++t.ky;
+            }
+        }
+    }
+    __device__ __forceinline__ uint32_t off(const It& t, int kc_end) const {
+        const int ty = t.ty0 - t.ky * dh, tx = t.tx0 - t.kx * dw;
+        int oy = ty, ox = tx;
+        bool ok = t.ok && t.kc < kc_end && t.kc < kc_total && ty >= 0 && tx >= 0;
+        if (sh != 1) {
+            oy = ty / sh;
+            ok = ok && oy * sh == ty;
+        }
+        if (sw != 1) {
+            ox = tx / sw;
+            ok = ok && ox * sw == tx;
+        }
+        ok = ok && oy < OH && ox < OW;
+        return ok ? t.base + ((uint32_t)(oy * OW + ox) * CPC + t.cc) * 16u : OOB;
     }
 };
 
@@ -127,30 +187,47 @@ struct LoadConvDgrad {
 // (oy, ox, nc) over a CHWN16 input (16 consecutive images of one channel and pixel).
 struct LoadWgradX {
     const int8_t* xT;
+    uint32_t bytes;
     int H, W, NPC, OW, sh, sw, pt, pl, dh, dw, KW, CIP, rows, kc_total;
-    int64_t plane;  // bytes per channel plane (H*W*Np)
-    struct Row {
-        const int8_t* base;
-        int offy, offx;
+    uint32_t plane;  // bytes per channel plane (H*W*Np)
+    __device__ __forceinline__ const int8_t* ptr() const { return xT; }
+    struct It {
+        uint32_t base;
+        int offy, offx, oy, ox, nc, kc;
+        bool ok;
     };
-    __device__ __forceinline__ Row row(int r) const {
-        if (r >= rows) return {nullptr, 0, 0};
-        const int ci = r % CIP;
-        const int tap = r / CIP;
-        const int ky = tap / KW;
-        const int kx = tap - ky * KW;
-        return {xT + (int64_t)ci * plane, ky * dh - pt, kx * dw - pl};
-    }
-    __device__ __forceinline__ v4i load(const Row& R, int kc) const {
-        if (R.base == nullptr || kc >= kc_total) return zero4();
+    __device__ __forceinline__ It begin(int r, int kc) const {
+        It t;
+        t.ok = r < rows;
+        const int rr = t.ok ? r : 0;
+        const int ci = rr % CIP, tap = rr / CIP, ky = tap / KW, kx = tap - ky * KW;
+        t.base = (uint32_t)ci * plane;
+        t.offy = ky * dh - pt;
+        t.offx = kx * dw - pl;
         const int pix = kc / NPC;
-        const int nc = kc - pix * NPC;
-        const int oy = pix / OW;
-        const int ox = pix - oy * OW;
-        const int iy = oy * sh + R.offy;
-        const int ix = ox * sw + R.offx;
-        if ((unsigned)iy >= (unsigned)H || (unsigned)ix >= (unsigned)W) return zero4();
-        return *(const v4i*)(R.base + ((int64_t)(iy * W + ix) * NPC + nc) * 16);
+        t.nc = kc - pix * NPC;
+        t.oy = pix / OW;
+        t.ox = pix - t.oy * OW;
+        t.kc = kc;
+        return t;
+    }
+    template <int S>
+    __device__ __forceinline__ void next(It& t) const {
+        t.kc += S;
+        t.nc += S;
+        while (t.nc >= NPC) {
+            t.nc -= NPC;
+            if (++t.ox == OW) {
+                t.ox = 0;
+                ++t.oy;
+            }
+        }
+    }
+    __device__ __forceinline__ uint32_t off(const It& t, int kc_end) const {
+        const int iy = t.oy * sh + t.offy, ix = t.ox * sw + t.offx;
+        const bool ok = t.ok && t.kc < kc_end && t.kc < kc_total && (unsigned)iy < (unsigned)H &&
+                        (unsigned)ix < (unsigned)W;
+        return ok ? t.base + ((uint32_t)(iy * W + ix) * NPC + t.nc) * 16u : OOB;
     }
 };
 
@@ -216,7 +293,7 @@ __device__ __forceinline__ void publish_max(uint32_t* amax, uint32_t m) {
 
 // =====================================================================================
 // The GEMM: C[m][n] = sum_k A[m][k] * B[n][k], int8 x int8 -> exact int32.
-//   256 threads = 4 waves; BM x BN block tile; 64-byte K step (two 32-deep MFMAs);
+//   256 threads = 4 waves; BM x BN block tile; 128-byte K step (four 32-deep MFMAs);
 //   LDS double buffer with one barrier per step; 16-byte chunks XOR-swizzled so the
 //   ds_read_b128 fragment reads of 32 rows are bank-conflict free.  Workgroups are
 //   remapped so each XCD walks a contiguous range of tiles (A-row panels stay in one L2).
@@ -227,7 +304,7 @@ __device__ __forceinline__ void publish_max(uint32_t* amax, uint32_t m) {
 //                (+ fused relu / relu-grad mask, + exponent)   (second pass)
 //   EPI_SLAB     int32 partial sums of one K split -> slab[blockIdx.y] (reduced later)
 // =====================================================================================
-constexpr int BK = 64;        // K bytes per step
+constexpr int BK = 128;       // K bytes per step
 constexpr int CPS = BK / 16;  // 16-byte chunks per row per step
 
 enum EpiMode { EPI_STORE = 0, EPI_AMAX = 1, EPI_REQUANT = 2, EPI_SLAB = 3 };
@@ -246,7 +323,9 @@ struct Epi {
     int8_t* exp_out = nullptr;
 };
 
-__device__ __forceinline__ int lds_off(int r, int c) { return r * BK + ((c ^ ((r >> 2) & 3)) << 4); }
+// 128-byte rows, 16-byte chunk c of row r stored at chunk c ^ ((r >> 1) & 7): the 16-lane
+// groups of a 32-row ds_read_b128 fragment read then hit 16 distinct bank slots.
+__device__ __forceinline__ int lds_off(int r, int c) { return r * BK + ((c ^ ((r >> 1) & 7)) << 4); }
 
 // bijective XCD remap: blocks b, b+8, b+16, ... (one XCD under round-robin dispatch) get
 // consecutive tile ids.  Speed only; any placement is correct.
@@ -282,37 +361,45 @@ __global__ void __launch_bounds__(256) gemm_i8_kernel(LA la, LB lb, int M, int N
     const int kc_end = min(kc_total, kc_begin + kc_per_split);
     const int nsteps = kc_end > kc_begin ? (kc_end - kc_begin + CPS - 1) / CPS : 0;
 
-    typename LA::Row ra[A_LD];
-    typename LB::Row rb[B_LD];
-    int ar[A_LD], ac[A_LD], br[B_LD], bc[B_LD];
+    static_assert(A_CH % 256 == 0 && B_CH % 256 == 0, "staging");
+    const __amdgpu_buffer_rsrc_t rA = make_rsrc(la.ptr(), la.bytes);
+    const __amdgpu_buffer_rsrc_t rB = make_rsrc(lb.ptr(), lb.bytes);
+    typename LA::It ia[A_LD];
+    typename LB::It ib[B_LD];
 #pragma unroll
     for (int i = 0; i < A_LD; ++i) {
         const int id = tid + i * 256;
-        ar[i] = id / CPS;
-        ac[i] = id % CPS;
-        ra[i] = la.row(id < A_CH ? m0 + ar[i] : 0x7fffffff);
+        ia[i] = la.begin(m0 + id / CPS, kc_begin + id % CPS);
     }
 #pragma unroll
     for (int i = 0; i < B_LD; ++i) {
         const int id = tid + i * 256;
-        br[i] = id / CPS;
-        bc[i] = id % CPS;
-        rb[i] = lb.row(id < B_CH ? n0 + br[i] : 0x7fffffff);
+        ib[i] = lb.begin(n0 + id / CPS, kc_begin + id % CPS);
     }
     v4i sa[A_LD], sb[B_LD];
-    auto gload = [&](int kc0) {
+    auto gload = [&]() {
 #pragma unroll
-        for (int i = 0; i < A_LD; ++i) sa[i] = la.load(ra[i], kc0 + ac[i] < kc_end ? kc0 + ac[i] : 0x7fffffff);
+        for (int i = 0; i < A_LD; ++i) {
+            sa[i] = buf_load16(rA, la.off(ia[i], kc_end));
+            la.template next<CPS>(ia[i]);
+        }
 #pragma unroll
-        for (int i = 0; i < B_LD; ++i) sb[i] = lb.load(rb[i], kc0 + bc[i] < kc_end ? kc0 + bc[i] : 0x7fffffff);
+        for (int i = 0; i < B_LD; ++i) {
+            sb[i] = buf_load16(rB, lb.off(ib[i], kc_end));
+            lb.template next<CPS>(ib[i]);
+        }
     };
     auto sstore = [&](int buf) {
 #pragma unroll
-        for (int i = 0; i < A_LD; ++i)
-            if (A_CH % 256 == 0 || tid + i * 256 < A_CH) *(v4i*)(sA + buf * A_BYTES + lds_off(ar[i], ac[i])) = sa[i];
+        for (int i = 0; i < A_LD; ++i) {
+            const int id = tid + i * 256;
+            *(v4i*)(sA + buf * A_BYTES + lds_off(id / CPS, id % CPS)) = sa[i];
+        }
 #pragma unroll
-        for (int i = 0; i < B_LD; ++i)
-            if (B_CH % 256 == 0 || tid + i * 256 < B_CH) *(v4i*)(sB + buf * B_BYTES + lds_off(br[i], bc[i])) = sb[i];
+        for (int i = 0; i < B_LD; ++i) {
+            const int id = tid + i * 256;
+            *(v4i*)(sB + buf * B_BYTES + lds_off(id / CPS, id % CPS)) = sb[i];
+        }
     };
 
     v16i acc[TM][TN];
@@ -324,17 +411,17 @@ __global__ void __launch_bounds__(256) gemm_i8_kernel(LA la, LB lb, int M, int N
             for (int i = 0; i < 16; ++i) acc[a][b][i] = 0;
 
     if (nsteps > 0) {
-        gload(kc_begin);
+        gload();
         sstore(0);
     }
     __syncthreads();
     for (int s = 0; s < nsteps; ++s) {
         const int buf = s & 1;
-        if (s + 1 < nsteps) gload(kc_begin + (s + 1) * CPS);
+        if (s + 1 < nsteps) gload();
         const int8_t* cA = sA + buf * A_BYTES;
         const int8_t* cB = sB + buf * B_BYTES;
 #pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
+        for (int kk = 0; kk < BK / 32; ++kk) {
             const int c = kk * 2 + (lane >> 5);
             v4i fa[TM], fb[TN];
 #pragma unroll
@@ -446,18 +533,19 @@ static GemmPlan plan_gemm(int M, int N, int kc_total, bool recompute_ok, size_t 
     p.tiles = ((M + p.bm - 1) / p.bm) * ((N + p.bn - 1) / p.bn);
     const int steps = (kc_total + CPS - 1) / CPS;
     p.kc_per_split = steps * CPS;
-    if (p.tiles >= 160 || steps < 24) {
-        // enough workgroups: one pass; small K makes recomputing cheaper than an int32 round trip
+    if (p.tiles >= 160 || kc_total < 96) {
+        // enough workgroups (or too little K to split): one pass; for small K recomputing the
+        // GEMM is cheaper than an int32 round trip through HBM
         p.strat = (recompute_ok && kc_total * 16 <= 1152) ? STRAT_RECOMPUTE : STRAT_STORE;
         return p;
     }
     int s = (320 + p.tiles - 1) / p.tiles;
-    const int max_s = steps / 8;
+    const int max_s = steps / 4;
     if (s > max_s) s = max_s;
     const size_t slab = (size_t)M * N;
     while (s > 1 && (size_t)s * slab > ws_elems) --s;
     if (s < 2) {
-        p.strat = STRAT_STORE;
+        p.strat = (recompute_ok && kc_total * 16 <= 1152) ? STRAT_RECOMPUTE : STRAT_STORE;
         return p;
     }
     const int per = ((steps + s - 1) / s) * CPS;
@@ -574,6 +662,15 @@ static hipError_t act_phase2(const LA& la, const LB& lb, int M, int N, int kc_to
 }
 
 // ------------------------------------------------------------------------------ per-op wrappers
+static LoadRowMajor rowmajor(const int8_t* p, int64_t ld, int rows, int kc_total) {
+    LoadRowMajor r;
+    r.p = p;
+    r.ld = ld;
+    r.rows = rows;
+    r.kc_total = kc_total;
+    r.bytes = (uint32_t)(ld * rows);
+    return r;
+}
 static LoadConvFwd fwd_loader(const ConvGeom& g, const int8_t* x) {
     LoadConvFwd la;
     la.x = x;
@@ -591,7 +688,8 @@ static LoadConvFwd fwd_loader(const ConvGeom& g, const int8_t* x) {
     la.dw = g.dw;
     la.M = g.n * g.oh * g.ow;
     la.kc_total = g.kh * g.kw * la.CPC;
-    la.img = (int64_t)g.h * g.w * g.cip;
+    la.img = (uint32_t)((int64_t)g.h * g.w * g.cip);
+    la.bytes = (uint32_t)((int64_t)g.n * la.img);
     return la;
 }
 static LoadConvDgrad dgrad_loader(const ConvGeom& g, const int8_t* dy) {
@@ -611,7 +709,8 @@ static LoadConvDgrad dgrad_loader(const ConvGeom& g, const int8_t* dy) {
     la.dw = g.dw;
     la.M = g.n * g.h * g.w;
     la.kc_total = g.kh * g.kw * la.CPC;
-    la.img = (int64_t)g.oh * g.ow * g.cop;
+    la.img = (uint32_t)((int64_t)g.oh * g.ow * g.cop);
+    la.bytes = (uint32_t)((int64_t)g.n * la.img);
     return la;
 }
 static LoadWgradX wgrad_loader(const ConvGeom& g, const int8_t* xT) {
@@ -631,7 +730,8 @@ static LoadWgradX wgrad_loader(const ConvGeom& g, const int8_t* xT) {
     lb.CIP = g.cip;
     lb.rows = g.kh * g.kw * g.cip;
     lb.kc_total = g.oh * g.ow * lb.NPC;
-    lb.plane = (int64_t)g.h * g.w * g.np;
+    lb.plane = (uint32_t)((int64_t)g.h * g.w * g.np);
+    lb.bytes = (uint32_t)((int64_t)g.cip * lb.plane);
     return lb;
 }
 
@@ -649,54 +749,54 @@ size_t matmul_workspace(int M, int ldc, int k16) { return plan_ws_elems(M, ldc, 
 hipError_t conv_fwd_acc(const ConvGeom& g, const int8_t* x, const int8_t* w, int32_t* acc, uint32_t* amax,
                         void* ws, size_t ws_bytes, hipStream_t st) {
     LoadConvFwd la = fwd_loader(g, x);
-    LoadRowMajor lb{w, (int64_t)g.kh * g.kw * g.cip, g.c_out, la.kc_total};
+    LoadRowMajor lb = rowmajor(w, (int64_t)g.kh * g.kw * g.cip, g.c_out, la.kc_total);
     return gemm_acc(la, lb, la.M, g.cop, la.kc_total, acc, amax, (int32_t*)ws, ws_bytes / 4, st);
 }
 
 hipError_t conv_dgrad_acc(const ConvGeom& g, const int8_t* dy, const int8_t* wt, int32_t* acc, uint32_t* amax,
                           void* ws, size_t ws_bytes, hipStream_t st) {
     LoadConvDgrad la = dgrad_loader(g, dy);
-    LoadRowMajor lb{wt, (int64_t)g.kh * g.kw * g.cop, g.c_in, la.kc_total};
+    LoadRowMajor lb = rowmajor(wt, (int64_t)g.kh * g.kw * g.cop, g.c_in, la.kc_total);
     return gemm_acc(la, lb, la.M, g.cip, la.kc_total, acc, amax, (int32_t*)ws, ws_bytes / 4, st);
 }
 
 hipError_t conv_wgrad_acc(const ConvGeom& g, const int8_t* xT, const int8_t* dyT, int32_t* acc, uint32_t* amax,
                           void* ws, size_t ws_bytes, hipStream_t st) {
     LoadWgradX lb = wgrad_loader(g, xT);
-    LoadRowMajor la{dyT, (int64_t)g.oh * g.ow * g.np, g.c_out, lb.kc_total};
+    LoadRowMajor la = rowmajor(dyT, (int64_t)g.oh * g.ow * g.np, g.c_out, lb.kc_total);
     return gemm_acc(la, lb, g.c_out, lb.rows, lb.kc_total, acc, amax, (int32_t*)ws, ws_bytes / 4, st);
 }
 
 hipError_t matmul_acc(int M, int O, int k16, const int8_t* B, int64_t ldb, const int8_t* A, int64_t lda, int32_t* acc,
                       int64_t ldc, uint32_t* amax, void* ws, size_t ws_bytes, hipStream_t st) {
     const int kc_total = k16 / 16;
-    LoadRowMajor la{B, ldb, M, kc_total};
-    LoadRowMajor lb{A, lda, O, kc_total};  // rows >= O read as zero, so columns O..ldc are 0
+    LoadRowMajor la = rowmajor(B, ldb, M, kc_total);
+    LoadRowMajor lb = rowmajor(A, lda, O, kc_total);  // rows >= O read as zero, so columns O..ldc are 0
     return gemm_acc(la, lb, M, (int)ldc, kc_total, acc, amax, (int32_t*)ws, ws_bytes / 4, st);
 }
 
 hipError_t conv_fwd_phase1(const ConvGeom& g, const int8_t* x, const int8_t* w, int32_t* acc, uint32_t* amax,
                            void* ws, size_t ws_bytes, hipStream_t st) {
     LoadConvFwd la = fwd_loader(g, x);
-    LoadRowMajor lb{w, (int64_t)g.kh * g.kw * g.cip, g.c_out, la.kc_total};
+    LoadRowMajor lb = rowmajor(w, (int64_t)g.kh * g.kw * g.cip, g.c_out, la.kc_total);
     return act_phase1(la, lb, la.M, g.cop, la.kc_total, acc, amax, (int32_t*)ws, ws_bytes / 4, st);
 }
 hipError_t conv_fwd_phase2(const ConvGeom& g, const int8_t* x, const int8_t* w, const int32_t* acc,
                            const uint32_t* amax, const ActOut& o, size_t ws_bytes, hipStream_t st) {
     LoadConvFwd la = fwd_loader(g, x);
-    LoadRowMajor lb{w, (int64_t)g.kh * g.kw * g.cip, g.c_out, la.kc_total};
+    LoadRowMajor lb = rowmajor(w, (int64_t)g.kh * g.kw * g.cip, g.c_out, la.kc_total);
     return act_phase2(la, lb, la.M, g.cop, la.kc_total, acc, amax, o, ws_bytes / 4, st);
 }
 hipError_t conv_dgrad_phase1(const ConvGeom& g, const int8_t* dy, const int8_t* wt, int32_t* acc, uint32_t* amax,
                              void* ws, size_t ws_bytes, hipStream_t st) {
     LoadConvDgrad la = dgrad_loader(g, dy);
-    LoadRowMajor lb{wt, (int64_t)g.kh * g.kw * g.cop, g.c_in, la.kc_total};
+    LoadRowMajor lb = rowmajor(wt, (int64_t)g.kh * g.kw * g.cop, g.c_in, la.kc_total);
     return act_phase1(la, lb, la.M, g.cip, la.kc_total, acc, amax, (int32_t*)ws, ws_bytes / 4, st);
 }
 hipError_t conv_dgrad_phase2(const ConvGeom& g, const int8_t* dy, const int8_t* wt, const int32_t* acc,
                              const uint32_t* amax, const ActOut& o, size_t ws_bytes, hipStream_t st) {
     LoadConvDgrad la = dgrad_loader(g, dy);
-    LoadRowMajor lb{wt, (int64_t)g.kh * g.kw * g.cop, g.c_in, la.kc_total};
+    LoadRowMajor lb = rowmajor(wt, (int64_t)g.kh * g.kw * g.cop, g.c_in, la.kc_total);
     return act_phase2(la, lb, la.M, g.cip, la.kc_total, acc, amax, o, ws_bytes / 4, st);
 }
 
