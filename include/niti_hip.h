@@ -135,8 +135,9 @@ int niti_conv_fwd_acc(const niti_geom* g, const int8_t* x_nhwc16, const int8_t* 
 /* acc[n*h*w][cip] int32 = input gradient of the conv for dy (NHWC16) and w^T (IHWO16) */
 int niti_conv_dgrad_acc(const niti_geom* g, const int8_t* dy_nhwc16, const int8_t* wt_ihwo16, int32_t* acc,
                         uint32_t* amax, void* workspace, size_t workspace_bytes, void* stream);
-/* acc[co][kh][kw][cip] int32 = weight gradient for x (CHWN16) and dy (CHWN16) */
-int niti_conv_wgrad_acc(const niti_geom* g, const int8_t* x_chwn16, const int8_t* dy_chwn16, int32_t* acc,
+/* acc[co][kh][kw][cip] int32 = weight gradient for x (NHWC16) and dy (NHWC16): a K-major GEMM
+ * over the pixels whose operand tiles are transposed in LDS (ds_read_b64_tr_b8) */
+int niti_conv_wgrad_acc(const niti_geom* g, const int8_t* x_nhwc16, const int8_t* dy_nhwc16, int32_t* acc,
                         uint32_t* amax, void* workspace, size_t workspace_bytes, void* stream);
 /* acc[m][ldc] = sum_k B[m][k] A[o][k] (columns o..ldc = 0); K zero padded to k16; ldb/lda bytes */
 int niti_matmul_acc(int m, int o, int k16, const int8_t* B, int64_t ldb, const int8_t* A, int64_t lda,

@@ -28,45 +28,43 @@ namespace niti {
 // ------------------------------------------------------------------ boundary converters
 namespace {
 
-// C4(x^T): dims [Ci(batch), N(channel), H, W] -> x CHWN16 [Cip][H][W][Np]
-struct C4TransposedToChwn16 {
+// C4(x^T): dims [Ci(batch), N(channel), H, W] -> x NHWC16 [N][HW][Cip]
+struct C4TransposedToNhwc16 {
     const int8_t* x;
-    int n, ci, hw, np;
+    int n, ci, hw, cip;
     int8_t* out;
-    __device__ void operator()(int64_t i) const {  // i over [cip][hw][np]
-        const int b = (int)(i % np);
-        const int64_t r = i / np;
+    __device__ void operator()(int64_t i) const {  // i over [n][hw][cip]
+        const int c = (int)(i % cip);
+        const int64_t r = i / cip;
         const int64_t p = r % hw;
-        const int c = (int)(r / hw);
-        out[i] = (c < ci && b < n) ? x[(((int64_t)(b >> 2) * ci + c) * hw + p) * 4 + (b & 3)] : (int8_t)0;
+        const int b = (int)(r / hw);
+        out[i] = c < ci ? x[(((int64_t)(b >> 2) * ci + c) * hw + p) * 4 + (b & 3)] : (int8_t)0;
     }
 };
 
-// dy^T NCHW [Co][N][OHW] -> dy CHWN16 [Cop][OHW][Np]
-struct NchwTransposedToChwn16 {
+// dy^T NCHW [Co][N][OHW] -> dy NHWC16 [N][OHW][Cop]
+struct NchwTransposedToNhwc16 {
     const int8_t* d;
-    int n, co, hw, np;
+    int n, co, hw, cop;
     int8_t* out;
     __device__ void operator()(int64_t i) const {
-        const int b = (int)(i % np);
-        const int64_t r = i / np;
+        const int c = (int)(i % cop);
+        const int64_t r = i / cop;
         const int64_t p = r % hw;
-        const int c = (int)(r / hw);
-        out[i] = (c < co && b < n) ? d[((int64_t)c * n + b) * hw + p] : (int8_t)0;
+        const int b = (int)(r / hw);
+        out[i] = c < co ? d[((int64_t)c * n + b) * hw + p] : (int8_t)0;
     }
 };
 
-// NHWC [N][HW][C] -> CHWN16 [Cp][HW][Np]
-struct NhwcToChwn16 {
+// NHWC [N][HW][C] -> NHWC16 [N][HW][Cp]
+struct NhwcToNhwc16 {
     const int8_t* x;
-    int n, c, hw, np;
+    int c, cp;
     int8_t* out;
     __device__ void operator()(int64_t i) const {
-        const int b = (int)(i % np);
-        const int64_t r = i / np;
-        const int64_t p = r % hw;
-        const int ch = (int)(r / hw);
-        out[i] = (ch < c && b < n) ? x[((int64_t)b * hw + p) * c + ch] : (int8_t)0;
+        const int ch = (int)(i % cp);
+        const int64_t r = i / cp;
+        out[i] = ch < c ? x[r * c + ch] : (int8_t)0;
     }
 };
 
@@ -312,7 +310,7 @@ class DeconvInt8Execution : public Execution {
 
 // ------------------------------------------------------------------ NITI_GradientConv_Int8 (715)
 // A conv of C4(x^T) [Ci, N, H, W] with dy^T [Co, N, OH', OW'] as its kernel; computed as the
-// native weight-gradient GEMM (K = OH'*OW'*N) followed by PSTO(bw-2).
+// native weight-gradient GEMM (K = N*OH'*OW' pixels) followed by PSTO(bw-2).
 class GradientConvInt8Execution : public Execution {
    public:
     explicit GradientConvInt8Execution(const niti_conv2d_common& c) : common_(c) {}
@@ -348,8 +346,8 @@ class GradientConvInt8Execution : public Execution {
         if (!g.finalize() || g.oh != dyt.dims[2] || g.ow != dyt.dims[3]) return NITI_COMPUTE_SIZE_ERROR;
         g_ = g;
         ws_.release();
-        xT_ = (int8_t*)ws_.alloc((size_t)g_.cip * g_.h * g_.w * g_.np);
-        dyT_ = (int8_t*)ws_.alloc((size_t)g_.cop * g_.oh * g_.ow * g_.np);
+        xT_ = (int8_t*)ws_.alloc((size_t)g_.n * g_.h * g_.w * g_.cip);
+        dyT_ = (int8_t*)ws_.alloc((size_t)g_.n * g_.oh * g_.ow * g_.cop);
         acc_ = (int32_t*)ws_.alloc((size_t)g_.c_out * g_.kh * g_.kw * g_.cip * 4);
         g8_ = (int8_t*)ws_.alloc((size_t)g_.c_out * g_.kh * g_.kw * g_.cip);
         amax_ = (uint32_t*)ws_.alloc(16);
@@ -361,10 +359,10 @@ class GradientConvInt8Execution : public Execution {
     int onExecute(const niti_tensor* in, int nin, const niti_tensor* out, int nout, hipStream_t st) override {
         if (!acc_) return NITI_NO_EXECUTION;
         const int hw = g_.h * g_.w, ohw = g_.oh * g_.ow, kk = g_.kh * g_.kw;
-        NITI_TRY(launch_map((int64_t)g_.cip * hw * g_.np,
-                            C4TransposedToChwn16{(const int8_t*)in[0].data, g_.n, g_.c_in, hw, g_.np, xT_}, st));
-        NITI_TRY(launch_map((int64_t)g_.cop * ohw * g_.np,
-                            NchwTransposedToChwn16{(const int8_t*)in[1].data, g_.n, g_.c_out, ohw, g_.np, dyT_}, st));
+        NITI_TRY(launch_map((int64_t)g_.n * hw * g_.cip,
+                            C4TransposedToNhwc16{(const int8_t*)in[0].data, g_.n, g_.c_in, hw, g_.cip, xT_}, st));
+        NITI_TRY(launch_map((int64_t)g_.n * ohw * g_.cop,
+                            NchwTransposedToNhwc16{(const int8_t*)in[1].data, g_.n, g_.c_out, ohw, g_.cop, dyT_}, st));
         const int64_t nacc = (int64_t)g_.c_out * kk * g_.cip;
         NITI_TRY(hipMemsetAsync(amax_, 0, 4, st));
         NITI_TRY(conv_wgrad_acc(g_, xT_, dyT_, acc_, amax_, slab_, slab_bytes_, st));
@@ -450,8 +448,8 @@ class DspMatmulGradientExecution : public Execution {
         if (o.dims[0] != kh || o.dims[1] != kw || o.dims[2] != g_.c_in || o.dims[3] != g_.c_out)
             return NITI_COMPUTE_SIZE_ERROR;
         ws_.release();
-        xT_ = (int8_t*)ws_.alloc((size_t)g_.cip * g_.h * g_.w * g_.np);
-        dyT_ = (int8_t*)ws_.alloc((size_t)g_.cop * g_.oh * g_.ow * g_.np);
+        xT_ = (int8_t*)ws_.alloc((size_t)g_.n * g_.h * g_.w * g_.cip);
+        dyT_ = (int8_t*)ws_.alloc((size_t)g_.n * g_.oh * g_.ow * g_.cop);
         acc_ = (int32_t*)ws_.alloc((size_t)g_.c_out * kh * kw * g_.cip * 4);
         g8_ = (int8_t*)ws_.alloc((size_t)g_.c_out * kh * kw * g_.cip);
         amax_ = (uint32_t*)ws_.alloc(16);
@@ -463,8 +461,8 @@ class DspMatmulGradientExecution : public Execution {
     int onExecute(const niti_tensor* in, int nin, const niti_tensor* out, int nout, hipStream_t st) override {
         if (!acc_) return NITI_NO_EXECUTION;
         const int hw = g_.h * g_.w, ohw = g_.oh * g_.ow, kk = g_.kh * g_.kw;
-        NITI_TRY(launch_map((int64_t)g_.cip * hw * g_.np, NhwcToChwn16{(const int8_t*)in[0].data, g_.n, g_.c_in, hw, g_.np, xT_}, st));
-        NITI_TRY(launch_map((int64_t)g_.cop * ohw * g_.np, NhwcToChwn16{(const int8_t*)in[1].data, g_.n, g_.c_out, ohw, g_.np, dyT_}, st));
+        NITI_TRY(launch_map((int64_t)g_.n * hw * g_.cip, NhwcToNhwc16{(const int8_t*)in[0].data, g_.c_in, g_.cip, xT_}, st));
+        NITI_TRY(launch_map((int64_t)g_.n * ohw * g_.cop, NhwcToNhwc16{(const int8_t*)in[1].data, g_.c_out, g_.cop, dyT_}, st));
         const int64_t nacc = (int64_t)g_.c_out * kk * g_.cip;
         NITI_TRY(hipMemsetAsync(amax_, 0, 4, st));
         NITI_TRY(conv_wgrad_acc(g_, xT_, dyT_, acc_, amax_, slab_, slab_bytes_, st));

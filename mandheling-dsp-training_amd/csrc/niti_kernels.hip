@@ -183,54 +183,6 @@ struct LoadConvDgrad {
     }
 };
 
-// Weight-gradient conv, B operand: row r = (ky, kx, ci) of the OHWI16 gradient, K-chunk =
-// (oy, ox, nc) over a CHWN16 input (16 consecutive images of one channel and pixel).
-struct LoadWgradX {
-    const int8_t* xT;
-    uint32_t bytes;
-    int H, W, NPC, OW, sh, sw, pt, pl, dh, dw, KW, CIP, rows, kc_total;
-    uint32_t plane;  // bytes per channel plane (H*W*Np)
-    __device__ __forceinline__ const int8_t* ptr() const { return xT; }
-    struct It {
-        uint32_t base;
-        int offy, offx, oy, ox, nc, kc;
-        bool ok;
-    };
-    __device__ __forceinline__ It begin(int r, int kc) const {
-        It t;
-        t.ok = r < rows;
-        const int rr = t.ok ? r : 0;
-        const int ci = rr % CIP, tap = rr / CIP, ky = tap / KW, kx = tap - ky * KW;
-        t.base = (uint32_t)ci * plane;
-        t.offy = ky * dh - pt;
-        t.offx = kx * dw - pl;
-        const int pix = kc / NPC;
-        t.nc = kc - pix * NPC;
-        t.oy = pix / OW;
-        t.ox = pix - t.oy * OW;
-        t.kc = kc;
-        return t;
-    }
-    template <int S>
-    __device__ __forceinline__ void next(It& t) const {
-        t.kc += S;
-        t.nc += S;
-        while (t.nc >= NPC) {
-            t.nc -= NPC;
-            if (++t.ox == OW) {
-                t.ox = 0;
-                ++t.oy;
-            }
-        }
-    }
-    __device__ __forceinline__ uint32_t off(const It& t, int kc_end) const {
-        const int iy = t.oy * sh + t.offy, ix = t.ox * sw + t.offx;
-        const bool ok = t.ok && t.kc < kc_end && t.kc < kc_total && (unsigned)iy < (unsigned)H &&
-                        (unsigned)ix < (unsigned)W;
-        return ok ? t.base + ((uint32_t)(iy * W + ix) * NPC + t.nc) * 16u : OOB;
-    }
-};
-
 // =====================================================================================
 // Range estimate and PSTO helpers (used by the GEMM epilogue and the requant kernels)
 // =====================================================================================
@@ -332,6 +284,69 @@ __device__ __forceinline__ int lds_off(int r, int c) { return r * BK + ((c ^ ((r
 __device__ __forceinline__ int xcd_remap(int b, int nwg) {
     const int xcd = b & 7, q = nwg >> 3, r = nwg & 7;
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+}
+
+// Shared epilogue: D[row][col] of the 32x32 MFMA tiles, row = (i&3) + 8*(i>>2) + 4*(lane>>5),
+// col = lane&31.  `smem` is reused for the block max (every LDS read finished at the last barrier).
+template <int BM, int BN, int WM, int WN, int MODE>
+__device__ __forceinline__ void gemm_epilogue(v16i (&acc)[BM / WM / 32][BN / WN / 32], int m0, int n0, int M, int N,
+                                              const Epi& epi, int8_t* smem) {
+    constexpr int TM = BM / WM / 32;
+    constexpr int TN = BN / WN / 32;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wid = tid >> 6;
+    const int wm = wid / WN, wn = wid % WN;
+    int rq_shift = 2;
+    bool rq_raw = false;
+    if (MODE == EPI_REQUANT) {
+        const int shift = bitwidth_of(*epi.amax) - 7;  // NITI_Conv_Int8.cpp:262-307
+        rq_shift = shift > 1 ? shift : 2;
+        rq_raw = shift <= 0;
+        if (blockIdx.x == 0 && blockIdx.y == 0 && tid == 0 && epi.exp_out != nullptr) {
+            const int inc = shift > 1 ? shift : (shift == 1 ? 2 : 0);
+            const int ein = epi.exp_in ? (int)*epi.exp_in : 0;
+            const int ws = epi.wscale ? (int)*epi.wscale : 0;
+            *epi.exp_out = (int8_t)(ein + ws + inc);
+        }
+    }
+    int32_t* Cs = MODE == EPI_SLAB ? epi.C + (int64_t)blockIdx.y * epi.slab_stride : epi.C;
+    uint32_t lmax = 0;
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int b = 0; b < TN; ++b) {
+            const int col = n0 + wn * (BN / WN) + b * 32 + (lane & 31);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int row = m0 + wm * (BM / WM) + a * 32 + (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
+                const int v = acc[a][b][i];
+                if (row < M && col < N) {
+                    if (MODE == EPI_STORE || MODE == EPI_SLAB) Cs[(int64_t)row * epi.ldc + col] = v;
+                    if (MODE == EPI_STORE || MODE == EPI_AMAX) {
+                        const uint32_t u = uabs32(v);
+                        lmax = lmax > u ? lmax : u;
+                    }
+                    if (MODE == EPI_REQUANT) {
+                        int32_t q = rq_raw ? (int32_t)(int8_t)v : psto_any(v, rq_shift);
+                        if (epi.relu && q < 0) q = 0;
+                        if (epi.relu_mask != nullptr && epi.relu_mask[(int64_t)row * epi.ldo + col] <= 0) q = 0;
+                        epi.out[(int64_t)row * epi.ldo + col] = (int8_t)q;
+                    }
+                }
+            }
+        }
+    if (MODE == EPI_STORE || MODE == EPI_AMAX) {
+        lmax = wave_max(lmax);
+        uint32_t* red = (uint32_t*)smem;  // all LDS reads finished at the last barrier
+        if (lane == 0) red[wid] = lmax;
+        __syncthreads();
+        if (tid == 0) {
+            uint32_t m = red[0];
+            for (int i = 1; i < 4; ++i) m = m > red[i] ? m : red[i];
+            if (epi.amax != nullptr) publish_max(epi.amax, m);
+        }
+    }
 }
 
 template <int BM, int BN, int WM, int WN, class LA, class LB, int MODE>
@@ -438,57 +453,235 @@ __global__ void __launch_bounds__(256) gemm_i8_kernel(LA la, LB lb, int M, int N
         __syncthreads();
     }
 
-    // epilogue: D[row][col], row = (i&3) + 8*(i>>2) + 4*(lane>>5), col = lane&31
-    int rq_shift = 2;
-    bool rq_raw = false;
-    if (MODE == EPI_REQUANT) {
-        const int shift = bitwidth_of(*epi.amax) - 7;  // NITI_Conv_Int8.cpp:262-307
-        rq_shift = shift > 1 ? shift : 2;
-        rq_raw = shift <= 0;
-        if (blockIdx.x == 0 && blockIdx.y == 0 && tid == 0 && epi.exp_out != nullptr) {
-            const int inc = shift > 1 ? shift : (shift == 1 ? 2 : 0);
-            const int ein = epi.exp_in ? (int)*epi.exp_in : 0;
-            const int ws = epi.wscale ? (int)*epi.wscale : 0;
-            *epi.exp_out = (int8_t)(ein + ws + inc);
-        }
+    gemm_epilogue<BM, BN, WM, WN, MODE>(acc, m0, n0, M, N, epi, smem);
+}
+
+// =====================================================================================
+// K-major GEMM for the weight gradient: C[m][n] = sum_k A[k][m] * B[k][n].
+// The reduction runs over pixels (n, oy, ox), which are the OUTER index of the NHWC16
+// activations.  Both operand tiles are staged into LDS as they lie in HBM -- [k rows][16-byte
+// column chunks], i.e. NHWC rows of dy and im2col rows of x -- and the MFMA fragments are
+// read transposed with ds_read_b64_tr_b8 (gfx950): per 16-lane group, lane 2q+p names row q,
+// columns 8p..8p+7 of an 8 x 16 byte block, and lane j receives column j of the 8 rows.  Two
+// such reads give a lane the 16 consecutive k of its column that v_mfma_i32_32x32x32_i8
+// expects.  No transposed copy of any activation is ever written to HBM.
+// =====================================================================================
+constexpr int KT_BK = 64;  // k rows (pixels) per step
+
+// multiply-shift division for 0 <= n < 2^31 (Granlund-Montgomery, round-up variant)
+struct FastDiv {
+    uint32_t m = 1, s = 0, d = 1;
+};
+static FastDiv make_fastdiv(uint32_t d) {
+    FastDiv f;
+    f.d = d;
+    f.s = 0;
+    while ((1ull << f.s) < d) ++f.s;
+    f.m = (uint32_t)((((uint64_t)1 << 32) * ((1ull << f.s) - d)) / d + 1);
+    return f;
+}
+__device__ __forceinline__ uint32_t fdiv(const FastDiv& f, uint32_t n) { return (__umulhi(n, f.m) + n) >> f.s; }
+
+// 16-byte chunk c of LDS row r (BM bytes per row) lives at chunk c ^ swz(r): the 32 lanes of
+// a half-wave transposed read (8 consecutive rows x 4 eight-byte columns) then cover all 64
+// banks once.
+template <int BW>
+__device__ __forceinline__ int kt_swz(int r) {
+    return BW == 128 ? ((r >> 1) & 3) * 2 : (BW == 64 ? ((r >> 2) & 1) * 2 : 0);
+}
+template <int BW>
+__device__ __forceinline__ int kt_off16(int r, int c) { return r * BW + ((c ^ kt_swz<BW>(r)) << 4); }
+template <int BW>
+__device__ __forceinline__ int kt_off8(int r, int c8) {
+    return r * BW + (((c8 >> 1) ^ kt_swz<BW>(r)) << 4) + ((c8 & 1) << 3);
+}
+
+typedef int v2i __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ v2i ds_tr8(const int8_t* p) {
+    return __builtin_amdgcn_ds_read_tr8_b64_v2i32((__attribute__((address_space(3))) v2i*)(p));
+}
+
+// A (and plain B) operand: row-major [K rows][ld bytes], column chunk = 16 consecutive M.
+struct KtRows {
+    const int8_t* p;
+    uint32_t bytes;
+    int64_t ld;
+    int cols;  // valid columns (multiple of 16)
+    int K;
+    __device__ __forceinline__ const int8_t* ptr() const { return p; }
+    struct It {
+        uint32_t off;
+        int k;
+        bool ok;
+    };
+    __device__ __forceinline__ It begin(int k, int c16) const {
+        return {(uint32_t)(k * ld + c16 * 16), k, c16 * 16 < cols};
     }
-    int32_t* Cs = MODE == EPI_SLAB ? epi.C + (int64_t)blockIdx.y * epi.slab_stride : epi.C;
-    uint32_t lmax = 0;
+    template <int S>
+    __device__ __forceinline__ void next(It& t) const {
+        t.k += S;
+        t.off += (uint32_t)(S * ld);
+    }
+    __device__ __forceinline__ uint32_t off(const It& t, int k_end) const {
+        return (t.ok && t.k < k_end && t.k < K) ? t.off : OOB;
+    }
+};
+
+// B operand of the weight gradient: column n' = (ky, kx, ci) of the OHWI16 gradient, row k =
+// output pixel (n, oy, ox); the value is x[n][oy*sh - pt + ky*dh][ox*sw - pl + kx*dw][ci]
+// from an NHWC16 activation (zero outside the image).
+struct KtIm2col {
+    const int8_t* x;
+    uint32_t bytes;
+    int H, W, OH, OW, CIP, KW, sh, sw, pt, pl, dh, dw, ncols, K;
+    FastDiv fOW, fOH;
+    __device__ __forceinline__ const int8_t* ptr() const { return x; }
+    struct It {
+        int k, ci0, offy, offx;
+        bool ok;
+    };
+    __device__ __forceinline__ It begin(int k, int c16) const {
+        It t;
+        const int nn = c16 * 16;
+        t.ok = nn < ncols;
+        const int tap = t.ok ? nn / CIP : 0;
+        t.ci0 = nn - tap * CIP;
+        const int ky = tap / KW, kx = tap - ky * KW;
+        t.offy = ky * dh - pt;
+        t.offx = kx * dw - pl;
+        t.k = k;
+        return t;
+    }
+    template <int S>
+    __device__ __forceinline__ void next(It& t) const { t.k += S; }
+    __device__ __forceinline__ uint32_t off(const It& t, int k_end) const {
+        if (!t.ok || t.k >= k_end || t.k >= K) return OOB;
+        const uint32_t q = fdiv(fOW, (uint32_t)t.k);
+        const int ox = t.k - (int)q * OW;
+        const uint32_t n = fdiv(fOH, q);
+        const int oy = (int)q - (int)n * OH;
+        const int iy = oy * sh + t.offy, ix = ox * sw + t.offx;
+        if ((unsigned)iy >= (unsigned)H || (unsigned)ix >= (unsigned)W) return OOB;
+        return (((uint32_t)n * H + iy) * W + ix) * (uint32_t)CIP + t.ci0;
+    }
+};
+
+template <int BM, int BN, int WM, int WN, class LA, class LB, int MODE>
+__global__ void __launch_bounds__(256) gemm_kt_kernel(LA la, LB lb, int M, int N, int tiles_n, int k_total,
+                                                       int k_per_split, Epi epi) {
+    static_assert(WM * WN == 4, "4 waves");
+    constexpr int TM = BM / WM / 32;
+    constexpr int TN = BN / WN / 32;
+    constexpr int A_CPR = BM / 16, B_CPR = BN / 16;  // 16-byte chunks per k row
+    constexpr int A_CH = KT_BK * A_CPR, B_CH = KT_BK * B_CPR;
+    constexpr int A_LD = (A_CH + 255) / 256, B_LD = (B_CH + 255) / 256;
+    constexpr int A_BYTES = KT_BK * BM, B_BYTES = KT_BK * BN;
+    __shared__ __attribute__((aligned(16))) int8_t smem[2 * (A_BYTES + B_BYTES)];
+    int8_t* sA = smem;
+    int8_t* sB = smem + 2 * A_BYTES;
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wid = tid >> 6;
+    const int wm = wid / WN, wn = wid % WN;
+    const int tile = xcd_remap(blockIdx.x, gridDim.x);
+    const int tm_ = tile / tiles_n, tn_ = tile % tiles_n;
+    const int m0 = tm_ * BM, n0 = tn_ * BN;
+    const int k_begin = blockIdx.y * k_per_split;
+    const int k_end = min(k_total, k_begin + k_per_split);
+    const int nsteps = k_end > k_begin ? (k_end - k_begin + KT_BK - 1) / KT_BK : 0;
+
+    const __amdgpu_buffer_rsrc_t rA = make_rsrc(la.ptr(), la.bytes);
+    const __amdgpu_buffer_rsrc_t rB = make_rsrc(lb.ptr(), lb.bytes);
+    typename LA::It ia[A_LD];
+    typename LB::It ib[B_LD];
+#pragma unroll
+    for (int i = 0; i < A_LD; ++i) {
+        const int id = tid + i * 256;
+        ia[i] = la.begin(k_begin + id / A_CPR, m0 / 16 + id % A_CPR);
+    }
+#pragma unroll
+    for (int i = 0; i < B_LD; ++i) {
+        const int id = tid + i * 256;
+        ib[i] = lb.begin(k_begin + id / B_CPR, n0 / 16 + id % B_CPR);
+    }
+    v4i sa[A_LD], sb[B_LD];
+    auto gload = [&]() {
+#pragma unroll
+        for (int i = 0; i < A_LD; ++i) {
+            sa[i] = buf_load16(rA, la.off(ia[i], k_end));
+            la.template next<KT_BK>(ia[i]);
+        }
+#pragma unroll
+        for (int i = 0; i < B_LD; ++i) {
+            sb[i] = buf_load16(rB, lb.off(ib[i], k_end));
+            lb.template next<KT_BK>(ib[i]);
+        }
+    };
+    auto sstore = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < A_LD; ++i) {
+            const int id = tid + i * 256;
+            if (A_CH % 256 == 0 || id < A_CH) *(v4i*)(sA + buf * A_BYTES + kt_off16<BM>(id / A_CPR, id % A_CPR)) = sa[i];
+        }
+#pragma unroll
+        for (int i = 0; i < B_LD; ++i) {
+            const int id = tid + i * 256;
+            if (B_CH % 256 == 0 || id < B_CH) *(v4i*)(sB + buf * B_BYTES + kt_off16<BN>(id / B_CPR, id % B_CPR)) = sb[i];
+        }
+    };
+
+    v16i acc[TM][TN];
 #pragma unroll
     for (int a = 0; a < TM; ++a)
 #pragma unroll
-        for (int b = 0; b < TN; ++b) {
-            const int col = n0 + wn * (BN / WN) + b * 32 + (lane & 31);
+        for (int b = 0; b < TN; ++b)
 #pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const int row = m0 + wm * (BM / WM) + a * 32 + (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
-                const int v = acc[a][b][i];
-                if (row < M && col < N) {
-                    if (MODE == EPI_STORE || MODE == EPI_SLAB) Cs[(int64_t)row * epi.ldc + col] = v;
-                    if (MODE == EPI_STORE || MODE == EPI_AMAX) {
-                        const uint32_t u = uabs32(v);
-                        lmax = lmax > u ? lmax : u;
-                    }
-                    if (MODE == EPI_REQUANT) {
-                        int32_t q = rq_raw ? (int32_t)(int8_t)v : psto_any(v, rq_shift);
-                        if (epi.relu && q < 0) q = 0;
-                        if (epi.relu_mask != nullptr && epi.relu_mask[(int64_t)row * epi.ldo + col] <= 0) q = 0;
-                        epi.out[(int64_t)row * epi.ldo + col] = (int8_t)q;
-                    }
-                }
-            }
-        }
-    if (MODE == EPI_STORE || MODE == EPI_AMAX) {
-        lmax = wave_max(lmax);
-        uint32_t* red = (uint32_t*)smem;  // all LDS reads finished at the last barrier
-        if (lane == 0) red[wid] = lmax;
-        __syncthreads();
-        if (tid == 0) {
-            uint32_t m = red[0];
-            for (int i = 1; i < 4; ++i) m = m > red[i] ? m : red[i];
-            if (epi.amax != nullptr) publish_max(epi.amax, m);
-        }
+            for (int i = 0; i < 16; ++i) acc[a][b][i] = 0;
+
+    // transposed-read geometry of this lane (see the header comment)
+    const int rq = (lane & 15) >> 1;                          // row within an 8-row block
+    const int cofs = 16 * ((lane >> 4) & 1) + 8 * (lane & 1);  // column byte within a 32-column tile
+    const int rh = 16 * (lane >> 5);                          // k half
+
+    if (nsteps > 0) {
+        gload();
+        sstore(0);
     }
+    __syncthreads();
+    for (int s = 0; s < nsteps; ++s) {
+        const int buf = s & 1;
+        if (s + 1 < nsteps) gload();
+        const int8_t* cA = sA + buf * A_BYTES;
+        const int8_t* cB = sB + buf * B_BYTES;
+#pragma unroll
+        for (int kk = 0; kk < KT_BK / 32; ++kk) {
+            const int r0 = kk * 32 + rh + rq;
+            v4i fa[TM], fb[TN];
+#pragma unroll
+            for (int a = 0; a < TM; ++a) {
+                const int c8 = (wm * (BM / WM) + a * 32 + cofs) >> 3;
+                const v2i x0 = ds_tr8(cA + kt_off8<BM>(r0, c8));
+                const v2i x1 = ds_tr8(cA + kt_off8<BM>(r0 + 8, c8));
+                fa[a] = v4i{x0[0], x0[1], x1[0], x1[1]};
+            }
+#pragma unroll
+            for (int b = 0; b < TN; ++b) {
+                const int c8 = (wn * (BN / WN) + b * 32 + cofs) >> 3;
+                const v2i y0 = ds_tr8(cB + kt_off8<BN>(r0, c8));
+                const v2i y1 = ds_tr8(cB + kt_off8<BN>(r0 + 8, c8));
+                fb[b] = v4i{y0[0], y0[1], y1[0], y1[1]};
+            }
+#pragma unroll
+            for (int a = 0; a < TM; ++a)
+#pragma unroll
+                for (int b = 0; b < TN; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[a], fb[b], acc[a][b], 0, 0, 0);
+        }
+        if (s + 1 < nsteps) sstore(buf ^ 1);
+        __syncthreads();
+    }
+    gemm_epilogue<BM, BN, WM, WN, MODE>(acc, m0, n0, M, N, epi, smem);
 }
 
 // Sum of K-split slabs -> C (+ max|C|).  n = elements per slab (multiple of 4).
@@ -526,17 +719,20 @@ struct GemmPlan {
     Strategy strat = STRAT_STORE;
 };
 
-static GemmPlan plan_gemm(int M, int N, int kc_total, bool recompute_ok, size_t ws_elems) {
+// k_total: K extent in the kernel's units (16-byte chunks for gemm_i8_kernel, rows for
+// gemm_kt_kernel); k_step: units per K step; k_bytes: K in bytes (recompute threshold).
+static GemmPlan plan_gemm(int M, int N, int k_total, int k_step, int k_bytes, bool recompute_ok, size_t ws_elems) {
     GemmPlan p;
     p.bn = N <= 32 ? 32 : (N <= 64 ? 64 : 128);
     p.bm = (M <= 64 && p.bn >= 64) ? 64 : 128;
     p.tiles = ((M + p.bm - 1) / p.bm) * ((N + p.bn - 1) / p.bn);
-    const int steps = (kc_total + CPS - 1) / CPS;
-    p.kc_per_split = steps * CPS;
-    if (p.tiles >= 160 || kc_total < 96) {
+    const int steps = (k_total + k_step - 1) / k_step;
+    p.kc_per_split = steps * k_step;
+    const bool recompute = recompute_ok && k_bytes <= 1152;
+    if (p.tiles >= 160 || steps < 12) {
         // enough workgroups (or too little K to split): one pass; for small K recomputing the
         // GEMM is cheaper than an int32 round trip through HBM
-        p.strat = (recompute_ok && kc_total * 16 <= 1152) ? STRAT_RECOMPUTE : STRAT_STORE;
+        p.strat = recompute ? STRAT_RECOMPUTE : STRAT_STORE;
         return p;
     }
     int s = (320 + p.tiles - 1) / p.tiles;
@@ -545,32 +741,37 @@ static GemmPlan plan_gemm(int M, int N, int kc_total, bool recompute_ok, size_t 
     const size_t slab = (size_t)M * N;
     while (s > 1 && (size_t)s * slab > ws_elems) --s;
     if (s < 2) {
-        p.strat = (recompute_ok && kc_total * 16 <= 1152) ? STRAT_RECOMPUTE : STRAT_STORE;
+        p.strat = recompute ? STRAT_RECOMPUTE : STRAT_STORE;
         return p;
     }
-    const int per = ((steps + s - 1) / s) * CPS;
-    p.splits = (kc_total + per - 1) / per;
+    const int per = ((steps + s - 1) / s) * k_step;
+    p.splits = (k_total + per - 1) / per;
     p.kc_per_split = per;
     p.strat = STRAT_SLAB;
     return p;
 }
 
-static size_t plan_ws_elems(int M, int N, int kc_total) {
-    GemmPlan p = plan_gemm(M, N, kc_total, false, (size_t)-1);
+static size_t plan_ws_elems(int M, int N, int k_total, int k_step) {
+    GemmPlan p = plan_gemm(M, N, k_total, k_step, 1 << 30, false, (size_t)-1);
     return p.strat == STRAT_SLAB ? (size_t)p.splits * M * N : 0;
 }
 
-template <class LA, class LB, int MODE>
-static hipError_t launch_mode(const GemmPlan& p, const LA& la, const LB& lb, int M, int N, int kc_total,
+template <class LA, class LB, int MODE, bool KT>
+static hipError_t launch_mode(const GemmPlan& p, const LA& la, const LB& lb, int M, int N, int k_total,
                               const Epi& epi, hipStream_t st) {
+    const int k_step = KT ? KT_BK : CPS;
     const int splits = MODE == EPI_SLAB ? p.splits : 1;
-    const int per = MODE == EPI_SLAB ? p.kc_per_split : ((kc_total + CPS - 1) / CPS) * CPS;
-#define NITI_LAUNCH(BM_, BN_, WM_, WN_)                                                                \
-    do {                                                                                               \
-        const int tm = (M + BM_ - 1) / BM_, tn = (N + BN_ - 1) / BN_;                                  \
-        dim3 grid(tm * tn, splits);                                                                    \
-        hipLaunchKernelGGL((gemm_i8_kernel<BM_, BN_, WM_, WN_, LA, LB, MODE>), grid, dim3(256), 0, st, \
-                           la, lb, M, N, tn, kc_total, per, epi);                                      \
+    const int per = MODE == EPI_SLAB ? p.kc_per_split : ((k_total + k_step - 1) / k_step) * k_step;
+#define NITI_LAUNCH(BM_, BN_, WM_, WN_)                                                                          \
+    do {                                                                                                         \
+        const int tm = (M + BM_ - 1) / BM_, tn = (N + BN_ - 1) / BN_;                                            \
+        dim3 grid(tm * tn, splits);                                                                              \
+        if (KT)                                                                                                  \
+            hipLaunchKernelGGL((gemm_kt_kernel<BM_, BN_, WM_, WN_, LA, LB, MODE>), grid, dim3(256), 0, st, la, lb, \
+                               M, N, tn, k_total, per, epi);                                                     \
+        else                                                                                                     \
+            hipLaunchKernelGGL((gemm_i8_kernel<BM_, BN_, WM_, WN_, LA, LB, MODE>), grid, dim3(256), 0, st, la, lb, \
+                               M, N, tn, k_total, per, epi);                                                     \
     } while (0)
     if (p.bn == 32)
         NITI_LAUNCH(128, 32, 4, 1);
@@ -597,24 +798,25 @@ static hipError_t splitk_reduce(const GemmPlan& p, const int32_t* slab, int64_t 
 }
 
 // Materialise C [M][N] int32 (+ max|C| if amax): STORE, or SLAB + reduce.
-template <class LA, class LB>
+template <class LA, class LB, bool KT = false>
 static hipError_t gemm_acc(const LA& la, const LB& lb, int M, int N, int kc_total, int32_t* C, uint32_t* amax,
                            int32_t* ws, size_t ws_elems, hipStream_t st) {
     if (M <= 0 || N <= 0) return hipSuccess;
-    GemmPlan p = plan_gemm(M, N, kc_total, false, ws ? ws_elems : 0);
+    const int k_step = KT ? KT_BK : CPS;
+    GemmPlan p = plan_gemm(M, N, kc_total, k_step, 1 << 30, false, ws ? ws_elems : 0);
     Epi e;
     if (p.strat == STRAT_SLAB) {
         e.C = ws;
         e.ldc = N;
         e.slab_stride = (int64_t)M * N;
-        hipError_t r = launch_mode<LA, LB, EPI_SLAB>(p, la, lb, M, N, kc_total, e, st);
+        hipError_t r = launch_mode<LA, LB, EPI_SLAB, KT>(p, la, lb, M, N, kc_total, e, st);
         if (r != hipSuccess) return r;
         return splitk_reduce(p, ws, (int64_t)M * N, C, amax, st);
     }
     e.C = C;
     e.ldc = N;
     e.amax = amax;
-    return launch_mode<LA, LB, EPI_STORE>(p, la, lb, M, N, kc_total, e, st);
+    return launch_mode<LA, LB, EPI_STORE, KT>(p, la, lb, M, N, kc_total, e, st);
 }
 
 // Two-phase activation GEMM (forward / input gradient): phase 1 establishes max|acc| (and
@@ -622,11 +824,11 @@ static hipError_t gemm_acc(const LA& la, const LB& lb, int M, int N, int kc_tota
 template <class LA, class LB>
 static hipError_t act_phase1(const LA& la, const LB& lb, int M, int N, int kc_total, int32_t* acc, uint32_t* amax,
                              int32_t* ws, size_t ws_elems, hipStream_t st) {
-    GemmPlan p = plan_gemm(M, N, kc_total, true, ws ? ws_elems : 0);
+    GemmPlan p = plan_gemm(M, N, kc_total, CPS, kc_total * 16, true, ws ? ws_elems : 0);
     if (p.strat == STRAT_RECOMPUTE) {
         Epi e;
         e.amax = amax;
-        return launch_mode<LA, LB, EPI_AMAX>(p, la, lb, M, N, kc_total, e, st);
+        return launch_mode<LA, LB, EPI_AMAX, false>(p, la, lb, M, N, kc_total, e, st);
     }
     return gemm_acc(la, lb, M, N, kc_total, acc, amax, ws, ws_elems, st);
 }
@@ -634,7 +836,7 @@ static hipError_t act_phase1(const LA& la, const LB& lb, int M, int N, int kc_to
 template <class LA, class LB>
 static hipError_t act_phase2(const LA& la, const LB& lb, int M, int N, int kc_total, const int32_t* acc,
                              const uint32_t* amax, const ActOut& o, size_t ws_elems, hipStream_t st) {
-    GemmPlan p = plan_gemm(M, N, kc_total, true, ws_elems);
+    GemmPlan p = plan_gemm(M, N, kc_total, CPS, kc_total * 16, true, ws_elems);
     if (p.strat == STRAT_RECOMPUTE) {
         Epi e;
         e.amax = const_cast<uint32_t*>(amax);
@@ -645,7 +847,7 @@ static hipError_t act_phase2(const LA& la, const LB& lb, int M, int N, int kc_to
         e.exp_in = o.exp_in;
         e.wscale = o.wscale;
         e.exp_out = o.exp_out;
-        return launch_mode<LA, LB, EPI_REQUANT>(p, la, lb, M, N, kc_total, e, st);
+        return launch_mode<LA, LB, EPI_REQUANT, false>(p, la, lb, M, N, kc_total, e, st);
     }
     ActRequant r;
     r.acc = acc;
@@ -713,38 +915,43 @@ static LoadConvDgrad dgrad_loader(const ConvGeom& g, const int8_t* dy) {
     la.bytes = (uint32_t)((int64_t)g.n * la.img);
     return la;
 }
-static LoadWgradX wgrad_loader(const ConvGeom& g, const int8_t* xT) {
-    LoadWgradX lb;
-    lb.xT = xT;
-    lb.H = g.h;
-    lb.W = g.w;
-    lb.NPC = g.np / 16;
-    lb.OW = g.ow;
-    lb.sh = g.sh;
-    lb.sw = g.sw;
-    lb.pt = g.pt;
-    lb.pl = g.pl;
-    lb.dh = g.dh;
-    lb.dw = g.dw;
-    lb.KW = g.kw;
-    lb.CIP = g.cip;
-    lb.rows = g.kh * g.kw * g.cip;
-    lb.kc_total = g.oh * g.ow * lb.NPC;
-    lb.plane = (uint32_t)((int64_t)g.h * g.w * g.np);
-    lb.bytes = (uint32_t)((int64_t)g.cip * lb.plane);
-    return lb;
+static void wgrad_operands(const ConvGeom& g, const int8_t* x, const int8_t* dy, KtRows* la, KtIm2col* lb) {
+    const int K = g.n * g.oh * g.ow;
+    la->p = dy;
+    la->ld = g.cop;
+    la->cols = g.cop;
+    la->K = K;
+    la->bytes = (uint32_t)((int64_t)K * g.cop);
+    lb->x = x;
+    lb->H = g.h;
+    lb->W = g.w;
+    lb->OH = g.oh;
+    lb->OW = g.ow;
+    lb->CIP = g.cip;
+    lb->KW = g.kw;
+    lb->sh = g.sh;
+    lb->sw = g.sw;
+    lb->pt = g.pt;
+    lb->pl = g.pl;
+    lb->dh = g.dh;
+    lb->dw = g.dw;
+    lb->ncols = g.kh * g.kw * g.cip;
+    lb->K = K;
+    lb->fOW = make_fastdiv((uint32_t)g.ow);
+    lb->fOH = make_fastdiv((uint32_t)g.oh);
+    lb->bytes = (uint32_t)((int64_t)g.n * g.h * g.w * g.cip);
 }
 
 size_t conv_fwd_workspace(const ConvGeom& g) {
-    return plan_ws_elems(g.n * g.oh * g.ow, g.cop, g.kh * g.kw * g.cip / 16) * sizeof(int32_t);
+    return plan_ws_elems(g.n * g.oh * g.ow, g.cop, g.kh * g.kw * g.cip / 16, CPS) * sizeof(int32_t);
 }
 size_t conv_dgrad_workspace(const ConvGeom& g) {
-    return plan_ws_elems(g.n * g.h * g.w, g.cip, g.kh * g.kw * g.cop / 16) * sizeof(int32_t);
+    return plan_ws_elems(g.n * g.h * g.w, g.cip, g.kh * g.kw * g.cop / 16, CPS) * sizeof(int32_t);
 }
 size_t conv_wgrad_workspace(const ConvGeom& g) {
-    return plan_ws_elems(g.c_out, g.kh * g.kw * g.cip, g.oh * g.ow * g.np / 16) * sizeof(int32_t);
+    return plan_ws_elems(g.c_out, g.kh * g.kw * g.cip, g.n * g.oh * g.ow, KT_BK) * sizeof(int32_t);
 }
-size_t matmul_workspace(int M, int ldc, int k16) { return plan_ws_elems(M, ldc, k16 / 16) * sizeof(int32_t); }
+size_t matmul_workspace(int M, int ldc, int k16) { return plan_ws_elems(M, ldc, k16 / 16, CPS) * sizeof(int32_t); }
 
 hipError_t conv_fwd_acc(const ConvGeom& g, const int8_t* x, const int8_t* w, int32_t* acc, uint32_t* amax,
                         void* ws, size_t ws_bytes, hipStream_t st) {
@@ -760,11 +967,13 @@ hipError_t conv_dgrad_acc(const ConvGeom& g, const int8_t* dy, const int8_t* wt,
     return gemm_acc(la, lb, la.M, g.cip, la.kc_total, acc, amax, (int32_t*)ws, ws_bytes / 4, st);
 }
 
-hipError_t conv_wgrad_acc(const ConvGeom& g, const int8_t* xT, const int8_t* dyT, int32_t* acc, uint32_t* amax,
+hipError_t conv_wgrad_acc(const ConvGeom& g, const int8_t* x, const int8_t* dy, int32_t* acc, uint32_t* amax,
                           void* ws, size_t ws_bytes, hipStream_t st) {
-    LoadWgradX lb = wgrad_loader(g, xT);
-    LoadRowMajor la = rowmajor(dyT, (int64_t)g.oh * g.ow * g.np, g.c_out, lb.kc_total);
-    return gemm_acc(la, lb, g.c_out, lb.rows, lb.kc_total, acc, amax, (int32_t*)ws, ws_bytes / 4, st);
+    KtRows la;
+    KtIm2col lb;
+    wgrad_operands(g, x, dy, &la, &lb);
+    return gemm_acc<KtRows, KtIm2col, true>(la, lb, g.c_out, lb.ncols, lb.K, acc, amax, (int32_t*)ws, ws_bytes / 4,
+                                            st);
 }
 
 hipError_t matmul_acc(int M, int O, int k16, const int8_t* B, int64_t ldb, const int8_t* A, int64_t lda, int32_t* acc,

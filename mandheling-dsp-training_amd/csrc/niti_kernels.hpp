@@ -47,8 +47,9 @@ hipError_t conv_fwd_acc(const ConvGeom& g, const int8_t* x_nhwc16, const int8_t*
 // acc[M = n*h*w][cip] = transposed conv of dy (NHWC16) with w^T (IHWO16): the input gradient
 hipError_t conv_dgrad_acc(const ConvGeom& g, const int8_t* dy_nhwc16, const int8_t* wt_ihwo16, int32_t* acc,
                           uint32_t* amax, void* ws, size_t ws_bytes, hipStream_t st);
-// acc[co][kh][kw][cip] = sum over (n, oy, ox) of dy * x (x, dy CHWN16): the weight gradient
-hipError_t conv_wgrad_acc(const ConvGeom& g, const int8_t* x_chwn16, const int8_t* dy_chwn16, int32_t* acc,
+// acc[co][kh][kw][cip] = sum over (n, oy, ox) of dy * x (x, dy NHWC16): the weight gradient,
+// a K-major GEMM over pixels whose operand tiles are transposed in LDS (ds_read_b64_tr_b8)
+hipError_t conv_wgrad_acc(const ConvGeom& g, const int8_t* x_nhwc16, const int8_t* dy_nhwc16, int32_t* acc,
                           uint32_t* amax, void* ws, size_t ws_bytes, hipStream_t st);
 // acc[m][o] = sum_k B[m][k] * A[o][k] (NITI_Matmul_Int8); k16 multiple of 16 (zero padded rows),
 // ldb/lda bytes, ldc elements (multiple of 16; columns o..ldc come out 0)

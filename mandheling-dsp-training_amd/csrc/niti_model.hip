@@ -67,9 +67,7 @@ struct Layer {
     int8_t* r = nullptr;     // conv (+relu) output NHWC16 [n][oh][ow][cop]
     int8_t* p = nullptr;     // pooled NHWC16
     int8_t* flat = nullptr;  // flattened NHWC16 [n][1][1][c*ph*pw]
-    int8_t* xT = nullptr;    // input CHWN16
     int8_t* dy = nullptr;    // output gradient NHWC16 [n][oh][ow][cop]
-    int8_t* dyT = nullptr;   // CHWN16
     int8_t* dtmp = nullptr;  // gradient wrt the pooled / flattened output
     int8_t* dflat = nullptr;
     int32_t* dwacc = nullptr;  // [co][kk][cip]
@@ -193,13 +191,11 @@ int Model::build(int arch_, int batch_) {
             l.flat = (int8_t*)ws.alloc((size_t)n * round_up(fc, 16));
             l.dflat = (int8_t*)ws.alloc((size_t)n * round_up(fc, 16));
         }
-        l.xT = (int8_t*)ws.alloc((size_t)g.cip * g.h * g.w * g.np);
         l.dy = (int8_t*)ws.alloc(out_px * g.cop);
-        l.dyT = (int8_t*)ws.alloc((size_t)g.cop * g.oh * g.ow * g.np);
         l.dwacc = (int32_t*)ws.alloc(l.w_elems() * 4);
         l.g8 = (int8_t*)ws.alloc(l.w_elems());
         l.exp = (int8_t*)ws.alloc(16);
-        if (!l.w || !l.ws_dev || !l.wT || !l.r || !l.xT || !l.dy || !l.dyT || !l.dwacc || !l.g8 || !l.exp)
+        if (!l.w || !l.ws_dev || !l.wT || !l.r || !l.dy || !l.dwacc || !l.g8 || !l.exp)
             return NITI_OUT_OF_MEMORY;
         if (hipMemset(l.w, 0, l.w_elems()) != hipSuccess) return NITI_NO_EXECUTION;
         if (hipMemset(l.ws_dev, 0, 16) != hipSuccess) return NITI_NO_EXECUTION;
@@ -275,10 +271,8 @@ int Model::step(const int8_t* x_nchw, int exp_in, const int32_t* labels, hipStre
         Layer& l = L[i];
         const ConvGeom& g = l.g;
         const int64_t we = l.w_elems();
-        MTRY(nhwc16_to_chwn16(l.in, n, g.h * g.w, g.cip, g.np, l.xT, st));
-        MTRY(nhwc16_to_chwn16(l.dy, n, g.oh * g.ow, g.cop, g.np, l.dyT, st));
         probe(i, 2, true, st);
-        MTRY(conv_wgrad_acc(g, l.xT, l.dyT, l.dwacc, dp ? nullptr : amax + 3 * i + 2, slab, slab_bytes, st));
+        MTRY(conv_wgrad_acc(g, l.in, l.dy, l.dwacc, dp ? nullptr : amax + 3 * i + 2, slab, slab_bytes, st));
         probe(i, 2, false, st);
         if (dp) {
             CTRY(ncclAllReduce(l.dwacc, l.dwacc, (size_t)we, ncclInt32, ncclSum, comm, st));

@@ -133,8 +133,8 @@ def test_conv_wgrad_native(T, ops, oracle, geo):
     dy = oracle.synth_dy(rng, (n, co, g.oh, g.ow))
     dw_ref, bw_ref, acc_ref, _ = oracle.conv_wgrad(g, x, dy)
     gg = ops.geom(n, ci, h, w, co, k, stride=s, pad=p)
-    xT = ops.nchw_to_chwn16(dev(T, x))
-    dyT = ops.nchw_to_chwn16(dev(T, dy))
+    xT = ops.nchw_to_nhwc16(dev(T, x))
+    dyT = ops.nchw_to_nhwc16(dev(T, dy))
     acc = ops.conv_wgrad_acc(gg, xT, dyT)
     got = acc.cpu().numpy()  # [co][kh][kw][cip]
     assert np.array_equal(got[..., :ci].transpose(0, 3, 1, 2), acc_ref)
@@ -397,14 +397,14 @@ def test_vgg11_batch256_layers_sampled(T, ops, oracle):
             want = int((dyp[b, :, yy:yy + 3, xx:xx + 3] * wf[:, c]).sum())
             assert accd[(b * hh + yy) * hh + xx, c] == want
         # weight gradient + linearity over the batch split
-        xT = ops.nchw_to_chwn16(dev(T, x))
-        dyT = ops.nchw_to_chwn16(dev(T, dy))
+        xT = ops.nchw_to_nhwc16(dev(T, x))
+        dyT = ops.nchw_to_nhwc16(dev(T, dy))
         accw = ops.conv_wgrad_acc(gg, xT, dyT).cpu().numpy()
         for _ in range(128):
             o, c, ky, kx = (int(rng.integers(0, v)) for v in (co, ci, 3, 3))
             want = int((xp[:, c, ky:ky + hh, kx:kx + hh] * dy[:, o].astype(np.int64)).sum())
             assert accw[o, ky, kx, c] == want
         g1 = ops.geom(128, ci, hh, hh, co, k, pad=p)
-        a1 = ops.conv_wgrad_acc(g1, ops.nchw_to_chwn16(dev(T, x[:128])), ops.nchw_to_chwn16(dev(T, dy[:128])))
-        a2 = ops.conv_wgrad_acc(g1, ops.nchw_to_chwn16(dev(T, x[128:])), ops.nchw_to_chwn16(dev(T, dy[128:])))
+        a1 = ops.conv_wgrad_acc(g1, ops.nchw_to_nhwc16(dev(T, x[:128])), ops.nchw_to_nhwc16(dev(T, dy[:128])))
+        a2 = ops.conv_wgrad_acc(g1, ops.nchw_to_nhwc16(dev(T, x[128:])), ops.nchw_to_nhwc16(dev(T, dy[128:])))
         assert np.array_equal((a1 + a2).cpu().numpy(), accw)

@@ -1,0 +1,42 @@
+"""Summarise a rocprofv3 --kernel-trace CSV: per-kernel totals per step and the last step's launches."""
+import collections
+import csv
+import sys
+
+path = sys.argv[1]
+steps = int(sys.argv[2]) if len(sys.argv) > 2 else 13
+rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
+dur = lambda r: (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3  # noqa: E731
+
+
+def short(n):
+    n = n.split("(")[0].replace("void niti::", "").replace("niti::", "")
+    return n.replace("gemm_i8_kernel", "gemm").replace("Load", "")[:70]
+
+
+tot = collections.defaultdict(float)
+cnt = collections.Counter()
+for r in rows:
+    tot[short(r["Kernel_Name"])] += dur(r)
+    cnt[short(r["Kernel_Name"])] += 1
+print(f"{'us/step':>9} {'calls/step':>10}  kernel")
+for k, v in sorted(tot.items(), key=lambda x: -x[1]):
+    print(f"{v / steps:9.1f} {cnt[k] / steps:10.1f}  {k}")
+print("total busy us/step", sum(tot.values()) / steps)
+# last step: from the last loss_grad to the end
+idx = max(i for i, r in enumerate(rows) if "loss_grad" in r["Kernel_Name"])
+prev = max(i for i, r in enumerate(rows[:idx]) if "loss_grad" in r["Kernel_Name"]) if any(
+    "loss_grad" in r["Kernel_Name"] for r in rows[:idx]) else 0
+start = prev + 1
+for i in range(start, len(rows)):
+    if "NchwToNhwc16" in rows[i]["Kernel_Name"] and i > start:
+        break
+seg = rows[start:]
+print("\nlast step launches (from the forward of the step):")
+first = next(i for i, r in enumerate(rows) if i > prev and "NchwToNhwc16" in r["Kernel_Name"])
+seg = rows[first:]
+span = (int(seg[-1]["End_Timestamp"]) - int(seg[0]["Start_Timestamp"])) / 1e3
+for r in seg:
+    g = f"{int(r['Grid_Size_X']) // int(r['Workgroup_Size_X'])}x{r['Grid_Size_Y']}"
+    print(f"{dur(r):8.2f} us  grid {g:>10}  {short(r['Kernel_Name'])}")
+print("step span us", span, "busy", sum(dur(r) for r in seg))
