@@ -154,6 +154,11 @@ int niti_requant_act(const int32_t* acc, int64_t rows, int ldc, const uint32_t* 
  * g_out optional; w_update optional fused NITI_SGD step w <- clip(w - g, +-127). */
 int niti_requant_grad(const int32_t* acc, int64_t n, const uint32_t* amax, int rule, int8_t* g_out,
                       int8_t* w_update, void* stream);
+/* Fused NITI_SGD step for one layer: g = rule(acc [co][kk][cip], amax), w <- clip(w - g, +-127)
+ * on the OHWI16 weights, the updated weights also written to wt (IHWO16, may be NULL) and g to
+ * g_out (OHWI16, may be NULL). */
+int niti_sgd_update(const int32_t* acc, const uint32_t* amax, int rule, int co, int ci, int kk, int cip, int cop,
+                    int8_t* w_ohwi16, int8_t* wt_ihwo16, int8_t* g_out, void* stream);
 /* layout helpers */
 int niti_nhwc16_to_chwn16(const int8_t* in, int n, int hw, int cp, int np, int8_t* out, void* stream);
 int niti_ohwi16_to_ihwo16(const int8_t* w, int co, int ci, int kk, int cip, int cop, int8_t* wt, void* stream);

@@ -168,6 +168,12 @@ int niti_requant_grad(const int32_t* acc, int64_t n, const uint32_t* amax, int r
     return code(niti::requant_grad(acc, n, amax, rule, g_out, w, S(stream)));
 }
 
+int niti_sgd_update(const int32_t* acc, const uint32_t* amax, int rule, int co, int ci, int kk, int cip, int cop,
+                    int8_t* w, int8_t* wt, int8_t* g_out, void* stream) {
+    if (rule != 2 && rule != 3) return NITI_INVALID_VALUE;
+    return code(niti::sgd_update(acc, amax, rule, co, ci, kk, cip, cop, w, wt, g_out, S(stream)));
+}
+
 int niti_nhwc16_to_chwn16(const int8_t* in, int n, int hw, int cp, int np, int8_t* out, void* stream) {
     return code(niti::nhwc16_to_chwn16(in, n, hw, cp, np, out, S(stream)));
 }

@@ -684,14 +684,33 @@ __global__ void __launch_bounds__(256) gemm_kt_kernel(LA la, LB lb, int M, int N
     gemm_epilogue<BM, BN, WM, WN, MODE>(acc, m0, n0, M, N, epi, smem);
 }
 
-// Sum of K-split slabs -> C (+ max|C|).  n = elements per slab (multiple of 4).
-__global__ void splitk_reduce_kernel(const int32_t* __restrict__ slab, int splits, int64_t stride, int64_t n4,
+// Sum of K-split slabs -> C (+ max|C|).  A block covers 256/G v4i elements with G threads
+// per element, each summing every G-th slab with 4 loads in flight; the G partials meet in
+// registers (shfl_xor inside the wave).  Splits are many and outputs small for the weight
+// gradient (e.g. VGG-11 L1: 160 slabs of 9 K elements), so split-level parallelism matters.
+__global__ void splitk_reduce_kernel(const int32_t* __restrict__ slab, int splits, int64_t stride, int64_t n4, int G,
                                      int32_t* __restrict__ C, uint32_t* __restrict__ amax) {
+    const int g = threadIdx.x & (G - 1);
+    const int64_t e = (int64_t)blockIdx.x * (256 / G) + threadIdx.x / G;
+    v4i s = {0, 0, 0, 0};
+    if (e < n4) {
+        const v4i* base = (const v4i*)slab + e;
+        const int64_t st4 = stride / 4;
+        int z = g;
+        for (; z + 3 * G < splits; z += 4 * G) {
+            const v4i a0 = base[(int64_t)z * st4], a1 = base[(int64_t)(z + G) * st4];
+            const v4i a2 = base[(int64_t)(z + 2 * G) * st4], a3 = base[(int64_t)(z + 3 * G) * st4];
+            s += (a0 + a1) + (a2 + a3);
+        }
+        for (; z < splits; z += G) s += base[(int64_t)z * st4];
+    }
+    for (int o = G >> 1; o > 0; o >>= 1) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) s[j] += __shfl_xor(s[j], o, 64);
+    }
     uint32_t m = 0;
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
-        v4i s = ((const v4i*)slab)[i];
-        for (int z = 1; z < splits; ++z) s += ((const v4i*)(slab + z * stride))[i];
-        ((v4i*)C)[i] = s;
+    if (g == 0 && e < n4) {
+        ((v4i*)C)[e] = s;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const uint32_t u = uabs32(s[j]);
@@ -789,10 +808,11 @@ static hipError_t launch_mode(const GemmPlan& p, const LA& la, const LB& lb, int
 
 static hipError_t splitk_reduce(const GemmPlan& p, const int32_t* slab, int64_t n, int32_t* C, uint32_t* amax,
                                 hipStream_t st) {
-    int64_t blocks = (n / 4 + 255) / 256;
-    if (blocks > 1024) blocks = 1024;
-    if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, st, slab, p.splits, n, n / 4, C,
+    int G = 1;
+    while (G < 16 && G < p.splits) G <<= 1;
+    const int64_t n4 = n / 4;
+    const int64_t blocks = (n4 + (256 / G) - 1) / (256 / G);
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, st, slab, p.splits, n, n4, G, C,
                        amax);
     return hipGetLastError();
 }
@@ -1125,6 +1145,60 @@ hipError_t requant_grad(const int32_t* acc, int64_t n, const uint32_t* amax, int
     return hipGetLastError();
 }
 
+// Fused NITI_SGD step on a 64(co) x 64(ci) tile of one tap: g = gradient rule(acc), w <- clip(w - g)
+// in OHWI16, and the updated weights also written transposed (IHWO16, the input-gradient B
+// operand) through an LDS tile -- the transposed copy never needs a pass of its own.
+__global__ void sgd_update_kernel(const int32_t* __restrict__ acc, const uint32_t* __restrict__ amax, int rule, int co,
+                                  int ci, int kk, int cip, int cop, int8_t* __restrict__ w, int8_t* __restrict__ wT,
+                                  int8_t* __restrict__ g_out) {
+    __shared__ int8_t T[64][64 + 4];
+    const int co0 = blockIdx.y * 64, ci0 = blockIdx.x * 64, k = blockIdx.z;
+    const int t = threadIdx.x;
+    const int bw = bitwidth_of(*amax);
+    const int sh = bw - rule;
+    {
+        const int r = t >> 2, c = (t & 3) * 16;
+        v16c wn;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) wn[j] = 0;
+        if (co0 + r < co && ci0 + c < cip) {
+            const int64_t idx = ((int64_t)(co0 + r) * kk + k) * cip + ci0 + c;
+            const v4i* a4 = (const v4i*)(acc + idx);
+            const v16c wo = *(const v16c*)(w + idx);
+            v16c g;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const v4i v = a4[q];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) g[q * 4 + e] = (signed char)(bw == 0 ? 0 : psto_any(v[e], sh));
+            }
+#pragma unroll
+            for (int j = 0; j < 16; ++j) wn[j] = (signed char)clip127((int32_t)wo[j] - (int32_t)g[j]);
+            *(v16c*)(w + idx) = wn;
+            if (g_out != nullptr) *(v16c*)(g_out + idx) = g;
+        }
+#pragma unroll
+        for (int j = 0; j < 16; ++j) T[r][c + j] = wn[j];
+    }
+    __syncthreads();
+    if (wT != nullptr) {
+        const int r = t >> 2, c = (t & 3) * 16;  // r: ci within the tile, c: co offset
+        if (ci0 + r < ci && co0 + c < cop) {
+            v16c o;
+#pragma unroll
+            for (int j = 0; j < 16; ++j) o[j] = T[c + j][r];
+            *(v16c*)(wT + ((int64_t)(ci0 + r) * kk + k) * cop + co0 + c) = o;
+        }
+    }
+}
+
+hipError_t sgd_update(const int32_t* acc, const uint32_t* amax, int rule, int co, int ci, int kk, int cip, int cop,
+                      int8_t* w, int8_t* wT, int8_t* g_out, hipStream_t st) {
+    dim3 grid((cip + 63) / 64, (cop + 63) / 64, kk);
+    hipLaunchKernelGGL(sgd_update_kernel, grid, dim3(256), 0, st, acc, amax, rule, co, ci, kk, cip, cop, w, wT, g_out);
+    return hipGetLastError();
+}
+
 // =====================================================================================
 // The rest of the step: pool / relu-grad / loss-grad
 // =====================================================================================
@@ -1227,8 +1301,54 @@ __global__ void maxpool_grad_kernel(const int8_t* __restrict__ x, const int8_t* 
     }
 }
 
+// Non-overlapping windows (k == s, no padding, windows tile the input): one thread per window
+// and 16 channels scans its k*k pixels once in the reference's (ky, kx) order.
+__global__ void maxpool_grad_tiled_kernel(const int8_t* __restrict__ x, const int8_t* __restrict__ y,
+                                          const int8_t* __restrict__ dy, int n, int h, int w, int cp, int k,
+                                          int oh, int ow, int relu, int8_t* __restrict__ dx) {
+    const int groups = cp / 16;
+    const int64_t total = (int64_t)n * oh * ow * groups;
+    for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+        int64_t r = t;
+        const int gi = (int)(r % groups);
+        r /= groups;
+        const int ox = (int)(r % ow);
+        r /= ow;
+        const int oy = (int)(r % oh);
+        const int b = (int)(r / oh);
+        const int64_t po = (((int64_t)b * oh + oy) * ow + ox) * cp + gi * 16;
+        const v16c mv = *(const v16c*)(y + po);
+        const v16c dv = *(const v16c*)(dy + po);
+        unsigned done = 0;
+        for (int ky = 0; ky < k; ++ky)
+            for (int kx = 0; kx < k; ++kx) {
+                const int64_t pi = (((int64_t)b * h + oy * k + ky) * w + ox * k + kx) * cp + gi * 16;
+                const v16c xv = *(const v16c*)(x + pi);
+                v16c o;
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    const bool take = !((done >> j) & 1u) && xv[j] >= mv[j];
+                    if (take) done |= 1u << j;
+                    signed char d = take ? dv[j] : (signed char)0;
+                    if (relu && xv[j] <= 0) d = 0;
+                    o[j] = d;
+                }
+                *(v16c*)(dx + pi) = o;
+            }
+    }
+}
+
 hipError_t maxpool_relu_grad_nhwc16(const int8_t* x, const int8_t* y, const int8_t* dy, int n, int h, int w, int cp,
                                     int k, int s, int p, int oh, int ow, int relu, int8_t* dx, hipStream_t st) {
+    if (k == s && p == 0 && oh * k == h && ow * k == w) {
+        const int64_t total = (int64_t)n * oh * ow * (cp / 16);
+        int64_t blocks = (total + 255) / 256;
+        if (blocks > 4096) blocks = 4096;
+        if (blocks < 1) blocks = 1;
+        hipLaunchKernelGGL(maxpool_grad_tiled_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, y, dy, n, h, w, cp,
+                           k, oh, ow, relu, dx);
+        return hipGetLastError();
+    }
     const int64_t total = (int64_t)n * h * w * (cp / 16);
     int64_t blocks = (total + 255) / 256;
     if (blocks > 4096) blocks = 4096;
@@ -1261,60 +1381,67 @@ hipError_t relu_grad_nhwc16(const int8_t* x, const int8_t* dy, int64_t n, int8_t
 
 __device__ __forceinline__ int64_t ipow2_64(int64_t t) { return (int64_t)pow2_x86((int)(t & 31)); }
 
-// NITI_CPULossGrad_Int8.cpp:81-200, one thread per sample.
+// NITI_CPULossGrad_Int8.cpp:81-200, one thread per sample, the class row in registers.
+constexpr int LOSS_MAXC = 16;
 __global__ void loss_grad_kernel(const int8_t* __restrict__ logits, int batch, int classes, int ld,
                                  const int8_t* __restrict__ ascale_p, const int32_t* __restrict__ labels,
                                  int8_t* __restrict__ out) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= batch) return;
     const int as = (int)*ascale_p;
-    int64_t o[64];
+    int64_t o[LOSS_MAXC];
     const int8_t* L = logits + (int64_t)i * ld;
     if (as > -7) {
-        int64_t sv[64];
+        int64_t sv[LOSS_MAXC];
         int64_t mx = 0;
-        for (int j = 0; j < classes; ++j) {
-            int64_t t = (int64_t)L[j] * 47274;
-            t = t / (1 << 15);
-            sv[j] = as >= 0 ? t * ipow2_64(as) : t / ipow2_64(-as);
-            if (j == 0 || mx < sv[j]) mx = sv[j];
+#pragma unroll
+        for (int j = 0; j < LOSS_MAXC; ++j) {
+            if (j < classes) {
+                int64_t t = (int64_t)L[j] * 47274;
+                t = t / (1 << 15);
+                sv[j] = as >= 0 ? t * ipow2_64(as) : t / ipow2_64(-as);
+                if (j == 0 || mx < sv[j]) mx = sv[j];
+            }
         }
         mx -= 10;
-        for (int j = 0; j < classes; ++j) {
-            int64_t t = sv[j] - mx;
+#pragma unroll
+        for (int j = 0; j < LOSS_MAXC; ++j) {
+            int64_t t = j < classes ? sv[j] - mx : 0;
             t = t > 0 ? t : 0;
-            o[j] = ipow2_64(t) - 1;
+            o[j] = j < classes ? ipow2_64(t) - 1 : 0;
         }
     } else {
         const int64_t base = ipow2_64(1 - 2 * (int64_t)as);
         const int64_t sb = ipow2_64(1 - (int64_t)as);
-        for (int j = 0; j < classes; ++j) {
-            const int64_t t = L[j];
-            o[j] = base + t * sb + t * t;
+#pragma unroll
+        for (int j = 0; j < LOSS_MAXC; ++j) {
+            const int64_t t = j < classes ? L[j] : 0;
+            o[j] = j < classes ? base + t * sb + t * t : 0;
         }
     }
     int64_t sum = 0;
-    for (int j = 0; j < classes; ++j) sum += o[j];
+#pragma unroll
+    for (int j = 0; j < LOSS_MAXC; ++j) sum += o[j];
     int64_t gs = 0;
-    for (int j = 0; j < classes; ++j) {
-        o[j] = (o[j] * (1 << 11)) / sum;
+#pragma unroll
+    for (int j = 0; j < LOSS_MAXC; ++j) {
+        o[j] = j < classes ? (o[j] * (1 << 11)) / sum : 0;
         gs += o[j];
     }
     const int tgt = labels[i];
     int8_t* O = out + (int64_t)i * ld;
     for (int j = 0; j < ld; ++j) {
-        if (j >= classes) {
-            O[j] = 0;
-            continue;
-        }
-        const int32_t gf = (int32_t)(j == tgt ? o[j] - gs : o[j]);
-        O[j] = (int8_t)psto_any(gf, 4);
+        int32_t gf = 0;
+#pragma unroll
+        for (int q = 0; q < LOSS_MAXC; ++q)
+            if (q == j) gf = (int32_t)(q == tgt ? o[q] - gs : o[q]);
+        O[j] = j < classes ? (int8_t)psto_any(gf, 4) : (int8_t)0;
     }
 }
 
 hipError_t loss_grad(const int8_t* logits, int batch, int classes, int ld, const int8_t* ascale, const int32_t* labels,
                      int8_t* out, hipStream_t st) {
-    if (classes > 64 || classes > ld) return hipErrorInvalidValue;
+    if (classes > LOSS_MAXC || classes > ld) return hipErrorInvalidValue;
     hipLaunchKernelGGL(loss_grad_kernel, dim3((batch + 63) / 64), dim3(64), 0, st, logits, batch, classes, ld, ascale,
                        labels, out);
     return hipGetLastError();

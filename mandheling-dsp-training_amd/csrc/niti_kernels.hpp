@@ -103,6 +103,11 @@ hipError_t requant_act(const ActRequant& r, hipStream_t st);
 hipError_t requant_grad(const int32_t* acc, int64_t n, const uint32_t* amax, int rule, int8_t* g_out,
                         int8_t* w_update, hipStream_t st);
 
+// Fused NITI_SGD on an OHWI16 layer: g = rule(acc, amax), w <- clip(w - g, +-127); the new weights
+// are also written transposed to wT (IHWO16, may be null) and g to g_out (may be null).
+hipError_t sgd_update(const int32_t* acc, const uint32_t* amax, int rule, int co, int ci, int kk, int cip, int cop,
+                      int8_t* w, int8_t* wT, int8_t* g_out, hipStream_t st);
+
 // ---- the rest of the NITI step -----------------------------------------
 hipError_t maxpool_nhwc16(const int8_t* x, int n, int h, int w, int cp, int k, int s, int p, int8_t* y,
                           int oh, int ow, hipStream_t st);
@@ -112,7 +117,7 @@ hipError_t maxpool_relu_grad_nhwc16(const int8_t* x, const int8_t* y, const int8
                                     int8_t* dx, hipStream_t st);
 hipError_t relu_grad_nhwc16(const int8_t* x, const int8_t* dy, int64_t n, int8_t* out, hipStream_t st);
 // logits int8 [batch][ld] (first `classes` used), labels int32 [batch] (class index);
-// out int8 [batch][ld] (padded lanes zeroed).  NITI_CPULossGrad_Int8.cpp:81-200.
+// out int8 [batch][ld] (padded lanes zeroed).  classes <= 16.  NITI_CPULossGrad_Int8.cpp:81-200.
 hipError_t loss_grad(const int8_t* logits, int batch, int classes, int ld, const int8_t* ascale,
                      const int32_t* labels, int8_t* out, hipStream_t st);
 

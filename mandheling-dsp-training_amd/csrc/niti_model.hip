@@ -63,7 +63,7 @@ struct Layer {
     int8_t* w = nullptr;     // OHWI16
     int8_t* ws_dev = nullptr;  // wscale scalar
     // per step
-    int8_t* wT = nullptr;    // IHWO16
+    int8_t* wT = nullptr;    // IHWO16, kept in step with w by sgd_update
     int8_t* r = nullptr;     // conv (+relu) output NHWC16 [n][oh][ow][cop]
     int8_t* p = nullptr;     // pooled NHWC16
     int8_t* flat = nullptr;  // flattened NHWC16 [n][1][1][c*ph*pw]
@@ -280,7 +280,6 @@ int Model::step(const int8_t* x_nchw, int exp_in, const int32_t* labels, hipStre
         }
         if (i > 0) {
             Layer& pv = L[i - 1];
-            MTRY(ohwi16_to_ihwo16(l.w, g.c_out, g.c_in, g.kh * g.kw, g.cip, g.cop, l.wT, st));
             probe(i, 1, true, st);
             MTRY(conv_dgrad_phase1(g, l.dy, l.wT, acc, amax + 3 * i + 1, slab, slab_bytes, st));
             if (dp && exact) CTRY(ncclAllReduce(amax + 3 * i + 1, amax + 3 * i + 1, 1, ncclUint32, ncclMax, comm, st));
@@ -308,7 +307,8 @@ int Model::step(const int8_t* x_nchw, int exp_in, const int32_t* labels, hipStre
                 probe(i, 1, false, st);
             }
         }
-        MTRY(requant_grad(l.dwacc, we, amax + 3 * i + 2, RULE_WGRAD_BW2, l.g8, l.w, st));
+        MTRY(sgd_update(l.dwacc, amax + 3 * i + 2, RULE_WGRAD_BW2, g.c_out, g.c_in, g.kh * g.kw, g.cip, g.cop, l.w,
+                        i > 0 ? l.wT : nullptr, l.g8, st));
     }
     return NITI_NO_ERROR;
 }
@@ -355,6 +355,7 @@ int niti_model_set_weight(niti_model_t m, int layer, const int8_t* w_host, int w
     int rc = NITI_NO_ERROR;
     if (hipMemcpy(tmp, w_host, n, hipMemcpyHostToDevice) != hipSuccess ||
         niti::oihw_to_ohwi16(tmp, l.g.c_out, l.g.c_in, l.g.kh * l.g.kw, l.g.cip, l.w, nullptr) != hipSuccess ||
+        niti::oihw_to_ihwo16(tmp, l.g.c_out, l.g.c_in, l.g.kh * l.g.kw, l.g.cop, l.wT, nullptr) != hipSuccess ||
         hipMemset(l.ws_dev, (int)(int8_t)wscale, 1) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
         rc = NITI_NO_EXECUTION;
     l.wscale = (int8_t)wscale;

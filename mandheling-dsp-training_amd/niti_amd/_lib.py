@@ -86,6 +86,7 @@ def lib():
         "niti_absmax_i32": (ci, [vp, i64, vp, vp]),
         "niti_requant_act": (ci, [vp, i64, ci, vp, vp, vp, vp, ci, vp, vp, vp]),
         "niti_requant_grad": (ci, [vp, i64, vp, ci, vp, vp, vp]),
+        "niti_sgd_update": (ci, [vp, vp, ci, ci, ci, ci, ci, ci, vp, vp, vp, vp]),
         "niti_nhwc16_to_chwn16": (ci, [vp, ci, ci, ci, ci, vp, vp]),
         "niti_ohwi16_to_ihwo16": (ci, [vp, ci, ci, ci, ci, ci, vp, vp]),
         "niti_nchw_to_nhwc16": (ci, [vp, ci, ci, ci, ci, vp, vp]),

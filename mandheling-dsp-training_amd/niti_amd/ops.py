@@ -211,6 +211,17 @@ def requant_grad(acc, amax, rule=2, w_update=None, stream=None):
     return g
 
 
+def sgd_update(acc, amax, w16, ci, rule=2, stream=None):
+    """acc [co][kh][kw][cip] int32, w16 OHWI16 int8 (updated in place) -> (wT IHWO16, g OHWI16)."""
+    co, kh, kw, cip = acc.shape
+    cop = r16(co)
+    wT = torch.zeros((ci, kh, kw, cop), dtype=torch.int8, device=acc.device)
+    g = torch.empty(acc.shape, dtype=torch.int8, device=acc.device)
+    check(L.lib().niti_sgd_update(_ptr(acc), _ptr(amax), rule, co, ci, kh * kw, cip, cop, _ptr(w16), _ptr(wT), _ptr(g),
+                                  _stream(stream)), "sgd_update")
+    return wT, g
+
+
 def maxpool(x16, k=2, s=2, p=0, stream=None):
     n, h, w, cp = x16.shape
     oh = (h + 2 * p - min(k, h)) // s + 1

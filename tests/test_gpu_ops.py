@@ -147,6 +147,18 @@ def test_conv_wgrad_native(T, ops, oracle, geo):
     # fused SGD: 0 - g, clipped
     assert np.array_equal(w16.cpu().numpy()[..., :ci].transpose(0, 3, 1, 2),
                           oracle.sgd_update(np.zeros_like(dw_ref), dw_ref))
+    # tiled SGD kernel: w <- clip(w - g) in OHWI16 plus the transposed IHWO16 copy
+    rng2 = np.random.default_rng(104)
+    w0, _ = oracle.synth_w(rng2, (co, ci, k, k))
+    w16b = ops.oihw_to_ohwi16(dev(T, w0))
+    wT, g2 = ops.sgd_update(acc, amax, w16b, ci, rule=2)
+    w_new = oracle.sgd_update(w0, dw_ref)
+    assert np.array_equal(g2.cpu().numpy()[..., :ci].transpose(0, 3, 1, 2), dw_ref)
+    assert np.array_equal(w16b.cpu().numpy()[..., :ci].transpose(0, 3, 1, 2), w_new)
+    assert not w16b.cpu().numpy()[..., ci:].any()
+    wTn = wT.cpu().numpy()  # [ci][kh][kw][cop]
+    assert np.array_equal(wTn[..., :co].transpose(3, 0, 1, 2), w_new)
+    assert not wTn[..., co:].any()
 
 
 # --------------------------------------------------------------------------- drop-in Executions
