@@ -245,10 +245,9 @@ __device__ __forceinline__ void publish_max(uint32_t* amax, uint32_t m) {
 
 // =====================================================================================
 // The GEMM: C[m][n] = sum_k A[m][k] * B[n][k], int8 x int8 -> exact int32.
-//   256 threads = 4 waves; BM x BN block tile; 128-byte K step (four 32-deep MFMAs);
-//   LDS double buffer with one barrier per step; 16-byte chunks XOR-swizzled so the
-//   ds_read_b128 fragment reads of 32 rows are bank-conflict free.  Workgroups are
-//   remapped so each XCD walks a contiguous range of tiles (A-row panels stay in one L2).
+//   256 threads = 4 waves; BM x BN block tile; 4-stage LDS pipeline (gemm_kernel below).
+//   Workgroups are remapped so each XCD walks a contiguous range of tiles (A-row panels
+//   stay in one L2).
 // Epilogues:
 //   EPI_STORE    int32 C + max|C| (one word, agent-scope atomic)
 //   EPI_AMAX     max|C| only                          (first pass of the recompute strategy)
@@ -256,7 +255,7 @@ __device__ __forceinline__ void publish_max(uint32_t* amax, uint32_t m) {
 //                (+ fused relu / relu-grad mask, + exponent)   (second pass)
 //   EPI_SLAB     int32 partial sums of one K split -> slab[blockIdx.y] (reduced later)
 // =====================================================================================
-constexpr int BK = 128;       // K bytes per step
+constexpr int BK = 64;        // K bytes per step (KT = false)
 constexpr int CPS = BK / 16;  // 16-byte chunks per row per step
 
 enum EpiMode { EPI_STORE = 0, EPI_AMAX = 1, EPI_REQUANT = 2, EPI_SLAB = 3 };
@@ -275,9 +274,6 @@ struct Epi {
     int8_t* exp_out = nullptr;
 };
 
-// 128-byte rows, 16-byte chunk c of row r stored at chunk c ^ ((r >> 1) & 7): the 16-lane
-// groups of a 32-row ds_read_b128 fragment read then hit 16 distinct bank slots.
-__device__ __forceinline__ int lds_off(int r, int c) { return r * BK + ((c ^ ((r >> 1) & 7)) << 4); }
 
 // bijective XCD remap: blocks b, b+8, b+16, ... (one XCD under round-robin dispatch) get
 // consecutive tile ids.  Speed only; any placement is correct.
@@ -347,113 +343,6 @@ __device__ __forceinline__ void gemm_epilogue(v16i (&acc)[BM / WM / 32][BN / WN 
             if (epi.amax != nullptr) publish_max(epi.amax, m);
         }
     }
-}
-
-template <int BM, int BN, int WM, int WN, class LA, class LB, int MODE>
-__global__ void __launch_bounds__(256) gemm_i8_kernel(LA la, LB lb, int M, int N, int tiles_n, int kc_total,
-                                                       int kc_per_split, Epi epi) {
-    static_assert(WM * WN == 4, "4 waves");
-    constexpr int TM = BM / WM / 32;
-    constexpr int TN = BN / WN / 32;
-    static_assert(TM >= 1 && TN >= 1, "tile");
-    constexpr int A_CH = BM * CPS;  // chunks per step
-    constexpr int B_CH = BN * CPS;
-    constexpr int A_LD = (A_CH + 255) / 256;
-    constexpr int B_LD = (B_CH + 255) / 256;
-    constexpr int A_BYTES = BM * BK, B_BYTES = BN * BK;
-    __shared__ __attribute__((aligned(16))) int8_t smem[2 * (A_BYTES + B_BYTES)];
-    int8_t* sA = smem;
-    int8_t* sB = smem + 2 * A_BYTES;
-
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wid = tid >> 6;
-    const int wm = wid / WN, wn = wid % WN;
-    const int tile = xcd_remap(blockIdx.x, gridDim.x);
-    const int tm_ = tile / tiles_n, tn_ = tile % tiles_n;
-    const int m0 = tm_ * BM, n0 = tn_ * BN;
-    const int kc_begin = blockIdx.y * kc_per_split;
-    const int kc_end = min(kc_total, kc_begin + kc_per_split);
-    const int nsteps = kc_end > kc_begin ? (kc_end - kc_begin + CPS - 1) / CPS : 0;
-
-    static_assert(A_CH % 256 == 0 && B_CH % 256 == 0, "staging");
-    const __amdgpu_buffer_rsrc_t rA = make_rsrc(la.ptr(), la.bytes);
-    const __amdgpu_buffer_rsrc_t rB = make_rsrc(lb.ptr(), lb.bytes);
-    typename LA::It ia[A_LD];
-    typename LB::It ib[B_LD];
-#pragma unroll
-    for (int i = 0; i < A_LD; ++i) {
-        const int id = tid + i * 256;
-        ia[i] = la.begin(m0 + id / CPS, kc_begin + id % CPS);
-    }
-#pragma unroll
-    for (int i = 0; i < B_LD; ++i) {
-        const int id = tid + i * 256;
-        ib[i] = lb.begin(n0 + id / CPS, kc_begin + id % CPS);
-    }
-    v4i sa[A_LD], sb[B_LD];
-    auto gload = [&]() {
-#pragma unroll
-        for (int i = 0; i < A_LD; ++i) {
-            sa[i] = buf_load16(rA, la.off(ia[i], kc_end));
-            la.template next<CPS>(ia[i]);
-        }
-#pragma unroll
-        for (int i = 0; i < B_LD; ++i) {
-            sb[i] = buf_load16(rB, lb.off(ib[i], kc_end));
-            lb.template next<CPS>(ib[i]);
-        }
-    };
-    auto sstore = [&](int buf) {
-#pragma unroll
-        for (int i = 0; i < A_LD; ++i) {
-            const int id = tid + i * 256;
-            *(v4i*)(sA + buf * A_BYTES + lds_off(id / CPS, id % CPS)) = sa[i];
-        }
-#pragma unroll
-        for (int i = 0; i < B_LD; ++i) {
-            const int id = tid + i * 256;
-            *(v4i*)(sB + buf * B_BYTES + lds_off(id / CPS, id % CPS)) = sb[i];
-        }
-    };
-
-    v16i acc[TM][TN];
-#pragma unroll
-    for (int a = 0; a < TM; ++a)
-#pragma unroll
-        for (int b = 0; b < TN; ++b)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) acc[a][b][i] = 0;
-
-    if (nsteps > 0) {
-        gload();
-        sstore(0);
-    }
-    __syncthreads();
-    for (int s = 0; s < nsteps; ++s) {
-        const int buf = s & 1;
-        if (s + 1 < nsteps) gload();
-        const int8_t* cA = sA + buf * A_BYTES;
-        const int8_t* cB = sB + buf * B_BYTES;
-#pragma unroll
-        for (int kk = 0; kk < BK / 32; ++kk) {
-            const int c = kk * 2 + (lane >> 5);
-            v4i fa[TM], fb[TN];
-#pragma unroll
-            for (int a = 0; a < TM; ++a) fa[a] = *(const v4i*)(cA + lds_off(wm * (BM / WM) + a * 32 + (lane & 31), c));
-#pragma unroll
-            for (int b = 0; b < TN; ++b) fb[b] = *(const v4i*)(cB + lds_off(wn * (BN / WN) + b * 32 + (lane & 31), c));
-#pragma unroll
-            for (int a = 0; a < TM; ++a)
-#pragma unroll
-                for (int b = 0; b < TN; ++b)
-                    acc[a][b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[a], fb[b], acc[a][b], 0, 0, 0);
-        }
-        if (s + 1 < nsteps) sstore(buf ^ 1);
-        __syncthreads();
-    }
-
-    gemm_epilogue<BM, BN, WM, WN, MODE>(acc, m0, n0, M, N, epi, smem);
 }
 
 // =====================================================================================
@@ -566,19 +455,58 @@ struct KtIm2col {
     }
 };
 
-template <int BM, int BN, int WM, int WN, class LA, class LB, int MODE>
-__global__ void __launch_bounds__(256) gemm_kt_kernel(LA la, LB lb, int M, int N, int tiles_n, int k_total,
-                                                       int k_per_split, Epi epi) {
+// =====================================================================================
+// The GEMM kernel (both operand orientations), a STAGES-deep LDS pipeline fed by LDS-DMA.
+//
+//   KT = false  C[m][n] = sum_k A[m][k] B[n][k]: tiles are [BM|BN rows][BK=64 bytes of K];
+//               fragments by ds_read_b128 (forward conv, input-gradient conv, matmul).
+//   KT = true   C[m][n] = sum_k A[k][m] B[k][n]: tiles are [KT_BK=64 k rows][BM|BN bytes];
+//               fragments by ds_read_b64_tr_b8 (weight gradient; see gemm_kt notes above).
+//
+// Staging: every 1 KiB of a tile is one buffer_load_dwordx4 ... lds wave-instruction (the
+// LDS image is lane-linear per instruction); the XOR swizzle of the image is applied by
+// choosing which global 16-byte chunk each lane fetches.  Out-of-range chunks read zeros.
+// Pipeline: loads for step s+STAGES-1 are issued right after the barrier of step s, into
+// the stage step s-1 used; before that barrier every wave waits with a counted vmcnt for its
+// own step-s loads only, so up to STAGES-2 later steps stay in flight across the barrier.
+// All LDS lives in one __shared__ array and the loop issues no register loads, so hipcc has
+// no reason to drain vmcnt early (cdna_hip_programming.md §5, "Pipelining across barriers").
+// =====================================================================================
+constexpr int STAGES = 4;
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, int8_t* lds_wave_base, uint32_t off) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_wave_base, 16, off, 0, 0,
+                                             0);
+}
+
+// swizzled 16-byte chunk of LDS row r (row of RB bytes) for the two orientations
+template <bool KT, int RB>
+__device__ __forceinline__ int swz16(int r) {
+    if (KT) return kt_swz<RB>(r);
+    return (r >> 2) & 3;  // 64-byte rows: ds_read_b128 fragment reads conflict-free
+}
+
+template <int BM, int BN, int WM, int WN, class LA, class LB, int MODE, bool KT>
+__global__ void __launch_bounds__(256) gemm_kernel(LA la, LB lb, int M, int N, int tiles_n, int k_total,
+                                                    int k_per_split, Epi epi) {
     static_assert(WM * WN == 4, "4 waves");
     constexpr int TM = BM / WM / 32;
     constexpr int TN = BN / WN / 32;
-    constexpr int A_CPR = BM / 16, B_CPR = BN / 16;  // 16-byte chunks per k row
-    constexpr int A_CH = KT_BK * A_CPR, B_CH = KT_BK * B_CPR;
-    constexpr int A_LD = (A_CH + 255) / 256, B_LD = (B_CH + 255) / 256;
-    constexpr int A_BYTES = KT_BK * BM, B_BYTES = KT_BK * BN;
-    __shared__ __attribute__((aligned(16))) int8_t smem[2 * (A_BYTES + B_BYTES)];
-    int8_t* sA = smem;
-    int8_t* sB = smem + 2 * A_BYTES;
+    // staging geometry: rows x row-bytes per operand tile
+    constexpr int A_ROWS = KT ? KT_BK : BM, A_RB = KT ? BM : BK;
+    constexpr int B_ROWS = KT ? KT_BK : BN, B_RB = KT ? BN : BK;
+    constexpr int A_BYTES = A_ROWS * A_RB, B_BYTES = B_ROWS * B_RB;
+    constexpr int A_PW = A_BYTES / 1024 / 4, B_PW = B_BYTES / 1024 / 4;  // DMA instructions per wave
+    static_assert(A_PW >= 1 && B_PW >= 1 && A_BYTES % 4096 == 0 && B_BYTES % 4096 == 0, "tile too small");
+    constexpr int LOADS = A_PW + B_PW;  // per lane per step
+    constexpr int STAGE_BYTES = A_BYTES + B_BYTES;
+    constexpr int K_STEP = KT ? KT_BK : CPS;  // K units per step
+    __shared__ __attribute__((aligned(16))) int8_t smem[STAGES * STAGE_BYTES];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -589,45 +517,36 @@ __global__ void __launch_bounds__(256) gemm_kt_kernel(LA la, LB lb, int M, int N
     const int m0 = tm_ * BM, n0 = tn_ * BN;
     const int k_begin = blockIdx.y * k_per_split;
     const int k_end = min(k_total, k_begin + k_per_split);
-    const int nsteps = k_end > k_begin ? (k_end - k_begin + KT_BK - 1) / KT_BK : 0;
+    const int nsteps = k_end > k_begin ? (k_end - k_begin + K_STEP - 1) / K_STEP : 0;
 
     const __amdgpu_buffer_rsrc_t rA = make_rsrc(la.ptr(), la.bytes);
     const __amdgpu_buffer_rsrc_t rB = make_rsrc(lb.ptr(), lb.bytes);
-    typename LA::It ia[A_LD];
-    typename LB::It ib[B_LD];
+    typename LA::It ia[A_PW];
+    typename LB::It ib[B_PW];
 #pragma unroll
-    for (int i = 0; i < A_LD; ++i) {
-        const int id = tid + i * 256;
-        ia[i] = la.begin(k_begin + id / A_CPR, m0 / 16 + id % A_CPR);
+    for (int i = 0; i < A_PW; ++i) {
+        const int byte = (wid * A_PW + i) * 1024 + lane * 16;
+        const int r = byte / A_RB, c = ((byte % A_RB) >> 4) ^ swz16<KT, A_RB>(r);
+        ia[i] = KT ? la.begin(k_begin + r, m0 / 16 + c) : la.begin(m0 + r, k_begin + c);
     }
 #pragma unroll
-    for (int i = 0; i < B_LD; ++i) {
-        const int id = tid + i * 256;
-        ib[i] = lb.begin(k_begin + id / B_CPR, n0 / 16 + id % B_CPR);
+    for (int i = 0; i < B_PW; ++i) {
+        const int byte = (wid * B_PW + i) * 1024 + lane * 16;
+        const int r = byte / B_RB, c = ((byte % B_RB) >> 4) ^ swz16<KT, B_RB>(r);
+        ib[i] = KT ? lb.begin(k_begin + r, n0 / 16 + c) : lb.begin(n0 + r, k_begin + c);
     }
-    v4i sa[A_LD], sb[B_LD];
-    auto gload = [&]() {
+    auto issue = [&](int stage) {
+        int8_t* sa = smem + stage * STAGE_BYTES;
+        int8_t* sb = sa + A_BYTES;
 #pragma unroll
-        for (int i = 0; i < A_LD; ++i) {
-            sa[i] = buf_load16(rA, la.off(ia[i], k_end));
-            la.template next<KT_BK>(ia[i]);
+        for (int i = 0; i < A_PW; ++i) {
+            dma16(rA, sa + (wid * A_PW + i) * 1024, la.off(ia[i], k_end));
+            la.template next<K_STEP>(ia[i]);
         }
 #pragma unroll
-        for (int i = 0; i < B_LD; ++i) {
-            sb[i] = buf_load16(rB, lb.off(ib[i], k_end));
-            lb.template next<KT_BK>(ib[i]);
-        }
-    };
-    auto sstore = [&](int buf) {
-#pragma unroll
-        for (int i = 0; i < A_LD; ++i) {
-            const int id = tid + i * 256;
-            if (A_CH % 256 == 0 || id < A_CH) *(v4i*)(sA + buf * A_BYTES + kt_off16<BM>(id / A_CPR, id % A_CPR)) = sa[i];
-        }
-#pragma unroll
-        for (int i = 0; i < B_LD; ++i) {
-            const int id = tid + i * 256;
-            if (B_CH % 256 == 0 || id < B_CH) *(v4i*)(sB + buf * B_BYTES + kt_off16<BN>(id / B_CPR, id % B_CPR)) = sb[i];
+        for (int i = 0; i < B_PW; ++i) {
+            dma16(rB, sb + (wid * B_PW + i) * 1024, lb.off(ib[i], k_end));
+            lb.template next<K_STEP>(ib[i]);
         }
     };
 
@@ -639,48 +558,78 @@ __global__ void __launch_bounds__(256) gemm_kt_kernel(LA la, LB lb, int M, int N
 #pragma unroll
             for (int i = 0; i < 16; ++i) acc[a][b][i] = 0;
 
-    // transposed-read geometry of this lane (see the header comment)
-    const int rq = (lane & 15) >> 1;                          // row within an 8-row block
-    const int cofs = 16 * ((lane >> 4) & 1) + 8 * (lane & 1);  // column byte within a 32-column tile
-    const int rh = 16 * (lane >> 5);                          // k half
+    // transposed-read geometry (KT)
+    const int rq = (lane & 15) >> 1;
+    const int cofs = 16 * ((lane >> 4) & 1) + 8 * (lane & 1);
+    const int rh = 16 * (lane >> 5);
 
-    if (nsteps > 0) {
-        gload();
-        sstore(0);
+#pragma unroll
+    for (int st = 0; st < STAGES - 1; ++st)
+        if (st < nsteps) issue(st);
+
+    for (int s = 0; s < nsteps; ++s) {
+        // own loads of step s done; later steps may stay in flight
+        const int later = min(STAGES - 2, nsteps - 1 - s);
+        if (later >= 2)
+            wait_vmcnt<2 * LOADS>();
+        else if (later == 1)
+            wait_vmcnt<LOADS>();
+        else
+            wait_vmcnt<0>();
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (s + STAGES - 1 < nsteps) issue((s + STAGES - 1) % STAGES);
+        const int8_t* cA = smem + (s % STAGES) * STAGE_BYTES;
+        const int8_t* cB = cA + A_BYTES;
+        if (KT) {
+#pragma unroll
+            for (int kk = 0; kk < KT_BK / 32; ++kk) {
+                const int r0 = kk * 32 + rh + rq;
+                v4i fa[TM], fb[TN];
+#pragma unroll
+                for (int a = 0; a < TM; ++a) {
+                    const int c8 = (wm * (BM / WM) + a * 32 + cofs) >> 3;
+                    const v2i x0 = ds_tr8(cA + kt_off8<BM>(r0, c8));
+                    const v2i x1 = ds_tr8(cA + kt_off8<BM>(r0 + 8, c8));
+                    fa[a] = v4i{x0[0], x0[1], x1[0], x1[1]};
+                }
+#pragma unroll
+                for (int b = 0; b < TN; ++b) {
+                    const int c8 = (wn * (BN / WN) + b * 32 + cofs) >> 3;
+                    const v2i y0 = ds_tr8(cB + kt_off8<BN>(r0, c8));
+                    const v2i y1 = ds_tr8(cB + kt_off8<BN>(r0 + 8, c8));
+                    fb[b] = v4i{y0[0], y0[1], y1[0], y1[1]};
+                }
+#pragma unroll
+                for (int a = 0; a < TM; ++a)
+#pragma unroll
+                    for (int b = 0; b < TN; ++b)
+                        acc[a][b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[a], fb[b], acc[a][b], 0, 0, 0);
+            }
+        } else {
+#pragma unroll
+            for (int kk = 0; kk < BK / 32; ++kk) {
+                const int c = kk * 2 + (lane >> 5);
+                v4i fa[TM], fb[TN];
+#pragma unroll
+                for (int a = 0; a < TM; ++a) {
+                    const int r = wm * (BM / WM) + a * 32 + (lane & 31);
+                    fa[a] = *(const v4i*)(cA + r * BK + ((c ^ swz16<false, BK>(r)) << 4));
+                }
+#pragma unroll
+                for (int b = 0; b < TN; ++b) {
+                    const int r = wn * (BN / WN) + b * 32 + (lane & 31);
+                    fb[b] = *(const v4i*)(cB + r * BK + ((c ^ swz16<false, BK>(r)) << 4));
+                }
+#pragma unroll
+                for (int a = 0; a < TM; ++a)
+#pragma unroll
+                    for (int b = 0; b < TN; ++b)
+                        acc[a][b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[a], fb[b], acc[a][b], 0, 0, 0);
+            }
+        }
     }
     __syncthreads();
-    for (int s = 0; s < nsteps; ++s) {
-        const int buf = s & 1;
-        if (s + 1 < nsteps) gload();
-        const int8_t* cA = sA + buf * A_BYTES;
-        const int8_t* cB = sB + buf * B_BYTES;
-#pragma unroll
-        for (int kk = 0; kk < KT_BK / 32; ++kk) {
-            const int r0 = kk * 32 + rh + rq;
-            v4i fa[TM], fb[TN];
-#pragma unroll
-            for (int a = 0; a < TM; ++a) {
-                const int c8 = (wm * (BM / WM) + a * 32 + cofs) >> 3;
-                const v2i x0 = ds_tr8(cA + kt_off8<BM>(r0, c8));
-                const v2i x1 = ds_tr8(cA + kt_off8<BM>(r0 + 8, c8));
-                fa[a] = v4i{x0[0], x0[1], x1[0], x1[1]};
-            }
-#pragma unroll
-            for (int b = 0; b < TN; ++b) {
-                const int c8 = (wn * (BN / WN) + b * 32 + cofs) >> 3;
-                const v2i y0 = ds_tr8(cB + kt_off8<BN>(r0, c8));
-                const v2i y1 = ds_tr8(cB + kt_off8<BN>(r0 + 8, c8));
-                fb[b] = v4i{y0[0], y0[1], y1[0], y1[1]};
-            }
-#pragma unroll
-            for (int a = 0; a < TM; ++a)
-#pragma unroll
-                for (int b = 0; b < TN; ++b)
-                    acc[a][b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[a], fb[b], acc[a][b], 0, 0, 0);
-        }
-        if (s + 1 < nsteps) sstore(buf ^ 1);
-        __syncthreads();
-    }
     gemm_epilogue<BM, BN, WM, WN, MODE>(acc, m0, n0, M, N, epi, smem);
 }
 
@@ -738,11 +687,11 @@ struct GemmPlan {
     Strategy strat = STRAT_STORE;
 };
 
-// k_total: K extent in the kernel's units (16-byte chunks for gemm_i8_kernel, rows for
-// gemm_kt_kernel); k_step: units per K step; k_bytes: K in bytes (recompute threshold).
+// k_total: K extent in the kernel's units (16-byte chunks for KT = false, k rows for
+// KT = true); k_step: units per K step; k_bytes: K in bytes (recompute threshold).
 static GemmPlan plan_gemm(int M, int N, int k_total, int k_step, int k_bytes, bool recompute_ok, size_t ws_elems) {
     GemmPlan p;
-    p.bn = N <= 32 ? 32 : (N <= 64 ? 64 : 128);
+    p.bn = N <= 64 ? 64 : 128;
     p.bm = (M <= 64 && p.bn >= 64) ? 64 : 128;
     p.tiles = ((M + p.bm - 1) / p.bm) * ((N + p.bn - 1) / p.bn);
     const int steps = (k_total + k_step - 1) / k_step;
@@ -785,16 +734,10 @@ static hipError_t launch_mode(const GemmPlan& p, const LA& la, const LB& lb, int
     do {                                                                                                         \
         const int tm = (M + BM_ - 1) / BM_, tn = (N + BN_ - 1) / BN_;                                            \
         dim3 grid(tm * tn, splits);                                                                              \
-        if (KT)                                                                                                  \
-            hipLaunchKernelGGL((gemm_kt_kernel<BM_, BN_, WM_, WN_, LA, LB, MODE>), grid, dim3(256), 0, st, la, lb, \
-                               M, N, tn, k_total, per, epi);                                                     \
-        else                                                                                                     \
-            hipLaunchKernelGGL((gemm_i8_kernel<BM_, BN_, WM_, WN_, LA, LB, MODE>), grid, dim3(256), 0, st, la, lb, \
-                               M, N, tn, k_total, per, epi);                                                     \
+        hipLaunchKernelGGL((gemm_kernel<BM_, BN_, WM_, WN_, LA, LB, MODE, KT>), grid, dim3(256), 0, st, la, lb,   \
+                           M, N, tn, k_total, per, epi);                                                         \
     } while (0)
-    if (p.bn == 32)
-        NITI_LAUNCH(128, 32, 4, 1);
-    else if (p.bn == 64 && p.bm == 64)
+    if (p.bn == 64 && p.bm == 64)
         NITI_LAUNCH(64, 64, 2, 2);
     else if (p.bn == 64)
         NITI_LAUNCH(128, 64, 2, 2);
@@ -808,9 +751,9 @@ static hipError_t launch_mode(const GemmPlan& p, const LA& la, const LB& lb, int
 
 static hipError_t splitk_reduce(const GemmPlan& p, const int32_t* slab, int64_t n, int32_t* C, uint32_t* amax,
                                 hipStream_t st) {
-    int G = 1;
-    while (G < 16 && G < p.splits) G <<= 1;
     const int64_t n4 = n / 4;
+    int G = 1;  // split-level parallelism only where the output alone cannot fill the GPU
+    while (G < 16 && G * 2 <= p.splits && n4 * G < 131072) G <<= 1;
     const int64_t blocks = (n4 + (256 / G) - 1) / (256 / G);
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, st, slab, p.splits, n, n4, G, C,
                        amax);
