@@ -10,6 +10,8 @@
 // reduces max|acc| per workgroup and atomically max-es it into one word; the requant
 // kernel reads that word (after a kernel boundary -- or an RCCL all-reduce(MAX) in
 // data-parallel exact mode) and applies the shift.
+#include <type_traits>
+
 #include "niti_kernels.hpp"
 #include "niti_map.hpp"
 
@@ -41,7 +43,7 @@ __device__ __forceinline__ v4i zero4() {
 // turns (row, chunk) into a byte offset inside one tensor, or OOB (>= 2^31) for a zero
 // chunk (padding, out-of-image taps, rows past M, chunks past the K split).  Loads are
 // raw buffer loads, so an OOB offset reads zeros without a branch.  Per-thread iterators
-// advance by CPS chunks per K step with compares instead of divisions.
+// advance by one K step (a template chunk count) with compares instead of divisions.
 // =====================================================================================
 constexpr uint32_t OOB = 0x80000000u;
 
@@ -51,29 +53,6 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const int8_t* p, uin
 __device__ __forceinline__ v4i buf_load16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
     return __builtin_bit_cast(v4i, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0));
 }
-
-// Plain row-major operand: row r at r*ld, K-chunks contiguous.
-struct LoadRowMajor {
-    const int8_t* p;
-    int64_t ld;
-    int rows;
-    int kc_total;
-    uint32_t bytes;
-    __device__ __forceinline__ const int8_t* ptr() const { return p; }
-    struct It {
-        uint32_t base;
-        int kc;
-        bool ok;
-    };
-    __device__ __forceinline__ It begin(int r, int kc) const {
-        return {r < rows ? (uint32_t)(r * ld) : 0u, kc, r < rows};
-    }
-    template <int S>
-    __device__ __forceinline__ void next(It& t) const { t.kc += S; }
-    __device__ __forceinline__ uint32_t off(const It& t, int kc_end) const {
-        return (t.ok && t.kc < kc_end && t.kc < kc_total) ? t.base + (uint32_t)t.kc * 16u : OOB;
-    }
-};
 
 // Forward conv, A operand: row m = output pixel (n, oy, ox) of an NHWC16 input, K-chunk
 // kc = (ky, kx, cc) with cc the 16-channel group (the im2col of Int8FunctionsOpt.cpp:342-392,
@@ -255,8 +234,8 @@ __device__ __forceinline__ void publish_max(uint32_t* amax, uint32_t m) {
 //                (+ fused relu / relu-grad mask, + exponent)   (second pass)
 //   EPI_SLAB     int32 partial sums of one K split -> slab[blockIdx.y] (reduced later)
 // =====================================================================================
-constexpr int BK = 64;        // K bytes per step (KT = false)
-constexpr int CPS = BK / 16;  // 16-byte chunks per row per step
+// K bytes per step (KT = false) is the A loader's BK: 128 (full 128-byte lines per row and
+// step) where the operand allows it, else 64.
 
 enum EpiMode { EPI_STORE = 0, EPI_AMAX = 1, EPI_REQUANT = 2, EPI_SLAB = 3 };
 
@@ -284,15 +263,12 @@ __device__ __forceinline__ int xcd_remap(int b, int nwg) {
 
 // Shared epilogue: D[row][col] of the 32x32 MFMA tiles, row = (i&3) + 8*(i>>2) + 4*(lane>>5),
 // col = lane&31.  `smem` is reused for the block max (every LDS read finished at the last barrier).
-template <int BM, int BN, int WM, int WN, int MODE>
-__device__ __forceinline__ void gemm_epilogue(v16i (&acc)[BM / WM / 32][BN / WN / 32], int m0, int n0, int M, int N,
-                                              const Epi& epi, int8_t* smem) {
-    constexpr int TM = BM / WM / 32;
-    constexpr int TN = BN / WN / 32;
+template <int TM, int TN, int NW, int MODE>
+__device__ __forceinline__ void gemm_epilogue(v16i (&acc)[TM][TN], int r0, int c0, int M, int N, const Epi& epi,
+                                              int8_t* smem) {
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wid = tid >> 6;
-    const int wm = wid / WN, wn = wid % WN;
     int rq_shift = 2;
     bool rq_raw = false;
     if (MODE == EPI_REQUANT) {
@@ -312,10 +288,10 @@ __device__ __forceinline__ void gemm_epilogue(v16i (&acc)[BM / WM / 32][BN / WN 
     for (int a = 0; a < TM; ++a)
 #pragma unroll
         for (int b = 0; b < TN; ++b) {
-            const int col = n0 + wn * (BN / WN) + b * 32 + (lane & 31);
+            const int col = c0 + b * 32 + (lane & 31);
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
-                const int row = m0 + wm * (BM / WM) + a * 32 + (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
+                const int row = r0 + a * 32 + (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
                 const int v = acc[a][b][i];
                 if (row < M && col < N) {
                     if (MODE == EPI_STORE || MODE == EPI_SLAB) Cs[(int64_t)row * epi.ldc + col] = v;
@@ -339,7 +315,7 @@ __device__ __forceinline__ void gemm_epilogue(v16i (&acc)[BM / WM / 32][BN / WN 
         __syncthreads();
         if (tid == 0) {
             uint32_t m = red[0];
-            for (int i = 1; i < 4; ++i) m = m > red[i] ? m : red[i];
+            for (int i = 1; i < NW; ++i) m = m > red[i] ? m : red[i];
             if (epi.amax != nullptr) publish_max(epi.amax, m);
         }
     }
@@ -390,32 +366,6 @@ __device__ __forceinline__ v2i ds_tr8(const int8_t* p) {
     return __builtin_amdgcn_ds_read_tr8_b64_v2i32((__attribute__((address_space(3))) v2i*)(p));
 }
 
-// A (and plain B) operand: row-major [K rows][ld bytes], column chunk = 16 consecutive M.
-struct KtRows {
-    const int8_t* p;
-    uint32_t bytes;
-    int64_t ld;
-    int cols;  // valid columns (multiple of 16)
-    int K;
-    __device__ __forceinline__ const int8_t* ptr() const { return p; }
-    struct It {
-        uint32_t off;
-        int k;
-        bool ok;
-    };
-    __device__ __forceinline__ It begin(int k, int c16) const {
-        return {(uint32_t)(k * ld + c16 * 16), k, c16 * 16 < cols};
-    }
-    template <int S>
-    __device__ __forceinline__ void next(It& t) const {
-        t.k += S;
-        t.off += (uint32_t)(S * ld);
-    }
-    __device__ __forceinline__ uint32_t off(const It& t, int k_end) const {
-        return (t.ok && t.k < k_end && t.k < K) ? t.off : OOB;
-    }
-};
-
 // B operand of the weight gradient: column n' = (ky, kx, ci) of the OHWI16 gradient, row k =
 // output pixel (n, oy, ox); the value is x[n][oy*sh - pt + ky*dh][ox*sw - pl + kx*dw][ci]
 // from an NHWC16 activation (zero outside the image).
@@ -456,6 +406,258 @@ struct KtIm2col {
 };
 
 // =====================================================================================
+// Staging interface of the GEMM kernel.  A loader splits each DMA slot's byte offset into a
+// per-lane part (Lane, fixed when the block starts) and a wave-uniform part (Uni, advanced
+// once per K step in scalar registers and passed as the buffer instruction's soffset), so the
+// steady-state K loop does almost no vector address arithmetic:
+//   Lane lane(a, b, k_begin)  NON-KT: a = GEMM row, b = 16-byte chunk inside the K step
+//                             KT:     a = k row inside the step, b = absolute column chunk
+//   Uni  uni(k_begin, k_end)  fetch<S>(Lane&, Uni) -> voffset   soff(Uni) -> soffset
+//   step<S>(Uni&)             advance one K step (S chunks, or S k rows)
+// A voffset of OOB reads zeros; a valid voffset + soffset stays inside the tensor.
+// =====================================================================================
+
+// Any per-lane iterator loader (LoadConvFwd / LoadConvDgrad / KtIm2col) behind the interface:
+// the general case (ragged channels, strided input gradient, unaligned pixel counts).
+template <class G, bool KT_>
+struct PerLane {
+    static constexpr int BK = 64;
+    G g;
+    uint32_t bytes;
+    __device__ __forceinline__ const int8_t* ptr() const { return g.ptr(); }
+    struct Lane {
+        typename G::It it;
+    };
+    struct Uni {
+        int k_end;
+    };
+    __device__ __forceinline__ Lane lane(int a, int b, int kb) const {
+        return {KT_ ? g.begin(kb + a, b) : g.begin(a, kb + b)};
+    }
+    __device__ __forceinline__ Uni uni(int, int ke) const { return {ke}; }
+    template <int S>
+    __device__ __forceinline__ uint32_t fetch(Lane& l, const Uni& u) const {
+        const uint32_t o = g.off(l.it, u.k_end);
+        g.template next<S>(l.it);
+        return o;
+    }
+    __device__ __forceinline__ uint32_t soff(const Uni&) const { return 0u; }
+    template <int S>
+    __device__ __forceinline__ void step(Uni&) const {}
+};
+template <class G, bool KT_>
+static PerLane<G, KT_> per_lane(const G& g) {
+    PerLane<G, KT_> r;
+    r.g = g;
+    r.bytes = g.bytes;
+    return r;
+}
+
+// Row-major operand [rows][ld] with K chunks contiguous (weights, matmul operands).
+struct RowsK {
+    static constexpr int BK = 64;
+    const int8_t* p;
+    int64_t ld;
+    int rows, kc_total;
+    uint32_t bytes;
+    __device__ __forceinline__ const int8_t* ptr() const { return p; }
+    struct Lane {
+        uint32_t cur;
+        int c;
+    };
+    struct Uni {
+        int kc0, kc_end;
+    };
+    __device__ __forceinline__ Lane lane(int row, int c, int) const {
+        return {row < rows ? (uint32_t)(row * ld + c * 16) : OOB, c};
+    }
+    __device__ __forceinline__ Uni uni(int kb, int ke) const { return {kb, ke < kc_total ? ke : kc_total}; }
+    template <int S>
+    __device__ __forceinline__ uint32_t fetch(Lane& l, const Uni& u) const {
+        if (u.kc0 + S <= u.kc_end) return l.cur;
+        return u.kc0 + l.c < u.kc_end ? l.cur : OOB;
+    }
+    __device__ __forceinline__ uint32_t soff(const Uni& u) const { return (uint32_t)u.kc0 * 16u; }
+    template <int S>
+    __device__ __forceinline__ void step(Uni& u) const { u.kc0 += S; }
+};
+
+// Convolution operand whose K steps never straddle a tap (channels padded to a multiple of
+// 64 bytes, kh*kw <= 32): row = pixel, K = (ky, kx, channel).  Each lane keeps a bit mask of
+// the taps that fall inside the image for its pixel and re-derives its voffset only when the
+// step enters a new tap; the channel offset inside the tap is the uniform soffset.
+//   forward:         source x [N][SH][SW][C], y0 = oy*sh - pt, tap moves by +(ky*dh, kx*dw)
+//   input gradient:  source dy [N][OH][OW][C] (stride 1), y0 = iy + pt, tap moves by -(ky*dh, kx*dw)
+template <int BKB>
+struct ConvTaps {
+    static constexpr int BK = BKB;
+    const int8_t* src;
+    uint32_t bytes;
+    int SH, SW, CPC;  // source image and channel chunks
+    int PH, PW;       // pixel grid of the GEMM rows
+    int sh, sw, oy_add, ox_add, dh, dw, KH, KW, M;
+    int sgn;  // +1 forward, -1 input gradient
+    uint32_t img;
+    __device__ __forceinline__ const int8_t* ptr() const { return src; }
+    struct Lane {
+        int base;
+        uint32_t mask, cur;
+    };
+    struct Uni {
+        int cc, ky, kx, tapoff;
+        bool fresh;
+    };
+    __device__ __forceinline__ Lane lane(int m, int c, int) const {
+        Lane l;
+        l.cur = OOB;
+        l.mask = 0;
+        l.base = 0;
+        if (m < M) {
+            const int px = m % PW, r = m / PW, py = r % PH, n = r / PH;
+            const int y0 = py * sh + oy_add, x0 = px * sw + ox_add;
+            l.base = (int)((uint32_t)n * img) + ((y0 * SW + x0) * CPC + c) * 16;
+            for (int ky = 0, t = 0; ky < KH; ++ky)
+                for (int kx = 0; kx < KW; ++kx, ++t) {
+                    const int y = y0 + sgn * ky * dh, x = x0 + sgn * kx * dw;
+                    if ((unsigned)y < (unsigned)SH && (unsigned)x < (unsigned)SW) l.mask |= 1u << t;
+                }
+        }
+        return l;
+    }
+    __device__ __forceinline__ int tap_off(int ky, int kx) const { return sgn * ((ky * dh * SW + kx * dw) * CPC * 16); }
+    __device__ __forceinline__ Uni uni(int kb, int) const {
+        Uni u;
+        const int tap = kb / CPC;
+        u.cc = kb - tap * CPC;
+        u.ky = tap / KW;
+        u.kx = tap - u.ky * KW;
+        u.tapoff = tap_off(u.ky, u.kx);
+        u.fresh = true;
+        return u;
+    }
+    template <int S>
+    __device__ __forceinline__ uint32_t fetch(Lane& l, const Uni& u) const {
+        if (u.fresh) l.cur = ((l.mask >> (u.ky * KW + u.kx)) & 1u) ? (uint32_t)(l.base + u.tapoff) : OOB;
+        return l.cur;
+    }
+    __device__ __forceinline__ uint32_t soff(const Uni& u) const { return (uint32_t)u.cc * 16u; }
+    template <int S>
+    __device__ __forceinline__ void step(Uni& u) const {
+        u.cc += S;
+        u.fresh = u.cc >= CPC;
+        if (u.fresh) {
+            u.cc = 0;
+            if (++u.kx == KW) {
+                u.kx = 0;
+                ++u.ky;
+            }
+            u.tapoff = tap_off(u.ky, u.kx);
+        }
+    }
+};
+
+// K-major rows (weight gradient A operand: dy [pixels][cop]); the k row offset is uniform.
+struct KtRowsU {
+    static constexpr int BK = 64;
+    const int8_t* p;
+    uint32_t bytes;
+    int64_t ld;
+    int cols, K;
+    __device__ __forceinline__ const int8_t* ptr() const { return p; }
+    struct Lane {
+        uint32_t cur;
+        int r;
+    };
+    struct Uni {
+        int k0, k_end;
+    };
+    __device__ __forceinline__ Lane lane(int r, int c16, int) const {
+        return {c16 * 16 < cols ? (uint32_t)(r * ld + c16 * 16) : OOB, r};
+    }
+    __device__ __forceinline__ Uni uni(int kb, int ke) const { return {kb, ke < K ? ke : K}; }
+    template <int S>
+    __device__ __forceinline__ uint32_t fetch(Lane& l, const Uni& u) const {
+        if (u.k0 + S <= u.k_end) return l.cur;
+        return l.r < u.k_end - u.k0 ? l.cur : OOB;
+    }
+    __device__ __forceinline__ uint32_t soff(const Uni& u) const { return (uint32_t)((int64_t)u.k0 * ld); }
+    template <int S>
+    __device__ __forceinline__ void step(Uni& u) const { u.k0 += S; }
+};
+
+// Weight-gradient B operand (im2col of x, rows = output pixels) when every 64-pixel K step is
+// a whole number of output rows of one image (OW | 64, 64 | OH*OW) or of whole images
+// (OH*OW | 64): a lane's position inside the step is then the same at every step, and only
+// the step's image / first row (uniform) moves.
+struct KtIm2colU {
+    static constexpr int BK = 64;
+    const int8_t* x;
+    uint32_t bytes;
+    int H, W, OH, OW, CIP, KW, sh, sw, pt, pl, dh, dw, ncols, K;
+    bool rows_mode;  // true: a step = 64/OW output rows of one image; false: 64/(OH*OW) images
+    __device__ __forceinline__ const int8_t* ptr() const { return x; }
+    struct Lane {
+        int rel, dy, r;
+        bool ok;
+    };
+    struct Uni {
+        int k0, k_end, n0, oy0, ubase;
+    };
+    __device__ __forceinline__ Lane lane(int r, int c16, int) const {
+        Lane l;
+        const int nn = c16 * 16;
+        l.ok = nn < ncols;
+        const int tap = l.ok ? nn / CIP : 0;
+        const int ci0 = nn - tap * CIP;
+        const int ky = tap / KW, kx = tap - ky * KW;
+        int dn = 0, rem = r;
+        if (!rows_mode) {
+            dn = r / (OH * OW);
+            rem = r - dn * OH * OW;
+        }
+        const int doy = rem / OW, dox = rem - doy * OW;
+        const int ix = dox * sw + kx * dw - pl;
+        l.dy = doy * sh + ky * dh - pt;
+        l.ok = l.ok && (unsigned)ix < (unsigned)W;
+        if (!rows_mode) l.ok = l.ok && (unsigned)l.dy < (unsigned)H;
+        l.rel = ((dn * H + l.dy) * W + ix) * CIP + ci0;
+        l.r = r;
+        return l;
+    }
+    __device__ __forceinline__ Uni uni(int kb, int ke) const {
+        Uni u;
+        u.k0 = kb;
+        u.k_end = ke < K ? ke : K;
+        u.n0 = kb / (OH * OW);
+        u.oy0 = (kb - u.n0 * OH * OW) / OW;
+        u.ubase = (u.n0 * H + u.oy0 * sh) * W * CIP;
+        return u;
+    }
+    template <int S>
+    __device__ __forceinline__ uint32_t fetch(Lane& l, const Uni& u) const {
+        bool v = l.ok;
+        if (rows_mode) v = v && (unsigned)(u.oy0 * sh + l.dy) < (unsigned)H;
+        if (u.k0 + S > u.k_end) v = v && l.r < u.k_end - u.k0;
+        return v ? (uint32_t)(u.ubase + l.rel) : OOB;
+    }
+    __device__ __forceinline__ uint32_t soff(const Uni&) const { return 0u; }
+    template <int S>
+    __device__ __forceinline__ void step(Uni& u) const {
+        u.k0 += S;
+        if (rows_mode) {
+            u.oy0 += S / OW;
+            if (u.oy0 >= OH) {
+                u.oy0 = 0;
+                ++u.n0;
+            }
+        } else {
+            u.n0 += S / (OH * OW);
+        }
+        u.ubase = (u.n0 * H + u.oy0 * sh) * W * CIP;
+    }
+};
+
+// =====================================================================================
 // The GEMM kernel (both operand orientations), a STAGES-deep LDS pipeline fed by LDS-DMA.
 //
 //   KT = false  C[m][n] = sum_k A[m][k] B[n][k]: tiles are [BM|BN rows][BK=64 bytes of K];
@@ -472,46 +674,105 @@ struct KtIm2col {
 // All LDS lives in one __shared__ array and the loop issues no register loads, so hipcc has
 // no reason to drain vmcnt early (cdna_hip_programming.md §5, "Pipelining across barriers").
 // =====================================================================================
-constexpr int STAGES = 4;
+constexpr int LDS_STAGE_BUDGET = 64 * 1024;  // pipeline depth = min(MAX_STAGES, budget / stage bytes)
+constexpr int MAX_STAGES = 4;               // (deeper pipelines measured no faster at one block per CU)
+#ifndef NITI_ABLATE
+#define NITI_ABLATE 0  // diagnostic builds only: 1 = no global->LDS copies, 2 = no MFMA
+#endif
+
 
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, int8_t* lds_wave_base, uint32_t off) {
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_wave_base, 16, off, 0, 0,
-                                             0);
+// wait until at most `later` steps of this wave's loads (L each) are outstanding
+template <int L, int MAXL>
+__device__ __forceinline__ void wait_steps(int later) {
+    if (MAXL >= 6 && later >= 6)
+        wait_vmcnt<6 * L>();
+    else if (MAXL >= 5 && later == 5)
+        wait_vmcnt<5 * L>();
+    else if (MAXL >= 4 && later == 4)
+        wait_vmcnt<4 * L>();
+    else if (MAXL >= 3 && later == 3)
+        wait_vmcnt<3 * L>();
+    else if (MAXL >= 2 && later == 2)
+        wait_vmcnt<2 * L>();
+    else if (MAXL >= 1 && later == 1)
+        wait_vmcnt<L>();
+    else
+        wait_vmcnt<0>();
+}
+
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+__device__ __forceinline__ v4i lds_b128(uint32_t a) {
+    v4i r;
+    asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"(a));
+    return r;
+}
+// two transposed 8x8-byte reads, rows r and r+8 (ROW8 = 8 rows of the image in bytes)
+__device__ __forceinline__ v4i lds_tr8x2(uint32_t a, int row8) {
+    v2i x0, x1;
+    asm volatile("ds_read_b64_tr_b8 %0, %1" : "=v"(x0) : "v"(a));
+    asm volatile("ds_read_b64_tr_b8 %0, %1" : "=v"(x1) : "v"(a + row8));
+    return v4i{x0[0], x0[1], x1[0], x1[1]};
+}
+template <int N>
+__device__ __forceinline__ void lgkm_wait() {
+    asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N < 15 ? N : 15));
+}
+// orders a use of v after the preceding (volatile) wait
+__device__ __forceinline__ void reg_fence(v4i& v) { asm volatile("" : "+v"(v)); }
+
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, int8_t* lds_wave_base, uint32_t voff, uint32_t soff) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_wave_base, 16, voff,
+                                             soff, 0, 0);
 }
 
 // swizzled 16-byte chunk of LDS row r (row of RB bytes) for the two orientations
 template <bool KT, int RB>
 __device__ __forceinline__ int swz16(int r) {
     if (KT) return kt_swz<RB>(r);
-    return (r >> 2) & 3;  // 64-byte rows: ds_read_b128 fragment reads conflict-free
+    // ds_read_b128 fragment reads conflict-free: 64-byte rows (r>>2)&3, 128-byte rows (r>>1)&7
+    return RB == 128 ? (r >> 1) & 7 : (r >> 2) & 3;
 }
 
-template <int BM, int BN, int WM, int WN, class LA, class LB, int MODE, bool KT>
-__global__ void __launch_bounds__(256) gemm_kernel(LA la, LB lb, int M, int N, int tiles_n, int k_total,
-                                                    int k_per_split, Epi epi) {
-    static_assert(WM * WN == 4, "4 waves");
+template <int BM, int BN, int WM, int WN, class LA, class LB, int MODE, bool KT, int NW>
+__global__ void __launch_bounds__(NW * 64) gemm_kernel(LA la, LB lb, int M, int N, int tiles_n, int k_total,
+                                                        int k_per_split, Epi epi) {
+    static_assert(WM * WN == 4, "4 wave positions");
+    static_assert(NW == 4 || NW == 8, "4 or 8 waves");
+    constexpr int KG = NW / 4;  // wave groups splitting each step's K sub-steps
     constexpr int TM = BM / WM / 32;
     constexpr int TN = BN / WN / 32;
     // staging geometry: rows x row-bytes per operand tile
+    constexpr int BK = KT ? 64 : LA::BK;
     constexpr int A_ROWS = KT ? KT_BK : BM, A_RB = KT ? BM : BK;
     constexpr int B_ROWS = KT ? KT_BK : BN, B_RB = KT ? BN : BK;
     constexpr int A_BYTES = A_ROWS * A_RB, B_BYTES = B_ROWS * B_RB;
-    constexpr int A_PW = A_BYTES / 1024 / 4, B_PW = B_BYTES / 1024 / 4;  // DMA instructions per wave
-    static_assert(A_PW >= 1 && B_PW >= 1 && A_BYTES % 4096 == 0 && B_BYTES % 4096 == 0, "tile too small");
+    constexpr int A_PW = A_BYTES / 1024 / NW, B_PW = B_BYTES / 1024 / NW;  // DMA instructions per wave
+    static_assert(A_PW >= 1 && B_PW >= 1 && A_BYTES % (1024 * NW) == 0 && B_BYTES % (1024 * NW) == 0,
+                  "tile too small for the wave count");
     constexpr int LOADS = A_PW + B_PW;  // per lane per step
     constexpr int STAGE_BYTES = A_BYTES + B_BYTES;
-    constexpr int K_STEP = KT ? KT_BK : CPS;  // K units per step
-    __shared__ __attribute__((aligned(16))) int8_t smem[STAGES * STAGE_BYTES];
+    constexpr int STAGES_FIT = LDS_STAGE_BUDGET / STAGE_BYTES;
+    constexpr int STAGES = STAGES_FIT >= MAX_STAGES ? MAX_STAGES : (STAGES_FIT >= 2 ? STAGES_FIT : 2);
+    constexpr int K_STEP = KT ? KT_BK : BK / 16;  // K units (k rows or 16-byte chunks) per step
+    constexpr int KSUB = (KT ? KT_BK : BK) / 32;   // 32-deep MFMA sub-steps per step
+    constexpr int KW_ = KSUB / KG;                 // sub-steps per wave per step
+    static_assert(KSUB % KG == 0, "sub-steps split evenly");
+    constexpr int XCH_BYTES = KG > 1 ? NW * (TM / 2) * TN * 64 * 64 : 0;  // accumulator exchange
+    constexpr int SMEM = STAGES * STAGE_BYTES > XCH_BYTES ? STAGES * STAGE_BYTES : XCH_BYTES;
+    __shared__ __attribute__((aligned(16))) int8_t smem[SMEM];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
-    const int wid = tid >> 6;
-    const int wm = wid / WN, wn = wid % WN;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: LDS bases stay scalar
+    const int kg = wid >> 2, wq = wid & 3;
+    const int wm = wq / WN, wn = wq % WN;
     const int tile = xcd_remap(blockIdx.x, gridDim.x);
     const int tm_ = tile / tiles_n, tn_ = tile % tiles_n;
     const int m0 = tm_ * BM, n0 = tn_ * BN;
@@ -521,33 +782,38 @@ __global__ void __launch_bounds__(256) gemm_kernel(LA la, LB lb, int M, int N, i
 
     const __amdgpu_buffer_rsrc_t rA = make_rsrc(la.ptr(), la.bytes);
     const __amdgpu_buffer_rsrc_t rB = make_rsrc(lb.ptr(), lb.bytes);
-    typename LA::It ia[A_PW];
-    typename LB::It ib[B_PW];
+    typename LA::Lane ia[A_PW];
+    typename LB::Lane ib[B_PW];
 #pragma unroll
     for (int i = 0; i < A_PW; ++i) {
         const int byte = (wid * A_PW + i) * 1024 + lane * 16;
         const int r = byte / A_RB, c = ((byte % A_RB) >> 4) ^ swz16<KT, A_RB>(r);
-        ia[i] = KT ? la.begin(k_begin + r, m0 / 16 + c) : la.begin(m0 + r, k_begin + c);
+        ia[i] = KT ? la.lane(r, m0 / 16 + c, k_begin) : la.lane(m0 + r, c, k_begin);
     }
 #pragma unroll
     for (int i = 0; i < B_PW; ++i) {
         const int byte = (wid * B_PW + i) * 1024 + lane * 16;
         const int r = byte / B_RB, c = ((byte % B_RB) >> 4) ^ swz16<KT, B_RB>(r);
-        ib[i] = KT ? lb.begin(k_begin + r, n0 / 16 + c) : lb.begin(n0 + r, k_begin + c);
+        ib[i] = KT ? lb.lane(r, n0 / 16 + c, k_begin) : lb.lane(n0 + r, c, k_begin);
     }
+    typename LA::Uni ua = la.uni(k_begin, k_end);
+    typename LB::Uni ub = lb.uni(k_begin, k_end);
     auto issue = [&](int stage) {
         int8_t* sa = smem + stage * STAGE_BYTES;
         int8_t* sb = sa + A_BYTES;
+        const uint32_t soa = la.soff(ua), sob = lb.soff(ub);
 #pragma unroll
         for (int i = 0; i < A_PW; ++i) {
-            dma16(rA, sa + (wid * A_PW + i) * 1024, la.off(ia[i], k_end));
-            la.template next<K_STEP>(ia[i]);
+            const uint32_t vo = la.template fetch<K_STEP>(ia[i], ua);
+            if (NITI_ABLATE != 1) dma16(rA, sa + (wid * A_PW + i) * 1024, vo, soa);
         }
 #pragma unroll
         for (int i = 0; i < B_PW; ++i) {
-            dma16(rB, sb + (wid * B_PW + i) * 1024, lb.off(ib[i], k_end));
-            lb.template next<K_STEP>(ib[i]);
+            const uint32_t vo = lb.template fetch<K_STEP>(ib[i], ub);
+            if (NITI_ABLATE != 1) dma16(rB, sb + (wid * B_PW + i) * 1024, vo, sob);
         }
+        la.template step<K_STEP>(ua);
+        lb.template step<K_STEP>(ub);
     };
 
     v16i acc[TM][TN];
@@ -558,79 +824,149 @@ __global__ void __launch_bounds__(256) gemm_kernel(LA la, LB lb, int M, int N, i
 #pragma unroll
             for (int i = 0; i < 16; ++i) acc[a][b][i] = 0;
 
-    // transposed-read geometry (KT)
-    const int rq = (lane & 15) >> 1;
-    const int cofs = 16 * ((lane >> 4) & 1) + 8 * (lane & 1);
-    const int rh = 16 * (lane >> 5);
+    // per-lane fragment offsets inside a stage (loop invariant); wave group kg takes the
+    // sub-steps kk = kg, kg + KG, ...
+    const uint32_t smem_base = lds_addr(smem);
+    uint32_t offA[KW_][TM], offB[KW_][TN];
+#pragma unroll
+    for (int j = 0; j < KW_; ++j) {
+        const int kk = kg + KG * j;
+        if (KT) {
+            // transposed reads: lane 2q+p of each 16-lane group names row q, 8-byte column p
+            const int r0 = kk * 32 + 16 * (lane >> 5) + ((lane & 15) >> 1);
+            const int cofs = 16 * ((lane >> 4) & 1) + 8 * (lane & 1);
+#pragma unroll
+            for (int a = 0; a < TM; ++a) offA[j][a] = kt_off8<BM>(r0, (wm * (BM / WM) + a * 32 + cofs) >> 3);
+#pragma unroll
+            for (int b = 0; b < TN; ++b) offB[j][b] = kt_off8<BN>(r0, (wn * (BN / WN) + b * 32 + cofs) >> 3);
+        } else {
+            const int c = kk * 2 + (lane >> 5);
+#pragma unroll
+            for (int a = 0; a < TM; ++a) {
+                const int r = wm * (BM / WM) + a * 32 + (lane & 31);
+                offA[j][a] = r * BK + ((c ^ swz16<false, BK>(r)) << 4);
+            }
+#pragma unroll
+            for (int b = 0; b < TN; ++b) {
+                const int r = wn * (BN / WN) + b * 32 + (lane & 31);
+                offB[j][b] = r * BK + ((c ^ swz16<false, BK>(r)) << 4);
+            }
+        }
+    }
+
+    // Fragments are double-buffered in registers: the reads for step s+1 are issued right
+    // after the barrier of iteration s and fly while step s's MFMAs run.  Fragment reads are
+    // inline asm: hipcc cannot tell them apart from the LDS-DMA writes still in flight to the
+    // other stages and would otherwise drain vmcnt(0) before every ds_read.
+    // Stage reuse: iteration s refills the stage of step s-1, whose reads every wave waited
+    // for before its step s-1 MFMAs, i.e. before the barrier of iteration s.
+    static_assert(STAGES >= 3, "register double buffering needs three stages");
+    constexpr int READS = KT ? 2 * (TM + TN) : (TM + TN);  // per sub-step
+    constexpr int RW = KW_ * READS;                        // per wave per step
+    v4i fa[2][KW_][TM], fb[2][KW_][TN];
+    auto read_frags = [&](auto buf_c, int step) {
+        constexpr int BUF = decltype(buf_c)::value;
+        const uint32_t sA = smem_base + (uint32_t)((step % STAGES) * STAGE_BYTES);
+        const uint32_t sB = sA + A_BYTES;
+#pragma unroll
+        for (int j = 0; j < KW_; ++j) {
+#pragma unroll
+            for (int a = 0; a < TM; ++a)
+                fa[BUF][j][a] = KT ? lds_tr8x2(sA + offA[j][a], BM * 8) : lds_b128(sA + offA[j][a]);
+#pragma unroll
+            for (int b = 0; b < TN; ++b)
+                fb[BUF][j][b] = KT ? lds_tr8x2(sB + offB[j][b], BN * 8) : lds_b128(sB + offB[j][b]);
+        }
+    };
+    auto body = [&](auto cur_c, int s) {
+        constexpr int CUR = decltype(cur_c)::value;
+        const bool more = s + 1 < nsteps;
+        if (more) wait_steps<LOADS, STAGES - 3>(min(STAGES - 3, nsteps - 2 - s));  // own step s+1 loads landed
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (s + STAGES - 1 < nsteps) issue((s + STAGES - 1) % STAGES);
+        if (more) {
+            read_frags(std::integral_constant<int, 1 - CUR>(), s + 1);
+            lgkm_wait<RW>();  // step s's fragments (requested one iteration earlier) are in
+        } else {
+            lgkm_wait<0>();
+        }
+#pragma unroll
+        for (int j = 0; j < KW_; ++j) {
+#pragma unroll
+            for (int a = 0; a < TM; ++a) reg_fence(fa[CUR][j][a]);
+#pragma unroll
+            for (int b = 0; b < TN; ++b) reg_fence(fb[CUR][j][b]);
+        }
+#pragma unroll
+        for (int j = 0; j < KW_; ++j)
+#pragma unroll
+            for (int a = 0; a < TM; ++a)
+#pragma unroll
+                for (int b = 0; b < TN; ++b) {
+                    if (NITI_ABLATE == 2) {
+                        acc[a][b][0] += fa[CUR][j][a][0] ^ fb[CUR][j][b][1];
+                    } else {
+                        acc[a][b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[CUR][j][a], fb[CUR][j][b], acc[a][b], 0,
+                                                                          0, 0);
+                    }
+                }
+        __builtin_amdgcn_sched_barrier(0);
+    };
 
 #pragma unroll
     for (int st = 0; st < STAGES - 1; ++st)
         if (st < nsteps) issue(st);
-
-    for (int s = 0; s < nsteps; ++s) {
-        // own loads of step s done; later steps may stay in flight
-        const int later = min(STAGES - 2, nsteps - 1 - s);
-        if (later >= 2)
-            wait_vmcnt<2 * LOADS>();
-        else if (later == 1)
-            wait_vmcnt<LOADS>();
-        else
-            wait_vmcnt<0>();
+    if (nsteps > 0) {
+        wait_steps<LOADS, STAGES - 2>(min(STAGES - 2, nsteps - 1));
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        if (s + STAGES - 1 < nsteps) issue((s + STAGES - 1) % STAGES);
-        const int8_t* cA = smem + (s % STAGES) * STAGE_BYTES;
-        const int8_t* cB = cA + A_BYTES;
-        if (KT) {
-#pragma unroll
-            for (int kk = 0; kk < KT_BK / 32; ++kk) {
-                const int r0 = kk * 32 + rh + rq;
-                v4i fa[TM], fb[TN];
-#pragma unroll
-                for (int a = 0; a < TM; ++a) {
-                    const int c8 = (wm * (BM / WM) + a * 32 + cofs) >> 3;
-                    const v2i x0 = ds_tr8(cA + kt_off8<BM>(r0, c8));
-                    const v2i x1 = ds_tr8(cA + kt_off8<BM>(r0 + 8, c8));
-                    fa[a] = v4i{x0[0], x0[1], x1[0], x1[1]};
-                }
-#pragma unroll
-                for (int b = 0; b < TN; ++b) {
-                    const int c8 = (wn * (BN / WN) + b * 32 + cofs) >> 3;
-                    const v2i y0 = ds_tr8(cB + kt_off8<BN>(r0, c8));
-                    const v2i y1 = ds_tr8(cB + kt_off8<BN>(r0 + 8, c8));
-                    fb[b] = v4i{y0[0], y0[1], y1[0], y1[1]};
-                }
-#pragma unroll
-                for (int a = 0; a < TM; ++a)
-#pragma unroll
-                    for (int b = 0; b < TN; ++b)
-                        acc[a][b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[a], fb[b], acc[a][b], 0, 0, 0);
-            }
-        } else {
-#pragma unroll
-            for (int kk = 0; kk < BK / 32; ++kk) {
-                const int c = kk * 2 + (lane >> 5);
-                v4i fa[TM], fb[TN];
-#pragma unroll
-                for (int a = 0; a < TM; ++a) {
-                    const int r = wm * (BM / WM) + a * 32 + (lane & 31);
-                    fa[a] = *(const v4i*)(cA + r * BK + ((c ^ swz16<false, BK>(r)) << 4));
-                }
-#pragma unroll
-                for (int b = 0; b < TN; ++b) {
-                    const int r = wn * (BN / WN) + b * 32 + (lane & 31);
-                    fb[b] = *(const v4i*)(cB + r * BK + ((c ^ swz16<false, BK>(r)) << 4));
-                }
-#pragma unroll
-                for (int a = 0; a < TM; ++a)
-#pragma unroll
-                    for (int b = 0; b < TN; ++b)
-                        acc[a][b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[a], fb[b], acc[a][b], 0, 0, 0);
-            }
-        }
+        read_frags(std::integral_constant<int, 0>(), 0);
+    }
+    for (int s = 0; s < nsteps; s += 2) {
+        body(std::integral_constant<int, 0>(), s);
+        if (s + 1 < nsteps) body(std::integral_constant<int, 1>(), s + 1);
     }
     __syncthreads();
-    gemm_epilogue<BM, BN, WM, WN, MODE>(acc, m0, n0, M, N, epi, smem);
+    if constexpr (KG == 1) {
+        gemm_epilogue<TM, TN, NW, MODE>(acc, m0 + wm * (BM / WM), n0 + wn * (BN / WN), M, N, epi, smem);
+    } else {
+        // The two wave groups hold partial sums of the same tiles: group 0 keeps tile rows
+        // a < TM/2 and sends the rest, group 1 the reverse; one LDS exchange, then each wave
+        // finishes half of the tiles.
+        constexpr int TH = TM / 2;
+        v4i* xbuf = (v4i*)smem;
+        const int send_a = kg == 0 ? TH : 0;
+#pragma unroll
+        for (int a = 0; a < TH; ++a)
+#pragma unroll
+            for (int b = 0; b < TN; ++b)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const v16i& t = acc[send_a + a][b];
+                    xbuf[((wid * TH + a) * TN + b) * 256 + q * 64 + lane] = v4i{t[4 * q], t[4 * q + 1], t[4 * q + 2], t[4 * q + 3]};
+                }
+        __syncthreads();
+        const int partner = (1 - kg) * 4 + wq;
+        const int keep_a = kg == 0 ? 0 : TH;
+        v16i keep[TH][TN];
+#pragma unroll
+        for (int a = 0; a < TH; ++a)
+#pragma unroll
+            for (int b = 0; b < TN; ++b) {
+                keep[a][b] = acc[keep_a + a][b];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const v4i v = xbuf[((partner * TH + a) * TN + b) * 256 + q * 64 + lane];
+                    keep[a][b][4 * q] += v[0];
+                    keep[a][b][4 * q + 1] += v[1];
+                    keep[a][b][4 * q + 2] += v[2];
+                    keep[a][b][4 * q + 3] += v[3];
+                }
+            }
+        __syncthreads();  // exchange buffer is reused by the epilogue's block max
+        gemm_epilogue<TH, TN, NW, MODE>(keep, m0 + wm * (BM / WM) + keep_a * 32, n0 + wn * (BN / WN), M, N, epi, smem);
+    }
 }
 
 // Sum of K-split slabs -> C (+ max|C|).  A block covers 256/G v4i elements with G threads
@@ -727,24 +1063,24 @@ static size_t plan_ws_elems(int M, int N, int k_total, int k_step) {
 template <class LA, class LB, int MODE, bool KT>
 static hipError_t launch_mode(const GemmPlan& p, const LA& la, const LB& lb, int M, int N, int k_total,
                               const Epi& epi, hipStream_t st) {
-    const int k_step = KT ? KT_BK : CPS;
+    const int k_step = KT ? KT_BK : LA::BK / 16;
     const int splits = MODE == EPI_SLAB ? p.splits : 1;
     const int per = MODE == EPI_SLAB ? p.kc_per_split : ((k_total + k_step - 1) / k_step) * k_step;
-#define NITI_LAUNCH(BM_, BN_, WM_, WN_)                                                                          \
+#define NITI_LAUNCH(BM_, BN_, WM_, WN_, NW_)                                                                     \
     do {                                                                                                         \
         const int tm = (M + BM_ - 1) / BM_, tn = (N + BN_ - 1) / BN_;                                            \
         dim3 grid(tm * tn, splits);                                                                              \
-        hipLaunchKernelGGL((gemm_kernel<BM_, BN_, WM_, WN_, LA, LB, MODE, KT>), grid, dim3(256), 0, st, la, lb,   \
-                           M, N, tn, k_total, per, epi);                                                         \
+        hipLaunchKernelGGL((gemm_kernel<BM_, BN_, WM_, WN_, LA, LB, MODE, KT, NW_>), grid, dim3(NW_ * 64), 0, st, \
+                           la, lb, M, N, tn, k_total, per, epi);                                                 \
     } while (0)
     if (p.bn == 64 && p.bm == 64)
-        NITI_LAUNCH(64, 64, 2, 2);
+        NITI_LAUNCH(64, 64, 2, 2, 4);
     else if (p.bn == 64)
-        NITI_LAUNCH(128, 64, 2, 2);
+        NITI_LAUNCH(128, 64, 2, 2, 4);
     else if (p.bm == 64)
-        NITI_LAUNCH(64, 128, 1, 4);
+        NITI_LAUNCH(64, 128, 1, 4, 4);
     else
-        NITI_LAUNCH(128, 128, 2, 2);
+        NITI_LAUNCH(128, 128, 2, 2, 8);
 #undef NITI_LAUNCH
     return hipGetLastError();
 }
@@ -765,7 +1101,7 @@ template <class LA, class LB, bool KT = false>
 static hipError_t gemm_acc(const LA& la, const LB& lb, int M, int N, int kc_total, int32_t* C, uint32_t* amax,
                            int32_t* ws, size_t ws_elems, hipStream_t st) {
     if (M <= 0 || N <= 0) return hipSuccess;
-    const int k_step = KT ? KT_BK : CPS;
+    const int k_step = KT ? KT_BK : LA::BK / 16;
     GemmPlan p = plan_gemm(M, N, kc_total, k_step, 1 << 30, false, ws ? ws_elems : 0);
     Epi e;
     if (p.strat == STRAT_SLAB) {
@@ -787,7 +1123,7 @@ static hipError_t gemm_acc(const LA& la, const LB& lb, int M, int N, int kc_tota
 template <class LA, class LB>
 static hipError_t act_phase1(const LA& la, const LB& lb, int M, int N, int kc_total, int32_t* acc, uint32_t* amax,
                              int32_t* ws, size_t ws_elems, hipStream_t st) {
-    GemmPlan p = plan_gemm(M, N, kc_total, CPS, kc_total * 16, true, ws ? ws_elems : 0);
+    GemmPlan p = plan_gemm(M, N, kc_total, LA::BK / 16, kc_total * 16, true, ws ? ws_elems : 0);
     if (p.strat == STRAT_RECOMPUTE) {
         Epi e;
         e.amax = amax;
@@ -799,7 +1135,7 @@ static hipError_t act_phase1(const LA& la, const LB& lb, int M, int N, int kc_to
 template <class LA, class LB>
 static hipError_t act_phase2(const LA& la, const LB& lb, int M, int N, int kc_total, const int32_t* acc,
                              const uint32_t* amax, const ActOut& o, size_t ws_elems, hipStream_t st) {
-    GemmPlan p = plan_gemm(M, N, kc_total, CPS, kc_total * 16, true, ws_elems);
+    GemmPlan p = plan_gemm(M, N, kc_total, LA::BK / 16, kc_total * 16, true, ws_elems);
     if (p.strat == STRAT_RECOMPUTE) {
         Epi e;
         e.amax = const_cast<uint32_t*>(amax);
@@ -827,8 +1163,8 @@ static hipError_t act_phase2(const LA& la, const LB& lb, int M, int N, int kc_to
 }
 
 // ------------------------------------------------------------------------------ per-op wrappers
-static LoadRowMajor rowmajor(const int8_t* p, int64_t ld, int rows, int kc_total) {
-    LoadRowMajor r;
+static RowsK rows_k(const int8_t* p, int64_t ld, int rows, int kc_total) {
+    RowsK r;
     r.p = p;
     r.ld = ld;
     r.rows = rows;
@@ -878,7 +1214,52 @@ static LoadConvDgrad dgrad_loader(const ConvGeom& g, const int8_t* dy) {
     la.bytes = (uint32_t)((int64_t)g.n * la.img);
     return la;
 }
-static void wgrad_operands(const ConvGeom& g, const int8_t* x, const int8_t* dy, KtRows* la, KtIm2col* lb) {
+// Tap-aligned operands (ConvTaps) where the channel padding allows it, else the per-lane loaders.
+template <int BKB>
+static ConvTaps<BKB> conv_taps(const ConvGeom& g, const int8_t* src, bool fwd) {
+    ConvTaps<BKB> t;
+    t.src = src;
+    t.SH = fwd ? g.h : g.oh;
+    t.SW = fwd ? g.w : g.ow;
+    t.CPC = (fwd ? g.cip : g.cop) / 16;
+    t.PH = fwd ? g.oh : g.h;
+    t.PW = fwd ? g.ow : g.w;
+    t.sh = fwd ? g.sh : 1;
+    t.sw = fwd ? g.sw : 1;
+    t.oy_add = fwd ? -g.pt : g.pt;
+    t.ox_add = fwd ? -g.pl : g.pl;
+    t.dh = g.dh;
+    t.dw = g.dw;
+    t.KH = g.kh;
+    t.KW = g.kw;
+    t.M = g.n * t.PH * t.PW;
+    t.sgn = fwd ? 1 : -1;
+    t.img = (uint32_t)((int64_t)t.SH * t.SW * t.CPC * 16);
+    t.bytes = (uint32_t)((int64_t)g.n * t.img);
+    return t;
+}
+// K bytes per step of the forward / input-gradient operand (0 = per-lane loader, 64 bytes)
+static int fwd_taps_bk(const ConvGeom& g) {
+    if (g.kh * g.kw > 32) return 0;
+    return g.cip % 64 == 0 ? 64 : 0;  // 128-byte steps measured slower (one block per CU)
+}
+static int dgrad_taps_bk(const ConvGeom& g) {
+    if (g.kh * g.kw > 32 || g.sh != 1 || g.sw != 1) return 0;
+    return g.cop % 64 == 0 ? 64 : 0;
+}
+template <class F>
+static hipError_t with_fwd_operand(const ConvGeom& g, const int8_t* x, F&& f) {
+    const int bk = fwd_taps_bk(g);
+    if (bk == 64) return f(conv_taps<64>(g, x, true));
+    return f(per_lane<LoadConvFwd, false>(fwd_loader(g, x)));
+}
+template <class F>
+static hipError_t with_dgrad_operand(const ConvGeom& g, const int8_t* dy, F&& f) {
+    const int bk = dgrad_taps_bk(g);
+    if (bk == 64) return f(conv_taps<64>(g, dy, false));
+    return f(per_lane<LoadConvDgrad, false>(dgrad_loader(g, dy)));
+}
+static void wgrad_operands(const ConvGeom& g, const int8_t* x, const int8_t* dy, KtRowsU* la, KtIm2col* lb) {
     const int K = g.n * g.oh * g.ow;
     la->p = dy;
     la->ld = g.cop;
@@ -906,70 +1287,110 @@ static void wgrad_operands(const ConvGeom& g, const int8_t* x, const int8_t* dy,
 }
 
 size_t conv_fwd_workspace(const ConvGeom& g) {
-    return plan_ws_elems(g.n * g.oh * g.ow, g.cop, g.kh * g.kw * g.cip / 16, CPS) * sizeof(int32_t);
+    const int bk = fwd_taps_bk(g) ? fwd_taps_bk(g) : 64;
+    return plan_ws_elems(g.n * g.oh * g.ow, g.cop, g.kh * g.kw * g.cip / 16, bk / 16) * sizeof(int32_t);
 }
 size_t conv_dgrad_workspace(const ConvGeom& g) {
-    return plan_ws_elems(g.n * g.h * g.w, g.cip, g.kh * g.kw * g.cop / 16, CPS) * sizeof(int32_t);
+    const int bk = dgrad_taps_bk(g) ? dgrad_taps_bk(g) : 64;
+    return plan_ws_elems(g.n * g.h * g.w, g.cip, g.kh * g.kw * g.cop / 16, bk / 16) * sizeof(int32_t);
 }
 size_t conv_wgrad_workspace(const ConvGeom& g) {
     return plan_ws_elems(g.c_out, g.kh * g.kw * g.cip, g.n * g.oh * g.ow, KT_BK) * sizeof(int32_t);
 }
-size_t matmul_workspace(int M, int ldc, int k16) { return plan_ws_elems(M, ldc, k16 / 16, CPS) * sizeof(int32_t); }
+size_t matmul_workspace(int M, int ldc, int k16) {
+    return plan_ws_elems(M, ldc, k16 / 16, RowsK::BK / 16) * sizeof(int32_t);
+}
 
 hipError_t conv_fwd_acc(const ConvGeom& g, const int8_t* x, const int8_t* w, int32_t* acc, uint32_t* amax,
                         void* ws, size_t ws_bytes, hipStream_t st) {
-    LoadConvFwd la = fwd_loader(g, x);
-    LoadRowMajor lb = rowmajor(w, (int64_t)g.kh * g.kw * g.cip, g.c_out, la.kc_total);
-    return gemm_acc(la, lb, la.M, g.cop, la.kc_total, acc, amax, (int32_t*)ws, ws_bytes / 4, st);
+    const int kc_total = g.kh * g.kw * g.cip / 16;
+    const RowsK lb = rows_k(w, (int64_t)g.kh * g.kw * g.cip, g.c_out, kc_total);
+    return with_fwd_operand(g, x, [&](const auto& la) {
+        return gemm_acc(la, lb, g.n * g.oh * g.ow, g.cop, kc_total, acc, amax, (int32_t*)ws, ws_bytes / 4, st);
+    });
 }
 
 hipError_t conv_dgrad_acc(const ConvGeom& g, const int8_t* dy, const int8_t* wt, int32_t* acc, uint32_t* amax,
                           void* ws, size_t ws_bytes, hipStream_t st) {
-    LoadConvDgrad la = dgrad_loader(g, dy);
-    LoadRowMajor lb = rowmajor(wt, (int64_t)g.kh * g.kw * g.cop, g.c_in, la.kc_total);
-    return gemm_acc(la, lb, la.M, g.cip, la.kc_total, acc, amax, (int32_t*)ws, ws_bytes / 4, st);
+    const int kc_total = g.kh * g.kw * g.cop / 16;
+    const RowsK lb = rows_k(wt, (int64_t)g.kh * g.kw * g.cop, g.c_in, kc_total);
+    return with_dgrad_operand(g, dy, [&](const auto& la) {
+        return gemm_acc(la, lb, g.n * g.h * g.w, g.cip, kc_total, acc, amax, (int32_t*)ws, ws_bytes / 4, st);
+    });
 }
 
 hipError_t conv_wgrad_acc(const ConvGeom& g, const int8_t* x, const int8_t* dy, int32_t* acc, uint32_t* amax,
                           void* ws, size_t ws_bytes, hipStream_t st) {
-    KtRows la;
-    KtIm2col lb;
-    wgrad_operands(g, x, dy, &la, &lb);
-    return gemm_acc<KtRows, KtIm2col, true>(la, lb, g.c_out, lb.ncols, lb.K, acc, amax, (int32_t*)ws, ws_bytes / 4,
-                                            st);
+    KtRowsU la;
+    KtIm2col lg;
+    wgrad_operands(g, x, dy, &la, &lg);
+    const int ohw = g.oh * g.ow;
+    const bool rows_mode = ohw % KT_BK == 0 && KT_BK % g.ow == 0;
+    if (rows_mode || KT_BK % ohw == 0) {
+        KtIm2colU lb;
+        lb.x = x;
+        lb.bytes = lg.bytes;
+        lb.H = g.h;
+        lb.W = g.w;
+        lb.OH = g.oh;
+        lb.OW = g.ow;
+        lb.CIP = g.cip;
+        lb.KW = g.kw;
+        lb.sh = g.sh;
+        lb.sw = g.sw;
+        lb.pt = g.pt;
+        lb.pl = g.pl;
+        lb.dh = g.dh;
+        lb.dw = g.dw;
+        lb.ncols = lg.ncols;
+        lb.K = lg.K;
+        lb.rows_mode = rows_mode;
+        return gemm_acc<KtRowsU, KtIm2colU, true>(la, lb, g.c_out, lg.ncols, lg.K, acc, amax, (int32_t*)ws,
+                                                  ws_bytes / 4, st);
+    }
+    return gemm_acc<KtRowsU, PerLane<KtIm2col, true>, true>(la, per_lane<KtIm2col, true>(lg), g.c_out, lg.ncols, lg.K,
+                                                            acc, amax, (int32_t*)ws, ws_bytes / 4, st);
 }
 
 hipError_t matmul_acc(int M, int O, int k16, const int8_t* B, int64_t ldb, const int8_t* A, int64_t lda, int32_t* acc,
                       int64_t ldc, uint32_t* amax, void* ws, size_t ws_bytes, hipStream_t st) {
     const int kc_total = k16 / 16;
-    LoadRowMajor la = rowmajor(B, ldb, M, kc_total);
-    LoadRowMajor lb = rowmajor(A, lda, O, kc_total);  // rows >= O read as zero, so columns O..ldc are 0
+    const RowsK la = rows_k(B, ldb, M, kc_total);
+    const RowsK lb = rows_k(A, lda, O, kc_total);  // rows >= O read as zero, so columns O..ldc are 0
     return gemm_acc(la, lb, M, (int)ldc, kc_total, acc, amax, (int32_t*)ws, ws_bytes / 4, st);
 }
 
 hipError_t conv_fwd_phase1(const ConvGeom& g, const int8_t* x, const int8_t* w, int32_t* acc, uint32_t* amax,
                            void* ws, size_t ws_bytes, hipStream_t st) {
-    LoadConvFwd la = fwd_loader(g, x);
-    LoadRowMajor lb = rowmajor(w, (int64_t)g.kh * g.kw * g.cip, g.c_out, la.kc_total);
-    return act_phase1(la, lb, la.M, g.cop, la.kc_total, acc, amax, (int32_t*)ws, ws_bytes / 4, st);
+    const int kc_total = g.kh * g.kw * g.cip / 16;
+    const RowsK lb = rows_k(w, (int64_t)g.kh * g.kw * g.cip, g.c_out, kc_total);
+    return with_fwd_operand(g, x, [&](const auto& la) {
+        return act_phase1(la, lb, g.n * g.oh * g.ow, g.cop, kc_total, acc, amax, (int32_t*)ws, ws_bytes / 4, st);
+    });
 }
 hipError_t conv_fwd_phase2(const ConvGeom& g, const int8_t* x, const int8_t* w, const int32_t* acc,
                            const uint32_t* amax, const ActOut& o, size_t ws_bytes, hipStream_t st) {
-    LoadConvFwd la = fwd_loader(g, x);
-    LoadRowMajor lb = rowmajor(w, (int64_t)g.kh * g.kw * g.cip, g.c_out, la.kc_total);
-    return act_phase2(la, lb, la.M, g.cop, la.kc_total, acc, amax, o, ws_bytes / 4, st);
+    const int kc_total = g.kh * g.kw * g.cip / 16;
+    const RowsK lb = rows_k(w, (int64_t)g.kh * g.kw * g.cip, g.c_out, kc_total);
+    return with_fwd_operand(g, x, [&](const auto& la) {
+        return act_phase2(la, lb, g.n * g.oh * g.ow, g.cop, kc_total, acc, amax, o, ws_bytes / 4, st);
+    });
 }
 hipError_t conv_dgrad_phase1(const ConvGeom& g, const int8_t* dy, const int8_t* wt, int32_t* acc, uint32_t* amax,
                              void* ws, size_t ws_bytes, hipStream_t st) {
-    LoadConvDgrad la = dgrad_loader(g, dy);
-    LoadRowMajor lb = rowmajor(wt, (int64_t)g.kh * g.kw * g.cop, g.c_in, la.kc_total);
-    return act_phase1(la, lb, la.M, g.cip, la.kc_total, acc, amax, (int32_t*)ws, ws_bytes / 4, st);
+    const int kc_total = g.kh * g.kw * g.cop / 16;
+    const RowsK lb = rows_k(wt, (int64_t)g.kh * g.kw * g.cop, g.c_in, kc_total);
+    return with_dgrad_operand(g, dy, [&](const auto& la) {
+        return act_phase1(la, lb, g.n * g.h * g.w, g.cip, kc_total, acc, amax, (int32_t*)ws, ws_bytes / 4, st);
+    });
 }
 hipError_t conv_dgrad_phase2(const ConvGeom& g, const int8_t* dy, const int8_t* wt, const int32_t* acc,
                              const uint32_t* amax, const ActOut& o, size_t ws_bytes, hipStream_t st) {
-    LoadConvDgrad la = dgrad_loader(g, dy);
-    LoadRowMajor lb = rowmajor(wt, (int64_t)g.kh * g.kw * g.cop, g.c_in, la.kc_total);
-    return act_phase2(la, lb, la.M, g.cip, la.kc_total, acc, amax, o, ws_bytes / 4, st);
+    const int kc_total = g.kh * g.kw * g.cop / 16;
+    const RowsK lb = rows_k(wt, (int64_t)g.kh * g.kw * g.cop, g.c_in, kc_total);
+    return with_dgrad_operand(g, dy, [&](const auto& la) {
+        return act_phase2(la, lb, g.n * g.h * g.w, g.cip, kc_total, acc, amax, o, ws_bytes / 4, st);
+    });
 }
 
 // =====================================================================================

@@ -9,7 +9,8 @@ import os
 import re
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_lib", "libniti_hip.so")
+# NITI_HIP_LIB selects another build of the same library (diagnostic variants under tools/)
+LIB_PATH = os.environ.get("NITI_HIP_LIB") or os.path.join(_HERE, "_lib", "libniti_hip.so")
 HEADER = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "include", "niti_hip.h")
 
 # MNN::ErrorCode names (include/MNN/ErrorCode.hpp:17-30)
