@@ -64,7 +64,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=256, help="images per GPU per step")
     ap.add_argument("--arch", default="vgg11", choices=["vgg11", "lenet"])
-    ap.add_argument("--cpu-sample", type=int, default=32, help="images in the CPU baseline sample (0 = skip)")
+    ap.add_argument("--cpu-sample", type=int, default=128, help="images in the CPU baseline sample (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=4, help="reference default: MnistUtils.cpp:43")
     ap.add_argument("--probe-layer", type=int, default=3, help="layer whose GEMM is timed for the roofline")
     ap.add_argument("--probe-phase", type=int, default=2, help="0 fwd, 1 input grad, 2 weight grad")

@@ -232,7 +232,7 @@ __device__ __forceinline__ void publish_max(uint32_t* amax, uint32_t m) {
 //   EPI_AMAX     max|C| only                          (first pass of the recompute strategy)
 //   EPI_REQUANT  reads the max word, applies the NITI forward shift rule, writes int8
 //                (+ fused relu / relu-grad mask, + exponent)   (second pass)
-//   EPI_SLAB     int32 partial sums of one K split -> slab[blockIdx.y] (reduced later)
+//   EPI_SLAB     int32 partial sums of one K split -> slab[split] (reduced later)
 // =====================================================================================
 // K bytes per step (KT = false) is the A loader's BK: 128 (full 128-byte lines per row and
 // step) where the operand allows it, else 64.
@@ -265,7 +265,7 @@ __device__ __forceinline__ int xcd_remap(int b, int nwg) {
 // col = lane&31.  `smem` is reused for the block max (every LDS read finished at the last barrier).
 template <int TM, int TN, int NW, int MODE>
 __device__ __forceinline__ void gemm_epilogue(v16i (&acc)[TM][TN], int r0, int c0, int M, int N, const Epi& epi,
-                                              int8_t* smem) {
+                                              int8_t* smem, int split) {
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wid = tid >> 6;
@@ -282,7 +282,7 @@ __device__ __forceinline__ void gemm_epilogue(v16i (&acc)[TM][TN], int r0, int c
             *epi.exp_out = (int8_t)(ein + ws + inc);
         }
     }
-    int32_t* Cs = MODE == EPI_SLAB ? epi.C + (int64_t)blockIdx.y * epi.slab_stride : epi.C;
+    int32_t* Cs = MODE == EPI_SLAB ? epi.C + (int64_t)split * epi.slab_stride : epi.C;
     uint32_t lmax = 0;
 #pragma unroll
     for (int a = 0; a < TM; ++a)
@@ -773,10 +773,12 @@ __global__ void __launch_bounds__(NW * 64) gemm_kernel(LA la, LB lb, int M, int 
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: LDS bases stay scalar
     const int kg = wid >> 2, wq = wid & 3;
     const int wm = wq / WN, wn = wq % WN;
-    const int tile = xcd_remap(blockIdx.x, gridDim.x);
+    // XCD-aware tile order inside each K split.  (A split-major order over the whole grid, which
+    // keeps one K range per XCD and cuts the weight gradient's HBM fetch ~8x, measured slower.)
+    const int split = blockIdx.y, tile = xcd_remap(blockIdx.x, gridDim.x);
     const int tm_ = tile / tiles_n, tn_ = tile % tiles_n;
     const int m0 = tm_ * BM, n0 = tn_ * BN;
-    const int k_begin = blockIdx.y * k_per_split;
+    const int k_begin = split * k_per_split;
     const int k_end = min(k_total, k_begin + k_per_split);
     const int nsteps = k_end > k_begin ? (k_end - k_begin + K_STEP - 1) / K_STEP : 0;
 
@@ -929,7 +931,7 @@ __global__ void __launch_bounds__(NW * 64) gemm_kernel(LA la, LB lb, int M, int 
     }
     __syncthreads();
     if constexpr (KG == 1) {
-        gemm_epilogue<TM, TN, NW, MODE>(acc, m0 + wm * (BM / WM), n0 + wn * (BN / WN), M, N, epi, smem);
+        gemm_epilogue<TM, TN, NW, MODE>(acc, m0 + wm * (BM / WM), n0 + wn * (BN / WN), M, N, epi, smem, split);
     } else {
         // The two wave groups hold partial sums of the same tiles: group 0 keeps tile rows
         // a < TM/2 and sends the rest, group 1 the reverse; one LDS exchange, then each wave
@@ -965,7 +967,8 @@ __global__ void __launch_bounds__(NW * 64) gemm_kernel(LA la, LB lb, int M, int 
                 }
             }
         __syncthreads();  // exchange buffer is reused by the epilogue's block max
-        gemm_epilogue<TH, TN, NW, MODE>(keep, m0 + wm * (BM / WM) + keep_a * 32, n0 + wn * (BN / WN), M, N, epi, smem);
+        gemm_epilogue<TH, TN, NW, MODE>(keep, m0 + wm * (BM / WM) + keep_a * 32, n0 + wn * (BN / WN), M, N, epi, smem,
+                                        split);
     }
 }
 
