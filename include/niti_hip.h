@@ -114,6 +114,13 @@ void niti_destroy_execution(niti_execution_t e);
 size_t niti_execution_workspace_bytes(niti_execution_t e);
 
 /* ============================ 2. native split primitives ============================== */
+/* A range estimate (max|acc| of one tensor, NITI_RangeEstimate's input, CommonOptFunction.cpp:
+ * 1565-1576) is carried in a buffer of NITI_MAX_WORDS uint32 words that the caller zeroes before
+ * the producing call.  Producers atomically max into one of 64 slots (one per 128-byte line,
+ * word 32*i), spreading the atomics; the value is the max over the slots, which is what every
+ * consumer below reads.  An all-reduce (MAX) over the whole buffer of every rank gives the
+ * global range in data-parallel exact mode. */
+#define NITI_MAX_WORDS 2048
 /* Native layouts (padded lanes zero): NHWC16 [N][H][W][round16(C)]; CHWN16 [round16(C)][H][W]
  * [round16(N)]; OHWI16 weights [Co][KH][KW][round16(Ci)]; IHWO16 [Ci][KH][KW][round16(Co)]. */
 typedef struct niti_geom {
@@ -129,7 +136,7 @@ int niti_geom_finalize(niti_geom* g);
  * (or NULL) is allowed: the op then runs unsplit. */
 int niti_conv_workspace_bytes(const niti_geom* g, int op, size_t* bytes);
 int niti_matmul_workspace_bytes(int m, int ldc, int k16, size_t* bytes);
-/* acc[n*oh*ow][cop] int32 = conv(x, w); if amax: *amax = max(*amax, max|acc|) (caller zeroes it) */
+/* acc[n*oh*ow][cop] int32 = conv(x, w); if amax (NITI_MAX_WORDS words): range max-ed in */
 int niti_conv_fwd_acc(const niti_geom* g, const int8_t* x_nhwc16, const int8_t* w_ohwi16, int32_t* acc,
                       uint32_t* amax, void* workspace, size_t workspace_bytes, void* stream);
 /* acc[n*h*w][cip] int32 = input gradient of the conv for dy (NHWC16) and w^T (IHWO16) */

@@ -212,7 +212,7 @@ class ConvInt8Execution : public Execution {
         x16_ = (int8_t*)ws_.alloc((size_t)g_.n * g_.h * g_.w * g_.cip);
         w16_ = (int8_t*)ws_.alloc((size_t)g_.c_out * g_.kh * g_.kw * g_.cip);
         acc_ = (int32_t*)ws_.alloc((size_t)g_.n * g_.oh * g_.ow * g_.cop * 4);
-        amax_ = (uint32_t*)ws_.alloc(16);
+        amax_ = (uint32_t*)ws_.alloc(MAX_BYTES);
         slab_bytes_ = conv_fwd_workspace(g_);
         slab_ = slab_bytes_ ? ws_.alloc(slab_bytes_) : nullptr;
         if (slab_bytes_ && !slab_) return NITI_OUT_OF_MEMORY;
@@ -223,7 +223,7 @@ class ConvInt8Execution : public Execution {
         NITI_TRY(c4_to_nhwc16((const int8_t*)in[0].data, g_.n, g_.c_in, g_.h * g_.w, g_.cip, x16_, st));
         // reorderWeight every call: weights change each step (NITI_Conv_Int8.cpp:177)
         NITI_TRY(oihw_to_ohwi16((const int8_t*)in[1].data, g_.c_out, g_.c_in, g_.kh * g_.kw, g_.cip, w16_, st));
-        NITI_TRY(hipMemsetAsync(amax_, 0, 4, st));
+        NITI_TRY(hipMemsetAsync(amax_, 0, MAX_BYTES, st));
         NITI_TRY(conv_fwd_acc(g_, x16_, w16_, acc_, amax_, slab_, slab_bytes_, st));
         ActRequant r;
         r.acc = acc_;
@@ -273,7 +273,7 @@ class DeconvInt8Execution : public Execution {
         x16_ = (int8_t*)ws_.alloc((size_t)g_.n * g_.h * g_.w * g_.cip);
         w16_ = (int8_t*)ws_.alloc((size_t)g_.c_out * g_.kh * g_.kw * g_.cip);
         acc_ = (int32_t*)ws_.alloc((size_t)g_.n * g_.oh * g_.ow * g_.cop * 4);
-        amax_ = (uint32_t*)ws_.alloc(16);
+        amax_ = (uint32_t*)ws_.alloc(MAX_BYTES);
         slab_bytes_ = conv_fwd_workspace(g_);
         slab_ = slab_bytes_ ? ws_.alloc(slab_bytes_) : nullptr;
         if (slab_bytes_ && !slab_) return NITI_OUT_OF_MEMORY;
@@ -283,7 +283,7 @@ class DeconvInt8Execution : public Execution {
         if (!acc_) return NITI_NO_EXECUTION;
         NITI_TRY(c4_to_nhwc16((const int8_t*)in[0].data, g_.n, g_.c_in, g_.h * g_.w, g_.cip, x16_, st));
         NITI_TRY(oihw_to_ohwi16((const int8_t*)in[1].data, g_.c_out, g_.c_in, g_.kh * g_.kw, g_.cip, w16_, st, true));
-        NITI_TRY(hipMemsetAsync(amax_, 0, 4, st));
+        NITI_TRY(hipMemsetAsync(amax_, 0, MAX_BYTES, st));
         NITI_TRY(conv_fwd_acc(g_, x16_, w16_, acc_, amax_, slab_, slab_bytes_, st));
         ActRequant r;
         r.acc = acc_;
@@ -350,7 +350,7 @@ class GradientConvInt8Execution : public Execution {
         dyT_ = (int8_t*)ws_.alloc((size_t)g_.n * g_.oh * g_.ow * g_.cop);
         acc_ = (int32_t*)ws_.alloc((size_t)g_.c_out * g_.kh * g_.kw * g_.cip * 4);
         g8_ = (int8_t*)ws_.alloc((size_t)g_.c_out * g_.kh * g_.kw * g_.cip);
-        amax_ = (uint32_t*)ws_.alloc(16);
+        amax_ = (uint32_t*)ws_.alloc(MAX_BYTES);
         slab_bytes_ = conv_wgrad_workspace(g_);
         slab_ = slab_bytes_ ? ws_.alloc(slab_bytes_) : nullptr;
         if (slab_bytes_ && !slab_) return NITI_OUT_OF_MEMORY;
@@ -364,7 +364,7 @@ class GradientConvInt8Execution : public Execution {
         NITI_TRY(launch_map((int64_t)g_.n * ohw * g_.cop,
                             NchwTransposedToNhwc16{(const int8_t*)in[1].data, g_.n, g_.c_out, ohw, g_.cop, dyT_}, st));
         const int64_t nacc = (int64_t)g_.c_out * kk * g_.cip;
-        NITI_TRY(hipMemsetAsync(amax_, 0, 4, st));
+        NITI_TRY(hipMemsetAsync(amax_, 0, MAX_BYTES, st));
         NITI_TRY(conv_wgrad_acc(g_, xT_, dyT_, acc_, amax_, slab_, slab_bytes_, st));
         NITI_TRY(requant_grad(acc_, nacc, amax_, RULE_WGRAD_BW2, g8_, nullptr, st));
         NITI_TRY(launch_map((int64_t)((g_.c_out + 3) / 4) * g_.c_in * kk * 4,
@@ -402,7 +402,7 @@ class MatmulInt8Execution : public Execution {
         a16_ = (int8_t*)ws_.alloc((size_t)o_ * k16_);
         acc_ = (int32_t*)ws_.alloc((size_t)m_ * ldc_ * 4);
         g8_ = (int8_t*)ws_.alloc((size_t)m_ * ldc_);
-        amax_ = (uint32_t*)ws_.alloc(16);
+        amax_ = (uint32_t*)ws_.alloc(MAX_BYTES);
         slab_bytes_ = matmul_workspace(m_, ldc_, k16_);
         slab_ = slab_bytes_ ? ws_.alloc(slab_bytes_) : nullptr;
         if (slab_bytes_ && !slab_) return NITI_OUT_OF_MEMORY;
@@ -412,7 +412,7 @@ class MatmulInt8Execution : public Execution {
         if (!acc_) return NITI_NO_EXECUTION;
         NITI_TRY(pad_rows((const int8_t*)in[0].data, m_, k_, k16_, b16_, st));
         NITI_TRY(pad_rows((const int8_t*)in[1].data, o_, k_, k16_, a16_, st));
-        NITI_TRY(hipMemsetAsync(amax_, 0, 4, st));
+        NITI_TRY(hipMemsetAsync(amax_, 0, MAX_BYTES, st));
         NITI_TRY(matmul_acc(m_, o_, k16_, b16_, k16_, a16_, k16_, acc_, ldc_, amax_, slab_, slab_bytes_, st));
         NITI_TRY(requant_grad(acc_, (int64_t)m_ * ldc_, amax_, RULE_MATMUL_BW3, g8_, nullptr, st));
         NITI_TRY(launch_map((int64_t)m_ * o_, UnpadRows{g8_, o_, ldc_, (int8_t*)out[0].data}, st));
@@ -452,7 +452,7 @@ class DspMatmulGradientExecution : public Execution {
         dyT_ = (int8_t*)ws_.alloc((size_t)g_.n * g_.oh * g_.ow * g_.cop);
         acc_ = (int32_t*)ws_.alloc((size_t)g_.c_out * kh * kw * g_.cip * 4);
         g8_ = (int8_t*)ws_.alloc((size_t)g_.c_out * kh * kw * g_.cip);
-        amax_ = (uint32_t*)ws_.alloc(16);
+        amax_ = (uint32_t*)ws_.alloc(MAX_BYTES);
         slab_bytes_ = conv_wgrad_workspace(g_);
         slab_ = slab_bytes_ ? ws_.alloc(slab_bytes_) : nullptr;
         if (slab_bytes_ && !slab_) return NITI_OUT_OF_MEMORY;
@@ -464,7 +464,7 @@ class DspMatmulGradientExecution : public Execution {
         NITI_TRY(launch_map((int64_t)g_.n * hw * g_.cip, NhwcToNhwc16{(const int8_t*)in[0].data, g_.c_in, g_.cip, xT_}, st));
         NITI_TRY(launch_map((int64_t)g_.n * ohw * g_.cop, NhwcToNhwc16{(const int8_t*)in[1].data, g_.c_out, g_.cop, dyT_}, st));
         const int64_t nacc = (int64_t)g_.c_out * kk * g_.cip;
-        NITI_TRY(hipMemsetAsync(amax_, 0, 4, st));
+        NITI_TRY(hipMemsetAsync(amax_, 0, MAX_BYTES, st));
         NITI_TRY(conv_wgrad_acc(g_, xT_, dyT_, acc_, amax_, slab_, slab_bytes_, st));
         NITI_TRY(requant_grad(acc_, nacc, amax_, RULE_WGRAD_BW2, g8_, nullptr, st));
         NITI_TRY(launch_map((int64_t)kk * g_.c_in * g_.c_out, Ohwi16ToHwio{g8_, g_.c_out, g_.c_in, kk, g_.cip, (int8_t*)out[0].data}, st));

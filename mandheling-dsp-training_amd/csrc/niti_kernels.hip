@@ -218,8 +218,21 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
 
 // One atomic per workgroup, skipped when the word already holds a larger value (the
 // single max word is otherwise a serialisation point for thousands of workgroups).
+// A range is MAX_SLOTS words on separate 128-byte lines: each block publishes into one slot
+// (spread by block id), so no line sees more than grid/MAX_SLOTS atomics.  With one word,
+// every block of a launch whose blocks all finish together (2048 reduce blocks) read 0 and
+// queued its atomic on the same line: ~25 us of serialised atomics per launch.
 __device__ __forceinline__ void publish_max(uint32_t* amax, uint32_t m) {
-    if (m != 0u && m > __hip_atomic_load(amax, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(amax, m);
+    if (m == 0u) return;
+    const uint32_t slot = (blockIdx.x + blockIdx.y * 13u + blockIdx.z * 7u) & (MAX_SLOTS - 1);
+    uint32_t* w = amax + slot * MAX_SLOT_STRIDE;
+    if (m > __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(w, m);
+}
+// max|acc| of a range: the max over its slots, one slot per lane (call with the whole wave
+// active; read after a kernel boundary or collective)
+__device__ __forceinline__ uint32_t read_max(const uint32_t* amax) {
+    static_assert(MAX_SLOTS == 64, "one slot per lane");
+    return wave_max(amax[(threadIdx.x & 63) * MAX_SLOT_STRIDE]);
 }
 
 // =====================================================================================
@@ -272,7 +285,7 @@ __device__ __forceinline__ void gemm_epilogue(v16i (&acc)[TM][TN], int r0, int c
     int rq_shift = 2;
     bool rq_raw = false;
     if (MODE == EPI_REQUANT) {
-        const int shift = bitwidth_of(*epi.amax) - 7;  // NITI_Conv_Int8.cpp:262-307
+        const int shift = bitwidth_of(read_max(epi.amax)) - 7;  // NITI_Conv_Int8.cpp:262-307
         rq_shift = shift > 1 ? shift : 2;
         rq_raw = shift <= 0;
         if (blockIdx.x == 0 && blockIdx.y == 0 && tid == 0 && epi.exp_out != nullptr) {
@@ -677,7 +690,8 @@ struct KtIm2colU {
 constexpr int LDS_STAGE_BUDGET = 64 * 1024;  // pipeline depth = min(MAX_STAGES, budget / stage bytes)
 constexpr int MAX_STAGES = 4;               // (deeper pipelines measured no faster at one block per CU)
 #ifndef NITI_ABLATE
-#define NITI_ABLATE 0  // diagnostic builds only: 1 = no global->LDS copies, 2 = no MFMA
+#define NITI_ABLATE 0  // diagnostic builds only: 1 = no global->LDS copies, 2 = no MFMA,
+                       // 3 = no copies and no per-step barrier, 4 = no per-step barrier
 #endif
 
 
@@ -807,12 +821,12 @@ __global__ void __launch_bounds__(NW * 64) gemm_kernel(LA la, LB lb, int M, int 
 #pragma unroll
         for (int i = 0; i < A_PW; ++i) {
             const uint32_t vo = la.template fetch<K_STEP>(ia[i], ua);
-            if (NITI_ABLATE != 1) dma16(rA, sa + (wid * A_PW + i) * 1024, vo, soa);
+            if (NITI_ABLATE != 1 && NITI_ABLATE != 3) dma16(rA, sa + (wid * A_PW + i) * 1024, vo, soa);
         }
 #pragma unroll
         for (int i = 0; i < B_PW; ++i) {
             const uint32_t vo = lb.template fetch<K_STEP>(ib[i], ub);
-            if (NITI_ABLATE != 1) dma16(rB, sb + (wid * B_PW + i) * 1024, vo, sob);
+            if (NITI_ABLATE != 1 && NITI_ABLATE != 3) dma16(rB, sb + (wid * B_PW + i) * 1024, vo, sob);
         }
         la.template step<K_STEP>(ua);
         lb.template step<K_STEP>(ub);
@@ -884,7 +898,7 @@ __global__ void __launch_bounds__(NW * 64) gemm_kernel(LA la, LB lb, int M, int 
         constexpr int CUR = decltype(cur_c)::value;
         const bool more = s + 1 < nsteps;
         if (more) wait_steps<LOADS, STAGES - 3>(min(STAGES - 3, nsteps - 2 - s));  // own step s+1 loads landed
-        __builtin_amdgcn_s_barrier();
+        if (NITI_ABLATE < 3) __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         if (s + STAGES - 1 < nsteps) issue((s + STAGES - 1) % STAGES);
         if (more) {
@@ -973,7 +987,7 @@ __global__ void __launch_bounds__(NW * 64) gemm_kernel(LA la, LB lb, int M, int 
 }
 
 // Sum of K-split slabs -> C (+ max|C|).  A block covers 256/G v4i elements with G threads
-// per element, each summing every G-th slab with 4 loads in flight; the G partials meet in
+// per element, each summing every G-th slab with 8 loads in flight; the G partials meet in
 // registers (shfl_xor inside the wave).  Splits are many and outputs small for the weight
 // gradient (e.g. VGG-11 L1: 160 slabs of 9 K elements), so split-level parallelism matters.
 __global__ void splitk_reduce_kernel(const int32_t* __restrict__ slab, int splits, int64_t stride, int64_t n4, int G,
@@ -984,13 +998,17 @@ __global__ void splitk_reduce_kernel(const int32_t* __restrict__ slab, int split
     if (e < n4) {
         const v4i* base = (const v4i*)slab + e;
         const int64_t st4 = stride / 4;
-        int z = g;
-        for (; z + 3 * G < splits; z += 4 * G) {
-            const v4i a0 = base[(int64_t)z * st4], a1 = base[(int64_t)(z + G) * st4];
-            const v4i a2 = base[(int64_t)(z + 2 * G) * st4], a3 = base[(int64_t)(z + 3 * G) * st4];
-            s += (a0 + a1) + (a2 + a3);
+        // up to 8 independent loads in flight per pass (predicated, no dependent chain)
+        for (int z0 = g; z0 < splits; z0 += 8 * G) {
+            v4i v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int z = z0 + j * G;
+                v[j] = z < splits ? __builtin_nontemporal_load(base + (int64_t)z * st4) : v4i{0, 0, 0, 0};
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) s += v[j];
         }
-        for (; z < splits; z += G) s += base[(int64_t)z * st4];
     }
     for (int o = G >> 1; o > 0; o >>= 1) {
 #pragma unroll
@@ -1028,6 +1046,15 @@ struct GemmPlan {
 
 // k_total: K extent in the kernel's units (16-byte chunks for KT = false, k rows for
 // KT = true); k_step: units per K step; k_bytes: K in bytes (recompute threshold).
+// Distance between K-split slabs: an odd number of 4 KiB pages, so the same offset in every
+// slab falls in a different HBM channel (a power-of-two stride such as 8 MiB put all S reads
+// of one output element on one channel: the 3-slab reduces ran at ~1 TB/s).
+static size_t slab_stride_elems(int M, int N) {
+    size_t pages = ((size_t)M * N * 4 + 4095) / 4096;
+    if ((pages & 1) == 0) ++pages;
+    return pages * 1024;
+}
+
 static GemmPlan plan_gemm(int M, int N, int k_total, int k_step, int k_bytes, bool recompute_ok, size_t ws_elems) {
     GemmPlan p;
     p.bn = N <= 64 ? 64 : 128;
@@ -1045,7 +1072,7 @@ static GemmPlan plan_gemm(int M, int N, int k_total, int k_step, int k_bytes, bo
     int s = (320 + p.tiles - 1) / p.tiles;
     const int max_s = steps / 4;
     if (s > max_s) s = max_s;
-    const size_t slab = (size_t)M * N;
+    const size_t slab = slab_stride_elems(M, N);
     while (s > 1 && (size_t)s * slab > ws_elems) --s;
     if (s < 2) {
         p.strat = recompute ? STRAT_RECOMPUTE : STRAT_STORE;
@@ -1060,7 +1087,7 @@ static GemmPlan plan_gemm(int M, int N, int k_total, int k_step, int k_bytes, bo
 
 static size_t plan_ws_elems(int M, int N, int k_total, int k_step) {
     GemmPlan p = plan_gemm(M, N, k_total, k_step, 1 << 30, false, (size_t)-1);
-    return p.strat == STRAT_SLAB ? (size_t)p.splits * M * N : 0;
+    return p.strat == STRAT_SLAB ? (size_t)p.splits * slab_stride_elems(M, N) : 0;
 }
 
 template <class LA, class LB, int MODE, bool KT>
@@ -1088,13 +1115,13 @@ static hipError_t launch_mode(const GemmPlan& p, const LA& la, const LB& lb, int
     return hipGetLastError();
 }
 
-static hipError_t splitk_reduce(const GemmPlan& p, const int32_t* slab, int64_t n, int32_t* C, uint32_t* amax,
-                                hipStream_t st) {
+static hipError_t splitk_reduce(const GemmPlan& p, const int32_t* slab, int64_t n, int64_t stride, int32_t* C,
+                                uint32_t* amax, hipStream_t st) {
     const int64_t n4 = n / 4;
     int G = 1;  // split-level parallelism only where the output alone cannot fill the GPU
     while (G < 16 && G * 2 <= p.splits && n4 * G < 131072) G <<= 1;
     const int64_t blocks = (n4 + (256 / G) - 1) / (256 / G);
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, st, slab, p.splits, n, n4, G, C,
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, st, slab, p.splits, stride, n4, G, C,
                        amax);
     return hipGetLastError();
 }
@@ -1110,10 +1137,10 @@ static hipError_t gemm_acc(const LA& la, const LB& lb, int M, int N, int kc_tota
     if (p.strat == STRAT_SLAB) {
         e.C = ws;
         e.ldc = N;
-        e.slab_stride = (int64_t)M * N;
+        e.slab_stride = (int64_t)slab_stride_elems(M, N);
         hipError_t r = launch_mode<LA, LB, EPI_SLAB, KT>(p, la, lb, M, N, kc_total, e, st);
         if (r != hipSuccess) return r;
-        return splitk_reduce(p, ws, (int64_t)M * N, C, amax, st);
+        return splitk_reduce(p, ws, (int64_t)M * N, e.slab_stride, C, amax, st);
     }
     e.C = C;
     e.ldc = N;
@@ -1438,7 +1465,7 @@ hipError_t absmax_i32(const int32_t* a, int64_t n, uint32_t* amax, hipStream_t s
 
 // forward / deconv rule, NITI_Conv_Int8.cpp:262-307: shift>1 PSTO(shift); ==1 PSTO(2); else raw cast
 __global__ void requant_act_kernel(ActRequant r) {
-    const int bw = bitwidth_of(*r.amax);
+    const int bw = bitwidth_of(read_max(r.amax));
     const int shift = bw - 7;
     const int s = shift > 1 ? shift : 2;
     const bool raw = shift <= 0;
@@ -1494,7 +1521,7 @@ hipError_t requant_act(const ActRequant& r, hipStream_t st) {
 
 __global__ void requant_grad_kernel(const int32_t* __restrict__ acc, int64_t n, const uint32_t* __restrict__ amax,
                                     int rule, int8_t* __restrict__ g_out, int8_t* __restrict__ w) {
-    const int bw = bitwidth_of(*amax);
+    const int bw = bitwidth_of(read_max(amax));
     const int s = bw - rule;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         const int32_t g = bw == 0 ? 0 : psto_any(acc[i], s);
@@ -1521,7 +1548,7 @@ __global__ void sgd_update_kernel(const int32_t* __restrict__ acc, const uint32_
     __shared__ int8_t T[64][64 + 4];
     const int co0 = blockIdx.y * 64, ci0 = blockIdx.x * 64, k = blockIdx.z;
     const int t = threadIdx.x;
-    const int bw = bitwidth_of(*amax);
+    const int bw = bitwidth_of(read_max(amax));
     const int sh = bw - rule;
     {
         const int r = t >> 2, c = (t & 3) * 16;

@@ -18,6 +18,15 @@ namespace niti {
 
 inline int round_up(int x, int m) { return (x + m - 1) / m * m; }
 
+// A range estimate (max|acc| of one tensor) is kept in MAX_SLOTS words, one per 128-byte
+// line (MAX_WORDS words in all, zeroed before the producing launch); publishers atomically
+// max into one slot each, readers take the max over the slots (NITI_MAX_WORDS in
+// include/niti_hip.h).  Atomics serialise per cache line, so the slots must not share one.
+constexpr int MAX_SLOTS = 64;
+constexpr int MAX_SLOT_STRIDE = 32;  // words (128 bytes)
+constexpr int MAX_WORDS = MAX_SLOTS * MAX_SLOT_STRIDE;
+constexpr size_t MAX_BYTES = MAX_WORDS * sizeof(uint32_t);
+
 struct ConvGeom {
     int n, c_in, h, w;
     int c_out, kh, kw;

@@ -87,8 +87,9 @@ struct Model {
     int32_t* acc = nullptr; // shared fwd / dgrad accumulator
     void* slab = nullptr;   // split-K slabs (shared, sequential on the stream)
     size_t slab_bytes = 0;
-    uint32_t* amax = nullptr;
+    uint32_t* amax = nullptr;  // 3 ranges per layer (forward, input gradient, weight gradient)
     size_t amax_bytes = 0;
+    uint32_t* rng(int layer, int which) { return amax + (size_t)(3 * layer + which) * MAX_WORDS; }
     ncclComm_t comm = nullptr;
     int world = 1, rank = 0, exact = 1;
     // hipGraph of one step
@@ -217,7 +218,7 @@ int Model::build(int arch_, int batch_) {
         slab = ws.alloc(slab_bytes);
         if (!slab) return NITI_OUT_OF_MEMORY;
     }
-    amax_bytes = (size_t)round_up(3 * nl, 4) * 4;
+    amax_bytes = (size_t)3 * nl * MAX_BYTES;
     amax = (uint32_t*)ws.alloc(amax_bytes);
     if (!x0 || !exp0 || !acc || !amax) return NITI_OUT_OF_MEMORY;
     if (hipMemset(x0, 0, (size_t)n * in_h * in_w * round_up(in_c, 16)) != hipSuccess) return NITI_NO_EXECUTION;
@@ -245,15 +246,15 @@ int Model::step(const int8_t* x_nchw, int exp_in, const int32_t* labels, hipStre
         Layer& l = L[i];
         const ConvGeom& g = l.g;
         probe(i, 0, true, st);
-        MTRY(conv_fwd_phase1(g, l.in, l.w, acc, amax + 3 * i, slab, slab_bytes, st));
-        if (dp && exact) CTRY(ncclAllReduce(amax + 3 * i, amax + 3 * i, 1, ncclUint32, ncclMax, comm, st));
+        MTRY(conv_fwd_phase1(g, l.in, l.w, acc, rng(i, 0), slab, slab_bytes, st));
+        if (dp && exact) CTRY(ncclAllReduce(rng(i, 0), rng(i, 0), MAX_WORDS, ncclUint32, ncclMax, comm, st));
         ActOut o;
         o.out = l.r;
         o.relu = l.relu;
         o.exp_in = i == 0 ? exp0 : L[i - 1].exp;
         o.wscale = l.ws_dev;
         o.exp_out = l.exp;
-        MTRY(conv_fwd_phase2(g, l.in, l.w, acc, amax + 3 * i, o, slab_bytes, st));
+        MTRY(conv_fwd_phase2(g, l.in, l.w, acc, rng(i, 0), o, slab_bytes, st));
         probe(i, 0, false, st);
         if (l.pool) MTRY(maxpool_nhwc16(l.r, n, g.oh, g.ow, g.cop, 2, 2, 0, l.p, l.ph, l.pw, st));
         if (l.flatten) {
@@ -272,22 +273,22 @@ int Model::step(const int8_t* x_nchw, int exp_in, const int32_t* labels, hipStre
         const ConvGeom& g = l.g;
         const int64_t we = l.w_elems();
         probe(i, 2, true, st);
-        MTRY(conv_wgrad_acc(g, l.in, l.dy, l.dwacc, dp ? nullptr : amax + 3 * i + 2, slab, slab_bytes, st));
+        MTRY(conv_wgrad_acc(g, l.in, l.dy, l.dwacc, dp ? nullptr : rng(i, 2), slab, slab_bytes, st));
         probe(i, 2, false, st);
         if (dp) {
             CTRY(ncclAllReduce(l.dwacc, l.dwacc, (size_t)we, ncclInt32, ncclSum, comm, st));
-            MTRY(absmax_i32(l.dwacc, we, amax + 3 * i + 2, st));
+            MTRY(absmax_i32(l.dwacc, we, rng(i, 2), st));
         }
         if (i > 0) {
             Layer& pv = L[i - 1];
             probe(i, 1, true, st);
-            MTRY(conv_dgrad_phase1(g, l.dy, l.wT, acc, amax + 3 * i + 1, slab, slab_bytes, st));
-            if (dp && exact) CTRY(ncclAllReduce(amax + 3 * i + 1, amax + 3 * i + 1, 1, ncclUint32, ncclMax, comm, st));
+            MTRY(conv_dgrad_phase1(g, l.dy, l.wT, acc, rng(i, 1), slab, slab_bytes, st));
+            if (dp && exact) CTRY(ncclAllReduce(rng(i, 1), rng(i, 1), MAX_WORDS, ncclUint32, ncclMax, comm, st));
             const ConvGeom& pg = pv.g;
             ActOut o;
             if (pv.flatten) {
                 o.out = pv.dflat;
-                MTRY(conv_dgrad_phase2(g, l.dy, l.wT, acc, amax + 3 * i + 1, o, slab_bytes, st));
+                MTRY(conv_dgrad_phase2(g, l.dy, l.wT, acc, rng(i, 1), o, slab_bytes, st));
                 probe(i, 1, false, st);
                 const int fc = pg.c_out * pv.ph * pv.pw, ld = round_up(fc, 16);
                 MTRY(launch_map((int64_t)n * pv.ph * pv.pw * pg.cop,
@@ -296,18 +297,18 @@ int Model::step(const int8_t* x_nchw, int exp_in, const int32_t* labels, hipStre
                                               pv.relu, pv.dy, st));
             } else if (pv.pool) {
                 o.out = pv.dtmp;
-                MTRY(conv_dgrad_phase2(g, l.dy, l.wT, acc, amax + 3 * i + 1, o, slab_bytes, st));
+                MTRY(conv_dgrad_phase2(g, l.dy, l.wT, acc, rng(i, 1), o, slab_bytes, st));
                 probe(i, 1, false, st);
                 MTRY(maxpool_relu_grad_nhwc16(pv.r, pv.p, pv.dtmp, n, pg.oh, pg.ow, pg.cop, 2, 2, 0, pv.ph, pv.pw,
                                               pv.relu, pv.dy, st));
             } else {
                 o.relu_mask = pv.relu ? pv.r : nullptr;
                 o.out = pv.dy;
-                MTRY(conv_dgrad_phase2(g, l.dy, l.wT, acc, amax + 3 * i + 1, o, slab_bytes, st));
+                MTRY(conv_dgrad_phase2(g, l.dy, l.wT, acc, rng(i, 1), o, slab_bytes, st));
                 probe(i, 1, false, st);
             }
         }
-        MTRY(sgd_update(l.dwacc, amax + 3 * i + 2, RULE_WGRAD_BW2, g.c_out, g.c_in, g.kh * g.kw, g.cip, g.cop, l.w,
+        MTRY(sgd_update(l.dwacc, rng(i, 2), RULE_WGRAD_BW2, g.c_out, g.c_in, g.kh * g.kw, g.cip, g.cop, l.w,
                         i > 0 ? l.wT : nullptr, l.g8, st));
     }
     return NITI_NO_ERROR;

@@ -192,6 +192,19 @@ def matmul_acc(B16, A16, ldc, amax=None, use_workspace=True, stream=None):
     return acc
 
 
+MAX_WORDS = 2048  # NITI_MAX_WORDS: words per range-estimate buffer (64 slots, one per 128 B)
+
+
+def new_range(device="cuda"):
+    """A zeroed range-estimate buffer (NITI_MAX_WORDS uint32 words, held as int32)."""
+    return torch.zeros(MAX_WORDS, dtype=torch.int32, device=device)
+
+
+def range_max(amax) -> int:
+    """max|acc| recorded in a range buffer: the max over its words."""
+    return int(amax.view(-1, MAX_WORDS).max(dim=1).values.max().item())
+
+
 def absmax(acc, amax, stream=None):
     check(L.lib().niti_absmax_i32(_ptr(acc), acc.numel(), _ptr(amax), _stream(stream)), "absmax")
 

@@ -44,7 +44,7 @@ def dev(T, a, dtype=None):
 
 
 def zeros_u32(T):
-    return T.zeros(4, dtype=T.int32, device="cuda")
+    return T.zeros(2048, dtype=T.int32, device="cuda")  # NITI_MAX_WORDS words per range
 
 
 def i8s(T, v):
@@ -71,7 +71,7 @@ def test_matmul_acc_exact(T, ops, m, o, k, split):
     got = acc.cpu().numpy()
     assert np.array_equal(got[:, :o], want)
     assert not got[:, o:].any()
-    assert int(amax[0].item()) == int(np.abs(want).max())
+    assert ops.range_max(amax) == int(np.abs(want).max())
 
 
 # --------------------------------------------------------------------------- native conv ops
@@ -95,7 +95,7 @@ def test_conv_fwd_native(T, ops, oracle, geo):
     got = acc.cpu().numpy()
     assert np.array_equal(got[:, :co], nchw_to_nhwc_acc(acc_ref))
     assert not got[:, co:].any()
-    assert int(amax[0].item()) == int(np.abs(acc_ref.astype(np.int64)).max())
+    assert ops.range_max(amax) == int(np.abs(acc_ref.astype(np.int64)).max())
     e_out = i8s(T, 0)
     y16 = ops.requant_act(acc, amax, exp_in=i8s(T, -7), wscale=i8s(T, ws), exp_out=e_out)
     y = y16.cpu().numpy()[:, :co].reshape(n, g.oh, g.ow, co).transpose(0, 3, 1, 2)

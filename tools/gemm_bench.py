@@ -45,7 +45,7 @@ def main():
     s = C.c_void_p(torch.cuda.current_stream().cuda_stream)
     n = args.batch
     if args.sweep:
-        amax = torch.zeros(8, dtype=torch.int32, device="cuda")
+        amax = torch.zeros(2048, dtype=torch.int32, device="cuda")
         for (m, o) in ((16384, 256), (32768, 256), (16384, 512)):
             for k in (128, 256, 512, 1024, 2048, 4096, 8192):
                 B = torch.randint(-127, 128, (m, k), dtype=torch.int8, device="cuda")
@@ -61,7 +61,7 @@ def main():
     layers = [(3, 64, 32), (64, 128, 16), (128, 256, 8), (256, 256, 8), (256, 512, 4), (512, 512, 4),
               (512, 512, 2), (512, 512, 2)]
     dev = "cuda"
-    amax = torch.zeros(8, dtype=torch.int32, device=dev)
+    amax = torch.zeros(2048, dtype=torch.int32, device=dev)
     rows = []
     for li, (ci, co, h) in enumerate(layers):
         if args.only and str(li) not in args.only.split(","):
