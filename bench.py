@@ -68,6 +68,7 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=4, help="reference default: MnistUtils.cpp:43")
     ap.add_argument("--probe-layer", type=int, default=3, help="layer whose GEMM is timed for the roofline")
     ap.add_argument("--probe-phase", type=int, default=2, help="0 fwd, 1 input grad, 2 weight grad")
+    ap.add_argument("--graph", action="store_true", help="replay the step as a hipGraph (slower on ROCm 7.2)")
     args = ap.parse_args()
 
     import numpy as np
@@ -87,6 +88,7 @@ def main():
 
     arch = niti_amd.ARCH_VGG11 if args.arch == "vgg11" else niti_amd.ARCH_LENET
     model = NitiModel(arch, args.batch)
+    model.set_graph(args.graph)
     for i, (w, s) in enumerate(synth_weights(model.layers, seed=17)):
         model.set_weight(i, w, s)
     if world > 1:
@@ -99,11 +101,15 @@ def main():
     x = torch.from_numpy(rng.integers(-127, 128, (args.batch, l0["c_in"], l0["h"], l0["w"])).astype(np.int8)).cuda()
     labels = torch.from_numpy(rng.integers(0, 10, args.batch).astype(np.int32)).cuda()
 
+    # The probe (HIP events around one GEMM, on the stream it runs on) is armed before the
+    # warmup: the step is replayed as a hipGraph and arming it re-captures the graph, which
+    # must not happen inside the timed region.  Warmup launches are read and discarded.
+    probe_layer = args.probe_layer if args.probe_layer < len(model.layers) else len(model.layers) - 1
+    model.set_probe(probe_layer, args.probe_phase, args.steps + args.warmup)
     for _ in range(args.warmup):
         model.train_step(x, -3, labels)
     torch.cuda.synchronize()
-    probe_layer = args.probe_layer if args.probe_layer < len(model.layers) else len(model.layers) - 1
-    model.set_probe(probe_layer, args.probe_phase, args.steps)
+    model.probe_read()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()

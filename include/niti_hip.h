@@ -209,6 +209,9 @@ int niti_model_get_tap(niti_model_t m, int layer, int which, int8_t* host, size_
 /* Algorithmic int8 MACs per step (unpadded channels; no zero-dilation taps). */
 int64_t niti_model_step_macs(niti_model_t m);
 
+/* Replay the step as a hipGraph (single device only -- with a communicator attached the step
+ * always runs as direct launches).  Default 0 (direct launches: measured faster on ROCm 7.2). */
+int niti_model_set_graph(niti_model_t m, int enable);
 /* Kernel probe: HIP events on the step's stream around one GEMM launch (layer, phase
  * 0 = forward, 1 = input gradient, 2 = weight gradient) for up to max_launches steps;
  * layer < 0 disables.  probe_read synchronises those events and returns the summed

@@ -109,6 +109,7 @@ def lib():
         "niti_model_get_logits": (ci, [vp, vp, C.POINTER(ci), vp]),
         "niti_model_get_tap": (ci, [vp, ci, ci, vp, C.c_size_t, vp]),
         "niti_model_step_macs": (i64, [vp]),
+        "niti_model_set_graph": (ci, [vp, ci]),
         "niti_model_set_probe": (ci, [vp, ci, ci, ci]),
         "niti_model_probe_read": (ci, [vp, C.POINTER(C.c_double), C.POINTER(ci)]),
         "niti_dp_get_unique_id": (ci, [C.c_char_p]),

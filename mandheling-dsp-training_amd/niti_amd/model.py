@@ -65,6 +65,10 @@ class NitiModel:
                                            _stream(stream)), "get_tap")
         return out
 
+    def set_graph(self, enable: bool):
+        """Replay the step as a hipGraph (default) or launch its kernels directly."""
+        check(self._lib.niti_model_set_graph(self._h, int(enable)), "set_graph")
+
     def set_probe(self, layer: int, phase: int, max_launches: int = 256):
         check(self._lib.niti_model_set_probe(self._h, layer, phase, max_launches), "set_probe")
 

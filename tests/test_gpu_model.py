@@ -18,12 +18,16 @@ def T():
     return torch
 
 
-def _run(T, arch, layers, batch, steps=2, seed=5):
+def _run(T, arch, layers, batch, steps=2, seed=5, graph=False, reuse_buffers=True):
+    """reuse_buffers: new data goes into the same device tensors every step, so with graph=True
+    steps after the first replay the captured graph instead of re-capturing it."""
     import niti_model_ref as R
     from niti_amd.model import NitiModel
     rng = np.random.default_rng(seed)
     W, S = R.init_weights(layers, seed=seed)
     m = NitiModel(arch, batch)
+    m.set_graph(graph)
+    xd = ld = None
     for i, (w, s) in enumerate(zip(W, S)):
         m.set_weight(i, w, s)
     for i in range(len(layers)):
@@ -34,8 +38,12 @@ def _run(T, arch, layers, batch, steps=2, seed=5):
         labels = rng.integers(0, 10, batch).astype(np.int32)
         exp_in = -3
         newW, rec = R.train_step(layers, W, S, x, exp_in, labels)
-        xd = T.from_numpy(x).cuda()
-        ld = T.from_numpy(labels).cuda()
+        if xd is None or not reuse_buffers:
+            xd = T.from_numpy(x).cuda()
+            ld = T.from_numpy(labels).cuda()
+        else:
+            xd.copy_(T.from_numpy(x))
+            ld.copy_(T.from_numpy(labels))
         m.train_step(xd, exp_in, ld)
         logits, e = m.logits()
         assert e == rec["exp"][-1], (step, e, rec["exp"][-1])
@@ -52,6 +60,13 @@ def test_lenet_step_matches_oracle(T):
     import niti_amd
     import niti_model_ref as R
     _run(T, niti_amd.ARCH_LENET, R.lenet_layers(), batch=64)
+
+
+@pytest.mark.parametrize("graph,reuse", [(True, True), (True, False)])
+def test_lenet_step_graph_replay_and_recapture(T, graph, reuse):
+    import niti_amd
+    import niti_model_ref as R
+    _run(T, niti_amd.ARCH_LENET, R.lenet_layers(), batch=16, steps=3, seed=11, graph=graph, reuse_buffers=reuse)
 
 
 def test_vgg11_step_matches_oracle(T):
