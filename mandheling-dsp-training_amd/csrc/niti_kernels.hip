@@ -1167,6 +1167,7 @@ static hipError_t act_phase2(const LA& la, const LB& lb, int M, int N, int kc_to
                              const uint32_t* amax, const ActOut& o, size_t ws_elems, hipStream_t st) {
     GemmPlan p = plan_gemm(M, N, kc_total, LA::BK / 16, kc_total * 16, true, ws_elems);
     if (p.strat == STRAT_RECOMPUTE) {
+        if (o.pool.pool_out != nullptr || o.pool.dx != nullptr) return hipErrorInvalidValue;
         Epi e;
         e.amax = const_cast<uint32_t*>(amax);
         e.out = o.out;
@@ -1189,10 +1190,19 @@ static hipError_t act_phase2(const LA& la, const LB& lb, int M, int N, int kc_to
     r.relu = o.relu;
     r.relu_mask = o.relu_mask;
     r.out_nhwc16 = o.out;
+    r.pool = o.pool;
     return requant_act(r, st);
 }
 
 // ------------------------------------------------------------------------------ per-op wrappers
+bool conv_fwd_phase2_separate(const ConvGeom& g, size_t ws_bytes) {
+    const int kc = g.kh * g.kw * g.cip / 16;  // every forward operand loader steps 64 bytes
+    return plan_gemm(g.n * g.oh * g.ow, g.cop, kc, 64 / 16, kc * 16, true, ws_bytes / 4).strat != STRAT_RECOMPUTE;
+}
+bool conv_dgrad_phase2_separate(const ConvGeom& g, size_t ws_bytes) {
+    const int kc = g.kh * g.kw * g.cop / 16;
+    return plan_gemm(g.n * g.h * g.w, g.cip, kc, 64 / 16, kc * 16, true, ws_bytes / 4).strat != STRAT_RECOMPUTE;
+}
 static RowsK rows_k(const int8_t* p, int64_t ld, int rows, int kc_total) {
     RowsK r;
     r.p = p;
@@ -1464,19 +1474,86 @@ hipError_t absmax_i32(const int32_t* a, int64_t n, uint32_t* amax, hipStream_t s
 }
 
 // forward / deconv rule, NITI_Conv_Int8.cpp:262-307: shift>1 PSTO(shift); ==1 PSTO(2); else raw cast
+// NITI forward shift rule on 16 consecutive channels of one accumulator row
+__device__ __forceinline__ v16c requant16(const int32_t* src, bool raw, int s, int relu) {
+    const v4i* p = (const v4i*)src;
+    v16c q;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const v4i v = p[j];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            int32_t o = raw ? (int32_t)(int8_t)v[e] : psto_any(v[e], s);
+            if (relu && o < 0) o = 0;
+            q[j * 4 + e] = (signed char)o;
+        }
+    }
+    return q;
+}
+
 __global__ void requant_act_kernel(ActRequant r) {
     const int bw = bitwidth_of(read_max(r.amax));
     const int shift = bw - 7;
     const int s = shift > 1 ? shift : 2;
     const bool raw = shift <= 0;
     const int groups = r.ldc / 16;
-    const int64_t total = r.rows * groups;
     if (blockIdx.x == 0 && threadIdx.x == 0 && r.exp_out != nullptr) {
         const int inc = shift > 1 ? shift : (shift == 1 ? 2 : 0);
         const int ein = r.exp_in ? (int)*r.exp_in : 0;
         const int ws = r.wscale ? (int)*r.wscale : 0;
         *r.exp_out = (int8_t)(ein + ws + inc);
     }
+    if (r.pool.pool_out != nullptr || r.pool.dx != nullptr) {
+        // one thread per (pooled pixel, 16-channel group)
+        const int H = r.pool.H, W = r.pool.W, ph = H / 2, pw = W / 2;
+        const int64_t np = r.pool.dx != nullptr ? r.rows : r.rows / 4;  // pooled pixels
+        const int64_t total = np * groups;
+        for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+             t += (int64_t)gridDim.x * blockDim.x) {
+            const int64_t pp = t / groups;
+            const int gi = (int)(t - pp * groups);
+            const int px = (int)(pp % pw);
+            const int64_t rest = pp / pw;
+            const int py = (int)(rest % ph);
+            const int64_t b = rest / ph;
+            const int64_t m0 = (b * H + 2 * py) * W + 2 * px;  // window's first pixel
+            const int64_t win[4] = {m0, m0 + 1, m0 + W, m0 + W + 1};
+            if (r.pool.pool_out != nullptr) {
+                v16c mx;
+#pragma unroll
+                for (int j = 0; j < 16; ++j) mx[j] = (signed char)-128;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const v16c q = requant16(r.acc + win[k] * r.ldc + gi * 16, raw, s, r.relu);
+                    *(v16c*)(r.out_nhwc16 + win[k] * r.ldc + gi * 16) = q;
+#pragma unroll
+                    for (int j = 0; j < 16; ++j) mx[j] = q[j] > mx[j] ? q[j] : mx[j];
+                }
+                *(v16c*)(r.pool.pool_out + pp * r.ldc + gi * 16) = mx;
+            } else {
+                const v16c q = requant16(r.acc + pp * r.ldc + gi * 16, raw, s, 0);
+                if (r.out_nhwc16 != nullptr) *(v16c*)(r.out_nhwc16 + pp * r.ldc + gi * 16) = q;
+                const v16c mv = *(const v16c*)(r.pool.y + pp * r.ldc + gi * 16);
+                unsigned done = 0;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const v16c xv = *(const v16c*)(r.pool.x + win[k] * r.ldc + gi * 16);
+                    v16c o;
+#pragma unroll
+                    for (int j = 0; j < 16; ++j) {
+                        const bool take = !((done >> j) & 1u) && xv[j] >= mv[j];
+                        if (take) done |= 1u << j;
+                        signed char d = take ? q[j] : (signed char)0;
+                        if (r.pool.relu && xv[j] <= 0) d = 0;
+                        o[j] = d;
+                    }
+                    *(v16c*)(r.pool.dx + win[k] * r.ldc + gi * 16) = o;
+                }
+            }
+        }
+        return;
+    }
+    const int64_t total = r.rows * groups;
     for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
         const int64_t m = t / groups;
         const int gi = (int)(t - m * groups);
@@ -1511,6 +1588,14 @@ __global__ void requant_act_kernel(ActRequant r) {
 
 hipError_t requant_act(const ActRequant& r, hipStream_t st) {
     if (r.ldc % 16 != 0 || r.acc == nullptr || r.amax == nullptr) return hipErrorInvalidValue;
+    if (r.pool.pool_out != nullptr || r.pool.dx != nullptr) {
+        if (r.pool.H % 2 || r.pool.W % 2 || r.pool.H <= 0 || r.pool.W <= 0) return hipErrorInvalidValue;
+        if (r.pool.pool_out != nullptr && (r.out_nhwc16 == nullptr || r.rows % ((int64_t)r.pool.H * r.pool.W)))
+            return hipErrorInvalidValue;
+        if (r.pool.dx != nullptr && (r.pool.x == nullptr || r.pool.y == nullptr ||
+                                     r.rows % ((int64_t)(r.pool.H / 2) * (r.pool.W / 2))))
+            return hipErrorInvalidValue;
+    }
     const int64_t total = r.rows * (r.ldc / 16);
     int64_t blocks = (total + 255) / 256;
     if (blocks > 4096) blocks = 4096;
@@ -1542,23 +1627,21 @@ hipError_t requant_grad(const int32_t* acc, int64_t n, const uint32_t* amax, int
 // Fused NITI_SGD step on a 64(co) x 64(ci) tile of one tap: g = gradient rule(acc), w <- clip(w - g)
 // in OHWI16, and the updated weights also written transposed (IHWO16, the input-gradient B
 // operand) through an LDS tile -- the transposed copy never needs a pass of its own.
-__global__ void sgd_update_kernel(const int32_t* __restrict__ acc, const uint32_t* __restrict__ amax, int rule, int co,
-                                  int ci, int kk, int cip, int cop, int8_t* __restrict__ w, int8_t* __restrict__ wT,
-                                  int8_t* __restrict__ g_out) {
-    __shared__ int8_t T[64][64 + 4];
-    const int co0 = blockIdx.y * 64, ci0 = blockIdx.x * 64, k = blockIdx.z;
+// One 64 (co) x 64 (ci) tile of one tap: g = rule(acc, range), w <- clip(w - g, +-127) in OHWI16,
+// the same tile transposed through LDS into IHWO16 (the input-gradient operand), g to g_out.
+__device__ __forceinline__ void sgd_tile(const SgdJob& J, int ci0, int co0, int k, int8_t (*T)[64 + 4]) {
     const int t = threadIdx.x;
-    const int bw = bitwidth_of(read_max(amax));
-    const int sh = bw - rule;
+    const int bw = bitwidth_of(read_max(J.amax));
+    const int sh = bw - J.rule;
     {
         const int r = t >> 2, c = (t & 3) * 16;
         v16c wn;
 #pragma unroll
         for (int j = 0; j < 16; ++j) wn[j] = 0;
-        if (co0 + r < co && ci0 + c < cip) {
-            const int64_t idx = ((int64_t)(co0 + r) * kk + k) * cip + ci0 + c;
-            const v4i* a4 = (const v4i*)(acc + idx);
-            const v16c wo = *(const v16c*)(w + idx);
+        if (co0 + r < J.co && ci0 + c < J.cip) {
+            const int64_t idx = ((int64_t)(co0 + r) * J.kk + k) * J.cip + ci0 + c;
+            const v4i* a4 = (const v4i*)(J.acc + idx);
+            const v16c wo = *(const v16c*)(J.w + idx);
             v16c g;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
@@ -1568,29 +1651,57 @@ __global__ void sgd_update_kernel(const int32_t* __restrict__ acc, const uint32_
             }
 #pragma unroll
             for (int j = 0; j < 16; ++j) wn[j] = (signed char)clip127((int32_t)wo[j] - (int32_t)g[j]);
-            *(v16c*)(w + idx) = wn;
-            if (g_out != nullptr) *(v16c*)(g_out + idx) = g;
+            *(v16c*)(J.w + idx) = wn;
+            if (J.g_out != nullptr) *(v16c*)(J.g_out + idx) = g;
         }
 #pragma unroll
         for (int j = 0; j < 16; ++j) T[r][c + j] = wn[j];
     }
     __syncthreads();
-    if (wT != nullptr) {
+    if (J.wT != nullptr) {
         const int r = t >> 2, c = (t & 3) * 16;  // r: ci within the tile, c: co offset
-        if (ci0 + r < ci && co0 + c < cop) {
+        if (ci0 + r < J.ci && co0 + c < J.cop) {
             v16c o;
 #pragma unroll
             for (int j = 0; j < 16; ++j) o[j] = T[c + j][r];
-            *(v16c*)(wT + ((int64_t)(ci0 + r) * kk + k) * cop + co0 + c) = o;
+            *(v16c*)(J.wT + ((int64_t)(ci0 + r) * J.kk + k) * J.cop + co0 + c) = o;
         }
     }
 }
 
+// Every layer's NITI_SGD update of a step in one launch: block b belongs to the job whose
+// [start, start + tiles) range holds it (the updates are independent; the input gradients
+// that read the old weights have all run by then).
+__global__ void sgd_update_kernel(SgdJobs jobs) {
+    __shared__ int8_t T[64][64 + 4];
+    int b = blockIdx.x, j = 0;
+    while (j + 1 < jobs.n && b >= jobs.start[j + 1]) ++j;
+    const SgdJob& J = jobs.job[j];
+    b -= jobs.start[j];
+    const int tx = (J.cip + 63) / 64, ty = (J.cop + 63) / 64;
+    const int k = b / (tx * ty), rem = b - k * tx * ty;
+    sgd_tile(J, (rem % tx) * 64, (rem / tx) * 64, k, T);
+}
+
+hipError_t sgd_update_many(const SgdJob* jobs, int n, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    if (n > SGD_MAX_JOBS) return hipErrorInvalidValue;
+    SgdJobs J{};
+    J.n = n;
+    int total = 0;
+    for (int i = 0; i < n; ++i) {
+        J.job[i] = jobs[i];
+        J.start[i] = total;
+        total += ((jobs[i].cip + 63) / 64) * ((jobs[i].cop + 63) / 64) * jobs[i].kk;
+    }
+    hipLaunchKernelGGL(sgd_update_kernel, dim3(total), dim3(256), 0, st, J);
+    return hipGetLastError();
+}
+
 hipError_t sgd_update(const int32_t* acc, const uint32_t* amax, int rule, int co, int ci, int kk, int cip, int cop,
                       int8_t* w, int8_t* wT, int8_t* g_out, hipStream_t st) {
-    dim3 grid((cip + 63) / 64, (cop + 63) / 64, kk);
-    hipLaunchKernelGGL(sgd_update_kernel, grid, dim3(256), 0, st, acc, amax, rule, co, ci, kk, cip, cop, w, wT, g_out);
-    return hipGetLastError();
+    SgdJob j{acc, amax, rule, co, ci, kk, cip, cop, w, wT, g_out};
+    return sgd_update_many(&j, 1, st);
 }
 
 // =====================================================================================

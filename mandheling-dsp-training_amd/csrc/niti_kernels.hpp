@@ -69,14 +69,34 @@ hipError_t matmul_acc(int M, int O, int k16, const int8_t* B, int64_t ldb, const
 // tensor-wide max|acc| (either materialising acc, or -- for small K -- computing the max
 // only and recomputing the GEMM in phase 2 with the requantisation in its epilogue).
 // Between the phases a data-parallel run all-reduces *amax (MAX).
+// 2x2 / stride-2 max pool fused into the requantisation (NITI_Maxpool_Int8.cpp:24-72 and its
+// gradient NITI_CPUPoolGrad_Int8.cpp:21-77, first max wins), for images with even H, W:
+//  forward: rows are pixels of [n][H][W]; pool_out [n][H/2][W/2] gets the window max of the
+//           (relu'd) output, which is also written whole to `out`
+//  backward: rows are pooled pixels [n][H/2][W/2]; each requantised value goes to the first
+//           maximum of its window of x (the forward's pre-pool output, max y) in dx [n][H][W],
+//           zero elsewhere and where x <= 0 when relu (NITI_CPUReluGrad_Int8.cpp:28-62)
+struct PoolFuse {
+    int8_t* pool_out = nullptr;
+    const int8_t* x = nullptr;
+    const int8_t* y = nullptr;
+    int8_t* dx = nullptr;
+    int relu = 0;
+    int H = 0, W = 0;  // pre-pool image size
+};
 struct ActOut {
-    int8_t* out = nullptr;             // NHWC16 [rows][ld]
+    int8_t* out = nullptr;             // NHWC16 [rows][ld] (may be null with pool.dx)
     int relu = 0;                      // fused NITI_Relu_Int8
     const int8_t* relu_mask = nullptr; // fused NITI_ReluGrad_Int8 (out = mask > 0 ? q : 0)
     const int8_t* exp_in = nullptr;
     const int8_t* wscale = nullptr;
     int8_t* exp_out = nullptr;
+    PoolFuse pool;                     // only where the phase runs as a separate requant pass
 };
+// whether phase 2 of the forward / input-gradient conv requantises in a separate pass (and so
+// can take ActOut::pool); otherwise it recomputes the GEMM with a requantising epilogue
+bool conv_fwd_phase2_separate(const ConvGeom& g, size_t ws_bytes);
+bool conv_dgrad_phase2_separate(const ConvGeom& g, size_t ws_bytes);
 hipError_t conv_fwd_phase1(const ConvGeom& g, const int8_t* x, const int8_t* w, int32_t* acc, uint32_t* amax,
                            void* ws, size_t ws_bytes, hipStream_t st);
 hipError_t conv_fwd_phase2(const ConvGeom& g, const int8_t* x, const int8_t* w, const int32_t* acc,
@@ -104,6 +124,7 @@ struct ActRequant {
     // optional reference-layout copy: MNN C4 [ceil(C/4)][N][HW][4]; rows = N*HW
     int8_t* out_c4 = nullptr;
     int c_real = 0, n = 0, hw = 0;
+    PoolFuse pool;  // fused 2x2 max pool / pool gradient (see ActOut)
 };
 hipError_t requant_act(const ActRequant& r, hipStream_t st);
 
@@ -114,6 +135,23 @@ hipError_t requant_grad(const int32_t* acc, int64_t n, const uint32_t* amax, int
 
 // Fused NITI_SGD on an OHWI16 layer: g = rule(acc, amax), w <- clip(w - g, +-127); the new weights
 // are also written transposed to wT (IHWO16, may be null) and g to g_out (may be null).
+// One layer's NITI_SGD update (rule-2/3 requant of the int32 gradient, w <- clip(w - g),
+// transposed copy); sgd_update_many runs several layers' updates in one launch.
+struct SgdJob {
+    const int32_t* acc;
+    const uint32_t* amax;
+    int rule, co, ci, kk, cip, cop;
+    int8_t* w;
+    int8_t* wT;
+    int8_t* g_out;
+};
+constexpr int SGD_MAX_JOBS = 24;
+struct SgdJobs {
+    SgdJob job[SGD_MAX_JOBS];
+    int start[SGD_MAX_JOBS];
+    int n;
+};
+hipError_t sgd_update_many(const SgdJob* jobs, int n, hipStream_t st);
 hipError_t sgd_update(const int32_t* acc, const uint32_t* amax, int rule, int co, int ci, int kk, int cip, int cop,
                       int8_t* w, int8_t* wT, int8_t* g_out, hipStream_t st);
 

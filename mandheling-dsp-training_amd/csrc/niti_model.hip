@@ -329,6 +329,8 @@ int Model::run(const int8_t* x_nchw, int exp_in, const int32_t* labels, hipStrea
     const int n = batch;
     const int nl = (int)L.size();
     const bool dp = comm != nullptr && world > 1;
+    SgdJob jobs[SGD_MAX_JOBS];
+    if (nl > SGD_MAX_JOBS) return NITI_NOT_SUPPORT;
     MTRY(hipMemsetAsync(amax, 0, amax_bytes, st));
     MTRY(hipMemsetAsync(exp0, exp_in, 1, st));
     MTRY(nchw_to_nhwc16(x_nchw, n, in_c, in_h * in_w, round_up(in_c, 16), x0, st));
@@ -345,9 +347,16 @@ int Model::run(const int8_t* x_nchw, int exp_in, const int32_t* labels, hipStrea
         o.exp_in = i == 0 ? exp0 : L[i - 1].exp;
         o.wscale = l.ws_dev;
         o.exp_out = l.exp;
+        // the 2x2 pool rides along the separate requant pass when there is one
+        const bool fuse_pool = l.pool && g.oh % 2 == 0 && g.ow % 2 == 0 && conv_fwd_phase2_separate(g, slab_bytes);
+        if (fuse_pool) {
+            o.pool.pool_out = l.p;
+            o.pool.H = g.oh;
+            o.pool.W = g.ow;
+        }
         MTRY(conv_fwd_phase2(g, l.in, l.w, acc, rng(i, 0), o, slab_bytes, st));
         probe(i, 0, false, st);
-        if (l.pool) MTRY(maxpool_nhwc16(l.r, n, g.oh, g.ow, g.cop, 2, 2, 0, l.p, l.ph, l.pw, st));
+        if (l.pool && !fuse_pool) MTRY(maxpool_nhwc16(l.r, n, g.oh, g.ow, g.cop, 2, 2, 0, l.p, l.ph, l.pw, st));
         if (l.flatten) {
             const int fc = g.c_out * l.ph * l.pw, ld = round_up(fc, 16);
             MTRY(launch_map((int64_t)n * ld, FlattenFwd{l.p, l.ph * l.pw, g.c_out, g.cop, ld, l.flat}, st));
@@ -387,11 +396,23 @@ int Model::run(const int8_t* x_nchw, int exp_in, const int32_t* labels, hipStrea
                 MTRY(maxpool_relu_grad_nhwc16(pv.r, pv.p, pv.dtmp, n, pg.oh, pg.ow, pg.cop, 2, 2, 0, pv.ph, pv.pw,
                                               pv.relu, pv.dy, st));
             } else if (pv.pool) {
-                o.out = pv.dtmp;
+                const bool fuse = pg.oh % 2 == 0 && pg.ow % 2 == 0 && conv_dgrad_phase2_separate(g, slab_bytes);
+                if (fuse) {  // pool gradient + relu gradient ride along the requant pass
+                    o.out = nullptr;
+                    o.pool.x = pv.r;
+                    o.pool.y = pv.p;
+                    o.pool.dx = pv.dy;
+                    o.pool.relu = pv.relu;
+                    o.pool.H = pg.oh;
+                    o.pool.W = pg.ow;
+                } else {
+                    o.out = pv.dtmp;
+                }
                 MTRY(conv_dgrad_phase2(g, l.dy, l.wT, acc, rng(i, 1), o, slab_bytes, st));
                 probe(i, 1, false, st);
-                MTRY(maxpool_relu_grad_nhwc16(pv.r, pv.p, pv.dtmp, n, pg.oh, pg.ow, pg.cop, 2, 2, 0, pv.ph, pv.pw,
-                                              pv.relu, pv.dy, st));
+                if (!fuse)
+                    MTRY(maxpool_relu_grad_nhwc16(pv.r, pv.p, pv.dtmp, n, pg.oh, pg.ow, pg.cop, 2, 2, 0, pv.ph,
+                                                  pv.pw, pv.relu, pv.dy, st));
             } else {
                 o.relu_mask = pv.relu ? pv.r : nullptr;
                 o.out = pv.dy;
@@ -399,9 +420,12 @@ int Model::run(const int8_t* x_nchw, int exp_in, const int32_t* labels, hipStrea
                 probe(i, 1, false, st);
             }
         }
-        MTRY(sgd_update(l.dwacc, rng(i, 2), RULE_WGRAD_BW2, g.c_out, g.c_in, g.kh * g.kw, g.cip, g.cop, l.w,
-                        i > 0 ? l.wT : nullptr, l.g8, st));
+        // NITI_SGD (NITI_SGD.hpp:20-54) for this layer is deferred: every layer's update runs
+        // in one launch after the backward pass (the input gradients above read the old weights)
+        jobs[i] = SgdJob{l.dwacc, rng(i, 2), RULE_WGRAD_BW2, g.c_out, g.c_in, g.kh * g.kw, g.cip, g.cop, l.w,
+                         i > 0 ? l.wT : nullptr, l.g8};
     }
+    MTRY(sgd_update_many(jobs, nl, st));
     return NITI_NO_ERROR;
 }
 
