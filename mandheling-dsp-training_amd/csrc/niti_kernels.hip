@@ -10,6 +10,8 @@
 // reduces max|acc| per workgroup and atomically max-es it into one word; the requant
 // kernel reads that word (after a kernel boundary -- or an RCCL all-reduce(MAX) in
 // data-parallel exact mode) and applies the shift.
+#include <stdlib.h>
+
 #include <type_traits>
 
 #include "niti_kernels.hpp"
@@ -1069,9 +1071,15 @@ static GemmPlan plan_gemm(int M, int N, int k_total, int k_step, int k_bytes, bo
         p.strat = recompute ? STRAT_RECOMPUTE : STRAT_STORE;
         return p;
     }
-    int s = (320 + p.tiles - 1) / p.tiles;
+    // one block per CU: tiles * splits <= 256 (measured best against 320 and 512 block targets
+    // on the VGG-11 weight and input gradients, tools/gpu_splits.sh)
+    int s = 256 / p.tiles;
     const int max_s = steps / 4;
     if (s > max_s) s = max_s;
+    if (const char* f = getenv("NITI_DIAG_SPLITS")) {  // diagnostics (tools/): force the split count
+        const int v = atoi(f);
+        if (v >= 1) s = v < steps ? v : steps;
+    }
     const size_t slab = slab_stride_elems(M, N);
     while (s > 1 && (size_t)s * slab > ws_elems) --s;
     if (s < 2) {
