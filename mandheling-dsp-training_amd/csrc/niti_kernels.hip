@@ -278,9 +278,12 @@ __device__ __forceinline__ int xcd_remap(int b, int nwg) {
 
 // Shared epilogue: D[row][col] of the 32x32 MFMA tiles, row = (i&3) + 8*(i>>2) + 4*(lane>>5),
 // col = lane&31.  `smem` is reused for the block max (every LDS read finished at the last barrier).
-template <int TM, int TN, int NW, int MODE>
+// REQUANT: the int8 tile is staged in LDS ([BM][BN + 16] bytes) and written out as 16-byte
+// row chunks (the MFMA C layout gives each lane one column of 16 rows, i.e. byte stores);
+// the relu-grad mask is applied in the same pass.
+template <int TM, int TN, int NW, int MODE, int BM, int BN>
 __device__ __forceinline__ void gemm_epilogue(v16i (&acc)[TM][TN], int r0, int c0, int M, int N, const Epi& epi,
-                                              int8_t* smem, int split) {
+                                              int8_t* smem, int split, int m0, int n0) {
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wid = tid >> 6;
@@ -314,15 +317,32 @@ __device__ __forceinline__ void gemm_epilogue(v16i (&acc)[TM][TN], int r0, int c
                         const uint32_t u = uabs32(v);
                         lmax = lmax > u ? lmax : u;
                     }
-                    if (MODE == EPI_REQUANT) {
-                        int32_t q = rq_raw ? (int32_t)(int8_t)v : psto_any(v, rq_shift);
-                        if (epi.relu && q < 0) q = 0;
-                        if (epi.relu_mask != nullptr && epi.relu_mask[(int64_t)row * epi.ldo + col] <= 0) q = 0;
-                        epi.out[(int64_t)row * epi.ldo + col] = (int8_t)q;
-                    }
+                }
+                if (MODE == EPI_REQUANT) {
+                    int32_t q = rq_raw ? (int32_t)(int8_t)v : psto_any(v, rq_shift);
+                    if (epi.relu && q < 0) q = 0;
+                    smem[(row - m0) * (BN + 16) + (col - n0)] = (int8_t)q;
                 }
             }
         }
+    if (MODE == EPI_REQUANT) {
+        __syncthreads();
+        constexpr int CPR = BN / 16;  // 16-byte chunks per tile row
+        for (int t = tid; t < BM * CPR; t += NW * 64) {
+            const int rl = t / CPR, cl = (t - rl * CPR) * 16;
+            const int row = m0 + rl, col = n0 + cl;
+            if (row < M && col < N) {  // N is a multiple of 16
+                v16c q = *(const v16c*)(smem + rl * (BN + 16) + cl);
+                const int64_t o = (int64_t)row * epi.ldo + col;
+                if (epi.relu_mask != nullptr) {
+                    const v16c mk = *(const v16c*)(epi.relu_mask + o);
+#pragma unroll
+                    for (int j = 0; j < 16; ++j) q[j] = mk[j] > 0 ? q[j] : (signed char)0;
+                }
+                *(v16c*)(epi.out + o) = q;
+            }
+        }
+    }
     if (MODE == EPI_STORE || MODE == EPI_AMAX) {
         lmax = wave_max(lmax);
         uint32_t* red = (uint32_t*)smem;  // all LDS reads finished at the last barrier
@@ -782,6 +802,7 @@ __global__ void __launch_bounds__(NW * 64) gemm_kernel(LA la, LB lb, int M, int 
     static_assert(KSUB % KG == 0, "sub-steps split evenly");
     constexpr int XCH_BYTES = KG > 1 ? NW * (TM / 2) * TN * 64 * 64 : 0;  // accumulator exchange
     constexpr int SMEM = STAGES * STAGE_BYTES > XCH_BYTES ? STAGES * STAGE_BYTES : XCH_BYTES;
+    static_assert(SMEM >= BM * (BN + 16), "requant epilogue staging fits in the pipeline's LDS");
     __shared__ __attribute__((aligned(16))) int8_t smem[SMEM];
 
     const int tid = threadIdx.x;
@@ -947,7 +968,8 @@ __global__ void __launch_bounds__(NW * 64) gemm_kernel(LA la, LB lb, int M, int 
     }
     __syncthreads();
     if constexpr (KG == 1) {
-        gemm_epilogue<TM, TN, NW, MODE>(acc, m0 + wm * (BM / WM), n0 + wn * (BN / WN), M, N, epi, smem, split);
+        gemm_epilogue<TM, TN, NW, MODE, BM, BN>(acc, m0 + wm * (BM / WM), n0 + wn * (BN / WN), M, N, epi, smem, split,
+                                                m0, n0);
     } else {
         // The two wave groups hold partial sums of the same tiles: group 0 keeps tile rows
         // a < TM/2 and sends the rest, group 1 the reverse; one LDS exchange, then each wave
@@ -983,8 +1005,8 @@ __global__ void __launch_bounds__(NW * 64) gemm_kernel(LA la, LB lb, int M, int 
                 }
             }
         __syncthreads();  // exchange buffer is reused by the epilogue's block max
-        gemm_epilogue<TH, TN, NW, MODE>(keep, m0 + wm * (BM / WM) + keep_a * 32, n0 + wn * (BN / WN), M, N, epi, smem,
-                                        split);
+        gemm_epilogue<TH, TN, NW, MODE, BM, BN>(keep, m0 + wm * (BM / WM) + keep_a * 32, n0 + wn * (BN / WN), M, N,
+                                                epi, smem, split, m0, n0);
     }
 }
 
