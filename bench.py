@@ -176,9 +176,9 @@ def main():
         "int8_mfma_tops": round(tops, 2),
         "int8_mfma_frac_of_peak": round(tops / PEAK_INT8_TOPS, 4),
         "roofline": {
-            "kernel": f"VGG-11 conv{probe_layer + 1} {phase_name} (gemm_kernel KT=true + split-K reduce; "
-                      f"layer index {probe_layer})" if args.probe_phase == 2 else
-                      f"VGG-11 conv{probe_layer + 1} {phase_name} (gemm_kernel; layer index {probe_layer})",
+            "kernel": f"VGG-11 conv{probe_layer + 1} {phase_name} GEMM launch (gemm_kernel, "
+                      f"{'K-major over pixels, split-K slabs' if args.probe_phase == 2 else 'implicit im2col'}; "
+                      f"layer index {probe_layer})",
             "bound": "mfma",
             "achieved": round(achieved, 2) if achieved else None,
             "peak": round(PEAK_INT8_TOPS, 1),

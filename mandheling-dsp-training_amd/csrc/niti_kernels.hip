@@ -258,6 +258,7 @@ struct Epi {
     int32_t* C = nullptr;  // STORE: C; SLAB: slab base
     int64_t ldc = 0;
     int64_t slab_stride = 0;  // elements between K-split slabs
+    int split_major = 0;      // XCD-aware order over (split, tile) instead of tiles only
     uint32_t* amax = nullptr;
     int8_t* out = nullptr;  // REQUANT output [M][ldo]
     int64_t ldo = 0;
@@ -812,7 +813,12 @@ __global__ void __launch_bounds__(NW * 64) gemm_kernel(LA la, LB lb, int M, int 
     const int wm = wq / WN, wn = wq % WN;
     // XCD-aware tile order inside each K split.  (A split-major order over the whole grid, which
     // keeps one K range per XCD and cuts the weight gradient's HBM fetch ~8x, measured slower.)
-    const int split = blockIdx.y, tile = xcd_remap(blockIdx.x, gridDim.x);
+    int split = blockIdx.y, tile = xcd_remap(blockIdx.x, gridDim.x);
+    if (epi.split_major) {  // one K range per XCD: its operand panels are fetched into one L2
+        const int logical = xcd_remap(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
+        split = logical / gridDim.x;
+        tile = logical - split * gridDim.x;
+    }
     const int tm_ = tile / tiles_n, tn_ = tile % tiles_n;
     const int m0 = tm_ * BM, n0 = tn_ * BN;
     const int k_begin = split * k_per_split;
@@ -1159,7 +1165,7 @@ static hipError_t splitk_reduce(const GemmPlan& p, const int32_t* slab, int64_t 
 // Materialise C [M][N] int32 (+ max|C| if amax): STORE, or SLAB + reduce.
 template <class LA, class LB, bool KT = false>
 static hipError_t gemm_acc(const LA& la, const LB& lb, int M, int N, int kc_total, int32_t* C, uint32_t* amax,
-                           int32_t* ws, size_t ws_elems, hipStream_t st) {
+                           int32_t* ws, size_t ws_elems, hipStream_t st, hipEvent_t after_gemm = nullptr) {
     if (M <= 0 || N <= 0) return hipSuccess;
     const int k_step = KT ? KT_BK : LA::BK / 16;
     GemmPlan p = plan_gemm(M, N, kc_total, k_step, 1 << 30, false, ws ? ws_elems : 0);
@@ -1168,14 +1174,18 @@ static hipError_t gemm_acc(const LA& la, const LB& lb, int M, int N, int kc_tota
         e.C = ws;
         e.ldc = N;
         e.slab_stride = (int64_t)slab_stride_elems(M, N);
+        if (const char* f = getenv("NITI_DIAG_SPLIT_MAJOR")) e.split_major = atoi(f);
         hipError_t r = launch_mode<LA, LB, EPI_SLAB, KT>(p, la, lb, M, N, kc_total, e, st);
+        if (r == hipSuccess && after_gemm != nullptr) r = hipEventRecord(after_gemm, st);
         if (r != hipSuccess) return r;
         return splitk_reduce(p, ws, (int64_t)M * N, e.slab_stride, C, amax, st);
     }
     e.C = C;
     e.ldc = N;
     e.amax = amax;
-    return launch_mode<LA, LB, EPI_STORE, KT>(p, la, lb, M, N, kc_total, e, st);
+    hipError_t r = launch_mode<LA, LB, EPI_STORE, KT>(p, la, lb, M, N, kc_total, e, st);
+    if (r == hipSuccess && after_gemm != nullptr) r = hipEventRecord(after_gemm, st);
+    return r;
 }
 
 // Two-phase activation GEMM (forward / input gradient): phase 1 establishes max|acc| (and
@@ -1390,7 +1400,7 @@ hipError_t conv_dgrad_acc(const ConvGeom& g, const int8_t* dy, const int8_t* wt,
 }
 
 hipError_t conv_wgrad_acc(const ConvGeom& g, const int8_t* x, const int8_t* dy, int32_t* acc, uint32_t* amax,
-                          void* ws, size_t ws_bytes, hipStream_t st) {
+                          void* ws, size_t ws_bytes, hipStream_t st, hipEvent_t after_gemm) {
     KtRowsU la;
     KtIm2col lg;
     wgrad_operands(g, x, dy, &la, &lg);
@@ -1416,10 +1426,10 @@ hipError_t conv_wgrad_acc(const ConvGeom& g, const int8_t* x, const int8_t* dy, 
         lb.K = lg.K;
         lb.rows_mode = rows_mode;
         return gemm_acc<KtRowsU, KtIm2colU, true>(la, lb, g.c_out, lg.ncols, lg.K, acc, amax, (int32_t*)ws,
-                                                  ws_bytes / 4, st);
+                                                  ws_bytes / 4, st, after_gemm);
     }
     return gemm_acc<KtRowsU, PerLane<KtIm2col, true>, true>(la, per_lane<KtIm2col, true>(lg), g.c_out, lg.ncols, lg.K,
-                                                            acc, amax, (int32_t*)ws, ws_bytes / 4, st);
+                                                            acc, amax, (int32_t*)ws, ws_bytes / 4, st, after_gemm);
 }
 
 hipError_t matmul_acc(int M, int O, int k16, const int8_t* B, int64_t ldb, const int8_t* A, int64_t lda, int32_t* acc,

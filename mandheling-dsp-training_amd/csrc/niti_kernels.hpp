@@ -59,7 +59,7 @@ hipError_t conv_dgrad_acc(const ConvGeom& g, const int8_t* dy_nhwc16, const int8
 // acc[co][kh][kw][cip] = sum over (n, oy, ox) of dy * x (x, dy NHWC16): the weight gradient,
 // a K-major GEMM over pixels whose operand tiles are transposed in LDS (ds_read_b64_tr_b8)
 hipError_t conv_wgrad_acc(const ConvGeom& g, const int8_t* x_nhwc16, const int8_t* dy_nhwc16, int32_t* acc,
-                          uint32_t* amax, void* ws, size_t ws_bytes, hipStream_t st);
+                          uint32_t* amax, void* ws, size_t ws_bytes, hipStream_t st, hipEvent_t after_gemm = nullptr);
 // acc[m][o] = sum_k B[m][k] * A[o][k] (NITI_Matmul_Int8); k16 multiple of 16 (zero padded rows),
 // ldb/lda bytes, ldc elements (multiple of 16; columns o..ldc come out 0)
 hipError_t matmul_acc(int M, int O, int k16, const int8_t* B, int64_t ldb, const int8_t* A, int64_t lda,

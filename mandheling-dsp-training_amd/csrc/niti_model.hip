@@ -146,6 +146,12 @@ struct Model {
             ++probe_count;
         }
     }
+    // the end event of a probe that the callee records itself (right after the GEMM launch)
+    hipEvent_t probe_end_event(int layer, int phase) {
+        if (layer != probe_layer || phase != probe_phase || capturing || probe_count >= (int)ev0.size())
+            return nullptr;
+        return ev1[probe_count++];
+    }
     void clear_probe() {
         for (auto e : ev0) (void)hipEventDestroy(e);
         for (auto e : ev1) (void)hipEventDestroy(e);
@@ -372,9 +378,10 @@ int Model::run(const int8_t* x_nchw, int exp_in, const int32_t* labels, hipStrea
         Layer& l = L[i];
         const ConvGeom& g = l.g;
         const int64_t we = l.w_elems();
+        // the weight-gradient probe brackets the GEMM launch alone (not its split-K reduce)
         probe(i, 2, true, st);
-        MTRY(conv_wgrad_acc(g, l.in, l.dy, l.dwacc, dp ? nullptr : rng(i, 2), slab, slab_bytes, st));
-        probe(i, 2, false, st);
+        MTRY(conv_wgrad_acc(g, l.in, l.dy, l.dwacc, dp ? nullptr : rng(i, 2), slab, slab_bytes, st,
+                            probe_end_event(i, 2)));
         if (dp) {
             CTRY(ncclAllReduce(l.dwacc, l.dwacc, (size_t)we, ncclInt32, ncclSum, comm, st));
             MTRY(absmax_i32(l.dwacc, we, rng(i, 2), st));

@@ -3,8 +3,8 @@
 
 FETCH_SIZE / WRITE_SIZE are read per dispatch (KB); FETCH_SIZE is doubled (gfx950: it counts
 64 B per 128-B request, MI355X_MICROARCH.md HBM section).  The probe is the VGG-11 conv4 weight
-gradient: the KT GEMM dispatch with the layer's grid plus the split-K reduce that follows it.
-usage: traffic.py <pmcF dir> <pmcW dir> [out.json]
+gradient GEMM: the KT gemm_kernel dispatch with the layer's grid (tiles x splits x 512 threads).
+usage: traffic.py <pmcF dir> <pmcW dir> [out.json] [grid_x_work_items grid_y]
 """
 import csv
 import glob
@@ -31,16 +31,17 @@ def main():
                 print(f"calib NchwToNhwc16: fetch x2 = {2 * F[i][2]:.0f} KB (expect 768 KB), "
                       f"write = {W.get(i, ('', 0, 0))[2]:.0f} KB (expect 4096 KB)")
                 break
+    gx = int(sys.argv[4]) if len(sys.argv) > 4 else 36 * 512
+    gy = int(sys.argv[5]) if len(sys.argv) > 5 else 7
+    want = set()
+    for f in glob.glob(f"{sys.argv[1]}/*kernel_trace.csv"):
+        for r in csv.DictReader(open(f)):
+            if "KtIm2colU" in r["Kernel_Name"] and int(r["Grid_Size_X"]) == gx and int(r["Grid_Size_Y"]) == gy:
+                want.add(int(r["Dispatch_Id"]))
     probes = []
-    ids = sorted(F)
-    for k, i in enumerate(ids):
-        name, grid, _ = F[i]
-        if "KtIm2colU" in name and "128, 128" in name and ", 3, true" in name and grid == 36 * 9 * 512:
-            j = ids[k + 1] if k + 1 < len(ids) else None
-            parts = [i] + ([j] if j is not None and "splitk_reduce" in F[j][0] else [])
-            fetch = sum(2 * F[p][2] for p in parts)
-            write = sum(W[p][2] for p in parts if p in W)
-            probes.append((fetch, write))
+    for i in sorted(F):
+        if i in want:
+            probes.append((2 * F[i][2], W[i][2] if i in W else 0.0))
     if not probes:
         sys.exit("probe dispatches not found")
     fetch = sum(p[0] for p in probes) / len(probes) * 1024
@@ -50,7 +51,8 @@ def main():
         out = {"vgg11_b256_L3_p2": {"hbm_bytes_per_launch": round(fetch + write),
                                     "fetch_bytes": round(fetch), "write_bytes": round(write),
                                     "launches_averaged": len(probes),
-                                    "kernels": "gemm_kernel<128,128,2,2,KtRowsU,KtIm2colU,SLAB,KT,8> + splitk_reduce_kernel",
+                                    "kernel": "gemm_kernel<128,128,2,2,KtRowsU,KtIm2colU,SLAB,KT,8> (conv4 weight gradient)",
+                                    "grid": [gx, gy],
                                     "method": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950) and --pmc WRITE_SIZE, separate passes"}}
         json.dump(out, open(sys.argv[3], "w"), indent=1)
 
