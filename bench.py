@@ -69,6 +69,7 @@ def main():
     ap.add_argument("--probe-layer", type=int, default=3, help="layer whose GEMM is timed for the roofline")
     ap.add_argument("--probe-phase", type=int, default=2, help="0 fwd, 1 input grad, 2 weight grad")
     ap.add_argument("--graph", action="store_true", help="replay the step as a hipGraph (slower on ROCm 7.2)")
+    ap.add_argument("--no-autotune", action="store_true", help="keep the fixed default GEMM plans")
     args = ap.parse_args()
 
     import numpy as np
@@ -100,6 +101,17 @@ def main():
     rng = np.random.default_rng(100 + rank)
     x = torch.from_numpy(rng.integers(-127, 128, (args.batch, l0["c_in"], l0["h"], l0["w"])).astype(np.int8)).cuda()
     labels = torch.from_numpy(rng.integers(0, 10, args.batch).astype(np.int32)).cuda()
+
+    # Setup (untimed): one step to fill the buffers, then per-shape GEMM plan autotuning
+    # (niti_model_autotune: candidate tile / split-K plans timed per layer phase).
+    tune_s = 0.0
+    if not args.no_autotune:
+        model.train_step(x, -3, labels)
+        ta = time.perf_counter()
+        model.autotune()
+        torch.cuda.synchronize()
+        tune_s = time.perf_counter() - ta
+    plans = model.plans()
 
     # The probe (HIP events around one GEMM, on the stream it runs on) is armed before the
     # warmup: the step is replayed as a hipGraph and arming it re-captures the graph, which
@@ -188,7 +200,9 @@ def main():
             "avg_launch_us": round(k_avg_s * 1e6, 2) if probe_n else None,
             "launches": probe_n,
             "ops_per_launch": k_ops,
+            "plan": dict(zip(("bm", "bn", "splits", "strategy"), plans[(probe_layer, args.probe_phase)])),
         },
+        "autotune_s": round(tune_s, 2) if not args.no_autotune else None,
         "cpu_baseline": cpu,
     }
     if rank == 0:

@@ -212,6 +212,21 @@ int64_t niti_model_step_macs(niti_model_t m);
 /* Replay the step as a hipGraph (single device only -- with a communicator attached the step
  * always runs as direct launches).  Default 0 (direct launches: measured faster on ROCm 7.2). */
 int niti_model_set_graph(niti_model_t m, int enable);
+/* Per-shape GEMM plan autotuning (no counterpart in the reference, whose CPU kernels have a
+ * fixed blocking, NITI_Conv_Int8.cpp:159-253): times every layer phase under candidate plans
+ * (tile shape, store / recompute / split-K count) on `stream` and keeps the fastest for this
+ * process.  Plans never change results.  Call after one train_step (it reuses that step's
+ * buffers); weights are not touched.  reps <= 0 uses 5.  Synchronises `stream`. */
+int niti_model_autotune(niti_model_t m, int reps, void* stream);
+/* The plan a layer phase (0 forward, 1 input gradient, 2 weight gradient) runs with:
+ * {bm, bn, splits, strategy 0 store / 1 recompute / 2 split-K}. */
+int niti_model_plan_info(niti_model_t m, int layer, int phase, int info[4]);
+/* Force a plan for a layer phase ({bm 64|128, bn 64|128, splits >= 1, strategy}; split counts
+ * beyond the K steps or the workspace are clamped; recompute on the weight gradient means
+ * store); plan = NULL restores the default.  Overrides are per process, keyed by GEMM shape. */
+int niti_model_plan_set(niti_model_t m, int layer, int phase, const int plan[4]);
+/* Drop every plan override of the process (autotuned or forced). */
+void niti_plan_reset(void);
 /* Kernel probe: HIP events on the step's stream around one GEMM launch (layer, phase
  * 0 = forward, 1 = input gradient, 2 = weight gradient) for up to max_launches steps;
  * layer < 0 disables.  probe_read synchronises those events and returns the summed

@@ -12,6 +12,8 @@
 // data-parallel exact mode) and applies the shift.
 #include <stdlib.h>
 
+#include <map>
+#include <mutex>
 #include <type_traits>
 
 #include "niti_kernels.hpp"
@@ -1085,13 +1087,77 @@ static size_t slab_stride_elems(int M, int N) {
     return pages * 1024;
 }
 
-static GemmPlan plan_gemm(int M, int N, int k_total, int k_step, int k_bytes, bool recompute_ok, size_t ws_elems) {
+// Plan overrides: the model's autotuner (niti_model.hip, Model::autotune) times candidate
+// plans for each of its GEMM shapes on the device and records the fastest here; plan_gemm
+// consults the table first.  Every plan computes the same exact int32 sums, so an override
+// changes speed only, never a result.
+namespace {
+std::mutex g_plan_mu;
+std::map<PlanKey, PlanChoice> g_plan_tab;
+}  // namespace
+
+void plan_override_set(const PlanKey& k, const PlanChoice& c) {
+    std::lock_guard<std::mutex> lk(g_plan_mu);
+    g_plan_tab[k] = c;
+}
+void plan_override_clear(const PlanKey& k) {
+    std::lock_guard<std::mutex> lk(g_plan_mu);
+    g_plan_tab.erase(k);
+}
+void plan_override_clear_all() {
+    std::lock_guard<std::mutex> lk(g_plan_mu);
+    g_plan_tab.clear();
+}
+static bool plan_override_get(const PlanKey& k, PlanChoice* c) {
+    std::lock_guard<std::mutex> lk(g_plan_mu);
+    auto it = g_plan_tab.find(k);
+    if (it == g_plan_tab.end()) return false;
+    *c = it->second;
+    return true;
+}
+
+static void plan_slab(GemmPlan& p, int s, int k_total, int k_step, int steps, bool recompute, int M, int N,
+                      size_t ws_elems) {
+    if (s > steps) s = steps;
+    const size_t slab = slab_stride_elems(M, N);
+    while (s > 1 && (size_t)s * slab > ws_elems) --s;
+    if (s < 2) {
+        p.strat = recompute ? STRAT_RECOMPUTE : STRAT_STORE;
+        return;
+    }
+    const int per = ((steps + s - 1) / s) * k_step;
+    p.splits = (k_total + per - 1) / per;
+    p.kc_per_split = per;
+    p.strat = p.splits > 1 ? STRAT_SLAB : (recompute ? STRAT_RECOMPUTE : STRAT_STORE);
+    if (p.splits == 1) p.kc_per_split = steps * k_step;
+}
+
+static GemmPlan plan_gemm(int M, int N, int k_total, int k_step, int k_bytes, bool recompute_ok, size_t ws_elems,
+                          int op = -1) {
     GemmPlan p;
-    p.bn = N <= 64 ? 64 : 128;
-    p.bm = (M <= 64 && p.bn >= 64) ? 64 : 128;
-    p.tiles = ((M + p.bm - 1) / p.bm) * ((N + p.bn - 1) / p.bn);
     const int steps = (k_total + k_step - 1) / k_step;
     p.kc_per_split = steps * k_step;
+    PlanChoice c;
+    if (op >= 0 && plan_override_get(PlanKey{op, M, N, k_total}, &c)) {
+        p.bm = c.bm == 64 ? 64 : 128;
+        p.bn = c.bn == 64 ? 64 : 128;
+        p.tiles = ((M + p.bm - 1) / p.bm) * ((N + p.bn - 1) / p.bn);
+        if (c.strat == STRAT_SLAB) {
+            plan_slab(p, c.splits, k_total, k_step, steps, false, M, N, ws_elems);
+        } else {
+            p.strat = c.strat == STRAT_RECOMPUTE && recompute_ok ? STRAT_RECOMPUTE : STRAT_STORE;
+        }
+        return p;
+    }
+    p.bn = N <= 64 ? 64 : 128;
+    p.bm = (M <= 64 && p.bn >= 64) ? 64 : 128;
+    if (const char* f = getenv("NITI_DIAG_TILE")) {  // diagnostics (tools/): force a tile shape
+        const int v = atoi(f);
+        if (v == 64 || v == 6464) p.bm = p.bn = 64;
+        if (v == 12864) { p.bm = 128; p.bn = 64; }
+        if (v == 64128) { p.bm = 64; p.bn = 128; }
+    }
+    p.tiles = ((M + p.bm - 1) / p.bm) * ((N + p.bn - 1) / p.bn);
     const bool recompute = recompute_ok && k_bytes <= 1152;
     if (p.tiles >= 160 || steps < 12) {
         // enough workgroups (or too little K to split): one pass; for small K recomputing the
@@ -1108,18 +1174,21 @@ static GemmPlan plan_gemm(int M, int N, int k_total, int k_step, int k_bytes, bo
         const int v = atoi(f);
         if (v >= 1) s = v < steps ? v : steps;
     }
-    const size_t slab = slab_stride_elems(M, N);
-    while (s > 1 && (size_t)s * slab > ws_elems) --s;
-    if (s < 2) {
-        p.strat = recompute ? STRAT_RECOMPUTE : STRAT_STORE;
-        return p;
-    }
-    const int per = ((steps + s - 1) / s) * k_step;
-    p.splits = (k_total + per - 1) / per;
-    p.kc_per_split = per;
-    p.strat = STRAT_SLAB;
+    plan_slab(p, s, k_total, k_step, steps, recompute, M, N, ws_elems);
     return p;
 }
+
+PlanChoice plan_query(const PlanKey& k, int k_step, bool recompute_ok, size_t ws_bytes) {
+    const GemmPlan p = plan_gemm(k.M, k.N, k.K, k_step, k.K * 16, recompute_ok, ws_bytes / 4, k.op);
+    PlanChoice c;
+    c.bm = p.bm;
+    c.bn = p.bn;
+    c.splits = p.strat == STRAT_SLAB ? p.splits : 1;
+    c.strat = p.strat;
+    return c;
+}
+
+size_t plan_slab_bytes(int M, int N, int splits) { return (size_t)splits * slab_stride_elems(M, N) * 4; }
 
 static size_t plan_ws_elems(int M, int N, int k_total, int k_step) {
     GemmPlan p = plan_gemm(M, N, k_total, k_step, 1 << 30, false, (size_t)-1);
@@ -1162,13 +1231,10 @@ static hipError_t splitk_reduce(const GemmPlan& p, const int32_t* slab, int64_t 
     return hipGetLastError();
 }
 
-// Materialise C [M][N] int32 (+ max|C| if amax): STORE, or SLAB + reduce.
+// Materialise C [M][N] int32 (+ max|C| if amax) under plan p: STORE, or SLAB + reduce.
 template <class LA, class LB, bool KT = false>
-static hipError_t gemm_acc(const LA& la, const LB& lb, int M, int N, int kc_total, int32_t* C, uint32_t* amax,
-                           int32_t* ws, size_t ws_elems, hipStream_t st, hipEvent_t after_gemm = nullptr) {
-    if (M <= 0 || N <= 0) return hipSuccess;
-    const int k_step = KT ? KT_BK : LA::BK / 16;
-    GemmPlan p = plan_gemm(M, N, kc_total, k_step, 1 << 30, false, ws ? ws_elems : 0);
+static hipError_t gemm_acc_plan(const GemmPlan& p, const LA& la, const LB& lb, int M, int N, int kc_total, int32_t* C,
+                                uint32_t* amax, int32_t* ws, hipStream_t st, hipEvent_t after_gemm = nullptr) {
     Epi e;
     if (p.strat == STRAT_SLAB) {
         e.C = ws;
@@ -1188,24 +1254,34 @@ static hipError_t gemm_acc(const LA& la, const LB& lb, int M, int N, int kc_tota
     return r;
 }
 
+template <class LA, class LB, bool KT = false>
+static hipError_t gemm_acc(int op, const LA& la, const LB& lb, int M, int N, int kc_total, int32_t* C, uint32_t* amax,
+                           int32_t* ws, size_t ws_elems, hipStream_t st, hipEvent_t after_gemm = nullptr) {
+    if (M <= 0 || N <= 0) return hipSuccess;
+    const int k_step = KT ? KT_BK : LA::BK / 16;
+    const GemmPlan p = plan_gemm(M, N, kc_total, k_step, 1 << 30, false, ws ? ws_elems : 0, op);
+    return gemm_acc_plan<LA, LB, KT>(p, la, lb, M, N, kc_total, C, amax, ws, st, after_gemm);
+}
+
 // Two-phase activation GEMM (forward / input gradient): phase 1 establishes max|acc| (and
 // materialises acc unless the plan recomputes); phase 2 writes the requantised int8.
 template <class LA, class LB>
-static hipError_t act_phase1(const LA& la, const LB& lb, int M, int N, int kc_total, int32_t* acc, uint32_t* amax,
-                             int32_t* ws, size_t ws_elems, hipStream_t st) {
-    GemmPlan p = plan_gemm(M, N, kc_total, LA::BK / 16, kc_total * 16, true, ws ? ws_elems : 0);
+static hipError_t act_phase1(int op, const LA& la, const LB& lb, int M, int N, int kc_total, int32_t* acc,
+                             uint32_t* amax, int32_t* ws, size_t ws_elems, hipStream_t st) {
+    if (M <= 0 || N <= 0) return hipSuccess;
+    const GemmPlan p = plan_gemm(M, N, kc_total, LA::BK / 16, kc_total * 16, true, ws ? ws_elems : 0, op);
     if (p.strat == STRAT_RECOMPUTE) {
         Epi e;
         e.amax = amax;
         return launch_mode<LA, LB, EPI_AMAX, false>(p, la, lb, M, N, kc_total, e, st);
     }
-    return gemm_acc(la, lb, M, N, kc_total, acc, amax, ws, ws_elems, st);
+    return gemm_acc_plan<LA, LB, false>(p, la, lb, M, N, kc_total, acc, amax, ws, st);
 }
 
 template <class LA, class LB>
-static hipError_t act_phase2(const LA& la, const LB& lb, int M, int N, int kc_total, const int32_t* acc,
+static hipError_t act_phase2(int op, const LA& la, const LB& lb, int M, int N, int kc_total, const int32_t* acc,
                              const uint32_t* amax, const ActOut& o, size_t ws_elems, hipStream_t st) {
-    GemmPlan p = plan_gemm(M, N, kc_total, LA::BK / 16, kc_total * 16, true, ws_elems);
+    const GemmPlan p = plan_gemm(M, N, kc_total, LA::BK / 16, kc_total * 16, true, ws_elems, op);
     if (p.strat == STRAT_RECOMPUTE) {
         if (o.pool.pool_out != nullptr || o.pool.dx != nullptr) return hipErrorInvalidValue;
         Epi e;
@@ -1237,11 +1313,13 @@ static hipError_t act_phase2(const LA& la, const LB& lb, int M, int N, int kc_to
 // ------------------------------------------------------------------------------ per-op wrappers
 bool conv_fwd_phase2_separate(const ConvGeom& g, size_t ws_bytes) {
     const int kc = g.kh * g.kw * g.cip / 16;  // every forward operand loader steps 64 bytes
-    return plan_gemm(g.n * g.oh * g.ow, g.cop, kc, 64 / 16, kc * 16, true, ws_bytes / 4).strat != STRAT_RECOMPUTE;
+    return plan_gemm(g.n * g.oh * g.ow, g.cop, kc, 64 / 16, kc * 16, true, ws_bytes / 4, PLAN_FWD).strat !=
+           STRAT_RECOMPUTE;
 }
 bool conv_dgrad_phase2_separate(const ConvGeom& g, size_t ws_bytes) {
     const int kc = g.kh * g.kw * g.cop / 16;
-    return plan_gemm(g.n * g.h * g.w, g.cip, kc, 64 / 16, kc * 16, true, ws_bytes / 4).strat != STRAT_RECOMPUTE;
+    return plan_gemm(g.n * g.h * g.w, g.cip, kc, 64 / 16, kc * 16, true, ws_bytes / 4, PLAN_DGRAD).strat !=
+           STRAT_RECOMPUTE;
 }
 static RowsK rows_k(const int8_t* p, int64_t ld, int rows, int kc_total) {
     RowsK r;
@@ -1366,6 +1444,17 @@ static void wgrad_operands(const ConvGeom& g, const int8_t* x, const int8_t* dy,
     lb->bytes = (uint32_t)((int64_t)g.n * g.h * g.w * g.cip);
 }
 
+PlanKey conv_plan_key(int op, const ConvGeom& g) {
+    if (op == PLAN_FWD) return PlanKey{op, g.n * g.oh * g.ow, g.cop, g.kh * g.kw * g.cip / 16};
+    if (op == PLAN_DGRAD) return PlanKey{op, g.n * g.h * g.w, g.cip, g.kh * g.kw * g.cop / 16};
+    return PlanKey{PLAN_WGRAD, g.c_out, g.kh * g.kw * g.cip, g.n * g.oh * g.ow};
+}
+int conv_plan_k_step(int op, const ConvGeom& g) {
+    if (op == PLAN_FWD) return (fwd_taps_bk(g) ? fwd_taps_bk(g) : 64) / 16;
+    if (op == PLAN_DGRAD) return (dgrad_taps_bk(g) ? dgrad_taps_bk(g) : 64) / 16;
+    return KT_BK;
+}
+
 size_t conv_fwd_workspace(const ConvGeom& g) {
     const int bk = fwd_taps_bk(g) ? fwd_taps_bk(g) : 64;
     return plan_ws_elems(g.n * g.oh * g.ow, g.cop, g.kh * g.kw * g.cip / 16, bk / 16) * sizeof(int32_t);
@@ -1386,7 +1475,7 @@ hipError_t conv_fwd_acc(const ConvGeom& g, const int8_t* x, const int8_t* w, int
     const int kc_total = g.kh * g.kw * g.cip / 16;
     const RowsK lb = rows_k(w, (int64_t)g.kh * g.kw * g.cip, g.c_out, kc_total);
     return with_fwd_operand(g, x, [&](const auto& la) {
-        return gemm_acc(la, lb, g.n * g.oh * g.ow, g.cop, kc_total, acc, amax, (int32_t*)ws, ws_bytes / 4, st);
+        return gemm_acc(PLAN_FWD, la, lb, g.n * g.oh * g.ow, g.cop, kc_total, acc, amax, (int32_t*)ws, ws_bytes / 4, st);
     });
 }
 
@@ -1395,7 +1484,7 @@ hipError_t conv_dgrad_acc(const ConvGeom& g, const int8_t* dy, const int8_t* wt,
     const int kc_total = g.kh * g.kw * g.cop / 16;
     const RowsK lb = rows_k(wt, (int64_t)g.kh * g.kw * g.cop, g.c_in, kc_total);
     return with_dgrad_operand(g, dy, [&](const auto& la) {
-        return gemm_acc(la, lb, g.n * g.h * g.w, g.cip, kc_total, acc, amax, (int32_t*)ws, ws_bytes / 4, st);
+        return gemm_acc(PLAN_DGRAD, la, lb, g.n * g.h * g.w, g.cip, kc_total, acc, amax, (int32_t*)ws, ws_bytes / 4, st);
     });
 }
 
@@ -1425,10 +1514,10 @@ hipError_t conv_wgrad_acc(const ConvGeom& g, const int8_t* x, const int8_t* dy, 
         lb.ncols = lg.ncols;
         lb.K = lg.K;
         lb.rows_mode = rows_mode;
-        return gemm_acc<KtRowsU, KtIm2colU, true>(la, lb, g.c_out, lg.ncols, lg.K, acc, amax, (int32_t*)ws,
+        return gemm_acc<KtRowsU, KtIm2colU, true>(PLAN_WGRAD, la, lb, g.c_out, lg.ncols, lg.K, acc, amax, (int32_t*)ws,
                                                   ws_bytes / 4, st, after_gemm);
     }
-    return gemm_acc<KtRowsU, PerLane<KtIm2col, true>, true>(la, per_lane<KtIm2col, true>(lg), g.c_out, lg.ncols, lg.K,
+    return gemm_acc<KtRowsU, PerLane<KtIm2col, true>, true>(PLAN_WGRAD, la, per_lane<KtIm2col, true>(lg), g.c_out, lg.ncols, lg.K,
                                                             acc, amax, (int32_t*)ws, ws_bytes / 4, st, after_gemm);
 }
 
@@ -1437,7 +1526,7 @@ hipError_t matmul_acc(int M, int O, int k16, const int8_t* B, int64_t ldb, const
     const int kc_total = k16 / 16;
     const RowsK la = rows_k(B, ldb, M, kc_total);
     const RowsK lb = rows_k(A, lda, O, kc_total);  // rows >= O read as zero, so columns O..ldc are 0
-    return gemm_acc(la, lb, M, (int)ldc, kc_total, acc, amax, (int32_t*)ws, ws_bytes / 4, st);
+    return gemm_acc(PLAN_MATMUL, la, lb, M, (int)ldc, kc_total, acc, amax, (int32_t*)ws, ws_bytes / 4, st);
 }
 
 hipError_t conv_fwd_phase1(const ConvGeom& g, const int8_t* x, const int8_t* w, int32_t* acc, uint32_t* amax,
@@ -1445,7 +1534,7 @@ hipError_t conv_fwd_phase1(const ConvGeom& g, const int8_t* x, const int8_t* w, 
     const int kc_total = g.kh * g.kw * g.cip / 16;
     const RowsK lb = rows_k(w, (int64_t)g.kh * g.kw * g.cip, g.c_out, kc_total);
     return with_fwd_operand(g, x, [&](const auto& la) {
-        return act_phase1(la, lb, g.n * g.oh * g.ow, g.cop, kc_total, acc, amax, (int32_t*)ws, ws_bytes / 4, st);
+        return act_phase1(PLAN_FWD, la, lb, g.n * g.oh * g.ow, g.cop, kc_total, acc, amax, (int32_t*)ws, ws_bytes / 4, st);
     });
 }
 hipError_t conv_fwd_phase2(const ConvGeom& g, const int8_t* x, const int8_t* w, const int32_t* acc,
@@ -1453,7 +1542,7 @@ hipError_t conv_fwd_phase2(const ConvGeom& g, const int8_t* x, const int8_t* w, 
     const int kc_total = g.kh * g.kw * g.cip / 16;
     const RowsK lb = rows_k(w, (int64_t)g.kh * g.kw * g.cip, g.c_out, kc_total);
     return with_fwd_operand(g, x, [&](const auto& la) {
-        return act_phase2(la, lb, g.n * g.oh * g.ow, g.cop, kc_total, acc, amax, o, ws_bytes / 4, st);
+        return act_phase2(PLAN_FWD, la, lb, g.n * g.oh * g.ow, g.cop, kc_total, acc, amax, o, ws_bytes / 4, st);
     });
 }
 hipError_t conv_dgrad_phase1(const ConvGeom& g, const int8_t* dy, const int8_t* wt, int32_t* acc, uint32_t* amax,
@@ -1461,7 +1550,7 @@ hipError_t conv_dgrad_phase1(const ConvGeom& g, const int8_t* dy, const int8_t* 
     const int kc_total = g.kh * g.kw * g.cop / 16;
     const RowsK lb = rows_k(wt, (int64_t)g.kh * g.kw * g.cop, g.c_in, kc_total);
     return with_dgrad_operand(g, dy, [&](const auto& la) {
-        return act_phase1(la, lb, g.n * g.h * g.w, g.cip, kc_total, acc, amax, (int32_t*)ws, ws_bytes / 4, st);
+        return act_phase1(PLAN_DGRAD, la, lb, g.n * g.h * g.w, g.cip, kc_total, acc, amax, (int32_t*)ws, ws_bytes / 4, st);
     });
 }
 hipError_t conv_dgrad_phase2(const ConvGeom& g, const int8_t* dy, const int8_t* wt, const int32_t* acc,
@@ -1469,7 +1558,7 @@ hipError_t conv_dgrad_phase2(const ConvGeom& g, const int8_t* dy, const int8_t* 
     const int kc_total = g.kh * g.kw * g.cop / 16;
     const RowsK lb = rows_k(wt, (int64_t)g.kh * g.kw * g.cop, g.c_in, kc_total);
     return with_dgrad_operand(g, dy, [&](const auto& la) {
-        return act_phase2(la, lb, g.n * g.h * g.w, g.cip, kc_total, acc, amax, o, ws_bytes / 4, st);
+        return act_phase2(PLAN_DGRAD, la, lb, g.n * g.h * g.w, g.cip, kc_total, acc, amax, o, ws_bytes / 4, st);
     });
 }
 

@@ -50,6 +50,32 @@ size_t conv_fwd_workspace(const ConvGeom& g);
 size_t conv_dgrad_workspace(const ConvGeom& g);
 size_t conv_wgrad_workspace(const ConvGeom& g);
 size_t matmul_workspace(int M, int ldc, int k16);
+
+// Per-shape plan overrides (filled by the model's autotuner).  A plan is a tile shape (bm x bn,
+// 64 or 128 each), a strategy (0 store acc, 1 recompute the GEMM for the requantisation --
+// forward / input gradient only, 2 split-K slabs + reduce) and a split count.  Keys: op and the
+// GEMM extents (M, N, K in the planner's units).  Overrides never change results.
+enum PlanOp { PLAN_FWD = 0, PLAN_DGRAD = 1, PLAN_WGRAD = 2, PLAN_MATMUL = 3 };
+struct PlanKey {
+    int op, M, N, K;
+    bool operator<(const PlanKey& o) const {
+        if (op != o.op) return op < o.op;
+        if (M != o.M) return M < o.M;
+        if (N != o.N) return N < o.N;
+        return K < o.K;
+    }
+};
+struct PlanChoice {
+    int bm = 128, bn = 128, splits = 1, strat = 0;
+};
+PlanKey conv_plan_key(int op, const ConvGeom& g);
+int conv_plan_k_step(int op, const ConvGeom& g);
+void plan_override_set(const PlanKey& k, const PlanChoice& c);
+void plan_override_clear(const PlanKey& k);
+void plan_override_clear_all();
+// the plan the GEMM of key k runs with now (override or default) under a workspace of ws_bytes
+PlanChoice plan_query(const PlanKey& k, int k_step, bool recompute_ok, size_t ws_bytes);
+size_t plan_slab_bytes(int M, int N, int splits);
 // acc[M = n*oh*ow][cop] = conv(x NHWC16, w OHWI16)
 hipError_t conv_fwd_acc(const ConvGeom& g, const int8_t* x_nhwc16, const int8_t* w_ohwi16, int32_t* acc,
                         uint32_t* amax, void* ws, size_t ws_bytes, hipStream_t st);

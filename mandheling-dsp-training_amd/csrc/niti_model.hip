@@ -14,6 +14,7 @@
 #include <rccl/rccl.h>
 #include <string.h>
 
+#include <algorithm>
 #include <memory>
 #include <vector>
 
@@ -133,7 +134,7 @@ struct Model {
     int probe_layer = -1, probe_phase = -1, probe_count = 0;
     std::vector<hipEvent_t> ev0, ev1;
     void probe(int layer, int phase, bool begin, hipStream_t st) {
-        if (layer != probe_layer || phase != probe_phase) return;
+        if (layer != probe_layer || phase != probe_phase || tuning) return;
         if (capturing) {
             seg_cut(st);
             return;
@@ -148,7 +149,7 @@ struct Model {
     }
     // the end event of a probe that the callee records itself (right after the GEMM launch)
     hipEvent_t probe_end_event(int layer, int phase) {
-        if (layer != probe_layer || phase != probe_phase || capturing || probe_count >= (int)ev0.size())
+        if (layer != probe_layer || phase != probe_phase || capturing || tuning || probe_count >= (int)ev0.size())
             return nullptr;
         return ev1[probe_count++];
     }
@@ -162,6 +163,21 @@ struct Model {
     }
 
     int build(int arch_, int batch_);
+    bool tuning = false;  // autotune in progress: no collectives, no probe
+    int fwd_layer(int i, hipStream_t st);
+    int wgrad_layer(int i, hipStream_t st);
+    int dgrad_layer(int i, hipStream_t st);
+    int autotune(hipStream_t st, int reps);
+    // grow the split-K workspace (the old one stays owned by ws until the model is destroyed)
+    bool ensure_slab(size_t bytes) {
+        if (slab_bytes >= bytes) return true;
+        if (hipDeviceSynchronize() != hipSuccess) return false;
+        void* s2 = ws.alloc(bytes);
+        if (!s2) return false;
+        slab = s2;
+        slab_bytes = bytes;
+        return true;
+    }
     int run(const int8_t* x_nchw, int exp_in, const int32_t* labels, hipStream_t st);
     int step(const int8_t* x_nchw, int exp_in, const int32_t* labels, hipStream_t st);
     ~Model() {
@@ -331,104 +347,220 @@ int Model::step(const int8_t* x_nchw, int exp_in, const int32_t* labels, hipStre
     return NITI_NO_ERROR;
 }
 
+// One layer's forward: GEMM range pass -> [all-reduce MAX] -> requantise (+relu, fused pool
+// when the requant is a separate pass) -> pool / flatten.
+int Model::fwd_layer(int i, hipStream_t st) {
+    const int n = batch;
+    const bool dp = comm != nullptr && world > 1 && !tuning;
+    Layer& l = L[i];
+    const ConvGeom& g = l.g;
+    probe(i, 0, true, st);
+    MTRY(conv_fwd_phase1(g, l.in, l.w, acc, rng(i, 0), slab, slab_bytes, st));
+    if (dp && exact) CTRY(ncclAllReduce(rng(i, 0), rng(i, 0), MAX_WORDS, ncclUint32, ncclMax, comm, st));
+    ActOut o;
+    o.out = l.r;
+    o.relu = l.relu;
+    o.exp_in = i == 0 ? exp0 : L[i - 1].exp;
+    o.wscale = l.ws_dev;
+    o.exp_out = l.exp;
+    // the 2x2 pool rides along the separate requant pass when there is one
+    const bool fuse_pool = l.pool && g.oh % 2 == 0 && g.ow % 2 == 0 && conv_fwd_phase2_separate(g, slab_bytes);
+    if (fuse_pool) {
+        o.pool.pool_out = l.p;
+        o.pool.H = g.oh;
+        o.pool.W = g.ow;
+    }
+    MTRY(conv_fwd_phase2(g, l.in, l.w, acc, rng(i, 0), o, slab_bytes, st));
+    probe(i, 0, false, st);
+    if (l.pool && !fuse_pool) MTRY(maxpool_nhwc16(l.r, n, g.oh, g.ow, g.cop, 2, 2, 0, l.p, l.ph, l.pw, st));
+    if (l.flatten) {
+        const int fc = g.c_out * l.ph * l.pw, ld = round_up(fc, 16);
+        MTRY(launch_map((int64_t)n * ld, FlattenFwd{l.p, l.ph * l.pw, g.c_out, g.cop, ld, l.flat}, st));
+    }
+    return NITI_NO_ERROR;
+}
+
+// One layer's weight gradient (the int32 gradient and, single device, its range).
+int Model::wgrad_layer(int i, hipStream_t st) {
+    const bool dp = comm != nullptr && world > 1 && !tuning;
+    Layer& l = L[i];
+    const ConvGeom& g = l.g;
+    const int64_t we = l.w_elems();
+    // the weight-gradient probe brackets the GEMM launch alone (not its split-K reduce)
+    probe(i, 2, true, st);
+    MTRY(conv_wgrad_acc(g, l.in, l.dy, l.dwacc, dp ? nullptr : rng(i, 2), slab, slab_bytes, st,
+                        probe_end_event(i, 2)));
+    if (dp) {
+        CTRY(ncclAllReduce(l.dwacc, l.dwacc, (size_t)we, ncclInt32, ncclSum, comm, st));
+        MTRY(absmax_i32(l.dwacc, we, rng(i, 2), st));
+    }
+    return NITI_NO_ERROR;
+}
+
+// Input gradient of layer i (i > 0) into the previous layer's output gradient, with the
+// previous layer's pool / flatten / relu gradients.
+int Model::dgrad_layer(int i, hipStream_t st) {
+    const int n = batch;
+    const bool dp = comm != nullptr && world > 1 && !tuning;
+    Layer& l = L[i];
+    const ConvGeom& g = l.g;
+    Layer& pv = L[i - 1];
+    probe(i, 1, true, st);
+    MTRY(conv_dgrad_phase1(g, l.dy, l.wT, acc, rng(i, 1), slab, slab_bytes, st));
+    if (dp && exact) CTRY(ncclAllReduce(rng(i, 1), rng(i, 1), MAX_WORDS, ncclUint32, ncclMax, comm, st));
+    const ConvGeom& pg = pv.g;
+    ActOut o;
+    if (pv.flatten) {
+        o.out = pv.dflat;
+        MTRY(conv_dgrad_phase2(g, l.dy, l.wT, acc, rng(i, 1), o, slab_bytes, st));
+        probe(i, 1, false, st);
+        const int fc = pg.c_out * pv.ph * pv.pw, ld = round_up(fc, 16);
+        MTRY(launch_map((int64_t)n * pv.ph * pv.pw * pg.cop,
+                        FlattenBwd{pv.dflat, pv.ph * pv.pw, pg.c_out, pg.cop, ld, pv.dtmp}, st));
+        MTRY(maxpool_relu_grad_nhwc16(pv.r, pv.p, pv.dtmp, n, pg.oh, pg.ow, pg.cop, 2, 2, 0, pv.ph, pv.pw, pv.relu,
+                                      pv.dy, st));
+    } else if (pv.pool) {
+        const bool fuse = pg.oh % 2 == 0 && pg.ow % 2 == 0 && conv_dgrad_phase2_separate(g, slab_bytes);
+        if (fuse) {  // pool gradient + relu gradient ride along the requant pass
+            o.out = nullptr;
+            o.pool.x = pv.r;
+            o.pool.y = pv.p;
+            o.pool.dx = pv.dy;
+            o.pool.relu = pv.relu;
+            o.pool.H = pg.oh;
+            o.pool.W = pg.ow;
+        } else {
+            o.out = pv.dtmp;
+        }
+        MTRY(conv_dgrad_phase2(g, l.dy, l.wT, acc, rng(i, 1), o, slab_bytes, st));
+        probe(i, 1, false, st);
+        if (!fuse)
+            MTRY(maxpool_relu_grad_nhwc16(pv.r, pv.p, pv.dtmp, n, pg.oh, pg.ow, pg.cop, 2, 2, 0, pv.ph, pv.pw,
+                                          pv.relu, pv.dy, st));
+    } else {
+        o.relu_mask = pv.relu ? pv.r : nullptr;
+        o.out = pv.dy;
+        MTRY(conv_dgrad_phase2(g, l.dy, l.wT, acc, rng(i, 1), o, slab_bytes, st));
+        probe(i, 1, false, st);
+    }
+    return NITI_NO_ERROR;
+}
+
+// Per-shape plan autotuning.  For every GEMM of the step (layer x {forward, weight gradient,
+// input gradient}) time the layer's whole phase -- GEMM(s), split-K reduce, requantisation,
+// fused / separate pool -- under each candidate plan on the caller's stream and keep the
+// fastest as a plan override (niti_kernels.hpp).  Candidates: 4 tile shapes x {store acc,
+// recompute (activation GEMMs), split-K 2..64 within the tuning workspace}.  The layer phases
+// are idempotent on the buffers left by the previous step, so tuning leaves the weights
+// untouched; a fixed default plan (plan_gemm) is the starting point and is kept unless beaten.
+int Model::autotune(hipStream_t st, int reps) {
+    if (reps < 1) reps = 5;
+    const int nl = (int)L.size();
+    if (!ensure_slab(size_t(96) << 20)) return NITI_OUT_OF_MEMORY;  // split-K room for the candidates
+    drop_graph();
+    hipEvent_t ev[4];
+    for (auto& e : ev)
+        if (hipEventCreate(&e) != hipSuccess) return NITI_NO_EXECUTION;
+    tuning = true;
+    int rc = NITI_NO_ERROR;
+    auto run_op = [&](int i, int op) {
+        return op == PLAN_FWD ? fwd_layer(i, st) : op == PLAN_WGRAD ? wgrad_layer(i, st) : dgrad_layer(i, st);
+    };
+    // min over three event-bracketed batches of `reps` back-to-back runs (no host sync inside)
+    auto time_op = [&](int i, int op, float* us) -> int {
+        int r = run_op(i, op);
+        float best = 1e30f;
+        for (int t = 0; t < 3 && r == NITI_NO_ERROR; ++t) {
+            if (hipEventRecord(ev[0], st) != hipSuccess) return NITI_NO_EXECUTION;
+            for (int k = 0; k < reps && r == NITI_NO_ERROR; ++k) r = run_op(i, op);
+            if (hipEventRecord(ev[1], st) != hipSuccess || hipEventSynchronize(ev[1]) != hipSuccess)
+                return NITI_NO_EXECUTION;
+            float ms = 0.f;
+            if (hipEventElapsedTime(&ms, ev[0], ev[1]) != hipSuccess) return NITI_NO_EXECUTION;
+            best = std::min(best, ms * 1000.f / reps);
+        }
+        *us = best;
+        return r;
+    };
+    if (hipMemsetAsync(amax, 0, amax_bytes, st) != hipSuccess) rc = NITI_NO_EXECUTION;
+    static const int tiles[4][2] = {{128, 128}, {128, 64}, {64, 128}, {64, 64}};
+    static const int split_opts[] = {2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64};
+    for (int i = 0; i < nl && rc == NITI_NO_ERROR; ++i) {
+        for (int op : {PLAN_FWD, PLAN_WGRAD, PLAN_DGRAD}) {
+            if (op == PLAN_DGRAD && i == 0) continue;
+            const ConvGeom& g = L[i].g;
+            const PlanKey key = conv_plan_key(op, g);
+            const int k_step = conv_plan_k_step(op, g);
+            const int steps = (key.K + k_step - 1) / k_step;
+            const bool act = op != PLAN_WGRAD;
+            plan_override_clear(key);
+            PlanChoice best = plan_query(key, k_step, act, slab_bytes);
+            float best_us = 0.f;
+            rc = time_op(i, op, &best_us);
+            for (const auto& t : tiles) {
+                if (rc != NITI_NO_ERROR) break;
+                std::vector<PlanChoice> cands;
+                PlanChoice c;
+                c.bm = t[0];
+                c.bn = t[1];
+                c.splits = 1;
+                c.strat = 0;
+                cands.push_back(c);
+                if (act) {
+                    c.strat = 1;
+                    cands.push_back(c);
+                }
+                for (int s : split_opts) {
+                    if (s > steps / 2 || plan_slab_bytes(key.M, key.N, s) > slab_bytes) break;
+                    c.strat = 2;
+                    c.splits = s;
+                    cands.push_back(c);
+                }
+                for (const PlanChoice& cand : cands) {
+                    plan_override_set(key, cand);
+                    float us = 0.f;
+                    rc = time_op(i, op, &us);
+                    if (rc != NITI_NO_ERROR) break;
+                    if (us < best_us) {
+                        best_us = us;
+                        best = cand;
+                    }
+                }
+            }
+            plan_override_set(key, best);
+            if (rc != NITI_NO_ERROR) break;
+        }
+    }
+    tuning = false;
+    for (auto e : ev) (void)hipEventDestroy(e);
+    if (hipStreamSynchronize(st) != hipSuccess) rc = NITI_NO_EXECUTION;
+    return rc;
+}
+
 int Model::run(const int8_t* x_nchw, int exp_in, const int32_t* labels, hipStream_t st) {
     const int n = batch;
     const int nl = (int)L.size();
-    const bool dp = comm != nullptr && world > 1;
     SgdJob jobs[SGD_MAX_JOBS];
     if (nl > SGD_MAX_JOBS) return NITI_NOT_SUPPORT;
     MTRY(hipMemsetAsync(amax, 0, amax_bytes, st));
     MTRY(hipMemsetAsync(exp0, exp_in, 1, st));
     MTRY(nchw_to_nhwc16(x_nchw, n, in_c, in_h * in_w, round_up(in_c, 16), x0, st));
-    // ------------------------------------------------------------------ forward
     for (int i = 0; i < nl; ++i) {
-        Layer& l = L[i];
-        const ConvGeom& g = l.g;
-        probe(i, 0, true, st);
-        MTRY(conv_fwd_phase1(g, l.in, l.w, acc, rng(i, 0), slab, slab_bytes, st));
-        if (dp && exact) CTRY(ncclAllReduce(rng(i, 0), rng(i, 0), MAX_WORDS, ncclUint32, ncclMax, comm, st));
-        ActOut o;
-        o.out = l.r;
-        o.relu = l.relu;
-        o.exp_in = i == 0 ? exp0 : L[i - 1].exp;
-        o.wscale = l.ws_dev;
-        o.exp_out = l.exp;
-        // the 2x2 pool rides along the separate requant pass when there is one
-        const bool fuse_pool = l.pool && g.oh % 2 == 0 && g.ow % 2 == 0 && conv_fwd_phase2_separate(g, slab_bytes);
-        if (fuse_pool) {
-            o.pool.pool_out = l.p;
-            o.pool.H = g.oh;
-            o.pool.W = g.ow;
-        }
-        MTRY(conv_fwd_phase2(g, l.in, l.w, acc, rng(i, 0), o, slab_bytes, st));
-        probe(i, 0, false, st);
-        if (l.pool && !fuse_pool) MTRY(maxpool_nhwc16(l.r, n, g.oh, g.ow, g.cop, 2, 2, 0, l.p, l.ph, l.pw, st));
-        if (l.flatten) {
-            const int fc = g.c_out * l.ph * l.pw, ld = round_up(fc, 16);
-            MTRY(launch_map((int64_t)n * ld, FlattenFwd{l.p, l.ph * l.pw, g.c_out, g.cop, ld, l.flat}, st));
-        }
+        const int rc = fwd_layer(i, st);
+        if (rc != NITI_NO_ERROR) return rc;
     }
-    // ------------------------------------------------------------------ loss gradient
     {
         Layer& t = L[nl - 1];
         MTRY(loss_grad(t.r, n, t.g.c_out, t.g.cop, t.exp, labels, t.dy, st));
     }
-    // ------------------------------------------------------------------ backward
     for (int i = nl - 1; i >= 0; --i) {
-        Layer& l = L[i];
-        const ConvGeom& g = l.g;
-        const int64_t we = l.w_elems();
-        // the weight-gradient probe brackets the GEMM launch alone (not its split-K reduce)
-        probe(i, 2, true, st);
-        MTRY(conv_wgrad_acc(g, l.in, l.dy, l.dwacc, dp ? nullptr : rng(i, 2), slab, slab_bytes, st,
-                            probe_end_event(i, 2)));
-        if (dp) {
-            CTRY(ncclAllReduce(l.dwacc, l.dwacc, (size_t)we, ncclInt32, ncclSum, comm, st));
-            MTRY(absmax_i32(l.dwacc, we, rng(i, 2), st));
-        }
-        if (i > 0) {
-            Layer& pv = L[i - 1];
-            probe(i, 1, true, st);
-            MTRY(conv_dgrad_phase1(g, l.dy, l.wT, acc, rng(i, 1), slab, slab_bytes, st));
-            if (dp && exact) CTRY(ncclAllReduce(rng(i, 1), rng(i, 1), MAX_WORDS, ncclUint32, ncclMax, comm, st));
-            const ConvGeom& pg = pv.g;
-            ActOut o;
-            if (pv.flatten) {
-                o.out = pv.dflat;
-                MTRY(conv_dgrad_phase2(g, l.dy, l.wT, acc, rng(i, 1), o, slab_bytes, st));
-                probe(i, 1, false, st);
-                const int fc = pg.c_out * pv.ph * pv.pw, ld = round_up(fc, 16);
-                MTRY(launch_map((int64_t)n * pv.ph * pv.pw * pg.cop,
-                                FlattenBwd{pv.dflat, pv.ph * pv.pw, pg.c_out, pg.cop, ld, pv.dtmp}, st));
-                MTRY(maxpool_relu_grad_nhwc16(pv.r, pv.p, pv.dtmp, n, pg.oh, pg.ow, pg.cop, 2, 2, 0, pv.ph, pv.pw,
-                                              pv.relu, pv.dy, st));
-            } else if (pv.pool) {
-                const bool fuse = pg.oh % 2 == 0 && pg.ow % 2 == 0 && conv_dgrad_phase2_separate(g, slab_bytes);
-                if (fuse) {  // pool gradient + relu gradient ride along the requant pass
-                    o.out = nullptr;
-                    o.pool.x = pv.r;
-                    o.pool.y = pv.p;
-                    o.pool.dx = pv.dy;
-                    o.pool.relu = pv.relu;
-                    o.pool.H = pg.oh;
-                    o.pool.W = pg.ow;
-                } else {
-                    o.out = pv.dtmp;
-                }
-                MTRY(conv_dgrad_phase2(g, l.dy, l.wT, acc, rng(i, 1), o, slab_bytes, st));
-                probe(i, 1, false, st);
-                if (!fuse)
-                    MTRY(maxpool_relu_grad_nhwc16(pv.r, pv.p, pv.dtmp, n, pg.oh, pg.ow, pg.cop, 2, 2, 0, pv.ph,
-                                                  pv.pw, pv.relu, pv.dy, st));
-            } else {
-                o.relu_mask = pv.relu ? pv.r : nullptr;
-                o.out = pv.dy;
-                MTRY(conv_dgrad_phase2(g, l.dy, l.wT, acc, rng(i, 1), o, slab_bytes, st));
-                probe(i, 1, false, st);
-            }
-        }
+        int rc = wgrad_layer(i, st);
+        if (rc == NITI_NO_ERROR && i > 0) rc = dgrad_layer(i, st);
+        if (rc != NITI_NO_ERROR) return rc;
         // NITI_SGD (NITI_SGD.hpp:20-54) for this layer is deferred: every layer's update runs
         // in one launch after the backward pass (the input gradients above read the old weights)
+        Layer& l = L[i];
+        const ConvGeom& g = l.g;
         jobs[i] = SgdJob{l.dwacc, rng(i, 2), RULE_WGRAD_BW2, g.c_out, g.c_in, g.kh * g.kw, g.cip, g.cop, l.w,
                          i > 0 ? l.wT : nullptr, l.g8};
     }
@@ -568,6 +700,50 @@ int niti_model_set_graph(niti_model_t m, int enable) {
     m->m.use_graph = enable != 0;
     return NITI_NO_ERROR;
 }
+
+int niti_model_autotune(niti_model_t m, int reps, void* stream) {
+    if (!m) return NITI_INVALID_VALUE;
+    return m->m.autotune((hipStream_t)stream, reps);
+}
+
+int niti_model_plan_info(niti_model_t m, int layer, int phase, int info[4]) {
+    if (!m || !info || layer < 0 || layer >= (int)m->m.L.size() || phase < 0 || phase > 2)
+        return NITI_INVALID_VALUE;
+    const niti::ConvGeom& g = m->m.L[layer].g;
+    const int op = phase == 0 ? niti::PLAN_FWD : phase == 1 ? niti::PLAN_DGRAD : niti::PLAN_WGRAD;
+    const niti::PlanChoice c =
+        niti::plan_query(niti::conv_plan_key(op, g), niti::conv_plan_k_step(op, g), phase != 2, m->m.slab_bytes);
+    info[0] = c.bm;
+    info[1] = c.bn;
+    info[2] = c.splits;
+    info[3] = c.strat;
+    return NITI_NO_ERROR;
+}
+
+int niti_model_plan_set(niti_model_t m, int layer, int phase, const int plan[4]) {
+    if (!m || layer < 0 || layer >= (int)m->m.L.size() || phase < 0 || phase > 2) return NITI_INVALID_VALUE;
+    const int op = phase == 0 ? niti::PLAN_FWD : phase == 1 ? niti::PLAN_DGRAD : niti::PLAN_WGRAD;
+    const niti::PlanKey k = niti::conv_plan_key(op, m->m.L[layer].g);
+    if (plan == nullptr) {
+        niti::plan_override_clear(k);
+    } else {
+        if ((plan[0] != 64 && plan[0] != 128) || (plan[1] != 64 && plan[1] != 128) || plan[2] < 1 || plan[3] < 0 ||
+            plan[3] > 2)
+            return NITI_INVALID_VALUE;
+        niti::PlanChoice c;
+        c.bm = plan[0];
+        c.bn = plan[1];
+        c.splits = plan[2];
+        c.strat = plan[3];
+        if (c.strat == 2 && !m->m.ensure_slab(std::min(niti::plan_slab_bytes(k.M, k.N, c.splits), size_t(1) << 30)))
+            return NITI_OUT_OF_MEMORY;
+        niti::plan_override_set(k, c);
+    }
+    m->m.drop_graph();
+    return NITI_NO_ERROR;
+}
+
+void niti_plan_reset(void) { niti::plan_override_clear_all(); }
 
 int niti_model_set_probe(niti_model_t m, int layer, int phase, int max_launches) {
     if (!m || max_launches < 0) return NITI_INVALID_VALUE;

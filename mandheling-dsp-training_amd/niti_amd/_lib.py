@@ -110,6 +110,10 @@ def lib():
         "niti_model_get_tap": (ci, [vp, ci, ci, vp, C.c_size_t, vp]),
         "niti_model_step_macs": (i64, [vp]),
         "niti_model_set_graph": (ci, [vp, ci]),
+        "niti_model_autotune": (ci, [vp, ci, vp]),
+        "niti_model_plan_info": (ci, [vp, ci, ci, C.POINTER(ci)]),
+        "niti_model_plan_set": (ci, [vp, ci, ci, C.POINTER(ci)]),
+        "niti_plan_reset": (None, []),
         "niti_model_set_probe": (ci, [vp, ci, ci, ci]),
         "niti_model_probe_read": (ci, [vp, C.POINTER(C.c_double), C.POINTER(ci)]),
         "niti_dp_get_unique_id": (ci, [C.c_char_p]),

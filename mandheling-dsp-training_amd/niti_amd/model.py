@@ -65,8 +65,36 @@ class NitiModel:
                                            _stream(stream)), "get_tap")
         return out
 
+    def autotune(self, reps: int = 5, stream=None):
+        """Time candidate GEMM plans per layer phase and keep the fastest (niti_model_autotune).
+        Call after one train_step; plans never change results."""
+        check(self._lib.niti_model_autotune(self._h, int(reps), _stream(stream)), "autotune")
+
+    def plans(self):
+        """{(layer, phase): (bm, bn, splits, strategy)}; phase 0 fwd / 1 input grad / 2 weight grad,
+        strategy 0 store / 1 recompute / 2 split-K."""
+        out = {}
+        for i in range(len(self.layers)):
+            for ph in (0, 1, 2):
+                if ph == 1 and i == 0:
+                    continue
+                info = (C.c_int * 4)()
+                check(self._lib.niti_model_plan_info(self._h, i, ph, info), "plan_info")
+                out[(i, ph)] = tuple(info)
+        return out
+
+    def set_plan(self, layer: int, phase: int, plan=None):
+        """Force (bm, bn, splits, strategy) for one layer phase; None restores the default."""
+        arr = None if plan is None else (C.c_int * 4)(*[int(v) for v in plan])
+        check(self._lib.niti_model_plan_set(self._h, layer, phase, arr), "plan_set")
+
+    @staticmethod
+    def reset_plans():
+        """Drop every plan override in this process."""
+        L.lib().niti_plan_reset()
+
     def set_graph(self, enable: bool):
-        """Replay the step as a hipGraph (default) or launch its kernels directly."""
+        """Replay the step as a hipGraph or launch its kernels directly (default)."""
         check(self._lib.niti_model_set_graph(self._h, int(enable)), "set_graph")
 
     def set_probe(self, layer: int, phase: int, max_launches: int = 256):

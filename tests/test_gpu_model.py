@@ -18,9 +18,10 @@ def T():
     return torch
 
 
-def _run(T, arch, layers, batch, steps=2, seed=5, graph=False, reuse_buffers=True):
+def _run(T, arch, layers, batch, steps=2, seed=5, graph=False, reuse_buffers=True, prepare=None):
     """reuse_buffers: new data goes into the same device tensors every step, so with graph=True
-    steps after the first replay the captured graph instead of re-capturing it."""
+    steps after the first replay the captured graph instead of re-capturing it.
+    prepare(model, x, labels): called after one throwaway step (weights are reset after it)."""
     import niti_model_ref as R
     from niti_amd.model import NitiModel
     rng = np.random.default_rng(seed)
@@ -28,11 +29,18 @@ def _run(T, arch, layers, batch, steps=2, seed=5, graph=False, reuse_buffers=Tru
     m = NitiModel(arch, batch)
     m.set_graph(graph)
     xd = ld = None
+    l0 = layers[0]
+    if prepare is not None:
+        xt = T.from_numpy(rng.integers(-127, 128, (batch, l0["ci"], l0["h"], l0["h"])).astype(np.int8)).cuda()
+        lt = T.from_numpy(rng.integers(0, 10, batch).astype(np.int32)).cuda()
+        for i, (w, s) in enumerate(zip(W, S)):
+            m.set_weight(i, w, s)
+        m.train_step(xt, -3, lt)
+        prepare(m, xt, lt)
     for i, (w, s) in enumerate(zip(W, S)):
         m.set_weight(i, w, s)
     for i in range(len(layers)):
         assert np.array_equal(m.get_weight(i), W[i])
-    l0 = layers[0]
     for step in range(steps):
         x = rng.integers(-127, 128, (batch, l0["ci"], l0["h"], l0["h"])).astype(np.int8)
         labels = rng.integers(0, 10, batch).astype(np.int32)
@@ -79,3 +87,45 @@ def test_vgg11_ragged_batch(T):
     import niti_amd
     import niti_model_ref as R
     _run(T, niti_amd.ARCH_VGG11, R.vgg11_layers(), batch=5, steps=1, seed=9)
+
+
+# Plans (tile shape, store / recompute / split-K count) change speed only: every forced plan and
+# the autotuned set must still reproduce the oracle bit for bit.
+PLANS = [(128, 128, 1, 0), (64, 64, 1, 1), (128, 64, 3, 2), (64, 128, 7, 2), (128, 128, 16, 2), (64, 64, 2, 2)]
+
+
+@pytest.mark.parametrize("pi", range(len(PLANS)))
+def test_vgg11_step_forced_plans(T, pi):
+    import niti_amd
+    import niti_model_ref as R
+    from niti_amd.model import NitiModel
+
+    def force(m, x, labels):
+        for i in range(len(m.layers)):
+            for ph in (0, 1, 2):
+                if not (ph == 1 and i == 0):
+                    m.set_plan(i, ph, PLANS[pi])
+
+    try:
+        _run(T, niti_amd.ARCH_VGG11, R.vgg11_layers(), batch=8, steps=1, seed=21 + pi, prepare=force)
+    finally:
+        NitiModel.reset_plans()
+
+
+def test_vgg11_step_autotuned(T):
+    import niti_amd
+    import niti_model_ref as R
+    from niti_amd.model import NitiModel
+    seen = {}
+
+    def tune(m, x, labels):
+        m.autotune(reps=1)
+        seen.update(m.plans())
+
+    try:
+        _run(T, niti_amd.ARCH_VGG11, R.vgg11_layers(), batch=8, steps=2, seed=3, prepare=tune)
+    finally:
+        NitiModel.reset_plans()
+    assert len(seen) == 3 * 9 - 1
+    for (bm, bn, splits, strat) in seen.values():
+        assert bm in (64, 128) and bn in (64, 128) and splits >= 1 and strat in (0, 1, 2)
