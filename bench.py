@@ -70,6 +70,7 @@ def main():
     ap.add_argument("--probe-phase", type=int, default=2, help="0 fwd, 1 input grad, 2 weight grad")
     ap.add_argument("--graph", action="store_true", help="replay the step as a hipGraph (slower on ROCm 7.2)")
     ap.add_argument("--no-autotune", action="store_true", help="keep the fixed default GEMM plans")
+    ap.add_argument("--no-overlap", action="store_true", help="weight gradients on the step stream")
     args = ap.parse_args()
 
     import numpy as np
@@ -90,6 +91,7 @@ def main():
     arch = niti_amd.ARCH_VGG11 if args.arch == "vgg11" else niti_amd.ARCH_LENET
     model = NitiModel(arch, args.batch)
     model.set_graph(args.graph)
+    model.set_overlap(not args.no_overlap)
     for i, (w, s) in enumerate(synth_weights(model.layers, seed=17)):
         model.set_weight(i, w, s)
     if world > 1:

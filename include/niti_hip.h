@@ -212,6 +212,10 @@ int64_t niti_model_step_macs(niti_model_t m);
 /* Replay the step as a hipGraph (single device only -- with a communicator attached the step
  * always runs as direct launches).  Default 0 (direct launches: measured faster on ROCm 7.2). */
 int niti_model_set_graph(niti_model_t m, int enable);
+/* Run the weight gradients on a second HIP stream, overlapping the input-gradient chain
+ * (default 1; the update waits for both; with a communicator it needs the second RCCL
+ * communicator attach_comm splits off, else the step stays on one stream). */
+int niti_model_set_overlap(niti_model_t m, int enable);
 /* Per-shape GEMM plan autotuning (no counterpart in the reference, whose CPU kernels have a
  * fixed blocking, NITI_Conv_Int8.cpp:159-253): times every layer phase under candidate plans
  * (tile shape, store / recompute / split-K count) on `stream` and keeps the fastest for this

@@ -86,8 +86,20 @@ struct Model {
     int8_t* x0 = nullptr;   // NHWC16 input
     int8_t* exp0 = nullptr; // input exponent
     int32_t* acc = nullptr; // shared fwd / dgrad accumulator
-    void* slab = nullptr;   // split-K slabs (shared, sequential on the stream)
+    void* slab = nullptr;   // split-K slabs of the forward / input-gradient GEMMs (step stream)
     size_t slab_bytes = 0;
+    void* slab_w = nullptr; // split-K slabs of the weight-gradient GEMMs (their own stream)
+    size_t slab_w_bytes = 0;
+    // The weight gradient of layer i and the input gradient of layer i both read dy_i and
+    // nothing else the other writes, so the weight gradients run on a second stream, each
+    // released by an event after its dy is produced, and overlap the input-gradient chain
+    // (the launches are small enough that one alone leaves most of the chip idle).  The SGD
+    // launch joins the two streams.
+    bool overlap = true;
+    hipStream_t side = nullptr;
+    std::vector<hipEvent_t> ev_dy;
+    hipEvent_t ev_side = nullptr;
+    ncclComm_t comm_w = nullptr;  // the side stream's collectives (split from comm)
     uint32_t* amax = nullptr;  // 3 ranges per layer (forward, input gradient, weight gradient)
     size_t amax_bytes = 0;
     uint32_t* rng(int layer, int which) { return amax + (size_t)(3 * layer + which) * MAX_WORDS; }
@@ -168,15 +180,27 @@ struct Model {
     int wgrad_layer(int i, hipStream_t st);
     int dgrad_layer(int i, hipStream_t st);
     int autotune(hipStream_t st, int reps);
-    // grow the split-K workspace (the old one stays owned by ws until the model is destroyed)
-    bool ensure_slab(size_t bytes) {
-        if (slab_bytes >= bytes) return true;
+    // grow a split-K workspace (the old one stays owned by ws until the model is destroyed)
+    bool ensure_slab(size_t bytes, bool wgrad) {
+        void*& p = wgrad ? slab_w : slab;
+        size_t& have = wgrad ? slab_w_bytes : slab_bytes;
+        if (have >= bytes) return true;
         if (hipDeviceSynchronize() != hipSuccess) return false;
         void* s2 = ws.alloc(bytes);
         if (!s2) return false;
-        slab = s2;
-        slab_bytes = bytes;
+        p = s2;
+        have = bytes;
         return true;
+    }
+    size_t ws_bytes_for(int op) const { return op == PLAN_WGRAD ? slab_w_bytes : slab_bytes; }
+    int ensure_streams() {
+        if (side) return NITI_NO_ERROR;
+        if (hipStreamCreateWithFlags(&side, hipStreamNonBlocking) != hipSuccess) return NITI_NO_EXECUTION;
+        if (hipEventCreateWithFlags(&ev_side, hipEventDisableTiming) != hipSuccess) return NITI_NO_EXECUTION;
+        ev_dy.resize(L.size());
+        for (auto& e : ev_dy)
+            if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return NITI_NO_EXECUTION;
+        return NITI_NO_ERROR;
     }
     int run(const int8_t* x_nchw, int exp_in, const int32_t* labels, hipStream_t st);
     int step(const int8_t* x_nchw, int exp_in, const int32_t* labels, hipStream_t st);
@@ -186,6 +210,10 @@ struct Model {
         if (gin) (void)hipEventDestroy(gin);
         if (gout) (void)hipEventDestroy(gout);
         if (gstream) (void)hipStreamDestroy(gstream);
+        for (auto e : ev_dy) (void)hipEventDestroy(e);
+        if (ev_side) (void)hipEventDestroy(ev_side);
+        if (side) (void)hipStreamDestroy(side);
+        if (comm_w) (void)ncclCommDestroy(comm_w);
         if (comm) (void)ncclCommDestroy(comm);
     }
 };
@@ -270,7 +298,7 @@ int Model::build(int arch_, int batch_) {
         acc_elems = std::max(acc_elems, (size_t)n * g.h * g.w * g.cip);
         slab_bytes = std::max(slab_bytes, conv_fwd_workspace(g));
         slab_bytes = std::max(slab_bytes, conv_dgrad_workspace(g));
-        slab_bytes = std::max(slab_bytes, conv_wgrad_workspace(g));
+        slab_w_bytes = std::max(slab_w_bytes, conv_wgrad_workspace(g));
         // layer input / its C alignment with the previous output
         if (i == 0) {
             l.in = x0;
@@ -283,6 +311,10 @@ int Model::build(int arch_, int batch_) {
     if (slab_bytes) {
         slab = ws.alloc(slab_bytes);
         if (!slab) return NITI_OUT_OF_MEMORY;
+    }
+    if (slab_w_bytes) {
+        slab_w = ws.alloc(slab_w_bytes);
+        if (!slab_w) return NITI_OUT_OF_MEMORY;
     }
     amax_bytes = (size_t)3 * nl * MAX_BYTES;
     amax = (uint32_t*)ws.alloc(amax_bytes);
@@ -388,10 +420,10 @@ int Model::wgrad_layer(int i, hipStream_t st) {
     const int64_t we = l.w_elems();
     // the weight-gradient probe brackets the GEMM launch alone (not its split-K reduce)
     probe(i, 2, true, st);
-    MTRY(conv_wgrad_acc(g, l.in, l.dy, l.dwacc, dp ? nullptr : rng(i, 2), slab, slab_bytes, st,
+    MTRY(conv_wgrad_acc(g, l.in, l.dy, l.dwacc, dp ? nullptr : rng(i, 2), slab_w, slab_w_bytes, st,
                         probe_end_event(i, 2)));
     if (dp) {
-        CTRY(ncclAllReduce(l.dwacc, l.dwacc, (size_t)we, ncclInt32, ncclSum, comm, st));
+        CTRY(ncclAllReduce(l.dwacc, l.dwacc, (size_t)we, ncclInt32, ncclSum, st == side ? comm_w : comm, st));
         MTRY(absmax_i32(l.dwacc, we, rng(i, 2), st));
     }
     return NITI_NO_ERROR;
@@ -456,7 +488,8 @@ int Model::dgrad_layer(int i, hipStream_t st) {
 int Model::autotune(hipStream_t st, int reps) {
     if (reps < 1) reps = 5;
     const int nl = (int)L.size();
-    if (!ensure_slab(size_t(96) << 20)) return NITI_OUT_OF_MEMORY;  // split-K room for the candidates
+    // split-K room for the candidates
+    if (!ensure_slab(size_t(96) << 20, false) || !ensure_slab(size_t(96) << 20, true)) return NITI_OUT_OF_MEMORY;
     drop_graph();
     hipEvent_t ev[4];
     for (auto& e : ev)
@@ -494,7 +527,8 @@ int Model::autotune(hipStream_t st, int reps) {
             const int steps = (key.K + k_step - 1) / k_step;
             const bool act = op != PLAN_WGRAD;
             plan_override_clear(key);
-            PlanChoice best = plan_query(key, k_step, act, slab_bytes);
+            const size_t wsb = ws_bytes_for(op);
+            PlanChoice best = plan_query(key, k_step, act, wsb);
             float best_us = 0.f;
             rc = time_op(i, op, &best_us);
             for (const auto& t : tiles) {
@@ -511,7 +545,7 @@ int Model::autotune(hipStream_t st, int reps) {
                     cands.push_back(c);
                 }
                 for (int s : split_opts) {
-                    if (s > steps / 2 || plan_slab_bytes(key.M, key.N, s) > slab_bytes) break;
+                    if (s > steps / 2 || plan_slab_bytes(key.M, key.N, s) > wsb) break;
                     c.strat = 2;
                     c.splits = s;
                     cands.push_back(c);
@@ -553,8 +587,20 @@ int Model::run(const int8_t* x_nchw, int exp_in, const int32_t* labels, hipStrea
         Layer& t = L[nl - 1];
         MTRY(loss_grad(t.r, n, t.g.c_out, t.g.cop, t.exp, labels, t.dy, st));
     }
+    // weight gradients on the side stream (not inside a graph capture, and in data-parallel
+    // runs only with a second communicator for it)
+    const bool ov = overlap && !capturing && (comm == nullptr || comm_w != nullptr);
+    if (ov) {
+        const int rc = ensure_streams();
+        if (rc != NITI_NO_ERROR) return rc;
+    }
+    hipStream_t wst = ov ? side : st;
     for (int i = nl - 1; i >= 0; --i) {
-        int rc = wgrad_layer(i, st);
+        if (ov) {  // dy_i is ready on the step stream
+            MTRY(hipEventRecord(ev_dy[i], st));
+            MTRY(hipStreamWaitEvent(side, ev_dy[i], 0));
+        }
+        int rc = wgrad_layer(i, wst);
         if (rc == NITI_NO_ERROR && i > 0) rc = dgrad_layer(i, st);
         if (rc != NITI_NO_ERROR) return rc;
         // NITI_SGD (NITI_SGD.hpp:20-54) for this layer is deferred: every layer's update runs
@@ -563,6 +609,10 @@ int Model::run(const int8_t* x_nchw, int exp_in, const int32_t* labels, hipStrea
         const ConvGeom& g = l.g;
         jobs[i] = SgdJob{l.dwacc, rng(i, 2), RULE_WGRAD_BW2, g.c_out, g.c_in, g.kh * g.kw, g.cip, g.cop, l.w,
                          i > 0 ? l.wT : nullptr, l.g8};
+    }
+    if (ov) {  // every weight gradient is in before the update
+        MTRY(hipEventRecord(ev_side, side));
+        MTRY(hipStreamWaitEvent(st, ev_side, 0));
     }
     MTRY(sgd_update_many(jobs, nl, st));
     return NITI_NO_ERROR;
@@ -694,6 +744,12 @@ int64_t niti_model_step_macs(niti_model_t m) {
     return s;
 }
 
+int niti_model_set_overlap(niti_model_t m, int enable) {
+    if (!m) return NITI_INVALID_VALUE;
+    m->m.overlap = enable != 0;
+    return NITI_NO_ERROR;
+}
+
 int niti_model_set_graph(niti_model_t m, int enable) {
     if (!m) return NITI_INVALID_VALUE;
     m->m.drop_graph();
@@ -712,7 +768,7 @@ int niti_model_plan_info(niti_model_t m, int layer, int phase, int info[4]) {
     const niti::ConvGeom& g = m->m.L[layer].g;
     const int op = phase == 0 ? niti::PLAN_FWD : phase == 1 ? niti::PLAN_DGRAD : niti::PLAN_WGRAD;
     const niti::PlanChoice c =
-        niti::plan_query(niti::conv_plan_key(op, g), niti::conv_plan_k_step(op, g), phase != 2, m->m.slab_bytes);
+        niti::plan_query(niti::conv_plan_key(op, g), niti::conv_plan_k_step(op, g), phase != 2, m->m.ws_bytes_for(op));
     info[0] = c.bm;
     info[1] = c.bn;
     info[2] = c.splits;
@@ -735,7 +791,8 @@ int niti_model_plan_set(niti_model_t m, int layer, int phase, const int plan[4])
         c.bn = plan[1];
         c.splits = plan[2];
         c.strat = plan[3];
-        if (c.strat == 2 && !m->m.ensure_slab(std::min(niti::plan_slab_bytes(k.M, k.N, c.splits), size_t(1) << 30)))
+        if (c.strat == 2 &&
+            !m->m.ensure_slab(std::min(niti::plan_slab_bytes(k.M, k.N, c.splits), size_t(1) << 30), op == niti::PLAN_WGRAD))
             return NITI_OUT_OF_MEMORY;
         niti::plan_override_set(k, c);
     }
@@ -790,6 +847,11 @@ int niti_model_attach_comm(niti_model_t m, const char id[NITI_UNIQUE_ID_BYTES], 
     ncclComm_t c = nullptr;
     if (ncclCommInitRank(&c, world, u, rank) != ncclSuccess) return NITI_NO_EXECUTION;
     m->m.comm = c;
+    // a second communicator for the weight-gradient all-reduces on the side stream (collectives
+    // of one communicator must not be issued from two streams at once); without it the weight
+    // gradients stay on the step stream
+    ncclComm_t cw = nullptr;
+    if (world > 1 && ncclCommSplit(c, 0, rank, &cw, nullptr) == ncclSuccess) m->m.comm_w = cw;
     m->m.world = world;
     m->m.rank = rank;
     m->m.exact = exact ? 1 : 0;

@@ -111,6 +111,7 @@ def lib():
         "niti_model_step_macs": (i64, [vp]),
         "niti_model_set_graph": (ci, [vp, ci]),
         "niti_model_autotune": (ci, [vp, ci, vp]),
+        "niti_model_set_overlap": (ci, [vp, ci]),
         "niti_model_plan_info": (ci, [vp, ci, ci, C.POINTER(ci)]),
         "niti_model_plan_set": (ci, [vp, ci, ci, C.POINTER(ci)]),
         "niti_plan_reset": (None, []),

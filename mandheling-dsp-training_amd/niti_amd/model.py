@@ -93,6 +93,10 @@ class NitiModel:
         """Drop every plan override in this process."""
         L.lib().niti_plan_reset()
 
+    def set_overlap(self, enable: bool):
+        """Weight gradients on a second stream overlapping the input gradients (default on)."""
+        check(self._lib.niti_model_set_overlap(self._h, int(enable)), "set_overlap")
+
     def set_graph(self, enable: bool):
         """Replay the step as a hipGraph or launch its kernels directly (default)."""
         check(self._lib.niti_model_set_graph(self._h, int(enable)), "set_graph")

@@ -18,7 +18,7 @@ def T():
     return torch
 
 
-def _run(T, arch, layers, batch, steps=2, seed=5, graph=False, reuse_buffers=True, prepare=None):
+def _run(T, arch, layers, batch, steps=2, seed=5, graph=False, reuse_buffers=True, prepare=None, overlap=True):
     """reuse_buffers: new data goes into the same device tensors every step, so with graph=True
     steps after the first replay the captured graph instead of re-capturing it.
     prepare(model, x, labels): called after one throwaway step (weights are reset after it)."""
@@ -28,6 +28,7 @@ def _run(T, arch, layers, batch, steps=2, seed=5, graph=False, reuse_buffers=Tru
     W, S = R.init_weights(layers, seed=seed)
     m = NitiModel(arch, batch)
     m.set_graph(graph)
+    m.set_overlap(overlap)
     xd = ld = None
     l0 = layers[0]
     if prepare is not None:
@@ -81,6 +82,12 @@ def test_vgg11_step_matches_oracle(T):
     import niti_amd
     import niti_model_ref as R
     _run(T, niti_amd.ARCH_VGG11, R.vgg11_layers(), batch=8, steps=2)
+
+
+def test_vgg11_step_single_stream(T):
+    import niti_amd
+    import niti_model_ref as R
+    _run(T, niti_amd.ARCH_VGG11, R.vgg11_layers(), batch=8, steps=2, seed=6, overlap=False)
 
 
 def test_vgg11_ragged_batch(T):

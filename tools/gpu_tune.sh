@@ -6,7 +6,7 @@ timeout -k 10 600 python -m pytest tests -m gpu -x -q -p no:cacheprovider > gpur
 rc=$?
 echo "pytest rc=$rc"; tail -15 gpurun_out/pytest_gpu_tune.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-for flag in "" "--no-autotune" ""; do
+for flag in "" "--no-overlap" "--no-autotune" ""; do
   timeout -k 10 300 python bench.py --steps 30 --warmup 5 --cpu-sample 0 $flag > gpurun_out/bench_tune.log 2>&1
   rc=$?; echo "bench [$flag] rc=$rc"; tail -2 gpurun_out/bench_tune.log
   if [ $rc -ne 0 ]; then exit $rc; fi
