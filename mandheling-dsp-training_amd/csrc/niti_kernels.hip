@@ -1715,6 +1715,163 @@ __global__ void requant_act_kernel(ActRequant r) {
     }
 }
 
+// Streaming requantisation (the training step's path; out_c4 uses requant_act_kernel above).
+// A unit is 4 channels (one 16-byte int32 load, one 4-byte int8 store): consecutive lanes take
+// consecutive channel quads, so every wave instruction moves whole contiguous runs (a full
+// 1 KiB of accumulator per load), and each thread keeps RQ_U units' loads in flight.
+//   RQ_PLAIN     unit over [rows][ldc/4]: out = requant (+relu) (& relu_mask > 0)
+//   RQ_POOL_FWD  unit over [pooled pixel][ldc/4]: requant (+relu) the 2x2 window -> out, max -> pool_out
+//   RQ_POOL_BWD  unit over [pooled pixel = row][ldc/4]: requant, route to the window's first max
+//                of x (relu: and x > 0) in dx, zero elsewhere (+ optional out)
+enum { RQ_PLAIN = 0, RQ_POOL_FWD = 1, RQ_POOL_BWD = 2 };
+constexpr int RQ_U = 4;
+
+struct RqGeom {
+    FastDiv fq, fpw, fph;  // by quads per row, pooled width, pooled height
+    int qpr, W;            // quads per row, pre-pool width
+    uint32_t units;
+};
+
+__device__ __forceinline__ uint32_t rq4(v4i v, bool raw, int s, int relu) {
+    uint32_t o = 0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        int32_t q = raw ? (int32_t)(int8_t)v[e] : psto_fast(v[e], s);
+        if (relu && q < 0) q = 0;
+        o |= ((uint32_t)q & 0xffu) << (8 * e);
+    }
+    return o;
+}
+__device__ __forceinline__ uint32_t bmax4(uint32_t a, uint32_t b) {
+    uint32_t o = 0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const int x = (int8_t)(a >> (8 * e)), y = (int8_t)(b >> (8 * e));
+        o |= ((uint32_t)(x > y ? x : y) & 0xffu) << (8 * e);
+    }
+    return o;
+}
+
+template <int MODE>
+__global__ void __launch_bounds__(256) requant_quad_kernel(ActRequant r, RqGeom g) {
+    const int bw = bitwidth_of(read_max(r.amax));  // whole wave active
+    const int shift = bw - 7;
+    const int s = shift > 1 ? shift : 2;
+    const bool raw = shift <= 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0 && r.exp_out != nullptr) {
+        const int inc = shift > 1 ? shift : (shift == 1 ? 2 : 0);
+        const int ein = r.exp_in ? (int)*r.exp_in : 0;
+        const int ws = r.wscale ? (int)*r.wscale : 0;
+        *r.exp_out = (int8_t)(ein + ws + inc);
+    }
+    const uint32_t stride = gridDim.x * 256u;
+    const int ldc = r.ldc;
+    for (uint32_t u0 = blockIdx.x * 256u + threadIdx.x; u0 < g.units; u0 += stride * RQ_U) {
+        if (MODE == RQ_PLAIN) {
+            v4i v[RQ_U];
+            uint32_t mk[RQ_U];
+#pragma unroll
+            for (int j = 0; j < RQ_U; ++j) {
+                const uint32_t u = u0 + j * stride;
+                v[j] = u < g.units ? __builtin_nontemporal_load((const v4i*)r.acc + u) : v4i{0, 0, 0, 0};
+                mk[j] = (r.relu_mask != nullptr && u < g.units) ? ((const uint32_t*)r.relu_mask)[u] : 0x01010101u;
+            }
+#pragma unroll
+            for (int j = 0; j < RQ_U; ++j) {
+                const uint32_t u = u0 + j * stride;
+                if (u >= g.units) break;
+                uint32_t o = rq4(v[j], raw, s, r.relu);
+                if (r.relu_mask != nullptr) {
+                    uint32_t keep = 0;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        if ((int8_t)(mk[j] >> (8 * e)) > 0) keep |= 0xffu << (8 * e);
+                    o &= keep;
+                }
+                ((uint32_t*)r.out_nhwc16)[u] = o;
+            }
+        } else {
+            // window rows of each unit
+            int64_t wrow[RQ_U];
+            uint32_t pp_[RQ_U];
+            int cq_[RQ_U];
+#pragma unroll
+            for (int j = 0; j < RQ_U; ++j) {
+                const uint32_t u = u0 + j * stride;
+                const uint32_t uu = u < g.units ? u : 0u;
+                const uint32_t pp = fdiv(g.fq, uu);
+                cq_[j] = (int)(uu - pp * (uint32_t)g.qpr);
+                const uint32_t rest = fdiv(g.fpw, pp);
+                const int px = (int)(pp - rest * g.fpw.d);
+                const uint32_t b = fdiv(g.fph, rest);
+                const int py = (int)(rest - b * g.fph.d);
+                wrow[j] = ((int64_t)b * (2 * g.fph.d) + 2 * py) * g.W + 2 * px;
+                pp_[j] = pp;
+            }
+            if (MODE == RQ_POOL_FWD) {
+                v4i v[RQ_U][4];
+#pragma unroll
+                for (int j = 0; j < RQ_U; ++j)
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const int64_t row = wrow[j] + (k & 1) + (k >> 1) * g.W;
+                        v[j][k] = u0 + j * stride < g.units
+                                      ? __builtin_nontemporal_load((const v4i*)(r.acc + row * ldc) + cq_[j])
+                                      : v4i{0, 0, 0, 0};
+                    }
+#pragma unroll
+                for (int j = 0; j < RQ_U; ++j) {
+                    if (u0 + j * stride >= g.units) break;
+                    uint32_t mx = 0x80808080u;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const int64_t row = wrow[j] + (k & 1) + (k >> 1) * g.W;
+                        const uint32_t o = rq4(v[j][k], raw, s, r.relu);
+                        ((uint32_t*)(r.out_nhwc16 + row * ldc))[cq_[j]] = o;
+                        mx = bmax4(mx, o);
+                    }
+                    ((uint32_t*)(r.pool.pool_out + (int64_t)pp_[j] * ldc))[cq_[j]] = mx;
+                }
+            } else {
+                v4i v[RQ_U];
+                uint32_t yv[RQ_U], xv[RQ_U][4];
+#pragma unroll
+                for (int j = 0; j < RQ_U; ++j) {
+                    const bool ok = u0 + j * stride < g.units;
+                    v[j] = ok ? __builtin_nontemporal_load((const v4i*)(r.acc + (int64_t)pp_[j] * ldc) + cq_[j])
+                              : v4i{0, 0, 0, 0};
+                    yv[j] = ok ? ((const uint32_t*)(r.pool.y + (int64_t)pp_[j] * ldc))[cq_[j]] : 0u;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const int64_t row = wrow[j] + (k & 1) + (k >> 1) * g.W;
+                        xv[j][k] = ok ? ((const uint32_t*)(r.pool.x + row * ldc))[cq_[j]] : 0u;
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < RQ_U; ++j) {
+                    if (u0 + j * stride >= g.units) break;
+                    const uint32_t q = rq4(v[j], raw, s, 0);
+                    if (r.out_nhwc16 != nullptr) ((uint32_t*)(r.out_nhwc16 + (int64_t)pp_[j] * ldc))[cq_[j]] = q;
+                    uint32_t done = 0;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        uint32_t o = 0;
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            const int x = (int8_t)(xv[j][k] >> (8 * e)), m = (int8_t)(yv[j] >> (8 * e));
+                            const bool take = !((done >> e) & 1u) && x >= m;
+                            if (take) done |= 1u << e;
+                            if (take && !(r.pool.relu && x <= 0)) o |= q & (0xffu << (8 * e));
+                        }
+                        const int64_t row = wrow[j] + (k & 1) + (k >> 1) * g.W;
+                        ((uint32_t*)(r.pool.dx + row * ldc))[cq_[j]] = o;
+                    }
+                }
+            }
+        }
+    }
+}
+
 hipError_t requant_act(const ActRequant& r, hipStream_t st) {
     if (r.ldc % 16 != 0 || r.acc == nullptr || r.amax == nullptr) return hipErrorInvalidValue;
     if (r.pool.pool_out != nullptr || r.pool.dx != nullptr) {
@@ -1724,6 +1881,32 @@ hipError_t requant_act(const ActRequant& r, hipStream_t st) {
         if (r.pool.dx != nullptr && (r.pool.x == nullptr || r.pool.y == nullptr ||
                                      r.rows % ((int64_t)(r.pool.H / 2) * (r.pool.W / 2))))
             return hipErrorInvalidValue;
+    }
+    if (r.out_c4 == nullptr) {
+        const bool pf = r.pool.pool_out != nullptr, pb = r.pool.dx != nullptr;
+        if (!pf && !pb && r.out_nhwc16 == nullptr) return hipErrorInvalidValue;
+        RqGeom g;
+        g.qpr = r.ldc / 4;
+        g.W = r.pool.W;
+        const int64_t rows = pf ? r.rows / 4 : r.rows;  // pooled pixels for the pool modes
+        const int64_t units = rows * g.qpr;
+        if (units >= (int64_t)1 << 31) return hipErrorInvalidValue;
+        g.units = (uint32_t)units;
+        g.fq = make_fastdiv((uint32_t)g.qpr);
+        if (pf || pb) {
+            g.fpw = make_fastdiv((uint32_t)(r.pool.W / 2));
+            g.fph = make_fastdiv((uint32_t)(r.pool.H / 2));
+        }
+        int64_t blocks = (units + 256 * RQ_U - 1) / (256 * RQ_U);
+        if (blocks > 2048) blocks = 2048;
+        if (blocks < 1) blocks = 1;
+        if (pf)
+            hipLaunchKernelGGL(requant_quad_kernel<RQ_POOL_FWD>, dim3((unsigned)blocks), dim3(256), 0, st, r, g);
+        else if (pb)
+            hipLaunchKernelGGL(requant_quad_kernel<RQ_POOL_BWD>, dim3((unsigned)blocks), dim3(256), 0, st, r, g);
+        else
+            hipLaunchKernelGGL(requant_quad_kernel<RQ_PLAIN>, dim3((unsigned)blocks), dim3(256), 0, st, r, g);
+        return hipGetLastError();
     }
     const int64_t total = r.rows * (r.ldc / 16);
     int64_t blocks = (total + 255) / 256;

@@ -36,7 +36,15 @@ print("\nlast step launches (from the forward of the step):")
 first = next(i for i, r in enumerate(rows) if i > prev and "NchwToNhwc16" in r["Kernel_Name"])
 seg = rows[first:]
 span = (int(seg[-1]["End_Timestamp"]) - int(seg[0]["Start_Timestamp"])) / 1e3
+t0 = int(seg[0]["Start_Timestamp"])
+qcol = "Queue_Id" if "Queue_Id" in seg[0] else ("Stream_Id" if "Stream_Id" in seg[0] else None)
+last_end = {}
+print(f"{'start':>8} {'dur':>7} {'gap':>6}  q  grid        kernel")
 for r in seg:
     g = f"{int(r['Grid_Size_X']) // int(r['Workgroup_Size_X'])}x{r['Grid_Size_Y']}"
-    print(f"{dur(r):8.2f} us  grid {g:>10}  {short(r['Kernel_Name'])}")
-print("step span us", span, "busy", sum(dur(r) for r in seg))
+    q = r[qcol] if qcol else "-"
+    s0, e0 = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+    gap = (s0 - last_end[q]) / 1e3 if q in last_end else 0.0
+    last_end[q] = e0
+    print(f"{(s0 - t0) / 1e3:8.2f} {dur(r):7.2f} {gap:6.2f} {q:>2}  {g:>10}  {short(r['Kernel_Name'])}")
+print("step span us", span, "busy", sum(dur(r) for r in seg), "launches", len(seg))
