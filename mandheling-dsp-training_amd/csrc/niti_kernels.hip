@@ -284,6 +284,11 @@ __device__ __forceinline__ int xcd_remap(int b, int nwg) {
 // REQUANT: the int8 tile is staged in LDS ([BM][BN + 16] bytes) and written out as 16-byte
 // row chunks (the MFMA C layout gives each lane one column of 16 rows, i.e. byte stores);
 // the relu-grad mask is applied in the same pass.
+// whether the STORE / SLAB epilogue stages the int32 tile through LDS (tiles up to 128 x 128)
+constexpr bool epi_stage_c(int mode, int bm, int bn) {
+    return (mode == EPI_STORE || mode == EPI_SLAB) && bm * (bn + 4) * 4 <= 72 * 1024;
+}
+
 template <int TM, int TN, int NW, int MODE, int BM, int BN>
 __device__ __forceinline__ void gemm_epilogue(v16i (&acc)[TM][TN], int r0, int c0, int M, int N, const Epi& epi,
                                               int8_t* smem, int split, int m0, int n0) {
@@ -304,6 +309,9 @@ __device__ __forceinline__ void gemm_epilogue(v16i (&acc)[TM][TN], int r0, int c
         }
     }
     int32_t* Cs = MODE == EPI_SLAB ? epi.C + (int64_t)split * epi.slab_stride : epi.C;
+    constexpr bool STAGE_C = epi_stage_c(MODE, BM, BN);
+    constexpr int LDT = BN + 4;  // int32 row pitch of the staged C tile (STORE / SLAB)
+    int32_t* ctile = (int32_t*)smem;
     uint32_t lmax = 0;
 #pragma unroll
     for (int a = 0; a < TM; ++a)
@@ -314,8 +322,9 @@ __device__ __forceinline__ void gemm_epilogue(v16i (&acc)[TM][TN], int r0, int c
             for (int i = 0; i < 16; ++i) {
                 const int row = r0 + a * 32 + (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
                 const int v = acc[a][b][i];
+                if (STAGE_C) ctile[(row - m0) * LDT + (col - n0)] = v;
                 if (row < M && col < N) {
-                    if (MODE == EPI_STORE || MODE == EPI_SLAB) Cs[(int64_t)row * epi.ldc + col] = v;
+                    if (!STAGE_C && (MODE == EPI_STORE || MODE == EPI_SLAB)) Cs[(int64_t)row * epi.ldc + col] = v;
                     if (MODE == EPI_STORE || MODE == EPI_AMAX) {
                         const uint32_t u = uabs32(v);
                         lmax = lmax > u ? lmax : u;
@@ -346,9 +355,22 @@ __device__ __forceinline__ void gemm_epilogue(v16i (&acc)[TM][TN], int r0, int c
             }
         }
     }
+    if (STAGE_C) {
+        // the int32 tile leaves as whole 16-byte row chunks (one dword per lane per MFMA row
+        // would be 4x the store instructions, and store issue bounds this epilogue)
+        __syncthreads();
+        constexpr int CPR = BN / 4;
+        for (int t = tid; t < BM * CPR; t += NW * 64) {
+            const int rl = t / CPR, cl = (t - rl * CPR) * 4;
+            const int row = m0 + rl, col = n0 + cl;
+            if (row < M && col < N)  // N is a multiple of 16
+                *(v4i*)(Cs + (int64_t)row * epi.ldc + col) = *(const v4i*)(ctile + rl * LDT + cl);
+        }
+    }
     if (MODE == EPI_STORE || MODE == EPI_AMAX) {
         lmax = wave_max(lmax);
-        uint32_t* red = (uint32_t*)smem;  // all LDS reads finished at the last barrier
+        __syncthreads();  // LDS reads of the staged tile / the last K step are finished
+        uint32_t* red = (uint32_t*)smem;
         if (lane == 0) red[wid] = lmax;
         __syncthreads();
         if (tid == 0) {
@@ -390,7 +412,7 @@ __device__ __forceinline__ uint32_t fdiv(const FastDiv& f, uint32_t n) { return 
 // banks once.
 template <int BW>
 __device__ __forceinline__ int kt_swz(int r) {
-    return BW == 128 ? ((r >> 1) & 3) * 2 : (BW == 64 ? ((r >> 2) & 1) * 2 : 0);
+    return BW == 256 ? (r & 7) * 2 : (BW == 128 ? ((r >> 1) & 3) * 2 : (BW == 64 ? ((r >> 2) & 1) * 2 : 0));
 }
 template <int BW>
 __device__ __forceinline__ int kt_off16(int r, int c) { return r * BW + ((c ^ kt_swz<BW>(r)) << 4); }
@@ -712,8 +734,14 @@ struct KtIm2colU {
 // All LDS lives in one __shared__ array and the loop issues no register loads, so hipcc has
 // no reason to drain vmcnt early (cdna_hip_programming.md §5, "Pipelining across barriers").
 // =====================================================================================
-constexpr int LDS_STAGE_BUDGET = 64 * 1024;  // pipeline depth = min(MAX_STAGES, budget / stage bytes)
-constexpr int MAX_STAGES = 4;               // (deeper pipelines measured no faster at one block per CU)
+#ifndef NITI_LDS_BUDGET_KB
+#define NITI_LDS_BUDGET_KB 96
+#endif
+#ifndef NITI_MAX_STAGES
+#define NITI_MAX_STAGES 4
+#endif
+constexpr int LDS_STAGE_BUDGET = NITI_LDS_BUDGET_KB * 1024;  // pipeline depth = min(MAX_STAGES, budget / stage bytes)
+constexpr int MAX_STAGES = NITI_MAX_STAGES;
 #ifndef NITI_ABLATE
 #define NITI_ABLATE 0  // diagnostic builds only: 1 = no global->LDS copies, 2 = no MFMA,
                        // 3 = no copies and no per-step barrier, 4 = no per-step barrier
@@ -782,9 +810,10 @@ __device__ __forceinline__ int swz16(int r) {
 template <int BM, int BN, int WM, int WN, class LA, class LB, int MODE, bool KT, int NW>
 __global__ void __launch_bounds__(NW * 64) gemm_kernel(LA la, LB lb, int M, int N, int tiles_n, int k_total,
                                                         int k_per_split, Epi epi) {
-    static_assert(WM * WN == 4, "4 wave positions");
+    constexpr int WP = WM * WN;  // wave positions over the output tile
     static_assert(NW == 4 || NW == 8, "4 or 8 waves");
-    constexpr int KG = NW / 4;  // wave groups splitting each step's K sub-steps
+    static_assert(NW % WP == 0 && NW / WP <= 2, "one or two wave groups");
+    constexpr int KG = NW / WP;  // wave groups splitting each step's K sub-steps
     constexpr int TM = BM / WM / 32;
     constexpr int TN = BN / WN / 32;
     // staging geometry: rows x row-bytes per operand tile
@@ -804,14 +833,16 @@ __global__ void __launch_bounds__(NW * 64) gemm_kernel(LA la, LB lb, int M, int 
     constexpr int KW_ = KSUB / KG;                 // sub-steps per wave per step
     static_assert(KSUB % KG == 0, "sub-steps split evenly");
     constexpr int XCH_BYTES = KG > 1 ? NW * (TM / 2) * TN * 64 * 64 : 0;  // accumulator exchange
-    constexpr int SMEM = STAGES * STAGE_BYTES > XCH_BYTES ? STAGES * STAGE_BYTES : XCH_BYTES;
+    constexpr int SMEM0 = STAGES * STAGE_BYTES > XCH_BYTES ? STAGES * STAGE_BYTES : XCH_BYTES;
+    constexpr int CT_BYTES = epi_stage_c(MODE, BM, BN) ? BM * (BN + 4) * 4 : 0;  // staged C tile
+    constexpr int SMEM = SMEM0 > CT_BYTES ? SMEM0 : CT_BYTES;
     static_assert(SMEM >= BM * (BN + 16), "requant epilogue staging fits in the pipeline's LDS");
     __shared__ __attribute__((aligned(16))) int8_t smem[SMEM];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: LDS bases stay scalar
-    const int kg = wid >> 2, wq = wid & 3;
+    const int kg = wid / WP, wq = wid % WP;
     const int wm = wq / WN, wn = wq % WN;
     // XCD-aware tile order inside each K split.  (A split-major order over the whole grid, which
     // keeps one K range per XCD and cuts the weight gradient's HBM fetch ~8x, measured slower.)
@@ -995,7 +1026,7 @@ __global__ void __launch_bounds__(NW * 64) gemm_kernel(LA la, LB lb, int M, int 
                     xbuf[((wid * TH + a) * TN + b) * 256 + q * 64 + lane] = v4i{t[4 * q], t[4 * q + 1], t[4 * q + 2], t[4 * q + 3]};
                 }
         __syncthreads();
-        const int partner = (1 - kg) * 4 + wq;
+        const int partner = (1 - kg) * WP + wq;
         const int keep_a = kg == 0 ? 0 : TH;
         v16i keep[TH][TN];
 #pragma unroll
@@ -1139,8 +1170,8 @@ static GemmPlan plan_gemm(int M, int N, int k_total, int k_step, int k_bytes, bo
     p.kc_per_split = steps * k_step;
     PlanChoice c;
     if (op >= 0 && plan_override_get(PlanKey{op, M, N, k_total}, &c)) {
-        p.bm = c.bm == 64 ? 64 : 128;
-        p.bn = c.bn == 64 ? 64 : 128;
+        p.bm = c.bm == 64 ? 64 : (c.bm == 256 ? 256 : 128);
+        p.bn = c.bn == 64 ? 64 : (c.bn == 256 ? 256 : 128);
         p.tiles = ((M + p.bm - 1) / p.bm) * ((N + p.bn - 1) / p.bn);
         if (c.strat == STRAT_SLAB) {
             plan_slab(p, c.splits, k_total, k_step, steps, false, M, N, ws_elems);
@@ -1156,6 +1187,9 @@ static GemmPlan plan_gemm(int M, int N, int k_total, int k_step, int k_bytes, bo
         if (v == 64 || v == 6464) p.bm = p.bn = 64;
         if (v == 12864) { p.bm = 128; p.bn = 64; }
         if (v == 64128) { p.bm = 64; p.bn = 128; }
+        if (v == 256128) { p.bm = 256; p.bn = 128; }
+        if (v == 128256) { p.bm = 128; p.bn = 256; }
+        if (v == 256256) { p.bm = 256; p.bn = 256; }
     }
     p.tiles = ((M + p.bm - 1) / p.bm) * ((N + p.bn - 1) / p.bn);
     const bool recompute = recompute_ok && k_bytes <= 1152;
@@ -1208,12 +1242,20 @@ static hipError_t launch_mode(const GemmPlan& p, const LA& la, const LB& lb, int
         hipLaunchKernelGGL((gemm_kernel<BM_, BN_, WM_, WN_, LA, LB, MODE, KT, NW_>), grid, dim3(NW_ * 64), 0, st, \
                            la, lb, M, N, tn, k_total, per, epi);                                                 \
     } while (0)
+    // per-wave tiles: 64x64 (two wave groups over K for 128x128), 64x32 / 32x64 for the
+    // 4-wave shapes, 128x64 for 256x256
     if (p.bn == 64 && p.bm == 64)
         NITI_LAUNCH(64, 64, 2, 2, 4);
     else if (p.bn == 64)
         NITI_LAUNCH(128, 64, 2, 2, 4);
     else if (p.bm == 64)
         NITI_LAUNCH(64, 128, 1, 4, 4);
+    else if (p.bm == 256 && p.bn == 256)
+        NITI_LAUNCH(256, 256, 2, 4, 8);
+    else if (p.bm == 256)
+        NITI_LAUNCH(256, 128, 4, 2, 8);
+    else if (p.bn == 256)
+        NITI_LAUNCH(128, 256, 2, 4, 8);
     else
         NITI_LAUNCH(128, 128, 2, 2, 8);
 #undef NITI_LAUNCH

@@ -516,7 +516,7 @@ int Model::autotune(hipStream_t st, int reps) {
         return r;
     };
     if (hipMemsetAsync(amax, 0, amax_bytes, st) != hipSuccess) rc = NITI_NO_EXECUTION;
-    static const int tiles[4][2] = {{128, 128}, {128, 64}, {64, 128}, {64, 64}};
+    static const int tiles[6][2] = {{128, 128}, {128, 64}, {64, 128}, {64, 64}, {256, 128}, {128, 256}};
     static const int split_opts[] = {2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64};
     for (int i = 0; i < nl && rc == NITI_NO_ERROR; ++i) {
         for (int op : {PLAN_FWD, PLAN_WGRAD, PLAN_DGRAD}) {
@@ -783,8 +783,8 @@ int niti_model_plan_set(niti_model_t m, int layer, int phase, const int plan[4])
     if (plan == nullptr) {
         niti::plan_override_clear(k);
     } else {
-        if ((plan[0] != 64 && plan[0] != 128) || (plan[1] != 64 && plan[1] != 128) || plan[2] < 1 || plan[3] < 0 ||
-            plan[3] > 2)
+        auto tile_ok = [](int t) { return t == 64 || t == 128 || t == 256; };
+        if (!tile_ok(plan[0]) || !tile_ok(plan[1]) || plan[2] < 1 || plan[3] < 0 || plan[3] > 2)
             return NITI_INVALID_VALUE;
         niti::PlanChoice c;
         c.bm = plan[0];
