@@ -135,6 +135,10 @@ int niti_geom_finalize(niti_geom* g);
  * few tiles for 256 CUs (op 0 forward, 1 input gradient, 2 weight gradient).  Passing less
  * (or NULL) is allowed: the op then runs unsplit. */
 int niti_conv_workspace_bytes(const niti_geom* g, int op, size_t* bytes);
+/* The plan a conv GEMM of geometry g runs with under a workspace of ws_bytes (op 0 forward,
+ * 1 input gradient, 2 weight gradient): info = {bm, bn, splits, strategy}; bm = bn = 32 is the
+ * tap-sharing weight-gradient kernel (stride-1 3x3, Cip % 32 == 0, Cop % 64 == 0). */
+int niti_conv_plan_info(const niti_geom* g, int op, size_t ws_bytes, int info[4]);
 int niti_matmul_workspace_bytes(int m, int ldc, int k16, size_t* bytes);
 /* acc[n*oh*ow][cop] int32 = conv(x, w); if amax (NITI_MAX_WORDS words): range max-ed in */
 int niti_conv_fwd_acc(const niti_geom* g, const int8_t* x_nhwc16, const int8_t* w_ohwi16, int32_t* acc,

@@ -111,6 +111,19 @@ int niti_conv_workspace_bytes(const niti_geom* g, int op, size_t* bytes) {
     return NITI_NO_ERROR;
 }
 
+int niti_conv_plan_info(const niti_geom* g, int op, size_t ws_bytes, int info[4]) {
+    if (!g || !info || op < 0 || op > 2) return NITI_INVALID_VALUE;
+    niti::ConvGeom r = to_geom(g);
+    if (!r.finalize()) return NITI_INVALID_VALUE;
+    const int pop = op == 0 ? niti::PLAN_FWD : op == 1 ? niti::PLAN_DGRAD : niti::PLAN_WGRAD;
+    const niti::PlanChoice c = niti::conv_plan_query(pop, r, op != 2, ws_bytes);
+    info[0] = c.bm;
+    info[1] = c.bn;
+    info[2] = c.splits;
+    info[3] = c.strat;
+    return NITI_NO_ERROR;
+}
+
 int niti_matmul_workspace_bytes(int m, int ldc, int k16, size_t* bytes) {
     if (!bytes || ldc % 16 || k16 % 16) return NITI_INVALID_VALUE;
     *bytes = niti::matmul_workspace(m, ldc, k16);

@@ -15,6 +15,9 @@
 #include <map>
 #include <mutex>
 #include <type_traits>
+#include <vector>
+#include <algorithm>
+#include <stdio.h>
 
 #include "niti_kernels.hpp"
 #include "niti_map.hpp"
@@ -1099,12 +1102,353 @@ __global__ void splitk_reduce_kernel(const int32_t* __restrict__ slab, int split
     }
 }
 
+// =====================================================================================
+// Tap-sharing weight gradient (NITI_GradientConv_Int8, NITI_GradientConv_Int8.cpp:165-298)
+// for stride-1, dilation-1 convolutions with Cip % 32 == 0 and Cop % 64 == 0.
+//
+//   C[co][tap][ci] = sum over output pixels p of dy[p][co] * x[p + tap][ci]
+//
+// The generic KT GEMM stages an im2col panel per (tap, channel) column tile, so x is fetched
+// once per tap.  Here a block owns 64 output channels x ALL taps x 32 input channels.  Pixels
+// come in REGION STEPS of 64 output pixels (whole output rows of one image, or whole images);
+// a region step stages the zero-padded input region its pixels touch (rows RH = band + KH - 1,
+// cols RW = OW + KW - 1; out-of-image pixels read zeros through the buffer range check) once,
+// as 32-byte LDS rows, and every tap's B fragment is the same transposed read shifted by the
+// tap's region offset (ky*RW + kx rows).  32-byte rows keep each half-wave's transposed read
+// (8 consecutive region rows x 32 B = 256 contiguous bytes) conflict-free at any shift.
+//
+// A K step is two region steps (128 pixels).  8 waves, two per SIMD: wave w owns output-
+// channel half cg = w & 1 and K group kg = w >> 1 (the 32-pixel sub-step kg of every step), so
+// one wave's fragment reads and barrier wait hide under the other wave's MFMAs.  A step is one
+// MFMA stream per wave with the next step's fragment reads (a tap's x fragment is re-read
+// into its registers right after its MFMA) and the LDS-DMA issue in the gaps; every LDS
+// address is a per-lane register plus a compile-time stage offset (the K loop is unrolled by
+// the pipeline stages).  The 4 K groups' partial tiles meet through LDS two taps at a time,
+// and the int32 tile leaves as 16-byte row chunks.  Blocks: tiles (co64 x ci32) x K splits,
+// split-major under the XCD remap, so a split's tiles share one XCD's L2 and each XCD reads
+// only its own pixel range of x and dy.
+// =====================================================================================
+struct WgTaps {
+    const int8_t* x;   // NHWC16 [N][H][W][CIP]
+    const int8_t* dy;  // NHWC16 [N][OH][OW][COP]
+    uint32_t xbytes, dybytes;
+    int H, W, OH, OW, CIP, COP, KW, pt, pl;
+    int c_out;         // rows of C that exist
+    int RH, RW;        // region rows / columns per region image
+    int PPI;           // output pixels per region image (64 in band mode)
+    int imgs;          // region images per region step (1 in band mode)
+    int band;          // 1: a region step is 64 / OW output rows of one image
+    int rows_per_step;
+    int rs_total;      // region steps (K / 64)
+    int BPI;           // region steps per image group (OH / rows_per_step in band mode, else 1)
+    int steps_total, steps_per_split;  // K steps of two region steps
+    int tiles_ci, tiles;  // 32-channel input tiles; tiles per K split
+    FastDiv fRW, fRPI, fPPI, fOW, fOHW, fTiles, fTci, fBPI;
+    unsigned long long* stamps;  // diagnostic builds (NITI_STAMPS): per-block s_memtime marks
+};
+#ifndef NITI_STAMPS
+#define NITI_STAMPS 0
+#endif
+#define TAPS_STAMP(k)                                                                                         \
+    do {                                                                                                      \
+        if (NITI_STAMPS && g.stamps != nullptr && tid == 0) {                                                 \
+            g.stamps[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memtime();                                    \
+            if ((k) == 0 || (k) == 5) g.stamps[blockIdx.x * 8 + 6 + ((k) == 5)] = __builtin_amdgcn_s_memrealtime(); \
+        }                                                                                                     \
+    } while (0)
+
+template <int IMM>
+__device__ __forceinline__ v2i tr8_at(uint32_t a) {
+    v2i r;
+    asm volatile("ds_read_b64_tr_b8 %0, %1 offset:%2" : "=v"(r) : "v"(a), "n"(IMM));
+    return r;
+}
+
+constexpr int TAPS_THREADS = 512;
+
+template <int NT, int XPW, int MODE>
+__global__ void __launch_bounds__(TAPS_THREADS) wgrad_taps_kernel(WgTaps g, Epi epi) {
+    constexpr int NW = TAPS_THREADS / 64;
+    constexpr int STAGES = XPW == 1 ? 4 : 3;  // stage offsets are DS immediates (< 64 KiB)
+    constexpr int UNR = STAGES % 2 == 0 ? STAGES : 2 * STAGES;  // K-loop unroll: stage and dy buffer static
+    constexpr int XB = XPW * 4096;  // one region: 4 KiB x XPW of LDS-DMA (1 KiB per instruction)
+    constexpr int DB = 8192;        // dy: 128 pixels x 64 bytes
+    constexpr int SB = 2 * XB + DB;
+    constexpr int LOADS = XPW + 1;  // DMA instructions per wave per step (region w >> 2; dy)
+    constexpr int TR = 2;           // taps per K-group reduction round
+    constexpr int LDT = NT * 32 + 4;  // staged C tile pitch (int32)
+    constexpr int CT = 64 * LDT * 4;
+    constexpr int SLOT = TR * 32 * 32 * 4;  // one wave's partial of TR taps, [tap][32][32] int32
+    constexpr int RED = CT + NW * SLOT;
+    constexpr int SMEM = STAGES * SB > RED ? STAGES * SB : RED;
+    static_assert((STAGES - 1) * SB + 512 < 65536, "stage offsets fit the DS immediate");
+    __shared__ __attribute__((aligned(16))) int8_t smem[SMEM];
+
+    const int tid = threadIdx.x;
+    TAPS_STAMP(0);
+    const int lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int cg = wid & 1, kg = wid >> 1;
+    const int logical = xcd_remap(blockIdx.x, gridDim.x);
+    const int split = (int)fdiv(g.fTiles, (uint32_t)logical);
+    const int tile = logical - split * g.tiles;
+    const int tco = (int)fdiv(g.fTci, (uint32_t)tile), tci = tile - tco * g.tiles_ci;
+    const int co0 = tco * 64, ci0 = tci * 32;
+    const int s_begin = split * g.steps_per_split;
+    const int s_end = min(g.steps_total, s_begin + g.steps_per_split);
+    const int nsteps = s_end > s_begin ? s_end - s_begin : 0;
+
+    const __amdgpu_buffer_rsrc_t rX = make_rsrc(g.x, g.xbytes);
+    const __amdgpu_buffer_rsrc_t rD = make_rsrc(g.dy, g.dybytes);
+
+    // region DMA lanes: wave w fills region dreg = w >> 2 of the stage, chunks ((w & 3) * XPW +
+    // i) * 64 + lane; chunk c (16 bytes) = region row c >> 1, half c & 1
+    const int rpi = g.RH * g.RW;
+    const int dreg = wid >> 2;
+    int xrel[XPW], xry[XPW];
+    bool xok[XPW];
+#pragma unroll
+    for (int i = 0; i < XPW; ++i) {
+        const int c = ((wid & 3) * XPW + i) * 64 + lane;
+        const int q = c >> 1;
+        const int img = (int)fdiv(g.fRPI, (uint32_t)q), rr = q - img * rpi;
+        const int ry = (int)fdiv(g.fRW, (uint32_t)rr), rx = rr - ry * g.RW;
+        const int ix = rx - g.pl;
+        xok[i] = q < g.imgs * rpi && (unsigned)ix < (unsigned)g.W;
+        xry[i] = ry;
+        xrel[i] = ((img * g.H + ry) * g.W + ix) * g.CIP + 16 * (c & 1) + ci0;
+    }
+    // dy DMA lane: 128 rows of 64 bytes, 16-byte chunk dc of row r lands at dc ^ swz(r)
+    const int dch = wid * 64 + lane;
+    const int drow = dch >> 2;
+    const uint32_t dvo = (uint32_t)(drow * g.COP + co0 + 16 * ((dch & 3) ^ kt_swz<64>(drow)));
+
+    // LDS-DMA of K step `step` (block-relative) into `stage`: region 2 * step + dreg and rows
+    // [128 * step, +128) of dy; every wave-uniform offset follows from the region index with
+    // one multiply-shift division (no per-step branches)
+    auto issue = [&](int stage, int step) {
+        int8_t* sx = smem + stage * SB + dreg * XB;
+        int8_t* sd = smem + stage * SB + 2 * XB;
+        const int r = (s_begin + step) * 2 + dreg;
+        const int q = (int)fdiv(g.fBPI, (uint32_t)r);
+        const int ybase = (r - q * g.BPI) * g.rows_per_step - g.pt;
+        const int ub = (q * g.imgs * g.H + ybase) * g.W * g.CIP;
+        const bool rok = r < g.rs_total;
+#pragma unroll
+        for (int i = 0; i < XPW; ++i) {
+            const bool v = rok && xok[i] && (unsigned)(ybase + xry[i]) < (unsigned)g.H;
+            if (NITI_ABLATE != 1)
+                dma16(rX, sx + ((wid & 3) * XPW + i) * 1024, v ? (uint32_t)(ub + xrel[i]) : OOB, 0u);
+        }
+        const int pix0 = (s_begin + step) * 128;
+        if (NITI_ABLATE != 1)
+            dma16(rD, sd + wid * 1024, drow < g.rs_total * 64 - pix0 ? dvo : OOB, (uint32_t)pix0 * (uint32_t)g.COP);
+    };
+
+    // fragment addresses (stage 0; later stages add a compile-time offset): rows p and p + 8
+    // of the wave's 32-pixel sub-step, 8-byte column cofs of the lane's 32-column block
+    const uint32_t smem_base = lds_addr(smem);
+    const int xreg = kg >> 1, sub = kg & 1;
+    const int p0 = sub * 32 + 16 * (lane >> 5) + ((lane & 15) >> 1);  // pixel inside the region step
+    const int cofs = 16 * ((lane >> 4) & 1) + 8 * (lane & 1);
+    const uint32_t aD = smem_base + 2 * XB + (uint32_t)kt_off8<64>(xreg * 64 + p0, (cg * 32 + cofs) >> 3);  // +8 rows: +512
+    auto qrow = [&](int p) {
+        const int img = (int)fdiv(g.fPPI, (uint32_t)p), rem = p - img * g.PPI;
+        const int oy = (int)fdiv(g.fOW, (uint32_t)rem), ox = rem - oy * g.OW;
+        return img * rpi + oy * g.RW + ox;
+    };
+    const uint32_t rbase = smem_base + (uint32_t)(xreg * XB);
+    const uint32_t aX0 = rbase + (uint32_t)(qrow(p0) * 32 + cofs);
+    const uint32_t aX1 = rbase + (uint32_t)(qrow(p0 + 8) * 32 + cofs);
+    uint32_t aX[NT][2];
+    {
+        int ky = 0, kx = 0;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const uint32_t o = (uint32_t)((ky * g.RW + kx) * 32);
+            aX[t][0] = aX0 + o;
+            aX[t][1] = aX1 + o;
+            if (++kx == g.KW) {
+                kx = 0;
+                ++ky;
+            }
+        }
+    }
+
+    v16i acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[t][i] = 0;
+    // the dy fragment is double-buffered (read early in the previous step's stream); a tap's x
+    // fragment is re-read into the same registers right after its MFMA
+    v4i fd[2], fx[NT];
+
+    auto read_d = [&](auto st_c, auto buf_c) {
+        constexpr int ST = decltype(st_c)::value, BUF = decltype(buf_c)::value;
+        const v2i d0 = tr8_at<ST * SB>(aD), d1 = tr8_at<ST * SB + 512>(aD);
+        fd[BUF] = v4i{d0[0], d0[1], d1[0], d1[1]};
+    };
+    auto read_x = [&](auto st_c, auto t_c) {
+        constexpr int ST = decltype(st_c)::value, T = decltype(t_c)::value;
+        const v2i x0 = tr8_at<ST * SB>(aX[T][0]), x1 = tr8_at<ST * SB>(aX[T][1]);
+        fx[T] = v4i{x0[0], x0[1], x1[0], x1[1]};
+    };
+    // MFMA t of step s (stage ST, dy buffer CUR); after it: tap t of step s + 1 (and, after
+    // MFMA 0, its dy); the LDS-DMA of step s + STAGES - 1 after MFMA 1.  Before MFMA t a counted
+    // lgkm wait lets through only the reads younger than tap t's (clamped at 15: conservative).
+    // SS: steady state (a next step and the DMA step both exist: straight-line code); else
+    // `more` / `dma` decide at run time (the last steps of the block).
+    auto gap = [&](auto u_c, auto t_c, auto ss_c, int s, bool more, bool dma) {
+        constexpr int U = decltype(u_c)::value, T = decltype(t_c)::value;
+        constexpr bool SS = decltype(ss_c)::value;
+        constexpr int ST = U % STAGES, CUR = U & 1, NST = (ST + 1) % STAGES;
+        if (SS || more)
+            lgkm_wait<2 * (NT - 1 - T) + (T > 0 ? 2 * T + 2 : 0)>();
+        else
+            lgkm_wait<2 * (NT - 1 - T)>();
+        reg_fence(fx[T]);
+        if constexpr (T == 0) reg_fence(fd[CUR]);
+        if (NITI_ABLATE == 2)
+            acc[T][0] += fd[CUR][0] ^ fx[T][1];
+        else
+            acc[T] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fd[CUR], fx[T], acc[T], 0, 0, 0);
+        if (SS || more) {
+            if constexpr (T == 0) read_d(std::integral_constant<int, NST>(), std::integral_constant<int, CUR ^ 1>());
+            read_x(std::integral_constant<int, NST>(), t_c);
+        }
+        if constexpr (T == 1) {
+            if (SS || dma) issue((ST + STAGES - 1) % STAGES, s + STAGES - 1);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto body = [&](auto u_c, auto ss_c, int s) {
+        constexpr bool SS = decltype(ss_c)::value;
+        const bool more = s + 1 < nsteps, dma = s + STAGES - 1 < nsteps;
+        // own loads of step s + 1 landed (steps up to s + 2 may be in flight)
+        if (SS)
+            wait_vmcnt<(STAGES - 3) * LOADS>();
+        else if (more)
+            wait_steps<LOADS, STAGES - 3>(min(STAGES - 3, nsteps - 2 - s));
+        if (NITI_ABLATE != 4) __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        [&]<int... T>(std::integer_sequence<int, T...>) {
+            (gap(u_c, std::integral_constant<int, T>(), ss_c, s, more, dma), ...);
+        }(std::make_integer_sequence<int, NT>());
+    };
+
+#pragma unroll
+    for (int st = 0; st < STAGES - 1; ++st)
+        if (st < nsteps) issue(st, st);
+    if (nsteps > 0) {
+        wait_steps<LOADS, STAGES - 2>(min(STAGES - 2, nsteps - 1));
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        read_d(std::integral_constant<int, 0>(), std::integral_constant<int, 0>());
+        [&]<int... T>(std::integer_sequence<int, T...>) {
+            (read_x(std::integral_constant<int, 0>(), std::integral_constant<int, T>()), ...);
+        }(std::make_integer_sequence<int, NT>());
+    }
+    TAPS_STAMP(1);
+    // steady state: UNR straight-line steps per iteration while every step has its DMA; then
+    // the tail with run-time conditions, UNR steps per iteration
+    int s = 0;
+    for (; s + UNR + STAGES - 2 < nsteps; s += UNR) {
+        [&]<int... U>(std::integer_sequence<int, U...>) {
+            (body(std::integral_constant<int, U>(), std::true_type(), s + U), ...);
+        }(std::make_integer_sequence<int, UNR>());
+    }
+    for (; s < nsteps; s += UNR) {
+        [&]<int... U>(std::integer_sequence<int, U...>) {
+            ((s + U < nsteps ? body(std::integral_constant<int, U>(), std::false_type(), s + U) : void()), ...);
+        }(std::make_integer_sequence<int, UNR>());
+    }
+    lgkm_wait<0>();
+    __syncthreads();
+    TAPS_STAMP(2);
+
+    // the 4 K groups meet, TR taps per round: every wave writes its partial [tap][32][32] to its
+    // slot, then each thread sums one 4-element chunk of a row over the 4 K groups' slots into
+    // the staged tile ct [64][LDT] (row = output channel, column = tap * 32 + channel)
+    int32_t* ct = (int32_t*)smem;
+    int32_t* slot = (int32_t*)(smem + CT);
+#pragma unroll
+    for (int t0 = 0; t0 < NT; t0 += TR) {
+#pragma unroll
+        for (int u = 0; u < TR; ++u) {
+            if (t0 + u < NT) {
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const int row = (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
+                    slot[wid * (SLOT / 4) + (u * 32 + row) * 32 + (lane & 31)] = acc[t0 + u][i];
+                }
+            }
+        }
+        __syncthreads();
+        {
+            // 64 rows x 8 chunks per tap: one chunk per thread
+#pragma unroll
+            for (int uu = 0; uu < TR; ++uu) {
+                if (t0 + uu < NT) {
+                    const int row = tid >> 3, ch = tid & 7;  // 64 rows x 8 chunks = 512 threads
+                    const int c = row >> 5, r = row & 31;
+                    v4i sum = {0, 0, 0, 0};
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+                        sum += *(const v4i*)(slot + (2 * k + c) * (SLOT / 4) + (uu * 32 + r) * 32 + ch * 4);
+                    *(v4i*)(ct + row * LDT + (t0 + uu) * 32 + ch * 4) = sum;
+                }
+            }
+        }
+        __syncthreads();
+    }
+    TAPS_STAMP(3);
+    // 16-byte row chunks: 8 consecutive threads write one 128-byte (tap, 32-channel) segment
+    int32_t* Cs = MODE == EPI_SLAB ? epi.C + (int64_t)split * epi.slab_stride : epi.C;
+    constexpr int CPR = NT * 8;  // chunks per tile row
+    const int rows = min(64, g.c_out - co0);
+    uint32_t lmax = 0;
+    for (int c = tid; c < rows * CPR; c += TAPS_THREADS) {
+        const int row = c / CPR, rem = c - row * CPR;
+        const int t = rem >> 3, part = rem & 7;
+        const v4i v = *(const v4i*)(ct + row * LDT + t * 32 + part * 4);
+        *(v4i*)(Cs + (int64_t)(co0 + row) * epi.ldc + t * g.CIP + ci0 + part * 4) = v;
+        if (MODE == EPI_STORE) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t uu = uabs32(v[j]);
+                lmax = lmax > uu ? lmax : uu;
+            }
+        }
+    }
+    if (MODE == EPI_STORE) {
+        lmax = wave_max(lmax);
+        __syncthreads();
+        uint32_t* red = (uint32_t*)smem;
+        if (lane == 0) red[wid] = lmax;
+        __syncthreads();
+        if (tid == 0 && epi.amax != nullptr) {
+            uint32_t m = red[0];
+            for (int i = 1; i < NW; ++i) m = m > red[i] ? m : red[i];
+            publish_max(epi.amax, m);
+        }
+    }
+    if (NITI_STAMPS) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        TAPS_STAMP(5);
+    }
+}
+
+
 // ------------------------------------------------------------------------------ planning
 enum Strategy { STRAT_STORE = 0, STRAT_RECOMPUTE = 1, STRAT_SLAB = 2 };
 
 struct GemmPlan {
     int bm = 128, bn = 128, tiles = 1, splits = 1, kc_per_split = 0;
     Strategy strat = STRAT_STORE;
+    bool taps = false;  // weight gradient on wgrad_taps_kernel (kc_per_split counts 128-pixel steps)
 };
 
 // k_total: K extent in the kernel's units (16-byte chunks for KT = false, k rows for
@@ -1486,6 +1830,178 @@ static void wgrad_operands(const ConvGeom& g, const int8_t* x, const int8_t* dy,
     lb->bytes = (uint32_t)((int64_t)g.n * g.h * g.w * g.cip);
 }
 
+// ------------------------------------------------------------------------------ tap-sharing wgrad
+// Geometry of wgrad_taps_kernel, or false where it does not apply (the generic KT GEMM runs).
+static bool wgrad_taps_geom(const ConvGeom& g, const int8_t* x, const int8_t* dy, WgTaps* t) {
+    if (const char* f = getenv("NITI_DIAG_NO_TAPS")) {  // diagnostics / tests: generic KT GEMM only
+        if (atoi(f) != 0) return false;
+    }
+    if (g.kh * g.kw != 9 || g.sh != 1 || g.sw != 1 || g.dh != 1 || g.dw != 1) return false;
+    if (g.cip % 32 != 0 || g.cop % 64 != 0) return false;
+    const int64_t ohw = (int64_t)g.oh * g.ow;
+    const int64_t K = (int64_t)g.n * ohw;
+    const int64_t xbytes = (int64_t)g.n * g.h * g.w * g.cip, dybytes = K * g.cop;
+    if (K % 64 != 0 || xbytes >= (int64_t)OOB || dybytes >= (int64_t)OOB) return false;
+    WgTaps w{};
+    if (64 % g.ow == 0 && ohw % 64 == 0) {
+        w.band = 1;
+        w.rows_per_step = 64 / g.ow;
+        w.RH = w.rows_per_step + g.kh - 1;
+        w.imgs = 1;
+        w.PPI = 64;
+    } else if (64 % ohw == 0) {
+        w.band = 0;
+        w.rows_per_step = 0;
+        w.RH = g.oh + g.kh - 1;
+        w.imgs = (int)(64 / ohw);
+        w.PPI = (int)ohw;
+    } else {
+        return false;
+    }
+    w.RW = g.ow + g.kw - 1;
+    if (w.imgs * w.RH * w.RW > 256) return false;  // region rows (XPW <= 2)
+    w.x = x;
+    w.dy = dy;
+    w.xbytes = (uint32_t)xbytes;
+    w.dybytes = (uint32_t)dybytes;
+    w.H = g.h;
+    w.W = g.w;
+    w.OH = g.oh;
+    w.OW = g.ow;
+    w.CIP = g.cip;
+    w.COP = g.cop;
+    w.KW = g.kw;
+    w.pt = g.pt;
+    w.pl = g.pl;
+    w.c_out = g.c_out;
+    w.rs_total = (int)(K / 64);
+    w.steps_total = (w.rs_total + 1) / 2;
+    w.steps_per_split = w.steps_total;
+    w.tiles_ci = g.cip / 32;
+    w.tiles = (g.cop / 64) * w.tiles_ci;
+    w.fRW = make_fastdiv((uint32_t)w.RW);
+    w.fRPI = make_fastdiv((uint32_t)(w.RH * w.RW));
+    w.fPPI = make_fastdiv((uint32_t)w.PPI);
+    w.fOW = make_fastdiv((uint32_t)g.ow);
+    w.fOHW = make_fastdiv((uint32_t)ohw);
+    w.fTiles = make_fastdiv((uint32_t)w.tiles);
+    w.fTci = make_fastdiv((uint32_t)w.tiles_ci);
+    w.BPI = w.band ? g.oh / w.rows_per_step : 1;
+    w.fBPI = make_fastdiv((uint32_t)w.BPI);
+    *t = w;
+    return true;
+}
+
+bool conv_wgrad_taps_ok(const ConvGeom& g) {
+    WgTaps t;
+    return wgrad_taps_geom(g, nullptr, nullptr, &t);
+}
+
+// splits: override (ov) or one block per CU with >= 4 steps per split
+static GemmPlan plan_taps(const WgTaps& t, int M, int N, size_t ws_elems, const PlanChoice* ov) {
+    GemmPlan p;
+    p.taps = true;
+    p.bm = p.bn = PLAN_TAPS_TILE;
+    p.tiles = t.tiles;
+    int s;
+    if (ov != nullptr) {
+        s = ov->strat == STRAT_SLAB ? ov->splits : 1;
+    } else {
+        s = 256 / t.tiles;
+        if (s > t.steps_total / 4) s = t.steps_total / 4;
+        if (const char* f = getenv("NITI_DIAG_SPLITS")) s = atoi(f);  // diagnostics / tests
+    }
+    if (s < 1) s = 1;
+    p.kc_per_split = t.steps_total;
+    p.strat = STRAT_STORE;
+    if (s >= 2) plan_slab(p, s, t.steps_total, 1, t.steps_total, false, M, N, ws_elems);
+    return p;
+}
+
+#if NITI_STAMPS
+// diagnostic builds only: medians over blocks of the stamp intervals (us at the kernel's clock)
+static void taps_stamp_report(const unsigned long long* d, int blocks, hipStream_t st) {
+    std::vector<unsigned long long> h((size_t)blocks * 8);
+    if (hipStreamSynchronize(st) != hipSuccess ||
+        hipMemcpy(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost) != hipSuccess)
+        return;
+    auto med = [&](int a, int b) {
+        std::vector<double> v;
+        for (int i = 0; i < blocks; ++i) v.push_back((double)(h[i * 8 + b] - h[i * 8 + a]));
+        std::sort(v.begin(), v.end());
+        return v[v.size() / 2];
+    };
+    unsigned long long t0 = ~0ull, t1 = 0, r0 = ~0ull, r1 = 0;
+    for (int i = 0; i < blocks; ++i) {
+        t0 = std::min(t0, h[i * 8]);
+        t1 = std::max(t1, h[i * 8 + 5]);
+        r0 = std::min(r0, h[i * 8 + 6]);
+        r1 = std::max(r1, h[i * 8 + 7]);
+    }
+    const double ghz = (double)(t1 - t0) / ((double)(r1 - r0) * 10.0);  // memrealtime = 100 MHz
+    fprintf(stderr, "taps stamps: blocks %d clk %.2f GHz span %.2f us | prologue %.0f loop %.0f xchg %.0f store %.0f cyc\n",
+            blocks, ghz, (r1 - r0) / 100.0, med(0, 1), med(1, 2), med(2, 3), med(3, 5));
+}
+#endif
+
+template <int MODE>
+static hipError_t launch_taps(const GemmPlan& p, WgTaps t, const Epi& e, hipStream_t st) {
+    const int splits = MODE == EPI_SLAB ? p.splits : 1;
+    t.steps_per_split = MODE == EPI_SLAB ? p.kc_per_split : t.steps_total;
+    const dim3 grid((unsigned)(t.tiles * splits));
+    t.stamps = nullptr;
+#if NITI_STAMPS
+    static unsigned long long* sbuf = nullptr;
+    if (sbuf == nullptr && hipMalloc(&sbuf, 4096 * 8 * 8) != hipSuccess) sbuf = nullptr;
+    if (grid.x <= 4096) t.stamps = sbuf;
+#endif
+    if (t.imgs * t.RH * t.RW * 32 > 4096)
+        hipLaunchKernelGGL((wgrad_taps_kernel<9, 2, MODE>), grid, dim3(TAPS_THREADS), 0, st, t, e);
+    else
+        hipLaunchKernelGGL((wgrad_taps_kernel<9, 1, MODE>), grid, dim3(TAPS_THREADS), 0, st, t, e);
+#if NITI_STAMPS
+    if (t.stamps) taps_stamp_report(t.stamps, (int)grid.x, st);
+#endif
+    return hipGetLastError();
+}
+
+static hipError_t wgrad_taps_run(const GemmPlan& p, const WgTaps& t, int M, int N, int32_t* C, uint32_t* amax,
+                                 int32_t* ws, hipStream_t st, hipEvent_t after_gemm) {
+    Epi e;
+    if (p.strat == STRAT_SLAB) {
+        e.C = ws;
+        e.ldc = N;
+        e.slab_stride = (int64_t)slab_stride_elems(M, N);
+        hipError_t r = launch_taps<EPI_SLAB>(p, t, e, st);
+        if (r == hipSuccess && after_gemm != nullptr) r = hipEventRecord(after_gemm, st);
+        if (r != hipSuccess) return r;
+        return splitk_reduce(p, ws, (int64_t)M * N, e.slab_stride, C, amax, st);
+    }
+    e.C = C;
+    e.ldc = N;
+    e.amax = amax;
+    hipError_t r = launch_taps<EPI_STORE>(p, t, e, st);
+    if (r == hipSuccess && after_gemm != nullptr) r = hipEventRecord(after_gemm, st);
+    return r;
+}
+
+PlanChoice conv_plan_query(int op, const ConvGeom& g, bool recompute_ok, size_t ws_bytes) {
+    const PlanKey key = conv_plan_key(op, g);
+    WgTaps t;
+    PlanChoice c;
+    if (op == PLAN_WGRAD && wgrad_taps_geom(g, nullptr, nullptr, &t)) {
+        const bool has = plan_override_get(key, &c);
+        if (!has || c.bm == PLAN_TAPS_TILE) {
+            const GemmPlan p = plan_taps(t, key.M, key.N, ws_bytes / 4, has ? &c : nullptr);
+            c.bm = c.bn = PLAN_TAPS_TILE;
+            c.splits = p.strat == STRAT_SLAB ? p.splits : 1;
+            c.strat = p.strat;
+            return c;
+        }
+    }
+    return plan_query(key, conv_plan_k_step(op, g), recompute_ok, ws_bytes);
+}
+
 PlanKey conv_plan_key(int op, const ConvGeom& g) {
     if (op == PLAN_FWD) return PlanKey{op, g.n * g.oh * g.ow, g.cop, g.kh * g.kw * g.cip / 16};
     if (op == PLAN_DGRAD) return PlanKey{op, g.n * g.h * g.w, g.cip, g.kh * g.kw * g.cop / 16};
@@ -1506,7 +2022,14 @@ size_t conv_dgrad_workspace(const ConvGeom& g) {
     return plan_ws_elems(g.n * g.h * g.w, g.cip, g.kh * g.kw * g.cop / 16, bk / 16) * sizeof(int32_t);
 }
 size_t conv_wgrad_workspace(const ConvGeom& g) {
-    return plan_ws_elems(g.c_out, g.kh * g.kw * g.cip, g.n * g.oh * g.ow, KT_BK) * sizeof(int32_t);
+    const int M = g.c_out, N = g.kh * g.kw * g.cip;
+    size_t e = plan_ws_elems(M, N, g.n * g.oh * g.ow, KT_BK);
+    WgTaps t;
+    if (wgrad_taps_geom(g, nullptr, nullptr, &t)) {
+        const GemmPlan p = plan_taps(t, M, N, (size_t)-1, nullptr);
+        if (p.strat == STRAT_SLAB) e = std::max(e, (size_t)p.splits * slab_stride_elems(M, N));
+    }
+    return e * sizeof(int32_t);
 }
 size_t matmul_workspace(int M, int ldc, int k16) {
     return plan_ws_elems(M, ldc, k16 / 16, RowsK::BK / 16) * sizeof(int32_t);
@@ -1532,6 +2055,16 @@ hipError_t conv_dgrad_acc(const ConvGeom& g, const int8_t* dy, const int8_t* wt,
 
 hipError_t conv_wgrad_acc(const ConvGeom& g, const int8_t* x, const int8_t* dy, int32_t* acc, uint32_t* amax,
                           void* ws, size_t ws_bytes, hipStream_t st, hipEvent_t after_gemm) {
+    WgTaps tg;
+    if (wgrad_taps_geom(g, x, dy, &tg)) {
+        const int M = g.c_out, N = g.kh * g.kw * g.cip;
+        PlanChoice c;
+        const bool has = plan_override_get(conv_plan_key(PLAN_WGRAD, g), &c);
+        if (!has || c.bm == PLAN_TAPS_TILE) {
+            const GemmPlan p = plan_taps(tg, M, N, ws ? ws_bytes / 4 : 0, has ? &c : nullptr);
+            return wgrad_taps_run(p, tg, M, N, acc, amax, (int32_t*)ws, st, after_gemm);
+        }
+    }
     KtRowsU la;
     KtIm2col lg;
     wgrad_operands(g, x, dy, &la, &lg);

@@ -68,7 +68,13 @@ struct PlanKey {
 struct PlanChoice {
     int bm = 128, bn = 128, splits = 1, strat = 0;
 };
+// bm = bn = PLAN_TAPS_TILE selects the tap-sharing weight-gradient kernel (64 output channels x
+// all taps x 32 input channels per block) where conv_wgrad_taps_ok(g)
+constexpr int PLAN_TAPS_TILE = 32;
+bool conv_wgrad_taps_ok(const ConvGeom& g);
 PlanKey conv_plan_key(int op, const ConvGeom& g);
+// the plan a conv GEMM runs with now (override or default), tap-sharing wgrad included
+PlanChoice conv_plan_query(int op, const ConvGeom& g, bool recompute_ok, size_t ws_bytes);
 int conv_plan_k_step(int op, const ConvGeom& g);
 void plan_override_set(const PlanKey& k, const PlanChoice& c);
 void plan_override_clear(const PlanKey& k);

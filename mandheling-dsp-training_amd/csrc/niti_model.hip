@@ -481,7 +481,8 @@ int Model::dgrad_layer(int i, hipStream_t st) {
 // Per-shape plan autotuning.  For every GEMM of the step (layer x {forward, weight gradient,
 // input gradient}) time the layer's whole phase -- GEMM(s), split-K reduce, requantisation,
 // fused / separate pool -- under each candidate plan on the caller's stream and keep the
-// fastest as a plan override (niti_kernels.hpp).  Candidates: 4 tile shapes x {store acc,
+// fastest as a plan override (niti_kernels.hpp).  Candidates: the tap-sharing weight-gradient
+// kernel where it applies and 6 GEMM tile shapes, each x {store acc,
 // recompute (activation GEMMs), split-K 2..64 within the tuning workspace}.  The layer phases
 // are idempotent on the buffers left by the previous step, so tuning leaves the weights
 // untouched; a fixed default plan (plan_gemm) is the starting point and is kept unless beaten.
@@ -516,7 +517,8 @@ int Model::autotune(hipStream_t st, int reps) {
         return r;
     };
     if (hipMemsetAsync(amax, 0, amax_bytes, st) != hipSuccess) rc = NITI_NO_EXECUTION;
-    static const int tiles[6][2] = {{128, 128}, {128, 64}, {64, 128}, {64, 64}, {256, 128}, {128, 256}};
+    static const int tiles[7][2] = {{PLAN_TAPS_TILE, PLAN_TAPS_TILE}, {128, 128}, {128, 64}, {64, 128}, {64, 64},
+                                    {256, 128}, {128, 256}};
     static const int split_opts[] = {2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64};
     for (int i = 0; i < nl && rc == NITI_NO_ERROR; ++i) {
         for (int op : {PLAN_FWD, PLAN_WGRAD, PLAN_DGRAD}) {
@@ -528,11 +530,13 @@ int Model::autotune(hipStream_t st, int reps) {
             const bool act = op != PLAN_WGRAD;
             plan_override_clear(key);
             const size_t wsb = ws_bytes_for(op);
-            PlanChoice best = plan_query(key, k_step, act, wsb);
+            PlanChoice best = conv_plan_query(op, g, act, wsb);
             float best_us = 0.f;
             rc = time_op(i, op, &best_us);
+            const bool taps = op == PLAN_WGRAD && conv_wgrad_taps_ok(g);
             for (const auto& t : tiles) {
                 if (rc != NITI_NO_ERROR) break;
+                if (t[0] == PLAN_TAPS_TILE && !taps) continue;
                 std::vector<PlanChoice> cands;
                 PlanChoice c;
                 c.bm = t[0];
@@ -767,8 +771,7 @@ int niti_model_plan_info(niti_model_t m, int layer, int phase, int info[4]) {
         return NITI_INVALID_VALUE;
     const niti::ConvGeom& g = m->m.L[layer].g;
     const int op = phase == 0 ? niti::PLAN_FWD : phase == 1 ? niti::PLAN_DGRAD : niti::PLAN_WGRAD;
-    const niti::PlanChoice c =
-        niti::plan_query(niti::conv_plan_key(op, g), niti::conv_plan_k_step(op, g), phase != 2, m->m.ws_bytes_for(op));
+    const niti::PlanChoice c = niti::conv_plan_query(op, g, phase != 2, m->m.ws_bytes_for(op));
     info[0] = c.bm;
     info[1] = c.bn;
     info[2] = c.splits;
@@ -784,7 +787,10 @@ int niti_model_plan_set(niti_model_t m, int layer, int phase, const int plan[4])
         niti::plan_override_clear(k);
     } else {
         auto tile_ok = [](int t) { return t == 64 || t == 128 || t == 256; };
-        if (!tile_ok(plan[0]) || !tile_ok(plan[1]) || plan[2] < 1 || plan[3] < 0 || plan[3] > 2)
+        const bool taps = plan[0] == niti::PLAN_TAPS_TILE && plan[1] == niti::PLAN_TAPS_TILE &&
+                          op == niti::PLAN_WGRAD && niti::conv_wgrad_taps_ok(m->m.L[layer].g);
+        if ((!taps && (!tile_ok(plan[0]) || !tile_ok(plan[1]))) || plan[2] < 1 || plan[3] < 0 || plan[3] > 2 ||
+            (taps && plan[3] == 1))
             return NITI_INVALID_VALUE;
         niti::PlanChoice c;
         c.bm = plan[0];

@@ -80,6 +80,7 @@ def lib():
         "niti_geom_finalize": (ci, [C.POINTER(Geom)]),
         "niti_conv_workspace_bytes": (ci, [C.POINTER(Geom), ci, C.POINTER(C.c_size_t)]),
         "niti_matmul_workspace_bytes": (ci, [ci, ci, ci, C.POINTER(C.c_size_t)]),
+        "niti_conv_plan_info": (ci, [C.POINTER(Geom), ci, C.c_size_t, C.POINTER(C.c_int)]),
         "niti_conv_fwd_acc": (ci, [C.POINTER(Geom), vp, vp, vp, vp, vp, C.c_size_t, vp]),
         "niti_conv_dgrad_acc": (ci, [C.POINTER(Geom), vp, vp, vp, vp, vp, C.c_size_t, vp]),
         "niti_conv_wgrad_acc": (ci, [C.POINTER(Geom), vp, vp, vp, vp, vp, C.c_size_t, vp]),

@@ -171,6 +171,22 @@ def conv_dgrad_acc(g: L.Geom, dy16, wt16, amax, stream=None):
     return acc
 
 
+def conv_plan(g: L.Geom, op: int, ws_bytes: int | None = None):
+    """(bm, bn, splits, strategy) the conv GEMM `op` (0 fwd, 1 dgrad, 2 wgrad) runs with."""
+    if ws_bytes is None:
+        n = C.c_size_t(0)
+        check(L.lib().niti_conv_workspace_bytes(C.byref(g), op, C.byref(n)), "workspace")
+        ws_bytes = int(n.value)
+    info = (C.c_int * 4)()
+    check(L.lib().niti_conv_plan_info(C.byref(g), op, ws_bytes, info), "conv_plan_info")
+    return tuple(info)
+
+
+def wgrad_taps_ok(g: L.Geom) -> bool:
+    """Whether the weight gradient of g runs on the tap-sharing kernel (wgrad_taps_kernel)."""
+    return conv_plan(g, 2)[0] == 32
+
+
 def conv_wgrad_acc(g: L.Geom, xT, dyT, amax=None, stream=None):
     acc = torch.empty((g.c_out, g.kh, g.kw, g.cip), dtype=torch.int32, device=xT.device)
     ws, nb = conv_workspace(g, 2, xT.device)

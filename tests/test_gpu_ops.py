@@ -161,6 +161,43 @@ def test_conv_wgrad_native(T, ops, oracle, geo):
     assert not wTn[..., co:].any()
 
 
+# tap-sharing weight gradient (wgrad_taps_kernel): every step mode and split plan
+TAPS_GEOMS = [
+    (3, 64, 8, 8, 128, 1),     # band: one 8x8 image per 64-pixel step
+    (1, 32, 16, 16, 64, 1),    # band: 4 rows of a 16x16 image
+    (1, 32, 32, 32, 64, 1),    # band: 2 rows of a 32x32 image (two-KiB region DMA per wave)
+    (8, 64, 4, 4, 64, 1),      # whole images: 4 per step
+    (16, 32, 2, 2, 128, 1),    # whole images: 16 per step
+    (2, 32, 10, 10, 50, 0),    # no padding (10x10 -> 8x8), c_out not a multiple of 64
+    (4, 96, 8, 8, 64, 1),      # 3 input-channel tiles
+]
+
+
+@pytest.mark.parametrize("geo", TAPS_GEOMS)
+@pytest.mark.parametrize("splits", ["", "1", "3"])
+def test_conv_wgrad_taps(T, ops, oracle, geo, splits, monkeypatch):
+    n, ci, h, w, co, p = geo
+    rng = np.random.default_rng(211)
+    g = oracle.geom(n, ci, h, w, co, 3, stride=1, pad=p)
+    x = rng.integers(-127, 128, (n, ci, h, w)).astype(np.int8)
+    dy = rng.integers(-127, 128, (n, co, g.oh, g.ow)).astype(np.int8)
+    _, _, acc_ref, _ = oracle.conv_wgrad(g, x, dy)
+    gg = ops.geom(n, ci, h, w, co, 3, stride=1, pad=p)
+    assert ops.wgrad_taps_ok(gg)
+    xT = ops.nchw_to_nhwc16(dev(T, x))
+    dyT = ops.nchw_to_nhwc16(dev(T, dy))
+    if splits:
+        monkeypatch.setenv("NITI_DIAG_SPLITS", splits)
+    amax = zeros_u32(T)
+    acc = ops.conv_wgrad_acc(gg, xT, dyT, amax)
+    got = acc.cpu().numpy()
+    assert np.array_equal(got[..., :ci].transpose(0, 3, 1, 2), acc_ref)
+    assert not got[..., ci:].any()
+    assert ops.range_max(amax) == int(np.abs(acc_ref.astype(np.int64)).max())
+    monkeypatch.setenv("NITI_DIAG_NO_TAPS", "1")  # the generic K-major GEMM agrees bit for bit
+    assert np.array_equal(ops.conv_wgrad_acc(gg, xT, dyT).cpu().numpy(), got)
+
+
 # --------------------------------------------------------------------------- drop-in Executions
 def _c4_dims(a):
     return list(a.shape)

@@ -27,7 +27,10 @@ def main():
     ap.add_argument("--tiles", default="0")
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--op", type=int, default=2)
+    ap.add_argument("--notaps", action="store_true", help="generic K-major GEMM only (NITI_DIAG_NO_TAPS)")
     args = ap.parse_args()
+    if args.notaps:
+        os.environ["NITI_DIAG_NO_TAPS"] = "1"
     lib = L.lib()
     s = C.c_void_p(torch.cuda.current_stream().cuda_stream)
     ci, co, h = LAYERS[args.layer]
