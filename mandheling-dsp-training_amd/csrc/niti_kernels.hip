@@ -1165,22 +1165,27 @@ __device__ __forceinline__ v2i tr8_at(uint32_t a) {
 }
 
 constexpr int TAPS_THREADS = 512;
+#ifndef NITI_TAPS_NT
+#define NITI_TAPS_NT 0  // nontemporal (L2-bypassing) stores of the int32 tile
+#endif
 
 template <int NT, int XPW, int MODE>
 __global__ void __launch_bounds__(TAPS_THREADS) wgrad_taps_kernel(WgTaps g, Epi epi) {
     constexpr int NW = TAPS_THREADS / 64;
-    constexpr int STAGES = XPW == 1 ? 4 : 3;  // stage offsets are DS immediates (< 64 KiB)
-    constexpr int UNR = STAGES % 2 == 0 ? STAGES : 2 * STAGES;  // K-loop unroll: stage and dy buffer static
-    constexpr int XB = XPW * 4096;  // one region: 4 KiB x XPW of LDS-DMA (1 KiB per instruction)
-    constexpr int DB = 8192;        // dy: 128 pixels x 64 bytes
-    constexpr int SB = 2 * XB + DB;
-    constexpr int LOADS = XPW + 1;  // DMA instructions per wave per step (region w >> 2; dy)
-    constexpr int TR = 2;           // taps per K-group reduction round
-    constexpr int LDT = NT * 32 + 4;  // staged C tile pitch (int32)
+    static_assert(NW == 8, "8 waves: tap half x K group x output-channel half");
+    static_assert(NT == 9, "3x3 taps");
+    constexpr int STAGES = 4;
+    constexpr int XB = XPW * 4096;  // region: 4 KiB x XPW of LDS-DMA (1 KiB per instruction)
+    constexpr int DB = 4096;        // dy: 64 pixels x 64 bytes
+    constexpr int ZB = XPW == 2 ? 4096 : 0;  // XPW 2: sink of the 4 waves without a dy chunk
+    constexpr int SB = XB + DB + ZB;
+    constexpr int LOADS = XPW;      // DMA instructions per wave per step
+    constexpr int TA = (NT + 1) / 2;  // taps of wave half 0 (half 1 takes the rest)
+    constexpr int XCH = 2 * 2 * TA * 4096;  // exchange: one 32x32 int32 tile per (tap half, cg, tap)
+    constexpr int LDT = NT * 32 + 4;        // staged C tile pitch (int32)
     constexpr int CT = 64 * LDT * 4;
-    constexpr int SLOT = TR * 32 * 32 * 4;  // one wave's partial of TR taps, [tap][32][32] int32
-    constexpr int RED = CT + NW * SLOT;
-    constexpr int SMEM = STAGES * SB > RED ? STAGES * SB : RED;
+    constexpr int SMEM0 = STAGES * SB > XCH ? STAGES * SB : XCH;
+    constexpr int SMEM = SMEM0 > CT ? SMEM0 : CT;
     static_assert((STAGES - 1) * SB + 512 < 65536, "stage offsets fit the DS immediate");
     __shared__ __attribute__((aligned(16))) int8_t smem[SMEM];
 
@@ -1188,7 +1193,8 @@ __global__ void __launch_bounds__(TAPS_THREADS) wgrad_taps_kernel(WgTaps g, Epi 
     TAPS_STAMP(0);
     const int lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int cg = wid & 1, kg = wid >> 1;
+    // waves w and w + 4 share a SIMD (cyclic SIMD order): one takes TA taps, the other NT - TA
+    const int th = wid >> 2, kg = (wid >> 1) & 1, cg = wid & 1;
     const int logical = xcd_remap(blockIdx.x, gridDim.x);
     const int split = (int)fdiv(g.fTiles, (uint32_t)logical);
     const int tile = logical - split * g.tiles;
@@ -1201,210 +1207,218 @@ __global__ void __launch_bounds__(TAPS_THREADS) wgrad_taps_kernel(WgTaps g, Epi 
     const __amdgpu_buffer_rsrc_t rX = make_rsrc(g.x, g.xbytes);
     const __amdgpu_buffer_rsrc_t rD = make_rsrc(g.dy, g.dybytes);
 
-    // region DMA lanes: wave w fills region dreg = w >> 2 of the stage, chunks ((w & 3) * XPW +
-    // i) * 64 + lane; chunk c (16 bytes) = region row c >> 1, half c & 1
+    // DMA lanes.  XPW 1: waves 0-3 fill the region (chunk c = (w * 64 + lane) = region row
+    // c >> 1, half c & 1), waves 4-7 the 64 x 64-byte dy tile.  XPW 2: every wave one region
+    // chunk block; waves 0-3 also the dy tile, waves 4-7 a dummy (zeros into the stage's sink)
+    // so that every wave counts the same loads.
     const int rpi = g.RH * g.RW;
-    const int dreg = wid >> 2;
-    int xrel[XPW], xry[XPW];
-    bool xok[XPW];
-#pragma unroll
-    for (int i = 0; i < XPW; ++i) {
-        const int c = ((wid & 3) * XPW + i) * 64 + lane;
+    const bool xw = XPW == 2 || wid < 4;  // this wave's first DMA is a region chunk block
+    const int xblk = XPW == 2 ? wid : (wid & 3);
+    int xrel = 0, xry = 0;
+    bool xok = false;
+    {
+        const int c = xblk * 64 + lane;
         const int q = c >> 1;
         const int img = (int)fdiv(g.fRPI, (uint32_t)q), rr = q - img * rpi;
         const int ry = (int)fdiv(g.fRW, (uint32_t)rr), rx = rr - ry * g.RW;
         const int ix = rx - g.pl;
-        xok[i] = q < g.imgs * rpi && (unsigned)ix < (unsigned)g.W;
-        xry[i] = ry;
-        xrel[i] = ((img * g.H + ry) * g.W + ix) * g.CIP + 16 * (c & 1) + ci0;
+        xok = q < g.imgs * rpi && (unsigned)ix < (unsigned)g.W;
+        xry = ry;
+        xrel = ((img * g.H + ry) * g.W + ix) * g.CIP + 16 * (c & 1) + ci0;
     }
-    // dy DMA lane: 128 rows of 64 bytes, 16-byte chunk dc of row r lands at dc ^ swz(r)
-    const int dch = wid * 64 + lane;
+    const int dch = (wid & 3) * 64 + lane;
     const int drow = dch >> 2;
     const uint32_t dvo = (uint32_t)(drow * g.COP + co0 + 16 * ((dch & 3) ^ kt_swz<64>(drow)));
+    const bool dw = XPW == 1 ? !xw : wid < 4;  // this wave loads a dy chunk block
 
-    // LDS-DMA of K step `step` (block-relative) into `stage`: region 2 * step + dreg and rows
-    // [128 * step, +128) of dy; every wave-uniform offset follows from the region index with
-    // one multiply-shift division (no per-step branches)
+    // LDS-DMA of region step `step` (block-relative) into `stage`; wave-uniform offsets from the
+    // region index by one multiply-shift division (no per-step branches)
     auto issue = [&](int stage, int step) {
-        int8_t* sx = smem + stage * SB + dreg * XB;
-        int8_t* sd = smem + stage * SB + 2 * XB;
-        const int r = (s_begin + step) * 2 + dreg;
+        int8_t* st0 = smem + stage * SB;
+        const int r = s_begin + step;
         const int q = (int)fdiv(g.fBPI, (uint32_t)r);
         const int ybase = (r - q * g.BPI) * g.rows_per_step - g.pt;
         const int ub = (q * g.imgs * g.H + ybase) * g.W * g.CIP;
-        const bool rok = r < g.rs_total;
-#pragma unroll
-        for (int i = 0; i < XPW; ++i) {
-            const bool v = rok && xok[i] && (unsigned)(ybase + xry[i]) < (unsigned)g.H;
-            if (NITI_ABLATE != 1)
-                dma16(rX, sx + ((wid & 3) * XPW + i) * 1024, v ? (uint32_t)(ub + xrel[i]) : OOB, 0u);
+        if (xw) {
+            const bool v = xok && (unsigned)(ybase + xry) < (unsigned)g.H;
+            if (NITI_ABLATE != 1) dma16(rX, st0 + xblk * 1024, v ? (uint32_t)(ub + xrel) : OOB, 0u);
         }
-        const int pix0 = (s_begin + step) * 128;
-        if (NITI_ABLATE != 1)
-            dma16(rD, sd + wid * 1024, drow < g.rs_total * 64 - pix0 ? dvo : OOB, (uint32_t)pix0 * (uint32_t)g.COP);
+        if (dw) {
+            if (NITI_ABLATE != 1) dma16(rD, st0 + XB + (wid & 3) * 1024, dvo, (uint32_t)r * 64u * (uint32_t)g.COP);
+        } else if (XPW == 2) {
+            if (NITI_ABLATE != 1) dma16(rD, st0 + XB + DB + (wid & 3) * 1024, OOB, 0u);
+        }
     };
 
     // fragment addresses (stage 0; later stages add a compile-time offset): rows p and p + 8
     // of the wave's 32-pixel sub-step, 8-byte column cofs of the lane's 32-column block
     const uint32_t smem_base = lds_addr(smem);
-    const int xreg = kg >> 1, sub = kg & 1;
-    const int p0 = sub * 32 + 16 * (lane >> 5) + ((lane & 15) >> 1);  // pixel inside the region step
+    const int p0 = kg * 32 + 16 * (lane >> 5) + ((lane & 15) >> 1);
     const int cofs = 16 * ((lane >> 4) & 1) + 8 * (lane & 1);
-    const uint32_t aD = smem_base + 2 * XB + (uint32_t)kt_off8<64>(xreg * 64 + p0, (cg * 32 + cofs) >> 3);  // +8 rows: +512
+    const uint32_t aD = smem_base + XB + (uint32_t)kt_off8<64>(p0, (cg * 32 + cofs) >> 3);  // +8 rows: +512
     auto qrow = [&](int p) {
         const int img = (int)fdiv(g.fPPI, (uint32_t)p), rem = p - img * g.PPI;
         const int oy = (int)fdiv(g.fOW, (uint32_t)rem), ox = rem - oy * g.OW;
         return img * rpi + oy * g.RW + ox;
     };
-    const uint32_t rbase = smem_base + (uint32_t)(xreg * XB);
-    const uint32_t aX0 = rbase + (uint32_t)(qrow(p0) * 32 + cofs);
-    const uint32_t aX1 = rbase + (uint32_t)(qrow(p0 + 8) * 32 + cofs);
-    uint32_t aX[NT][2];
-    {
-        int ky = 0, kx = 0;
+    const uint32_t aX0 = smem_base + (uint32_t)(qrow(p0) * 32 + cofs);
+    const uint32_t aX1 = smem_base + (uint32_t)(qrow(p0 + 8) * 32 + cofs);
+
+    // everything below runs per tap half TH (compile time): taps [T0, T0 + NTW)
+    auto run = [&](auto th_c) {
+        constexpr int TH = decltype(th_c)::value;
+        constexpr int T0 = TH ? TA : 0, NTW = TH ? NT - TA : TA;
+        uint32_t aX[NTW][2];
 #pragma unroll
-        for (int t = 0; t < NT; ++t) {
+        for (int j = 0; j < NTW; ++j) {
+            const int t = T0 + j, ky = t / 3, kx = t % 3;
             const uint32_t o = (uint32_t)((ky * g.RW + kx) * 32);
-            aX[t][0] = aX0 + o;
-            aX[t][1] = aX1 + o;
-            if (++kx == g.KW) {
-                kx = 0;
-                ++ky;
+            aX[j][0] = aX0 + o;
+            aX[j][1] = aX1 + o;
+        }
+        v16i acc[NTW];
+#pragma unroll
+        for (int j = 0; j < NTW; ++j)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) acc[j][i] = 0;
+        // dy double-buffered (read early in the previous step's stream); a tap's x fragment is
+        // re-read into its registers right after its MFMA
+        v4i fd[2], fx[NTW];
+        auto read_d = [&](auto st_c, auto buf_c) {
+            constexpr int ST = decltype(st_c)::value, BUF = decltype(buf_c)::value;
+            const v2i d0 = tr8_at<ST * SB>(aD), d1 = tr8_at<ST * SB + 512>(aD);
+            fd[BUF] = v4i{d0[0], d0[1], d1[0], d1[1]};
+        };
+        auto read_x = [&](auto st_c, auto j_c) {
+            constexpr int ST = decltype(st_c)::value, J = decltype(j_c)::value;
+            const v2i x0 = tr8_at<ST * SB>(aX[J][0]), x1 = tr8_at<ST * SB>(aX[J][1]);
+            fx[J] = v4i{x0[0], x0[1], x1[0], x1[1]};
+        };
+        // MFMA j of step s (stage ST, dy buffer CUR); after it: tap j of step s + 1 (after MFMA
+        // 0 also its dy), and after MFMA 1 the LDS-DMA of step s + STAGES - 1.  Before MFMA j a
+        // counted lgkm wait lets through exactly the reads issued after tap j's (<= 2 NTW).
+        auto gap = [&](auto u_c, auto j_c, auto ss_c, int s, bool more, bool dma) {
+            constexpr int U = decltype(u_c)::value, J = decltype(j_c)::value;
+            constexpr bool SS = decltype(ss_c)::value;
+            constexpr int ST = U % STAGES, CUR = U & 1, NST = (ST + 1) % STAGES;
+            if (SS || more)
+                lgkm_wait<2 * (NTW - 1 - J) + (J > 0 ? 2 * J + 2 : 0)>();
+            else
+                lgkm_wait<2 * (NTW - 1 - J)>();
+            reg_fence(fx[J]);
+            if constexpr (J == 0) reg_fence(fd[CUR]);
+            if (NITI_ABLATE == 2)
+                acc[J][0] += fd[CUR][0] ^ fx[J][1];
+            else
+                acc[J] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fd[CUR], fx[J], acc[J], 0, 0, 0);
+            if (SS || more) {
+                if constexpr (J == 0) read_d(std::integral_constant<int, NST>(), std::integral_constant<int, CUR ^ 1>());
+                read_x(std::integral_constant<int, NST>(), j_c);
+            }
+            if constexpr (J == 1) {
+                if (SS || dma) issue((ST + STAGES - 1) % STAGES, s + STAGES - 1);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        };
+        auto body = [&](auto u_c, auto ss_c, int s) {
+            constexpr bool SS = decltype(ss_c)::value;
+            const bool more = s + 1 < nsteps, dma = s + STAGES - 1 < nsteps;
+            // own loads of step s + 1 landed (steps up to s + 2 may be in flight)
+            if (SS)
+                wait_vmcnt<(STAGES - 3) * LOADS>();
+            else if (more)
+                wait_steps<LOADS, STAGES - 3>(min(STAGES - 3, nsteps - 2 - s));
+            if (NITI_ABLATE != 4) __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+            [&]<int... J>(std::integer_sequence<int, J...>) {
+                (gap(u_c, std::integral_constant<int, J>(), ss_c, s, more, dma), ...);
+            }(std::make_integer_sequence<int, NTW>());
+        };
+
+#pragma unroll
+        for (int st = 0; st < STAGES - 1; ++st)
+            if (st < nsteps) issue(st, st);
+        if (nsteps > 0) {
+            wait_steps<LOADS, STAGES - 2>(min(STAGES - 2, nsteps - 1));
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            read_d(std::integral_constant<int, 0>(), std::integral_constant<int, 0>());
+            [&]<int... J>(std::integer_sequence<int, J...>) {
+                (read_x(std::integral_constant<int, 0>(), std::integral_constant<int, J>()), ...);
+            }(std::make_integer_sequence<int, NTW>());
+        }
+        TAPS_STAMP(1);
+        // steady state: STAGES straight-line steps per iteration while every step has its DMA;
+        // then the tail with run-time conditions
+        int s = 0;
+        for (; s + 2 * STAGES - 2 < nsteps; s += STAGES) {
+            [&]<int... U>(std::integer_sequence<int, U...>) {
+                (body(std::integral_constant<int, U>(), std::true_type(), s + U), ...);
+            }(std::make_integer_sequence<int, STAGES>());
+        }
+        for (; s < nsteps; s += STAGES) {
+            [&]<int... U>(std::integer_sequence<int, U...>) {
+                ((s + U < nsteps ? body(std::integral_constant<int, U>(), std::false_type(), s + U) : void()), ...);
+            }(std::make_integer_sequence<int, STAGES>());
+        }
+        lgkm_wait<0>();
+        __syncthreads();
+        TAPS_STAMP(2);
+
+        // the two K groups meet: K group 0 keeps taps [0, KA) of the wave's set, group 1 the
+        // rest; each sends the other part (MFMA C layout, 16-byte LDS writes), adds its
+        // partner's, then writes the kept tiles row-major into the staged tile ct [64][LDT]
+        constexpr int KA = (NTW + 1) / 2;
+        v4i* xbuf = (v4i*)smem;
+        const int xs0 = (th * 2 + cg) * TA * 256;  // v4i index of the wave pair's first tile
+#pragma unroll
+        for (int j = 0; j < NTW; ++j) {
+            const bool mine = kg == 0 ? j < KA : j >= KA;
+            if (!mine) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    xbuf[xs0 + j * 256 + q * 64 + lane] =
+                        v4i{acc[j][4 * q], acc[j][4 * q + 1], acc[j][4 * q + 2], acc[j][4 * q + 3]};
             }
         }
-    }
-
-    v16i acc[NT];
+        __syncthreads();
 #pragma unroll
-    for (int t = 0; t < NT; ++t)
+        for (int j = 0; j < NTW; ++j) {
+            const bool mine = kg == 0 ? j < KA : j >= KA;
+            if (mine) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) acc[t][i] = 0;
-    // the dy fragment is double-buffered (read early in the previous step's stream); a tap's x
-    // fragment is re-read into the same registers right after its MFMA
-    v4i fd[2], fx[NT];
-
-    auto read_d = [&](auto st_c, auto buf_c) {
-        constexpr int ST = decltype(st_c)::value, BUF = decltype(buf_c)::value;
-        const v2i d0 = tr8_at<ST * SB>(aD), d1 = tr8_at<ST * SB + 512>(aD);
-        fd[BUF] = v4i{d0[0], d0[1], d1[0], d1[1]};
-    };
-    auto read_x = [&](auto st_c, auto t_c) {
-        constexpr int ST = decltype(st_c)::value, T = decltype(t_c)::value;
-        const v2i x0 = tr8_at<ST * SB>(aX[T][0]), x1 = tr8_at<ST * SB>(aX[T][1]);
-        fx[T] = v4i{x0[0], x0[1], x1[0], x1[1]};
-    };
-    // MFMA t of step s (stage ST, dy buffer CUR); after it: tap t of step s + 1 (and, after
-    // MFMA 0, its dy); the LDS-DMA of step s + STAGES - 1 after MFMA 1.  Before MFMA t a counted
-    // lgkm wait lets through only the reads younger than tap t's (clamped at 15: conservative).
-    // SS: steady state (a next step and the DMA step both exist: straight-line code); else
-    // `more` / `dma` decide at run time (the last steps of the block).
-    auto gap = [&](auto u_c, auto t_c, auto ss_c, int s, bool more, bool dma) {
-        constexpr int U = decltype(u_c)::value, T = decltype(t_c)::value;
-        constexpr bool SS = decltype(ss_c)::value;
-        constexpr int ST = U % STAGES, CUR = U & 1, NST = (ST + 1) % STAGES;
-        if (SS || more)
-            lgkm_wait<2 * (NT - 1 - T) + (T > 0 ? 2 * T + 2 : 0)>();
-        else
-            lgkm_wait<2 * (NT - 1 - T)>();
-        reg_fence(fx[T]);
-        if constexpr (T == 0) reg_fence(fd[CUR]);
-        if (NITI_ABLATE == 2)
-            acc[T][0] += fd[CUR][0] ^ fx[T][1];
-        else
-            acc[T] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fd[CUR], fx[T], acc[T], 0, 0, 0);
-        if (SS || more) {
-            if constexpr (T == 0) read_d(std::integral_constant<int, NST>(), std::integral_constant<int, CUR ^ 1>());
-            read_x(std::integral_constant<int, NST>(), t_c);
+                for (int q = 0; q < 4; ++q) {
+                    const v4i v = xbuf[xs0 + j * 256 + q * 64 + lane];
+                    acc[j][4 * q] += v[0];
+                    acc[j][4 * q + 1] += v[1];
+                    acc[j][4 * q + 2] += v[2];
+                    acc[j][4 * q + 3] += v[3];
+                }
+            }
         }
-        if constexpr (T == 1) {
-            if (SS || dma) issue((ST + STAGES - 1) % STAGES, s + STAGES - 1);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-    };
-    auto body = [&](auto u_c, auto ss_c, int s) {
-        constexpr bool SS = decltype(ss_c)::value;
-        const bool more = s + 1 < nsteps, dma = s + STAGES - 1 < nsteps;
-        // own loads of step s + 1 landed (steps up to s + 2 may be in flight)
-        if (SS)
-            wait_vmcnt<(STAGES - 3) * LOADS>();
-        else if (more)
-            wait_steps<LOADS, STAGES - 3>(min(STAGES - 3, nsteps - 2 - s));
-        if (NITI_ABLATE != 4) __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-        [&]<int... T>(std::integer_sequence<int, T...>) {
-            (gap(u_c, std::integral_constant<int, T>(), ss_c, s, more, dma), ...);
-        }(std::make_integer_sequence<int, NT>());
-    };
-
+        __syncthreads();  // ct overlays the exchange buffer
+        int32_t* ct = (int32_t*)smem;
 #pragma unroll
-    for (int st = 0; st < STAGES - 1; ++st)
-        if (st < nsteps) issue(st, st);
-    if (nsteps > 0) {
-        wait_steps<LOADS, STAGES - 2>(min(STAGES - 2, nsteps - 1));
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-        read_d(std::integral_constant<int, 0>(), std::integral_constant<int, 0>());
-        [&]<int... T>(std::integer_sequence<int, T...>) {
-            (read_x(std::integral_constant<int, 0>(), std::integral_constant<int, T>()), ...);
-        }(std::make_integer_sequence<int, NT>());
-    }
-    TAPS_STAMP(1);
-    // steady state: UNR straight-line steps per iteration while every step has its DMA; then
-    // the tail with run-time conditions, UNR steps per iteration
-    int s = 0;
-    for (; s + UNR + STAGES - 2 < nsteps; s += UNR) {
-        [&]<int... U>(std::integer_sequence<int, U...>) {
-            (body(std::integral_constant<int, U>(), std::true_type(), s + U), ...);
-        }(std::make_integer_sequence<int, UNR>());
-    }
-    for (; s < nsteps; s += UNR) {
-        [&]<int... U>(std::integer_sequence<int, U...>) {
-            ((s + U < nsteps ? body(std::integral_constant<int, U>(), std::false_type(), s + U) : void()), ...);
-        }(std::make_integer_sequence<int, UNR>());
-    }
-    lgkm_wait<0>();
-    __syncthreads();
-    TAPS_STAMP(2);
-
-    // the 4 K groups meet, TR taps per round: every wave writes its partial [tap][32][32] to its
-    // slot, then each thread sums one 4-element chunk of a row over the 4 K groups' slots into
-    // the staged tile ct [64][LDT] (row = output channel, column = tap * 32 + channel)
-    int32_t* ct = (int32_t*)smem;
-    int32_t* slot = (int32_t*)(smem + CT);
-#pragma unroll
-    for (int t0 = 0; t0 < NT; t0 += TR) {
-#pragma unroll
-        for (int u = 0; u < TR; ++u) {
-            if (t0 + u < NT) {
+        for (int j = 0; j < NTW; ++j) {
+            const bool mine = kg == 0 ? j < KA : j >= KA;
+            if (mine) {
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {
-                    const int row = (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
-                    slot[wid * (SLOT / 4) + (u * 32 + row) * 32 + (lane & 31)] = acc[t0 + u][i];
+                    const int row = cg * 32 + (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
+                    ct[row * LDT + (T0 + j) * 32 + (lane & 31)] = acc[j][i];
                 }
             }
         }
-        __syncthreads();
-        {
-            // 64 rows x 8 chunks per tap: one chunk per thread
-#pragma unroll
-            for (int uu = 0; uu < TR; ++uu) {
-                if (t0 + uu < NT) {
-                    const int row = tid >> 3, ch = tid & 7;  // 64 rows x 8 chunks = 512 threads
-                    const int c = row >> 5, r = row & 31;
-                    v4i sum = {0, 0, 0, 0};
-#pragma unroll
-                    for (int k = 0; k < 4; ++k)
-                        sum += *(const v4i*)(slot + (2 * k + c) * (SLOT / 4) + (uu * 32 + r) * 32 + ch * 4);
-                    *(v4i*)(ct + row * LDT + (t0 + uu) * 32 + ch * 4) = sum;
-                }
-            }
-        }
-        __syncthreads();
-    }
+    };
+    if (th == 0)
+        run(std::integral_constant<int, 0>());
+    else
+        run(std::integral_constant<int, 1>());
+    __syncthreads();
     TAPS_STAMP(3);
     // 16-byte row chunks: 8 consecutive threads write one 128-byte (tap, 32-channel) segment
+    const int32_t* ct = (const int32_t*)smem;
     int32_t* Cs = MODE == EPI_SLAB ? epi.C + (int64_t)split * epi.slab_stride : epi.C;
     constexpr int CPR = NT * 8;  // chunks per tile row
     const int rows = min(64, g.c_out - co0);
@@ -1413,7 +1427,11 @@ __global__ void __launch_bounds__(TAPS_THREADS) wgrad_taps_kernel(WgTaps g, Epi 
         const int row = c / CPR, rem = c - row * CPR;
         const int t = rem >> 3, part = rem & 7;
         const v4i v = *(const v4i*)(ct + row * LDT + t * 32 + part * 4);
-        *(v4i*)(Cs + (int64_t)(co0 + row) * epi.ldc + t * g.CIP + ci0 + part * 4) = v;
+        v4i* dst = (v4i*)(Cs + (int64_t)(co0 + row) * epi.ldc + t * g.CIP + ci0 + part * 4);
+        if (NITI_TAPS_NT)
+            __builtin_nontemporal_store(v, dst);
+        else
+            *dst = v;
         if (MODE == EPI_STORE) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
@@ -1448,7 +1466,7 @@ enum Strategy { STRAT_STORE = 0, STRAT_RECOMPUTE = 1, STRAT_SLAB = 2 };
 struct GemmPlan {
     int bm = 128, bn = 128, tiles = 1, splits = 1, kc_per_split = 0;
     Strategy strat = STRAT_STORE;
-    bool taps = false;  // weight gradient on wgrad_taps_kernel (kc_per_split counts 128-pixel steps)
+    bool taps = false;  // weight gradient on wgrad_taps_kernel (kc_per_split counts 64-pixel region steps)
 };
 
 // k_total: K extent in the kernel's units (16-byte chunks for KT = false, k rows for
@@ -1836,7 +1854,7 @@ static bool wgrad_taps_geom(const ConvGeom& g, const int8_t* x, const int8_t* dy
     if (const char* f = getenv("NITI_DIAG_NO_TAPS")) {  // diagnostics / tests: generic KT GEMM only
         if (atoi(f) != 0) return false;
     }
-    if (g.kh * g.kw != 9 || g.sh != 1 || g.sw != 1 || g.dh != 1 || g.dw != 1) return false;
+    if (g.kh != 3 || g.kw != 3 || g.sh != 1 || g.sw != 1 || g.dh != 1 || g.dw != 1) return false;
     if (g.cip % 32 != 0 || g.cop % 64 != 0) return false;
     const int64_t ohw = (int64_t)g.oh * g.ow;
     const int64_t K = (int64_t)g.n * ohw;
@@ -1875,7 +1893,7 @@ static bool wgrad_taps_geom(const ConvGeom& g, const int8_t* x, const int8_t* dy
     w.pl = g.pl;
     w.c_out = g.c_out;
     w.rs_total = (int)(K / 64);
-    w.steps_total = (w.rs_total + 1) / 2;
+    w.steps_total = w.rs_total;
     w.steps_per_split = w.steps_total;
     w.tiles_ci = g.cip / 32;
     w.tiles = (g.cop / 64) * w.tiles_ci;
