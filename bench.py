@@ -71,6 +71,8 @@ def main():
     ap.add_argument("--graph", action="store_true", help="replay the step as a hipGraph (slower on ROCm 7.2)")
     ap.add_argument("--no-autotune", action="store_true", help="keep the fixed default GEMM plans")
     ap.add_argument("--no-overlap", action="store_true", help="weight gradients on the step stream")
+    ap.add_argument("--probe-plan", default="", help="bm,bn,splits,strategy forced on the probed GEMM after "
+                                                     "autotuning (PMC passes re-use the timed run's plan)")
     args = ap.parse_args()
 
     import numpy as np
@@ -113,12 +115,14 @@ def main():
         model.autotune()
         torch.cuda.synchronize()
         tune_s = time.perf_counter() - ta
+    probe_layer = args.probe_layer if args.probe_layer < len(model.layers) else len(model.layers) - 1
+    if args.probe_plan:
+        model.set_plan(probe_layer, args.probe_phase, [int(v) for v in args.probe_plan.split(",")])
     plans = model.plans()
 
     # The probe (HIP events around one GEMM, on the stream it runs on) is armed before the
     # warmup: the step is replayed as a hipGraph and arming it re-captures the graph, which
     # must not happen inside the timed region.  Warmup launches are read and discarded.
-    probe_layer = args.probe_layer if args.probe_layer < len(model.layers) else len(model.layers) - 1
     model.set_probe(probe_layer, args.probe_phase, args.steps + args.warmup)
     for _ in range(args.warmup):
         model.train_step(x, -3, labels)
@@ -139,7 +143,22 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     probe_ms, probe_n = model.probe_read()
+    span_ms, span_n = model.probe_read_span()
+    # the same launch alone (after the timed region, nothing else on the GPU): in the step the
+    # weight gradients share the chip with the input-gradient chain on the other stream
+    iso_reps = 20
+    model.set_probe(probe_layer, args.probe_phase, iso_reps)
+    for _ in range(iso_reps):
+        model.run_phase(probe_layer, args.probe_phase)
+    torch.cuda.synchronize()
+    iso_ms, iso_n = model.probe_read()
+    iso_span_ms, iso_span_n = model.probe_read_span()
     model.set_probe(-1, 0, 0)
+    # HIP events on the launch stream time the launch (dispatch to completion, as rocprofv3 does);
+    # the weight-gradient kernel also times itself from inside (first block start -> last block
+    # end on the device wall clock), which leaves out its launch ramp and end-of-kernel writeback
+    span_us = span_ms / span_n * 1e3 if span_n else None
+    iso_span_us = iso_span_ms / iso_span_n * 1e3 if iso_span_n else None
 
     ms_per_step = elapsed / args.steps * 1e3
     images = args.batch * world * args.steps
@@ -151,6 +170,8 @@ def main():
     k_ops = 2 * args.batch * pl["oh"] * pl["ow"] * pl["c_out"] * pl["c_in"] * pl["kh"] * pl["kw"]
     k_avg_s = probe_ms / max(probe_n, 1) / 1e3
     achieved = k_ops / k_avg_s / 1e12 if probe_n else None
+    iso_s = iso_ms / max(iso_n, 1) / 1e3
+    iso_achieved = k_ops / iso_s / 1e12 if iso_n else None
     traffic = None
     tfile = os.path.join(ROOT, "profiles", "traffic.json")
     if os.path.exists(tfile):
@@ -169,6 +190,14 @@ def main():
                          f"reference-structured C restatement, float32 accumulation), {secs:.1f} s"}
 
     phase_name = {0: "forward conv", 1: "input-gradient conv", 2: "weight-gradient conv"}[args.probe_phase]
+    pplan = plans[(probe_layer, args.probe_phase)]
+    if args.probe_phase == 2 and pplan[0] == 32:
+        kname = ("wgrad_taps_kernel: tap-sharing weight gradient, one padded input region per 64-pixel step "
+                 f"for all 9 taps, {pplan[2]} K splits")
+    elif args.probe_phase == 2:
+        kname = f"gemm_kernel {pplan[0]}x{pplan[1]}, K-major over pixels, {pplan[2]} K splits"
+    else:
+        kname = f"gemm_kernel {pplan[0]}x{pplan[1]}, implicit im2col"
     line = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -190,9 +219,7 @@ def main():
         "int8_mfma_tops": round(tops, 2),
         "int8_mfma_frac_of_peak": round(tops / PEAK_INT8_TOPS, 4),
         "roofline": {
-            "kernel": f"VGG-11 conv{probe_layer + 1} {phase_name} GEMM launch (gemm_kernel, "
-                      f"{'K-major over pixels, split-K slabs' if args.probe_phase == 2 else 'implicit im2col'}; "
-                      f"layer index {probe_layer})",
+            "kernel": f"VGG-11 conv{probe_layer + 1} {phase_name} launch ({kname}; layer index {probe_layer})",
             "bound": "mfma",
             "achieved": round(achieved, 2) if achieved else None,
             "peak": round(PEAK_INT8_TOPS, 1),
@@ -200,9 +227,17 @@ def main():
             "frac": round(achieved / PEAK_INT8_TOPS, 4) if achieved else None,
             "traffic": traffic,
             "avg_launch_us": round(k_avg_s * 1e6, 2) if probe_n else None,
+            "timing": "HIP events on the launch stream",
+            "in_kernel_span_us": round(span_us, 2) if span_us else None,
             "launches": probe_n,
             "ops_per_launch": k_ops,
             "plan": dict(zip(("bm", "bn", "splits", "strategy"), plans[(probe_layer, args.probe_phase)])),
+            "isolated": {"avg_launch_us": round(iso_s * 1e6, 2) if iso_n else None,
+                         "achieved": round(iso_achieved, 2) if iso_achieved else None,
+                         "frac": round(iso_achieved / PEAK_INT8_TOPS, 4) if iso_achieved else None,
+                         "launches": iso_n,
+                         "in_kernel_span_us": round(iso_span_us, 2) if iso_span_us else None,
+                         "note": "same launch re-run alone after the timed region (no side-stream overlap)"},
         },
         "autotune_s": round(tune_s, 2) if not args.no_autotune else None,
         "cpu_baseline": cpu,

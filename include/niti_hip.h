@@ -241,6 +241,14 @@ void niti_plan_reset(void);
  * duration and the number of launches timed, then resets the count. */
 int niti_model_set_probe(niti_model_t m, int layer, int phase, int max_launches);
 int niti_model_probe_read(niti_model_t m, double* total_ms, int* count);
+/* Weight-gradient probes (phase 2) also time the launch from inside: the kernel min-es its
+ * blocks' start and max-es their end on the device wall clock (s_memrealtime); this returns the
+ * summed first-block-start -> last-block-end spans and their count, then re-arms. */
+int niti_model_probe_read_span(niti_model_t m, double* total_ms, int* count);
+/* Runs one layer phase of the last step again on `stream` (phase 0 forward, 1 input gradient,
+ * 2 weight gradient; buffers as the step left them, weights untouched), single-device and
+ * without the side stream: the isolated measurement next to the in-step probe. */
+int niti_model_run_phase(niti_model_t m, int layer, int phase, void* stream);
 
 /* ---- data parallel over RCCL (xGMI) ---------------------------------------------------- */
 #define NITI_UNIQUE_ID_BYTES 128

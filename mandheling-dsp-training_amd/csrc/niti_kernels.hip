@@ -19,6 +19,8 @@
 #include <algorithm>
 #include <stdio.h>
 
+#include <hip/hip_ext.h>
+
 #include "niti_kernels.hpp"
 #include "niti_map.hpp"
 
@@ -272,8 +274,21 @@ struct Epi {
     const int8_t* exp_in = nullptr;
     const int8_t* wscale = nullptr;
     int8_t* exp_out = nullptr;
+    unsigned long long* span = nullptr;  // kernel-span probe slot (probe_span_arm)
 };
 
+
+// kernel-span probe: first block start / last block end on the device wall clock
+__device__ __forceinline__ void span_begin(unsigned long long* span) {
+    if (span != nullptr && threadIdx.x == 0) atomicMin(span, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+}
+__device__ __forceinline__ void span_end(unsigned long long* span) {
+    if (span != nullptr) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) atomicMax(span + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    }
+}
 
 // bijective XCD remap: blocks b, b+8, b+16, ... (one XCD under round-robin dispatch) get
 // consecutive tile ids.  Speed only; any placement is correct.
@@ -842,6 +857,7 @@ __global__ void __launch_bounds__(NW * 64) gemm_kernel(LA la, LB lb, int M, int 
     static_assert(SMEM >= BM * (BN + 16), "requant epilogue staging fits in the pipeline's LDS");
     __shared__ __attribute__((aligned(16))) int8_t smem[SMEM];
 
+    span_begin(epi.span);
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: LDS bases stay scalar
@@ -1050,6 +1066,7 @@ __global__ void __launch_bounds__(NW * 64) gemm_kernel(LA la, LB lb, int M, int 
         gemm_epilogue<TH, TN, NW, MODE, BM, BN>(keep, m0 + wm * (BM / WM) + keep_a * 32, n0 + wn * (BN / WN), M, N,
                                                 epi, smem, split, m0, n0);
     }
+    span_end(epi.span);
 }
 
 // Sum of K-split slabs -> C (+ max|C|).  A block covers 256/G v4i elements with G threads
@@ -1145,6 +1162,7 @@ struct WgTaps {
     int tiles_ci, tiles;  // 32-channel input tiles; tiles per K split
     FastDiv fRW, fRPI, fPPI, fOW, fOHW, fTiles, fTci, fBPI;
     unsigned long long* stamps;  // diagnostic builds (NITI_STAMPS): per-block s_memtime marks
+    unsigned long long* span;    // kernel-span probe slot (probe_span_arm)
 };
 #ifndef NITI_STAMPS
 #define NITI_STAMPS 0
@@ -1190,6 +1208,7 @@ __global__ void __launch_bounds__(TAPS_THREADS) wgrad_taps_kernel(WgTaps g, Epi 
     __shared__ __attribute__((aligned(16))) int8_t smem[SMEM];
 
     const int tid = threadIdx.x;
+    span_begin(g.span);
     TAPS_STAMP(0);
     const int lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1457,8 +1476,29 @@ __global__ void __launch_bounds__(TAPS_THREADS) wgrad_taps_kernel(WgTaps g, Epi 
         __syncthreads();
         TAPS_STAMP(5);
     }
+    span_end(g.span);
 }
 
+
+// Kernel-event probe: the next weight-gradient launch records these two events as part of its
+// own dispatch (hipExtLaunchKernel), i.e. the kernel's begin / end as rocprofv3 sees them.
+static hipEvent_t g_ev_next[2] = {nullptr, nullptr};
+void probe_events_arm(hipEvent_t begin, hipEvent_t end) {
+    g_ev_next[0] = begin;
+    g_ev_next[1] = end;
+}
+static void take_events(hipEvent_t* b, hipEvent_t* e) {
+    *b = g_ev_next[0];
+    *e = g_ev_next[1];
+    g_ev_next[0] = g_ev_next[1] = nullptr;
+}
+static unsigned long long* g_span_next = nullptr;
+void probe_span_arm(unsigned long long* slot) { g_span_next = slot; }
+static unsigned long long* take_span() {
+    unsigned long long* p = g_span_next;
+    g_span_next = nullptr;
+    return p;
+}
 
 // ------------------------------------------------------------------------------ planning
 enum Strategy { STRAT_STORE = 0, STRAT_RECOMPUTE = 1, STRAT_SLAB = 2 };
@@ -1597,12 +1637,18 @@ static hipError_t launch_mode(const GemmPlan& p, const LA& la, const LB& lb, int
     const int k_step = KT ? KT_BK : LA::BK / 16;
     const int splits = MODE == EPI_SLAB ? p.splits : 1;
     const int per = MODE == EPI_SLAB ? p.kc_per_split : ((k_total + k_step - 1) / k_step) * k_step;
-#define NITI_LAUNCH(BM_, BN_, WM_, WN_, NW_)                                                                     \
-    do {                                                                                                         \
-        const int tm = (M + BM_ - 1) / BM_, tn = (N + BN_ - 1) / BN_;                                            \
-        dim3 grid(tm * tn, splits);                                                                              \
-        hipLaunchKernelGGL((gemm_kernel<BM_, BN_, WM_, WN_, LA, LB, MODE, KT, NW_>), grid, dim3(NW_ * 64), 0, st, \
-                           la, lb, M, N, tn, k_total, per, epi);                                                 \
+    hipEvent_t ev_b = nullptr, ev_e = nullptr;
+    if (KT) take_events(&ev_b, &ev_e);  // weight gradient: the kernel-event probe, if armed
+#define NITI_LAUNCH(BM_, BN_, WM_, WN_, NW_)                                                                      \
+    do {                                                                                                          \
+        const int tm = (M + BM_ - 1) / BM_, tn = (N + BN_ - 1) / BN_;                                             \
+        dim3 grid(tm * tn, splits);                                                                               \
+        if (ev_b != nullptr)                                                                                      \
+            hipExtLaunchKernelGGL((gemm_kernel<BM_, BN_, WM_, WN_, LA, LB, MODE, KT, NW_>), grid, dim3(NW_ * 64), \
+                                  0, st, ev_b, ev_e, 0, la, lb, M, N, tn, k_total, per, epi);                     \
+        else                                                                                                      \
+            hipLaunchKernelGGL((gemm_kernel<BM_, BN_, WM_, WN_, LA, LB, MODE, KT, NW_>), grid, dim3(NW_ * 64), 0, \
+                               st, la, lb, M, N, tn, k_total, per, epi);                                          \
     } while (0)
     // per-wave tiles: 64x64 (two wave groups over K for 128x128), 64x32 / 32x64 for the
     // 4-wave shapes, 128x64 for 256x256
@@ -1640,6 +1686,7 @@ template <class LA, class LB, bool KT = false>
 static hipError_t gemm_acc_plan(const GemmPlan& p, const LA& la, const LB& lb, int M, int N, int kc_total, int32_t* C,
                                 uint32_t* amax, int32_t* ws, hipStream_t st, hipEvent_t after_gemm = nullptr) {
     Epi e;
+    if (KT) e.span = take_span();  // weight gradient: the kernel-span probe slot, if armed
     if (p.strat == STRAT_SLAB) {
         e.C = ws;
         e.ldc = N;
@@ -1968,15 +2015,25 @@ static hipError_t launch_taps(const GemmPlan& p, WgTaps t, const Epi& e, hipStre
     t.steps_per_split = MODE == EPI_SLAB ? p.kc_per_split : t.steps_total;
     const dim3 grid((unsigned)(t.tiles * splits));
     t.stamps = nullptr;
+    t.span = e.span;
 #if NITI_STAMPS
     static unsigned long long* sbuf = nullptr;
     if (sbuf == nullptr && hipMalloc(&sbuf, 4096 * 8 * 8) != hipSuccess) sbuf = nullptr;
     if (grid.x <= 4096) t.stamps = sbuf;
 #endif
-    if (t.imgs * t.RH * t.RW * 32 > 4096)
-        hipLaunchKernelGGL((wgrad_taps_kernel<9, 2, MODE>), grid, dim3(TAPS_THREADS), 0, st, t, e);
-    else
-        hipLaunchKernelGGL((wgrad_taps_kernel<9, 1, MODE>), grid, dim3(TAPS_THREADS), 0, st, t, e);
+    hipEvent_t ev_b = nullptr, ev_e = nullptr;
+    take_events(&ev_b, &ev_e);  // the kernel-event probe, if armed
+    if (t.imgs * t.RH * t.RW * 32 > 4096) {
+        if (ev_b != nullptr)
+            hipExtLaunchKernelGGL((wgrad_taps_kernel<9, 2, MODE>), grid, dim3(TAPS_THREADS), 0, st, ev_b, ev_e, 0, t, e);
+        else
+            hipLaunchKernelGGL((wgrad_taps_kernel<9, 2, MODE>), grid, dim3(TAPS_THREADS), 0, st, t, e);
+    } else {
+        if (ev_b != nullptr)
+            hipExtLaunchKernelGGL((wgrad_taps_kernel<9, 1, MODE>), grid, dim3(TAPS_THREADS), 0, st, ev_b, ev_e, 0, t, e);
+        else
+            hipLaunchKernelGGL((wgrad_taps_kernel<9, 1, MODE>), grid, dim3(TAPS_THREADS), 0, st, t, e);
+    }
 #if NITI_STAMPS
     if (t.stamps) taps_stamp_report(t.stamps, (int)grid.x, st);
 #endif
@@ -1986,6 +2043,7 @@ static hipError_t launch_taps(const GemmPlan& p, WgTaps t, const Epi& e, hipStre
 static hipError_t wgrad_taps_run(const GemmPlan& p, const WgTaps& t, int M, int N, int32_t* C, uint32_t* amax,
                                  int32_t* ws, hipStream_t st, hipEvent_t after_gemm) {
     Epi e;
+    e.span = take_span();
     if (p.strat == STRAT_SLAB) {
         e.C = ws;
         e.ldc = N;

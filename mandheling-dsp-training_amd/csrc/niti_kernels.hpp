@@ -88,6 +88,13 @@ hipError_t conv_fwd_acc(const ConvGeom& g, const int8_t* x_nhwc16, const int8_t*
 // acc[M = n*h*w][cip] = transposed conv of dy (NHWC16) with w^T (IHWO16): the input gradient
 hipError_t conv_dgrad_acc(const ConvGeom& g, const int8_t* dy_nhwc16, const int8_t* wt_ihwo16, int32_t* acc,
                           uint32_t* amax, void* ws, size_t ws_bytes, hipStream_t st);
+// Kernel-span probe: the next weight-gradient GEMM launch (either kernel) min-es its blocks'
+// start and max-es their end s_memrealtime (device wall clock) into slot[0] / slot[1]; the slot
+// is consumed by that launch.  Host-side, not thread-safe (one model per thread).
+void probe_span_arm(unsigned long long* slot);
+// Kernel-event probe: the next weight-gradient GEMM launch records `begin` / `end` as part of its
+// own dispatch (hipExtLaunchKernel: the kernel's begin and end, as rocprofv3 times it).
+void probe_events_arm(hipEvent_t begin, hipEvent_t end);
 // acc[co][kh][kw][cip] = sum over (n, oy, ox) of dy * x (x, dy NHWC16): the weight gradient,
 // a K-major GEMM over pixels whose operand tiles are transposed in LDS (ds_read_b64_tr_b8)
 hipError_t conv_wgrad_acc(const ConvGeom& g, const int8_t* x_nhwc16, const int8_t* dy_nhwc16, int32_t* acc,

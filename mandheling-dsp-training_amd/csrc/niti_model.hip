@@ -145,6 +145,22 @@ struct Model {
     // graph the probe points are segment boundaries and the events go between the launches
     int probe_layer = -1, probe_phase = -1, probe_count = 0;
     std::vector<hipEvent_t> ev0, ev1;
+    // kernel-span probe (weight gradient): per launch {min block start, max block end} on the
+    // device wall clock, written by the kernel itself (niti_kernels.hpp probe_span_arm)
+    unsigned long long* span = nullptr;
+    int span_cap = 0, span_count = 0;
+    void arm_kernel_events(int layer, int phase) {
+        if (layer != probe_layer || phase != probe_phase || tuning || capturing || probe_count >= (int)ev0.size())
+            return;
+        probe_events_arm(ev0[probe_count], ev1[probe_count]);
+        ++probe_count;
+    }
+    void arm_span(int layer, int phase) {
+        if (layer != probe_layer || phase != probe_phase || tuning || capturing || span == nullptr ||
+            span_count >= span_cap)
+            return;
+        probe_span_arm(span + 2 * span_count++);
+    }
     void probe(int layer, int phase, bool begin, hipStream_t st) {
         if (layer != probe_layer || phase != probe_phase || tuning) return;
         if (capturing) {
@@ -172,6 +188,9 @@ struct Model {
         ev1.clear();
         probe_count = 0;
         probe_layer = probe_phase = -1;
+        if (span) (void)hipFree(span);
+        span = nullptr;
+        span_cap = span_count = 0;
     }
 
     int build(int arch_, int batch_);
@@ -422,9 +441,14 @@ int Model::wgrad_layer(int i, hipStream_t st) {
     const ConvGeom& g = l.g;
     const int64_t we = l.w_elems();
     // the weight-gradient probe brackets the GEMM launch alone (not its split-K reduce)
-    probe(i, 2, true, st);
+    // the weight-gradient probe is the GEMM launch's own begin / end (its split-K reduce excluded)
+    if (capturing)
+        probe(i, 2, true, st);
+    else
+        arm_kernel_events(i, 2);
+    arm_span(i, 2);
     MTRY(conv_wgrad_acc(g, l.in, l.dy, l.dwacc, dp ? nullptr : rng(i, 2), slab_w, slab_w_bytes, st,
-                        probe_end_event(i, 2)));
+                        capturing ? probe_end_event(i, 2) : nullptr));
     if (dp) {
         CTRY(ncclAllReduce(l.dwacc, l.dwacc, (size_t)we, ncclInt32, ncclSum, st == side ? comm_w : comm, st));
         MTRY(absmax_i32(l.dwacc, we, rng(i, 2), st));
@@ -771,6 +795,20 @@ int niti_model_autotune(niti_model_t m, int reps, void* stream) {
     return m->m.autotune((hipStream_t)stream, reps);
 }
 
+int niti_model_run_phase(niti_model_t m, int layer, int phase, void* stream) {
+    if (!m || layer < 0 || layer >= (int)m->m.L.size() || phase < 0 || phase > 2 || (phase == 1 && layer == 0))
+        return NITI_INVALID_VALUE;
+    const bool t = m->m.tuning;
+    m->m.tuning = false;  // keep the probe armed; collectives stay off (single-device phase)
+    ncclComm_t c = m->m.comm;
+    m->m.comm = nullptr;
+    hipStream_t st = (hipStream_t)stream;
+    const int rc = phase == 0 ? m->m.fwd_layer(layer, st) : phase == 1 ? m->m.dgrad_layer(layer, st) : m->m.wgrad_layer(layer, st);
+    m->m.comm = c;
+    m->m.tuning = t;
+    return rc;
+}
+
 int niti_model_plan_info(niti_model_t m, int layer, int phase, int info[4]) {
     if (!m || !info || layer < 0 || layer >= (int)m->m.L.size() || phase < 0 || phase > 2)
         return NITI_INVALID_VALUE;
@@ -822,9 +860,52 @@ int niti_model_set_probe(niti_model_t m, int layer, int phase, int max_launches)
     m->m.ev0.resize(max_launches);
     m->m.ev1.resize(max_launches);
     for (int i = 0; i < max_launches; ++i)
-        if (hipEventCreateWithFlags(&m->m.ev0[i], hipEventReleaseToDevice) != hipSuccess ||
-            hipEventCreateWithFlags(&m->m.ev1[i], hipEventReleaseToDevice) != hipSuccess)
+        // timing events without the system-scope cache writeback / invalidate (it delays the
+        // launch after the begin marker and is not needed to read the timestamps)
+        if (hipEventCreateWithFlags(&m->m.ev0[i], hipEventDisableSystemFence) != hipSuccess ||
+            hipEventCreateWithFlags(&m->m.ev1[i], hipEventDisableSystemFence) != hipSuccess)
             return NITI_OUT_OF_MEMORY;
+    if (phase == 2 && max_launches > 0) {
+        std::vector<unsigned long long> init(2 * (size_t)max_launches);
+        for (int i = 0; i < max_launches; ++i) {
+            init[2 * i] = ~0ull;
+            init[2 * i + 1] = 0;
+        }
+        if (hipMalloc(&m->m.span, init.size() * 8) != hipSuccess ||
+            hipMemcpy(m->m.span, init.data(), init.size() * 8, hipMemcpyHostToDevice) != hipSuccess)
+            return NITI_OUT_OF_MEMORY;
+        m->m.span_cap = max_launches;
+    }
+    return NITI_NO_ERROR;
+}
+
+int niti_model_probe_read_span(niti_model_t m, double* total_ms, int* count) {
+    if (!m || !total_ms || !count) return NITI_INVALID_VALUE;
+    *total_ms = 0;
+    *count = 0;
+    if (m->m.span == nullptr || m->m.span_count == 0) return NITI_NO_ERROR;
+    int dev = 0, khz = 0;
+    if (hipDeviceSynchronize() != hipSuccess || hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0)
+        return NITI_NO_EXECUTION;
+    std::vector<unsigned long long> h(2 * (size_t)m->m.span_count);
+    if (hipMemcpy(h.data(), m->m.span, h.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return NITI_NO_EXECUTION;
+    double t = 0;
+    int n = 0;
+    for (int i = 0; i < m->m.span_count; ++i)
+        if (h[2 * i + 1] > h[2 * i]) {
+            t += (double)(h[2 * i + 1] - h[2 * i]) / khz;  // ticks / kHz = ms
+            ++n;
+        }
+    *total_ms = t;
+    *count = n;
+    // re-arm the slots for the next measurement
+    for (size_t i = 0; i < h.size(); i += 2) {
+        h[i] = ~0ull;
+        h[i + 1] = 0;
+    }
+    if (hipMemcpy(m->m.span, h.data(), h.size() * 8, hipMemcpyHostToDevice) != hipSuccess) return NITI_NO_EXECUTION;
+    m->m.span_count = 0;
     return NITI_NO_ERROR;
 }
 

@@ -110,6 +110,16 @@ class NitiModel:
         check(self._lib.niti_model_probe_read(self._h, C.byref(t), C.byref(n)), "probe_read")
         return float(t.value), int(n.value)
 
+    def run_phase(self, layer: int, phase: int, stream=None):
+        """One layer phase of the last step again (0 fwd, 1 input grad, 2 weight grad), alone."""
+        check(self._lib.niti_model_run_phase(self._h, int(layer), int(phase), _stream(stream)), "run_phase")
+
+    def probe_read_span(self):
+        """(summed ms, launches) of the weight-gradient probe's in-kernel spans (device wall clock)."""
+        t, n = C.c_double(0), C.c_int(0)
+        check(self._lib.niti_model_probe_read_span(self._h, C.byref(t), C.byref(n)), "probe_read_span")
+        return t.value, n.value
+
     def step_macs(self) -> int:
         return int(self._lib.niti_model_step_macs(self._h))
 

@@ -3,8 +3,11 @@
 
 FETCH_SIZE / WRITE_SIZE are read per dispatch (KB); FETCH_SIZE is doubled (gfx950: it counts
 64 B per 128-B request, MI355X_MICROARCH.md HBM section).  The probe is the VGG-11 conv4 weight
-gradient GEMM: the KT gemm_kernel dispatch with the layer's grid (tiles x splits x 512 threads).
-usage: traffic.py <pmcF dir> <pmcW dir> [out.json] [grid_x_work_items grid_y]
+gradient launch, picked by kernel-name substring and grid (work items x, y) -- both from the
+bench line's roofline block.
+usage: traffic.py <pmcF dir> <pmcW dir> [out.json] [grid_x_work_items grid_y [name_substring [last_n]]]
+last_n: only the last n matching dispatches (bench.py re-runs the probed phase alone 20 times at
+the end, so the last 20 are the probe even when another layer's launch has the same grid)
 """
 import csv
 import glob
@@ -33,25 +36,31 @@ def main():
                 break
     gx = int(sys.argv[4]) if len(sys.argv) > 4 else 36 * 512
     gy = int(sys.argv[5]) if len(sys.argv) > 5 else 7
+    sub = sys.argv[6] if len(sys.argv) > 6 else "KtIm2colU"
     want = set()
+    kname = ""
     for f in glob.glob(f"{sys.argv[1]}/*kernel_trace.csv"):
         for r in csv.DictReader(open(f)):
-            if "KtIm2colU" in r["Kernel_Name"] and int(r["Grid_Size_X"]) == gx and int(r["Grid_Size_Y"]) == gy:
+            if sub in r["Kernel_Name"] and int(r["Grid_Size_X"]) == gx and int(r["Grid_Size_Y"]) == gy:
                 want.add(int(r["Dispatch_Id"]))
-    probes = []
-    for i in sorted(F):
-        if i in want:
-            probes.append((2 * F[i][2], W[i][2] if i in W else 0.0))
+                kname = r["Kernel_Name"].split("(")[0]
+    last_n = int(sys.argv[7]) if len(sys.argv) > 7 else 0
+    ids = [i for i in sorted(F) if i in want]
+    wids = [i for i in sorted(W) if sub in W[i][0] and W[i][1] == gx * gy]
+    if last_n:
+        ids, wids = ids[-last_n:], wids[-last_n:]
+    probes = [(2 * F[i][2], 0.0) for i in ids]
+    wr = [W[i][2] for i in wids]
     if not probes:
         sys.exit("probe dispatches not found")
     fetch = sum(p[0] for p in probes) / len(probes) * 1024
-    write = sum(p[1] for p in probes) / len(probes) * 1024
+    write = sum(wr) / max(len(wr), 1) * 1024
     print(f"probe launches {len(probes)}: fetch {fetch / 1e6:.2f} MB, write {write / 1e6:.2f} MB per launch")
     if len(sys.argv) > 3:
         out = {"vgg11_b256_L3_p2": {"hbm_bytes_per_launch": round(fetch + write),
                                     "fetch_bytes": round(fetch), "write_bytes": round(write),
                                     "launches_averaged": len(probes),
-                                    "kernel": "gemm_kernel<128,128,2,2,KtRowsU,KtIm2colU,SLAB,KT,8> (conv4 weight gradient)",
+                                    "kernel": f"{kname} (conv4 weight gradient)",
                                     "grid": [gx, gy],
                                     "method": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950) and --pmc WRITE_SIZE, separate passes"}}
         json.dump(out, open(sys.argv[3], "w"), indent=1)
