@@ -62,9 +62,12 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=256, help="images per GPU per step")
-    ap.add_argument("--arch", default="vgg11", choices=["vgg11", "lenet"])
-    ap.add_argument("--cpu-sample", type=int, default=128, help="images in the CPU baseline sample (0 = skip)")
+    ap.add_argument("--batch", type=int, default=0, help="images per GPU per step (0: 256 VGG-11 / LeNet, "
+                                                         "64 VGG-16 = BASELINE cfg 4's 512 over 8 GPUs)")
+    ap.add_argument("--arch", default="vgg11", choices=["vgg11", "lenet", "vgg16"])
+    ap.add_argument("--in-hw", type=int, default=0, help="input resolution (0: the architecture's own)")
+    ap.add_argument("--cpu-sample", type=int, default=-1, help="images in the CPU baseline sample "
+                                                               "(-1: 128 VGG-11 / LeNet, 1 VGG-16; 0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=4, help="reference default: MnistUtils.cpp:43")
     ap.add_argument("--probe-layer", type=int, default=3, help="layer whose GEMM is timed for the roofline")
     ap.add_argument("--probe-phase", type=int, default=2, help="0 fwd, 1 input grad, 2 weight grad")
@@ -90,8 +93,12 @@ def main():
     import niti_amd
     from niti_amd.model import NitiModel
 
-    arch = niti_amd.ARCH_VGG11 if args.arch == "vgg11" else niti_amd.ARCH_LENET
-    model = NitiModel(arch, args.batch)
+    arch = {"vgg11": niti_amd.ARCH_VGG11, "lenet": niti_amd.ARCH_LENET, "vgg16": niti_amd.ARCH_VGG16}[args.arch]
+    if args.batch <= 0:
+        args.batch = 64 if arch == niti_amd.ARCH_VGG16 else 256
+    if args.cpu_sample < 0:
+        args.cpu_sample = 1 if arch == niti_amd.ARCH_VGG16 else 128
+    model = NitiModel(arch, args.batch, args.in_hw)
     model.set_graph(args.graph)
     model.set_overlap(not args.no_overlap)
     for i, (w, s) in enumerate(synth_weights(model.layers, seed=17)):
@@ -104,7 +111,8 @@ def main():
     l0 = model.layers[0]
     rng = np.random.default_rng(100 + rank)
     x = torch.from_numpy(rng.integers(-127, 128, (args.batch, l0["c_in"], l0["h"], l0["w"])).astype(np.int8)).cuda()
-    labels = torch.from_numpy(rng.integers(0, 10, args.batch).astype(np.int32)).cuda()
+    labels = torch.from_numpy(rng.integers(0, 1000 if arch == niti_amd.ARCH_VGG16 else 10,
+                                           args.batch).astype(np.int32)).cuda()
 
     # Setup (untimed): one step to fill the buffers, then per-shape GEMM plan autotuning
     # (niti_model_autotune: candidate tile / split-K plans timed per layer phase).
@@ -128,6 +136,7 @@ def main():
         model.train_step(x, -3, labels)
     torch.cuda.synchronize()
     model.probe_read()
+    model.probe_read_span()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -186,7 +195,7 @@ def main():
     if rank == 0 and world == 1 and args.cpu_sample > 0:
         v, secs = cpu_baseline(model.layers, args.cpu_sample, args.cpu_threads)
         cpu = {"value": round(v, 3), "unit": "images/s", "cores": args.cpu_threads, "kind": "port",
-               "sample": f"{args.cpu_sample} images of the VGG-11 step (every conv: fwd + weight grad + input grad, "
+               "sample": f"{args.cpu_sample} images of the {args.arch.upper()} step (every conv: fwd + weight grad + input grad, "
                          f"reference-structured C restatement, float32 accumulation), {secs:.1f} s"}
 
     phase_name = {0: "forward conv", 1: "input-gradient conv", 2: "weight-gradient conv"}[args.probe_phase]
@@ -199,7 +208,8 @@ def main():
     else:
         kname = f"gemm_kernel {pplan[0]}x{pplan[1]}, implicit im2col"
     line = {
-        "metric": METRIC,
+        "metric": METRIC if arch == niti_amd.ARCH_VGG11 else METRIC.replace("VGG-11 batch 256",
+                                                                              f"{args.arch.upper()} batch {args.batch}"),
         "value": round(value, 2),
         "unit": "images/s",
         "n_gpus": world,
@@ -212,14 +222,15 @@ def main():
         "dtype": "int8",
         "data": "synthetic (random int8 images, labels; seeded niti_normal_int8 weights)",
         "config": {"workload": f"{args.arch.upper()} NITI int8 training step (fwd+relu+pool, loss grad, "
-                               f"weight grad, input grad, SGD), 3x32x32" if arch == niti_amd.ARCH_VGG11 else
-                               "LeNet NITI int8 training step, 1x28x28",
+                               f"weight grad, input grad, SGD), {l0['c_in']}x{l0['h']}x{l0['w']}"
+                               + (", 4096-4096-1000 head" if arch == niti_amd.ARCH_VGG16 else "")
+                               if arch != niti_amd.ARCH_LENET else "LeNet NITI int8 training step, 1x28x28",
                    "global_batch": args.batch * world, "per_gpu_batch": args.batch,
                    "parallelism": f"dp{world} exact (RCCL all-reduce MAX ranges + SUM int32 grads)"},
         "int8_mfma_tops": round(tops, 2),
         "int8_mfma_frac_of_peak": round(tops / PEAK_INT8_TOPS, 4),
         "roofline": {
-            "kernel": f"VGG-11 conv{probe_layer + 1} {phase_name} launch ({kname}; layer index {probe_layer})",
+            "kernel": f"{args.arch.upper()} conv{probe_layer + 1} {phase_name} launch ({kname}; layer index {probe_layer})",
             "bound": "mfma",
             "achieved": round(achieved, 2) if achieved else None,
             "peak": round(PEAK_INT8_TOPS, 1),

@@ -188,13 +188,18 @@ int niti_loss_grad(const int8_t* logits, int batch, int classes, int ld, const i
                    const int32_t* labels, int8_t* out, void* stream);
 
 /* ============================ 3. device-resident training step ========================= */
-enum niti_arch { NITI_ARCH_LENET = 1, NITI_ARCH_VGG11 = 2 };
+/* LeNet on MNIST 1x28x28 (cfg 1/2); VGG-11 on CIFAR 3x32x32 (cfg 3); VGG-16 on ImageNet 3x224x224
+ * with the 4096-4096-1000 head (cfg 4; niti_model_create2 takes another input size, a multiple
+ * of 32, e.g. 32 for the oracle-checked tests) */
+enum niti_arch { NITI_ARCH_LENET = 1, NITI_ARCH_VGG11 = 2, NITI_ARCH_VGG16 = 3 };
 typedef struct niti_model* niti_model_t;
 
 /* batch = this rank's images per step.  Weights start zero; load them with
  * niti_model_set_weight (OIHW int8, host memory) -- the reference initialises them with a
  * time-seeded RNG (nn/Distributions.cpp:26-51), so callers supply their own. */
 int niti_model_create(int arch, int batch, niti_model_t* out);
+/* The same with the input resolution (in_hw x in_hw; 0 = the architecture's default). */
+int niti_model_create2(int arch, int batch, int in_hw, niti_model_t* out);
 void niti_model_destroy(niti_model_t m);
 int niti_model_num_layers(niti_model_t m);
 /* per layer: {c_in, c_out, kh, kw, h_in, w_in, oh, ow, pad, stride, relu, pool} */

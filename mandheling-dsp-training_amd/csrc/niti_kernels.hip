@@ -2907,9 +2907,94 @@ __global__ void loss_grad_kernel(const int8_t* __restrict__ logits, int batch, i
     }
 }
 
+// The same arithmetic for wide class rows (ImageNet heads, up to LOSS_WIDE_MAXC classes): one
+// 256-thread block per sample, the row's max / sums reduced in LDS (int64, exact).
+constexpr int LOSS_WIDE_PER = 8;
+constexpr int LOSS_WIDE_MAXC = 256 * LOSS_WIDE_PER;
+__device__ int64_t block_reduce_i64(int64_t v, bool is_max, int64_t* red) {
+    const int tid = threadIdx.x;
+    red[tid] = v;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (tid < o) red[tid] = is_max ? (red[tid] > red[tid + o] ? red[tid] : red[tid + o]) : red[tid] + red[tid + o];
+        __syncthreads();
+    }
+    const int64_t r = red[0];
+    __syncthreads();
+    return r;
+}
+__global__ void __launch_bounds__(256) loss_grad_wide_kernel(const int8_t* __restrict__ logits, int classes, int ld,
+                                                             const int8_t* __restrict__ ascale_p,
+                                                             const int32_t* __restrict__ labels,
+                                                             int8_t* __restrict__ out) {
+    __shared__ int64_t red[256];
+    const int i = blockIdx.x, tid = threadIdx.x;
+    const int as = (int)*ascale_p;
+    const int8_t* L = logits + (int64_t)i * ld;
+    int64_t o[LOSS_WIDE_PER];
+    if (as > -7) {
+        int64_t sv[LOSS_WIDE_PER];
+        int64_t mx = INT64_MIN;
+#pragma unroll
+        for (int k = 0; k < LOSS_WIDE_PER; ++k) {
+            const int j = tid + 256 * k;
+            if (j < classes) {
+                int64_t t = (int64_t)L[j] * 47274;
+                t = t / (1 << 15);
+                sv[k] = as >= 0 ? t * ipow2_64(as) : t / ipow2_64(-as);
+                mx = mx > sv[k] ? mx : sv[k];
+            }
+        }
+        mx = block_reduce_i64(mx, true, red) - 10;
+#pragma unroll
+        for (int k = 0; k < LOSS_WIDE_PER; ++k) {
+            const int j = tid + 256 * k;
+            int64_t t = j < classes ? sv[k] - mx : 0;
+            t = t > 0 ? t : 0;
+            o[k] = j < classes ? ipow2_64(t) - 1 : 0;
+        }
+    } else {
+        const int64_t base = ipow2_64(1 - 2 * (int64_t)as);
+        const int64_t sb = ipow2_64(1 - (int64_t)as);
+#pragma unroll
+        for (int k = 0; k < LOSS_WIDE_PER; ++k) {
+            const int j = tid + 256 * k;
+            const int64_t t = j < classes ? L[j] : 0;
+            o[k] = j < classes ? base + t * sb + t * t : 0;
+        }
+    }
+    int64_t part = 0;
+#pragma unroll
+    for (int k = 0; k < LOSS_WIDE_PER; ++k) part += o[k];
+    const int64_t sum = block_reduce_i64(part, false, red);
+    part = 0;
+#pragma unroll
+    for (int k = 0; k < LOSS_WIDE_PER; ++k) {
+        const int j = tid + 256 * k;
+        o[k] = j < classes ? (o[k] * (1 << 11)) / sum : 0;
+        part += o[k];
+    }
+    const int64_t gs = block_reduce_i64(part, false, red);
+    const int tgt = labels[i];
+    int8_t* O = out + (int64_t)i * ld;
+    for (int j = tid; j < ld; j += 256) {
+        const int k = j >> 8;
+        int32_t gf = 0;
+#pragma unroll
+        for (int q = 0; q < LOSS_WIDE_PER; ++q)
+            if (q == k) gf = (int32_t)(j == tgt ? o[q] - gs : o[q]);
+        O[j] = j < classes ? (int8_t)psto_any(gf, 4) : (int8_t)0;
+    }
+}
+
 hipError_t loss_grad(const int8_t* logits, int batch, int classes, int ld, const int8_t* ascale, const int32_t* labels,
                      int8_t* out, hipStream_t st) {
-    if (classes > LOSS_MAXC || classes > ld) return hipErrorInvalidValue;
+    if (classes > ld || classes > LOSS_WIDE_MAXC || ld > LOSS_WIDE_MAXC) return hipErrorInvalidValue;
+    if (classes > LOSS_MAXC) {
+        hipLaunchKernelGGL(loss_grad_wide_kernel, dim3((unsigned)batch), dim3(256), 0, st, logits, classes, ld, ascale,
+                           labels, out);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(loss_grad_kernel, dim3((batch + 63) / 64), dim3(64), 0, st, logits, batch, classes, ld, ascale,
                        labels, out);
     return hipGetLastError();

@@ -203,7 +203,8 @@ hipError_t maxpool_relu_grad_nhwc16(const int8_t* x, const int8_t* y, const int8
                                     int8_t* dx, hipStream_t st);
 hipError_t relu_grad_nhwc16(const int8_t* x, const int8_t* dy, int64_t n, int8_t* out, hipStream_t st);
 // logits int8 [batch][ld] (first `classes` used), labels int32 [batch] (class index);
-// out int8 [batch][ld] (padded lanes zeroed).  classes <= 16.  NITI_CPULossGrad_Int8.cpp:81-200.
+// out int8 [batch][ld] (padded lanes zeroed).  classes <= 2048 (one thread per sample up to 16,
+// one block per sample above).  NITI_CPULossGrad_Int8.cpp:81-200.
 hipError_t loss_grad(const int8_t* logits, int batch, int classes, int ld, const int8_t* ascale,
                      const int32_t* labels, int8_t* out, hipStream_t st);
 

@@ -193,7 +193,7 @@ struct Model {
         span_cap = span_count = 0;
     }
 
-    int build(int arch_, int batch_);
+    int build(int arch_, int batch_, int in_hw = 0);
     bool tuning = false;  // autotune in progress: no collectives, no probe
     int fwd_layer(int i, hipStream_t st);
     int wgrad_layer(int i, hipStream_t st);
@@ -261,7 +261,7 @@ static void add_conv(Model& m, int ci, int co, int k, int pad, int h, int relu, 
     m.L.push_back(l);
 }
 
-int Model::build(int arch_, int batch_) {
+int Model::build(int arch_, int batch_, int in_hw) {
     arch = arch_;
     batch = batch_;
     if (arch == NITI_ARCH_LENET) {  // mnistTrain.cpp:131-181
@@ -283,6 +283,23 @@ int Model::build(int arch_, int batch_) {
         add_conv(*this, 512, 512, 3, 1, 2, 1, 0);
         add_conv(*this, 512, 512, 3, 1, 2, 1, 1);
         add_conv(*this, 512, 12, 1, 0, 1, 0, 0);
+    } else if (arch == NITI_ARCH_VGG16) {  // VGG-16 (configuration D), NITI layers (BASELINE cfg 4)
+        const int r = in_hw > 0 ? in_hw : 224;
+        if (r % 32 != 0) return NITI_INVALID_VALUE;
+        in_c = 3;
+        in_h = in_w = r;
+        classes = 1000;
+        static const int cfg[13][3] = {{3, 64, 0},    {64, 64, 1},   {64, 128, 0},  {128, 128, 1}, {128, 256, 0},
+                                       {256, 256, 0}, {256, 256, 1}, {256, 512, 0}, {512, 512, 0}, {512, 512, 1},
+                                       {512, 512, 0}, {512, 512, 0}, {512, 512, 1}};
+        int h = r;
+        for (int i = 0; i < 13; ++i) {
+            add_conv(*this, cfg[i][0], cfg[i][1], 3, 1, h, 1, cfg[i][2], /*flatten=*/i == 12);
+            if (cfg[i][2]) h /= 2;
+        }
+        add_conv(*this, 512 * h * h, 4096, 1, 0, 1, 1, 0);
+        add_conv(*this, 4096, 4096, 1, 0, 1, 1, 0);
+        add_conv(*this, 4096, 1000, 1, 0, 1, 0, 0);
     } else {
         return NITI_NOT_SUPPORT;
     }
@@ -660,10 +677,12 @@ struct niti_model {
 
 extern "C" {
 
-int niti_model_create(int arch, int batch, niti_model_t* out) {
-    if (!out || batch <= 0) return NITI_INVALID_VALUE;
+int niti_model_create(int arch, int batch, niti_model_t* out) { return niti_model_create2(arch, batch, 0, out); }
+
+int niti_model_create2(int arch, int batch, int in_hw, niti_model_t* out) {
+    if (!out || batch <= 0 || in_hw < 0) return NITI_INVALID_VALUE;
     auto* h = new niti_model();
-    const int rc = h->m.build(arch, batch);
+    const int rc = h->m.build(arch, batch, in_hw);
     if (rc != NITI_NO_ERROR) {
         delete h;
         return rc;

@@ -24,7 +24,7 @@ OP_GRADIENT_CONV_INT8 = 715
 OP_DSP_MATMUL_GRADIENT_INT8 = 818
 FORMAT_NCHW, FORMAT_NHWC, FORMAT_NC4HW4 = 0, 1, 2
 PAD_CAFFE, PAD_VALID, PAD_SAME = 0, 1, 2
-ARCH_LENET, ARCH_VGG11 = 1, 2
+ARCH_LENET, ARCH_VGG11, ARCH_VGG16 = 1, 2, 3
 
 
 class NitiError(RuntimeError):
@@ -101,6 +101,7 @@ def lib():
         "niti_relu_grad": (ci, [vp, vp, i64, vp, vp]),
         "niti_loss_grad": (ci, [vp, ci, ci, ci, vp, vp, vp, vp]),
         "niti_model_create": (ci, [ci, ci, C.POINTER(vp)]),
+        "niti_model_create2": (ci, [ci, ci, ci, C.POINTER(vp)]),
         "niti_model_destroy": (None, [vp]),
         "niti_model_num_layers": (ci, [vp]),
         "niti_model_layer_info": (ci, [vp, ci, C.POINTER(ci)]),

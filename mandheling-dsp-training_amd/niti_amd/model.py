@@ -14,10 +14,10 @@ from .ops import _stream
 class NitiModel:
     """NITIInt8Train's model + NITI_SGD step, on one GPU (optionally one rank of a DP group)."""
 
-    def __init__(self, arch: int, batch: int):
+    def __init__(self, arch: int, batch: int, in_hw: int = 0):
         self._lib = L.lib()
         h = C.c_void_p()
-        check(self._lib.niti_model_create(arch, batch, C.byref(h)), "model_create")
+        check(self._lib.niti_model_create2(arch, batch, int(in_hw), C.byref(h)), "model_create")
         self._h = h
         self.arch, self.batch = arch, batch
         self.layers = []

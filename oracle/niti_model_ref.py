@@ -33,6 +33,22 @@ def vgg11_layers():
     return L
 
 
+def vgg16_layers(hw=224):
+    """VGG-16 (configuration D) with the 4096-4096-1000 head; hw a multiple of 32."""
+    L = []
+    h = hw
+    cfg = [(3, 64, 0), (64, 64, 1), (64, 128, 0), (128, 128, 1), (128, 256, 0), (256, 256, 0), (256, 256, 1),
+           (256, 512, 0), (512, 512, 0), (512, 512, 1), (512, 512, 0), (512, 512, 0), (512, 512, 1)]
+    for i, (ci, co, pool) in enumerate(cfg):
+        L.append(dict(ci=ci, co=co, k=3, pad=1, h=h, relu=1, pool=pool, flatten=int(i == 12)))
+        if pool:
+            h //= 2
+    L.append(dict(ci=512 * h * h, co=4096, k=1, pad=0, h=1, relu=1, pool=0, flatten=0))
+    L.append(dict(ci=4096, co=4096, k=1, pad=0, h=1, relu=1, pool=0, flatten=0))
+    L.append(dict(ci=4096, co=1000, k=1, pad=0, h=1, relu=0, pool=0, flatten=0))
+    return L
+
+
 def init_weights(layers, seed=17):
     rng = np.random.default_rng(seed)
     W, S = [], []
@@ -49,7 +65,7 @@ def onehot(labels, classes=10):
     return oh
 
 
-def train_step(layers, W, S, x, exp_in, labels):
+def train_step(layers, W, S, x, exp_in, labels, classes=10):
     """Returns (new weights, record) where record holds logits, exponents and per-layer taps."""
     n = x.shape[0]
     rec = dict(inp=[], y=[], r=[], p=[], exp=[], dw=[], dy=[], geom=[])
@@ -76,7 +92,7 @@ def train_step(layers, W, S, x, exp_in, labels):
             a = a.reshape(n, -1, 1, 1)
     last = layers[-1]
     logits = rec["r"][-1].reshape(n, last["co"])
-    d = O.loss_grad(logits, rec["exp"][-1], onehot(labels)).reshape(n, last["co"], 1, 1)
+    d = O.loss_grad(logits, rec["exp"][-1], onehot(labels, classes)).reshape(n, last["co"], 1, 1)
     dy = [None] * len(layers)
     dy[-1] = d
     newW = list(W)

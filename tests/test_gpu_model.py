@@ -18,7 +18,8 @@ def T():
     return torch
 
 
-def _run(T, arch, layers, batch, steps=2, seed=5, graph=False, reuse_buffers=True, prepare=None, overlap=True):
+def _run(T, arch, layers, batch, steps=2, seed=5, graph=False, reuse_buffers=True, prepare=None, overlap=True,
+         in_hw=0, classes=10):
     """reuse_buffers: new data goes into the same device tensors every step, so with graph=True
     steps after the first replay the captured graph instead of re-capturing it.
     prepare(model, x, labels): called after one throwaway step (weights are reset after it)."""
@@ -26,14 +27,14 @@ def _run(T, arch, layers, batch, steps=2, seed=5, graph=False, reuse_buffers=Tru
     from niti_amd.model import NitiModel
     rng = np.random.default_rng(seed)
     W, S = R.init_weights(layers, seed=seed)
-    m = NitiModel(arch, batch)
+    m = NitiModel(arch, batch, in_hw)
     m.set_graph(graph)
     m.set_overlap(overlap)
     xd = ld = None
     l0 = layers[0]
     if prepare is not None:
         xt = T.from_numpy(rng.integers(-127, 128, (batch, l0["ci"], l0["h"], l0["h"])).astype(np.int8)).cuda()
-        lt = T.from_numpy(rng.integers(0, 10, batch).astype(np.int32)).cuda()
+        lt = T.from_numpy(rng.integers(0, classes, batch).astype(np.int32)).cuda()
         for i, (w, s) in enumerate(zip(W, S)):
             m.set_weight(i, w, s)
         m.train_step(xt, -3, lt)
@@ -44,9 +45,9 @@ def _run(T, arch, layers, batch, steps=2, seed=5, graph=False, reuse_buffers=Tru
         assert np.array_equal(m.get_weight(i), W[i])
     for step in range(steps):
         x = rng.integers(-127, 128, (batch, l0["ci"], l0["h"], l0["h"])).astype(np.int8)
-        labels = rng.integers(0, 10, batch).astype(np.int32)
+        labels = rng.integers(0, classes, batch).astype(np.int32)
         exp_in = -3
-        newW, rec = R.train_step(layers, W, S, x, exp_in, labels)
+        newW, rec = R.train_step(layers, W, S, x, exp_in, labels, classes=classes)
         if xd is None or not reuse_buffers:
             xd = T.from_numpy(x).cuda()
             ld = T.from_numpy(labels).cuda()
@@ -136,3 +137,39 @@ def test_vgg11_step_autotuned(T):
     assert len(seen) == 3 * 9 - 1
     for (bm, bn, splits, strat) in seen.values():
         assert bm in (64, 128) and bn in (64, 128) and splits >= 1 and strat in (0, 1, 2)
+
+
+def test_vgg16_step_matches_oracle(T):
+    """BASELINE cfg 4's network (VGG-16, 4096-4096-1000 head, 1000-class loss) at 32x32 input:
+    the whole step, every tap, against the oracle."""
+    import niti_amd
+    import niti_model_ref as R
+    _run(T, niti_amd.ARCH_VGG16, R.vgg16_layers(32), batch=2, steps=1, seed=13, in_hw=32, classes=1000)
+
+
+def test_vgg16_224_step_layer_parity(T):
+    """VGG-16 at ImageNet size (224x224, batch 2): one device step; the first conv's forward, the
+    last conv's weight gradient (from the step's own input / dy taps) and the 1000-class loss
+    gradient against the oracle."""
+    import niti_amd
+    import niti_model_ref as R
+    import niti_oracle as O
+    from niti_amd.model import NitiModel
+    layers = R.vgg16_layers(224)
+    W, S = R.init_weights(layers, seed=29)
+    rng = np.random.default_rng(29)
+    m = NitiModel(niti_amd.ARCH_VGG16, 2)
+    for i, (w, s) in enumerate(zip(W, S)):
+        m.set_weight(i, w, s)
+    x = rng.integers(-127, 128, (2, 3, 224, 224)).astype(np.int8)
+    labels = rng.integers(0, 1000, 2).astype(np.int32)
+    m.train_step(T.from_numpy(x).cuda(), -3, T.from_numpy(labels).cuda())
+    g0 = O.geom(2, 3, 224, 224, 64, 3, pad=1)
+    y0, _, _, _ = O.conv_fwd(g0, x, W[0], -3, S[0])
+    assert np.array_equal(m.tap(0, 0), O.relu(y0))
+    g12 = O.geom(2, 512, 14, 14, 512, 3, pad=1)
+    dw12, _, _, _ = O.conv_wgrad(g12, m.tap(11, 0), m.tap(12, 2))
+    assert np.array_equal(m.tap(12, 1), dw12)
+    logits, e = m.logits()
+    want = O.loss_grad(logits, e, R.onehot(labels, 1000))
+    assert np.array_equal(m.tap(15, 2).reshape(2, 1000), want)

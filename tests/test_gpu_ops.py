@@ -411,6 +411,24 @@ def test_pool_relu_loss_kernels(T, ops, oracle):
         assert not got[:, 12:].any()
 
 
+@pytest.mark.parametrize("classes", [17, 100, 1000])
+def test_loss_grad_wide_rows(T, ops, oracle, classes):
+    """NITI_LOSS_Grad_Int8 over ImageNet-wide class rows (one block per sample), every ascale branch."""
+    rng = np.random.default_rng(classes)
+    ld = (classes + 15) // 16 * 16
+    for ascale in (-12, -7, -6, -3, 0, 2):
+        logits = rng.integers(-127, 128, (9, classes)).astype(np.int8)
+        labels = rng.integers(0, classes, 9).astype(np.int32)
+        oh = np.zeros((9, classes), np.int32)
+        oh[np.arange(9), labels] = 1
+        want = oracle.loss_grad(logits, ascale, oh)
+        lg = np.zeros((9, ld), np.int8)
+        lg[:, :classes] = logits
+        got = ops.loss_grad(dev(T, lg), classes, i8s(T, ascale), dev(T, labels)).cpu().numpy()
+        assert np.array_equal(got[:, :classes], want), ascale
+        assert not got[:, classes:].any()
+
+
 # --------------------------------------------------------------------------- full sizes
 def _sample_check(acc_fn, n_samples, rng):
     for _ in range(n_samples):
