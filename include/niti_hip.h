@@ -51,7 +51,12 @@ enum niti_op_type {
     NITI_OP_DECONV_INT8 = 701,             /* NITI_DeCONV_Int8        -> NITI_DeConv_Int8.cpp:187-332 */
     NITI_OP_MATMUL_INT8 = 713,             /* NITI_MatMul_Int8        -> NITI_Matmul_Int8.cpp:140-231 */
     NITI_OP_GRADIENT_CONV_INT8 = 715,      /* NITI_GradientCONV_Int8  -> NITI_GradientConv_Int8.cpp:165-298 */
-    NITI_OP_DSP_MATMUL_GRADIENT_INT8 = 818 /* NITI_DSP_MATMUL_GRADIENT_Int8 -> NITI_DSPMatmulGradientConv_Int8.cpp:105-553 */
+    NITI_OP_DSP_CONV_INT8 = 800,           /* NITI_DSP_CONV_Int8      -> NITI_DSPConv_Int8.cpp:160-455 */
+    NITI_OP_DSP_DECONV_INT8 = 811,         /* NITI_DSP_DECONV_Int8    -> NITI_DSPDeConv_Int8.cpp */
+    NITI_OP_DSP_MATMUL_GRADIENT_INT8 = 818, /* NITI_DSP_MATMUL_GRADIENT_Int8 -> NITI_DSPMatmulGradientConv_Int8.cpp:105-553 */
+    NITI_OP_DSP_PARALLEL_GRADIENTCONV_INT8 = 820,   /* -> NITI_DSPParallelGradientConv_Int8.cpp (818's tensors) */
+    NITI_OP_DSP_GRADIENT_SPLITBATCHCONV_INT8 = 821, /* -> NITI_DSPGradientSplitBatchConv_Int8.cpp (822's tensors) */
+    NITI_OP_DSP_TRANSPOSEGRADIENT_CONV_INT8 = 822 /* -> NITI_DSPTransposeGradientConv_Int8.cpp:137-440 */
 };
 
 /* ---- tensor formats: MNN_DATA_FORMAT (schema/default/Tensor.fbs:12-18) ---------------------- */
@@ -102,6 +107,15 @@ int niti_create_execution(int op_type, const niti_conv2d_common* common, niti_ex
  *  NITI_OP_DSP_MATMUL_GRADIENT_INT8
  *                             in {x NHWC [N,Ci,H,W], dy NHWC [N,Co,OH,OW]} out{dw HWIO [KH,KW,Ci,Co] as
  *                                 dims {KH,KW,Ci,Co}}
+ *  NITI_OP_DSP_CONV_INT8, NITI_OP_DSP_DECONV_INT8
+ *                             in {x NHWC [N,Ci,H,W], w HWIO as dims {KH,KW,Ci,Co}, exp_in int8[1],
+ *                                 wscale int8[1]}                         out{y NHWC [N,Co,OH,OW], exp_out int8[1]}
+ *                             (the deconv slot gets the graph's padded/dilated dy and rotated weights)
+ *  NITI_OP_DSP_PARALLEL_GRADIENTCONV_INT8 as NITI_OP_DSP_MATMUL_GRADIENT_INT8, KH x KW from dw's dims
+ *  NITI_OP_DSP_TRANSPOSEGRADIENT_CONV_INT8, NITI_OP_DSP_GRADIENT_SPLITBATCHCONV_INT8 (stride 1; the graph
+ *                             dilates dy for stride 2)
+ *                             in {x^T NHWC [Ci,N,H,W], dy NHWC [N,Co,OH,OW], 0, 0}
+ *                             out{dw NHWC [Ci,Co,KH,KW] (kernel size from the shapes), exp_out int8[1] (optional)}
  * Output channel counts must be multiples of 4 on NC4HW4 outputs (the reference sizes its
  * int32 accumulator N*C*H*W but its GEMM writes ceil(C/4)*4 channels): NITI_NOT_SUPPORT. */
 int niti_execution_resize(niti_execution_t e, const niti_tensor* inputs, int n_in, const niti_tensor* outputs,

@@ -100,6 +100,48 @@ struct Ohwi16ToHwio {
     }
 };
 
+// w HWIO [KK][Ci][Co] -> OHWI16 [Co][KK][Cip] (the DSP ops' weights, NN.cpp:1155-1156)
+struct HwioToOhwi16 {
+    const int8_t* w;
+    int co, ci, kk, cip;
+    int8_t* out;
+    __device__ void operator()(int64_t i) const {  // i over [co][kk][cip]
+        const int c = (int)(i % cip);
+        const int64_t r = i / cip;
+        const int k = (int)(r % kk);
+        const int o = (int)(r / kk);
+        out[i] = c < ci ? w[((int64_t)k * ci + c) * co + o] : (int8_t)0;
+    }
+};
+
+// x^T [Ci][H][W][N] (NHWC dims batch = Ci, channel = N) -> x NHWC16 [N][HW][Cip]
+struct CiHwnToNhwc16 {
+    const int8_t* x;
+    int n, ci, hw, cip;
+    int8_t* out;
+    __device__ void operator()(int64_t i) const {  // i over [n][hw][cip]
+        const int c = (int)(i % cip);
+        const int64_t r = i / cip;
+        const int64_t p = r % hw;
+        const int b = (int)(r / hw);
+        out[i] = c < ci ? x[((int64_t)c * hw + p) * n + b] : (int8_t)0;
+    }
+};
+
+// g OHWI16 [Co][KK][Cip] -> [Ci][KK][Co] (the transposed-gradient op's NHWC output: batch = Ci)
+struct Ohwi16ToIhwo {
+    const int8_t* g;
+    int co, ci, kk, cip;
+    int8_t* out;
+    __device__ void operator()(int64_t i) const {  // i over [ci][kk][co]
+        const int o = (int)(i % co);
+        const int64_t r = i / co;
+        const int k = (int)(r % kk);
+        const int c = (int)(r / kk);
+        out[i] = g[((int64_t)o * kk + k) * cip + c];
+    }
+};
+
 // [rows][ld] int8 -> [rows][cols]
 struct UnpadRows {
     const int8_t* in;
@@ -433,15 +475,20 @@ class MatmulInt8Execution : public Execution {
 // requantises on the Hexagon (round-to-nearest, then /16 on the CPU,
 // NITI_DSPMatmulGradientConv_Int8.cpp:543-550); this backend gives the op the CPU path's
 // numerics (NITI_GradientConv_Int8: PSTO(bw-2)), SURVEY.md §8(a) A5.
+// NITI_DSP_PARALLEL_GRADIENTCONV_Int8 (820) has the same tensors; its graph rule sets the common's
+// kernel to dy's OH x OW (grad/NITI_DSPConv_Int8_Grad.cpp:151-153, shape rule
+// ShapeNITI_Conv_Int8.cpp:146-233), so its filter size comes from the output tensor.
 class DspMatmulGradientExecution : public Execution {
    public:
-    explicit DspMatmulGradientExecution(const niti_conv2d_common& c) : common_(c) {}
+    explicit DspMatmulGradientExecution(const niti_conv2d_common& c, bool kernel_from_output = false)
+        : common_(c), kernel_from_output_(kernel_from_output) {}
     int onResize(const niti_tensor* in, int nin, const niti_tensor* out, int nout) override {
         if (nin < 2 || nout < 1) return NITI_INVALID_VALUE;
         const niti_tensor &x = in[0], &dy = in[1], &o = out[0];
         if (x.format != NITI_FORMAT_NHWC || dy.format != NITI_FORMAT_NHWC) return NITI_NOT_SUPPORT;
         if (common_.group > 1 || common_.dilate_x > 1 || common_.dilate_y > 1) return NITI_NOT_SUPPORT;
-        const int kh = common_.kernel_y, kw = common_.kernel_x;
+        const int kh = kernel_from_output_ ? o.dims[0] : common_.kernel_y;
+        const int kw = kernel_from_output_ ? o.dims[1] : common_.kernel_x;
         if (!geom_from_common(common_, x.dims[0], x.dims[1], x.dims[2], x.dims[3], dy.dims[1], kh, kw, &g_))
             return NITI_COMPUTE_SIZE_ERROR;
         if (dy.dims[0] != g_.n || dy.dims[2] != g_.oh || dy.dims[3] != g_.ow) return NITI_COMPUTE_SIZE_ERROR;
@@ -473,8 +520,160 @@ class DspMatmulGradientExecution : public Execution {
 
    private:
     niti_conv2d_common common_;
+    bool kernel_from_output_;
     ConvGeom g_{};
     int8_t *xT_ = nullptr, *dyT_ = nullptr, *g8_ = nullptr;
+    int32_t* acc_ = nullptr;
+    uint32_t* amax_ = nullptr;
+    void* slab_ = nullptr;
+    size_t slab_bytes_ = 0;
+};
+
+// ------------------------------------------------------------------ NITI_DSP_CONV_Int8 (800) / NITI_DSP_DECONV_Int8 (811)
+// Op slots of the DSP forward conv and input-gradient conv: x (or dy) NHWC, weights HWIO
+// [KH][KW][Ci][Co], exp_in, wscale -> y NHWC, exp_out (NITI_DSPConv_Int8.cpp:160-455,
+// NITI_DSPDeConv_Int8.cpp: pad + supernode conv, exp_out = exp_in + wscale + shift :399-400).
+// The deconv's graph rule (grad/NITI_DSPConv_Int8_Grad.cpp:35-130) hands it dy (dilated by
+// LeftPoolGrad for stride 2) and the rotated, transposed weights with the extra pad, so both
+// ops are one stride-s conv.  The DSP requantises round-to-nearest on the Hexagon; this
+// backend gives both the CPU path's numerics (NITI_Conv_Int8.cpp:255-307: shift = bw - 7,
+// PSTO; exp_out = exp_in + wscale + the applied increment), SURVEY.md §8(f)-2.
+class DspConvExecution : public Execution {
+   public:
+    explicit DspConvExecution(const niti_conv2d_common& c) : common_(c) {}
+    int onResize(const niti_tensor* in, int nin, const niti_tensor* out, int nout) override {
+        if (nin < 4 || nout < 2) return NITI_INVALID_VALUE;
+        const niti_tensor &x = in[0], &w = in[1], &y = out[0];
+        if (x.format != NITI_FORMAT_NHWC || y.format != NITI_FORMAT_NHWC) return NITI_NOT_SUPPORT;
+        if (common_.group > 1) return NITI_NOT_SUPPORT;
+        // x, y NHWC with logical dims {N, C, H, W}; w HWIO as dims {KH, KW, Ci, Co}
+        if (w.dims[2] != x.dims[1]) return NITI_COMPUTE_SIZE_ERROR;
+        if (!geom_from_common(common_, x.dims[0], x.dims[1], x.dims[2], x.dims[3], w.dims[3], w.dims[0], w.dims[1], &g_))
+            return NITI_COMPUTE_SIZE_ERROR;
+        if (y.dims[0] != g_.n || y.dims[1] != g_.c_out || y.dims[2] != g_.oh || y.dims[3] != g_.ow)
+            return NITI_COMPUTE_SIZE_ERROR;
+        ws_.release();
+        x16_ = (int8_t*)ws_.alloc((size_t)g_.n * g_.h * g_.w * g_.cip);
+        w16_ = (int8_t*)ws_.alloc((size_t)g_.c_out * g_.kh * g_.kw * g_.cip);
+        acc_ = (int32_t*)ws_.alloc((size_t)g_.n * g_.oh * g_.ow * g_.cop * 4);
+        y16_ = (int8_t*)ws_.alloc((size_t)g_.n * g_.oh * g_.ow * g_.cop);
+        amax_ = (uint32_t*)ws_.alloc(MAX_BYTES);
+        slab_bytes_ = conv_fwd_workspace(g_);
+        slab_ = slab_bytes_ ? ws_.alloc(slab_bytes_) : nullptr;
+        if (slab_bytes_ && !slab_) return NITI_OUT_OF_MEMORY;
+        return (x16_ && w16_ && acc_ && y16_ && amax_) ? NITI_NO_ERROR : NITI_OUT_OF_MEMORY;
+    }
+    int onExecute(const niti_tensor* in, int nin, const niti_tensor* out, int nout, hipStream_t st) override {
+        if (!acc_) return NITI_NO_EXECUTION;
+        const int kk = g_.kh * g_.kw;
+        NITI_TRY(launch_map((int64_t)g_.n * g_.h * g_.w * g_.cip, NhwcToNhwc16{(const int8_t*)in[0].data, g_.c_in, g_.cip, x16_}, st));
+        NITI_TRY(launch_map((int64_t)g_.c_out * kk * g_.cip,
+                            HwioToOhwi16{(const int8_t*)in[1].data, g_.c_out, g_.c_in, kk, g_.cip, w16_}, st));
+        NITI_TRY(hipMemsetAsync(amax_, 0, MAX_BYTES, st));
+        NITI_TRY(conv_fwd_acc(g_, x16_, w16_, acc_, amax_, slab_, slab_bytes_, st));
+        ActRequant r;
+        r.acc = acc_;
+        r.rows = (int64_t)g_.n * g_.oh * g_.ow;
+        r.ldc = g_.cop;
+        r.amax = amax_;
+        r.exp_in = (const int8_t*)in[2].data;
+        r.wscale = (const int8_t*)in[3].data;
+        r.exp_out = nout > 1 ? (int8_t*)out[1].data : nullptr;
+        r.out_nhwc16 = y16_;
+        NITI_TRY(requant_act(r, st));
+        const int64_t rows = (int64_t)g_.n * g_.oh * g_.ow;
+        NITI_TRY(launch_map(rows * g_.c_out, UnpadRows{y16_, g_.c_out, g_.cop, (int8_t*)out[0].data}, st));
+        return NITI_NO_ERROR;
+    }
+
+   private:
+    niti_conv2d_common common_;
+    ConvGeom g_{};
+    int8_t *x16_ = nullptr, *w16_ = nullptr, *y16_ = nullptr;
+    int32_t* acc_ = nullptr;
+    uint32_t* amax_ = nullptr;
+    void* slab_ = nullptr;
+    size_t slab_bytes_ = 0;
+};
+
+// ------------------------------------------------------------------ NITI_DSP_TRANSPOSEGRADIENT_CONV_Int8 (822)
+// Op slot of the DSP weight gradient the graph emits with parallel.txt = 0
+// (grad/NITI_DSPConv_Int8_Grad.cpp:216-219): x^T [Ci][H][W][N] (transpose {3,1,2,0} of the NHWC
+// input), dy NHWC [N][OH][OW][Co], two zero scalars -> dw [Ci][KH][KW][Co] (shape rule
+// ShapeNITI_Conv_Int8.cpp:239-320 with the kernel = dy's OH x OW) and an exponent
+// (NITI_DSPTransposeGradientConv_Int8.cpp:137-440).  The DSP requantises round-to-nearest
+// and divides by 32 (:426-432); this backend gives the CPU weight-gradient numerics
+// (NITI_GradientConv_Int8.cpp:272-296: PSTO(bw - 2)) and exp_out = the applied shift.
+// Stride 1 only: for stride 2 the graph dilates dy with LeftPoolGrad and sets stride 1 (:160-190).
+// NITI_DSP_GRADIENT_SPLITBatchCONV_Int8 (821), the stride-2 variant for 8 < OW <= 16, has the
+// same tensors and shape rule (ShapeNITI_Conv_Int8.cpp:529-531).
+class DspTransposeGradientExecution : public Execution {
+   public:
+    explicit DspTransposeGradientExecution(const niti_conv2d_common& c) : common_(c) {}
+    int onResize(const niti_tensor* in, int nin, const niti_tensor* out, int nout) override {
+        if (nin < 2 || nout < 1) return NITI_INVALID_VALUE;
+        const niti_tensor &xt = in[0], &dy = in[1], &o = out[0];
+        if (xt.format != NITI_FORMAT_NHWC || dy.format != NITI_FORMAT_NHWC) return NITI_NOT_SUPPORT;
+        if (common_.group > 1 || common_.dilate_x > 1 || common_.dilate_y > 1 || common_.stride_x > 1 ||
+            common_.stride_y > 1)
+            return NITI_NOT_SUPPORT;
+        // NHWC logical dims {N, C, H, W}: x^T {Ci, N, H, W}, dy {N, Co, OH, OW}, dw {Ci, Co, KH, KW}
+        const int ci = xt.dims[0], n = xt.dims[1], h = xt.dims[2], w = xt.dims[3];
+        if (dy.dims[0] != n) return NITI_COMPUTE_SIZE_ERROR;
+        const int co = dy.dims[1];
+        const int pt = common_.has_pads ? common_.pads[0] : common_.pad_y;
+        const int pl = common_.has_pads ? common_.pads[1] : common_.pad_x;
+        const int pb = common_.has_pads ? common_.pads[2] : common_.pad_y;
+        const int pr = common_.has_pads ? common_.pads[3] : common_.pad_x;
+        const int kh = h + pt + pb - dy.dims[2] + 1, kw = w + pl + pr - dy.dims[3] + 1;
+        if (kh <= 0 || kw <= 0) return NITI_COMPUTE_SIZE_ERROR;
+        ConvGeom r{};
+        r.n = n;
+        r.c_in = ci;
+        r.h = h;
+        r.w = w;
+        r.c_out = co;
+        r.kh = kh;
+        r.kw = kw;
+        r.sh = r.sw = r.dh = r.dw = 1;
+        r.pt = pt;
+        r.pl = pl;
+        r.pb = pb;
+        r.pr = pr;
+        if (!r.finalize() || r.oh != dy.dims[2] || r.ow != dy.dims[3]) return NITI_COMPUTE_SIZE_ERROR;
+        g_ = r;
+        if (o.dims[0] != ci || o.dims[1] != co || o.dims[2] != kh || o.dims[3] != kw) return NITI_COMPUTE_SIZE_ERROR;
+        ws_.release();
+        x16_ = (int8_t*)ws_.alloc((size_t)g_.n * g_.h * g_.w * g_.cip);
+        dy16_ = (int8_t*)ws_.alloc((size_t)g_.n * g_.oh * g_.ow * g_.cop);
+        acc_ = (int32_t*)ws_.alloc((size_t)g_.c_out * kh * kw * g_.cip * 4);
+        g8_ = (int8_t*)ws_.alloc((size_t)g_.c_out * kh * kw * g_.cip);
+        amax_ = (uint32_t*)ws_.alloc(MAX_BYTES);
+        slab_bytes_ = conv_wgrad_workspace(g_);
+        slab_ = slab_bytes_ ? ws_.alloc(slab_bytes_) : nullptr;
+        if (slab_bytes_ && !slab_) return NITI_OUT_OF_MEMORY;
+        return (x16_ && dy16_ && acc_ && g8_ && amax_) ? NITI_NO_ERROR : NITI_OUT_OF_MEMORY;
+    }
+    int onExecute(const niti_tensor* in, int nin, const niti_tensor* out, int nout, hipStream_t st) override {
+        if (!acc_) return NITI_NO_EXECUTION;
+        const int hw = g_.h * g_.w, ohw = g_.oh * g_.ow, kk = g_.kh * g_.kw;
+        NITI_TRY(launch_map((int64_t)g_.n * hw * g_.cip,
+                            CiHwnToNhwc16{(const int8_t*)in[0].data, g_.n, g_.c_in, hw, g_.cip, x16_}, st));
+        NITI_TRY(launch_map((int64_t)g_.n * ohw * g_.cop, NhwcToNhwc16{(const int8_t*)in[1].data, g_.c_out, g_.cop, dy16_}, st));
+        const int64_t nacc = (int64_t)g_.c_out * kk * g_.cip;
+        NITI_TRY(hipMemsetAsync(amax_, 0, MAX_BYTES, st));
+        NITI_TRY(conv_wgrad_acc(g_, x16_, dy16_, acc_, amax_, slab_, slab_bytes_, st));
+        NITI_TRY(requant_grad(acc_, nacc, amax_, RULE_WGRAD_BW2, g8_, nullptr, st));
+        NITI_TRY(launch_map((int64_t)g_.c_in * kk * g_.c_out,
+                            Ohwi16ToIhwo{g8_, g_.c_out, g_.c_in, kk, g_.cip, (int8_t*)out[0].data}, st));
+        if (nout > 1 && out[1].data != nullptr) NITI_TRY(grad_exponent(amax_, RULE_WGRAD_BW2, (int8_t*)out[1].data, st));
+        return NITI_NO_ERROR;
+    }
+
+   private:
+    niti_conv2d_common common_;
+    ConvGeom g_{};
+    int8_t *x16_ = nullptr, *dy16_ = nullptr, *g8_ = nullptr;
     int32_t* acc_ = nullptr;
     uint32_t* amax_ = nullptr;
     void* slab_ = nullptr;
@@ -501,6 +700,11 @@ Execution* create_execution(int op_type, const niti_conv2d_common* c, int* err) 
         case NITI_OP_GRADIENT_CONV_INT8: return new GradientConvInt8Execution(cc);
         case NITI_OP_MATMUL_INT8: return new MatmulInt8Execution();
         case NITI_OP_DSP_MATMUL_GRADIENT_INT8: return new DspMatmulGradientExecution(cc);
+        case NITI_OP_DSP_CONV_INT8:
+        case NITI_OP_DSP_DECONV_INT8: return new DspConvExecution(cc);
+        case NITI_OP_DSP_PARALLEL_GRADIENTCONV_INT8: return new DspMatmulGradientExecution(cc, true);
+        case NITI_OP_DSP_GRADIENT_SPLITBATCHCONV_INT8:
+        case NITI_OP_DSP_TRANSPOSEGRADIENT_CONV_INT8: return new DspTransposeGradientExecution(cc);
         default: *err = NITI_NOT_SUPPORT; return nullptr;
     }
 }

@@ -2907,6 +2907,18 @@ __global__ void loss_grad_kernel(const int8_t* __restrict__ logits, int batch, i
     }
 }
 
+// Exponent of a requantised weight gradient, for the DSP op slots whose graph carries one:
+// the applied PSTO shift bw - rule (0 when the gradient is all zero), as the DSP ops add their
+// requantisation shift to exp_in + wscale (NITI_DSPTransposeGradientConv_Int8.cpp:438-439).
+__global__ void grad_exponent_kernel(const uint32_t* __restrict__ amax, int rule, int8_t* __restrict__ out) {
+    const int bw = bitwidth_of(read_max(amax));  // whole wave active
+    if (threadIdx.x == 0) *out = (int8_t)(bw == 0 ? 0 : bw - rule);
+}
+hipError_t grad_exponent(const uint32_t* amax, int rule, int8_t* out, hipStream_t st) {
+    hipLaunchKernelGGL(grad_exponent_kernel, dim3(1), dim3(64), 0, st, amax, rule, out);
+    return hipGetLastError();
+}
+
 // The same arithmetic for wide class rows (ImageNet heads, up to LOSS_WIDE_MAXC classes): one
 // 256-thread block per sample, the row's max / sums reduced in LDS (int64, exact).
 constexpr int LOSS_WIDE_PER = 8;

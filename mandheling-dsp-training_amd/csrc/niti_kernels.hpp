@@ -191,6 +191,8 @@ struct SgdJobs {
     int n;
 };
 hipError_t sgd_update_many(const SgdJob* jobs, int n, hipStream_t st);
+// exponent of a requantised weight gradient: bw - rule (0 for an all-zero gradient)
+hipError_t grad_exponent(const uint32_t* amax, int rule, int8_t* out, hipStream_t st);
 hipError_t sgd_update(const int32_t* acc, const uint32_t* amax, int rule, int co, int ci, int kk, int cip, int cop,
                       int8_t* w, int8_t* wT, int8_t* g_out, hipStream_t st);
 

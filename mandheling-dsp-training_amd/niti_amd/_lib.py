@@ -21,7 +21,12 @@ OP_CONV_INT8 = 700
 OP_DECONV_INT8 = 701
 OP_MATMUL_INT8 = 713
 OP_GRADIENT_CONV_INT8 = 715
+OP_DSP_CONV_INT8 = 800
+OP_DSP_DECONV_INT8 = 811
 OP_DSP_MATMUL_GRADIENT_INT8 = 818
+OP_DSP_PARALLEL_GRADIENTCONV_INT8 = 820
+OP_DSP_GRADIENT_SPLITBATCHCONV_INT8 = 821
+OP_DSP_TRANSPOSEGRADIENT_CONV_INT8 = 822
 FORMAT_NCHW, FORMAT_NHWC, FORMAT_NC4HW4 = 0, 1, 2
 PAD_CAFFE, PAD_VALID, PAD_SAME = 0, 1, 2
 ARCH_LENET, ARCH_VGG11, ARCH_VGG16 = 1, 2, 3

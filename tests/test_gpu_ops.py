@@ -316,23 +316,130 @@ def test_exec_matmul_int8(T, ops, oracle, m, o, k):
     assert np.array_equal(out.cpu().numpy().T, dwT_ref)
 
 
+@pytest.mark.parametrize("op", [818, 820])
 @pytest.mark.parametrize("geo", [GEOMS[1], GEOMS[4], GEOMS[7]])
-def test_exec_dsp_matmul_gradient(T, ops, oracle, geo):
+def test_exec_dsp_matmul_gradient(T, ops, oracle, geo, op):
+    """818, and 820 (PARALLEL_GRADIENTCONV: its common carries dy's OH x OW as the kernel)."""
     import niti_amd
     n, ci, h, w, co, k, s, p = geo
+    if op == 820 and s != 1:
+        pytest.skip("the graph emits 820 only for stride 1")
     g = oracle.geom(n, ci, h, w, co, k, stride=s, pad=p)
     rng = np.random.default_rng(205)
     x = oracle.synth_x(rng, (n, ci, h, w))
     dy = oracle.synth_dy(rng, (n, co, g.oh, g.ow))
     dw_ref, _, _, _ = oracle.conv_wgrad(g, x, dy)
     out = T.zeros((k, k, ci, co), dtype=T.int8, device="cuda")
-    ex = ops.NITIExecution(niti_amd.OP_DSP_MATMUL_GRADIENT_INT8, ops.conv_common(k, stride=s, pad=p))
+    ex = ops.NITIExecution(op, ops.conv_common(k if op == 818 else (g.oh, g.ow), stride=s, pad=p))
     ins = [ops.tensor(dev(T, x.transpose(0, 2, 3, 1)), (n, ci, h, w), niti_amd.FORMAT_NHWC),
            ops.tensor(dev(T, dy.transpose(0, 2, 3, 1)), (n, co, g.oh, g.ow), niti_amd.FORMAT_NHWC)]
     outs = [ops.tensor(out, (k, k, ci, co))]
     assert ex.resize(ins, outs) == 0
     assert ex.execute(ins, outs) == 0
     assert np.array_equal(out.cpu().numpy().transpose(3, 2, 0, 1), dw_ref)
+
+
+@pytest.mark.parametrize("geo", GEOMS)
+def test_exec_dsp_conv_int8(T, ops, oracle, geo):
+    """NITI_DSP_CONV_Int8 slot: x NHWC, w HWIO -> y NHWC + exp_out, CPU conv numerics."""
+    import niti_amd
+    n, ci, h, w, co, k, s, p = geo
+    g = oracle.geom(n, ci, h, w, co, k, stride=s, pad=p)
+    rng = np.random.default_rng(206)
+    x = oracle.synth_x(rng, (n, ci, h, w))
+    wt, ws = oracle.synth_w(rng, (co, ci, k, k))
+    y_ref, e_ref, _, _ = oracle.conv_fwd(g, x, wt, -7, ws)
+    y = T.zeros((n, g.oh, g.ow, co), dtype=T.int8, device="cuda")
+    e_out = i8s(T, 0)
+    ex = ops.NITIExecution(niti_amd.OP_DSP_CONV_INT8, ops.conv_common(k, stride=s, pad=p))
+    ins = [ops.tensor(dev(T, x.transpose(0, 2, 3, 1)), (n, ci, h, w), niti_amd.FORMAT_NHWC),
+           ops.tensor(dev(T, wt.transpose(2, 3, 1, 0)), (k, k, ci, co)),
+           ops.tensor(i8s(T, -7), (1, 1, 1, 1)), ops.tensor(i8s(T, ws), (1, 1, 1, 1))]
+    outs = [ops.tensor(y, (n, co, g.oh, g.ow), niti_amd.FORMAT_NHWC), ops.tensor(e_out, (1, 1, 1, 1))]
+    assert ex.resize(ins, outs) == 0
+    assert ex.execute(ins, outs) == 0
+    assert np.array_equal(y.cpu().numpy(), y_ref.transpose(0, 2, 3, 1))
+    assert int(e_out.item()) == e_ref
+
+
+@pytest.mark.parametrize("geo", [gg for gg in GEOMS if gg[2] > 1])
+def test_exec_dsp_deconv_int8(T, ops, oracle, geo):
+    """NITI_DSP_DECONV_Int8 slot on what grad/NITI_DSPConv_Int8_Grad.cpp:60-120 hands it: dy (stride 2:
+    LeftPoolGrad-dilated to ow x ow), pad + extraPad in the common, weights
+    transpose(rot180(transpose(w, {2,3,0,1})), {2,3,1,0}) and zero exponents."""
+    import niti_amd
+    n, ci, h, w, co, k, s, p = geo
+    g = oracle.geom(n, ci, h, w, co, k, stride=s, pad=p)
+    rng = np.random.default_rng(207)
+    dy = oracle.synth_dy(rng, (n, co, g.oh, g.ow))
+    wt, _ = oracle.synth_w(rng, (co, ci, k, k))
+    dx_ref, inc_ref, _, _ = oracle.conv_dgrad(g, dy, wt)
+    d = dy
+    if s == 2:
+        ow1 = w + 2 * p - k + 1
+        d = np.zeros((n, co, ow1, ow1), np.int8)
+        d[:, :, ::2, ::2][:, :, :g.oh, :g.ow] = dy
+    if (w - (d.shape[3] + 2 * p - k + 1)) % 2 or (h - (d.shape[2] + 2 * p - k + 1)) % 2:
+        pytest.skip("reference extra-pad arithmetic undefined for this shape")
+    e = (w - (d.shape[3] + 2 * p - k + 1)) // 2
+    if h - (d.shape[2] + 2 * (p + e) - k + 1):
+        pytest.skip("reference pads H and W by the same W-derived extra pad")
+    hwio = wt.transpose(2, 3, 1, 0)                                        # forward weights [k][k][ci][co]
+    wr = np.flip(hwio.transpose(2, 3, 0, 1), axis=(2, 3)).transpose(2, 3, 1, 0)  # [k][k][co][ci]
+    out = T.zeros((n, h, w, ci), dtype=T.int8, device="cuda")
+    e_out = i8s(T, 99)
+    ex = ops.NITIExecution(niti_amd.OP_DSP_DECONV_INT8, ops.conv_common(k, stride=1, pad=p + e))
+    ins = [ops.tensor(dev(T, d.transpose(0, 2, 3, 1)), (n, co, d.shape[2], d.shape[3]), niti_amd.FORMAT_NHWC),
+           ops.tensor(dev(T, wr), (k, k, co, ci)), ops.tensor(i8s(T, 0), (1, 1, 1, 1)),
+           ops.tensor(i8s(T, 0), (1, 1, 1, 1))]
+    outs = [ops.tensor(out, (n, ci, h, w), niti_amd.FORMAT_NHWC), ops.tensor(e_out, (1, 1, 1, 1))]
+    assert ex.resize(ins, outs) == 0
+    assert ex.execute(ins, outs) == 0
+    assert np.array_equal(out.cpu().numpy(), dx_ref.transpose(0, 2, 3, 1))
+    assert int(e_out.item()) == inc_ref
+
+
+@pytest.mark.parametrize("op", [822, 821])
+@pytest.mark.parametrize("geo", GEOMS)
+def test_exec_dsp_transpose_gradient_conv(T, ops, oracle, geo, op):
+    """NITI_DSP_TRANSPOSEGRADIENT_CONV_Int8 / GRADIENT_SPLITBatchCONV slots
+    (grad/NITI_DSPConv_Int8_Grad.cpp:160-219): {x^T = transpose(x, {3,1,2,0}), dy (stride 2:
+    LeftPoolGrad-dilated to ow x ow, stride 1 in the common), 0, 0} -> dw [Ci][KH][KW][Co] + bw - 2."""
+    n, ci, h, w, co, k, s, p = geo
+    if s == 2 and h != w:
+        pytest.skip("the graph dilates dy to a square ow x ow")
+    g = oracle.geom(n, ci, h, w, co, k, stride=s, pad=p)
+    rng = np.random.default_rng(208)
+    x = oracle.synth_x(rng, (n, ci, h, w))
+    dy = oracle.synth_dy(rng, (n, co, g.oh, g.ow))
+    dw_ref, bw, _, _ = oracle.conv_wgrad(g, x, dy)
+    d = dy
+    if s == 2:
+        ow1 = w + 2 * p - k + 1
+        d = np.zeros((n, co, ow1, ow1), np.int8)
+        d[:, :, ::2, ::2][:, :, :g.oh, :g.ow] = dy
+    xt = x.transpose(1, 2, 3, 0)                                   # NHWC x transposed {3,1,2,0}: [ci][h][w][n]
+    out = T.zeros((ci, k, k, co), dtype=T.int8, device="cuda")
+    e_out = i8s(T, 99)
+    ex = ops.NITIExecution(op, ops.conv_common((d.shape[3], d.shape[2]), stride=1, pad=p))
+    import niti_amd
+    ins = [ops.tensor(dev(T, xt), (ci, n, h, w), niti_amd.FORMAT_NHWC),
+           ops.tensor(dev(T, d.transpose(0, 2, 3, 1)), (n, co, d.shape[2], d.shape[3]), niti_amd.FORMAT_NHWC),
+           ops.tensor(i8s(T, 0), (1, 1, 1, 1)), ops.tensor(i8s(T, 0), (1, 1, 1, 1))]
+    outs = [ops.tensor(out, (ci, co, k, k), niti_amd.FORMAT_NHWC), ops.tensor(e_out, (1, 1, 1, 1))]
+    assert ex.resize(ins, outs) == 0
+    assert ex.execute(ins, outs) == 0
+    assert np.array_equal(out.cpu().numpy().transpose(3, 0, 1, 2), dw_ref)
+    assert int(e_out.item()) == (bw - 2 if bw else 0)
+
+
+def test_exec_dsp_transpose_gradient_rejects_stride2(T, ops):
+    import niti_amd
+    ex = ops.NITIExecution(niti_amd.OP_DSP_TRANSPOSEGRADIENT_CONV_INT8, ops.conv_common(3, stride=2, pad=1))
+    a = T.zeros((64,), dtype=T.int8, device="cuda")
+    ins = [ops.tensor(a, (2, 2, 4, 4), niti_amd.FORMAT_NHWC), ops.tensor(a, (2, 2, 2, 2), niti_amd.FORMAT_NHWC)]
+    outs = [ops.tensor(a, (2, 2, 3, 3), niti_amd.FORMAT_NHWC)]
+    assert ex.resize(ins, outs) == 2  # NOT_SUPPORT: the graph dilates dy (LeftPoolGrad) for stride 2
 
 
 # --------------------------------------------------------------------------- requant edge cases
