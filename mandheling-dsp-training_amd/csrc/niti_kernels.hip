@@ -761,7 +761,7 @@ struct KtIm2colU {
 constexpr int LDS_STAGE_BUDGET = NITI_LDS_BUDGET_KB * 1024;  // pipeline depth = min(MAX_STAGES, budget / stage bytes)
 constexpr int MAX_STAGES = NITI_MAX_STAGES;
 #ifndef NITI_ABLATE
-#define NITI_ABLATE 0  // diagnostic builds only: 1 = no global->LDS copies, 2 = no MFMA,
+#define NITI_ABLATE 0  // diagnostic builds only: 1 = no global->LDS copies, 2 = no MFMA, 5 = no taps tile stores, 6 = 2 + 5, 7 = 1 + 5, 8 = empty taps kernel,
                        // 3 = no copies and no per-step barrier, 4 = no per-step barrier
 #endif
 
@@ -1073,12 +1073,39 @@ __global__ void __launch_bounds__(NW * 64) gemm_kernel(LA la, LB lb, int M, int 
 // per element, each summing every G-th slab with 8 loads in flight; the G partials meet in
 // registers (shfl_xor inside the wave).  Splits are many and outputs small for the weight
 // gradient (e.g. VGG-11 L1: 160 slabs of 9 K elements), so split-level parallelism matters.
+// Where a 16-byte slab chunk e lands in C: the same place (GEMM slabs are [M][N] like C), or,
+// for the tap-sharing kernel's tile-blocked slabs ([tile][64 rows][NT taps][32 ch], each block's
+// partial tile one contiguous 72 KiB run), row co0 + r, columns t * CIP + ci0 + 4 * part of C.
+struct SlabLinear {
+    __device__ bool operator()(int64_t e, int64_t* dst) const {
+        *dst = e;
+        return true;
+    }
+};
+struct SlabTapsBlocked {
+    int tiles_ci, cip4, c_out, ld4;  // ld4 = NT * CIP / 4
+    FastDiv fTile, fRow, fPart, fTci;   // 64 * 72 v4i per tile, 72 per row, 8 per tap, tiles_ci
+    __device__ bool operator()(int64_t e, int64_t* dst) const {
+        const uint32_t u = (uint32_t)e;
+        const uint32_t tile = fdiv(fTile, u), rem = u - tile * 4608u;
+        const uint32_t row = fdiv(fRow, rem), rc = rem - row * 72u;
+        const uint32_t t = fdiv(fPart, rc), part = rc - t * 8u;
+        const uint32_t tco = fdiv(fTci, tile), tci = tile - tco * (uint32_t)tiles_ci;
+        const int co = (int)(tco * 64u + row);
+        *dst = (int64_t)co * ld4 + t * cip4 + tci * 8u + part;
+        return co < c_out;
+    }
+};
+
+template <class MAP>
 __global__ void splitk_reduce_kernel(const int32_t* __restrict__ slab, int splits, int64_t stride, int64_t n4, int G,
-                                     int32_t* __restrict__ C, uint32_t* __restrict__ amax) {
+                                     int32_t* __restrict__ C, uint32_t* __restrict__ amax, MAP map) {
     const int g = threadIdx.x & (G - 1);
     const int64_t e = (int64_t)blockIdx.x * (256 / G) + threadIdx.x / G;
+    int64_t de = 0;
+    const bool live = e < n4 && map(e, &de);
     v4i s = {0, 0, 0, 0};
-    if (e < n4) {
+    if (live) {
         const v4i* base = (const v4i*)slab + e;
         const int64_t st4 = stride / 4;
         // up to 8 independent loads in flight per pass (predicated, no dependent chain)
@@ -1098,8 +1125,8 @@ __global__ void splitk_reduce_kernel(const int32_t* __restrict__ slab, int split
         for (int j = 0; j < 4; ++j) s[j] += __shfl_xor(s[j], o, 64);
     }
     uint32_t m = 0;
-    if (g == 0 && e < n4) {
-        ((v4i*)C)[e] = s;
+    if (g == 0 && live) {
+        ((v4i*)C)[de] = s;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const uint32_t u = uabs32(s[j]);
@@ -1183,6 +1210,9 @@ __device__ __forceinline__ v2i tr8_at(uint32_t a) {
 }
 
 constexpr int TAPS_THREADS = 512;
+#ifndef NITI_TAPS_STAGES1
+#define NITI_TAPS_STAGES1 4  // pipeline stages of the one-DMA-per-wave (XPW 1) kernel
+#endif
 #ifndef NITI_TAPS_NT
 #define NITI_TAPS_NT 0  // nontemporal (L2-bypassing) stores of the int32 tile
 #endif
@@ -1192,7 +1222,8 @@ __global__ void __launch_bounds__(TAPS_THREADS) wgrad_taps_kernel(WgTaps g, Epi 
     constexpr int NW = TAPS_THREADS / 64;
     static_assert(NW == 8, "8 waves: tap half x K group x output-channel half");
     static_assert(NT == 9, "3x3 taps");
-    constexpr int STAGES = 4;
+    constexpr int STAGES = XPW == 1 ? NITI_TAPS_STAGES1 : 4;  // stage offsets stay below the 64 KiB DS immediate
+    static_assert(STAGES % 2 == 0, "the dy fragment buffer alternates with the step parity");
     constexpr int XB = XPW * 4096;  // region: 4 KiB x XPW of LDS-DMA (1 KiB per instruction)
     constexpr int DB = 4096;        // dy: 64 pixels x 64 bytes
     constexpr int ZB = XPW == 2 ? 4096 : 0;  // XPW 2: sink of the 4 waves without a dy chunk
@@ -1208,6 +1239,10 @@ __global__ void __launch_bounds__(TAPS_THREADS) wgrad_taps_kernel(WgTaps g, Epi 
     __shared__ __attribute__((aligned(16))) int8_t smem[SMEM];
 
     const int tid = threadIdx.x;
+    if (NITI_ABLATE == 8) {  // diagnostic: launch cost of the grid alone
+        if (tid == 0 && g.span == (unsigned long long*)1) smem[0] = 1;
+        return;
+    }
     span_begin(g.span);
     TAPS_STAMP(0);
     const int lane = tid & 63;
@@ -1260,12 +1295,12 @@ __global__ void __launch_bounds__(TAPS_THREADS) wgrad_taps_kernel(WgTaps g, Epi 
         const int ub = (q * g.imgs * g.H + ybase) * g.W * g.CIP;
         if (xw) {
             const bool v = xok && (unsigned)(ybase + xry) < (unsigned)g.H;
-            if (NITI_ABLATE != 1) dma16(rX, st0 + xblk * 1024, v ? (uint32_t)(ub + xrel) : OOB, 0u);
+            if (NITI_ABLATE != 1 && NITI_ABLATE != 7) dma16(rX, st0 + xblk * 1024, v ? (uint32_t)(ub + xrel) : OOB, 0u);
         }
         if (dw) {
-            if (NITI_ABLATE != 1) dma16(rD, st0 + XB + (wid & 3) * 1024, dvo, (uint32_t)r * 64u * (uint32_t)g.COP);
+            if (NITI_ABLATE != 1 && NITI_ABLATE != 7) dma16(rD, st0 + XB + (wid & 3) * 1024, dvo, (uint32_t)r * 64u * (uint32_t)g.COP);
         } else if (XPW == 2) {
-            if (NITI_ABLATE != 1) dma16(rD, st0 + XB + DB + (wid & 3) * 1024, OOB, 0u);
+            if (NITI_ABLATE != 1 && NITI_ABLATE != 7) dma16(rD, st0 + XB + DB + (wid & 3) * 1024, OOB, 0u);
         }
     };
 
@@ -1326,7 +1361,7 @@ __global__ void __launch_bounds__(TAPS_THREADS) wgrad_taps_kernel(WgTaps g, Epi 
                 lgkm_wait<2 * (NTW - 1 - J)>();
             reg_fence(fx[J]);
             if constexpr (J == 0) reg_fence(fd[CUR]);
-            if (NITI_ABLATE == 2)
+            if (NITI_ABLATE == 2 || NITI_ABLATE == 6)
                 acc[J][0] += fd[CUR][0] ^ fx[J][1];
             else
                 acc[J] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fd[CUR], fx[J], acc[J], 0, 0, 0);
@@ -1437,8 +1472,11 @@ __global__ void __launch_bounds__(TAPS_THREADS) wgrad_taps_kernel(WgTaps g, Epi 
     __syncthreads();
     TAPS_STAMP(3);
     // 16-byte row chunks: 8 consecutive threads write one 128-byte (tap, 32-channel) segment
+    // (SLAB: the block's partial tile as one contiguous run of its split's tile-blocked slab --
+    // sequential 16-byte stores drain at HBM write speed, where 128-byte segments strided over
+    // the [co][tap][ci] matrix by all 256 blocks at once drained at ~2.7 TB/s)
     const int32_t* ct = (const int32_t*)smem;
-    int32_t* Cs = MODE == EPI_SLAB ? epi.C + (int64_t)split * epi.slab_stride : epi.C;
+    int32_t* Cs = MODE == EPI_SLAB ? epi.C + (int64_t)split * epi.slab_stride + (int64_t)tile * (64 * NT * 32) : epi.C;
     constexpr int CPR = NT * 8;  // chunks per tile row
     const int rows = min(64, g.c_out - co0);
     uint32_t lmax = 0;
@@ -1446,8 +1484,11 @@ __global__ void __launch_bounds__(TAPS_THREADS) wgrad_taps_kernel(WgTaps g, Epi 
         const int row = c / CPR, rem = c - row * CPR;
         const int t = rem >> 3, part = rem & 7;
         const v4i v = *(const v4i*)(ct + row * LDT + t * 32 + part * 4);
-        v4i* dst = (v4i*)(Cs + (int64_t)(co0 + row) * epi.ldc + t * g.CIP + ci0 + part * 4);
-        if (NITI_TAPS_NT)
+        v4i* dst = MODE == EPI_SLAB ? (v4i*)(Cs + c * 4)
+                                    : (v4i*)(Cs + (int64_t)(co0 + row) * epi.ldc + t * g.CIP + ci0 + part * 4);
+        if (NITI_ABLATE >= 5)  // diagnostic: no tile stores (timing of the rest)
+            asm volatile("" ::"v"(v), "v"(dst));
+        else if (NITI_TAPS_NT)
             __builtin_nontemporal_store(v, dst);
         else
             *dst = v;
@@ -1670,14 +1711,15 @@ static hipError_t launch_mode(const GemmPlan& p, const LA& la, const LB& lb, int
     return hipGetLastError();
 }
 
+template <class MAP = SlabLinear>
 static hipError_t splitk_reduce(const GemmPlan& p, const int32_t* slab, int64_t n, int64_t stride, int32_t* C,
-                                uint32_t* amax, hipStream_t st) {
+                                uint32_t* amax, hipStream_t st, MAP map = MAP()) {
     const int64_t n4 = n / 4;
     int G = 1;  // split-level parallelism only where the output alone cannot fill the GPU
     while (G < 16 && G * 2 <= p.splits && n4 * G < 131072) G <<= 1;
     const int64_t blocks = (n4 + (256 / G) - 1) / (256 / G);
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, st, slab, p.splits, stride, n4, G, C,
-                       amax);
+    hipLaunchKernelGGL(splitk_reduce_kernel<MAP>, dim3((unsigned)blocks), dim3(256), 0, st, slab, p.splits, stride, n4,
+                       G, C, amax, map);
     return hipGetLastError();
 }
 
@@ -1963,6 +2005,9 @@ bool conv_wgrad_taps_ok(const ConvGeom& g) {
 }
 
 // splits: override (ov) or one block per CU with >= 4 steps per split
+// rows of a tile-blocked taps slab: whole 64-row output-channel tiles
+static int taps_slab_rows(const WgTaps& t) { return t.COP / 64 * 64; }
+
 static GemmPlan plan_taps(const WgTaps& t, int M, int N, size_t ws_elems, const PlanChoice* ov) {
     GemmPlan p;
     p.taps = true;
@@ -1979,7 +2024,8 @@ static GemmPlan plan_taps(const WgTaps& t, int M, int N, size_t ws_elems, const 
     if (s < 1) s = 1;
     p.kc_per_split = t.steps_total;
     p.strat = STRAT_STORE;
-    if (s >= 2) plan_slab(p, s, t.steps_total, 1, t.steps_total, false, M, N, ws_elems);
+    if (s >= 2) plan_slab(p, s, t.steps_total, 1, t.steps_total, false, taps_slab_rows(t), N, ws_elems);
+    (void)M;
     return p;
 }
 
@@ -2045,13 +2091,23 @@ static hipError_t wgrad_taps_run(const GemmPlan& p, const WgTaps& t, int M, int 
     Epi e;
     e.span = take_span();
     if (p.strat == STRAT_SLAB) {
+        const int mb = taps_slab_rows(t);
         e.C = ws;
         e.ldc = N;
-        e.slab_stride = (int64_t)slab_stride_elems(M, N);
+        e.slab_stride = (int64_t)slab_stride_elems(mb, N);
         hipError_t r = launch_taps<EPI_SLAB>(p, t, e, st);
         if (r == hipSuccess && after_gemm != nullptr) r = hipEventRecord(after_gemm, st);
         if (r != hipSuccess) return r;
-        return splitk_reduce(p, ws, (int64_t)M * N, e.slab_stride, C, amax, st);
+        SlabTapsBlocked map;
+        map.tiles_ci = t.tiles_ci;
+        map.cip4 = t.CIP / 4;
+        map.c_out = M;
+        map.ld4 = N / 4;
+        map.fTile = make_fastdiv(4608);
+        map.fRow = make_fastdiv(72);
+        map.fPart = make_fastdiv(8);
+        map.fTci = make_fastdiv((uint32_t)t.tiles_ci);
+        return splitk_reduce(p, ws, (int64_t)mb * N, e.slab_stride, C, amax, st, map);
     }
     e.C = C;
     e.ldc = N;
@@ -2103,7 +2159,7 @@ size_t conv_wgrad_workspace(const ConvGeom& g) {
     WgTaps t;
     if (wgrad_taps_geom(g, nullptr, nullptr, &t)) {
         const GemmPlan p = plan_taps(t, M, N, (size_t)-1, nullptr);
-        if (p.strat == STRAT_SLAB) e = std::max(e, (size_t)p.splits * slab_stride_elems(M, N));
+        if (p.strat == STRAT_SLAB) e = std::max(e, (size_t)p.splits * slab_stride_elems(taps_slab_rows(t), N));
     }
     return e * sizeof(int32_t);
 }
