@@ -1161,16 +1161,16 @@ __global__ void splitk_reduce_kernel(const int32_t* __restrict__ slab, int split
 // tap's region offset (ky*RW + kx rows).  32-byte rows keep each half-wave's transposed read
 // (8 consecutive region rows x 32 B = 256 contiguous bytes) conflict-free at any shift.
 //
-// A K step is two region steps (128 pixels).  8 waves, two per SIMD: wave w owns output-
-// channel half cg = w & 1 and K group kg = w >> 1 (the 32-pixel sub-step kg of every step), so
-// one wave's fragment reads and barrier wait hide under the other wave's MFMAs.  A step is one
-// MFMA stream per wave with the next step's fragment reads (a tap's x fragment is re-read
-// into its registers right after its MFMA) and the LDS-DMA issue in the gaps; every LDS
-// address is a per-lane register plus a compile-time stage offset (the K loop is unrolled by
-// the pipeline stages).  The 4 K groups' partial tiles meet through LDS two taps at a time,
-// and the int32 tile leaves as 16-byte row chunks.  Blocks: tiles (co64 x ci32) x K splits,
-// split-major under the XCD remap, so a split's tiles share one XCD's L2 and each XCD reads
-// only its own pixel range of x and dy.
+// A K step is one region step.  8 waves, two per SIMD: K group kg (the step's 32-pixel half)
+// x tap group tg (TapGroup: 5 or 4 of the 18 (output-channel half, tap) tiles, paired 5 + 4 on
+// a SIMD), so one wave's fragment reads and barrier wait hide under the other wave's MFMAs.
+// A step is one MFMA stream per wave with the next step's fragment reads (double-buffered)
+// and the LDS-DMA issue in the gaps; every LDS address is a per-lane register plus a
+// compile-time stage offset (the K loop is unrolled by the pipeline stages).  The two K
+// groups' partial tiles meet through LDS, and the int32 tile leaves as 16-byte row chunks
+// (split-K: one contiguous run of a tile-blocked slab).  Blocks: tiles (co64 x ci32) x K
+// splits, split-major under the XCD remap, so a split's tiles share one XCD's L2 and each XCD
+// reads only its own pixel range of x and dy.
 // =====================================================================================
 struct WgTaps {
     const int8_t* x;   // NHWC16 [N][H][W][CIP]
@@ -1210,6 +1210,24 @@ __device__ __forceinline__ v2i tr8_at(uint32_t a) {
 }
 
 constexpr int TAPS_THREADS = 512;
+
+// The four tap groups of a K group's 18 (output-channel half, tap) tiles: the two waves on one
+// SIMD hold 5 + 4 tiles (9 MFMAs per SIMD per step), and a wave reads both dy halves plus 2-3 x
+// taps per step (18 fragments per K group, where per-channel-half waves read 22).  Tile j of
+// group G is (ch(j), tap(xi(j))); x tap i is read after MFMA i + 1, both dy halves after MFMA 0.
+template <int G>
+struct TapGroup {
+    static constexpr int NX = G < 2 ? 3 : 2;     // x taps
+    static constexpr int NTILE = G < 2 ? 5 : 4;  // MFMA tiles
+    static constexpr int tap(int i) { return G == 0 ? i : G == 1 ? 2 + i : G == 2 ? 5 + i : 7 + i; }
+    static constexpr int ch(int j) { return G == 1 ? ((j + 1) & 1) : (j & 1); }
+    static constexpr int xi(int j) { return G == 1 ? (j + 1) >> 1 : j >> 1; }
+    // ds_reads a step issues before its MFMA j (its reads of the next step)
+    static constexpr int cum(int j) { return j == 0 ? 0 : 4 + 2 * (j - 1 < NX ? j - 1 : NX); }
+    // reads issued after the last read of MFMA j's x tap: 2 per later x tap of the previous
+    // step, plus this step's reads so far
+    static constexpr int wait(int j, bool more) { return 2 * (NX - 1 - xi(j)) + (more ? cum(j) : 0); }
+};
 #ifndef NITI_TAPS_STAGES1
 #define NITI_TAPS_STAGES1 4  // pipeline stages of the one-DMA-per-wave (XPW 1) kernel
 #endif
@@ -1220,8 +1238,8 @@ constexpr int TAPS_THREADS = 512;
 template <int NT, int XPW, int MODE>
 __global__ void __launch_bounds__(TAPS_THREADS) wgrad_taps_kernel(WgTaps g, Epi epi) {
     constexpr int NW = TAPS_THREADS / 64;
-    static_assert(NW == 8, "8 waves: tap half x K group x output-channel half");
-    static_assert(NT == 9, "3x3 taps");
+    static_assert(NW == 8, "8 waves: 4 tap groups x K group");
+    static_assert(NT == 9, "3x3 taps (the tap groups of TapGroup)");
     constexpr int STAGES = XPW == 1 ? NITI_TAPS_STAGES1 : 4;  // stage offsets stay below the 64 KiB DS immediate
     static_assert(STAGES % 2 == 0, "the dy fragment buffer alternates with the step parity");
     constexpr int XB = XPW * 4096;  // region: 4 KiB x XPW of LDS-DMA (1 KiB per instruction)
@@ -1229,8 +1247,8 @@ __global__ void __launch_bounds__(TAPS_THREADS) wgrad_taps_kernel(WgTaps g, Epi 
     constexpr int ZB = XPW == 2 ? 4096 : 0;  // XPW 2: sink of the 4 waves without a dy chunk
     constexpr int SB = XB + DB + ZB;
     constexpr int LOADS = XPW;      // DMA instructions per wave per step
-    constexpr int TA = (NT + 1) / 2;  // taps of wave half 0 (half 1 takes the rest)
-    constexpr int XCH = 2 * 2 * TA * 4096;  // exchange: one 32x32 int32 tile per (tap half, cg, tap)
+    constexpr int TA = 5;                   // most (output-channel half, tap) tiles of one wave
+    constexpr int XCH = 4 * TA * 4096;      // exchange: one 32x32 int32 tile per (tap group, tile)
     constexpr int LDT = NT * 32 + 4;        // staged C tile pitch (int32)
     constexpr int CT = 64 * LDT * 4;
     constexpr int SMEM0 = STAGES * SB > XCH ? STAGES * SB : XCH;
@@ -1247,8 +1265,9 @@ __global__ void __launch_bounds__(TAPS_THREADS) wgrad_taps_kernel(WgTaps g, Epi 
     TAPS_STAMP(0);
     const int lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-    // waves w and w + 4 share a SIMD (cyclic SIMD order): one takes TA taps, the other NT - TA
-    const int th = wid >> 2, kg = (wid >> 1) & 1, cg = wid & 1;
+    // waves w and w + 4 share a SIMD (cyclic SIMD order): tap group tg (TapGroup) and K group kg;
+    // the groups paired on a SIMD (0 + 2, 1 + 3) hold 5 + 4 tiles, 9 MFMAs per SIMD per step
+    const int kg = (wid >> 1) & 1, tg = (wid >> 2) * 2 + (wid & 1);
     const int logical = xcd_remap(blockIdx.x, gridDim.x);
     const int split = (int)fdiv(g.fTiles, (uint32_t)logical);
     const int tile = logical - split * g.tiles;
@@ -1309,7 +1328,8 @@ __global__ void __launch_bounds__(TAPS_THREADS) wgrad_taps_kernel(WgTaps g, Epi 
     const uint32_t smem_base = lds_addr(smem);
     const int p0 = kg * 32 + 16 * (lane >> 5) + ((lane & 15) >> 1);
     const int cofs = 16 * ((lane >> 4) & 1) + 8 * (lane & 1);
-    const uint32_t aD = smem_base + XB + (uint32_t)kt_off8<64>(p0, (cg * 32 + cofs) >> 3);  // +8 rows: +512
+    const uint32_t aD0 = smem_base + XB + (uint32_t)kt_off8<64>(p0, cofs >> 3);  // +8 rows: +512
+    const uint32_t aD1 = smem_base + XB + (uint32_t)kt_off8<64>(p0, (32 + cofs) >> 3);
     auto qrow = [&](int p) {
         const int img = (int)fdiv(g.fPPI, (uint32_t)p), rem = p - img * g.PPI;
         const int oy = (int)fdiv(g.fOW, (uint32_t)rem), ox = rem - oy * g.OW;
@@ -1318,56 +1338,63 @@ __global__ void __launch_bounds__(TAPS_THREADS) wgrad_taps_kernel(WgTaps g, Epi 
     const uint32_t aX0 = smem_base + (uint32_t)(qrow(p0) * 32 + cofs);
     const uint32_t aX1 = smem_base + (uint32_t)(qrow(p0 + 8) * 32 + cofs);
 
-    // everything below runs per tap half TH (compile time): taps [T0, T0 + NTW)
-    auto run = [&](auto th_c) {
-        constexpr int TH = decltype(th_c)::value;
-        constexpr int T0 = TH ? TA : 0, NTW = TH ? NT - TA : TA;
-        uint32_t aX[NTW][2];
+    // everything below runs per tap group G (compile time, TapGroup): its x taps, its
+    // (output-channel half, tap) tiles and the step's fragment reads
+    auto run = [&](auto g_c) {
+        using TG = TapGroup<decltype(g_c)::value>;
+        constexpr int NX = TG::NX, NTW = TG::NTILE;
+        uint32_t aX[NX][2];
 #pragma unroll
-        for (int j = 0; j < NTW; ++j) {
-            const int t = T0 + j, ky = t / 3, kx = t % 3;
+        for (int i = 0; i < NX; ++i) {
+            const int t = TG::tap(i), ky = t / 3, kx = t % 3;
             const uint32_t o = (uint32_t)((ky * g.RW + kx) * 32);
-            aX[j][0] = aX0 + o;
-            aX[j][1] = aX1 + o;
+            aX[i][0] = aX0 + o;
+            aX[i][1] = aX1 + o;
         }
         v16i acc[NTW];
 #pragma unroll
         for (int j = 0; j < NTW; ++j)
 #pragma unroll
             for (int i = 0; i < 16; ++i) acc[j][i] = 0;
-        // dy double-buffered (read early in the previous step's stream); a tap's x fragment is
-        // re-read into its registers right after its MFMA
-        v4i fd[2], fx[NTW];
+        // both dy halves and the group's x taps, double-buffered by step parity: step s + 1's
+        // fragments are read during step s, both dy halves after MFMA 0, x tap i after MFMA i + 1
+        v4i fd[2][2], fx[2][NX];
         auto read_d = [&](auto st_c, auto buf_c) {
             constexpr int ST = decltype(st_c)::value, BUF = decltype(buf_c)::value;
-            const v2i d0 = tr8_at<ST * SB>(aD), d1 = tr8_at<ST * SB + 512>(aD);
-            fd[BUF] = v4i{d0[0], d0[1], d1[0], d1[1]};
+            const v2i a0 = tr8_at<ST * SB>(aD0), a1 = tr8_at<ST * SB + 512>(aD0);
+            const v2i b0 = tr8_at<ST * SB>(aD1), b1 = tr8_at<ST * SB + 512>(aD1);
+            fd[BUF][0] = v4i{a0[0], a0[1], a1[0], a1[1]};
+            fd[BUF][1] = v4i{b0[0], b0[1], b1[0], b1[1]};
         };
-        auto read_x = [&](auto st_c, auto j_c) {
-            constexpr int ST = decltype(st_c)::value, J = decltype(j_c)::value;
-            const v2i x0 = tr8_at<ST * SB>(aX[J][0]), x1 = tr8_at<ST * SB>(aX[J][1]);
-            fx[J] = v4i{x0[0], x0[1], x1[0], x1[1]};
+        auto read_x = [&](auto st_c, auto buf_c, auto i_c) {
+            constexpr int ST = decltype(st_c)::value, BUF = decltype(buf_c)::value, I = decltype(i_c)::value;
+            const v2i x0 = tr8_at<ST * SB>(aX[I][0]), x1 = tr8_at<ST * SB>(aX[I][1]);
+            fx[BUF][I] = v4i{x0[0], x0[1], x1[0], x1[1]};
         };
-        // MFMA j of step s (stage ST, dy buffer CUR); after it: tap j of step s + 1 (after MFMA
-        // 0 also its dy), and after MFMA 1 the LDS-DMA of step s + STAGES - 1.  Before MFMA j a
-        // counted lgkm wait lets through exactly the reads issued after tap j's (<= 2 NTW).
+        // MFMA j of step s (stage ST, buffers CUR); after it, the next step's reads of gap j
+        // (into CUR ^ 1) and after MFMA 1 the LDS-DMA of step s + STAGES - 1.  The counted lgkm
+        // wait before MFMA j lets through the reads issued after its x tap's (TapGroup::wait).
         auto gap = [&](auto u_c, auto j_c, auto ss_c, int s, bool more, bool dma) {
             constexpr int U = decltype(u_c)::value, J = decltype(j_c)::value;
             constexpr bool SS = decltype(ss_c)::value;
             constexpr int ST = U % STAGES, CUR = U & 1, NST = (ST + 1) % STAGES;
+            constexpr int CH = TG::ch(J), XI = TG::xi(J);
             if (SS || more)
-                lgkm_wait<2 * (NTW - 1 - J) + (J > 0 ? 2 * J + 2 : 0)>();
+                lgkm_wait<TG::wait(J, true)>();
             else
-                lgkm_wait<2 * (NTW - 1 - J)>();
-            reg_fence(fx[J]);
-            if constexpr (J == 0) reg_fence(fd[CUR]);
+                lgkm_wait<TG::wait(J, false)>();
+            reg_fence(fx[CUR][XI]);
+            reg_fence(fd[CUR][CH]);
             if (NITI_ABLATE == 2 || NITI_ABLATE == 6)
-                acc[J][0] += fd[CUR][0] ^ fx[J][1];
+                acc[J][0] += fd[CUR][CH][0] ^ fx[CUR][XI][1];
             else
-                acc[J] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fd[CUR], fx[J], acc[J], 0, 0, 0);
-            if (SS || more) {
-                if constexpr (J == 0) read_d(std::integral_constant<int, NST>(), std::integral_constant<int, CUR ^ 1>());
-                read_x(std::integral_constant<int, NST>(), j_c);
+                acc[J] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fd[CUR][CH], fx[CUR][XI], acc[J], 0, 0, 0);
+            if ((SS || more) && NITI_ABLATE != 9) {
+                if constexpr (J == 0)
+                    read_d(std::integral_constant<int, NST>(), std::integral_constant<int, CUR ^ 1>());
+                else if constexpr (J - 1 < NX)
+                    read_x(std::integral_constant<int, NST>(), std::integral_constant<int, CUR ^ 1>(),
+                           std::integral_constant<int, J - 1>());
             }
             if constexpr (J == 1) {
                 if (SS || dma) issue((ST + STAGES - 1) % STAGES, s + STAGES - 1);
@@ -1397,10 +1424,13 @@ __global__ void __launch_bounds__(TAPS_THREADS) wgrad_taps_kernel(WgTaps g, Epi 
             wait_steps<LOADS, STAGES - 2>(min(STAGES - 2, nsteps - 1));
             __builtin_amdgcn_s_barrier();
             asm volatile("" ::: "memory");
+            // step 0's reads in a step's gap order (its first waits count on that order)
             read_d(std::integral_constant<int, 0>(), std::integral_constant<int, 0>());
-            [&]<int... J>(std::integer_sequence<int, J...>) {
-                (read_x(std::integral_constant<int, 0>(), std::integral_constant<int, J>()), ...);
-            }(std::make_integer_sequence<int, NTW>());
+            [&]<int... I>(std::integer_sequence<int, I...>) {
+                (read_x(std::integral_constant<int, 0>(), std::integral_constant<int, 0>(),
+                        std::integral_constant<int, I>()),
+                 ...);
+            }(std::make_integer_sequence<int, NX>());
         }
         TAPS_STAMP(1);
         // steady state: STAGES straight-line steps per iteration while every step has its DMA;
@@ -1420,12 +1450,12 @@ __global__ void __launch_bounds__(TAPS_THREADS) wgrad_taps_kernel(WgTaps g, Epi 
         __syncthreads();
         TAPS_STAMP(2);
 
-        // the two K groups meet: K group 0 keeps taps [0, KA) of the wave's set, group 1 the
-        // rest; each sends the other part (MFMA C layout, 16-byte LDS writes), adds its
-        // partner's, then writes the kept tiles row-major into the staged tile ct [64][LDT]
+        // the two K groups meet: K group 0 keeps tiles [0, KA) of the group, K group 1 the rest;
+        // each sends the other part (MFMA C layout, 16-byte LDS writes), adds its partner's,
+        // then writes the kept tiles row-major into the staged tile ct [64][LDT]
         constexpr int KA = (NTW + 1) / 2;
         v4i* xbuf = (v4i*)smem;
-        const int xs0 = (th * 2 + cg) * TA * 256;  // v4i index of the wave pair's first tile
+        const int xs0 = tg * TA * 256;  // v4i index of the group's first tile
 #pragma unroll
         for (int j = 0; j < NTW; ++j) {
             const bool mine = kg == 0 ? j < KA : j >= KA;
@@ -1457,18 +1487,21 @@ __global__ void __launch_bounds__(TAPS_THREADS) wgrad_taps_kernel(WgTaps g, Epi 
         for (int j = 0; j < NTW; ++j) {
             const bool mine = kg == 0 ? j < KA : j >= KA;
             if (mine) {
+                const int ch = TG::ch(j), tap = TG::tap(TG::xi(j));
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {
-                    const int row = cg * 32 + (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
-                    ct[row * LDT + (T0 + j) * 32 + (lane & 31)] = acc[j][i];
+                    const int row = ch * 32 + (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
+                    ct[row * LDT + tap * 32 + (lane & 31)] = acc[j][i];
                 }
             }
         }
     };
-    if (th == 0)
-        run(std::integral_constant<int, 0>());
-    else
-        run(std::integral_constant<int, 1>());
+    switch (tg) {
+        case 0: run(std::integral_constant<int, 0>()); break;
+        case 1: run(std::integral_constant<int, 1>()); break;
+        case 2: run(std::integral_constant<int, 2>()); break;
+        default: run(std::integral_constant<int, 3>()); break;
+    }
     __syncthreads();
     TAPS_STAMP(3);
     // 16-byte row chunks: 8 consecutive threads write one 128-byte (tap, 32-channel) segment
