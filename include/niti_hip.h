@@ -126,6 +126,12 @@ int niti_execution_execute(niti_execution_t e, const niti_tensor* inputs, int n_
 void niti_destroy_execution(niti_execution_t e);
 /* bytes of device workspace the handle holds after resize */
 size_t niti_execution_workspace_bytes(niti_execution_t e);
+/* CPUTensorConverter::convert (source/backend/cpu/CPUTensorConvert.cpp:98-210) for int8 device
+ * tensors: NCHW <-> NHWC <-> NC4HW4 (MNN CPU layout [ceil(C/4)][N][H][W][4], pad lanes written as
+ * zero).  src and dst have the same logical dims {N, C, H, W}; asynchronous on `stream`.
+ * COMPUTE_SIZE_ERROR on a dims mismatch, NOT_SUPPORT on another format, INVALID_VALUE on NULL or
+ * in-place buffers. */
+int niti_tensor_convert(const niti_tensor* src, const niti_tensor* dst, void* stream);
 
 /* ============================ 2. native split primitives ============================== */
 /* A range estimate (max|acc| of one tensor, NITI_RangeEstimate's input, CommonOptFunction.cpp:

@@ -69,6 +69,11 @@ void niti_destroy_execution(niti_execution_t e) { delete e; }
 
 size_t niti_execution_workspace_bytes(niti_execution_t e) { return e ? e->impl->workspaceBytes() : 0; }
 
+int niti_tensor_convert(const niti_tensor* src, const niti_tensor* dst, void* stream) {
+    if (!src || !dst) return NITI_INVALID_VALUE;
+    return niti::convert_tensor(*src, *dst, S(stream));
+}
+
 // ------------------------------------------------------------------ section 2
 int niti_geom_finalize(niti_geom* g) {
     if (!g) return NITI_INVALID_VALUE;

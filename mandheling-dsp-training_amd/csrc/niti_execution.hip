@@ -680,6 +680,63 @@ class DspTransposeGradientExecution : public Execution {
     size_t slab_bytes_ = 0;
 };
 
+// ------------------------------------------------------------------ tensor format conversion
+// CPUTensorConverter::convert (CPUTensorConvert.cpp:98-210) for int8 tensors between NCHW,
+// NHWC and MNN's CPU NC4HW4 ([ceil(C/4)][N][H][W][4], pad lanes zero), SURVEY.md §8(f)-3.
+// One pass over the destination: element i decodes to (n, c, h, w) in the destination format
+// and reads the source element in its own format.
+struct FormatIndex {
+    int N, C, H, W;
+    __device__ int64_t index(int f, int n, int c, int h, int w) const {
+        if (f == NITI_FORMAT_NCHW) return (((int64_t)n * C + c) * H + h) * W + w;
+        if (f == NITI_FORMAT_NHWC) return (((int64_t)n * H + h) * W + w) * C + c;
+        return ((((int64_t)(c >> 2) * N + n) * H + h) * W + w) * 4 + (c & 3);
+    }
+    __device__ void decode(int f, int64_t i, int* n, int* c, int* h, int* w) const {
+        if (f == NITI_FORMAT_NCHW) {
+            *w = (int)(i % W), i /= W;
+            *h = (int)(i % H), i /= H;
+            *c = (int)(i % C), *n = (int)(i / C);
+        } else if (f == NITI_FORMAT_NHWC) {
+            *c = (int)(i % C), i /= C;
+            *w = (int)(i % W), i /= W;
+            *h = (int)(i % H), *n = (int)(i / H);
+        } else {
+            const int lane = (int)(i & 3);
+            i >>= 2;
+            *w = (int)(i % W), i /= W;
+            *h = (int)(i % H), i /= H;
+            *n = (int)(i % N);
+            *c = (int)(i / N) * 4 + lane;
+        }
+    }
+};
+struct ConvertFormat {
+    const int8_t* src;
+    int8_t* dst;
+    FormatIndex ix;
+    int sf, df;
+    __device__ void operator()(int64_t i) const {
+        int n, c, h, w;
+        ix.decode(df, i, &n, &c, &h, &w);
+        dst[i] = c < ix.C ? src[ix.index(sf, n, c, h, w)] : (int8_t)0;
+    }
+};
+
+int convert_tensor(const niti_tensor& s, const niti_tensor& d, hipStream_t st) {
+    for (int k = 0; k < 4; ++k)
+        if (s.dims[k] != d.dims[k] || s.dims[k] <= 0) return NITI_COMPUTE_SIZE_ERROR;
+    auto ok = [](int f) { return f == NITI_FORMAT_NCHW || f == NITI_FORMAT_NHWC || f == NITI_FORMAT_NC4HW4; };
+    if (!ok(s.format) || !ok(d.format)) return NITI_NOT_SUPPORT;
+    if (s.data == nullptr || d.data == nullptr || s.data == d.data) return NITI_INVALID_VALUE;
+    const FormatIndex ix{s.dims[0], s.dims[1], s.dims[2], s.dims[3]};
+    const int64_t cs = d.format == NITI_FORMAT_NC4HW4 ? (int64_t)(ix.C + 3) / 4 * 4 : ix.C;
+    const int64_t total = (int64_t)ix.N * cs * ix.H * ix.W;
+    const hipError_t e =
+        launch_map(total, ConvertFormat{(const int8_t*)s.data, (int8_t*)d.data, ix, s.format, d.format}, st);
+    return e == hipSuccess ? NITI_NO_ERROR : NITI_INVALID_VALUE;
+}
+
 Execution* create_execution(int op_type, const niti_conv2d_common* c, int* err) {
     *err = NITI_NO_ERROR;
     niti_conv2d_common dflt{};

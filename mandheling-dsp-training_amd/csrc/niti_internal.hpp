@@ -35,6 +35,8 @@ class Execution {
 };
 
 Execution* create_execution(int op_type, const niti_conv2d_common* common, int* err);
+// CPUTensorConverter::convert for int8 NCHW / NHWC / NC4HW4 (returns an ErrorCode value)
+int convert_tensor(const niti_tensor& src, const niti_tensor& dst, hipStream_t st);
 bool geom_from_common(const niti_conv2d_common& c, int n, int ci, int h, int w, int co, int kh, int kw,
                       ConvGeom* g);
 

@@ -82,6 +82,7 @@ def lib():
         "niti_execution_execute": (ci, [vp, tp, ci, tp, ci, vp]),
         "niti_destroy_execution": (None, [vp]),
         "niti_execution_workspace_bytes": (C.c_size_t, [vp]),
+        "niti_tensor_convert": (ci, [tp, tp, vp]),
         "niti_geom_finalize": (ci, [C.POINTER(Geom)]),
         "niti_conv_workspace_bytes": (ci, [C.POINTER(Geom), ci, C.POINTER(C.c_size_t)]),
         "niti_matmul_workspace_bytes": (ci, [ci, ci, ci, C.POINTER(C.c_size_t)]),

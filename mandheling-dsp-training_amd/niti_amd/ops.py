@@ -32,6 +32,12 @@ def tensor(t: torch.Tensor, dims, fmt=L.FORMAT_NCHW) -> L.Tensor:
     return v
 
 
+def convert(src: L.Tensor, dst: L.Tensor, stream=None) -> int:
+    """CPUTensorConverter::convert (CPUTensorConvert.cpp:98-210): int8 NCHW / NHWC / NC4HW4."""
+    s = stream if stream is not None else torch.cuda.current_stream().cuda_stream
+    return L.lib().niti_tensor_convert(C.byref(src), C.byref(dst), C.c_void_p(s))
+
+
 def conv_common(kernel, stride=1, pad=0, dilate=1, pads=None, pad_mode=L.PAD_CAFFE, input_count=0,
                 output_count=0, group=1) -> L.ConvCommon:
     kx, ky = (kernel, kernel) if isinstance(kernel, int) else kernel

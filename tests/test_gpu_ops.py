@@ -442,6 +442,37 @@ def test_exec_dsp_transpose_gradient_rejects_stride2(T, ops):
     assert ex.resize(ins, outs) == 2  # NOT_SUPPORT: the graph dilates dy (LeftPoolGrad) for stride 2
 
 
+# --------------------------------------------------------------------------- tensor formats (§8(f)-3)
+def _as_format(x_nchw, fmt, oracle):
+    if fmt == 0:
+        return np.ascontiguousarray(x_nchw)
+    if fmt == 1:
+        return np.ascontiguousarray(x_nchw.transpose(0, 2, 3, 1))
+    return oracle.nchw_to_c4(x_nchw)  # MNN CPU NC4HW4 [C/4][N][H][W][4] (oracle restatement)
+
+
+@pytest.mark.parametrize("shape", [(2, 5, 3, 7), (1, 8, 4, 4), (3, 1, 1, 9), (4, 130, 2, 3)])
+@pytest.mark.parametrize("sf,df", [(a, b) for a in range(3) for b in range(3) if a != b])
+def test_tensor_convert(T, ops, oracle, shape, sf, df):
+    n, c, h, w = shape
+    rng = np.random.default_rng(209)
+    x = rng.integers(-128, 128, size=shape, dtype=np.int8)
+    src = _as_format(x, sf, oracle)
+    want = _as_format(x, df, oracle)
+    d_src = dev(T, src)
+    d_dst = T.full(want.shape, 77, dtype=T.int8, device="cuda")  # pad lanes must come back zero
+    assert ops.convert(ops.tensor(d_src, shape, sf), ops.tensor(d_dst, shape, df)) == 0
+    assert np.array_equal(d_dst.cpu().numpy(), want)
+
+
+def test_tensor_convert_errors(T, ops):
+    a = T.zeros(64, dtype=T.int8, device="cuda")
+    b = T.zeros(64, dtype=T.int8, device="cuda")
+    assert ops.convert(ops.tensor(a, (1, 4, 2, 2), 0), ops.tensor(b, (1, 4, 2, 3), 1)) == 3  # COMPUTE_SIZE_ERROR
+    assert ops.convert(ops.tensor(a, (1, 4, 2, 2), 0), ops.tensor(b, (1, 4, 2, 2), 7)) == 2  # NOT_SUPPORT
+    assert ops.convert(ops.tensor(a, (1, 4, 2, 2), 0), ops.tensor(a, (1, 4, 2, 2), 1)) == 5  # in place
+
+
 # --------------------------------------------------------------------------- requant edge cases
 @pytest.mark.parametrize("vals", [[0, 0, 0], [128, -5, 3], [200, -103, 101], [40000, -1007, 0], [1, -1, 0],
                                   [2**30, -(2**30) + 7, 12345], [127, -127, 64]])
