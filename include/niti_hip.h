@@ -52,7 +52,12 @@ enum niti_op_type {
     NITI_OP_MATMUL_INT8 = 713,             /* NITI_MatMul_Int8        -> NITI_Matmul_Int8.cpp:140-231 */
     NITI_OP_GRADIENT_CONV_INT8 = 715,      /* NITI_GradientCONV_Int8  -> NITI_GradientConv_Int8.cpp:165-298 */
     NITI_OP_DSP_CONV_INT8 = 800,           /* NITI_DSP_CONV_Int8      -> NITI_DSPConv_Int8.cpp:160-455 */
+    NITI_OP_DSP_RELU_INT8 = 801,           /* NITI_DSP_RELU_Int8      -> NITI_DSPRelu_Int8.cpp */
+    NITI_OP_DSP_MAXPOOL_INT8 = 802,        /* NITI_DSP_MAXPOOL_Int8   -> NITI_DSPMaxpool_Int8.cpp */
+    NITI_OP_DSP_RELUGRAD_INT8 = 805,       /* NITI_DSP_RELUGRAD_Int8  -> NITI_DSPReluGrad_Int8.cpp */
+    NITI_OP_DSP_MAXPOOLGRAD_INT8 = 807,    /* NITI_DSP_MAXPOOLGRAD_Int8 -> NITI_DSPMaxPoolGrad_Int8.cpp */
     NITI_OP_DSP_DECONV_INT8 = 811,         /* NITI_DSP_DECONV_Int8    -> NITI_DSPDeConv_Int8.cpp */
+    NITI_OP_DSP_NOP_INT8 = 817,            /* NITI_DSP_NOP_Int8       -> NITI_DSPNop_Int8.cpp */
     NITI_OP_DSP_MATMUL_GRADIENT_INT8 = 818, /* NITI_DSP_MATMUL_GRADIENT_Int8 -> NITI_DSPMatmulGradientConv_Int8.cpp:105-553 */
     NITI_OP_DSP_PARALLEL_GRADIENTCONV_INT8 = 820,   /* -> NITI_DSPParallelGradientConv_Int8.cpp (818's tensors) */
     NITI_OP_DSP_GRADIENT_SPLITBATCHCONV_INT8 = 821, /* -> NITI_DSPGradientSplitBatchConv_Int8.cpp (822's tensors) */
@@ -112,6 +117,11 @@ int niti_create_execution(int op_type, const niti_conv2d_common* common, niti_ex
  *                                 wscale int8[1]}                         out{y NHWC [N,Co,OH,OW], exp_out int8[1]}
  *                             (the deconv slot gets the graph's padded/dilated dy and rotated weights)
  *  NITI_OP_DSP_PARALLEL_GRADIENTCONV_INT8 as NITI_OP_DSP_MATMUL_GRADIENT_INT8, KH x KW from dw's dims
+ *  NITI_OP_DSP_RELU_INT8 / NITI_OP_DSP_NOP_INT8 in {x NHWC} out{y NHWC}; NITI_OP_DSP_RELUGRAD_INT8
+ *                             in {x, dy} out{dx}; common may be NULL for these three
+ *  NITI_OP_DSP_MAXPOOL_INT8   in {x NHWC, ascale int8[1]} out{y NHWC, ascale int8[1]}; the pool's
+ *                             kernel / stride / pad in the common's kernel_x/y, stride_x/y, pad_x/y
+ *  NITI_OP_DSP_MAXPOOLGRAD_INT8 in {x, y, dy} NHWC out{dx NHWC}
  *  NITI_OP_DSP_TRANSPOSEGRADIENT_CONV_INT8, NITI_OP_DSP_GRADIENT_SPLITBATCHCONV_INT8 (stride 1; the graph
  *                             dilates dy for stride 2)
  *                             in {x^T NHWC [Ci,N,H,W], dy NHWC [N,Co,OH,OW], 0, 0}

@@ -680,6 +680,109 @@ class DspTransposeGradientExecution : public Execution {
     size_t slab_bytes_ = 0;
 };
 
+// ------------------------------------------------------------------ NITI_DSP element-wise slots
+// NITI_DSP_RELU_Int8 (801) {x} -> {max(x, 0)}; NITI_DSP_RELUGRAD_Int8 (805) {x, dy} -> {x > 0 ? dy : 0}
+// (grad/NITI_ReluGrad_Int8.cpp:29-47); NITI_DSP_NOP_Int8 (817) {x} -> {x} (the DSP binary add's
+// gradient, grad/NITI_DSPBinaryGrad.cpp:14-42); NITI_DSP_MAXPOOL_Int8 (802) {x, ascale} ->
+// {y, ascale} (NITI_DSPMaxpool_Int8.cpp:183 passes the scale through) and
+// NITI_DSP_MAXPOOLGRAD_Int8 (807) {x, y, dy} -> {dx} (grad/NITI_Pool_Int8_Grad.cpp:40-64), on
+// NHWC tensors with the CPU path's numerics (NITI_CPURelu_Int8.cpp:28-61,
+// NITI_CPUReluGrad_Int8.cpp:28-62, NITI_Maxpool_Int8.cpp:24-72, NITI_CPUPoolGrad_Int8.cpp:21-77:
+// first maximum wins).  The pool's NITI_Pool_Int8 {kernelX/Y, strideX/Y, padX/Y} arrive in the
+// common's kernel / stride / pad fields (square windows).
+struct ReluMap {
+    const int8_t* x;
+    int8_t* y;
+    __device__ void operator()(int64_t i) const { y[i] = x[i] > 0 ? x[i] : (int8_t)0; }
+};
+struct CopyMap {
+    const int8_t* x;
+    int8_t* y;
+    __device__ void operator()(int64_t i) const { y[i] = x[i]; }
+};
+
+class DspElementwiseExecution : public Execution {
+   public:
+    DspElementwiseExecution(int op, const niti_conv2d_common& c) : op_(op), common_(c) {}
+    int onResize(const niti_tensor* in, int nin, const niti_tensor* out, int nout) override {
+        const int need = op_ == NITI_OP_DSP_RELUGRAD_INT8 ? 2 : op_ == NITI_OP_DSP_MAXPOOLGRAD_INT8 ? 3 : 1;
+        if (nin < need || nout < 1) return NITI_INVALID_VALUE;
+        for (int i = 0; i < need; ++i)
+            if (in[i].format != NITI_FORMAT_NHWC) return NITI_NOT_SUPPORT;
+        if (out[0].format != NITI_FORMAT_NHWC) return NITI_NOT_SUPPORT;
+        const niti_tensor& x = in[0];
+        n_ = x.dims[0], c_ = x.dims[1], h_ = x.dims[2], w_ = x.dims[3];
+        elems_ = (int64_t)n_ * c_ * h_ * w_;
+        ready_ = false;
+        if (op_ == NITI_OP_DSP_MAXPOOL_INT8 || op_ == NITI_OP_DSP_MAXPOOLGRAD_INT8) {
+            k_ = common_.kernel_x, s_ = common_.stride_x, p_ = common_.pad_x;
+            if (common_.kernel_y != k_ || common_.stride_y != s_ || common_.pad_y != p_ || k_ < 1 || s_ < 1 || p_ < 0)
+                return NITI_NOT_SUPPORT;
+            oh_ = (h_ + 2 * p_ - std::min(k_, h_)) / s_ + 1;
+            ow_ = (w_ + 2 * p_ - std::min(k_, w_)) / s_ + 1;
+            const niti_tensor& y = op_ == NITI_OP_DSP_MAXPOOL_INT8 ? out[0] : in[1];
+            if (y.dims[0] != n_ || y.dims[1] != c_ || y.dims[2] != oh_ || y.dims[3] != ow_) return NITI_COMPUTE_SIZE_ERROR;
+            if (op_ == NITI_OP_DSP_MAXPOOLGRAD_INT8) {
+                for (int k = 0; k < 4; ++k)
+                    if (in[2].dims[k] != y.dims[k] || out[0].dims[k] != x.dims[k]) return NITI_COMPUTE_SIZE_ERROR;
+            }
+            cp_ = (c_ + 15) / 16 * 16;
+            ws_.release();
+            const size_t big = (size_t)n_ * h_ * w_ * cp_, small = (size_t)n_ * oh_ * ow_ * cp_;
+            x16_ = (int8_t*)ws_.alloc(big);
+            y16_ = (int8_t*)ws_.alloc(small);
+            if (op_ == NITI_OP_DSP_MAXPOOLGRAD_INT8) {
+                dy16_ = (int8_t*)ws_.alloc(small);
+                dx16_ = (int8_t*)ws_.alloc(big);
+                if (!dy16_ || !dx16_) return NITI_OUT_OF_MEMORY;
+            }
+            if (!x16_ || !y16_) return NITI_OUT_OF_MEMORY;
+        } else {
+            for (int k = 0; k < 4; ++k)
+                if (out[0].dims[k] != x.dims[k] || (need == 2 && in[1].dims[k] != x.dims[k])) return NITI_COMPUTE_SIZE_ERROR;
+        }
+        ready_ = true;
+        return NITI_NO_ERROR;
+    }
+    int onExecute(const niti_tensor* in, int nin, const niti_tensor* out, int nout, hipStream_t st) override {
+        if (!ready_) return NITI_NO_EXECUTION;
+        const int8_t* x = (const int8_t*)in[0].data;
+        int8_t* o = (int8_t*)out[0].data;
+        switch (op_) {
+            case NITI_OP_DSP_RELU_INT8: NITI_TRY(launch_map(elems_, ReluMap{x, o}, st)); break;
+            case NITI_OP_DSP_NOP_INT8: NITI_TRY(launch_map(elems_, CopyMap{x, o}, st)); break;
+            case NITI_OP_DSP_RELUGRAD_INT8: NITI_TRY(relu_grad_nhwc16(x, (const int8_t*)in[1].data, elems_, o, st)); break;
+            case NITI_OP_DSP_MAXPOOL_INT8: {
+                const int64_t rows = (int64_t)n_ * oh_ * ow_;
+                NITI_TRY(launch_map((int64_t)n_ * h_ * w_ * cp_, NhwcToNhwc16{x, c_, cp_, x16_}, st));
+                NITI_TRY(maxpool_nhwc16(x16_, n_, h_, w_, cp_, k_, s_, p_, y16_, oh_, ow_, st));
+                NITI_TRY(launch_map(rows * c_, UnpadRows{y16_, c_, cp_, o}, st));
+                if (nin > 1 && nout > 1 && in[1].data && out[1].data)
+                    NITI_TRY(hipMemcpyAsync(out[1].data, in[1].data, 1, hipMemcpyDeviceToDevice, st));
+                break;
+            }
+            default: {  // NITI_OP_DSP_MAXPOOLGRAD_INT8
+                const int64_t small = (int64_t)n_ * oh_ * ow_ * cp_, rows = (int64_t)n_ * h_ * w_;
+                NITI_TRY(launch_map(rows * cp_, NhwcToNhwc16{x, c_, cp_, x16_}, st));
+                NITI_TRY(launch_map(small, NhwcToNhwc16{(const int8_t*)in[1].data, c_, cp_, y16_}, st));
+                NITI_TRY(launch_map(small, NhwcToNhwc16{(const int8_t*)in[2].data, c_, cp_, dy16_}, st));
+                NITI_TRY(maxpool_relu_grad_nhwc16(x16_, y16_, dy16_, n_, h_, w_, cp_, k_, s_, p_, oh_, ow_, 0, dx16_, st));
+                NITI_TRY(launch_map(rows * c_, UnpadRows{dx16_, c_, cp_, o}, st));
+                break;
+            }
+        }
+        return NITI_NO_ERROR;
+    }
+
+   private:
+    int op_;
+    niti_conv2d_common common_;
+    bool ready_ = false;
+    int n_ = 0, c_ = 0, h_ = 0, w_ = 0, k_ = 0, s_ = 0, p_ = 0, oh_ = 0, ow_ = 0, cp_ = 0;
+    int64_t elems_ = 0;
+    int8_t *x16_ = nullptr, *y16_ = nullptr, *dy16_ = nullptr, *dx16_ = nullptr;
+};
+
 // ------------------------------------------------------------------ tensor format conversion
 // CPUTensorConverter::convert (CPUTensorConvert.cpp:98-210) for int8 tensors between NCHW,
 // NHWC and MNN's CPU NC4HW4 ([ceil(C/4)][N][H][W][4], pad lanes zero), SURVEY.md §8(f)-3.
@@ -743,7 +846,9 @@ Execution* create_execution(int op_type, const niti_conv2d_common* c, int* err) 
     dflt.kernel_x = dflt.kernel_y = dflt.stride_x = dflt.stride_y = dflt.dilate_x = dflt.dilate_y = 1;
     dflt.group = 1;
     const niti_conv2d_common& cc = c ? *c : dflt;
-    if (op_type != NITI_OP_MATMUL_INT8 && c == nullptr) {
+    const bool no_params = op_type == NITI_OP_MATMUL_INT8 || op_type == NITI_OP_DSP_RELU_INT8 ||
+                           op_type == NITI_OP_DSP_RELUGRAD_INT8 || op_type == NITI_OP_DSP_NOP_INT8;
+    if (!no_params && c == nullptr) {
         *err = NITI_INVALID_VALUE;
         return nullptr;
     }
@@ -760,6 +865,11 @@ Execution* create_execution(int op_type, const niti_conv2d_common* c, int* err) 
         case NITI_OP_DSP_CONV_INT8:
         case NITI_OP_DSP_DECONV_INT8: return new DspConvExecution(cc);
         case NITI_OP_DSP_PARALLEL_GRADIENTCONV_INT8: return new DspMatmulGradientExecution(cc, true);
+        case NITI_OP_DSP_RELU_INT8:
+        case NITI_OP_DSP_RELUGRAD_INT8:
+        case NITI_OP_DSP_NOP_INT8:
+        case NITI_OP_DSP_MAXPOOL_INT8:
+        case NITI_OP_DSP_MAXPOOLGRAD_INT8: return new DspElementwiseExecution(op_type, cc);
         case NITI_OP_DSP_GRADIENT_SPLITBATCHCONV_INT8:
         case NITI_OP_DSP_TRANSPOSEGRADIENT_CONV_INT8: return new DspTransposeGradientExecution(cc);
         default: *err = NITI_NOT_SUPPORT; return nullptr;

@@ -22,6 +22,11 @@ OP_DECONV_INT8 = 701
 OP_MATMUL_INT8 = 713
 OP_GRADIENT_CONV_INT8 = 715
 OP_DSP_CONV_INT8 = 800
+OP_DSP_RELU_INT8 = 801
+OP_DSP_MAXPOOL_INT8 = 802
+OP_DSP_RELUGRAD_INT8 = 805
+OP_DSP_MAXPOOLGRAD_INT8 = 807
+OP_DSP_NOP_INT8 = 817
 OP_DSP_DECONV_INT8 = 811
 OP_DSP_MATMUL_GRADIENT_INT8 = 818
 OP_DSP_PARALLEL_GRADIENTCONV_INT8 = 820

@@ -45,12 +45,13 @@ def test_create_execution_validation(L):
     c.group = 2
     assert lib.niti_create_execution(700, C.byref(c), C.byref(h)) == 2      # grouped conv: NOT_SUPPORT
     c.group = 1
-    for op in (700, 701, 715, 800, 811, 818, 820, 821, 822):
+    for op in (700, 701, 715, 800, 802, 807, 811, 818, 820, 821, 822):
         assert lib.niti_create_execution(op, C.byref(c), C.byref(h)) == 0
         assert lib.niti_execution_workspace_bytes(h) == 0
         lib.niti_destroy_execution(h)
-    assert lib.niti_create_execution(713, None, C.byref(h)) == 0
-    lib.niti_destroy_execution(h)
+    for op in (713, 801, 805, 817):  # no parameters: common may be NULL
+        assert lib.niti_create_execution(op, None, C.byref(h)) == 0
+        lib.niti_destroy_execution(h)
 
 
 def test_geometry(L):

@@ -442,6 +442,56 @@ def test_exec_dsp_transpose_gradient_rejects_stride2(T, ops):
     assert ex.resize(ins, outs) == 2  # NOT_SUPPORT: the graph dilates dy (LeftPoolGrad) for stride 2
 
 
+@pytest.mark.parametrize("op", [801, 817, 805])
+@pytest.mark.parametrize("shape", [(2, 5, 3, 7), (4, 64, 8, 8)])
+def test_exec_dsp_relu_family(T, ops, oracle, op, shape):
+    """NITI_DSP_RELU / NOP / RELUGRAD slots on NHWC tensors (CPU numerics)."""
+    n, c, h, w = shape
+    rng = np.random.default_rng(210)
+    x = rng.integers(-128, 128, size=(n, h, w, c), dtype=np.int8)
+    dy = rng.integers(-128, 128, size=(n, h, w, c), dtype=np.int8)
+    want = {801: oracle.relu(x), 817: x, 805: oracle.relu_grad(x, dy)}[op]
+    out = T.zeros((n, h, w, c), dtype=T.int8, device="cuda")
+    ex = ops.NITIExecution(op, None)
+    ins = [ops.tensor(dev(T, x), shape, 1)] + ([ops.tensor(dev(T, dy), shape, 1)] if op == 805 else [])
+    outs = [ops.tensor(out, shape, 1)]
+    assert ex.resize(ins, outs) == 0
+    assert ex.execute(ins, outs) == 0
+    assert np.array_equal(out.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("geo", [(2, 20, 12, 12, 2, 2, 0), (3, 5, 9, 9, 3, 2, 1), (2, 64, 5, 5, 2, 2, 0),
+                                 (1, 130, 4, 4, 2, 2, 0)])
+def test_exec_dsp_maxpool_and_grad(T, ops, oracle, geo):
+    """NITI_DSP_MAXPOOL (ascale passed through) and NITI_DSP_MAXPOOLGRAD slots, NHWC, first max wins."""
+    n, c, h, w, k, s, p = geo
+    rng = np.random.default_rng(211)
+    x = rng.integers(-8, 8, size=(n, c, h, w), dtype=np.int8)  # small range: ties exercise first-max-wins
+    y_ref = oracle.maxpool(x, k, s, p)
+    oh, ow = y_ref.shape[2], y_ref.shape[3]
+    dy = rng.integers(-128, 128, size=(n, c, oh, ow), dtype=np.int8)
+    dx_ref = oracle.maxpool_grad(x, y_ref, dy, k, s, p)
+    nhwc = lambda a: np.ascontiguousarray(a.transpose(0, 2, 3, 1))
+    common = ops.conv_common(k, stride=s, pad=p)
+    y = T.zeros((n, oh, ow, c), dtype=T.int8, device="cuda")
+    sc_out = i8s(T, 0)
+    ex = ops.NITIExecution(802, common)
+    ins = [ops.tensor(dev(T, nhwc(x)), (n, c, h, w), 1), ops.tensor(i8s(T, -5), (1, 1, 1, 1))]
+    outs = [ops.tensor(y, (n, c, oh, ow), 1), ops.tensor(sc_out, (1, 1, 1, 1))]
+    assert ex.resize(ins, outs) == 0
+    assert ex.execute(ins, outs) == 0
+    assert np.array_equal(y.cpu().numpy(), nhwc(y_ref))
+    assert int(sc_out.item()) == -5
+    dx = T.zeros((n, h, w, c), dtype=T.int8, device="cuda")
+    eg = ops.NITIExecution(807, common)
+    ins = [ops.tensor(dev(T, nhwc(x)), (n, c, h, w), 1), ops.tensor(y, (n, c, oh, ow), 1),
+           ops.tensor(dev(T, nhwc(dy)), (n, c, oh, ow), 1)]
+    outs = [ops.tensor(dx, (n, c, h, w), 1)]
+    assert eg.resize(ins, outs) == 0
+    assert eg.execute(ins, outs) == 0
+    assert np.array_equal(dx.cpu().numpy(), nhwc(dx_ref))
+
+
 # --------------------------------------------------------------------------- tensor formats (§8(f)-3)
 def _as_format(x_nchw, fmt, oracle):
     if fmt == 0:
