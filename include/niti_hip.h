@@ -49,11 +49,13 @@ enum niti_error_code {
 enum niti_op_type {
     NITI_OP_CONV_INT8 = 700,               /* NITI_CONV_Int8          -> NITI_Conv_Int8.cpp:162-310 */
     NITI_OP_DECONV_INT8 = 701,             /* NITI_DeCONV_Int8        -> NITI_DeConv_Int8.cpp:187-332 */
+    NITI_OP_LOSS_GRAD_INT8 = 711,          /* NITI_LOSS_Grad_Int8     -> NITI_CPULossGrad_Int8.cpp:81-200 */
     NITI_OP_MATMUL_INT8 = 713,             /* NITI_MatMul_Int8        -> NITI_Matmul_Int8.cpp:140-231 */
     NITI_OP_GRADIENT_CONV_INT8 = 715,      /* NITI_GradientCONV_Int8  -> NITI_GradientConv_Int8.cpp:165-298 */
     NITI_OP_DSP_CONV_INT8 = 800,           /* NITI_DSP_CONV_Int8      -> NITI_DSPConv_Int8.cpp:160-455 */
     NITI_OP_DSP_RELU_INT8 = 801,           /* NITI_DSP_RELU_Int8      -> NITI_DSPRelu_Int8.cpp */
     NITI_OP_DSP_MAXPOOL_INT8 = 802,        /* NITI_DSP_MAXPOOL_Int8   -> NITI_DSPMaxpool_Int8.cpp */
+    NITI_OP_DSP_LOSSGRAD_INT8 = 804,       /* NITI_DSP_LOSSGRAD_Int8  -> NITI_DSPLossGrad_Int8.cpp */
     NITI_OP_DSP_RELUGRAD_INT8 = 805,       /* NITI_DSP_RELUGRAD_Int8  -> NITI_DSPReluGrad_Int8.cpp */
     NITI_OP_DSP_MAXPOOLGRAD_INT8 = 807,    /* NITI_DSP_MAXPOOLGRAD_Int8 -> NITI_DSPMaxPoolGrad_Int8.cpp */
     NITI_OP_DSP_DECONV_INT8 = 811,         /* NITI_DSP_DECONV_Int8    -> NITI_DSPDeConv_Int8.cpp */
@@ -122,6 +124,9 @@ int niti_create_execution(int op_type, const niti_conv2d_common* common, niti_ex
  *  NITI_OP_DSP_MAXPOOL_INT8   in {x NHWC, ascale int8[1]} out{y NHWC, ascale int8[1]}; the pool's
  *                             kernel / stride / pad in the common's kernel_x/y, stride_x/y, pad_x/y
  *  NITI_OP_DSP_MAXPOOLGRAD_INT8 in {x, y, dy} NHWC out{dx NHWC}
+ *  NITI_OP_LOSS_GRAD_INT8, NITI_OP_DSP_LOSSGRAD_INT8 (common may be NULL)
+ *                             in {logits int8 [batch, classes], ascale int8[1], target int32 one-hot
+ *                                 [batch, tc], dy (unused)} out{grad int8 [batch, classes]}; classes <= 2048
  *  NITI_OP_DSP_TRANSPOSEGRADIENT_CONV_INT8, NITI_OP_DSP_GRADIENT_SPLITBATCHCONV_INT8 (stride 1; the graph
  *                             dilates dy for stride 2)
  *                             in {x^T NHWC [Ci,N,H,W], dy NHWC [N,Co,OH,OW], 0, 0}

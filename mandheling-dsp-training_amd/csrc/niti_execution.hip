@@ -783,6 +783,52 @@ class DspElementwiseExecution : public Execution {
     int8_t *x16_ = nullptr, *y16_ = nullptr, *dy16_ = nullptr, *dx16_ = nullptr;
 };
 
+// ------------------------------------------------------------------ loss gradient slots
+// NITI_LOSS_Grad_Int8 (711, NITI_CPULossGrad_Int8.cpp:81-200) and NITI_DSP_LOSSGRAD_Int8 (804,
+// grad/NITI_SoftmaxGrad.cpp:41-66 builds either from the same inputs): {logits int8 [batch][classes],
+// ascale int8[1], target int32 one-hot [batch][tc], dy (unused)} -> {grad int8 [batch][classes]}.
+// The target row's first 1 is the class (:169-178); a row without one counts as class 0.
+struct OnehotToIndex {
+    const int32_t* t;
+    int tc;
+    int32_t* label;
+    __device__ void operator()(int64_t i) const {
+        int32_t k = 0;
+        for (int j = tc - 1; j >= 0; --j)
+            if (t[i * tc + j] == 1) k = j;
+        label[i] = k;
+    }
+};
+
+class LossGradExecution : public Execution {
+   public:
+    int onResize(const niti_tensor* in, int nin, const niti_tensor* out, int nout) override {
+        if (nin < 3 || nout < 1) return NITI_INVALID_VALUE;
+        const niti_tensor &x = in[0], &t = in[2], &o = out[0];
+        if (x.format == NITI_FORMAT_NC4HW4 || o.format == NITI_FORMAT_NC4HW4) return NITI_NOT_SUPPORT;
+        batch_ = x.dims[0];
+        classes_ = x.dims[1] * x.dims[2] * x.dims[3];
+        tc_ = t.dims[1] * t.dims[2] * t.dims[3];
+        if (batch_ <= 0 || classes_ <= 0 || classes_ > 2048 || t.dims[0] != batch_ || tc_ <= 0)
+            return classes_ > 2048 ? NITI_NOT_SUPPORT : NITI_COMPUTE_SIZE_ERROR;
+        if (o.dims[0] != batch_ || o.dims[1] * o.dims[2] * o.dims[3] != classes_) return NITI_COMPUTE_SIZE_ERROR;
+        ws_.release();
+        label_ = (int32_t*)ws_.alloc((size_t)batch_ * 4);
+        return label_ ? NITI_NO_ERROR : NITI_OUT_OF_MEMORY;
+    }
+    int onExecute(const niti_tensor* in, int nin, const niti_tensor* out, int nout, hipStream_t st) override {
+        if (!label_) return NITI_NO_EXECUTION;
+        NITI_TRY(launch_map(batch_, OnehotToIndex{(const int32_t*)in[2].data, tc_, label_}, st));
+        NITI_TRY(loss_grad((const int8_t*)in[0].data, batch_, classes_, classes_, (const int8_t*)in[1].data, label_,
+                           (int8_t*)out[0].data, st));
+        return NITI_NO_ERROR;
+    }
+
+   private:
+    int batch_ = 0, classes_ = 0, tc_ = 0;
+    int32_t* label_ = nullptr;
+};
+
 // ------------------------------------------------------------------ tensor format conversion
 // CPUTensorConverter::convert (CPUTensorConvert.cpp:98-210) for int8 tensors between NCHW,
 // NHWC and MNN's CPU NC4HW4 ([ceil(C/4)][N][H][W][4], pad lanes zero), SURVEY.md §8(f)-3.
@@ -847,7 +893,8 @@ Execution* create_execution(int op_type, const niti_conv2d_common* c, int* err) 
     dflt.group = 1;
     const niti_conv2d_common& cc = c ? *c : dflt;
     const bool no_params = op_type == NITI_OP_MATMUL_INT8 || op_type == NITI_OP_DSP_RELU_INT8 ||
-                           op_type == NITI_OP_DSP_RELUGRAD_INT8 || op_type == NITI_OP_DSP_NOP_INT8;
+                           op_type == NITI_OP_DSP_RELUGRAD_INT8 || op_type == NITI_OP_DSP_NOP_INT8 ||
+                           op_type == NITI_OP_LOSS_GRAD_INT8 || op_type == NITI_OP_DSP_LOSSGRAD_INT8;
     if (!no_params && c == nullptr) {
         *err = NITI_INVALID_VALUE;
         return nullptr;
@@ -865,6 +912,8 @@ Execution* create_execution(int op_type, const niti_conv2d_common* c, int* err) 
         case NITI_OP_DSP_CONV_INT8:
         case NITI_OP_DSP_DECONV_INT8: return new DspConvExecution(cc);
         case NITI_OP_DSP_PARALLEL_GRADIENTCONV_INT8: return new DspMatmulGradientExecution(cc, true);
+        case NITI_OP_LOSS_GRAD_INT8:
+        case NITI_OP_DSP_LOSSGRAD_INT8: return new LossGradExecution();
         case NITI_OP_DSP_RELU_INT8:
         case NITI_OP_DSP_RELUGRAD_INT8:
         case NITI_OP_DSP_NOP_INT8:

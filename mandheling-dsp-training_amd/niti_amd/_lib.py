@@ -19,11 +19,13 @@ ERROR_NAMES = {0: "NO_ERROR", 1: "OUT_OF_MEMORY", 2: "NOT_SUPPORT", 3: "COMPUTE_
 
 OP_CONV_INT8 = 700
 OP_DECONV_INT8 = 701
+OP_LOSS_GRAD_INT8 = 711
 OP_MATMUL_INT8 = 713
 OP_GRADIENT_CONV_INT8 = 715
 OP_DSP_CONV_INT8 = 800
 OP_DSP_RELU_INT8 = 801
 OP_DSP_MAXPOOL_INT8 = 802
+OP_DSP_LOSSGRAD_INT8 = 804
 OP_DSP_RELUGRAD_INT8 = 805
 OP_DSP_MAXPOOLGRAD_INT8 = 807
 OP_DSP_NOP_INT8 = 817

@@ -49,7 +49,7 @@ def test_create_execution_validation(L):
         assert lib.niti_create_execution(op, C.byref(c), C.byref(h)) == 0
         assert lib.niti_execution_workspace_bytes(h) == 0
         lib.niti_destroy_execution(h)
-    for op in (713, 801, 805, 817):  # no parameters: common may be NULL
+    for op in (711, 713, 801, 804, 805, 817):  # no parameters: common may be NULL
         assert lib.niti_create_execution(op, None, C.byref(h)) == 0
         lib.niti_destroy_execution(h)
 

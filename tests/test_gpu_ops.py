@@ -492,6 +492,26 @@ def test_exec_dsp_maxpool_and_grad(T, ops, oracle, geo):
     assert np.array_equal(dx.cpu().numpy(), nhwc(dx_ref))
 
 
+@pytest.mark.parametrize("op", [711, 804])
+@pytest.mark.parametrize("batch,classes,ascale", [(7, 10, -7), (5, 10, -3), (3, 1000, -5), (2, 17, 0)])
+def test_exec_loss_grad(T, ops, oracle, op, batch, classes, ascale):
+    """NITI_LOSS_Grad / NITI_DSP_LOSSGRAD slots: logits, ascale, one-hot int32 target, dy -> grad."""
+    rng = np.random.default_rng(212)
+    logits = rng.integers(-128, 128, size=(batch, classes), dtype=np.int8)
+    labels = rng.integers(0, classes, size=batch)
+    onehot = np.zeros((batch, classes), np.int32)
+    onehot[np.arange(batch), labels] = 1
+    want = oracle.loss_grad(logits, ascale, onehot)
+    out = T.zeros((batch, classes), dtype=T.int8, device="cuda")
+    ex = ops.NITIExecution(op, None)
+    ins = [ops.tensor(dev(T, logits), (batch, classes)), ops.tensor(i8s(T, ascale), (1, 1, 1, 1)),
+           ops.tensor(dev(T, onehot), (batch, classes)), ops.tensor(dev(T, logits), (batch, classes))]
+    outs = [ops.tensor(out, (batch, classes))]
+    assert ex.resize(ins, outs) == 0
+    assert ex.execute(ins, outs) == 0
+    assert np.array_equal(out.cpu().numpy(), want)
+
+
 # --------------------------------------------------------------------------- tensor formats (§8(f)-3)
 def _as_format(x_nchw, fmt, oracle):
     if fmt == 0:
