@@ -55,10 +55,16 @@ enum niti_op_type {
     NITI_OP_DSP_CONV_INT8 = 800,           /* NITI_DSP_CONV_Int8      -> NITI_DSPConv_Int8.cpp:160-455 */
     NITI_OP_DSP_RELU_INT8 = 801,           /* NITI_DSP_RELU_Int8      -> NITI_DSPRelu_Int8.cpp */
     NITI_OP_DSP_MAXPOOL_INT8 = 802,        /* NITI_DSP_MAXPOOL_Int8   -> NITI_DSPMaxpool_Int8.cpp */
+    NITI_OP_DSP_RESHAPE_INT8 = 803,        /* NITI_DSP_RESHAPE_Int8   -> NITI_DSPReshape_Int8.cpp */
     NITI_OP_DSP_LOSSGRAD_INT8 = 804,       /* NITI_DSP_LOSSGRAD_Int8  -> NITI_DSPLossGrad_Int8.cpp */
     NITI_OP_DSP_RELUGRAD_INT8 = 805,       /* NITI_DSP_RELUGRAD_Int8  -> NITI_DSPReluGrad_Int8.cpp */
     NITI_OP_DSP_MAXPOOLGRAD_INT8 = 807,    /* NITI_DSP_MAXPOOLGRAD_Int8 -> NITI_DSPMaxPoolGrad_Int8.cpp */
+    NITI_OP_DSP_TRANSPOSE_INT8 = 808,      /* NITI_DSP_TRANSPOSE_Int8 -> NITI_DSPTranspose_Int8.cpp */
+    NITI_OP_DSP_WEIGHTROTATE180_INT8 = 809, /* NITI_DSP_WEIGHTROTATE180_REF_Int8 -> NITI_DSPWeightRotateRef_Int8.cpp */
     NITI_OP_DSP_DECONV_INT8 = 811,         /* NITI_DSP_DECONV_Int8    -> NITI_DSPDeConv_Int8.cpp */
+    NITI_OP_DSP_RESHAPEGRAD_INT8 = 813,    /* NITI_DSP_RESHAPEGrad_Int8 -> NITI_DSPReshapeGrad_Int8.cpp */
+    NITI_OP_DSP_LEFTPOOLGRAD_DECONV_INT8 = 814,   /* -> NITI_DSPLeftPoolGrad_Int8.cpp */
+    NITI_OP_DSP_LEFTPOOLGRAD_GRADIENT_INT8 = 815, /* -> NITI_DSPLeftPoolGrad_Int8.cpp */
     NITI_OP_DSP_NOP_INT8 = 817,            /* NITI_DSP_NOP_Int8       -> NITI_DSPNop_Int8.cpp */
     NITI_OP_DSP_MATMUL_GRADIENT_INT8 = 818, /* NITI_DSP_MATMUL_GRADIENT_Int8 -> NITI_DSPMatmulGradientConv_Int8.cpp:105-553 */
     NITI_OP_DSP_PARALLEL_GRADIENTCONV_INT8 = 820,   /* -> NITI_DSPParallelGradientConv_Int8.cpp (818's tensors) */
@@ -124,6 +130,11 @@ int niti_create_execution(int op_type, const niti_conv2d_common* common, niti_ex
  *  NITI_OP_DSP_MAXPOOL_INT8   in {x NHWC, ascale int8[1]} out{y NHWC, ascale int8[1]}; the pool's
  *                             kernel / stride / pad in the common's kernel_x/y, stride_x/y, pad_x/y
  *  NITI_OP_DSP_MAXPOOLGRAD_INT8 in {x, y, dy} NHWC out{dx NHWC}
+ *  NITI_OP_DSP_TRANSPOSE_INT8 in {x, perm int32[4] (device)} out{x permuted}; WEIGHTROTATE180 in {w}
+ *                             out{w, raw axes 2, 3 reversed}; RESHAPE / RESHAPEGRAD in {x} out{same bytes};
+ *                             all on the stored axis order ([N][H][W][C] for NHWC), common may be NULL
+ *  NITI_OP_DSP_LEFTPOOLGRAD_DECONV_INT8 / _GRADIENT_INT8 in {dy NHWC} out{NHWC, dy[i][j] at
+ *                             (stride_y*i, stride_x*j), zeros elsewhere}; stride in the common
  *  NITI_OP_LOSS_GRAD_INT8, NITI_OP_DSP_LOSSGRAD_INT8 (common may be NULL)
  *                             in {logits int8 [batch, classes], ascale int8[1], target int32 one-hot
  *                                 [batch, tc], dy (unused)} out{grad int8 [batch, classes]}; classes <= 2048

@@ -829,6 +829,148 @@ class LossGradExecution : public Execution {
     int32_t* label_ = nullptr;
 };
 
+// ------------------------------------------------------------------ NITI_DSP layout slots
+// The DSP graph's data-movement ops, on the tensors' stored (raw) axis order -- [N][H][W][C] for
+// NHWC, [N][C][H][W] for NCHW -- as MNN's NHWC kernels index them:
+//   NITI_DSP_TRANSPOSE_Int8 (808)   {x, perm int32[4]} -> x permuted (NeuralNetWorkOp.cpp:2170-2182)
+//   NITI_DSP_WEIGHTROTATE180_REF_Int8 (809) {w} -> w with raw axes 2 and 3 reversed (the graph
+//                                    applies it to transpose(w, {2,3,0,1}): the kernel window)
+//   NITI_DSP_LEFTPOOLGRAD_DECONV / _GRADIENT_Int8 (814 / 815) {dy NHWC} -> NHWC of the output's
+//                                    size with dy[i][j] at (s*i, s*j) and zeros elsewhere
+//                                    (NeuralNetWorkOp.cpp:2202-2230; stride in the common)
+//   NITI_DSP_RESHAPE_Int8 / RESHAPEGrad (803 / 813) {x} -> the same bytes under the output's dims
+struct Raw4 {
+    int d[4];
+};
+static Raw4 raw_dims(const niti_tensor& t) {
+    if (t.format == NITI_FORMAT_NHWC) return Raw4{{t.dims[0], t.dims[2], t.dims[3], t.dims[1]}};
+    return Raw4{{t.dims[0], t.dims[1], t.dims[2], t.dims[3]}};
+}
+struct PermuteMap {
+    const int8_t* x;
+    int8_t* y;
+    int od[4];
+    int64_t is[4];  // input stride of output axis k
+    __device__ void operator()(int64_t i) const {
+        int64_t off = 0, r = i;
+#pragma unroll
+        for (int k = 3; k >= 0; --k) {
+            off += (r % od[k]) * is[k];
+            r /= od[k];
+        }
+        y[i] = x[off];
+    }
+};
+struct Rotate180Map {
+    const int8_t* x;
+    int8_t* y;
+    int H, W;
+    __device__ void operator()(int64_t i) const {
+        const int j = (int)(i % W), r = (int)((i / W) % H);
+        const int64_t base = i - (int64_t)r * W - j;
+        y[i] = x[base + (int64_t)(H - 1 - r) * W + (W - 1 - j)];
+    }
+};
+struct LeftPoolGradMap {
+    const int8_t* dy;
+    int8_t* y;
+    int C, OW2, OH2, IH, IW, sy, sx;  // output OH2 x OW2, input IH x IW
+    __device__ void operator()(int64_t i) const {
+        const int c = (int)(i % C);
+        int64_t r = i / C;
+        const int ox = (int)(r % OW2);
+        r /= OW2;
+        const int oy = (int)(r % OH2);
+        const int64_t n = r / OH2;
+        int8_t v = 0;
+        if (oy % sy == 0 && ox % sx == 0 && oy / sy < IH && ox / sx < IW)
+            v = dy[((n * IH + oy / sy) * IW + ox / sx) * C + c];
+        y[i] = v;
+    }
+};
+
+class DspLayoutExecution : public Execution {
+   public:
+    DspLayoutExecution(int op, const niti_conv2d_common& c) : op_(op), common_(c) {}
+    int onResize(const niti_tensor* in, int nin, const niti_tensor* out, int nout) override {
+        if (nin < (op_ == NITI_OP_DSP_TRANSPOSE_INT8 ? 2 : 1) || nout < 1) return NITI_INVALID_VALUE;
+        ready_ = false;
+        const Raw4 xi = raw_dims(in[0]), yo = raw_dims(out[0]);
+        n_ = 1;
+        for (int k = 0; k < 4; ++k) n_ *= yo.d[k];
+        int64_t nx = 1;
+        for (int k = 0; k < 4; ++k) nx *= xi.d[k];
+        switch (op_) {
+            case NITI_OP_DSP_TRANSPOSE_INT8: {
+                int perm[4];
+                if (hipMemcpy(perm, in[1].data, sizeof(perm), hipMemcpyDeviceToHost) != hipSuccess) return NITI_INVALID_VALUE;
+                int64_t st[4];
+                st[3] = 1;
+                for (int k = 2; k >= 0; --k) st[k] = st[k + 1] * xi.d[k + 1];
+                int seen = 0;
+                for (int k = 0; k < 4; ++k) {
+                    if (perm[k] < 0 || perm[k] > 3 || (seen >> perm[k]) & 1) return NITI_INVALID_VALUE;
+                    seen |= 1 << perm[k];
+                    if (yo.d[k] != xi.d[perm[k]]) return NITI_COMPUTE_SIZE_ERROR;
+                    pm_.od[k] = yo.d[k];
+                    pm_.is[k] = st[perm[k]];
+                }
+                break;
+            }
+            case NITI_OP_DSP_WEIGHTROTATE180_INT8:
+                for (int k = 0; k < 4; ++k)
+                    if (xi.d[k] != yo.d[k]) return NITI_COMPUTE_SIZE_ERROR;
+                rh_ = xi.d[2], rw_ = xi.d[3];
+                break;
+            case NITI_OP_DSP_LEFTPOOLGRAD_DECONV_INT8:
+            case NITI_OP_DSP_LEFTPOOLGRAD_GRADIENT_INT8:
+                if (in[0].format != NITI_FORMAT_NHWC || out[0].format != NITI_FORMAT_NHWC) return NITI_NOT_SUPPORT;
+                if (common_.stride_x < 1 || common_.stride_y < 1) return NITI_INVALID_VALUE;
+                if (xi.d[0] != yo.d[0] || xi.d[3] != yo.d[3]) return NITI_COMPUTE_SIZE_ERROR;
+                lp_ = LeftPoolGradMap{nullptr, nullptr, xi.d[3], yo.d[2], yo.d[1], xi.d[1], xi.d[2], common_.stride_y,
+                                      common_.stride_x};
+                break;
+            default:  // reshape: same bytes
+                if (nx != n_) return NITI_COMPUTE_SIZE_ERROR;
+                break;
+        }
+        ready_ = true;
+        return NITI_NO_ERROR;
+    }
+    int onExecute(const niti_tensor* in, int nin, const niti_tensor* out, int nout, hipStream_t st) override {
+        if (!ready_) return NITI_NO_EXECUTION;
+        const int8_t* x = (const int8_t*)in[0].data;
+        int8_t* y = (int8_t*)out[0].data;
+        switch (op_) {
+            case NITI_OP_DSP_TRANSPOSE_INT8: {
+                PermuteMap m = pm_;
+                m.x = x, m.y = y;
+                NITI_TRY(launch_map(n_, m, st));
+                break;
+            }
+            case NITI_OP_DSP_WEIGHTROTATE180_INT8: NITI_TRY(launch_map(n_, Rotate180Map{x, y, rh_, rw_}, st)); break;
+            case NITI_OP_DSP_LEFTPOOLGRAD_DECONV_INT8:
+            case NITI_OP_DSP_LEFTPOOLGRAD_GRADIENT_INT8: {
+                LeftPoolGradMap m = lp_;
+                m.dy = x, m.y = y;
+                NITI_TRY(launch_map(n_, m, st));
+                break;
+            }
+            default: NITI_TRY(launch_map(n_, CopyMap{x, y}, st)); break;
+        }
+        return NITI_NO_ERROR;
+    }
+
+   private:
+    int op_;
+    niti_conv2d_common common_;
+    bool ready_ = false;
+    int64_t n_ = 0;
+    int rh_ = 0, rw_ = 0;
+    PermuteMap pm_{};
+    LeftPoolGradMap lp_{};
+};
+
 // ------------------------------------------------------------------ tensor format conversion
 // CPUTensorConverter::convert (CPUTensorConvert.cpp:98-210) for int8 tensors between NCHW,
 // NHWC and MNN's CPU NC4HW4 ([ceil(C/4)][N][H][W][4], pad lanes zero), SURVEY.md §8(f)-3.
@@ -894,7 +1036,9 @@ Execution* create_execution(int op_type, const niti_conv2d_common* c, int* err) 
     const niti_conv2d_common& cc = c ? *c : dflt;
     const bool no_params = op_type == NITI_OP_MATMUL_INT8 || op_type == NITI_OP_DSP_RELU_INT8 ||
                            op_type == NITI_OP_DSP_RELUGRAD_INT8 || op_type == NITI_OP_DSP_NOP_INT8 ||
-                           op_type == NITI_OP_LOSS_GRAD_INT8 || op_type == NITI_OP_DSP_LOSSGRAD_INT8;
+                           op_type == NITI_OP_LOSS_GRAD_INT8 || op_type == NITI_OP_DSP_LOSSGRAD_INT8 ||
+                           op_type == NITI_OP_DSP_TRANSPOSE_INT8 || op_type == NITI_OP_DSP_WEIGHTROTATE180_INT8 ||
+                           op_type == NITI_OP_DSP_RESHAPE_INT8 || op_type == NITI_OP_DSP_RESHAPEGRAD_INT8;
     if (!no_params && c == nullptr) {
         *err = NITI_INVALID_VALUE;
         return nullptr;
@@ -914,6 +1058,12 @@ Execution* create_execution(int op_type, const niti_conv2d_common* c, int* err) 
         case NITI_OP_DSP_PARALLEL_GRADIENTCONV_INT8: return new DspMatmulGradientExecution(cc, true);
         case NITI_OP_LOSS_GRAD_INT8:
         case NITI_OP_DSP_LOSSGRAD_INT8: return new LossGradExecution();
+        case NITI_OP_DSP_TRANSPOSE_INT8:
+        case NITI_OP_DSP_WEIGHTROTATE180_INT8:
+        case NITI_OP_DSP_LEFTPOOLGRAD_DECONV_INT8:
+        case NITI_OP_DSP_LEFTPOOLGRAD_GRADIENT_INT8:
+        case NITI_OP_DSP_RESHAPE_INT8:
+        case NITI_OP_DSP_RESHAPEGRAD_INT8: return new DspLayoutExecution(op_type, cc);
         case NITI_OP_DSP_RELU_INT8:
         case NITI_OP_DSP_RELUGRAD_INT8:
         case NITI_OP_DSP_NOP_INT8:

@@ -25,9 +25,15 @@ OP_GRADIENT_CONV_INT8 = 715
 OP_DSP_CONV_INT8 = 800
 OP_DSP_RELU_INT8 = 801
 OP_DSP_MAXPOOL_INT8 = 802
+OP_DSP_RESHAPE_INT8 = 803
 OP_DSP_LOSSGRAD_INT8 = 804
 OP_DSP_RELUGRAD_INT8 = 805
 OP_DSP_MAXPOOLGRAD_INT8 = 807
+OP_DSP_TRANSPOSE_INT8 = 808
+OP_DSP_WEIGHTROTATE180_INT8 = 809
+OP_DSP_RESHAPEGRAD_INT8 = 813
+OP_DSP_LEFTPOOLGRAD_DECONV_INT8 = 814
+OP_DSP_LEFTPOOLGRAD_GRADIENT_INT8 = 815
 OP_DSP_NOP_INT8 = 817
 OP_DSP_DECONV_INT8 = 811
 OP_DSP_MATMUL_GRADIENT_INT8 = 818

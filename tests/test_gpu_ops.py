@@ -512,6 +512,73 @@ def test_exec_loss_grad(T, ops, oracle, op, batch, classes, ascale):
     assert np.array_equal(out.cpu().numpy(), want)
 
 
+def _run_exec(ops, op, common, ins, outs):
+    ex = ops.NITIExecution(op, common)
+    assert ex.resize(ins, outs) == 0
+    assert ex.execute(ins, outs) == 0
+
+
+def _nhwc_dims(raw):  # stored [N][H][W][C] -> logical {N, C, H, W}
+    return (raw[0], raw[3], raw[1], raw[2])
+
+
+@pytest.mark.parametrize("perm", [(3, 1, 2, 0), (2, 3, 0, 1), (2, 3, 1, 0), (0, 1, 2, 3)])
+def test_exec_dsp_transpose(T, ops, perm):
+    """NITI_DSP_TRANSPOSE on the stored axis order (the graph's transpose(x, {3,1,2,0}) etc.)."""
+    rng = np.random.default_rng(213)
+    x = rng.integers(-128, 128, size=(3, 5, 4, 7), dtype=np.int8)  # stored NHWC [N][H][W][C]
+    want = np.ascontiguousarray(x.transpose(perm))
+    out = T.zeros(want.shape, dtype=T.int8, device="cuda")
+    p = T.tensor(perm, dtype=T.int32, device="cuda")
+    _run_exec(ops, 808, None, [ops.tensor(dev(T, x), _nhwc_dims(x.shape), 1), ops.tensor(p, (4, 1, 1, 1))],
+              [ops.tensor(out, _nhwc_dims(want.shape), 1)])
+    assert np.array_equal(out.cpu().numpy(), want)
+
+
+def test_exec_dsp_deconv_weight_chain(T, ops, oracle):
+    """transpose(rot180(transpose(w, {2,3,0,1})), {2,3,1,0}) through the 808 / 809 slots equals the
+    rotated weights the deconv slot test builds on the host (grad/NITI_DSPConv_Int8_Grad.cpp:88-92)."""
+    rng = np.random.default_rng(214)
+    k, ci, co = 3, 6, 10
+    hwio = rng.integers(-128, 128, size=(k, k, ci, co), dtype=np.int8)
+    want = np.ascontiguousarray(np.flip(hwio.transpose(2, 3, 0, 1), axis=(2, 3)).transpose(2, 3, 1, 0))
+    t1 = T.zeros((ci, co, k, k), dtype=T.int8, device="cuda")
+    t2 = T.zeros((ci, co, k, k), dtype=T.int8, device="cuda")
+    t3 = T.zeros((k, k, co, ci), dtype=T.int8, device="cuda")
+    p1 = T.tensor([2, 3, 0, 1], dtype=T.int32, device="cuda")
+    p2 = T.tensor([2, 3, 1, 0], dtype=T.int32, device="cuda")
+    _run_exec(ops, 808, None, [ops.tensor(dev(T, hwio), hwio.shape, 0), ops.tensor(p1, (4, 1, 1, 1))],
+              [ops.tensor(t1, t1.shape, 0)])
+    _run_exec(ops, 809, None, [ops.tensor(t1, t1.shape, 0)], [ops.tensor(t2, t2.shape, 0)])
+    _run_exec(ops, 808, None, [ops.tensor(t2, t2.shape, 0), ops.tensor(p2, (4, 1, 1, 1))],
+              [ops.tensor(t3, t3.shape, 0)])
+    assert np.array_equal(t3.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("op", [814, 815])
+@pytest.mark.parametrize("n,c,oh,ow1", [(2, 5, 4, 7), (3, 64, 8, 16), (1, 3, 1, 2)])
+def test_exec_dsp_leftpoolgrad(T, ops, op, n, c, oh, ow1):
+    rng = np.random.default_rng(215)
+    dy = rng.integers(-128, 128, size=(n, oh, oh, c), dtype=np.int8)
+    want = np.zeros((n, ow1, ow1, c), np.int8)
+    sub = want[:, ::2, ::2, :]
+    m = min(oh, sub.shape[1])
+    sub[:, :m, :m, :] = dy[:, :m, :m, :]
+    out = T.full((n, ow1, ow1, c), 9, dtype=T.int8, device="cuda")
+    _run_exec(ops, op, ops.conv_common(1, stride=2), [ops.tensor(dev(T, dy), (n, c, oh, oh), 1)],
+              [ops.tensor(out, (n, c, ow1, ow1), 1)])
+    assert np.array_equal(out.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("op", [803, 813])
+def test_exec_dsp_reshape(T, ops, op):
+    rng = np.random.default_rng(216)
+    x = rng.integers(-128, 128, size=(4, 2, 2, 32), dtype=np.int8)
+    out = T.zeros((4, 128), dtype=T.int8, device="cuda")
+    _run_exec(ops, op, None, [ops.tensor(dev(T, x), _nhwc_dims(x.shape), 1)], [ops.tensor(out, (4, 128, 1, 1), 1)])
+    assert np.array_equal(out.cpu().numpy(), x.reshape(4, 128))
+
+
 # --------------------------------------------------------------------------- tensor formats (§8(f)-3)
 def _as_format(x_nchw, fmt, oracle):
     if fmt == 0:
