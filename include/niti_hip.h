@@ -62,11 +62,14 @@ enum niti_op_type {
     NITI_OP_DSP_TRANSPOSE_INT8 = 808,      /* NITI_DSP_TRANSPOSE_Int8 -> NITI_DSPTranspose_Int8.cpp */
     NITI_OP_DSP_WEIGHTROTATE180_INT8 = 809, /* NITI_DSP_WEIGHTROTATE180_REF_Int8 -> NITI_DSPWeightRotateRef_Int8.cpp */
     NITI_OP_DSP_DECONV_INT8 = 811,         /* NITI_DSP_DECONV_Int8    -> NITI_DSPDeConv_Int8.cpp */
+    NITI_OP_DSP_GRADIENTCONV_INT8 = 810,   /* NITI_DSP_GRADIENTCONV_Int8 -> NITI_DSPGradientConv_Int8.cpp (818's tensors) */
+    NITI_OP_DSP_PAD_INT8 = 812,            /* NITI_DSP_PAD_Int8       -> NITI_DSPPAD_Int8.cpp */
     NITI_OP_DSP_RESHAPEGRAD_INT8 = 813,    /* NITI_DSP_RESHAPEGrad_Int8 -> NITI_DSPReshapeGrad_Int8.cpp */
     NITI_OP_DSP_LEFTPOOLGRAD_DECONV_INT8 = 814,   /* -> NITI_DSPLeftPoolGrad_Int8.cpp */
     NITI_OP_DSP_LEFTPOOLGRAD_GRADIENT_INT8 = 815, /* -> NITI_DSPLeftPoolGrad_Int8.cpp */
     NITI_OP_DSP_NOP_INT8 = 817,            /* NITI_DSP_NOP_Int8       -> NITI_DSPNop_Int8.cpp */
     NITI_OP_DSP_MATMUL_GRADIENT_INT8 = 818, /* NITI_DSP_MATMUL_GRADIENT_Int8 -> NITI_DSPMatmulGradientConv_Int8.cpp:105-553 */
+    NITI_OP_DSP_MATMUL_INT8 = 819,         /* NITI_DSP_MATMUL_Int8    -> NITI_DSPMatmul_Int8.cpp (818's tensors) */
     NITI_OP_DSP_PARALLEL_GRADIENTCONV_INT8 = 820,   /* -> NITI_DSPParallelGradientConv_Int8.cpp (818's tensors) */
     NITI_OP_DSP_GRADIENT_SPLITBATCHCONV_INT8 = 821, /* -> NITI_DSPGradientSplitBatchConv_Int8.cpp (822's tensors) */
     NITI_OP_DSP_TRANSPOSEGRADIENT_CONV_INT8 = 822 /* -> NITI_DSPTransposeGradientConv_Int8.cpp:137-440 */
@@ -124,7 +127,8 @@ int niti_create_execution(int op_type, const niti_conv2d_common* common, niti_ex
  *                             in {x NHWC [N,Ci,H,W], w HWIO as dims {KH,KW,Ci,Co}, exp_in int8[1],
  *                                 wscale int8[1]}                         out{y NHWC [N,Co,OH,OW], exp_out int8[1]}
  *                             (the deconv slot gets the graph's padded/dilated dy and rotated weights)
- *  NITI_OP_DSP_PARALLEL_GRADIENTCONV_INT8 as NITI_OP_DSP_MATMUL_GRADIENT_INT8, KH x KW from dw's dims
+ *  NITI_OP_DSP_GRADIENTCONV_INT8, NITI_OP_DSP_MATMUL_INT8, NITI_OP_DSP_PARALLEL_GRADIENTCONV_INT8
+ *                             as NITI_OP_DSP_MATMUL_GRADIENT_INT8, KH x KW from dw's dims
  *  NITI_OP_DSP_RELU_INT8 / NITI_OP_DSP_NOP_INT8 in {x NHWC} out{y NHWC}; NITI_OP_DSP_RELUGRAD_INT8
  *                             in {x, dy} out{dx}; common may be NULL for these three
  *  NITI_OP_DSP_MAXPOOL_INT8   in {x NHWC, ascale int8[1]} out{y NHWC, ascale int8[1]}; the pool's
@@ -133,6 +137,7 @@ int niti_create_execution(int op_type, const niti_conv2d_common* common, niti_ex
  *  NITI_OP_DSP_TRANSPOSE_INT8 in {x, perm int32[4] (device)} out{x permuted}; WEIGHTROTATE180 in {w}
  *                             out{w, raw axes 2, 3 reversed}; RESHAPE / RESHAPEGRAD in {x} out{same bytes};
  *                             all on the stored axis order ([N][H][W][C] for NHWC), common may be NULL
+ *  NITI_OP_DSP_PAD_INT8       in {x NHWC} out{NHWC with a zero border of common.pad_x pixels}
  *  NITI_OP_DSP_LEFTPOOLGRAD_DECONV_INT8 / _GRADIENT_INT8 in {dy NHWC} out{NHWC, dy[i][j] at
  *                             (stride_y*i, stride_x*j), zeros elsewhere}; stride in the common
  *  NITI_OP_LOSS_GRAD_INT8, NITI_OP_DSP_LOSSGRAD_INT8 (common may be NULL)

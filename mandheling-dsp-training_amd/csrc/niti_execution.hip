@@ -475,7 +475,8 @@ class MatmulInt8Execution : public Execution {
 // requantises on the Hexagon (round-to-nearest, then /16 on the CPU,
 // NITI_DSPMatmulGradientConv_Int8.cpp:543-550); this backend gives the op the CPU path's
 // numerics (NITI_GradientConv_Int8: PSTO(bw-2)), SURVEY.md §8(a) A5.
-// NITI_DSP_PARALLEL_GRADIENTCONV_Int8 (820) has the same tensors; its graph rule sets the common's
+// NITI_DSP_GRADIENTCONV_Int8 (810), NITI_DSP_MATMUL_Int8 (819) and
+// NITI_DSP_PARALLEL_GRADIENTCONV_Int8 (820) have the same tensors; the graph rule sets the common's
 // kernel to dy's OH x OW (grad/NITI_DSPConv_Int8_Grad.cpp:151-153, shape rule
 // ShapeNITI_Conv_Int8.cpp:146-233), so its filter size comes from the output tensor.
 class DspMatmulGradientExecution : public Execution {
@@ -839,6 +840,8 @@ class LossGradExecution : public Execution {
 //                                    size with dy[i][j] at (s*i, s*j) and zeros elsewhere
 //                                    (NeuralNetWorkOp.cpp:2202-2230; stride in the common)
 //   NITI_DSP_RESHAPE_Int8 / RESHAPEGrad (803 / 813) {x} -> the same bytes under the output's dims
+//   NITI_DSP_PAD_Int8 (812)          {x NHWC} -> NHWC with a zero border of NITI_PAD_Int8.pad pixels
+//                                    (ShapeNITI_Pad_Int8.cpp:42-68; the pad in the common's pad_x)
 struct Raw4 {
     int d[4];
 };
@@ -889,6 +892,22 @@ struct LeftPoolGradMap {
     }
 };
 
+struct PadMap {  // NHWC zero border of p pixels
+    const int8_t* x;
+    int8_t* y;
+    int C, OW, OH, H, W, p;
+    __device__ void operator()(int64_t i) const {
+        const int c = (int)(i % C);
+        int64_t r = i / C;
+        const int ox = (int)(r % OW);
+        r /= OW;
+        const int oy = (int)(r % OH);
+        const int64_t n = r / OH;
+        const int iy = oy - p, ix = ox - p;
+        y[i] = (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W ? x[((n * H + iy) * W + ix) * C + c] : (int8_t)0;
+    }
+};
+
 class DspLayoutExecution : public Execution {
    public:
     DspLayoutExecution(int op, const niti_conv2d_common& c) : op_(op), common_(c) {}
@@ -930,6 +949,14 @@ class DspLayoutExecution : public Execution {
                 lp_ = LeftPoolGradMap{nullptr, nullptr, xi.d[3], yo.d[2], yo.d[1], xi.d[1], xi.d[2], common_.stride_y,
                                       common_.stride_x};
                 break;
+            case NITI_OP_DSP_PAD_INT8: {
+                const int p = common_.pad_x;
+                if (in[0].format != NITI_FORMAT_NHWC || out[0].format != NITI_FORMAT_NHWC || p < 0) return NITI_NOT_SUPPORT;
+                if (yo.d[0] != xi.d[0] || yo.d[3] != xi.d[3] || yo.d[1] != xi.d[1] + 2 * p || yo.d[2] != xi.d[2] + 2 * p)
+                    return NITI_COMPUTE_SIZE_ERROR;
+                pad_ = PadMap{nullptr, nullptr, xi.d[3], yo.d[2], yo.d[1], xi.d[1], xi.d[2], p};
+                break;
+            }
             default:  // reshape: same bytes
                 if (nx != n_) return NITI_COMPUTE_SIZE_ERROR;
                 break;
@@ -956,6 +983,12 @@ class DspLayoutExecution : public Execution {
                 NITI_TRY(launch_map(n_, m, st));
                 break;
             }
+            case NITI_OP_DSP_PAD_INT8: {
+                PadMap m = pad_;
+                m.x = x, m.y = y;
+                NITI_TRY(launch_map(n_, m, st));
+                break;
+            }
             default: NITI_TRY(launch_map(n_, CopyMap{x, y}, st)); break;
         }
         return NITI_NO_ERROR;
@@ -967,6 +1000,7 @@ class DspLayoutExecution : public Execution {
     bool ready_ = false;
     int64_t n_ = 0;
     int rh_ = 0, rw_ = 0;
+    PadMap pad_{};
     PermuteMap pm_{};
     LeftPoolGradMap lp_{};
 };
@@ -1055,6 +1089,8 @@ Execution* create_execution(int op_type, const niti_conv2d_common* c, int* err) 
         case NITI_OP_DSP_MATMUL_GRADIENT_INT8: return new DspMatmulGradientExecution(cc);
         case NITI_OP_DSP_CONV_INT8:
         case NITI_OP_DSP_DECONV_INT8: return new DspConvExecution(cc);
+        case NITI_OP_DSP_GRADIENTCONV_INT8:
+        case NITI_OP_DSP_MATMUL_INT8:
         case NITI_OP_DSP_PARALLEL_GRADIENTCONV_INT8: return new DspMatmulGradientExecution(cc, true);
         case NITI_OP_LOSS_GRAD_INT8:
         case NITI_OP_DSP_LOSSGRAD_INT8: return new LossGradExecution();
@@ -1062,6 +1098,7 @@ Execution* create_execution(int op_type, const niti_conv2d_common* c, int* err) 
         case NITI_OP_DSP_WEIGHTROTATE180_INT8:
         case NITI_OP_DSP_LEFTPOOLGRAD_DECONV_INT8:
         case NITI_OP_DSP_LEFTPOOLGRAD_GRADIENT_INT8:
+        case NITI_OP_DSP_PAD_INT8:
         case NITI_OP_DSP_RESHAPE_INT8:
         case NITI_OP_DSP_RESHAPEGRAD_INT8: return new DspLayoutExecution(op_type, cc);
         case NITI_OP_DSP_RELU_INT8:

@@ -316,13 +316,14 @@ def test_exec_matmul_int8(T, ops, oracle, m, o, k):
     assert np.array_equal(out.cpu().numpy().T, dwT_ref)
 
 
-@pytest.mark.parametrize("op", [818, 820])
+@pytest.mark.parametrize("op", [818, 810, 819, 820])
 @pytest.mark.parametrize("geo", [GEOMS[1], GEOMS[4], GEOMS[7]])
 def test_exec_dsp_matmul_gradient(T, ops, oracle, geo, op):
-    """818, and 820 (PARALLEL_GRADIENTCONV: its common carries dy's OH x OW as the kernel)."""
+    """818, and 810 / 819 / 820 (GRADIENTCONV, MATMUL, PARALLEL_GRADIENTCONV: their common carries dy's OH x OW
+    as the kernel; ShapeNITI_Conv_Int8.cpp:146-233 sizes all three)."""
     import niti_amd
     n, ci, h, w, co, k, s, p = geo
-    if op == 820 and s != 1:
+    if op != 818 and s != 1:
         pytest.skip("the graph emits 820 only for stride 1")
     g = oracle.geom(n, ci, h, w, co, k, stride=s, pad=p)
     rng = np.random.default_rng(205)
@@ -567,6 +568,17 @@ def test_exec_dsp_leftpoolgrad(T, ops, op, n, c, oh, ow1):
     out = T.full((n, ow1, ow1, c), 9, dtype=T.int8, device="cuda")
     _run_exec(ops, op, ops.conv_common(1, stride=2), [ops.tensor(dev(T, dy), (n, c, oh, oh), 1)],
               [ops.tensor(out, (n, c, ow1, ow1), 1)])
+    assert np.array_equal(out.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("p", [0, 1, 2])
+def test_exec_dsp_pad(T, ops, p):
+    rng = np.random.default_rng(217)
+    x = rng.integers(-128, 128, size=(2, 5, 6, 3), dtype=np.int8)
+    want = np.pad(x, ((0, 0), (p, p), (p, p), (0, 0)))
+    out = T.full(want.shape, 9, dtype=T.int8, device="cuda")
+    _run_exec(ops, 812, ops.conv_common(1, pad=p), [ops.tensor(dev(T, x), _nhwc_dims(x.shape), 1)],
+              [ops.tensor(out, _nhwc_dims(want.shape), 1)])
     assert np.array_equal(out.cpu().numpy(), want)
 
 
