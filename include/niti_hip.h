@@ -49,6 +49,10 @@ enum niti_error_code {
 enum niti_op_type {
     NITI_OP_CONV_INT8 = 700,               /* NITI_CONV_Int8          -> NITI_Conv_Int8.cpp:162-310 */
     NITI_OP_DECONV_INT8 = 701,             /* NITI_DeCONV_Int8        -> NITI_DeConv_Int8.cpp:187-332 */
+    NITI_OP_RELU_INT8 = 703,               /* NITI_Relu_Int8          -> NITI_CPURelu_Int8.cpp:28-61 */
+    NITI_OP_RELUGRAD_INT8 = 704,           /* NITI_ReluGrad_Int8      -> NITI_CPUReluGrad_Int8.cpp:28-62 */
+    NITI_OP_MAXPOOL_INT8 = 705,            /* NITI_Maxpool_Int8       -> NITI_Maxpool_Int8.cpp:24-175 */
+    NITI_OP_POOLGRAD_INT8 = 706,           /* NITI_PoolGrad_Int8      -> NITI_CPUPoolGrad_Int8.cpp:21-77 */
     NITI_OP_LOSS_GRAD_INT8 = 711,          /* NITI_LOSS_Grad_Int8     -> NITI_CPULossGrad_Int8.cpp:81-200 */
     NITI_OP_MATMUL_INT8 = 713,             /* NITI_MatMul_Int8        -> NITI_Matmul_Int8.cpp:140-231 */
     NITI_OP_GRADIENT_CONV_INT8 = 715,      /* NITI_GradientCONV_Int8  -> NITI_GradientConv_Int8.cpp:165-298 */
@@ -129,6 +133,8 @@ int niti_create_execution(int op_type, const niti_conv2d_common* common, niti_ex
  *                             (the deconv slot gets the graph's padded/dilated dy and rotated weights)
  *  NITI_OP_DSP_GRADIENTCONV_INT8, NITI_OP_DSP_MATMUL_INT8, NITI_OP_DSP_PARALLEL_GRADIENTCONV_INT8
  *                             as NITI_OP_DSP_MATMUL_GRADIENT_INT8, KH x KW from dw's dims
+ *  NITI_OP_RELU_INT8, NITI_OP_RELUGRAD_INT8, NITI_OP_MAXPOOL_INT8, NITI_OP_POOLGRAD_INT8: as the DSP
+ *                             slots below, on NC4HW4 (relu / relu grad also NCHW or NHWC) tensors
  *  NITI_OP_DSP_RELU_INT8 / NITI_OP_DSP_NOP_INT8 in {x NHWC} out{y NHWC}; NITI_OP_DSP_RELUGRAD_INT8
  *                             in {x, dy} out{dx}; common may be NULL for these three
  *  NITI_OP_DSP_MAXPOOL_INT8   in {x NHWC, ascale int8[1]} out{y NHWC, ascale int8[1]}; the pool's

@@ -681,7 +681,10 @@ class DspTransposeGradientExecution : public Execution {
     size_t slab_bytes_ = 0;
 };
 
-// ------------------------------------------------------------------ NITI_DSP element-wise slots
+// ------------------------------------------------------------------ element-wise slots (CPU graph and DSP graph)
+// The CPU graph's NITI_Relu_Int8 (703), NITI_ReluGrad_Int8 (704), NITI_Maxpool_Int8 (705,
+// {x, ascale} -> {y, ascale}, NITI_Maxpool_Int8.cpp:128-175) and NITI_PoolGrad_Int8 (706) take
+// the same execution on NC4HW4 (or, element-wise, NCHW) tensors.
 // NITI_DSP_RELU_Int8 (801) {x} -> {max(x, 0)}; NITI_DSP_RELUGRAD_Int8 (805) {x, dy} -> {x > 0 ? dy : 0}
 // (grad/NITI_ReluGrad_Int8.cpp:29-47); NITI_DSP_NOP_Int8 (817) {x} -> {x} (the DSP binary add's
 // gradient, grad/NITI_DSPBinaryGrad.cpp:14-42); NITI_DSP_MAXPOOL_Int8 (802) {x, ascale} ->
@@ -696,6 +699,12 @@ struct ReluMap {
     int8_t* y;
     __device__ void operator()(int64_t i) const { y[i] = x[i] > 0 ? x[i] : (int8_t)0; }
 };
+struct ReluGradMap {
+    const int8_t* x;
+    const int8_t* dy;
+    int8_t* y;
+    __device__ void operator()(int64_t i) const { y[i] = x[i] > 0 ? dy[i] : (int8_t)0; }
+};
 struct CopyMap {
     const int8_t* x;
     int8_t* y;
@@ -704,35 +713,66 @@ struct CopyMap {
 
 class DspElementwiseExecution : public Execution {
    public:
-    DspElementwiseExecution(int op, const niti_conv2d_common& c) : op_(op), common_(c) {}
+    enum Kind { RELU, RELUGRAD, NOP, POOL, POOLGRAD };
+    DspElementwiseExecution(int op, const niti_conv2d_common& c) : common_(c) {
+        cpu_ = op >= NITI_OP_RELU_INT8 && op <= NITI_OP_POOLGRAD_INT8;
+        switch (op) {
+            case NITI_OP_RELU_INT8:
+            case NITI_OP_DSP_RELU_INT8: kind_ = RELU; break;
+            case NITI_OP_RELUGRAD_INT8:
+            case NITI_OP_DSP_RELUGRAD_INT8: kind_ = RELUGRAD; break;
+            case NITI_OP_MAXPOOL_INT8:
+            case NITI_OP_DSP_MAXPOOL_INT8: kind_ = POOL; break;
+            case NITI_OP_POOLGRAD_INT8:
+            case NITI_OP_DSP_MAXPOOLGRAD_INT8: kind_ = POOLGRAD; break;
+            default: kind_ = NOP; break;
+        }
+    }
+    // NHWC-equivalent dims {n, c, h, w} of t: NHWC as is; for the CPU slots NC4HW4
+    // [C/4][N][H][W][4] is NHWC with n * ceil(c / 4) images of 4 channels (the CPU ops work per
+    // 4-channel plane, NITI_CPUPoolGrad_Int8.cpp:28-40), and element-wise ops also take NCHW
+    bool view(const niti_tensor& t, int d[4]) const {
+        if (t.format == NITI_FORMAT_NHWC || (cpu_ && kind_ != POOL && kind_ != POOLGRAD && t.format == NITI_FORMAT_NCHW)) {
+            for (int k = 0; k < 4; ++k) d[k] = t.dims[k];
+            return true;
+        }
+        if (cpu_ && t.format == NITI_FORMAT_NC4HW4) {
+            d[0] = t.dims[0] * ((t.dims[1] + 3) / 4), d[1] = 4, d[2] = t.dims[2], d[3] = t.dims[3];
+            return true;
+        }
+        return false;
+    }
     int onResize(const niti_tensor* in, int nin, const niti_tensor* out, int nout) override {
-        const int need = op_ == NITI_OP_DSP_RELUGRAD_INT8 ? 2 : op_ == NITI_OP_DSP_MAXPOOLGRAD_INT8 ? 3 : 1;
+        const int need = kind_ == RELUGRAD ? 2 : kind_ == POOLGRAD ? 3 : 1;
         if (nin < need || nout < 1) return NITI_INVALID_VALUE;
-        for (int i = 0; i < need; ++i)
-            if (in[i].format != NITI_FORMAT_NHWC) return NITI_NOT_SUPPORT;
-        if (out[0].format != NITI_FORMAT_NHWC) return NITI_NOT_SUPPORT;
-        const niti_tensor& x = in[0];
-        n_ = x.dims[0], c_ = x.dims[1], h_ = x.dims[2], w_ = x.dims[3];
+        int xd[4], od[4], d1[4] = {0, 0, 0, 0}, d2[4] = {0, 0, 0, 0};
+        if (!view(in[0], xd) || !view(out[0], od)) return NITI_NOT_SUPPORT;
+        if (need >= 2 && !view(in[1], d1)) return NITI_NOT_SUPPORT;
+        if (need >= 3 && !view(in[2], d2)) return NITI_NOT_SUPPORT;
+        for (int i = 1; i < need; ++i)
+            if (in[i].format != in[0].format) return NITI_NOT_SUPPORT;
+        if (out[0].format != in[0].format) return NITI_NOT_SUPPORT;
+        n_ = xd[0], c_ = xd[1], h_ = xd[2], w_ = xd[3];
         elems_ = (int64_t)n_ * c_ * h_ * w_;
         ready_ = false;
-        if (op_ == NITI_OP_DSP_MAXPOOL_INT8 || op_ == NITI_OP_DSP_MAXPOOLGRAD_INT8) {
+        if (kind_ == POOL || kind_ == POOLGRAD) {
             k_ = common_.kernel_x, s_ = common_.stride_x, p_ = common_.pad_x;
             if (common_.kernel_y != k_ || common_.stride_y != s_ || common_.pad_y != p_ || k_ < 1 || s_ < 1 || p_ < 0)
                 return NITI_NOT_SUPPORT;
             oh_ = (h_ + 2 * p_ - std::min(k_, h_)) / s_ + 1;
             ow_ = (w_ + 2 * p_ - std::min(k_, w_)) / s_ + 1;
-            const niti_tensor& y = op_ == NITI_OP_DSP_MAXPOOL_INT8 ? out[0] : in[1];
-            if (y.dims[0] != n_ || y.dims[1] != c_ || y.dims[2] != oh_ || y.dims[3] != ow_) return NITI_COMPUTE_SIZE_ERROR;
-            if (op_ == NITI_OP_DSP_MAXPOOLGRAD_INT8) {
+            const int* yd = kind_ == POOL ? od : d1;
+            if (yd[0] != n_ || yd[1] != c_ || yd[2] != oh_ || yd[3] != ow_) return NITI_COMPUTE_SIZE_ERROR;
+            if (kind_ == POOLGRAD) {
                 for (int k = 0; k < 4; ++k)
-                    if (in[2].dims[k] != y.dims[k] || out[0].dims[k] != x.dims[k]) return NITI_COMPUTE_SIZE_ERROR;
+                    if (d2[k] != yd[k] || od[k] != xd[k]) return NITI_COMPUTE_SIZE_ERROR;
             }
             cp_ = (c_ + 15) / 16 * 16;
             ws_.release();
             const size_t big = (size_t)n_ * h_ * w_ * cp_, small = (size_t)n_ * oh_ * ow_ * cp_;
             x16_ = (int8_t*)ws_.alloc(big);
             y16_ = (int8_t*)ws_.alloc(small);
-            if (op_ == NITI_OP_DSP_MAXPOOLGRAD_INT8) {
+            if (kind_ == POOLGRAD) {
                 dy16_ = (int8_t*)ws_.alloc(small);
                 dx16_ = (int8_t*)ws_.alloc(big);
                 if (!dy16_ || !dx16_) return NITI_OUT_OF_MEMORY;
@@ -740,7 +780,7 @@ class DspElementwiseExecution : public Execution {
             if (!x16_ || !y16_) return NITI_OUT_OF_MEMORY;
         } else {
             for (int k = 0; k < 4; ++k)
-                if (out[0].dims[k] != x.dims[k] || (need == 2 && in[1].dims[k] != x.dims[k])) return NITI_COMPUTE_SIZE_ERROR;
+                if (od[k] != xd[k] || (need == 2 && d1[k] != xd[k])) return NITI_COMPUTE_SIZE_ERROR;
         }
         ready_ = true;
         return NITI_NO_ERROR;
@@ -749,11 +789,11 @@ class DspElementwiseExecution : public Execution {
         if (!ready_) return NITI_NO_EXECUTION;
         const int8_t* x = (const int8_t*)in[0].data;
         int8_t* o = (int8_t*)out[0].data;
-        switch (op_) {
-            case NITI_OP_DSP_RELU_INT8: NITI_TRY(launch_map(elems_, ReluMap{x, o}, st)); break;
-            case NITI_OP_DSP_NOP_INT8: NITI_TRY(launch_map(elems_, CopyMap{x, o}, st)); break;
-            case NITI_OP_DSP_RELUGRAD_INT8: NITI_TRY(relu_grad_nhwc16(x, (const int8_t*)in[1].data, elems_, o, st)); break;
-            case NITI_OP_DSP_MAXPOOL_INT8: {
+        switch (kind_) {
+            case RELU: NITI_TRY(launch_map(elems_, ReluMap{x, o}, st)); break;
+            case NOP: NITI_TRY(launch_map(elems_, CopyMap{x, o}, st)); break;
+            case RELUGRAD: NITI_TRY(launch_map(elems_, ReluGradMap{x, (const int8_t*)in[1].data, o}, st)); break;
+            case POOL: {
                 const int64_t rows = (int64_t)n_ * oh_ * ow_;
                 NITI_TRY(launch_map((int64_t)n_ * h_ * w_ * cp_, NhwcToNhwc16{x, c_, cp_, x16_}, st));
                 NITI_TRY(maxpool_nhwc16(x16_, n_, h_, w_, cp_, k_, s_, p_, y16_, oh_, ow_, st));
@@ -762,7 +802,7 @@ class DspElementwiseExecution : public Execution {
                     NITI_TRY(hipMemcpyAsync(out[1].data, in[1].data, 1, hipMemcpyDeviceToDevice, st));
                 break;
             }
-            default: {  // NITI_OP_DSP_MAXPOOLGRAD_INT8
+            default: {  // POOLGRAD
                 const int64_t small = (int64_t)n_ * oh_ * ow_ * cp_, rows = (int64_t)n_ * h_ * w_;
                 NITI_TRY(launch_map(rows * cp_, NhwcToNhwc16{x, c_, cp_, x16_}, st));
                 NITI_TRY(launch_map(small, NhwcToNhwc16{(const int8_t*)in[1].data, c_, cp_, y16_}, st));
@@ -776,7 +816,8 @@ class DspElementwiseExecution : public Execution {
     }
 
    private:
-    int op_;
+    Kind kind_ = NOP;
+    bool cpu_ = false;
     niti_conv2d_common common_;
     bool ready_ = false;
     int n_ = 0, c_ = 0, h_ = 0, w_ = 0, k_ = 0, s_ = 0, p_ = 0, oh_ = 0, ow_ = 0, cp_ = 0;
@@ -1069,6 +1110,7 @@ Execution* create_execution(int op_type, const niti_conv2d_common* c, int* err) 
     dflt.group = 1;
     const niti_conv2d_common& cc = c ? *c : dflt;
     const bool no_params = op_type == NITI_OP_MATMUL_INT8 || op_type == NITI_OP_DSP_RELU_INT8 ||
+                           op_type == NITI_OP_RELU_INT8 || op_type == NITI_OP_RELUGRAD_INT8 ||
                            op_type == NITI_OP_DSP_RELUGRAD_INT8 || op_type == NITI_OP_DSP_NOP_INT8 ||
                            op_type == NITI_OP_LOSS_GRAD_INT8 || op_type == NITI_OP_DSP_LOSSGRAD_INT8 ||
                            op_type == NITI_OP_DSP_TRANSPOSE_INT8 || op_type == NITI_OP_DSP_WEIGHTROTATE180_INT8 ||
@@ -1101,6 +1143,10 @@ Execution* create_execution(int op_type, const niti_conv2d_common* c, int* err) 
         case NITI_OP_DSP_PAD_INT8:
         case NITI_OP_DSP_RESHAPE_INT8:
         case NITI_OP_DSP_RESHAPEGRAD_INT8: return new DspLayoutExecution(op_type, cc);
+        case NITI_OP_RELU_INT8:
+        case NITI_OP_RELUGRAD_INT8:
+        case NITI_OP_MAXPOOL_INT8:
+        case NITI_OP_POOLGRAD_INT8:
         case NITI_OP_DSP_RELU_INT8:
         case NITI_OP_DSP_RELUGRAD_INT8:
         case NITI_OP_DSP_NOP_INT8:

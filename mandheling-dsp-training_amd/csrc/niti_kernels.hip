@@ -2916,8 +2916,9 @@ hipError_t maxpool_relu_grad_nhwc16(const int8_t* x, const int8_t* y, const int8
 }
 
 __global__ void relu_grad_kernel(const int8_t* __restrict__ x, const int8_t* __restrict__ dy, int64_t n16,
-                                 int8_t* __restrict__ out) {
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n16; i += (int64_t)gridDim.x * blockDim.x) {
+                                 int64_t n, int8_t* __restrict__ out) {
+    const int64_t t0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    for (int64_t i = t0; i < n16; i += (int64_t)gridDim.x * blockDim.x) {
         const v16c xv = ((const v16c*)x)[i];
         const v16c dv = ((const v16c*)dy)[i];
         v16c o;
@@ -2925,14 +2926,17 @@ __global__ void relu_grad_kernel(const int8_t* __restrict__ x, const int8_t* __r
         for (int j = 0; j < 16; ++j) o[j] = xv[j] > 0 ? dv[j] : (signed char)0;
         ((v16c*)out)[i] = o;
     }
+    const int64_t e = n16 * 16 + t0;  // the last n % 16 elements
+    if (e < n) out[e] = x[e] > 0 ? dy[e] : (int8_t)0;
 }
 
 hipError_t relu_grad_nhwc16(const int8_t* x, const int8_t* dy, int64_t n, int8_t* out, hipStream_t st) {
+    if (((uintptr_t)x | (uintptr_t)dy | (uintptr_t)out) & 15) return hipErrorInvalidValue;  // 16-byte vectors
     const int64_t n16 = n / 16;
     int64_t blocks = (n16 + 255) / 256;
     if (blocks > 4096) blocks = 4096;
     if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL(relu_grad_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, dy, n16, out);
+    hipLaunchKernelGGL(relu_grad_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, dy, n16, n, out);
     return hipGetLastError();
 }
 

@@ -19,6 +19,10 @@ ERROR_NAMES = {0: "NO_ERROR", 1: "OUT_OF_MEMORY", 2: "NOT_SUPPORT", 3: "COMPUTE_
 
 OP_CONV_INT8 = 700
 OP_DECONV_INT8 = 701
+OP_RELU_INT8 = 703
+OP_RELUGRAD_INT8 = 704
+OP_MAXPOOL_INT8 = 705
+OP_POOLGRAD_INT8 = 706
 OP_LOSS_GRAD_INT8 = 711
 OP_MATMUL_INT8 = 713
 OP_GRADIENT_CONV_INT8 = 715

@@ -591,6 +591,37 @@ def test_exec_dsp_reshape(T, ops, op):
     assert np.array_equal(out.cpu().numpy(), x.reshape(4, 128))
 
 
+@pytest.mark.parametrize("geo", [(2, 20, 12, 12, 2, 2, 0), (3, 6, 9, 9, 3, 2, 1), (4, 64, 8, 8, 2, 2, 0)])
+def test_exec_cpu_pool_relu_c4(T, ops, oracle, geo):
+    """The CPU graph's NITI_Relu / NITI_ReluGrad / NITI_Maxpool / NITI_PoolGrad slots (703-706) on NC4HW4."""
+    n, c, h, w, k, s, p = geo
+    rng = np.random.default_rng(218)
+    x = rng.integers(-8, 8, size=(n, c, h, w), dtype=np.int8)
+    g = rng.integers(-128, 128, size=(n, c, h, w), dtype=np.int8)
+    c4 = oracle.nchw_to_c4
+    dims = (n, c, h, w)
+    out = T.zeros(c4(x).shape, dtype=T.int8, device="cuda")
+    _run_exec(ops, 703, None, [ops.tensor(dev(T, c4(x)), dims, 2)], [ops.tensor(out, dims, 2)])
+    assert np.array_equal(out.cpu().numpy(), c4(oracle.relu(x)))
+    _run_exec(ops, 704, None, [ops.tensor(dev(T, c4(x)), dims, 2), ops.tensor(dev(T, c4(g)), dims, 2)],
+              [ops.tensor(out, dims, 2)])
+    assert np.array_equal(out.cpu().numpy(), c4(oracle.relu_grad(x, g)))
+    y_ref = oracle.maxpool(x, k, s, p)
+    oh, ow = y_ref.shape[2], y_ref.shape[3]
+    dy = rng.integers(-128, 128, size=(n, c, oh, ow), dtype=np.int8)
+    ydims = (n, c, oh, ow)
+    y = T.zeros(c4(y_ref).shape, dtype=T.int8, device="cuda")
+    sc = i8s(T, 0)
+    common = ops.conv_common(k, stride=s, pad=p)
+    _run_exec(ops, 705, common, [ops.tensor(dev(T, c4(x)), dims, 2), ops.tensor(i8s(T, 3), (1, 1, 1, 1))],
+              [ops.tensor(y, ydims, 2), ops.tensor(sc, (1, 1, 1, 1))])
+    assert np.array_equal(y.cpu().numpy(), c4(y_ref))
+    assert int(sc.item()) == 3
+    _run_exec(ops, 706, common, [ops.tensor(dev(T, c4(x)), dims, 2), ops.tensor(y, ydims, 2),
+                                 ops.tensor(dev(T, c4(dy)), ydims, 2)], [ops.tensor(out, dims, 2)])
+    assert np.array_equal(out.cpu().numpy(), c4(oracle.maxpool_grad(x, y_ref, dy, k, s, p)))
+
+
 # --------------------------------------------------------------------------- tensor formats (§8(f)-3)
 def _as_format(x_nchw, fmt, oracle):
     if fmt == 0:
