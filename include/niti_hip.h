@@ -55,7 +55,9 @@ enum niti_op_type {
     NITI_OP_POOLGRAD_INT8 = 706,           /* NITI_PoolGrad_Int8      -> NITI_CPUPoolGrad_Int8.cpp:21-77 */
     NITI_OP_LOSS_GRAD_INT8 = 711,          /* NITI_LOSS_Grad_Int8     -> NITI_CPULossGrad_Int8.cpp:81-200 */
     NITI_OP_MATMUL_INT8 = 713,             /* NITI_MatMul_Int8        -> NITI_Matmul_Int8.cpp:140-231 */
+    NITI_OP_PAD_INT8 = 714,                /* NITI_PAD_Int8           -> NITI_Pad_Int8.cpp:24-62 */
     NITI_OP_GRADIENT_CONV_INT8 = 715,      /* NITI_GradientCONV_Int8  -> NITI_GradientConv_Int8.cpp:165-298 */
+    NITI_OP_LEFTPOOLGRAD_INT8 = 718,       /* NITI_LeftPoolGrad_Int8  -> NITI_CPULeftPoolGrad_Int8.cpp:18-52 */
     NITI_OP_DSP_CONV_INT8 = 800,           /* NITI_DSP_CONV_Int8      -> NITI_DSPConv_Int8.cpp:160-455 */
     NITI_OP_DSP_RELU_INT8 = 801,           /* NITI_DSP_RELU_Int8      -> NITI_DSPRelu_Int8.cpp */
     NITI_OP_DSP_MAXPOOL_INT8 = 802,        /* NITI_DSP_MAXPOOL_Int8   -> NITI_DSPMaxpool_Int8.cpp */
@@ -144,6 +146,8 @@ int niti_create_execution(int op_type, const niti_conv2d_common* common, niti_ex
  *                             out{w, raw axes 2, 3 reversed}; RESHAPE / RESHAPEGRAD in {x} out{same bytes};
  *                             all on the stored axis order ([N][H][W][C] for NHWC), common may be NULL
  *  NITI_OP_DSP_PAD_INT8       in {x NHWC} out{NHWC with a zero border of common.pad_x pixels}
+ *  NITI_OP_PAD_INT8 (NCHW), NITI_OP_LEFTPOOLGRAD_INT8 (NC4HW4): the CPU graph's pad and stride
+ *                             dilation, parameters as the DSP slots'
  *  NITI_OP_DSP_LEFTPOOLGRAD_DECONV_INT8 / _GRADIENT_INT8 in {dy NHWC} out{NHWC, dy[i][j] at
  *                             (stride_y*i, stride_x*j), zeros elsewhere}; stride in the common
  *  NITI_OP_LOSS_GRAD_INT8, NITI_OP_DSP_LOSSGRAD_INT8 (common may be NULL)

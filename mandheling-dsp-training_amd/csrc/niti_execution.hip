@@ -955,7 +955,20 @@ class DspLayoutExecution : public Execution {
     int onResize(const niti_tensor* in, int nin, const niti_tensor* out, int nout) override {
         if (nin < (op_ == NITI_OP_DSP_TRANSPOSE_INT8 ? 2 : 1) || nout < 1) return NITI_INVALID_VALUE;
         ready_ = false;
-        const Raw4 xi = raw_dims(in[0]), yo = raw_dims(out[0]);
+        // the CPU graph's NITI_PAD_Int8 (714) pads NCHW planes (NITI_Pad_Int8.cpp:24-62) and its
+        // NITI_LeftPoolGrad_Int8 (718) dilates NC4HW4 4-channel planes (NITI_CPULeftPoolGrad_Int8.cpp:
+        // 18-47): both are the NHWC maps below on [N*C][H][W][1] / [N*C4][H][W][4] views
+        Raw4 xi = raw_dims(in[0]), yo = raw_dims(out[0]);
+        if (op_ == NITI_OP_PAD_INT8 || op_ == NITI_OP_LEFTPOOLGRAD_INT8) {
+            const int f = op_ == NITI_OP_PAD_INT8 ? NITI_FORMAT_NCHW : NITI_FORMAT_NC4HW4;
+            if (in[0].format != f || out[0].format != f) return NITI_NOT_SUPPORT;
+            if (in[0].dims[0] != out[0].dims[0] || in[0].dims[1] != out[0].dims[1]) return NITI_COMPUTE_SIZE_ERROR;
+            auto v = [&](const niti_tensor& t) {
+                return f == NITI_FORMAT_NCHW ? Raw4{{t.dims[0] * t.dims[1], t.dims[2], t.dims[3], 1}}
+                                             : Raw4{{t.dims[0] * ((t.dims[1] + 3) / 4), t.dims[2], t.dims[3], 4}};
+            };
+            xi = v(in[0]), yo = v(out[0]);
+        }
         n_ = 1;
         for (int k = 0; k < 4; ++k) n_ *= yo.d[k];
         int64_t nx = 1;
@@ -982,17 +995,22 @@ class DspLayoutExecution : public Execution {
                     if (xi.d[k] != yo.d[k]) return NITI_COMPUTE_SIZE_ERROR;
                 rh_ = xi.d[2], rw_ = xi.d[3];
                 break;
+            case NITI_OP_LEFTPOOLGRAD_INT8:
             case NITI_OP_DSP_LEFTPOOLGRAD_DECONV_INT8:
             case NITI_OP_DSP_LEFTPOOLGRAD_GRADIENT_INT8:
-                if (in[0].format != NITI_FORMAT_NHWC || out[0].format != NITI_FORMAT_NHWC) return NITI_NOT_SUPPORT;
+                if (op_ != NITI_OP_LEFTPOOLGRAD_INT8 && (in[0].format != NITI_FORMAT_NHWC || out[0].format != NITI_FORMAT_NHWC))
+                    return NITI_NOT_SUPPORT;
                 if (common_.stride_x < 1 || common_.stride_y < 1) return NITI_INVALID_VALUE;
                 if (xi.d[0] != yo.d[0] || xi.d[3] != yo.d[3]) return NITI_COMPUTE_SIZE_ERROR;
                 lp_ = LeftPoolGradMap{nullptr, nullptr, xi.d[3], yo.d[2], yo.d[1], xi.d[1], xi.d[2], common_.stride_y,
                                       common_.stride_x};
                 break;
+            case NITI_OP_PAD_INT8:
             case NITI_OP_DSP_PAD_INT8: {
                 const int p = common_.pad_x;
-                if (in[0].format != NITI_FORMAT_NHWC || out[0].format != NITI_FORMAT_NHWC || p < 0) return NITI_NOT_SUPPORT;
+                if (p < 0 || (op_ == NITI_OP_DSP_PAD_INT8 &&
+                              (in[0].format != NITI_FORMAT_NHWC || out[0].format != NITI_FORMAT_NHWC)))
+                    return NITI_NOT_SUPPORT;
                 if (yo.d[0] != xi.d[0] || yo.d[3] != xi.d[3] || yo.d[1] != xi.d[1] + 2 * p || yo.d[2] != xi.d[2] + 2 * p)
                     return NITI_COMPUTE_SIZE_ERROR;
                 pad_ = PadMap{nullptr, nullptr, xi.d[3], yo.d[2], yo.d[1], xi.d[1], xi.d[2], p};
@@ -1017,6 +1035,7 @@ class DspLayoutExecution : public Execution {
                 break;
             }
             case NITI_OP_DSP_WEIGHTROTATE180_INT8: NITI_TRY(launch_map(n_, Rotate180Map{x, y, rh_, rw_}, st)); break;
+            case NITI_OP_LEFTPOOLGRAD_INT8:
             case NITI_OP_DSP_LEFTPOOLGRAD_DECONV_INT8:
             case NITI_OP_DSP_LEFTPOOLGRAD_GRADIENT_INT8: {
                 LeftPoolGradMap m = lp_;
@@ -1024,6 +1043,7 @@ class DspLayoutExecution : public Execution {
                 NITI_TRY(launch_map(n_, m, st));
                 break;
             }
+            case NITI_OP_PAD_INT8:
             case NITI_OP_DSP_PAD_INT8: {
                 PadMap m = pad_;
                 m.x = x, m.y = y;
@@ -1140,6 +1160,8 @@ Execution* create_execution(int op_type, const niti_conv2d_common* c, int* err) 
         case NITI_OP_DSP_WEIGHTROTATE180_INT8:
         case NITI_OP_DSP_LEFTPOOLGRAD_DECONV_INT8:
         case NITI_OP_DSP_LEFTPOOLGRAD_GRADIENT_INT8:
+        case NITI_OP_PAD_INT8:
+        case NITI_OP_LEFTPOOLGRAD_INT8:
         case NITI_OP_DSP_PAD_INT8:
         case NITI_OP_DSP_RESHAPE_INT8:
         case NITI_OP_DSP_RESHAPEGRAD_INT8: return new DspLayoutExecution(op_type, cc);

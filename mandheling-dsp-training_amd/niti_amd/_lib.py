@@ -25,6 +25,8 @@ OP_MAXPOOL_INT8 = 705
 OP_POOLGRAD_INT8 = 706
 OP_LOSS_GRAD_INT8 = 711
 OP_MATMUL_INT8 = 713
+OP_PAD_INT8 = 714
+OP_LEFTPOOLGRAD_INT8 = 718
 OP_GRADIENT_CONV_INT8 = 715
 OP_DSP_CONV_INT8 = 800
 OP_DSP_RELU_INT8 = 801

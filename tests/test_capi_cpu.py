@@ -45,7 +45,7 @@ def test_create_execution_validation(L):
     c.group = 2
     assert lib.niti_create_execution(700, C.byref(c), C.byref(h)) == 2      # grouped conv: NOT_SUPPORT
     c.group = 1
-    for op in (700, 701, 705, 706, 715, 800, 802, 807, 810, 811, 812, 814, 815, 818, 819, 820, 821, 822):
+    for op in (700, 701, 705, 706, 714, 715, 718, 800, 802, 807, 810, 811, 812, 814, 815, 818, 819, 820, 821, 822):
         assert lib.niti_create_execution(op, C.byref(c), C.byref(h)) == 0
         assert lib.niti_execution_workspace_bytes(h) == 0
         lib.niti_destroy_execution(h)

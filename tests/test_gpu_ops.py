@@ -622,6 +622,25 @@ def test_exec_cpu_pool_relu_c4(T, ops, oracle, geo):
     assert np.array_equal(out.cpu().numpy(), c4(oracle.maxpool_grad(x, y_ref, dy, k, s, p)))
 
 
+def test_exec_cpu_pad_and_leftpoolgrad(T, ops, oracle):
+    """The CPU graph's NITI_PAD (714, NCHW) and NITI_LeftPoolGrad (718, NC4HW4): the dy the deconv gets
+    (grad/NITI_Conv_Int8_Grad.cpp:101)."""
+    rng = np.random.default_rng(219)
+    n, c, oh, ow1, e = 3, 6, 5, 9, 1
+    dy = rng.integers(-128, 128, size=(n, c, oh, oh), dtype=np.int8)
+    d = np.zeros((n, c, ow1, ow1), np.int8)
+    d[:, :, ::2, ::2] = dy
+    c4 = oracle.nchw_to_c4
+    out4 = T.full(c4(d).shape, 9, dtype=T.int8, device="cuda")
+    _run_exec(ops, 718, ops.conv_common(1, stride=2), [ops.tensor(dev(T, c4(dy)), dy.shape, 2)],
+              [ops.tensor(out4, d.shape, 2)])
+    assert np.array_equal(out4.cpu().numpy(), c4(d))
+    want = np.pad(d, ((0, 0), (0, 0), (e, e), (e, e)))
+    outp = T.full(want.shape, 9, dtype=T.int8, device="cuda")
+    _run_exec(ops, 714, ops.conv_common(1, pad=e), [ops.tensor(dev(T, d), d.shape, 0)], [ops.tensor(outp, want.shape, 0)])
+    assert np.array_equal(outp.cpu().numpy(), want)
+
+
 # --------------------------------------------------------------------------- tensor formats (§8(f)-3)
 def _as_format(x_nchw, fmt, oracle):
     if fmt == 0:
