@@ -20,6 +20,7 @@ class NitiModel:
         check(self._lib.niti_model_create2(arch, batch, int(in_hw), C.byref(h)), "model_create")
         self._h = h
         self.arch, self.batch = arch, batch
+        self._wscale = {}
         self.layers = []
         for i in range(self._lib.niti_model_num_layers(h)):
             info = (C.c_int * 12)()
@@ -35,6 +36,24 @@ class NitiModel:
         w = np.ascontiguousarray(w, dtype=np.int8)
         assert w.shape == self.weight_shape(i), (w.shape, self.weight_shape(i))
         check(self._lib.niti_model_set_weight(self._h, i, w.ctypes.data_as(C.c_void_p), int(wscale)), "set_weight")
+        self._wscale[i] = int(wscale)
+
+    def save(self, path: str):
+        """Snapshot the device weights + wscales (mnistTrain.cpp:375-376 `Variable::save`)."""
+        from .checkpoint import save_params
+        if len(self._wscale) != len(self.layers):
+            raise ValueError("save() before every layer's weight was set")
+        save_params(path, [self.get_weight(i) for i in range(len(self.layers))],
+                    [self._wscale[i] for i in range(len(self.layers))], self.arch)
+
+    def load(self, path: str):
+        """Restore a snapshot written by save() into this model's device weights."""
+        from .checkpoint import load_params
+        weights, wscales, arch = load_params(path)
+        if arch != self.arch or len(weights) != len(self.layers):
+            raise ValueError(f"snapshot is arch {arch} with {len(weights)} layers, model is arch {self.arch}")
+        for i, (w, s) in enumerate(zip(weights, wscales)):
+            self.set_weight(i, w, s)
 
     def get_weight(self, i) -> np.ndarray:
         w = np.empty(self.weight_shape(i), np.int8)
