@@ -91,6 +91,10 @@ def lib():
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"libniti_hip.so not built ({LIB_PATH}); run __graft_entry__.build() or "
                           f"make -C mandheling-dsp-training_amd/csrc")
+    # torch ships its own libamdhip64.so.7 (same soname as /opt/rocm's).  Load torch first so
+    # this library binds to the runtime torch uses; loaded the other way round, torch is bound to
+    # /opt/rocm's copy and the first allocation in the process fails (seen on the GPU box).
+    import torch  # noqa: F401
     L = C.CDLL(LIB_PATH)
     vp, i32, i64, ci = C.c_void_p, C.c_int32, C.c_int64, C.c_int
     tp = C.POINTER(Tensor)
