@@ -15,8 +15,10 @@ int code(hipError_t e) {
     if (e == hipErrorInvalidValue) return NITI_INVALID_VALUE;
     return NITI_NO_EXECUTION;
 }
-niti::ConvGeom to_geom(const niti_geom* g) {
-    niti::ConvGeom r{};
+// false when ConvGeom::finalize rejects the geometry (callers return COMPUTE_SIZE_ERROR)
+bool to_geom(const niti_geom* g, niti::ConvGeom* out) {
+    niti::ConvGeom& r = *out;
+    r = niti::ConvGeom{};
     r.n = g->n;
     r.c_in = g->c_in;
     r.h = g->h;
@@ -32,8 +34,7 @@ niti::ConvGeom to_geom(const niti_geom* g) {
     r.pr = g->pad_r;
     r.dh = g->dilate_h;
     r.dw = g->dilate_w;
-    r.finalize();
-    return r;
+    return r.finalize();
 }
 inline hipStream_t S(void* s) { return (hipStream_t)s; }
 }  // namespace
@@ -104,7 +105,8 @@ int niti_geom_finalize(niti_geom* g) {
 
 int niti_conv_workspace_bytes(const niti_geom* g, int op, size_t* bytes) {
     if (!g || !bytes) return NITI_INVALID_VALUE;
-    const niti::ConvGeom r = to_geom(g);
+    niti::ConvGeom r;
+    if (!to_geom(g, &r)) return NITI_COMPUTE_SIZE_ERROR;
     if (op == 0)
         *bytes = niti::conv_fwd_workspace(r);
     else if (op == 1)
@@ -118,8 +120,8 @@ int niti_conv_workspace_bytes(const niti_geom* g, int op, size_t* bytes) {
 
 int niti_conv_plan_info(const niti_geom* g, int op, size_t ws_bytes, int info[4]) {
     if (!g || !info || op < 0 || op > 2) return NITI_INVALID_VALUE;
-    niti::ConvGeom r = to_geom(g);
-    if (!r.finalize()) return NITI_INVALID_VALUE;
+    niti::ConvGeom r;
+    if (!to_geom(g, &r)) return NITI_INVALID_VALUE;
     const int pop = op == 0 ? niti::PLAN_FWD : op == 1 ? niti::PLAN_DGRAD : niti::PLAN_WGRAD;
     const niti::PlanChoice c = niti::conv_plan_query(pop, r, op != 2, ws_bytes);
     info[0] = c.bm;
@@ -138,19 +140,25 @@ int niti_matmul_workspace_bytes(int m, int ldc, int k16, size_t* bytes) {
 int niti_conv_fwd_acc(const niti_geom* g, const int8_t* x, const int8_t* w, int32_t* acc, uint32_t* amax, void* ws,
                       size_t ws_bytes, void* stream) {
     if (!g) return NITI_INVALID_VALUE;
-    return code(niti::conv_fwd_acc(to_geom(g), x, w, acc, amax, ws, ws_bytes, S(stream)));
+    niti::ConvGeom r;
+    if (!to_geom(g, &r)) return NITI_COMPUTE_SIZE_ERROR;
+    return code(niti::conv_fwd_acc(r, x, w, acc, amax, ws, ws_bytes, S(stream)));
 }
 
 int niti_conv_dgrad_acc(const niti_geom* g, const int8_t* dy, const int8_t* wt, int32_t* acc, uint32_t* amax,
                         void* ws, size_t ws_bytes, void* stream) {
     if (!g) return NITI_INVALID_VALUE;
-    return code(niti::conv_dgrad_acc(to_geom(g), dy, wt, acc, amax, ws, ws_bytes, S(stream)));
+    niti::ConvGeom r;
+    if (!to_geom(g, &r)) return NITI_COMPUTE_SIZE_ERROR;
+    return code(niti::conv_dgrad_acc(r, dy, wt, acc, amax, ws, ws_bytes, S(stream)));
 }
 
 int niti_conv_wgrad_acc(const niti_geom* g, const int8_t* x, const int8_t* dy, int32_t* acc, uint32_t* amax,
                         void* ws, size_t ws_bytes, void* stream) {
     if (!g) return NITI_INVALID_VALUE;
-    return code(niti::conv_wgrad_acc(to_geom(g), x, dy, acc, amax, ws, ws_bytes, S(stream)));
+    niti::ConvGeom r;
+    if (!to_geom(g, &r)) return NITI_COMPUTE_SIZE_ERROR;
+    return code(niti::conv_wgrad_acc(r, x, dy, acc, amax, ws, ws_bytes, S(stream)));
 }
 
 int niti_matmul_acc(int m, int o, int k16, const int8_t* B, int64_t ldb, const int8_t* A, int64_t lda, int32_t* acc,

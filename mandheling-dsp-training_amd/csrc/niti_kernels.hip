@@ -34,6 +34,10 @@ bool ConvGeom::finalize() {
     if (n <= 0 || c_in <= 0 || h <= 0 || w <= 0 || c_out <= 0 || kh <= 0 || kw <= 0) return false;
     if (sh <= 0 || sw <= 0 || dh <= 0 || dw <= 0) return false;
     const int keh = dh * (kh - 1) + 1, kew = dw * (kw - 1) + 1;
+    if (pt < 0 || pb < 0 || pl < 0 || pr < 0) return false;
+    // reject before dividing: C++ division truncates toward zero, so a negative numerator
+    // smaller than the stride would otherwise still give oh = 1
+    if (h + pt + pb < keh || w + pl + pr < kew) return false;
     oh = (h + pt + pb - keh) / sh + 1;  // ShapeNITI_Conv_Int8.cpp:58-76
     ow = (w + pl + pr - kew) / sw + 1;
     cip = round_up(c_in, 16);

@@ -21,7 +21,7 @@ from safetensors.numpy import load_file, save_file
 FORMAT = "niti-int8-params-v1"
 
 
-def save_params(path: str, weights, wscales, arch: int) -> None:
+def save_params(path: str, weights, wscales, arch: int, in_hw: int = 0) -> None:
     """Write per-layer int8 OIHW weights and their int8 wscale side-car."""
     if len(weights) != len(wscales):
         raise ValueError(f"{len(weights)} weights but {len(wscales)} wscales")
@@ -34,7 +34,8 @@ def save_params(path: str, weights, wscales, arch: int) -> None:
             raise ValueError(f"layer {i}: wscale {s} does not fit int8")
         tensors[f"layer{i}.weight"] = np.ascontiguousarray(w)
         tensors[f"layer{i}.wscale"] = np.array([int(s)], np.int8)
-    save_file(tensors, path, metadata={"format": FORMAT, "arch": str(int(arch)), "num_layers": str(len(weights))})
+    save_file(tensors, path, metadata={"format": FORMAT, "arch": str(int(arch)), "num_layers": str(len(weights)),
+                                       "in_hw": str(int(in_hw))})
 
 
 def load_params(path: str):
@@ -45,7 +46,13 @@ def load_params(path: str):
         meta = f.metadata() or {}
     if meta.get("format") != FORMAT:
         raise ValueError(f"{path}: not a {FORMAT} snapshot (format={meta.get('format')!r})")
-    n = int(meta["num_layers"])
+    try:
+        n = int(meta["num_layers"])
+        arch = int(meta["arch"])
+    except (KeyError, ValueError, TypeError) as e:
+        raise ValueError(f"{path}: malformed snapshot metadata ({e!r})") from None
+    if n <= 0:
+        raise ValueError(f"{path}: num_layers {n}")
     t = load_file(path)
     weights, wscales = [], []
     for i in range(n):
@@ -54,4 +61,4 @@ def load_params(path: str):
             raise ValueError(f"{path}: layer {i} missing or malformed")
         weights.append(w)
         wscales.append(int(s[0]))
-    return weights, wscales, int(meta["arch"])
+    return weights, wscales, arch

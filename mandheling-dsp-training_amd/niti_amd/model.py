@@ -33,8 +33,13 @@ class NitiModel:
         return (l["c_out"], l["c_in"], l["kh"], l["kw"])
 
     def set_weight(self, i, w: np.ndarray, wscale: int):
-        w = np.ascontiguousarray(w, dtype=np.int8)
-        assert w.shape == self.weight_shape(i), (w.shape, self.weight_shape(i))
+        if not 0 <= i < len(self.layers):
+            raise ValueError(f"layer {i} out of range (model has {len(self.layers)})")
+        w = np.asarray(w)
+        if w.dtype != np.int8 or tuple(w.shape) != self.weight_shape(i):
+            # checked here, not by an assert: the C ABI copies weight_shape(i) bytes from w
+            raise ValueError(f"layer {i}: weight {w.dtype} {tuple(w.shape)}, want int8 {self.weight_shape(i)}")
+        w = np.ascontiguousarray(w)
         check(self._lib.niti_model_set_weight(self._h, i, w.ctypes.data_as(C.c_void_p), int(wscale)), "set_weight")
         self._wscale[i] = int(wscale)
 
@@ -44,7 +49,8 @@ class NitiModel:
         if len(self._wscale) != len(self.layers):
             raise ValueError("save() before every layer's weight was set")
         save_params(path, [self.get_weight(i) for i in range(len(self.layers))],
-                    [self._wscale[i] for i in range(len(self.layers))], self.arch)
+                    [self._wscale[i] for i in range(len(self.layers))], self.arch,
+                    in_hw=self.layers[0]["h"])
 
     def load(self, path: str):
         """Restore a snapshot written by save() into this model's device weights."""
@@ -52,6 +58,11 @@ class NitiModel:
         weights, wscales, arch = load_params(path)
         if arch != self.arch or len(weights) != len(self.layers):
             raise ValueError(f"snapshot is arch {arch} with {len(weights)} layers, model is arch {self.arch}")
+        # every layer's shape before any device write (a VGG-16 snapshot taken at another input
+        # size has the same arch and layer count but a different first FC layer)
+        for i, w in enumerate(weights):
+            if tuple(w.shape) != self.weight_shape(i):
+                raise ValueError(f"snapshot layer {i} is {tuple(w.shape)}, model layer is {self.weight_shape(i)}")
         for i, (w, s) in enumerate(zip(weights, wscales)):
             self.set_weight(i, w, s)
 

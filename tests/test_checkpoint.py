@@ -32,6 +32,16 @@ def test_params_rejects_bad_input(tmp_path):
     save_file({"x": np.zeros(3, np.int8)}, p)
     with pytest.raises(ValueError):
         load_params(p)
+    # right format tag, missing / non-numeric / non-positive layer count or arch
+    w = {"layer0.weight": np.zeros((1, 1, 1, 1), np.int8), "layer0.wscale": np.zeros(1, np.int8)}
+    for meta in ({"format": "niti-int8-params-v1", "arch": "1"},
+                 {"format": "niti-int8-params-v1", "arch": "1", "num_layers": "two"},
+                 {"format": "niti-int8-params-v1", "arch": "1", "num_layers": "0"},
+                 {"format": "niti-int8-params-v1", "num_layers": "1"},
+                 {"format": "niti-int8-params-v1", "arch": "x", "num_layers": "1"}):
+        save_file(w, p, metadata=meta)
+        with pytest.raises(ValueError):
+            load_params(p)
 
 
 @pytest.mark.gpu
