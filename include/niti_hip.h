@@ -248,6 +248,17 @@ int niti_relu_grad(const int8_t* x, const int8_t* dy, int64_t n, int8_t* out, vo
 int niti_loss_grad(const int8_t* logits, int batch, int classes, int ld, const int8_t* ascale,
                    const int32_t* labels, int8_t* out, void* stream);
 
+/* NITIInt8Train's input quantiser (execution-engine/tools/train/source/demo/MnistUtils.cpp:83-93):
+ * mean / std / range of the uint8 batch, x = round((p - mean) / std / range * 127), ascale =
+ * int8(ceil(ln(range)) - 7).  Split so data-parallel ranks can all-reduce the statistics:
+ * stats (4 x uint64, device) = {sum p, sum p^2 (SUM over ranks), max p, 255 - min p (MAX)};
+ * count = pixels the statistics cover (all ranks').  The float contract (exact integer
+ * statistics, the per-pixel formula in the reference's operation order) is stated in
+ * csrc/niti_quant.hip.  out_nchw int8 [n][c][hw]; ascale int8 device scalar (may be NULL). */
+int niti_image_stats(const uint8_t* images_nchw, int64_t n, uint64_t* stats, void* stream);
+int niti_image_quantize(const uint8_t* images_nchw, int n, int c, int hw, const uint64_t* stats, int64_t count,
+                        int8_t* out_nchw, int8_t* ascale, void* stream);
+
 /* ============================ 3. device-resident training step ========================= */
 /* LeNet on MNIST 1x28x28 (cfg 1/2); VGG-11 on CIFAR 3x32x32 (cfg 3); VGG-16 on ImageNet 3x224x224
  * with the 4096-4096-1000 head (cfg 4; niti_model_create2 takes another input size, a multiple
@@ -271,6 +282,12 @@ int niti_model_get_weight(niti_model_t m, int layer, int8_t* w_oihw_host);
  * x: NCHW int8 device [batch][C][H][W]; labels: int32 device [batch]; exp_in: input ascale.
  * Asynchronous on `stream`. */
 int niti_model_train_step(niti_model_t m, const int8_t* x_nchw, int exp_in, const int32_t* labels, void* stream);
+/* The same step from uint8 images [batch][C][H][W] (device): the input quantiser
+ * (niti_image_stats / niti_image_quantize, statistics all-reduced in exact data-parallel mode)
+ * runs on device first and supplies x and exp_in -- NITIInt8Train's whole per-batch work. */
+int niti_model_train_step_images(niti_model_t m, const uint8_t* images_nchw, const int32_t* labels, void* stream);
+/* Read back (synchronising): the step's quantised input x (NCHW int8) and its exponent. */
+int niti_model_get_input(niti_model_t m, int8_t* x_nchw_host, int* ascale, void* stream);
 /* Read back (synchronising `stream`): logits [batch][classes] int8 and their exponent. */
 int niti_model_get_logits(niti_model_t m, int8_t* logits_host, int* exp_out, void* stream);
 /* Per-layer debug taps (synchronising): which = 0 fwd output (post relu, pre pool, NCHW),
@@ -283,8 +300,8 @@ int64_t niti_model_step_macs(niti_model_t m);
  * always runs as direct launches).  Default 0 (direct launches: measured faster on ROCm 7.2). */
 int niti_model_set_graph(niti_model_t m, int enable);
 /* Run the weight gradients on a second HIP stream, overlapping the input-gradient chain
- * (default 1; the update waits for both; with a communicator it needs the second RCCL
- * communicator attach_comm splits off, else the step stays on one stream). */
+ * (default 1; the update waits for both).  With a communicator every collective is still
+ * issued on the step stream, in program order, through one communicator. */
 int niti_model_set_overlap(niti_model_t m, int enable);
 /* Per-shape GEMM plan autotuning (no counterpart in the reference, whose CPU kernels have a
  * fixed blocking, NITI_Conv_Int8.cpp:159-253): times every layer phase under candidate plans
@@ -320,10 +337,21 @@ int niti_model_run_phase(niti_model_t m, int layer, int phase, void* stream);
 #define NITI_UNIQUE_ID_BYTES 128
 /* rank 0 creates the id; every rank receives it out of band (torch.distributed store). */
 int niti_dp_get_unique_id(char id[NITI_UNIQUE_ID_BYTES]);
-/* Attach an RCCL communicator: exact mode all-reduces (MAX) every forward and input-gradient
- * range and (SUM) every int32 weight-gradient accumulator, so N ranks of batch b are
- * bit-identical to one device of batch N*b.  exact=0 keeps ranges shard-local (not parity). */
+/* Attach an RCCL communicator (one per model; all its collectives go on the step stream in
+ * program order): exact mode all-reduces the input quantiser's statistics (SUM / MAX), every
+ * forward and input-gradient range (MAX) and every int32 weight-gradient accumulator (SUM), so
+ * N ranks of batch b are bit-identical to one device of batch N*b.  exact=0 keeps the
+ * statistics and ranges shard-local (not parity; the gradient SUM stays). */
 int niti_model_attach_comm(niti_model_t m, const char id[NITI_UNIQUE_ID_BYTES], int rank, int world, int exact);
+
+/* In-process rank group on ONE device (tests and single-GPU rehearsal of the protocol): each
+ * of `world` host threads drives one model attached with its rank; every collective
+ * synchronises the caller's stream and the last rank to arrive reduces all ranks' buffers on
+ * the device.  Same calls, order and streams as the RCCL path; no second GPU needed. */
+typedef struct niti_local_group* niti_local_group_t;
+int niti_local_group_create(int world, niti_local_group_t* out);
+void niti_local_group_destroy(niti_local_group_t g);
+int niti_model_attach_local(niti_model_t m, niti_local_group_t g, int rank, int exact);
 
 /* library build info */
 const char* niti_version(void);

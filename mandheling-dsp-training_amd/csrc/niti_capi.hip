@@ -233,6 +233,17 @@ int niti_relu_grad(const int8_t* x, const int8_t* dy, int64_t n, int8_t* out, vo
     if (n % 16) return NITI_INVALID_VALUE;
     return code(niti::relu_grad_nhwc16(x, dy, n, out, S(stream)));
 }
+int niti_image_stats(const uint8_t* images, int64_t n, uint64_t* stats, void* stream) {
+    if (!images || !stats || n <= 0) return NITI_INVALID_VALUE;
+    return code(niti::image_stats(images, n, reinterpret_cast<unsigned long long*>(stats), S(stream)));
+}
+int niti_image_quantize(const uint8_t* images, int n, int c, int hw, const uint64_t* stats, int64_t count,
+                        int8_t* out_nchw, int8_t* ascale, void* stream) {
+    if (!images || !stats || !out_nchw || n <= 0 || c <= 0 || hw <= 0 || count < (int64_t)n * c * hw)
+        return NITI_INVALID_VALUE;
+    return code(niti::image_quantize(images, n, c, hw, c, reinterpret_cast<const unsigned long long*>(stats), count,
+                                     out_nchw, ascale, false, S(stream)));
+}
 int niti_loss_grad(const int8_t* logits, int batch, int classes, int ld, const int8_t* ascale, const int32_t* labels,
                    int8_t* out, void* stream) {
     return code(niti::loss_grad(logits, batch, classes, ld, ascale, labels, out, S(stream)));

@@ -210,6 +210,15 @@ hipError_t relu_grad_nhwc16(const int8_t* x, const int8_t* dy, int64_t n, int8_t
 hipError_t loss_grad(const int8_t* logits, int batch, int classes, int ld, const int8_t* ascale,
                      const int32_t* labels, int8_t* out, hipStream_t st);
 
+// ---- input quantiser (MnistUtils.cpp:83-93; niti_quant.hip states the exact contract) -------
+// stats (4 x u64, device) = {S1 = sum x, S2 = sum x^2, xmax, 255 - xmin} of n uint8 pixels
+hipError_t image_stats(const uint8_t* img, int64_t n, unsigned long long* stats, hipStream_t st);
+// x = round((p - mean) / std / range * 127) from stats over `count` pixels (count > n*c*hw when
+// the statistics were all-reduced over data-parallel ranks); out NHWC16 [n][hw][cp] (nhwc16) or
+// NCHW; *ascale = int8(ceil(ln(range)) - 7) (ascale may be null)
+hipError_t image_quantize(const uint8_t* img, int n, int c, int hw, int cp, const unsigned long long* stats,
+                          int64_t count, int8_t* out, int8_t* ascale, bool nhwc16, hipStream_t st);
+
 // ---- layout transforms --------------------------------------------------------------------
 // NHWC16 [N][H][W][Cp] -> CHWN16 [Cp][H][W][Np]
 hipError_t nhwc16_to_chwn16(const int8_t* in, int n, int hw, int cp, int np, int8_t* out, hipStream_t st);

@@ -8,14 +8,17 @@
 //               NITI_DeCONV_Int8 (input gradient, skipped for the first layer exactly as the
 //               lazy reference graph skips it), pool / relu gradients
 //   update    : w <- clip(w - g, +-127)  (NITI_SGD.hpp:49-52)
-// With an RCCL communicator (exact mode) every forward / input-gradient range is
-// all-reduced with MAX and every int32 weight-gradient accumulator with SUM before it is
-// requantised, so N ranks of batch b reproduce one device of batch N*b bit for bit.
+// With a communicator (exact mode) the input quantiser's statistics are all-reduced (SUM,
+// MAX), every forward / input-gradient range with MAX and every int32 weight-gradient
+// accumulator with SUM before it is requantised, so N ranks of batch b reproduce one device of
+// batch N*b bit for bit.
 #include <rccl/rccl.h>
 #include <string.h>
 
 #include <algorithm>
+#include <condition_variable>
 #include <memory>
+#include <mutex>
 #include <vector>
 
 #include "../../include/niti_hip.h"
@@ -54,6 +57,127 @@ struct FlattenBwd {
 };
 
 }  // namespace
+
+// ---------------------------------------------------------------------------- collectives
+// The data-parallel step's collectives.  Every rank issues the same sequence, all of it on the
+// step stream through ONE communicator, so no two collectives are ever in flight at once on a
+// rank and the order is the program order on every rank: no cross-stream or cross-communicator
+// interleaving exists that could deadlock (round 1 split a second communicator for the weight
+// gradients on the side stream; that concurrency is gone).  The weight-gradient GEMMs still run
+// on the side stream; their SUMs are issued on the step stream one layer later (Model::run).
+enum CollOp { COLL_MAX_U32 = 0, COLL_SUM_I32 = 1, COLL_SUM_U64 = 2, COLL_MAX_U64 = 3 };
+
+struct Collective {
+    virtual ~Collective() = default;
+    virtual int size() const = 0;
+    // in place, on stream st, asynchronous where the transport allows
+    virtual hipError_t allreduce(void* p, size_t n, CollOp op, hipStream_t st) = 0;
+};
+
+struct RcclCollective final : Collective {
+    ncclComm_t comm = nullptr;
+    int world = 1;
+    ~RcclCollective() override {
+        if (comm) (void)ncclCommDestroy(comm);
+    }
+    int size() const override { return world; }
+    hipError_t allreduce(void* p, size_t n, CollOp op, hipStream_t st) override {
+        static const ncclDataType_t ty[4] = {ncclUint32, ncclInt32, ncclUint64, ncclUint64};
+        static const ncclRedOp_t ro[4] = {ncclMax, ncclSum, ncclSum, ncclMax};
+        return ncclAllReduce(p, p, n, ty[op], ro[op], comm, st) == ncclSuccess ? hipSuccess : hipErrorUnknown;
+    }
+};
+
+// In-process group of `world` ranks on ONE device, one host thread per rank (tests): each
+// collective synchronises the caller's stream, the last rank to arrive reduces every rank's
+// buffer on the device and writes the result back to all of them.  It runs the model's exact
+// data-parallel protocol -- the same calls, in the same order, on the same streams -- with a
+// transport that needs no second GPU.
+struct LocalGroup {
+    static constexpr int MAX_RANKS = 16;
+    int world = 1;
+    std::mutex mu;
+    std::condition_variable cv;
+    int arrived = 0;
+    unsigned long long gen = 0;
+    void* ptr[MAX_RANKS] = {};
+    size_t n = 0;
+    int op = -1;
+    bool mismatch = false;
+    hipError_t err = hipSuccess;
+    hipStream_t rst = nullptr;
+    ~LocalGroup() {
+        if (rst) (void)hipStreamDestroy(rst);
+    }
+};
+
+namespace {
+struct RankPtrs {
+    void* p[LocalGroup::MAX_RANKS];
+    int world;
+};
+template <class T, bool MAX>
+__global__ void local_reduce_kernel(RankPtrs r, size_t n) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        T v = static_cast<T*>(r.p[0])[i];
+        for (int k = 1; k < r.world; ++k) {
+            const T t = static_cast<T*>(r.p[k])[i];
+            v = MAX ? (t > v ? t : v) : (T)(v + t);
+        }
+        for (int k = 0; k < r.world; ++k) static_cast<T*>(r.p[k])[i] = v;
+    }
+}
+}  // namespace
+
+struct LocalCollective final : Collective {
+    std::shared_ptr<LocalGroup> g;
+    int rank = 0;
+    int size() const override { return g->world; }
+    hipError_t allreduce(void* p, size_t n, CollOp op, hipStream_t st) override {
+        hipError_t e = hipStreamSynchronize(st);
+        std::unique_lock<std::mutex> lk(g->mu);
+        const unsigned long long my_gen = g->gen;
+        if (g->arrived == 0) {
+            g->n = n;
+            g->op = op;
+            g->mismatch = false;
+            g->err = hipSuccess;
+        } else if (g->n != n || g->op != op) {
+            g->mismatch = true;  // ranks disagree on the sequence: a protocol bug
+        }
+        g->ptr[rank] = p;
+        if (e != hipSuccess) g->err = e;
+        if (++g->arrived == g->world) {
+            if (!g->mismatch && g->err == hipSuccess) {
+                RankPtrs r{};
+                for (int k = 0; k < g->world; ++k) r.p[k] = g->ptr[k];
+                r.world = g->world;
+                const unsigned blocks = (unsigned)std::min<size_t>((n + 255) / 256, 1024);
+                if (blocks > 0) {
+                    if (op == COLL_MAX_U32)
+                        hipLaunchKernelGGL((local_reduce_kernel<uint32_t, true>), dim3(blocks), dim3(256), 0, g->rst, r, n);
+                    else if (op == COLL_SUM_I32)
+                        hipLaunchKernelGGL((local_reduce_kernel<int32_t, false>), dim3(blocks), dim3(256), 0, g->rst, r, n);
+                    else if (op == COLL_SUM_U64)
+                        hipLaunchKernelGGL((local_reduce_kernel<unsigned long long, false>), dim3(blocks), dim3(256), 0,
+                                           g->rst, r, n);
+                    else
+                        hipLaunchKernelGGL((local_reduce_kernel<unsigned long long, true>), dim3(blocks), dim3(256), 0,
+                                           g->rst, r, n);
+                    g->err = hipGetLastError();
+                    if (g->err == hipSuccess) g->err = hipStreamSynchronize(g->rst);
+                }
+            }
+            if (g->mismatch) g->err = hipErrorInvalidValue;
+            g->arrived = 0;
+            ++g->gen;
+            g->cv.notify_all();
+        } else {
+            g->cv.wait(lk, [&] { return g->gen != my_gen; });
+        }
+        return g->err;
+    }
+};
 
 struct Layer {
     ConvGeom g{};
@@ -99,12 +223,15 @@ struct Model {
     hipStream_t side = nullptr;
     std::vector<hipEvent_t> ev_dy;
     hipEvent_t ev_side = nullptr;
-    ncclComm_t comm_w = nullptr;  // the side stream's collectives (split from comm)
+    std::vector<hipEvent_t> ev_w;  // weight gradient i done on the side stream (data parallel)
     uint32_t* amax = nullptr;  // 3 ranges per layer (forward, input gradient, weight gradient)
     size_t amax_bytes = 0;
     uint32_t* rng(int layer, int which) { return amax + (size_t)(3 * layer + which) * MAX_WORDS; }
-    ncclComm_t comm = nullptr;
+    std::unique_ptr<Collective> coll;
     int world = 1, rank = 0, exact = 1;
+    bool dp() const { return coll != nullptr && world > 1 && !tuning; }
+    // input quantiser statistics {S1, S2, xmax, 255 - xmin} (niti_quant.hip)
+    unsigned long long* qstats = nullptr;
     // Optional hipGraph replay of the single-device step: ~95 launches become one graph launch
     // (or three when a probe splits it around the probed GEMM).  Captured on an internal
     // stream, fenced against the caller's stream with events; re-captured when the captured
@@ -222,10 +349,16 @@ struct Model {
         ev_dy.resize(L.size());
         for (auto& e : ev_dy)
             if (hipEventCreateWithFlags(&e, kFlags) != hipSuccess) return NITI_NO_EXECUTION;
+        ev_w.resize(L.size());
+        for (auto& e : ev_w)
+            if (hipEventCreateWithFlags(&e, kFlags) != hipSuccess) return NITI_NO_EXECUTION;
         return NITI_NO_ERROR;
     }
-    int run(const int8_t* x_nchw, int exp_in, const int32_t* labels, hipStream_t st);
-    int step(const int8_t* x_nchw, int exp_in, const int32_t* labels, hipStream_t st);
+    // x_nchw int8 with exponent exp_in, or (x_nchw == null) uint8 images through the on-device
+    // input quantiser (MnistUtils.cpp:83-93)
+    int run(const int8_t* x_nchw, int exp_in, const uint8_t* images, const int32_t* labels, hipStream_t st);
+    int step(const int8_t* x_nchw, int exp_in, const uint8_t* images, const int32_t* labels, hipStream_t st);
+    int reduce_wgrad(int i, hipStream_t st, bool ov);
     ~Model() {
         clear_probe();
         drop_graph();
@@ -233,10 +366,10 @@ struct Model {
         if (gout) (void)hipEventDestroy(gout);
         if (gstream) (void)hipStreamDestroy(gstream);
         for (auto e : ev_dy) (void)hipEventDestroy(e);
+        for (auto e : ev_w) (void)hipEventDestroy(e);
         if (ev_side) (void)hipEventDestroy(ev_side);
         if (side) (void)hipStreamDestroy(side);
-        if (comm_w) (void)ncclCommDestroy(comm_w);
-        if (comm) (void)ncclCommDestroy(comm);
+        coll.reset();
     }
 };
 
@@ -347,6 +480,8 @@ int Model::build(int arch_, int batch_, int in_hw) {
         }
     }
     acc = (int32_t*)ws.alloc(acc_elems * 4);
+    qstats = (unsigned long long*)ws.alloc(64);
+    if (!qstats) return NITI_OUT_OF_MEMORY;
     if (slab_bytes) {
         slab = ws.alloc(slab_bytes);
         if (!slab) return NITI_OUT_OF_MEMORY;
@@ -368,13 +503,13 @@ int Model::build(int arch_, int batch_, int in_hw) {
     } while (0)
 #define CTRY(expr)                                             \
     do {                                                       \
-        if ((expr) != ncclSuccess) return NITI_NO_EXECUTION;   \
+        if ((expr) != hipSuccess) return NITI_NO_EXECUTION;    \
     } while (0)
 
-int Model::step(const int8_t* x_nchw, int exp_in, const int32_t* labels, hipStream_t st) {
-    if (!use_graph || comm != nullptr) return run(x_nchw, exp_in, labels, st);
+int Model::step(const int8_t* x_nchw, int exp_in, const uint8_t* images, const int32_t* labels, hipStream_t st) {
+    if (!use_graph || coll != nullptr) return run(x_nchw, exp_in, images, labels, st);
     Key k;
-    k.x = x_nchw;
+    k.x = x_nchw ? (const void*)x_nchw : (const void*)images;
     k.labels = labels;
     k.exp_in = exp_in;
     k.pl = probe_layer;
@@ -389,7 +524,7 @@ int Model::step(const int8_t* x_nchw, int exp_in, const int32_t* labels, hipStre
         MTRY(hipStreamBeginCapture(gstream, hipStreamCaptureModeThreadLocal));
         capturing = true;
         cap_err = hipSuccess;
-        const int rc = run(x_nchw, exp_in, labels, gstream);
+        const int rc = run(x_nchw, exp_in, images, labels, gstream);
         hipGraph_t g = nullptr;
         hipError_t e = hipStreamEndCapture(gstream, &g);
         capturing = false;
@@ -401,7 +536,7 @@ int Model::step(const int8_t* x_nchw, int exp_in, const int32_t* labels, hipStre
             drop_graph();
             use_graph = false;  // fall back to direct launches for this model
             (void)hipGetLastError();
-            return run(x_nchw, exp_in, labels, st);
+            return run(x_nchw, exp_in, images, labels, st);
         }
         key = k;
     }
@@ -422,12 +557,12 @@ int Model::step(const int8_t* x_nchw, int exp_in, const int32_t* labels, hipStre
 // when the requant is a separate pass) -> pool / flatten.
 int Model::fwd_layer(int i, hipStream_t st) {
     const int n = batch;
-    const bool dp = comm != nullptr && world > 1 && !tuning;
+    const bool dp = this->dp();
     Layer& l = L[i];
     const ConvGeom& g = l.g;
     probe(i, 0, true, st);
     MTRY(conv_fwd_phase1(g, l.in, l.w, acc, rng(i, 0), slab, slab_bytes, st));
-    if (dp && exact) CTRY(ncclAllReduce(rng(i, 0), rng(i, 0), MAX_WORDS, ncclUint32, ncclMax, comm, st));
+    if (dp && exact) CTRY(coll->allreduce(rng(i, 0), MAX_WORDS, COLL_MAX_U32, st));
     ActOut o;
     o.out = l.r;
     o.relu = l.relu;
@@ -451,12 +586,12 @@ int Model::fwd_layer(int i, hipStream_t st) {
     return NITI_NO_ERROR;
 }
 
-// One layer's weight gradient (the int32 gradient and, single device, its range).
+// One layer's weight gradient (the int32 gradient and, single device, its range; data
+// parallel, the SUM and the range follow in reduce_wgrad on the step stream).
 int Model::wgrad_layer(int i, hipStream_t st) {
-    const bool dp = comm != nullptr && world > 1 && !tuning;
+    const bool dp = this->dp();
     Layer& l = L[i];
     const ConvGeom& g = l.g;
-    const int64_t we = l.w_elems();
     // the weight-gradient probe brackets the GEMM launch alone (not its split-K reduce)
     // the weight-gradient probe is the GEMM launch's own begin / end (its split-K reduce excluded)
     if (capturing)
@@ -466,10 +601,17 @@ int Model::wgrad_layer(int i, hipStream_t st) {
     arm_span(i, 2);
     MTRY(conv_wgrad_acc(g, l.in, l.dy, l.dwacc, dp ? nullptr : rng(i, 2), slab_w, slab_w_bytes, st,
                         capturing ? probe_end_event(i, 2) : nullptr));
-    if (dp) {
-        CTRY(ncclAllReduce(l.dwacc, l.dwacc, (size_t)we, ncclInt32, ncclSum, st == side ? comm_w : comm, st));
-        MTRY(absmax_i32(l.dwacc, we, rng(i, 2), st));
-    }
+    return NITI_NO_ERROR;
+}
+
+// Data parallel: SUM layer i's int32 weight gradient over the ranks, then its range, on the step
+// stream (after the side stream's weight-gradient GEMM when the streams overlap).
+int Model::reduce_wgrad(int i, hipStream_t st, bool ov) {
+    Layer& l = L[i];
+    const int64_t we = l.w_elems();
+    if (ov) MTRY(hipStreamWaitEvent(st, ev_w[i], 0));
+    CTRY(coll->allreduce(l.dwacc, (size_t)we, COLL_SUM_I32, st));
+    MTRY(absmax_i32(l.dwacc, we, rng(i, 2), st));
     return NITI_NO_ERROR;
 }
 
@@ -477,13 +619,13 @@ int Model::wgrad_layer(int i, hipStream_t st) {
 // previous layer's pool / flatten / relu gradients.
 int Model::dgrad_layer(int i, hipStream_t st) {
     const int n = batch;
-    const bool dp = comm != nullptr && world > 1 && !tuning;
+    const bool dp = this->dp();
     Layer& l = L[i];
     const ConvGeom& g = l.g;
     Layer& pv = L[i - 1];
     probe(i, 1, true, st);
     MTRY(conv_dgrad_phase1(g, l.dy, l.wT, acc, rng(i, 1), slab, slab_bytes, st));
-    if (dp && exact) CTRY(ncclAllReduce(rng(i, 1), rng(i, 1), MAX_WORDS, ncclUint32, ncclMax, comm, st));
+    if (dp && exact) CTRY(coll->allreduce(rng(i, 1), MAX_WORDS, COLL_MAX_U32, st));
     const ConvGeom& pg = pv.g;
     ActOut o;
     if (pv.flatten) {
@@ -619,14 +761,28 @@ int Model::autotune(hipStream_t st, int reps) {
     return rc;
 }
 
-int Model::run(const int8_t* x_nchw, int exp_in, const int32_t* labels, hipStream_t st) {
+int Model::run(const int8_t* x_nchw, int exp_in, const uint8_t* images, const int32_t* labels, hipStream_t st) {
     const int n = batch;
     const int nl = (int)L.size();
+    const bool dp = this->dp();
     SgdJob jobs[SGD_MAX_JOBS];
     if (nl > SGD_MAX_JOBS) return NITI_NOT_SUPPORT;
     MTRY(hipMemsetAsync(amax, 0, amax_bytes, st));
-    MTRY(hipMemsetAsync(exp0, exp_in, 1, st));
-    MTRY(nchw_to_nhwc16(x_nchw, n, in_c, in_h * in_w, round_up(in_c, 16), x0, st));
+    if (x_nchw != nullptr) {
+        MTRY(hipMemsetAsync(exp0, exp_in, 1, st));
+        MTRY(nchw_to_nhwc16(x_nchw, n, in_c, in_h * in_w, round_up(in_c, 16), x0, st));
+    } else {
+        // NITIInt8Train's input quantiser (MnistUtils.cpp:83-93): batch statistics (global over
+        // the ranks in exact mode), then x and its exponent ascale straight into the layer-0 input
+        const int64_t px = (int64_t)n * in_c * in_h * in_w;
+        MTRY(image_stats(images, px, qstats, st));
+        if (dp && exact) {
+            CTRY(coll->allreduce(qstats, 2, COLL_SUM_U64, st));
+            CTRY(coll->allreduce(qstats + 2, 2, COLL_MAX_U64, st));
+        }
+        MTRY(image_quantize(images, n, in_c, in_h * in_w, round_up(in_c, 16), qstats,
+                            dp && exact ? px * world : px, x0, exp0, true, st));
+    }
     for (int i = 0; i < nl; ++i) {
         const int rc = fwd_layer(i, st);
         if (rc != NITI_NO_ERROR) return rc;
@@ -635,9 +791,8 @@ int Model::run(const int8_t* x_nchw, int exp_in, const int32_t* labels, hipStrea
         Layer& t = L[nl - 1];
         MTRY(loss_grad(t.r, n, t.g.c_out, t.g.cop, t.exp, labels, t.dy, st));
     }
-    // weight gradients on the side stream (not inside a graph capture, and in data-parallel
-    // runs only with a second communicator for it)
-    const bool ov = overlap && !capturing && (comm == nullptr || comm_w != nullptr);
+    // weight gradients on the side stream (not inside a graph capture)
+    const bool ov = overlap && !capturing;
     if (ov) {
         const int rc = ensure_streams();
         if (rc != NITI_NO_ERROR) return rc;
@@ -651,7 +806,11 @@ int Model::run(const int8_t* x_nchw, int exp_in, const int32_t* labels, hipStrea
             MTRY(hipStreamWaitEvent(side, ev_dy[i], 0));
         }
         int rc = wgrad_layer(i, wst);
+        if (rc == NITI_NO_ERROR && ov && dp) MTRY(hipEventRecord(ev_w[i], side));
         if (rc == NITI_NO_ERROR && i > 0) rc = dgrad_layer(i, st);
+        // data parallel: the previous layer's gradient SUM goes on the step stream behind this
+        // layer's input gradient (its GEMM ran beside two input-gradient layers by then)
+        if (rc == NITI_NO_ERROR && dp && i + 1 < nl) rc = reduce_wgrad(i + 1, st, ov);
         if (rc != NITI_NO_ERROR) return rc;
         // NITI_SGD (NITI_SGD.hpp:20-54) for this layer is deferred: every layer's update runs
         // in one launch after the backward pass (the input gradients above read the old weights)
@@ -659,6 +818,10 @@ int Model::run(const int8_t* x_nchw, int exp_in, const int32_t* labels, hipStrea
         const ConvGeom& g = l.g;
         jobs[i] = SgdJob{l.dwacc, rng(i, 2), RULE_WGRAD_BW2, g.c_out, g.c_in, g.kh * g.kw, g.cip, g.cop, l.w,
                          i > 0 ? l.wT : nullptr, l.g8};
+    }
+    if (dp) {
+        const int rc = reduce_wgrad(0, st, ov);
+        if (rc != NITI_NO_ERROR) return rc;
     }
     if (ov) {  // every weight gradient is in before the update
         MTRY(hipEventRecord(ev_side, side));
@@ -736,7 +899,29 @@ int niti_model_get_weight(niti_model_t m, int layer, int8_t* w_host) {
 
 int niti_model_train_step(niti_model_t m, const int8_t* x_nchw, int exp_in, const int32_t* labels, void* stream) {
     if (!m || !x_nchw || !labels) return NITI_INVALID_VALUE;
-    return m->m.step(x_nchw, exp_in, labels, (hipStream_t)stream);
+    return m->m.step(x_nchw, exp_in, nullptr, labels, (hipStream_t)stream);
+}
+
+int niti_model_train_step_images(niti_model_t m, const uint8_t* images_nchw, const int32_t* labels, void* stream) {
+    if (!m || !images_nchw || !labels) return NITI_INVALID_VALUE;
+    return m->m.step(nullptr, 0, images_nchw, labels, (hipStream_t)stream);
+}
+
+int niti_model_get_input(niti_model_t m, int8_t* x_nchw_host, int* ascale, void* stream) {
+    if (!m || !x_nchw_host) return NITI_INVALID_VALUE;
+    niti::Model& mm = m->m;
+    const int n = mm.batch, hw = mm.in_h * mm.in_w;
+    if (hipStreamSynchronize((hipStream_t)stream) != hipSuccess) return NITI_NO_EXECUTION;
+    const size_t need = (size_t)n * mm.in_c * hw;
+    int8_t* tmp = nullptr;
+    if (hipMalloc(&tmp, need) != hipSuccess) return NITI_OUT_OF_MEMORY;
+    int8_t e = 0;
+    hipError_t err = niti::nhwc16_to_nchw(mm.x0, n, mm.in_c, hw, niti::round_up(mm.in_c, 16), tmp, nullptr);
+    if (err == hipSuccess) err = hipMemcpy(x_nchw_host, tmp, need, hipMemcpyDeviceToHost);
+    if (err == hipSuccess) err = hipMemcpy(&e, mm.exp0, 1, hipMemcpyDeviceToHost);
+    (void)hipFree(tmp);
+    if (ascale) *ascale = e;
+    return err == hipSuccess ? NITI_NO_ERROR : NITI_NO_EXECUTION;
 }
 
 int niti_model_get_logits(niti_model_t m, int8_t* logits_host, int* exp_out, void* stream) {
@@ -819,11 +1004,10 @@ int niti_model_run_phase(niti_model_t m, int layer, int phase, void* stream) {
         return NITI_INVALID_VALUE;
     const bool t = m->m.tuning;
     m->m.tuning = false;  // keep the probe armed; collectives stay off (single-device phase)
-    ncclComm_t c = m->m.comm;
-    m->m.comm = nullptr;
+    std::unique_ptr<niti::Collective> c = std::move(m->m.coll);
     hipStream_t st = (hipStream_t)stream;
     const int rc = phase == 0 ? m->m.fwd_layer(layer, st) : phase == 1 ? m->m.dgrad_layer(layer, st) : m->m.wgrad_layer(layer, st);
-    m->m.comm = c;
+    m->m.coll = std::move(c);
     m->m.tuning = t;
     return rc;
 }
@@ -953,18 +1137,47 @@ int niti_dp_get_unique_id(char id[NITI_UNIQUE_ID_BYTES]) {
 }
 
 int niti_model_attach_comm(niti_model_t m, const char id[NITI_UNIQUE_ID_BYTES], int rank, int world, int exact) {
-    if (!m || world < 1 || rank < 0 || rank >= world) return NITI_INVALID_VALUE;
+    if (!m || !id || world < 1 || rank < 0 || rank >= world) return NITI_INVALID_VALUE;
     ncclUniqueId u;
     memcpy(&u, id, sizeof(u));
-    ncclComm_t c = nullptr;
-    if (ncclCommInitRank(&c, world, u, rank) != ncclSuccess) return NITI_NO_EXECUTION;
-    m->m.comm = c;
-    // a second communicator for the weight-gradient all-reduces on the side stream (collectives
-    // of one communicator must not be issued from two streams at once); without it the weight
-    // gradients stay on the step stream
-    ncclComm_t cw = nullptr;
-    if (world > 1 && ncclCommSplit(c, 0, rank, &cw, nullptr) == ncclSuccess) m->m.comm_w = cw;
+    auto c = std::make_unique<niti::RcclCollective>();
+    if (ncclCommInitRank(&c->comm, world, u, rank) != ncclSuccess) return NITI_NO_EXECUTION;
+    c->world = world;
+    m->m.drop_graph();
+    m->m.coll = std::move(c);
     m->m.world = world;
+    m->m.rank = rank;
+    m->m.exact = exact ? 1 : 0;
+    return NITI_NO_ERROR;
+}
+
+struct niti_local_group {
+    std::shared_ptr<niti::LocalGroup> g;
+};
+
+int niti_local_group_create(int world, niti_local_group_t* out) {
+    if (!out || world < 1 || world > niti::LocalGroup::MAX_RANKS) return NITI_INVALID_VALUE;
+    auto* h = new niti_local_group();
+    h->g = std::make_shared<niti::LocalGroup>();
+    h->g->world = world;
+    if (hipStreamCreateWithFlags(&h->g->rst, hipStreamNonBlocking) != hipSuccess) {
+        delete h;
+        return NITI_NO_EXECUTION;
+    }
+    *out = h;
+    return NITI_NO_ERROR;
+}
+
+void niti_local_group_destroy(niti_local_group_t g) { delete g; }
+
+int niti_model_attach_local(niti_model_t m, niti_local_group_t g, int rank, int exact) {
+    if (!m || !g || rank < 0 || rank >= g->g->world) return NITI_INVALID_VALUE;
+    auto c = std::make_unique<niti::LocalCollective>();
+    c->g = g->g;
+    c->rank = rank;
+    m->m.drop_graph();
+    m->m.coll = std::move(c);
+    m->m.world = g->g->world;
     m->m.rank = rank;
     m->m.exact = exact ? 1 : 0;
     return NITI_NO_ERROR;

@@ -152,6 +152,13 @@ def lib():
         "niti_model_probe_read_span": (ci, [vp, C.POINTER(C.c_double), C.POINTER(ci)]),
         "niti_dp_get_unique_id": (ci, [C.c_char_p]),
         "niti_model_attach_comm": (ci, [vp, C.c_char_p, ci, ci, ci]),
+        "niti_image_stats": (ci, [vp, i64, vp, vp]),
+        "niti_image_quantize": (ci, [vp, ci, ci, ci, vp, i64, vp, vp, vp]),
+        "niti_model_train_step_images": (ci, [vp, vp, vp, vp]),
+        "niti_model_get_input": (ci, [vp, vp, C.POINTER(ci), vp]),
+        "niti_local_group_create": (ci, [ci, C.POINTER(vp)]),
+        "niti_local_group_destroy": (None, [vp]),
+        "niti_model_attach_local": (ci, [vp, vp, ci, ci]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

@@ -76,6 +76,23 @@ class NitiModel:
         check(self._lib.niti_model_train_step(self._h, C.c_void_p(x.data_ptr()), int(exp_in),
                                               C.c_void_p(labels.data_ptr()), _stream(stream)), "train_step")
 
+    def train_step_images(self, images: torch.Tensor, labels: torch.Tensor, stream=None):
+        """One step from uint8 images [batch][C][H][W]: the input quantiser (MnistUtils.cpp:83-93)
+        runs on device and supplies x and its exponent."""
+        assert images.dtype == torch.uint8 and images.is_contiguous() and labels.dtype == torch.int32
+        check(self._lib.niti_model_train_step_images(self._h, C.c_void_p(images.data_ptr()),
+                                                     C.c_void_p(labels.data_ptr()), _stream(stream)),
+              "train_step_images")
+
+    def input(self, stream=None):
+        """The last step's quantised input x (NCHW int8) and its exponent."""
+        l0 = self.layers[0]
+        out = np.empty((self.batch, l0["c_in"], l0["h"], l0["w"]), np.int8)
+        e = C.c_int()
+        check(self._lib.niti_model_get_input(self._h, out.ctypes.data_as(C.c_void_p), C.byref(e), _stream(stream)),
+              "get_input")
+        return out, int(e.value)
+
     def logits(self, stream=None):
         last = self.layers[-1]
         out = np.empty((self.batch, last["c_out"]), np.int8)
@@ -156,6 +173,11 @@ class NitiModel:
     def attach_comm(self, unique_id: bytes, rank: int, world: int, exact: bool = True):
         check(self._lib.niti_model_attach_comm(self._h, unique_id, rank, world, 1 if exact else 0), "attach_comm")
 
+    def attach_local(self, group: "LocalGroup", rank: int, exact: bool = True):
+        """Join an in-process rank group on this device (one host thread per rank)."""
+        check(self._lib.niti_model_attach_local(self._h, group._h, rank, 1 if exact else 0), "attach_local")
+        self._group = group  # keep the group alive as long as the model
+
     @staticmethod
     def unique_id() -> bytes:
         buf = C.create_string_buffer(128)
@@ -166,4 +188,22 @@ class NitiModel:
         h = getattr(self, "_h", None)
         if h:
             self._lib.niti_model_destroy(h)
+            self._h = None
+
+
+class LocalGroup:
+    """niti_local_group: `world` ranks of the data-parallel protocol on ONE device, one host
+    thread per rank, collectives reduced on the device (include/niti_hip.h)."""
+
+    def __init__(self, world: int):
+        self._lib = L.lib()
+        h = C.c_void_p()
+        check(self._lib.niti_local_group_create(int(world), C.byref(h)), "local_group_create")
+        self._h = h
+        self.world = world
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            self._lib.niti_local_group_destroy(h)
             self._h = None

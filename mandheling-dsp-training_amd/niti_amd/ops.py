@@ -287,3 +287,24 @@ def loss_grad(logits, classes, ascale_dev, labels, stream=None):
     check(L.lib().niti_loss_grad(_ptr(logits), b, classes, ld, _ptr(ascale_dev), _ptr(labels), _ptr(out),
                                  _stream(stream)), "loss_grad")
     return out
+
+
+def image_stats(images: torch.Tensor, stream=None):
+    """{sum p, sum p^2, max p, 255 - min p} (int64 device [4], u64 values) of a uint8 image batch
+    (the input quantiser's statistics, MnistUtils.cpp:83-93; SUM / MAX over DP ranks)."""
+    assert images.dtype == torch.uint8 and images.is_contiguous()
+    stats = torch.zeros(4, dtype=torch.int64, device=images.device)  # u64 values < 2^63
+    check(L.lib().niti_image_stats(_ptr(images), images.numel(), _ptr(stats), _stream(stream)), "image_stats")
+    return stats
+
+
+def image_quantize(images: torch.Tensor, stats: torch.Tensor, count: int | None = None, stream=None):
+    """x int8 NCHW and its exponent (device int8 [1]) from uint8 images [n][c][h][w] and the
+    statistics over `count` pixels (default: this batch's)."""
+    assert images.dtype == torch.uint8 and images.is_contiguous() and images.dim() == 4
+    n, c, h, w = images.shape
+    out = torch.empty(images.shape, dtype=torch.int8, device=images.device)
+    ascale = torch.zeros(1, dtype=torch.int8, device=images.device)
+    check(L.lib().niti_image_quantize(_ptr(images), n, c, h * w, _ptr(stats), int(count or images.numel()),
+                                      _ptr(out), _ptr(ascale), _stream(stream)), "image_quantize")
+    return out, ascale

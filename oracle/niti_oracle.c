@@ -750,6 +750,56 @@ int32_t niti_ref_quantize_input(const float* x, int64_t n, int8_t* out) {
     return (int32_t)(int8_t)(bw - 7.0f);
 }
 
+/* MnistUtils.cpp:83-93 stated over exact integer statistics of the uint8 pixels (the
+ * reference leaves its float summation order to MNN's reductions; this is the order-free
+ * contract the device implements, mandheling-dsp-training_amd/csrc/niti_quant.hip):
+ *   S1 = sum p, S2 = sum p^2, xmin, xmax over `count` pixels (stats[] = {S1, S2, xmax, 255-xmin})
+ *   mean = float(S1) / float(count); ss = S2 - 2 mean S1 + count mean^2 (double, this order);
+ *   sd = sqrtf(float(ss / count)); range = max(|xmax - mean|, |xmin - mean|) / sd (float);
+ *   x = (int8) roundf(((p - mean) / sd) / range * 127); ascale = int8(ceil(log(range)) - 7).
+ * std == 0 (a constant batch, 0/0 in the reference): x = 0, ascale = -7.
+ * This file is compiled without FMA contraction (x86-64 baseline, -ffp-contract=off). */
+void niti_ref_image_stats(const uint8_t* img, int64_t n, uint64_t stats[4]) {
+    uint64_t s1 = 0, s2 = 0;
+    uint32_t mx = 0, mn = 255;
+    for (int64_t i = 0; i < n; ++i) {
+        const uint32_t p = img[i];
+        s1 += p;
+        s2 += (uint64_t)p * p;
+        if (p > mx) mx = p;
+        if (p < mn) mn = p;
+    }
+    stats[0] = s1;
+    stats[1] = s2;
+    stats[2] = mx;
+    stats[3] = 255u - mn;
+}
+
+int32_t niti_ref_image_quantize(const uint8_t* img, int64_t n, const uint64_t stats[4], int64_t count, int8_t* out) {
+    const double s1 = (double)stats[0], s2 = (double)stats[1];
+    const float xmax = (float)stats[2], xmin = (float)(255u - stats[3]);
+    const float mean = (float)stats[0] / (float)count;
+    const double m = (double)mean;
+    const double a = 2.0 * m;
+    const double b = a * s1;
+    const double c = (double)count * m;
+    const double d = c * m;
+    const double ss = (s2 - b) + d;
+    const float var = (float)(ss / (double)count);
+    const float sd = sqrtf(var > 0.f ? var : 0.f);
+    if (!(sd > 0.f)) {
+        memset(out, 0, (size_t)n);
+        return -7;
+    }
+    const float hi = fabsf(xmax - mean) / sd, lo = fabsf(xmin - mean) / sd;
+    const float range = hi > lo ? hi : lo;
+    for (int64_t i = 0; i < n; ++i) {
+        const float y = ((float)img[i] - mean) / sd;
+        out[i] = (int8_t)(int)roundf(y / range * 127.0f);
+    }
+    return (int32_t)(int8_t)(int)(ceil(log((double)range)) - 7.0);
+}
+
 /* ---------------------------------------------------------------------------- */
 /* CPU baseline: one layer's fwd + wgrad (+ dgrad) in the reference's structure  */
 /* ---------------------------------------------------------------------------- */

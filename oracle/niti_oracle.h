@@ -134,6 +134,9 @@ void niti_ref_loss_grad(const int8_t* logits, int batch, int classes, int32_t as
 /* NITI_SGD.hpp:49-52 + niti_execute BinaryUtils.hpp:278-299: w <- clip(w - g, +-127) */
 void niti_ref_sgd_update(int8_t* w, const int8_t* g, int64_t n);
 /* MnistUtils.cpp:83-93: float batch -> int8, returns ascale */
+/* the input quantiser over exact integer statistics (the device contract, niti_quant.hip) */
+void niti_ref_image_stats(const uint8_t* img, int64_t n, uint64_t stats[4]);
+int32_t niti_ref_image_quantize(const uint8_t* img, int64_t n, const uint64_t stats[4], int64_t count, int8_t* out);
 int32_t niti_ref_quantize_input(const float* x, int64_t n, int8_t* out);
 
 /* ---------------- CPU baseline ---------------- */

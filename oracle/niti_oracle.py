@@ -85,6 +85,8 @@ def _declare(L):
         "niti_ref_loss_grad": (None, [vp, C.c_int, C.c_int, i32, vp, C.c_int, vp]),
         "niti_ref_sgd_update": (None, [vp, vp, i64]),
         "niti_ref_quantize_input": (i32, [vp, i64, vp]),
+        "niti_ref_image_stats": (None, [vp, i64, vp]),
+        "niti_ref_image_quantize": (i32, [vp, i64, vp, i64, vp]),
         "niti_ref_layer_step": (C.c_int, [gp, vp, vp, vp, vp, vp, vp, C.c_int, C.c_int]),
     }
     for name, (res, args) in sig.items():
@@ -308,6 +310,24 @@ def quantize_input(x):
     x = _c(x, np.float32)
     out = np.empty(x.shape, np.int8)
     a = lib().niti_ref_quantize_input(_p(x), x.size, _p(out))
+    return out, int(a)
+
+
+def image_stats(images):
+    """{S1, S2, xmax, 255 - xmin} (uint64) of uint8 pixels (niti_ref_image_stats)."""
+    img = _c(images, np.uint8)
+    st = np.zeros(4, np.uint64)
+    lib().niti_ref_image_stats(_p(img), img.size, _p(st))
+    return st
+
+
+def quantize_images(images, stats=None, count=None):
+    """MnistUtils.cpp:83-93 over exact integer statistics: (x int8 same shape, ascale).  stats /
+    count default to this batch's own (data-parallel ranks pass the global ones)."""
+    img = _c(images, np.uint8)
+    st = image_stats(img) if stats is None else np.ascontiguousarray(stats, np.uint64)
+    out = np.empty(img.shape, np.int8)
+    a = lib().niti_ref_image_quantize(_p(img), img.size, _p(st), int(count or img.size), _p(out))
     return out, int(a)
 
 
