@@ -38,23 +38,41 @@ def synth_weights(layers, seed):
     return out
 
 
-def cpu_baseline(layers, sample, threads):
-    """The oracle's reference-structured restatement (C4, 16x4 GEMM unit, float32 accumulation,
-    batch-split threads) timed on this host for one VGG-11 step on `sample` images."""
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(arch, sample, threads_list):
+    """The oracle's reference-structured restatement of the WHOLE NITIInt8Train step (input
+    quantiser, NITI_Conv_Int8 forwards in MNN C4 with the 16x4 GEMM unit and float32
+    accumulation, relu / maxpool, NITI_LOSS_Grad, the grad graph's weight and input gradients,
+    pool / relu gradients, NITI_SGD) on `sample` images, timed on this host once per thread count
+    (batch-split pthreads as NITI_Conv_Int8.cpp:224-229).  Test infrastructure, never the product."""
     import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import niti_model_ref as R
     import niti_oracle as O
+    layers = {"vgg11": R.vgg11_layers, "lenet": R.lenet_layers}[arch]()
+    W, S = R.init_weights(layers, seed=17)
     rng = np.random.default_rng(1)
-    t_total = 0.0
-    for i, l in enumerate(layers):
-        g = O.geom(sample, l["c_in"], l["h"], l["w"], l["c_out"], l["kh"], pad=l["pad"])
-        x = O.synth_x(rng, (sample, l["c_in"], l["h"], l["w"]))
-        w, _ = O.synth_w(rng, (l["c_out"], l["c_in"], l["kh"], l["kw"]))
-        dy = O.synth_dy(rng, (sample, l["c_out"], g.oh, g.ow))
+    l0 = layers[0]
+    img = rng.integers(0, 256, (sample, l0["ci"], l0["h"], l0["h"])).astype(np.uint8)
+    labels = rng.integers(0, 10, sample).astype(np.int32)
+    legs = []
+    for t in threads_list:
+        O.set_threads(t)
         t0 = time.perf_counter()
-        O.layer_step(g, x, w, dy, threads=threads, with_dgrad=i > 0)
-        t_total += time.perf_counter() - t0
-    return sample / t_total, t_total
+        x, a = O.quantize_images(img)
+        R.train_step(layers, W, S, x, a, labels, impl="mnn", threads=t, acc_mode=O.ACC_F32_SEQ)
+        secs = time.perf_counter() - t0
+        legs.append({"threads": t, "value": round(sample / secs, 3), "seconds": round(secs, 2)})
+    return legs
 
 
 def main():
@@ -67,8 +85,11 @@ def main():
     ap.add_argument("--arch", default="vgg11", choices=["vgg11", "lenet", "vgg16"])
     ap.add_argument("--in-hw", type=int, default=0, help="input resolution (0: the architecture's own)")
     ap.add_argument("--cpu-sample", type=int, default=-1, help="images in the CPU baseline sample "
-                                                               "(-1: 128 VGG-11 / LeNet, 1 VGG-16; 0 = skip)")
-    ap.add_argument("--cpu-threads", type=int, default=4, help="reference default: MnistUtils.cpp:43")
+                                                               "(-1: 64 VGG-11, 256 LeNet, 0 VGG-16 = skip)")
+    ap.add_argument("--cpu-threads", type=int, default=4, help="first CPU leg (reference default: MnistUtils.cpp:43); "
+                                                               "the second leg uses every core of this process")
+    ap.add_argument("--int8-input", action="store_true", help="feed pre-quantised int8 x with a fixed exponent "
+                                                              "instead of uint8 images through the device quantiser")
     ap.add_argument("--probe-layer", type=int, default=3, help="layer whose GEMM is timed for the roofline")
     ap.add_argument("--probe-phase", type=int, default=2, help="0 fwd, 1 input grad, 2 weight grad")
     ap.add_argument("--graph", action="store_true", help="replay the step as a hipGraph (slower on ROCm 7.2)")
@@ -97,7 +118,7 @@ def main():
     if args.batch <= 0:
         args.batch = 64 if arch == niti_amd.ARCH_VGG16 else 256
     if args.cpu_sample < 0:
-        args.cpu_sample = 1 if arch == niti_amd.ARCH_VGG16 else 128
+        args.cpu_sample = {niti_amd.ARCH_VGG16: 0, niti_amd.ARCH_LENET: 256}.get(arch, 64)
     model = NitiModel(arch, args.batch, args.in_hw)
     model.set_graph(args.graph)
     model.set_overlap(not args.no_overlap)
@@ -110,15 +131,25 @@ def main():
 
     l0 = model.layers[0]
     rng = np.random.default_rng(100 + rank)
-    x = torch.from_numpy(rng.integers(-127, 128, (args.batch, l0["c_in"], l0["h"], l0["w"])).astype(np.int8)).cuda()
+    shape = (args.batch, l0["c_in"], l0["h"], l0["w"])
+    if args.int8_input:
+        x = torch.from_numpy(rng.integers(-127, 128, shape).astype(np.int8)).cuda()
+    else:  # uint8 images: the on-device input quantiser is part of every timed step
+        x = torch.from_numpy(rng.integers(0, 256, shape).astype(np.uint8)).cuda()
     labels = torch.from_numpy(rng.integers(0, 1000 if arch == niti_amd.ARCH_VGG16 else 10,
                                            args.batch).astype(np.int32)).cuda()
+
+    def step():
+        if args.int8_input:
+            model.train_step(x, -3, labels)
+        else:
+            model.train_step_images(x, labels)
 
     # Setup (untimed): one step to fill the buffers, then per-shape GEMM plan autotuning
     # (niti_model_autotune: candidate tile / split-K plans timed per layer phase).
     tune_s = 0.0
     if not args.no_autotune:
-        model.train_step(x, -3, labels)
+        step()
         ta = time.perf_counter()
         model.autotune()
         torch.cuda.synchronize()
@@ -133,7 +164,7 @@ def main():
     # must not happen inside the timed region.  Warmup launches are read and discarded.
     model.set_probe(probe_layer, args.probe_phase, args.steps + args.warmup)
     for _ in range(args.warmup):
-        model.train_step(x, -3, labels)
+        step()
     torch.cuda.synchronize()
     model.probe_read()
     model.probe_read_span()
@@ -142,7 +173,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        model.train_step(x, -3, labels)
+        step()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -192,11 +223,19 @@ def main():
             traffic = None
 
     cpu = None
-    if rank == 0 and world == 1 and args.cpu_sample > 0:
-        v, secs = cpu_baseline(model.layers, args.cpu_sample, args.cpu_threads)
-        cpu = {"value": round(v, 3), "unit": "images/s", "cores": args.cpu_threads, "kind": "port",
-               "sample": f"{args.cpu_sample} images of the {args.arch.upper()} step (every conv: fwd + weight grad + input grad, "
-                         f"reference-structured C restatement, float32 accumulation), {secs:.1f} s"}
+    if rank == 0 and world == 1 and args.cpu_sample > 0 and args.arch in ("vgg11", "lenet"):
+        # every core this process may use: the affinity set, capped by the box's CPU share
+        # (OMP_NUM_THREADS, 16 per GPU on the pool) -- the thread count is reported as `cores`
+        all_cores = len(os.sched_getaffinity(0))
+        if os.environ.get("OMP_NUM_THREADS", "").isdigit():
+            all_cores = max(1, min(all_cores, int(os.environ["OMP_NUM_THREADS"])))
+        legs = cpu_baseline(args.arch, args.cpu_sample, sorted({args.cpu_threads, all_cores}))
+        best = max(legs, key=lambda l: l["value"])
+        cpu = {"value": best["value"], "unit": "images/s", "cores": best["threads"], "kind": "port",
+               "sample": f"{args.cpu_sample} images through the whole {args.arch.upper()} NITIInt8Train step (input "
+                         f"quantiser, fwd + relu/pool, loss grad, weight + input grads, pool/relu grads, NITI_SGD) in the "
+                         f"oracle's reference-structured C restatement (MNN C4, 16x4 unit, float32 accumulation)",
+               "legs": legs, "cpu_model": cpu_model()}
 
     phase_name = {0: "forward conv", 1: "input-gradient conv", 2: "weight-gradient conv"}[args.probe_phase]
     pplan = plans[(probe_layer, args.probe_phase)]
@@ -220,7 +259,9 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "int8",
-        "data": "synthetic (random int8 images, labels; seeded niti_normal_int8 weights)",
+        "data": ("synthetic (random int8 x, fixed exponent" if args.int8_input else
+                 "synthetic (random uint8 images through the on-device input quantiser") +
+                "; random labels; seeded niti_normal_int8 weights)",
         "config": {"workload": f"{args.arch.upper()} NITI int8 training step (fwd+relu+pool, loss grad, "
                                f"weight grad, input grad, SGD), {l0['c_in']}x{l0['h']}x{l0['w']}"
                                + (", 4096-4096-1000 head" if arch == niti_amd.ARCH_VGG16 else "")

@@ -65,18 +65,31 @@ def onehot(labels, classes=10):
     return oh
 
 
-def train_step(layers, W, S, x, exp_in, labels, classes=10):
-    """Returns (new weights, record) where record holds logits, exponents and per-layer taps."""
+def train_step(layers, W, S, x, exp_in, labels, classes=10, impl="naive", threads=1, wgrad_stats=False,
+               acc_mode=None):
+    """Returns (new weights, record) where record holds logits, exponents and per-layer taps.
+
+    impl "naive": the exact NCHW restatement; "mnn": the reference-structured one (C4 layout,
+    16x4 GEMM unit, the grad graph's transposes / LeftPoolGrad / rot180), exact accumulation, on
+    `threads` pthreads (acc_mode O.ACC_F32_SEQ: the reference's float32 accumulation, as the CPU
+    baseline runs it; default exact).  wgrad_stats: record per layer the weight gradient's 2^24-guard and int32
+    overflow counts (naive pass) and how many int32 sums / int8 gradients the reference's float32
+    accumulation (Int8FunctionsOpt.cpp:211-226) would change (mnn pass, ACC_F32_SEQ)."""
     n = x.shape[0]
-    rec = dict(inp=[], y=[], r=[], p=[], exp=[], dw=[], dy=[], geom=[])
+    rec = dict(inp=[], y=[], r=[], p=[], exp=[], dw=[], dy=[], geom=[], wstats=[])
+    mnn = impl == "mnn"
+    am = O.ACC_EXACT if acc_mode is None else acc_mode
     a = x
     exp = exp_in
     for i, l in enumerate(layers):
         g = O.geom(n, l["ci"], l["h"], l["h"], l["co"], l["k"], pad=l["pad"])
         rec["geom"].append(g)
         rec["inp"].append(a)
-        y, exp, _, st = O.conv_fwd(g, a, W[i], exp, S[i])
-        assert st.overflow == 0
+        if mnn:
+            y, exp, _ = O.mnn_conv_fwd(g, a, W[i], exp, S[i], am, threads)
+        else:
+            y, exp, _, st = O.conv_fwd(g, a, W[i], exp, S[i])
+            assert st.overflow == 0
         r = O.relu(y) if l["relu"] else y
         rec["y"].append(y)
         rec["r"].append(r)
@@ -98,10 +111,22 @@ def train_step(layers, W, S, x, exp_in, labels, classes=10):
     newW = list(W)
     for i in range(len(layers) - 1, -1, -1):
         g = rec["geom"][i]
-        dw, bw, _, _ = O.conv_wgrad(g, rec["inp"][i], dy[i])
+        if mnn:
+            dw, bw, acc = O.mnn_conv_wgrad(g, rec["inp"][i], dy[i], am, threads)
+        else:
+            dw, bw, acc, _ = O.conv_wgrad(g, rec["inp"][i], dy[i])
+        if wgrad_stats:
+            _, st = O.conv_wgrad_acc(g, rec["inp"][i], dy[i])
+            dwf, bwf, accf = O.mnn_conv_wgrad(g, rec["inp"][i], dy[i], O.ACC_F32_SEQ, threads)
+            rec["wstats"].insert(0, dict(layer=i, outputs=int(acc.size), guard=int(st.guard),
+                                         overflow=int(st.overflow), f32_int32_diff=int((accf != acc).sum()),
+                                         f32_int8_diff=int((dwf != dw).sum()), bw=bw, bw_f32=bwf))
         rec["dw"].insert(0, dw)
         if i > 0:
-            dx, _, _, _ = O.conv_dgrad(g, dy[i], W[i])
+            if mnn:
+                dx, _, _ = O.mnn_conv_dgrad(g, dy[i], W[i], am, threads)
+            else:
+                dx, _, _, _ = O.conv_dgrad(g, dy[i], W[i])
             pl = layers[i - 1]
             if pl["flatten"]:
                 dx = dx.reshape(rec["p"][i - 1].shape)

@@ -158,86 +158,159 @@ static inline void stat_add(niti_ref_stats* st, int64_t s, int64_t a) {
 /* naive exact-integer restatement                                              */
 /* ---------------------------------------------------------------------------- */
 
+/* The naive loops run over contiguous ranges of their outermost index on niti_ref_set_threads()
+ * pthreads (default 1); each output is still one exact int64 sum, so the thread count changes
+ * nothing but the wall time.  Stats are per-range and summed. */
+static int g_naive_threads = 1;
+void niti_ref_set_threads(int threads) { g_naive_threads = threads < 1 ? 1 : threads > 256 ? 256 : threads; }
+
+typedef void (*range_fn)(const void* ctx, int64_t b0, int64_t b1, niti_ref_stats* st);
+typedef struct {
+    range_fn f;
+    const void* ctx;
+    int64_t b0, b1;
+    niti_ref_stats st;
+} range_job;
+static void* range_worker(void* p) {
+    range_job* J = (range_job*)p;
+    J->f(J->ctx, J->b0, J->b1, &J->st);
+    return NULL;
+}
+static void par_range(int64_t n, range_fn f, const void* ctx, niti_ref_stats* st) {
+    int t = g_naive_threads;
+    if (t > n) t = n > 0 ? (int)n : 1;
+    range_job jobs[256];
+    pthread_t tids[256];
+    for (int i = 0; i < t; ++i) {
+        jobs[i].f = f;
+        jobs[i].ctx = ctx;
+        jobs[i].b0 = n * i / t;
+        jobs[i].b1 = n * (i + 1) / t;
+        jobs[i].st.guard = jobs[i].st.overflow = 0;
+    }
+    if (t == 1) {
+        range_worker(&jobs[0]);
+    } else {
+        for (int i = 0; i < t; ++i) pthread_create(&tids[i], NULL, range_worker, &jobs[i]);
+        for (int i = 0; i < t; ++i) pthread_join(tids[i], NULL);
+    }
+    if (st)
+        for (int i = 0; i < t; ++i) {
+            st->guard += jobs[i].st.guard;
+            st->overflow += jobs[i].st.overflow;
+        }
+}
+
+typedef struct {
+    const niti_ref_geom* g;
+    const int8_t *a, *b;
+    int32_t* acc;
+} conv_ctx;
+
+static void fwd_range(const void* c, int64_t b0, int64_t b1, niti_ref_stats* st) {
+    const conv_ctx* C = (const conv_ctx*)c;
+    const niti_ref_geom* g = C->g;
+    const int8_t *x = C->a, *w = C->b;
+    for (int64_t r = b0; r < b1; ++r) { /* r = n * c_out + co */
+        const int n = (int)(r / g->c_out), co = (int)(r % g->c_out);
+        for (int oy = 0; oy < g->oh; ++oy)
+            for (int ox = 0; ox < g->ow; ++ox) {
+                int64_t s = 0, a = 0;
+                for (int ci = 0; ci < g->c_in; ++ci)
+                    for (int ky = 0; ky < g->kh; ++ky) {
+                        const int iy = oy * g->stride_h - g->pad_t + ky * g->dilate_h;
+                        if (iy < 0 || iy >= g->h) continue;
+                        for (int kx = 0; kx < g->kw; ++kx) {
+                            const int ix = ox * g->stride_w - g->pad_l + kx * g->dilate_w;
+                            if (ix < 0 || ix >= g->w) continue;
+                            const int32_t p = (int32_t)x[(((int64_t)n * g->c_in + ci) * g->h + iy) * g->w + ix] *
+                                              (int32_t)w[(((int64_t)co * g->c_in + ci) * g->kh + ky) * g->kw + kx];
+                            s += p;
+                            a += p < 0 ? -p : p;
+                        }
+                    }
+                stat_add(st, s, a);
+                C->acc[(((int64_t)n * g->c_out + co) * g->oh + oy) * g->ow + ox] = (int32_t)(uint32_t)s;
+            }
+    }
+}
+
 void niti_ref_conv_fwd_acc(const niti_ref_geom* g, const int8_t* x, const int8_t* w, int32_t* acc,
                            niti_ref_stats* st) {
-    for (int n = 0; n < g->n; ++n)
-        for (int co = 0; co < g->c_out; ++co)
-            for (int oy = 0; oy < g->oh; ++oy)
-                for (int ox = 0; ox < g->ow; ++ox) {
-                    int64_t s = 0, a = 0;
-                    for (int ci = 0; ci < g->c_in; ++ci)
-                        for (int ky = 0; ky < g->kh; ++ky) {
-                            const int iy = oy * g->stride_h - g->pad_t + ky * g->dilate_h;
-                            if (iy < 0 || iy >= g->h) continue;
-                            for (int kx = 0; kx < g->kw; ++kx) {
-                                const int ix = ox * g->stride_w - g->pad_l + kx * g->dilate_w;
-                                if (ix < 0 || ix >= g->w) continue;
-                                const int32_t p =
-                                    (int32_t)x[(((int64_t)n * g->c_in + ci) * g->h + iy) * g->w + ix] *
-                                    (int32_t)w[(((int64_t)co * g->c_in + ci) * g->kh + ky) * g->kw + kx];
-                                s += p;
-                                a += p < 0 ? -p : p;
-                            }
+    const conv_ctx c = {g, x, w, acc};
+    par_range((int64_t)g->n * g->c_out, fwd_range, &c, st);
+}
+
+static void wgrad_range(const void* c, int64_t b0, int64_t b1, niti_ref_stats* st) {
+    const conv_ctx* C = (const conv_ctx*)c;
+    const niti_ref_geom* g = C->g;
+    const int8_t *x = C->a, *dy = C->b;
+    for (int64_t r = b0; r < b1; ++r) { /* r = co * c_in + ci */
+        const int co = (int)(r / g->c_in), ci = (int)(r % g->c_in);
+        for (int ky = 0; ky < g->kh; ++ky)
+            for (int kx = 0; kx < g->kw; ++kx) {
+                int64_t s = 0, a = 0;
+                for (int n = 0; n < g->n; ++n)
+                    for (int oy = 0; oy < g->oh; ++oy) {
+                        const int iy = oy * g->stride_h - g->pad_t + ky * g->dilate_h;
+                        if (iy < 0 || iy >= g->h) continue;
+                        for (int ox = 0; ox < g->ow; ++ox) {
+                            const int ix = ox * g->stride_w - g->pad_l + kx * g->dilate_w;
+                            if (ix < 0 || ix >= g->w) continue;
+                            const int32_t p = (int32_t)x[(((int64_t)n * g->c_in + ci) * g->h + iy) * g->w + ix] *
+                                              (int32_t)dy[(((int64_t)n * g->c_out + co) * g->oh + oy) * g->ow + ox];
+                            s += p;
+                            a += p < 0 ? -p : p;
                         }
-                    stat_add(st, s, a);
-                    acc[(((int64_t)n * g->c_out + co) * g->oh + oy) * g->ow + ox] = (int32_t)(uint32_t)s;
-                }
+                    }
+                stat_add(st, s, a);
+                C->acc[(((int64_t)co * g->c_in + ci) * g->kh + ky) * g->kw + kx] = (int32_t)(uint32_t)s;
+            }
+    }
 }
 
 void niti_ref_conv_wgrad_acc(const niti_ref_geom* g, const int8_t* x, const int8_t* dy, int32_t* acc,
                              niti_ref_stats* st) {
-    for (int co = 0; co < g->c_out; ++co)
-        for (int ci = 0; ci < g->c_in; ++ci)
-            for (int ky = 0; ky < g->kh; ++ky)
-                for (int kx = 0; kx < g->kw; ++kx) {
-                    int64_t s = 0, a = 0;
-                    for (int n = 0; n < g->n; ++n)
-                        for (int oy = 0; oy < g->oh; ++oy) {
-                            const int iy = oy * g->stride_h - g->pad_t + ky * g->dilate_h;
-                            if (iy < 0 || iy >= g->h) continue;
-                            for (int ox = 0; ox < g->ow; ++ox) {
-                                const int ix = ox * g->stride_w - g->pad_l + kx * g->dilate_w;
-                                if (ix < 0 || ix >= g->w) continue;
-                                const int32_t p =
-                                    (int32_t)x[(((int64_t)n * g->c_in + ci) * g->h + iy) * g->w + ix] *
-                                    (int32_t)dy[(((int64_t)n * g->c_out + co) * g->oh + oy) * g->ow + ox];
-                                s += p;
-                                a += p < 0 ? -p : p;
-                            }
+    const conv_ctx c = {g, x, dy, acc};
+    par_range((int64_t)g->c_out * g->c_in, wgrad_range, &c, st);
+}
+
+static void dgrad_range(const void* c, int64_t b0, int64_t b1, niti_ref_stats* st) {
+    const conv_ctx* C = (const conv_ctx*)c;
+    const niti_ref_geom* g = C->g;
+    const int8_t *dy = C->a, *w = C->b;
+    for (int64_t r = b0; r < b1; ++r) { /* r = n * c_in + ci */
+        const int n = (int)(r / g->c_in), ci = (int)(r % g->c_in);
+        for (int iy = 0; iy < g->h; ++iy)
+            for (int ix = 0; ix < g->w; ++ix) {
+                int64_t s = 0, a = 0;
+                for (int co = 0; co < g->c_out; ++co)
+                    for (int ky = 0; ky < g->kh; ++ky) {
+                        const int ty = iy + g->pad_t - ky * g->dilate_h;
+                        if (ty < 0 || ty % g->stride_h) continue;
+                        const int oy = ty / g->stride_h;
+                        if (oy >= g->oh) continue;
+                        for (int kx = 0; kx < g->kw; ++kx) {
+                            const int tx = ix + g->pad_l - kx * g->dilate_w;
+                            if (tx < 0 || tx % g->stride_w) continue;
+                            const int ox = tx / g->stride_w;
+                            if (ox >= g->ow) continue;
+                            const int32_t p = (int32_t)dy[(((int64_t)n * g->c_out + co) * g->oh + oy) * g->ow + ox] *
+                                              (int32_t)w[(((int64_t)co * g->c_in + ci) * g->kh + ky) * g->kw + kx];
+                            s += p;
+                            a += p < 0 ? -p : p;
                         }
-                    stat_add(st, s, a);
-                    acc[(((int64_t)co * g->c_in + ci) * g->kh + ky) * g->kw + kx] = (int32_t)(uint32_t)s;
-                }
+                    }
+                stat_add(st, s, a);
+                C->acc[(((int64_t)n * g->c_in + ci) * g->h + iy) * g->w + ix] = (int32_t)(uint32_t)s;
+            }
+    }
 }
 
 void niti_ref_conv_dgrad_acc(const niti_ref_geom* g, const int8_t* dy, const int8_t* w, int32_t* acc,
                              niti_ref_stats* st) {
-    for (int n = 0; n < g->n; ++n)
-        for (int ci = 0; ci < g->c_in; ++ci)
-            for (int iy = 0; iy < g->h; ++iy)
-                for (int ix = 0; ix < g->w; ++ix) {
-                    int64_t s = 0, a = 0;
-                    for (int co = 0; co < g->c_out; ++co)
-                        for (int ky = 0; ky < g->kh; ++ky) {
-                            const int ty = iy + g->pad_t - ky * g->dilate_h;
-                            if (ty < 0 || ty % g->stride_h) continue;
-                            const int oy = ty / g->stride_h;
-                            if (oy >= g->oh) continue;
-                            for (int kx = 0; kx < g->kw; ++kx) {
-                                const int tx = ix + g->pad_l - kx * g->dilate_w;
-                                if (tx < 0 || tx % g->stride_w) continue;
-                                const int ox = tx / g->stride_w;
-                                if (ox >= g->ow) continue;
-                                const int32_t p =
-                                    (int32_t)dy[(((int64_t)n * g->c_out + co) * g->oh + oy) * g->ow + ox] *
-                                    (int32_t)w[(((int64_t)co * g->c_in + ci) * g->kh + ky) * g->kw + kx];
-                                s += p;
-                                a += p < 0 ? -p : p;
-                            }
-                        }
-                    stat_add(st, s, a);
-                    acc[(((int64_t)n * g->c_in + ci) * g->h + iy) * g->w + ix] = (int32_t)(uint32_t)s;
-                }
+    const conv_ctx c = {g, dy, w, acc};
+    par_range((int64_t)g->n * g->c_in, dgrad_range, &c, st);
 }
 
 void niti_ref_matmul_acc(int m, int o, int k, const int8_t* B, const int8_t* A, int32_t* acc,

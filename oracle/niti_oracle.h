@@ -74,6 +74,8 @@ typedef struct niti_ref_stats {
 
 /* ---------------- naive exact-integer restatement (NCHW / OIHW) ---------------- */
 /* acc[n][co][oy][ox] = sum_{ci,ky,kx} x[n][ci][iy][ix] * w[co][ci][ky][kx]   (NITI_Conv_Int8.cpp:162-249) */
+/* threads used by the naive restatement (results do not depend on it; default 1) */
+void niti_ref_set_threads(int threads);
 void niti_ref_conv_fwd_acc(const niti_ref_geom* g, const int8_t* x, const int8_t* w, int32_t* acc,
                            niti_ref_stats* st);
 /* acc[co][ci][ky][kx] = sum_{n,oy,ox} x[n][ci][iy][ix] * dy[n][co][oy][ox]

@@ -86,6 +86,7 @@ def _declare(L):
         "niti_ref_sgd_update": (None, [vp, vp, i64]),
         "niti_ref_quantize_input": (i32, [vp, i64, vp]),
         "niti_ref_image_stats": (None, [vp, i64, vp]),
+        "niti_ref_set_threads": (None, [C.c_int]),
         "niti_ref_image_quantize": (i32, [vp, i64, vp, i64, vp]),
         "niti_ref_layer_step": (C.c_int, [gp, vp, vp, vp, vp, vp, vp, C.c_int, C.c_int]),
     }
@@ -151,6 +152,11 @@ def requant_matmul(acc):
 
 
 # ----------------------------------------------------------------------------- naive exact
+def set_threads(n: int):
+    """pthreads of the naive restatement (results independent of it)."""
+    lib().niti_ref_set_threads(int(n))
+
+
 def conv_fwd_acc(g: Geom, x, w):
     x, w = _c(x, np.int8), _c(w, np.int8)
     acc = np.empty((g.n, g.c_out, g.oh, g.ow), np.int32)
