@@ -85,7 +85,7 @@ def main():
     ap.add_argument("--arch", default="vgg11", choices=["vgg11", "lenet", "vgg16"])
     ap.add_argument("--in-hw", type=int, default=0, help="input resolution (0: the architecture's own)")
     ap.add_argument("--cpu-sample", type=int, default=-1, help="images in the CPU baseline sample "
-                                                               "(-1: 64 VGG-11, 256 LeNet, 0 VGG-16 = skip)")
+                                                               "(-1: 128 VGG-11, 512 LeNet, 0 VGG-16 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=4, help="first CPU leg (reference default: MnistUtils.cpp:43); "
                                                                "the second leg uses every core of this process")
     ap.add_argument("--int8-input", action="store_true", help="feed pre-quantised int8 x with a fixed exponent "
@@ -118,7 +118,7 @@ def main():
     if args.batch <= 0:
         args.batch = 64 if arch == niti_amd.ARCH_VGG16 else 256
     if args.cpu_sample < 0:
-        args.cpu_sample = {niti_amd.ARCH_VGG16: 0, niti_amd.ARCH_LENET: 256}.get(arch, 64)
+        args.cpu_sample = {niti_amd.ARCH_VGG16: 0, niti_amd.ARCH_LENET: 512}.get(arch, 128)
     model = NitiModel(arch, args.batch, args.in_hw)
     model.set_graph(args.graph)
     model.set_overlap(not args.no_overlap)
