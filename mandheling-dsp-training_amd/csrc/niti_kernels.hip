@@ -1236,7 +1236,10 @@ struct TapGroup {
 #define NITI_TAPS_STAGES1 4  // pipeline stages of the one-DMA-per-wave (XPW 1) kernel
 #endif
 #ifndef NITI_TAPS_NT
-#define NITI_TAPS_NT 0  // nontemporal (L2-bypassing) stores of the int32 tile
+#define NITI_TAPS_NT 0  // nontemporal (L2-bypassing) stores of the int32 tile (2: write-through sc1)
+#endif
+#ifndef NITI_TAPS_PRIO
+#define NITI_TAPS_PRIO 0  // s_setprio 1 for the second-dispatched half (waves 4-7) over the K loop
 #endif
 
 template <int NT, int XPW, int MODE>
@@ -1437,6 +1440,7 @@ __global__ void __launch_bounds__(TAPS_THREADS) wgrad_taps_kernel(WgTaps g, Epi 
             }(std::make_integer_sequence<int, NX>());
         }
         TAPS_STAMP(1);
+        if (NITI_TAPS_PRIO && wid >= 4) __builtin_amdgcn_s_setprio(1);
         // steady state: STAGES straight-line steps per iteration while every step has its DMA;
         // then the tail with run-time conditions
         int s = 0;
@@ -1451,6 +1455,7 @@ __global__ void __launch_bounds__(TAPS_THREADS) wgrad_taps_kernel(WgTaps g, Epi 
             }(std::make_integer_sequence<int, STAGES>());
         }
         lgkm_wait<0>();
+        if (NITI_TAPS_PRIO && wid >= 4) __builtin_amdgcn_s_setprio(0);
         __syncthreads();
         TAPS_STAMP(2);
 
@@ -1525,6 +1530,8 @@ __global__ void __launch_bounds__(TAPS_THREADS) wgrad_taps_kernel(WgTaps g, Epi 
                                     : (v4i*)(Cs + (int64_t)(co0 + row) * epi.ldc + t * g.CIP + ci0 + part * 4);
         if (NITI_ABLATE >= 5)  // diagnostic: no tile stores (timing of the rest)
             asm volatile("" ::"v"(v), "v"(dst));
+        else if (NITI_TAPS_NT == 2)
+            asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(dst), "v"(v) : "memory");
         else if (NITI_TAPS_NT)
             __builtin_nontemporal_store(v, dst);
         else

@@ -13,6 +13,7 @@
 // accumulator with SUM before it is requantised, so N ranks of batch b reproduce one device of
 // batch N*b bit for bit.
 #include <rccl/rccl.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -341,7 +342,17 @@ struct Model {
     size_t ws_bytes_for(int op) const { return op == PLAN_WGRAD ? slab_w_bytes : slab_bytes; }
     int ensure_streams() {
         if (side) return NITI_NO_ERROR;
-        if (hipStreamCreateWithFlags(&side, hipStreamNonBlocking) != hipSuccess) return NITI_NO_EXECUTION;
+        // NITI_DIAG_SIDE_PRIORITY (diagnostics): -1 high / 1 low priority for the weight-gradient stream
+        int prio = 0;
+        if (const char* f = getenv("NITI_DIAG_SIDE_PRIORITY")) prio = atoi(f);
+        int lo = 0, hi = 0;
+        (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+        if (prio != 0) {
+            if (hipStreamCreateWithPriority(&side, hipStreamNonBlocking, prio < 0 ? hi : lo) != hipSuccess)
+                return NITI_NO_EXECUTION;
+        } else if (hipStreamCreateWithFlags(&side, hipStreamNonBlocking) != hipSuccess) {
+            return NITI_NO_EXECUTION;
+        }
         // cross-stream hand-offs on one device need a device-scope release only (the default
         // system-scope fence writes back and invalidates the caches: ~7 us per record, measured)
         constexpr unsigned kFlags = hipEventDisableTiming | hipEventReleaseToDevice;
