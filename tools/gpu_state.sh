@@ -1,0 +1,10 @@
+# Full GPU suite + smoke + default bench at the current tree (one call).
+set -u
+cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
+TAG=${TAG:-r02b}
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/gpu_tests_$TAG.log 2>&1
+rc=$?; tail -4 gpurun_out/gpu_tests_$TAG.log; echo "pytest rc=$rc"; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1
+rc=$?; tail -2 gpurun_out/smoke_$TAG.log; echo "smoke rc=$rc"; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 400 python3 bench.py > gpurun_out/bench_$TAG.log 2>&1
+rc=$?; echo "bench rc=$rc"; grep metric gpurun_out/bench_$TAG.log; exit $rc
