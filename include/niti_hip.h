@@ -211,6 +211,20 @@ int niti_conv_dgrad_acc(const niti_geom* g, const int8_t* dy_nhwc16, const int8_
  * over the pixels whose operand tiles are transposed in LDS (ds_read_b64_tr_b8) */
 int niti_conv_wgrad_acc(const niti_geom* g, const int8_t* x_nhwc16, const int8_t* dy_nhwc16, int32_t* acc,
                         uint32_t* amax, void* workspace, size_t workspace_bytes, void* stream);
+/* P16 pixel blocks: an activation of P pixels (P % 16 == 0) and Cp channels as [P/16][Cp][16], so the
+ * 16 consecutive pixels of one channel are 16 contiguous bytes -- the MFMA operand fragment of the
+ * weight gradient, loaded straight into registers. */
+int niti_nhwc16_to_p16(const int8_t* in_nhwc16, int64_t pixels, int cp, int8_t* out_p16, void* stream);
+/* Weight gradient on P16 operands (3x3, stride 1, pad 1, Cip % 32 == 0, Cop % 32 == 0, n*oh*ow % 32 == 0,
+ * ow in {2, 4, 8, 16} with oh = ow for 2 and 4, oh even for 8):
+ * acc[co][kh][kw][cip] int32 (rows < c_out written) and, if amax, its range.  splits <= 0 picks the
+ * default.  The workspace holds the split-K partials (niti_conv_wgrad_p16_workspace bytes, 0 without a
+ * split).  NOT_SUPPORT for other geometries. */
+int niti_conv_wgrad_p16_workspace(const niti_geom* g, int splits, size_t* bytes);
+/* diagnostics: device buffer (8 u64 per block) for the per-block stamps of stamp builds; NULL disarms */
+void niti_diag_wgrad_stamps(void* buf);
+int niti_conv_wgrad_p16_acc(const niti_geom* g, const int8_t* x_p16, const int8_t* dy_p16, int32_t* acc,
+                            uint32_t* amax, void* workspace, size_t workspace_bytes, int splits, void* stream);
 /* acc[m][ldc] = sum_k B[m][k] A[o][k] (columns o..ldc = 0); K zero padded to k16; ldb/lda bytes */
 int niti_matmul_acc(int m, int o, int k16, const int8_t* B, int64_t ldb, const int8_t* A, int64_t lda,
                     int32_t* acc, int64_t ldc, uint32_t* amax, void* workspace, size_t workspace_bytes,

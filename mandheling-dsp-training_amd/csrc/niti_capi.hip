@@ -161,6 +161,33 @@ int niti_conv_wgrad_acc(const niti_geom* g, const int8_t* x, const int8_t* dy, i
     return code(niti::conv_wgrad_acc(r, x, dy, acc, amax, ws, ws_bytes, S(stream)));
 }
 
+int niti_nhwc16_to_p16(const int8_t* in, int64_t pixels, int cp, int8_t* out, void* stream) {
+    if (!in || !out || pixels <= 0 || pixels % 16 || cp <= 0 || cp % 16) return NITI_INVALID_VALUE;
+    return code(niti::nhwc16_to_p16(in, pixels, cp, out, S(stream)));
+}
+
+void niti_diag_wgrad_stamps(void* buf) { niti::wgrad_stamps_arm((unsigned long long*)buf); }
+
+int niti_conv_wgrad_p16_workspace(const niti_geom* g, int splits, size_t* bytes) {
+    if (!g || !bytes) return NITI_INVALID_VALUE;
+    niti::ConvGeom r;
+    if (!to_geom(g, &r)) return NITI_COMPUTE_SIZE_ERROR;
+    if (!niti::conv_wgrad_p16_ok(r)) return NITI_NOT_SUPPORT;
+    *bytes = niti::conv_wgrad_p16_workspace(r, splits);
+    return NITI_NO_ERROR;
+}
+
+int niti_conv_wgrad_p16_acc(const niti_geom* g, const int8_t* x, const int8_t* dy, int32_t* acc, uint32_t* amax,
+                            void* ws, size_t ws_bytes, int splits, void* stream) {
+    if (!g || !x || !dy || !acc) return NITI_INVALID_VALUE;
+    niti::ConvGeom r;
+    if (!to_geom(g, &r)) return NITI_COMPUTE_SIZE_ERROR;
+    if (!niti::conv_wgrad_p16_ok(r)) return NITI_NOT_SUPPORT;
+    if (splits <= 0) splits = niti::conv_wgrad_p16_splits(r);
+    if (ws_bytes < niti::conv_wgrad_p16_workspace(r, splits) || (ws_bytes > 0 && !ws)) return NITI_INVALID_VALUE;
+    return code(niti::conv_wgrad_p16(r, x, dy, acc, amax, ws, ws_bytes, splits, S(stream)));
+}
+
 int niti_matmul_acc(int m, int o, int k16, const int8_t* B, int64_t ldb, const int8_t* A, int64_t lda, int32_t* acc,
                     int64_t ldc, uint32_t* amax, void* ws, size_t ws_bytes, void* stream) {
     if (k16 % 16 || ldb % 16 || lda % 16 || ldc % 16 || ldc < o) return NITI_INVALID_VALUE;

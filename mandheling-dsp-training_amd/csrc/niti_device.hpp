@@ -1,0 +1,151 @@
+// niti_device.hpp -- gfx950 device helpers shared by the kernel translation units
+// (niti_kernels.hip, niti_wgrad.hip): buffer resources and LDS-DMA, counted waits,
+// transposed LDS reads, multiply-shift division, the range-estimate max words and the
+// XCD-aware block remap.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "niti_kernels.hpp"
+
+namespace niti {
+
+typedef int v2i __attribute__((ext_vector_type(2)));
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v16i __attribute__((ext_vector_type(16)));
+typedef signed char v16c __attribute__((ext_vector_type(16)));
+
+// byte offset that reads zeros through the buffer range check
+constexpr uint32_t OOB = 0x80000000u;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ v4i buf_load16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_bit_cast(v4i, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0));
+}
+
+// multiply-shift division for 0 <= n < 2^31 (Granlund-Montgomery, round-up variant)
+struct FastDiv {
+    uint32_t m = 1, s = 0, d = 1;
+};
+static inline FastDiv make_fastdiv(uint32_t d) {
+    FastDiv f;
+    f.d = d;
+    f.s = 0;
+    while ((1ull << f.s) < d) ++f.s;
+    f.m = (uint32_t)((((uint64_t)1 << 32) * ((1ull << f.s) - d)) / d + 1);
+    return f;
+}
+__device__ __forceinline__ uint32_t fdiv(const FastDiv& f, uint32_t n) { return (__umulhi(n, f.m) + n) >> f.s; }
+
+__device__ __forceinline__ uint32_t uabs32(int v) { return v < 0 ? 0u - (uint32_t)v : (uint32_t)v; }
+
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint32_t t = __shfl_xor(v, o, 64);
+        v = v > t ? v : t;
+    }
+    return v;
+}
+
+// One atomic per workgroup, skipped when the word already holds a larger value (the
+// single max word is otherwise a serialisation point for thousands of workgroups).
+// A range is MAX_SLOTS words on separate 128-byte lines: each block publishes into one slot
+// (spread by block id), so no line sees more than grid/MAX_SLOTS atomics.  With one word,
+// every block of a launch whose blocks all finish together (2048 reduce blocks) read 0 and
+// queued its atomic on the same line: ~25 us of serialised atomics per launch.
+__device__ __forceinline__ void publish_max(uint32_t* amax, uint32_t m) {
+    if (m == 0u) return;
+    const uint32_t slot = (blockIdx.x + blockIdx.y * 13u + blockIdx.z * 7u) & (MAX_SLOTS - 1);
+    uint32_t* w = amax + slot * MAX_SLOT_STRIDE;
+    if (m > __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(w, m);
+}
+// max|acc| of a range: the max over its slots, one slot per lane (call with the whole wave
+// active; read after a kernel boundary or collective)
+__device__ __forceinline__ uint32_t read_max(const uint32_t* amax) {
+    static_assert(MAX_SLOTS == 64, "one slot per lane");
+    return wave_max(amax[(threadIdx.x & 63) * MAX_SLOT_STRIDE]);
+}
+
+// kernel-span probe: first block start / last block end on the device wall clock
+__device__ __forceinline__ void span_begin(unsigned long long* span) {
+    if (span != nullptr && threadIdx.x == 0) atomicMin(span, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+}
+__device__ __forceinline__ void span_end(unsigned long long* span) {
+    if (span != nullptr) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) atomicMax(span + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    }
+}
+
+// bijective XCD remap: blocks b, b+8, b+16, ... (one XCD under round-robin dispatch) get
+// consecutive tile ids.  Speed only; any placement is correct.
+__device__ __forceinline__ int xcd_remap(int b, int nwg) {
+    const int xcd = b & 7, q = nwg >> 3, r = nwg & 7;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// wait until at most `later` steps of this wave's loads (L each) are outstanding
+template <int L, int MAXL>
+__device__ __forceinline__ void wait_steps(int later) {
+    if (MAXL >= 6 && later >= 6)
+        wait_vmcnt<6 * L>();
+    else if (MAXL >= 5 && later == 5)
+        wait_vmcnt<5 * L>();
+    else if (MAXL >= 4 && later == 4)
+        wait_vmcnt<4 * L>();
+    else if (MAXL >= 3 && later == 3)
+        wait_vmcnt<3 * L>();
+    else if (MAXL >= 2 && later == 2)
+        wait_vmcnt<2 * L>();
+    else if (MAXL >= 1 && later == 1)
+        wait_vmcnt<L>();
+    else
+        wait_vmcnt<0>();
+}
+
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+__device__ __forceinline__ v4i lds_b128(uint32_t a) {
+    v4i r;
+    asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"(a));
+    return r;
+}
+// two transposed 8x8-byte reads, rows r and r+8 (ROW8 = 8 rows of the image in bytes)
+__device__ __forceinline__ v4i lds_tr8x2(uint32_t a, int row8) {
+    v2i x0, x1;
+    asm volatile("ds_read_b64_tr_b8 %0, %1" : "=v"(x0) : "v"(a));
+    asm volatile("ds_read_b64_tr_b8 %0, %1" : "=v"(x1) : "v"(a + row8));
+    return v4i{x0[0], x0[1], x1[0], x1[1]};
+}
+// one transposed read at a compile-time immediate offset
+template <int IMM>
+__device__ __forceinline__ v2i tr8_at(uint32_t a) {
+    v2i r;
+    asm volatile("ds_read_b64_tr_b8 %0, %1 offset:%2" : "=v"(r) : "v"(a), "n"(IMM));
+    return r;
+}
+template <int N>
+__device__ __forceinline__ void lgkm_wait() {
+    asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N < 15 ? N : 15));
+}
+// orders a use of v after the preceding (volatile) wait
+__device__ __forceinline__ void reg_fence(v4i& v) { asm volatile("" : "+v"(v)); }
+
+// LDS-DMA: 16 bytes per lane from the buffer into the wave's 1 KiB LDS block (lane-linear)
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, int8_t* lds_wave_base, uint32_t voff, uint32_t soff) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_wave_base, 16, voff,
+                                             soff, 0, 0);
+}
+
+}  // namespace niti

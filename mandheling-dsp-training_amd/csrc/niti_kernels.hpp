@@ -99,6 +99,21 @@ void probe_events_arm(hipEvent_t begin, hipEvent_t end);
 // a K-major GEMM over pixels whose operand tiles are transposed in LDS (ds_read_b64_tr_b8)
 hipError_t conv_wgrad_acc(const ConvGeom& g, const int8_t* x_nhwc16, const int8_t* dy_nhwc16, int32_t* acc,
                           uint32_t* amax, void* ws, size_t ws_bytes, hipStream_t st, hipEvent_t after_gemm = nullptr);
+// C[i] = sum over z < splits of slab[z * stride + i] (+ max|C| into amax); n % 4 == 0
+hipError_t splitk_reduce_linear(const int32_t* slab, int splits, int64_t n, int64_t stride, int32_t* C,
+                                uint32_t* amax, hipStream_t st);
+// ---- weight gradient on P16 pixel blocks (niti_wgrad.hip) --------------------------------
+// P16: [pixels/16][Cp][16] int8 (Cp % 16 == 0, pixels % 16 == 0)
+hipError_t nhwc16_to_p16(const int8_t* in, int64_t pixels, int cp, int8_t* out, hipStream_t st);
+bool conv_wgrad_p16_ok(const ConvGeom& g);
+// diagnostic builds (NITI_WG_STAMPS): per-block stamps of the following launches, 8 u64 per block
+void wgrad_stamps_arm(unsigned long long* buf);
+int conv_wgrad_p16_splits(const ConvGeom& g);
+// workspace: the split-K partial slabs (0 bytes when the plan does not split)
+size_t conv_wgrad_p16_workspace(const ConvGeom& g, int splits);
+hipError_t conv_wgrad_p16(const ConvGeom& g, const int8_t* x_p16, const int8_t* dy_p16, int32_t* acc,
+                          uint32_t* amax, void* ws, size_t ws_bytes, int splits, hipStream_t st,
+                          hipEvent_t ev_b = nullptr, hipEvent_t ev_e = nullptr, unsigned long long* span = nullptr);
 // acc[m][o] = sum_k B[m][k] * A[o][k] (NITI_Matmul_Int8); k16 multiple of 16 (zero padded rows),
 // ldb/lda bytes, ldc elements (multiple of 16; columns o..ldc come out 0)
 hipError_t matmul_acc(int M, int O, int k16, const int8_t* B, int64_t ldb, const int8_t* A, int64_t lda,

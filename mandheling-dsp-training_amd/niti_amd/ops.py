@@ -201,6 +201,33 @@ def conv_wgrad_acc(g: L.Geom, xT, dyT, amax=None, stream=None):
     return acc
 
 
+def nhwc16_to_p16(x16: torch.Tensor, stream=None):
+    """NHWC16 [N][H][W][Cp] -> P16 pixel blocks [N*H*W/16][Cp][16]."""
+    cp = x16.shape[-1]
+    px = x16.numel() // cp
+    out = torch.empty((px // 16, cp, 16), dtype=torch.int8, device=x16.device)
+    check(L.lib().niti_nhwc16_to_p16(_ptr(x16), px, cp, _ptr(out), _stream(stream)), "nhwc16->p16")
+    return out
+
+
+def wgrad_p16_workspace(g: L.Geom, splits: int = 0, device="cuda"):
+    n = C.c_size_t()
+    check(L.lib().niti_conv_wgrad_p16_workspace(C.byref(g), splits, C.byref(n)), "p16 workspace")
+    return torch.zeros(max(int(n.value), 16), dtype=torch.uint8, device=device), int(n.value)
+
+
+def conv_wgrad_p16_acc(g: L.Geom, xP, dyP, amax=None, splits: int = 0, ws=None, stream=None):
+    """Weight gradient acc[co][kh][kw][cip] from P16 operands (niti_wgrad.hip); rows >= c_out stay 0."""
+    acc = torch.zeros((g.c_out, g.kh, g.kw, g.cip), dtype=torch.int32, device=xP.device)
+    if ws is None:
+        ws, nb = wgrad_p16_workspace(g, splits, xP.device)
+    else:
+        nb = ws.numel()
+    check(L.lib().niti_conv_wgrad_p16_acc(C.byref(g), _ptr(xP), _ptr(dyP), _ptr(acc), _ptr(amax), _ptr(ws), nb,
+                                          splits, _stream(stream)), "conv_wgrad_p16_acc")
+    return acc
+
+
 def matmul_acc(B16, A16, ldc, amax=None, use_workspace=True, stream=None):
     m, k16 = B16.shape
     o = A16.shape[0]
