@@ -141,6 +141,7 @@ __device__ __forceinline__ void lgkm_wait() {
 }
 // orders a use of v after the preceding (volatile) wait
 __device__ __forceinline__ void reg_fence(v4i& v) { asm volatile("" : "+v"(v)); }
+__device__ __forceinline__ void reg_fence(v2i& v) { asm volatile("" : "+v"(v)); }
 
 // LDS-DMA: 16 bytes per lane from the buffer into the wave's 1 KiB LDS block (lane-linear)
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, int8_t* lds_wave_base, uint32_t voff, uint32_t soff) {

@@ -1499,12 +1499,16 @@ void plan_override_clear_all() {
     std::lock_guard<std::mutex> lk(g_plan_mu);
     g_plan_tab.clear();
 }
-static bool plan_override_get(const PlanKey& k, PlanChoice* c) {
+bool plan_override_lookup(const PlanKey& k, PlanChoice* c) {
     std::lock_guard<std::mutex> lk(g_plan_mu);
     auto it = g_plan_tab.find(k);
     if (it == g_plan_tab.end()) return false;
     *c = it->second;
     return true;
+}
+// the NHWC16 planners ignore P16 weight-gradient plans (the model runs those itself)
+static bool plan_override_get(const PlanKey& k, PlanChoice* c) {
+    return plan_override_lookup(k, c) && c->bm != PLAN_P16_TILE;
 }
 
 static void plan_slab(GemmPlan& p, int s, int k_total, int k_step, int steps, bool recompute, int M, int N,

@@ -71,6 +71,10 @@ struct PlanChoice {
 // bm = bn = PLAN_TAPS_TILE selects the tap-sharing weight-gradient kernel (64 output channels x
 // all taps x 32 input channels per block) where conv_wgrad_taps_ok(g)
 constexpr int PLAN_TAPS_TILE = 32;
+// bm = bn = PLAN_P16_TILE: the P16 weight gradient (niti_wgrad.hip, splits = its K split), which the
+// model runs on P16 copies of x and dy; the NHWC16 entry points ignore such plans
+constexpr int PLAN_P16_TILE = 16;
+bool plan_override_lookup(const PlanKey& k, PlanChoice* c);
 bool conv_wgrad_taps_ok(const ConvGeom& g);
 PlanKey conv_plan_key(int op, const ConvGeom& g);
 // the plan a conv GEMM runs with now (override or default), tap-sharing wgrad included

@@ -215,6 +215,31 @@ struct Model {
     size_t slab_bytes = 0;
     void* slab_w = nullptr; // split-K slabs of the weight-gradient GEMMs (their own stream)
     size_t slab_w_bytes = 0;
+    // P16 copies of the weight-gradient operands (niti_wgrad.hip), reused layer by layer on the
+    // weight-gradient stream
+    int8_t* xp16 = nullptr;
+    int8_t* dp16 = nullptr;
+    // the K split the P16 weight gradient of layer i runs with, 0 when layer i runs on the NHWC16
+    // kernels (a plan override of another tile, or a geometry the P16 kernel does not take)
+    int wgrad_p16_splits(int i) const {
+        const ConvGeom& g = L[i].g;
+        if (!conv_wgrad_p16_ok(g)) return 0;
+        PlanChoice c;
+        if (plan_override_lookup(conv_plan_key(PLAN_WGRAD, g), &c)) return c.bm == PLAN_P16_TILE ? c.splits : 0;
+        return conv_wgrad_p16_splits(g);
+    }
+    // the probed launch's own begin / end events and span slot (P16 weight gradient)
+    void probe_launch(int layer, int phase, hipEvent_t* b, hipEvent_t* e, unsigned long long** sp) {
+        *b = *e = nullptr;
+        *sp = nullptr;
+        if (layer != probe_layer || phase != probe_phase || tuning || capturing) return;
+        if (probe_count < (int)ev0.size()) {
+            *b = ev0[probe_count];
+            *e = ev1[probe_count];
+            ++probe_count;
+        }
+        if (span != nullptr && span_count < span_cap) *sp = span + 2 * span_count++;
+    }
     // The weight gradient of layer i and the input gradient of layer i both read dy_i and
     // nothing else the other writes, so the weight gradients run on a second stream, each
     // released by an event after its dy is produced, and overlap the input-gradient chain
@@ -450,7 +475,7 @@ int Model::build(int arch_, int batch_, int in_hw) {
     const int n = batch;
     x0 = (int8_t*)ws.alloc((size_t)n * in_h * in_w * round_up(in_c, 16));
     exp0 = (int8_t*)ws.alloc(16);
-    size_t acc_elems = 0;
+    size_t acc_elems = 0, p16x = 0, p16d = 0;
     const int nl = (int)L.size();
     for (int i = 0; i < nl; ++i) {
         Layer& l = L[i];
@@ -482,6 +507,11 @@ int Model::build(int arch_, int batch_, int in_hw) {
         slab_bytes = std::max(slab_bytes, conv_fwd_workspace(g));
         slab_bytes = std::max(slab_bytes, conv_dgrad_workspace(g));
         slab_w_bytes = std::max(slab_w_bytes, conv_wgrad_workspace(g));
+        if (conv_wgrad_p16_ok(g)) {
+            slab_w_bytes = std::max(slab_w_bytes, conv_wgrad_p16_workspace(g, 8));
+            p16x = std::max(p16x, (size_t)n * g.h * g.w * g.cip);
+            p16d = std::max(p16d, out_px * g.cop);
+        }
         // layer input / its C alignment with the previous output
         if (i == 0) {
             l.in = x0;
@@ -491,6 +521,11 @@ int Model::build(int arch_, int batch_, int in_hw) {
         }
     }
     acc = (int32_t*)ws.alloc(acc_elems * 4);
+    if (p16x) {
+        xp16 = (int8_t*)ws.alloc(p16x);
+        dp16 = (int8_t*)ws.alloc(p16d);
+        if (!xp16 || !dp16) return NITI_OUT_OF_MEMORY;
+    }
     qstats = (unsigned long long*)ws.alloc(64);
     if (!qstats) return NITI_OUT_OF_MEMORY;
     if (slab_bytes) {
@@ -603,6 +638,17 @@ int Model::wgrad_layer(int i, hipStream_t st) {
     const bool dp = this->dp();
     Layer& l = L[i];
     const ConvGeom& g = l.g;
+    if (const int s = wgrad_p16_splits(i)) {
+        // P16 weight gradient: x and dy to pixel blocks, then the register-fed kernel (+ its
+        // split-K reduce); the probe times the kernel launch itself
+        MTRY(nhwc16_to_p16(l.in, (int64_t)g.n * g.h * g.w, g.cip, xp16, st));
+        MTRY(nhwc16_to_p16(l.dy, (int64_t)g.n * g.oh * g.ow, g.cop, dp16, st));
+        hipEvent_t eb, ee;
+        unsigned long long* sp;
+        probe_launch(i, 2, &eb, &ee, &sp);
+        MTRY(conv_wgrad_p16(g, xp16, dp16, l.dwacc, dp ? nullptr : rng(i, 2), slab_w, slab_w_bytes, s, st, eb, ee, sp));
+        return NITI_NO_ERROR;
+    }
     // the weight-gradient probe brackets the GEMM launch alone (not its split-K reduce)
     // the weight-gradient probe is the GEMM launch's own begin / end (its split-K reduce excluded)
     if (capturing)
@@ -728,9 +774,31 @@ int Model::autotune(hipStream_t st, int reps) {
             plan_override_clear(key);
             const size_t wsb = ws_bytes_for(op);
             PlanChoice best = conv_plan_query(op, g, act, wsb);
+            if (op == PLAN_WGRAD && wgrad_p16_splits(i) > 0) {
+                best.bm = best.bn = PLAN_P16_TILE;
+                best.splits = wgrad_p16_splits(i);
+                best.strat = best.splits > 1 ? 2 : 0;
+            }
             float best_us = 0.f;
             rc = time_op(i, op, &best_us);
             const bool taps = op == PLAN_WGRAD && conv_wgrad_taps_ok(g);
+            if (op == PLAN_WGRAD && conv_wgrad_p16_ok(g)) {
+                for (int sp : {1, 2, 4, 8}) {
+                    if (rc != NITI_NO_ERROR) break;
+                    if (conv_wgrad_p16_workspace(g, sp) > slab_w_bytes) continue;
+                    PlanChoice cand;
+                    cand.bm = cand.bn = PLAN_P16_TILE;
+                    cand.splits = sp;
+                    cand.strat = sp > 1 ? 2 : 0;
+                    plan_override_set(key, cand);
+                    float us = 0.f;
+                    rc = time_op(i, op, &us);
+                    if (rc == NITI_NO_ERROR && us < best_us) {
+                        best_us = us;
+                        best = cand;
+                    }
+                }
+            }
             for (const auto& t : tiles) {
                 if (rc != NITI_NO_ERROR) break;
                 if (t[0] == PLAN_TAPS_TILE && !taps) continue;
@@ -1028,7 +1096,12 @@ int niti_model_plan_info(niti_model_t m, int layer, int phase, int info[4]) {
         return NITI_INVALID_VALUE;
     const niti::ConvGeom& g = m->m.L[layer].g;
     const int op = phase == 0 ? niti::PLAN_FWD : phase == 1 ? niti::PLAN_DGRAD : niti::PLAN_WGRAD;
-    const niti::PlanChoice c = niti::conv_plan_query(op, g, phase != 2, m->m.ws_bytes_for(op));
+    niti::PlanChoice c = niti::conv_plan_query(op, g, phase != 2, m->m.ws_bytes_for(op));
+    if (phase == 2 && m->m.wgrad_p16_splits(layer) > 0) {
+        c.bm = c.bn = niti::PLAN_P16_TILE;
+        c.splits = m->m.wgrad_p16_splits(layer);
+        c.strat = c.splits > 1 ? 2 : 0;
+    }
     info[0] = c.bm;
     info[1] = c.bn;
     info[2] = c.splits;
@@ -1044,17 +1117,24 @@ int niti_model_plan_set(niti_model_t m, int layer, int phase, const int plan[4])
         niti::plan_override_clear(k);
     } else {
         auto tile_ok = [](int t) { return t == 64 || t == 128 || t == 256; };
+        const niti::ConvGeom& g = m->m.L[layer].g;
         const bool taps = plan[0] == niti::PLAN_TAPS_TILE && plan[1] == niti::PLAN_TAPS_TILE &&
-                          op == niti::PLAN_WGRAD && niti::conv_wgrad_taps_ok(m->m.L[layer].g);
-        if ((!taps && (!tile_ok(plan[0]) || !tile_ok(plan[1]))) || plan[2] < 1 || plan[3] < 0 || plan[3] > 2 ||
-            (taps && plan[3] == 1))
+                          op == niti::PLAN_WGRAD && niti::conv_wgrad_taps_ok(g);
+        const bool p16 = plan[0] == niti::PLAN_P16_TILE && plan[1] == niti::PLAN_P16_TILE &&
+                         op == niti::PLAN_WGRAD && niti::conv_wgrad_p16_ok(g);
+        if ((!taps && !p16 && (!tile_ok(plan[0]) || !tile_ok(plan[1]))) || plan[2] < 1 || plan[3] < 0 ||
+            plan[3] > 2 || ((taps || p16) && plan[3] == 1))
             return NITI_INVALID_VALUE;
+        if (p16) {
+            if (plan[2] > 64) return NITI_INVALID_VALUE;
+            if (!m->m.ensure_slab(niti::conv_wgrad_p16_workspace(g, plan[2]), true)) return NITI_OUT_OF_MEMORY;
+        }
         niti::PlanChoice c;
         c.bm = plan[0];
         c.bn = plan[1];
         c.splits = plan[2];
         c.strat = plan[3];
-        if (c.strat == 2 &&
+        if (c.strat == 2 && !p16 &&
             !m->m.ensure_slab(std::min(niti::plan_slab_bytes(k.M, k.N, c.splits), size_t(1) << 30), op == niti::PLAN_WGRAD))
             return NITI_OUT_OF_MEMORY;
         niti::plan_override_set(k, c);

@@ -34,6 +34,7 @@
 #include <hip/hip_ext.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "niti_device.hpp"
 #include "niti_kernels.hpp"
@@ -225,8 +226,11 @@ __global__ void __launch_bounds__(NW * 64) wgrad_p16_kernel(WgP16 g) {
     static_assert(D % KPI == 0, "unrolled steps cover whole images");
     const uint32_t vup_first = h ? ci16 + UPOFF : OOB, vup = lx + UPOFF;
     const uint32_t vdn = lx + xrow, vdn_last = h ? OOB : lx + xrow;
+    // ring slot: dy, the x block, the rows above / below (OW 8: one 8-byte row each)
+    typedef typename std::conditional<OW == 8, v2i, v4i>::type Row;
     struct Ring {
-        v4i d, x, up, dn;
+        v4i d, x;
+        Row up, dn;
     };
     Ring ring[D];
     auto issue = [&](Ring& r, auto u_c, int j) {
@@ -239,10 +243,8 @@ __global__ void __launch_bounds__(NW * 64) wgrad_p16_kernel(WgP16 g) {
         if constexpr (NB) {
             constexpr bool first = U % KPI == 0, last = U % KPI == KPI - 1;
             if constexpr (OW == 8) {
-                const v2i u = first ? asm_load8(rX, vup_first, sx) : asm_load8(rX, vup, sx - xrow);
-                const v2i w = asm_load8(rX, last ? vdn_last : vdn, sx);
-                r.up = v4i{u[0], u[1], 0, 0};
-                r.dn = v4i{w[0], w[1], 0, 0};
+                r.up = first ? asm_load8(rX, vup_first, sx) : asm_load8(rX, vup, sx - xrow);
+                r.dn = asm_load8(rX, last ? vdn_last : vdn, sx);
             } else {
                 r.up = first ? asm_load16(rX, vup_first, sx) : asm_load16(rX, vup, sx - xrow);
                 r.dn = asm_load16(rX, last ? vdn_last : vdn, sx);
@@ -264,7 +266,15 @@ __global__ void __launch_bounds__(NW * 64) wgrad_p16_kernel(WgP16 g) {
             reg_fence(r.up);
             reg_fence(r.dn);
         }
-        const v4i d = r.d, xc = r.x, up = r.up, dn = r.dn;
+        const v4i d = r.d, xc = r.x;
+        v4i up, dn;
+        if constexpr (OW == 8) {
+            up = v4i{r.up[0], r.up[1], 0, 0};
+            dn = v4i{r.dn[0], r.dn[1], 0, 0};
+        } else if constexpr (OW == 16) {
+            up = r.up;
+            dn = r.dn;
+        }
         [&]<int... T>(std::integer_sequence<int, T...>) {
             (([&] {
                  constexpr int KY = T / 3, KX = T % 3;
@@ -285,7 +295,20 @@ __global__ void __launch_bounds__(NW * 64) wgrad_p16_kernel(WgP16 g) {
             (step(std::integral_constant<int, U>(), j0), ...);
         }(std::make_integer_sequence<int, D>());
     }
+    // The last D look-ahead loads (and all of them for a wave without K groups) are never consumed:
+    // to hipcc their destination registers are dead at once, and it may hand them to other values
+    // while the loads are still in flight.  Drain, then touch every ring register, so none of them
+    // is reused before its data has landed.
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int u = 0; u < D; ++u) {
+        reg_fence(ring[u].d);
+        reg_fence(ring[u].x);
+        if constexpr (NB) {
+            reg_fence(ring[u].up);
+            reg_fence(ring[u].dn);
+        }
+    }
     WG_STAMP(2);
 
     // the waves meet: each adds its partial tile into the zeroed LDS tile (ds_add, the two

@@ -117,6 +117,13 @@ class NitiModel:
         Call after one train_step; plans never change results."""
         check(self._lib.niti_model_autotune(self._h, int(reps), _stream(stream)), "autotune")
 
+    def plan(self, layer: int, phase: int):
+        """(bm, bn, splits, strategy) of one layer phase; 32x32 = the tap-sharing weight gradient,
+        16x16 = the P16 weight gradient."""
+        info = (C.c_int * 4)()
+        check(self._lib.niti_model_plan_info(self._h, layer, phase, info), "plan_info")
+        return tuple(info)
+
     def plans(self):
         """{(layer, phase): (bm, bn, splits, strategy)}; phase 0 fwd / 1 input grad / 2 weight grad,
         strategy 0 store / 1 recompute / 2 split-K."""
@@ -125,9 +132,7 @@ class NitiModel:
             for ph in (0, 1, 2):
                 if ph == 1 and i == 0:
                     continue
-                info = (C.c_int * 4)()
-                check(self._lib.niti_model_plan_info(self._h, i, ph, info), "plan_info")
-                out[(i, ph)] = tuple(info)
+                out[(i, ph)] = self.plan(i, ph)
         return out
 
     def set_plan(self, layer: int, phase: int, plan=None):

@@ -75,3 +75,24 @@ def test_no_fallback_when_library_missing(tmp_path, monkeypatch):
     with pytest.raises(ImportError):
         _lib.lib()
     importlib.reload(_lib)
+
+
+def test_wgrad_p16_no_inflight_register_reuse(tmp_path):
+    """The P16 weight-gradient kernel issues its operand loads from inline asm (hipcc does not count
+    them): no instruction may touch a register such a load is still writing.  Compiles
+    niti_wgrad.hip to gfx950 assembly and scans it (tools/isa_inflight.py)."""
+    import os
+    import shutil
+    import subprocess
+    import sys
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    if not os.path.exists(hipcc):
+        pytest.skip("no hipcc")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    src = os.path.join(root, "mandheling-dsp-training_amd", "csrc", "niti_wgrad.hip")
+    asm = tmp_path / "niti_wgrad.s"
+    subprocess.run([hipcc, "--offload-arch=gfx950", "--cuda-device-only", "-O3", "-std=c++20", "-S", src, "-o",
+                    str(asm)], check=True)
+    r = subprocess.run([sys.executable, os.path.join(root, "tools", "isa_inflight.py"), str(asm)],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout

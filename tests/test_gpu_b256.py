@@ -110,3 +110,21 @@ def test_vgg11_b256_taps_split_step_full_parity(T, case, splits):
     finally:
         NitiModel.reset_plans()
     assert plans[(3, 2)][:2] == (32, 32) and plans[(3, 2)][3] == 2
+
+
+@pytest.mark.parametrize("splits", [1, 4])
+def test_vgg11_b256_p16_split_step_full_parity(T, case, splits):
+    """The P16 weight gradient (niti_wgrad.hip) forced on every layer it takes, unsplit and 4-way
+    split-K (partials reduced by splitk_reduce_linear)."""
+    from niti_amd.model import NitiModel
+
+    def force(m):
+        for i in range(len(m.layers)):
+            if m.plan(i, 2)[:2] == (16, 16):
+                m.set_plan(i, 2, (16, 16, splits, 2 if splits > 1 else 0))
+
+    try:
+        plans = _step_and_compare(T, case, force)
+    finally:
+        NitiModel.reset_plans()
+    assert plans[(3, 2)] == (16, 16, splits, 2 if splits > 1 else 0)

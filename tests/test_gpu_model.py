@@ -137,10 +137,14 @@ def test_vgg11_step_autotuned(T):
     assert len(seen) == 3 * 9 - 1
     # The plan contract niti_model_plan_set enforces (niti_model.hip), not which plan won the
     # timing: GEMM tiles are 64..256 wide; the tap-sharing weight-gradient kernel reports 32x32
-    # and runs unsplit (strategy 0) or split-K (strategy 2), never recompute (strategy 1).
+    # and the P16 weight-gradient kernel 16x16, both unsplit (strategy 0) or split-K (strategy 2),
+    # never recompute (strategy 1).
     for (layer, phase), (bm, bn, splits, strat) in seen.items():
         assert splits >= 1 and strat in (0, 1, 2), (layer, phase)
-        if bm == 32 or bn == 32:
+        if bm in (16, 32) or bn in (16, 32):
+            assert bm == bn and phase == 2 and strat in (0, 2), (layer, phase, bm, bn, strat)
+            assert strat == 2 or splits == 1, (layer, phase, splits, strat)
+        elif bm == 32 or bn == 32:
             assert (bm, bn) == (32, 32) and phase == 2 and strat in (0, 2), (layer, phase, bm, bn, strat)
             assert strat == 2 or splits == 1, (layer, phase, splits, strat)
         else:
