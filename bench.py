@@ -97,6 +97,9 @@ def main():
     ap.add_argument("--no-overlap", action="store_true", help="weight gradients on the step stream")
     ap.add_argument("--probe-plan", default="", help="bm,bn,splits,strategy forced on the probed GEMM after "
                                                      "autotuning (PMC passes re-use the timed run's plan)")
+    ap.add_argument("--wgrad-p16", type=int, default=-1, help="force the P16 weight gradient on every layer it "
+                                                              "takes with this many K splits (0: its default; "
+                                                              "-1: the autotuner's choice)")
     args = ap.parse_args()
 
     import numpy as np
@@ -148,12 +151,17 @@ def main():
     # Setup (untimed): one step to fill the buffers, then per-shape GEMM plan autotuning
     # (niti_model_autotune: candidate tile / split-K plans timed per layer phase).
     tune_s = 0.0
+    p16_default = {i: p for (i, ph), p in model.plans().items() if ph == 2 and p[:2] == (16, 16)}
     if not args.no_autotune:
         step()
         ta = time.perf_counter()
         model.autotune()
         torch.cuda.synchronize()
         tune_s = time.perf_counter() - ta
+    for i, p in p16_default.items():
+        if args.wgrad_p16 >= 0:
+            sp = args.wgrad_p16 or p[2]
+            model.set_plan(i, 2, (16, 16, sp, 2 if sp > 1 else 0))
     probe_layer = args.probe_layer if args.probe_layer < len(model.layers) else len(model.layers) - 1
     if args.probe_plan:
         model.set_plan(probe_layer, args.probe_phase, [int(v) for v in args.probe_plan.split(",")])

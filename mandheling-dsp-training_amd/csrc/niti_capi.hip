@@ -1,11 +1,25 @@
 // niti_capi.hip -- extern "C" entry points of sections 1 and 2 of include/niti_hip.h.
 #include "../../include/niti_hip.h"
+#include <vector>
+
 #include "niti_internal.hpp"
 #include "niti_kernels.hpp"
 
+// Host tensors: MNN's CPU backend hands Executions Tensor::host<T>() pointers
+// (source/core/Execution.hpp:24-82, express/Executor.cpp:559-569).  Any tensor whose pointer is
+// not device memory (hipPointerGetAttributes) is staged through a device buffer the handle keeps:
+// inputs and outputs copied in before onExecute, outputs copied back after, and the call returns
+// once the host outputs are written (the CPU backend's onExecute is synchronous).
 struct niti_execution {
     niti::Execution* impl = nullptr;
-    ~niti_execution() { delete impl; }
+    int op = 0;
+    std::vector<void*> stage;
+    std::vector<size_t> stage_bytes;
+    ~niti_execution() {
+        delete impl;
+        for (void* p : stage)
+            if (p) (void)hipFree(p);
+    }
 };
 
 namespace {
@@ -37,6 +51,32 @@ bool to_geom(const niti_geom* g, niti::ConvGeom* out) {
     return r.finalize();
 }
 inline hipStream_t S(void* s) { return (hipStream_t)s; }
+// true for pageable or pinned host memory (anything hipPointerGetAttributes does not report as
+// device or managed memory)
+bool is_host_pointer(const void* p) {
+    hipPointerAttribute_t a{};
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return true;
+    }
+    return a.type != hipMemoryTypeDevice && a.type != hipMemoryTypeManaged;
+}
+
+// bytes of one Execution tensor: int8 elements, NC4HW4 with the channel count rounded up to 4
+// (MNN's CPU layout [ceil(C/4)][N][H][W][4]); the loss gradient's one-hot target and the
+// transpose's permutation are int32
+size_t tensor_bytes(int op, bool is_out, int idx, const niti_tensor& t) {
+    int64_t d[4];
+    for (int k = 0; k < 4; ++k) {
+        if (t.dims[k] < 0) return 0;
+        d[k] = t.dims[k];
+    }
+    if (!is_out && idx == 2 && (op == NITI_OP_LOSS_GRAD_INT8 || op == NITI_OP_DSP_LOSSGRAD_INT8))
+        return (size_t)(d[0] * d[1] * d[2] * d[3] * 4);
+    if (!is_out && idx == 1 && op == NITI_OP_DSP_TRANSPOSE_INT8) return 4 * sizeof(int32_t);
+    if (t.format == NITI_FORMAT_NC4HW4) return (size_t)(d[0] * ((d[1] + 3) / 4) * 4 * d[2] * d[3]);
+    return (size_t)(d[0] * d[1] * d[2] * d[3]);
+}
 }  // namespace
 
 extern "C" {
@@ -51,6 +91,7 @@ int niti_create_execution(int op_type, const niti_conv2d_common* common, niti_ex
     if (!e) return err;
     auto* h = new niti_execution();
     h->impl = e;
+    h->op = op_type;
     *out = h;
     return NITI_NO_ERROR;
 }
@@ -62,8 +103,46 @@ int niti_execution_resize(niti_execution_t e, const niti_tensor* in, int nin, co
 
 int niti_execution_execute(niti_execution_t e, const niti_tensor* in, int nin, const niti_tensor* out, int nout,
                            void* stream) {
-    if (!e || !in || !out) return NITI_INVALID_VALUE;
-    return e->impl->onExecute(in, nin, out, nout, S(stream));
+    if (!e || !in || !out || nin < 0 || nout < 0) return NITI_INVALID_VALUE;
+    const hipStream_t st = S(stream);
+    bool any_host = false;
+    for (int i = 0; i < nin + nout && !any_host; ++i) {
+        const niti_tensor& t = i < nin ? in[i] : out[i - nin];
+        any_host = t.data != nullptr && is_host_pointer(t.data);
+    }
+    if (!any_host) return e->impl->onExecute(in, nin, out, nout, st);
+    // stage every host tensor through the handle's device buffers
+    std::vector<niti_tensor> di(in, in + nin), dout(out, out + nout);
+    if (e->stage.size() < (size_t)(nin + nout)) {
+        e->stage.resize(nin + nout, nullptr);
+        e->stage_bytes.resize(nin + nout, 0);
+    }
+    for (int i = 0; i < nin + nout; ++i) {
+        const bool is_out = i >= nin;
+        niti_tensor& t = is_out ? dout[i - nin] : di[i];
+        if (t.data == nullptr || !is_host_pointer(t.data)) continue;
+        const size_t bytes = tensor_bytes(e->op, is_out, is_out ? i - nin : i, t);
+        if (bytes == 0) return NITI_INVALID_VALUE;
+        if (e->stage_bytes[i] < bytes) {
+            if (e->stage[i]) (void)hipFree(e->stage[i]);
+            e->stage[i] = nullptr;
+            e->stage_bytes[i] = 0;
+            if (hipMalloc(&e->stage[i], bytes) != hipSuccess) return NITI_OUT_OF_MEMORY;
+            e->stage_bytes[i] = bytes;
+        }
+        // outputs too: an Execution may leave parts of its output untouched (pad lanes, scalars)
+        if (hipMemcpyAsync(e->stage[i], t.data, bytes, hipMemcpyHostToDevice, st) != hipSuccess)
+            return NITI_NO_EXECUTION;
+        t.data = e->stage[i];
+    }
+    const int rc = e->impl->onExecute(di.data(), nin, dout.data(), nout, st);
+    if (rc != NITI_NO_ERROR) return rc;
+    for (int k = 0; k < nout; ++k)
+        if (dout[k].data != out[k].data &&
+            hipMemcpyAsync(out[k].data, dout[k].data, tensor_bytes(e->op, true, k, out[k]), hipMemcpyDeviceToHost,
+                           st) != hipSuccess)
+            return NITI_NO_EXECUTION;
+    return hipStreamSynchronize(st) == hipSuccess ? NITI_NO_ERROR : NITI_NO_EXECUTION;
 }
 
 void niti_destroy_execution(niti_execution_t e) { delete e; }

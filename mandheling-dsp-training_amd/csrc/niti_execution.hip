@@ -976,7 +976,7 @@ class DspLayoutExecution : public Execution {
         switch (op_) {
             case NITI_OP_DSP_TRANSPOSE_INT8: {
                 int perm[4];
-                if (hipMemcpy(perm, in[1].data, sizeof(perm), hipMemcpyDeviceToHost) != hipSuccess) return NITI_INVALID_VALUE;
+                if (hipMemcpy(perm, in[1].data, sizeof(perm), hipMemcpyDefault) != hipSuccess) return NITI_INVALID_VALUE;
                 int64_t st[4];
                 st[3] = 1;
                 for (int k = 2; k >= 0; --k) st[k] = st[k + 1] * xi.d[k + 1];

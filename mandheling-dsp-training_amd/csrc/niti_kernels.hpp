@@ -109,6 +109,15 @@ hipError_t splitk_reduce_linear(const int32_t* slab, int splits, int64_t n, int6
 // ---- weight gradient on P16 pixel blocks (niti_wgrad.hip) --------------------------------
 // P16: [pixels/16][Cp][16] int8 (Cp % 16 == 0, pixels % 16 == 0)
 hipError_t nhwc16_to_p16(const int8_t* in, int64_t pixels, int cp, int8_t* out, hipStream_t st);
+// several conversions in one launch (at most P16_MAX_JOBS)
+struct P16Conv {
+    const int8_t* in = nullptr;
+    int64_t pixels = 0;
+    int cp = 0;
+    int8_t* out = nullptr;
+};
+constexpr int P16_MAX_JOBS = 16;
+hipError_t nhwc16_to_p16_many(const P16Conv* jobs, int n, hipStream_t st);
 bool conv_wgrad_p16_ok(const ConvGeom& g);
 // diagnostic builds (NITI_WG_STAMPS): per-block stamps of the following launches, 8 u64 per block
 void wgrad_stamps_arm(unsigned long long* buf);

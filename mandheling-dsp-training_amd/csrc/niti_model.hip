@@ -215,10 +215,27 @@ struct Model {
     size_t slab_bytes = 0;
     void* slab_w = nullptr; // split-K slabs of the weight-gradient GEMMs (their own stream)
     size_t slab_w_bytes = 0;
-    // P16 copies of the weight-gradient operands (niti_wgrad.hip), reused layer by layer on the
-    // weight-gradient stream
-    int8_t* xp16 = nullptr;
+    // P16 copies of the weight-gradient operands (niti_wgrad.hip): one input copy per layer (all
+    // converted together when the backward pass starts, off the step stream), one output-gradient
+    // copy reused layer by layer on the weight-gradient stream
+    std::vector<int8_t*> xp16;
     int8_t* dp16 = nullptr;
+    bool xp16_ready = false;  // run(): every P16 layer's input copy is already converted
+    int convert_p16_inputs(hipStream_t st) {
+        P16Conv jobs[P16_MAX_JOBS];
+        int n = 0;
+        for (int j = 0; j < (int)L.size(); ++j)
+            if (wgrad_p16_splits(j)) {
+                const ConvGeom& g = L[j].g;
+                jobs[n++] = P16Conv{L[j].in, (int64_t)g.n * g.h * g.w, g.cip, xp16[j]};
+                if (n == P16_MAX_JOBS || j + 1 == (int)L.size()) {
+                    if (nhwc16_to_p16_many(jobs, n, st) != hipSuccess) return NITI_NO_EXECUTION;
+                    n = 0;
+                }
+            }
+        if (n > 0 && nhwc16_to_p16_many(jobs, n, st) != hipSuccess) return NITI_NO_EXECUTION;
+        return NITI_NO_ERROR;
+    }
     // the K split the P16 weight gradient of layer i runs with, 0 when layer i runs on the NHWC16
     // kernels (a plan override of another tile, or a geometry the P16 kernel does not take)
     int wgrad_p16_splits(int i) const {
@@ -475,8 +492,9 @@ int Model::build(int arch_, int batch_, int in_hw) {
     const int n = batch;
     x0 = (int8_t*)ws.alloc((size_t)n * in_h * in_w * round_up(in_c, 16));
     exp0 = (int8_t*)ws.alloc(16);
-    size_t acc_elems = 0, p16x = 0, p16d = 0;
+    size_t acc_elems = 0, p16d = 0;
     const int nl = (int)L.size();
+    xp16.assign(nl, nullptr);
     for (int i = 0; i < nl; ++i) {
         Layer& l = L[i];
         const ConvGeom& g = l.g;
@@ -509,7 +527,8 @@ int Model::build(int arch_, int batch_, int in_hw) {
         slab_w_bytes = std::max(slab_w_bytes, conv_wgrad_workspace(g));
         if (conv_wgrad_p16_ok(g)) {
             slab_w_bytes = std::max(slab_w_bytes, conv_wgrad_p16_workspace(g, 8));
-            p16x = std::max(p16x, (size_t)n * g.h * g.w * g.cip);
+            xp16[i] = (int8_t*)ws.alloc((size_t)n * g.h * g.w * g.cip);
+            if (!xp16[i]) return NITI_OUT_OF_MEMORY;
             p16d = std::max(p16d, out_px * g.cop);
         }
         // layer input / its C alignment with the previous output
@@ -521,10 +540,9 @@ int Model::build(int arch_, int batch_, int in_hw) {
         }
     }
     acc = (int32_t*)ws.alloc(acc_elems * 4);
-    if (p16x) {
-        xp16 = (int8_t*)ws.alloc(p16x);
+    if (p16d) {
         dp16 = (int8_t*)ws.alloc(p16d);
-        if (!xp16 || !dp16) return NITI_OUT_OF_MEMORY;
+        if (!dp16) return NITI_OUT_OF_MEMORY;
     }
     qstats = (unsigned long long*)ws.alloc(64);
     if (!qstats) return NITI_OUT_OF_MEMORY;
@@ -639,14 +657,15 @@ int Model::wgrad_layer(int i, hipStream_t st) {
     Layer& l = L[i];
     const ConvGeom& g = l.g;
     if (const int s = wgrad_p16_splits(i)) {
-        // P16 weight gradient: x and dy to pixel blocks, then the register-fed kernel (+ its
-        // split-K reduce); the probe times the kernel launch itself
-        MTRY(nhwc16_to_p16(l.in, (int64_t)g.n * g.h * g.w, g.cip, xp16, st));
+        // P16 weight gradient: x (unless run() converted every input already) and dy to pixel
+        // blocks, then the register-fed kernel (+ its split-K reduce); the probe times the kernel
+        // launch itself
+        if (!xp16_ready) MTRY(nhwc16_to_p16(l.in, (int64_t)g.n * g.h * g.w, g.cip, xp16[i], st));
         MTRY(nhwc16_to_p16(l.dy, (int64_t)g.n * g.oh * g.ow, g.cop, dp16, st));
         hipEvent_t eb, ee;
         unsigned long long* sp;
         probe_launch(i, 2, &eb, &ee, &sp);
-        MTRY(conv_wgrad_p16(g, xp16, dp16, l.dwacc, dp ? nullptr : rng(i, 2), slab_w, slab_w_bytes, s, st, eb, ee, sp));
+        MTRY(conv_wgrad_p16(g, xp16[i], dp16, l.dwacc, dp ? nullptr : rng(i, 2), slab_w, slab_w_bytes, s, st, eb, ee, sp));
         return NITI_NO_ERROR;
     }
     // the weight-gradient probe brackets the GEMM launch alone (not its split-K reduce)
@@ -779,6 +798,16 @@ int Model::autotune(hipStream_t st, int reps) {
                 best.splits = wgrad_p16_splits(i);
                 best.strat = best.splits > 1 ? 2 : 0;
             }
+            // P16 candidates are timed without their input conversion: run() converts every
+            // layer's input in one launch off the step stream when the backward pass starts
+            xp16_ready = false;
+            if (op == PLAN_WGRAD && conv_wgrad_p16_ok(g)) {
+                if (nhwc16_to_p16(L[i].in, (int64_t)g.n * g.h * g.w, g.cip, xp16[i], st) != hipSuccess) {
+                    rc = NITI_NO_EXECUTION;
+                    break;
+                }
+                xp16_ready = true;
+            }
             float best_us = 0.f;
             rc = time_op(i, op, &best_us);
             const bool taps = op == PLAN_WGRAD && conv_wgrad_taps_ok(g);
@@ -831,9 +860,11 @@ int Model::autotune(hipStream_t st, int reps) {
                 }
             }
             plan_override_set(key, best);
+            xp16_ready = false;
             if (rc != NITI_NO_ERROR) break;
         }
     }
+    xp16_ready = false;
     tuning = false;
     for (auto e : ev) (void)hipEventDestroy(e);
     if (hipStreamSynchronize(st) != hipSuccess) rc = NITI_NO_EXECUTION;
@@ -846,6 +877,7 @@ int Model::run(const int8_t* x_nchw, int exp_in, const uint8_t* images, const in
     const bool dp = this->dp();
     SgdJob jobs[SGD_MAX_JOBS];
     if (nl > SGD_MAX_JOBS) return NITI_NOT_SUPPORT;
+    xp16_ready = false;
     MTRY(hipMemsetAsync(amax, 0, amax_bytes, st));
     if (x_nchw != nullptr) {
         MTRY(hipMemsetAsync(exp0, exp_in, 1, st));
@@ -884,6 +916,11 @@ int Model::run(const int8_t* x_nchw, int exp_in, const uint8_t* images, const in
             MTRY(hipEventRecord(ev_dy[i], st));
             MTRY(hipStreamWaitEvent(side, ev_dy[i], 0));
         }
+        if (i == nl - 1) {  // the forward outputs are final: every P16 input copy in one go
+            const int rc = convert_p16_inputs(wst);
+            if (rc != NITI_NO_ERROR) return rc;
+            xp16_ready = true;
+        }
         int rc = wgrad_layer(i, wst);
         if (rc == NITI_NO_ERROR && ov && dp) MTRY(hipEventRecord(ev_w[i], side));
         if (rc == NITI_NO_ERROR && i > 0) rc = dgrad_layer(i, st);
@@ -906,6 +943,7 @@ int Model::run(const int8_t* x_nchw, int exp_in, const uint8_t* images, const in
         MTRY(hipEventRecord(ev_side, side));
         MTRY(hipStreamWaitEvent(st, ev_side, 0));
     }
+    xp16_ready = false;
     MTRY(sgd_update_many(jobs, nl, st));
     return NITI_NO_ERROR;
 }

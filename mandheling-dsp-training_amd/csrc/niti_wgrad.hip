@@ -72,6 +72,10 @@ constexpr int P16_WAVES = 4;           // one wave per SIMD
 #ifndef NITI_WG_ABLATE
 #define NITI_WG_ABLATE 0
 #endif
+// NITI_WG_ATOMIC_OUT = 1 (diagnostic timing): split partials atomically added into C instead of slabs
+#ifndef NITI_WG_ATOMIC_OUT
+#define NITI_WG_ATOMIC_OUT 0
+#endif
 #define WG_STAMP(k)                                                                            \
     do {                                                                                       \
         if (NITI_WG_STAMPS && g.stamps != nullptr && threadIdx.x == 0) {                        \
@@ -166,7 +170,7 @@ __device__ __forceinline__ v4i asm_load16(__amdgpu_buffer_rsrc_t r, uint32_t vof
 
 template <int OW, int NW, int D>
 __global__ void __launch_bounds__(NW * 64) wgrad_p16_kernel(WgP16 g) {
-    static_assert(D >= 2, "the next K group's window must be resident");
+    static_assert(D >= 2 && D % 2 == 0, "the next K group's window must be resident; operand buffers alternate");
     // the block's tile, row-major [co 32][tap 9][ci 32] int32 (every wave adds its partial into it),
     // plus the block-max scratch
     constexpr int SMEM = P16_TILE * 4 + 64;
@@ -255,19 +259,21 @@ __global__ void __launch_bounds__(NW * 64) wgrad_p16_kernel(WgP16 g) {
         ((ring[U] = Ring{}, issue(ring[U], std::integral_constant<int, U>(), U)), ...);
     }(std::make_integer_sequence<int, D>());
     WG_STAMP(1);
-    auto step = [&](auto u_c, int j0) {
-        constexpr int u = decltype(u_c)::value;
-        Ring& r = ring[u];
-        // K group j's loads have landed (K groups j+1 .. j+D-1 may still be in flight)
-        wait_vmcnt<L * (D - 1)>();
+    // Software pipeline: the tap operands of K group j + 1 (dy shifted for kx = 0 / 2, x rows for
+    // ky = 0 / 2; kx = ky = 1 are the ring registers themselves) are built while K group j's nine
+    // MFMAs run, so the VALU work fills MFMA gaps instead of stalling the pipe at every K group.
+    struct Ops {
+        v4i a0, a2, b0, b2;
+    };
+    Ops ops[2];
+    auto prep = [&](Ring& r, Ops& o) {
         reg_fence(r.d);
         reg_fence(r.x);
         if constexpr (NB) {
             reg_fence(r.up);
             reg_fence(r.dn);
         }
-        const v4i d = r.d, xc = r.x;
-        v4i up, dn;
+        v4i up{0, 0, 0, 0}, dn{0, 0, 0, 0};
         if constexpr (OW == 8) {
             up = v4i{r.up[0], r.up[1], 0, 0};
             dn = v4i{r.dn[0], r.dn[1], 0, 0};
@@ -275,20 +281,38 @@ __global__ void __launch_bounds__(NW * 64) wgrad_p16_kernel(WgP16 g) {
             up = r.up;
             dn = r.dn;
         }
+        if constexpr (NITI_WG_ABLATE == 3) {
+            o.a0 = o.a2 = r.d;
+            o.b0 = o.b2 = r.x;
+        } else {
+            o.a0 = dy_tap<OW, 0>(r.d);
+            o.a2 = dy_tap<OW, 2>(r.d);
+            o.b0 = x_tap<OW, 0>(up, r.x, dn);
+            o.b2 = x_tap<OW, 2>(up, r.x, dn);
+        }
+    };
+    wait_vmcnt<L * (D - 1)>();  // K group 0 has landed
+    prep(ring[0], ops[0]);
+    auto step = [&](auto u_c, int j0) {
+        constexpr int u = decltype(u_c)::value, un = (u + 1) % D;
+        // K group j + 1 has landed (j + 2 .. j + D - 1 may still be in flight): its operands
+        wait_vmcnt<L * (D - 2)>();
+        prep(ring[un], ops[(u + 1) & 1]);
+        const Ops& o = ops[u & 1];
+        const v4i A[3] = {o.a0, ring[u].d, o.a2};
+        const v4i B[3] = {o.b0, ring[u].x, o.b2};
         [&]<int... T>(std::integer_sequence<int, T...>) {
             (([&] {
                  constexpr int KY = T / 3, KX = T % 3;
-                 const v4i A = NITI_WG_ABLATE == 3 ? d : dy_tap<OW, KX>(d);
-                 const v4i B = NITI_WG_ABLATE == 3 ? xc : x_tap<OW, KY>(up, xc, dn);
                  if constexpr (NITI_WG_ABLATE == 2)
-                     acc[T][0] += A[0] ^ B[1];
+                     acc[T][0] += A[KX][0] ^ B[KY][1];
                  else
-                     acc[T] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A, B, acc[T], 0, 0, 0);
+                     acc[T] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[KX], B[KY], acc[T], 0, 0, 0);
              }()),
              ...);
         }(std::make_integer_sequence<int, 9>());
         // slot u is free again: K group j + D
-        issue(r, u_c, j0 + u + D);
+        issue(ring[u], u_c, j0 + u + D);
     };
     for (int j0 = 0; j0 < n_w; j0 += D) {
         [&]<int... U>(std::integer_sequence<int, U...>) {
@@ -336,7 +360,14 @@ __global__ void __launch_bounds__(NW * 64) wgrad_p16_kernel(WgP16 g) {
         const int row = c / 72, rem = c - row * 72, t = rem >> 3, c4 = rem & 7;
         const v4i v = ((const v4i*)tile_lds)[c];
         if (co0 + row < g.c_out && NITI_WG_ABLATE != 5) {
-            *(v4i*)(dst + (int64_t)(co0 + row) * g.ldc + t * g.CIP + ci0 + 4 * c4) = v;
+            if (NITI_WG_ATOMIC_OUT && partial) {  // diagnostic: split-K partials added into C
+                int32_t* q = g.C + (int64_t)(co0 + row) * g.ldc + t * g.CIP + ci0 + 4 * c4;
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    __hip_atomic_fetch_add(q + e, v[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                *(v4i*)(dst + (int64_t)(co0 + row) * g.ldc + t * g.CIP + ci0 + 4 * c4) = v;
+            }
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 const uint32_t u = uabs32(v[e]);
@@ -362,9 +393,59 @@ __global__ void __launch_bounds__(NW * 64) wgrad_p16_kernel(WgP16 g) {
     span_end(g.span);
 }
 
-// NHWC16 [P][CP] -> P16 [P/16][CP][16]: one thread per (16-pixel block, 16-channel chunk), a
-// 16 x 16 byte transpose in registers
-__global__ void nhwc16_to_p16_kernel(const int8_t* __restrict__ in, int64_t blocks, int cp, int8_t* __restrict__ out) {
+// NHWC16 [P][CP] -> P16 [P/16][CP][16].  A 16-pixel block is 16 * CP contiguous bytes on both
+// sides (16 rows of CP channels in, CP rows of 16 pixels out), so each workgroup copies whole
+// blocks into LDS with 16-byte coalesced loads and writes them back transposed: a lane gathers one
+// channel's 16 pixels with byte reads (4 lanes share each LDS dword, no bank conflicts) and stores
+// one 16-byte chunk, consecutive lanes consecutive chunks.  CP is a power of two from 32 to 1024:
+// a workgroup takes 256 / CP blocks (CP <= 256) or one block (CP > 256).  One launch serves up to
+// P16_MAX_JOBS tensors, each owning a contiguous range of workgroups.
+struct P16Job {
+    const int8_t* in;
+    int8_t* out;
+    int64_t blocks;
+    int lg;       // log2 CP
+    uint32_t wg0; // first workgroup
+};
+struct P16Jobs {
+    P16Job j[P16_MAX_JOBS];
+    int n;
+};
+
+__global__ void __launch_bounds__(256) nhwc16_to_p16_kernel(P16Jobs J) {
+    __shared__ __attribute__((aligned(16))) int8_t tile[16 * 1024];
+    const uint32_t wg = blockIdx.x;
+    int k = 0;
+    while (k + 1 < J.n && wg >= J.j[k + 1].wg0) ++k;
+    const P16Job jb = J.j[k];
+    const int lg = jb.lg, cp = 1 << lg;
+    const int bpw = lg < 8 ? 1 << (8 - lg) : 1;
+    const int64_t b0 = (int64_t)(wg - jb.wg0) * bpw;
+    const int nb = (int)(jb.blocks - b0 < bpw ? jb.blocks - b0 : bpw);
+    const int bytes = nb * 16 * cp;
+    const int8_t* src = jb.in + b0 * 16 * cp;
+    for (int o = threadIdx.x * 16; o < bytes; o += 256 * 16) *(v4i*)(tile + o) = *(const v4i*)(src + o);
+    __syncthreads();
+    int8_t* dst = jb.out + b0 * 16 * cp;
+    for (int t = threadIdx.x; t < (nb << lg); t += 256) {
+        const int bl = t >> lg, c = t & (cp - 1);
+        const uint8_t* s = (const uint8_t*)tile + (bl << (lg + 4)) + c;
+        v4i o;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            uint32_t w = 0;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) w |= (uint32_t)s[(4 * q + e) << lg] << (8 * e);
+            o[q] = (int)w;
+        }
+        *(v4i*)(dst + (int64_t)t * 16) = o;
+    }
+}
+
+// any CP % 16 == 0: one thread per (16-pixel block, 16-channel chunk), a 16 x 16 byte transpose
+// in registers
+__global__ void nhwc16_to_p16_any_kernel(const int8_t* __restrict__ in, int64_t blocks, int cp,
+                                         int8_t* __restrict__ out) {
     const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
     const int cc = cp / 16;
     if (e >= blocks * cc) return;
@@ -382,12 +463,36 @@ __global__ void nhwc16_to_p16_kernel(const int8_t* __restrict__ in, int64_t bloc
     }
 }
 
-hipError_t nhwc16_to_p16(const int8_t* in, int64_t pixels, int cp, int8_t* out, hipStream_t st) {
-    if (cp % 16 != 0 || pixels % 16 != 0) return hipErrorInvalidValue;
-    const int64_t n = pixels / 16 * (cp / 16);
-    hipLaunchKernelGGL(nhwc16_to_p16_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, in, pixels / 16, cp,
-                       out);
+hipError_t nhwc16_to_p16_many(const P16Conv* jobs, int n, hipStream_t st) {
+    if (n < 0 || n > P16_MAX_JOBS) return hipErrorInvalidValue;
+    P16Jobs J{};
+    uint32_t wg = 0;
+    for (int i = 0; i < n; ++i) {
+        const P16Conv& c = jobs[i];
+        if (c.cp <= 0 || c.cp % 16 != 0 || c.pixels < 0 || c.pixels % 16 != 0) return hipErrorInvalidValue;
+        if (c.pixels == 0) continue;
+        const int64_t blocks = c.pixels / 16;
+        if ((c.cp & (c.cp - 1)) != 0 || c.cp < 32 || c.cp > 1024) {  // not a power of two: generic kernel
+            const int64_t t = blocks * (c.cp / 16);
+            hipLaunchKernelGGL(nhwc16_to_p16_any_kernel, dim3((unsigned)((t + 255) / 256)), dim3(256), 0, st, c.in,
+                               blocks, c.cp, c.out);
+            continue;
+        }
+        int lg = 0;
+        while ((1 << lg) < c.cp) ++lg;
+        const int bpw = lg < 8 ? 1 << (8 - lg) : 1;
+        const int64_t wgs = (blocks + bpw - 1) / bpw;
+        if ((int64_t)wg + wgs > 0x7fffffff) return hipErrorInvalidValue;
+        J.j[J.n++] = P16Job{c.in, c.out, blocks, lg, wg};
+        wg += (uint32_t)wgs;
+    }
+    if (J.n > 0) hipLaunchKernelGGL(nhwc16_to_p16_kernel, dim3(wg), dim3(256), 0, st, J);
     return hipGetLastError();
+}
+
+hipError_t nhwc16_to_p16(const int8_t* in, int64_t pixels, int cp, int8_t* out, hipStream_t st) {
+    const P16Conv c{in, pixels, cp, out};
+    return nhwc16_to_p16_many(&c, 1, st);
 }
 
 // ---- host side --------------------------------------------------------------------------------
@@ -483,7 +588,7 @@ hipError_t conv_wgrad_p16(const ConvGeom& g, const int8_t* x_p16, const int8_t* 
             hipLaunchKernelGGL(k, grid, dim3(NW * 64), 0, st, t);
     };
     switch (g.ow) {
-        case 8: launch(wgrad_p16_kernel<8, NW, 6>); break;
+        case 8: launch(wgrad_p16_kernel<8, NW, 8>); break;
         case 16: launch(wgrad_p16_kernel<16, NW, 8>); break;
         case 4: launch(wgrad_p16_kernel<4, NW, 6>); break;
         default: launch(wgrad_p16_kernel<2, NW, 6>); break;

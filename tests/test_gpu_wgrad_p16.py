@@ -86,3 +86,15 @@ def test_wgrad_p16_rejects_unsupported(T, ops):
     x = T.zeros(64, dtype=T.int8, device="cuda")
     with pytest.raises(L.NitiError):
         ops.conv_wgrad_p16_acc(gg, x, x)
+
+
+@pytest.mark.parametrize("pixels,cp", [(16, 32), (48, 32), (4096, 32), (2064, 64), (1024, 128), (272, 256),
+                                       (1024, 512), (80, 1024), (64, 48), (1056, 96)])
+def test_nhwc16_to_p16_layout(T, ops, pixels, cp):
+    """P16 [pixels/16][cp][16] is the NHWC16 [pixels][cp] tensor with each 16-pixel block transposed:
+    the LDS-staged kernel (power-of-two cp, ragged last workgroup) and the generic one (48, 96)."""
+    rng = np.random.default_rng(pixels + cp)
+    a = rng.integers(-128, 128, (pixels, cp)).astype(np.int8)
+    want = a.reshape(pixels // 16, 16, cp).transpose(0, 2, 1).copy()
+    got = ops.nhwc16_to_p16(T.from_numpy(a).cuda()).cpu().numpy().reshape(pixels // 16, cp, 16)
+    assert np.array_equal(got, want)

@@ -24,16 +24,13 @@ for k, v in sorted(tot.items(), key=lambda x: -x[1]):
     print(f"{v / steps:9.1f} {cnt[k] / steps:10.1f}  {k}")
 print("total busy us/step", sum(tot.values()) / steps)
 # last step: from the last loss_grad to the end
+def is_start(r):  # a step's first kernel: the input quantiser or the int8 input's relayout
+    return "image_stats" in r["Kernel_Name"] or "NchwToNhwc16" in r["Kernel_Name"]
+
+
 idx = max(i for i, r in enumerate(rows) if "loss_grad" in r["Kernel_Name"])
-prev = max(i for i, r in enumerate(rows[:idx]) if "loss_grad" in r["Kernel_Name"]) if any(
-    "loss_grad" in r["Kernel_Name"] for r in rows[:idx]) else 0
-start = prev + 1
-for i in range(start, len(rows)):
-    if "NchwToNhwc16" in rows[i]["Kernel_Name"] and i > start:
-        break
-seg = rows[start:]
+first = max(i for i, r in enumerate(rows[:idx]) if is_start(r))
 print("\nlast step launches (from the forward of the step):")
-first = next(i for i, r in enumerate(rows) if i > prev and "NchwToNhwc16" in r["Kernel_Name"])
 seg = rows[first:]
 span = (int(seg[-1]["End_Timestamp"]) - int(seg[0]["Start_Timestamp"])) / 1e3
 t0 = int(seg[0]["Start_Timestamp"])
