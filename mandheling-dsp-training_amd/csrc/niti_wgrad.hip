@@ -73,6 +73,15 @@ constexpr int P16_WAVES = 4;           // one wave per SIMD
 #define NITI_WG_ABLATE 0
 #endif
 // NITI_WG_ATOMIC_OUT = 1 (diagnostic timing): split partials atomically added into C instead of slabs
+// ring depth (K groups in flight) of the 8x8-image kernel; diagnostic builds vary it (the K loop
+// ran the same 358 cycles per K group at depth 4, 6 and 8 on conv4; deeper rings only lengthen
+// the prologue)
+#ifndef NITI_WG_D8
+#define NITI_WG_D8 4
+#endif
+#ifndef NITI_WG_D4  // ... and of the 4x4 / 2x2-image kernels
+#define NITI_WG_D4 4
+#endif
 #ifndef NITI_WG_ATOMIC_OUT
 #define NITI_WG_ATOMIC_OUT 0
 #endif
@@ -588,10 +597,10 @@ hipError_t conv_wgrad_p16(const ConvGeom& g, const int8_t* x_p16, const int8_t* 
             hipLaunchKernelGGL(k, grid, dim3(NW * 64), 0, st, t);
     };
     switch (g.ow) {
-        case 8: launch(wgrad_p16_kernel<8, NW, 8>); break;
+        case 8: launch(wgrad_p16_kernel<8, NW, NITI_WG_D8>); break;
         case 16: launch(wgrad_p16_kernel<16, NW, 8>); break;
-        case 4: launch(wgrad_p16_kernel<4, NW, 6>); break;
-        default: launch(wgrad_p16_kernel<2, NW, 6>); break;
+        case 4: launch(wgrad_p16_kernel<4, NW, NITI_WG_D4>); break;
+        default: launch(wgrad_p16_kernel<2, NW, NITI_WG_D4>); break;
     }
     hipError_t e = hipGetLastError();
     if (e == hipSuccess && t.splits > 1)
