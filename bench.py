@@ -94,7 +94,10 @@ def main():
     ap.add_argument("--probe-phase", type=int, default=2, help="0 fwd, 1 input grad, 2 weight grad")
     ap.add_argument("--graph", action="store_true", help="replay the step as a hipGraph (slower on ROCm 7.2)")
     ap.add_argument("--no-autotune", action="store_true", help="keep the fixed default GEMM plans")
-    ap.add_argument("--no-overlap", action="store_true", help="weight gradients on the step stream")
+    ap.add_argument("--overlap", action="store_true",
+                    help="weight gradients on a second stream beside the input-gradient chain (measured within 1 %% "
+                         "of the single-stream step on MI355X, and it slows the overlapped kernels by sharing the CUs)")
+    ap.add_argument("--no-overlap", action="store_true", help="(default) weight gradients on the step stream")
     ap.add_argument("--probe-plan", default="", help="bm,bn,splits,strategy forced on the probed GEMM after "
                                                      "autotuning (PMC passes re-use the timed run's plan)")
     ap.add_argument("--wgrad-p16", type=int, default=-1, help="force the P16 weight gradient on every layer it "
@@ -124,7 +127,7 @@ def main():
         args.cpu_sample = {niti_amd.ARCH_VGG16: 0, niti_amd.ARCH_LENET: 512}.get(arch, 128)
     model = NitiModel(arch, args.batch, args.in_hw)
     model.set_graph(args.graph)
-    model.set_overlap(not args.no_overlap)
+    model.set_overlap(args.overlap and not args.no_overlap)
     for i, (w, s) in enumerate(synth_weights(model.layers, seed=17)):
         model.set_weight(i, w, s)
     if world > 1:
@@ -279,7 +282,9 @@ def main():
                                + (", 4096-4096-1000 head" if arch == niti_amd.ARCH_VGG16 else "")
                                if arch != niti_amd.ARCH_LENET else "LeNet NITI int8 training step, 1x28x28",
                    "global_batch": args.batch * world, "per_gpu_batch": args.batch,
-                   "parallelism": f"dp{world} exact (RCCL all-reduce MAX ranges + SUM int32 grads)"},
+                   "parallelism": f"dp{world} exact (RCCL all-reduce MAX ranges + SUM int32 grads)",
+                   "streams": "weight gradients beside the input-gradient chain on a second stream" if args.overlap
+                   and not args.no_overlap else "one stream (weight gradient, then input gradient, per layer)"},
         "int8_mfma_tops": round(tops, 2),
         "int8_mfma_frac_of_peak": round(tops / PEAK_INT8_TOPS, 4),
         "roofline": {

@@ -82,6 +82,9 @@ constexpr int P16_WAVES = 4;           // one wave per SIMD
 #ifndef NITI_WG_D4  // ... and of the 4x4 / 2x2-image kernels
 #define NITI_WG_D4 4
 #endif
+#ifndef NITI_WG_NT_OUT
+#define NITI_WG_NT_OUT 1
+#endif
 #ifndef NITI_WG_ATOMIC_OUT
 #define NITI_WG_ATOMIC_OUT 0
 #endif
@@ -374,6 +377,8 @@ __global__ void __launch_bounds__(NW * 64) wgrad_p16_kernel(WgP16 g) {
 #pragma unroll
                 for (int e = 0; e < 4; ++e)
                     __hip_atomic_fetch_add(q + e, v[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else if (NITI_WG_NT_OUT) {  // streaming stores: the partials leave L2 during the kernel
+                __builtin_nontemporal_store(v, (v4i*)(dst + (int64_t)(co0 + row) * g.ldc + t * g.CIP + ci0 + 4 * c4));
             } else {
                 *(v4i*)(dst + (int64_t)(co0 + row) * g.ldc + t * g.CIP + ci0 + 4 * c4) = v;
             }
