@@ -64,6 +64,7 @@ enum niti_op_type {
     NITI_OP_DSP_RESHAPE_INT8 = 803,        /* NITI_DSP_RESHAPE_Int8   -> NITI_DSPReshape_Int8.cpp */
     NITI_OP_DSP_LOSSGRAD_INT8 = 804,       /* NITI_DSP_LOSSGRAD_Int8  -> NITI_DSPLossGrad_Int8.cpp */
     NITI_OP_DSP_RELUGRAD_INT8 = 805,       /* NITI_DSP_RELUGRAD_Int8  -> NITI_DSPReluGrad_Int8.cpp */
+    NITI_OP_DSP_MAXPOOLGRAD_REF_INT8 = 806, /* NITI_DSP_MAXPOOLGRAD_REF_Int8 -> NITI_DSPMaxPoolGradRef_Int8.cpp:17-80 */
     NITI_OP_DSP_MAXPOOLGRAD_INT8 = 807,    /* NITI_DSP_MAXPOOLGRAD_Int8 -> NITI_DSPMaxPoolGrad_Int8.cpp */
     NITI_OP_DSP_TRANSPOSE_INT8 = 808,      /* NITI_DSP_TRANSPOSE_Int8 -> NITI_DSPTranspose_Int8.cpp */
     NITI_OP_DSP_WEIGHTROTATE180_INT8 = 809, /* NITI_DSP_WEIGHTROTATE180_REF_Int8 -> NITI_DSPWeightRotateRef_Int8.cpp */
@@ -142,6 +143,11 @@ int niti_create_execution(int op_type, const niti_conv2d_common* common, niti_ex
  *  NITI_OP_DSP_MAXPOOL_INT8   in {x NHWC, ascale int8[1]} out{y NHWC, ascale int8[1]}; the pool's
  *                             kernel / stride / pad in the common's kernel_x/y, stride_x/y, pad_x/y
  *  NITI_OP_DSP_MAXPOOLGRAD_INT8 in {x, y, dy} NHWC out{dx NHWC}
+ *  NITI_OP_DSP_MAXPOOLGRAD_REF_INT8 (806) in {x, y, dy} NHWC out{dx NHWC}: the reference's literal
+ *                             walk (x read as [batch][height][width * channel], y / dy at
+ *                             (offset * bc) / kernelX / kernelY, untouched bytes kept); kernel /
+ *                             stride in the common; NOT_SUPPORT for stride < kernel or windows
+ *                             past the tensor (order-dependent / out of bounds in the reference)
  *  NITI_OP_DSP_TRANSPOSE_INT8 in {x, perm int32[4] (device)} out{x permuted}; WEIGHTROTATE180 in {w}
  *                             out{w, raw axes 2, 3 reversed}; RESHAPE / RESHAPEGRAD in {x} out{same bytes};
  *                             all on the stored axis order ([N][H][W][C] for NHWC), common may be NULL

@@ -825,6 +825,86 @@ class DspElementwiseExecution : public Execution {
     int8_t *x16_ = nullptr, *y16_ = nullptr, *dy16_ = nullptr, *dx16_ = nullptr;
 };
 
+// ------------------------------------------------------------------ 806: reference max-pool grad
+// NITI_DSP_MAXPOOLGRAD_REF_Int8 (NITI_DSPMaxPoolGradRef_Int8.cpp:17-80), restated literally.  The
+// op reads its NHWC tensors as [ih = batch][iw = height][ib = width][ic = channel] (:23-28) and
+// walks windows (i, j) with i += strideX over ih, j += strideY over iw (:36-37); per window and
+// per 128-byte chunk of the bc = ib * ic plane (:41-43; a tail of bc % 128 bytes is never
+// visited) it routes dy to the first (ky outer, kx inner) position whose x equals the pooled y and
+// writes 0 to the window's other positions (:59-88).  y and dy are read at
+// (offset * bc) / kernelX / kernelY, offset = i * iw + j (:54-55), integer division in that order.
+// Output bytes no window visits keep their value.  Overlapping windows (stride < kernel) make the
+// reference's result depend on its sequential order and windows reaching past the tensor read out
+// of bounds there: both are NOT_SUPPORT.
+struct PoolGradRefMap {
+    const int8_t* x;   // origin
+    const int8_t* y;   // outputOrigin (pooled)
+    const int8_t* dy;  // outputDiff
+    int8_t* out;
+    int64_t bc, chunk;  // plane bytes, visited bytes per window (bc / 128 * 128)
+    int iw, sx, sy, kx, ky, nwj;
+    __device__ void operator()(int64_t t) const {
+        const int64_t w = t / chunk, e = t - w * chunk;
+        const int wi = (int)(w / nwj), wj = (int)(w - (int64_t)wi * nwj);
+        const int64_t offset = (int64_t)(wi * sx) * iw + wj * sy;
+        const int64_t yo = offset * bc / kx / ky + e;
+        const int8_t m = y[yo], g = dy[yo];
+        bool done = false;
+        for (int a = 0; a < ky; ++a)
+            for (int b = 0; b < kx; ++b) {
+                const int64_t o = (offset + (int64_t)a * iw + b) * bc + e;
+                const bool take = !done && x[o] == m;
+                out[o] = take ? g : (int8_t)0;
+                done = done || take;
+            }
+    }
+};
+
+class DspMaxPoolGradRefExecution : public Execution {
+   public:
+    explicit DspMaxPoolGradRefExecution(const niti_conv2d_common& c) : c_(c) {}
+    int onResize(const niti_tensor* in, int nin, const niti_tensor* out, int nout) override {
+        ready_ = false;
+        if (nin < 3 || nout < 1) return NITI_INVALID_VALUE;
+        for (int i = 0; i < 3; ++i)
+            if (in[i].format != NITI_FORMAT_NHWC) return NITI_NOT_SUPPORT;
+        if (out[0].format != NITI_FORMAT_NHWC) return NITI_NOT_SUPPORT;
+        // logical {N, C, H, W} of NHWC storage: ih = N, iw = H, ib = W, ic = C
+        ih_ = in[0].dims[0], iw_ = in[0].dims[2];
+        bc_ = (int64_t)in[0].dims[3] * in[0].dims[1];
+        sx_ = c_.stride_x, sy_ = c_.stride_y, kx_ = c_.kernel_x, ky_ = c_.kernel_y;
+        if (sx_ < 1 || sy_ < 1 || kx_ < 1 || ky_ < 1 || ih_ < 1 || iw_ < 1 || bc_ < 1) return NITI_INVALID_VALUE;
+        if (sx_ < ky_ || sy_ < kx_) return NITI_NOT_SUPPORT;  // overlapping windows
+        for (int k = 0; k < 4; ++k)
+            if (out[0].dims[k] != in[0].dims[k]) return NITI_COMPUTE_SIZE_ERROR;
+        nwi_ = (ih_ + sx_ - 1) / sx_, nwj_ = (iw_ + sy_ - 1) / sy_;
+        if ((nwi_ - 1) * sx_ + ky_ > ih_ || (nwj_ - 1) * sy_ + kx_ > iw_) return NITI_NOT_SUPPORT;  // past the tensor
+        chunk_ = bc_ / 128 * 128;
+        const int64_t offset_last = (int64_t)((nwi_ - 1) * sx_) * iw_ + (nwj_ - 1) * sy_;
+        const int64_t ylen = (int64_t)in[1].dims[0] * in[1].dims[1] * in[1].dims[2] * in[1].dims[3];
+        const int64_t dlen = (int64_t)in[2].dims[0] * in[2].dims[1] * in[2].dims[2] * in[2].dims[3];
+        if (chunk_ > 0 && (offset_last * bc_ / kx_ / ky_ + chunk_ > ylen || offset_last * bc_ / kx_ / ky_ + chunk_ > dlen))
+            return NITI_COMPUTE_SIZE_ERROR;
+        ready_ = true;
+        return NITI_NO_ERROR;
+    }
+    int onExecute(const niti_tensor* in, int nin, const niti_tensor* out, int nout, hipStream_t st) override {
+        if (!ready_) return NITI_NO_EXECUTION;
+        if (chunk_ == 0) return NITI_NO_ERROR;
+        NITI_TRY(launch_map((int64_t)nwi_ * nwj_ * chunk_,
+                            PoolGradRefMap{(const int8_t*)in[0].data, (const int8_t*)in[1].data, (const int8_t*)in[2].data,
+                                           (int8_t*)out[0].data, bc_, chunk_, iw_, sx_, sy_, kx_, ky_, nwj_},
+                            st));
+        return NITI_NO_ERROR;
+    }
+
+   private:
+    niti_conv2d_common c_;
+    bool ready_ = false;
+    int ih_ = 0, iw_ = 0, sx_ = 0, sy_ = 0, kx_ = 0, ky_ = 0, nwi_ = 0, nwj_ = 0;
+    int64_t bc_ = 0, chunk_ = 0;
+};
+
 // ------------------------------------------------------------------ loss gradient slots
 // NITI_LOSS_Grad_Int8 (711, NITI_CPULossGrad_Int8.cpp:81-200) and NITI_DSP_LOSSGRAD_Int8 (804,
 // grad/NITI_SoftmaxGrad.cpp:41-66 builds either from the same inputs): {logits int8 [batch][classes],
@@ -1174,6 +1254,7 @@ Execution* create_execution(int op_type, const niti_conv2d_common* c, int* err) 
         case NITI_OP_DSP_NOP_INT8:
         case NITI_OP_DSP_MAXPOOL_INT8:
         case NITI_OP_DSP_MAXPOOLGRAD_INT8: return new DspElementwiseExecution(op_type, cc);
+        case NITI_OP_DSP_MAXPOOLGRAD_REF_INT8: return new DspMaxPoolGradRefExecution(cc);
         case NITI_OP_DSP_GRADIENT_SPLITBATCHCONV_INT8:
         case NITI_OP_DSP_TRANSPOSEGRADIENT_CONV_INT8: return new DspTransposeGradientExecution(cc);
         default: *err = NITI_NOT_SUPPORT; return nullptr;

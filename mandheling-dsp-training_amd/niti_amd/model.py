@@ -66,6 +66,36 @@ class NitiModel:
         for i, (w, s) in enumerate(zip(weights, wscales)):
             self.set_weight(i, w, s)
 
+    def save_mnn(self, path: str):
+        """The reference's own snapshot: `Variable::save(model->parameters(), path)` -- an MNN Net
+        flatbuffer of one TrainableParam Blob per layer weight (int8 OIHW, express/Expr.cpp:833-965)
+        -- plus `path.wscale.json` with the weight scales the NITI modules keep outside their
+        parameters.  `Variable::load` + `Module::loadParameters` read the .mnn unchanged."""
+        from . import mnn_snapshot
+        if len(self._wscale) != len(self.layers):
+            raise ValueError("save_mnn() before every layer's weight was set")
+        mnn_snapshot.save(path, [self.get_weight(i) for i in range(len(self.layers))],
+                          [self._wscale[i] for i in range(len(self.layers))],
+                          meta={"arch": int(self.arch), "in_hw": int(self.layers[0]["h"])})
+
+    def load_mnn(self, path: str):
+        """`Module::loadParameters(Variable::load(path))` (mnistTrain.cpp:375-376): the weights in
+        file order; the wscales from the side-car when there is one, otherwise the model keeps its
+        own (as the reference's modules do).  Every shape is checked before any device write."""
+        from . import mnn_snapshot
+        weights, wscales, _ = mnn_snapshot.load(path)
+        if len(weights) != len(self.layers):
+            raise ValueError(f"{path}: {len(weights)} parameters, model has {len(self.layers)} layers")
+        for i, w in enumerate(weights):
+            if tuple(w.shape) != self.weight_shape(i):
+                raise ValueError(f"snapshot parameter {i} is {tuple(w.shape)}, model layer is {self.weight_shape(i)}")
+        if wscales is None:
+            if len(self._wscale) != len(self.layers):
+                raise ValueError(f"{path}: no wscale side-car and the model's scales are not set")
+            wscales = [self._wscale[i] for i in range(len(self.layers))]
+        for i, (w, s) in enumerate(zip(weights, wscales)):
+            self.set_weight(i, w, s)
+
     def get_weight(self, i) -> np.ndarray:
         w = np.empty(self.weight_shape(i), np.int8)
         check(self._lib.niti_model_get_weight(self._h, i, w.ctypes.data_as(C.c_void_p)), "get_weight")

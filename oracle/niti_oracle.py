@@ -296,6 +296,35 @@ def maxpool_grad(x, y, dy, k=2, s=2, p=0):
     return dx
 
 
+def maxpool_grad_ref806(x, y, dy, out, kx=2, ky=2, sx=2, sy=2):
+    """NITI_DSP_MAXPOOLGRAD_REF_Int8 (NITI_DSPMaxPoolGradRef_Int8.cpp:17-80), its loops restated
+    in Python (small sizes only).  x and out are raw NHWC [N][H][W][C] buffers read as
+    [ih = N][iw = H][ib * ic] (:23-28); y / dy are flat buffers indexed at
+    (offset * bc) // kx // ky (:54-55).  out is updated in place and returned: bytes no window
+    visits keep their value (the op never zeroes its output)."""
+    x = np.ascontiguousarray(x).reshape(-1)
+    y = np.ascontiguousarray(y).reshape(-1)
+    dy = np.ascontiguousarray(dy).reshape(-1)
+    shp = out.shape
+    o = np.ascontiguousarray(out).reshape(-1).copy()
+    ih, iw, bc = shp[0], shp[1], shp[2] * shp[3]
+    for i in range(0, ih, sx):                       # :36
+        for j in range(0, iw, sy):                   # :37
+            offset = i * iw + j                      # :39
+            for m in range(bc // 128):               # :43
+                base = offset * bc // kx // ky + m * 128
+                yb, db = y[base:base + 128], dy[base:base + 128]
+                finish = np.zeros(128, bool)
+                for a in range(ky):                  # :59
+                    for b in range(kx):              # :61
+                        ko = (offset + a * iw + b) * bc + m * 128
+                        same = x[ko:ko + 128] == yb
+                        take = same & ~finish
+                        o[ko:ko + 128] = np.where(take, db, 0)
+                        finish |= take
+    return o.reshape(shp)
+
+
 def loss_grad(logits, ascale, onehot):
     logits = _c(logits, np.int8)
     onehot = _c(onehot, np.int32)

@@ -163,3 +163,33 @@ def test_host_dsp_transpose(T, ops):
     _run(ops, 808, None, [ops.tensor(host(T, x), nd(x.shape), 1), ops.tensor(T.tensor(perm, dtype=T.int32), (4, 1, 1, 1))],
          [ops.tensor(out, nd(want.shape), 1)])
     assert np.array_equal(out.numpy(), want)
+
+
+@pytest.mark.parametrize("shape,k,s", [((4, 8, 8, 32), 2, 2), ((6, 4, 4, 64), 2, 2), ((5, 6, 6, 40), 2, 3),
+                                       ((3, 9, 9, 48), 3, 3)])
+def test_dsp_maxpool_grad_ref_806(T, ops, oracle, shape, k, s):
+    """Slot 806 (NITI_DSPMaxPoolGradRef_Int8.cpp:17-80) on device tensors against the oracle's loop
+    restatement: its [batch][height][width * channel] reading, its y / dy index and the bytes it
+    leaves untouched (output pre-filled with a marker)."""
+    rng = np.random.default_rng(308 + k + s)
+    n, h, w, c = shape
+    x = rng.integers(-4, 4, size=shape, dtype=np.int8)           # ties exercise the first-match rule
+    ylen = max(n * h * w * c // (k * k), 1) + 1024
+    y = rng.integers(-4, 4, size=ylen, dtype=np.int8)
+    y[: x.size // (k * k)] = x.reshape(-1)[::k * k][: x.size // (k * k)]  # many exact matches
+    dy = rng.integers(-127, 128, size=ylen, dtype=np.int8)
+    init = np.full(shape, 77, np.int8)
+    want = oracle.maxpool_grad_ref806(x, y, dy, init, k, k, s, s)
+    out = T.from_numpy(init.copy()).cuda()
+    nd = (n, c, h, w)
+    _run(ops, 806, ops.conv_common(k, stride=s),
+         [ops.tensor(T.from_numpy(x).cuda(), nd, 1), ops.tensor(T.from_numpy(y).cuda(), (ylen, 1, 1, 1), 1),
+          ops.tensor(T.from_numpy(dy).cuda(), (ylen, 1, 1, 1), 1)], [ops.tensor(out, nd, 1)])
+    assert np.array_equal(out.cpu().numpy(), want)
+
+
+def test_dsp_maxpool_grad_ref_806_rejects_overlap(T, ops):
+    x = T.zeros((2, 4, 4, 128), dtype=T.int8, device="cuda")
+    ex = ops.NITIExecution(806, ops.conv_common(3, stride=2))
+    t = ops.tensor(x, (2, 128, 4, 4), 1)
+    assert ex.resize([t, t, t], [t]) == 2  # NOT_SUPPORT: stride < kernel (order-dependent in the reference)

@@ -93,3 +93,21 @@ def test_psto_matches_formula(oracle):
             pr = pr * 2
         out = np.clip(q + (qp > pr) * np.sign(a), -127, 127)
         assert (oracle.psto(a.astype(np.int32), s) == out).all(), s
+
+
+def test_maxpool_grad_ref806_walk(oracle):
+    """NITI_DSPMaxPoolGradRef_Int8.cpp:36-88 on one 2x2 window over a 128-byte plane: dy goes to the
+    first position (ky outer, kx inner) whose x equals y; the window's other positions get 0."""
+    x = np.zeros((2, 2, 1, 128), np.int8)
+    x[1, 0, 0, :] = 5
+    x[0, 1, 0, 3] = 5
+    y = np.full(128, 5, np.int8)
+    dy = np.arange(128, dtype=np.int8)
+    r = oracle.maxpool_grad_ref806(x, y, dy, np.full((2, 2, 1, 128), 9, np.int8)).reshape(4, 128)
+    assert (r[0] == 0).all() and r[1][3] == 3 and (np.delete(r[1], 3) == 0).all()
+    assert r[2][3] == 0 and (np.delete(r[2], 3) == np.delete(dy, 3)).all() and (r[3] == 0).all()
+    # a plane tail (bc % 128) is never visited: those bytes keep their value
+    x2 = np.zeros((2, 2, 1, 130), np.int8)
+    r2 = oracle.maxpool_grad_ref806(x2, np.zeros(200, np.int8), np.ones(200, np.int8),
+                                    np.full((2, 2, 1, 130), 9, np.int8)).reshape(-1)
+    assert (r2[128:130] == 9).all() and r2[0] == 1
