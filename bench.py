@@ -75,6 +75,50 @@ def cpu_baseline(arch, sample, threads_list):
     return legs
 
 
+def bench_resnet18(args):
+    """BASELINE config 5's network: ResNet-18 at 224x224, 1000 classes, one GPU (the data-parallel
+    path is wired for the VGG driver only).  A step: uint8 images through the device input
+    quantiser, then the whole NITI_SGD step on the HIP ops (niti_amd.resnet)."""
+    import numpy as np
+    import torch
+    from niti_amd import ops
+    from niti_amd.resnet import ResNet18
+    torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+    hw = args.in_hw or 224
+    batch = args.batch or 128
+    m = ResNet18(batch, hw, 1000)
+    layers = [dict(c_out=l["co"], c_in=l["ci"], kh=l["k"], kw=l["k"]) for l in m.convs]
+    for i, (w, s) in enumerate(synth_weights(layers, seed=17)):
+        m.set_weight(i, w, s)
+    rng = np.random.default_rng(100)
+    img = torch.from_numpy(rng.integers(0, 256, (batch, 3, hw, hw)).astype(np.uint8)).cuda()
+    labels = torch.from_numpy(rng.integers(0, 1000, batch).astype(np.int32)).cuda()
+
+    def step():
+        x, a = ops.image_quantize(img, ops.image_stats(img))
+        m.train_step(x, a, labels)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    tops = 2 * m.step_macs() * args.steps / el / 1e12
+    print(json.dumps({
+        "metric": "training images/sec + int8 MFMA TOPS, ResNet-18 ImageNet-224 (BASELINE config 5 network)",
+        "value": round(batch * args.steps / el, 2), "unit": "images/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "int8",
+        "data": "synthetic (random uint8 images through the on-device input quantiser; random labels; seeded weights)",
+        "config": {"workload": f"ResNet-18 NITI int8 training step, 3x{hw}x{hw}, 1000 classes", "global_batch": batch,
+                   "per_gpu_batch": batch, "parallelism": "single GPU (host-driven op sequence, niti_amd.resnet)"},
+        "int8_mfma_tops": round(tops, 2), "int8_mfma_frac_of_peak": round(tops / PEAK_INT8_TOPS, 4),
+        "roofline": None, "cpu_baseline": None}))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -82,7 +126,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=0, help="images per GPU per step (0: 256 VGG-11 / LeNet, "
                                                          "64 VGG-16 = BASELINE cfg 4's 512 over 8 GPUs)")
-    ap.add_argument("--arch", default="vgg11", choices=["vgg11", "lenet", "vgg16"])
+    ap.add_argument("--arch", default="vgg11", choices=["vgg11", "lenet", "vgg16", "resnet18"])
     ap.add_argument("--in-hw", type=int, default=0, help="input resolution (0: the architecture's own)")
     ap.add_argument("--cpu-sample", type=int, default=-1, help="images in the CPU baseline sample "
                                                                "(-1: 128 VGG-11, 512 LeNet, 0 VGG-16 = skip)")
@@ -104,6 +148,8 @@ def main():
                                                               "takes with this many K splits (0: its default; "
                                                               "-1: the autotuner's choice)")
     args = ap.parse_args()
+    if args.arch == "resnet18":
+        return bench_resnet18(args)
 
     import numpy as np
     import torch

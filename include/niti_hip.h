@@ -260,6 +260,16 @@ int niti_nhwc16_to_nchw(const int8_t* x, int n, int c, int hw, int cp, int8_t* o
 int niti_oihw_to_ohwi16(const int8_t* w, int co, int ci, int kk, int cip, int8_t* out, void* stream);
 int niti_ohwi16_to_oihw(const int8_t* w, int co, int ci, int kk, int cip, int8_t* out, void* stream);
 /* rest of the step, NHWC16 */
+/* ResNet pieces (niti_resnet.hip; the reference's NITI_Eltwise_Int8 is an empty stub,
+ * NITI_Eltwise_Int8.cpp:20-28, so the rule is this library's): z = hi * 2^d + (lo >> r) with
+ * d = min(|ea - eb|, 23), r = |ea - eb| - d, hi the operand of the larger exponent (a on ties);
+ * *ez = e_hi - d; max|z| into amax.  n % 16 == 0; requantise z with niti_requant_act. */
+int niti_residual_add(const int8_t* a, const int8_t* ea, const int8_t* b, const int8_t* eb, int64_t n, int32_t* z,
+                      int8_t* ez, uint32_t* amax, void* stream);
+/* global sum pool: acc[img][c] = sum over hw pixels of x NHWC16 [n][hw][cp] (+ max into amax) */
+int niti_sum_pool(const int8_t* x, int n, int hw, int cp, int32_t* acc, uint32_t* amax, void* stream);
+/* its gradient: dx[img][p][c] = dy[img][c] */
+int niti_sum_pool_grad(const int8_t* dy, int n, int hw, int cp, int8_t* dx, void* stream);
 int niti_maxpool(const int8_t* x, int n, int h, int w, int cp, int k, int s, int p, int8_t* y, int oh, int ow,
                  void* stream);
 int niti_maxpool_grad(const int8_t* x, const int8_t* y, const int8_t* dy, int n, int h, int w, int cp, int k,

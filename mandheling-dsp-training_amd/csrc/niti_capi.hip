@@ -327,6 +327,16 @@ int niti_oihw_to_ohwi16(const int8_t* w, int co, int ci, int kk, int cip, int8_t
 int niti_ohwi16_to_oihw(const int8_t* w, int co, int ci, int kk, int cip, int8_t* out, void* stream) {
     return code(niti::ohwi16_to_oihw(w, co, ci, kk, cip, out, S(stream)));
 }
+int niti_residual_add(const int8_t* a, const int8_t* ea, const int8_t* b, const int8_t* eb, int64_t n, int32_t* z,
+                      int8_t* ez, uint32_t* amax, void* stream) {
+    return code(niti::residual_add(a, ea, b, eb, n, z, ez, amax, S(stream)));
+}
+int niti_sum_pool(const int8_t* x, int n, int hw, int cp, int32_t* acc, uint32_t* amax, void* stream) {
+    return code(niti::sum_pool(x, n, hw, cp, acc, amax, S(stream)));
+}
+int niti_sum_pool_grad(const int8_t* dy, int n, int hw, int cp, int8_t* dx, void* stream) {
+    return code(niti::sum_pool_grad(dy, n, hw, cp, dx, S(stream)));
+}
 int niti_maxpool(const int8_t* x, int n, int h, int w, int cp, int k, int s, int p, int8_t* y, int oh, int ow,
                  void* stream) {
     return code(niti::maxpool_nhwc16(x, n, h, w, cp, k, s, p, y, oh, ow, S(stream)));

@@ -106,6 +106,13 @@ hipError_t conv_wgrad_acc(const ConvGeom& g, const int8_t* x_nhwc16, const int8_
 // C[i] = sum over z < splits of slab[z * stride + i] (+ max|C| into amax); n % 4 == 0
 hipError_t splitk_reduce_linear(const int32_t* slab, int splits, int64_t n, int64_t stride, int32_t* C,
                                 uint32_t* amax, hipStream_t st);
+// ---- residual add / global sum pool (niti_resnet.hip) ------------------------------------
+// z = aligned a + b (int32, n % 16 == 0 elements), its exponent into ez, max|z| into amax
+hipError_t residual_add(const int8_t* a, const int8_t* ea, const int8_t* b, const int8_t* eb, int64_t n,
+                        int32_t* z, int8_t* ez, uint32_t* amax, hipStream_t st);
+// acc[n][cp] = sum over hw pixels of x NHWC16 (+ max into amax); its gradient: dy broadcast
+hipError_t sum_pool(const int8_t* x, int n, int hw, int cp, int32_t* acc, uint32_t* amax, hipStream_t st);
+hipError_t sum_pool_grad(const int8_t* dy, int n, int hw, int cp, int8_t* dx, hipStream_t st);
 // ---- weight gradient on P16 pixel blocks (niti_wgrad.hip) --------------------------------
 // P16: [pixels/16][Cp][16] int8 (Cp % 16 == 0, pixels % 16 == 0)
 hipError_t nhwc16_to_p16(const int8_t* in, int64_t pixels, int cp, int8_t* out, hipStream_t st);

@@ -1,0 +1,115 @@
+// niti_resnet.hip -- the element-wise pieces a ResNet step adds to the NITI ops: the residual add
+// (and the gradient sum at a block input) with power-of-two exponent alignment, and the global
+// sum pool with its gradient.
+//
+// The reference defines no residual rule: NITI_Eltwise_Int8 is an empty stub
+// (execution-engine/source/backend/cpu/NITI_Eltwise_Int8.cpp:20-28).  The rule here keeps NITI's
+// integer-only arithmetic and its one requantisation per tensor:
+//   z = hi * 2^d + (lo >> r)        d = min(|ea - eb|, 23), r = |ea - eb| - d  (arithmetic shift)
+// where hi is the operand with the larger exponent (a on ties) and lo the other one; z is exact in
+// int32 (128 * 2^23 + 128 < 2^31) with exponent e_hi - d.  z then takes the forward path's range
+// estimate and PSTO requantisation (requant_act: shift = bitwidth(max|z|) - 7, exponent
+// e_z + inc), relu included for a block output.  The global pool is the sum over the pixels
+// (int32, the exponent unchanged) followed by the same requantisation; its gradient hands dy to
+// every pixel of the image.  oracle/niti_resnet_ref.py restates all three.
+#include "niti_device.hpp"
+#include "niti_kernels.hpp"
+
+namespace niti {
+
+__device__ __forceinline__ int32_t shr_floor(int32_t v, int r) { return r >= 31 ? (v < 0 ? -1 : 0) : v >> r; }
+
+__global__ void __launch_bounds__(256) residual_add_kernel(const int8_t* __restrict__ a, const int8_t* __restrict__ ea,
+                                                           const int8_t* __restrict__ b, const int8_t* __restrict__ eb,
+                                                           int64_t n16, int32_t* __restrict__ z,
+                                                           int8_t* __restrict__ ez, uint32_t* __restrict__ amax) {
+    const int xa = *ea, xb = *eb;
+    const bool a_hi = xa >= xb;
+    const int diff = a_hi ? xa - xb : xb - xa;
+    const int d = diff < 23 ? diff : 23, r = diff - d;
+    if (blockIdx.x == 0 && threadIdx.x == 0 && ez != nullptr) *ez = (int8_t)((a_hi ? xa : xb) - d);
+    uint32_t m = 0;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += (int64_t)gridDim.x * 256) {
+        const v16c va = ((const v16c*)a)[i], vb = ((const v16c*)b)[i];
+        v4i out[4];
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const int32_t hi = a_hi ? va[e] : vb[e], lo = a_hi ? vb[e] : va[e];
+            const int32_t s = hi * (1 << d) + shr_floor(lo, r);
+            out[e >> 2][e & 3] = s;
+            const uint32_t u = uabs32(s);
+            m = m > u ? m : u;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) ((v4i*)z)[4 * i + q] = out[q];
+    }
+    if (amax != nullptr) {
+        m = wave_max(m);
+        __shared__ uint32_t red[4];
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+        __syncthreads();
+        if (threadIdx.x == 0) publish_max(amax, max(max(red[0], red[1]), max(red[2], red[3])));
+    }
+}
+
+hipError_t residual_add(const int8_t* a, const int8_t* ea, const int8_t* b, const int8_t* eb, int64_t n,
+                        int32_t* z, int8_t* ez, uint32_t* amax, hipStream_t st) {
+    if (n < 0 || n % 16 != 0 || !a || !b || !ea || !eb || !z) return hipErrorInvalidValue;
+    const int64_t n16 = n / 16;
+    int64_t blocks = (n16 + 255) / 256;
+    blocks = blocks < 1 ? 1 : blocks > 2048 ? 2048 : blocks;
+    hipLaunchKernelGGL(residual_add_kernel, dim3((unsigned)blocks), dim3(256), 0, st, a, ea, b, eb, n16, z, ez, amax);
+    return hipGetLastError();
+}
+
+// acc[img][c] = sum over the image's hw pixels of x[img][p][c] (NHWC16, cp % 16 == 0): one thread
+// per (image, channel), consecutive threads consecutive channels
+__global__ void __launch_bounds__(256) sum_pool_kernel(const int8_t* __restrict__ x, int n, int hw, int cp,
+                                                       int32_t* __restrict__ acc, uint32_t* __restrict__ amax) {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    uint32_t m = 0;
+    if (t < (int64_t)n * cp) {
+        const int64_t img = t / cp;
+        const int c = (int)(t - img * cp);
+        const int8_t* p = x + img * hw * cp + c;
+        int32_t s = 0;
+        for (int i = 0; i < hw; ++i) s += p[(int64_t)i * cp];
+        acc[t] = s;
+        m = uabs32(s);
+    }
+    if (amax != nullptr) {
+        m = wave_max(m);
+        __shared__ uint32_t red[4];
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+        __syncthreads();
+        if (threadIdx.x == 0) publish_max(amax, max(max(red[0], red[1]), max(red[2], red[3])));
+    }
+}
+
+hipError_t sum_pool(const int8_t* x, int n, int hw, int cp, int32_t* acc, uint32_t* amax, hipStream_t st) {
+    if (n <= 0 || hw <= 0 || cp <= 0 || cp % 16 != 0 || (int64_t)hw * 127 * 2 > 0x7fffffff) return hipErrorInvalidValue;
+    const int64_t t = (int64_t)n * cp;
+    hipLaunchKernelGGL(sum_pool_kernel, dim3((unsigned)((t + 255) / 256)), dim3(256), 0, st, x, n, hw, cp, acc, amax);
+    return hipGetLastError();
+}
+
+// dx[img][p][c] = dy[img][c] for every pixel p (16-byte chunks)
+__global__ void __launch_bounds__(256) sum_pool_grad_kernel(const int8_t* __restrict__ dy, int64_t total16, int hw,
+                                                            int c16, int8_t* __restrict__ dx) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total16; i += (int64_t)gridDim.x * 256) {
+        const int64_t img = i / ((int64_t)hw * c16);
+        const int ch = (int)(i % c16);
+        ((v4i*)dx)[i] = ((const v4i*)dy)[img * c16 + ch];
+    }
+}
+
+hipError_t sum_pool_grad(const int8_t* dy, int n, int hw, int cp, int8_t* dx, hipStream_t st) {
+    if (n <= 0 || hw <= 0 || cp <= 0 || cp % 16 != 0) return hipErrorInvalidValue;
+    const int64_t total16 = (int64_t)n * hw * (cp / 16);
+    int64_t blocks = (total16 + 255) / 256;
+    blocks = blocks > 4096 ? 4096 : blocks;
+    hipLaunchKernelGGL(sum_pool_grad_kernel, dim3((unsigned)blocks), dim3(256), 0, st, dy, total16, hw, cp / 16, dx);
+    return hipGetLastError();
+}
+
+}  // namespace niti

@@ -129,6 +129,9 @@ def lib():
         "niti_nhwc16_to_nchw": (ci, [vp, ci, ci, ci, ci, vp, vp]),
         "niti_oihw_to_ohwi16": (ci, [vp, ci, ci, ci, ci, vp, vp]),
         "niti_ohwi16_to_oihw": (ci, [vp, ci, ci, ci, ci, vp, vp]),
+        "niti_residual_add": (ci, [vp, vp, vp, vp, i64, vp, vp, vp, vp]),
+        "niti_sum_pool": (ci, [vp, ci, ci, ci, vp, vp, vp]),
+        "niti_sum_pool_grad": (ci, [vp, ci, ci, ci, vp, vp]),
         "niti_maxpool": (ci, [vp] + [ci] * 7 + [vp, ci, ci, vp]),
         "niti_maxpool_grad": (ci, [vp, vp, vp] + [ci] * 10 + [vp, vp]),
         "niti_relu_grad": (ci, [vp, vp, i64, vp, vp]),

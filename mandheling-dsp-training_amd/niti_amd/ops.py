@@ -284,6 +284,32 @@ def sgd_update(acc, amax, w16, ci, rule=2, stream=None):
     return wT, g
 
 
+def residual_add(a, ea, b, eb, amax, stream=None):
+    """Exponent-aligned int32 sum of two int8 tensors (niti_resnet.hip) -> (z int32, ez int8 [1])."""
+    assert a.shape == b.shape and a.dtype == b.dtype == torch.int8
+    z = torch.empty(a.shape, dtype=torch.int32, device=a.device)
+    ez = torch.zeros(1, dtype=torch.int8, device=a.device)
+    check(L.lib().niti_residual_add(_ptr(a), _ptr(ea), _ptr(b), _ptr(eb), a.numel(), _ptr(z), _ptr(ez), _ptr(amax),
+                                    _stream(stream)), "residual_add")
+    return z, ez
+
+
+def sum_pool(x16, amax, stream=None):
+    """Global sum pool of x NHWC16 [n][h][w][cp] -> acc int32 [n][cp]."""
+    n, h, w, cp = x16.shape
+    acc = torch.empty((n, cp), dtype=torch.int32, device=x16.device)
+    check(L.lib().niti_sum_pool(_ptr(x16), n, h * w, cp, _ptr(acc), _ptr(amax), _stream(stream)), "sum_pool")
+    return acc
+
+
+def sum_pool_grad(dy16, h, w, stream=None):
+    """dx [n][h][w][cp] = dy [n][cp] at every pixel."""
+    n, cp = dy16.shape
+    dx = torch.empty((n, h, w, cp), dtype=torch.int8, device=dy16.device)
+    check(L.lib().niti_sum_pool_grad(_ptr(dy16), n, h * w, cp, _ptr(dx), _stream(stream)), "sum_pool_grad")
+    return dx
+
+
 def maxpool(x16, k=2, s=2, p=0, stream=None):
     n, h, w, cp = x16.shape
     oh = (h + 2 * p - min(k, h)) // s + 1

@@ -1,0 +1,212 @@
+"""ResNet-18 NITI int8 training step on the HIP ops (BASELINE.json config 5).
+
+The reference has no ResNet NITI model and its NITI_Eltwise_Int8 is an empty stub
+(execution-engine/source/backend/cpu/NITI_Eltwise_Int8.cpp:20-28); the residual and pooling rules
+are this library's (csrc/niti_resnet.hip, restated in oracle/niti_resnet_ref.py).  Every op runs on
+the device through the C ABI (niti_amd.ops): the convs on the int8 MFMA GEMMs with their range
+estimate and requantisation, the 7x7 / 2 stem, the 3x3 / 2 max pool, the 1x1 / 2 projections, the
+exponent-aligned residual adds, the global sum pool, the 1000-way head and NITI_SGD.  Activations
+stay in HBM as NHWC16 and every exponent stays a device int8 scalar: a step never synchronises the
+host.  Data parallel: not wired for this network (the VGG driver in csrc/niti_model.hip is).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import ops
+
+
+def resnet18_convs(hw=224, classes=1000):
+    """The 21 parameter layers in parameter order (conv1; per basic block conv a, conv b and the
+    1x1 / 2 projection of the first block of stages 2-4; the fc head as a 1x1 conv)."""
+    L = [dict(name="conv1", ci=3, co=64, k=7, stride=2, pad=3, h=hw)]
+    h = (hw + 6 - 7) // 2 + 1
+    h = (h + 2 - 3) // 2 + 1
+    ci = 64
+    for stage, co in enumerate((64, 128, 256, 512)):
+        for blk in range(2):
+            s = 2 if stage > 0 and blk == 0 else 1
+            L.append(dict(name=f"layer{stage + 1}.{blk}.a", ci=ci, co=co, k=3, stride=s, pad=1, h=h))
+            ho = (h + 2 - 3) // s + 1
+            L.append(dict(name=f"layer{stage + 1}.{blk}.b", ci=co, co=co, k=3, stride=1, pad=1, h=ho))
+            if s != 1 or ci != co:
+                L.append(dict(name=f"layer{stage + 1}.{blk}.proj", ci=ci, co=co, k=1, stride=s, pad=0, h=h))
+            ci, h = co, ho
+    L.append(dict(name="fc", ci=512, co=classes, k=1, stride=1, pad=0, h=1))
+    for l in L:
+        l["oh"] = (l["h"] + 2 * l["pad"] - l["k"]) // l["stride"] + 1
+    return L
+
+
+def _blocks(convs):
+    out, i = [], 1
+    while i < len(convs) - 1:
+        proj = i + 2 if convs[i + 2]["name"].endswith("proj") else None
+        out.append((i, i + 1, proj))
+        i += 3 if proj else 2
+    return out
+
+
+class ResNet18:
+    def __init__(self, batch: int, in_hw: int = 224, classes: int = 1000, device="cuda"):
+        if in_hw % 32 or in_hw < 32:
+            raise ValueError("in_hw must be a multiple of 32")
+        self.batch, self.in_hw, self.classes, self.dev = batch, in_hw, classes, device
+        self.convs = resnet18_convs(in_hw, classes)
+        self.blocks = _blocks(self.convs)
+        n = batch
+        self.geoms = [ops.geom(n, l["ci"], l["h"], l["h"], l["co"], l["k"], stride=l["stride"], pad=l["pad"])
+                      for l in self.convs]
+        self.w16 = [None] * len(self.convs)
+        self.wT = [None] * len(self.convs)
+        self.wscale = [None] * len(self.convs)
+        self.ws_dev = [None] * len(self.convs)
+        self.record = False
+        self.rec = {}
+
+    @property
+    def layers(self):
+        return self.convs
+
+    def weight_shape(self, i):
+        l = self.convs[i]
+        return (l["co"], l["ci"], l["k"], l["k"])
+
+    def set_weight(self, i, w: np.ndarray, wscale: int):
+        w = np.asarray(w)
+        if w.dtype != np.int8 or tuple(w.shape) != self.weight_shape(i):
+            raise ValueError(f"layer {i}: weight {w.dtype} {tuple(w.shape)}, want int8 {self.weight_shape(i)}")
+        self.w16[i] = ops.oihw_to_ohwi16(torch.from_numpy(np.ascontiguousarray(w)).to(self.dev))
+        self.wT[i] = ops.ohwi16_to_ihwo16(self.w16[i], self.convs[i]["ci"])
+        self.wscale[i] = int(wscale)
+        self.ws_dev[i] = torch.tensor([wscale], dtype=torch.int8, device=self.dev)
+
+    def get_weight(self, i) -> np.ndarray:
+        return ops.ohwi16_to_oihw(self.w16[i], self.convs[i]["ci"]).cpu().numpy()
+
+    # ---------------------------------------------------------------- pieces
+    def _nchw(self, t16, c):  # [n, h, w, cp] NHWC16 -> NCHW int8 (host, records only)
+        return t16.cpu().numpy()[..., :c].transpose(0, 3, 1, 2).copy()
+
+    def _fwd(self, i, x16, e_in, relu):
+        l, g = self.convs[i], self.geoms[i]
+        amax = ops.new_range(self.dev)
+        acc = ops.conv_fwd_acc(g, x16, self.w16[i], amax)
+        e_out = torch.zeros(1, dtype=torch.int8, device=self.dev)
+        y = ops.requant_act(acc, amax, exp_in=e_in, wscale=self.ws_dev[i], exp_out=e_out, relu=relu)
+        y = y.view(self.batch, l["oh"], l["oh"], -1)
+        if self.record:
+            self.rec.setdefault("fwd", {})[i] = (y, relu)
+        return y, e_out
+
+    def _dgrad(self, i, dy16, e_dy):
+        l, g = self.convs[i], self.geoms[i]
+        amax = ops.new_range(self.dev)
+        acc = ops.conv_dgrad_acc(g, dy16, self.wT[i], amax)
+        e_dx = torch.zeros(1, dtype=torch.int8, device=self.dev)
+        dx = ops.requant_act(acc, amax, exp_in=e_dy, wscale=self.ws_dev[i], exp_out=e_dx)
+        return dx.view(self.batch, l["h"], l["h"], -1), e_dx
+
+    def _wgrad_update(self, i, x16, dy16):
+        amax = ops.new_range(self.dev)
+        acc = ops.conv_wgrad_acc(self.geoms[i], x16, dy16, amax)
+        wT, g8 = ops.sgd_update(acc, amax, self.w16[i], self.convs[i]["ci"], rule=2)
+        self.wT[i] = wT
+        if self.record:
+            self.rec.setdefault("dy", {})[i] = dy16
+            self.rec.setdefault("dw", {})[i] = g8
+
+    def _add(self, a, ea, b, eb, relu):
+        amax = ops.new_range(self.dev)
+        z, ez = ops.residual_add(a, ea, b, eb, amax)
+        e_out = torch.zeros(1, dtype=torch.int8, device=self.dev)
+        q = ops.requant_act(z.view(-1, z.shape[-1]), amax, exp_in=ez, exp_out=e_out, relu=relu)
+        return q.view(a.shape), e_out
+
+    # ---------------------------------------------------------------- step
+    def train_step(self, x: torch.Tensor, exp_in: int, labels: torch.Tensor):
+        """One NITI_SGD step on x int8 NCHW [n][3][hw][hw] (device) with exponent exp_in (an int or
+        a device int8 [1], e.g. the input quantiser's ascale)."""
+        n = self.batch
+        if tuple(x.shape) != (n, 3, self.in_hw, self.in_hw) or x.dtype != torch.int8:
+            raise ValueError(f"x must be int8 {(n, 3, self.in_hw, self.in_hw)}")
+        if any(w is None for w in self.w16):
+            raise ValueError("set every layer's weight first")
+        self.rec = {}
+        x0 = ops.nchw_to_nhwc16(x)
+        e0 = exp_in if isinstance(exp_in, torch.Tensor) else torch.tensor([exp_in], dtype=torch.int8, device=self.dev)
+        saved_in = {}
+        # stem
+        r0, e = self._fwd(0, x0, e0, relu=True)
+        saved_in[0] = x0
+        p0 = ops.maxpool(r0, 3, 2, 1)
+        u, eu = p0, e
+        saved = []
+        for (ia, ib, ip) in self.blocks:
+            h, eh = self._fwd(ia, u, eu, relu=True)
+            yb, eb = self._fwd(ib, h, eh, relu=False)
+            saved_in[ia], saved_in[ib] = u, h
+            if ip is not None:
+                sc, es = self._fwd(ip, u, eu, relu=False)
+                saved_in[ip] = u
+            else:
+                sc, es = u, eu
+            out, eo = self._add(yb, eb, sc, es, relu=True)
+            saved.append((h, out))
+            u, eu = out, eo
+        # global sum pool, head, loss gradient
+        amax = ops.new_range(self.dev)
+        gsum = ops.sum_pool(u, amax)
+        eg = torch.zeros(1, dtype=torch.int8, device=self.dev)
+        g8 = ops.requant_act(gsum, amax, exp_in=eu, exp_out=eg).view(n, 1, 1, -1)
+        fc = len(self.convs) - 1
+        saved_in[fc] = g8
+        logits, el = self._fwd(fc, g8, eg, relu=False)
+        logits = logits.view(n, -1)
+        d = ops.loss_grad(logits, self.classes, el, labels).view(n, 1, 1, -1)
+        ed = torch.zeros(1, dtype=torch.int8, device=self.dev)
+        if self.record:
+            self.rec.update(logits=logits, exp_logits=el, pool=g8)
+        # backward: each layer's input gradient reads the old weights before its update
+        dg, edg = self._dgrad(fc, d, ed)
+        self._wgrad_update(fc, g8, d)
+        hh = u.shape[1]
+        du, edu = ops.sum_pool_grad(dg.view(n, -1), hh, hh), edg
+        for k in range(len(self.blocks) - 1, -1, -1):
+            ia, ib, ip = self.blocks[k]
+            h, out = saved[k]
+            dz = ops.relu_grad(out, du)
+            dh, edh = self._dgrad(ib, dz, edu)
+            self._wgrad_update(ib, h, dz)
+            dh = ops.relu_grad(h, dh)
+            dua, edua = self._dgrad(ia, dh, edh)
+            self._wgrad_update(ia, saved_in[ia], dh)
+            if ip is not None:
+                dus, edus = self._dgrad(ip, dz, edu)
+                self._wgrad_update(ip, saved_in[ip], dz)
+            else:
+                dus, edus = dz, edu
+            du, edu = self._add(dua, edua, dus, edus, relu=False)
+        dp = ops.maxpool_grad(r0, p0, du, 3, 2, 1)
+        d0 = ops.relu_grad(r0, dp)
+        self._wgrad_update(0, x0, d0)
+
+    def taps(self):
+        """Host copies of the last recorded step (record = True): per parameter layer the
+        requantised forward output (pre-relu values where relu follows are not kept: relu'd
+        outputs), its output gradient and int8 weight gradient, NCHW / OIHW; logits + exponent."""
+        out = {"fwd": {}, "dy": {}, "dw": {}}
+        for i, (y, _) in self.rec.get("fwd", {}).items():
+            out["fwd"][i] = self._nchw(y, self.convs[i]["co"])
+        for i, dy in self.rec.get("dy", {}).items():
+            out["dy"][i] = self._nchw(dy, self.convs[i]["co"])
+        for i, g8 in self.rec.get("dw", {}).items():
+            out["dw"][i] = g8.cpu().numpy()[..., :self.convs[i]["ci"]].transpose(0, 3, 1, 2).copy()
+        if "logits" in self.rec:
+            out["logits"] = self.rec["logits"].cpu().numpy()[:, :self.classes].copy()
+            out["exp_logits"] = int(self.rec["exp_logits"].item())
+        return out
+
+    def step_macs(self) -> int:
+        return sum(self.batch * l["oh"] * l["oh"] * l["co"] * l["ci"] * l["k"] * l["k"] for l in self.convs)

@@ -1,0 +1,77 @@
+"""ResNet-18 (BASELINE config 5) NITI step on the HIP ops against the oracle restatement.
+
+The reference has no ResNet NITI model and no residual rule (NITI_Eltwise_Int8.cpp:20-28 is an
+empty stub); oracle/niti_resnet_ref.py states the rules this library uses (exponent-aligned
+residual add and gradient sum, global sum pool, gradient exponents), so this parity is unpinned by
+construction.  Everything else -- the 7x7 / 2 stem, the 3x3 / 2 max pool, stride-2 3x3 and 1x1
+projection convs and their input / weight gradients, the 1000-way head, NITI_SGD -- follows the
+reference ops and must match bit for bit: every conv's requantised output, output gradient and
+int8 weight gradient, the logits and their exponent, and the updated weights, over two steps."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def T():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import niti_amd  # noqa: F401
+    return torch
+
+
+@pytest.mark.parametrize("hw,batch,classes", [(32, 2, 10), (64, 3, 1000)])
+def test_resnet18_step_matches_oracle(T, hw, batch, classes):
+    import niti_oracle as O
+    import niti_resnet_ref as RR
+    from niti_amd.resnet import ResNet18
+    convs = RR.resnet18_convs(hw, classes)
+    W, S = RR.init_weights(convs, seed=hw + batch)
+    rng = np.random.default_rng(hw * batch)
+    m = ResNet18(batch, hw, classes)
+    assert [c["name"] for c in m.convs] == [c["name"] for c in convs]
+    for i, (w, s) in enumerate(zip(W, S)):
+        m.set_weight(i, w, s)
+    m.record = True
+    for step in range(2):
+        x = rng.integers(-127, 128, (batch, 3, hw, hw)).astype(np.int8)
+        labels = rng.integers(0, classes, batch).astype(np.int32)
+        newW, rec = RR.train_step(convs, W, S, x, -2, labels, classes=classes)
+        m.train_step(T.from_numpy(x).cuda(), -2, T.from_numpy(labels).cuda())
+        t = m.taps()
+        assert t["exp_logits"] == rec["exp_logits"] and np.array_equal(t["logits"], rec["logits"]), step
+        for i, c in enumerate(convs):
+            relu = m.rec["fwd"][i][1]
+            want = O.relu(rec["fwd"][i]) if relu else rec["fwd"][i]
+            assert np.array_equal(t["fwd"][i], want), ("fwd", step, c["name"])
+            assert np.array_equal(t["dy"][i], rec["dy"][i]), ("dy", step, c["name"])
+            assert np.array_equal(t["dw"][i], rec["dw"][i]), ("dw", step, c["name"])
+            assert np.array_equal(m.get_weight(i), newW[i]), ("w", step, c["name"])
+        W = newW
+
+
+def test_residual_add_and_sum_pool(T):
+    """The two new kernels alone: exponent gaps 0..30 (the 23-bit cap and the floor shift of the
+    low operand), and the sum pool with its broadcast gradient."""
+    import niti_resnet_ref as RR
+    from niti_amd import ops
+    rng = np.random.default_rng(7)
+    a = rng.integers(-128, 128, (4, 5, 5, 32)).astype(np.int8)
+    b = rng.integers(-128, 128, (4, 5, 5, 32)).astype(np.int8)
+    for ea, eb in [(0, 0), (3, -2), (-5, 4), (10, -20), (-30, 0), (7, 7)]:
+        amax = ops.new_range()
+        z, ez = ops.residual_add(T.from_numpy(a).cuda(), T.tensor([ea], dtype=T.int8, device="cuda"),
+                                 T.from_numpy(b).cuda(), T.tensor([eb], dtype=T.int8, device="cuda"), amax)
+        zr, ezr = RR.residual_add(a, ea, b, eb)
+        assert np.array_equal(z.cpu().numpy(), zr) and int(ez.item()) == ezr, (ea, eb)
+        assert ops.range_max(amax) == int(np.abs(zr.astype(np.int64)).max())
+    x = rng.integers(-128, 128, (3, 7, 7, 48)).astype(np.int8)
+    amax = ops.new_range()
+    acc = ops.sum_pool(T.from_numpy(x).cuda(), amax).cpu().numpy()
+    assert np.array_equal(acc, x.astype(np.int32).sum(axis=(1, 2)))
+    assert ops.range_max(amax) == int(np.abs(acc).max())
+    dy = rng.integers(-128, 128, (3, 48)).astype(np.int8)
+    dx = ops.sum_pool_grad(T.from_numpy(dy).cuda(), 7, 7).cpu().numpy()
+    assert np.array_equal(dx, np.broadcast_to(dy[:, None, None, :], (3, 7, 7, 48)))

@@ -111,3 +111,17 @@ def test_maxpool_grad_ref806_walk(oracle):
     r2 = oracle.maxpool_grad_ref806(x2, np.zeros(200, np.int8), np.ones(200, np.int8),
                                     np.full((2, 2, 1, 130), 9, np.int8)).reshape(-1)
     assert (r2[128:130] == 9).all() and r2[0] == 1
+
+
+def test_residual_rule(oracle):
+    """The residual add / gradient sum rule of oracle/niti_resnet_ref.py (this library's: the
+    reference's NITI_Eltwise_Int8.cpp:20-28 is a stub)."""
+    import niti_resnet_ref as RR
+    a = np.array([100, -100, 1, -1], np.int8)
+    b = np.array([3, -3, 127, -128], np.int8)
+    z, e = RR.residual_add(a, 2, b, 0)          # a has the larger exponent: a * 4 + b, exponent 0
+    assert e == 0 and z.tolist() == [403, -403, 131, -132]
+    z, e = RR.residual_add(a, 0, b, 30)         # gap 30: b * 2^23 + (a >> 7) (floor), exponent 7
+    assert e == 7 and z.tolist() == [3 * 2**23 + 0, -3 * 2**23 - 1, 127 * 2**23 + 0, -128 * 2**23 - 1]
+    z, e = RR.residual_add(a, -4, b, -4)        # ties: a is hi, exponent unchanged
+    assert e == -4 and z.tolist() == [103, -103, 128, -129]
