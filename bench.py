@@ -95,15 +95,27 @@ def bench_resnet18(args):
     labels = torch.from_numpy(rng.integers(0, 1000, batch).astype(np.int32)).cuda()
 
     def step():
-        x, a = ops.image_quantize(img, ops.image_stats(img))
-        m.train_step(x, a, labels)
+        m.train_step_images(img, labels)
 
-    for _ in range(args.warmup):
+    for _ in range(max(args.warmup, 1)):
         step()
     torch.cuda.synchronize()
+    run = step
+    graph = None
+    if args.graph:  # the whole step (~450 launches from Python) captured once, replayed as one graph
+        try:
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                step()
+            run = graph.replay
+            run()
+            torch.cuda.synchronize()
+        except RuntimeError as e:  # not capturable here: direct launches
+            print(f"graph capture failed ({e}); direct launches", file=sys.stderr)
+            graph, run = None, step
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
+        run()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     tops = 2 * m.step_macs() * args.steps / el / 1e12
@@ -114,7 +126,8 @@ def bench_resnet18(args):
         "scaling": "weak", "vs_baseline": None, "dtype": "int8",
         "data": "synthetic (random uint8 images through the on-device input quantiser; random labels; seeded weights)",
         "config": {"workload": f"ResNet-18 NITI int8 training step, 3x{hw}x{hw}, 1000 classes", "global_batch": batch,
-                   "per_gpu_batch": batch, "parallelism": "single GPU (host-driven op sequence, niti_amd.resnet)"},
+                   "per_gpu_batch": batch, "parallelism": "single GPU (host-driven op sequence, niti_amd.resnet)",
+                   "launch": "hipGraph replay of the captured step" if graph is not None else "direct launches"},
         "int8_mfma_tops": round(tops, 2), "int8_mfma_frac_of_peak": round(tops / PEAK_INT8_TOPS, 4),
         "roofline": None, "cpu_baseline": None}))
 

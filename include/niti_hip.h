@@ -288,6 +288,9 @@ int niti_loss_grad(const int8_t* logits, int batch, int classes, int ld, const i
 int niti_image_stats(const uint8_t* images_nchw, int64_t n, uint64_t* stats, void* stream);
 int niti_image_quantize(const uint8_t* images_nchw, int n, int c, int hw, const uint64_t* stats, int64_t count,
                         int8_t* out_nchw, int8_t* ascale, void* stream);
+/* the same, x written as NHWC16 [n][hw][cp] (cp % 16 == 0, pad channels 0): a conv's input layout */
+int niti_image_quantize_nhwc16(const uint8_t* images_nchw, int n, int c, int hw, int cp, const uint64_t* stats,
+                               int64_t count, int8_t* out_nhwc16, int8_t* ascale, void* stream);
 
 /* ============================ 3. device-resident training step ========================= */
 /* LeNet on MNIST 1x28x28 (cfg 1/2); VGG-11 on CIFAR 3x32x32 (cfg 3); VGG-16 on ImageNet 3x224x224

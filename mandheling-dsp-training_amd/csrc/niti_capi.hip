@@ -360,6 +360,14 @@ int niti_image_quantize(const uint8_t* images, int n, int c, int hw, const uint6
     return code(niti::image_quantize(images, n, c, hw, c, reinterpret_cast<const unsigned long long*>(stats), count,
                                      out_nchw, ascale, false, S(stream)));
 }
+int niti_image_quantize_nhwc16(const uint8_t* images, int n, int c, int hw, int cp, const uint64_t* stats,
+                               int64_t count, int8_t* out_nhwc16, int8_t* ascale, void* stream) {
+    if (!images || !stats || !out_nhwc16 || n <= 0 || c <= 0 || hw <= 0 || cp < c || cp % 16 ||
+        count < (int64_t)n * c * hw)
+        return NITI_INVALID_VALUE;
+    return code(niti::image_quantize(images, n, c, hw, cp, reinterpret_cast<const unsigned long long*>(stats), count,
+                                     out_nhwc16, ascale, true, S(stream)));
+}
 int niti_loss_grad(const int8_t* logits, int batch, int classes, int ld, const int8_t* ascale, const int32_t* labels,
                    int8_t* out, void* stream) {
     return code(niti::loss_grad(logits, batch, classes, ld, ascale, labels, out, S(stream)));

@@ -161,6 +161,7 @@ def lib():
         "niti_model_attach_comm": (ci, [vp, C.c_char_p, ci, ci, ci]),
         "niti_image_stats": (ci, [vp, i64, vp, vp]),
         "niti_image_quantize": (ci, [vp, ci, ci, ci, vp, i64, vp, vp, vp]),
+        "niti_image_quantize_nhwc16": (ci, [vp, ci, ci, ci, ci, vp, i64, vp, vp, vp]),
         "niti_model_train_step_images": (ci, [vp, vp, vp, vp]),
         "niti_model_get_input": (ci, [vp, vp, C.POINTER(ci), vp]),
         "niti_local_group_create": (ci, [ci, C.POINTER(vp)]),

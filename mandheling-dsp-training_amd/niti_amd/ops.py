@@ -273,22 +273,27 @@ def requant_grad(acc, amax, rule=2, w_update=None, stream=None):
     return g
 
 
-def sgd_update(acc, amax, w16, ci, rule=2, stream=None):
-    """acc [co][kh][kw][cip] int32, w16 OHWI16 int8 (updated in place) -> (wT IHWO16, g OHWI16)."""
+def sgd_update(acc, amax, w16, ci, rule=2, stream=None, wT=None, g=None):
+    """acc [co][kh][kw][cip] int32, w16 OHWI16 int8 (updated in place) -> (wT IHWO16, g OHWI16);
+    wT / g may be given (written in place, e.g. persistent buffers of a captured step)."""
     co, kh, kw, cip = acc.shape
     cop = r16(co)
-    wT = torch.zeros((ci, kh, kw, cop), dtype=torch.int8, device=acc.device)
-    g = torch.empty(acc.shape, dtype=torch.int8, device=acc.device)
+    if wT is None:
+        wT = torch.zeros((ci, kh, kw, cop), dtype=torch.int8, device=acc.device)
+    if g is None:
+        g = torch.empty(acc.shape, dtype=torch.int8, device=acc.device)
+    assert wT.shape == (ci, kh, kw, cop) and g.shape == acc.shape
     check(L.lib().niti_sgd_update(_ptr(acc), _ptr(amax), rule, co, ci, kh * kw, cip, cop, _ptr(w16), _ptr(wT), _ptr(g),
                                   _stream(stream)), "sgd_update")
     return wT, g
 
 
-def residual_add(a, ea, b, eb, amax, stream=None):
+def residual_add(a, ea, b, eb, amax, stream=None, ez=None):
     """Exponent-aligned int32 sum of two int8 tensors (niti_resnet.hip) -> (z int32, ez int8 [1])."""
     assert a.shape == b.shape and a.dtype == b.dtype == torch.int8
     z = torch.empty(a.shape, dtype=torch.int32, device=a.device)
-    ez = torch.zeros(1, dtype=torch.int8, device=a.device)
+    if ez is None:
+        ez = torch.zeros(1, dtype=torch.int8, device=a.device)
     check(L.lib().niti_residual_add(_ptr(a), _ptr(ea), _ptr(b), _ptr(eb), a.numel(), _ptr(z), _ptr(ez), _ptr(amax),
                                     _stream(stream)), "residual_add")
     return z, ez
@@ -360,4 +365,16 @@ def image_quantize(images: torch.Tensor, stats: torch.Tensor, count: int | None 
     ascale = torch.zeros(1, dtype=torch.int8, device=images.device)
     check(L.lib().niti_image_quantize(_ptr(images), n, c, h * w, _ptr(stats), int(count or images.numel()),
                                       _ptr(out), _ptr(ascale), _stream(stream)), "image_quantize")
+    return out, ascale
+
+
+def image_quantize_nhwc16(images: torch.Tensor, stats: torch.Tensor, count: int | None = None, stream=None):
+    """image_quantize with x written as NHWC16 [n][h][w][16 * ceil(c / 16)] (a conv input)."""
+    assert images.dtype == torch.uint8 and images.is_contiguous() and images.dim() == 4
+    n, c, h, w = images.shape
+    out = torch.empty((n, h, w, r16(c)), dtype=torch.int8, device=images.device)
+    ascale = torch.zeros(1, dtype=torch.int8, device=images.device)
+    check(L.lib().niti_image_quantize_nhwc16(_ptr(images), n, c, h * w, r16(c), _ptr(stats),
+                                             int(count or images.numel()), _ptr(out), _ptr(ascale), _stream(stream)),
+          "image_quantize_nhwc16")
     return out, ascale

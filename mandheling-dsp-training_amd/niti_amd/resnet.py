@@ -64,6 +64,21 @@ class ResNet18:
         self.ws_dev = [None] * len(self.convs)
         self.record = False
         self.rec = {}
+        # range buffers and exponent scalars of one step, allocated once and handed out in order
+        # (one memset clears every range; exponents are always written before they are read)
+        self._ranges = torch.zeros((160, ops.MAX_WORDS), dtype=torch.int32, device=device)
+        self._exps = torch.zeros(160, dtype=torch.int8, device=device)
+        self._ri = self._ei = 0
+
+    def _range(self):
+        r = self._ranges[self._ri]
+        self._ri += 1
+        return r
+
+    def _exp(self):
+        e = self._exps[self._ei:self._ei + 1]
+        self._ei += 1
+        return e
 
     @property
     def layers(self):
@@ -77,10 +92,18 @@ class ResNet18:
         w = np.asarray(w)
         if w.dtype != np.int8 or tuple(w.shape) != self.weight_shape(i):
             raise ValueError(f"layer {i}: weight {w.dtype} {tuple(w.shape)}, want int8 {self.weight_shape(i)}")
-        self.w16[i] = ops.oihw_to_ohwi16(torch.from_numpy(np.ascontiguousarray(w)).to(self.dev))
-        self.wT[i] = ops.ohwi16_to_ihwo16(self.w16[i], self.convs[i]["ci"])
+        w16 = ops.oihw_to_ohwi16(torch.from_numpy(np.ascontiguousarray(w)).to(self.dev))
+        wT = ops.ohwi16_to_ihwo16(w16, self.convs[i]["ci"])
+        if self.w16[i] is None:
+            self.w16[i], self.wT[i] = w16, wT
+        else:  # in place: a captured step holds these addresses
+            self.w16[i].copy_(w16)
+            self.wT[i].copy_(wT)
         self.wscale[i] = int(wscale)
-        self.ws_dev[i] = torch.tensor([wscale], dtype=torch.int8, device=self.dev)
+        if self.ws_dev[i] is None:
+            self.ws_dev[i] = torch.tensor([wscale], dtype=torch.int8, device=self.dev)
+        else:
+            self.ws_dev[i].fill_(int(wscale))
 
     def get_weight(self, i) -> np.ndarray:
         return ops.ohwi16_to_oihw(self.w16[i], self.convs[i]["ci"]).cpu().numpy()
@@ -91,9 +114,9 @@ class ResNet18:
 
     def _fwd(self, i, x16, e_in, relu):
         l, g = self.convs[i], self.geoms[i]
-        amax = ops.new_range(self.dev)
+        amax = self._range()
         acc = ops.conv_fwd_acc(g, x16, self.w16[i], amax)
-        e_out = torch.zeros(1, dtype=torch.int8, device=self.dev)
+        e_out = self._exp()
         y = ops.requant_act(acc, amax, exp_in=e_in, wscale=self.ws_dev[i], exp_out=e_out, relu=relu)
         y = y.view(self.batch, l["oh"], l["oh"], -1)
         if self.record:
@@ -102,25 +125,26 @@ class ResNet18:
 
     def _dgrad(self, i, dy16, e_dy):
         l, g = self.convs[i], self.geoms[i]
-        amax = ops.new_range(self.dev)
+        amax = self._range()
         acc = ops.conv_dgrad_acc(g, dy16, self.wT[i], amax)
-        e_dx = torch.zeros(1, dtype=torch.int8, device=self.dev)
+        e_dx = self._exp()
         dx = ops.requant_act(acc, amax, exp_in=e_dy, wscale=self.ws_dev[i], exp_out=e_dx)
         return dx.view(self.batch, l["h"], l["h"], -1), e_dx
 
     def _wgrad_update(self, i, x16, dy16):
-        amax = ops.new_range(self.dev)
+        amax = self._range()
         acc = ops.conv_wgrad_acc(self.geoms[i], x16, dy16, amax)
-        wT, g8 = ops.sgd_update(acc, amax, self.w16[i], self.convs[i]["ci"], rule=2)
-        self.wT[i] = wT
+        # the transposed copy is rewritten in place (its input gradient above read it first), so a
+        # captured step keeps reading the same buffer
+        _, g8 = ops.sgd_update(acc, amax, self.w16[i], self.convs[i]["ci"], rule=2, wT=self.wT[i])
         if self.record:
             self.rec.setdefault("dy", {})[i] = dy16
             self.rec.setdefault("dw", {})[i] = g8
 
     def _add(self, a, ea, b, eb, relu):
-        amax = ops.new_range(self.dev)
-        z, ez = ops.residual_add(a, ea, b, eb, amax)
-        e_out = torch.zeros(1, dtype=torch.int8, device=self.dev)
+        amax = self._range()
+        z, ez = ops.residual_add(a, ea, b, eb, amax, ez=self._exp())
+        e_out = self._exp()
         q = ops.requant_act(z.view(-1, z.shape[-1]), amax, exp_in=ez, exp_out=e_out, relu=relu)
         return q.view(a.shape), e_out
 
@@ -129,12 +153,15 @@ class ResNet18:
         """One NITI_SGD step on x int8 NCHW [n][3][hw][hw] (device) with exponent exp_in (an int or
         a device int8 [1], e.g. the input quantiser's ascale)."""
         n = self.batch
-        if tuple(x.shape) != (n, 3, self.in_hw, self.in_hw) or x.dtype != torch.int8:
-            raise ValueError(f"x must be int8 {(n, 3, self.in_hw, self.in_hw)}")
+        if x.dtype != torch.int8 or tuple(x.shape) not in ((n, 3, self.in_hw, self.in_hw),
+                                                            (n, self.in_hw, self.in_hw, 16)):
+            raise ValueError(f"x must be int8 NCHW {(n, 3, self.in_hw, self.in_hw)} or NHWC16")
         if any(w is None for w in self.w16):
             raise ValueError("set every layer's weight first")
         self.rec = {}
-        x0 = ops.nchw_to_nhwc16(x)
+        self._ranges.zero_()
+        self._ri = self._ei = 0
+        x0 = ops.nchw_to_nhwc16(x) if x.shape[1] == 3 else x
         e0 = exp_in if isinstance(exp_in, torch.Tensor) else torch.tensor([exp_in], dtype=torch.int8, device=self.dev)
         saved_in = {}
         # stem
@@ -156,16 +183,17 @@ class ResNet18:
             saved.append((h, out))
             u, eu = out, eo
         # global sum pool, head, loss gradient
-        amax = ops.new_range(self.dev)
+        amax = self._range()
         gsum = ops.sum_pool(u, amax)
-        eg = torch.zeros(1, dtype=torch.int8, device=self.dev)
+        eg = self._exp()
         g8 = ops.requant_act(gsum, amax, exp_in=eu, exp_out=eg).view(n, 1, 1, -1)
         fc = len(self.convs) - 1
         saved_in[fc] = g8
         logits, el = self._fwd(fc, g8, eg, relu=False)
         logits = logits.view(n, -1)
         d = ops.loss_grad(logits, self.classes, el, labels).view(n, 1, 1, -1)
-        ed = torch.zeros(1, dtype=torch.int8, device=self.dev)
+        ed = self._exp()
+        ed.zero_()
         if self.record:
             self.rec.update(logits=logits, exp_logits=el, pool=g8)
         # backward: each layer's input gradient reads the old weights before its update
@@ -191,6 +219,12 @@ class ResNet18:
         dp = ops.maxpool_grad(r0, p0, du, 3, 2, 1)
         d0 = ops.relu_grad(r0, dp)
         self._wgrad_update(0, x0, d0)
+
+    def train_step_images(self, images: torch.Tensor, labels: torch.Tensor):
+        """NITIInt8Train's input quantiser (MnistUtils.cpp:83-93) on uint8 images [n][3][hw][hw],
+        straight into the stem's NHWC16 input, then the step."""
+        x, a = ops.image_quantize_nhwc16(images, ops.image_stats(images))
+        self.train_step(x, a, labels)
 
     def taps(self):
         """Host copies of the last recorded step (record = True): per parameter layer the

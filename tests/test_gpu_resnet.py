@@ -75,3 +75,39 @@ def test_residual_add_and_sum_pool(T):
     dy = rng.integers(-128, 128, (3, 48)).astype(np.int8)
     dx = ops.sum_pool_grad(T.from_numpy(dy).cuda(), 7, 7).cpu().numpy()
     assert np.array_equal(dx, np.broadcast_to(dy[:, None, None, :], (3, 7, 7, 48)))
+
+
+def test_resnet18_images_and_graph_replay(T):
+    """uint8 images through the NHWC16 input quantiser, then the step captured as a hipGraph and
+    replayed on new data: each replay equals the oracle step (quantiser included)."""
+    import niti_oracle as O
+    import niti_resnet_ref as RR
+    from niti_amd.resnet import ResNet18
+    hw, batch, classes = 32, 2, 10
+    convs = RR.resnet18_convs(hw, classes)
+    W, S = RR.init_weights(convs, seed=77)
+    rng = np.random.default_rng(77)
+    m = ResNet18(batch, hw, classes)
+    for i, (w, s) in enumerate(zip(W, S)):
+        m.set_weight(i, w, s)
+    img = T.zeros((batch, 3, hw, hw), dtype=T.uint8, device="cuda")
+    lab = T.zeros(batch, dtype=T.int32, device="cuda")
+    m.train_step_images(img, lab)          # warm-up (allocator), then restore the weights
+    for i, (w, s) in enumerate(zip(W, S)):
+        m.set_weight(i, w, s)
+    g = T.cuda.CUDAGraph()
+    imgs = [rng.integers(0, 256, (batch, 3, hw, hw)).astype(np.uint8) for _ in range(3)]
+    labs = [rng.integers(0, classes, batch).astype(np.int32) for _ in range(3)]
+    img.copy_(T.from_numpy(imgs[0]))
+    lab.copy_(T.from_numpy(labs[0]))
+    with T.cuda.graph(g):
+        m.train_step_images(img, lab)      # capture only: nothing runs
+    for step in range(2):
+        img.copy_(T.from_numpy(imgs[step]))
+        lab.copy_(T.from_numpy(labs[step]))
+        g.replay()
+        T.cuda.synchronize()
+        x, a = O.quantize_images(imgs[step])
+        W, _ = RR.train_step(convs, W, S, x, a, labs[step], classes=classes)
+        for i in range(len(convs)):
+            assert np.array_equal(m.get_weight(i), W[i]), (step, convs[i]["name"])
