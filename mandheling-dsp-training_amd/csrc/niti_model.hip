@@ -779,6 +779,11 @@ int Model::autotune(hipStream_t st, int reps) {
         return r;
     };
     if (hipMemsetAsync(amax, 0, amax_bytes, st) != hipSuccess) rc = NITI_NO_EXECUTION;
+    // NITI_DIAG_TUNE_LOG=1 (diagnostics): every candidate's time on stderr
+    const bool log = getenv("NITI_DIAG_TUNE_LOG") != nullptr;
+    auto note = [&](int i, int op, const PlanChoice& c, float us) {
+        if (log) fprintf(stderr, "tune layer %d op %d plan (%d,%d,%d,%d) %.2f us\n", i, op, c.bm, c.bn, c.splits, c.strat, us);
+    };
     static const int tiles[7][2] = {{PLAN_TAPS_TILE, PLAN_TAPS_TILE}, {128, 128}, {128, 64}, {64, 128}, {64, 64},
                                     {256, 128}, {128, 256}};
     static const int split_opts[] = {2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64};
@@ -810,6 +815,7 @@ int Model::autotune(hipStream_t st, int reps) {
             }
             float best_us = 0.f;
             rc = time_op(i, op, &best_us);
+            note(i, op, best, best_us);
             const bool taps = op == PLAN_WGRAD && conv_wgrad_taps_ok(g);
             if (op == PLAN_WGRAD && conv_wgrad_p16_ok(g)) {
                 for (int sp : {1, 2, 4, 8}) {
@@ -822,6 +828,7 @@ int Model::autotune(hipStream_t st, int reps) {
                     plan_override_set(key, cand);
                     float us = 0.f;
                     rc = time_op(i, op, &us);
+                    note(i, op, cand, us);
                     if (rc == NITI_NO_ERROR && us < best_us) {
                         best_us = us;
                         best = cand;
@@ -852,6 +859,7 @@ int Model::autotune(hipStream_t st, int reps) {
                     plan_override_set(key, cand);
                     float us = 0.f;
                     rc = time_op(i, op, &us);
+                    note(i, op, cand, us);
                     if (rc != NITI_NO_ERROR) break;
                     if (us < best_us) {
                         best_us = us;

@@ -31,6 +31,8 @@ namespace niti {
 
 namespace {
 
+typedef signed char v16c __attribute__((ext_vector_type(16)));
+
 __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
@@ -140,7 +142,10 @@ __device__ __forceinline__ int8_t quant_pixel(uint32_t p, const QuantParams& q) 
     return (int8_t)(int)roundf(y / q.range * 127.0f);
 }
 
-// out: NHWC16 [n][hw][cp] (nhwc = true, the step's layer-0 input) or NCHW [n][c][hw]
+// out: NHWC16 [n][hw][cp] (nhwc = true, the step's layer-0 input: one thread per pixel, its c
+// channels packed into 16-byte stores) or NCHW [n][c][hw] (one thread per element).  Thread 0 of
+// each block derives the parameters (double log / sqrt), so the grid is kept to a few blocks per
+// CU and each thread loops.
 template <bool NHWC>
 __global__ void __launch_bounds__(256) image_quant_kernel(const uint8_t* __restrict__ img, int n, int c, int hw,
                                                           int cp, const unsigned long long* __restrict__ stats,
@@ -153,16 +158,28 @@ __global__ void __launch_bounds__(256) image_quant_kernel(const uint8_t* __restr
     }
     __syncthreads();
     const QuantParams q = sq;
-    const int64_t total = NHWC ? (int64_t)n * hw * cp : (int64_t)n * c * hw;
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-        if (NHWC) {
-            const int ch = (int)(i % cp);
-            const int64_t r = i / cp;
-            const int64_t px = r % hw, b = r / hw;
-            out[i] = ch < c ? quant_pixel(img[(b * c + ch) * hw + px], q) : (int8_t)0;
-        } else {
-            out[i] = quant_pixel(img[i], q);
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    if (NHWC) {
+        const int64_t pixels = (int64_t)n * hw;
+        const int c16 = cp / 16;
+        for (int64_t pxl = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; pxl < pixels; pxl += stride) {
+            const int64_t b = pxl / hw, px = pxl - b * hw;
+            const uint8_t* src = img + b * c * hw + px;
+            int8_t* dst = out + pxl * cp;
+            for (int k = 0; k < c16; ++k) {
+                v16c v;
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    const int ch = 16 * k + j;
+                    v[j] = ch < c ? quant_pixel(src[(int64_t)ch * hw], q) : (int8_t)0;
+                }
+                *(v16c*)(dst + 16 * k) = v;
+            }
         }
+    } else {
+        const int64_t total = (int64_t)n * c * hw;
+        for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += stride)
+            out[i] = quant_pixel(img[i], q);
     }
 }
 
@@ -172,8 +189,10 @@ hipError_t image_stats(const uint8_t* img, int64_t n, unsigned long long* stats,
     if (n <= 0) return hipErrorInvalidValue;
     hipError_t e = hipMemsetAsync(stats, 0, 4 * sizeof(unsigned long long), st);
     if (e != hipSuccess) return e;
-    int64_t blocks = (n / 16 + 255) / 256;
-    blocks = blocks < 1 ? 1 : blocks > 1024 ? 1024 : blocks;
+    // a few blocks, each thread looping over 16-byte loads: every block ends in 4 device-scope
+    // atomics on one cache line, and 192 blocks of them serialised into ~8 us
+    int64_t blocks = (n / 16 + 2047) / 2048;
+    blocks = blocks < 1 ? 1 : blocks > 32 ? 32 : blocks;
     hipLaunchKernelGGL(image_stats_kernel, dim3((unsigned)blocks), dim3(256), 0, st, img, n, stats);
     return hipGetLastError();
 }
@@ -181,9 +200,10 @@ hipError_t image_stats(const uint8_t* img, int64_t n, unsigned long long* stats,
 hipError_t image_quantize(const uint8_t* img, int n, int c, int hw, int cp, const unsigned long long* stats,
                           int64_t count, int8_t* out, int8_t* ascale, bool nhwc16, hipStream_t st) {
     if (n <= 0 || c <= 0 || hw <= 0 || count <= 0 || (nhwc16 && cp < c)) return hipErrorInvalidValue;
-    const int64_t total = nhwc16 ? (int64_t)n * hw * cp : (int64_t)n * c * hw;
+    if (nhwc16 && cp % 16 != 0) return hipErrorInvalidValue;
+    const int64_t total = nhwc16 ? (int64_t)n * hw : (int64_t)n * c * hw;
     int64_t blocks = (total + 255) / 256;
-    blocks = blocks > 4096 ? 4096 : blocks;
+    blocks = blocks > 512 ? 512 : blocks;
     if (nhwc16)
         hipLaunchKernelGGL(image_quant_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, st, img, n, c, hw, cp,
                            stats, count, out, ascale);
