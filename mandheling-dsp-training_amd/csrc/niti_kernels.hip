@@ -2621,15 +2621,20 @@ __device__ __forceinline__ void sgd_tile(const SgdJob& J, int ci0, int co0, int 
 // Every layer's NITI_SGD update of a step in one launch: block b belongs to the job whose
 // [start, start + tiles) range holds it (the updates are independent; the input gradients
 // that read the old weights have all run by then).
-__global__ void sgd_update_kernel(SgdJobs jobs) {
+__global__ void sgd_update_kernel(SgdJobs jobs, int total) {
     __shared__ int8_t T[64][64 + 4];
-    int b = blockIdx.x, j = 0;
-    while (j + 1 < jobs.n && b >= jobs.start[j + 1]) ++j;
-    const SgdJob& J = jobs.job[j];
-    b -= jobs.start[j];
-    const int tx = (J.cip + 63) / 64, ty = (J.cop + 63) / 64;
-    const int k = b / (tx * ty), rem = b - k * tx * ty;
-    sgd_tile(J, (rem % tx) * 64, (rem / tx) * 64, k, T);
+    // a block takes tiles b, b + gridDim, ...: one resident wave of blocks instead of a full
+    // wave plus a straggling partial one
+    for (int bb = blockIdx.x; bb < total; bb += gridDim.x) {
+        int b = bb, j = 0;
+        while (j + 1 < jobs.n && b >= jobs.start[j + 1]) ++j;
+        const SgdJob& J = jobs.job[j];
+        b -= jobs.start[j];
+        const int tx = (J.cip + 63) / 64, ty = (J.cop + 63) / 64;
+        const int k = b / (tx * ty), rem = b - k * tx * ty;
+        if (bb != (int)blockIdx.x) __syncthreads();  // the previous tile's transposed reads are done
+        sgd_tile(J, (rem % tx) * 64, (rem / tx) * 64, k, T);
+    }
 }
 
 hipError_t sgd_update_many(const SgdJob* jobs, int n, hipStream_t st) {
@@ -2643,7 +2648,8 @@ hipError_t sgd_update_many(const SgdJob* jobs, int n, hipStream_t st) {
         J.start[i] = total;
         total += ((jobs[i].cip + 63) / 64) * ((jobs[i].cop + 63) / 64) * jobs[i].kk;
     }
-    hipLaunchKernelGGL(sgd_update_kernel, dim3(total), dim3(256), 0, st, J);
+    const int grid = total < 1536 ? total : 1536;  // 6 blocks per CU
+    hipLaunchKernelGGL(sgd_update_kernel, dim3(grid), dim3(256), 0, st, J, total);
     return hipGetLastError();
 }
 
