@@ -2509,6 +2509,159 @@ __global__ void __launch_bounds__(256) requant_quad_kernel(ActRequant r, RqGeom 
     }
 }
 
+// ---- first layer on its im2col copy (K = 32) -------------------------------------------------
+// y[p][co] = sum_k xcol[p][k] * w[co][k], k < 32: one v_mfma_i32_32x32x32_i8 per 32 pixels x 32
+// output channels, both operands straight from memory (a lane's 16-byte fragment is 16
+// consecutive k of one row).  Pass 0 publishes max|y| (NITI_RangeEstimate); pass 1 recomputes y
+// and requantises it with the forward rule (as requant_quad_kernel), relu, stores the NHWC16
+// output and, with pool_out, the 2x2 max pool of the relu'd values.  A wave takes a pair of
+// output rows segment by segment (32 pixels of each row), so each pooled pixel's four inputs
+// sit in one lane: the x pairs in adjacent accumulator registers, the y pair in the two rows'
+// accumulators.  Requires OW % 32 == 0 and OH even (VGG's 32x32 and 224x224 first layers).
+struct Conv0 {
+    const int8_t* x;  // xcol [P][32]
+    const int8_t* w;  // [co][32]
+    uint32_t wbytes;
+    int co, cop, oh, ow;
+    int64_t units;    // (image, row pair, 32-pixel segment)
+    uint32_t* amax;   // pass 0 out / pass 1 in
+    int8_t* out;      // NHWC16 [P][cop]
+    int8_t* pool_out; // [P / 4][cop] or null
+    const int8_t *exp_in, *wscale;
+    int8_t* exp_out;
+    int relu;
+};
+
+template <int PASS>
+__global__ void __launch_bounds__(256) conv0_kernel(Conv0 g) {
+    const int lane = threadIdx.x & 63;
+    const int wave = blockIdx.x * 4 + (threadIdx.x >> 6), nwaves = gridDim.x * 4;
+    const int h = lane >> 5, c = lane & 31;
+    const __amdgpu_buffer_rsrc_t rw = make_rsrc(g.w, g.wbytes);
+    int s = 2, shift = 0;
+    bool raw = false;
+    if (PASS == 1) {
+        const int bw = bitwidth_of(read_max(g.amax));
+        shift = bw - 7;
+        s = shift > 1 ? shift : 2;
+        raw = shift <= 0;
+        if (blockIdx.x == 0 && threadIdx.x == 0 && g.exp_out != nullptr) {
+            const int inc = shift > 1 ? shift : (shift == 1 ? 2 : 0);
+            *g.exp_out = (int8_t)((g.exp_in ? (int)*g.exp_in : 0) + (g.wscale ? (int)*g.wscale : 0) + inc);
+        }
+    }
+    const int tiles = g.cop / 32;
+    uint32_t m = 0;
+    const int segs = g.ow / 32, pairs = g.oh / 2;
+    for (int64_t u = wave; u < g.units; u += nwaves) {
+        const int seg = (int)(u % segs);
+        const int64_t rest = u / segs;
+        const int pr = (int)(rest % pairs);
+        const int64_t img = rest / pairs;
+        const int64_t p0 = (img * g.oh + 2 * pr) * g.ow + seg * 32;  // first pixel of the top row segment
+        v4i a[2];
+#pragma unroll
+        for (int r = 0; r < 2; ++r) a[r] = *(const v4i*)(g.x + (p0 + (int64_t)r * g.ow + c) * 32 + 16 * h);
+        for (int t = 0; t < tiles; ++t) {
+            const v4i b = buf_load16(rw, (uint32_t)((t * 32 + c) * 32 + 16 * h));
+            v16i acc[2];
+#pragma unroll
+            for (int r = 0; r < 2; ++r)
+                acc[r] = __builtin_amdgcn_mfma_i32_32x32x32_i8(b, a[r], v16i{}, 0, 0, 0);
+            // acc[r][i]: output channel t * 32 + (i & 3) + 8 (i >> 2) + 4 h, pixel p0 + r * ow + c
+            if (PASS == 0) {
+#pragma unroll
+                for (int r = 0; r < 2; ++r)
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) {
+                        const int ch = t * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+                        const uint32_t v = ch < g.co ? uabs32(acc[r][i]) : 0u;
+                        m = m > v ? m : v;
+                    }
+            } else {
+                int8_t q[2][16];
+#pragma unroll
+                for (int r = 0; r < 2; ++r)
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) {
+                        int32_t v = raw ? (int32_t)(int8_t)acc[r][i] : psto_fast(acc[r][i], s);
+                        if (g.relu && v < 0) v = 0;
+                        q[r][i] = (int8_t)v;
+                    }
+                // 16 channels per lane, 4 runs of 4 consecutive channels: one dword each
+#pragma unroll
+                for (int r = 0; r < 2; ++r) {
+                    int8_t* o = g.out + (p0 + (int64_t)r * g.ow + c) * g.cop + t * 32 + 4 * h;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const uint32_t d = (uint32_t)(uint8_t)q[r][4 * j] | (uint32_t)(uint8_t)q[r][4 * j + 1] << 8 |
+                                           (uint32_t)(uint8_t)q[r][4 * j + 2] << 16 | (uint32_t)(uint8_t)q[r][4 * j + 3] << 24;
+                        *(uint32_t*)(o + 8 * j) = d;
+                    }
+                }
+                if (g.pool_out != nullptr) {
+                    // the pixel pair (c, c ^ 1) sits in lanes c and c ^ 1: exchange, max, even lanes store
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        uint32_t d = 0;
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            const int i = 4 * j + e;
+                            const int v0 = q[0][i] > q[1][i] ? q[0][i] : q[1][i];
+                            const int v1 = __shfl_xor(v0, 1, 64);
+                            d |= (uint32_t)(uint8_t)(v0 > v1 ? v0 : v1) << (8 * e);
+                        }
+                        if ((c & 1) == 0) {
+                            const int64_t pp = (img * (g.oh / 2) + pr) * (g.ow / 2) + seg * 16 + (c >> 1);
+                            *(uint32_t*)(g.pool_out + pp * g.cop + t * 32 + 4 * h + 8 * j) = d;
+                        }
+                    }
+                }
+            }
+        }
+    }
+    if (PASS == 0) {
+        m = wave_max(m);
+        __shared__ uint32_t red[4];
+        if (lane == 0) red[threadIdx.x >> 6] = m;
+        __syncthreads();
+        if (threadIdx.x == 0) publish_max(g.amax, max(max(red[0], red[1]), max(red[2], red[3])));
+    }
+}
+
+bool conv0_ok(const ConvGeom& g) {
+    return g.kh == 1 && g.kw == 1 && g.c_in == 32 && g.cip == 32 && g.ow % 32 == 0 && g.oh % 2 == 0 && g.sh == 1 &&
+           g.pt == 0 && g.cop % 32 == 0;
+}
+
+hipError_t conv0_fwd(const ConvGeom& g, const int8_t* xcol, const int8_t* w, uint32_t* amax, const ActOut& o,
+                     int pass, hipStream_t st) {
+    if (!conv0_ok(g) || o.out == nullptr || o.relu_mask != nullptr) return hipErrorInvalidValue;
+    Conv0 k{};
+    k.x = xcol;
+    k.w = w;
+    k.wbytes = (uint32_t)((int64_t)g.c_out * 32);
+    k.co = g.c_out;
+    k.cop = g.cop;
+    k.oh = g.oh;
+    k.ow = g.ow;
+    k.units = (int64_t)g.n * (g.oh / 2) * (g.ow / 32);
+    k.amax = amax;
+    k.out = o.out;
+    k.pool_out = o.pool.pool_out;
+    k.exp_in = o.exp_in;
+    k.wscale = o.wscale;
+    k.exp_out = o.exp_out;
+    k.relu = o.relu;
+    int64_t blocks = (k.units + 3) / 4;
+    blocks = blocks > 1024 ? 1024 : blocks;
+    if (pass == 0)
+        hipLaunchKernelGGL(conv0_kernel<0>, dim3((unsigned)blocks), dim3(256), 0, st, k);
+    else
+        hipLaunchKernelGGL(conv0_kernel<1>, dim3((unsigned)blocks), dim3(256), 0, st, k);
+    return hipGetLastError();
+}
+
 hipError_t requant_act(const ActRequant& r, hipStream_t st) {
     if (r.ldc % 16 != 0 || r.acc == nullptr || r.amax == nullptr) return hipErrorInvalidValue;
     if (r.pool.pool_out != nullptr || r.pool.dx != nullptr) {

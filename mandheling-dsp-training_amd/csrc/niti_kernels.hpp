@@ -170,6 +170,12 @@ struct ActOut {
 // whether phase 2 of the forward / input-gradient conv requantises in a separate pass (and so
 // can take ActOut::pool); otherwise it recomputes the GEMM with a requantising epilogue
 bool conv_fwd_phase2_separate(const ConvGeom& g, size_t ws_bytes);
+// the first layer as a K = 32 conv over its im2col copy (1x1 geometry, OW % 32 == 0, OH even):
+// range pass + requantise / relu / 2x2 pool pass on register-fed MFMAs (niti_kernels.hip)
+bool conv0_ok(const ConvGeom& g);
+// pass 0: range into amax; pass 1: requantise with it (a MAX all-reduce may sit between them)
+hipError_t conv0_fwd(const ConvGeom& g, const int8_t* xcol, const int8_t* w, uint32_t* amax, const ActOut& o,
+                     int pass, hipStream_t st);
 bool conv_dgrad_phase2_separate(const ConvGeom& g, size_t ws_bytes);
 hipError_t conv_fwd_phase1(const ConvGeom& g, const int8_t* x, const int8_t* w, int32_t* acc, uint32_t* amax,
                            void* ws, size_t ws_bytes, hipStream_t st);

@@ -31,6 +31,64 @@ namespace niti {
 
 namespace {
 
+// im2col of the first layer: xcol[p][(ky * KW + kx) * C + c] = x[n][oy * sh + ky - pt][ox * sw + kx - pl][c]
+// (NHWC16 input, zero outside the image and for k >= C * KH * KW), one output pixel (32 bytes) per
+// thread; C / KH / KW as template arguments keep the byte positions compile-time (VGG 3/3/3,
+// LeNet 1/5/5), 0 selects the runtime fallback.
+template <int C, int KH, int KW>
+struct Im2Col32 {
+    const int8_t* x;
+    int cip, h, w, oh, ow, c, kh, kw, sh, sw, pt, pl;
+    int8_t* out;
+    __device__ void operator()(int64_t p) const {
+        typedef signed char v16c_t __attribute__((ext_vector_type(16)));
+        const int64_t img = p / ((int64_t)oh * ow);
+        const int r = (int)(p - img * oh * ow);
+        const int oy = r / ow, ox = r - (r / ow) * ow;
+        const int8_t* base = x + img * h * w * cip;
+        if constexpr (C > 0) {
+            v16c_t v[2] = {v16c_t{}, v16c_t{}};
+#pragma unroll
+            for (int ky = 0; ky < KH; ++ky)
+#pragma unroll
+                for (int kx = 0; kx < KW; ++kx) {
+                    const int iy = oy * sh + ky - pt, ix = ox * sw + kx - pl;
+                    const bool ok = iy >= 0 && iy < h && ix >= 0 && ix < w;
+                    const int8_t* src = base + ((int64_t)iy * w + ix) * cip;
+#pragma unroll
+                    for (int ch = 0; ch < C; ++ch) {
+                        const int k = (ky * KW + kx) * C + ch;
+                        v[k >> 4][k & 15] = ok ? src[ch] : (int8_t)0;
+                    }
+                }
+            *(v16c_t*)(out + p * 32) = v[0];
+            *(v16c_t*)(out + p * 32 + 16) = v[1];
+        } else {
+            int k = 0;
+            for (int ky = 0; ky < kh; ++ky)
+                for (int kx = 0; kx < kw; ++kx) {
+                    const int iy = oy * sh + ky - pt, ix = ox * sw + kx - pl;
+                    const bool ok = iy >= 0 && iy < h && ix >= 0 && ix < w;
+                    for (int ch = 0; ch < c; ++ch, ++k)
+                        out[p * 32 + k] = ok ? base[((int64_t)iy * w + ix) * cip + ch] : (int8_t)0;
+                }
+            for (; k < 32; ++k) out[p * 32 + k] = 0;
+        }
+    }
+};
+
+static hipError_t im2col32(const ConvGeom& o, const int8_t* x16, int8_t* out, hipStream_t st) {
+    const int64_t px = (int64_t)o.n * o.oh * o.ow;
+    const int cip = round_up(o.c_in, 16);
+    if (o.c_in == 3 && o.kh == 3 && o.kw == 3)
+        return launch_map(px, Im2Col32<3, 3, 3>{x16, cip, o.h, o.w, o.oh, o.ow, 3, 3, 3, o.sh, o.sw, o.pt, o.pl, out}, st);
+    if (o.c_in == 1 && o.kh == 5 && o.kw == 5)
+        return launch_map(px, Im2Col32<1, 5, 5>{x16, cip, o.h, o.w, o.oh, o.ow, 1, 5, 5, o.sh, o.sw, o.pt, o.pl, out}, st);
+    return launch_map(px, Im2Col32<0, 0, 0>{x16, cip, o.h, o.w, o.oh, o.ow, o.c_in, o.kh, o.kw, o.sh, o.sw, o.pt, o.pl,
+                                            out},
+                      st);
+}
+
 // NCHW flatten of a pooled NHWC16 map: out[n][c*HW + p] = in[n][p][c] (c < C); LeNet's
 // _Reshape(x, {0, -1, 1, 1}) after _Convert(x, NCHW) (mnistTrain.cpp:175-176).
 struct FlattenFwd {
@@ -200,8 +258,16 @@ struct Layer {
     int8_t* g8 = nullptr;    // int8 weight gradient OHWI16
     int8_t* exp = nullptr;   // exponent of this layer's output
     const int8_t* in = nullptr;  // NHWC16 input (previous output or x0)
+    // First layer with C_in * KH * KW <= 32 (VGG: 3 x 3 x 3, LeNet: 1 x 5 x 5): the conv runs as a
+    // 1x1 conv over an im2col copy of its input (xcol [pixels][32], k = (ky * KW + kx) * C_in + c,
+    // zero padded), so its GEMMs take K = 32 instead of 16 channels x 9 taps and the padded taps
+    // cost nothing.  g is that 1x1 geometry; og the layer as the network defines it (reported,
+    // weights and taps converted to / from it on the host).
+    int col = 0;
+    ConvGeom og{};
+    int8_t* xcol = nullptr;
     int64_t w_elems() const { return (int64_t)g.c_out * g.kh * g.kw * g.cip; }
-    int64_t macs() const { return (int64_t)g.n * g.oh * g.ow * g.c_out * g.c_in * g.kh * g.kw; }
+    int64_t macs() const { return (int64_t)og.n * og.oh * og.ow * og.c_out * og.c_in * og.kh * og.kw; }
 };
 
 struct Model {
@@ -437,6 +503,7 @@ static void add_conv(Model& m, int ci, int co, int k, int pad, int h, int relu, 
     l.g.pt = l.g.pl = l.g.pb = l.g.pr = pad;
     l.g.dh = l.g.dw = 1;
     l.g.finalize();
+    l.og = l.g;
     l.relu = relu;
     l.pool = pool;
     l.flatten = flatten;
@@ -490,6 +557,26 @@ int Model::build(int arch_, int batch_, int in_hw) {
         return NITI_NOT_SUPPORT;
     }
     const int n = batch;
+    {
+        Layer& f = L[0];
+        const ConvGeom o = f.og;
+        if (o.c_in * o.kh * o.kw <= 32 && o.dh == 1 && o.dw == 1) {
+            f.col = 1;
+            ConvGeom c{};
+            c.n = o.n;
+            c.c_in = 32;
+            c.h = o.oh;
+            c.w = o.ow;
+            c.c_out = o.c_out;
+            c.kh = c.kw = 1;
+            c.sh = c.sw = 1;
+            c.dh = c.dw = 1;
+            c.finalize();
+            f.g = c;
+            f.xcol = (int8_t*)ws.alloc((size_t)n * o.oh * o.ow * 32);
+            if (!f.xcol) return NITI_OUT_OF_MEMORY;
+        }
+    }
     x0 = (int8_t*)ws.alloc((size_t)n * in_h * in_w * round_up(in_c, 16));
     exp0 = (int8_t*)ws.alloc(16);
     size_t acc_elems = 0, p16d = 0;
@@ -533,7 +620,7 @@ int Model::build(int arch_, int batch_, int in_hw) {
         }
         // layer input / its C alignment with the previous output
         if (i == 0) {
-            l.in = x0;
+            l.in = l.col ? l.xcol : x0;
         } else {
             const Layer& pr = L[i - 1];
             l.in = pr.flatten ? pr.flat : (pr.pool ? pr.p : pr.r);
@@ -625,6 +712,21 @@ int Model::fwd_layer(int i, hipStream_t st) {
     Layer& l = L[i];
     const ConvGeom& g = l.g;
     probe(i, 0, true, st);
+    if (l.col && conv0_ok(g) && !l.flatten) {
+        // first layer on its im2col copy: range pass, [all-reduce MAX], requant + relu + pool pass
+        ActOut o;
+        o.out = l.r;
+        o.relu = l.relu;
+        o.exp_in = exp0;
+        o.wscale = l.ws_dev;
+        o.exp_out = l.exp;
+        o.pool.pool_out = l.pool ? l.p : nullptr;
+        MTRY(conv0_fwd(g, l.in, l.w, rng(i, 0), o, 0, st));
+        if (dp && exact) CTRY(coll->allreduce(rng(i, 0), MAX_WORDS, COLL_MAX_U32, st));
+        MTRY(conv0_fwd(g, l.in, l.w, rng(i, 0), o, 1, st));
+        probe(i, 0, false, st);
+        return NITI_NO_ERROR;
+    }
     MTRY(conv_fwd_phase1(g, l.in, l.w, acc, rng(i, 0), slab, slab_bytes, st));
     if (dp && exact) CTRY(coll->allreduce(rng(i, 0), MAX_WORDS, COLL_MAX_U32, st));
     ActOut o;
@@ -902,6 +1004,7 @@ int Model::run(const int8_t* x_nchw, int exp_in, const uint8_t* images, const in
         MTRY(image_quantize(images, n, in_c, in_h * in_w, round_up(in_c, 16), qstats,
                             dp && exact ? px * world : px, x0, exp0, true, st));
     }
+    if (L[0].col) MTRY(im2col32(L[0].og, x0, L[0].xcol, st));
     for (int i = 0; i < nl; ++i) {
         const int rc = fwd_layer(i, st);
         if (rc != NITI_NO_ERROR) return rc;
@@ -986,14 +1089,34 @@ int niti_model_num_layers(niti_model_t m) { return m ? (int)m->m.L.size() : 0; }
 int niti_model_layer_info(niti_model_t m, int layer, int info[12]) {
     if (!m || layer < 0 || layer >= (int)m->m.L.size()) return NITI_INVALID_VALUE;
     const niti::Layer& l = m->m.L[layer];
-    const int v[12] = {l.g.c_in, l.g.c_out, l.g.kh, l.g.kw, l.g.h, l.g.w, l.g.oh, l.g.ow, l.g.pt, l.g.sh, l.relu, l.pool};
+    const niti::ConvGeom& g = l.og;  // the layer as the network defines it
+    const int v[12] = {g.c_in, g.c_out, g.kh, g.kw, g.h, g.w, g.oh, g.ow, g.pt, g.sh, l.relu, l.pool};
     memcpy(info, v, sizeof(v));
     return NITI_NO_ERROR;
+}
+
+// the first layer's im2col weights [co][32] (k = (ky * KW + kx) * C_in + c) <-> OIHW
+static void col_from_oihw(const niti::ConvGeom& o, const int8_t* w, int8_t* wc) {
+    memset(wc, 0, (size_t)o.c_out * 32);
+    for (int co = 0; co < o.c_out; ++co)
+        for (int c = 0; c < o.c_in; ++c)
+            for (int t = 0; t < o.kh * o.kw; ++t) wc[co * 32 + t * o.c_in + c] = w[((size_t)co * o.c_in + c) * o.kh * o.kw + t];
+}
+static void oihw_from_col(const niti::ConvGeom& o, const int8_t* wc, int8_t* w) {
+    for (int co = 0; co < o.c_out; ++co)
+        for (int c = 0; c < o.c_in; ++c)
+            for (int t = 0; t < o.kh * o.kw; ++t) w[((size_t)co * o.c_in + c) * o.kh * o.kw + t] = wc[co * 32 + t * o.c_in + c];
 }
 
 int niti_model_set_weight(niti_model_t m, int layer, const int8_t* w_host, int wscale) {
     if (!m || layer < 0 || layer >= (int)m->m.L.size() || !w_host) return NITI_INVALID_VALUE;
     niti::Layer& l = m->m.L[layer];
+    std::vector<int8_t> colw;
+    if (l.col) {  // upload the [co][32] im2col weights as the 1x1 geometry's OIHW
+        colw.resize((size_t)l.g.c_out * 32);
+        col_from_oihw(l.og, w_host, colw.data());
+        w_host = colw.data();
+    }
     const size_t n = (size_t)l.g.c_out * l.g.c_in * l.g.kh * l.g.kw;
     int8_t* tmp = nullptr;
     if (hipMalloc(&tmp, n) != hipSuccess) return NITI_OUT_OF_MEMORY;
@@ -1015,9 +1138,11 @@ int niti_model_get_weight(niti_model_t m, int layer, int8_t* w_host) {
     int8_t* tmp = nullptr;
     if (hipDeviceSynchronize() != hipSuccess || hipMalloc(&tmp, n) != hipSuccess) return NITI_OUT_OF_MEMORY;
     int rc = NITI_NO_ERROR;
+    std::vector<int8_t> colw(l.col ? n : 0);
     if (niti::ohwi16_to_oihw(l.w, l.g.c_out, l.g.c_in, l.g.kh * l.g.kw, l.g.cip, tmp, nullptr) != hipSuccess ||
-        hipMemcpy(w_host, tmp, n, hipMemcpyDeviceToHost) != hipSuccess)
+        hipMemcpy(l.col ? colw.data() : w_host, tmp, n, hipMemcpyDeviceToHost) != hipSuccess)
         rc = NITI_NO_EXECUTION;
+    if (rc == NITI_NO_ERROR && l.col) oihw_from_col(l.og, colw.data(), w_host);
     (void)hipFree(tmp);
     return rc;
 }
@@ -1078,7 +1203,8 @@ int niti_model_get_tap(niti_model_t m, int layer, int which, int8_t* host, size_
         need = (size_t)g.c_out * g.c_in * g.kh * g.kw;
     else
         return NITI_INVALID_VALUE;
-    if (bytes < need) return NITI_INVALID_VALUE;
+    const size_t out_need = which == 1 && l.col ? (size_t)l.og.c_out * l.og.c_in * l.og.kh * l.og.kw : need;
+    if (bytes < out_need) return NITI_INVALID_VALUE;
     if (hipMalloc(&tmp, need) != hipSuccess) return NITI_OUT_OF_MEMORY;
     hipError_t e;
     if (which == 0)
@@ -1087,7 +1213,13 @@ int niti_model_get_tap(niti_model_t m, int layer, int which, int8_t* host, size_
         e = niti::nhwc16_to_nchw(l.dy, n, g.c_out, g.oh * g.ow, g.cop, tmp, nullptr);
     else
         e = niti::ohwi16_to_oihw(l.g8, g.c_out, g.c_in, g.kh * g.kw, g.cip, tmp, nullptr);
-    if (e == hipSuccess) e = hipMemcpy(host, tmp, need, hipMemcpyDeviceToHost);
+    if (which == 1 && l.col) {
+        std::vector<int8_t> colw(need);
+        if (e == hipSuccess) e = hipMemcpy(colw.data(), tmp, need, hipMemcpyDeviceToHost);
+        if (e == hipSuccess) oihw_from_col(l.og, colw.data(), host);
+    } else if (e == hipSuccess) {
+        e = hipMemcpy(host, tmp, need, hipMemcpyDeviceToHost);
+    }
     (void)hipFree(tmp);
     return e == hipSuccess ? NITI_NO_ERROR : NITI_NO_EXECUTION;
 }

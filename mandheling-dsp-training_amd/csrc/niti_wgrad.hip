@@ -82,6 +82,11 @@ constexpr int P16_WAVES = 4;           // one wave per SIMD
 #ifndef NITI_WG_D4  // ... and of the 4x4 / 2x2-image kernels
 #define NITI_WG_D4 4
 #endif
+// merge of the 4 waves' partial tiles: 1 = register-owned quarters exchanged through LDS,
+// 0 = ds_add into one LDS tile (diagnostic builds A/B them)
+#ifndef NITI_WG_MERGE
+#define NITI_WG_MERGE 1
+#endif
 #ifndef NITI_WG_NT_OUT
 #define NITI_WG_NT_OUT 1
 #endif
@@ -185,8 +190,13 @@ __global__ void __launch_bounds__(NW * 64) wgrad_p16_kernel(WgP16 g) {
     static_assert(D >= 2 && D % 2 == 0, "the next K group's window must be resident; operand buffers alternate");
     // the block's tile, row-major [co 32][tap 9][ci 32] int32 (every wave adds its partial into it),
     // plus the block-max scratch
-    constexpr int SMEM = P16_TILE * 4 + 64;
-    __shared__ __attribute__((aligned(16))) int8_t smem[SMEM];
+    // merge 0: one row-major LDS tile every wave ds_adds into; merge 1: every wave's partial
+    // tile, [wave][tap][quarter][lane] (4 x 36 KiB)
+    constexpr int SMEM = (NITI_WG_MERGE ? 4 * P16_TILE * 4 : P16_TILE * 4) + 64;
+    // typed as 16-byte vectors: the exchange stores / loads go through lds4 itself (byte-array
+    // storage accessed as v4i is an aliasing violation the optimiser is free to act on)
+    __shared__ v4i lds4[SMEM / 16];
+    int8_t* smem = (int8_t*)lds4;
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -226,7 +236,8 @@ __global__ void __launch_bounds__(NW * 64) wgrad_p16_kernel(WgP16 g) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) acc[t][i] = 0;
     int32_t* tile_lds = (int32_t*)smem;
-    for (int e = tid; e < P16_TILE / 4; e += NW * 64) ((v4i*)tile_lds)[e] = v4i{0, 0, 0, 0};
+    if (!NITI_WG_MERGE)
+        for (int e = tid; e < P16_TILE / 4; e += NW * 64) ((v4i*)tile_lds)[e] = v4i{0, 0, 0, 0};
 
     // OW 8 / 16: the rows above / below the lane's block are loaded as well (OW 8: the 8-byte row
     // of the block before / after, OW 16: the whole block).  Runs are whole images (KPI K groups
@@ -347,6 +358,49 @@ __global__ void __launch_bounds__(NW * 64) wgrad_p16_kernel(WgP16 g) {
     }
     WG_STAMP(2);
 
+    constexpr int THREADS = NW * 64;
+    const bool partial = g.splits > 1;
+    int32_t* dst = partial ? g.slab + (int64_t)split * g.slab_stride : g.C;
+    uint32_t lmax = 0;
+    uint32_t* red = (uint32_t*)(smem + SMEM - 64);
+    if constexpr (NITI_WG_MERGE) {
+        static_assert(NW == 4, "one accumulator row quarter per wave");
+        // The waves meet through 16-byte lane-linear LDS writes: every wave stores its whole
+        // partial tile as [wave][tap][quarter][lane] (quarter q = accumulator registers 4q..4q+3,
+        // rows 8q + 0..3 + 4h), then wave w sums the four waves' quarter w and stores those rows
+        // straight from registers -- no atomics, no row-major staging tile.
+#pragma unroll
+        for (int t = 0; t < 9; ++t)
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                lds4[((wid * 9 + t) * 4 + q) * 64 + lane] =
+                    v4i{acc[t][4 * q], acc[t][4 * q + 1], acc[t][4 * q + 2], acc[t][4 * q + 3]};
+        __syncthreads();  // every partial tile is in LDS (waits for the slowest wave's K loop)
+        WG_STAMP(3);
+        v4i sum[9];
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+            sum[t] = lds4[((0 * 9 + t) * 4 + wid) * 64 + lane];
+#pragma unroll
+            for (int w = 1; w < 4; ++w) sum[t] += lds4[((w * 9 + t) * 4 + wid) * 64 + lane];
+        }
+        WG_STAMP(4);
+        // rows 8w + j + 4h, column lane & 31: 128-byte runs per half-wave and register
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int row = 8 * wid + j + 4 * (lane >> 5);
+            if (co0 + row < g.c_out && NITI_WG_ABLATE != 5) {
+                int32_t* o = dst + (int64_t)(co0 + row) * g.ldc + ci0 + (lane & 31);
+#pragma unroll
+                for (int t = 0; t < 9; ++t) {
+                    const int32_t v = sum[t][j];
+                    __builtin_nontemporal_store(v, o + t * g.CIP);
+                    const uint32_t u = uabs32(v);
+                    lmax = lmax > u ? lmax : u;
+                }
+            }
+        }
+    } else {
     // the waves meet: each adds its partial tile into the zeroed LDS tile (ds_add, the two
     // half-waves on separate 128-byte rows); then every thread stores 16-byte row chunks
     __syncthreads();  // the zeroed tile (the K loop has no barrier; this one waits for the slowest wave)
@@ -364,10 +418,6 @@ __global__ void __launch_bounds__(NW * 64) wgrad_p16_kernel(WgP16 g) {
 
     // ---- output: C[co][tap][ci] (S = 1), or this split's C-shaped partial (reduced by
     // splitk_reduce_linear); chunk c = (row, tap, 4 columns)
-    constexpr int THREADS = NW * 64;
-    const bool partial = g.splits > 1;
-    int32_t* dst = partial ? g.slab + (int64_t)split * g.slab_stride : g.C;
-    uint32_t lmax = 0;
     for (int c = tid; c < P16_TILE / 4; c += THREADS) {
         const int row = c / 72, rem = c - row * 72, t = rem >> 3, c4 = rem & 7;
         const v4i v = ((const v4i*)tile_lds)[c];
@@ -389,9 +439,9 @@ __global__ void __launch_bounds__(NW * 64) wgrad_p16_kernel(WgP16 g) {
             }
         }
     }
+    }
     if (!partial && g.amax != nullptr) {
         lmax = wave_max(lmax);
-        uint32_t* red = (uint32_t*)(smem + P16_TILE * 4);
         if (lane == 0) red[wid] = lmax;
         __syncthreads();
         if (tid == 0) {
