@@ -2588,33 +2588,38 @@ __global__ void __launch_bounds__(256) conv0_kernel(Conv0 g) {
                         if (g.relu && v < 0) v = 0;
                         q[r][i] = (int8_t)v;
                     }
-                // 16 channels per lane, 4 runs of 4 consecutive channels: one dword each
+                // lane (pixel c, half h) holds channels 8j + 4h + 0..3 as dword D[j]; one half-wave
+                // swap per pair (D0, D2), (D1, D3) gives the lower half channels 0..15 and the
+                // upper half 16..31 of its pixel: one 16-byte store per lane and tile
+                auto pack = [&](const int8_t* v) {
+                    uint32_t d[4];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        d[j] = (uint32_t)(uint8_t)v[4 * j] | (uint32_t)(uint8_t)v[4 * j + 1] << 8 |
+                               (uint32_t)(uint8_t)v[4 * j + 2] << 16 | (uint32_t)(uint8_t)v[4 * j + 3] << 24;
+                    const auto x02 = __builtin_amdgcn_permlane32_swap(d[0], d[2], false, false);
+                    const auto x13 = __builtin_amdgcn_permlane32_swap(d[1], d[3], false, false);
+                    return v4i{(int)x02[0], (int)x02[1], (int)x13[0], (int)x13[1]};
+                };
 #pragma unroll
                 for (int r = 0; r < 2; ++r) {
-                    int8_t* o = g.out + (p0 + (int64_t)r * g.ow + c) * g.cop + t * 32 + 4 * h;
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        const uint32_t d = (uint32_t)(uint8_t)q[r][4 * j] | (uint32_t)(uint8_t)q[r][4 * j + 1] << 8 |
-                                           (uint32_t)(uint8_t)q[r][4 * j + 2] << 16 | (uint32_t)(uint8_t)q[r][4 * j + 3] << 24;
-                        *(uint32_t*)(o + 8 * j) = d;
-                    }
+                    const v4i v = pack(q[r]);
+                    *(v4i*)(g.out + (p0 + (int64_t)r * g.ow + c) * g.cop + t * 32 + 16 * h) = v;
                 }
                 if (g.pool_out != nullptr) {
-                    // the pixel pair (c, c ^ 1) sits in lanes c and c ^ 1: exchange, max, even lanes store
+                    // vertical max in the lane, horizontal with the neighbour pixel (lane c ^ 1);
+                    // even lanes store their pooled pixel
+                    int8_t pm[16];
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        uint32_t d = 0;
-#pragma unroll
-                        for (int e = 0; e < 4; ++e) {
-                            const int i = 4 * j + e;
-                            const int v0 = q[0][i] > q[1][i] ? q[0][i] : q[1][i];
-                            const int v1 = __shfl_xor(v0, 1, 64);
-                            d |= (uint32_t)(uint8_t)(v0 > v1 ? v0 : v1) << (8 * e);
-                        }
-                        if ((c & 1) == 0) {
-                            const int64_t pp = (img * (g.oh / 2) + pr) * (g.ow / 2) + seg * 16 + (c >> 1);
-                            *(uint32_t*)(g.pool_out + pp * g.cop + t * 32 + 4 * h + 8 * j) = d;
-                        }
+                    for (int i = 0; i < 16; ++i) {
+                        const int v0 = q[0][i] > q[1][i] ? q[0][i] : q[1][i];
+                        const int v1 = __shfl_xor(v0, 1, 64);
+                        pm[i] = (int8_t)(v0 > v1 ? v0 : v1);
+                    }
+                    const v4i v = pack(pm);
+                    if ((c & 1) == 0) {
+                        const int64_t pp = (img * (g.oh / 2) + pr) * (g.ow / 2) + seg * 16 + (c >> 1);
+                        *(v4i*)(g.pool_out + pp * g.cop + t * 32 + 16 * h) = v;
                     }
                 }
             }
