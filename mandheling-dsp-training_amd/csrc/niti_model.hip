@@ -54,11 +54,12 @@ struct Im2Col32 {
                 for (int kx = 0; kx < KW; ++kx) {
                     const int iy = oy * sh + ky - pt, ix = ox * sw + kx - pl;
                     const bool ok = iy >= 0 && iy < h && ix >= 0 && ix < w;
-                    const int8_t* src = base + ((int64_t)iy * w + ix) * cip;
+                    // the pixel's first 16 channels in one 16-byte load (zeros outside the image)
+                    const v16c_t px = ok ? *(const v16c_t*)(base + ((int64_t)iy * w + ix) * cip) : v16c_t{};
 #pragma unroll
                     for (int ch = 0; ch < C; ++ch) {
                         const int k = (ky * KW + kx) * C + ch;
-                        v[k >> 4][k & 15] = ok ? src[ch] : (int8_t)0;
+                        v[k >> 4][k & 15] = px[ch];
                     }
                 }
             *(v16c_t*)(out + p * 32) = v[0];
