@@ -90,6 +90,11 @@ constexpr int P16_WAVES = 4;           // one wave per SIMD
 #ifndef NITI_WG_NT_OUT
 #define NITI_WG_NT_OUT 1
 #endif
+// NITI_WG_SWAP = 1: the MFMAs compute the transposed tile (x taps as A, dy taps as B), so after the
+// merge a lane holds 4 consecutive ci of one co and the slab stores are 16 bytes wide
+#ifndef NITI_WG_SWAP
+#define NITI_WG_SWAP 1
+#endif
 #ifndef NITI_WG_ATOMIC_OUT
 #define NITI_WG_ATOMIC_OUT 0
 #endif
@@ -190,8 +195,8 @@ __global__ void __launch_bounds__(NW * 64) wgrad_p16_kernel(WgP16 g) {
     static_assert(D >= 2 && D % 2 == 0, "the next K group's window must be resident; operand buffers alternate");
     // the block's tile, row-major [co 32][tap 9][ci 32] int32 (every wave adds its partial into it),
     // plus the block-max scratch
-    // merge 0: one row-major LDS tile every wave ds_adds into; merge 1: every wave's partial
-    // tile, [wave][tap][quarter][lane] (4 x 36 KiB)
+    // merge 0: one row-major LDS tile every wave ds_adds into; merge 1: quarter slots
+    // [src wave][dst wave][tap][lane] (16 x 9 KiB, the 4 diagonal slots unused)
     constexpr int SMEM = (NITI_WG_MERGE ? 4 * P16_TILE * 4 : P16_TILE * 4) + 64;
     // typed as 16-byte vectors: the exchange stores / loads go through lds4 itself (byte-array
     // storage accessed as v4i is an aliasing violation the optimiser is free to act on)
@@ -329,6 +334,8 @@ __global__ void __launch_bounds__(NW * 64) wgrad_p16_kernel(WgP16 g) {
                  constexpr int KY = T / 3, KX = T % 3;
                  if constexpr (NITI_WG_ABLATE == 2)
                      acc[T][0] += A[KX][0] ^ B[KY][1];
+                 else if constexpr (NITI_WG_MERGE && NITI_WG_SWAP)  // C^T: a lane holds one co, rows = ci
+                     acc[T] = __builtin_amdgcn_mfma_i32_32x32x32_i8(B[KY], A[KX], acc[T], 0, 0, 0);
                  else
                      acc[T] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[KX], B[KY], acc[T], 0, 0, 0);
              }()),
@@ -365,24 +372,82 @@ __global__ void __launch_bounds__(NW * 64) wgrad_p16_kernel(WgP16 g) {
     uint32_t* red = (uint32_t*)(smem + SMEM - 64);
     if constexpr (NITI_WG_MERGE) {
         static_assert(NW == 4, "one accumulator row quarter per wave");
-        // The waves meet through 16-byte lane-linear LDS writes: every wave stores its whole
-        // partial tile as [wave][tap][quarter][lane] (quarter q = accumulator registers 4q..4q+3,
-        // rows 8q + 0..3 + 4h), then wave w sums the four waves' quarter w and stores those rows
-        // straight from registers -- no atomics, no row-major staging tile.
-#pragma unroll
-        for (int t = 0; t < 9; ++t)
+        if constexpr (NITI_WG_SWAP) {
+            // The tile is C^T: lane (co = lane & 31, h = lane >> 5) holds, in accumulator registers
+            // 4q..4q+3, the 16 bytes ci 8q + 4h + 0..3 of row co.  Wave w owns rows co 8w..8w+7:
+            // every wave writes its whole partial tile to LDS, slot [src wave][q][tap], and wave w's
+            // lane (r = lane >> 3, c = lane & 7) sums the four waves' 16 bytes ci 4c..4c+3 of row
+            // 8w + r -- so each store instruction covers 8 rows x 128 contiguous bytes (9 16-byte
+            // stores per wave; the tail is store-issue bound, 36 dword stores took 3x as long).
+            // The lane position inside a slot is XOR-swizzled by s = (2q + h) + 8 (q & 1): a
+            // ds_write_b128 group (8 consecutive lanes, fixed q and h) stays a permutation of one
+            // 128-byte run, and the 16 lanes of each ds_read_b128 group ({0-3,12-15,20-27}, ...)
+            // land on 16 different 16-byte bank slots (XOR by 2q + h alone leaves them 2-way).
 #pragma unroll
             for (int q = 0; q < 4; ++q)
-                lds4[((wid * 9 + t) * 4 + q) * 64 + lane] =
-                    v4i{acc[t][4 * q], acc[t][4 * q + 1], acc[t][4 * q + 2], acc[t][4 * q + 3]};
-        __syncthreads();  // every partial tile is in LDS (waits for the slowest wave's K loop)
-        WG_STAMP(3);
+#pragma unroll
+                for (int t = 0; t < 9; ++t)
+                    lds4[((wid * 4 + q) * 9 + t) * 64 + (lane ^ (2 * q + (lane >> 5) + 8 * (q & 1)))] =
+                        v4i{acc[t][4 * q], acc[t][4 * q + 1], acc[t][4 * q + 2], acc[t][4 * q + 3]};
+            __syncthreads();  // every partial tile is in LDS (waits for the slowest wave's K loop)
+            WG_STAMP(3);
+            const int r = lane >> 3, c = lane & 7, co = 8 * wid + r;
+            const int pos = (co + 32 * (c & 1)) ^ (c + 8 * ((c >> 1) & 1)), q = c >> 1;
+            v4i sum[9];
+#pragma unroll
+            for (int t = 0; t < 9; ++t) sum[t] = lds4[((0 * 4 + q) * 9 + t) * 64 + pos];
+#pragma unroll
+            for (int w = 1; w < 4; ++w)
+#pragma unroll
+                for (int t = 0; t < 9; ++t) sum[t] += lds4[((w * 4 + q) * 9 + t) * 64 + pos];
+            WG_STAMP(4);
+            if (co0 + co < g.c_out && NITI_WG_ABLATE != 5) {
+                int32_t* o = dst + (int64_t)(co0 + co) * g.ldc + ci0 + 4 * c;
+#pragma unroll
+                for (int t = 0; t < 9; ++t) {
+                    __builtin_nontemporal_store(sum[t], (v4i*)(o + t * g.CIP));
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const uint32_t u = uabs32(sum[t][j]);
+                        lmax = lmax > u ? lmax : u;
+                    }
+                }
+            }
+        } else {
+        // The waves meet through 16-byte lane-linear LDS writes: quarter q of a wave's partial tile
+        // is accumulator registers 4q..4q+3 (rows 8q + 0..3 + 4h); wave w owns quarter w, sends
+        // the other three to their owners, adds the three it receives to its own and stores those
+        // rows straight from registers -- no atomics, no row-major staging tile.
+        // slot [src wave][dst wave][tap][lane]: a wave writes only the three quarters it does
+        // not own and keeps its own quarter in registers
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            if (q != wid) {
+#pragma unroll
+                for (int t = 0; t < 9; ++t)
+                    lds4[((wid * 4 + q) * 9 + t) * 64 + lane] =
+                        v4i{acc[t][4 * q], acc[t][4 * q + 1], acc[t][4 * q + 2], acc[t][4 * q + 3]};
+            }
         v4i sum[9];
+        switch (wid) {  // the own quarter, registers 4w..4w+3 (static indices per case)
+#define NITI_OWN(W)                                                                                          \
+    case W:                                                                                                  \
+        for (int t = 0; t < 9; ++t) sum[t] = v4i{acc[t][4 * W], acc[t][4 * W + 1], acc[t][4 * W + 2], acc[t][4 * W + 3]}; \
+        break;
+            NITI_OWN(0)
+            NITI_OWN(1)
+            NITI_OWN(2)
+            default:
+                NITI_OWN(3)
+#undef NITI_OWN
+        }
+        __syncthreads();  // every quarter is in LDS (waits for the slowest wave's K loop)
+        WG_STAMP(3);
 #pragma unroll
-        for (int t = 0; t < 9; ++t) {
-            sum[t] = lds4[((0 * 9 + t) * 4 + wid) * 64 + lane];
+        for (int k = 1; k < 4; ++k) {  // the other three waves, no branches: all 27 reads in flight
+            const int w = (wid + k) & 3;
 #pragma unroll
-            for (int w = 1; w < 4; ++w) sum[t] += lds4[((w * 9 + t) * 4 + wid) * 64 + lane];
+            for (int t = 0; t < 9; ++t) sum[t] += lds4[((w * 4 + wid) * 9 + t) * 64 + lane];
         }
         WG_STAMP(4);
         // rows 8w + j + 4h, column lane & 31: 128-byte runs per half-wave and register
@@ -399,6 +464,7 @@ __global__ void __launch_bounds__(NW * 64) wgrad_p16_kernel(WgP16 g) {
                     lmax = lmax > u ? lmax : u;
                 }
             }
+        }
         }
     } else {
     // the waves meet: each adds its partial tile into the zeroed LDS tile (ds_add, the two
