@@ -98,6 +98,12 @@ constexpr int P16_WAVES = 4;           // one wave per SIMD
 #ifndef NITI_WG_ATOMIC_OUT
 #define NITI_WG_ATOMIC_OUT 0
 #endif
+// per-wave stamps (diagnostic): wave start and K-loop end after the 8 block stamps
+#define WG_WSTAMP(k)                                                                                       \
+    do {                                                                                                   \
+        if (NITI_WG_STAMPS && g.stamps != nullptr && (threadIdx.x & 63) == 0)                              \
+            g.stamps[gridDim.x * 8 + (blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 + (k)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
 #define WG_STAMP(k)                                                                            \
     do {                                                                                       \
         if (NITI_WG_STAMPS && g.stamps != nullptr && threadIdx.x == 0) {                        \
@@ -208,6 +214,7 @@ __global__ void __launch_bounds__(NW * 64) wgrad_p16_kernel(WgP16 g) {
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     span_begin(g.span);
     WG_STAMP(0);
+    WG_WSTAMP(0);
     const int logical = xcd_remap(blockIdx.x, gridDim.x);
     const int split = (int)fdiv(g.fTiles, (uint32_t)logical);
     const int tile = logical - split * g.tiles;
@@ -364,6 +371,7 @@ __global__ void __launch_bounds__(NW * 64) wgrad_p16_kernel(WgP16 g) {
         }
     }
     WG_STAMP(2);
+    WG_WSTAMP(1);
 
     constexpr int THREADS = NW * 64;
     const bool partial = g.splits > 1;

@@ -26,7 +26,7 @@ def main():
     tiles = (co // 32) * (ci // 32)
     for s in splits:
         ws, _ = ops.wgrad_p16_workspace(g, s)
-        st = torch.zeros(tiles * s * 8, dtype=torch.int64, device="cuda")
+        st = torch.zeros(tiles * s * 16, dtype=torch.int64, device="cuda")
         for _ in range(3):
             ops.conv_wgrad_p16_acc(g, xP, dP, amax, splits=s, ws=ws)
         torch.cuda.synchronize()
@@ -37,7 +37,9 @@ def main():
         e.record()
         torch.cuda.synchronize()
         L.lib().niti_diag_wgrad_stamps(None)
-        a = st.view(-1, 8).cpu().numpy().astype(np.int64)
+        allst = st.cpu().numpy().astype(np.int64)
+        a = allst[:tiles * s * 8].reshape(-1, 8)
+        wv = allst[tiles * s * 8:].reshape(-1, 4, 2)  # [block][wave][start, loop end]
         steps = -(-((kg_total + s - 1) // s) // 4)  # K groups per wave (4 waves)
         last = a[:, 5] > a[:, 0]  # blocks that wrote the output (last arrivers / all)
         clk = np.median((a[last, 5] - a[last, 0]) / np.maximum(a[last, 7] - a[last, 6], 1) * 100.0)
@@ -54,6 +56,14 @@ def main():
               f"cycles prologue {m[0]:.0f} loop {m[1]:.0f} ({m[1] / steps:.0f}/K group) slowest wave {m[2]:.0f} "
               f"LDS adds {m[3]:.0f} output {m[4]:.0f}; start spread {spread:.2f} us, first start to last end {wall:.2f} us, "
               f"clock {clk:.0f} MHz; last K loop ends at {loop_end:.2f} us", flush=True)
+        if wv[:, :, 0].min() > 0:
+            ws0 = wv[:, :, 0] - wv[:, :1, 0]
+            we = wv[:, :, 1] - wv[:, :1, 1]
+            dur = wv[:, :, 1] - wv[:, :, 0]
+            print(f"  per wave (cycles, mean over blocks): start - wave0 {ws0.mean(0).round()}, loop end - wave0 "
+                  f"{we.mean(0).round()}, duration {dur.mean(0).round()}; end spread in a block mean "
+                  f"{(wv[:, :, 1].max(1) - wv[:, :, 1].min(1)).mean():.0f} max {(wv[:, :, 1].max(1) - wv[:, :, 1].min(1)).max():.0f}; "
+                  f"slowest wave id histogram {np.bincount(wv[:, :, 1].argmax(1), minlength=4)}", flush=True)
 
 
 def C_ptr(t):
