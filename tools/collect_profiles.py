@@ -39,25 +39,38 @@ def main():
         "the timeline below is the last training step\n" + out)
     # probe dispatches in the profiled run: the probed kernel and grid, in-step vs isolated (last 20)
     plan = prof["roofline"]["plan"]
-    name = "wgrad_taps_kernel" if plan["bm"] == 32 else "gemm_kernel"
+    p16 = plan["bm"] == 16  # the P16 weight-gradient kernel (niti_wgrad.hip)
+    name = "wgrad_p16_kernel" if p16 else "wgrad_taps_kernel" if plan["bm"] == 32 else "gemm_kernel"
     rows = sorted(csv.DictReader(open(trace)), key=lambda r: int(r["Start_Timestamp"]))
     blocks = 32 * plan["splits"] if plan["bm"] == 32 else None
     sel = [r for r in rows if name in r["Kernel_Name"] and (blocks is None or int(r["Grid_Size_X"]) == blocks * 512)]
+    if p16:  # the probe's grid: the last 20 dispatches are the isolated re-runs
+        gx_p16 = int(sel[-1]["Grid_Size_X"])
+        sel = [r for r in sel if int(r["Grid_Size_X"]) == gx_p16]
     d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in sel]
     steps = prof["steps"] + prof["warmup"]
     instep, iso = d[-(20 + steps):-20], d[-20:]
+    R, Rp = bench["roofline"], prof["roofline"]
+    ops = R["ops_per_launch"]
+    iso_avg = sum(iso) / len(iso)
     with open(f"{P}/{tag}_probe_dispatches.txt", "w") as f:
-        f.write(f"probe: {sel[-1]['Kernel_Name'].split('(')[0]} grid {sel[-1]['Grid_Size_X']} work items, plan {plan}\n")
-        f.write(f"in-step launches (warmup + timed, overlapped with the input-gradient stream): n={len(instep)} "
-                f"avg {sum(instep) / len(instep):.2f} us min {min(instep):.2f} max {max(instep):.2f}\n")
-        f.write(f"isolated launches (re-run alone after the timed region): n={len(iso)} "
-                f"avg {sum(iso) / len(iso):.2f} us min {min(iso):.2f} max {max(iso):.2f}\n")
-        f.write(f"bench under rocprof (HIP events): avg_launch_us {prof['roofline']['avg_launch_us']} (in-step), "
-                f"{prof['roofline']['isolated']['avg_launch_us']} (isolated); in-kernel span "
-                f"{prof['roofline'].get('in_kernel_span_us')} / {prof['roofline']['isolated'].get('in_kernel_span_us')}\n")
+        kn = sel[-1]["Kernel_Name"].split("(")[0]
+        f.write(f"probe {kn}, grid {int(sel[-1]['Grid_Size_X']) // int(sel[-1]['Workgroup_Size_X'])} x "
+                f"{sel[-1]['Workgroup_Size_X']} threads, plan {plan}\n")
+        f.write(f"rocprofv3 --kernel-trace of `bench.py --cpu-sample 0 --probe-plan ...` (tools/gpu_full.sh, TAG={tag}):\n")
+        f.write(f"  isolated re-runs after the timed region (last 20 dispatches): avg {iso_avg:.2f} us, "
+                f"min {min(iso):.2f}, max {max(iso):.2f}\n")
+        if instep:
+            f.write(f"  in-step dispatches (warmup + timed): n={len(instep)} avg {sum(instep) / len(instep):.2f} us\n")
+        f.write(f"same run, bench.py HIP events (under the profiler): in-step avg {Rp['avg_launch_us']} us, isolated avg "
+                f"{Rp['isolated']['avg_launch_us']} us, in-kernel span {Rp.get('in_kernel_span_us')} us\n")
+        f.write(f"ops per launch {ops}; at the rocprof isolated duration: {ops / iso_avg / 1e6:.1f} TOPS = "
+                f"{ops / iso_avg / 1e6 / R['peak']:.3f} of {R['peak']:.0f} TOPS\n")
+        f.write(f"unprofiled bench line ({tag}_bench.json): in-step {R['avg_launch_us']} us = {R['frac']:.4f} of peak, "
+                f"isolated {R['isolated']['avg_launch_us']} us = {R['isolated']['frac']:.4f}\n")
     print(open(f"{P}/{tag}_probe_dispatches.txt").read())
     # PMC: probe rows + calibration
-    gx = blocks * 512 if blocks else 0
+    gx = gx_p16 if p16 else blocks * 512 if blocks else 0
     out = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "traffic.py"), f"{G}/pmcF_{tag}", f"{G}/pmcW_{tag}",
                           f"{P}/traffic.json", str(gx), "1", name, "20"], capture_output=True, text=True, check=True).stdout
     open(f"{P}/{tag}_traffic.txt", "w").write(out)
