@@ -1706,7 +1706,7 @@ static hipError_t act_phase2(int op, const LA& la, const LB& lb, int M, int N, i
                              const uint32_t* amax, const ActOut& o, size_t ws_elems, hipStream_t st) {
     const GemmPlan p = plan_gemm(M, N, kc_total, LA::BK / 16, kc_total * 16, true, ws_elems, op);
     if (p.strat == STRAT_RECOMPUTE) {
-        if (o.pool.pool_out != nullptr || o.pool.dx != nullptr) return hipErrorInvalidValue;
+        if (o.pool.pool_out != nullptr || o.pool.dx != nullptr || o.out_p16 != nullptr) return hipErrorInvalidValue;
         Epi e;
         e.amax = const_cast<uint32_t*>(amax);
         e.out = o.out;
@@ -1730,6 +1730,7 @@ static hipError_t act_phase2(int op, const LA& la, const LB& lb, int M, int N, i
     r.relu_mask = o.relu_mask;
     r.out_nhwc16 = o.out;
     r.pool = o.pool;
+    r.out_p16 = o.out_p16;
     return requant_act(r, st);
 }
 
@@ -2509,6 +2510,140 @@ __global__ void __launch_bounds__(256) requant_quad_kernel(ActRequant r, RqGeom 
     }
 }
 
+// Requantisation passes that also leave the P16 copy ([pixels/16][ldc][16], niti_wgrad.hip) of
+// their output, so the input-gradient chain hands dy to the P16 weight gradient without a layout
+// launch of its own.  A thread takes one channel quad of a run of output pixels covering whole
+// 16-pixel blocks -- RQ_PLAIN: 16 rows; RQ_POOL_BWD: G pooled pixels whose 2x2 windows are 4G
+// consecutive dx pixels (G = 4: a pooled row of an 8x8 image, one 4x4 image, four 2x2 images;
+// G = 8: a pooled row of a 16x16 image).  It computes and stores the NHWC16 output exactly as
+// requant_quad_kernel does, then transposes each 4 pixels x 4 channels in registers (v_perm) and
+// writes every block's 4 channels x 16 pixels as 64 contiguous bytes (consecutive lanes,
+// consecutive quads: a wave stores whole 4 KiB runs).
+template <int W>
+__host__ __device__ constexpr int p16_group() { return W == 16 ? 8 : 4; }
+// position, inside the run, of corner k (0: top left, 1: top right, 2, 3: bottom) of pooled pixel j
+template <int W>
+__device__ constexpr int p16_loc(int j, int k) {
+    if constexpr (W >= 8) return (k >> 1) * W + 2 * j + (k & 1);               // one pooled row
+    else if constexpr (W == 4) return (2 * (j >> 1) + (k >> 1)) * 4 + 2 * (j & 1) + (k & 1);  // one image
+    else return 4 * j + 2 * (k >> 1) + (k & 1);                                  // four 2x2 images
+}
+
+template <int MODE, int W>
+__global__ void __launch_bounds__(256) requant_p16_kernel(ActRequant r, RqGeom g) {
+    constexpr int G = MODE == RQ_PLAIN ? 16 : p16_group<W>();  // rows (pooled pixels) per thread
+    constexpr int NPX = MODE == RQ_PLAIN ? 16 : 4 * G;         // output pixels per thread
+    const int bw = bitwidth_of(read_max(r.amax));
+    const int shift = bw - 7;
+    const int s = shift > 1 ? shift : 2;
+    const bool raw = shift <= 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0 && r.exp_out != nullptr) {
+        const int inc = shift > 1 ? shift : (shift == 1 ? 2 : 0);
+        const int ein = r.exp_in ? (int)*r.exp_in : 0;
+        const int ws = r.wscale ? (int)*r.wscale : 0;
+        *r.exp_out = (int8_t)(ein + ws + inc);
+    }
+    const int ldc = r.ldc;
+    for (uint32_t u = blockIdx.x * 256u + threadIdx.x; u < g.units; u += gridDim.x * 256u) {
+        const uint32_t grp = fdiv(g.fq, u);
+        const int cq = (int)(u - grp * (uint32_t)g.qpr);
+        const int64_t d0 = (int64_t)grp * NPX;  // the run's first output pixel
+        uint32_t d[NPX];
+        if constexpr (MODE == RQ_PLAIN) {
+            v4i v[16];
+            uint32_t mk[16];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                v[i] = __builtin_nontemporal_load((const v4i*)(r.acc + (d0 + i) * ldc) + cq);
+                mk[i] = r.relu_mask != nullptr ? ((const uint32_t*)(r.relu_mask + (d0 + i) * ldc))[cq] : 0x01010101u;
+            }
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                uint32_t o = rq4(v[i], raw, s, r.relu);
+                if (r.relu_mask != nullptr) {
+                    uint32_t keep = 0;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        if ((int8_t)(mk[i] >> (8 * e)) > 0) keep |= 0xffu << (8 * e);
+                    o &= keep;
+                }
+                ((uint32_t*)(r.out_nhwc16 + (d0 + i) * ldc))[cq] = o;
+                d[i] = o;
+            }
+        } else {
+            const int64_t p0 = (int64_t)grp * G;  // the run's first pooled pixel
+            v4i v[G];
+            uint32_t yv[G], xv[G][4];
+#pragma unroll
+            for (int j = 0; j < G; ++j) {
+                v[j] = __builtin_nontemporal_load((const v4i*)(r.acc + (p0 + j) * ldc) + cq);
+                yv[j] = ((const uint32_t*)(r.pool.y + (p0 + j) * ldc))[cq];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) xv[j][k] = ((const uint32_t*)(r.pool.x + (d0 + p16_loc<W>(j, k)) * ldc))[cq];
+            }
+#pragma unroll
+            for (int j = 0; j < G; ++j) {
+                const uint32_t q = rq4(v[j], raw, s, 0);
+                if (r.out_nhwc16 != nullptr) ((uint32_t*)(r.out_nhwc16 + (p0 + j) * ldc))[cq] = q;
+                uint32_t done = 0;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    uint32_t o = 0;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const int x = (int8_t)(xv[j][k] >> (8 * e)), m = (int8_t)(yv[j] >> (8 * e));
+                        const bool take = !((done >> e) & 1u) && x >= m;
+                        if (take) done |= 1u << e;
+                        if (take && !(r.pool.relu && x <= 0)) o |= q & (0xffu << (8 * e));
+                    }
+                    ((uint32_t*)(r.pool.dx + (d0 + p16_loc<W>(j, k)) * ldc))[cq] = o;
+                    d[p16_loc<W>(j, k)] = o;
+                }
+            }
+        }
+#pragma unroll
+        for (int b = 0; b < NPX / 16; ++b) {
+            v4i c[4];  // channel e: the block's 16 pixels
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {  // 4x4 byte transpose of pixels 16b + 4t .. 4t + 3
+                const uint32_t a0 = d[16 * b + 4 * t], a1 = d[16 * b + 4 * t + 1], a2 = d[16 * b + 4 * t + 2],
+                               a3 = d[16 * b + 4 * t + 3];
+                const uint32_t t0 = __builtin_amdgcn_perm(a1, a0, 0x05010400u);  // a0.0 a1.0 a0.1 a1.1
+                const uint32_t t1 = __builtin_amdgcn_perm(a1, a0, 0x07030602u);  // a0.2 a1.2 a0.3 a1.3
+                const uint32_t t2 = __builtin_amdgcn_perm(a3, a2, 0x05010400u);
+                const uint32_t t3 = __builtin_amdgcn_perm(a3, a2, 0x07030602u);
+                c[0][t] = (int)__builtin_amdgcn_perm(t2, t0, 0x05040100u);
+                c[1][t] = (int)__builtin_amdgcn_perm(t2, t0, 0x07060302u);
+                c[2][t] = (int)__builtin_amdgcn_perm(t3, t1, 0x05040100u);
+                c[3][t] = (int)__builtin_amdgcn_perm(t3, t1, 0x07060302u);
+            }
+            int8_t* o = r.out_p16 + ((d0 / 16 + b) * ldc + 4 * cq) * 16;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) *(v4i*)(o + 16 * e) = c[e];
+        }
+    }
+}
+
+template <int MODE>
+static void launch_requant_p16(const ActRequant& r, RqGeom g, int64_t blocks, hipStream_t st) {
+    switch (MODE == RQ_PLAIN ? 0 : r.pool.W) {
+        case 0: hipLaunchKernelGGL((requant_p16_kernel<RQ_PLAIN, 0>), dim3((unsigned)blocks), dim3(256), 0, st, r, g); break;
+        case 2: hipLaunchKernelGGL((requant_p16_kernel<RQ_POOL_BWD, 2>), dim3((unsigned)blocks), dim3(256), 0, st, r, g); break;
+        case 4: hipLaunchKernelGGL((requant_p16_kernel<RQ_POOL_BWD, 4>), dim3((unsigned)blocks), dim3(256), 0, st, r, g); break;
+        case 8: hipLaunchKernelGGL((requant_p16_kernel<RQ_POOL_BWD, 8>), dim3((unsigned)blocks), dim3(256), 0, st, r, g); break;
+        default: hipLaunchKernelGGL((requant_p16_kernel<RQ_POOL_BWD, 16>), dim3((unsigned)blocks), dim3(256), 0, st, r, g); break;
+    }
+}
+
+bool requant_p16_ok(const ActRequant& r) {
+    if (r.ldc % 16 != 0 || r.out_c4 != nullptr || r.pool.pool_out != nullptr) return false;
+    if (r.pool.dx == nullptr) return r.out_nhwc16 != nullptr && r.rows % 16 == 0;
+    const int W = r.pool.W;
+    if (r.pool.H != W || !(W == 2 || W == 4 || W == 8 || W == 16)) return false;
+    const int gsz = W == 16 ? p16_group<16>() : p16_group<8>();
+    return r.rows % gsz == 0;
+}
+
 // ---- first layer on its im2col copy (K = 32) -------------------------------------------------
 // y[p][co] = sum_k xcol[p][k] * w[co][k], k < 32: one v_mfma_i32_32x32x32_i8 per 32 pixels x 32
 // output channels, both operands straight from memory (a lane's 16-byte fragment is 16
@@ -2676,6 +2811,25 @@ hipError_t requant_act(const ActRequant& r, hipStream_t st) {
         if (r.pool.dx != nullptr && (r.pool.x == nullptr || r.pool.y == nullptr ||
                                      r.rows % ((int64_t)(r.pool.H / 2) * (r.pool.W / 2))))
             return hipErrorInvalidValue;
+    }
+    if (r.out_p16 != nullptr) {  // the output (dx with the pool gradient) also as its P16 copy
+        if (!requant_p16_ok(r)) return hipErrorInvalidValue;
+        RqGeom g{};
+        g.qpr = r.ldc / 4;
+        g.W = r.pool.W;
+        const int gsz = r.pool.dx == nullptr ? 16 : (r.pool.W == 16 ? p16_group<16>() : p16_group<8>());
+        const int64_t units = r.rows / gsz * g.qpr;
+        if (units >= (int64_t)1 << 31) return hipErrorInvalidValue;
+        if (units == 0) return hipSuccess;
+        g.units = (uint32_t)units;
+        g.fq = make_fastdiv((uint32_t)g.qpr);
+        int64_t blocks = (units + 255) / 256;
+        if (blocks > 2048) blocks = 2048;
+        if (r.pool.dx == nullptr)
+            launch_requant_p16<RQ_PLAIN>(r, g, blocks, st);
+        else
+            launch_requant_p16<RQ_POOL_BWD>(r, g, blocks, st);
+        return hipGetLastError();
     }
     if (r.out_c4 == nullptr) {
         const bool pf = r.pool.pool_out != nullptr, pb = r.pool.dx != nullptr;

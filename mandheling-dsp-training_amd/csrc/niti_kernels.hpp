@@ -166,6 +166,7 @@ struct ActOut {
     const int8_t* wscale = nullptr;
     int8_t* exp_out = nullptr;
     PoolFuse pool;                     // only where the phase runs as a separate requant pass
+    int8_t* out_p16 = nullptr;         // P16 copy of the output (of pool.dx), separate pass only
 };
 // whether phase 2 of the forward / input-gradient conv requantises in a separate pass (and so
 // can take ActOut::pool); otherwise it recomputes the GEMM with a requantising epilogue
@@ -205,8 +206,14 @@ struct ActRequant {
     int8_t* out_c4 = nullptr;
     int c_real = 0, n = 0, hw = 0;
     PoolFuse pool;  // fused 2x2 max pool / pool gradient (see ActOut)
+    // optional P16 copy [pixels/16][ldc][16] of out_nhwc16 (of pool.dx with the pool gradient):
+    // the weight-gradient operand of niti_wgrad.hip, written by the same pass
+    int8_t* out_p16 = nullptr;
 };
 hipError_t requant_act(const ActRequant& r, hipStream_t st);
+// whether requant_act can write out_p16 for this pass: plain (rows % 16 == 0) or the 2x2 pool
+// gradient of a square 2 / 4 / 8 / 16 image
+bool requant_p16_ok(const ActRequant& r);
 
 // Gradient rule: bw==0 -> 0, else PSTO(bw - rule).  Optional fused NITI_SGD update
 // w <- clip(w - g, +-127) (NITI_SGD.hpp:49-52, BinaryUtils.hpp:278-299).

@@ -283,11 +283,13 @@ struct Model {
     void* slab_w = nullptr; // split-K slabs of the weight-gradient GEMMs (their own stream)
     size_t slab_w_bytes = 0;
     // P16 copies of the weight-gradient operands (niti_wgrad.hip): one input copy per layer (all
-    // converted together when the backward pass starts, off the step stream), one output-gradient
-    // copy reused layer by layer on the weight-gradient stream
-    std::vector<int8_t*> xp16;
-    int8_t* dp16 = nullptr;
+    // converted together when the backward pass starts, off the step stream) and one
+    // output-gradient copy per layer, written by the input-gradient requantisation that produces
+    // dy (requant_act's out_p16) where that pass can, else converted before the weight gradient
+    std::vector<int8_t*> xp16, dp16;
+    std::vector<char> dp16_valid;  // dp16[i] holds L[i].dy as it is now
     bool xp16_ready = false;  // run(): every P16 layer's input copy is already converted
+    bool fuse_dp16 = true;    // NITI_P16_SEPARATE=1: always the separate conversion (A/B)
     int convert_p16_inputs(hipStream_t st) {
         P16Conv jobs[P16_MAX_JOBS];
         int n = 0;
@@ -580,9 +582,12 @@ int Model::build(int arch_, int batch_, int in_hw) {
     }
     x0 = (int8_t*)ws.alloc((size_t)n * in_h * in_w * round_up(in_c, 16));
     exp0 = (int8_t*)ws.alloc(16);
-    size_t acc_elems = 0, p16d = 0;
+    size_t acc_elems = 0;
     const int nl = (int)L.size();
     xp16.assign(nl, nullptr);
+    dp16.assign(nl, nullptr);
+    dp16_valid.assign(nl, 0);
+    if (const char* e = getenv("NITI_P16_SEPARATE")) fuse_dp16 = atoi(e) == 0;
     for (int i = 0; i < nl; ++i) {
         Layer& l = L[i];
         const ConvGeom& g = l.g;
@@ -616,8 +621,8 @@ int Model::build(int arch_, int batch_, int in_hw) {
         if (conv_wgrad_p16_ok(g)) {
             slab_w_bytes = std::max(slab_w_bytes, conv_wgrad_p16_workspace(g, 8));
             xp16[i] = (int8_t*)ws.alloc((size_t)n * g.h * g.w * g.cip);
-            if (!xp16[i]) return NITI_OUT_OF_MEMORY;
-            p16d = std::max(p16d, out_px * g.cop);
+            dp16[i] = (int8_t*)ws.alloc(out_px * g.cop);
+            if (!xp16[i] || !dp16[i]) return NITI_OUT_OF_MEMORY;
         }
         // layer input / its C alignment with the previous output
         if (i == 0) {
@@ -628,10 +633,6 @@ int Model::build(int arch_, int batch_, int in_hw) {
         }
     }
     acc = (int32_t*)ws.alloc(acc_elems * 4);
-    if (p16d) {
-        dp16 = (int8_t*)ws.alloc(p16d);
-        if (!dp16) return NITI_OUT_OF_MEMORY;
-    }
     qstats = (unsigned long long*)ws.alloc(64);
     if (!qstats) return NITI_OUT_OF_MEMORY;
     if (slab_bytes) {
@@ -764,11 +765,14 @@ int Model::wgrad_layer(int i, hipStream_t st) {
         // blocks, then the register-fed kernel (+ its split-K reduce); the probe times the kernel
         // launch itself
         if (!xp16_ready) MTRY(nhwc16_to_p16(l.in, (int64_t)g.n * g.h * g.w, g.cip, xp16[i], st));
-        MTRY(nhwc16_to_p16(l.dy, (int64_t)g.n * g.oh * g.ow, g.cop, dp16, st));
+        if (!dp16_valid[i]) {
+            MTRY(nhwc16_to_p16(l.dy, (int64_t)g.n * g.oh * g.ow, g.cop, dp16[i], st));
+            dp16_valid[i] = 1;
+        }
         hipEvent_t eb, ee;
         unsigned long long* sp;
         probe_launch(i, 2, &eb, &ee, &sp);
-        MTRY(conv_wgrad_p16(g, xp16[i], dp16, l.dwacc, dp ? nullptr : rng(i, 2), slab_w, slab_w_bytes, s, st, eb, ee, sp));
+        MTRY(conv_wgrad_p16(g, xp16[i], dp16[i], l.dwacc, dp ? nullptr : rng(i, 2), slab_w, slab_w_bytes, s, st, eb, ee, sp));
         return NITI_NO_ERROR;
     }
     // the weight-gradient probe brackets the GEMM launch alone (not its split-K reduce)
@@ -806,6 +810,10 @@ int Model::dgrad_layer(int i, hipStream_t st) {
     MTRY(conv_dgrad_phase1(g, l.dy, l.wT, acc, rng(i, 1), slab, slab_bytes, st));
     if (dp && exact) CTRY(coll->allreduce(rng(i, 1), MAX_WORDS, COLL_MAX_U32, st));
     const ConvGeom& pg = pv.g;
+    // dy of layer i - 1 is rewritten here; its P16 copy comes along where the requant pass can
+    // write it (the plain and the fused pool-gradient passes), else wgrad_layer converts it
+    int8_t* p16_out = fuse_dp16 && wgrad_p16_splits(i - 1) > 0 ? dp16[i - 1] : nullptr;
+    dp16_valid[i - 1] = 0;
     ActOut o;
     if (pv.flatten) {
         o.out = pv.dflat;
@@ -826,6 +834,7 @@ int Model::dgrad_layer(int i, hipStream_t st) {
             o.pool.relu = pv.relu;
             o.pool.H = pg.oh;
             o.pool.W = pg.ow;
+            o.out_p16 = p16_out;
         } else {
             o.out = pv.dtmp;
         }
@@ -837,9 +846,11 @@ int Model::dgrad_layer(int i, hipStream_t st) {
     } else {
         o.relu_mask = pv.relu ? pv.r : nullptr;
         o.out = pv.dy;
+        if (conv_dgrad_phase2_separate(g, slab_bytes)) o.out_p16 = p16_out;
         MTRY(conv_dgrad_phase2(g, l.dy, l.wT, acc, rng(i, 1), o, slab_bytes, st));
         probe(i, 1, false, st);
     }
+    if (o.out_p16 != nullptr) dp16_valid[i - 1] = 1;
     return NITI_NO_ERROR;
 }
 
@@ -1013,6 +1024,7 @@ int Model::run(const int8_t* x_nchw, int exp_in, const uint8_t* images, const in
     {
         Layer& t = L[nl - 1];
         MTRY(loss_grad(t.r, n, t.g.c_out, t.g.cop, t.exp, labels, t.dy, st));
+        dp16_valid[nl - 1] = 0;
     }
     // weight gradients on the side stream (not inside a graph capture)
     const bool ov = overlap && !capturing;
