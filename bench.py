@@ -76,21 +76,30 @@ def cpu_baseline(arch, sample, threads_list):
 
 
 def bench_resnet18(args):
-    """BASELINE config 5's network: ResNet-18 at 224x224, 1000 classes, one GPU (the data-parallel
-    path is wired for the VGG driver only).  A step: uint8 images through the device input
-    quantiser, then the whole NITI_SGD step on the HIP ops (niti_amd.resnet)."""
+    """BASELINE config 5's network: ResNet-18 at 224x224, 1000 classes.  A step: uint8 images
+    through the device input quantiser, then the whole NITI_SGD step on the HIP ops
+    (niti_amd.resnet).  Under torchrun (WORLD_SIZE > 1) every rank steps its own batch and the
+    exact data-parallel protocol runs over RCCL (niti_amd.dp.TorchComm, backend "nccl")."""
     import numpy as np
     import torch
     from niti_amd import ops
     from niti_amd.resnet import ResNet18
     torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    comm = None
+    if world > 1:
+        import torch.distributed as dist
+        from niti_amd.dp import TorchComm
+        dist.init_process_group("nccl", device_id=torch.device("cuda", torch.cuda.current_device()))
+        comm = TorchComm()
     hw = args.in_hw or 224
     batch = args.batch or 128
-    m = ResNet18(batch, hw, 1000)
+    m = ResNet18(batch, hw, 1000, comm=comm)
     layers = [dict(c_out=l["co"], c_in=l["ci"], kh=l["k"], kw=l["k"]) for l in m.convs]
     for i, (w, s) in enumerate(synth_weights(layers, seed=17)):
         m.set_weight(i, w, s)
-    rng = np.random.default_rng(100)
+    rng = np.random.default_rng(100 + rank)
     img = torch.from_numpy(rng.integers(0, 256, (batch, 3, hw, hw)).astype(np.uint8)).cuda()
     labels = torch.from_numpy(rng.integers(0, 1000, batch).astype(np.int32)).cuda()
 
@@ -102,7 +111,7 @@ def bench_resnet18(args):
     torch.cuda.synchronize()
     run = step
     graph = None
-    if args.graph:  # the whole step (~450 launches from Python) captured once, replayed as one graph
+    if args.graph and comm is None:  # the whole step (~450 launches) captured once, replayed as one graph
         try:
             graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(graph):
@@ -113,23 +122,39 @@ def bench_resnet18(args):
         except RuntimeError as e:  # not capturable here: direct launches
             print(f"graph capture failed ({e}); direct launches", file=sys.stderr)
             graph, run = None, step
+    if comm is not None:
+        comm.dist.barrier()
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         run()
     torch.cuda.synchronize()
+    if comm is not None:
+        comm.dist.barrier()
     el = time.perf_counter() - t0
-    tops = 2 * m.step_macs() * args.steps / el / 1e12
+    if comm is not None:  # the slowest rank's time
+        t = torch.tensor([el], dtype=torch.float64, device="cuda")
+        comm.dist.all_reduce(t, op=comm.dist.ReduceOp.MAX)
+        el = float(t.item())
+    tops = 2 * m.step_macs() * world * args.steps / el / 1e12
+    if rank != 0:
+        comm.dist.destroy_process_group()
+        return
     print(json.dumps({
         "metric": "training images/sec + int8 MFMA TOPS, ResNet-18 ImageNet-224 (BASELINE config 5 network)",
-        "value": round(batch * args.steps / el, 2), "unit": "images/s", "n_gpus": 1, "steps": args.steps,
+        "value": round(batch * world * args.steps / el, 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "int8",
         "data": "synthetic (random uint8 images through the on-device input quantiser; random labels; seeded weights)",
-        "config": {"workload": f"ResNet-18 NITI int8 training step, 3x{hw}x{hw}, 1000 classes", "global_batch": batch,
-                   "per_gpu_batch": batch, "parallelism": "single GPU (host-driven op sequence, niti_amd.resnet)",
+        "config": {"workload": f"ResNet-18 NITI int8 training step, 3x{hw}x{hw}, 1000 classes",
+                   "global_batch": batch * world, "per_gpu_batch": batch,
+                   "parallelism": (f"dp{world} exact (RCCL all-reduce MAX ranges + SUM int32 grads, niti_amd.dp)"
+                                   if comm is not None else "single GPU (host-driven op sequence, niti_amd.resnet)"),
                    "launch": "hipGraph replay of the captured step" if graph is not None else "direct launches"},
         "int8_mfma_tops": round(tops, 2), "int8_mfma_frac_of_peak": round(tops / PEAK_INT8_TOPS, 4),
         "roofline": None, "cpu_baseline": None}))
+    if comm is not None:
+        comm.dist.destroy_process_group()
 
 
 def main():

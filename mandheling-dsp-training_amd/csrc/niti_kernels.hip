@@ -2513,8 +2513,7 @@ __global__ void __launch_bounds__(256) requant_quad_kernel(ActRequant r, RqGeom 
 // Requantisation passes that also leave the P16 copy ([pixels/16][ldc][16], niti_wgrad.hip) of
 // their output, so the input-gradient chain hands dy to the P16 weight gradient without a layout
 // launch of its own.  A thread takes one channel quad of a run of output pixels covering whole
-// 16-pixel blocks -- RQ_PLAIN: 16 rows; RQ_POOL_BWD: G pooled pixels whose 2x2 windows are 4G
-// consecutive dx pixels (G = 4: a pooled row of an 8x8 image, one 4x4 image, four 2x2 images;
+// 16-pixel blocks -- G pooled pixels whose 2x2 windows are 4G consecutive dx pixels (G = 4: a pooled row of an 8x8 image, one 4x4 image, four 2x2 images;
 // G = 8: a pooled row of a 16x16 image).  It computes and stores the NHWC16 output exactly as
 // requant_quad_kernel does, then transposes each 4 pixels x 4 channels in registers (v_perm) and
 // writes every block's 4 channels x 16 pixels as 64 contiguous bytes (consecutive lanes,
@@ -2531,8 +2530,9 @@ __device__ constexpr int p16_loc(int j, int k) {
 
 template <int MODE, int W>
 __global__ void __launch_bounds__(256) requant_p16_kernel(ActRequant r, RqGeom g) {
-    constexpr int G = MODE == RQ_PLAIN ? 16 : p16_group<W>();  // rows (pooled pixels) per thread
-    constexpr int NPX = MODE == RQ_PLAIN ? 16 : 4 * G;         // output pixels per thread
+    static_assert(MODE == RQ_POOL_BWD, "the plain pass is requant_p16_plain_kernel");
+    constexpr int G = p16_group<W>();  // pooled pixels per thread
+    constexpr int NPX = 4 * G;         // dx pixels per thread
     const int bw = bitwidth_of(read_max(r.amax));
     const int shift = bw - 7;
     const int s = shift > 1 ? shift : 2;
@@ -2549,28 +2549,7 @@ __global__ void __launch_bounds__(256) requant_p16_kernel(ActRequant r, RqGeom g
         const int cq = (int)(u - grp * (uint32_t)g.qpr);
         const int64_t d0 = (int64_t)grp * NPX;  // the run's first output pixel
         uint32_t d[NPX];
-        if constexpr (MODE == RQ_PLAIN) {
-            v4i v[16];
-            uint32_t mk[16];
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                v[i] = __builtin_nontemporal_load((const v4i*)(r.acc + (d0 + i) * ldc) + cq);
-                mk[i] = r.relu_mask != nullptr ? ((const uint32_t*)(r.relu_mask + (d0 + i) * ldc))[cq] : 0x01010101u;
-            }
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                uint32_t o = rq4(v[i], raw, s, r.relu);
-                if (r.relu_mask != nullptr) {
-                    uint32_t keep = 0;
-#pragma unroll
-                    for (int e = 0; e < 4; ++e)
-                        if ((int8_t)(mk[i] >> (8 * e)) > 0) keep |= 0xffu << (8 * e);
-                    o &= keep;
-                }
-                ((uint32_t*)(r.out_nhwc16 + (d0 + i) * ldc))[cq] = o;
-                d[i] = o;
-            }
-        } else {
+        {
             const int64_t p0 = (int64_t)grp * G;  // the run's first pooled pixel
             v4i v[G];
             uint32_t yv[G], xv[G][4];
@@ -2624,10 +2603,63 @@ __global__ void __launch_bounds__(256) requant_p16_kernel(ActRequant r, RqGeom g
     }
 }
 
+// The plain pass with 4 rows per thread (4x the threads of the 16-row form above, which ran
+// latency-bound at one block per CU): lanes 4 cq + sub take rows 4 sub .. 4 sub + 3 of a 16-row
+// block and channel quad cq, so the four lanes of a quad write each channel's 16 P16 bytes as
+// four adjacent dwords.
+__global__ void __launch_bounds__(256) requant_p16_plain_kernel(ActRequant r, RqGeom g) {
+    const int bw = bitwidth_of(read_max(r.amax));
+    const int shift = bw - 7;
+    const int s = shift > 1 ? shift : 2;
+    const bool raw = shift <= 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0 && r.exp_out != nullptr) {
+        const int inc = shift > 1 ? shift : (shift == 1 ? 2 : 0);
+        const int ein = r.exp_in ? (int)*r.exp_in : 0;
+        const int ws = r.wscale ? (int)*r.wscale : 0;
+        *r.exp_out = (int8_t)(ein + ws + inc);
+    }
+    const int ldc = r.ldc;
+    for (uint32_t u = blockIdx.x * 256u + threadIdx.x; u < g.units; u += gridDim.x * 256u) {
+        const int sub = (int)(u & 3u);
+        const uint32_t qu = u >> 2;
+        const uint32_t blk = fdiv(g.fq, qu);
+        const int cq = (int)(qu - blk * (uint32_t)g.qpr);
+        const int64_t row0 = (int64_t)blk * 16 + 4 * sub;
+        v4i v[4];
+        uint32_t mk[4], d[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            v[i] = __builtin_nontemporal_load((const v4i*)(r.acc + (row0 + i) * ldc) + cq);
+            mk[i] = r.relu_mask != nullptr ? ((const uint32_t*)(r.relu_mask + (row0 + i) * ldc))[cq] : 0x01010101u;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            uint32_t o = rq4(v[i], raw, s, r.relu);
+            if (r.relu_mask != nullptr) {
+                uint32_t keep = 0;
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    if ((int8_t)(mk[i] >> (8 * e)) > 0) keep |= 0xffu << (8 * e);
+                o &= keep;
+            }
+            ((uint32_t*)(r.out_nhwc16 + (row0 + i) * ldc))[cq] = o;
+            d[i] = o;
+        }
+        const uint32_t t0 = __builtin_amdgcn_perm(d[1], d[0], 0x05010400u);
+        const uint32_t t1 = __builtin_amdgcn_perm(d[1], d[0], 0x07030602u);
+        const uint32_t t2 = __builtin_amdgcn_perm(d[3], d[2], 0x05010400u);
+        const uint32_t t3 = __builtin_amdgcn_perm(d[3], d[2], 0x07030602u);
+        uint32_t* o = (uint32_t*)(r.out_p16 + ((int64_t)blk * ldc + 4 * cq) * 16) + sub;
+        o[0] = __builtin_amdgcn_perm(t2, t0, 0x05040100u);
+        o[4] = __builtin_amdgcn_perm(t2, t0, 0x07060302u);
+        o[8] = __builtin_amdgcn_perm(t3, t1, 0x05040100u);
+        o[12] = __builtin_amdgcn_perm(t3, t1, 0x07060302u);
+    }
+}
+
 template <int MODE>
 static void launch_requant_p16(const ActRequant& r, RqGeom g, int64_t blocks, hipStream_t st) {
-    switch (MODE == RQ_PLAIN ? 0 : r.pool.W) {
-        case 0: hipLaunchKernelGGL((requant_p16_kernel<RQ_PLAIN, 0>), dim3((unsigned)blocks), dim3(256), 0, st, r, g); break;
+    switch (r.pool.W) {
         case 2: hipLaunchKernelGGL((requant_p16_kernel<RQ_POOL_BWD, 2>), dim3((unsigned)blocks), dim3(256), 0, st, r, g); break;
         case 4: hipLaunchKernelGGL((requant_p16_kernel<RQ_POOL_BWD, 4>), dim3((unsigned)blocks), dim3(256), 0, st, r, g); break;
         case 8: hipLaunchKernelGGL((requant_p16_kernel<RQ_POOL_BWD, 8>), dim3((unsigned)blocks), dim3(256), 0, st, r, g); break;
@@ -2818,7 +2850,8 @@ hipError_t requant_act(const ActRequant& r, hipStream_t st) {
         g.qpr = r.ldc / 4;
         g.W = r.pool.W;
         const int gsz = r.pool.dx == nullptr ? 16 : (r.pool.W == 16 ? p16_group<16>() : p16_group<8>());
-        const int64_t units = r.rows / gsz * g.qpr;
+        // plain: a thread per (16-row block, quad, quarter); pool gradient: per (run, quad)
+        const int64_t units = r.rows / gsz * g.qpr * (r.pool.dx == nullptr ? 4 : 1);
         if (units >= (int64_t)1 << 31) return hipErrorInvalidValue;
         if (units == 0) return hipSuccess;
         g.units = (uint32_t)units;
@@ -2826,7 +2859,7 @@ hipError_t requant_act(const ActRequant& r, hipStream_t st) {
         int64_t blocks = (units + 255) / 256;
         if (blocks > 2048) blocks = 2048;
         if (r.pool.dx == nullptr)
-            launch_requant_p16<RQ_PLAIN>(r, g, blocks, st);
+            hipLaunchKernelGGL(requant_p16_plain_kernel, dim3((unsigned)blocks), dim3(256), 0, st, r, g);
         else
             launch_requant_p16<RQ_POOL_BWD>(r, g, blocks, st);
         return hipGetLastError();

@@ -7,7 +7,10 @@ the device through the C ABI (niti_amd.ops): the convs on the int8 MFMA GEMMs wi
 estimate and requantisation, the 7x7 / 2 stem, the 3x3 / 2 max pool, the 1x1 / 2 projections, the
 exponent-aligned residual adds, the global sum pool, the 1000-way head and NITI_SGD.  Activations
 stay in HBM as NHWC16 and every exponent stays a device int8 scalar: a step never synchronises the
-host.  Data parallel: not wired for this network (the VGG driver in csrc/niti_model.hip is).
+host.  Data parallel (comm = niti_amd.dp.TorchComm / ThreadComm): the exact protocol of
+SURVEY.md §8(e) -- every range estimate MAX-reduced over the ranks before its requantisation, every
+int32 weight gradient SUM-reduced before its range and NITI_SGD, the input quantiser's statistics
+SUM / MAX-reduced -- so each rank is bit-identical to one device running the global batch.
 """
 from __future__ import annotations
 
@@ -49,10 +52,12 @@ def _blocks(convs):
 
 
 class ResNet18:
-    def __init__(self, batch: int, in_hw: int = 224, classes: int = 1000, device="cuda"):
+    def __init__(self, batch: int, in_hw: int = 224, classes: int = 1000, device="cuda", comm=None):
+        """batch: images per rank; comm: data-parallel collectives (niti_amd.dp), None for one device."""
         if in_hw % 32 or in_hw < 32:
             raise ValueError("in_hw must be a multiple of 32")
         self.batch, self.in_hw, self.classes, self.dev = batch, in_hw, classes, device
+        self.comm = comm
         self.convs = resnet18_convs(in_hw, classes)
         self.blocks = _blocks(self.convs)
         n = batch
@@ -79,6 +84,10 @@ class ResNet18:
         e = self._exps[self._ei:self._ei + 1]
         self._ei += 1
         return e
+
+    def _global_range(self, amax):  # NITI_RangeEstimate over the global batch
+        if self.comm is not None:
+            self.comm.all_max(amax)
 
     @property
     def layers(self):
@@ -116,6 +125,7 @@ class ResNet18:
         l, g = self.convs[i], self.geoms[i]
         amax = self._range()
         acc = ops.conv_fwd_acc(g, x16, self.w16[i], amax)
+        self._global_range(amax)
         e_out = self._exp()
         y = ops.requant_act(acc, amax, exp_in=e_in, wscale=self.ws_dev[i], exp_out=e_out, relu=relu)
         y = y.view(self.batch, l["oh"], l["oh"], -1)
@@ -127,6 +137,7 @@ class ResNet18:
         l, g = self.convs[i], self.geoms[i]
         amax = self._range()
         acc = ops.conv_dgrad_acc(g, dy16, self.wT[i], amax)
+        self._global_range(amax)
         e_dx = self._exp()
         dx = ops.requant_act(acc, amax, exp_in=e_dy, wscale=self.ws_dev[i], exp_out=e_dx)
         return dx.view(self.batch, l["h"], l["h"], -1), e_dx
@@ -134,6 +145,10 @@ class ResNet18:
     def _wgrad_update(self, i, x16, dy16):
         amax = self._range()
         acc = ops.conv_wgrad_acc(self.geoms[i], x16, dy16, amax)
+        if self.comm is not None:  # the global batch's gradient, then its range
+            self.comm.all_sum(acc)
+            amax.zero_()
+            ops.absmax(acc, amax)
         # the transposed copy is rewritten in place (its input gradient above read it first), so a
         # captured step keeps reading the same buffer
         _, g8 = ops.sgd_update(acc, amax, self.w16[i], self.convs[i]["ci"], rule=2, wT=self.wT[i])
@@ -144,6 +159,7 @@ class ResNet18:
     def _add(self, a, ea, b, eb, relu):
         amax = self._range()
         z, ez = ops.residual_add(a, ea, b, eb, amax, ez=self._exp())
+        self._global_range(amax)
         e_out = self._exp()
         q = ops.requant_act(z.view(-1, z.shape[-1]), amax, exp_in=ez, exp_out=e_out, relu=relu)
         return q.view(a.shape), e_out
@@ -185,6 +201,7 @@ class ResNet18:
         # global sum pool, head, loss gradient
         amax = self._range()
         gsum = ops.sum_pool(u, amax)
+        self._global_range(amax)
         eg = self._exp()
         g8 = ops.requant_act(gsum, amax, exp_in=eu, exp_out=eg).view(n, 1, 1, -1)
         fc = len(self.convs) - 1
@@ -223,7 +240,13 @@ class ResNet18:
     def train_step_images(self, images: torch.Tensor, labels: torch.Tensor):
         """NITIInt8Train's input quantiser (MnistUtils.cpp:83-93) on uint8 images [n][3][hw][hw],
         straight into the stem's NHWC16 input, then the step."""
-        x, a = ops.image_quantize_nhwc16(images, ops.image_stats(images))
+        stats = ops.image_stats(images)
+        count = images.numel()
+        if self.comm is not None:  # batch statistics over every rank's images
+            self.comm.all_sum(stats[:2])
+            self.comm.all_max(stats[2:])
+            count *= self.comm.world
+        x, a = ops.image_quantize_nhwc16(images, stats, count)
         self.train_step(x, a, labels)
 
     def taps(self):

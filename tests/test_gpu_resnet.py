@@ -111,3 +111,57 @@ def test_resnet18_images_and_graph_replay(T):
         W, _ = RR.train_step(convs, W, S, x, a, labs[step], classes=classes)
         for i in range(len(convs)):
             assert np.array_equal(m.get_weight(i), W[i]), (step, convs[i]["name"])
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_resnet18_data_parallel_equals_full_batch(T, world):
+    """Exact data parallelism (niti_amd.dp): `world` ranks of 2 images each, run as
+    threads on one device through ThreadComm, equal one device stepping the whole batch bit for
+    bit -- every rank's updated weights and logits, over two steps from uint8 images (the input
+    quantiser's statistics are global too)."""
+    import threading
+    import niti_resnet_ref as RR
+    from niti_amd.dp import ThreadComm
+    from niti_amd.resnet import ResNet18
+    hw, per, classes = 32, 2, 10
+    convs = RR.resnet18_convs(hw, classes)
+    W, S = RR.init_weights(convs, seed=5 + world)
+    rng = np.random.default_rng(world)
+    full = ResNet18(per * world, hw, classes)
+    full.record = True
+    comm = ThreadComm(world)
+    ranks = [ResNet18(per, hw, classes, comm=comm.rank(r)) for r in range(world)]
+    for m in [full] + ranks:
+        for i, (w, s) in enumerate(zip(W, S)):
+            m.set_weight(i, w, s)
+        m.record = True
+    for step in range(2):
+        img = rng.integers(0, 256, (per * world, 3, hw, hw)).astype(np.uint8)
+        lab = rng.integers(0, classes, per * world).astype(np.int32)
+        full.train_step_images(T.from_numpy(img).cuda(), T.from_numpy(lab).cuda())
+        errs = []
+
+        def run(r):
+            try:
+                sl = slice(r * per, (r + 1) * per)
+                ranks[r].train_step_images(T.from_numpy(np.ascontiguousarray(img[sl])).cuda(),
+                                           T.from_numpy(np.ascontiguousarray(lab[sl])).cuda())
+            except Exception as e:  # noqa: BLE001
+                errs.append(e)
+                comm._bar.abort()
+
+        th = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        assert not errs, errs
+        T.cuda.synchronize()
+        ft = full.taps()
+        for r, m in enumerate(ranks):
+            t = m.taps()
+            assert t["exp_logits"] == ft["exp_logits"], (step, r)
+            assert np.array_equal(t["logits"], ft["logits"][r * per:(r + 1) * per]), (step, r)
+            for i, c in enumerate(convs):
+                assert np.array_equal(t["dw"][i], ft["dw"][i]), ("dw", step, r, c["name"])
+                assert np.array_equal(m.get_weight(i), full.get_weight(i)), ("w", step, r, c["name"])
