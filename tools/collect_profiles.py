@@ -45,8 +45,9 @@ def main():
     blocks = 32 * plan["splits"] if plan["bm"] == 32 else None
     sel = [r for r in rows if name in r["Kernel_Name"] and (blocks is None or int(r["Grid_Size_X"]) == blocks * 512)]
     if p16:  # the probe's grid: the last 20 dispatches are the isolated re-runs
-        gx_p16 = int(sel[-1]["Grid_Size_X"])
-        sel = [r for r in sel if int(r["Grid_Size_X"]) == gx_p16]
+        gx_p16, kn_p16 = int(sel[-1]["Grid_Size_X"]), sel[-1]["Kernel_Name"]
+        # same instantiation and grid (other P16 layers can share the grid: <2,4,4> / <4,4,4>)
+        sel = [r for r in sel if int(r["Grid_Size_X"]) == gx_p16 and r["Kernel_Name"] == kn_p16]
     d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in sel]
     steps = prof["steps"] + prof["warmup"]
     instep, iso = d[-(20 + steps):-20], d[-20:]
