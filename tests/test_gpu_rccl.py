@@ -1,0 +1,93 @@
+"""The product's RCCL data-parallel path across real GPUs (niti_model_attach_comm, one process
+per GPU, exact mode): runs only where torch sees >= 2 devices (skipped on one-GPU boxes; the
+in-process transport of tests/test_dp_local.py covers the same protocol there).  Each rank steps
+its slice of the batch through the C++ model with the RCCL communicator, overlap on and off;
+rank 0 also steps the whole batch on its own device and every rank's weights and logits must
+equal that run bit for bit."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _n_devices():
+    try:
+        import torch
+        return torch.cuda.device_count()
+    except Exception:  # noqa: BLE001
+        return 0
+
+
+def _rank(rank, world, port, overlap, q):
+    sys.path.insert(0, os.path.join(ROOT, "mandheling-dsp-training_amd"))
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(rank)
+    import niti_amd
+    import niti_model_ref as R
+    from niti_amd.model import NitiModel
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        layers = R.vgg11_layers()
+        W, S = R.init_weights(layers, seed=29)
+        b = 4
+        rng = np.random.default_rng(7)
+        imgs = rng.integers(0, 256, (2, b * world, 3, 32, 32)).astype(np.uint8)
+        labs = rng.integers(0, 10, (2, b * world)).astype(np.int32)
+        uid = [NitiModel.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        m = NitiModel(niti_amd.ARCH_VGG11, b)
+        m.attach_comm(uid[0], rank, world, exact=True)
+        m.set_overlap(overlap)
+        for i, (w, s) in enumerate(zip(W, S)):
+            m.set_weight(i, w, s)
+        for step in range(2):
+            sl = slice(rank * b, (rank + 1) * b)
+            m.train_step_images(torch.from_numpy(imgs[step, sl].copy()).cuda(), torch.from_numpy(labs[step, sl].copy()).cuda())
+        torch.cuda.synchronize()
+        out = {"w": [m.get_weight(i) for i in range(len(layers))], "logits": m.logits()}
+        if rank == 0:
+            full = NitiModel(niti_amd.ARCH_VGG11, b * world)
+            for i, (w, s) in enumerate(zip(W, S)):
+                full.set_weight(i, w, s)
+            for step in range(2):
+                full.train_step_images(torch.from_numpy(imgs[step]).cuda(), torch.from_numpy(labs[step]).cuda())
+            torch.cuda.synchronize()
+            out["full_w"] = [full.get_weight(i) for i in range(len(layers))]
+            out["full_logits"] = full.logits()
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.skipif(_n_devices() < 2, reason="needs >= 2 GPUs (one rank per GPU over RCCL)")
+@pytest.mark.parametrize("overlap", [True, False])
+def test_rccl_dp_matches_full_batch(overlap):
+    import torch.multiprocessing as mp
+    world = 2
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_rank, args=(r, world, port, overlap, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in ps)
+    for p in ps:
+        p.join(120)
+        assert p.exitcode == 0
+    full_w, (fl, fe) = res[0]["full_w"], res[0]["full_logits"]
+    b = fl.shape[0] // world
+    for r in range(world):
+        lg, e = res[r]["logits"]
+        assert e == fe and np.array_equal(lg, fl[r * b:(r + 1) * b]), r
+        for i, w in enumerate(res[r]["w"]):
+            assert np.array_equal(w, full_w[i]), (r, i)
