@@ -2204,11 +2204,13 @@ hipError_t conv_dgrad_phase2(const ConvGeom& g, const int8_t* dy, const int8_t* 
 // Range estimate and requantisation
 // =====================================================================================
 
-__global__ void absmax_kernel(const int32_t* __restrict__ a, int64_t n, uint32_t* __restrict__ amax) {
+// max|a| of one range over blocks [0, nb) of the grid (block b of them), published to amax
+__device__ __forceinline__ void absmax_body(const int32_t* __restrict__ a, int64_t n, uint32_t* __restrict__ amax,
+                                            int64_t b, int64_t nb) {
     uint32_t m = 0;
     const int64_t n4 = n / 4;
     const v4i* a4 = (const v4i*)a;
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    for (int64_t i = b * blockDim.x + threadIdx.x; i < n4; i += nb * blockDim.x) {
         const v4i v = a4[i];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -2216,7 +2218,7 @@ __global__ void absmax_kernel(const int32_t* __restrict__ a, int64_t n, uint32_t
             m = m > u ? m : u;
         }
     }
-    for (int64_t i = n4 * 4 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    for (int64_t i = n4 * 4 + b * blockDim.x + threadIdx.x; i < n; i += nb * blockDim.x) {
         const uint32_t u = uabs32(a[i]);
         m = m > u ? m : u;
     }
@@ -2229,6 +2231,38 @@ __global__ void absmax_kernel(const int32_t* __restrict__ a, int64_t n, uint32_t
         m = m > red[0] ? m : red[0];
         publish_max(amax, m);
     }
+}
+
+__global__ void absmax_kernel(const int32_t* __restrict__ a, int64_t n, uint32_t* __restrict__ amax) {
+    absmax_body(a, n, amax, blockIdx.x, gridDim.x);
+}
+
+// several ranges in one launch: job k owns workgroups [b0_k, b0_{k+1})
+__global__ void absmax_many_kernel(AbsmaxJobs J) {
+    int k = 0;
+    while (k + 1 < J.n && blockIdx.x >= J.j[k + 1].b0) ++k;
+    const AbsmaxJob jb = J.j[k];
+    const uint32_t end = k + 1 < J.n ? J.j[k + 1].b0 : gridDim.x;
+    absmax_body(jb.a, jb.n, jb.amax, blockIdx.x - jb.b0, end - jb.b0);
+}
+
+hipError_t absmax_many(const AbsmaxJob* jobs, int n, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    if (n > ABSMAX_MAX_JOBS) return hipErrorInvalidValue;
+    AbsmaxJobs J{};
+    uint32_t wg = 0;
+    for (int i = 0; i < n; ++i) {
+        if (jobs[i].n <= 0) continue;
+        int64_t blocks = (jobs[i].n / 4 + 255) / 256;
+        if (blocks > 128) blocks = 128;
+        if (blocks < 1) blocks = 1;
+        J.j[J.n] = jobs[i];
+        J.j[J.n++].b0 = wg;
+        wg += (uint32_t)blocks;
+    }
+    if (J.n == 0) return hipSuccess;
+    hipLaunchKernelGGL(absmax_many_kernel, dim3(wg), dim3(256), 0, st, J);
+    return hipGetLastError();
 }
 
 hipError_t absmax_i32(const int32_t* a, int64_t n, uint32_t* amax, hipStream_t st) {

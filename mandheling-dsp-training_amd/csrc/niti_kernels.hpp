@@ -189,6 +189,19 @@ hipError_t conv_dgrad_phase2(const ConvGeom& g, const int8_t* dy, const int8_t* 
 
 // ---- range estimate + requantisation ----------------------------------------------------
 hipError_t absmax_i32(const int32_t* a, int64_t n, uint32_t* amax, hipStream_t st);
+// max|a| of several int32 ranges in one launch (b0 is filled in by absmax_many)
+struct AbsmaxJob {
+    const int32_t* a;
+    int64_t n;
+    uint32_t* amax;
+    uint32_t b0;
+};
+constexpr int ABSMAX_MAX_JOBS = 24;
+struct AbsmaxJobs {
+    AbsmaxJob j[ABSMAX_MAX_JOBS];
+    int n;
+};
+hipError_t absmax_many(const AbsmaxJob* jobs, int n, hipStream_t st);
 
 struct ActRequant {
     const int32_t* acc = nullptr;  // [rows][ldc]

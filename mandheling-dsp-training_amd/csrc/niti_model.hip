@@ -286,6 +286,8 @@ struct Model {
     // converted together when the backward pass starts, off the step stream) and one
     // output-gradient copy per layer, written by the input-gradient requantisation that produces
     // dy (requant_act's out_p16) where that pass can, else converted before the weight gradient
+    int32_t* grad_bucket = nullptr;  // every layer's dwacc, contiguous
+    size_t grad_bucket_elems = 0;
     std::vector<int8_t*> xp16, dp16;
     std::vector<char> dp16_valid;  // dp16[i] holds L[i].dy as it is now
     bool xp16_ready = false;  // run(): every P16 layer's input copy is already converted
@@ -335,7 +337,6 @@ struct Model {
     hipStream_t side = nullptr;
     std::vector<hipEvent_t> ev_dy;
     hipEvent_t ev_side = nullptr;
-    std::vector<hipEvent_t> ev_w;  // weight gradient i done on the side stream (data parallel)
     uint32_t* amax = nullptr;  // 3 ranges per layer (forward, input gradient, weight gradient)
     size_t amax_bytes = 0;
     uint32_t* rng(int layer, int which) { return amax + (size_t)(3 * layer + which) * MAX_WORDS; }
@@ -471,16 +472,13 @@ struct Model {
         ev_dy.resize(L.size());
         for (auto& e : ev_dy)
             if (hipEventCreateWithFlags(&e, kFlags) != hipSuccess) return NITI_NO_EXECUTION;
-        ev_w.resize(L.size());
-        for (auto& e : ev_w)
-            if (hipEventCreateWithFlags(&e, kFlags) != hipSuccess) return NITI_NO_EXECUTION;
         return NITI_NO_ERROR;
     }
     // x_nchw int8 with exponent exp_in, or (x_nchw == null) uint8 images through the on-device
     // input quantiser (MnistUtils.cpp:83-93)
     int run(const int8_t* x_nchw, int exp_in, const uint8_t* images, const int32_t* labels, hipStream_t st);
     int step(const int8_t* x_nchw, int exp_in, const uint8_t* images, const int32_t* labels, hipStream_t st);
-    int reduce_wgrad(int i, hipStream_t st, bool ov);
+    int reduce_wgrads(hipStream_t st);
     ~Model() {
         clear_probe();
         drop_graph();
@@ -488,7 +486,6 @@ struct Model {
         if (gout) (void)hipEventDestroy(gout);
         if (gstream) (void)hipStreamDestroy(gstream);
         for (auto e : ev_dy) (void)hipEventDestroy(e);
-        for (auto e : ev_w) (void)hipEventDestroy(e);
         if (ev_side) (void)hipEventDestroy(ev_side);
         if (side) (void)hipStreamDestroy(side);
         coll.reset();
@@ -584,6 +581,14 @@ int Model::build(int arch_, int batch_, int in_hw) {
     exp0 = (int8_t*)ws.alloc(16);
     size_t acc_elems = 0;
     const int nl = (int)L.size();
+    // every layer's int32 weight gradient in one contiguous bucket: data parallel, one SUM
+    // all-reduce covers the whole step's gradients
+    size_t grad_elems = 0;
+    for (const Layer& l : L) grad_elems += (size_t)l.w_elems();
+    grad_bucket = (int32_t*)ws.alloc(grad_elems * 4);
+    if (!grad_bucket) return NITI_OUT_OF_MEMORY;
+    grad_bucket_elems = grad_elems;
+    size_t grad_off = 0;
     xp16.assign(nl, nullptr);
     dp16.assign(nl, nullptr);
     dp16_valid.assign(nl, 0);
@@ -606,7 +611,8 @@ int Model::build(int arch_, int batch_, int in_hw) {
             l.dflat = (int8_t*)ws.alloc((size_t)n * round_up(fc, 16));
         }
         l.dy = (int8_t*)ws.alloc(out_px * g.cop);
-        l.dwacc = (int32_t*)ws.alloc(l.w_elems() * 4);
+        l.dwacc = grad_bucket + grad_off;
+        grad_off += (size_t)l.w_elems();
         l.g8 = (int8_t*)ws.alloc(l.w_elems());
         l.exp = (int8_t*)ws.alloc(16);
         if (!l.w || !l.ws_dev || !l.wT || !l.r || !l.dy || !l.dwacc || !l.g8 || !l.exp)
@@ -755,7 +761,7 @@ int Model::fwd_layer(int i, hipStream_t st) {
 }
 
 // One layer's weight gradient (the int32 gradient and, single device, its range; data
-// parallel, the SUM and the range follow in reduce_wgrad on the step stream).
+// parallel, the SUM and the range follow in reduce_wgrads after the backward pass).
 int Model::wgrad_layer(int i, hipStream_t st) {
     const bool dp = this->dp();
     Layer& l = L[i];
@@ -787,14 +793,17 @@ int Model::wgrad_layer(int i, hipStream_t st) {
     return NITI_NO_ERROR;
 }
 
-// Data parallel: SUM layer i's int32 weight gradient over the ranks, then its range, on the step
-// stream (after the side stream's weight-gradient GEMM when the streams overlap).
-int Model::reduce_wgrad(int i, hipStream_t st, bool ov) {
-    Layer& l = L[i];
-    const int64_t we = l.w_elems();
-    if (ov) MTRY(hipStreamWaitEvent(st, ev_w[i], 0));
-    CTRY(coll->allreduce(l.dwacc, (size_t)we, COLL_SUM_I32, st));
-    MTRY(absmax_i32(l.dwacc, we, rng(i, 2), st));
+// Data parallel: SUM every layer's int32 weight gradient over the ranks in one all-reduce of the
+// contiguous bucket (one bandwidth-bound call per step instead of one latency-paying call per
+// layer; no gradient can be requantised before its range is global anyway), then every layer's
+// range in one launch, on the step stream after the backward pass.
+int Model::reduce_wgrads(hipStream_t st) {
+    CTRY(coll->allreduce(grad_bucket, grad_bucket_elems, COLL_SUM_I32, st));
+    AbsmaxJob jobs[ABSMAX_MAX_JOBS];
+    const int nl = (int)L.size();
+    if (nl > ABSMAX_MAX_JOBS) return NITI_NOT_SUPPORT;
+    for (int i = 0; i < nl; ++i) jobs[i] = AbsmaxJob{L[i].dwacc, L[i].w_elems(), rng(i, 2), 0};
+    MTRY(absmax_many(jobs, nl, st));
     return NITI_NO_ERROR;
 }
 
@@ -1046,11 +1055,7 @@ int Model::run(const int8_t* x_nchw, int exp_in, const uint8_t* images, const in
             xp16_ready = true;
         }
         int rc = wgrad_layer(i, wst);
-        if (rc == NITI_NO_ERROR && ov && dp) MTRY(hipEventRecord(ev_w[i], side));
         if (rc == NITI_NO_ERROR && i > 0) rc = dgrad_layer(i, st);
-        // data parallel: the previous layer's gradient SUM goes on the step stream behind this
-        // layer's input gradient (its GEMM ran beside two input-gradient layers by then)
-        if (rc == NITI_NO_ERROR && dp && i + 1 < nl) rc = reduce_wgrad(i + 1, st, ov);
         if (rc != NITI_NO_ERROR) return rc;
         // NITI_SGD (NITI_SGD.hpp:20-54) for this layer is deferred: every layer's update runs
         // in one launch after the backward pass (the input gradients above read the old weights)
@@ -1059,13 +1064,13 @@ int Model::run(const int8_t* x_nchw, int exp_in, const uint8_t* images, const in
         jobs[i] = SgdJob{l.dwacc, rng(i, 2), RULE_WGRAD_BW2, g.c_out, g.c_in, g.kh * g.kw, g.cip, g.cop, l.w,
                          i > 0 ? l.wT : nullptr, l.g8};
     }
-    if (dp) {
-        const int rc = reduce_wgrad(0, st, ov);
-        if (rc != NITI_NO_ERROR) return rc;
-    }
     if (ov) {  // every weight gradient is in before the update
         MTRY(hipEventRecord(ev_side, side));
         MTRY(hipStreamWaitEvent(st, ev_side, 0));
+    }
+    if (dp) {  // the global batch's gradients: one SUM over the bucket, then every layer's range
+        const int rc = reduce_wgrads(st);
+        if (rc != NITI_NO_ERROR) return rc;
     }
     xp16_ready = false;
     MTRY(sgd_update_many(jobs, nl, st));
