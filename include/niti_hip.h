@@ -213,6 +213,23 @@ int niti_conv_fwd_acc(const niti_geom* g, const int8_t* x_nhwc16, const int8_t* 
 /* acc[n*h*w][cip] int32 = input gradient of the conv for dy (NHWC16) and w^T (IHWO16) */
 int niti_conv_dgrad_acc(const niti_geom* g, const int8_t* dy_nhwc16, const int8_t* wt_ihwo16, int32_t* acc,
                         uint32_t* amax, void* workspace, size_t workspace_bytes, void* stream);
+/* Two-phase forward / input-gradient conv with the NITI requantisation (NITI_Conv_Int8.cpp:255-307,
+ * NITI_DeConv_Int8.cpp:294-329), the training step's path: phase 1 puts max|acc| into amax (zeroed
+ * by the caller) -- materialising acc, or, for small K, computing the range only; a data-parallel
+ * caller all-reduces amax (MAX) between the phases; phase 2 writes out_nhwc16 = requant(acc) (+ relu,
+ * relu_mask as niti_requant_act) and exp_out, recomputing the GEMM where phase 1 stored nothing.
+ * acc ([rows][cop] / [rows][cip] int32) and the workspace size must be the same in both calls. */
+int niti_conv_fwd_phase1(const niti_geom* g, const int8_t* x_nhwc16, const int8_t* w_ohwi16, int32_t* acc,
+                         uint32_t* amax, void* workspace, size_t workspace_bytes, void* stream);
+int niti_conv_fwd_phase2(const niti_geom* g, const int8_t* x_nhwc16, const int8_t* w_ohwi16, const int32_t* acc,
+                         const uint32_t* amax, const int8_t* exp_in, const int8_t* wscale, int8_t* exp_out, int relu,
+                         const int8_t* relu_mask, int8_t* out_nhwc16, size_t workspace_bytes, void* stream);
+int niti_conv_dgrad_phase1(const niti_geom* g, const int8_t* dy_nhwc16, const int8_t* wt_ihwo16, int32_t* acc,
+                           uint32_t* amax, void* workspace, size_t workspace_bytes, void* stream);
+int niti_conv_dgrad_phase2(const niti_geom* g, const int8_t* dy_nhwc16, const int8_t* wt_ihwo16, const int32_t* acc,
+                           const uint32_t* amax, const int8_t* exp_in, const int8_t* wscale, int8_t* exp_out,
+                           int relu, const int8_t* relu_mask, int8_t* out_nhwc16, size_t workspace_bytes,
+                           void* stream);
 /* acc[co][kh][kw][cip] int32 = weight gradient for x (NHWC16) and dy (NHWC16): a K-major GEMM
  * over the pixels whose operand tiles are transposed in LDS (ds_read_b64_tr_b8) */
 int niti_conv_wgrad_acc(const niti_geom* g, const int8_t* x_nhwc16, const int8_t* dy_nhwc16, int32_t* acc,

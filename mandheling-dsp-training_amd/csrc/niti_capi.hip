@@ -232,6 +232,54 @@ int niti_conv_dgrad_acc(const niti_geom* g, const int8_t* dy, const int8_t* wt, 
     return code(niti::conv_dgrad_acc(r, dy, wt, acc, amax, ws, ws_bytes, S(stream)));
 }
 
+static niti::ActOut act_out(const int8_t* exp_in, const int8_t* wscale, int8_t* exp_out, int relu,
+                            const int8_t* relu_mask, int8_t* out) {
+    niti::ActOut o;
+    o.out = out;
+    o.relu = relu;
+    o.relu_mask = relu_mask;
+    o.exp_in = exp_in;
+    o.wscale = wscale;
+    o.exp_out = exp_out;
+    return o;
+}
+
+int niti_conv_fwd_phase1(const niti_geom* g, const int8_t* x, const int8_t* w, int32_t* acc, uint32_t* amax,
+                         void* ws, size_t ws_bytes, void* stream) {
+    if (!g || !x || !w || !acc || !amax) return NITI_INVALID_VALUE;
+    niti::ConvGeom r;
+    if (!to_geom(g, &r)) return NITI_COMPUTE_SIZE_ERROR;
+    return code(niti::conv_fwd_phase1(r, x, w, acc, amax, ws, ws ? ws_bytes : 0, S(stream)));
+}
+
+int niti_conv_fwd_phase2(const niti_geom* g, const int8_t* x, const int8_t* w, const int32_t* acc,
+                         const uint32_t* amax, const int8_t* exp_in, const int8_t* wscale, int8_t* exp_out, int relu,
+                         const int8_t* relu_mask, int8_t* out, size_t ws_bytes, void* stream) {
+    if (!g || !x || !w || !acc || !amax || !out) return NITI_INVALID_VALUE;
+    niti::ConvGeom r;
+    if (!to_geom(g, &r)) return NITI_COMPUTE_SIZE_ERROR;
+    return code(niti::conv_fwd_phase2(r, x, w, acc, amax, act_out(exp_in, wscale, exp_out, relu, relu_mask, out),
+                                      ws_bytes, S(stream)));
+}
+
+int niti_conv_dgrad_phase1(const niti_geom* g, const int8_t* dy, const int8_t* wt, int32_t* acc, uint32_t* amax,
+                           void* ws, size_t ws_bytes, void* stream) {
+    if (!g || !dy || !wt || !acc || !amax) return NITI_INVALID_VALUE;
+    niti::ConvGeom r;
+    if (!to_geom(g, &r)) return NITI_COMPUTE_SIZE_ERROR;
+    return code(niti::conv_dgrad_phase1(r, dy, wt, acc, amax, ws, ws ? ws_bytes : 0, S(stream)));
+}
+
+int niti_conv_dgrad_phase2(const niti_geom* g, const int8_t* dy, const int8_t* wt, const int32_t* acc,
+                           const uint32_t* amax, const int8_t* exp_in, const int8_t* wscale, int8_t* exp_out, int relu,
+                           const int8_t* relu_mask, int8_t* out, size_t ws_bytes, void* stream) {
+    if (!g || !dy || !wt || !acc || !amax || !out) return NITI_INVALID_VALUE;
+    niti::ConvGeom r;
+    if (!to_geom(g, &r)) return NITI_COMPUTE_SIZE_ERROR;
+    return code(niti::conv_dgrad_phase2(r, dy, wt, acc, amax, act_out(exp_in, wscale, exp_out, relu, relu_mask, out),
+                                        ws_bytes, S(stream)));
+}
+
 int niti_conv_wgrad_acc(const niti_geom* g, const int8_t* x, const int8_t* dy, int32_t* acc, uint32_t* amax,
                         void* ws, size_t ws_bytes, void* stream) {
     if (!g) return NITI_INVALID_VALUE;

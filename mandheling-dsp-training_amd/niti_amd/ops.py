@@ -177,6 +177,35 @@ def conv_dgrad_acc(g: L.Geom, dy16, wt16, amax, stream=None):
     return acc
 
 
+def _conv_requant(op, g: L.Geom, a, b, amax, exp_in, wscale, exp_out, relu, relu_mask, between, stream):
+    rows, ld = (g.n * g.oh * g.ow, g.cop) if op == 0 else (g.n * g.h * g.w, g.cip)
+    acc = torch.empty((rows, ld), dtype=torch.int32, device=a.device)
+    out = torch.empty((rows, ld), dtype=torch.int8, device=a.device)
+    ws, nb = conv_workspace(g, op, a.device)
+    lib = L.lib()
+    p1, p2 = (lib.niti_conv_fwd_phase1, lib.niti_conv_fwd_phase2) if op == 0 else \
+        (lib.niti_conv_dgrad_phase1, lib.niti_conv_dgrad_phase2)
+    check(p1(C.byref(g), _ptr(a), _ptr(b), _ptr(acc), _ptr(amax), _ptr(ws), nb, _stream(stream)), "conv phase 1")
+    if between is not None:  # e.g. the data-parallel MAX all-reduce of the range
+        between(amax)
+    check(p2(C.byref(g), _ptr(a), _ptr(b), _ptr(acc), _ptr(amax), _ptr(exp_in), _ptr(wscale), _ptr(exp_out),
+             1 if relu else 0, _ptr(relu_mask), _ptr(out), nb, _stream(stream)), "conv phase 2")
+    return out
+
+
+def conv_fwd_requant(g: L.Geom, x16, w16, amax, exp_in=None, wscale=None, exp_out=None, relu=False,
+                     relu_mask=None, between=None, stream=None):
+    """The forward conv with its NITI requantisation in two phases (range, [between(amax)],
+    requantise; small-K GEMMs recompute instead of storing int32): int8 [n*oh*ow][cop]."""
+    return _conv_requant(0, g, x16, w16, amax, exp_in, wscale, exp_out, relu, relu_mask, between, stream)
+
+
+def conv_dgrad_requant(g: L.Geom, dy16, wt16, amax, exp_in=None, wscale=None, exp_out=None, relu=False,
+                       relu_mask=None, between=None, stream=None):
+    """The input gradient with its requantisation in two phases: int8 [n*h*w][cip]."""
+    return _conv_requant(1, g, dy16, wt16, amax, exp_in, wscale, exp_out, relu, relu_mask, between, stream)
+
+
 def conv_plan(g: L.Geom, op: int, ws_bytes: int | None = None):
     """(bm, bn, splits, strategy) the conv GEMM `op` (0 fwd, 1 dgrad, 2 wgrad) runs with."""
     if ws_bytes is None:

@@ -121,6 +121,10 @@ class ResNet18:
     def _nchw(self, t16, c):  # [n, h, w, cp] NHWC16 -> NCHW int8 (host, records only)
         return t16.cpu().numpy()[..., :c].transpose(0, 3, 1, 2).copy()
 
+    # The convs store int32 and requantise in a separate pass (ops.conv_*_acc + requant_act): with
+    # the planner's default plans (no autotuning on this path) the two-phase form, which recomputes
+    # small-K GEMMs instead of storing them (ops.conv_fwd_requant), ran the step 9 % slower on
+    # MI355X (5.40 vs 4.94 ms at batch 128, 224x224).
     def _fwd(self, i, x16, e_in, relu):
         l, g = self.convs[i], self.geoms[i]
         amax = self._range()

@@ -14,7 +14,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "mandheling-dsp-training_amd"))
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, out):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from niti_amd.dp import TorchComm
@@ -28,24 +28,24 @@ def _worker(rank, world, port, q):
     c.all_sum(g)
     c.all_sum(s[:2])
     c.all_max(s[2:])
-    q.put((rank, r0, g0, r, g, s))
+    torch.save((rank, r0, g0, r, g, s), out)
     dist.destroy_process_group()
 
 
-def test_torch_comm_gloo_world2():
+def test_torch_comm_gloo_world2(tmp_path):
     import socket
     with socket.socket() as so:
         so.bind(("127.0.0.1", 0))
         port = so.getsockname()[1]
     ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    ps = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    paths = [str(tmp_path / f"rank{r}.pt") for r in range(2)]
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, paths[r])) for r in range(2)]
     for p in ps:
         p.start()
-    out = sorted([q.get(timeout=120) for _ in ps], key=lambda t: t[0])
     for p in ps:
-        p.join(60)
+        p.join(120)
         assert p.exitcode == 0
+    out = [torch.load(f, weights_only=True) for f in paths]
     (_, ra, ga, r1, g1, s1), (_, rb, gb, r2, g2, s2) = out
     assert torch.equal(r1, torch.maximum(ra, rb)) and torch.equal(r2, r1)
     assert torch.equal(g1, ga + gb) and torch.equal(g2, g1)

@@ -812,3 +812,37 @@ def test_vgg11_batch256_layers_sampled(T, ops, oracle):
         a1 = ops.conv_wgrad_acc(g1, ops.nchw_to_nhwc16(dev(T, x[:128])), ops.nchw_to_nhwc16(dev(T, dy[:128])))
         a2 = ops.conv_wgrad_acc(g1, ops.nchw_to_nhwc16(dev(T, x[128:])), ops.nchw_to_nhwc16(dev(T, dy[128:])))
         assert np.array_equal((a1 + a2).cpu().numpy(), accw)
+
+
+@pytest.mark.parametrize("h,ci,co,stride,relu", [(8, 64, 128, 1, True), (16, 32, 64, 1, False), (9, 48, 32, 2, True)])
+def test_conv_two_phase_requant_equals_store_path(T, h, ci, co, stride, relu):
+    """niti_conv_{fwd,dgrad}_phase1/2 (range, caller hook, requantise; small K recomputes the
+    GEMM) give the same int8 output and exponent as the int32 accumulate + niti_requant_act path."""
+    from niti_amd import ops
+    rng = np.random.default_rng(h * ci + co)
+    n = 3
+    g = ops.geom(n, ci, h, h, co, 3, stride=stride, pad=1)
+    x16 = ops.nchw_to_nhwc16(T.from_numpy(rng.integers(-127, 128, (n, ci, h, h)).astype(np.int8)).cuda())
+    w = rng.integers(-127, 128, (co, ci, 3, 3)).astype(np.int8)
+    w16 = ops.oihw_to_ohwi16(T.from_numpy(w).cuda())
+    wT = ops.ohwi16_to_ihwo16(w16, ci)
+    dy16 = ops.nchw_to_nhwc16(T.from_numpy(rng.integers(-127, 128, (n, co, g.oh, g.ow)).astype(np.int8)).cuda())
+    e_in = T.tensor([-3], dtype=T.int8, device="cuda")
+    ws8 = T.tensor([-6], dtype=T.int8, device="cuda")
+    for op in (0, 1):
+        a1, a2 = ops.new_range(), ops.new_range()
+        e1, e2 = T.zeros(1, dtype=T.int8, device="cuda"), T.zeros(1, dtype=T.int8, device="cuda")
+        seen = []
+        if op == 0:
+            acc = ops.conv_fwd_acc(g, x16, w16, a1)
+            want = ops.requant_act(acc, a1, exp_in=e_in, wscale=ws8, exp_out=e1, relu=relu)
+            got = ops.conv_fwd_requant(g, x16, w16, a2, exp_in=e_in, wscale=ws8, exp_out=e2, relu=relu,
+                                       between=lambda a: seen.append(ops.range_max(a)))
+        else:
+            acc = ops.conv_dgrad_acc(g, dy16, wT, a1)
+            want = ops.requant_act(acc, a1, exp_in=e_in, wscale=ws8, exp_out=e1)
+            got = ops.conv_dgrad_requant(g, dy16, wT, a2, exp_in=e_in, wscale=ws8, exp_out=e2,
+                                         between=lambda a: seen.append(ops.range_max(a)))
+        T.cuda.synchronize()
+        assert seen == [ops.range_max(a1)], op
+        assert T.equal(got, want) and e1.item() == e2.item(), op
