@@ -283,6 +283,11 @@ int niti_ohwi16_to_oihw(const int8_t* w, int co, int ci, int kk, int cip, int8_t
  * *ez = e_hi - d; max|z| into amax.  n % 16 == 0; requantise z with niti_requant_act. */
 int niti_residual_add(const int8_t* a, const int8_t* ea, const int8_t* b, const int8_t* eb, int64_t n, int32_t* z,
                       int8_t* ez, uint32_t* amax, void* stream);
+/* the fused form: with z = NULL above (range only; a data-parallel caller MAX-reduces amax next),
+ * out[n] int8 = the forward rule on z recomputed from a and b (+ relu), exactly as niti_requant_act
+ * on the stored z; *ez = e_hi - d and *exp_out = *ez + inc (either may be NULL). */
+int niti_residual_requant(const int8_t* a, const int8_t* ea, const int8_t* b, const int8_t* eb, int64_t n,
+                          const uint32_t* amax, int8_t* ez, int8_t* exp_out, int relu, int8_t* out, void* stream);
 /* global sum pool: acc[img][c] = sum over hw pixels of x NHWC16 [n][hw][cp] (+ max into amax) */
 int niti_sum_pool(const int8_t* x, int n, int hw, int cp, int32_t* acc, uint32_t* amax, void* stream);
 /* its gradient: dx[img][p][c] = dy[img][c] */

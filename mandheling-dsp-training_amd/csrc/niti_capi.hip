@@ -379,6 +379,10 @@ int niti_residual_add(const int8_t* a, const int8_t* ea, const int8_t* b, const 
                       int8_t* ez, uint32_t* amax, void* stream) {
     return code(niti::residual_add(a, ea, b, eb, n, z, ez, amax, S(stream)));
 }
+int niti_residual_requant(const int8_t* a, const int8_t* ea, const int8_t* b, const int8_t* eb, int64_t n,
+                          const uint32_t* amax, int8_t* ez, int8_t* exp_out, int relu, int8_t* out, void* stream) {
+    return code(niti::residual_requant(a, ea, b, eb, n, amax, ez, exp_out, relu, out, S(stream)));
+}
 int niti_sum_pool(const int8_t* x, int n, int hw, int cp, int32_t* acc, uint32_t* amax, void* stream) {
     return code(niti::sum_pool(x, n, hw, cp, acc, amax, S(stream)));
 }

@@ -70,6 +70,11 @@ __device__ __forceinline__ uint32_t read_max(const uint32_t* amax) {
     return wave_max(amax[(threadIdx.x & 63) * MAX_SLOT_STRIDE]);
 }
 
+// The residual rule (niti_resnet.hip): z = hi * 2^d + (lo >> r), arithmetic shift
+__device__ __forceinline__ int32_t residual_z(int32_t hi, int32_t lo, int d, int r) {
+    return hi * (1 << d) + (r >= 31 ? (lo < 0 ? -1 : 0) : lo >> r);
+}
+
 // kernel-span probe: first block start / last block end on the device wall clock
 __device__ __forceinline__ void span_begin(unsigned long long* span) {
     if (span != nullptr && threadIdx.x == 0) atomicMin(span, (unsigned long long)__builtin_amdgcn_s_memrealtime());

@@ -2710,6 +2710,53 @@ bool requant_p16_ok(const ActRequant& r) {
     return r.rows % gsz == 0;
 }
 
+// Residual add fused with its requantisation (the rule of niti_resnet.hip): the range comes from a
+// residual_add pass that stores no z (and, data parallel, a MAX all-reduce); this pass recomputes z
+// from the int8 operands and applies the forward rule exactly as requant_act (RQ_PLAIN) on z:
+// out = relu?(PSTO(z, shift) | (int8) z), *ez = e_hi - d, *exp_out = *ez + inc.
+__global__ void __launch_bounds__(256) residual_requant_kernel(const int8_t* __restrict__ a, const int8_t* __restrict__ ea,
+                                                               const int8_t* __restrict__ b, const int8_t* __restrict__ eb,
+                                                               int64_t n16, const uint32_t* __restrict__ amax,
+                                                               int8_t* __restrict__ ez, int8_t* __restrict__ exp_out,
+                                                               int relu, int8_t* __restrict__ out) {
+    const int xa = *ea, xb = *eb;
+    const bool a_hi = xa >= xb;
+    const int diff = a_hi ? xa - xb : xb - xa;
+    const int d = diff < 23 ? diff : 23, r = diff - d;
+    const int bw = bitwidth_of(read_max(amax));  // whole wave active
+    const int shift = bw - 7;
+    const int s = shift > 1 ? shift : 2;
+    const bool raw = shift <= 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        const int e_z = (a_hi ? xa : xb) - d;
+        if (ez != nullptr) *ez = (int8_t)e_z;
+        if (exp_out != nullptr) *exp_out = (int8_t)(e_z + (shift > 1 ? shift : (shift == 1 ? 2 : 0)));
+    }
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += (int64_t)gridDim.x * 256) {
+        const v16c va = ((const v16c*)a)[i], vb = ((const v16c*)b)[i];
+        v16c q;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const int32_t z = residual_z(a_hi ? va[e] : vb[e], a_hi ? vb[e] : va[e], d, r);
+            int32_t o = raw ? (int32_t)(int8_t)z : psto_fast(z, s);
+            if (relu && o < 0) o = 0;
+            q[e] = (signed char)o;
+        }
+        ((v16c*)out)[i] = q;
+    }
+}
+
+hipError_t residual_requant(const int8_t* a, const int8_t* ea, const int8_t* b, const int8_t* eb, int64_t n,
+                            const uint32_t* amax, int8_t* ez, int8_t* exp_out, int relu, int8_t* out, hipStream_t st) {
+    if (n < 0 || n % 16 != 0 || !a || !b || !ea || !eb || !amax || !out) return hipErrorInvalidValue;
+    const int64_t n16 = n / 16;
+    int64_t blocks = (n16 + 255) / 256;
+    blocks = blocks < 1 ? 1 : blocks > 2048 ? 2048 : blocks;
+    hipLaunchKernelGGL(residual_requant_kernel, dim3((unsigned)blocks), dim3(256), 0, st, a, ea, b, eb, n16, amax, ez,
+                       exp_out, relu, out);
+    return hipGetLastError();
+}
+
 // ---- first layer on its im2col copy (K = 32) -------------------------------------------------
 // y[p][co] = sum_k xcol[p][k] * w[co][k], k < 32: one v_mfma_i32_32x32x32_i8 per 32 pixels x 32
 // output channels, both operands straight from memory (a lane's 16-byte fragment is 16

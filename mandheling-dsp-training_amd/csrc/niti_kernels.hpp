@@ -110,6 +110,10 @@ hipError_t splitk_reduce_linear(const int32_t* slab, int splits, int64_t n, int6
 // z = aligned a + b (int32, n % 16 == 0 elements), its exponent into ez, max|z| into amax
 hipError_t residual_add(const int8_t* a, const int8_t* ea, const int8_t* b, const int8_t* eb, int64_t n,
                         int32_t* z, int8_t* ez, uint32_t* amax, hipStream_t st);
+// the fused form: z recomputed from a, b and requantised with the range in amax (from residual_add
+// with z = null); out int8 (n elements), *ez and *exp_out = *ez + inc (either may be null)
+hipError_t residual_requant(const int8_t* a, const int8_t* ea, const int8_t* b, const int8_t* eb, int64_t n,
+                            const uint32_t* amax, int8_t* ez, int8_t* exp_out, int relu, int8_t* out, hipStream_t st);
 // acc[n][cp] = sum over hw pixels of x NHWC16 (+ max into amax); its gradient: dy broadcast
 hipError_t sum_pool(const int8_t* x, int n, int hw, int cp, int32_t* acc, uint32_t* amax, hipStream_t st);
 hipError_t sum_pool_grad(const int8_t* dy, int n, int hw, int cp, int8_t* dx, hipStream_t st);

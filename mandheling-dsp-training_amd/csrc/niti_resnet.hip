@@ -11,13 +11,13 @@
 // estimate and PSTO requantisation (requant_act: shift = bitwidth(max|z|) - 7, exponent
 // e_z + inc), relu included for a block output.  The global pool is the sum over the pixels
 // (int32, the exponent unchanged) followed by the same requantisation; its gradient hands dy to
-// every pixel of the image.  oracle/niti_resnet_ref.py restates all three.
+// every pixel of the image.  oracle/niti_resnet_ref.py restates all three.  The fused form
+// (residual_requant in niti_kernels.hip) takes the range in a pass without z and recomputes z
+// from the int8 operands while requantising: 2 x 2 int8 reads instead of an int32 write + read.
 #include "niti_device.hpp"
 #include "niti_kernels.hpp"
 
 namespace niti {
-
-__device__ __forceinline__ int32_t shr_floor(int32_t v, int r) { return r >= 31 ? (v < 0 ? -1 : 0) : v >> r; }
 
 __global__ void __launch_bounds__(256) residual_add_kernel(const int8_t* __restrict__ a, const int8_t* __restrict__ ea,
                                                            const int8_t* __restrict__ b, const int8_t* __restrict__ eb,
@@ -35,13 +35,14 @@ __global__ void __launch_bounds__(256) residual_add_kernel(const int8_t* __restr
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
             const int32_t hi = a_hi ? va[e] : vb[e], lo = a_hi ? vb[e] : va[e];
-            const int32_t s = hi * (1 << d) + shr_floor(lo, r);
+            const int32_t s = residual_z(hi, lo, d, r);
             out[e >> 2][e & 3] = s;
             const uint32_t u = uabs32(s);
             m = m > u ? m : u;
         }
+        if (z != nullptr)  // else the range pass of the fused form (residual_requant)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) ((v4i*)z)[4 * i + q] = out[q];
+            for (int q = 0; q < 4; ++q) ((v4i*)z)[4 * i + q] = out[q];
     }
     if (amax != nullptr) {
         m = wave_max(m);
@@ -54,7 +55,7 @@ __global__ void __launch_bounds__(256) residual_add_kernel(const int8_t* __restr
 
 hipError_t residual_add(const int8_t* a, const int8_t* ea, const int8_t* b, const int8_t* eb, int64_t n,
                         int32_t* z, int8_t* ez, uint32_t* amax, hipStream_t st) {
-    if (n < 0 || n % 16 != 0 || !a || !b || !ea || !eb || !z) return hipErrorInvalidValue;
+    if (n < 0 || n % 16 != 0 || !a || !b || !ea || !eb || (!z && !amax)) return hipErrorInvalidValue;
     const int64_t n16 = n / 16;
     int64_t blocks = (n16 + 255) / 256;
     blocks = blocks < 1 ? 1 : blocks > 2048 ? 2048 : blocks;

@@ -134,6 +134,7 @@ def lib():
         "niti_oihw_to_ohwi16": (ci, [vp, ci, ci, ci, ci, vp, vp]),
         "niti_ohwi16_to_oihw": (ci, [vp, ci, ci, ci, ci, vp, vp]),
         "niti_residual_add": (ci, [vp, vp, vp, vp, i64, vp, vp, vp, vp]),
+        "niti_residual_requant": (ci, [vp, vp, vp, vp, i64, vp, vp, vp, ci, vp, vp]),
         "niti_sum_pool": (ci, [vp, ci, ci, ci, vp, vp, vp]),
         "niti_sum_pool_grad": (ci, [vp, ci, ci, ci, vp, vp]),
         "niti_maxpool": (ci, [vp] + [ci] * 7 + [vp, ci, ci, vp]),

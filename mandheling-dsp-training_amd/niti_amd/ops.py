@@ -328,6 +328,28 @@ def residual_add(a, ea, b, eb, amax, stream=None, ez=None):
     return z, ez
 
 
+def residual_range(a, ea, b, eb, amax, stream=None):
+    """max|z| of the residual add into amax, z not stored (the fused form's first pass)."""
+    assert a.shape == b.shape and a.dtype == b.dtype == torch.int8
+    check(L.lib().niti_residual_add(_ptr(a), _ptr(ea), _ptr(b), _ptr(eb), a.numel(), None, None, _ptr(amax),
+                                    _stream(stream)), "residual_range")
+
+
+def residual_requant(a, ea, b, eb, amax, ez=None, exp_out=None, relu=False, stream=None):
+    """int8 requant(aligned a + b) with the range in amax; the residual and output exponents into ez /
+    exp_out (device int8 [1], created when None) -> (out, ez, exp_out)."""
+    assert a.shape == b.shape and a.dtype == b.dtype == torch.int8
+    out = torch.empty(a.shape, dtype=torch.int8, device=a.device)
+    if ez is None:
+        ez = torch.zeros(1, dtype=torch.int8, device=a.device)
+    if exp_out is None:
+        exp_out = torch.zeros(1, dtype=torch.int8, device=a.device)
+    check(L.lib().niti_residual_requant(_ptr(a), _ptr(ea), _ptr(b), _ptr(eb), a.numel(), _ptr(amax), _ptr(ez),
+                                        _ptr(exp_out), 1 if relu else 0, _ptr(out), _stream(stream)),
+          "residual_requant")
+    return out, ez, exp_out
+
+
 def sum_pool(x16, amax, stream=None):
     """Global sum pool of x NHWC16 [n][h][w][cp] -> acc int32 [n][cp]."""
     n, h, w, cp = x16.shape

@@ -161,12 +161,14 @@ class ResNet18:
             self.rec.setdefault("dw", {})[i] = g8
 
     def _add(self, a, ea, b, eb, relu):
+        # fused residual requantisation: a range pass without the int32 z, then z recomputed from
+        # the int8 operands while requantising (2 x 2 int8 reads instead of an int32 write + read)
         amax = self._range()
-        z, ez = ops.residual_add(a, ea, b, eb, amax, ez=self._exp())
+        ops.residual_range(a, ea, b, eb, amax)
         self._global_range(amax)
-        e_out = self._exp()
-        q = ops.requant_act(z.view(-1, z.shape[-1]), amax, exp_in=ez, exp_out=e_out, relu=relu)
-        return q.view(a.shape), e_out
+        ez, e_out = self._exp(), self._exp()
+        q, _, _ = ops.residual_requant(a, ea, b, eb, amax, ez=ez, exp_out=e_out, relu=relu)
+        return q, e_out
 
     # ---------------------------------------------------------------- step
     def train_step(self, x: torch.Tensor, exp_in: int, labels: torch.Tensor):

@@ -165,3 +165,27 @@ def test_resnet18_data_parallel_equals_full_batch(T, world):
             for i, c in enumerate(convs):
                 assert np.array_equal(t["dw"][i], ft["dw"][i]), ("dw", step, r, c["name"])
                 assert np.array_equal(m.get_weight(i), full.get_weight(i)), ("w", step, r, c["name"])
+
+
+def test_residual_requant_fused_equals_two_pass(T):
+    """The fused residual requantisation (range pass without z, then z recomputed while
+    requantising) equals niti_residual_add + niti_requant_act on the stored z: every exponent gap
+    0..30, relu on and off."""
+    from niti_amd import ops
+    rng = np.random.default_rng(11)
+    n = 4096
+    for gap in list(range(0, 31, 3)) + [23, 24]:
+        for relu in (False, True):
+            a = T.from_numpy(rng.integers(-127, 128, n).astype(np.int8)).cuda()
+            b = T.from_numpy(rng.integers(-127, 128, n).astype(np.int8)).cuda()
+            ea = T.tensor([-5], dtype=T.int8, device="cuda")
+            eb = T.tensor([-5 - gap if gap % 2 else -5 + gap], dtype=T.int8, device="cuda")
+            a1, a2 = ops.new_range(), ops.new_range()
+            z, ez1 = ops.residual_add(a, ea, b, eb, a1)
+            e1 = T.zeros(1, dtype=T.int8, device="cuda")
+            want = ops.requant_act(z.view(-1, 16), a1, exp_in=ez1, exp_out=e1, relu=relu).view(-1)
+            ops.residual_range(a, ea, b, eb, a2)
+            got, ez2, e2 = ops.residual_requant(a, ea, b, eb, a2, relu=relu)
+            T.cuda.synchronize()
+            assert ops.range_max(a1) == ops.range_max(a2), gap
+            assert T.equal(got, want) and ez1.item() == ez2.item() and e1.item() == e2.item(), (gap, relu)
