@@ -75,15 +75,22 @@ __device__ __forceinline__ int32_t residual_z(int32_t hi, int32_t lo, int d, int
     return hi * (1 << d) + (r >= 31 ? (lo < 0 ? -1 : 0) : lo >> r);
 }
 
-// kernel-span probe: first block start / last block end on the device wall clock
-__device__ __forceinline__ void span_begin(unsigned long long* span) {
-    if (span != nullptr && threadIdx.x == 0) atomicMin(span, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+// kernel-span probe: every block writes its own {start, end} on the device wall clock into its
+// slot pair (plain stores, host takes min start / max end).  The first form max-ed every block's
+// start into one word with an atomic at block entry: 256 atomics on one address serialise at the
+// memory side, and the block's first counted vmcnt wait held until its atomic had completed.
+__device__ __forceinline__ unsigned long long span_begin(unsigned long long* span) {
+    return span != nullptr ? __builtin_amdgcn_s_memrealtime() : 0ull;
 }
-__device__ __forceinline__ void span_end(unsigned long long* span) {
+__device__ __forceinline__ void span_end(unsigned long long* span, unsigned long long t0) {
     if (span != nullptr) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (threadIdx.x == 0) atomicMax(span + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+        const unsigned b = blockIdx.x + blockIdx.y * gridDim.x;
+        if (threadIdx.x == 0 && b < (unsigned)SPAN_MAX_BLOCKS) {
+            span[2 * b] = t0;
+            span[2 * b + 1] = __builtin_amdgcn_s_memrealtime();
+        }
     }
 }
 

@@ -740,7 +740,7 @@ __global__ void __launch_bounds__(NW * 64) gemm_kernel(LA la, LB lb, int M, int 
     static_assert(SMEM >= BM * (BN + 16), "requant epilogue staging fits in the pipeline's LDS");
     __shared__ __attribute__((aligned(16))) int8_t smem[SMEM];
 
-    span_begin(epi.span);
+    const unsigned long long span_t0 = span_begin(epi.span);
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: LDS bases stay scalar
@@ -949,7 +949,7 @@ __global__ void __launch_bounds__(NW * 64) gemm_kernel(LA la, LB lb, int M, int 
         gemm_epilogue<TH, TN, NW, MODE, BM, BN>(keep, m0 + wm * (BM / WM) + keep_a * 32, n0 + wn * (BN / WN), M, N,
                                                 epi, smem, split, m0, n0);
     }
-    span_end(epi.span);
+    span_end(epi.span, span_t0);
 }
 
 // Sum of K-split slabs -> C (+ max|C|).  A block covers 256/G v4i elements with G threads
@@ -1141,7 +1141,7 @@ __global__ void __launch_bounds__(TAPS_THREADS) wgrad_taps_kernel(WgTaps g, Epi 
         if (tid == 0 && g.span == (unsigned long long*)1) smem[0] = 1;
         return;
     }
-    span_begin(g.span);
+    const unsigned long long span_t0 = span_begin(g.span);
     TAPS_STAMP(0);
     const int lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1434,7 +1434,7 @@ __global__ void __launch_bounds__(TAPS_THREADS) wgrad_taps_kernel(WgTaps g, Epi 
         __syncthreads();
         TAPS_STAMP(5);
     }
-    span_end(g.span);
+    span_end(g.span, span_t0);
 }
 
 

@@ -96,6 +96,8 @@ hipError_t conv_dgrad_acc(const ConvGeom& g, const int8_t* dy_nhwc16, const int8
 // start and max-es their end s_memrealtime (device wall clock) into slot[0] / slot[1]; the slot
 // is consumed by that launch.  Host-side, not thread-safe (one model per thread).
 void probe_span_arm(unsigned long long* slot);
+// a span slot is one {start, end} pair per block (block = blockIdx.x + blockIdx.y * gridDim.x)
+constexpr int SPAN_MAX_BLOCKS = 4096;
 // Kernel-event probe: the next weight-gradient GEMM launch records `begin` / `end` as part of its
 // own dispatch (hipExtLaunchKernel: the kernel's begin and end, as rocprofv3 times it).
 void probe_events_arm(hipEvent_t begin, hipEvent_t end);

@@ -326,7 +326,7 @@ struct Model {
             *e = ev1[probe_count];
             ++probe_count;
         }
-        if (span != nullptr && span_count < span_cap) *sp = span + 2 * span_count++;
+        if (span != nullptr && span_count < span_cap) *sp = span + 2 * SPAN_MAX_BLOCKS * span_count++;
     }
     // The weight gradient of layer i and the input gradient of layer i both read dy_i and
     // nothing else the other writes, so the weight gradients run on a second stream, each
@@ -399,7 +399,7 @@ struct Model {
         if (layer != probe_layer || phase != probe_phase || tuning || capturing || span == nullptr ||
             span_count >= span_cap)
             return;
-        probe_span_arm(span + 2 * span_count++);
+        probe_span_arm(span + 2 * SPAN_MAX_BLOCKS * span_count++);
     }
     void probe(int layer, int phase, bool begin, hipStream_t st) {
         if (layer != probe_layer || phase != probe_phase || tuning) return;
@@ -1355,14 +1355,9 @@ int niti_model_set_probe(niti_model_t m, int layer, int phase, int max_launches)
         if (hipEventCreateWithFlags(&m->m.ev0[i], hipEventDisableSystemFence) != hipSuccess ||
             hipEventCreateWithFlags(&m->m.ev1[i], hipEventDisableSystemFence) != hipSuccess)
             return NITI_OUT_OF_MEMORY;
-    if (phase == 2 && max_launches > 0) {
-        std::vector<unsigned long long> init(2 * (size_t)max_launches);
-        for (int i = 0; i < max_launches; ++i) {
-            init[2 * i] = ~0ull;
-            init[2 * i + 1] = 0;
-        }
-        if (hipMalloc(&m->m.span, init.size() * 8) != hipSuccess ||
-            hipMemcpy(m->m.span, init.data(), init.size() * 8, hipMemcpyHostToDevice) != hipSuccess)
+    if (phase == 2 && max_launches > 0) {  // per launch, a {start, end} pair per block (zero: no block)
+        const size_t bytes = (size_t)max_launches * 2 * niti::SPAN_MAX_BLOCKS * 8;
+        if (hipMalloc(&m->m.span, bytes) != hipSuccess || hipMemset(m->m.span, 0, bytes) != hipSuccess)
             return NITI_OUT_OF_MEMORY;
         m->m.span_cap = max_launches;
     }
@@ -1378,23 +1373,28 @@ int niti_model_probe_read_span(niti_model_t m, double* total_ms, int* count) {
     if (hipDeviceSynchronize() != hipSuccess || hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0)
         return NITI_NO_EXECUTION;
-    std::vector<unsigned long long> h(2 * (size_t)m->m.span_count);
+    constexpr size_t per = 2 * niti::SPAN_MAX_BLOCKS;
+    std::vector<unsigned long long> h(per * (size_t)m->m.span_count);
     if (hipMemcpy(h.data(), m->m.span, h.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return NITI_NO_EXECUTION;
     double t = 0;
     int n = 0;
-    for (int i = 0; i < m->m.span_count; ++i)
-        if (h[2 * i + 1] > h[2 * i]) {
-            t += (double)(h[2 * i + 1] - h[2 * i]) / khz;  // ticks / kHz = ms
+    for (int i = 0; i < m->m.span_count; ++i) {  // first block start to last block end of launch i
+        unsigned long long lo = ~0ull, hi = 0;
+        for (size_t b = 0; b < per; b += 2) {
+            const unsigned long long s0 = h[per * i + b], s1 = h[per * i + b + 1];
+            if (s1 == 0) continue;
+            lo = s0 < lo ? s0 : lo;
+            hi = s1 > hi ? s1 : hi;
+        }
+        if (hi > lo) {
+            t += (double)(hi - lo) / khz;  // ticks / kHz = ms
             ++n;
         }
+    }
     *total_ms = t;
     *count = n;
     // re-arm the slots for the next measurement
-    for (size_t i = 0; i < h.size(); i += 2) {
-        h[i] = ~0ull;
-        h[i + 1] = 0;
-    }
-    if (hipMemcpy(m->m.span, h.data(), h.size() * 8, hipMemcpyHostToDevice) != hipSuccess) return NITI_NO_EXECUTION;
+    if (hipMemset(m->m.span, 0, h.size() * 8) != hipSuccess) return NITI_NO_EXECUTION;
     m->m.span_count = 0;
     return NITI_NO_ERROR;
 }

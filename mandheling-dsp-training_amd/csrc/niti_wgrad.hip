@@ -223,7 +223,7 @@ __global__ void __launch_bounds__(NW * 64) wgrad_p16_kernel(WgP16 g) {
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-    span_begin(g.span);
+    const unsigned long long span_t0 = span_begin(g.span);
     WG_STAMP(0);
     WG_WSTAMP(0);
     const int logical = xcd_remap(blockIdx.x, gridDim.x);
@@ -553,7 +553,7 @@ __global__ void __launch_bounds__(NW * 64) wgrad_p16_kernel(WgP16 g) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         WG_STAMP(5);
     }
-    span_end(g.span);
+    span_end(g.span, span_t0);
 }
 
 // NHWC16 [P][CP] -> P16 [P/16][CP][16].  A 16-pixel block is 16 * CP contiguous bytes on both
