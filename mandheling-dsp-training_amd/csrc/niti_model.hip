@@ -290,7 +290,8 @@ struct Model {
     size_t grad_bucket_elems = 0;
     std::vector<int8_t*> xp16, dp16;
     std::vector<char> dp16_valid;  // dp16[i] holds L[i].dy as it is now
-    bool xp16_ready = false;  // run(): every P16 layer's input copy is already converted
+    std::vector<char> xp16_valid;  // xp16[i] holds L[i].in as it is now (cleared when a step starts)
+    void invalidate_xp16() { std::fill(xp16_valid.begin(), xp16_valid.end(), 0); }
     bool fuse_dp16 = true;    // NITI_P16_SEPARATE=1: always the separate conversion (A/B)
     int convert_p16_inputs(hipStream_t st) {
         P16Conv jobs[P16_MAX_JOBS];
@@ -299,6 +300,7 @@ struct Model {
             if (wgrad_p16_splits(j)) {
                 const ConvGeom& g = L[j].g;
                 jobs[n++] = P16Conv{L[j].in, (int64_t)g.n * g.h * g.w, g.cip, xp16[j]};
+                xp16_valid[j] = 1;
                 if (n == P16_MAX_JOBS || j + 1 == (int)L.size()) {
                     if (nhwc16_to_p16_many(jobs, n, st) != hipSuccess) return NITI_NO_EXECUTION;
                     n = 0;
@@ -590,6 +592,7 @@ int Model::build(int arch_, int batch_, int in_hw) {
     grad_bucket_elems = grad_elems;
     size_t grad_off = 0;
     xp16.assign(nl, nullptr);
+    xp16_valid.assign(nl, 0);
     dp16.assign(nl, nullptr);
     dp16_valid.assign(nl, 0);
     if (const char* e = getenv("NITI_P16_SEPARATE")) fuse_dp16 = atoi(e) == 0;
@@ -770,7 +773,10 @@ int Model::wgrad_layer(int i, hipStream_t st) {
         // P16 weight gradient: x (unless run() converted every input already) and dy to pixel
         // blocks, then the register-fed kernel (+ its split-K reduce); the probe times the kernel
         // launch itself
-        if (!xp16_ready) MTRY(nhwc16_to_p16(l.in, (int64_t)g.n * g.h * g.w, g.cip, xp16[i], st));
+        if (!xp16_valid[i]) {
+            MTRY(nhwc16_to_p16(l.in, (int64_t)g.n * g.h * g.w, g.cip, xp16[i], st));
+            xp16_valid[i] = 1;
+        }
         if (!dp16_valid[i]) {
             MTRY(nhwc16_to_p16(l.dy, (int64_t)g.n * g.oh * g.ow, g.cop, dp16[i], st));
             dp16_valid[i] = 1;
@@ -928,13 +934,13 @@ int Model::autotune(hipStream_t st, int reps) {
             }
             // P16 candidates are timed without their input conversion: run() converts every
             // layer's input in one launch off the step stream when the backward pass starts
-            xp16_ready = false;
+            invalidate_xp16();
             if (op == PLAN_WGRAD && conv_wgrad_p16_ok(g)) {
                 if (nhwc16_to_p16(L[i].in, (int64_t)g.n * g.h * g.w, g.cip, xp16[i], st) != hipSuccess) {
                     rc = NITI_NO_EXECUTION;
                     break;
                 }
-                xp16_ready = true;
+                xp16_valid[i] = 1;
             }
             float best_us = 0.f;
             rc = time_op(i, op, &best_us);
@@ -991,11 +997,11 @@ int Model::autotune(hipStream_t st, int reps) {
                 }
             }
             plan_override_set(key, best);
-            xp16_ready = false;
+            invalidate_xp16();
             if (rc != NITI_NO_ERROR) break;
         }
     }
-    xp16_ready = false;
+    invalidate_xp16();
     tuning = false;
     for (auto e : ev) (void)hipEventDestroy(e);
     if (hipStreamSynchronize(st) != hipSuccess) rc = NITI_NO_EXECUTION;
@@ -1008,7 +1014,7 @@ int Model::run(const int8_t* x_nchw, int exp_in, const uint8_t* images, const in
     const bool dp = this->dp();
     SgdJob jobs[SGD_MAX_JOBS];
     if (nl > SGD_MAX_JOBS) return NITI_NOT_SUPPORT;
-    xp16_ready = false;
+    invalidate_xp16();  // the forward pass rewrites every layer input
     MTRY(hipMemsetAsync(amax, 0, amax_bytes, st));
     if (x_nchw != nullptr) {
         MTRY(hipMemsetAsync(exp0, exp_in, 1, st));
@@ -1052,7 +1058,6 @@ int Model::run(const int8_t* x_nchw, int exp_in, const uint8_t* images, const in
         if (i == nl - 1) {  // the forward outputs are final: every P16 input copy in one go
             const int rc = convert_p16_inputs(wst);
             if (rc != NITI_NO_ERROR) return rc;
-            xp16_ready = true;
         }
         int rc = wgrad_layer(i, wst);
         if (rc == NITI_NO_ERROR && i > 0) rc = dgrad_layer(i, st);
@@ -1072,7 +1077,6 @@ int Model::run(const int8_t* x_nchw, int exp_in, const uint8_t* images, const in
         const int rc = reduce_wgrads(st);
         if (rc != NITI_NO_ERROR) return rc;
     }
-    xp16_ready = false;
     MTRY(sgd_update_many(jobs, nl, st));
     return NITI_NO_ERROR;
 }
