@@ -296,6 +296,10 @@ int niti_maxpool(const int8_t* x, int n, int h, int w, int cp, int k, int s, int
                  void* stream);
 int niti_maxpool_grad(const int8_t* x, const int8_t* y, const int8_t* dy, int n, int h, int w, int cp, int k,
                       int s, int p, int oh, int ow, int relu, int8_t* dx, void* stream);
+/* the same gradient in two passes over a caller workspace of n*oh*ow*cp bytes (each window's
+ * first-max position, then a gather per input pixel); equal results, for overlapping windows */
+int niti_maxpool_grad_ws(const int8_t* x, const int8_t* y, const int8_t* dy, int n, int h, int w, int cp, int k,
+                         int s, int p, int oh, int ow, int relu, int8_t* workspace, int8_t* dx, void* stream);
 int niti_relu_grad(const int8_t* x, const int8_t* dy, int64_t n, int8_t* out, void* stream);
 int niti_loss_grad(const int8_t* logits, int batch, int classes, int ld, const int8_t* ascale,
                    const int32_t* labels, int8_t* out, void* stream);

@@ -397,6 +397,11 @@ int niti_maxpool_grad(const int8_t* x, const int8_t* y, const int8_t* dy, int n,
                       int p, int oh, int ow, int relu, int8_t* dx, void* stream) {
     return code(niti::maxpool_relu_grad_nhwc16(x, y, dy, n, h, w, cp, k, s, p, oh, ow, relu, dx, S(stream)));
 }
+int niti_maxpool_grad_ws(const int8_t* x, const int8_t* y, const int8_t* dy, int n, int h, int w, int cp, int k,
+                         int s, int p, int oh, int ow, int relu, int8_t* ws, int8_t* dx, void* stream) {
+    if (!x || !y || !dy || !ws || !dx || n <= 0 || h <= 0 || w <= 0 || oh <= 0 || ow <= 0) return NITI_INVALID_VALUE;
+    return code(niti::maxpool_relu_grad_ws(x, y, dy, n, h, w, cp, k, s, p, oh, ow, relu, ws, dx, S(stream)));
+}
 int niti_relu_grad(const int8_t* x, const int8_t* dy, int64_t n, int8_t* out, void* stream) {
     if (n % 16) return NITI_INVALID_VALUE;
     return code(niti::relu_grad_nhwc16(x, dy, n, out, S(stream)));

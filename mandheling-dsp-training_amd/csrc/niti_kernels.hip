@@ -3244,6 +3244,99 @@ hipError_t maxpool_relu_grad_nhwc16(const int8_t* x, const int8_t* y, const int8
     return hipGetLastError();
 }
 
+// Overlapping windows in two passes over a caller workspace (the generic kernel above re-reads up
+// to 8 x vectors per window for every input pixel).  Pass 1, per window and 16 channels: the
+// position (ky * k + kx, in NITI_CPUPoolGrad_Int8.cpp's order, in-image elements only) of the
+// first element >= the window max y.  Pass 2, per input pixel: the sum (int8, wrapping, as the
+// reference's accumulation) of dy over the windows whose first max is this pixel, then the relu
+// mask.  Results equal maxpool_grad_kernel's.
+__global__ void maxpool_argmax_kernel(const int8_t* __restrict__ x, const int8_t* __restrict__ y, int n, int h, int w,
+                                      int cp, int k, int s, int p, int oh, int ow, int8_t* __restrict__ arg) {
+    const int groups = cp / 16;
+    const int64_t total = (int64_t)n * oh * ow * groups;
+    for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+        int64_t r = t;
+        const int gi = (int)(r % groups);
+        r /= groups;
+        const int ox = (int)(r % ow);
+        r /= ow;
+        const int oy = (int)(r % oh);
+        const int b = (int)(r / oh);
+        const v16c mv = *(const v16c*)(y + t * 16);
+        v16c a;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) a[j] = (signed char)-1;
+        uint32_t open = 0xffffu;
+        const int sy0 = oy * s - p, sx0 = ox * s - p;
+        for (int ky = 0; ky < k && open; ++ky) {
+            const int sy = sy0 + ky;
+            if (sy < 0 || sy >= h) continue;
+            for (int kx = 0; kx < k && open; ++kx) {
+                const int sx = sx0 + kx;
+                if (sx < 0 || sx >= w) continue;
+                const v16c xv = *(const v16c*)(x + (((int64_t)b * h + sy) * w + sx) * cp + gi * 16);
+#pragma unroll
+                for (int j = 0; j < 16; ++j)
+                    if (((open >> j) & 1u) && xv[j] >= mv[j]) {
+                        a[j] = (signed char)(ky * k + kx);
+                        open &= ~(1u << j);
+                    }
+            }
+        }
+        *(v16c*)(arg + t * 16) = a;
+    }
+}
+
+__global__ void maxpool_grad_gather_kernel(const int8_t* __restrict__ x, const int8_t* __restrict__ arg,
+                                           const int8_t* __restrict__ dy, int n, int h, int w, int cp, int k, int s,
+                                           int p, int oh, int ow, int relu, int8_t* __restrict__ dx) {
+    const int groups = cp / 16;
+    const int64_t total = (int64_t)n * h * w * groups;
+    for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+        int64_t r = t;
+        const int gi = (int)(r % groups);
+        r /= groups;
+        const int ix = (int)(r % w);
+        r /= w;
+        const int iy = (int)(r % h);
+        const int b = (int)(r / h);
+        v16c acc;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) acc[j] = 0;
+        const int oy_lo = max(0, (iy + p - k + s) / s), oy_hi = min(oh - 1, (iy + p) / s);
+        const int ox_lo = max(0, (ix + p - k + s) / s), ox_hi = min(ow - 1, (ix + p) / s);
+        for (int oy = oy_lo; oy <= oy_hi; ++oy)
+            for (int ox = ox_lo; ox <= ox_hi; ++ox) {
+                const int ky = iy - (oy * s - p), kx = ix - (ox * s - p);
+                if (ky < 0 || ky >= k || kx < 0 || kx >= k) continue;
+                const int64_t po = (((int64_t)b * oh + oy) * ow + ox) * cp + gi * 16;
+                const v16c av = *(const v16c*)(arg + po);
+                const v16c dv = *(const v16c*)(dy + po);
+                const signed char me = (signed char)(ky * k + kx);
+#pragma unroll
+                for (int j = 0; j < 16; ++j)
+                    if (av[j] == me) acc[j] = (signed char)(acc[j] + dv[j]);
+            }
+        if (relu) {
+            const v16c xv = *(const v16c*)(x + t * 16);
+#pragma unroll
+            for (int j = 0; j < 16; ++j) acc[j] = xv[j] > 0 ? acc[j] : (signed char)0;
+        }
+        *(v16c*)(dx + t * 16) = acc;
+    }
+}
+
+hipError_t maxpool_relu_grad_ws(const int8_t* x, const int8_t* y, const int8_t* dy, int n, int h, int w, int cp, int k,
+                                int s, int p, int oh, int ow, int relu, int8_t* ws, int8_t* dx, hipStream_t st) {
+    if (cp % 16 != 0 || k <= 0 || k > 11 || s <= 0 || ws == nullptr) return hipErrorInvalidValue;
+    const int64_t tw = (int64_t)n * oh * ow * (cp / 16), tx = (int64_t)n * h * w * (cp / 16);
+    auto blocks = [](int64_t t) { return (unsigned)std::max<int64_t>(1, std::min<int64_t>((t + 255) / 256, 8192)); };
+    hipLaunchKernelGGL(maxpool_argmax_kernel, dim3(blocks(tw)), dim3(256), 0, st, x, y, n, h, w, cp, k, s, p, oh, ow, ws);
+    hipLaunchKernelGGL(maxpool_grad_gather_kernel, dim3(blocks(tx)), dim3(256), 0, st, x, ws, dy, n, h, w, cp, k, s, p,
+                       oh, ow, relu, dx);
+    return hipGetLastError();
+}
+
 __global__ void relu_grad_kernel(const int8_t* __restrict__ x, const int8_t* __restrict__ dy, int64_t n16,
                                  int64_t n, int8_t* __restrict__ out) {
     const int64_t t0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;

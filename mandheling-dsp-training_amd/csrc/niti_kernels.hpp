@@ -271,6 +271,10 @@ hipError_t maxpool_relu_grad_nhwc16(const int8_t* x, const int8_t* y, const int8
                                     int w, int cp, int k, int s, int p, int oh, int ow, int relu,
                                     int8_t* dx, hipStream_t st);
 hipError_t relu_grad_nhwc16(const int8_t* x, const int8_t* dy, int64_t n, int8_t* out, hipStream_t st);
+// the same gradient in two passes over a workspace of n*oh*ow*cp bytes (each window's first-max
+// position, then a gather per input pixel): for overlapping windows (ResNet's 3x3 / 2 stem pool)
+hipError_t maxpool_relu_grad_ws(const int8_t* x, const int8_t* y, const int8_t* dy, int n, int h, int w, int cp, int k,
+                                int s, int p, int oh, int ow, int relu, int8_t* ws, int8_t* dx, hipStream_t st);
 // logits int8 [batch][ld] (first `classes` used), labels int32 [batch] (class index);
 // out int8 [batch][ld] (padded lanes zeroed).  classes <= 2048 (one thread per sample up to 16,
 // one block per sample above).  NITI_CPULossGrad_Int8.cpp:81-200.

@@ -139,6 +139,7 @@ def lib():
         "niti_sum_pool_grad": (ci, [vp, ci, ci, ci, vp, vp]),
         "niti_maxpool": (ci, [vp] + [ci] * 7 + [vp, ci, ci, vp]),
         "niti_maxpool_grad": (ci, [vp, vp, vp] + [ci] * 10 + [vp, vp]),
+        "niti_maxpool_grad_ws": (ci, [vp, vp, vp] + [ci] * 10 + [vp, vp, vp]),
         "niti_relu_grad": (ci, [vp, vp, i64, vp, vp]),
         "niti_loss_grad": (ci, [vp, ci, ci, ci, vp, vp, vp, vp]),
         "niti_model_create": (ci, [ci, ci, C.POINTER(vp)]),

@@ -375,12 +375,21 @@ def maxpool(x16, k=2, s=2, p=0, stream=None):
     return y
 
 
-def maxpool_grad(x16, y16, dy16, k=2, s=2, p=0, relu=False, stream=None):
+def maxpool_grad(x16, y16, dy16, k=2, s=2, p=0, relu=False, stream=None, two_pass=None):
+    """dx of the max pool (first max wins), relu mask optional.  Overlapping windows (k > s) run the
+    two-pass form over a workspace (niti_maxpool_grad_ws) unless two_pass=False."""
     n, h, w, cp = x16.shape
     oh, ow = y16.shape[1], y16.shape[2]
     dx = torch.empty_like(x16)
-    check(L.lib().niti_maxpool_grad(_ptr(x16), _ptr(y16), _ptr(dy16), n, h, w, cp, k, s, p, oh, ow,
-                                    1 if relu else 0, _ptr(dx), _stream(stream)), "maxpool_grad")
+    if two_pass is None:
+        two_pass = k > s
+    if two_pass:
+        ws = torch.empty_like(y16)
+        check(L.lib().niti_maxpool_grad_ws(_ptr(x16), _ptr(y16), _ptr(dy16), n, h, w, cp, k, s, p, oh, ow,
+                                           1 if relu else 0, _ptr(ws), _ptr(dx), _stream(stream)), "maxpool_grad_ws")
+    else:
+        check(L.lib().niti_maxpool_grad(_ptr(x16), _ptr(y16), _ptr(dy16), n, h, w, cp, k, s, p, oh, ow,
+                                        1 if relu else 0, _ptr(dx), _stream(stream)), "maxpool_grad")
     return dx
 
 

@@ -846,3 +846,25 @@ def test_conv_two_phase_requant_equals_store_path(T, h, ci, co, stride, relu):
         T.cuda.synchronize()
         assert seen == [ops.range_max(a1)], op
         assert T.equal(got, want) and e1.item() == e2.item(), op
+
+
+@pytest.mark.parametrize("geo", [(2, 64, 17, 17, 3, 2, 1), (3, 16, 12, 12, 3, 2, 1), (2, 32, 9, 9, 3, 1, 1),
+                                 (1, 48, 10, 10, 2, 2, 0), (2, 16, 11, 11, 5, 2, 2)])
+@pytest.mark.parametrize("relu", [False, True])
+def test_maxpool_grad_two_pass(T, ops, oracle, geo, relu):
+    """niti_maxpool_grad_ws (window first-max positions, then a gather per input pixel) equals the
+    oracle's NITI_CPUPoolGrad_Int8 restatement and the one-pass kernel, ties included."""
+    n, c, h, w, k, s, p = geo
+    rng = np.random.default_rng(h * k + c)
+    x = rng.integers(-6, 7, size=(n, c, h, w), dtype=np.int8)  # small range: many ties
+    y_ref = oracle.maxpool(x, k, s, p)
+    dy = rng.integers(-128, 128, size=y_ref.shape, dtype=np.int8)
+    want = oracle.maxpool_grad(x, y_ref, dy, k, s, p)
+    if relu:
+        want = oracle.relu_grad(x, want)
+    x16, y16, d16 = (ops.nchw_to_nhwc16(dev(T, a)) for a in (x, y_ref, dy))
+    got2 = ops.maxpool_grad(x16, y16, d16, k, s, p, relu=relu, two_pass=True)
+    got1 = ops.maxpool_grad(x16, y16, d16, k, s, p, relu=relu, two_pass=False)
+    T.cuda.synchronize()
+    assert T.equal(got1, got2)
+    assert np.array_equal(ops.nhwc16_to_nchw(got2, c).cpu().numpy(), want)
