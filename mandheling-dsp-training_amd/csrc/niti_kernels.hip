@@ -2961,7 +2961,11 @@ hipError_t requant_act(const ActRequant& r, hipStream_t st) {
             g.fph = make_fastdiv((uint32_t)(r.pool.H / 2));
         }
         int64_t blocks = (units + 256 * RQ_U - 1) / (256 * RQ_U);
-        if (blocks > 2048) blocks = 2048;
+        static const int64_t cap = [] {  // diagnostics (A/B): NITI_RQ_BLOCKS overrides the grid cap
+            const char* e = getenv("NITI_RQ_BLOCKS");
+            return e && atoi(e) > 0 ? (int64_t)atoi(e) : (int64_t)2048;
+        }();
+        if (blocks > cap) blocks = cap;
         if (blocks < 1) blocks = 1;
         if (pf)
             hipLaunchKernelGGL(requant_quad_kernel<RQ_POOL_FWD>, dim3((unsigned)blocks), dim3(256), 0, st, r, g);
