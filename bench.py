@@ -313,7 +313,11 @@ def main():
         try:
             tr = json.load(open(tfile))
             key = f"{args.arch}_b{args.batch}_L{probe_layer}_p{args.probe_phase}"
-            traffic = tr.get(key, {}).get("hbm_bytes_per_launch")
+            ent = tr.get(key, {})
+            # PMC bytes are per plan: report them only when this run's probed plan is the one the
+            # counters were collected under (profiles/traffic.json "plan")
+            if list(ent.get("plan", [])) == list(plans[(probe_layer, args.probe_phase)]):
+                traffic = ent.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
 

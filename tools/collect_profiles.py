@@ -76,6 +76,11 @@ def main():
                           f"{P}/traffic.json", str(gx), "1", name, "20"], capture_output=True, text=True, check=True).stdout
     open(f"{P}/{tag}_traffic.txt", "w").write(out)
     print(out)
+    # the plan the counters were collected under: bench.py reports the traffic only for that plan
+    tj = json.load(open(f"{P}/traffic.json"))
+    for v in tj.values():
+        v["plan"] = [plan["bm"], plan["bn"], plan["splits"], plan["strategy"]]
+    json.dump(tj, open(f"{P}/traffic.json", "w"), indent=1)
     for cnt, fn in (("pmcF", "fetch"), ("pmcW", "write")):
         src = glob.glob(f"{G}/{cnt}_{tag}/*counter_collection.csv")[0]
         rs = list(csv.DictReader(open(src)))
