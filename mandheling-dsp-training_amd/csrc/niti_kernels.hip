@@ -3008,9 +3008,9 @@ hipError_t requant_grad(const int32_t* acc, int64_t n, const uint32_t* amax, int
 // operand) through an LDS tile -- the transposed copy never needs a pass of its own.
 // One 64 (co) x 64 (ci) tile of one tap: g = rule(acc, range), w <- clip(w - g, +-127) in OHWI16,
 // the same tile transposed through LDS into IHWO16 (the input-gradient operand), g to g_out.
-__device__ __forceinline__ void sgd_tile(const SgdJob& J, int ci0, int co0, int k, int8_t (*T)[64 + 4]) {
+// bw: NITI_RangeEstimate of the job's gradient (read once per job by the caller)
+__device__ __forceinline__ void sgd_tile(const SgdJob& J, int bw, int ci0, int co0, int k, int8_t (*T)[64 + 4]) {
     const int t = threadIdx.x;
-    const int bw = bitwidth_of(read_max(J.amax));
     const int sh = bw - J.rule;
     {
         const int r = t >> 2, c = (t & 3) * 16;
@@ -3055,15 +3055,22 @@ __global__ void sgd_update_kernel(SgdJobs jobs, int total) {
     __shared__ int8_t T[64][64 + 4];
     // a block takes tiles b, b + gridDim, ...: one resident wave of blocks instead of a full
     // wave plus a straggling partial one
+    // the range of a job's gradient is read once per job a block visits (a dependent global read
+    // and wave reduction per tile was a latency round trip of every iteration)
+    int last_j = -1, bw = 0;
     for (int bb = blockIdx.x; bb < total; bb += gridDim.x) {
         int b = bb, j = 0;
         while (j + 1 < jobs.n && b >= jobs.start[j + 1]) ++j;
         const SgdJob& J = jobs.job[j];
+        if (j != last_j) {
+            bw = bitwidth_of(read_max(J.amax));
+            last_j = j;
+        }
         b -= jobs.start[j];
         const int tx = (J.cip + 63) / 64, ty = (J.cop + 63) / 64;
         const int k = b / (tx * ty), rem = b - k * tx * ty;
         if (bb != (int)blockIdx.x) __syncthreads();  // the previous tile's transposed reads are done
-        sgd_tile(J, (rem % tx) * 64, (rem / tx) * 64, k, T);
+        sgd_tile(J, bw, (rem % tx) * 64, (rem / tx) * 64, k, T);
     }
 }
 
