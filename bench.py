@@ -9,15 +9,81 @@ and the exact-mode RCCL all-reduces (MAX of every range, SUM of every int32 weig
 gradient) keep all ranks bit-identical to one device running the global batch.
 
 Prints ONE JSON line on rank 0 (contract in the task statement).
+
+Launch: `python bench.py --gpus N` with N > 1 and no WORLD_SIZE in the environment starts the N
+ranks itself (torch.distributed.run as a child process, 127.0.0.1 rendezvous, before anything
+touches the GPU) and exits with its code; under torchrun the world size must equal --gpus.
+`--global-batch G` holds the global batch fixed (G / N images per GPU, strong scaling, BASELINE
+configs 4 and 5: 512 and 1024 on 8 GPUs); otherwise every GPU trains `--batch` images (weak).
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "mandheling-dsp-training_amd"))
+
+
+def _free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n, argv):
+    """Start `n` ranks of this script under torch.distributed.run (one process per GPU) as a
+    child process and return its exit code.  Called before any GPU call in this process."""
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this pool (RCCL)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + list(argv)
+    return subprocess.call(cmd, env=env)
+
+
+def resolve_world(args):
+    """(world, rank, local_rank) from the torchrun environment, checked against --gpus."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus is not None and args.gpus != world:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    return world, int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0"))
+
+
+def per_gpu_batch(args, world, default):
+    """Images per GPU: --global-batch / world (strong scaling), else --batch or the default (weak)."""
+    if args.global_batch:
+        if args.global_batch % world:
+            raise SystemExit(f"bench.py: --global-batch {args.global_batch} is not a multiple of {world} GPUs")
+        return args.global_batch // world, "strong"
+    return (args.batch or default), "weak"
+
+
+def parallelism_label(world, what):
+    return f"dp{world} exact ({what})" if world > 1 else "single GPU"
+
+
+def spawn_check(args):
+    """--spawn-check (CPU, no GPU call): every rank joins a gloo group and all-reduces its rank;
+    rank 0 prints the line's launch fields.  Exercises the self-launch path on a CPU box."""
+    import torch
+    import torch.distributed as dist
+    world, rank, _ = resolve_world(args)
+    if world > 1:
+        dist.init_process_group("gloo")
+    t = torch.tensor([rank + 1], dtype=torch.int64)
+    if world > 1:
+        dist.all_reduce(t)
+    b, scaling = per_gpu_batch(args, world, 256)
+    if rank == 0:
+        print(json.dumps({"n_gpus": world, "ranks_sum": int(t.item()), "per_gpu_batch": b,
+                          "global_batch": b * world, "scaling": scaling,
+                          "parallelism": parallelism_label(world, "spawn check")}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
 
 PEAK_INT8_TOPS = 256 * 4 * 2048 * 2.4e9 / 1e12  # 256 CU x 4 SIMD x 2048 int8 op/clk x 2.4 GHz = 5033
 PEAK_HBM_GBS = 8000.0
@@ -48,7 +114,7 @@ def cpu_model():
     return "unknown"
 
 
-def cpu_baseline(arch, sample, threads_list):
+def cpu_baseline(arch, sample, threads_list, in_hw=0):
     """The oracle's reference-structured restatement of the WHOLE NITIInt8Train step (input
     quantiser, NITI_Conv_Int8 forwards in MNN C4 with the 16x4 GEMM unit and float32
     accumulation, relu / maxpool, NITI_LOSS_Grad, the grad graph's weight and input gradients,
@@ -58,18 +124,20 @@ def cpu_baseline(arch, sample, threads_list):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import niti_model_ref as R
     import niti_oracle as O
-    layers = {"vgg11": R.vgg11_layers, "lenet": R.lenet_layers}[arch]()
+    layers = {"vgg11": R.vgg11_layers, "lenet": R.lenet_layers,
+              "vgg16": lambda: R.vgg16_layers(in_hw or 224)}[arch]()
+    classes = 1000 if arch == "vgg16" else 10
     W, S = R.init_weights(layers, seed=17)
     rng = np.random.default_rng(1)
     l0 = layers[0]
     img = rng.integers(0, 256, (sample, l0["ci"], l0["h"], l0["h"])).astype(np.uint8)
-    labels = rng.integers(0, 10, sample).astype(np.int32)
+    labels = rng.integers(0, classes, sample).astype(np.int32)
     legs = []
     for t in threads_list:
         O.set_threads(t)
         t0 = time.perf_counter()
         x, a = O.quantize_images(img)
-        R.train_step(layers, W, S, x, a, labels, impl="mnn", threads=t, acc_mode=O.ACC_F32_SEQ)
+        R.train_step(layers, W, S, x, a, labels, classes=classes, impl="mnn", threads=t, acc_mode=O.ACC_F32_SEQ)
         secs = time.perf_counter() - t0
         legs.append({"threads": t, "value": round(sample / secs, 3), "seconds": round(secs, 2)})
     return legs
@@ -84,9 +152,8 @@ def bench_resnet18(args):
     import torch
     from niti_amd import ops
     from niti_amd.resnet import ResNet18
-    torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
+    world, rank, local = resolve_world(args)
+    torch.cuda.set_device(local)
     comm = None
     if world > 1:
         import torch.distributed as dist
@@ -94,7 +161,7 @@ def bench_resnet18(args):
         dist.init_process_group("nccl", device_id=torch.device("cuda", torch.cuda.current_device()))
         comm = TorchComm()
     hw = args.in_hw or 224
-    batch = args.batch or 128
+    batch, scaling = per_gpu_batch(args, world, 128)
     m = ResNet18(batch, hw, 1000, comm=comm)
     layers = [dict(c_out=l["co"], c_in=l["ci"], kh=l["k"], kw=l["k"]) for l in m.convs]
     for i, (w, s) in enumerate(synth_weights(layers, seed=17)):
@@ -144,12 +211,12 @@ def bench_resnet18(args):
         "metric": "training images/sec + int8 MFMA TOPS, ResNet-18 ImageNet-224 (BASELINE config 5 network)",
         "value": round(batch * world * args.steps / el, 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "int8",
+        "scaling": scaling, "vs_baseline": None, "dtype": "int8",
         "data": "synthetic (random uint8 images through the on-device input quantiser; random labels; seeded weights)",
         "config": {"workload": f"ResNet-18 NITI int8 training step, 3x{hw}x{hw}, 1000 classes",
                    "global_batch": batch * world, "per_gpu_batch": batch,
-                   "parallelism": (f"dp{world} exact (RCCL all-reduce MAX ranges + SUM int32 grads, niti_amd.dp)"
-                                   if comm is not None else "single GPU (host-driven op sequence, niti_amd.resnet)"),
+                   "parallelism": parallelism_label(world, "RCCL all-reduce MAX ranges + SUM int32 grads, niti_amd.dp"),
+                   "driver": "host-driven op sequence (niti_amd.resnet)",
                    "launch": "hipGraph replay of the captured step" if graph is not None else "direct launches"},
         "int8_mfma_tops": round(tops, 2), "int8_mfma_frac_of_peak": round(tops / PEAK_INT8_TOPS, 4),
         "roofline": None, "cpu_baseline": None}))
@@ -159,11 +226,15 @@ def bench_resnet18(args):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None, help="ranks (GPUs of this node); N > 1 outside torchrun "
+                                                           "launches the N ranks itself (default: 1, or WORLD_SIZE)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=0, help="images per GPU per step (0: 256 VGG-11 / LeNet, "
                                                          "64 VGG-16 = BASELINE cfg 4's 512 over 8 GPUs)")
+    ap.add_argument("--global-batch", type=int, default=0, help="hold the global batch fixed (strong scaling): "
+                                                                "global-batch / N images per GPU")
+    ap.add_argument("--spawn-check", action="store_true", help="CPU check of the multi-rank launch (gloo, no GPU)")
     ap.add_argument("--arch", default="vgg11", choices=["vgg11", "lenet", "vgg16", "resnet18"])
     ap.add_argument("--in-hw", type=int, default=0, help="input resolution (0: the architecture's own)")
     ap.add_argument("--cpu-sample", type=int, default=-1, help="images in the CPU baseline sample "
@@ -186,15 +257,17 @@ def main():
                                                               "takes with this many K splits (0: its default; "
                                                               "-1: the autotuner's choice)")
     args = ap.parse_args()
+    if args.gpus is not None and args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return spawn_ranks(args.gpus, sys.argv[1:])
+    if args.spawn_check:
+        return spawn_check(args)
     if args.arch == "resnet18":
         return bench_resnet18(args)
 
     import numpy as np
     import torch
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    world, rank, local = resolve_world(args)
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
@@ -205,10 +278,9 @@ def main():
     from niti_amd.model import NitiModel
 
     arch = {"vgg11": niti_amd.ARCH_VGG11, "lenet": niti_amd.ARCH_LENET, "vgg16": niti_amd.ARCH_VGG16}[args.arch]
-    if args.batch <= 0:
-        args.batch = 64 if arch == niti_amd.ARCH_VGG16 else 256
+    args.batch, scaling = per_gpu_batch(args, world, 64 if arch == niti_amd.ARCH_VGG16 else 256)
     if args.cpu_sample < 0:
-        args.cpu_sample = {niti_amd.ARCH_VGG16: 0, niti_amd.ARCH_LENET: 512}.get(arch, 128)
+        args.cpu_sample = {niti_amd.ARCH_VGG16: 2, niti_amd.ARCH_LENET: 512}.get(arch, 128)
     model = NitiModel(arch, args.batch, args.in_hw)
     model.set_graph(args.graph)
     model.set_overlap(args.overlap and not args.no_overlap)
@@ -322,13 +394,13 @@ def main():
             traffic = None
 
     cpu = None
-    if rank == 0 and world == 1 and args.cpu_sample > 0 and args.arch in ("vgg11", "lenet"):
+    if rank == 0 and world == 1 and args.cpu_sample > 0 and args.arch in ("vgg11", "lenet", "vgg16"):
         # every core this process may use: the affinity set, capped by the box's CPU share
         # (OMP_NUM_THREADS, 16 per GPU on the pool) -- the thread count is reported as `cores`
         all_cores = len(os.sched_getaffinity(0))
         if os.environ.get("OMP_NUM_THREADS", "").isdigit():
             all_cores = max(1, min(all_cores, int(os.environ["OMP_NUM_THREADS"])))
-        legs = cpu_baseline(args.arch, args.cpu_sample, sorted({args.cpu_threads, all_cores}))
+        legs = cpu_baseline(args.arch, args.cpu_sample, sorted({args.cpu_threads, all_cores}), args.in_hw)
         best = max(legs, key=lambda l: l["value"])
         cpu = {"value": best["value"], "unit": "images/s", "cores": best["threads"], "kind": "port",
                "sample": f"{args.cpu_sample} images through the whole {args.arch.upper()} NITIInt8Train step (input "
@@ -359,7 +431,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": "int8",
         "data": ("synthetic (random int8 x, fixed exponent" if args.int8_input else
@@ -370,7 +442,7 @@ def main():
                                + (", 4096-4096-1000 head" if arch == niti_amd.ARCH_VGG16 else "")
                                if arch != niti_amd.ARCH_LENET else "LeNet NITI int8 training step, 1x28x28",
                    "global_batch": args.batch * world, "per_gpu_batch": args.batch,
-                   "parallelism": f"dp{world} exact (RCCL all-reduce MAX ranges + SUM int32 grads)",
+                   "parallelism": parallelism_label(world, "RCCL all-reduce MAX ranges + SUM int32 grads"),
                    "streams": "weight gradients beside the input-gradient chain on a second stream" if args.overlap
                    and not args.no_overlap else "one stream (weight gradient, then input gradient, per layer)"},
         "int8_mfma_tops": round(tops, 2),
@@ -406,4 +478,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

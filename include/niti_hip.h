@@ -306,7 +306,8 @@ int niti_loss_grad(const int8_t* logits, int batch, int classes, int ld, const i
 
 /* NITIInt8Train's input quantiser (execution-engine/tools/train/source/demo/MnistUtils.cpp:83-93):
  * mean / std / range of the uint8 batch, x = round((p - mean) / std / range * 127), ascale =
- * int8(ceil(ln(range)) - 7).  Split so data-parallel ranks can all-reduce the statistics:
+ * int8(ceilf(logf(range)) - 7) in float.  The variance divisor is the reference's literal
+ * batchSize * 28 * 28 (:86), batchSize = count / (c * hw) images, for every image size.  Split so data-parallel ranks can all-reduce the statistics:
  * stats (4 x uint64, device) = {sum p, sum p^2 (SUM over ranks), max p, 255 - min p (MAX)};
  * count = pixels the statistics cover (all ranks').  The float contract (exact integer
  * statistics, the per-pixel formula in the reference's operation order) is stated in

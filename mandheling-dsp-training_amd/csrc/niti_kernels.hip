@@ -907,6 +907,20 @@ __global__ void __launch_bounds__(NW * 64) gemm_kernel(LA la, LB lb, int M, int 
         body(std::integral_constant<int, 0>(), s);
         if (s + 1 < nsteps) body(std::integral_constant<int, 1>(), s + 1);
     }
+    // The last step waited lgkmcnt(0), but hipcc sees the fragment registers of the merged
+    // "more" path as dead at the loop exit and may reuse them in the epilogue ahead of any wait;
+    // drain and touch every fragment register so none is reused while an asm read could be in
+    // flight (tools/isa_inflight.py scans for this).
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int j = 0; j < KW_; ++j) {
+#pragma unroll
+            for (int a = 0; a < TM; ++a) reg_fence(fa[u][j][a]);
+#pragma unroll
+            for (int b = 0; b < TN; ++b) reg_fence(fb[u][j][b]);
+        }
     __syncthreads();
     if constexpr (KG == 1) {
         gemm_epilogue<TM, TN, NW, MODE, BM, BN>(acc, m0 + wm * (BM / WM), n0 + wn * (BN / WN), M, N, epi, smem, split,
@@ -2961,11 +2975,7 @@ hipError_t requant_act(const ActRequant& r, hipStream_t st) {
             g.fph = make_fastdiv((uint32_t)(r.pool.H / 2));
         }
         int64_t blocks = (units + 256 * RQ_U - 1) / (256 * RQ_U);
-        static const int64_t cap = [] {  // diagnostics (A/B): NITI_RQ_BLOCKS overrides the grid cap
-            const char* e = getenv("NITI_RQ_BLOCKS");
-            return e && atoi(e) > 0 ? (int64_t)atoi(e) : (int64_t)2048;
-        }();
-        if (blocks > cap) blocks = cap;
+        if (blocks > 2048) blocks = 2048;
         if (blocks < 1) blocks = 1;
         if (pf)
             hipLaunchKernelGGL(requant_quad_kernel<RQ_POOL_FWD>, dim3((unsigned)blocks), dim3(256), 0, st, r, g);

@@ -119,12 +119,21 @@ struct FlattenBwd {
 }  // namespace
 
 // ---------------------------------------------------------------------------- collectives
-// The data-parallel step's collectives.  Every rank issues the same sequence, all of it on the
-// step stream through ONE communicator, so no two collectives are ever in flight at once on a
-// rank and the order is the program order on every rank: no cross-stream or cross-communicator
-// interleaving exists that could deadlock (round 1 split a second communicator for the weight
-// gradients on the side stream; that concurrency is gone).  The weight-gradient GEMMs still run
-// on the side stream; their SUMs are issued on the step stream one layer later (Model::run).
+// The data-parallel step's collectives run on two communicators, each used in one fixed program
+// order on every rank:
+//   ranges (`coll`, the step stream): the input quantiser's statistics and every forward /
+//     input-gradient range (MAX), each needed by the very next launch on the step stream;
+//   gradients (`coll_grad`, the comm stream `cst`): one SUM per gradient bucket (consecutive
+//     layers in backward order, ~8 MB or more), issued as soon as the bucket's weight gradients
+//     are in and followed on cst by those layers' ranges, so the SUMs overlap the rest of the
+//     backward pass.
+// RCCL serialises the operations of ONE communicator in issue order whatever stream they are on
+// (each launch waits for the communicator's previous one), so a range MAX on the same
+// communicator as a large SUM would wait for that SUM and stall the input-gradient chain behind
+// it.  With two communicators the step stream's MAXes never wait for a SUM; no operation of one
+// communicator waits for an operation of the other (the SUMs wait only for weight-gradient
+// kernels, the step stream for the SUMs only at the NITI_SGD join), and each communicator's
+// operations are issued in the same order on every rank, so the two cannot deadlock.
 enum CollOp { COLL_MAX_U32 = 0, COLL_SUM_I32 = 1, COLL_SUM_U64 = 2, COLL_MAX_U64 = 3 };
 
 struct Collective {
@@ -152,19 +161,28 @@ struct RcclCollective final : Collective {
 // collective synchronises the caller's stream, the last rank to arrive reduces every rank's
 // buffer on the device and writes the result back to all of them.  It runs the model's exact
 // data-parallel protocol -- the same calls, in the same order, on the same streams -- with a
-// transport that needs no second GPU.
-struct LocalGroup {
-    static constexpr int MAX_RANKS = 16;
-    int world = 1;
+// transport that needs no second GPU.  A group has one channel per communicator (ranges,
+// gradients), each its own rendezvous.
+struct LocalChannel {
     std::mutex mu;
     std::condition_variable cv;
     int arrived = 0;
     unsigned long long gen = 0;
-    void* ptr[MAX_RANKS] = {};
+    void* ptr[16] = {};
     size_t n = 0;
     int op = -1;
     bool mismatch = false;
     hipError_t err = hipSuccess;
+    // the result of generation g, published before the waiters are released: a waiter reads
+    // its own generation's slot, which a faster rank entering generation g + 1 cannot reset
+    // (generation g + 2 needs this waiter's arrival first)
+    hipError_t result[2] = {hipSuccess, hipSuccess};
+};
+
+struct LocalGroup {
+    static constexpr int MAX_RANKS = 16;
+    int world = 1;
+    LocalChannel ch[2];
     hipStream_t rst = nullptr;
     ~LocalGroup() {
         if (rst) (void)hipStreamDestroy(rst);
@@ -191,26 +209,27 @@ __global__ void local_reduce_kernel(RankPtrs r, size_t n) {
 
 struct LocalCollective final : Collective {
     std::shared_ptr<LocalGroup> g;
-    int rank = 0;
+    int rank = 0, chan = 0;
     int size() const override { return g->world; }
     hipError_t allreduce(void* p, size_t n, CollOp op, hipStream_t st) override {
+        LocalChannel& c = g->ch[chan];
         hipError_t e = hipStreamSynchronize(st);
-        std::unique_lock<std::mutex> lk(g->mu);
-        const unsigned long long my_gen = g->gen;
-        if (g->arrived == 0) {
-            g->n = n;
-            g->op = op;
-            g->mismatch = false;
-            g->err = hipSuccess;
-        } else if (g->n != n || g->op != op) {
-            g->mismatch = true;  // ranks disagree on the sequence: a protocol bug
+        std::unique_lock<std::mutex> lk(c.mu);
+        const unsigned long long my_gen = c.gen;
+        if (c.arrived == 0) {
+            c.n = n;
+            c.op = op;
+            c.mismatch = false;
+            c.err = hipSuccess;
+        } else if (c.n != n || c.op != op) {
+            c.mismatch = true;  // ranks disagree on the sequence: a protocol bug
         }
-        g->ptr[rank] = p;
-        if (e != hipSuccess) g->err = e;
-        if (++g->arrived == g->world) {
-            if (!g->mismatch && g->err == hipSuccess) {
+        c.ptr[rank] = p;
+        if (e != hipSuccess) c.err = e;
+        if (++c.arrived == g->world) {
+            if (!c.mismatch && c.err == hipSuccess) {
                 RankPtrs r{};
-                for (int k = 0; k < g->world; ++k) r.p[k] = g->ptr[k];
+                for (int k = 0; k < g->world; ++k) r.p[k] = c.ptr[k];
                 r.world = g->world;
                 const unsigned blocks = (unsigned)std::min<size_t>((n + 255) / 256, 1024);
                 if (blocks > 0) {
@@ -224,18 +243,19 @@ struct LocalCollective final : Collective {
                     else
                         hipLaunchKernelGGL((local_reduce_kernel<unsigned long long, true>), dim3(blocks), dim3(256), 0,
                                            g->rst, r, n);
-                    g->err = hipGetLastError();
-                    if (g->err == hipSuccess) g->err = hipStreamSynchronize(g->rst);
+                    c.err = hipGetLastError();
+                    if (c.err == hipSuccess) c.err = hipStreamSynchronize(g->rst);
                 }
             }
-            if (g->mismatch) g->err = hipErrorInvalidValue;
-            g->arrived = 0;
-            ++g->gen;
-            g->cv.notify_all();
+            if (c.mismatch) c.err = hipErrorInvalidValue;
+            c.result[my_gen & 1] = c.err;
+            c.arrived = 0;
+            ++c.gen;
+            c.cv.notify_all();
         } else {
-            g->cv.wait(lk, [&] { return g->gen != my_gen; });
+            c.cv.wait(lk, [&] { return c.gen != my_gen; });
         }
-        return g->err;
+        return c.result[my_gen & 1];
     }
 };
 
@@ -292,7 +312,7 @@ struct Model {
     std::vector<char> dp16_valid;  // dp16[i] holds L[i].dy as it is now
     std::vector<char> xp16_valid;  // xp16[i] holds L[i].in as it is now (cleared when a step starts)
     void invalidate_xp16() { std::fill(xp16_valid.begin(), xp16_valid.end(), 0); }
-    bool fuse_dp16 = true;    // NITI_P16_SEPARATE=1: always the separate conversion (A/B)
+    bool fuse_dp16 = true;    // dy's P16 copy written by the requantisation that produces dy
     int convert_p16_inputs(hipStream_t st) {
         P16Conv jobs[P16_MAX_JOBS];
         int n = 0;
@@ -342,9 +362,49 @@ struct Model {
     uint32_t* amax = nullptr;  // 3 ranges per layer (forward, input gradient, weight gradient)
     size_t amax_bytes = 0;
     uint32_t* rng(int layer, int which) { return amax + (size_t)(3 * layer + which) * MAX_WORDS; }
-    std::unique_ptr<Collective> coll;
+    // data parallel (see "collectives" above): ranges on the step stream through `coll`,
+    // gradient-bucket SUMs on the comm stream `cst` through `coll_grad`.  Attached at any world
+    // size (a world of 1 runs every collective call site on one GPU).
+    std::unique_ptr<Collective> coll, coll_grad;
     int world = 1, rank = 0, exact = 1;
-    bool dp() const { return coll != nullptr && world > 1 && !tuning; }
+    bool dp() const { return coll != nullptr && coll_grad != nullptr && !tuning; }
+    hipStream_t cst = nullptr;
+    std::vector<hipEvent_t> ev_bucket;  // per layer: the bucket closed after this layer's weight gradient
+    hipEvent_t ev_grads = nullptr;      // every bucket summed and ranged (the NITI_SGD join)
+    size_t bucket_min_bytes = size_t(8) << 20;
+    // the bucket a layer's gradient SUM rides in: layers (backward order) accumulate until the
+    // bucket holds bucket_min_bytes; closes_bucket[i] marks the layer whose weight gradient
+    // completes one (its first layer in memory order is bucket_lo[i])
+    std::vector<int> bucket_lo;
+    std::vector<char> closes_bucket;
+    void plan_buckets() {
+        const int nl = (int)L.size();
+        bucket_lo.assign(nl, 0);
+        closes_bucket.assign(nl, 0);
+        size_t acc = 0;
+        int hi = nl - 1;
+        for (int i = nl - 1; i >= 0; --i) {
+            acc += (size_t)L[i].w_elems() * 4;
+            if (acc >= bucket_min_bytes || i == 0) {
+                closes_bucket[i] = 1;
+                for (int j = i; j <= hi; ++j) bucket_lo[j] = i;
+                acc = 0;
+                hi = i - 1;
+            }
+        }
+    }
+    int ensure_comm_stream() {
+        if (cst) return NITI_NO_ERROR;
+        if (hipStreamCreateWithFlags(&cst, hipStreamNonBlocking) != hipSuccess) return NITI_NO_EXECUTION;
+        constexpr unsigned kFlags = hipEventDisableTiming | hipEventReleaseToDevice;
+        ev_bucket.assign(L.size(), nullptr);
+        for (auto& e : ev_bucket)
+            if (hipEventCreateWithFlags(&e, kFlags) != hipSuccess) return NITI_NO_EXECUTION;
+        if (hipEventCreateWithFlags(&ev_grads, kFlags) != hipSuccess) return NITI_NO_EXECUTION;
+        plan_buckets();
+        return NITI_NO_ERROR;
+    }
+    int sum_bucket(int hi_layer, hipStream_t wst);
     // input quantiser statistics {S1, S2, xmax, 255 - xmin} (niti_quant.hip)
     unsigned long long* qstats = nullptr;
     // Optional hipGraph replay of the single-device step: ~95 launches become one graph launch
@@ -456,17 +516,7 @@ struct Model {
     size_t ws_bytes_for(int op) const { return op == PLAN_WGRAD ? slab_w_bytes : slab_bytes; }
     int ensure_streams() {
         if (side) return NITI_NO_ERROR;
-        // NITI_DIAG_SIDE_PRIORITY (diagnostics): -1 high / 1 low priority for the weight-gradient stream
-        int prio = 0;
-        if (const char* f = getenv("NITI_DIAG_SIDE_PRIORITY")) prio = atoi(f);
-        int lo = 0, hi = 0;
-        (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
-        if (prio != 0) {
-            if (hipStreamCreateWithPriority(&side, hipStreamNonBlocking, prio < 0 ? hi : lo) != hipSuccess)
-                return NITI_NO_EXECUTION;
-        } else if (hipStreamCreateWithFlags(&side, hipStreamNonBlocking) != hipSuccess) {
-            return NITI_NO_EXECUTION;
-        }
+        if (hipStreamCreateWithFlags(&side, hipStreamNonBlocking) != hipSuccess) return NITI_NO_EXECUTION;
         // cross-stream hand-offs on one device need a device-scope release only (the default
         // system-scope fence writes back and invalidates the caches: ~7 us per record, measured)
         constexpr unsigned kFlags = hipEventDisableTiming | hipEventReleaseToDevice;
@@ -480,17 +530,21 @@ struct Model {
     // input quantiser (MnistUtils.cpp:83-93)
     int run(const int8_t* x_nchw, int exp_in, const uint8_t* images, const int32_t* labels, hipStream_t st);
     int step(const int8_t* x_nchw, int exp_in, const uint8_t* images, const int32_t* labels, hipStream_t st);
-    int reduce_wgrads(hipStream_t st);
     ~Model() {
         clear_probe();
         drop_graph();
+        if (cst) (void)hipStreamSynchronize(cst);
+        for (auto e : ev_bucket) (void)hipEventDestroy(e);
+        if (ev_grads) (void)hipEventDestroy(ev_grads);
         if (gin) (void)hipEventDestroy(gin);
         if (gout) (void)hipEventDestroy(gout);
         if (gstream) (void)hipStreamDestroy(gstream);
         for (auto e : ev_dy) (void)hipEventDestroy(e);
         if (ev_side) (void)hipEventDestroy(ev_side);
         if (side) (void)hipStreamDestroy(side);
+        coll_grad.reset();
         coll.reset();
+        if (cst) (void)hipStreamDestroy(cst);
     }
 };
 
@@ -595,7 +649,6 @@ int Model::build(int arch_, int batch_, int in_hw) {
     xp16_valid.assign(nl, 0);
     dp16.assign(nl, nullptr);
     dp16_valid.assign(nl, 0);
-    if (const char* e = getenv("NITI_P16_SEPARATE")) fuse_dp16 = atoi(e) == 0;
     for (int i = 0; i < nl; ++i) {
         Layer& l = L[i];
         const ConvGeom& g = l.g;
@@ -764,7 +817,7 @@ int Model::fwd_layer(int i, hipStream_t st) {
 }
 
 // One layer's weight gradient (the int32 gradient and, single device, its range; data
-// parallel, the SUM and the range follow in reduce_wgrads after the backward pass).
+// parallel, the SUM and the range follow on the comm stream in sum_bucket).
 int Model::wgrad_layer(int i, hipStream_t st) {
     const bool dp = this->dp();
     Layer& l = L[i];
@@ -799,17 +852,23 @@ int Model::wgrad_layer(int i, hipStream_t st) {
     return NITI_NO_ERROR;
 }
 
-// Data parallel: SUM every layer's int32 weight gradient over the ranks in one all-reduce of the
-// contiguous bucket (one bandwidth-bound call per step instead of one latency-paying call per
-// layer; no gradient can be requantised before its range is global anyway), then every layer's
-// range in one launch, on the step stream after the backward pass.
-int Model::reduce_wgrads(hipStream_t st) {
-    CTRY(coll->allreduce(grad_bucket, grad_bucket_elems, COLL_SUM_I32, st));
+// Data parallel: the bucket of layers [bucket_lo[hi], hi] (contiguous in grad_bucket) is complete
+// once layer bucket_lo[hi]'s weight gradient is in on `wst`: the comm stream waits for it, SUMs
+// the bucket's int32 gradients over the ranks and takes every layer's range of the summed
+// gradient (NITI_RangeEstimate over the global batch, NITI_GradientConv_Int8.cpp:274-296), while
+// the step stream goes on with the input-gradient chain.
+int Model::sum_bucket(int lo, hipStream_t wst) {
+    int hi = lo;
+    while (hi + 1 < (int)L.size() && bucket_lo[hi + 1] == lo) ++hi;
+    MTRY(hipEventRecord(ev_bucket[lo], wst));
+    MTRY(hipStreamWaitEvent(cst, ev_bucket[lo], 0));
+    size_t elems = 0;
+    for (int j = lo; j <= hi; ++j) elems += (size_t)L[j].w_elems();
+    CTRY(coll_grad->allreduce(L[lo].dwacc, elems, COLL_SUM_I32, cst));
     AbsmaxJob jobs[ABSMAX_MAX_JOBS];
-    const int nl = (int)L.size();
-    if (nl > ABSMAX_MAX_JOBS) return NITI_NOT_SUPPORT;
-    for (int i = 0; i < nl; ++i) jobs[i] = AbsmaxJob{L[i].dwacc, L[i].w_elems(), rng(i, 2), 0};
-    MTRY(absmax_many(jobs, nl, st));
+    if (hi - lo + 1 > ABSMAX_MAX_JOBS) return NITI_NOT_SUPPORT;
+    for (int j = lo; j <= hi; ++j) jobs[j - lo] = AbsmaxJob{L[j].dwacc, L[j].w_elems(), rng(j, 2), 0};
+    MTRY(absmax_many(jobs, hi - lo + 1, cst));
     return NITI_NO_ERROR;
 }
 
@@ -1014,6 +1073,10 @@ int Model::run(const int8_t* x_nchw, int exp_in, const uint8_t* images, const in
     const bool dp = this->dp();
     SgdJob jobs[SGD_MAX_JOBS];
     if (nl > SGD_MAX_JOBS) return NITI_NOT_SUPPORT;
+    if (dp) {
+        const int rc = ensure_comm_stream();
+        if (rc != NITI_NO_ERROR) return rc;
+    }
     invalidate_xp16();  // the forward pass rewrites every layer input
     MTRY(hipMemsetAsync(amax, 0, amax_bytes, st));
     if (x_nchw != nullptr) {
@@ -1060,6 +1123,8 @@ int Model::run(const int8_t* x_nchw, int exp_in, const uint8_t* images, const in
             if (rc != NITI_NO_ERROR) return rc;
         }
         int rc = wgrad_layer(i, wst);
+        // data parallel: a completed gradient bucket goes to the comm stream right away
+        if (rc == NITI_NO_ERROR && dp && closes_bucket[i]) rc = sum_bucket(i, wst);
         if (rc == NITI_NO_ERROR && i > 0) rc = dgrad_layer(i, st);
         if (rc != NITI_NO_ERROR) return rc;
         // NITI_SGD (NITI_SGD.hpp:20-54) for this layer is deferred: every layer's update runs
@@ -1069,13 +1134,12 @@ int Model::run(const int8_t* x_nchw, int exp_in, const uint8_t* images, const in
         jobs[i] = SgdJob{l.dwacc, rng(i, 2), RULE_WGRAD_BW2, g.c_out, g.c_in, g.kh * g.kw, g.cip, g.cop, l.w,
                          i > 0 ? l.wT : nullptr, l.g8};
     }
-    if (ov) {  // every weight gradient is in before the update
+    if (dp) {  // every bucket summed and ranged on the comm stream before the update
+        MTRY(hipEventRecord(ev_grads, cst));
+        MTRY(hipStreamWaitEvent(st, ev_grads, 0));
+    } else if (ov) {  // every weight gradient is in before the update
         MTRY(hipEventRecord(ev_side, side));
         MTRY(hipStreamWaitEvent(st, ev_side, 0));
-    }
-    if (dp) {  // the global batch's gradients: one SUM over the bucket, then every layer's range
-        const int rc = reduce_wgrads(st);
-        if (rc != NITI_NO_ERROR) return rc;
     }
     MTRY(sgd_update_many(jobs, nl, st));
     return NITI_NO_ERROR;
@@ -1283,10 +1347,11 @@ int niti_model_run_phase(niti_model_t m, int layer, int phase, void* stream) {
         return NITI_INVALID_VALUE;
     const bool t = m->m.tuning;
     m->m.tuning = false;  // keep the probe armed; collectives stay off (single-device phase)
-    std::unique_ptr<niti::Collective> c = std::move(m->m.coll);
+    std::unique_ptr<niti::Collective> c = std::move(m->m.coll), cg = std::move(m->m.coll_grad);
     hipStream_t st = (hipStream_t)stream;
     const int rc = phase == 0 ? m->m.fwd_layer(layer, st) : phase == 1 ? m->m.dgrad_layer(layer, st) : m->m.wgrad_layer(layer, st);
     m->m.coll = std::move(c);
+    m->m.coll_grad = std::move(cg);
     m->m.tuning = t;
     return rc;
 }
@@ -1434,8 +1499,14 @@ int niti_model_attach_comm(niti_model_t m, const char id[NITI_UNIQUE_ID_BYTES], 
     auto c = std::make_unique<niti::RcclCollective>();
     if (ncclCommInitRank(&c->comm, world, u, rank) != ncclSuccess) return NITI_NO_EXECUTION;
     c->world = world;
+    // the gradient communicator: split off the first (collective over the ranks), its own
+    // resources, so its SUMs and the ranges' MAXes are not serialised against each other
+    auto cg = std::make_unique<niti::RcclCollective>();
+    if (ncclCommSplit(c->comm, 0, rank, &cg->comm, nullptr) != ncclSuccess) return NITI_NO_EXECUTION;
+    cg->world = world;
     m->m.drop_graph();
     m->m.coll = std::move(c);
+    m->m.coll_grad = std::move(cg);
     m->m.world = world;
     m->m.rank = rank;
     m->m.exact = exact ? 1 : 0;
@@ -1466,8 +1537,14 @@ int niti_model_attach_local(niti_model_t m, niti_local_group_t g, int rank, int 
     auto c = std::make_unique<niti::LocalCollective>();
     c->g = g->g;
     c->rank = rank;
+    c->chan = 0;
+    auto cg = std::make_unique<niti::LocalCollective>();
+    cg->g = g->g;
+    cg->rank = rank;
+    cg->chan = 1;
     m->m.drop_graph();
     m->m.coll = std::move(c);
+    m->m.coll_grad = std::move(cg);
     m->m.world = g->g->world;
     m->m.rank = rank;
     m->m.exact = exact ? 1 : 0;

@@ -3,7 +3,7 @@
 // Reference (execution-engine/tools/train/source/demo/MnistUtils.cpp:83-93), per batch:
 //     cast  = float(images)                      uint8 pixels
 //     mean  = ReduceMean(cast)
-//     std   = sqrt(ReduceSum((cast - mean)^2) / count)
+//     std   = sqrt(ReduceSum((cast - mean)^2) / (batchSize * 28 * 28))   (:86, literally)
 //     Y     = (cast - mean) / std
 //     range = ReduceMax(|Y|)
 //     ascale = int8(ceil(ln(range)) - 7)          (natural log, as written)
@@ -14,7 +14,8 @@
 //     mean  = float(S1) / float(count)                       (= the float sequential sum while
 //                                                              S1 < 2^24, e.g. LeNet batch 64)
 //     ss    = double(S2) - 2 mean S1 + count mean^2           (double, no contraction)
-//     std   = sqrtf(float(ss / count))
+//     std   = sqrtf(float(ss / var_count))   var_count = images x 784, the reference's literal
+//                                              divisor for any image size (= count for MNIST)
 //     range = max(|float(xmax - mean)|, |float(xmin - mean)|) / std   (the max of |Y| sits at
 //             an extreme pixel: fl(x - mean) and fl(./std) are monotonic in x)
 // and the per-pixel formula is evaluated in float in the reference's operation order.  The
@@ -22,8 +23,10 @@
 // float-sequential restatement (niti_ref_quantize_input) agrees wherever the float sums are
 // exact.  Because the statistics are integers, data-parallel ranks all-reduce them (SUM S1, S2;
 // MAX xmax, 255 - xmin) and quantise their shard exactly as one device would the global batch.
-// A constant batch (std = 0) is undefined in the reference (0/0); here it quantises to zeros
-// with ascale = -7.
+// ascale is computed in float as the graph does (_Ceil(_Log(range)) on float tensors, :89-91),
+// logf taken as the correctly rounded float natural log, (float)log((double)range), so host and
+// device agree bit for bit.  A constant batch (std = 0) is undefined in the reference (0/0); here
+// it quantises to zeros with ascale = -7.
 #include "niti_kernels.hpp"
 #include "niti_map.hpp"
 
@@ -113,7 +116,7 @@ struct QuantParams {
 
 // The contract in the file header, evaluated without floating-point contraction so the host
 // oracle (gcc, x86-64: no FMA) computes the identical values.
-__device__ QuantParams quant_params(const unsigned long long* stats, int64_t count) {
+__device__ QuantParams quant_params(const unsigned long long* stats, int64_t count, int64_t var_count) {
 #pragma clang fp contract(off)
     QuantParams q;
     const double s1 = (double)stats[0], s2 = (double)stats[1];
@@ -121,7 +124,7 @@ __device__ QuantParams quant_params(const unsigned long long* stats, int64_t cou
     q.mean = (float)stats[0] / (float)count;
     const double m = (double)q.mean;
     const double ss = s2 - 2.0 * m * s1 + (double)count * m * m;
-    const float var = (float)(ss / (double)count);
+    const float var = (float)(ss / (double)var_count);
     q.sd = sqrtf(var > 0.f ? var : 0.f);
     q.ok = q.sd > 0.f;
     if (!q.ok) {
@@ -131,7 +134,7 @@ __device__ QuantParams quant_params(const unsigned long long* stats, int64_t cou
     }
     const float hi = fabsf(xmax - q.mean) / q.sd, lo = fabsf(xmin - q.mean) / q.sd;
     q.range = hi > lo ? hi : lo;
-    q.ascale = (int)(int8_t)(int)(ceil(log((double)q.range)) - 7.0);
+    q.ascale = (int)(int8_t)(int)(ceilf((float)log((double)q.range)) - 7.0f);
     return q;
 }
 
@@ -149,11 +152,11 @@ __device__ __forceinline__ int8_t quant_pixel(uint32_t p, const QuantParams& q) 
 template <bool NHWC>
 __global__ void __launch_bounds__(256) image_quant_kernel(const uint8_t* __restrict__ img, int n, int c, int hw,
                                                           int cp, const unsigned long long* __restrict__ stats,
-                                                          int64_t count, int8_t* __restrict__ out,
-                                                          int8_t* __restrict__ ascale) {
+                                                          int64_t count, int64_t var_count,
+                                                          int8_t* __restrict__ out, int8_t* __restrict__ ascale) {
     __shared__ QuantParams sq;
     if (threadIdx.x == 0) {
-        sq = quant_params(stats, count);
+        sq = quant_params(stats, count, var_count);
         if (blockIdx.x == 0 && ascale != nullptr) *ascale = (int8_t)sq.ascale;
     }
     __syncthreads();
@@ -202,14 +205,16 @@ hipError_t image_quantize(const uint8_t* img, int n, int c, int hw, int cp, cons
     if (n <= 0 || c <= 0 || hw <= 0 || count <= 0 || (nhwc16 && cp < c)) return hipErrorInvalidValue;
     if (nhwc16 && cp % 16 != 0) return hipErrorInvalidValue;
     const int64_t total = nhwc16 ? (int64_t)n * hw : (int64_t)n * c * hw;
+    // MnistUtils.cpp:86: the variance over batchSize * 28 * 28, batchSize = the images `count` covers
+    const int64_t var_count = count / ((int64_t)c * hw) * 784;
     int64_t blocks = (total + 255) / 256;
     blocks = blocks > 512 ? 512 : blocks;
     if (nhwc16)
         hipLaunchKernelGGL(image_quant_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, st, img, n, c, hw, cp,
-                           stats, count, out, ascale);
+                           stats, count, var_count, out, ascale);
     else
         hipLaunchKernelGGL(image_quant_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, st, img, n, c, hw, cp,
-                           stats, count, out, ascale);
+                           stats, count, var_count, out, ascale);
     return hipGetLastError();
 }
 

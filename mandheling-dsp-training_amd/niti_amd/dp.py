@@ -56,17 +56,23 @@ class ThreadComm:
         self._slots[r] = t
         self._bar.wait()
         if r == 0:
-            ts = self._slots
-            if any(x.shape != ts[0].shape or x.dtype != ts[0].dtype for x in ts):
-                raise ValueError("ranks disagree on the collective's tensor")
-            acc = ts[0].clone()
-            for x in ts[1:]:
-                if op == "max":
-                    torch.maximum(acc, x, out=acc)
-                else:
-                    acc.add_(x)
-            for x in ts:
-                x.copy_(acc)
+            try:
+                ts = self._slots
+                if any(x.shape != ts[0].shape or x.dtype != ts[0].dtype for x in ts):
+                    raise ValueError("ranks disagree on the collective's tensor")
+                acc = ts[0].clone()
+                for x in ts[1:]:
+                    if op == "max":
+                        torch.maximum(acc, x, out=acc)
+                    else:
+                        acc.add_(x)
+                for x in ts:
+                    x.copy_(acc)
+            except BaseException:
+                # release the peers at once (BrokenBarrierError) instead of after the timeout,
+                # and surface the real error on this rank
+                self._bar.abort()
+                raise
         self._bar.wait()
         self._slots[r] = None
 

@@ -272,4 +272,11 @@ class ResNet18:
         return out
 
     def step_macs(self) -> int:
-        return sum(self.batch * l["oh"] * l["oh"] * l["co"] * l["ci"] * l["k"] * l["k"] for l in self.convs)
+        """MACs of one step, counted as the VGG driver counts them (niti_model_step_macs): every
+        layer's forward and weight gradient, and the input gradient of every layer but the stem
+        (train_step never computes the stem's, as the lazy reference graph skips conv1's)."""
+        s = 0
+        for i, l in enumerate(self.convs):
+            f = self.batch * l["oh"] * l["oh"] * l["co"] * l["ci"] * l["k"] * l["k"]
+            s += 2 * f + (f if i > 0 else 0)
+        return s

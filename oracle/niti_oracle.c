@@ -805,20 +805,23 @@ void niti_ref_sgd_update(int8_t* w, const int8_t* g, int64_t n) {
     for (int64_t i = 0; i < n; ++i) w[i] = (int8_t)niti_ref_int8_clip((int32_t)w[i] - (int32_t)g[i]);
 }
 
-/* MnistUtils.cpp:83-93 (float math in the order the expression graph states it) */
-int32_t niti_ref_quantize_input(const float* x, int64_t n, int8_t* out) {
+/* MnistUtils.cpp:83-93 (float math in the order the expression graph states it).  The variance
+ * divisor is the reference's literal `batchSize * 28 * 28` (:86): var_n = images * 784 whatever the
+ * image size (for MNIST it equals the pixel count); the mean is ReduceMean over all n values.
+ * _Log on a float is taken as the correctly rounded float natural log, (float)log((double)r). */
+int32_t niti_ref_quantize_input(const float* x, int64_t n, int64_t var_n, int8_t* out) {
     float sum = 0.f;
     for (int64_t i = 0; i < n; ++i) sum += x[i];
     const float mean = sum / (float)n;
     float ss = 0.f;
     for (int64_t i = 0; i < n; ++i) ss += (x[i] - mean) * (x[i] - mean);
-    const float sd = sqrtf(ss / (float)n);
+    const float sd = sqrtf(ss / (float)var_n);
     float range = 0.f;
     for (int64_t i = 0; i < n; ++i) {
         const float y = fabsf((x[i] - mean) / sd);
         if (y > range) range = y;
     }
-    const float bw = ceilf(logf(range));
+    const float bw = ceilf((float)log((double)range));
     for (int64_t i = 0; i < n; ++i) out[i] = (int8_t)roundf((x[i] - mean) / sd / range * 127.0f);
     return (int32_t)(int8_t)(bw - 7.0f);
 }
@@ -828,8 +831,12 @@ int32_t niti_ref_quantize_input(const float* x, int64_t n, int8_t* out) {
  * contract the device implements, mandheling-dsp-training_amd/csrc/niti_quant.hip):
  *   S1 = sum p, S2 = sum p^2, xmin, xmax over `count` pixels (stats[] = {S1, S2, xmax, 255-xmin})
  *   mean = float(S1) / float(count); ss = S2 - 2 mean S1 + count mean^2 (double, this order);
- *   sd = sqrtf(float(ss / count)); range = max(|xmax - mean|, |xmin - mean|) / sd (float);
- *   x = (int8) roundf(((p - mean) / sd) / range * 127); ascale = int8(ceil(log(range)) - 7).
+ *   sd = sqrtf(float(ss / var_count)), var_count = the reference's literal divisor
+ *   `batchSize * 28 * 28` (MnistUtils.cpp:86: global images x 784 for any image size; equal to
+ *   count for MNIST); range = max(|xmax - mean|, |xmin - mean|) / sd (float);
+ *   x = (int8) roundf(((p - mean) / sd) / range * 127);
+ *   ascale = int8(ceilf(logf(range)) - 7) in float as the graph computes it (_Ceil(_Log(range)),
+ *   :89-91), logf taken as the correctly rounded float log, (float)log((double)range).
  * std == 0 (a constant batch, 0/0 in the reference): x = 0, ascale = -7.
  * This file is compiled without FMA contraction (x86-64 baseline, -ffp-contract=off). */
 void niti_ref_image_stats(const uint8_t* img, int64_t n, uint64_t stats[4]) {
@@ -848,7 +855,8 @@ void niti_ref_image_stats(const uint8_t* img, int64_t n, uint64_t stats[4]) {
     stats[3] = 255u - mn;
 }
 
-int32_t niti_ref_image_quantize(const uint8_t* img, int64_t n, const uint64_t stats[4], int64_t count, int8_t* out) {
+int32_t niti_ref_image_quantize(const uint8_t* img, int64_t n, const uint64_t stats[4], int64_t count,
+                                int64_t var_count, int8_t* out) {
     const double s1 = (double)stats[0], s2 = (double)stats[1];
     const float xmax = (float)stats[2], xmin = (float)(255u - stats[3]);
     const float mean = (float)stats[0] / (float)count;
@@ -858,7 +866,7 @@ int32_t niti_ref_image_quantize(const uint8_t* img, int64_t n, const uint64_t st
     const double c = (double)count * m;
     const double d = c * m;
     const double ss = (s2 - b) + d;
-    const float var = (float)(ss / (double)count);
+    const float var = (float)(ss / (double)var_count);
     const float sd = sqrtf(var > 0.f ? var : 0.f);
     if (!(sd > 0.f)) {
         memset(out, 0, (size_t)n);
@@ -870,7 +878,7 @@ int32_t niti_ref_image_quantize(const uint8_t* img, int64_t n, const uint64_t st
         const float y = ((float)img[i] - mean) / sd;
         out[i] = (int8_t)(int)roundf(y / range * 127.0f);
     }
-    return (int32_t)(int8_t)(int)(ceil(log((double)range)) - 7.0);
+    return (int32_t)(int8_t)(int)(ceilf((float)log((double)range)) - 7.0f);
 }
 
 /* ---------------------------------------------------------------------------- */

@@ -84,10 +84,10 @@ def _declare(L):
         "niti_ref_maxpool_grad": (None, [vp, vp, vp] + [C.c_int] * 9 + [vp]),
         "niti_ref_loss_grad": (None, [vp, C.c_int, C.c_int, i32, vp, C.c_int, vp]),
         "niti_ref_sgd_update": (None, [vp, vp, i64]),
-        "niti_ref_quantize_input": (i32, [vp, i64, vp]),
+        "niti_ref_quantize_input": (i32, [vp, i64, i64, vp]),
         "niti_ref_image_stats": (None, [vp, i64, vp]),
         "niti_ref_set_threads": (None, [C.c_int]),
-        "niti_ref_image_quantize": (i32, [vp, i64, vp, i64, vp]),
+        "niti_ref_image_quantize": (i32, [vp, i64, vp, i64, i64, vp]),
         "niti_ref_layer_step": (C.c_int, [gp, vp, vp, vp, vp, vp, vp, C.c_int, C.c_int]),
     }
     for name, (res, args) in sig.items():
@@ -341,10 +341,14 @@ def sgd_update(w, g):
     return w
 
 
+MNIST_VAR_PIXELS = 28 * 28  # MnistUtils.cpp:86 divides the variance by batchSize * 28 * 28, literally
+
+
 def quantize_input(x):
+    """x float [n][...]: the float-sequential restatement of MnistUtils.cpp:83-93."""
     x = _c(x, np.float32)
     out = np.empty(x.shape, np.int8)
-    a = lib().niti_ref_quantize_input(_p(x), x.size, _p(out))
+    a = lib().niti_ref_quantize_input(_p(x), x.size, x.shape[0] * MNIST_VAR_PIXELS, _p(out))
     return out, int(a)
 
 
@@ -358,11 +362,16 @@ def image_stats(images):
 
 def quantize_images(images, stats=None, count=None):
     """MnistUtils.cpp:83-93 over exact integer statistics: (x int8 same shape, ascale).  stats /
-    count default to this batch's own (data-parallel ranks pass the global ones)."""
+    count default to this batch's own (data-parallel ranks pass the global ones).  The variance
+    divisor is the reference's literal batchSize * 28 * 28 for the global batch (count / image
+    pixels images), whatever the image size."""
     img = _c(images, np.uint8)
     st = image_stats(img) if stats is None else np.ascontiguousarray(stats, np.uint64)
     out = np.empty(img.shape, np.int8)
-    a = lib().niti_ref_image_quantize(_p(img), img.size, _p(st), int(count or img.size), _p(out))
+    count = int(count or img.size)
+    per_image = int(np.prod(img.shape[1:]))
+    var_count = (count // per_image) * MNIST_VAR_PIXELS
+    a = lib().niti_ref_image_quantize(_p(img), img.size, _p(st), count, var_count, _p(out))
     return out, int(a)
 
 

@@ -77,10 +77,13 @@ def test_no_fallback_when_library_missing(tmp_path, monkeypatch):
     importlib.reload(_lib)
 
 
-def test_wgrad_p16_no_inflight_register_reuse(tmp_path):
-    """The P16 weight-gradient kernel issues its operand loads from inline asm (hipcc does not count
-    them): no instruction may touch a register such a load is still writing.  Compiles
-    niti_wgrad.hip to gfx950 assembly and scans it (tools/isa_inflight.py)."""
+@pytest.mark.parametrize("unit", ["niti_wgrad", "niti_kernels"])
+def test_asm_ring_kernels_no_inflight_register_reuse(tmp_path, unit):
+    """Kernels with inline-asm load rings count their own waits (hipcc does not know when such a
+    load lands): no instruction may touch a register such a load is still writing.  Compiles the
+    translation unit to gfx950 assembly and scans every asm-ring kernel in it (the P16 weight
+    gradient's buffer_load ring; the GEMM, tap-sharing and first-layer kernels' ds_read fragment
+    rings) with tools/isa_inflight.py."""
     import os
     import shutil
     import subprocess
@@ -89,10 +92,11 @@ def test_wgrad_p16_no_inflight_register_reuse(tmp_path):
     if not os.path.exists(hipcc):
         pytest.skip("no hipcc")
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    src = os.path.join(root, "mandheling-dsp-training_amd", "csrc", "niti_wgrad.hip")
-    asm = tmp_path / "niti_wgrad.s"
+    src = os.path.join(root, "mandheling-dsp-training_amd", "csrc", unit + ".hip")
+    asm = tmp_path / (unit + ".s")
     subprocess.run([hipcc, "--offload-arch=gfx950", "--cuda-device-only", "-O3", "-std=c++20", "-S", src, "-o",
-                    str(asm)], check=True)
+                    str(asm)], check=True, capture_output=True)
     r = subprocess.run([sys.executable, os.path.join(root, "tools", "isa_inflight.py"), str(asm)],
                        capture_output=True, text=True)
     assert r.returncode == 0, r.stdout
+    assert " 0 asm-ring kernels" not in r.stdout, r.stdout

@@ -73,3 +73,27 @@ def test_thread_comm_cpu():
         assert ts[r].tolist() == [2, 10, 5] and us[r].tolist() == [3, -3]
     with pytest.raises(ValueError):
         comm.rank(world)
+
+
+def test_thread_comm_mismatch_fails_fast():
+    """A shape mismatch raised by rank 0's reduction aborts the barrier: the peers fail at once
+    (BrokenBarrierError) instead of waiting out the timeout, and rank 0 surfaces the ValueError."""
+    import time
+    from niti_amd.dp import ThreadComm
+    comm = ThreadComm(2, timeout=60.0)
+    errs = {}
+
+    def run(r):
+        try:
+            comm.rank(r).all_sum(torch.zeros(2 + r, dtype=torch.int32))
+        except BaseException as e:  # noqa: BLE001
+            errs[r] = e
+
+    t0 = time.monotonic()
+    th = [threading.Thread(target=run, args=(r,)) for r in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(30)
+    assert time.monotonic() - t0 < 10
+    assert isinstance(errs[0], ValueError) and isinstance(errs[1], threading.BrokenBarrierError)

@@ -2,10 +2,11 @@
 
 `world` models of batch b, each driven by its own host thread on its own HIP stream and
 attached to an in-process rank group (niti_model_attach_local): the step runs the exact calls,
-order and streams of the RCCL path (one communicator, every collective on the step stream: the
-quantiser statistics SUM/MAX, every forward / input-gradient range MAX, every int32
-weight-gradient SUM one layer behind on the step stream while the weight-gradient GEMMs run on
-the side stream), with a transport that reduces on the same device.  Exact mode must make every
+order and streams of the RCCL path (two communicators: the quantiser statistics SUM/MAX and every
+forward / input-gradient range MAX on the step stream; the int32 weight-gradient SUM of every
+gradient bucket on the comm stream as soon as its weight gradients are in, followed there by the
+bucket's ranges, joined by the step stream before NITI_SGD), with a transport that reduces on
+the same device.  Exact mode must make every
 rank bit-identical to ONE model stepping the concatenated batch of world * b images: same
 weights, and each rank's activations / gradients equal its slice of the full batch's.
 """

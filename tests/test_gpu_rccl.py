@@ -1,9 +1,15 @@
-"""The product's RCCL data-parallel path across real GPUs (niti_model_attach_comm, one process
-per GPU, exact mode): runs only where torch sees >= 2 devices (skipped on one-GPU boxes; the
-in-process transport of tests/test_dp_local.py covers the same protocol there).  Each rank steps
-its slice of the batch through the C++ model with the RCCL communicator, overlap on and off;
-rank 0 also steps the whole batch on its own device and every rank's weights and logits must
-equal that run bit for bit."""
+"""The product's RCCL data-parallel path (niti_model_attach_comm, one process per GPU, exact mode).
+
+World 1, one GPU (runs on every GPU box): the model attaches a one-rank RCCL communicator, so
+every collective call site of the step runs on the hardware -- the two communicators (ranges on
+the step stream, the gradient buckets split off with ncclCommSplit on the comm stream), the
+bucket events, the per-bucket range launches and the NITI_SGD join -- and the result must equal
+the model without a communicator bit for bit.
+
+World 2 (only where torch sees >= 2 devices; the in-process transport of tests/test_dp_local.py
+covers the multi-rank protocol on one GPU): each rank steps its slice of the batch through the
+C++ model with the RCCL communicators, overlap on and off; rank 0 also steps the whole batch on
+its own device and every rank's weights and logits must equal that run bit for bit."""
 import os
 import socket
 import sys
@@ -65,6 +71,43 @@ def _rank(rank, world, port, overlap, q):
         q.put((rank, out))
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("arch,overlap", [("vgg11", False), ("vgg11", True), ("vgg16", False)])
+def test_rccl_world1_equals_no_comm(arch, overlap):
+    if _n_devices() < 1:
+        pytest.skip("no GPU")
+    import torch
+    sys.path.insert(0, os.path.join(ROOT, "mandheling-dsp-training_amd"))
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+    import niti_amd
+    import niti_model_ref as R
+    from niti_amd.model import NitiModel
+    a_id = niti_amd.ARCH_VGG11 if arch == "vgg11" else niti_amd.ARCH_VGG16
+    layers = R.vgg11_layers() if arch == "vgg11" else R.vgg16_layers(32)
+    W, S = R.init_weights(layers, seed=23)
+    b = 8 if arch == "vgg11" else 4
+    rng = np.random.default_rng(5)
+    imgs = rng.integers(0, 256, (2, b, 3, 32, 32)).astype(np.uint8)
+    labs = rng.integers(0, 10, (2, b)).astype(np.int32)
+    runs = []
+    for comm in (True, False):
+        m = NitiModel(a_id, b, 32 if arch == "vgg16" else 0)
+        if comm:
+            m.attach_comm(NitiModel.unique_id(), 0, 1, exact=True)
+        m.set_overlap(overlap)
+        for i, (w, s) in enumerate(zip(W, S)):
+            m.set_weight(i, w, s)
+        for step in range(2):
+            m.train_step_images(torch.from_numpy(imgs[step]).cuda(), torch.from_numpy(labs[step]).cuda())
+        torch.cuda.synchronize()
+        runs.append(([m.get_weight(i) for i in range(len(layers))], m.logits()))
+        del m
+    (wc, (lc, ec)), (wn, (ln, en)) = runs
+    assert ec == en and np.array_equal(lc, ln)
+    for i in range(len(layers)):
+        assert np.array_equal(wc[i], wn[i]), i
 
 
 @pytest.mark.skipif(_n_devices() < 2, reason="needs >= 2 GPUs (one rank per GPU over RCCL)")

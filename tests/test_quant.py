@@ -13,10 +13,18 @@ import niti_oracle as O
 
 
 def test_quant_known_answer():
-    # pixels {0, 255}: mean 127.5, std 127.5, Y = -1 / +1, range 1 -> x = -127 / 127, ascale = ceil(ln 1) - 7
-    img = np.array([[[[0, 255], [255, 0]]]], np.uint8)
+    # an MNIST-shaped image of pixels {0, 255}: mean 127.5, std 127.5 (the literal divisor
+    # batchSize * 28 * 28 is the pixel count), Y = -1 / +1, range 1 -> x = -127 / 127,
+    # ascale = ceil(ln 1) - 7
+    img = (np.indices((1, 1, 28, 28)).sum(0) % 2 * 255).astype(np.uint8)
     x, a = O.quantize_images(img)
     assert a == -7
+    assert np.array_equal(x, np.where(img > 0, 127, -127).astype(np.int8))
+    # not MNIST-shaped: MnistUtils.cpp:86 still divides the squared deviations by batchSize * 28 * 28,
+    # so for a 2x2 image std = sqrt(4 * 127.5^2 / 784) = 127.5 / 14, range = 14, ascale = ceil(ln 14) - 7
+    img = np.array([[[[0, 255], [255, 0]]]], np.uint8)
+    x, a = O.quantize_images(img)
+    assert a == -4
     assert x.tolist() == [[[[-127, 127], [127, -127]]]]
     st = O.image_stats(img)
     assert st.tolist() == [510, 2 * 255 * 255, 255, 255]
