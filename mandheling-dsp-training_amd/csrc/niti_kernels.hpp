@@ -193,6 +193,33 @@ hipError_t conv_dgrad_phase1(const ConvGeom& g, const int8_t* dy, const int8_t* 
 hipError_t conv_dgrad_phase2(const ConvGeom& g, const int8_t* dy, const int8_t* wt, const int32_t* acc,
                              const uint32_t* amax, const ActOut& o, size_t ws_bytes, hipStream_t st);
 
+// ---- forward conv of stride-1 pad-1 3x3 layers with the rescale fused (niti_rowconv.hip) -------
+// Activations in C32 [n][ceil(C/32)][H][W][32], weights in WF [Co/32][Ci/32][9][2][32][16] (a 1 KiB
+// MFMA fragment per (co block, ci block, tap)).  Square H = W in {2, 4, 8, 16}, Cop % 32 == 0.
+struct RowConvOut {
+    int8_t* out = nullptr;       // NHWC16 [n][H][W][cop] (relu'd)
+    int8_t* pool_out = nullptr;  // NHWC16 [n][H/2][W/2][cop] 2x2 max pool of out
+    int8_t* next = nullptr;      // C32 copy of the next layer's input (pooled when pool_out)
+    const int8_t* exp_in = nullptr;
+    const int8_t* wscale = nullptr;
+    int8_t* exp_out = nullptr;
+    int relu = 0;
+};
+constexpr int ROWCONV_BAR_WORDS = 2 * 19 * 32;  // grid-barrier state of one layer (both parities)
+bool rowconv_ok(const ConvGeom& g);
+// FUSED (one launch, in-kernel grid barrier) possible: one unit per wave, every workgroup resident
+bool rowconv_fused_ok(const ConvGeom& g);
+int rowconv_units(const ConvGeom& g);
+size_t rowconv_wf_bytes(int co, int ci);
+hipError_t nhwc16_to_c32(const int8_t* in, int n, int hw, int cp, int c, int8_t* out, hipStream_t st);
+// OHWI16 [co][9][cip] -> WF; transpose: the input-gradient conv's WF (rotate180, ci <-> co)
+hipError_t weights_to_wf(const int8_t* w_ohwi16, int co, int ci, int cip, bool transpose, int8_t* out,
+                         hipStream_t st);
+// mode 0 FUSED (bar, err, epoch != 0 required; epoch + 1 per launch), 1 RANGE (max|y| into amax),
+// 2 REQUANT (recompute with the max in amax, requantise, store)
+hipError_t rowconv_fwd(const ConvGeom& g, const int8_t* x_c32, const int8_t* wf, const RowConvOut& o, int mode,
+                       uint32_t* amax, uint32_t* bar, uint32_t epoch, uint32_t* err, hipStream_t st);
+
 // ---- range estimate + requantisation ----------------------------------------------------
 hipError_t absmax_i32(const int32_t* a, int64_t n, uint32_t* amax, hipStream_t st);
 // max|a| of several int32 ranges in one launch (b0 is filled in by absmax_many)

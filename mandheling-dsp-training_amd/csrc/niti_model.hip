@@ -287,6 +287,13 @@ struct Layer {
     int col = 0;
     ConvGeom og{};
     int8_t* xcol = nullptr;
+    // stride-1 pad-1 3x3 layers on the register-fed forward with the fused rescale
+    // (niti_rowconv.hip): its C32 input copy, fragment-major weights, grid-barrier state
+    int rc = 0;
+    int8_t* xc32 = nullptr;
+    int8_t* wf = nullptr;
+    uint32_t* bar = nullptr;
+    uint32_t epoch = 0;
     int64_t w_elems() const { return (int64_t)g.c_out * g.kh * g.kw * g.cip; }
     int64_t macs() const { return (int64_t)og.n * og.oh * og.ow * og.c_out * og.c_in * og.kh * og.kw; }
 };
@@ -313,6 +320,19 @@ struct Model {
     std::vector<char> xp16_valid;  // xp16[i] holds L[i].in as it is now (cleared when a step starts)
     void invalidate_xp16() { std::fill(xp16_valid.begin(), xp16_valid.end(), 0); }
     bool fuse_dp16 = true;    // dy's P16 copy written by the requantisation that produces dy
+    // register-fed forward (niti_rowconv.hip) for the layers it takes; xc32_valid[i]: L[i].xc32
+    // holds L[i].in as it is now (written by the previous layer's epilogue, else converted)
+    bool use_rowconv = true;
+    std::vector<char> xc32_valid;
+    uint32_t* rc_err = nullptr;
+    bool rowconv_layer(int i) const { return use_rowconv && L[i].rc; }
+    // refresh every rowconv layer's fragment-major weights from w (after set_weight / NITI_SGD)
+    int refresh_wf(hipStream_t st) {
+        for (Layer& l : L)
+            if (l.rc && weights_to_wf(l.w, l.g.c_out, l.g.c_in, l.g.cip, false, l.wf, st) != hipSuccess)
+                return NITI_NO_EXECUTION;
+        return NITI_NO_ERROR;
+    }
     int convert_p16_inputs(hipStream_t st) {
         P16Conv jobs[P16_MAX_JOBS];
         int n = 0;
@@ -649,6 +669,9 @@ int Model::build(int arch_, int batch_, int in_hw) {
     xp16_valid.assign(nl, 0);
     dp16.assign(nl, nullptr);
     dp16_valid.assign(nl, 0);
+    xc32_valid.assign(nl, 0);
+    rc_err = (uint32_t*)ws.alloc(64);
+    if (!rc_err || hipMemset(rc_err, 0, 64) != hipSuccess) return NITI_OUT_OF_MEMORY;
     for (int i = 0; i < nl; ++i) {
         Layer& l = L[i];
         const ConvGeom& g = l.g;
@@ -680,6 +703,16 @@ int Model::build(int arch_, int batch_, int in_hw) {
         slab_bytes = std::max(slab_bytes, conv_fwd_workspace(g));
         slab_bytes = std::max(slab_bytes, conv_dgrad_workspace(g));
         slab_w_bytes = std::max(slab_w_bytes, conv_wgrad_workspace(g));
+        if (!l.col && rowconv_ok(g)) {
+            l.rc = 1;
+            l.wf = (int8_t*)ws.alloc(rowconv_wf_bytes(g.c_out, g.c_in));
+            l.xc32 = (int8_t*)ws.alloc((size_t)n * round_up(g.c_in, 32) * g.h * g.w);
+            l.bar = (uint32_t*)ws.alloc(ROWCONV_BAR_WORDS * 4);
+            if (!l.wf || !l.xc32 || !l.bar) return NITI_OUT_OF_MEMORY;
+            if (hipMemset(l.bar, 0, ROWCONV_BAR_WORDS * 4) != hipSuccess ||
+                hipMemset(l.wf, 0, rowconv_wf_bytes(g.c_out, g.c_in)) != hipSuccess)
+                return NITI_NO_EXECUTION;
+        }
         if (conv_wgrad_p16_ok(g)) {
             slab_w_bytes = std::max(slab_w_bytes, conv_wgrad_p16_workspace(g, 8));
             xp16[i] = (int8_t*)ws.alloc((size_t)n * g.h * g.w * g.cip);
@@ -789,6 +822,38 @@ int Model::fwd_layer(int i, hipStream_t st) {
         if (dp && exact) CTRY(coll->allreduce(rng(i, 0), MAX_WORDS, COLL_MAX_U32, st));
         MTRY(conv0_fwd(g, l.in, l.w, rng(i, 0), o, 1, st));
         probe(i, 0, false, st);
+        return NITI_NO_ERROR;
+    }
+    if (rowconv_layer(i)) {
+        // register-fed forward, rescale fused: one launch with an in-kernel grid barrier (single
+        // device, every workgroup resident, not inside a graph capture), else a range launch,
+        // [all-reduce MAX], and a recompute-and-requantise launch
+        if (!xc32_valid[i]) {
+            MTRY(nhwc16_to_c32(l.in, n, g.h * g.w, g.cip, g.c_in, l.xc32, st));
+            xc32_valid[i] = 1;
+        }
+        RowConvOut o;
+        o.out = l.r;
+        o.pool_out = l.pool ? l.p : nullptr;
+        const bool feeds_next = i + 1 < (int)L.size() && rowconv_layer(i + 1) && !l.flatten;
+        o.next = feeds_next ? L[i + 1].xc32 : nullptr;
+        o.exp_in = i == 0 ? exp0 : L[i - 1].exp;
+        o.wscale = l.ws_dev;
+        o.exp_out = l.exp;
+        o.relu = l.relu;
+        if (!dp && !capturing && rowconv_fused_ok(g)) {
+            MTRY(rowconv_fwd(g, l.xc32, l.wf, o, 0, rng(i, 0), l.bar, ++l.epoch, rc_err, st));
+        } else {
+            MTRY(rowconv_fwd(g, l.xc32, l.wf, o, 1, rng(i, 0), nullptr, 0, nullptr, st));
+            if (dp && exact) CTRY(coll->allreduce(rng(i, 0), MAX_WORDS, COLL_MAX_U32, st));
+            MTRY(rowconv_fwd(g, l.xc32, l.wf, o, 2, rng(i, 0), nullptr, 0, nullptr, st));
+        }
+        if (feeds_next) xc32_valid[i + 1] = 1;
+        probe(i, 0, false, st);
+        if (l.flatten) {
+            const int fc = g.c_out * l.ph * l.pw, ld = round_up(fc, 16);
+            MTRY(launch_map((int64_t)n * ld, FlattenFwd{l.p, l.ph * l.pw, g.c_out, g.cop, ld, l.flat}, st));
+        }
         return NITI_NO_ERROR;
     }
     MTRY(conv_fwd_phase1(g, l.in, l.w, acc, rng(i, 0), slab, slab_bytes, st));
@@ -978,6 +1043,7 @@ int Model::autotune(hipStream_t st, int reps) {
     for (int i = 0; i < nl && rc == NITI_NO_ERROR; ++i) {
         for (int op : {PLAN_FWD, PLAN_WGRAD, PLAN_DGRAD}) {
             if (op == PLAN_DGRAD && i == 0) continue;
+            if (op == PLAN_FWD && rowconv_layer(i)) continue;  // no GEMM plan: the register-fed forward
             const ConvGeom& g = L[i].g;
             const PlanKey key = conv_plan_key(op, g);
             const int k_step = conv_plan_k_step(op, g);
@@ -1078,6 +1144,7 @@ int Model::run(const int8_t* x_nchw, int exp_in, const uint8_t* images, const in
         if (rc != NITI_NO_ERROR) return rc;
     }
     invalidate_xp16();  // the forward pass rewrites every layer input
+    std::fill(xc32_valid.begin(), xc32_valid.end(), 0);
     MTRY(hipMemsetAsync(amax, 0, amax_bytes, st));
     if (x_nchw != nullptr) {
         MTRY(hipMemsetAsync(exp0, exp_in, 1, st));
@@ -1142,7 +1209,7 @@ int Model::run(const int8_t* x_nchw, int exp_in, const uint8_t* images, const in
         MTRY(hipStreamWaitEvent(st, ev_side, 0));
     }
     MTRY(sgd_update_many(jobs, nl, st));
-    return NITI_NO_ERROR;
+    return refresh_wf(st);
 }
 
 }  // namespace niti
@@ -1210,7 +1277,9 @@ int niti_model_set_weight(niti_model_t m, int layer, const int8_t* w_host, int w
     if (hipMemcpy(tmp, w_host, n, hipMemcpyHostToDevice) != hipSuccess ||
         niti::oihw_to_ohwi16(tmp, l.g.c_out, l.g.c_in, l.g.kh * l.g.kw, l.g.cip, l.w, nullptr) != hipSuccess ||
         niti::oihw_to_ihwo16(tmp, l.g.c_out, l.g.c_in, l.g.kh * l.g.kw, l.g.cop, l.wT, nullptr) != hipSuccess ||
-        hipMemset(l.ws_dev, (int)(int8_t)wscale, 1) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+        hipMemset(l.ws_dev, (int)(int8_t)wscale, 1) != hipSuccess ||
+        (l.rc && niti::weights_to_wf(l.w, l.g.c_out, l.g.c_in, l.g.cip, false, l.wf, nullptr) != hipSuccess) ||
+        hipDeviceSynchronize() != hipSuccess)
         rc = NITI_NO_EXECUTION;
     l.wscale = (int8_t)wscale;
     (void)hipFree(tmp);
@@ -1328,6 +1397,21 @@ int niti_model_set_overlap(niti_model_t m, int enable) {
     if (!m) return NITI_INVALID_VALUE;
     m->m.overlap = enable != 0;
     return NITI_NO_ERROR;
+}
+
+int niti_model_set_rowconv(niti_model_t m, int enable) {
+    if (!m) return NITI_INVALID_VALUE;
+    m->m.use_rowconv = enable != 0;
+    m->m.drop_graph();
+    return NITI_NO_ERROR;
+}
+
+int niti_model_rowconv_error(niti_model_t m) {
+    if (!m) return NITI_INVALID_VALUE;
+    uint32_t e = 0;
+    if (hipDeviceSynchronize() != hipSuccess || hipMemcpy(&e, m->m.rc_err, 4, hipMemcpyDeviceToHost) != hipSuccess)
+        return NITI_NO_EXECUTION;
+    return (int)e;
 }
 
 int niti_model_set_graph(niti_model_t m, int enable) {

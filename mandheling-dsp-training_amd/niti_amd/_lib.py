@@ -154,6 +154,8 @@ def lib():
         "niti_model_get_tap": (ci, [vp, ci, ci, vp, C.c_size_t, vp]),
         "niti_model_step_macs": (i64, [vp]),
         "niti_model_set_graph": (ci, [vp, ci]),
+        "niti_model_set_rowconv": (ci, [vp, ci]),
+        "niti_model_rowconv_error": (ci, [vp]),
         "niti_model_autotune": (ci, [vp, ci, vp]),
         "niti_model_set_overlap": (ci, [vp, ci]),
         "niti_model_plan_info": (ci, [vp, ci, ci, C.POINTER(ci)]),

@@ -183,6 +183,15 @@ class NitiModel:
         """Replay the step as a hipGraph or launch its kernels directly (default)."""
         check(self._lib.niti_model_set_graph(self._h, int(enable)), "set_graph")
 
+    def set_rowconv(self, enable: bool):
+        """Forward convs of the stride-1 pad-1 3x3 layers on the register-fed kernel with the fused
+        rescale (default) or on the LDS-staged GEMM + requantisation pass; identical results."""
+        check(self._lib.niti_model_set_rowconv(self._h, int(enable)), "set_rowconv")
+
+    def rowconv_error(self) -> int:
+        """1 if an in-kernel grid barrier of the register-fed forward ever timed out."""
+        return int(self._lib.niti_model_rowconv_error(self._h))
+
     def set_probe(self, layer: int, phase: int, max_launches: int = 256):
         check(self._lib.niti_model_set_probe(self._h, layer, phase, max_launches), "set_probe")
 

@@ -19,7 +19,7 @@ def T():
 
 
 def _run(T, arch, layers, batch, steps=2, seed=5, graph=False, reuse_buffers=True, prepare=None, overlap=True,
-         in_hw=0, classes=10):
+         in_hw=0, classes=10, rowconv=True):
     """reuse_buffers: new data goes into the same device tensors every step, so with graph=True
     steps after the first replay the captured graph instead of re-capturing it.
     prepare(model, x, labels): called after one throwaway step (weights are reset after it)."""
@@ -30,6 +30,7 @@ def _run(T, arch, layers, batch, steps=2, seed=5, graph=False, reuse_buffers=Tru
     m = NitiModel(arch, batch, in_hw)
     m.set_graph(graph)
     m.set_overlap(overlap)
+    m.set_rowconv(rowconv)
     xd = ld = None
     l0 = layers[0]
     if prepare is not None:
@@ -64,6 +65,7 @@ def _run(T, arch, layers, batch, steps=2, seed=5, graph=False, reuse_buffers=Tru
             assert np.array_equal(m.tap(i, 1), rec["dw"][i]), ("dw", step, i)
             assert np.array_equal(m.get_weight(i), newW[i]), ("w", step, i)
         W = newW
+    assert m.rowconv_error() == 0  # no in-kernel grid barrier of the fused forward timed out
 
 
 def test_lenet_step_matches_oracle(T):
@@ -89,6 +91,22 @@ def test_vgg11_step_single_stream(T):
     import niti_amd
     import niti_model_ref as R
     _run(T, niti_amd.ARCH_VGG11, R.vgg11_layers(), batch=8, steps=2, seed=6, overlap=False)
+
+
+def test_vgg11_step_gemm_forward(T):
+    """The LDS-staged GEMM + requantisation forward (the register-fed fused one switched off)."""
+    import niti_amd
+    import niti_model_ref as R
+    _run(T, niti_amd.ARCH_VGG11, R.vgg11_layers(), batch=8, steps=2, seed=7, rowconv=False)
+
+
+@pytest.mark.parametrize("reuse", [True, False])
+def test_vgg11_step_graph_replay(T, reuse):
+    """Inside a graph capture the register-fed forward runs as range + recompute launches (the fused
+    launch's barrier epoch would be frozen by the capture)."""
+    import niti_amd
+    import niti_model_ref as R
+    _run(T, niti_amd.ARCH_VGG11, R.vgg11_layers(), batch=8, steps=3, seed=12, graph=True, reuse_buffers=reuse)
 
 
 def test_vgg11_ragged_batch(T):
