@@ -230,6 +230,25 @@ int niti_conv_dgrad_phase2(const niti_geom* g, const int8_t* dy_nhwc16, const in
                            const uint32_t* amax, const int8_t* exp_in, const int8_t* wscale, int8_t* exp_out,
                            int relu, const int8_t* relu_mask, int8_t* out_nhwc16, size_t workspace_bytes,
                            void* stream);
+/* Register-fed forward conv of stride-1 pad-1 3x3 layers with the NITI rescale fused
+ * (niti_rowconv.hip; square images of 2, 4, 8 or 16 pixels, c_out padded to 16 a multiple of 32):
+ * activations in C32 [n][ceil(C/32)][H][W][32], weights in WF [Co/32][Ci/32][9][2][32][16] (one
+ * 1 KiB MFMA fragment per co block, ci block and tap).  mode 0: one launch, max|y| reduced by an
+ * in-kernel grid barrier (state: NITI_ROWCONV_STATE_WORDS u32 zeroed once; epoch 1, 2, 3, ... one per
+ * call in stream order; err u32 set to 1 if the barrier ever timed out); mode 1: max|y| into amax
+ * (zeroed by the caller); mode 2: recompute and requantise with amax (a data-parallel caller
+ * all-reduces amax between modes 1 and 2).  Outputs: out_nhwc16 [n][H][W][cop] = relu?(requant(y)),
+ * pool_out_nhwc16 (may be NULL) its 2x2 max pool, next_c32 (may be NULL) the (pooled) output as the
+ * next layer's C32 input; exp_out = exp_in + wscale + inc. */
+#define NITI_ROWCONV_STATE_WORDS 1216
+int niti_conv_rows_ok(const niti_geom* g);
+int niti_nhwc16_to_c32(const int8_t* in_nhwc16, int n, int hw, int cp, int c, int8_t* out_c32, void* stream);
+int niti_weights_to_wf(const int8_t* w_ohwi16, int co, int ci, int cip, int transpose, int8_t* out_wf,
+                       void* stream);
+int niti_conv_fwd_rows(const niti_geom* g, const int8_t* x_c32, const int8_t* wf, const int8_t* exp_in,
+                       const int8_t* wscale, int8_t* exp_out, int relu, int8_t* out_nhwc16, int8_t* pool_out_nhwc16,
+                       int8_t* next_c32, int mode, uint32_t* amax, uint32_t* state, uint32_t epoch, uint32_t* err,
+                       void* stream);
 /* acc[co][kh][kw][cip] int32 = weight gradient for x (NHWC16) and dy (NHWC16): a K-major GEMM
  * over the pixels whose operand tiles are transposed in LDS (ds_read_b64_tr_b8) */
 int niti_conv_wgrad_acc(const niti_geom* g, const int8_t* x_nhwc16, const int8_t* dy_nhwc16, int32_t* acc,
@@ -246,6 +265,8 @@ int niti_nhwc16_to_p16(const int8_t* in_nhwc16, int64_t pixels, int cp, int8_t* 
 int niti_conv_wgrad_p16_workspace(const niti_geom* g, int splits, size_t* bytes);
 /* diagnostics: device buffer (8 u64 per block) for the per-block stamps of stamp builds; NULL disarms */
 void niti_diag_wgrad_stamps(void* buf);
+/* diagnostics: device buffer (8 u64 per wave) for the register-fed conv's per-wave stamps; NULL disarms */
+void niti_diag_rowconv_stamps(void* buf);
 int niti_conv_wgrad_p16_acc(const niti_geom* g, const int8_t* x_p16, const int8_t* dy_p16, int32_t* acc,
                             uint32_t* amax, void* workspace, size_t workspace_bytes, int splits, void* stream);
 /* acc[m][ldc] = sum_k B[m][k] A[o][k] (columns o..ldc = 0); K zero padded to k16; ldb/lda bytes */

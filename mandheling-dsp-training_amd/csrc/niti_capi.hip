@@ -244,6 +244,41 @@ static niti::ActOut act_out(const int8_t* exp_in, const int8_t* wscale, int8_t* 
     return o;
 }
 
+int niti_conv_rows_ok(const niti_geom* g) {
+    niti::ConvGeom r;
+    return g && to_geom(g, &r) && niti::rowconv_ok(r) ? 1 : 0;
+}
+
+int niti_nhwc16_to_c32(const int8_t* in, int n, int hw, int cp, int c, int8_t* out, void* stream) {
+    if (!in || !out || n <= 0 || hw <= 0 || c <= 0 || cp < c || cp % 16) return NITI_INVALID_VALUE;
+    return code(niti::nhwc16_to_c32(in, n, hw, cp, c, out, S(stream)));
+}
+
+int niti_weights_to_wf(const int8_t* w, int co, int ci, int cip, int transpose, int8_t* out, void* stream) {
+    if (!w || !out || co <= 0 || ci <= 0 || cip < ci || cip % 16) return NITI_INVALID_VALUE;
+    return code(niti::weights_to_wf(w, co, ci, cip, transpose != 0, out, S(stream)));
+}
+
+int niti_conv_fwd_rows(const niti_geom* g, const int8_t* x_c32, const int8_t* wf, const int8_t* exp_in,
+                       const int8_t* wscale, int8_t* exp_out, int relu, int8_t* out, int8_t* pool_out,
+                       int8_t* next_c32, int mode, uint32_t* amax, uint32_t* state, uint32_t epoch, uint32_t* err,
+                       void* stream) {
+    if (!g || !x_c32 || !wf || !amax || mode < 0 || mode > 2) return NITI_INVALID_VALUE;
+    niti::ConvGeom r;
+    if (!to_geom(g, &r)) return NITI_COMPUTE_SIZE_ERROR;
+    if (!niti::rowconv_ok(r)) return NITI_NOT_SUPPORT;
+    if (mode == 0 && !niti::rowconv_fused_ok(r)) return NITI_NOT_SUPPORT;
+    niti::RowConvOut o;
+    o.out = out;
+    o.pool_out = pool_out;
+    o.next = next_c32;
+    o.exp_in = exp_in;
+    o.wscale = wscale;
+    o.exp_out = exp_out;
+    o.relu = relu;
+    return code(niti::rowconv_fwd(r, x_c32, wf, o, mode, amax, state, epoch, err, S(stream)));
+}
+
 int niti_conv_fwd_phase1(const niti_geom* g, const int8_t* x, const int8_t* w, int32_t* acc, uint32_t* amax,
                          void* ws, size_t ws_bytes, void* stream) {
     if (!g || !x || !w || !acc || !amax) return NITI_INVALID_VALUE;
@@ -294,6 +329,7 @@ int niti_nhwc16_to_p16(const int8_t* in, int64_t pixels, int cp, int8_t* out, vo
 }
 
 void niti_diag_wgrad_stamps(void* buf) { niti::wgrad_stamps_arm((unsigned long long*)buf); }
+void niti_diag_rowconv_stamps(void* buf) { niti::rowconv_stamps_arm((unsigned long long*)buf); }
 
 int niti_conv_wgrad_p16_workspace(const niti_geom* g, int splits, size_t* bytes) {
     if (!g || !bytes) return NITI_INVALID_VALUE;

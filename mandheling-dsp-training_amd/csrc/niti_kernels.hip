@@ -3042,6 +3042,10 @@ __device__ __forceinline__ void sgd_tile(const SgdJob& J, int bw, int ci0, int c
             for (int j = 0; j < 16; ++j) wn[j] = (signed char)clip127((int32_t)wo[j] - (int32_t)g[j]);
             *(v16c*)(J.w + idx) = wn;
             if (J.g_out != nullptr) *(v16c*)(J.g_out + idx) = g;
+            if (J.wf != nullptr) {  // WF [co/32][ci/32][9][2][32][16]: this row's 16 ci of one co
+                const int o = co0 + r, i0 = ci0 + c, cb = (J.ci + 31) / 32;
+                *(v16c*)(J.wf + (((((int64_t)(o >> 5) * cb + (i0 >> 5)) * 9 + k) * 2 + ((i0 >> 4) & 1)) * 32 + (o & 31)) * 16) = wn;
+            }
         }
 #pragma unroll
         for (int j = 0; j < 16; ++j) T[r][c + j] = wn[j];
@@ -3054,6 +3058,10 @@ __device__ __forceinline__ void sgd_tile(const SgdJob& J, int bw, int ci0, int c
 #pragma unroll
             for (int j = 0; j < 16; ++j) o[j] = T[c + j][r];
             *(v16c*)(J.wT + ((int64_t)(ci0 + r) * J.kk + k) * J.cop + co0 + c) = o;
+            if (J.wft != nullptr) {  // the input gradient's WF: output channel ci, k = 16 co, tap 8 - k
+                const int i = ci0 + r, o0 = co0 + c, ob = (J.co + 31) / 32;
+                *(v16c*)(J.wft + (((((int64_t)(i >> 5) * ob + (o0 >> 5)) * 9 + (8 - k)) * 2 + ((o0 >> 4) & 1)) * 32 + (i & 31)) * 16) = o;
+            }
         }
     }
 }

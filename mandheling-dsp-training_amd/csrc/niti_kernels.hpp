@@ -14,6 +14,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "../../include/niti_hip.h"
+
 namespace niti {
 
 inline int round_up(int x, int m) { return (x + m - 1) / m * m; }
@@ -205,7 +207,8 @@ struct RowConvOut {
     int8_t* exp_out = nullptr;
     int relu = 0;
 };
-constexpr int ROWCONV_BAR_WORDS = 2 * 19 * 32;  // grid-barrier state of one layer (both parities)
+constexpr int ROWCONV_BAR_WORDS = 2 * 19 * 32;  // grid-barrier state (both parities)
+static_assert(ROWCONV_BAR_WORDS == NITI_ROWCONV_STATE_WORDS, "header constant");
 bool rowconv_ok(const ConvGeom& g);
 // FUSED (one launch, in-kernel grid barrier) possible: one unit per wave, every workgroup resident
 bool rowconv_fused_ok(const ConvGeom& g);
@@ -217,6 +220,8 @@ hipError_t weights_to_wf(const int8_t* w_ohwi16, int co, int ci, int cip, bool t
                          hipStream_t st);
 // mode 0 FUSED (bar, err, epoch != 0 required; epoch + 1 per launch), 1 RANGE (max|y| into amax),
 // 2 REQUANT (recompute with the max in amax, requantise, store)
+// diagnostics: 8 u64 per wave of the following launches (niti_diag_rowconv_stamps), null disarms
+void rowconv_stamps_arm(unsigned long long* buf);
 hipError_t rowconv_fwd(const ConvGeom& g, const int8_t* x_c32, const int8_t* wf, const RowConvOut& o, int mode,
                        uint32_t* amax, uint32_t* bar, uint32_t epoch, uint32_t* err, hipStream_t st);
 
@@ -277,6 +282,10 @@ struct SgdJob {
     int8_t* w;
     int8_t* wT;
     int8_t* g_out;
+    // 3x3 layers on the register-fed convs (niti_rowconv.hip): the new weights also as the
+    // forward's and the input gradient's fragment-major copies (may be null; kk == 9)
+    int8_t* wf = nullptr;
+    int8_t* wft = nullptr;
 };
 constexpr int SGD_MAX_JOBS = 24;
 struct SgdJobs {

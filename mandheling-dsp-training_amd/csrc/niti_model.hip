@@ -1200,6 +1200,8 @@ int Model::run(const int8_t* x_nchw, int exp_in, const uint8_t* images, const in
         const ConvGeom& g = l.g;
         jobs[i] = SgdJob{l.dwacc, rng(i, 2), RULE_WGRAD_BW2, g.c_out, g.c_in, g.kh * g.kw, g.cip, g.cop, l.w,
                          i > 0 ? l.wT : nullptr, l.g8};
+        jobs[i].wf = l.rc ? l.wf : nullptr;
+        jobs[i].wft = nullptr;
     }
     if (dp) {  // every bucket summed and ranged on the comm stream before the update
         MTRY(hipEventRecord(ev_grads, cst));
@@ -1208,8 +1210,8 @@ int Model::run(const int8_t* x_nchw, int exp_in, const uint8_t* images, const in
         MTRY(hipEventRecord(ev_side, side));
         MTRY(hipStreamWaitEvent(st, ev_side, 0));
     }
-    MTRY(sgd_update_many(jobs, nl, st));
-    return refresh_wf(st);
+    MTRY(sgd_update_many(jobs, nl, st));  // also rewrites the fragment-major weight copies
+    return NITI_NO_ERROR;
 }
 
 }  // namespace niti

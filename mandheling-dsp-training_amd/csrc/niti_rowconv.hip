@@ -139,7 +139,9 @@ struct RowConvArgs {
     const int8_t* wf; // WF [COB][CB][9][2][32][16]
     uint32_t xbytes, wbytes;
     int n, CB, COB;
-    int units, nbands;
+    int ngb, ngb4;    // (image group, band) pairs; rounded up to whole workgroups of 4
+    int nbands;
+    int wgs;          // workgroup tiles: COB * ngb4 / 4
     int8_t* out;      // NHWC16 [n][H][W][cop]
     int cop;
     int8_t* pool_out; // NHWC16 [n][H/2][W/2][cop] or null
@@ -152,79 +154,188 @@ struct RowConvArgs {
     uint32_t* bar;    // FUSED: barrier state
     uint32_t epoch;
     uint32_t* err;
+    unsigned long long* stamps;  // diagnostics (niti_diag_rowconv_stamps): 8 per wave, or null
 };
+
+// diagnostic stamps, 16 per wave: [0] start, [1] prologue issued, [2] cycles issuing loads, [3] K
+// loop done, [4] max reduced (+ grid barrier), [5] end, [6] cycles in the per-step waits +
+// barriers, [7] cycles in the per-step fragment reads (s_memtime, per-XCD clock); wave 0 of each
+// workgroup: [8] / [9] s_memrealtime (chip-wide 100 MHz) at the grid barrier's arrival / release
+#define RC_STAMP(k)                                                                                  \
+    do {                                                                                             \
+        if (a.stamps != nullptr && lane == 0)                                                        \
+            a.stamps[(blockIdx.x * 4 + wid) * 16 + (k)] = __builtin_amdgcn_s_memtime();              \
+    } while (0)
 
 enum RowMode { RC_FUSED = 0, RC_RANGE = 1, RC_REQUANT = 2 };
 
+// A workgroup tile is one co block x 4 consecutive (image group, band) pairs, one per wave: the
+// four waves share the co block's weight fragments, which the workgroup stages through LDS once
+// per 32-channel chunk (a 9 KiB contiguous run of WF) instead of each wave loading them.
 template <int W, int R>
 struct RowUnit {
     static constexpr int G = 32 / W, H = W, NR = R + 2;
     int cob, b, img;
-    bool img_ok;
-    __device__ RowUnit(const RowConvArgs& a, int u, int c) {
-        cob = u % a.COB;
-        const int rest = u / a.COB;
-        b = rest % a.nbands;
-        img = (rest / a.nbands) * G + c / W;
-        img_ok = img < a.n;
+    bool valid, img_ok;
+    __device__ RowUnit(const RowConvArgs& a, int wg, int wid, int c) {
+        const int per = a.ngb4 / 4;
+        cob = wg / per;
+        const int gb = (wg - cob * per) * 4 + wid;
+        valid = gb < a.ngb;
+        const int gbc = valid ? gb : 0;
+        b = gbc % a.nbands;
+        img = (gbc / a.nbands) * G + c / W;
+        img_ok = valid && img < a.n;
     }
 };
 
+constexpr int RC_MAX_STAGES = 3;
+constexpr int RC_PIECES = 12;               // 9 KiB of fragments as 3 x 1 KiB DMA per wave (3 dummies)
+constexpr int RC_STAGE_BYTES = RC_PIECES * 1024;
+constexpr int RC_LDS_BYTES = RC_MAX_STAGES * RC_STAGE_BYTES;
+
 // the accumulators of one unit: acc[r][i] = y[co = cob*32 + 8(i>>2) + 4h + (i&3)][row b*R + r][col]
+// Every wave of the workgroup runs this (an invalid unit reads zeros), so the barriers match.
+//
+// The kx taps are three loads of each input row at the lane's column ox - 1, ox, ox + 1 (a lane
+// whose neighbour column leaves the image row reads zeros through the buffer range check): no
+// cross-lane moves, no masks, no VALU in the loop.  S chunks are in flight: chunk c computes from
+// registers while c + 1 .. c + S - 1 load (rows into registers, the 9 weight fragments by LDS-DMA
+// into a ring shared by the workgroup's four waves).
 template <int W, int R>
-__device__ __forceinline__ void rowconv_compute(const RowConvArgs& a, const RowUnit<W, R>& U, int lane, v16i (&acc)[R]) {
+__device__ __forceinline__ void rowconv_compute(const RowConvArgs& a, const RowUnit<W, R>& U, int lane, int wid,
+                                                int8_t* smem, v16i (&acc)[R]) {
     constexpr int H = W, NR = R + 2;
+    // kx shifts: DPP row shifts of the centre column (zero fill at the 16-lane DPP row ends, a
+    // mask where a narrower image row ends inside a DPP row) -- one load per row: each 16-byte
+    // wave load costs the CU's texture addresser ~16 cycles, and three loads per row (the
+    // shifted columns from memory) made the K loop address-bound (stamps: 8.5k of 23k cycles
+    // issuing loads on conv4)
+    constexpr bool DPPX = true;
+    constexpr int KXL = DPPX ? 1 : 3;        // loads per row and chunk
+    constexpr int S = 3;                     // chunks in flight
+    constexpr int L = KXL * NR + 3;          // vector-memory instructions per wave per chunk
     const int h = lane >> 5, c = lane & 31, ox = c % W;
-    const bool row_start = ox == 0, row_end = ox == W - 1;
     const __amdgpu_buffer_rsrc_t rX = make_rsrc(a.x, a.xbytes);
     const __amdgpu_buffer_rsrc_t rW = make_rsrc(a.wf, a.wbytes);
     const uint32_t xl = U.img_ok ? (uint32_t)((((int64_t)U.img * a.CB * H) * W + ox) * 32 + 16 * h) : OOB;
-    const uint32_t wl = (uint32_t)(h * 512 + c * 16);
     constexpr uint32_t CHUNK = (uint32_t)H * W * 32;
     const int y0 = U.b * R - 1;
 #pragma unroll
     for (int r = 0; r < R; ++r)
 #pragma unroll
         for (int i = 0; i < 16; ++i) acc[r][i] = 0;
-    v4i X[2][NR], Wt[2][9];
-    auto load = [&](int buf, int cc) {
+    // per row and kx: the lane's byte offset in chunk 0, OOB outside the image (rows) or the row (kx)
+    uint32_t off[3][NR];
 #pragma unroll
-        for (int j = 0; j < NR; ++j) {
-            const int iy = y0 + j;
-            if (iy >= 0 && iy < H)
-                X[buf][j] = buf_load16(rX, xl + (uint32_t)cc * CHUNK + (uint32_t)iy * W * 32);
-            else
-                X[buf][j] = v4i{0, 0, 0, 0};
-        }
-        const uint32_t wo = (uint32_t)((U.cob * a.CB + cc) * 9) * 1024u;
-#pragma unroll
-        for (int t = 0; t < 9; ++t) Wt[buf][t] = buf_load16(rW, wl + wo + (uint32_t)t * 1024u);
-    };
-    auto compute = [&](int buf) {
-        v4i XL[NR], XR[NR];
-#pragma unroll
-        for (int j = 0; j < NR; ++j) {
-            XL[j] = shift_in_left<W>(X[buf][j], row_start);
-            XR[j] = shift_in_right<W>(X[buf][j], row_end);
-        }
-#pragma unroll
-        for (int r = 0; r < R; ++r)
-#pragma unroll
-            for (int ky = 0; ky < 3; ++ky) {
-                acc[r] = __builtin_amdgcn_mfma_i32_32x32x32_i8(Wt[buf][3 * ky], XL[r + ky], acc[r], 0, 0, 0);
-                acc[r] = __builtin_amdgcn_mfma_i32_32x32x32_i8(Wt[buf][3 * ky + 1], X[buf][r + ky], acc[r], 0, 0, 0);
-                acc[r] = __builtin_amdgcn_mfma_i32_32x32x32_i8(Wt[buf][3 * ky + 2], XR[r + ky], acc[r], 0, 0, 0);
-            }
-    };
-    load(0, 0);
-    int cc = 0;
-    for (; cc + 2 <= a.CB; cc += 2) {
-        if (cc + 1 < a.CB) load(1, cc + 1);
-        compute(0);
-        if (cc + 2 < a.CB) load(0, cc + 2);
-        compute(1);
+    for (int j = 0; j < NR; ++j) {
+        const int iy = y0 + j;
+        const bool row_ok = iy >= 0 && iy < H && xl != OOB;
+        const uint32_t base = xl + (uint32_t)iy * W * 32;
+        off[0][j] = row_ok && ox > 0 ? base - 32u : OOB;
+        off[1][j] = row_ok ? base : OOB;
+        off[2][j] = row_ok && ox < W - 1 ? base + 32u : OOB;
     }
-    if (cc < a.CB) compute(0);
+    // this wave's three DMA pieces of a chunk's 9 fragments (pieces 9..11 are dummies: OOB source)
+    const uint32_t dv2 = wid == 0 ? (uint32_t)lane * 16u : OOB;
+    const int cb = a.CB;
+    const uint32_t wbase = (uint32_t)(U.cob * cb * 9) * 1024u;
+    v4i X[S][KXL][NR];
+    auto issue = [&](auto st_c, int cc) {
+        constexpr int ST = decltype(st_c)::value;
+        int8_t* lds = smem + ST * RC_STAGE_BYTES;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const int piece = wid + 4 * k;  // 0..11
+            dma16(rW, lds + piece * 1024, k < 2 ? (uint32_t)lane * 16u : dv2,
+                  wbase + (uint32_t)cc * 9216u + (uint32_t)(piece < 9 ? piece : 0) * 1024u);
+        }
+#pragma unroll
+        for (int j = 0; j < NR; ++j)
+#pragma unroll
+            for (int kx = 0; kx < KXL; ++kx)
+                X[ST][kx][j] = buf_load16(rX, off[DPPX ? 1 : kx][j] + (uint32_t)cc * CHUNK);
+    };
+    const uint32_t lds_lane = lds_addr(smem) + (uint32_t)lane * 16u;
+    unsigned long long t_wait = 0, t_read = 0, t_issue = 0;
+    const bool stamp = a.stamps != nullptr;
+    auto step = [&](auto st_c, int cc) {
+        constexpr int ST = decltype(st_c)::value;
+        const unsigned long long s0 = stamp ? __builtin_amdgcn_s_memtime() : 0ull;
+        // own loads of chunk cc landed (the S - 2 later chunks' may still be in flight), then the
+        // barrier: every wave's DMA of chunk cc is in LDS, and every wave is done with the stage
+        // the next issue refills (chunk cc - 1's: read before that chunk's MFMAs)
+        const int later = cb - 1 - cc < S - 2 ? cb - 1 - cc : S - 2;
+        if (later >= 1)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(L) : "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        const unsigned long long s1 = stamp ? __builtin_amdgcn_s_memtime() : 0ull;
+        if (cc + S - 1 < cb) issue(std::integral_constant<int, (ST + S - 1) % S>(), cc + S - 1);
+        if (stamp) {
+            asm volatile("" ::: "memory");
+            t_issue += __builtin_amdgcn_s_memtime() - s1;
+        }
+        v4i w[9];
+#pragma unroll
+        for (int t = 0; t < 9; ++t) w[t] = lds_b128(lds_lane + (uint32_t)(ST * RC_STAGE_BYTES + t * 1024));
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int t = 0; t < 9; ++t) reg_fence(w[t]);
+        if (stamp) {
+            const unsigned long long s2 = __builtin_amdgcn_s_memtime();
+            t_wait += s1 - s0;
+            t_read += s2 - s1;
+        }
+        if constexpr (DPPX) {
+            v4i XL[NR], XR[NR];
+#pragma unroll
+            for (int j = 0; j < NR; ++j) {
+                XL[j] = shift_in_left<W>(X[ST][0][j], ox == 0);
+                XR[j] = shift_in_right<W>(X[ST][0][j], ox == W - 1);
+            }
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+#pragma unroll
+                for (int ky = 0; ky < 3; ++ky) {
+                    acc[r] = __builtin_amdgcn_mfma_i32_32x32x32_i8(w[3 * ky], XL[r + ky], acc[r], 0, 0, 0);
+                    acc[r] = __builtin_amdgcn_mfma_i32_32x32x32_i8(w[3 * ky + 1], X[ST][0][r + ky], acc[r], 0, 0, 0);
+                    acc[r] = __builtin_amdgcn_mfma_i32_32x32x32_i8(w[3 * ky + 2], XR[r + ky], acc[r], 0, 0, 0);
+                }
+        } else {
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+#pragma unroll
+                for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+                    for (int kx = 0; kx < 3; ++kx)
+                        acc[r] = __builtin_amdgcn_mfma_i32_32x32x32_i8(w[3 * ky + kx], X[ST][kx][r + ky], acc[r], 0, 0, 0);
+        }
+    };
+#pragma unroll
+    for (int k = 0; k + 1 < S; ++k)
+        if (k < cb) {
+            if (k == 0) issue(std::integral_constant<int, 0>(), 0);
+            if (k == 1) issue(std::integral_constant<int, 1>(), 1);
+        }
+    if (stamp && lane == 0) a.stamps[(blockIdx.x * 4 + wid) * 16 + 1] = __builtin_amdgcn_s_memtime();
+    for (int cc = 0; cc < cb; cc += S) {
+        step(std::integral_constant<int, 0>(), cc);
+        if (cc + 1 < cb) step(std::integral_constant<int, 1 % S>(), cc + 1);
+        if constexpr (S > 2)
+            if (cc + 2 < cb) step(std::integral_constant<int, 2 % S>(), cc + 2);
+    }
+    // the ring's LDS is reused by the next unit's prologue only after every wave's last reads
+    __builtin_amdgcn_s_barrier();
+    if (stamp && lane == 0) {
+        unsigned long long* st = a.stamps + (blockIdx.x * 4 + wid) * 16;
+        st[3] = __builtin_amdgcn_s_memtime();
+        st[2] = t_issue;
+        st[6] = t_wait;
+        st[7] = t_read;
+    }
 }
 
 __device__ __forceinline__ uint32_t pack4(const int8_t* v) {
@@ -247,18 +358,44 @@ __device__ __forceinline__ void rowconv_epilogue(const RowConvArgs& a, const Row
                                                  const v16i (&acc)[R], uint32_t gmax) {
     constexpr int H = W;
     const int h = lane >> 5, c = lane & 31, ox = c % W;
-    const int shift = bitwidth_rc(gmax) - 7;
-    const int s = shift > 1 ? shift : 2;
-    const bool raw = shift <= 0;
+    // NITI_Conv_Int8.cpp:266-307 with wave-uniform branches: shift <= 0 the raw int8 cast, else
+    // PSTO(acc, max(shift, 2)); under relu a negative value is 0 whatever its rounding, so the
+    // positive-only PSTO serves (ReLU after requantisation, NITI_Relu_Int8)
+    const int shift = __builtin_amdgcn_readfirstlane(bitwidth_rc(gmax) - 7);
     int8_t q[R][16];
+    if (shift <= 0) {
 #pragma unroll
-    for (int r = 0; r < R; ++r)
+        for (int r = 0; r < R; ++r)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            int32_t v = raw ? (int32_t)(int8_t)acc[r][i] : psto_rc(acc[r][i], s);
-            if (a.relu && v < 0) v = 0;
-            q[r][i] = (int8_t)v;
+            for (int i = 0; i < 16; ++i) {
+                const int32_t v = (int32_t)(int8_t)acc[r][i];
+                q[r][i] = (int8_t)(a.relu && v < 0 ? 0 : v);
+            }
+    } else {
+        const uint32_t s = shift > 1 ? shift : 2, hh = s >> 1, odd = s & 1;
+        auto pos = [&](uint32_t u) -> uint32_t {  // PSTO of u >= 0
+            const uint32_t qv = u >> s;
+            const uint32_t hi = __builtin_amdgcn_ubfe(u, hh, s - hh);
+            const uint32_t lo = __builtin_amdgcn_ubfe(u, 0, hh) << odd;
+            const uint32_t rr = qv + (hi > lo ? 1u : 0u);
+            return rr < 127u ? rr : 127u;
+        };
+        if (a.relu) {
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) q[r][i] = (int8_t)pos((uint32_t)max(acc[r][i], 0));
+        } else {
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const int32_t v = acc[r][i];
+                    const int32_t p = (int32_t)pos(uabs32(v));
+                    q[r][i] = (int8_t)(v < 0 ? -p : p);
+                }
         }
+    }
     const int64_t img = U.img;
     const int cb16 = U.cob * 32 + 16 * h;  // this lane's 16 channels after pack_cols
 #pragma unroll
@@ -279,7 +416,7 @@ __device__ __forceinline__ void rowconv_epilogue(const RowConvArgs& a, const Row
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
                 const int v0 = q[r][i] > q[r + 1][i] ? q[r][i] : q[r + 1][i];
-                const int v1 = __shfl_xor(v0, 1, 64);
+                const int v1 = __builtin_amdgcn_mov_dpp(v0, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]: lane ^ 1
                 pm[i] = (int8_t)(v0 > v1 ? v0 : v1);
             }
             const v4i v = pack_cols(pm);
@@ -311,26 +448,28 @@ __device__ __forceinline__ uint32_t max_abs16(const v16i& v, uint32_t m) {
 
 template <int W, int R, int MODE>
 __global__ void __launch_bounds__(256) rowconv_fwd_kernel(RowConvArgs a) {
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: DMA bases stay scalar
     const int c = lane & 31;
+    __shared__ __attribute__((aligned(16))) int8_t smem[RC_LDS_BYTES];
     __shared__ uint32_t red[4];
     __shared__ uint32_t gm;
     v16i acc[R];
+    RC_STAMP(0);
     if constexpr (MODE == RC_FUSED) {
-        const int u = blockIdx.x * 4 + wid;
+        const RowUnit<W, R> U(a, blockIdx.x, wid, c);
         uint32_t m = 0;
-        const RowUnit<W, R> U(a, u < a.units ? u : 0, c);
-        if (u < a.units) {
-            rowconv_compute<W, R>(a, U, lane, acc);
+        rowconv_compute<W, R>(a, U, lane, wid, smem, acc);
 #pragma unroll
-            for (int r = 0; r < R; ++r) m = max_abs16(acc[r], m);
-        }
+        for (int r = 0; r < R; ++r) m = max_abs16(acc[r], m);
         m = wave_max(m);
         if (lane == 0) red[wid] = m;
         __syncthreads();
         if (threadIdx.x == 0) {
             const uint32_t bm = max(max(red[0], red[1]), max(red[2], red[3]));
+            if (a.stamps != nullptr) a.stamps[blockIdx.x * 64 + 8] = __builtin_amdgcn_s_memrealtime();
             const uint32_t g = grid_max_barrier(a.bar, a.epoch, bm, a.err);
+            if (a.stamps != nullptr) a.stamps[blockIdx.x * 64 + 9] = __builtin_amdgcn_s_memrealtime();
             gm = g;
             if (blockIdx.x == 0) {
                 publish_max(a.amax, g);  // the layer's range, for the record
@@ -338,12 +477,14 @@ __global__ void __launch_bounds__(256) rowconv_fwd_kernel(RowConvArgs a) {
             }
         }
         __syncthreads();
-        if (u < a.units) rowconv_epilogue<W, R>(a, U, lane, acc, gm);
+        RC_STAMP(4);
+        if (U.valid) rowconv_epilogue<W, R>(a, U, lane, acc, gm);
+        RC_STAMP(5);
     } else if constexpr (MODE == RC_RANGE) {
         uint32_t m = 0;
-        for (int u = blockIdx.x * 4 + wid; u < a.units; u += gridDim.x * 4) {
-            const RowUnit<W, R> U(a, u, c);
-            rowconv_compute<W, R>(a, U, lane, acc);
+        for (int wg = blockIdx.x; wg < a.wgs; wg += gridDim.x) {
+            const RowUnit<W, R> U(a, wg, wid, c);
+            rowconv_compute<W, R>(a, U, lane, wid, smem, acc);
 #pragma unroll
             for (int r = 0; r < R; ++r) m = max_abs16(acc[r], m);
         }
@@ -351,13 +492,14 @@ __global__ void __launch_bounds__(256) rowconv_fwd_kernel(RowConvArgs a) {
         if (lane == 0) red[wid] = m;
         __syncthreads();
         if (threadIdx.x == 0) publish_max(a.amax, max(max(red[0], red[1]), max(red[2], red[3])));
+        RC_STAMP(5);
     } else {
         const uint32_t g = read_max(a.amax);
         if (blockIdx.x == 0 && threadIdx.x == 0) write_exponent(a, g);
-        for (int u = blockIdx.x * 4 + wid; u < a.units; u += gridDim.x * 4) {
-            const RowUnit<W, R> U(a, u, c);
-            rowconv_compute<W, R>(a, U, lane, acc);
-            rowconv_epilogue<W, R>(a, U, lane, acc, g);
+        for (int wg = blockIdx.x; wg < a.wgs; wg += gridDim.x) {
+            const RowUnit<W, R> U(a, wg, wid, c);
+            rowconv_compute<W, R>(a, U, lane, wid, smem, acc);
+            if (U.valid) rowconv_epilogue<W, R>(a, U, lane, acc, g);
         }
     }
 }
@@ -453,9 +595,10 @@ bool rowconv_ok(const ConvGeom& g) {
 static int rowconv_rows(const ConvGeom& g, int* units_out) {
     const int W = g.w, G = 32 / W;
     const int64_t groups = (g.n + G - 1) / G, cob = g.cop / 32;
-    int R = W < 8 ? W : 8;
+    int R = W == 16 ? 8 : (W < 4 ? W : 4);  // register budget: at most 4 rows of 3 loaded columns
     while (R > 2 && groups * (W / R) * cob < 768) R /= 2;
-    *units_out = (int)(groups * (W / R) * cob);
+    const int64_t ngb4 = (groups * (W / R) + 3) / 4 * 4;
+    *units_out = (int)(ngb4 * cob);  // waves, whole workgroups of 4
     return R;
 }
 
@@ -477,7 +620,6 @@ static hipError_t launch_rc(int W, int R, int grid, const RowConvArgs& a, hipStr
     RC_CASE(16, 8)
     RC_CASE(16, 4)
     RC_CASE(16, 2)
-    RC_CASE(8, 8)
     RC_CASE(8, 4)
     RC_CASE(8, 2)
     RC_CASE(4, 4)
@@ -486,6 +628,9 @@ static hipError_t launch_rc(int W, int R, int grid, const RowConvArgs& a, hipStr
 #undef RC_CASE
     return hipErrorInvalidValue;
 }
+
+static unsigned long long* g_rc_stamps = nullptr;
+void rowconv_stamps_arm(unsigned long long* buf) { g_rc_stamps = buf; }
 
 hipError_t rowconv_fwd(const ConvGeom& g, const int8_t* x_c32, const int8_t* wf, const RowConvOut& o, int mode,
                        uint32_t* amax, uint32_t* bar, uint32_t epoch, uint32_t* err, hipStream_t st) {
@@ -505,8 +650,11 @@ hipError_t rowconv_fwd(const ConvGeom& g, const int8_t* x_c32, const int8_t* wf,
     a.COB = COB;
     int units = 0;
     const int R = rowconv_rows(g, &units);
-    a.units = units;
+    const int G = 32 / g.w;
     a.nbands = g.h / R;
+    a.ngb = ((g.n + G - 1) / G) * a.nbands;
+    a.ngb4 = (a.ngb + 3) / 4 * 4;
+    a.wgs = COB * a.ngb4 / 4;
     a.out = o.out;
     a.cop = g.cop;
     a.pool_out = o.pool_out;
@@ -519,12 +667,13 @@ hipError_t rowconv_fwd(const ConvGeom& g, const int8_t* x_c32, const int8_t* wf,
     a.bar = bar;
     a.epoch = epoch;
     a.err = err;
+    a.stamps = g_rc_stamps;
     if (o.pool_out != nullptr && (R % 2 != 0 || g.h % 2 != 0)) return hipErrorInvalidValue;
     if (mode == RC_FUSED) {
         if (bar == nullptr || err == nullptr || epoch == 0 || units > 4 * 256) return hipErrorInvalidValue;
-        return launch_rc<RC_FUSED>(g.w, R, (units + 3) / 4, a, st);
+        return launch_rc<RC_FUSED>(g.w, R, a.wgs, a, st);
     }
-    int grid = (units + 3) / 4;
+    int grid = a.wgs;
     grid = grid > 1024 ? 1024 : grid;
     if (mode == RC_RANGE) return launch_rc<RC_RANGE>(g.w, R, grid, a, st);
     return launch_rc<RC_REQUANT>(g.w, R, grid, a, st);

@@ -114,11 +114,17 @@ def lib():
         "niti_conv_dgrad_acc": (ci, [C.POINTER(Geom), vp, vp, vp, vp, vp, C.c_size_t, vp]),
         "niti_conv_wgrad_acc": (ci, [C.POINTER(Geom), vp, vp, vp, vp, vp, C.c_size_t, vp]),
         "niti_conv_fwd_phase1": (ci, [C.POINTER(Geom), vp, vp, vp, vp, vp, C.c_size_t, vp]),
+        "niti_conv_rows_ok": (ci, [C.POINTER(Geom)]),
+        "niti_nhwc16_to_c32": (ci, [vp, ci, ci, ci, ci, vp, vp]),
+        "niti_weights_to_wf": (ci, [vp, ci, ci, ci, ci, vp, vp]),
+        "niti_conv_fwd_rows": (ci, [C.POINTER(Geom), vp, vp, vp, vp, vp, ci, vp, vp, vp, ci, vp, vp, C.c_uint32, vp,
+                                    vp]),
         "niti_conv_fwd_phase2": (ci, [C.POINTER(Geom), vp, vp, vp, vp, vp, vp, vp, ci, vp, vp, C.c_size_t, vp]),
         "niti_conv_dgrad_phase1": (ci, [C.POINTER(Geom), vp, vp, vp, vp, vp, C.c_size_t, vp]),
         "niti_conv_dgrad_phase2": (ci, [C.POINTER(Geom), vp, vp, vp, vp, vp, vp, vp, ci, vp, vp, C.c_size_t, vp]),
         "niti_nhwc16_to_p16": (ci, [vp, i64, ci, vp, vp]),
         "niti_diag_wgrad_stamps": (None, [vp]),
+        "niti_diag_rowconv_stamps": (None, [vp]),
         "niti_conv_wgrad_p16_workspace": (ci, [C.POINTER(Geom), ci, C.POINTER(C.c_size_t)]),
         "niti_conv_wgrad_p16_acc": (ci, [C.POINTER(Geom), vp, vp, vp, vp, vp, C.c_size_t, ci, vp]),
         "niti_matmul_acc": (ci, [ci, ci, ci, vp, i64, vp, i64, vp, i64, vp, vp, C.c_size_t, vp]),

@@ -193,6 +193,62 @@ def _conv_requant(op, g: L.Geom, a, b, amax, exp_in, wscale, exp_out, relu, relu
     return out
 
 
+ROWCONV_STATE_WORDS = 1216
+
+
+def conv_rows_ok(g: L.Geom) -> bool:
+    return bool(L.lib().niti_conv_rows_ok(C.byref(g)))
+
+
+def nhwc16_to_c32(x16: torch.Tensor, c: int, stream=None):
+    """NHWC16 [n][h][w][cp] -> C32 [n][ceil(c/32)][h][w][32] (the register-fed conv's activations)."""
+    n, h, w, cp = x16.shape
+    cb = (c + 31) // 32
+    out = torch.empty((n, cb, h, w, 32), dtype=torch.int8, device=x16.device)
+    check(L.lib().niti_nhwc16_to_c32(_ptr(x16), n, h * w, cp, c, _ptr(out), _stream(stream)), "nhwc16->c32")
+    return out
+
+
+def weights_to_wf(w16: torch.Tensor, ci: int, transpose=False, stream=None):
+    """OHWI16 [co][kh][kw][cip] (3x3) -> WF fragment-major weights (transpose: the input gradient's)."""
+    co, cip = w16.shape[0], w16.shape[-1]
+    ob, ib = ((ci if transpose else co) + 31) // 32, ((co if transpose else ci) + 31) // 32
+    out = torch.empty(ob * ib * 9 * 1024, dtype=torch.int8, device=w16.device)
+    check(L.lib().niti_weights_to_wf(_ptr(w16), co, ci, cip, int(transpose), _ptr(out), _stream(stream)), "wf")
+    return out
+
+
+class RowConvState:
+    """Grid-barrier state of the fused register-fed conv (mode 0) and its epoch counter."""
+
+    def __init__(self, device="cuda"):
+        self.state = torch.zeros(ROWCONV_STATE_WORDS, dtype=torch.int32, device=device)
+        self.err = torch.zeros(1, dtype=torch.int32, device=device)
+        self.epoch = 0
+
+
+def conv_fwd_rows(g: L.Geom, xc32, wf, amax, mode=0, state: RowConvState | None = None, exp_in=None, wscale=None,
+                  exp_out=None, relu=False, pool=False, next_c32=False, stream=None):
+    """The register-fed forward (niti_conv_fwd_rows): (out NHWC16, pooled NHWC16 or None,
+    next C32 or None).  mode 0 fused (state required), 1 range only, 2 requantise with amax."""
+    dev = xc32.device
+    out = None if mode == 1 else torch.empty((g.n, g.oh, g.ow, g.cop), dtype=torch.int8, device=dev)
+    pout = torch.empty((g.n, g.oh // 2, g.ow // 2, g.cop), dtype=torch.int8, device=dev) if pool and mode != 1 else None
+    nxt = None
+    if next_c32 and mode != 1:
+        hh, ww = (g.oh // 2, g.ow // 2) if pool else (g.oh, g.ow)
+        nxt = torch.empty((g.n, g.cop // 32, hh, ww, 32), dtype=torch.int8, device=dev)
+    st_ptr = err_ptr = None
+    epoch = 0
+    if mode == 0:
+        state.epoch += 1
+        epoch, st_ptr, err_ptr = state.epoch, _ptr(state.state), _ptr(state.err)
+    check(L.lib().niti_conv_fwd_rows(C.byref(g), _ptr(xc32), _ptr(wf), _ptr(exp_in), _ptr(wscale), _ptr(exp_out),
+                                     1 if relu else 0, _ptr(out), _ptr(pout), _ptr(nxt), mode, _ptr(amax), st_ptr,
+                                     epoch, err_ptr, _stream(stream)), "conv_fwd_rows")
+    return out, pout, nxt
+
+
 def conv_fwd_requant(g: L.Geom, x16, w16, amax, exp_in=None, wscale=None, exp_out=None, relu=False,
                      relu_mask=None, between=None, stream=None):
     """The forward conv with its NITI requantisation in two phases (range, [between(amax)],

@@ -77,7 +77,7 @@ def test_no_fallback_when_library_missing(tmp_path, monkeypatch):
     importlib.reload(_lib)
 
 
-@pytest.mark.parametrize("unit", ["niti_wgrad", "niti_kernels"])
+@pytest.mark.parametrize("unit", ["niti_wgrad", "niti_kernels", "niti_rowconv"])
 def test_asm_ring_kernels_no_inflight_register_reuse(tmp_path, unit):
     """Kernels with inline-asm load rings count their own waits (hipcc does not know when such a
     load lands): no instruction may touch a register such a load is still writing.  Compiles the

@@ -1,0 +1,88 @@
+"""The register-fed forward conv with the fused rescale (niti_conv_fwd_rows, csrc/niti_rowconv.hip)
+against the oracle's NITI_Conv_Int8 (NITI_Conv_Int8.cpp:162-310): requantised output, exponent,
+relu, the fused 2x2 max pool and the next layer's C32 copy, bit for bit, in all three modes (fused
+one-launch with the in-kernel grid barrier; range then recompute-and-requantise), on every image
+width the kernel takes, ragged image groups (batch not a multiple of 32 / W) and every branch of
+the shift rule (raw cast, shift == 1 -> 2, shift > 1)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def T():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import niti_amd  # noqa: F401
+    return torch
+
+
+def _case(T, n, ci, h, co, relu, pool, mode, seed, wmax=127, xmax=127):
+    import niti_oracle as O
+    from niti_amd import ops
+    rng = np.random.default_rng(seed)
+    g = O.geom(n, ci, h, h, co, 3, pad=1)
+    x = rng.integers(-xmax, xmax + 1, (n, ci, h, h)).astype(np.int8)
+    w = rng.integers(-wmax, wmax + 1, (co, ci, 3, 3)).astype(np.int8)
+    y_ref, e_ref, acc, _ = O.conv_fwd(g, x, w, -3, -5)
+    r_ref = O.relu(y_ref) if relu else y_ref
+    dev = lambda a: T.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    gg = ops.geom(n, ci, h, h, co, 3, pad=1)
+    assert ops.conv_rows_ok(gg)
+    x16 = ops.nchw_to_nhwc16(dev(x))
+    xc = ops.nhwc16_to_c32(x16, ci)
+    wf = ops.weights_to_wf(ops.oihw_to_ohwi16(dev(w)), ci)
+    ein, ws = dev(np.array([-3], np.int8)), dev(np.array([-5], np.int8))
+    eo = T.zeros(1, dtype=T.int8, device="cuda")
+    amax = ops.new_range()
+    st = ops.RowConvState()
+    kw = dict(exp_in=ein, wscale=ws, exp_out=eo, relu=relu, pool=pool, next_c32=True)
+    if mode == 0:
+        out, pout, nxt = ops.conv_fwd_rows(gg, xc, wf, amax, mode=0, state=st, **kw)
+    else:
+        ops.conv_fwd_rows(gg, xc, wf, amax, mode=1, **kw)
+        out, pout, nxt = ops.conv_fwd_rows(gg, xc, wf, amax, mode=2, **kw)
+    T.cuda.synchronize()
+    assert int(st.err.item()) == 0
+    got = out.cpu().numpy()[..., :co].transpose(0, 3, 1, 2)
+    assert np.array_equal(got, r_ref)
+    assert int(eo.item()) == e_ref
+    if pool:
+        p_ref = O.maxpool(r_ref)
+        assert np.array_equal(pout.cpu().numpy()[..., :co].transpose(0, 3, 1, 2), p_ref)
+        want_next = p_ref
+    else:
+        want_next = r_ref
+    nx = nxt.cpu().numpy()  # [n][cb][h][w][32]
+    nx = nx.transpose(0, 1, 4, 2, 3).reshape(n, -1, nx.shape[2], nx.shape[3])[:, :co]
+    assert np.array_equal(nx, want_next)
+    return int(np.abs(acc).max())
+
+
+@pytest.mark.parametrize("h", [2, 4, 8, 16])
+@pytest.mark.parametrize("mode", [0, 2])
+def test_rows_fwd_widths(T, h, mode):
+    for k, (n, ci, co, relu, pool) in enumerate([(3, 32, 32, True, True), (17, 64, 64, False, False),
+                                                  (1, 96, 32, True, False), (8, 32, 96, False, True)]):
+        if pool and h < 2:
+            continue
+        _case(T, n, ci, h, co, relu, pool, mode, seed=100 * h + 10 * mode + k)
+
+
+def test_rows_fwd_shift_branches(T):
+    """Small operands drive max|acc| through the raw-cast (bw <= 7), shift == 1 (bw == 8) and
+    shift > 1 branches of the rule (NITI_Conv_Int8.cpp:266-307)."""
+    seen = set()
+    for seed, (wmax, xmax) in enumerate([(1, 1), (1, 2), (1, 3), (2, 2), (2, 3), (3, 4), (127, 127)]):
+        for mode in (0, 2):
+            m = _case(T, 4, 32, 4, 32, False, False, mode, seed=900 + seed, wmax=wmax, xmax=xmax)
+            bw = 0 if m <= 1 else int(np.ceil(np.log2(m)))
+            seen.add("raw" if bw <= 7 else "one" if bw == 8 else "psto")
+    assert seen == {"raw", "one", "psto"}
+
+
+def test_rows_fwd_vgg11_conv4_shape(T):
+    """The headline layer's shape (VGG-11 conv4: 256 -> 256 at 8x8) at batch 32, fused launch."""
+    _case(T, 32, 256, 8, 256, True, True, 0, seed=4)

@@ -80,7 +80,7 @@ def scan(asm, name):
 
 
 # kernels whose fragment / operand loads are inline asm with hand-counted waits
-ASM_RING_KERNELS = r'(wgrad_p16_kernel|gemm_kernel|wgrad_taps_kernel|conv0_kernel)'
+ASM_RING_KERNELS = r'(wgrad_p16_kernel|gemm_kernel|wgrad_taps_kernel|conv0_kernel|rowconv_fwd_kernel)'
 
 
 def kernels(asm, pattern=ASM_RING_KERNELS):
