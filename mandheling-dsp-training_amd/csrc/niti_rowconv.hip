@@ -77,61 +77,57 @@ __device__ __forceinline__ v4i shift_in_right(v4i v, bool row_end) {
     return r;
 }
 
-// ---- grid barrier with the max folded in (mode FUSED) -----------------------------------------
-// State per parity (launch epoch & 1), every word on a 128-byte line of its own:
-//   cnt[8] arrivals per shard (workgroup b joins shard b & 7), mx[8] the shard's max,
-//   top_cnt shards complete, top_mx their max, gran the released {epoch, max} granule.
-// Every access is an agent-scope atomic or an sc1 (agent relaxed) access, the protocol measured
-// coherent across XCDs on gfx950 (MI355X_MICROARCH.md, inter-workgroup visibility): a workgroup
-// max-es its shard word and only then (its atomic has returned) counts itself in; the shard's last
-// arriver carries the shard max to the top, the top's last arriver releases the granule, every
-// workgroup polls the granule (one lane, s_sleep, bounded).  Launch e zeroes parity (e + 1) & 1
-// for the next launch: the previous launch that used it has completed (same stream).
+// ---- grid barrier with the range folded in (mode FUSED) ---------------------------------------
+// The requantisation needs only the tensor's bit width bw = ceil(log2 max|y|) (NITI_RangeEstimate),
+// and the bit width of a max is the max of the bit widths.  Each workgroup ORs (1 << its bw) into
+// its shard word and then adds (1 << 32) to the same 64-bit word -- two no-return atomics on ONE
+// address, so they are performed in order and no wait sits between them: once a shard's count is
+// complete, every OR of that shard is in.  One wave per workgroup polls the 8 shard words (lane s
+// reads shard s with agent-scope loads, s_sleep between polls, bounded) until every count is
+// complete; the global bw is the highest bit of the ORed words.  (The first form -- max words
+// carried up a two-level tree by returning atomics and a released granule -- took ~3 us from the
+// last arrival to the last release.)  Parity: launch e uses word set e & 1 and zeroes the other set
+// for launch e + 1 (the launch that used it last has completed: same stream).
 constexpr int BAR_LINE = 32;                         // words per 128-byte line
-constexpr int BAR_WORDS = (8 + 8 + 3) * BAR_LINE;    // one parity
+constexpr int BAR_WORDS = 19 * BAR_LINE;             // one parity (8 shard lines used)
 static_assert(2 * BAR_WORDS == ROWCONV_BAR_WORDS, "barrier state size");
 constexpr uint32_t BAR_SPIN_LIMIT = 1u << 22;
 
-__device__ __forceinline__ uint32_t* bar_word(uint32_t* base, int line) { return base + line * BAR_LINE; }
+__device__ __forceinline__ unsigned long long* bar_shard(uint32_t* base, int s) {
+    return (unsigned long long*)(base + s * BAR_LINE);
+}
 
-__device__ uint32_t grid_max_barrier(uint32_t* state, uint32_t epoch, uint32_t m, uint32_t* err) {
+// called by one whole wave of each workgroup (lane 0's bw); returns the grid's bw to every lane
+__device__ int grid_bw_barrier(uint32_t* state, uint32_t epoch, int bw, uint32_t* err, int lane) {
     uint32_t* S = state + (epoch & 1) * BAR_WORDS;
-    const int nwg = gridDim.x;
-    const int b = blockIdx.x;
-    if (b == 0) {  // reset the other parity for the next launch
-        uint32_t* T = state + ((epoch + 1) & 1) * BAR_WORDS;
-        for (int l = 0; l < 19; ++l) __hip_atomic_store(bar_word(T, l), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        unsigned long long* tg = (unsigned long long*)bar_word(T, 18);
-        __hip_atomic_store(tg, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    const int nwg = gridDim.x, b = blockIdx.x;
     const int nsh = nwg < 8 ? nwg : 8;
-    const int sh = b % nsh;
-    const uint32_t expect = (uint32_t)((nwg - sh + nsh - 1) / nsh);  // workgroups b' < nwg with b' % nsh == sh
-    (void)__hip_atomic_fetch_max(bar_word(S, 8 + sh), m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const uint32_t old = __hip_atomic_fetch_add(bar_word(S, sh), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    unsigned long long* gran = (unsigned long long*)bar_word(S, 18);
-    if (old == expect - 1) {  // this shard is complete: its max to the top
-        const uint32_t smax = __hip_atomic_fetch_max(bar_word(S, 8 + sh), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        (void)__hip_atomic_fetch_max(bar_word(S, 17), smax, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const uint32_t t = __hip_atomic_fetch_add(bar_word(S, 16), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (t == (uint32_t)nsh - 1) {  // every shard is in: release
-            const uint32_t g = __hip_atomic_fetch_max(bar_word(S, 17), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __hip_atomic_store(gran, ((unsigned long long)epoch << 32) | g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+    if (b == 0 && lane < 8)  // reset the other parity for the next launch
+        __hip_atomic_store(bar_shard(state + ((epoch + 1) & 1) * BAR_WORDS, lane), 0ull, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 0) {
+        unsigned long long* w = bar_shard(S, b % nsh);
+        __hip_atomic_fetch_or(w, 1ull << bw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(w, 1ull << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    // lane s < nsh polls shard s until its count is complete
+    const uint32_t expect = lane < nsh ? (uint32_t)((nwg - lane + nsh - 1) / nsh) : 0u;
     uint32_t spins = 0;
+    unsigned long long v = 0;
     for (;;) {
-        const unsigned long long v = __hip_atomic_load(gran, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if ((uint32_t)(v >> 32) == epoch) return (uint32_t)v;
+        v = lane < nsh ? __hip_atomic_load(bar_shard(S, lane), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+        const bool done = (uint32_t)(v >> 32) >= expect;
+        if (__all(done)) break;
         if (++spins > BAR_SPIN_LIMIT) {  // never hang the GPU: flag it and go on (results invalid)
-            __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            return 0xffffffffu;
+            if (lane == 0) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return 31;
         }
-        __builtin_amdgcn_s_sleep(2);
+        __builtin_amdgcn_s_sleep(1);
     }
+    uint32_t bits = (uint32_t)v;
+#pragma unroll
+    for (int o = 1; o < 8; o <<= 1) bits |= __shfl_xor(bits, o, 64);
+    return bits == 0u ? 0 : 31 - __clz((int)bits);
 }
 
 struct RowConvArgs {
@@ -189,7 +185,7 @@ struct RowUnit {
     }
 };
 
-constexpr int RC_MAX_STAGES = 3;
+constexpr int RC_MAX_STAGES = 4;
 constexpr int RC_PIECES = 12;               // 9 KiB of fragments as 3 x 1 KiB DMA per wave (3 dummies)
 constexpr int RC_STAGE_BYTES = RC_PIECES * 1024;
 constexpr int RC_LDS_BYTES = RC_MAX_STAGES * RC_STAGE_BYTES;
@@ -213,7 +209,7 @@ __device__ __forceinline__ void rowconv_compute(const RowConvArgs& a, const RowU
     // issuing loads on conv4)
     constexpr bool DPPX = true;
     constexpr int KXL = DPPX ? 1 : 3;        // loads per row and chunk
-    constexpr int S = 3;                     // chunks in flight
+    constexpr int S = 4;                     // ring stages: chunk c computes, c + 1 .. c + 3 in flight
     constexpr int L = KXL * NR + 3;          // vector-memory instructions per wave per chunk
     const int h = lane >> 5, c = lane & 31, ox = c % W;
     const __amdgpu_buffer_rsrc_t rX = make_rsrc(a.x, a.xbytes);
@@ -259,36 +255,42 @@ __device__ __forceinline__ void rowconv_compute(const RowConvArgs& a, const RowU
     const uint32_t lds_lane = lds_addr(smem) + (uint32_t)lane * 16u;
     unsigned long long t_wait = 0, t_read = 0, t_issue = 0;
     const bool stamp = a.stamps != nullptr;
-    auto step = [&](auto st_c, int cc) {
+    // Software pipeline, per step c: wait for chunk c + 1's own loads (c + 2 stays in flight) and
+    // meet at the barrier (chunk c + 1's weights are in LDS, chunk c - 1's stage is free), refill
+    // that stage with chunk c + 3, read chunk c + 1's weight fragments (landing while chunk c's MFMAs
+    // run), shift chunk c's rows and run its 9 R MFMAs.
+    v4i wreg[2][9];
+    auto read_w = [&](auto st_c, v4i (&w)[9]) {
         constexpr int ST = decltype(st_c)::value;
-        const unsigned long long s0 = stamp ? __builtin_amdgcn_s_memtime() : 0ull;
-        // own loads of chunk cc landed (the S - 2 later chunks' may still be in flight), then the
-        // barrier: every wave's DMA of chunk cc is in LDS, and every wave is done with the stage
-        // the next issue refills (chunk cc - 1's: read before that chunk's MFMAs)
-        const int later = cb - 1 - cc < S - 2 ? cb - 1 - cc : S - 2;
+#pragma unroll
+        for (int t = 0; t < 9; ++t) w[t] = lds_b128(lds_lane + (uint32_t)(ST * RC_STAGE_BYTES + t * 1024));
+    };
+    auto fence_w = [&](v4i (&w)[9]) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int t = 0; t < 9; ++t) reg_fence(w[t]);
+    };
+    auto arrive = [&](int later) {
         if (later >= 1)
             asm volatile("s_waitcnt vmcnt(%0)" ::"n"(L) : "memory");
         else
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
+    };
+    auto step = [&](auto st_c, int cc) {
+        constexpr int ST = decltype(st_c)::value, WB = ST & 1;
+        const unsigned long long s0 = stamp ? __builtin_amdgcn_s_memtime() : 0ull;
+        const bool more = cc + 1 < cb;
+        if (more) arrive(cc + 2 < cb ? 1 : 0);
         const unsigned long long s1 = stamp ? __builtin_amdgcn_s_memtime() : 0ull;
-        if (cc + S - 1 < cb) issue(std::integral_constant<int, (ST + S - 1) % S>(), cc + S - 1);
+        if (cc + 3 < cb) issue(std::integral_constant<int, (ST + 3) % S>(), cc + 3);
         if (stamp) {
             asm volatile("" ::: "memory");
             t_issue += __builtin_amdgcn_s_memtime() - s1;
         }
-        v4i w[9];
-#pragma unroll
-        for (int t = 0; t < 9; ++t) w[t] = lds_b128(lds_lane + (uint32_t)(ST * RC_STAGE_BYTES + t * 1024));
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-        for (int t = 0; t < 9; ++t) reg_fence(w[t]);
-        if (stamp) {
-            const unsigned long long s2 = __builtin_amdgcn_s_memtime();
-            t_wait += s1 - s0;
-            t_read += s2 - s1;
-        }
+        if (more) read_w(std::integral_constant<int, (ST + 1) % S>(), wreg[1 - WB]);
+        const v4i (&w)[9] = wreg[WB];
         if constexpr (DPPX) {
             v4i XL[NR], XR[NR];
 #pragma unroll
@@ -313,19 +315,29 @@ __device__ __forceinline__ void rowconv_compute(const RowConvArgs& a, const RowU
                     for (int kx = 0; kx < 3; ++kx)
                         acc[r] = __builtin_amdgcn_mfma_i32_32x32x32_i8(w[3 * ky + kx], X[ST][kx][r + ky], acc[r], 0, 0, 0);
         }
+        const unsigned long long s2 = stamp ? __builtin_amdgcn_s_memtime() : 0ull;
+        if (more) fence_w(wreg[1 - WB]);
+        if (stamp) {
+            t_wait += s1 - s0;
+            t_read += __builtin_amdgcn_s_memtime() - s2;
+        }
     };
 #pragma unroll
-    for (int k = 0; k + 1 < S; ++k)
+    for (int k = 0; k < S - 1; ++k)
         if (k < cb) {
             if (k == 0) issue(std::integral_constant<int, 0>(), 0);
             if (k == 1) issue(std::integral_constant<int, 1>(), 1);
+            if (k == 2) issue(std::integral_constant<int, 2>(), 2);
         }
+    arrive(cb > 1 ? 1 : 0);  // chunk 0 (chunk 1 / 2 may stay in flight: the wait keeps L per later chunk)
+    read_w(std::integral_constant<int, 0>(), wreg[0]);
+    fence_w(wreg[0]);
     if (stamp && lane == 0) a.stamps[(blockIdx.x * 4 + wid) * 16 + 1] = __builtin_amdgcn_s_memtime();
     for (int cc = 0; cc < cb; cc += S) {
         step(std::integral_constant<int, 0>(), cc);
-        if (cc + 1 < cb) step(std::integral_constant<int, 1 % S>(), cc + 1);
-        if constexpr (S > 2)
-            if (cc + 2 < cb) step(std::integral_constant<int, 2 % S>(), cc + 2);
+        if (cc + 1 < cb) step(std::integral_constant<int, 1>(), cc + 1);
+        if (cc + 2 < cb) step(std::integral_constant<int, 2>(), cc + 2);
+        if (cc + 3 < cb) step(std::integral_constant<int, 3>(), cc + 3);
     }
     // the ring's LDS is reused by the next unit's prologue only after every wave's last reads
     __builtin_amdgcn_s_barrier();
@@ -465,15 +477,16 @@ __global__ void __launch_bounds__(256) rowconv_fwd_kernel(RowConvArgs a) {
         m = wave_max(m);
         if (lane == 0) red[wid] = m;
         __syncthreads();
-        if (threadIdx.x == 0) {
+        if (wid == 0) {
             const uint32_t bm = max(max(red[0], red[1]), max(red[2], red[3]));
-            if (a.stamps != nullptr) a.stamps[blockIdx.x * 64 + 8] = __builtin_amdgcn_s_memrealtime();
-            const uint32_t g = grid_max_barrier(a.bar, a.epoch, bm, a.err);
-            if (a.stamps != nullptr) a.stamps[blockIdx.x * 64 + 9] = __builtin_amdgcn_s_memrealtime();
-            gm = g;
-            if (blockIdx.x == 0) {
-                publish_max(a.amax, g);  // the layer's range, for the record
-                write_exponent(a, g);
+            if (a.stamps != nullptr && lane == 0) a.stamps[blockIdx.x * 64 + 8] = __builtin_amdgcn_s_memrealtime();
+            const int gbw = grid_bw_barrier(a.bar, a.epoch, bitwidth_rc(bm), a.err, lane);
+            if (a.stamps != nullptr && lane == 0) a.stamps[blockIdx.x * 64 + 9] = __builtin_amdgcn_s_memrealtime();
+            // the rule only needs bw: 2^bw stands for the max (bitwidth_rc(2^bw) == bw)
+            const uint32_t g = gbw == 0 ? 0u : 1u << gbw;
+            if (lane == 0) {
+                gm = g;
+                if (blockIdx.x == 0) write_exponent(a, g);
             }
         }
         __syncthreads();
