@@ -279,6 +279,31 @@ int niti_conv_fwd_rows(const niti_geom* g, const int8_t* x_c32, const int8_t* wf
     return code(niti::rowconv_fwd(r, x_c32, wf, o, mode, amax, state, epoch, err, S(stream)));
 }
 
+int niti_conv_dgrad_rows(const niti_geom* g, const int8_t* dy_c32, const int8_t* wft, const int8_t* relu_mask,
+                         const int8_t* pool_x, const int8_t* pool_y, int pool_relu, int8_t* dx, int8_t* dx_c32,
+                         int mode, uint32_t* amax, uint32_t* state, uint32_t epoch, uint32_t* err, void* stream) {
+    if (!g || !dy_c32 || !wft || !amax || mode < 0 || mode > 2) return NITI_INVALID_VALUE;
+    if ((pool_x == nullptr) != (pool_y == nullptr) || (pool_x && relu_mask)) return NITI_INVALID_VALUE;
+    if (mode != 1 && dx == nullptr) return NITI_INVALID_VALUE;
+    niti::ConvGeom r, d;
+    if (!to_geom(g, &r)) return NITI_COMPUTE_SIZE_ERROR;
+    if (!niti::rowconv_dgrad_geom(r, &d)) return NITI_NOT_SUPPORT;
+    if (mode == 0 && !niti::rowconv_fused_ok(d)) return NITI_NOT_SUPPORT;
+    niti::RowConvOut o;
+    if (pool_x != nullptr) {
+        o.pool_x = pool_x;
+        o.pool_y = pool_y;
+        o.pool_dx = dx;
+        o.pool_dx_next = dx_c32;
+        o.pool_relu = pool_relu;
+    } else {
+        o.out = dx;
+        o.next = dx_c32;
+        o.relu_mask = relu_mask;
+    }
+    return code(niti::rowconv_fwd(d, dy_c32, wft, o, mode, amax, state, epoch, err, S(stream)));
+}
+
 int niti_conv_fwd_phase1(const niti_geom* g, const int8_t* x, const int8_t* w, int32_t* acc, uint32_t* amax,
                          void* ws, size_t ws_bytes, void* stream) {
     if (!g || !x || !w || !acc || !amax) return NITI_INVALID_VALUE;

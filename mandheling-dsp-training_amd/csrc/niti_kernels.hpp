@@ -206,10 +206,24 @@ struct RowConvOut {
     const int8_t* wscale = nullptr;
     int8_t* exp_out = nullptr;
     int relu = 0;
+    // input gradient (the conv of dy with the rotated transposed weights): the previous layer's
+    // relu gradient, out = relu_mask > 0 ? q : 0 (NITI_ReluGrad_Int8) ...
+    const int8_t* relu_mask = nullptr;
+    // ... or its 2x2 max-pool gradient: q of pooled pixel p goes to the first element of the
+    // window in pool_x (2H x 2W, NHWC16) that is >= pool_y[p] (NITI_CPUPoolGrad_Int8), zero
+    // elsewhere and, with pool_relu, where pool_x <= 0; written to pool_dx (+ its C32 copy)
+    const int8_t* pool_x = nullptr;
+    const int8_t* pool_y = nullptr;
+    int8_t* pool_dx = nullptr;
+    int8_t* pool_dx_next = nullptr;
+    int pool_relu = 0;
 };
 constexpr int ROWCONV_BAR_WORDS = 2 * 19 * 32;  // grid-barrier state (both parities)
 static_assert(ROWCONV_BAR_WORDS == NITI_ROWCONV_STATE_WORDS, "header constant");
 bool rowconv_ok(const ConvGeom& g);
+// the input-gradient conv of a stride-1 pad-1 3x3 layer as a forward conv (dy -> dx, ci <-> co);
+// false if the layer's input gradient cannot run on the row kernel
+bool rowconv_dgrad_geom(const ConvGeom& layer, ConvGeom* d);
 // FUSED (one launch, in-kernel grid barrier) possible: one unit per wave, every workgroup resident
 bool rowconv_fused_ok(const ConvGeom& g);
 int rowconv_units(const ConvGeom& g);

@@ -294,6 +294,12 @@ struct Layer {
     int8_t* wf = nullptr;
     uint32_t* bar = nullptr;
     uint32_t epoch = 0;
+    // its input gradient on the same kernel (rotated transposed weights in WF, dy in C32, the
+    // previous layer's relu / pool gradient in the epilogue); dg = that conv's geometry
+    int rcd = 0;
+    ConvGeom dg{};
+    int8_t* wft = nullptr;
+    int8_t* dyc32 = nullptr;
     int64_t w_elems() const { return (int64_t)g.c_out * g.kh * g.kw * g.cip; }
     int64_t macs() const { return (int64_t)og.n * og.oh * og.ow * og.c_out * og.c_in * og.kh * og.kw; }
 };
@@ -326,11 +332,18 @@ struct Model {
     std::vector<char> xc32_valid;
     uint32_t* rc_err = nullptr;
     bool rowconv_layer(int i) const { return use_rowconv && L[i].rc; }
+    // dyc32_valid[i]: L[i].dyc32 holds L[i].dy as it is now (written by the next layer's input
+    // gradient epilogue, else converted)
+    std::vector<char> dyc32_valid;
+    bool rowconv_dgrad_layer(int i) const { return use_rowconv && L[i].rcd; }
     // refresh every rowconv layer's fragment-major weights from w (after set_weight / NITI_SGD)
     int refresh_wf(hipStream_t st) {
-        for (Layer& l : L)
+        for (Layer& l : L) {
             if (l.rc && weights_to_wf(l.w, l.g.c_out, l.g.c_in, l.g.cip, false, l.wf, st) != hipSuccess)
                 return NITI_NO_EXECUTION;
+            if (l.rcd && weights_to_wf(l.w, l.g.c_out, l.g.c_in, l.g.cip, true, l.wft, st) != hipSuccess)
+                return NITI_NO_EXECUTION;
+        }
         return NITI_NO_ERROR;
     }
     int convert_p16_inputs(hipStream_t st) {
@@ -670,6 +683,7 @@ int Model::build(int arch_, int batch_, int in_hw) {
     dp16.assign(nl, nullptr);
     dp16_valid.assign(nl, 0);
     xc32_valid.assign(nl, 0);
+    dyc32_valid.assign(nl, 0);
     rc_err = (uint32_t*)ws.alloc(64);
     if (!rc_err || hipMemset(rc_err, 0, 64) != hipSuccess) return NITI_OUT_OF_MEMORY;
     for (int i = 0; i < nl; ++i) {
@@ -712,6 +726,19 @@ int Model::build(int arch_, int batch_, int in_hw) {
             if (hipMemset(l.bar, 0, ROWCONV_BAR_WORDS * 4) != hipSuccess ||
                 hipMemset(l.wf, 0, rowconv_wf_bytes(g.c_out, g.c_in)) != hipSuccess)
                 return NITI_NO_EXECUTION;
+            // the input gradient too, where the previous layer's output (pooled 2x2 or not) is
+            // this layer's input as is
+            const Layer* pv = i > 0 ? &L[i - 1] : nullptr;
+            const bool pv_ok = pv != nullptr && !pv->flatten && pv->g.cop == g.cip &&
+                               (pv->pool ? (pv->ph == g.h && pv->pw == g.w && pv->g.oh == 2 * g.h && pv->g.ow == 2 * g.w)
+                                         : (pv->g.oh == g.h && pv->g.ow == g.w));
+            if (pv_ok && rowconv_dgrad_geom(g, &l.dg)) {
+                l.rcd = 1;
+                l.wft = (int8_t*)ws.alloc(rowconv_wf_bytes(g.c_in, g.c_out));
+                l.dyc32 = (int8_t*)ws.alloc(out_px * round_up(g.c_out, 32));
+                if (!l.wft || !l.dyc32) return NITI_OUT_OF_MEMORY;
+                if (hipMemset(l.wft, 0, rowconv_wf_bytes(g.c_in, g.c_out)) != hipSuccess) return NITI_NO_EXECUTION;
+            }
         }
         if (conv_wgrad_p16_ok(g)) {
             slab_w_bytes = std::max(slab_w_bytes, conv_wgrad_p16_workspace(g, 8));
@@ -946,6 +973,39 @@ int Model::dgrad_layer(int i, hipStream_t st) {
     const ConvGeom& g = l.g;
     Layer& pv = L[i - 1];
     probe(i, 1, true, st);
+    if (rowconv_dgrad_layer(i)) {
+        // register-fed input gradient, its requantisation and the previous layer's relu / pool
+        // gradient fused; the previous layer's dy also in C32 when its own input gradient runs here
+        if (!dyc32_valid[i]) {
+            MTRY(nhwc16_to_c32(l.dy, n, g.oh * g.ow, g.cop, g.c_out, l.dyc32, st));
+            dyc32_valid[i] = 1;
+        }
+        RowConvOut o;
+        int8_t* next = rowconv_dgrad_layer(i - 1) ? pv.dyc32 : nullptr;
+        if (pv.pool) {
+            o.pool_x = pv.r;
+            o.pool_y = pv.p;
+            o.pool_dx = pv.dy;
+            o.pool_dx_next = next;
+            o.pool_relu = pv.relu;
+        } else {
+            o.out = pv.dy;
+            o.next = next;
+            o.relu_mask = pv.relu ? pv.r : nullptr;
+        }
+        const ConvGeom& d = l.dg;
+        if (!dp && !capturing && rowconv_fused_ok(d)) {
+            MTRY(rowconv_fwd(d, l.dyc32, l.wft, o, 0, rng(i, 1), l.bar, ++l.epoch, rc_err, st));
+        } else {
+            MTRY(rowconv_fwd(d, l.dyc32, l.wft, o, 1, rng(i, 1), nullptr, 0, nullptr, st));
+            if (dp && exact) CTRY(coll->allreduce(rng(i, 1), MAX_WORDS, COLL_MAX_U32, st));
+            MTRY(rowconv_fwd(d, l.dyc32, l.wft, o, 2, rng(i, 1), nullptr, 0, nullptr, st));
+        }
+        probe(i, 1, false, st);
+        dp16_valid[i - 1] = 0;
+        dyc32_valid[i - 1] = next != nullptr ? 1 : 0;
+        return NITI_NO_ERROR;
+    }
     MTRY(conv_dgrad_phase1(g, l.dy, l.wT, acc, rng(i, 1), slab, slab_bytes, st));
     if (dp && exact) CTRY(coll->allreduce(rng(i, 1), MAX_WORDS, COLL_MAX_U32, st));
     const ConvGeom& pg = pv.g;
@@ -1044,6 +1104,7 @@ int Model::autotune(hipStream_t st, int reps) {
         for (int op : {PLAN_FWD, PLAN_WGRAD, PLAN_DGRAD}) {
             if (op == PLAN_DGRAD && i == 0) continue;
             if (op == PLAN_FWD && rowconv_layer(i)) continue;  // no GEMM plan: the register-fed forward
+            if (op == PLAN_DGRAD && rowconv_dgrad_layer(i)) continue;
             const ConvGeom& g = L[i].g;
             const PlanKey key = conv_plan_key(op, g);
             const int k_step = conv_plan_k_step(op, g);
@@ -1145,6 +1206,7 @@ int Model::run(const int8_t* x_nchw, int exp_in, const uint8_t* images, const in
     }
     invalidate_xp16();  // the forward pass rewrites every layer input
     std::fill(xc32_valid.begin(), xc32_valid.end(), 0);
+    std::fill(dyc32_valid.begin(), dyc32_valid.end(), 0);
     MTRY(hipMemsetAsync(amax, 0, amax_bytes, st));
     if (x_nchw != nullptr) {
         MTRY(hipMemsetAsync(exp0, exp_in, 1, st));
@@ -1201,7 +1263,7 @@ int Model::run(const int8_t* x_nchw, int exp_in, const uint8_t* images, const in
         jobs[i] = SgdJob{l.dwacc, rng(i, 2), RULE_WGRAD_BW2, g.c_out, g.c_in, g.kh * g.kw, g.cip, g.cop, l.w,
                          i > 0 ? l.wT : nullptr, l.g8};
         jobs[i].wf = l.rc ? l.wf : nullptr;
-        jobs[i].wft = nullptr;
+        jobs[i].wft = l.rcd ? l.wft : nullptr;
     }
     if (dp) {  // every bucket summed and ranged on the comm stream before the update
         MTRY(hipEventRecord(ev_grads, cst));
@@ -1281,6 +1343,7 @@ int niti_model_set_weight(niti_model_t m, int layer, const int8_t* w_host, int w
         niti::oihw_to_ihwo16(tmp, l.g.c_out, l.g.c_in, l.g.kh * l.g.kw, l.g.cop, l.wT, nullptr) != hipSuccess ||
         hipMemset(l.ws_dev, (int)(int8_t)wscale, 1) != hipSuccess ||
         (l.rc && niti::weights_to_wf(l.w, l.g.c_out, l.g.c_in, l.g.cip, false, l.wf, nullptr) != hipSuccess) ||
+        (l.rcd && niti::weights_to_wf(l.w, l.g.c_out, l.g.c_in, l.g.cip, true, l.wft, nullptr) != hipSuccess) ||
         hipDeviceSynchronize() != hipSuccess)
         rc = NITI_NO_EXECUTION;
     l.wscale = (int8_t)wscale;

@@ -151,6 +151,12 @@ struct RowConvArgs {
     uint32_t epoch;
     uint32_t* err;
     unsigned long long* stamps;  // diagnostics (niti_diag_rowconv_stamps): 8 per wave, or null
+    const int8_t* relu_mask;     // input gradient: RowConvOut's relu / pool gradients
+    const int8_t* pool_x;
+    const int8_t* pool_y;
+    int8_t* pool_dx;
+    int8_t* pool_dx_next;
+    int pool_relu;
 };
 
 // diagnostic stamps, 16 per wave: [0] start, [1] prologue issued, [2] cycles issuing loads, [3] K
@@ -410,12 +416,46 @@ __device__ __forceinline__ void rowconv_epilogue(const RowConvArgs& a, const Row
     }
     const int64_t img = U.img;
     const int cb16 = U.cob * 32 + 16 * h;  // this lane's 16 channels after pack_cols
+    if (a.pool_dx != nullptr) {
+        // through the previous layer's 2x2 max pool: the window scan of maxpool_grad_tiled_kernel
+        constexpr int H2 = 2 * H, W2 = 2 * W;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const v4i pv = pack_cols(q[r]);
+            const int oy = U.b * R + r;
+            if (!U.img_ok) continue;
+            const v16c v = (v16c)pv;
+            const v16c m = *(const v16c*)(a.pool_y + ((img * H + oy) * W + ox) * a.cop + cb16);
+            v16c done = {};
+#pragma unroll
+            for (int ky = 0; ky < 2; ++ky)
+#pragma unroll
+                for (int kx = 0; kx < 2; ++kx) {
+                    const int iy = 2 * oy + ky, ix = 2 * ox + kx;
+                    const int64_t pi = ((img * H2 + iy) * W2 + ix) * a.cop + cb16;
+                    const v16c x = *(const v16c*)(a.pool_x + pi);
+                    const v16c take = (v16c)(x >= m) & ~done;
+                    done |= take;
+                    v16c d = v & take;
+                    if (a.pool_relu) d &= (v16c)(x > (v16c){});
+                    *(v16c*)(a.pool_dx + pi) = d;
+                    if (a.pool_dx_next != nullptr)
+                        *(v16c*)(a.pool_dx_next + (((img * a.COB + U.cob) * H2 + iy) * W2 + ix) * 32 + 16 * h) = d;
+                }
+        }
+        return;
+    }
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        const v4i v = pack_cols(q[r]);
+        v4i v = pack_cols(q[r]);
         const int oy = U.b * R + r;
         if (U.img_ok) {
-            *(v4i*)(a.out + ((img * H + oy) * W + ox) * a.cop + cb16) = v;
+            const int64_t po = ((img * H + oy) * W + ox) * a.cop + cb16;
+            if (a.relu_mask != nullptr) {
+                const v16c mk = *(const v16c*)(a.relu_mask + po);
+                v = (v4i)((v16c)v & (v16c)(mk > (v16c){}));
+            }
+            *(v4i*)(a.out + po) = v;
             if (a.next != nullptr && a.pool_out == nullptr)
                 *(v4i*)(a.next + (((img * a.COB + U.cob) * H + oy) * W + ox) * 32 + 16 * h) = v;
         }
@@ -602,6 +642,16 @@ bool rowconv_ok(const ConvGeom& g) {
     return true;
 }
 
+bool rowconv_dgrad_geom(const ConvGeom& l, ConvGeom* d) {
+    if (!rowconv_ok(l)) return false;
+    ConvGeom g = l;
+    g.c_in = l.c_out;
+    g.c_out = l.c_in;
+    if (!g.finalize() || g.cip != l.cop || g.cop != l.cip) return false;
+    *d = g;
+    return rowconv_ok(g);
+}
+
 // rows per band: the largest R (a power of two dividing H, at most 8: register budget) whose unit
 // count fills the chip (>= 768 waves), else R = 2, the most units; FUSED needs one unit per wave
 // and every workgroup resident (units <= 1024)
@@ -648,7 +698,10 @@ void rowconv_stamps_arm(unsigned long long* buf) { g_rc_stamps = buf; }
 hipError_t rowconv_fwd(const ConvGeom& g, const int8_t* x_c32, const int8_t* wf, const RowConvOut& o, int mode,
                        uint32_t* amax, uint32_t* bar, uint32_t epoch, uint32_t* err, hipStream_t st) {
     if (!rowconv_ok(g) || x_c32 == nullptr || wf == nullptr || amax == nullptr) return hipErrorInvalidValue;
-    if (mode != RC_RANGE && o.out == nullptr) return hipErrorInvalidValue;
+    if (mode != RC_RANGE && o.out == nullptr && o.pool_dx == nullptr) return hipErrorInvalidValue;
+    if (o.pool_dx != nullptr && (o.pool_x == nullptr || o.pool_y == nullptr || o.out != nullptr || o.pool_out != nullptr ||
+                                 o.relu_mask != nullptr || o.next != nullptr))
+        return hipErrorInvalidValue;
     RowConvArgs a{};
     const int CB = (g.c_in + 31) / 32, COB = g.cop / 32;
     const int64_t xb = (int64_t)g.n * CB * g.h * g.w * 32;
@@ -681,6 +734,12 @@ hipError_t rowconv_fwd(const ConvGeom& g, const int8_t* x_c32, const int8_t* wf,
     a.epoch = epoch;
     a.err = err;
     a.stamps = g_rc_stamps;
+    a.relu_mask = o.relu_mask;
+    a.pool_x = o.pool_x;
+    a.pool_y = o.pool_y;
+    a.pool_dx = o.pool_dx;
+    a.pool_dx_next = o.pool_dx_next;
+    a.pool_relu = o.pool_relu;
     if (o.pool_out != nullptr && (R % 2 != 0 || g.h % 2 != 0)) return hipErrorInvalidValue;
     if (mode == RC_FUSED) {
         if (bar == nullptr || err == nullptr || epoch == 0 || units > 4 * 256) return hipErrorInvalidValue;

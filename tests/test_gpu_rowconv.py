@@ -86,3 +86,76 @@ def test_rows_fwd_shift_branches(T):
 def test_rows_fwd_vgg11_conv4_shape(T):
     """The headline layer's shape (VGG-11 conv4: 256 -> 256 at 8x8) at batch 32, fused launch."""
     _case(T, 32, 256, 8, 256, True, True, 0, seed=4)
+
+
+def _dgrad_case(T, n, ci, h, co, pool, relu, mode, seed, wmax=127, dmax=127):
+    """The layer (ci -> co at h x h) input gradient on the row kernel against NITI's dgrad
+    (NITI_DeConv_Int8.cpp:294-329 requantised by the forward rule) followed by the previous
+    layer's relu gradient (NITI_ReluGrad_Int8) or its 2x2 max-pool + relu gradient
+    (NITI_CPUPoolGrad_Int8, maxpool_relu_grad)."""
+    import niti_oracle as O
+    from niti_amd import ops
+    rng = np.random.default_rng(seed)
+    g = O.geom(n, ci, h, h, co, 3, pad=1)
+    dy = rng.integers(-dmax, dmax + 1, (n, co, h, h)).astype(np.int8)
+    w = rng.integers(-wmax, wmax + 1, (co, ci, 3, 3)).astype(np.int8)
+    dq, _, acc, _ = O.conv_dgrad(g, dy, w)
+    dev = lambda a: T.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    nhwc = lambda a: ops.nchw_to_nhwc16(dev(a))  # noqa: E731
+    if pool:
+        px = rng.integers(-2, 6, (n, ci, 2 * h, 2 * h)).astype(np.int8)  # ties and non-positives
+        if relu:
+            px = np.maximum(px, 0).astype(np.int8)
+        py = O.maxpool(px)
+        want = O.maxpool_grad(px, py, dq)
+        if relu:
+            want = O.relu_grad(px, want)
+    else:
+        mk = rng.integers(-2, 3, (n, ci, h, h)).astype(np.int8)
+        want = O.relu_grad(mk, dq) if relu else dq
+    gg = ops.geom(n, ci, h, h, co, 3, pad=1)
+    dyc = ops.nhwc16_to_c32(nhwc(dy), co)
+    wft = ops.weights_to_wf(ops.oihw_to_ohwi16(dev(w)), ci, transpose=True)
+    amax = ops.new_range()
+    st = ops.RowConvState()
+    kw = dict(dx_c32=True)
+    if pool:
+        kw.update(pool_x=nhwc(px), pool_y=nhwc(py), pool_relu=relu)
+    elif relu:
+        kw.update(relu_mask=nhwc(mk))
+    if mode == 0:
+        dx, dxc = ops.conv_dgrad_rows(gg, dyc, wft, amax, mode=0, state=st, **kw)
+    else:
+        ops.conv_dgrad_rows(gg, dyc, wft, amax, mode=1, **kw)
+        dx, dxc = ops.conv_dgrad_rows(gg, dyc, wft, amax, mode=2, **kw)
+    T.cuda.synchronize()
+    assert int(st.err.item()) == 0
+    assert np.array_equal(dx.cpu().numpy()[..., :ci].transpose(0, 3, 1, 2), want)
+    nx = dxc.cpu().numpy()
+    nx = nx.transpose(0, 1, 4, 2, 3).reshape(n, -1, nx.shape[2], nx.shape[3])[:, :ci]
+    assert np.array_equal(nx, want)
+    return int(np.abs(acc).max())
+
+
+@pytest.mark.parametrize("h", [2, 4, 8, 16])
+@pytest.mark.parametrize("mode", [0, 2])
+def test_rows_dgrad_widths(T, h, mode):
+    for k, (n, ci, co, pool, relu) in enumerate([(3, 32, 32, True, True), (17, 64, 64, False, True),
+                                                  (1, 96, 32, True, False), (8, 32, 96, False, False)]):
+        _dgrad_case(T, n, ci, h, co, pool, relu, mode, seed=500 + 100 * h + 10 * mode + k)
+
+
+def test_rows_dgrad_shift_branches(T):
+    seen = set()
+    for seed, (wmax, dmax) in enumerate([(1, 1), (1, 2), (1, 3), (2, 2), (2, 3), (3, 4), (127, 127)]):
+        m = _dgrad_case(T, 4, 32, 4, 32, seed % 2 == 0, True, seed % 2, seed=700 + seed, wmax=wmax, dmax=dmax)
+        bw = 0 if m <= 1 else int(np.ceil(np.log2(m)))
+        seen.add("raw" if bw <= 7 else "one" if bw == 8 else "psto")
+    assert seen == {"raw", "one", "psto"}
+
+
+def test_rows_dgrad_vgg11_shapes(T):
+    """VGG-11's input gradients at batch 32: conv4 (256 -> 512 at 4x4, into conv3's pool) and
+    conv2 (128 -> 256 at 8x8, into conv1's pool), fused launches."""
+    _dgrad_case(T, 32, 256, 4, 512, True, True, 0, seed=41)
+    _dgrad_case(T, 32, 256, 8, 256, False, True, 0, seed=42)
