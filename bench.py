@@ -284,6 +284,7 @@ def main():
     model = NitiModel(arch, args.batch, args.in_hw)
     model.set_graph(args.graph)
     model.set_overlap(args.overlap and not args.no_overlap)
+    model.keep_grads(False)  # no int8 weight-gradient tap: NITI_SGD consumes the gradient in-kernel
     for i, (w, s) in enumerate(synth_weights(model.layers, seed=17)):
         model.set_weight(i, w, s)
     if world > 1:

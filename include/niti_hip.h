@@ -389,9 +389,14 @@ int niti_model_get_tap(niti_model_t m, int layer, int which, int8_t* host, size_
 /* Algorithmic int8 MACs per step (unpadded channels; no zero-dilation taps). */
 int64_t niti_model_step_macs(niti_model_t m);
 
-/* Forward convs of the stride-1 pad-1 3x3 layers on the register-fed kernel with the rescale fused
- * (niti_rowconv.hip; default 1), or on the LDS-staged GEMM + requantisation pass (0).  Results are
- * identical.  niti_model_rowconv_error: 1 if an in-kernel grid barrier ever timed out (synchronises). */
+/* Keep each step's int8 weight gradient for niti_model_get_tap(which = 1) (default 1).  With 0 the
+ * SGD kernel updates the weights from the int32 gradient without storing the int8 copy, and the
+ * tap returns NITI_INVALID_VALUE. */
+int niti_model_keep_grads(niti_model_t m, int enable);
+/* Forward convs and input gradients of the stride-1 pad-1 3x3 layers on the register-fed kernel
+ * with the rescale fused (niti_rowconv.hip; default 1), or on the LDS-staged GEMM + requantisation
+ * passes (0).  Results are identical.  niti_model_rowconv_error: 1 if an in-kernel grid barrier
+ * ever timed out (synchronises). */
 int niti_model_set_rowconv(niti_model_t m, int enable);
 int niti_model_rowconv_error(niti_model_t m);
 /* Replay the step as a hipGraph (single device only -- with a communicator attached the step

@@ -288,7 +288,7 @@ int niti_conv_dgrad_rows(const niti_geom* g, const int8_t* dy_c32, const int8_t*
     niti::ConvGeom r, d;
     if (!to_geom(g, &r)) return NITI_COMPUTE_SIZE_ERROR;
     if (!niti::rowconv_dgrad_geom(r, &d)) return NITI_NOT_SUPPORT;
-    if (mode == 0 && !niti::rowconv_fused_ok(d)) return NITI_NOT_SUPPORT;
+    if (mode == 0 && !niti::rowconv_fused_ok(d, true)) return NITI_NOT_SUPPORT;
     niti::RowConvOut o;
     if (pool_x != nullptr) {
         o.pool_x = pool_x;

@@ -225,8 +225,9 @@ bool rowconv_ok(const ConvGeom& g);
 // false if the layer's input gradient cannot run on the row kernel
 bool rowconv_dgrad_geom(const ConvGeom& layer, ConvGeom* d);
 // FUSED (one launch, in-kernel grid barrier) possible: one unit per wave, every workgroup resident
-bool rowconv_fused_ok(const ConvGeom& g);
-int rowconv_units(const ConvGeom& g);
+// dg: for the input-gradient epilogues (at most 4 rows per unit)
+bool rowconv_fused_ok(const ConvGeom& g, bool dg = false);
+int rowconv_units(const ConvGeom& g, bool dg = false);
 size_t rowconv_wf_bytes(int co, int ci);
 hipError_t nhwc16_to_c32(const int8_t* in, int n, int hw, int cp, int c, int8_t* out, hipStream_t st);
 // OHWI16 [co][9][cip] -> WF; transpose: the input-gradient conv's WF (rotate180, ci <-> co)

@@ -336,6 +336,17 @@ struct Model {
     // gradient epilogue, else converted)
     std::vector<char> dyc32_valid;
     bool rowconv_dgrad_layer(int i) const { return use_rowconv && L[i].rcd; }
+    // the int8 weight gradient of the last step kept for niti_model_get (which = 1)
+    bool keep_grads = true;
+    // IHWO16 weights of the layers whose input gradient ran on the row kernel (the SGD kernel
+    // skips them there) -- rebuilt when the GEMM input gradient takes over again
+    int refresh_wt(hipStream_t st) {
+        for (Layer& l : L)
+            if (l.rcd && ohwi16_to_ihwo16(l.w, l.g.c_out, l.g.c_in, l.g.kh * l.g.kw, l.g.cip, l.g.cop, l.wT, st) !=
+                             hipSuccess)
+                return NITI_NO_EXECUTION;
+        return NITI_NO_ERROR;
+    }
     // refresh every rowconv layer's fragment-major weights from w (after set_weight / NITI_SGD)
     int refresh_wf(hipStream_t st) {
         for (Layer& l : L) {
@@ -994,7 +1005,7 @@ int Model::dgrad_layer(int i, hipStream_t st) {
             o.relu_mask = pv.relu ? pv.r : nullptr;
         }
         const ConvGeom& d = l.dg;
-        if (!dp && !capturing && rowconv_fused_ok(d)) {
+        if (!dp && !capturing && rowconv_fused_ok(d, true)) {
             MTRY(rowconv_fwd(d, l.dyc32, l.wft, o, 0, rng(i, 1), l.bar, ++l.epoch, rc_err, st));
         } else {
             MTRY(rowconv_fwd(d, l.dyc32, l.wft, o, 1, rng(i, 1), nullptr, 0, nullptr, st));
@@ -1260,8 +1271,10 @@ int Model::run(const int8_t* x_nchw, int exp_in, const uint8_t* images, const in
         // in one launch after the backward pass (the input gradients above read the old weights)
         Layer& l = L[i];
         const ConvGeom& g = l.g;
+        // the IHWO16 transpose feeds only the GEMM input gradient, the int8 gradient only the
+        // niti_model_get tap (keep_grads)
         jobs[i] = SgdJob{l.dwacc, rng(i, 2), RULE_WGRAD_BW2, g.c_out, g.c_in, g.kh * g.kw, g.cip, g.cop, l.w,
-                         i > 0 ? l.wT : nullptr, l.g8};
+                         i > 0 && !rowconv_dgrad_layer(i) ? l.wT : nullptr, keep_grads ? l.g8 : nullptr};
         jobs[i].wf = l.rc ? l.wf : nullptr;
         jobs[i].wft = l.rcd ? l.wft : nullptr;
     }
@@ -1419,7 +1432,7 @@ int niti_model_get_tap(niti_model_t m, int layer, int which, int8_t* host, size_
     size_t need = 0;
     if (which == 0 || which == 2)
         need = (size_t)n * g.c_out * g.oh * g.ow;
-    else if (which == 1)
+    else if (which == 1 && m->m.keep_grads)
         need = (size_t)g.c_out * g.c_in * g.kh * g.kw;
     else
         return NITI_INVALID_VALUE;
@@ -1464,8 +1477,19 @@ int niti_model_set_overlap(niti_model_t m, int enable) {
     return NITI_NO_ERROR;
 }
 
+int niti_model_keep_grads(niti_model_t m, int enable) {
+    if (!m) return NITI_INVALID_VALUE;
+    m->m.keep_grads = enable != 0;
+    m->m.drop_graph();
+    return NITI_NO_ERROR;
+}
+
 int niti_model_set_rowconv(niti_model_t m, int enable) {
     if (!m) return NITI_INVALID_VALUE;
+    if (m->m.use_rowconv && enable == 0) {
+        const int rc = m->m.refresh_wt(nullptr);
+        if (rc != NITI_NO_ERROR || hipDeviceSynchronize() != hipSuccess) return NITI_NO_EXECUTION;
+    }
     m->m.use_rowconv = enable != 0;
     m->m.drop_graph();
     return NITI_NO_ERROR;

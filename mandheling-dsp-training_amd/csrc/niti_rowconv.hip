@@ -33,6 +33,9 @@
 #include "niti_kernels.hpp"
 #include "niti_map.hpp"
 
+#ifndef RC_EXP
+#define RC_EXP 0
+#endif
 namespace niti {
 
 __device__ __forceinline__ int bitwidth_rc(uint32_t m) { return m <= 1u ? 0 : 32 - __clz((int)(m - 1u)); }
@@ -97,8 +100,9 @@ __device__ __forceinline__ unsigned long long* bar_shard(uint32_t* base, int s) 
     return (unsigned long long*)(base + s * BAR_LINE);
 }
 
-// called by one whole wave of each workgroup (lane 0's bw); returns the grid's bw to every lane
-__device__ int grid_bw_barrier(uint32_t* state, uint32_t epoch, int bw, uint32_t* err, int lane) {
+// Called by one whole wave of each workgroup (lane 0's bw): the arrival, then -- after whatever
+// work the workgroup can do meanwhile -- the wait, which returns the grid's bw to every lane.
+__device__ void grid_bw_arrive(uint32_t* state, uint32_t epoch, int bw, int lane) {
     uint32_t* S = state + (epoch & 1) * BAR_WORDS;
     const int nwg = gridDim.x, b = blockIdx.x;
     const int nsh = nwg < 8 ? nwg : 8;
@@ -110,6 +114,12 @@ __device__ int grid_bw_barrier(uint32_t* state, uint32_t epoch, int bw, uint32_t
         __hip_atomic_fetch_or(w, 1ull << bw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_fetch_add(w, 1ull << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+}
+
+__device__ int grid_bw_wait(uint32_t* state, uint32_t epoch, uint32_t* err, int lane) {
+    uint32_t* S = state + (epoch & 1) * BAR_WORDS;
+    const int nwg = gridDim.x;
+    const int nsh = nwg < 8 ? nwg : 8;
     // lane s < nsh polls shard s until its count is complete
     const uint32_t expect = lane < nsh ? (uint32_t)((nwg - lane + nsh - 1) / nsh) : 0u;
     uint32_t spins = 0;
@@ -288,21 +298,21 @@ __device__ __forceinline__ void rowconv_compute(const RowConvArgs& a, const RowU
         constexpr int ST = decltype(st_c)::value, WB = ST & 1;
         const unsigned long long s0 = stamp ? __builtin_amdgcn_s_memtime() : 0ull;
         const bool more = cc + 1 < cb;
-        if (more) arrive(cc + 2 < cb ? 1 : 0);
+        if (more && !(RC_EXP & 2)) arrive(cc + 2 < cb ? 1 : 0);
         const unsigned long long s1 = stamp ? __builtin_amdgcn_s_memtime() : 0ull;
-        if (cc + 3 < cb) issue(std::integral_constant<int, (ST + 3) % S>(), cc + 3);
+        if (cc + 3 < cb && !(RC_EXP & 8)) issue(std::integral_constant<int, (ST + 3) % S>(), cc + 3);
         if (stamp) {
             asm volatile("" ::: "memory");
             t_issue += __builtin_amdgcn_s_memtime() - s1;
         }
-        if (more) read_w(std::integral_constant<int, (ST + 1) % S>(), wreg[1 - WB]);
-        const v4i (&w)[9] = wreg[WB];
+        if (more && !(RC_EXP & 4)) read_w(std::integral_constant<int, (ST + 1) % S>(), wreg[1 - WB]);
+        const v4i (&w)[9] = wreg[(RC_EXP & 4) ? 0 : WB];
         if constexpr (DPPX) {
             v4i XL[NR], XR[NR];
 #pragma unroll
             for (int j = 0; j < NR; ++j) {
-                XL[j] = shift_in_left<W>(X[ST][0][j], ox == 0);
-                XR[j] = shift_in_right<W>(X[ST][0][j], ox == W - 1);
+                XL[j] = (RC_EXP & 1) ? X[ST][0][j] : shift_in_left<W>(X[ST][0][j], ox == 0);
+                XR[j] = (RC_EXP & 1) ? X[ST][0][j] : shift_in_right<W>(X[ST][0][j], ox == W - 1);
             }
 #pragma unroll
             for (int r = 0; r < R; ++r)
@@ -371,9 +381,89 @@ __device__ __forceinline__ v4i pack_cols(const int8_t* q) {
     return v4i{(int)x02[0], (int)x02[1], (int)x13[0], (int)x13[1]};
 }
 
+// The input-gradient epilogue's operands (the relu mask, or the pool's input window and output),
+// loaded before the grid barrier and turned into byte masks while the barrier completes: the
+// epilogue then only ANDs the requantised gradient with them
+template <int R>
+struct EpiIn {
+    v4i x[R][4];  // pool: the 2x2 window of pool_x per row, then its routing masks
+    v4i y[R];     // pool: pool_y; relu: relu_mask, then its byte mask (one member for the tensors
+                  // at the output's own pixels: hipcc merges the two branches' loads into one)
+};
+
+// SWAR on 4 int8 lanes of a dword; a "hi" result is meaningful in bit 7 of each byte only
+constexpr uint32_t SW_H = 0x80808080u, SW_L = 0x7F7F7F7Fu;
+__device__ __forceinline__ uint32_t sw_ge_hi(uint32_t x, uint32_t m) {  // signed x >= m
+    const uint32_t ax = x ^ SW_H, bm = m ^ SW_H;  // as unsigned
+    const uint32_t t = (ax | SW_H) - (bm & SW_L);  // bit 7: low 7 bits of ax >= those of bm
+    const uint32_t d = ax ^ bm;                    // bit 7: the top bits differ -> ax's top bit decides
+    return ((d & ax) | (~d & t)) & SW_H;
+}
+__device__ __forceinline__ uint32_t sw_pos_hi(uint32_t x) {  // signed x > 0
+    const uint32_t nz = (((x & SW_L) + SW_L) | x) & SW_H;
+    return nz & ~x;
+}
+__device__ __forceinline__ uint32_t sw_expand(uint32_t hb) { return hb | (hb - (hb >> 7)); }
+
+template <int R>
+__device__ __forceinline__ void epi_masks(const RowConvArgs& a, EpiIn<R>& e) {
+    if (a.pool_dx != nullptr) {
+        // NITI_CPUPoolGrad_Int8's scan: the first window element >= the pool output takes it
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t m = (uint32_t)e.y[r][k];
+                uint32_t done = 0;
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const uint32_t x = (uint32_t)e.x[r][t][k];
+                    uint32_t take = sw_ge_hi(x, m) & ~done;
+                    done |= take;
+                    if (a.pool_relu) take &= sw_pos_hi(x);
+                    e.x[r][t][k] = (int)sw_expand(take);
+                }
+            }
+    } else if (a.relu_mask != nullptr) {
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) e.y[r][k] = (int)sw_expand(sw_pos_hi((uint32_t)e.y[r][k]));
+    }
+}
+
 template <int W, int R>
+__device__ __forceinline__ void epi_prefetch(const RowConvArgs& a, const RowUnit<W, R>& U, int lane, EpiIn<R>& e) {
+    constexpr int H = W;
+    const int h = lane >> 5, ox = (lane & 31) % W;
+    const int64_t img = U.img_ok ? U.img : 0;
+    const int cb16 = U.cob * 32 + 16 * h;
+    // the offsets pass through an empty asm: the loads cannot be hoisted into the K loop, where
+    // their registers would sit beside the operand ring
+    uint32_t z = 0;
+    asm volatile("" : "+s"(z));
+    // the tensor at the output's own pixels (pool_y or relu_mask) in one branch-free load per row
+    // (two branches writing e.y were merged by hipcc through a scratch array)
+    const bool pool = a.pool_dx != nullptr;
+    const int8_t* ps = (pool ? a.pool_y : a.relu_mask) + z;
+    const int8_t* px = a.pool_x + z;
+    if (!pool && a.relu_mask == nullptr) return;
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+        e.y[r] = *(const v4i*)(ps + ((img * H + U.b * R + r) * W + ox) * a.cop + cb16);
+    if (pool) {
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+                e.x[r][t] = *(const v4i*)(px + ((img * 2 * H + 2 * (U.b * R + r) + (t >> 1)) * 2 * W + 2 * ox + (t & 1)) *
+                                                   a.cop + cb16);
+    }
+}
+
+template <int W, int R, bool DG>
 __device__ __forceinline__ void rowconv_epilogue(const RowConvArgs& a, const RowUnit<W, R>& U, int lane,
-                                                 const v16i (&acc)[R], uint32_t gmax) {
+                                                 const v16i (&acc)[R], uint32_t gmax, const EpiIn<DG ? R : 1>& e) {
     constexpr int H = W;
     const int h = lane >> 5, c = lane & 31, ox = c % W;
     // NITI_Conv_Int8.cpp:266-307 with wave-uniform branches: shift <= 0 the raw int8 cast, else
@@ -416,32 +506,22 @@ __device__ __forceinline__ void rowconv_epilogue(const RowConvArgs& a, const Row
     }
     const int64_t img = U.img;
     const int cb16 = U.cob * 32 + 16 * h;  // this lane's 16 channels after pack_cols
-    if (a.pool_dx != nullptr) {
+    if (DG && a.pool_dx != nullptr) {
         // through the previous layer's 2x2 max pool: the window scan of maxpool_grad_tiled_kernel
         constexpr int H2 = 2 * H, W2 = 2 * W;
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            const v4i pv = pack_cols(q[r]);
+            const v4i v = pack_cols(q[r]);
             const int oy = U.b * R + r;
             if (!U.img_ok) continue;
-            const v16c v = (v16c)pv;
-            const v16c m = *(const v16c*)(a.pool_y + ((img * H + oy) * W + ox) * a.cop + cb16);
-            v16c done = {};
 #pragma unroll
-            for (int ky = 0; ky < 2; ++ky)
-#pragma unroll
-                for (int kx = 0; kx < 2; ++kx) {
-                    const int iy = 2 * oy + ky, ix = 2 * ox + kx;
-                    const int64_t pi = ((img * H2 + iy) * W2 + ix) * a.cop + cb16;
-                    const v16c x = *(const v16c*)(a.pool_x + pi);
-                    const v16c take = (v16c)(x >= m) & ~done;
-                    done |= take;
-                    v16c d = v & take;
-                    if (a.pool_relu) d &= (v16c)(x > (v16c){});
-                    *(v16c*)(a.pool_dx + pi) = d;
-                    if (a.pool_dx_next != nullptr)
-                        *(v16c*)(a.pool_dx_next + (((img * a.COB + U.cob) * H2 + iy) * W2 + ix) * 32 + 16 * h) = d;
-                }
+            for (int t = 0; t < 4; ++t) {
+                const int iy = 2 * oy + (t >> 1), ix = 2 * ox + (t & 1);
+                const v4i d = v & e.x[DG ? r : 0][t];  // the routing mask (epi_masks)
+                *(v4i*)(a.pool_dx + ((img * H2 + iy) * W2 + ix) * a.cop + cb16) = d;
+                if (a.pool_dx_next != nullptr)
+                    *(v4i*)(a.pool_dx_next + (((img * a.COB + U.cob) * H2 + iy) * W2 + ix) * 32 + 16 * h) = d;
+            }
         }
         return;
     }
@@ -451,10 +531,7 @@ __device__ __forceinline__ void rowconv_epilogue(const RowConvArgs& a, const Row
         const int oy = U.b * R + r;
         if (U.img_ok) {
             const int64_t po = ((img * H + oy) * W + ox) * a.cop + cb16;
-            if (a.relu_mask != nullptr) {
-                const v16c mk = *(const v16c*)(a.relu_mask + po);
-                v = (v4i)((v16c)v & (v16c)(mk > (v16c){}));
-            }
+            if (DG && a.relu_mask != nullptr) v &= e.y[DG ? r : 0];
             *(v4i*)(a.out + po) = v;
             if (a.next != nullptr && a.pool_out == nullptr)
                 *(v4i*)(a.next + (((img * a.COB + U.cob) * H + oy) * W + ox) * 32 + 16 * h) = v;
@@ -498,8 +575,9 @@ __device__ __forceinline__ uint32_t max_abs16(const v16i& v, uint32_t m) {
     return m;
 }
 
-template <int W, int R, int MODE>
-__global__ void __launch_bounds__(256) rowconv_fwd_kernel(RowConvArgs a) {
+// DG: the input-gradient epilogues (relu mask / pool gradient), their operands prefetched
+template <int W, int R, int MODE, bool DG>
+__global__ void __launch_bounds__(256, (RC_EXP & 16) ? 2 : 1) rowconv_fwd_kernel(RowConvArgs a) {
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: DMA bases stay scalar
     const int c = lane & 31;
@@ -512,6 +590,8 @@ __global__ void __launch_bounds__(256) rowconv_fwd_kernel(RowConvArgs a) {
         const RowUnit<W, R> U(a, blockIdx.x, wid, c);
         uint32_t m = 0;
         rowconv_compute<W, R>(a, U, lane, wid, smem, acc);
+        EpiIn<DG ? R : 1> ein = {};
+        if constexpr (DG) epi_prefetch<W, R>(a, U, lane, ein);
 #pragma unroll
         for (int r = 0; r < R; ++r) m = max_abs16(acc[r], m);
         m = wave_max(m);
@@ -520,7 +600,11 @@ __global__ void __launch_bounds__(256) rowconv_fwd_kernel(RowConvArgs a) {
         if (wid == 0) {
             const uint32_t bm = max(max(red[0], red[1]), max(red[2], red[3]));
             if (a.stamps != nullptr && lane == 0) a.stamps[blockIdx.x * 64 + 8] = __builtin_amdgcn_s_memrealtime();
-            const int gbw = grid_bw_barrier(a.bar, a.epoch, bitwidth_rc(bm), a.err, lane);
+            grid_bw_arrive(a.bar, a.epoch, bitwidth_rc(bm), lane);
+        }
+        if constexpr (DG) epi_masks<R>(a, ein);  // while the barrier completes
+        if (wid == 0) {
+            const int gbw = grid_bw_wait(a.bar, a.epoch, a.err, lane);
             if (a.stamps != nullptr && lane == 0) a.stamps[blockIdx.x * 64 + 9] = __builtin_amdgcn_s_memrealtime();
             // the rule only needs bw: 2^bw stands for the max (bitwidth_rc(2^bw) == bw)
             const uint32_t g = gbw == 0 ? 0u : 1u << gbw;
@@ -531,7 +615,7 @@ __global__ void __launch_bounds__(256) rowconv_fwd_kernel(RowConvArgs a) {
         }
         __syncthreads();
         RC_STAMP(4);
-        if (U.valid) rowconv_epilogue<W, R>(a, U, lane, acc, gm);
+        if (U.valid) rowconv_epilogue<W, R, DG>(a, U, lane, acc, gm, ein);
         RC_STAMP(5);
     } else if constexpr (MODE == RC_RANGE) {
         uint32_t m = 0;
@@ -552,7 +636,12 @@ __global__ void __launch_bounds__(256) rowconv_fwd_kernel(RowConvArgs a) {
         for (int wg = blockIdx.x; wg < a.wgs; wg += gridDim.x) {
             const RowUnit<W, R> U(a, wg, wid, c);
             rowconv_compute<W, R>(a, U, lane, wid, smem, acc);
-            if (U.valid) rowconv_epilogue<W, R>(a, U, lane, acc, g);
+            EpiIn<DG ? R : 1> ein = {};
+            if constexpr (DG) {
+                epi_prefetch<W, R>(a, U, lane, ein);
+                epi_masks<R>(a, ein);
+            }
+            if (U.valid) rowconv_epilogue<W, R, DG>(a, U, lane, acc, g, ein);
         }
     }
 }
@@ -655,32 +744,37 @@ bool rowconv_dgrad_geom(const ConvGeom& l, ConvGeom* d) {
 // rows per band: the largest R (a power of two dividing H, at most 8: register budget) whose unit
 // count fills the chip (>= 768 waves), else R = 2, the most units; FUSED needs one unit per wave
 // and every workgroup resident (units <= 1024)
-static int rowconv_rows(const ConvGeom& g, int* units_out) {
+static int rowconv_rows(const ConvGeom& g, bool dg, int* units_out) {
     const int W = g.w, G = 32 / W;
     const int64_t groups = (g.n + G - 1) / G, cob = g.cop / 32;
-    int R = W == 16 ? 8 : (W < 4 ? W : 4);  // register budget: at most 4 rows of 3 loaded columns
+    // register budget: 8 rows at W = 16 (DPP shifts), else 4; the input-gradient epilogue's
+    // prefetched operands (5 x 16 bytes per row) cap it at 4
+    int R = W == 16 && !dg ? 8 : (W < 4 ? W : 4);
+    if (RC_EXP & 16) R = 2;
     while (R > 2 && groups * (W / R) * cob < 768) R /= 2;
     const int64_t ngb4 = (groups * (W / R) + 3) / 4 * 4;
     *units_out = (int)(ngb4 * cob);  // waves, whole workgroups of 4
     return R;
 }
 
-int rowconv_units(const ConvGeom& g) {
+int rowconv_units(const ConvGeom& g, bool dg) {
     int u = 0;
-    (void)rowconv_rows(g, &u);
+    (void)rowconv_rows(g, dg, &u);
     return u;
 }
 
-bool rowconv_fused_ok(const ConvGeom& g) { return rowconv_ok(g) && rowconv_units(g) <= 4 * 256; }
+bool rowconv_fused_ok(const ConvGeom& g, bool dg) {
+    return rowconv_ok(g) && rowconv_units(g, dg) <= ((RC_EXP & 16) ? 8 : 4) * 256;
+}
 
-template <int MODE>
+template <int MODE, bool DG>
 static hipError_t launch_rc(int W, int R, int grid, const RowConvArgs& a, hipStream_t st) {
-#define RC_CASE(WW, RR)                                                                                       \
-    if (W == WW && R == RR) {                                                                                 \
-        hipLaunchKernelGGL((rowconv_fwd_kernel<WW, RR, MODE>), dim3((unsigned)grid), dim3(256), 0, st, a);    \
-        return hipGetLastError();                                                                             \
+#define RC_CASE(WW, RR)                                                                                        \
+    if (W == WW && R == RR) {                                                                                  \
+        hipLaunchKernelGGL((rowconv_fwd_kernel<WW, RR, MODE, DG>), dim3((unsigned)grid), dim3(256), 0, st, a); \
+        return hipGetLastError();                                                                              \
     }
-    RC_CASE(16, 8)
+    if constexpr (!DG) RC_CASE(16, 8)
     RC_CASE(16, 4)
     RC_CASE(16, 2)
     RC_CASE(8, 4)
@@ -714,8 +808,9 @@ hipError_t rowconv_fwd(const ConvGeom& g, const int8_t* x_c32, const int8_t* wf,
     a.n = g.n;
     a.CB = CB;
     a.COB = COB;
+    const bool dg = o.relu_mask != nullptr || o.pool_dx != nullptr;
     int units = 0;
-    const int R = rowconv_rows(g, &units);
+    const int R = rowconv_rows(g, dg, &units);
     const int G = 32 / g.w;
     a.nbands = g.h / R;
     a.ngb = ((g.n + G - 1) / G) * a.nbands;
@@ -742,13 +837,13 @@ hipError_t rowconv_fwd(const ConvGeom& g, const int8_t* x_c32, const int8_t* wf,
     a.pool_relu = o.pool_relu;
     if (o.pool_out != nullptr && (R % 2 != 0 || g.h % 2 != 0)) return hipErrorInvalidValue;
     if (mode == RC_FUSED) {
-        if (bar == nullptr || err == nullptr || epoch == 0 || units > 4 * 256) return hipErrorInvalidValue;
-        return launch_rc<RC_FUSED>(g.w, R, a.wgs, a, st);
+        if (bar == nullptr || err == nullptr || epoch == 0 || !rowconv_fused_ok(g, dg)) return hipErrorInvalidValue;
+        return dg ? launch_rc<RC_FUSED, true>(g.w, R, a.wgs, a, st) : launch_rc<RC_FUSED, false>(g.w, R, a.wgs, a, st);
     }
     int grid = a.wgs;
     grid = grid > 1024 ? 1024 : grid;
-    if (mode == RC_RANGE) return launch_rc<RC_RANGE>(g.w, R, grid, a, st);
-    return launch_rc<RC_REQUANT>(g.w, R, grid, a, st);
+    if (mode == RC_RANGE) return launch_rc<RC_RANGE, false>(g.w, R, grid, a, st);
+    return dg ? launch_rc<RC_REQUANT, true>(g.w, R, grid, a, st) : launch_rc<RC_REQUANT, false>(g.w, R, grid, a, st);
 }
 
 }  // namespace niti

@@ -162,6 +162,7 @@ def lib():
         "niti_model_step_macs": (i64, [vp]),
         "niti_model_set_graph": (ci, [vp, ci]),
         "niti_model_set_rowconv": (ci, [vp, ci]),
+        "niti_model_keep_grads": (ci, [vp, ci]),
         "niti_model_rowconv_error": (ci, [vp]),
         "niti_model_autotune": (ci, [vp, ci, vp]),
         "niti_model_set_overlap": (ci, [vp, ci]),

@@ -183,9 +183,15 @@ class NitiModel:
         """Replay the step as a hipGraph or launch its kernels directly (default)."""
         check(self._lib.niti_model_set_graph(self._h, int(enable)), "set_graph")
 
+    def keep_grads(self, enable: bool):
+        """Store each step's int8 weight gradient for tap(layer, 1) (default) or not: the SGD
+        kernel then updates the weights without writing the copy."""
+        check(self._lib.niti_model_keep_grads(self._h, int(enable)), "keep_grads")
+
     def set_rowconv(self, enable: bool):
-        """Forward convs of the stride-1 pad-1 3x3 layers on the register-fed kernel with the fused
-        rescale (default) or on the LDS-staged GEMM + requantisation pass; identical results."""
+        """Forward convs and input gradients of the stride-1 pad-1 3x3 layers on the register-fed
+        kernel with the fused rescale (default) or on the GEMM + requantisation passes; identical
+        results."""
         check(self._lib.niti_model_set_rowconv(self._h, int(enable)), "set_rowconv")
 
     def rowconv_error(self) -> int:

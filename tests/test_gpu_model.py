@@ -19,7 +19,7 @@ def T():
 
 
 def _run(T, arch, layers, batch, steps=2, seed=5, graph=False, reuse_buffers=True, prepare=None, overlap=True,
-         in_hw=0, classes=10, rowconv=True):
+         in_hw=0, classes=10, rowconv=True, keep_grads=True):
     """reuse_buffers: new data goes into the same device tensors every step, so with graph=True
     steps after the first replay the captured graph instead of re-capturing it.
     prepare(model, x, labels): called after one throwaway step (weights are reset after it)."""
@@ -30,7 +30,9 @@ def _run(T, arch, layers, batch, steps=2, seed=5, graph=False, reuse_buffers=Tru
     m = NitiModel(arch, batch, in_hw)
     m.set_graph(graph)
     m.set_overlap(overlap)
-    m.set_rowconv(rowconv)
+    sched = rowconv if isinstance(rowconv, (list, tuple)) else [rowconv] * steps
+    m.set_rowconv(sched[0])
+    m.keep_grads(keep_grads)
     xd = ld = None
     l0 = layers[0]
     if prepare is not None:
@@ -45,6 +47,7 @@ def _run(T, arch, layers, batch, steps=2, seed=5, graph=False, reuse_buffers=Tru
     for i in range(len(layers)):
         assert np.array_equal(m.get_weight(i), W[i])
     for step in range(steps):
+        m.set_rowconv(sched[step])  # switching paths mid-training keeps every weight copy current
         x = rng.integers(-127, 128, (batch, l0["ci"], l0["h"], l0["h"])).astype(np.int8)
         labels = rng.integers(0, classes, batch).astype(np.int32)
         exp_in = -3
@@ -62,7 +65,8 @@ def _run(T, arch, layers, batch, steps=2, seed=5, graph=False, reuse_buffers=Tru
         for i in range(len(layers)):
             assert np.array_equal(m.tap(i, 0), rec["r"][i]), ("fwd", step, i)
             assert np.array_equal(m.tap(i, 2), rec["dy"][i]), ("dy", step, i)
-            assert np.array_equal(m.tap(i, 1), rec["dw"][i]), ("dw", step, i)
+            if keep_grads:
+                assert np.array_equal(m.tap(i, 1), rec["dw"][i]), ("dw", step, i)
             assert np.array_equal(m.get_weight(i), newW[i]), ("w", step, i)
         W = newW
     assert m.rowconv_error() == 0  # no in-kernel grid barrier of the fused forward timed out
@@ -98,6 +102,16 @@ def test_vgg11_step_gemm_forward(T):
     import niti_amd
     import niti_model_ref as R
     _run(T, niti_amd.ARCH_VGG11, R.vgg11_layers(), batch=8, steps=2, seed=7, rowconv=False)
+
+
+def test_vgg11_step_path_switch_no_grad_tap(T):
+    """Row kernel -> GEMM passes -> row kernel across steps (the SGD kernel skips the IHWO16 copy
+    while the row kernel runs the input gradient; switching back rebuilds it), and the SGD step
+    without the int8 weight-gradient copy (the bench's setting)."""
+    import niti_amd
+    import niti_model_ref as R
+    _run(T, niti_amd.ARCH_VGG11, R.vgg11_layers(), batch=8, steps=4, seed=13, rowconv=[True, False, False, True],
+         keep_grads=False)
 
 
 @pytest.mark.parametrize("reuse", [True, False])

@@ -18,6 +18,8 @@ ap.add_argument("--reps", type=int, default=20)
 ap.add_argument("--layer", type=int, default=-1, help="only this VGG-11 layer index (1..7)")
 ap.add_argument("--modes", default="1,2,0")
 ap.add_argument("--stamps", action="store_true", help="per-wave in-kernel stamps (cycles) of one extra launch per mode")
+ap.add_argument("--dgrad", default="", help="time the layer's input gradient instead: 'fused' (the previous layer's "
+                "relu / pool gradient as in VGG-11) or 'plain' (requantised dx only)")
 args = ap.parse_args()
 PEAK = 256 * 4 * 2048 * 2.4e9 / 1e12
 layers = [(64, 128, 16, 1), (128, 256, 8, 0), (256, 256, 8, 1), (256, 512, 4, 0), (512, 512, 4, 1),
@@ -35,9 +37,23 @@ for li, (ci, co, h, pool) in enumerate(layers, start=1):
     wf = ops.weights_to_wf(ops.oihw_to_ohwi16(w), ci)
     amax = ops.new_range()
     res = {}
+    if args.dgrad:
+        prev_pool = li in (1, 2, 4, 6)  # conv0, conv1, conv3, conv5 pool
+        dyc = ops.nhwc16_to_c32(ops.nchw_to_nhwc16(torch.from_numpy(
+            rng.integers(-127, 128, (n, co, h, h)).astype(np.int8)).cuda()), co)
+        wft = ops.weights_to_wf(ops.oihw_to_ohwi16(w), ci, transpose=True)
+        hp = 2 * h if prev_pool else h
+        px = torch.from_numpy(np.maximum(rng.integers(-2, 6, (n, hp, hp, ci)), 0).astype(np.int8)).cuda()
+        py = torch.from_numpy(np.maximum(rng.integers(-2, 6, (n, h, h, ci)), 0).astype(np.int8)).cuda()
+        kw = {}
+        if args.dgrad == "fused":
+            kw = dict(pool_x=px, pool_y=py, pool_relu=True) if prev_pool else dict(relu_mask=px)
     for mode in [int(v) for v in args.modes.split(",")]:
-        f = lambda: ops.conv_fwd_rows(g, xc, wf, amax, mode=mode, state=st, relu=True, pool=bool(pool),  # noqa
-                                      next_c32=True)
+        if args.dgrad:
+            f = lambda: ops.conv_dgrad_rows(g, dyc, wft, amax, mode=mode, state=st, dx_c32=True, **kw)  # noqa
+        else:
+            f = lambda: ops.conv_fwd_rows(g, xc, wf, amax, mode=mode, state=st, relu=True, pool=bool(pool),  # noqa
+                                          next_c32=True)
         f()
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
