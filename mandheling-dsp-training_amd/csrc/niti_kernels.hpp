@@ -217,6 +217,8 @@ struct RowConvOut {
     int8_t* pool_dx = nullptr;
     int8_t* pool_dx_next = nullptr;
     int pool_relu = 0;
+    // input gradient: the same gradient in the weight gradient's P16 layout (rowconv_p16_ok)
+    int8_t* p16 = nullptr;
 };
 constexpr int ROWCONV_BAR_WORDS = 2 * 19 * 32;  // grid-barrier state (both parities)
 static_assert(ROWCONV_BAR_WORDS == NITI_ROWCONV_STATE_WORDS, "header constant");
@@ -224,6 +226,9 @@ bool rowconv_ok(const ConvGeom& g);
 // the input-gradient conv of a stride-1 pad-1 3x3 layer as a forward conv (dy -> dx, ci <-> co);
 // false if the layer's input gradient cannot run on the row kernel
 bool rowconv_dgrad_geom(const ConvGeom& layer, ConvGeom* d);
+// the input-gradient launch of geometry d (rowconv_dgrad_geom) can also write its output's P16
+// copy: a wave's pixels make whole 16-pixel blocks (pool: through a 2x2 pool)
+bool rowconv_p16_ok(const ConvGeom& d, bool pool);
 // FUSED (one launch, in-kernel grid barrier) possible: one unit per wave, every workgroup resident
 // dg: for the input-gradient epilogues (at most 4 rows per unit)
 bool rowconv_fused_ok(const ConvGeom& g, bool dg = false);

@@ -993,6 +993,9 @@ int Model::dgrad_layer(int i, hipStream_t st) {
         }
         RowConvOut o;
         int8_t* next = rowconv_dgrad_layer(i - 1) ? pv.dyc32 : nullptr;
+        // the previous layer's P16 dy for its weight gradient, when the launch's pixels make whole
+        // 16-pixel blocks; else wgrad_layer converts
+        o.p16 = fuse_dp16 && wgrad_p16_splits(i - 1) > 0 && rowconv_p16_ok(l.dg, pv.pool) ? dp16[i - 1] : nullptr;
         if (pv.pool) {
             o.pool_x = pv.r;
             o.pool_y = pv.p;
@@ -1013,7 +1016,7 @@ int Model::dgrad_layer(int i, hipStream_t st) {
             MTRY(rowconv_fwd(d, l.dyc32, l.wft, o, 2, rng(i, 1), nullptr, 0, nullptr, st));
         }
         probe(i, 1, false, st);
-        dp16_valid[i - 1] = 0;
+        dp16_valid[i - 1] = o.p16 != nullptr ? 1 : 0;
         dyc32_valid[i - 1] = next != nullptr ? 1 : 0;
         return NITI_NO_ERROR;
     }

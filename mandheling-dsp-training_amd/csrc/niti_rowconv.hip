@@ -167,6 +167,8 @@ struct RowConvArgs {
     int8_t* pool_dx;
     int8_t* pool_dx_next;
     int pool_relu;
+    int8_t* p16;                 // P16 [pixels/16][cop][16] copy of out / pool_dx, or null
+    int64_t p16_pixels;          // pixels of that tensor
 };
 
 // diagnostic stamps, 16 per wave: [0] start, [1] prologue issued, [2] cycles issuing loads, [3] K
@@ -205,6 +207,10 @@ constexpr int RC_MAX_STAGES = 4;
 constexpr int RC_PIECES = 12;               // 9 KiB of fragments as 3 x 1 KiB DMA per wave (3 dummies)
 constexpr int RC_STAGE_BYTES = RC_PIECES * 1024;
 constexpr int RC_LDS_BYTES = RC_MAX_STAGES * RC_STAGE_BYTES;
+// after the K loop the ring holds each wave's output tile for the P16 transpose: 32 channels x
+// (the wave's pixels: 32 R, or 128 R at the pool's input resolution) -- 16 KiB per wave at R = 4
+constexpr int RC_P16_WAVE_BYTES = 16 * 1024;
+constexpr int RC_SMEM_BYTES = RC_LDS_BYTES > 4 * RC_P16_WAVE_BYTES ? RC_LDS_BYTES : 4 * RC_P16_WAVE_BYTES;
 
 // the accumulators of one unit: acc[r][i] = y[co = cob*32 + 8(i>>2) + 4h + (i&3)][row b*R + r][col]
 // Every wave of the workgroup runs this (an invalid unit reads zeros), so the barriers match.
@@ -461,9 +467,35 @@ __device__ __forceinline__ void epi_prefetch(const RowConvArgs& a, const RowUnit
     }
 }
 
+// The wave's output tile, staged in LDS as rows of 32 channel bytes in pixel order (row =
+// (image, row, column) of the wave's pixels), leaves in the weight gradient's P16 layout: per 16-lane
+// group, two ds_read_b64_tr_b8 give lane j the 16 pixels of channel j (8 rows each), one 16-byte
+// store.  A round covers two 16-pixel blocks x 32 channels (the four groups).  ROWS: the wave's
+// band rows at the tile's resolution (R, or 2R through the pool), WD its image width.
+template <int ROWS, int WD, int G>
+__device__ __forceinline__ void p16_store(const RowConvArgs& a, int lane, const int8_t* tile, int img0, int y0, int hd,
+                                          int cob) {
+    constexpr int PPI = ROWS * WD;  // the tile's pixels per image (G images)
+    constexpr int NROWS = G * PPI;
+    static_assert(NROWS % 32 == 0 && NROWS * 32 <= RC_P16_WAVE_BYTES, "whole rounds in the wave's slot");
+    const int gi = lane >> 4, j = lane & 15, chalf = gi & 1;
+#pragma unroll
+    for (int q = 0; q < NROWS / 32; ++q) {
+        const int r0 = 16 * (2 * q + (gi >> 1));
+        const int8_t* t = tile + (r0 + (j >> 1)) * 32 + 16 * chalf + 8 * (j & 1);
+        const v2i lo = __builtin_amdgcn_ds_read_tr8_b64_v2i32((__attribute__((address_space(3))) v2i*)(t));
+        const v2i hi = __builtin_amdgcn_ds_read_tr8_b64_v2i32((__attribute__((address_space(3))) v2i*)(t + 8 * 32));
+        const int g = r0 / PPI, rem = r0 % PPI;
+        const int64_t P = ((int64_t)(img0 + g) * hd + y0 + rem / WD) * WD + rem % WD;
+        if (P < a.p16_pixels)
+            *(v4i*)(a.p16 + ((P >> 4) * a.cop + cob * 32 + 16 * chalf + j) * 16) = v4i{lo[0], lo[1], hi[0], hi[1]};
+    }
+}
+
 template <int W, int R, bool DG>
 __device__ __forceinline__ void rowconv_epilogue(const RowConvArgs& a, const RowUnit<W, R>& U, int lane,
-                                                 const v16i (&acc)[R], uint32_t gmax, const EpiIn<DG ? R : 1>& e) {
+                                                 const v16i (&acc)[R], uint32_t gmax, const EpiIn<DG ? R : 1>& e,
+                                                 int8_t* tile) {
     constexpr int H = W;
     const int h = lane >> 5, c = lane & 31, ox = c % W;
     // NITI_Conv_Int8.cpp:266-307 with wave-uniform branches: shift <= 0 the raw int8 cast, else
@@ -521,8 +553,12 @@ __device__ __forceinline__ void rowconv_epilogue(const RowConvArgs& a, const Row
                 *(v4i*)(a.pool_dx + ((img * H2 + iy) * W2 + ix) * a.cop + cb16) = d;
                 if (a.pool_dx_next != nullptr)
                     *(v4i*)(a.pool_dx_next + (((img * a.COB + U.cob) * H2 + iy) * W2 + ix) * 32 + 16 * h) = d;
+                if (a.p16 != nullptr)
+                    *(v4i*)(tile + ((((c / W) * 2 * R + 2 * r + (t >> 1)) * W2) + ix) * 32 + 16 * h) = d;
             }
         }
+        if constexpr (DG && R <= 4)
+            if (a.p16 != nullptr) p16_store<2 * R, 2 * W, 32 / W>(a, lane, tile, U.img - c / W, 2 * U.b * R, H2, U.cob);
         return;
     }
 #pragma unroll
@@ -535,8 +571,11 @@ __device__ __forceinline__ void rowconv_epilogue(const RowConvArgs& a, const Row
             *(v4i*)(a.out + po) = v;
             if (a.next != nullptr && a.pool_out == nullptr)
                 *(v4i*)(a.next + (((img * a.COB + U.cob) * H + oy) * W + ox) * 32 + 16 * h) = v;
+            if (DG && a.p16 != nullptr) *(v4i*)(tile + (((c / W) * R + r) * W + ox) * 32 + 16 * h) = v;
         }
     }
+    if constexpr (DG && (R * W >= 16 || W == 2))
+        if (a.p16 != nullptr) p16_store<R, W, 32 / W>(a, lane, tile, U.img - c / W, U.b * R, H, U.cob);
     if (a.pool_out != nullptr) {
         constexpr int HO = H / 2, WO = W / 2;
 #pragma unroll
@@ -581,7 +620,7 @@ __global__ void __launch_bounds__(256, (RC_EXP & 16) ? 2 : 1) rowconv_fwd_kernel
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: DMA bases stay scalar
     const int c = lane & 31;
-    __shared__ __attribute__((aligned(16))) int8_t smem[RC_LDS_BYTES];
+    __shared__ __attribute__((aligned(16))) int8_t smem[RC_SMEM_BYTES];
     __shared__ uint32_t red[4];
     __shared__ uint32_t gm;
     v16i acc[R];
@@ -615,7 +654,7 @@ __global__ void __launch_bounds__(256, (RC_EXP & 16) ? 2 : 1) rowconv_fwd_kernel
         }
         __syncthreads();
         RC_STAMP(4);
-        if (U.valid) rowconv_epilogue<W, R, DG>(a, U, lane, acc, gm, ein);
+        if (U.valid) rowconv_epilogue<W, R, DG>(a, U, lane, acc, gm, ein, smem + wid * RC_P16_WAVE_BYTES);
         RC_STAMP(5);
     } else if constexpr (MODE == RC_RANGE) {
         uint32_t m = 0;
@@ -641,7 +680,8 @@ __global__ void __launch_bounds__(256, (RC_EXP & 16) ? 2 : 1) rowconv_fwd_kernel
                 epi_prefetch<W, R>(a, U, lane, ein);
                 epi_masks<R>(a, ein);
             }
-            if (U.valid) rowconv_epilogue<W, R, DG>(a, U, lane, acc, g, ein);
+            if (U.valid) rowconv_epilogue<W, R, DG>(a, U, lane, acc, g, ein, smem + wid * RC_P16_WAVE_BYTES);
+            if (DG && a.p16 != nullptr) __syncthreads();  // the P16 tiles sit in the next unit's ring
         }
     }
 }
@@ -757,6 +797,15 @@ static int rowconv_rows(const ConvGeom& g, bool dg, int* units_out) {
     return R;
 }
 
+bool rowconv_p16_ok(const ConvGeom& d, bool pool) {
+    if (!rowconv_ok(d)) return false;
+    int u = 0;
+    const int R = rowconv_rows(d, true, &u), W = d.w;
+    const int64_t px = (int64_t)d.n * d.h * d.w * (pool ? 4 : 1);
+    if (px % 16 != 0) return false;
+    return pool || R * W >= 16 || (W == 2 && R == 2);
+}
+
 int rowconv_units(const ConvGeom& g, bool dg) {
     int u = 0;
     (void)rowconv_rows(g, dg, &u);
@@ -808,7 +857,7 @@ hipError_t rowconv_fwd(const ConvGeom& g, const int8_t* x_c32, const int8_t* wf,
     a.n = g.n;
     a.CB = CB;
     a.COB = COB;
-    const bool dg = o.relu_mask != nullptr || o.pool_dx != nullptr;
+    const bool dg = o.relu_mask != nullptr || o.pool_dx != nullptr || o.p16 != nullptr;
     int units = 0;
     const int R = rowconv_rows(g, dg, &units);
     const int G = 32 / g.w;
@@ -835,6 +884,9 @@ hipError_t rowconv_fwd(const ConvGeom& g, const int8_t* x_c32, const int8_t* wf,
     a.pool_dx = o.pool_dx;
     a.pool_dx_next = o.pool_dx_next;
     a.pool_relu = o.pool_relu;
+    a.p16 = o.p16;
+    a.p16_pixels = (int64_t)g.n * g.h * g.w * (o.pool_dx != nullptr ? 4 : 1);
+    if (o.p16 != nullptr && (!dg || !rowconv_p16_ok(g, o.pool_dx != nullptr))) return hipErrorInvalidValue;
     if (o.pool_out != nullptr && (R % 2 != 0 || g.h % 2 != 0)) return hipErrorInvalidValue;
     if (mode == RC_FUSED) {
         if (bar == nullptr || err == nullptr || epoch == 0 || !rowconv_fused_ok(g, dg)) return hipErrorInvalidValue;

@@ -250,23 +250,25 @@ def conv_fwd_rows(g: L.Geom, xc32, wf, amax, mode=0, state: RowConvState | None 
 
 
 def conv_dgrad_rows(g: L.Geom, dyc32, wft, amax, mode=0, state: RowConvState | None = None, relu_mask=None,
-                    pool_x=None, pool_y=None, pool_relu=False, dx_c32=False, stream=None):
+                    pool_x=None, pool_y=None, pool_relu=False, dx_c32=False, dx_p16=False, stream=None):
     """The input gradient on the register-fed kernel (niti_conv_dgrad_rows) for the layer of
-    geometry g: (dx NHWC16, dx C32 or None).  dx is [n][h][w][cip], or [n][2h][2w][cip] routed
-    through the previous layer's 2x2 max pool when pool_x / pool_y are given."""
+    geometry g: (dx NHWC16, dx C32 or None, dx P16 or None).  dx is [n][h][w][cip], or
+    [n][2h][2w][cip] routed through the previous layer's 2x2 max pool when pool_x / pool_y are
+    given."""
     dev = dyc32.device
     hh, ww = (2 * g.h, 2 * g.w) if pool_x is not None else (g.h, g.w)
     dx = None if mode == 1 else torch.empty((g.n, hh, ww, g.cip), dtype=torch.int8, device=dev)
     nxt = torch.empty((g.n, g.cip // 32, hh, ww, 32), dtype=torch.int8, device=dev) if dx_c32 and mode != 1 else None
+    p16 = torch.empty((g.n * hh * ww // 16, g.cip, 16), dtype=torch.int8, device=dev) if dx_p16 and mode != 1 else None
     st_ptr = err_ptr = None
     epoch = 0
     if mode == 0:
         state.epoch += 1
         epoch, st_ptr, err_ptr = state.epoch, _ptr(state.state), _ptr(state.err)
     check(L.lib().niti_conv_dgrad_rows(C.byref(g), _ptr(dyc32), _ptr(wft), _ptr(relu_mask), _ptr(pool_x),
-                                       _ptr(pool_y), 1 if pool_relu else 0, _ptr(dx), _ptr(nxt), mode, _ptr(amax),
-                                       st_ptr, epoch, err_ptr, _stream(stream)), "conv_dgrad_rows")
-    return dx, nxt
+                                       _ptr(pool_y), 1 if pool_relu else 0, _ptr(dx), _ptr(nxt), _ptr(p16), mode,
+                                       _ptr(amax), st_ptr, epoch, err_ptr, _stream(stream)), "conv_dgrad_rows")
+    return dx, nxt, p16
 
 
 def conv_fwd_requant(g: L.Geom, x16, w16, amax, exp_in=None, wscale=None, exp_out=None, relu=False,

@@ -118,22 +118,32 @@ def _dgrad_case(T, n, ci, h, co, pool, relu, mode, seed, wmax=127, dmax=127):
     wft = ops.weights_to_wf(ops.oihw_to_ohwi16(dev(w)), ci, transpose=True)
     amax = ops.new_range()
     st = ops.RowConvState()
-    kw = dict(dx_c32=True)
+    kw = dict(dx_c32=True, dx_p16=True)
     if pool:
         kw.update(pool_x=nhwc(px), pool_y=nhwc(py), pool_relu=relu)
     elif relu:
         kw.update(relu_mask=nhwc(mk))
-    if mode == 0:
-        dx, dxc = ops.conv_dgrad_rows(gg, dyc, wft, amax, mode=0, state=st, **kw)
-    else:
-        ops.conv_dgrad_rows(gg, dyc, wft, amax, mode=1, **kw)
-        dx, dxc = ops.conv_dgrad_rows(gg, dyc, wft, amax, mode=2, **kw)
+    from niti_amd._lib import NitiError
+
+    def launch(**k):
+        if mode == 0:
+            return ops.conv_dgrad_rows(gg, dyc, wft, amax, mode=0, state=st, **k)
+        ops.conv_dgrad_rows(gg, dyc, wft, amax, mode=1, **k)
+        return ops.conv_dgrad_rows(gg, dyc, wft, amax, mode=2, **k)
+    try:
+        dx, dxc, p16 = launch(**kw)
+    except NitiError as e:  # no whole 16-pixel blocks per wave (4x4 images, no pool, small batch) or tensor
+        assert e.code == 2 and not pool and (h == 4 or n * h * h % 16 != 0), (e, h, pool)
+        kw["dx_p16"] = False
+        dx, dxc, p16 = launch(**kw)
     T.cuda.synchronize()
     assert int(st.err.item()) == 0
     assert np.array_equal(dx.cpu().numpy()[..., :ci].transpose(0, 3, 1, 2), want)
     nx = dxc.cpu().numpy()
     nx = nx.transpose(0, 1, 4, 2, 3).reshape(n, -1, nx.shape[2], nx.shape[3])[:, :ci]
     assert np.array_equal(nx, want)
+    if p16 is not None:  # the weight gradient's pixel blocks, as niti_nhwc16_to_p16 lays them out
+        assert np.array_equal(p16.cpu().numpy(), ops.nhwc16_to_p16(dx).cpu().numpy())
     return int(np.abs(acc).max())
 
 

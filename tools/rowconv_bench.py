@@ -50,7 +50,8 @@ for li, (ci, co, h, pool) in enumerate(layers, start=1):
             kw = dict(pool_x=px, pool_y=py, pool_relu=True) if prev_pool else dict(relu_mask=px)
     for mode in [int(v) for v in args.modes.split(",")]:
         if args.dgrad:
-            f = lambda: ops.conv_dgrad_rows(g, dyc, wft, amax, mode=mode, state=st, dx_c32=True, **kw)  # noqa
+            f = lambda: ops.conv_dgrad_rows(g, dyc, wft, amax, mode=mode, state=st, dx_c32=True,  # noqa
+                                            dx_p16=args.dgrad == "fused", **kw)
         else:
             f = lambda: ops.conv_fwd_rows(g, xc, wf, amax, mode=mode, state=st, relu=True, pool=bool(pool),  # noqa
                                           next_c32=True)
