@@ -244,6 +244,13 @@ hipError_t weights_to_wf(const int8_t* w_ohwi16, int co, int ci, int cip, bool t
 void rowconv_stamps_arm(unsigned long long* buf);
 hipError_t rowconv_fwd(const ConvGeom& g, const int8_t* x_c32, const int8_t* wf, const RowConvOut& o, int mode,
                        uint32_t* amax, uint32_t* bar, uint32_t epoch, uint32_t* err, hipStream_t st);
+// A 1x1 layer over 1x1 maps (the classifier head) on the same kernel: rows output channels of
+// Σ_k x[n][k] w[row][k] (x [n][xld], w [rows][wld], row-major), with the same epilogues (the
+// pool-gradient one routes into 2x2 windows: the head's input is a 1x1 pooled map)
+bool rowconv_fc_ok(int n, int K, int rows, bool fused);
+hipError_t rowconv_fc(int n, int K, int rows, const int8_t* x, int xld, const int8_t* w, int wld,
+                      const RowConvOut& o, int mode, uint32_t* amax, uint32_t* bar, uint32_t epoch, uint32_t* err,
+                      hipStream_t st);
 
 // ---- range estimate + requantisation ----------------------------------------------------
 hipError_t absmax_i32(const int32_t* a, int64_t n, uint32_t* amax, hipStream_t st);

@@ -336,6 +336,20 @@ struct Model {
     // gradient epilogue, else converted)
     std::vector<char> dyc32_valid;
     bool rowconv_dgrad_layer(int i) const { return use_rowconv && L[i].rcd; }
+    // the classifier head (a 1x1 conv over 1x1 maps, at most 64 outputs) on the row kernel's
+    // W = 1 path: forward, and its input gradient into the previous layer's relu / 2x2 pool
+    bool head_layer(int i) const {
+        const Layer& l = L[i];
+        const ConvGeom& g = l.g;
+        return use_rowconv && !l.col && l.bar != nullptr && g.kh == 1 && g.kw == 1 && g.h == 1 && g.w == 1 &&
+               g.c_out <= 64 && !l.pool && !l.flatten;
+    }
+    bool head_dgrad_ok(int i) const {
+        if (i == 0 || !head_layer(i)) return false;
+        const Layer& pv = L[i - 1];
+        if (pv.flatten || pv.col || pv.g.cop != L[i].g.cip) return false;
+        return pv.pool ? (pv.ph == 1 && pv.pw == 1 && pv.g.oh == 2 && pv.g.ow == 2) : (pv.g.oh == 1 && pv.g.ow == 1);
+    }
     // the int8 weight gradient of the last step kept for niti_model_get (which = 1)
     bool keep_grads = true;
     // IHWO16 weights of the layers whose input gradient ran on the row kernel (the SGD kernel
@@ -728,6 +742,10 @@ int Model::build(int arch_, int batch_, int in_hw) {
         slab_bytes = std::max(slab_bytes, conv_fwd_workspace(g));
         slab_bytes = std::max(slab_bytes, conv_dgrad_workspace(g));
         slab_w_bytes = std::max(slab_w_bytes, conv_wgrad_workspace(g));
+        if (!l.col && g.kh == 1 && g.kw == 1 && g.h == 1 && g.w == 1 && g.c_out <= 64) {  // head_layer
+            l.bar = (uint32_t*)ws.alloc(ROWCONV_BAR_WORDS * 4);
+            if (!l.bar || hipMemset(l.bar, 0, ROWCONV_BAR_WORDS * 4) != hipSuccess) return NITI_OUT_OF_MEMORY;
+        }
         if (!l.col && rowconv_ok(g)) {
             l.rc = 1;
             l.wf = (int8_t*)ws.alloc(rowconv_wf_bytes(g.c_out, g.c_in));
@@ -862,6 +880,25 @@ int Model::fwd_layer(int i, hipStream_t st) {
         probe(i, 0, false, st);
         return NITI_NO_ERROR;
     }
+    if (head_layer(i)) {
+        // the classifier head on the row kernel (W = 1): one fused launch, or range + requantise
+        RowConvOut o;
+        o.out = l.r;
+        o.exp_in = i == 0 ? exp0 : L[i - 1].exp;
+        o.wscale = l.ws_dev;
+        o.exp_out = l.exp;
+        o.relu = l.relu;
+        const int K = g.c_in, rows = g.c_out;
+        if (!dp && !capturing && rowconv_fc_ok(n, K, rows, true)) {
+            MTRY(rowconv_fc(n, K, rows, l.in, g.cip, l.w, g.cip, o, 0, rng(i, 0), l.bar, ++l.epoch, rc_err, st));
+        } else {
+            MTRY(rowconv_fc(n, K, rows, l.in, g.cip, l.w, g.cip, o, 1, rng(i, 0), nullptr, 0, nullptr, st));
+            if (dp && exact) CTRY(coll->allreduce(rng(i, 0), MAX_WORDS, COLL_MAX_U32, st));
+            MTRY(rowconv_fc(n, K, rows, l.in, g.cip, l.w, g.cip, o, 2, rng(i, 0), nullptr, 0, nullptr, st));
+        }
+        probe(i, 0, false, st);
+        return NITI_NO_ERROR;
+    }
     if (rowconv_layer(i)) {
         // register-fed forward, rescale fused: one launch with an in-kernel grid barrier (single
         // device, every workgroup resident, not inside a graph capture), else a range launch,
@@ -984,6 +1021,36 @@ int Model::dgrad_layer(int i, hipStream_t st) {
     const ConvGeom& g = l.g;
     Layer& pv = L[i - 1];
     probe(i, 1, true, st);
+    if (head_dgrad_ok(i)) {
+        // the head's input gradient on the row kernel (W = 1), into the previous layer's relu or
+        // 2x2-pool gradient (+ its C32 / P16 copies)
+        RowConvOut o;
+        int8_t* next = rowconv_dgrad_layer(i - 1) ? pv.dyc32 : nullptr;
+        if (pv.pool) {
+            o.pool_x = pv.r;
+            o.pool_y = pv.p;
+            o.pool_dx = pv.dy;
+            o.pool_dx_next = next;
+            o.pool_relu = pv.relu;
+            o.p16 = fuse_dp16 && wgrad_p16_splits(i - 1) > 0 && (4 * n) % 16 == 0 ? dp16[i - 1] : nullptr;
+        } else {
+            o.out = pv.dy;
+            o.relu_mask = pv.relu ? pv.r : nullptr;
+            next = nullptr;  // a 1x1 previous layer has no row-kernel input gradient
+        }
+        const int K = g.c_out, rows = g.c_in;
+        if (!dp && !capturing && rowconv_fc_ok(n, K, rows, true)) {
+            MTRY(rowconv_fc(n, K, rows, l.dy, g.cop, l.wT, g.cop, o, 0, rng(i, 1), l.bar, ++l.epoch, rc_err, st));
+        } else {
+            MTRY(rowconv_fc(n, K, rows, l.dy, g.cop, l.wT, g.cop, o, 1, rng(i, 1), nullptr, 0, nullptr, st));
+            if (dp && exact) CTRY(coll->allreduce(rng(i, 1), MAX_WORDS, COLL_MAX_U32, st));
+            MTRY(rowconv_fc(n, K, rows, l.dy, g.cop, l.wT, g.cop, o, 2, rng(i, 1), nullptr, 0, nullptr, st));
+        }
+        probe(i, 1, false, st);
+        dp16_valid[i - 1] = o.p16 != nullptr ? 1 : 0;
+        dyc32_valid[i - 1] = next != nullptr ? 1 : 0;
+        return NITI_NO_ERROR;
+    }
     if (rowconv_dgrad_layer(i)) {
         // register-fed input gradient, its requantisation and the previous layer's relu / pool
         // gradient fused; the previous layer's dy also in C32 when its own input gradient runs here
@@ -1119,6 +1186,7 @@ int Model::autotune(hipStream_t st, int reps) {
             if (op == PLAN_DGRAD && i == 0) continue;
             if (op == PLAN_FWD && rowconv_layer(i)) continue;  // no GEMM plan: the register-fed forward
             if (op == PLAN_DGRAD && rowconv_dgrad_layer(i)) continue;
+            if ((op == PLAN_FWD && head_layer(i)) || (op == PLAN_DGRAD && head_dgrad_ok(i))) continue;
             const ConvGeom& g = L[i].g;
             const PlanKey key = conv_plan_key(op, g);
             const int k_step = conv_plan_k_step(op, g);

@@ -169,6 +169,9 @@ struct RowConvArgs {
     int pool_relu;
     int8_t* p16;                 // P16 [pixels/16][cop][16] copy of out / pool_dx, or null
     int64_t p16_pixels;          // pixels of that tensor
+    // W = 1 (1x1 maps, the classifier head): x is row-major [n][xld], the weights row-major
+    // [rows][wld] (OHWI16 forward, IHWO16 input gradient), K the reduced channels
+    int xld, wld, K, rows;
 };
 
 // diagnostic stamps, 16 per wave: [0] start, [1] prologue issued, [2] cycles issuing loads, [3] K
@@ -372,6 +375,28 @@ __device__ __forceinline__ void rowconv_compute(const RowConvArgs& a, const RowU
     }
 }
 
+// W = 1: a 1x1 map per image, 32 images per wave (the MFMA B columns), out channels cob*32 + 0..31
+// as the A rows; K in 32-channel chunks straight from the row-major tensors (zero past K / rows / n)
+template <int R>
+__device__ __forceinline__ void fc_compute(const RowConvArgs& a, const RowUnit<1, R>& U, int lane, v16i (&acc)[R]) {
+    static_assert(R == 1, "one row");
+    const int h = lane >> 5, c = lane & 31;
+    const int row = U.cob * 32 + c;
+    const __amdgpu_buffer_rsrc_t rX = make_rsrc(a.x, a.xbytes);
+    const __amdgpu_buffer_rsrc_t rW = make_rsrc(a.wf, a.wbytes);
+    const uint32_t xo = U.img_ok ? (uint32_t)U.img * (uint32_t)a.xld : OOB;
+    const uint32_t wo = row < a.rows ? (uint32_t)row * (uint32_t)a.wld : OOB;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[0][i] = 0;
+    for (int k0 = 0; k0 < a.K; k0 += 32) {
+        const int k = k0 + 16 * h;
+        const bool kin = k < a.K;
+        const v4i wv = buf_load16(rW, kin && wo != OOB ? wo + (uint32_t)k : OOB);
+        const v4i xv = buf_load16(rX, kin && xo != OOB ? xo + (uint32_t)k : OOB);
+        acc[0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(wv, xv, acc[0], 0, 0, 0);
+    }
+}
+
 __device__ __forceinline__ uint32_t pack4(const int8_t* v) {
     return (uint32_t)(uint8_t)v[0] | (uint32_t)(uint8_t)v[1] << 8 | (uint32_t)(uint8_t)v[2] << 16 |
            (uint32_t)(uint8_t)v[3] << 24;
@@ -568,7 +593,7 @@ __device__ __forceinline__ void rowconv_epilogue(const RowConvArgs& a, const Row
         if (U.img_ok) {
             const int64_t po = ((img * H + oy) * W + ox) * a.cop + cb16;
             if (DG && a.relu_mask != nullptr) v &= e.y[DG ? r : 0];
-            *(v4i*)(a.out + po) = v;
+            if (W > 1 || cb16 < a.cop) *(v4i*)(a.out + po) = v;  // a 1x1 head's 16 channels
             if (a.next != nullptr && a.pool_out == nullptr)
                 *(v4i*)(a.next + (((img * a.COB + U.cob) * H + oy) * W + ox) * 32 + 16 * h) = v;
             if (DG && a.p16 != nullptr) *(v4i*)(tile + (((c / W) * R + r) * W + ox) * 32 + 16 * h) = v;
@@ -614,6 +639,15 @@ __device__ __forceinline__ uint32_t max_abs16(const v16i& v, uint32_t m) {
     return m;
 }
 
+template <int W, int R>
+__device__ __forceinline__ void compute_unit(const RowConvArgs& a, const RowUnit<W, R>& U, int lane, int wid,
+                                             int8_t* smem, v16i (&acc)[R]) {
+    if constexpr (W == 1)
+        fc_compute<R>(a, U, lane, acc);
+    else
+        rowconv_compute<W, R>(a, U, lane, wid, smem, acc);
+}
+
 // DG: the input-gradient epilogues (relu mask / pool gradient), their operands prefetched
 template <int W, int R, int MODE, bool DG>
 __global__ void __launch_bounds__(256, (RC_EXP & 16) ? 2 : 1) rowconv_fwd_kernel(RowConvArgs a) {
@@ -628,7 +662,7 @@ __global__ void __launch_bounds__(256, (RC_EXP & 16) ? 2 : 1) rowconv_fwd_kernel
     if constexpr (MODE == RC_FUSED) {
         const RowUnit<W, R> U(a, blockIdx.x, wid, c);
         uint32_t m = 0;
-        rowconv_compute<W, R>(a, U, lane, wid, smem, acc);
+        compute_unit<W, R>(a, U, lane, wid, smem, acc);
         EpiIn<DG ? R : 1> ein = {};
         if constexpr (DG) epi_prefetch<W, R>(a, U, lane, ein);
 #pragma unroll
@@ -660,7 +694,7 @@ __global__ void __launch_bounds__(256, (RC_EXP & 16) ? 2 : 1) rowconv_fwd_kernel
         uint32_t m = 0;
         for (int wg = blockIdx.x; wg < a.wgs; wg += gridDim.x) {
             const RowUnit<W, R> U(a, wg, wid, c);
-            rowconv_compute<W, R>(a, U, lane, wid, smem, acc);
+            compute_unit<W, R>(a, U, lane, wid, smem, acc);
 #pragma unroll
             for (int r = 0; r < R; ++r) m = max_abs16(acc[r], m);
         }
@@ -674,7 +708,7 @@ __global__ void __launch_bounds__(256, (RC_EXP & 16) ? 2 : 1) rowconv_fwd_kernel
         if (blockIdx.x == 0 && threadIdx.x == 0) write_exponent(a, g);
         for (int wg = blockIdx.x; wg < a.wgs; wg += gridDim.x) {
             const RowUnit<W, R> U(a, wg, wid, c);
-            rowconv_compute<W, R>(a, U, lane, wid, smem, acc);
+            compute_unit<W, R>(a, U, lane, wid, smem, acc);
             EpiIn<DG ? R : 1> ein = {};
             if constexpr (DG) {
                 epi_prefetch<W, R>(a, U, lane, ein);
@@ -831,6 +865,7 @@ static hipError_t launch_rc(int W, int R, int grid, const RowConvArgs& a, hipStr
     RC_CASE(4, 4)
     RC_CASE(4, 2)
     RC_CASE(2, 2)
+    RC_CASE(1, 1)
 #undef RC_CASE
     return hipErrorInvalidValue;
 }
@@ -896,6 +931,73 @@ hipError_t rowconv_fwd(const ConvGeom& g, const int8_t* x_c32, const int8_t* wf,
     grid = grid > 1024 ? 1024 : grid;
     if (mode == RC_RANGE) return launch_rc<RC_RANGE, false>(g.w, R, grid, a, st);
     return dg ? launch_rc<RC_REQUANT, true>(g.w, R, grid, a, st) : launch_rc<RC_REQUANT, false>(g.w, R, grid, a, st);
+}
+
+// A 1x1 layer over 1x1 maps (the classifier head) on the same kernel with W = 1: out[n][cop] (or
+// the input gradient's epilogues) = requant(Σ_k x[n][k] w[row][k]) for rows = cop channels.
+bool rowconv_fc_ok(int n, int K, int rows, bool fused) {
+    if (n <= 0 || K <= 0 || rows <= 0) return false;
+    const int64_t units = (int64_t)((n + 31) / 32 + 3) / 4 * 4 * ((rows + 31) / 32);
+    return !fused || units <= 4 * 256;
+}
+
+hipError_t rowconv_fc(int n, int K, int rows, const int8_t* x, int xld, const int8_t* w, int wld,
+                      const RowConvOut& o, int mode, uint32_t* amax, uint32_t* bar, uint32_t epoch, uint32_t* err,
+                      hipStream_t st) {
+    if (!rowconv_fc_ok(n, K, rows, mode == RC_FUSED) || x == nullptr || w == nullptr || amax == nullptr)
+        return hipErrorInvalidValue;
+    if (xld % 16 != 0 || wld % 16 != 0 || xld < K || wld < K) return hipErrorInvalidValue;
+    if (mode != RC_RANGE && o.out == nullptr && o.pool_dx == nullptr) return hipErrorInvalidValue;
+    if (o.pool_out != nullptr || (o.pool_dx != nullptr && (o.pool_x == nullptr || o.pool_y == nullptr)))
+        return hipErrorInvalidValue;
+    const int64_t xb = (int64_t)n * xld, wb = (int64_t)rows * wld;
+    if (xb > 0x7fffffff || wb > 0x7fffffff) return hipErrorInvalidValue;
+    RowConvArgs a{};
+    a.x = x;
+    a.wf = w;
+    a.xbytes = (uint32_t)xb;
+    a.wbytes = (uint32_t)wb;
+    a.xld = xld;
+    a.wld = wld;
+    a.K = K;
+    a.rows = rows;
+    a.n = n;
+    a.CB = 0;
+    a.COB = (rows + 31) / 32;
+    a.nbands = 1;
+    a.ngb = (n + 31) / 32;
+    a.ngb4 = (a.ngb + 3) / 4 * 4;
+    a.wgs = a.COB * a.ngb4 / 4;
+    a.out = o.out;
+    a.cop = (rows + 15) / 16 * 16;
+    a.next = o.next;
+    a.exp_in = o.exp_in;
+    a.wscale = o.wscale;
+    a.exp_out = o.exp_out;
+    a.relu = o.relu;
+    a.amax = amax;
+    a.bar = bar;
+    a.epoch = epoch;
+    a.err = err;
+    a.stamps = nullptr;
+    a.relu_mask = o.relu_mask;
+    a.pool_x = o.pool_x;
+    a.pool_y = o.pool_y;
+    a.pool_dx = o.pool_dx;
+    a.pool_dx_next = o.pool_dx_next;
+    a.pool_relu = o.pool_relu;
+    a.p16 = o.p16;
+    a.p16_pixels = (int64_t)n * (o.pool_dx != nullptr ? 4 : 1);
+    const bool dg = o.relu_mask != nullptr || o.pool_dx != nullptr || o.p16 != nullptr;
+    if (o.p16 != nullptr && (o.pool_dx == nullptr || a.p16_pixels % 16 != 0)) return hipErrorInvalidValue;
+    if (o.next != nullptr && a.cop % 32 != 0) return hipErrorInvalidValue;
+    if (mode == RC_FUSED) {
+        if (bar == nullptr || err == nullptr || epoch == 0) return hipErrorInvalidValue;
+        return dg ? launch_rc<RC_FUSED, true>(1, 1, a.wgs, a, st) : launch_rc<RC_FUSED, false>(1, 1, a.wgs, a, st);
+    }
+    const int grid = a.wgs > 1024 ? 1024 : a.wgs;
+    if (mode == RC_RANGE) return launch_rc<RC_RANGE, false>(1, 1, grid, a, st);
+    return dg ? launch_rc<RC_REQUANT, true>(1, 1, grid, a, st) : launch_rc<RC_REQUANT, false>(1, 1, grid, a, st);
 }
 
 }  // namespace niti
