@@ -2789,6 +2789,7 @@ struct Conv0 {
     uint32_t* amax;   // pass 0 out / pass 1 in
     int8_t* out;      // NHWC16 [P][cop]
     int8_t* pool_out; // [P / 4][cop] or null
+    int8_t* pool_c32; // the pooled output as the next layer's C32 input [n][cop/32][oh/2][ow/2][32], or null
     const int8_t *exp_in, *wscale;
     int8_t* exp_out;
     int relu;
@@ -2882,6 +2883,10 @@ __global__ void __launch_bounds__(256) conv0_kernel(Conv0 g) {
                     if ((c & 1) == 0) {
                         const int64_t pp = (img * (g.oh / 2) + pr) * (g.ow / 2) + seg * 16 + (c >> 1);
                         *(v4i*)(g.pool_out + pp * g.cop + t * 32 + 16 * h) = v;
+                        if (g.pool_c32 != nullptr) {
+                            const int64_t hw2 = (int64_t)(g.oh / 2) * (g.ow / 2);
+                            *(v4i*)(g.pool_c32 + ((img * tiles + t) * hw2 + pp - img * hw2) * 32 + 16 * h) = v;
+                        }
                     }
                 }
             }
@@ -2902,8 +2907,9 @@ bool conv0_ok(const ConvGeom& g) {
 }
 
 hipError_t conv0_fwd(const ConvGeom& g, const int8_t* xcol, const int8_t* w, uint32_t* amax, const ActOut& o,
-                     int pass, hipStream_t st) {
+                     int pass, hipStream_t st, int8_t* pool_c32) {
     if (!conv0_ok(g) || o.out == nullptr || o.relu_mask != nullptr) return hipErrorInvalidValue;
+    if (pool_c32 != nullptr && o.pool.pool_out == nullptr) return hipErrorInvalidValue;
     Conv0 k{};
     k.x = xcol;
     k.w = w;
@@ -2916,6 +2922,7 @@ hipError_t conv0_fwd(const ConvGeom& g, const int8_t* xcol, const int8_t* w, uin
     k.amax = amax;
     k.out = o.out;
     k.pool_out = o.pool.pool_out;
+    k.pool_c32 = pool_c32;
     k.exp_in = o.exp_in;
     k.wscale = o.wscale;
     k.exp_out = o.exp_out;

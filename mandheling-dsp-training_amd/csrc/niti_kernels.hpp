@@ -184,7 +184,8 @@ bool conv_fwd_phase2_separate(const ConvGeom& g, size_t ws_bytes);
 bool conv0_ok(const ConvGeom& g);
 // pass 0: range into amax; pass 1: requantise with it (a MAX all-reduce may sit between them)
 hipError_t conv0_fwd(const ConvGeom& g, const int8_t* xcol, const int8_t* w, uint32_t* amax, const ActOut& o,
-                     int pass, hipStream_t st);
+                     int pass, hipStream_t st,
+                     int8_t* pool_c32 = nullptr);
 bool conv_dgrad_phase2_separate(const ConvGeom& g, size_t ws_bytes);
 hipError_t conv_fwd_phase1(const ConvGeom& g, const int8_t* x, const int8_t* w, int32_t* acc, uint32_t* amax,
                            void* ws, size_t ws_bytes, hipStream_t st);
@@ -248,6 +249,10 @@ hipError_t rowconv_fwd(const ConvGeom& g, const int8_t* x_c32, const int8_t* wf,
 // Σ_k x[n][k] w[row][k] (x [n][xld], w [rows][wld], row-major), with the same epilogues (the
 // pool-gradient one routes into 2x2 windows: the head's input is a 1x1 pooled map)
 bool rowconv_fc_ok(int n, int K, int rows, bool fused);
+// its weight gradient: dw [c_out][cip] int32 = Σ_p dy[p][co] x[p][ci] (c_out <= 32, cip % 32 == 0),
+// max|dw| published into amax (may be null)
+hipError_t head_wgrad(int n, int c_out, int cip, const int8_t* x, int xld, const int8_t* dy, int dld, int32_t* dw,
+                      uint32_t* amax, hipStream_t st);
 hipError_t rowconv_fc(int n, int K, int rows, const int8_t* x, int xld, const int8_t* w, int wld,
                       const RowConvOut& o, int mode, uint32_t* amax, uint32_t* bar, uint32_t epoch, uint32_t* err,
                       hipStream_t st);
@@ -352,6 +357,20 @@ hipError_t image_stats(const uint8_t* img, int64_t n, unsigned long long* stats,
 // NCHW; *ascale = int8(ceil(ln(range)) - 7) (ascale may be null)
 hipError_t image_quantize(const uint8_t* img, int n, int c, int hw, int cp, const unsigned long long* stats,
                           int64_t count, int8_t* out, int8_t* ascale, bool nhwc16, hipStream_t st);
+// the training step's form: per-block partial statistics (IMAGE_STATS_SLOTS x 4 u64, no
+// atomics), summed by their consumer; stats_finalize sums them into stats[4] (data parallel:
+// before the all-reduce)
+constexpr int IMAGE_STATS_SLOTS = 256;
+hipError_t image_stats_slots(const uint8_t* img, int64_t n, unsigned long long* slots, int* nslots, hipStream_t st);
+hipError_t stats_finalize(const unsigned long long* slots, int nslots, unsigned long long* stats, hipStream_t st);
+// the first layer's im2col copy (xcol [n*oh*ow][32]) straight from the NCHW batch: uint8 images
+// quantised with the statistics in `slots` (nslots partials over `count` pixels), or int8 pixels
+// as they are (quant = false); x_nchw (may be null) receives the int8 input; stride 1, C / KH / KW
+// = 3/3/3 or 1/5/5 (input_im2col_ok)
+bool input_im2col_ok(int c, int kh, int kw);
+hipError_t input_im2col(const void* in, bool quant, int n, int c, int h, int w, int kh, int kw, int pt, int pl,
+                        const unsigned long long* slots, int nslots, int64_t count, int8_t* x_nchw, int8_t* xcol,
+                        int8_t* ascale, hipStream_t st);
 
 // ---- layout transforms --------------------------------------------------------------------
 // NHWC16 [N][H][W][Cp] -> CHWN16 [Cp][H][W][Np]

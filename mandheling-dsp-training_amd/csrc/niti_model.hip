@@ -465,6 +465,9 @@ struct Model {
     int sum_bucket(int hi_layer, hipStream_t wst);
     // input quantiser statistics {S1, S2, xmax, 255 - xmin} (niti_quant.hip)
     unsigned long long* qstats = nullptr;
+    unsigned long long* qslots = nullptr;  // per-block partial statistics (IMAGE_STATS_SLOTS x 4)
+    int8_t* x0n = nullptr;                 // the int8 input NCHW (written by the fused input pass)
+    bool x0_nchw_valid = false;
     // Optional hipGraph replay of the single-device step: ~95 launches become one graph launch
     // (or three when a probe splits it around the probed GEMM).  Captured on an internal
     // stream, fenced against the caller's stream with events; re-captured when the captured
@@ -785,7 +788,9 @@ int Model::build(int arch_, int batch_, int in_hw) {
     }
     acc = (int32_t*)ws.alloc(acc_elems * 4);
     qstats = (unsigned long long*)ws.alloc(64);
-    if (!qstats) return NITI_OUT_OF_MEMORY;
+    qslots = (unsigned long long*)ws.alloc((size_t)IMAGE_STATS_SLOTS * 4 * sizeof(unsigned long long));
+    x0n = (int8_t*)ws.alloc((size_t)n * in_c * in_h * in_w);
+    if (!qstats || !qslots || !x0n) return NITI_OUT_OF_MEMORY;
     if (slab_bytes) {
         slab = ws.alloc(slab_bytes);
         if (!slab) return NITI_OUT_OF_MEMORY;
@@ -874,9 +879,12 @@ int Model::fwd_layer(int i, hipStream_t st) {
         o.wscale = l.ws_dev;
         o.exp_out = l.exp;
         o.pool.pool_out = l.pool ? l.p : nullptr;
+        // the pooled output also as the next layer's C32 input when it runs on the row kernel
+        const bool next_c32 = l.pool && i + 1 < (int)L.size() && rowconv_layer(i + 1);
         MTRY(conv0_fwd(g, l.in, l.w, rng(i, 0), o, 0, st));
         if (dp && exact) CTRY(coll->allreduce(rng(i, 0), MAX_WORDS, COLL_MAX_U32, st));
-        MTRY(conv0_fwd(g, l.in, l.w, rng(i, 0), o, 1, st));
+        MTRY(conv0_fwd(g, l.in, l.w, rng(i, 0), o, 1, st, next_c32 ? L[i + 1].xc32 : nullptr));
+        if (next_c32) xc32_valid[i + 1] = 1;
         probe(i, 0, false, st);
         return NITI_NO_ERROR;
     }
@@ -962,6 +970,13 @@ int Model::wgrad_layer(int i, hipStream_t st) {
     const bool dp = this->dp();
     Layer& l = L[i];
     const ConvGeom& g = l.g;
+    if (head_layer(i) && g.c_out <= 32 && g.cip % 32 == 0) {
+        // the classifier head: one small launch, its range published (single device)
+        probe(i, 2, true, st);
+        MTRY(head_wgrad(g.n, g.c_out, g.cip, l.in, g.cip, l.dy, g.cop, l.dwacc, dp ? nullptr : rng(i, 2), st));
+        probe(i, 2, false, st);
+        return NITI_NO_ERROR;
+    }
     if (const int s = wgrad_p16_splits(i)) {
         // P16 weight gradient: x (unless run() converted every input already) and dy to pixel
         // blocks, then the register-fed kernel (+ its split-K reduce); the probe times the kernel
@@ -1187,6 +1202,7 @@ int Model::autotune(hipStream_t st, int reps) {
             if (op == PLAN_FWD && rowconv_layer(i)) continue;  // no GEMM plan: the register-fed forward
             if (op == PLAN_DGRAD && rowconv_dgrad_layer(i)) continue;
             if ((op == PLAN_FWD && head_layer(i)) || (op == PLAN_DGRAD && head_dgrad_ok(i))) continue;
+            if (op == PLAN_WGRAD && head_layer(i) && L[i].g.c_out <= 32 && L[i].g.cip % 32 == 0) continue;
             const ConvGeom& g = L[i].g;
             const PlanKey key = conv_plan_key(op, g);
             const int k_step = conv_plan_k_step(op, g);
@@ -1290,22 +1306,42 @@ int Model::run(const int8_t* x_nchw, int exp_in, const uint8_t* images, const in
     std::fill(xc32_valid.begin(), xc32_valid.end(), 0);
     std::fill(dyc32_valid.begin(), dyc32_valid.end(), 0);
     MTRY(hipMemsetAsync(amax, 0, amax_bytes, st));
+    // the first layer's im2col copy straight from the batch where the fused pass takes the layer
+    const ConvGeom& o0 = L[0].og;
+    const bool fused_in = L[0].col && input_im2col_ok(o0.c_in, o0.kh, o0.kw) && o0.sh == 1 && o0.sw == 1;
+    x0_nchw_valid = fused_in;
     if (x_nchw != nullptr) {
         MTRY(hipMemsetAsync(exp0, exp_in, 1, st));
-        MTRY(nchw_to_nhwc16(x_nchw, n, in_c, in_h * in_w, round_up(in_c, 16), x0, st));
+        if (fused_in)
+            MTRY(input_im2col(x_nchw, false, n, in_c, in_h, in_w, o0.kh, o0.kw, o0.pt, o0.pl, nullptr, 0, 0, x0n,
+                              L[0].xcol, nullptr, st));
+        else
+            MTRY(nchw_to_nhwc16(x_nchw, n, in_c, in_h * in_w, round_up(in_c, 16), x0, st));
     } else {
-        // NITIInt8Train's input quantiser (MnistUtils.cpp:83-93): batch statistics (global over
-        // the ranks in exact mode), then x and its exponent ascale straight into the layer-0 input
+        // NITIInt8Train's input quantiser (MnistUtils.cpp:83-93): batch statistics (per-block
+        // partials; summed and all-reduced over the ranks in exact mode), then x and its exponent
+        // ascale straight into the layer-0 input
         const int64_t px = (int64_t)n * in_c * in_h * in_w;
-        MTRY(image_stats(images, px, qstats, st));
+        int ns = 0;
+        MTRY(image_stats_slots(images, px, qslots, &ns, st));
+        const unsigned long long* slots = qslots;
+        if ((dp && exact) || !fused_in) {
+            MTRY(stats_finalize(qslots, ns, qstats, st));
+            slots = qstats;
+            ns = 1;
+        }
         if (dp && exact) {
             CTRY(coll->allreduce(qstats, 2, COLL_SUM_U64, st));
             CTRY(coll->allreduce(qstats + 2, 2, COLL_MAX_U64, st));
         }
-        MTRY(image_quantize(images, n, in_c, in_h * in_w, round_up(in_c, 16), qstats,
-                            dp && exact ? px * world : px, x0, exp0, true, st));
+        const int64_t count = dp && exact ? px * world : px;
+        if (fused_in)
+            MTRY(input_im2col(images, true, n, in_c, in_h, in_w, o0.kh, o0.kw, o0.pt, o0.pl, slots, ns, count, x0n,
+                              L[0].xcol, exp0, st));
+        else
+            MTRY(image_quantize(images, n, in_c, in_h * in_w, round_up(in_c, 16), qstats, count, x0, exp0, true, st));
     }
-    if (L[0].col) MTRY(im2col32(L[0].og, x0, L[0].xcol, st));
+    if (L[0].col && !fused_in) MTRY(im2col32(L[0].og, x0, L[0].xcol, st));
     for (int i = 0; i < nl; ++i) {
         const int rc = fwd_layer(i, st);
         if (rc != NITI_NO_ERROR) return rc;
@@ -1470,7 +1506,8 @@ int niti_model_get_input(niti_model_t m, int8_t* x_nchw_host, int* ascale, void*
     int8_t* tmp = nullptr;
     if (hipMalloc(&tmp, need) != hipSuccess) return NITI_OUT_OF_MEMORY;
     int8_t e = 0;
-    hipError_t err = niti::nhwc16_to_nchw(mm.x0, n, mm.in_c, hw, niti::round_up(mm.in_c, 16), tmp, nullptr);
+    hipError_t err = mm.x0_nchw_valid ? hipMemcpy(tmp, mm.x0n, need, hipMemcpyDeviceToDevice)
+                                      : niti::nhwc16_to_nchw(mm.x0, n, mm.in_c, hw, niti::round_up(mm.in_c, 16), tmp, nullptr);
     if (err == hipSuccess) err = hipMemcpy(x_nchw_host, tmp, need, hipMemcpyDeviceToHost);
     if (err == hipSuccess) err = hipMemcpy(&e, mm.exp0, 1, hipMemcpyDeviceToHost);
     (void)hipFree(tmp);

@@ -35,6 +35,7 @@ namespace niti {
 namespace {
 
 typedef signed char v16c __attribute__((ext_vector_type(16)));
+typedef int v4i_q __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -48,9 +49,11 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
     return v;
 }
 
-// stats[0] += S1, stats[1] += S2, stats[2] max= xmax, stats[3] max= 255 - xmin
+// block b's partial statistics into slots[4 b .. 4 b + 3] = {S1, S2, xmax, 255 - xmin}: plain
+// stores, no atomics (device-scope u64 atomics of many blocks on one line serialise at the memory
+// side); the consumers sum the slots (stats_from_slots)
 __global__ void __launch_bounds__(256) image_stats_kernel(const uint8_t* __restrict__ img, int64_t n,
-                                                          unsigned long long* __restrict__ stats) {
+                                                          unsigned long long* __restrict__ slots) {
     unsigned long long s1 = 0, s2 = 0;
     uint32_t mx = 0, mn = 0;  // mn holds 255 - min
     const int64_t nv = n / 16;
@@ -93,19 +96,51 @@ __global__ void __launch_bounds__(256) image_stats_kernel(const uint8_t* __restr
         r[wv][3] = mn;
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned long long t[4] = {0, 0, 0, 0};
-        for (int k = 0; k < 4; ++k) {
-            t[0] += r[k][0];
-            t[1] += r[k][1];
-            t[2] = r[k][2] > t[2] ? r[k][2] : t[2];
-            t[3] = r[k][3] > t[3] ? r[k][3] : t[3];
-        }
-        atomicAdd(&stats[0], t[0]);
-        atomicAdd(&stats[1], t[1]);
-        atomicMax(&stats[2], t[2]);
-        atomicMax(&stats[3], t[3]);
+    if (threadIdx.x < 4) {
+        const int k = threadIdx.x;
+        unsigned long long t = 0;
+        for (int w = 0; w < 4; ++w) t = k < 2 ? t + r[w][k] : (r[w][k] > t ? r[w][k] : t);
+        slots[4 * blockIdx.x + k] = t;
     }
+}
+
+// the whole block sums nslots partials (S1, S2 added, the maxima max-ed) into out[4] (shared)
+__device__ void stats_from_slots(const unsigned long long* __restrict__ slots, int nslots, unsigned long long* out) {
+    __shared__ unsigned long long r[4][4];
+    unsigned long long s1 = 0, s2 = 0;
+    uint32_t mx = 0, mn = 0;
+    for (int b = threadIdx.x; b < nslots; b += blockDim.x) {
+        s1 += slots[4 * b];
+        s2 += slots[4 * b + 1];
+        mx = max(mx, (uint32_t)slots[4 * b + 2]);
+        mn = max(mn, (uint32_t)slots[4 * b + 3]);
+    }
+    s1 = wave_sum_u64(s1);
+    s2 = wave_sum_u64(s2);
+    mx = wave_max_u32(mx);
+    mn = wave_max_u32(mn);
+    const int wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        r[wv][0] = s1;
+        r[wv][1] = s2;
+        r[wv][2] = mx;
+        r[wv][3] = mn;
+    }
+    __syncthreads();
+    if (threadIdx.x < 4) {
+        const int k = threadIdx.x;
+        unsigned long long t = 0;
+        for (int w = 0; w < nw; ++w) t = k < 2 ? t + r[w][k] : (r[w][k] > t ? r[w][k] : t);
+        out[k] = t;
+    }
+    __syncthreads();
+}
+
+__global__ void __launch_bounds__(256) stats_finalize_kernel(const unsigned long long* __restrict__ slots, int nslots,
+                                                             unsigned long long* __restrict__ stats) {
+    __shared__ unsigned long long t[4];
+    stats_from_slots(slots, nslots, t);
+    if (threadIdx.x < 4) stats[threadIdx.x] = t[threadIdx.x];
 }
 
 struct QuantParams {
@@ -186,17 +221,135 @@ __global__ void __launch_bounds__(256) image_quant_kernel(const uint8_t* __restr
     }
 }
 
+// The first layer's input straight from the batch: quantise (or take the int8 pixels as they
+// are) and write the im2col copy the K = 32 first-layer conv reads, xcol[p][(ky KW + kx) C + c]
+// (32 bytes per output pixel, zero outside the image and for k >= C KH KW), in one pass.  A
+// workgroup takes one image's band of BAND output rows: it stages the band's input rows (halo
+// included) once in LDS as 4-byte pixels (C <= 4 channels), writes its own rows' int8 pixels
+// (NCHW, the input tap), then builds each output pixel's 32 bytes from the 4-byte pixels of its
+// taps.  The quantisation parameters come from the statistics slots (stats_from_slots).
+template <int C, int KH, int KW, bool QUANT>
+__global__ void __launch_bounds__(256) input_im2col_kernel(const void* __restrict__ in, int n, int h, int w, int oh,
+                                                           int ow, int pt, int pl, int band,
+                                                           const unsigned long long* __restrict__ slots, int nslots,
+                                                           int64_t count, int64_t var_count,
+                                                           int8_t* __restrict__ x_nchw, int8_t* __restrict__ xcol,
+                                                           int8_t* __restrict__ ascale) {
+    static_assert(C <= 4 && C * KH * KW <= 32, "one 32-byte im2col row");
+    extern __shared__ __attribute__((aligned(16))) uint32_t px[];  // [rows][w + KW - 1] 4-byte pixels
+    __shared__ QuantParams sq;
+    const int bands = (oh + band - 1) / band;
+    const int img = blockIdx.x / bands, oy0 = (blockIdx.x % bands) * band;
+    const int oy1 = min(oh, oy0 + band);
+    const int iy0 = oy0 - pt, rows = oy1 - oy0 + KH - 1, wp = w + KW - 1;
+    if constexpr (QUANT) {
+        __shared__ unsigned long long st[4];
+        stats_from_slots(slots, nslots, st);
+        if (threadIdx.x == 0) {
+            sq = quant_params(st, count, var_count);
+            if (blockIdx.x == 0 && ascale != nullptr) *ascale = (int8_t)sq.ascale;
+        }
+        __syncthreads();
+    }
+    const QuantParams q = sq;
+    // input rows this band writes to the tap: [oy0, oy0 + band), the last band through h
+    const bool last = blockIdx.x % bands == bands - 1;
+    const int own0 = oy0, own1 = last ? h : oy0 + band;
+    // the band's input rows (zero halo): one thread per (row, column) of the padded band
+    for (int t = threadIdx.x; t < rows * wp; t += blockDim.x) {
+        const int r = t / wp, xx = t - r * wp;
+        const int iy = iy0 + r, ix = xx - pl;
+        uint32_t v = 0;
+        if (iy >= 0 && iy < h && ix >= 0 && ix < w) {
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                const int64_t e = (((int64_t)img * C + c) * h + iy) * w + ix;
+                int8_t qv;
+                if constexpr (QUANT)
+                    qv = quant_pixel(((const uint8_t*)in)[e], q);
+                else
+                    qv = ((const int8_t*)in)[e];
+                v |= (uint32_t)(uint8_t)qv << (8 * c);
+                if (x_nchw != nullptr && iy >= own0 && iy < own1) x_nchw[e] = qv;
+            }
+        }
+        px[t] = v;
+    }
+    __syncthreads();
+    const int npx = (oy1 - oy0) * ow;
+    for (int t = threadIdx.x; t < npx; t += blockDim.x) {
+        const int oy = t / ow, ox = t - oy * ow;
+        uint32_t d[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+        for (int ky = 0; ky < KH; ++ky)
+#pragma unroll
+            for (int kx = 0; kx < KW; ++kx) {
+                const uint32_t v = px[(oy + ky) * wp + ox + kx];
+#pragma unroll
+                for (int c = 0; c < C; ++c) {
+                    const int k = (ky * KW + kx) * C + c;
+                    d[k >> 2] |= ((v >> (8 * c)) & 0xffu) << (8 * (k & 3));
+                }
+            }
+        int8_t* o = xcol + (((int64_t)img * oh + oy0 + oy) * ow + ox) * 32;
+        *(v4i_q*)o = v4i_q{(int)d[0], (int)d[1], (int)d[2], (int)d[3]};
+        *(v4i_q*)(o + 16) = v4i_q{(int)d[4], (int)d[5], (int)d[6], (int)d[7]};
+    }
+}
+
 }  // namespace
 
-hipError_t image_stats(const uint8_t* img, int64_t n, unsigned long long* stats, hipStream_t st) {
+// slots: IMAGE_STATS_SLOTS x 4 u64 of per-block partials
+hipError_t image_stats_slots(const uint8_t* img, int64_t n, unsigned long long* slots, int* nslots, hipStream_t st) {
     if (n <= 0) return hipErrorInvalidValue;
-    hipError_t e = hipMemsetAsync(stats, 0, 4 * sizeof(unsigned long long), st);
-    if (e != hipSuccess) return e;
-    // a few blocks, each thread looping over 16-byte loads: every block ends in 4 device-scope
-    // atomics on one cache line, and 192 blocks of them serialised into ~8 us
-    int64_t blocks = (n / 16 + 2047) / 2048;
-    blocks = blocks < 1 ? 1 : blocks > 32 ? 32 : blocks;
-    hipLaunchKernelGGL(image_stats_kernel, dim3((unsigned)blocks), dim3(256), 0, st, img, n, stats);
+    int64_t blocks = (n / 16 + 255) / 256;
+    blocks = blocks < 1 ? 1 : blocks > IMAGE_STATS_SLOTS ? IMAGE_STATS_SLOTS : blocks;
+    hipLaunchKernelGGL(image_stats_kernel, dim3((unsigned)blocks), dim3(256), 0, st, img, n, slots);
+    *nslots = (int)blocks;
+    return hipGetLastError();
+}
+
+hipError_t stats_finalize(const unsigned long long* slots, int nslots, unsigned long long* stats, hipStream_t st) {
+    hipLaunchKernelGGL(stats_finalize_kernel, dim3(1), dim3(256), 0, st, slots, nslots, stats);
+    return hipGetLastError();
+}
+
+bool input_im2col_ok(int c, int kh, int kw) { return (c == 3 && kh == 3 && kw == 3) || (c == 1 && kh == 5 && kw == 5); }
+
+hipError_t input_im2col(const void* in, bool quant, int n, int c, int h, int w, int kh, int kw, int pt, int pl,
+                        const unsigned long long* slots, int nslots, int64_t count, int8_t* x_nchw, int8_t* xcol,
+                        int8_t* ascale, hipStream_t st) {
+    if (!input_im2col_ok(c, kh, kw) || n <= 0 || (quant && (count <= 0 || slots == nullptr))) return hipErrorInvalidValue;
+    const int oh = h + 2 * pt - kh + 1, ow = w + 2 * pl - kw + 1;
+    if (oh <= 0 || ow <= 0) return hipErrorInvalidValue;
+    // bands of output rows: ~16 KiB of staged pixels, at least 2 workgroups per image at 32x32
+    int band = oh;
+    while (band > 1 && (int64_t)(band + kh - 1) * (w + kw - 1) * 4 > 16384) band = (band + 1) / 2;
+    if (oh >= 32 && band > oh / 2) band = (oh + 1) / 2;
+    const int bands = (oh + band - 1) / band;
+    const size_t lds = (size_t)(band + kh - 1) * (w + kw - 1) * 4;
+    const int64_t var_count = count / ((int64_t)c * h * w) * 784;  // MnistUtils.cpp:86 (see image_quantize)
+    const dim3 grid((unsigned)((int64_t)n * bands));
+#define IIC(CC, KK, Q)                                                                                            \
+    hipLaunchKernelGGL((input_im2col_kernel<CC, KK, KK, Q>), grid, dim3(256), lds, st, in, n, h, w, oh, ow, pt, pl, \
+                       band, slots, nslots, count, var_count, x_nchw, xcol, ascale)
+    if (c == 3 && quant)
+        IIC(3, 3, true);
+    else if (c == 3)
+        IIC(3, 3, false);
+    else if (quant)
+        IIC(1, 5, true);
+    else
+        IIC(1, 5, false);
+#undef IIC
+    return hipGetLastError();
+}
+
+hipError_t image_stats(const uint8_t* img, int64_t n, unsigned long long* stats, hipStream_t st) {
+    // the standalone op: one block's slot is the statistics (the step spreads the pixels over
+    // IMAGE_STATS_SLOTS blocks and sums their slots where it uses them)
+    if (n <= 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(image_stats_kernel, dim3(1), dim3(256), 0, st, img, n, stats);
     return hipGetLastError();
 }
 

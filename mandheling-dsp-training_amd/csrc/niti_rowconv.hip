@@ -933,6 +933,71 @@ hipError_t rowconv_fwd(const ConvGeom& g, const int8_t* x_c32, const int8_t* wf,
     return dg ? launch_rc<RC_REQUANT, true>(g.w, R, grid, a, st) : launch_rc<RC_REQUANT, false>(g.w, R, grid, a, st);
 }
 
+// ---- the classifier head's weight gradient ------------------------------------------------------
+// dw[co][ci] = Σ_p dy[p][co] x[p][ci] (exact int32) for co < 32: one workgroup per 32-channel ci
+// block, its four waves taking 32-pixel K chunks round robin.  A chunk's x [32 px][32 ci] and dy
+// [32 px][32 co] tiles go through the wave's own LDS slot and come back K-major by
+// ds_read_b64_tr_b8 (16-lane group g: channels 16 (g & 1) .. + 15, pixels 16 (g >> 1) .. + 15 = the
+// MFMA fragment of lanes 16 g .. 16 g + 15); the waves' tiles are summed through LDS, written
+// into dw (OHWI16 rows of cip) and their max published (NITI_RangeEstimate, single device).
+__global__ void __launch_bounds__(256) head_wgrad_kernel(const int8_t* __restrict__ x, int xld,
+                                                         const int8_t* __restrict__ dy, int dld, int n, int c_out,
+                                                         int cip, int32_t* __restrict__ dw, uint32_t* amax) {
+    __shared__ __attribute__((aligned(16))) int8_t tile[4][2][32 * 32];
+    __shared__ int32_t part[4][16][64];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int ci0 = blockIdx.x * 32;
+    const __amdgpu_buffer_rsrc_t rX = make_rsrc(x, (uint32_t)((int64_t)n * xld));
+    const __amdgpu_buffer_rsrc_t rD = make_rsrc(dy, (uint32_t)((int64_t)n * dld));
+    const int lp = lane >> 1, lh = (lane & 1) * 16;  // staging: pixel, 16-byte half
+    const int g = lane >> 4, j = lane & 15;
+    v16i acc = {};
+    for (int p0 = wid * 32; p0 < n; p0 += 128) {
+        const int p = p0 + lp;
+        const v4i xv = buf_load16(rX, p < n && ci0 + lh < xld ? (uint32_t)(p * xld + ci0 + lh) : OOB);
+        const v4i dv = buf_load16(rD, p < n && lh < dld ? (uint32_t)(p * dld + lh) : OOB);
+        *(v4i*)(&tile[wid][0][lp * 32 + lh]) = xv;
+        *(v4i*)(&tile[wid][1][lp * 32 + lh]) = dv;
+        v4i fr[2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const int8_t* b = &tile[wid][t][(16 * (g >> 1) + (j >> 1)) * 32 + 16 * (g & 1) + 8 * (j & 1)];
+            const v2i lo = __builtin_amdgcn_ds_read_tr8_b64_v2i32((__attribute__((address_space(3))) v2i*)(b));
+            const v2i hi = __builtin_amdgcn_ds_read_tr8_b64_v2i32((__attribute__((address_space(3))) v2i*)(b + 8 * 32));
+            fr[t] = v4i{lo[0], lo[1], hi[0], hi[1]};
+        }
+        // lane 16 g + j now holds channel 16 (g & 1) + j = lane & 31 and pixels 16 (g >> 1) + 0..15 =
+        // 16 (lane >> 5) + 0..15: the MFMA fragment as it is; A = dy (rows co), B = x (columns ci)
+        acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(fr[1], fr[0], acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) part[wid][i][lane] = acc[i];
+    __syncthreads();
+    if (wid != 0) return;
+    uint32_t m = 0;
+    const int ci = ci0 + (lane & 31), h = lane >> 5;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int32_t v = part[0][i][lane] + part[1][i][lane] + part[2][i][lane] + part[3][i][lane];
+        const int co = 8 * (i >> 2) + 4 * h + (i & 3);
+        if (co < c_out && ci < cip) {
+            dw[(int64_t)co * cip + ci] = v;
+            m = max(m, uabs32(v));
+        }
+    }
+    m = wave_max(m);
+    if (lane == 0 && amax != nullptr) publish_max(amax, m);
+}
+
+hipError_t head_wgrad(int n, int c_out, int cip, const int8_t* x, int xld, const int8_t* dy, int dld, int32_t* dw,
+                      uint32_t* amax, hipStream_t st) {
+    if (n <= 0 || c_out <= 0 || c_out > 32 || cip % 32 != 0 || xld < cip || dld < c_out || dld > 32) return hipErrorInvalidValue;
+    if (xld % 16 != 0 || dld % 16 != 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(head_wgrad_kernel, dim3((unsigned)(cip / 32)), dim3(256), 0, st, x, xld, dy, dld, n, c_out, cip,
+                       dw, amax);
+    return hipGetLastError();
+}
+
 // A 1x1 layer over 1x1 maps (the classifier head) on the same kernel with W = 1: out[n][cop] (or
 // the input gradient's epilogues) = requant(Σ_k x[n][k] w[row][k]) for rows = cop channels.
 bool rowconv_fc_ok(int n, int K, int rows, bool fused) {
