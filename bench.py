@@ -253,6 +253,9 @@ def main():
     ap.add_argument("--no-overlap", action="store_true", help="(default) weight gradients on the step stream")
     ap.add_argument("--probe-plan", default="", help="bm,bn,splits,strategy forced on the probed GEMM after "
                                                      "autotuning (PMC passes re-use the timed run's plan)")
+    ap.add_argument("--save-plans", default="", help="write the autotuned GEMM plans to this JSON file")
+    ap.add_argument("--load-plans", default="", help="use the GEMM plans of this JSON file (no autotuning): the "
+                                                     "profiled and PMC passes replay the timed run's launch sequence")
     ap.add_argument("--wgrad-p16", type=int, default=-1, help="force the P16 weight gradient on every layer it "
                                                               "takes with this many K splits (0: its default; "
                                                               "-1: the autotuner's choice)")
@@ -312,7 +315,12 @@ def main():
     # (niti_model_autotune: candidate tile / split-K plans timed per layer phase).
     tune_s = 0.0
     p16_default = {i: p for (i, ph), p in model.plans().items() if ph == 2 and p[:2] == (16, 16)}
-    if not args.no_autotune:
+    if args.load_plans:
+        step()
+        for k, p in json.load(open(args.load_plans)).items():
+            layer, phase = (int(v) for v in k.split(","))
+            model.set_plan(layer, phase, p)
+    elif not args.no_autotune:
         step()
         ta = time.perf_counter()
         model.autotune()
@@ -326,6 +334,8 @@ def main():
     if args.probe_plan:
         model.set_plan(probe_layer, args.probe_phase, [int(v) for v in args.probe_plan.split(",")])
     plans = model.plans()
+    if args.save_plans and rank == 0:
+        json.dump({f"{l},{p}": list(v) for (l, p), v in plans.items()}, open(args.save_plans, "w"))
 
     # The probe (HIP events around one GEMM, on the stream it runs on) is armed before the
     # warmup: the step is replayed as a hipGraph and arming it re-captures the graph, which
@@ -469,7 +479,7 @@ def main():
                          "in_kernel_span_us": round(iso_span_us, 2) if iso_span_us else None,
                          "note": "same launch re-run alone after the timed region (no side-stream overlap)"},
         },
-        "autotune_s": round(tune_s, 2) if not args.no_autotune else None,
+        "autotune_s": round(tune_s, 2) if not (args.no_autotune or args.load_plans) else None,
         "cpu_baseline": cpu,
     }
     if rank == 0:

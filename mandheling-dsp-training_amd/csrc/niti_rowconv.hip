@@ -194,10 +194,11 @@ struct RowUnit {
     static constexpr int G = 32 / W, H = W, NR = R + 2;
     int cob, b, img;
     bool valid, img_ok;
-    __device__ RowUnit(const RowConvArgs& a, int wg, int wid, int c) {
-        const int per = a.ngb4 / 4;
+    // ks: the K-split form -- one unit per workgroup, its four waves splitting the channel chunks
+    __device__ RowUnit(const RowConvArgs& a, int wg, int wid, int c, bool ks = false) {
+        const int per = ks ? a.ngb : a.ngb4 / 4;
         cob = wg / per;
-        const int gb = (wg - cob * per) * 4 + wid;
+        const int gb = ks ? wg - cob * per : (wg - cob * per) * 4 + wid;
         valid = gb < a.ngb;
         const int gbc = valid ? gb : 0;
         b = gbc % a.nbands;
@@ -214,6 +215,10 @@ constexpr int RC_LDS_BYTES = RC_MAX_STAGES * RC_STAGE_BYTES;
 // (the wave's pixels: 32 R, or 128 R at the pool's input resolution) -- 16 KiB per wave at R = 4
 constexpr int RC_P16_WAVE_BYTES = 16 * 1024;
 constexpr int RC_SMEM_BYTES = RC_LDS_BYTES > 4 * RC_P16_WAVE_BYTES ? RC_LDS_BYTES : 4 * RC_P16_WAVE_BYTES;
+// K-split form: every wave stages its own chunks' 9 fragments, all of them up front (NS <= 4)
+constexpr int RC_KS_MAX_NS = 4;
+constexpr int RC_KS_BYTES = 4 * RC_KS_MAX_NS * 9 * 1024;
+static_assert(RC_KS_BYTES >= 4 * RC_P16_WAVE_BYTES, "the P16 tile fits the K-split ring");
 
 // the accumulators of one unit: acc[r][i] = y[co = cob*32 + 8(i>>2) + 4h + (i&3)][row b*R + r][col]
 // Every wave of the workgroup runs this (an invalid unit reads zeros), so the barriers match.
@@ -223,7 +228,12 @@ constexpr int RC_SMEM_BYTES = RC_LDS_BYTES > 4 * RC_P16_WAVE_BYTES ? RC_LDS_BYTE
 // cross-lane moves, no masks, no VALU in the loop.  S chunks are in flight: chunk c computes from
 // registers while c + 1 .. c + S - 1 load (rows into registers, the 9 weight fragments by LDS-DMA
 // into a ring shared by the workgroup's four waves).
-template <int W, int R>
+// UNC (chunk count a multiple of the ring depth): every step waits, issues and reads
+// unconditionally -- the last steps load chunks past the end (never consumed) -- so the loop body
+// is straight-line code.  With the issue under a branch, hipcc's waitcnt pass takes the path that
+// skipped it and waits for vmcnt(3) before the first tap shift: the whole ring, the chunk just
+// issued included, drained every step.
+template <int W, int R, bool UNC>
 __device__ __forceinline__ void rowconv_compute(const RowConvArgs& a, const RowUnit<W, R>& U, int lane, int wid,
                                                 int8_t* smem, v16i (&acc)[R]) {
     constexpr int H = W, NR = R + 2;
@@ -306,10 +316,10 @@ __device__ __forceinline__ void rowconv_compute(const RowConvArgs& a, const RowU
     auto step = [&](auto st_c, int cc) {
         constexpr int ST = decltype(st_c)::value, WB = ST & 1;
         const unsigned long long s0 = stamp ? __builtin_amdgcn_s_memtime() : 0ull;
-        const bool more = cc + 1 < cb;
-        if (more && !(RC_EXP & 2)) arrive(cc + 2 < cb ? 1 : 0);
+        const bool more = UNC || cc + 1 < cb;
+        if (more && !(RC_EXP & 2)) arrive(UNC || cc + 2 < cb ? 1 : 0);
         const unsigned long long s1 = stamp ? __builtin_amdgcn_s_memtime() : 0ull;
-        if (cc + 3 < cb && !(RC_EXP & 8)) issue(std::integral_constant<int, (ST + 3) % S>(), cc + 3);
+        if ((UNC || cc + 3 < cb) && !(RC_EXP & 8)) issue(std::integral_constant<int, (ST + 3) % S>(), cc + 3);
         if (stamp) {
             asm volatile("" ::: "memory");
             t_issue += __builtin_amdgcn_s_memtime() - s1;
@@ -358,11 +368,22 @@ __device__ __forceinline__ void rowconv_compute(const RowConvArgs& a, const RowU
     read_w(std::integral_constant<int, 0>(), wreg[0]);
     fence_w(wreg[0]);
     if (stamp && lane == 0) a.stamps[(blockIdx.x * 4 + wid) * 16 + 1] = __builtin_amdgcn_s_memtime();
-    for (int cc = 0; cc < cb; cc += S) {
-        step(std::integral_constant<int, 0>(), cc);
-        if (cc + 1 < cb) step(std::integral_constant<int, 1>(), cc + 1);
-        if (cc + 2 < cb) step(std::integral_constant<int, 2>(), cc + 2);
-        if (cc + 3 < cb) step(std::integral_constant<int, 3>(), cc + 3);
+    if constexpr (UNC) {
+        for (int cc = 0; cc < cb; cc += S) {
+            step(std::integral_constant<int, 0>(), cc);
+            step(std::integral_constant<int, 1>(), cc + 1);
+            step(std::integral_constant<int, 2>(), cc + 2);
+            step(std::integral_constant<int, 3>(), cc + 3);
+        }
+        // the past-the-end chunks' loads (LDS-DMA into the ring the epilogue reuses) land first
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+        for (int cc = 0; cc < cb; cc += S) {
+            step(std::integral_constant<int, 0>(), cc);
+            if (cc + 1 < cb) step(std::integral_constant<int, 1>(), cc + 1);
+            if (cc + 2 < cb) step(std::integral_constant<int, 2>(), cc + 2);
+            if (cc + 3 < cb) step(std::integral_constant<int, 3>(), cc + 3);
+        }
     }
     // the ring's LDS is reused by the next unit's prologue only after every wave's last reads
     __builtin_amdgcn_s_barrier();
@@ -373,6 +394,102 @@ __device__ __forceinline__ void rowconv_compute(const RowConvArgs& a, const RowU
         st[6] = t_wait;
         st[7] = t_read;
     }
+}
+
+// K-split form for whole-image units (R == H: W = 2) on layers with too few units to fill the chip
+// (VGG-11's 2x2 layers: 256 units of 32 channels x 16 images, i.e. 64 workgroups of four): the
+// workgroup owns ONE unit and wave w takes the channel chunks w, w + 4, ..., NS = CB / 4 of them,
+// each wave staging its own chunks' weight fragments in its own LDS region (no barrier in the
+// loop).  Every load is issued up front (NS <= 4) in straight-line code, so hipcc's counted
+// waits are exact.  Rows 0 and R + 1 of the loaded band lie outside the image (y0 = -1, R == H):
+// they are neither loaded nor multiplied -- 6 of the 9 (ky, row) products of a 2-row unit remain.
+// The four partial tiles are summed through LDS into wave 0 (ks_reduce).
+template <int W, int R, int NS>
+__device__ __forceinline__ void rowconv_compute_ks(const RowConvArgs& a, const RowUnit<W, R>& U, int lane, int wid,
+                                                   int8_t* smem, v16i (&acc)[R]) {
+    static_assert(R == W && NS >= 1 && NS <= RC_KS_MAX_NS, "whole-image units, all chunks staged at once");
+    constexpr int H = W;
+    const int h = lane >> 5, c = lane & 31, ox = c % W;
+    const __amdgpu_buffer_rsrc_t rX = make_rsrc(a.x, a.xbytes);
+    const __amdgpu_buffer_rsrc_t rW = make_rsrc(a.wf, a.wbytes);
+    const uint32_t xl = U.img_ok ? (uint32_t)((((int64_t)U.img * a.CB * H) * W + ox) * 32 + 16 * h) : OOB;
+    constexpr uint32_t CHUNK = (uint32_t)H * W * 32;
+    const uint32_t wbase = (uint32_t)(U.cob * a.CB * 9) * 1024u;
+    int8_t* ring = smem + wid * (RC_KS_MAX_NS * 9 * 1024);
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[r][i] = 0;
+    v4i X[NS][R];  // the image's R rows of each of the wave's chunks
+#pragma unroll
+    for (int k = 0; k < NS; ++k) {
+        const uint32_t cc = (uint32_t)(wid + 4 * k);
+        // the counted waits below assume this issue order; the memory clobbers keep hipcc from
+        // hoisting a later chunk's row loads above an earlier chunk's DMA
+#pragma unroll
+        for (int t = 0; t < 9; ++t)
+            dma16(rW, ring + (k * 9 + t) * 1024, (uint32_t)lane * 16u, wbase + cc * 9216u + (uint32_t)t * 1024u);
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            X[k][r] = buf_load16(rX, xl == OOB ? OOB : xl + (uint32_t)r * W * 32 + cc * CHUNK);
+        asm volatile("" ::: "memory");
+    }
+    const uint32_t lds_lane = lds_addr(ring) + (uint32_t)lane * 16u;
+#pragma unroll
+    for (int k = 0; k < NS; ++k) {
+        // chunk k's DMA and rows are in once the later chunks' 9 + R loads are the only ones left
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 1 - k) * (9 + R)) : "memory");
+        v4i w[9];
+#pragma unroll
+        for (int t = 0; t < 9; ++t) w[t] = lds_b128(lds_lane + (uint32_t)((k * 9 + t) * 1024));
+        v4i XL[R], XR[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            reg_fence(X[k][r]);
+            XL[r] = shift_in_left<W>(X[k][r], ox == 0);
+            XR[r] = shift_in_right<W>(X[k][r], ox == W - 1);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int t = 0; t < 9; ++t) reg_fence(w[t]);
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int ky = 0; ky < 3; ++ky) {
+                const int j = r + ky - 1;  // the image row this tap reads
+                if (j < 0 || j >= R) continue;
+                acc[r] = __builtin_amdgcn_mfma_i32_32x32x32_i8(w[3 * ky], XL[j], acc[r], 0, 0, 0);
+                acc[r] = __builtin_amdgcn_mfma_i32_32x32x32_i8(w[3 * ky + 1], X[k][j], acc[r], 0, 0, 0);
+                acc[r] = __builtin_amdgcn_mfma_i32_32x32x32_i8(w[3 * ky + 2], XR[j], acc[r], 0, 0, 0);
+            }
+    }
+}
+
+// the four waves' partial tiles -> wave 0's acc (the other waves' acc stay partial); the ring is
+// free again afterwards (three barriers)
+template <int R>
+__device__ __forceinline__ void ks_reduce(v16i (&acc)[R], int8_t* smem, int wid, int lane) {
+    static_assert(3 * R * 16 * 64 * 4 <= RC_KS_BYTES, "partials fit the ring");
+    int32_t* part = (int32_t*)smem;
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (wid != 0) {
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) part[(((wid - 1) * R + r) * 16 + i) * 64 + lane] = acc[r][i];
+    }
+    __syncthreads();
+    if (wid == 0) {
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+                acc[r][i] += part[((0 * R + r) * 16 + i) * 64 + lane] + part[((1 * R + r) * 16 + i) * 64 + lane] +
+                             part[((2 * R + r) * 16 + i) * 64 + lane];
+    }
+    __syncthreads();
 }
 
 // W = 1: a 1x1 map per image, 32 images per wave (the MFMA B columns), out channels cob*32 + 0..31
@@ -639,34 +756,43 @@ __device__ __forceinline__ uint32_t max_abs16(const v16i& v, uint32_t m) {
     return m;
 }
 
-template <int W, int R>
+// KS = 0: four units per workgroup; KS = NS: one unit, K split over the waves (wave 0 holds the sum)
+template <int W, int R, bool UNC, int KS>
 __device__ __forceinline__ void compute_unit(const RowConvArgs& a, const RowUnit<W, R>& U, int lane, int wid,
                                              int8_t* smem, v16i (&acc)[R]) {
-    if constexpr (W == 1)
+    if constexpr (W == 1) {
         fc_compute<R>(a, U, lane, acc);
-    else
-        rowconv_compute<W, R>(a, U, lane, wid, smem, acc);
+    } else if constexpr (KS > 0) {
+        rowconv_compute_ks<W, R, KS>(a, U, lane, wid, smem, acc);
+        ks_reduce<R>(acc, smem, wid, lane);
+    } else {
+        rowconv_compute<W, R, UNC>(a, U, lane, wid, smem, acc);
+    }
 }
 
 // DG: the input-gradient epilogues (relu mask / pool gradient), their operands prefetched
-template <int W, int R, int MODE, bool DG>
+template <int W, int R, int MODE, bool DG, bool UNC, int KS>
 __global__ void __launch_bounds__(256, (RC_EXP & 16) ? 2 : 1) rowconv_fwd_kernel(RowConvArgs a) {
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: DMA bases stay scalar
     const int c = lane & 31;
-    __shared__ __attribute__((aligned(16))) int8_t smem[RC_SMEM_BYTES];
+    __shared__ __attribute__((aligned(16))) int8_t smem[KS > 0 ? RC_KS_BYTES : RC_SMEM_BYTES];
     __shared__ uint32_t red[4];
     __shared__ uint32_t gm;
     v16i acc[R];
+    // the waves that own a unit's result: all four, or wave 0 of a K-split workgroup
+    const bool owner = KS == 0 || wid == 0;
     RC_STAMP(0);
     if constexpr (MODE == RC_FUSED) {
-        const RowUnit<W, R> U(a, blockIdx.x, wid, c);
+        const RowUnit<W, R> U(a, blockIdx.x, wid, c, KS > 0);
         uint32_t m = 0;
-        compute_unit<W, R>(a, U, lane, wid, smem, acc);
+        compute_unit<W, R, UNC, KS>(a, U, lane, wid, smem, acc);
         EpiIn<DG ? R : 1> ein = {};
-        if constexpr (DG) epi_prefetch<W, R>(a, U, lane, ein);
+        if constexpr (DG)
+            if (owner) epi_prefetch<W, R>(a, U, lane, ein);
+        if (owner)
 #pragma unroll
-        for (int r = 0; r < R; ++r) m = max_abs16(acc[r], m);
+            for (int r = 0; r < R; ++r) m = max_abs16(acc[r], m);
         m = wave_max(m);
         if (lane == 0) red[wid] = m;
         __syncthreads();
@@ -675,7 +801,8 @@ __global__ void __launch_bounds__(256, (RC_EXP & 16) ? 2 : 1) rowconv_fwd_kernel
             if (a.stamps != nullptr && lane == 0) a.stamps[blockIdx.x * 64 + 8] = __builtin_amdgcn_s_memrealtime();
             grid_bw_arrive(a.bar, a.epoch, bitwidth_rc(bm), lane);
         }
-        if constexpr (DG) epi_masks<R>(a, ein);  // while the barrier completes
+        if constexpr (DG)
+            if (owner) epi_masks<R>(a, ein);  // while the barrier completes
         if (wid == 0) {
             const int gbw = grid_bw_wait(a.bar, a.epoch, a.err, lane);
             if (a.stamps != nullptr && lane == 0) a.stamps[blockIdx.x * 64 + 9] = __builtin_amdgcn_s_memrealtime();
@@ -688,15 +815,16 @@ __global__ void __launch_bounds__(256, (RC_EXP & 16) ? 2 : 1) rowconv_fwd_kernel
         }
         __syncthreads();
         RC_STAMP(4);
-        if (U.valid) rowconv_epilogue<W, R, DG>(a, U, lane, acc, gm, ein, smem + wid * RC_P16_WAVE_BYTES);
+        if (U.valid && owner) rowconv_epilogue<W, R, DG>(a, U, lane, acc, gm, ein, smem + wid * RC_P16_WAVE_BYTES);
         RC_STAMP(5);
     } else if constexpr (MODE == RC_RANGE) {
         uint32_t m = 0;
         for (int wg = blockIdx.x; wg < a.wgs; wg += gridDim.x) {
-            const RowUnit<W, R> U(a, wg, wid, c);
-            compute_unit<W, R>(a, U, lane, wid, smem, acc);
+            const RowUnit<W, R> U(a, wg, wid, c, KS > 0);
+            compute_unit<W, R, UNC, KS>(a, U, lane, wid, smem, acc);
+            if (owner)
 #pragma unroll
-            for (int r = 0; r < R; ++r) m = max_abs16(acc[r], m);
+                for (int r = 0; r < R; ++r) m = max_abs16(acc[r], m);
         }
         m = wave_max(m);
         if (lane == 0) red[wid] = m;
@@ -707,14 +835,16 @@ __global__ void __launch_bounds__(256, (RC_EXP & 16) ? 2 : 1) rowconv_fwd_kernel
         const uint32_t g = read_max(a.amax);
         if (blockIdx.x == 0 && threadIdx.x == 0) write_exponent(a, g);
         for (int wg = blockIdx.x; wg < a.wgs; wg += gridDim.x) {
-            const RowUnit<W, R> U(a, wg, wid, c);
-            compute_unit<W, R>(a, U, lane, wid, smem, acc);
+            const RowUnit<W, R> U(a, wg, wid, c, KS > 0);
+            compute_unit<W, R, UNC, KS>(a, U, lane, wid, smem, acc);
             EpiIn<DG ? R : 1> ein = {};
             if constexpr (DG) {
-                epi_prefetch<W, R>(a, U, lane, ein);
-                epi_masks<R>(a, ein);
+                if (owner) {
+                    epi_prefetch<W, R>(a, U, lane, ein);
+                    epi_masks<R>(a, ein);
+                }
             }
-            if (U.valid) rowconv_epilogue<W, R, DG>(a, U, lane, acc, g, ein, smem + wid * RC_P16_WAVE_BYTES);
+            if (U.valid && owner) rowconv_epilogue<W, R, DG>(a, U, lane, acc, g, ein, smem + wid * RC_P16_WAVE_BYTES);
             if (DG && a.p16 != nullptr) __syncthreads();  // the P16 tiles sit in the next unit's ring
         }
     }
@@ -840,22 +970,48 @@ bool rowconv_p16_ok(const ConvGeom& d, bool pool) {
     return pool || R * W >= 16 || (W == 2 && R == 2);
 }
 
+// the K-split form (rowconv_compute_ks): chunks per wave, or 0.  Whole-image 2-row units whose
+// one-unit-per-wave grid leaves the chip more than a quarter empty, and at most 4 chunks per wave
+static int rowconv_ks(const ConvGeom& g, bool dg) {
+    int u = 0;
+    const int R = rowconv_rows(g, dg, &u);
+    const int CB = (g.c_in + 31) / 32;
+    if (g.w != 2 || R != 2 || CB % 4 != 0 || CB / 4 > RC_KS_MAX_NS || u >= 768) return 0;
+    return CB / 4;
+}
+
+// waves of the launch (K-split: four per unit)
 int rowconv_units(const ConvGeom& g, bool dg) {
     int u = 0;
     (void)rowconv_rows(g, dg, &u);
+    if (rowconv_ks(g, dg) > 0) {
+        const int64_t units = (int64_t)(g.n + 15) / 16 * (g.cop / 32);  // W = 2: 16 images per unit
+        return (int)(units * 4);
+    }
     return u;
 }
 
+// FUSED needs every workgroup resident: one per CU (K-split: 144 KiB of LDS each)
 bool rowconv_fused_ok(const ConvGeom& g, bool dg) {
     return rowconv_ok(g) && rowconv_units(g, dg) <= ((RC_EXP & 16) ? 8 : 4) * 256;
 }
 
 template <int MODE, bool DG>
-static hipError_t launch_rc(int W, int R, int grid, const RowConvArgs& a, hipStream_t st) {
-#define RC_CASE(WW, RR)                                                                                        \
-    if (W == WW && R == RR) {                                                                                  \
-        hipLaunchKernelGGL((rowconv_fwd_kernel<WW, RR, MODE, DG>), dim3((unsigned)grid), dim3(256), 0, st, a); \
-        return hipGetLastError();                                                                              \
+static hipError_t launch_rc(int W, int R, int grid, const RowConvArgs& a, hipStream_t st, int ks = 0) {
+    if (ks > 0) {  // rowconv_ks: W = R = 2
+        if (ks == 4) hipLaunchKernelGGL((rowconv_fwd_kernel<2, 2, MODE, DG, false, 4>), dim3((unsigned)grid), dim3(256), 0, st, a);
+        else if (ks == 2) hipLaunchKernelGGL((rowconv_fwd_kernel<2, 2, MODE, DG, false, 2>), dim3((unsigned)grid), dim3(256), 0, st, a);
+        else if (ks == 1) hipLaunchKernelGGL((rowconv_fwd_kernel<2, 2, MODE, DG, false, 1>), dim3((unsigned)grid), dim3(256), 0, st, a);
+        else return hipErrorInvalidValue;
+        return hipGetLastError();
+    }
+#define RC_CASE(WW, RR)                                                                                              \
+    if (W == WW && R == RR) {                                                                                        \
+        if (WW > 1 && a.CB % 4 == 0)                                                                                 \
+            hipLaunchKernelGGL((rowconv_fwd_kernel<WW, RR, MODE, DG, true, 0>), dim3((unsigned)grid), dim3(256), 0, st, a); \
+        else                                                                                                         \
+            hipLaunchKernelGGL((rowconv_fwd_kernel<WW, RR, MODE, DG, false, 0>), dim3((unsigned)grid), dim3(256), 0, st, a); \
+        return hipGetLastError();                                                                                    \
     }
     if constexpr (!DG) RC_CASE(16, 8)
     RC_CASE(16, 4)
@@ -899,7 +1055,8 @@ hipError_t rowconv_fwd(const ConvGeom& g, const int8_t* x_c32, const int8_t* wf,
     a.nbands = g.h / R;
     a.ngb = ((g.n + G - 1) / G) * a.nbands;
     a.ngb4 = (a.ngb + 3) / 4 * 4;
-    a.wgs = COB * a.ngb4 / 4;
+    const int ks = rowconv_ks(g, dg);
+    a.wgs = ks > 0 ? COB * a.ngb : COB * a.ngb4 / 4;
     a.out = o.out;
     a.cop = g.cop;
     a.pool_out = o.pool_out;
@@ -925,12 +1082,12 @@ hipError_t rowconv_fwd(const ConvGeom& g, const int8_t* x_c32, const int8_t* wf,
     if (o.pool_out != nullptr && (R % 2 != 0 || g.h % 2 != 0)) return hipErrorInvalidValue;
     if (mode == RC_FUSED) {
         if (bar == nullptr || err == nullptr || epoch == 0 || !rowconv_fused_ok(g, dg)) return hipErrorInvalidValue;
-        return dg ? launch_rc<RC_FUSED, true>(g.w, R, a.wgs, a, st) : launch_rc<RC_FUSED, false>(g.w, R, a.wgs, a, st);
+        return dg ? launch_rc<RC_FUSED, true>(g.w, R, a.wgs, a, st, ks) : launch_rc<RC_FUSED, false>(g.w, R, a.wgs, a, st, ks);
     }
     int grid = a.wgs;
     grid = grid > 1024 ? 1024 : grid;
-    if (mode == RC_RANGE) return launch_rc<RC_RANGE, false>(g.w, R, grid, a, st);
-    return dg ? launch_rc<RC_REQUANT, true>(g.w, R, grid, a, st) : launch_rc<RC_REQUANT, false>(g.w, R, grid, a, st);
+    if (mode == RC_RANGE) return launch_rc<RC_RANGE, false>(g.w, R, grid, a, st, ks);
+    return dg ? launch_rc<RC_REQUANT, true>(g.w, R, grid, a, st, ks) : launch_rc<RC_REQUANT, false>(g.w, R, grid, a, st, ks);
 }
 
 // ---- the classifier head's weight gradient ------------------------------------------------------

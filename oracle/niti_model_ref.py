@@ -72,11 +72,13 @@ def train_step(layers, W, S, x, exp_in, labels, classes=10, impl="naive", thread
     impl "naive": the exact NCHW restatement; "mnn": the reference-structured one (C4 layout,
     16x4 GEMM unit, the grad graph's transposes / LeftPoolGrad / rot180), exact accumulation, on
     `threads` pthreads (acc_mode O.ACC_F32_SEQ: the reference's float32 accumulation, as the CPU
-    baseline runs it; default exact).  wgrad_stats: record per layer the weight gradient's 2^24-guard and int32
-    overflow counts (naive pass) and how many int32 sums / int8 gradients the reference's float32
-    accumulation (Int8FunctionsOpt.cpp:211-226) would change (mnn pass, ACC_F32_SEQ)."""
+    baseline runs it; default exact).  wgrad_stats: record per layer, for the weight gradient
+    ("wstats"), the forward ("fstats") and the input gradient ("dstats"), the 2^24-guard and int32
+    overflow counts (naive pass) and how many int32 sums / int8 outputs / exponents the reference's
+    float32 accumulation (Int8FunctionsOpt.cpp:211-226) would change on the same exact inputs (mnn
+    pass, ACC_F32_SEQ; the forward pass exposes no int32 tensor, so its int32 count is absent)."""
     n = x.shape[0]
-    rec = dict(inp=[], y=[], r=[], p=[], exp=[], dw=[], dy=[], geom=[], wstats=[])
+    rec = dict(inp=[], y=[], r=[], p=[], exp=[], dw=[], dy=[], geom=[], wstats=[], fstats=[], dstats=[])
     mnn = impl == "mnn"
     am = O.ACC_EXACT if acc_mode is None else acc_mode
     a = x
@@ -90,6 +92,11 @@ def train_step(layers, W, S, x, exp_in, labels, classes=10, impl="naive", thread
         else:
             y, exp, _, st = O.conv_fwd(g, a, W[i], exp, S[i])
             assert st.overflow == 0
+        if wgrad_stats:
+            _, st = O.conv_fwd_acc(g, a, W[i])
+            yf, ef, _ = O.mnn_conv_fwd(g, a, W[i], rec["exp"][-1] if i else exp_in, S[i], O.ACC_F32_SEQ, threads)
+            rec["fstats"].append(dict(layer=i, outputs=int(y.size), guard=int(st.guard), overflow=int(st.overflow),
+                                      f32_int8_diff=int((yf != y).sum()), exp_diff=int(ef != exp)))
         r = O.relu(y) if l["relu"] else y
         rec["y"].append(y)
         rec["r"].append(r)
@@ -124,9 +131,15 @@ def train_step(layers, W, S, x, exp_in, labels, classes=10, impl="naive", thread
         rec["dw"].insert(0, dw)
         if i > 0:
             if mnn:
-                dx, _, _ = O.mnn_conv_dgrad(g, dy[i], W[i], am, threads)
+                dx, dinc, dacc = O.mnn_conv_dgrad(g, dy[i], W[i], am, threads)
             else:
-                dx, _, _, _ = O.conv_dgrad(g, dy[i], W[i])
+                dx, dinc, dacc, _ = O.conv_dgrad(g, dy[i], W[i])
+            if wgrad_stats:
+                _, st = O.conv_dgrad_acc(g, dy[i], W[i])
+                dxf, dincf, daccf = O.mnn_conv_dgrad(g, dy[i], W[i], O.ACC_F32_SEQ, threads)
+                rec["dstats"].insert(0, dict(layer=i, outputs=int(dx.size), guard=int(st.guard),
+                                             overflow=int(st.overflow), f32_int32_diff=int((daccf != dacc).sum()),
+                                             f32_int8_diff=int((dxf != dx).sum()), exp_diff=int(dincf != dinc)))
             pl = layers[i - 1]
             if pl["flatten"]:
                 dx = dx.reshape(rec["p"][i - 1].shape)

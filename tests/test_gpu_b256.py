@@ -11,8 +11,8 @@ int8 weight gradient, updated weights, logits and their exponent.
 
 The reference accumulates in float32 (Int8FunctionsOpt.cpp:211-226), which equals the exact
 integer sum only while sum |x w| < 2^24.  The test prints, per layer, how many weight-gradient
-outputs exceed that guard and how many int32 sums / int8 gradients a float32 sequential
-accumulation changes at this batch, so "bit-exact" states its own domain: the device matches the
+outputs (and forward / input-gradient outputs) exceed that guard and how many int32 sums / int8
+values a float32 sequential accumulation changes at this batch, so "bit-exact" states its own domain: the device matches the
 exact sum everywhere, and matches the float32 reference wherever the printed counts are zero.
 """
 import os
@@ -54,7 +54,14 @@ def case():
         print("  layer {layer}: wgrad outputs {outputs}, sum|p| >= 2^24: {guard}, int32 overflow: {overflow}, "
               "float32 accumulation changes {f32_int32_diff} int32 sums / {f32_int8_diff} int8 gradients "
               "(bw {bw} vs {bw_f32})".format(**st))
-    assert all(st["overflow"] == 0 for st in rec["wstats"])
+    for st in rec["fstats"]:
+        print("  layer {layer} forward: outputs {outputs}, sum|p| >= 2^24: {guard}, int32 overflow: {overflow}, "
+              "float32 accumulation changes {f32_int8_diff} int8 outputs / {exp_diff} exponents".format(**st))
+    for st in rec["dstats"]:
+        print("  layer {layer} input gradient: outputs {outputs}, sum|p| >= 2^24: {guard}, int32 overflow: "
+              "{overflow}, float32 accumulation changes {f32_int32_diff} int32 sums / {f32_int8_diff} int8 outputs / "
+              "{exp_diff} exponents".format(**st))
+    assert all(st["overflow"] == 0 for st in rec["wstats"] + rec["fstats"] + rec["dstats"])
     return dict(layers=layers, W=W, S=S, img=img, labels=labels, x=x, ascale=ascale, newW=newW, rec=rec)
 
 

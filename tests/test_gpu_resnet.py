@@ -52,6 +52,38 @@ def test_resnet18_step_matches_oracle(T, hw, batch, classes):
         W = newW
 
 
+def test_resnet18_224_step_matches_oracle(T):
+    """BASELINE config 5's input size (224x224, batch 2, 1000 classes), one whole step against the
+    oracle: the 7x7 / 2 stem and its weight gradient over the 224-px input, the overlapping 3x3 / 2
+    max-pool gradient 112 -> 56 (the two-pass workspace kernel), the 56x56 stage's weight gradients
+    (the per-lane K-major loader) and every other tap, bit for bit."""
+    import niti_oracle as O
+    import niti_resnet_ref as RR
+    from niti_amd.resnet import ResNet18
+    O.set_threads(16)
+    hw, batch, classes = 224, 2, 1000
+    convs = RR.resnet18_convs(hw, classes)
+    W, S = RR.init_weights(convs, seed=224)
+    rng = np.random.default_rng(224)
+    m = ResNet18(batch, hw, classes)
+    for i, (w, s) in enumerate(zip(W, S)):
+        m.set_weight(i, w, s)
+    m.record = True
+    x = rng.integers(-127, 128, (batch, 3, hw, hw)).astype(np.int8)
+    labels = rng.integers(0, classes, batch).astype(np.int32)
+    newW, rec = RR.train_step(convs, W, S, x, -2, labels, classes=classes)
+    m.train_step(T.from_numpy(x).cuda(), -2, T.from_numpy(labels).cuda())
+    t = m.taps()
+    assert t["exp_logits"] == rec["exp_logits"] and np.array_equal(t["logits"], rec["logits"])
+    for i, c in enumerate(convs):
+        relu = m.rec["fwd"][i][1]
+        want = O.relu(rec["fwd"][i]) if relu else rec["fwd"][i]
+        assert np.array_equal(t["fwd"][i], want), ("fwd", c["name"])
+        assert np.array_equal(t["dy"][i], rec["dy"][i]), ("dy", c["name"])
+        assert np.array_equal(t["dw"][i], rec["dw"][i]), ("dw", c["name"])
+        assert np.array_equal(m.get_weight(i), newW[i]), ("w", c["name"])
+
+
 def test_residual_add_and_sum_pool(T):
     """The two new kernels alone: exponent gaps 0..30 (the 23-bit cap and the floor shift of the
     low operand), and the sum pool with its broadcast gradient."""

@@ -169,3 +169,24 @@ def test_rows_dgrad_vgg11_shapes(T):
     conv2 (128 -> 256 at 8x8, into conv1's pool), fused launches."""
     _dgrad_case(T, 32, 256, 4, 512, True, True, 0, seed=41)
     _dgrad_case(T, 32, 256, 8, 256, False, True, 0, seed=42)
+
+
+@pytest.mark.parametrize("mode", [0, 2])
+def test_rows_ks_2x2(T, mode):
+    """The K-split form (rowconv_compute_ks: 2x2 maps whose conv input channels are a multiple of
+    128 -- one unit per workgroup, the four waves splitting the channel chunks, partial tiles summed
+    through LDS), forward and input gradient, ragged batches, 1 / 2 / 4 chunks per wave."""
+    for k, (n, ci, co, relu, pool) in enumerate([(17, 128, 32, True, True), (33, 256, 64, False, False),
+                                                  (40, 512, 96, True, False), (16, 512, 512, True, True)]):
+        _case(T, n, ci, 2, co, relu, pool, mode, seed=900 + 10 * mode + k)
+    for k, (n, ci, co, pool, relu) in enumerate([(17, 32, 128, True, True), (33, 64, 256, False, True),
+                                                  (40, 96, 512, True, False), (16, 512, 512, False, False)]):
+        _dgrad_case(T, n, ci, 2, co, pool, relu, mode, seed=950 + 10 * mode + k)
+
+
+def test_rows_ks_vgg11_2x2_b256(T):
+    """VGG-11's 2x2 layers at the benchmarked batch (512 -> 512, 256 images: 256 K-split
+    workgroups), fused launches: conv7's forward with its pool and conv8's input gradient into
+    conv7's relu."""
+    _case(T, 256, 512, 2, 512, True, True, 0, seed=31)
+    _dgrad_case(T, 256, 512, 2, 512, False, True, 0, seed=32)

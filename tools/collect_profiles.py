@@ -58,7 +58,7 @@ def main():
         kn = sel[-1]["Kernel_Name"].split("(")[0]
         f.write(f"probe {kn}, grid {int(sel[-1]['Grid_Size_X']) // int(sel[-1]['Workgroup_Size_X'])} x "
                 f"{sel[-1]['Workgroup_Size_X']} threads, plan {plan}\n")
-        f.write(f"rocprofv3 --kernel-trace of `bench.py --cpu-sample 0 --probe-plan ...` (tools/gpu_full.sh, TAG={tag}):\n")
+        f.write(f"rocprofv3 --kernel-trace of `bench.py --cpu-sample 0 --load-plans ...` (tools/gpu_full.sh, TAG={tag}):\n")
         f.write(f"  isolated re-runs after the timed region (last 20 dispatches): avg {iso_avg:.2f} us, "
                 f"min {min(iso):.2f}, max {max(iso):.2f}\n")
         if instep:
@@ -90,6 +90,10 @@ def main():
             w = csv.DictWriter(f, fieldnames=list(rs[0].keys()))
             w.writeheader()
             w.writerows(keep)
+    # every launch of the last step: HBM bytes (PMC) over its un-counted duration
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "membound.py"), f"{G}/pmcF_{tag}", f"{G}/pmcW_{tag}",
+                        f"{G}/prof_{tag}", f"{P}/{tag}_step_hbm.txt"], capture_output=True, text=True)
+    print(r.stdout or r.stderr)
 
 
 if __name__ == "__main__":
