@@ -207,6 +207,57 @@ def bench_resnet18(args):
     if rank != 0:
         comm.dist.destroy_process_group()
         return
+    # roofline: the first 56x56 stage conv's forward GEMM (layer1.0.a, 64 -> 64, 3x3) re-run alone
+    # after the timed region, HIP events on the launch stream around 20 back-to-back launches
+    c = m.convs[1]
+    g = ops.geom(batch, c["ci"], c["h"], c["h"], c["co"], c["k"], stride=c["stride"], pad=c["pad"])
+    xr = ops.nchw_to_nhwc16(torch.from_numpy(rng.integers(-127, 128, (batch, c["ci"], c["h"], c["h"])).astype(np.int8)).cuda())
+    wr = ops.oihw_to_ohwi16(torch.from_numpy(rng.integers(-127, 128, (c["co"], c["ci"], c["k"], c["k"])).astype(np.int8)).cuda())
+    amax = ops.new_range()
+    ops.conv_fwd_acc(g, xr, wr, amax)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    reps = 20
+    e0.record()
+    for _ in range(reps):
+        ops.conv_fwd_acc(g, xr, wr, amax)
+    e1.record()
+    torch.cuda.synchronize()
+    k_us = e0.elapsed_time(e1) * 1e3 / reps
+    k_ops = 2 * batch * g.oh * g.ow * c["co"] * c["ci"] * c["k"] * c["k"]
+    roof = {"kernel": f"ResNet-18 {c['name']} forward GEMM (gemm_kernel, implicit im2col, int32 accumulate + range; "
+                      "re-run alone after the timed region)",
+            "bound": "mfma", "achieved": round(k_ops / k_us / 1e6, 2), "peak": round(PEAK_INT8_TOPS, 1),
+            "unit": "TFLOP/s", "frac": round(k_ops / k_us / 1e6 / PEAK_INT8_TOPS, 4), "traffic": None,
+            "avg_launch_us": round(k_us, 2), "timing": "HIP events around 20 back-to-back launches on one stream",
+            "ops_per_launch": k_ops}
+    cpu = None
+    if world == 1 and args.cpu_sample != 0:
+        # the oracle's ResNet-18 restatement (oracle/niti_resnet_ref.py) of the whole step
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import niti_oracle as O
+        import niti_resnet_ref as RR
+        sample = args.cpu_sample if args.cpu_sample > 0 else 1
+        convs = RR.resnet18_convs(hw, 1000)
+        W, S = RR.init_weights(convs, seed=17)
+        crng = np.random.default_rng(1)
+        cimg = crng.integers(0, 256, (sample, 3, hw, hw)).astype(np.uint8)
+        clab = crng.integers(0, 1000, sample).astype(np.int32)
+        all_cores = len(os.sched_getaffinity(0))
+        if os.environ.get("OMP_NUM_THREADS", "").isdigit():
+            all_cores = max(1, min(all_cores, int(os.environ["OMP_NUM_THREADS"])))
+        legs = []
+        for t in sorted({args.cpu_threads, all_cores}):
+            O.set_threads(t)
+            t0 = time.perf_counter()
+            x, a = O.quantize_images(cimg)
+            RR.train_step(convs, W, S, x, a, clab, classes=1000)
+            secs = time.perf_counter() - t0
+            legs.append({"threads": t, "value": round(sample / secs, 3), "seconds": round(secs, 2)})
+        best = max(legs, key=lambda l: l["value"])
+        cpu = {"value": best["value"], "unit": "images/s", "cores": best["threads"], "kind": "port",
+               "sample": f"{sample} image(s) at {hw}x{hw} through the whole ResNet-18 step in the oracle's exact C "
+                         f"restatement (oracle/niti_resnet_ref.py; conv threads split the batch/channels)",
+               "legs": legs, "cpu_model": cpu_model()}
     print(json.dumps({
         "metric": "training images/sec + int8 MFMA TOPS, ResNet-18 ImageNet-224 (BASELINE config 5 network)",
         "value": round(batch * world * args.steps / el, 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
@@ -219,7 +270,7 @@ def bench_resnet18(args):
                    "driver": "host-driven op sequence (niti_amd.resnet)",
                    "launch": "hipGraph replay of the captured step" if graph is not None else "direct launches"},
         "int8_mfma_tops": round(tops, 2), "int8_mfma_frac_of_peak": round(tops / PEAK_INT8_TOPS, 4),
-        "roofline": None, "cpu_baseline": None}))
+        "roofline": roof, "cpu_baseline": cpu}))
     if comm is not None:
         comm.dist.destroy_process_group()
 

@@ -98,17 +98,9 @@ constexpr int P16_WAVES = 4;           // one wave per SIMD
 #ifndef NITI_WG_ATOMIC_OUT
 #define NITI_WG_ATOMIC_OUT 0
 #endif
-// Diagnostic switches measured on MI355X (conv4, 4 splits, stamps; none shipped, all within noise):
-// NITI_WG_ZFIX = 1 pins the 144 accumulator zeroes ahead of the first ring wait (hipcc places the
-// v_accvgpr_writes after it): prologue + K loop 12.8k vs 12.7k cycles per block.
-#ifndef NITI_WG_ZFIX
-#define NITI_WG_ZFIX 0
-#endif
-// NITI_WG_SCHED = n > 0: sched_group_barrier interleave of the K group (1 MFMA, then n VALU, one
-// SALU): 321 (n = 2) / 323 (n = 3) vs 342 cycles per K group, but the block end moved < 1 %.
-#ifndef NITI_WG_SCHED
-#define NITI_WG_SCHED 0
-#endif
+// (Measured and dropped, round 2: zeroing the accumulators ahead of the first ring wait, and a
+// sched_group_barrier interleave of one MFMA with 2-3 VALU per K group -- 321 vs 342 cycles per K
+// group, but the block end moved < 1 %: the merge and the output dominate the tail.)
 // per-wave stamps (diagnostic): wave start and K-loop end after the 8 block stamps
 #define WG_WSTAMP(k)                                                                                       \
     do {                                                                                                   \
@@ -304,12 +296,6 @@ __global__ void __launch_bounds__(NW * 64) wgrad_p16_kernel(WgP16 g) {
     [&]<int... U>(std::integer_sequence<int, U...>) {
         ((ring[U] = Ring{}, issue(ring[U], std::integral_constant<int, U>(), U)), ...);
     }(std::make_integer_sequence<int, D>());
-#if NITI_WG_ZFIX
-    // pin the zeroed accumulators here, ahead of the first wait: their writes issue in the
-    // shadow of the ring loads instead of after K group 0 has landed
-#pragma unroll
-    for (int t = 0; t < 9; ++t) asm volatile("" : "+a"(acc[t]));
-#endif
     WG_STAMP(1);
     // Software pipeline: the tap operands of K group j + 1 (dy shifted for kx = 0 / 2, x rows for
     // ky = 0 / 2; kx = ky = 1 are the ring registers themselves) are built while K group j's nine
@@ -367,14 +353,6 @@ __global__ void __launch_bounds__(NW * 64) wgrad_p16_kernel(WgP16 g) {
         }(std::make_integer_sequence<int, 9>());
         // slot u is free again: K group j + D
         issue(ring[u], u_c, j0 + u + D);
-#if NITI_WG_SCHED
-#pragma unroll
-        for (int i = 0; i < 9; ++i) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);            // one MFMA
-            __builtin_amdgcn_sched_group_barrier(0x002, NITI_WG_SCHED, 0);  // then VALU
-            __builtin_amdgcn_sched_group_barrier(0x004, 1, 0);            // and SALU
-        }
-#endif
     };
     for (int j0 = 0; j0 < n_w; j0 += D) {
         [&]<int... U>(std::integer_sequence<int, U...>) {

@@ -72,15 +72,12 @@ def main():
     print(open(f"{P}/{tag}_probe_dispatches.txt").read())
     # PMC: probe rows + calibration
     gx = gx_p16 if p16 else blocks * 512 if blocks else 0
+    # the plan the counters were collected under: bench.py reports the traffic only for that plan
+    pl = ",".join(str(plan[k]) for k in ("bm", "bn", "splits", "strategy"))
     out = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "traffic.py"), f"{G}/pmcF_{tag}", f"{G}/pmcW_{tag}",
-                          f"{P}/traffic.json", str(gx), "1", name, "20"], capture_output=True, text=True, check=True).stdout
+                          f"{P}/traffic.json", "vgg11_b256_L3_p2", pl], capture_output=True, text=True, check=True).stdout
     open(f"{P}/{tag}_traffic.txt", "w").write(out)
     print(out)
-    # the plan the counters were collected under: bench.py reports the traffic only for that plan
-    tj = json.load(open(f"{P}/traffic.json"))
-    for v in tj.values():
-        v["plan"] = [plan["bm"], plan["bn"], plan["splits"], plan["strategy"]]
-    json.dump(tj, open(f"{P}/traffic.json", "w"), indent=1)
     for cnt, fn in (("pmcF", "fetch"), ("pmcW", "write")):
         src = glob.glob(f"{G}/{cnt}_{tag}/*counter_collection.csv")[0]
         rs = list(csv.DictReader(open(src)))
