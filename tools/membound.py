@@ -6,8 +6,8 @@ usage: membound.py <pmcF dir> <pmcW dir> <kernel-trace dir> [out.txt]
 Bytes: FETCH_SIZE (x2: gfx950 counts 64 B per 128-B request, MI355X_MICROARCH.md HBM section) and
 WRITE_SIZE per dispatch, from two separate --pmc passes of the same bench command.  Durations:
 the kernel trace of an un-counted run of that command (counter passes stretch kernels), matched
-by kernel name and grid; a launch the un-counted run does not have takes its counted duration
-(marked *).  The step is the last one of each run: the launches between the last two
+by kernel name, grid and occurrence; a launch the un-counted run does not have takes its counted
+duration (marked *).  The step is the last one of each run: the launches between the last two
 sgd_update_kernel dispatches.  GB/s = (fetch + write) / duration; frac = GB/s / 8000.
 """
 import collections
@@ -44,10 +44,12 @@ def main():
     for f in glob.glob(f"{sys.argv[3]}/*kernel_trace.csv"):
         trace += list(csv.DictReader(open(f)))
     trace = last_step(sorted(trace, key=lambda r: int(r["Start_Timestamp"])), "Kernel_Name")
+    # the k-th launch of a (kernel, grid) in the counted step takes the k-th such launch's duration
     dur = collections.defaultdict(list)
     for r in trace:
         g = int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])
         dur[(short(r["Kernel_Name"]), g)].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+    seen = collections.Counter()
     if [short(r["Kernel_Name"]) for r in F] != [short(r["Kernel_Name"]) for r in W]:
         sys.exit("the two counter passes ran different launch sequences")
     lines = [f"{'kernel':64} {'grid':>8} {'fetch MB':>9} {'write MB':>9} {'us':>7} {'GB/s':>7} {'frac':>6}"]
@@ -56,10 +58,12 @@ def main():
         name, g = short(f["Kernel_Name"]), int(f["Grid_Size"])
         fb = 2 * float(f["Counter_Value"]) * 1024
         wb = float(w["Counter_Value"]) * 1024
-        d = dur.get((name, g))
+        d = dur.get((name, g), [])
+        k = seen[(name, g)]
+        seen[(name, g)] += 1
         mark = ""
-        if d:
-            t = sum(d) / len(d)
+        if k < len(d):
+            t = d[k]
         else:
             t = (int(f["End_Timestamp"]) - int(f["Start_Timestamp"])) / 1e3
             mark = "*"
