@@ -68,6 +68,67 @@ struct NhwcToNhwc16 {
     }
 };
 
+// NHWC16 [n][hw][cp] -> C4 [ceil(c/4)][n][hw][4] (the pad lanes of the last quad zero); one
+// channel quad (4 bytes) per thread
+struct Nhwc16ToC4 {
+    const int8_t* in;
+    int n, c, hw, cp;
+    int8_t* out;
+    __device__ void operator()(int64_t i) const {  // i over [cq][n][hw]
+        const int p = (int)(i % hw);
+        const int64_t r = i / hw;
+        const int b = (int)(r % n);
+        const int cq = (int)(r / n);
+        uint32_t v = *(const uint32_t*)(in + ((int64_t)b * hw + p) * cp + 4 * cq);
+        const int live = c - 4 * cq;  // channels of this quad that exist
+        if (live < 4) v &= (1u << (8 * live)) - 1u;
+        *(uint32_t*)(out + i * 4) = v;
+    }
+};
+
+// The register-fed row kernel with the rescale fused (niti_rowconv.hip) behind the conv and
+// deconv Executions, where the geometry allows (stride-1 pad-1 3x3, square 2/4/8/16 maps,
+// c_out padded to a multiple of 32, the grid resident): x -> C32, OHWI16 -> fragment-major WF,
+// one fused launch into NHWC16, then C4.  Same results as the GEMM + requantisation path.
+struct RowPath {
+    Workspace ws;
+    int8_t *xc32 = nullptr, *wf = nullptr, *y16 = nullptr;
+    uint32_t *bar = nullptr, *err = nullptr;
+    uint32_t epoch = 0;
+    bool on = false;
+    int resize(const ConvGeom& g) {
+        ws.release();
+        on = rowconv_ok(g) && rowconv_fused_ok(g);
+        if (!on) return NITI_NO_ERROR;
+        const int cb = (g.c_in + 31) / 32;
+        xc32 = (int8_t*)ws.alloc((size_t)g.n * cb * g.h * g.w * 32);
+        wf = (int8_t*)ws.alloc(rowconv_wf_bytes(g.c_out, g.c_in));
+        y16 = (int8_t*)ws.alloc((size_t)g.n * g.oh * g.ow * g.cop);
+        bar = (uint32_t*)ws.alloc((ROWCONV_BAR_WORDS + 1) * sizeof(uint32_t));
+        if (!xc32 || !wf || !y16 || !bar) return NITI_OUT_OF_MEMORY;
+        err = bar + ROWCONV_BAR_WORDS;
+        if (hipMemset(bar, 0, (ROWCONV_BAR_WORDS + 1) * sizeof(uint32_t)) != hipSuccess) return NITI_NO_EXECUTION;
+        epoch = 0;
+        return NITI_NO_ERROR;
+    }
+    // x16 / w16: the Execution's NHWC16 input and OHWI16 weights (already converted)
+    hipError_t run(const ConvGeom& g, const int8_t* x16, const int8_t* w16, uint32_t* amax, const int8_t* exp_in,
+                   const int8_t* wscale, int8_t* exp_out, int8_t* out_c4, hipStream_t st) {
+        hipError_t e = nhwc16_to_c32(x16, g.n, g.h * g.w, g.cip, g.c_in, xc32, st);
+        if (e == hipSuccess) e = weights_to_wf(w16, g.c_out, g.c_in, g.cip, false, wf, st);
+        if (e != hipSuccess) return e;
+        RowConvOut o;
+        o.out = y16;
+        o.exp_in = exp_in;
+        o.wscale = wscale;
+        o.exp_out = exp_out;
+        e = rowconv_fwd(g, xc32, wf, o, 0, amax, bar, ++epoch, err, st);
+        if (e != hipSuccess) return e;
+        const int cq = (g.c_out + 3) / 4;
+        return launch_map((int64_t)cq * g.n * g.oh * g.ow, Nhwc16ToC4{y16, g.n, g.c_out, g.oh * g.ow, g.cop, out_c4}, st);
+    }
+};
+
 // g OHWI16 [Co][KK][Cip] -> C4 [ceil(Co/4)][Ci][KK][4] (the GradientConv output tensor,
 // batch = Ci, channel = Co)
 struct Ohwi16ToC4Grad {
@@ -258,7 +319,8 @@ class ConvInt8Execution : public Execution {
         slab_bytes_ = conv_fwd_workspace(g_);
         slab_ = slab_bytes_ ? ws_.alloc(slab_bytes_) : nullptr;
         if (slab_bytes_ && !slab_) return NITI_OUT_OF_MEMORY;
-        return (x16_ && w16_ && acc_ && amax_) ? NITI_NO_ERROR : NITI_OUT_OF_MEMORY;
+        if (!(x16_ && w16_ && acc_ && amax_)) return NITI_OUT_OF_MEMORY;
+        return rows_.resize(g_);
     }
     int onExecute(const niti_tensor* in, int nin, const niti_tensor* out, int nout, hipStream_t st) override {
         if (!acc_) return NITI_NO_EXECUTION;
@@ -266,6 +328,11 @@ class ConvInt8Execution : public Execution {
         // reorderWeight every call: weights change each step (NITI_Conv_Int8.cpp:177)
         NITI_TRY(oihw_to_ohwi16((const int8_t*)in[1].data, g_.c_out, g_.c_in, g_.kh * g_.kw, g_.cip, w16_, st));
         NITI_TRY(hipMemsetAsync(amax_, 0, MAX_BYTES, st));
+        if (rows_.on) {
+            NITI_TRY(rows_.run(g_, x16_, w16_, amax_, (const int8_t*)in[2].data, (const int8_t*)in[3].data,
+                               nout > 1 ? (int8_t*)out[1].data : nullptr, (int8_t*)out[0].data, st));
+            return NITI_NO_ERROR;
+        }
         NITI_TRY(conv_fwd_acc(g_, x16_, w16_, acc_, amax_, slab_, slab_bytes_, st));
         ActRequant r;
         r.acc = acc_;
@@ -291,6 +358,7 @@ class ConvInt8Execution : public Execution {
     uint32_t* amax_ = nullptr;
     void* slab_ = nullptr;
     size_t slab_bytes_ = 0;
+    RowPath rows_;
 };
 
 // ------------------------------------------------------------------ NITI_DeConv_Int8 (701)
@@ -319,13 +387,18 @@ class DeconvInt8Execution : public Execution {
         slab_bytes_ = conv_fwd_workspace(g_);
         slab_ = slab_bytes_ ? ws_.alloc(slab_bytes_) : nullptr;
         if (slab_bytes_ && !slab_) return NITI_OUT_OF_MEMORY;
-        return (x16_ && w16_ && acc_ && amax_) ? NITI_NO_ERROR : NITI_OUT_OF_MEMORY;
+        if (!(x16_ && w16_ && acc_ && amax_)) return NITI_OUT_OF_MEMORY;
+        return rows_.resize(g_);
     }
     int onExecute(const niti_tensor* in, int nin, const niti_tensor* out, int nout, hipStream_t st) override {
         if (!acc_) return NITI_NO_EXECUTION;
         NITI_TRY(c4_to_nhwc16((const int8_t*)in[0].data, g_.n, g_.c_in, g_.h * g_.w, g_.cip, x16_, st));
         NITI_TRY(oihw_to_ohwi16((const int8_t*)in[1].data, g_.c_out, g_.c_in, g_.kh * g_.kw, g_.cip, w16_, st, true));
         NITI_TRY(hipMemsetAsync(amax_, 0, MAX_BYTES, st));
+        if (rows_.on) {  // the forward rule without an exponent output (rotated w^T: a plain conv)
+            NITI_TRY(rows_.run(g_, x16_, w16_, amax_, nullptr, nullptr, nullptr, (int8_t*)out[0].data, st));
+            return NITI_NO_ERROR;
+        }
         NITI_TRY(conv_fwd_acc(g_, x16_, w16_, acc_, amax_, slab_, slab_bytes_, st));
         ActRequant r;
         r.acc = acc_;
@@ -348,6 +421,7 @@ class DeconvInt8Execution : public Execution {
     uint32_t* amax_ = nullptr;
     void* slab_ = nullptr;
     size_t slab_bytes_ = 0;
+    RowPath rows_;
 };
 
 // ------------------------------------------------------------------ NITI_GradientConv_Int8 (715)

@@ -21,6 +21,12 @@ GEOMS = [
     (7, 5, 6, 7, 12, 3, 1, 1),       # ragged everything
     (3, 40, 7, 5, 36, 3, 1, 0),      # non-square, no pad
     (3, 8, 9, 9, 12, 3, 2, 1),       # stride 2, channels % 4 == 0
+    # the conv / deconv Executions take the fused row kernel where the geometry allows (stride-1
+    # pad-1 3x3, square 2/4/8/16 maps, c_out padded to a multiple of 32): ragged channels, and the
+    # K-split 2x2 form (128 input channels)
+    (5, 40, 8, 8, 52, 3, 1, 1),
+    (9, 96, 2, 2, 128, 3, 1, 1),
+    (9, 128, 2, 2, 92, 3, 1, 1),
 ]
 
 
