@@ -139,22 +139,9 @@ void wgrad_stamps_arm(unsigned long long* buf);
 int conv_wgrad_p16_splits(const ConvGeom& g);
 // workspace: the split-K partial slabs (0 bytes when the plan does not split)
 size_t conv_wgrad_p16_workspace(const ConvGeom& g, int splits);
-// a split-K sum handed to a later launch: C[e] = sum over z < splits of slab[z * stride + e]
-// (n elements, n % 4 == 0, v4i-aligned), max|C| published into amax (may be null)
-struct SlabReduce {
-    const int32_t* slab = nullptr;
-    int splits = 0;
-    int64_t n = 0, stride = 0;
-    int32_t* C = nullptr;
-    uint32_t* amax = nullptr;
-};
-// defer (optional): with splits > 1 the partial slabs are left for the caller's next launch to
-// sum (the fused row kernel does it in its grid barrier's shadow, RowConvOut::red) instead of a
-// splitk_reduce launch here
 hipError_t conv_wgrad_p16(const ConvGeom& g, const int8_t* x_p16, const int8_t* dy_p16, int32_t* acc,
                           uint32_t* amax, void* ws, size_t ws_bytes, int splits, hipStream_t st,
-                          hipEvent_t ev_b = nullptr, hipEvent_t ev_e = nullptr, unsigned long long* span = nullptr,
-                          SlabReduce* defer = nullptr);
+                          hipEvent_t ev_b = nullptr, hipEvent_t ev_e = nullptr, unsigned long long* span = nullptr);
 // acc[m][o] = sum_k B[m][k] * A[o][k] (NITI_Matmul_Int8); k16 multiple of 16 (zero padded rows),
 // ldb/lda bytes, ldc elements (multiple of 16; columns o..ldc come out 0)
 hipError_t matmul_acc(int M, int O, int k16, const int8_t* B, int64_t ldb, const int8_t* A, int64_t lda,
@@ -233,9 +220,6 @@ struct RowConvOut {
     int pool_relu = 0;
     // input gradient: the same gradient in the weight gradient's P16 layout (rowconv_p16_ok)
     int8_t* p16 = nullptr;
-    // FUSED mode: a split-K weight-gradient sum (conv_wgrad_p16's defer) done by the workgroups
-    // between their grid-barrier arrival and its release
-    SlabReduce red;
 };
 constexpr int ROWCONV_BAR_WORDS = 2 * 19 * 32;  // grid-barrier state (both parities)
 static_assert(ROWCONV_BAR_WORDS == NITI_ROWCONV_STATE_WORDS, "header constant");

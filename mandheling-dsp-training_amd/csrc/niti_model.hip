@@ -487,10 +487,6 @@ struct Model {
         }
     } key;
     bool capturing = false;
-    // a split P16 weight gradient's slab sum, left for the same layer's fused input-gradient
-    // launch (run() on one stream, single device, not captured); defer_red enables it
-    SlabReduce pending_red;
-    bool defer_red = false;
     hipError_t cap_err = hipSuccess;
     void drop_graph() {
         for (auto e : segs) (void)hipGraphExecDestroy(e);
@@ -996,11 +992,7 @@ int Model::wgrad_layer(int i, hipStream_t st) {
         hipEvent_t eb, ee;
         unsigned long long* sp;
         probe_launch(i, 2, &eb, &ee, &sp);
-        // the slab sum rides in the same layer's fused input-gradient launch, which follows on this
-        // stream (dgrad_layer), where it fills that kernel's grid-barrier wait
-        const bool defer = defer_red && i > 0 && rowconv_dgrad_layer(i) && rowconv_fused_ok(l.dg, true);
-        MTRY(conv_wgrad_p16(g, xp16[i], dp16[i], l.dwacc, dp ? nullptr : rng(i, 2), slab_w, slab_w_bytes, s, st, eb, ee, sp,
-                            defer ? &pending_red : nullptr));
+        MTRY(conv_wgrad_p16(g, xp16[i], dp16[i], l.dwacc, dp ? nullptr : rng(i, 2), slab_w, slab_w_bytes, s, st, eb, ee, sp));
         return NITI_NO_ERROR;
     }
     // the weight-gradient probe brackets the GEMM launch alone (not its split-K reduce)
@@ -1099,8 +1091,6 @@ int Model::dgrad_layer(int i, hipStream_t st) {
         }
         const ConvGeom& d = l.dg;
         if (!dp && !capturing && rowconv_fused_ok(d, true)) {
-            o.red = pending_red;  // this layer's deferred weight-gradient slab sum, if any
-            pending_red = SlabReduce{};
             MTRY(rowconv_fwd(d, l.dyc32, l.wft, o, 0, rng(i, 1), l.bar, ++l.epoch, rc_err, st));
         } else {
             MTRY(rowconv_fwd(d, l.dyc32, l.wft, o, 1, rng(i, 1), nullptr, 0, nullptr, st));
@@ -1368,14 +1358,6 @@ int Model::run(const int8_t* x_nchw, int exp_in, const uint8_t* images, const in
         if (rc != NITI_NO_ERROR) return rc;
     }
     hipStream_t wst = ov ? side : st;
-    // one stream, one device, direct launches: a split weight gradient's slab sum can wait for the
-    // same layer's fused input-gradient launch (the next launch on the stream)
-    defer_red = !ov && !dp && !capturing;
-    pending_red = SlabReduce{};
-    struct DeferOff {  // any return from here on (errors included) ends the deferral
-        bool& f;
-        ~DeferOff() { f = false; }
-    } defer_off{defer_red};
     for (int i = nl - 1; i >= 0; --i) {
         // (an event record leaves a ~6.5 us bubble before the next launch on the step stream;
         // hipStreamWriteValue64 / WaitValue64 run as blit kernels here and cost more)
@@ -1402,12 +1384,6 @@ int Model::run(const int8_t* x_nchw, int exp_in, const uint8_t* images, const in
                          i > 0 && !rowconv_dgrad_layer(i) ? l.wT : nullptr, keep_grads ? l.g8 : nullptr};
         jobs[i].wf = l.rc ? l.wf : nullptr;
         jobs[i].wft = l.rcd ? l.wft : nullptr;
-    }
-    defer_red = false;
-    if (pending_red.splits > 1) {  // not taken by an input-gradient launch: sum it here
-        const SlabReduce r = pending_red;
-        pending_red = SlabReduce{};
-        MTRY(splitk_reduce_linear(r.slab, r.splits, r.n, r.stride, r.C, r.amax, st));
     }
     if (dp) {  // every bucket summed and ranged on the comm stream before the update
         MTRY(hipEventRecord(ev_grads, cst));

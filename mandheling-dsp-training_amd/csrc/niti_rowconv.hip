@@ -169,7 +169,6 @@ struct RowConvArgs {
     int pool_relu;
     int8_t* p16;                 // P16 [pixels/16][cop][16] copy of out / pool_dx, or null
     int64_t p16_pixels;          // pixels of that tensor
-    SlabReduce red;              // FUSED: a deferred split-K sum (RowConvOut::red), splits 0 if none
     // W = 1 (1x1 maps, the classifier head): x is row-major [n][xld], the weights row-major
     // [rows][wld] (OHWI16 forward, IHWO16 input gradient), K the reduced channels
     int xld, wld, K, rows;
@@ -741,31 +740,6 @@ __device__ __forceinline__ void rowconv_epilogue(const RowConvArgs& a, const Row
     }
 }
 
-// this workgroup's share of a deferred split-K weight-gradient sum (conv_wgrad_p16's defer): a
-// contiguous run of 16-byte elements, all splits summed, C written, the run's max|C| published --
-// done between the grid barrier's arrival and its release, where the workgroup would only wait
-__device__ void slab_reduce_share(const SlabReduce& r, int lane, int wid) {
-    const int64_t n4 = r.n / 4;
-    const int64_t per = (n4 + gridDim.x - 1) / gridDim.x;
-    const int64_t e0 = (int64_t)blockIdx.x * per, e1 = min(n4, e0 + per);
-    const v4i* s = (const v4i*)r.slab;
-    const int64_t st4 = r.stride / 4;
-    uint32_t m = 0;
-    for (int64_t e = e0 + threadIdx.x; e < e1; e += blockDim.x) {
-        v4i acc = s[e];
-        for (int z = 1; z < r.splits; ++z) acc += s[z * st4 + e];
-        ((v4i*)r.C)[e] = acc;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint32_t u = uabs32(acc[k]);
-            m = m > u ? m : u;
-        }
-    }
-    m = wave_max(m);
-    if (lane == 0 && r.amax != nullptr) publish_max(r.amax, m);
-    (void)wid;
-}
-
 __device__ __forceinline__ void write_exponent(const RowConvArgs& a, uint32_t gmax) {
     if (a.exp_out == nullptr) return;
     const int shift = bitwidth_rc(gmax) - 7;
@@ -829,7 +803,6 @@ __global__ void __launch_bounds__(256, (RC_EXP & 16) ? 2 : 1) rowconv_fwd_kernel
         }
         if constexpr (DG)
             if (owner) epi_masks<R>(a, ein);  // while the barrier completes
-        if (a.red.splits > 1) slab_reduce_share(a.red, lane, wid);
         if (wid == 0) {
             const int gbw = grid_bw_wait(a.bar, a.epoch, a.err, lane);
             if (a.stamps != nullptr && lane == 0) a.stamps[blockIdx.x * 64 + 9] = __builtin_amdgcn_s_memrealtime();
@@ -1105,8 +1078,6 @@ hipError_t rowconv_fwd(const ConvGeom& g, const int8_t* x_c32, const int8_t* wf,
     a.pool_relu = o.pool_relu;
     a.p16 = o.p16;
     a.p16_pixels = (int64_t)g.n * g.h * g.w * (o.pool_dx != nullptr ? 4 : 1);
-    a.red = o.red;
-    if (o.red.splits > 1 && (mode != RC_FUSED || o.red.n % 4 != 0 || o.red.stride % 4 != 0)) return hipErrorInvalidValue;
     if (o.p16 != nullptr && (!dg || !rowconv_p16_ok(g, o.pool_dx != nullptr))) return hipErrorInvalidValue;
     if (o.pool_out != nullptr && (R % 2 != 0 || g.h % 2 != 0)) return hipErrorInvalidValue;
     if (mode == RC_FUSED) {

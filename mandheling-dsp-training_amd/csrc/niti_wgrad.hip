@@ -698,7 +698,7 @@ size_t conv_wgrad_p16_workspace(const ConvGeom& g, int splits) {
 
 hipError_t conv_wgrad_p16(const ConvGeom& g, const int8_t* x_p16, const int8_t* dy_p16, int32_t* acc,
                           uint32_t* amax, void* ws, size_t ws_bytes, int splits, hipStream_t st, hipEvent_t ev_b,
-                          hipEvent_t ev_e, unsigned long long* span, SlabReduce* defer) {
+                          hipEvent_t ev_e, unsigned long long* span) {
     WgP16 t;
     if (!p16_geom(g, &t)) return hipErrorInvalidValue;
     if (splits <= 0) splits = conv_wgrad_p16_splits(g);
@@ -735,15 +735,8 @@ hipError_t conv_wgrad_p16(const ConvGeom& g, const int8_t* x_p16, const int8_t* 
         default: launch(wgrad_p16_kernel<2, NW, NITI_WG_D4>); break;
     }
     hipError_t e = hipGetLastError();
-    if (e == hipSuccess && t.splits > 1) {
-        const int64_t n = (int64_t)g.c_out * 9 * g.cip;
-        if (defer != nullptr)
-            *defer = SlabReduce{t.slab, t.splits, n, t.slab_stride, acc, amax};
-        else
-            e = splitk_reduce_linear(t.slab, t.splits, n, t.slab_stride, acc, amax, st);
-    } else if (defer != nullptr) {
-        *defer = SlabReduce{};
-    }
+    if (e == hipSuccess && t.splits > 1)
+        e = splitk_reduce_linear(t.slab, t.splits, (int64_t)g.c_out * 9 * g.cip, t.slab_stride, acc, amax, st);
     return e;
 }
 
