@@ -301,7 +301,10 @@ def main():
     ap.add_argument("--overlap", action="store_true",
                     help="weight gradients on a second stream beside the input-gradient chain (measured within 1 %% "
                          "of the single-stream step on MI355X, and it slows the overlapped kernels by sharing the CUs)")
-    ap.add_argument("--no-overlap", action="store_true", help="(default) weight gradients on the step stream")
+    ap.add_argument("--no-overlap", action="store_true", help="weight gradients on the step stream (the default on one "
+                                                              "GPU; data parallel defaults to the side stream, where the "
+                                                              "weight gradients run while the input-gradient chain waits "
+                                                              "on its range all-reduces)")
     ap.add_argument("--probe-plan", default="", help="bm,bn,splits,strategy forced on the probed GEMM after "
                                                      "autotuning (PMC passes re-use the timed run's plan)")
     ap.add_argument("--save-plans", default="", help="write the autotuned GEMM plans to this JSON file")
@@ -337,7 +340,10 @@ def main():
         args.cpu_sample = {niti_amd.ARCH_VGG16: 2, niti_amd.ARCH_LENET: 512}.get(arch, 128)
     model = NitiModel(arch, args.batch, args.in_hw)
     model.set_graph(args.graph)
-    model.set_overlap(args.overlap and not args.no_overlap)
+    # data parallel: the input-gradient chain stops at every layer for a MAX all-reduce of its range
+    # (latency-bound); weight gradients on the side stream fill those waits
+    overlap = (args.overlap or world > 1) and not args.no_overlap
+    model.set_overlap(overlap)
     model.keep_grads(False)  # no int8 weight-gradient tap: NITI_SGD consumes the gradient in-kernel
     for i, (w, s) in enumerate(synth_weights(model.layers, seed=17)):
         model.set_weight(i, w, s)
@@ -505,8 +511,8 @@ def main():
                                if arch != niti_amd.ARCH_LENET else "LeNet NITI int8 training step, 1x28x28",
                    "global_batch": args.batch * world, "per_gpu_batch": args.batch,
                    "parallelism": parallelism_label(world, "RCCL all-reduce MAX ranges + SUM int32 grads"),
-                   "streams": "weight gradients beside the input-gradient chain on a second stream" if args.overlap
-                   and not args.no_overlap else "one stream (weight gradient, then input gradient, per layer)"},
+                   "streams": "weight gradients beside the input-gradient chain on a second stream" if overlap
+                   else "one stream (weight gradient, then input gradient, per layer)"},
         "int8_mfma_tops": round(tops, 2),
         "int8_mfma_frac_of_peak": round(tops / PEAK_INT8_TOPS, 4),
         "roofline": {
