@@ -307,6 +307,10 @@ def main():
                                                               "on its range all-reduces)")
     ap.add_argument("--probe-plan", default="", help="bm,bn,splits,strategy forced on the probed GEMM after "
                                                      "autotuning (PMC passes re-use the timed run's plan)")
+    ap.add_argument("--dp-path", action="store_true", help="diagnostic: run the data-parallel step on one GPU (a "
+                                                           "one-rank in-process group: the two-launch row kernels, "
+                                                           "the range / gradient collectives as no-ops) to time the "
+                                                           "protocol's own cost without the network")
     ap.add_argument("--save-plans", default="", help="write the autotuned GEMM plans to this JSON file")
     ap.add_argument("--load-plans", default="", help="use the GEMM plans of this JSON file (no autotuning): the "
                                                      "profiled and PMC passes replay the timed run's launch sequence")
@@ -351,6 +355,10 @@ def main():
         uid = [NitiModel.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         model.attach_comm(uid[0], rank, world, exact=True)
+    elif args.dp_path:
+        from niti_amd.model import LocalGroup
+        dp_group = LocalGroup(1)
+        model.attach_local(dp_group, 0, exact=True)
 
     l0 = model.layers[0]
     rng = np.random.default_rng(100 + rank)

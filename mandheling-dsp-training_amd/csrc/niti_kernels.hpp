@@ -220,7 +220,12 @@ struct RowConvOut {
     int pool_relu = 0;
     // input gradient: the same gradient in the weight gradient's P16 layout (rowconv_p16_ok)
     int8_t* p16 = nullptr;
+    // modes RANGE + REQUANT (data parallel: the MAX all-reduce sits between them): the range
+    // launch also stores every unit's int32 accumulators here (rowconv_acc_bytes) and the
+    // requantise launch reads them back instead of recomputing the GEMM
+    int32_t* acc_store = nullptr;
 };
+size_t rowconv_acc_bytes(const ConvGeom& g, bool dg);
 constexpr int ROWCONV_BAR_WORDS = 2 * 19 * 32;  // grid-barrier state (both parities)
 static_assert(ROWCONV_BAR_WORDS == NITI_ROWCONV_STATE_WORDS, "header constant");
 bool rowconv_ok(const ConvGeom& g);

@@ -212,6 +212,7 @@ struct LocalCollective final : Collective {
     int rank = 0, chan = 0;
     int size() const override { return g->world; }
     hipError_t allreduce(void* p, size_t n, CollOp op, hipStream_t st) override {
+        if (g->world == 1) return hipSuccess;  // one rank: the all-reduce is the identity
         LocalChannel& c = g->ch[chan];
         hipError_t e = hipStreamSynchronize(st);
         std::unique_lock<std::mutex> lk(c.mu);
@@ -331,6 +332,10 @@ struct Model {
     bool use_rowconv = true;
     std::vector<char> xc32_valid;
     uint32_t* rc_err = nullptr;
+    // the row kernels' accumulator store for their two-launch form (data parallel, graph capture):
+    // the range launch keeps its int32 accumulators here, the requantise launch reads them back
+    int32_t* rc_acc = nullptr;
+    size_t rc_acc_size = 0;
     bool rowconv_layer(int i) const { return use_rowconv && L[i].rc; }
     // dyc32_valid[i]: L[i].dyc32 holds L[i].dy as it is now (written by the next layer's input
     // gradient epilogue, else converted)
@@ -758,6 +763,7 @@ int Model::build(int arch_, int batch_, int in_hw) {
             if (hipMemset(l.bar, 0, ROWCONV_BAR_WORDS * 4) != hipSuccess ||
                 hipMemset(l.wf, 0, rowconv_wf_bytes(g.c_out, g.c_in)) != hipSuccess)
                 return NITI_NO_EXECUTION;
+            rc_acc_size = std::max(rc_acc_size, rowconv_acc_bytes(g, false));
             // the input gradient too, where the previous layer's output (pooled 2x2 or not) is
             // this layer's input as is
             const Layer* pv = i > 0 ? &L[i - 1] : nullptr;
@@ -766,6 +772,7 @@ int Model::build(int arch_, int batch_, int in_hw) {
                                          : (pv->g.oh == g.h && pv->g.ow == g.w));
             if (pv_ok && rowconv_dgrad_geom(g, &l.dg)) {
                 l.rcd = 1;
+                rc_acc_size = std::max(rc_acc_size, rowconv_acc_bytes(l.dg, true));
                 l.wft = (int8_t*)ws.alloc(rowconv_wf_bytes(g.c_in, g.c_out));
                 l.dyc32 = (int8_t*)ws.alloc(out_px * round_up(g.c_out, 32));
                 if (!l.wft || !l.dyc32) return NITI_OUT_OF_MEMORY;
@@ -798,6 +805,10 @@ int Model::build(int arch_, int batch_, int in_hw) {
     if (slab_w_bytes) {
         slab_w = ws.alloc(slab_w_bytes);
         if (!slab_w) return NITI_OUT_OF_MEMORY;
+    }
+    if (rc_acc_size) {
+        rc_acc = (int32_t*)ws.alloc(rc_acc_size);
+        if (!rc_acc) return NITI_OUT_OF_MEMORY;
     }
     amax_bytes = (size_t)3 * nl * MAX_BYTES;
     amax = (uint32_t*)ws.alloc(amax_bytes);
@@ -927,6 +938,7 @@ int Model::fwd_layer(int i, hipStream_t st) {
         if (!dp && !capturing && rowconv_fused_ok(g)) {
             MTRY(rowconv_fwd(g, l.xc32, l.wf, o, 0, rng(i, 0), l.bar, ++l.epoch, rc_err, st));
         } else {
+            o.acc_store = rc_acc;
             MTRY(rowconv_fwd(g, l.xc32, l.wf, o, 1, rng(i, 0), nullptr, 0, nullptr, st));
             if (dp && exact) CTRY(coll->allreduce(rng(i, 0), MAX_WORDS, COLL_MAX_U32, st));
             MTRY(rowconv_fwd(g, l.xc32, l.wf, o, 2, rng(i, 0), nullptr, 0, nullptr, st));
@@ -1093,6 +1105,7 @@ int Model::dgrad_layer(int i, hipStream_t st) {
         if (!dp && !capturing && rowconv_fused_ok(d, true)) {
             MTRY(rowconv_fwd(d, l.dyc32, l.wft, o, 0, rng(i, 1), l.bar, ++l.epoch, rc_err, st));
         } else {
+            o.acc_store = rc_acc;
             MTRY(rowconv_fwd(d, l.dyc32, l.wft, o, 1, rng(i, 1), nullptr, 0, nullptr, st));
             if (dp && exact) CTRY(coll->allreduce(rng(i, 1), MAX_WORDS, COLL_MAX_U32, st));
             MTRY(rowconv_fwd(d, l.dyc32, l.wft, o, 2, rng(i, 1), nullptr, 0, nullptr, st));

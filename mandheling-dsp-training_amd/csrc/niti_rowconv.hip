@@ -169,6 +169,7 @@ struct RowConvArgs {
     int pool_relu;
     int8_t* p16;                 // P16 [pixels/16][cop][16] copy of out / pool_dx, or null
     int64_t p16_pixels;          // pixels of that tensor
+    int32_t* acc_store;          // RANGE writes / REQUANT reads every unit's accumulators, or null
     // W = 1 (1x1 maps, the classifier head): x is row-major [n][xld], the weights row-major
     // [rows][wld] (OHWI16 forward, IHWO16 input gradient), K the reduced channels
     int xld, wld, K, rows;
@@ -740,6 +741,36 @@ __device__ __forceinline__ void rowconv_epilogue(const RowConvArgs& a, const Row
     }
 }
 
+// a unit's accumulators in acc_store: [unit][r][i / 4][lane][4] -- one 1 KiB wave store / load per
+// 4 registers (unit = workgroup tile x 4 + wave; a K-split workgroup's unit is its wave 0's)
+template <int R>
+__device__ __forceinline__ int32_t* acc_slot(const RowConvArgs& a, int wg, int wid, int lane) {
+    return a.acc_store + ((int64_t)(wg * 4 + wid) * R) * 1024 + lane * 4;
+}
+template <int R>
+__device__ __forceinline__ void acc_put(const RowConvArgs& a, int wg, int wid, int lane, const v16i (&acc)[R]) {
+    int32_t* p = acc_slot<R>(a, wg, wid, lane);
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            *(v4i*)(p + r * 1024 + q * 256) = v4i{acc[r][4 * q], acc[r][4 * q + 1], acc[r][4 * q + 2], acc[r][4 * q + 3]};
+}
+template <int R>
+__device__ __forceinline__ void acc_get(const RowConvArgs& a, int wg, int wid, int lane, v16i (&acc)[R]) {
+    const int32_t* p = acc_slot<R>(a, wg, wid, lane);
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const v4i v = *(const v4i*)(p + r * 1024 + q * 256);
+            acc[r][4 * q] = v[0];
+            acc[r][4 * q + 1] = v[1];
+            acc[r][4 * q + 2] = v[2];
+            acc[r][4 * q + 3] = v[3];
+        }
+}
+
 __device__ __forceinline__ void write_exponent(const RowConvArgs& a, uint32_t gmax) {
     if (a.exp_out == nullptr) return;
     const int shift = bitwidth_rc(gmax) - 7;
@@ -822,9 +853,11 @@ __global__ void __launch_bounds__(256, (RC_EXP & 16) ? 2 : 1) rowconv_fwd_kernel
         for (int wg = blockIdx.x; wg < a.wgs; wg += gridDim.x) {
             const RowUnit<W, R> U(a, wg, wid, c, KS > 0);
             compute_unit<W, R, UNC, KS>(a, U, lane, wid, smem, acc);
-            if (owner)
+            if (owner) {
 #pragma unroll
                 for (int r = 0; r < R; ++r) m = max_abs16(acc[r], m);
+                if (a.acc_store != nullptr) acc_put<R>(a, wg, wid, lane, acc);
+            }
         }
         m = wave_max(m);
         if (lane == 0) red[wid] = m;
@@ -836,7 +869,11 @@ __global__ void __launch_bounds__(256, (RC_EXP & 16) ? 2 : 1) rowconv_fwd_kernel
         if (blockIdx.x == 0 && threadIdx.x == 0) write_exponent(a, g);
         for (int wg = blockIdx.x; wg < a.wgs; wg += gridDim.x) {
             const RowUnit<W, R> U(a, wg, wid, c, KS > 0);
-            compute_unit<W, R, UNC, KS>(a, U, lane, wid, smem, acc);
+            if (a.acc_store != nullptr) {  // the range launch's accumulators (uniform branch)
+                if (owner) acc_get<R>(a, wg, wid, lane, acc);
+            } else {
+                compute_unit<W, R, UNC, KS>(a, U, lane, wid, smem, acc);
+            }
             EpiIn<DG ? R : 1> ein = {};
             if constexpr (DG) {
                 if (owner) {
@@ -961,6 +998,18 @@ static int rowconv_rows(const ConvGeom& g, bool dg, int* units_out) {
     return R;
 }
 
+static int rowconv_ks(const ConvGeom& g, bool dg);
+
+// the accumulator store of modes RANGE + REQUANT: every wave slot of the launch, R x 1 KiB x 4
+size_t rowconv_acc_bytes(const ConvGeom& g, bool dg) {
+    if (!rowconv_ok(g)) return 0;
+    int u = 0;
+    const int R = rowconv_rows(g, dg, &u);
+    const int G = 32 / g.w, ngb = ((g.n + G - 1) / G) * (g.h / R), ngb4 = (ngb + 3) / 4 * 4, COB = g.cop / 32;
+    const int64_t wgs = rowconv_ks(g, dg) > 0 ? (int64_t)COB * ngb : (int64_t)COB * ngb4 / 4;
+    return (size_t)wgs * 4 * R * 1024 * sizeof(int32_t);
+}
+
 bool rowconv_p16_ok(const ConvGeom& d, bool pool) {
     if (!rowconv_ok(d)) return false;
     int u = 0;
@@ -1078,6 +1127,7 @@ hipError_t rowconv_fwd(const ConvGeom& g, const int8_t* x_c32, const int8_t* wf,
     a.pool_relu = o.pool_relu;
     a.p16 = o.p16;
     a.p16_pixels = (int64_t)g.n * g.h * g.w * (o.pool_dx != nullptr ? 4 : 1);
+    a.acc_store = mode == RC_FUSED ? nullptr : o.acc_store;
     if (o.p16 != nullptr && (!dg || !rowconv_p16_ok(g, o.pool_dx != nullptr))) return hipErrorInvalidValue;
     if (o.pool_out != nullptr && (R % 2 != 0 || g.h % 2 != 0)) return hipErrorInvalidValue;
     if (mode == RC_FUSED) {
