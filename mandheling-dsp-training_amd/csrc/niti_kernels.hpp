@@ -373,9 +373,16 @@ hipError_t stats_finalize(const unsigned long long* slots, int nslots, unsigned 
 // as they are (quant = false); x_nchw (may be null) receives the int8 input; stride 1, C / KH / KW
 // = 3/3/3 or 1/5/5 (input_im2col_ok)
 bool input_im2col_ok(int c, int kh, int kw);
+// optional: the first conv's range (NITI_RangeEstimate of its int32 output) from the im2col rows as
+// they are built -- w [co][32] (the K = 32 conv0 weights), cop <= 64 -- published into amax
+struct Conv0Range {
+    const int8_t* w = nullptr;
+    int co = 0, cop = 0;
+    uint32_t* amax = nullptr;
+};
 hipError_t input_im2col(const void* in, bool quant, int n, int c, int h, int w, int kh, int kw, int pt, int pl,
                         const unsigned long long* slots, int nslots, int64_t count, int8_t* x_nchw, int8_t* xcol,
-                        int8_t* ascale, hipStream_t st);
+                        int8_t* ascale, hipStream_t st, const Conv0Range& r0 = Conv0Range{});
 
 // ---- layout transforms --------------------------------------------------------------------
 // NHWC16 [N][H][W][Cp] -> CHWN16 [Cp][H][W][Np]

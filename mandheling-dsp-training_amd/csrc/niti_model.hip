@@ -336,6 +336,8 @@ struct Model {
     // the range launch keeps its int32 accumulators here, the requantise launch reads them back
     int32_t* rc_acc = nullptr;
     size_t rc_acc_size = 0;
+    // the first layer's range came with its im2col copy (input_im2col's Conv0Range) this step
+    bool conv0_ranged = false;
     bool rowconv_layer(int i) const { return use_rowconv && L[i].rc; }
     // dyc32_valid[i]: L[i].dyc32 holds L[i].dy as it is now (written by the next layer's input
     // gradient epilogue, else converted)
@@ -892,7 +894,8 @@ int Model::fwd_layer(int i, hipStream_t st) {
         o.pool.pool_out = l.pool ? l.p : nullptr;
         // the pooled output also as the next layer's C32 input when it runs on the row kernel
         const bool next_c32 = l.pool && i + 1 < (int)L.size() && rowconv_layer(i + 1);
-        MTRY(conv0_fwd(g, l.in, l.w, rng(i, 0), o, 0, st));
+        if (!conv0_ranged) MTRY(conv0_fwd(g, l.in, l.w, rng(i, 0), o, 0, st));
+        conv0_ranged = false;
         if (dp && exact) CTRY(coll->allreduce(rng(i, 0), MAX_WORDS, COLL_MAX_U32, st));
         MTRY(conv0_fwd(g, l.in, l.w, rng(i, 0), o, 1, st, next_c32 ? L[i + 1].xc32 : nullptr));
         if (next_c32) xc32_valid[i + 1] = 1;
@@ -1323,11 +1326,20 @@ int Model::run(const int8_t* x_nchw, int exp_in, const uint8_t* images, const in
     const ConvGeom& o0 = L[0].og;
     const bool fused_in = L[0].col && input_im2col_ok(o0.c_in, o0.kh, o0.kw) && o0.sh == 1 && o0.sw == 1;
     x0_nchw_valid = fused_in;
+    // the first conv's range pass rides in the im2col launch (its rows are in registers there)
+    Conv0Range r0;
+    if (fused_in && conv0_ok(L[0].g) && !L[0].flatten && L[0].g.cop <= 64) {
+        r0.w = L[0].w;
+        r0.co = L[0].g.c_out;
+        r0.cop = L[0].g.cop;
+        r0.amax = rng(0, 0);
+    }
+    conv0_ranged = r0.w != nullptr;
     if (x_nchw != nullptr) {
         MTRY(hipMemsetAsync(exp0, exp_in, 1, st));
         if (fused_in)
             MTRY(input_im2col(x_nchw, false, n, in_c, in_h, in_w, o0.kh, o0.kw, o0.pt, o0.pl, nullptr, 0, 0, x0n,
-                              L[0].xcol, nullptr, st));
+                              L[0].xcol, nullptr, st, r0));
         else
             MTRY(nchw_to_nhwc16(x_nchw, n, in_c, in_h * in_w, round_up(in_c, 16), x0, st));
     } else {
@@ -1350,7 +1362,7 @@ int Model::run(const int8_t* x_nchw, int exp_in, const uint8_t* images, const in
         const int64_t count = dp && exact ? px * world : px;
         if (fused_in)
             MTRY(input_im2col(images, true, n, in_c, in_h, in_w, o0.kh, o0.kw, o0.pt, o0.pl, slots, ns, count, x0n,
-                              L[0].xcol, exp0, st));
+                              L[0].xcol, exp0, st, r0));
         else
             MTRY(image_quantize(images, n, in_c, in_h * in_w, round_up(in_c, 16), qstats, count, x0, exp0, true, st));
     }

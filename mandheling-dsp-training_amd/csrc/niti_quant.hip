@@ -27,6 +27,7 @@
 // logf taken as the correctly rounded float natural log, (float)log((double)range), so host and
 // device agree bit for bit.  A constant batch (std = 0) is undefined in the reference (0/0); here
 // it quantises to zeros with ascale = -7.
+#include "niti_device.hpp"
 #include "niti_kernels.hpp"
 #include "niti_map.hpp"
 
@@ -244,7 +245,7 @@ __global__ void __launch_bounds__(256) input_im2col_kernel(const void* __restric
                                                            const unsigned long long* __restrict__ slots, int nslots,
                                                            int64_t count, int64_t var_count,
                                                            int8_t* __restrict__ x_nchw, int8_t* __restrict__ xcol,
-                                                           int8_t* __restrict__ ascale) {
+                                                           int8_t* __restrict__ ascale, Conv0Range r0) {
     static_assert(C <= 4 && C * KH * KW <= 32, "one 32-byte im2col row");
     extern __shared__ __attribute__((aligned(16))) uint32_t px[];  // [rows][w + KW - 1] 4-byte pixels
     __shared__ QuantParams sq;
@@ -287,23 +288,76 @@ __global__ void __launch_bounds__(256) input_im2col_kernel(const void* __restric
     }
     __syncthreads();
     const int npx = (oy1 - oy0) * ow;
-    for (int t = threadIdx.x; t < npx; t += blockDim.x) {
+    // the first conv's range (r0.w set): its GEMM over the rows just built, K = 32, one
+    // v_mfma_i32_32x32x32_i8 per 32 pixels x 32 output channels -- the wave's 64 pixels are two
+    // B tiles after one half-wave swap (lane l holds pixel l's 32 bytes; a tile wants lane l and
+    // l + 32 to hold the two 16-byte halves of pixel l), the weights' A fragments loaded once
+    const int lane = threadIdx.x & 63, hh = lane >> 5;
+    v4i wa[2] = {};
+    if (r0.w != nullptr) {
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const int co = t * 32 + (lane & 31);
+            if (t * 32 < r0.cop && co < r0.co) wa[t] = *(const v4i*)(r0.w + co * 32 + 16 * hh);
+        }
+    }
+    uint32_t m0 = 0;
+    const int npx_r = r0.w != nullptr ? (npx + blockDim.x - 1) / blockDim.x * blockDim.x : npx;
+    for (int t = threadIdx.x; t < npx_r; t += blockDim.x) {
         const int oy = t / ow, ox = t - oy * ow;
-        uint32_t d[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        uint32_t d[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // t >= npx (a whole-wave MFMA pass): a zero column
+        const int ld = t < npx ? (oy * wp + ox) : 0;  // (past the band: any staged pixel, masked below)
+        const uint32_t keep = t < npx ? 0xffffffffu : 0u;
 #pragma unroll
         for (int ky = 0; ky < KH; ++ky)
 #pragma unroll
             for (int kx = 0; kx < KW; ++kx) {
-                const uint32_t v = px[(oy + ky) * wp + ox + kx];
+                const uint32_t v = px[ld + ky * wp + kx] & keep;
 #pragma unroll
                 for (int c = 0; c < C; ++c) {
                     const int k = (ky * KW + kx) * C + c;
                     d[k >> 2] |= ((v >> (8 * c)) & 0xffu) << (8 * (k & 3));
                 }
             }
-        int8_t* o = xcol + (((int64_t)img * oh + oy0 + oy) * ow + ox) * 32;
-        *(v4i_q*)o = v4i_q{(int)d[0], (int)d[1], (int)d[2], (int)d[3]};
-        *(v4i_q*)(o + 16) = v4i_q{(int)d[4], (int)d[5], (int)d[6], (int)d[7]};
+        if (t < npx) {
+            int8_t* o = xcol + (((int64_t)img * oh + oy0 + oy) * ow + ox) * 32;
+            *(v4i_q*)o = v4i_q{(int)d[0], (int)d[1], (int)d[2], (int)d[3]};
+            *(v4i_q*)(o + 16) = v4i_q{(int)d[4], (int)d[5], (int)d[6], (int)d[7]};
+        }
+        if (r0.w != nullptr) {
+            // lanes < 32: own bytes 0..15 (tile 0) and, from lane + 32, its bytes 0..15 (tile 1);
+            // lanes >= 32: from lane - 32, its bytes 16..31 (tile 0) and own bytes 16..31 (tile 1)
+            // v_permlane32_swap(x, y) swaps the lower half-wave's y with the upper half-wave's x:
+            // lanes >= 32 get y of lane - 32 as the first result, lanes < 32 get x of lane + 32 as
+            // the second (conv0_kernel's pack() relies on the same)
+            v4i b0, b1;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const auto sw = __builtin_amdgcn_permlane32_swap(d[j], d[4 + j], false, false);
+                b0[j] = hh == 0 ? (int)d[j] : (int)sw[0];
+                b1[j] = hh == 0 ? (int)sw[1] : (int)d[4 + j];
+            }
+#pragma unroll
+            for (int tc = 0; tc < 2; ++tc) {
+                if (tc * 32 >= r0.cop) break;
+#pragma unroll
+                for (int tp = 0; tp < 2; ++tp) {
+                    const v16i acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(wa[tc], tp ? b1 : b0, v16i{}, 0, 0, 0);
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) {
+                        const uint32_t u = uabs32(acc[i]);
+                        m0 = m0 > u ? m0 : u;
+                    }
+                }
+            }
+        }
+    }
+    if (r0.w != nullptr) {  // output channels >= co have zero weights: their sums are 0
+        m0 = wave_max_u32(m0);
+        __shared__ uint32_t red0[4];
+        if (lane == 0) red0[threadIdx.x >> 6] = m0;
+        __syncthreads();
+        if (threadIdx.x == 0) publish_max(r0.amax, max(max(red0[0], red0[1]), max(red0[2], red0[3])));
     }
 }
 
@@ -328,8 +382,9 @@ bool input_im2col_ok(int c, int kh, int kw) { return (c == 3 && kh == 3 && kw ==
 
 hipError_t input_im2col(const void* in, bool quant, int n, int c, int h, int w, int kh, int kw, int pt, int pl,
                         const unsigned long long* slots, int nslots, int64_t count, int8_t* x_nchw, int8_t* xcol,
-                        int8_t* ascale, hipStream_t st) {
+                        int8_t* ascale, hipStream_t st, const Conv0Range& r0) {
     if (!input_im2col_ok(c, kh, kw) || n <= 0 || (quant && (count <= 0 || slots == nullptr))) return hipErrorInvalidValue;
+    if (r0.w != nullptr && (r0.amax == nullptr || r0.cop > 64 || r0.cop % 32 != 0 || r0.co > r0.cop)) return hipErrorInvalidValue;
     const int oh = h + 2 * pt - kh + 1, ow = w + 2 * pl - kw + 1;
     if (oh <= 0 || ow <= 0) return hipErrorInvalidValue;
     // bands of output rows: ~16 KiB of staged pixels, at least 2 workgroups per image at 32x32
@@ -342,7 +397,7 @@ hipError_t input_im2col(const void* in, bool quant, int n, int c, int h, int w, 
     const dim3 grid((unsigned)((int64_t)n * bands));
 #define IIC(CC, KK, Q)                                                                                            \
     hipLaunchKernelGGL((input_im2col_kernel<CC, KK, KK, Q>), grid, dim3(256), lds, st, in, n, h, w, oh, ow, pt, pl, \
-                       band, slots, nslots, count, var_count, x_nchw, xcol, ascale)
+                       band, slots, nslots, count, var_count, x_nchw, xcol, ascale, r0)
     if (c == 3 && quant)
         IIC(3, 3, true);
     else if (c == 3)
