@@ -301,10 +301,7 @@ def main():
     ap.add_argument("--overlap", action="store_true",
                     help="weight gradients on a second stream beside the input-gradient chain (measured within 1 %% "
                          "of the single-stream step on MI355X, and it slows the overlapped kernels by sharing the CUs)")
-    ap.add_argument("--no-overlap", action="store_true", help="weight gradients on the step stream (the default on one "
-                                                              "GPU; data parallel defaults to the side stream, where the "
-                                                              "weight gradients run while the input-gradient chain waits "
-                                                              "on its range all-reduces)")
+    ap.add_argument("--no-overlap", action="store_true", help="(default) weight gradients on the step stream")
     ap.add_argument("--probe-plan", default="", help="bm,bn,splits,strategy forced on the probed GEMM after "
                                                      "autotuning (PMC passes re-use the timed run's plan)")
     ap.add_argument("--dp-path", action="store_true", help="diagnostic: run the data-parallel step on one GPU (a "
@@ -344,9 +341,10 @@ def main():
         args.cpu_sample = {niti_amd.ARCH_VGG16: 2, niti_amd.ARCH_LENET: 512}.get(arch, 128)
     model = NitiModel(arch, args.batch, args.in_hw)
     model.set_graph(args.graph)
-    # data parallel: the input-gradient chain stops at every layer for a MAX all-reduce of its range
-    # (latency-bound); weight gradients on the side stream fill those waits
-    overlap = (args.overlap or world > 1) and not args.no_overlap
+    # (data parallel keeps the default too: a third stream beside the step stream and the gradient
+    # communicator's stream would share the process's 4 hardware queues with two RCCL
+    # communicators, whose spinning kernels must never queue behind one another)
+    overlap = args.overlap and not args.no_overlap
     model.set_overlap(overlap)
     model.keep_grads(False)  # no int8 weight-gradient tap: NITI_SGD consumes the gradient in-kernel
     for i, (w, s) in enumerate(synth_weights(model.layers, seed=17)):
