@@ -146,8 +146,9 @@ struct Collective {
 struct RcclCollective final : Collective {
     ncclComm_t comm = nullptr;
     int world = 1;
+    bool owns = true;  // false: another RcclCollective's communicator (the no-split fallback)
     ~RcclCollective() override {
-        if (comm) (void)ncclCommDestroy(comm);
+        if (comm && owns) (void)ncclCommDestroy(comm);
     }
     int size() const override { return world; }
     hipError_t allreduce(void* p, size_t n, CollOp op, hipStream_t st) override {
@@ -434,6 +435,9 @@ struct Model {
     int world = 1, rank = 0, exact = 1;
     bool dp() const { return coll != nullptr && coll_grad != nullptr && !tuning; }
     hipStream_t cst = nullptr;
+    // the gradient SUMs share the range communicator (ncclCommSplit unavailable): they then run on
+    // the weight-gradient stream itself, keeping that one communicator in program order
+    bool shared_comm = false;
     std::vector<hipEvent_t> ev_bucket;  // per layer: the bucket closed after this layer's weight gradient
     hipEvent_t ev_grads = nullptr;      // every bucket summed and ranged (the NITI_SGD join)
     size_t bucket_min_bytes = size_t(8) << 20;
@@ -1031,6 +1035,16 @@ int Model::sum_bucket(int lo, hipStream_t wst) {
     int hi = lo;
     while (hi + 1 < (int)L.size() && bucket_lo[hi + 1] == lo) ++hi;
     MTRY(hipEventRecord(ev_bucket[lo], wst));
+    if (shared_comm) {  // one communicator: the SUMs stay in the step's program order
+        size_t elems = 0;
+        for (int j = lo; j <= hi; ++j) elems += (size_t)L[j].w_elems();
+        CTRY(coll_grad->allreduce(L[lo].dwacc, elems, COLL_SUM_I32, wst));
+        AbsmaxJob jobs[ABSMAX_MAX_JOBS];
+        if (hi - lo + 1 > ABSMAX_MAX_JOBS) return NITI_NOT_SUPPORT;
+        for (int j = lo; j <= hi; ++j) jobs[j - lo] = AbsmaxJob{L[j].dwacc, L[j].w_elems(), rng(j, 2), 0};
+        MTRY(absmax_many(jobs, hi - lo + 1, wst));
+        return NITI_NO_ERROR;
+    }
     MTRY(hipStreamWaitEvent(cst, ev_bucket[lo], 0));
     size_t elems = 0;
     for (int j = lo; j <= hi; ++j) elems += (size_t)L[j].w_elems();
@@ -1377,7 +1391,7 @@ int Model::run(const int8_t* x_nchw, int exp_in, const uint8_t* images, const in
         dp16_valid[nl - 1] = 0;
     }
     // weight gradients on the side stream (not inside a graph capture)
-    const bool ov = overlap && !capturing;
+    const bool ov = overlap && !capturing && !(dp && shared_comm);  // one communicator: one stream
     if (ov) {
         const int rc = ensure_streams();
         if (rc != NITI_NO_ERROR) return rc;
@@ -1808,8 +1822,15 @@ int niti_model_attach_comm(niti_model_t m, const char id[NITI_UNIQUE_ID_BYTES], 
     // the gradient communicator: split off the first (collective over the ranks), its own
     // resources, so its SUMs and the ranges' MAXes are not serialised against each other
     auto cg = std::make_unique<niti::RcclCollective>();
-    if (ncclCommSplit(c->comm, 0, rank, &cg->comm, nullptr) != ncclSuccess) return NITI_NO_EXECUTION;
+    bool shared = false;
+    if (ncclCommSplit(c->comm, 0, rank, &cg->comm, nullptr) != ncclSuccess) {
+        // no split: the gradient SUMs use the range communicator, in the step's program order
+        cg->comm = c->comm;
+        cg->owns = false;
+        shared = true;
+    }
     cg->world = world;
+    m->m.shared_comm = shared;
     m->m.drop_graph();
     m->m.coll = std::move(c);
     m->m.coll_grad = std::move(cg);
@@ -1847,9 +1868,13 @@ int niti_model_attach_local(niti_model_t m, niti_local_group_t g, int rank, int 
     auto cg = std::make_unique<niti::LocalCollective>();
     cg->g = g->g;
     cg->rank = rank;
-    cg->chan = 1;
+    // NITI_DIAG_SHARED_COMM=1 (tests): the gradient SUMs on the range channel, as attach_comm's
+    // no-split fallback runs them on one RCCL communicator
+    const bool shared = getenv("NITI_DIAG_SHARED_COMM") != nullptr;
+    cg->chan = shared ? 0 : 1;
     m->m.drop_graph();
     m->m.coll = std::move(c);
+    m->m.shared_comm = shared;
     m->m.coll_grad = std::move(cg);
     m->m.world = g->g->world;
     m->m.rank = rank;
