@@ -294,7 +294,8 @@ def main():
                                                                "the second leg uses every core of this process")
     ap.add_argument("--int8-input", action="store_true", help="feed pre-quantised int8 x with a fixed exponent "
                                                               "instead of uint8 images through the device quantiser")
-    ap.add_argument("--probe-layer", type=int, default=3, help="layer whose GEMM is timed for the roofline")
+    ap.add_argument("--probe-layer", type=int, default=-1, help="layer whose GEMM is timed for the roofline (default: "
+                                                                "3, VGG-11 / VGG-16 conv4; LeNet: 1, its 5x5 conv2)")
     ap.add_argument("--probe-phase", type=int, default=2, help="0 fwd, 1 input grad, 2 weight grad")
     ap.add_argument("--graph", action="store_true", help="replay the step as a hipGraph (slower on ROCm 7.2)")
     ap.add_argument("--no-autotune", action="store_true", help="keep the fixed default GEMM plans")
@@ -393,6 +394,8 @@ def main():
         if args.wgrad_p16 >= 0:
             sp = args.wgrad_p16 or p[2]
             model.set_plan(i, 2, (16, 16, sp, 2 if sp > 1 else 0))
+    if args.probe_layer < 0:
+        args.probe_layer = 1 if arch == niti_amd.ARCH_LENET else 3
     probe_layer = args.probe_layer if args.probe_layer < len(model.layers) else len(model.layers) - 1
     if args.probe_plan:
         model.set_plan(probe_layer, args.probe_phase, [int(v) for v in args.probe_plan.split(",")])
