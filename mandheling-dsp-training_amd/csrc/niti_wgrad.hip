@@ -30,7 +30,11 @@
 // Split K: the blocks of a split tile store their partial tiles (plain stores, C's layout) into
 // per-split slabs, which splitk_reduce_linear sums into C with the max|C| of NITI_RangeEstimate.
 // (An in-launch combine -- write-through partials, an arrival ticket, the last block summing --
-// was measured: the publish and the latency-bound combine took ~15 us of a 26 us launch.)
+// was measured: the publish and the latency-bound combine took ~15 us of a 26 us launch.  Round 3
+// measured it again on the current kernel -- plain slab stores, agent-scope fences around a
+// per-tile arrival word, the last split summing the others' slabs with 36 loads in flight: an 8x8 layer
+// 26.1 us against 10.3 us + a 4.8 us reduce launch, and the autotuner then preferred the taps
+// kernel for conv4; step 0.423 ms against 0.403 ms.)
 #include <hip/hip_ext.h>
 
 #include <algorithm>
