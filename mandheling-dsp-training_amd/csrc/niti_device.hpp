@@ -161,4 +161,46 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, int8_t* lds_wave
                                              soff, 0, 0);
 }
 
+// P16 conversion jobs (niti_wgrad.hip: nhwc16_to_p16_many; niti_kernels.hip: loss_grad_p16)
+struct P16Job {
+    const int8_t* in;
+    int8_t* out;
+    int64_t blocks;
+    int lg;       // log2 CP
+    uint32_t wg0; // first workgroup
+};
+struct P16Jobs {
+    P16Job j[P16_MAX_JOBS];
+    int n;
+};
+
+// one workgroup's share of a P16Jobs launch (256 threads; tile: 16 KiB of LDS, 16-byte aligned)
+__device__ __forceinline__ void p16_convert_block(const P16Jobs& J, uint32_t wg, int8_t* tile) {
+    int k = 0;
+    while (k + 1 < J.n && wg >= J.j[k + 1].wg0) ++k;
+    const P16Job jb = J.j[k];
+    const int lg = jb.lg, cp = 1 << lg;
+    const int bpw = lg < 8 ? 1 << (8 - lg) : 1;
+    const int64_t b0 = (int64_t)(wg - jb.wg0) * bpw;
+    const int nb = (int)(jb.blocks - b0 < bpw ? jb.blocks - b0 : bpw);
+    const int bytes = nb * 16 * cp;
+    const int8_t* src = jb.in + b0 * 16 * cp;
+    for (int o = threadIdx.x * 16; o < bytes; o += 256 * 16) *(v4i*)(tile + o) = *(const v4i*)(src + o);
+    __syncthreads();
+    int8_t* dst = jb.out + b0 * 16 * cp;
+    for (int t = threadIdx.x; t < (nb << lg); t += 256) {
+        const int bl = t >> lg, c = t & (cp - 1);
+        const uint8_t* s = (const uint8_t*)tile + (bl << (lg + 4)) + c;
+        v4i o;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            uint32_t w = 0;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) w |= (uint32_t)s[(4 * q + e) << lg] << (8 * e);
+            o[q] = (int)w;
+        }
+        *(v4i*)(dst + (int64_t)t * 16) = o;
+    }
+}
+
 }  // namespace niti

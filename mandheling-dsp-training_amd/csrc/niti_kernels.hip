@@ -3413,10 +3413,9 @@ __device__ __forceinline__ int64_t group16_reduce(int64_t v, bool is_max) {
     }
     return v;
 }
-__global__ void __launch_bounds__(256) loss_grad_kernel(const int8_t* __restrict__ logits, int batch, int classes,
-                                                        int ld, const int8_t* __restrict__ ascale_p,
-                                                        const int32_t* __restrict__ labels, int8_t* __restrict__ out) {
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void loss_rows16(const int8_t* __restrict__ logits, int batch, int classes, int ld,
+                                            const int8_t* __restrict__ ascale_p, const int32_t* __restrict__ labels,
+                                            int8_t* __restrict__ out, int t) {
     const int i = t >> 4, j = t & 15;
     const bool row = i < batch;  // whole groups stay in the shuffles
     const bool cls = row && j < classes;
@@ -3448,6 +3447,24 @@ __global__ void __launch_bounds__(256) loss_grad_kernel(const int8_t* __restrict
     int8_t* O = out + (int64_t)i * ld;
     if (j < ld) O[j] = cls ? (int8_t)psto_any(gf, 4) : (int8_t)0;
     for (int jj = j + 16; jj < ld; jj += 16) O[jj] = 0;
+}
+__global__ void __launch_bounds__(256) loss_grad_kernel(const int8_t* __restrict__ logits, int batch, int classes,
+                                                        int ld, const int8_t* __restrict__ ascale_p,
+                                                        const int32_t* __restrict__ labels, int8_t* __restrict__ out) {
+    loss_rows16(logits, batch, classes, ld, ascale_p, labels, out, blockIdx.x * blockDim.x + threadIdx.x);
+}
+// The loss gradient and the backward pass's P16 copies of the layer inputs in one launch: the
+// first lw workgroups take the loss rows, the rest the conversion jobs (independent data: the
+// copies read forward activations only).  Saves a launch at the head of the backward pass.
+__global__ void __launch_bounds__(256) loss_grad_p16_kernel(const int8_t* __restrict__ logits, int batch, int classes,
+                                                            int ld, const int8_t* __restrict__ ascale_p,
+                                                            const int32_t* __restrict__ labels,
+                                                            int8_t* __restrict__ out, int lw, P16Jobs J) {
+    __shared__ __attribute__((aligned(16))) int8_t tile[16 * 1024];
+    if ((int)blockIdx.x < lw)
+        loss_rows16(logits, batch, classes, ld, ascale_p, labels, out, blockIdx.x * blockDim.x + threadIdx.x);
+    else
+        p16_convert_block(J, blockIdx.x - lw, tile);
 }
 
 // Exponent of a requantised weight gradient, for the DSP op slots whose graph carries one:
@@ -3540,6 +3557,25 @@ __global__ void __launch_bounds__(256) loss_grad_wide_kernel(const int8_t* __res
             if (q == k) gf = (int32_t)(j == tgt ? o[q] - gs : o[q]);
         O[j] = j < classes ? (int8_t)psto_any(gf, 4) : (int8_t)0;
     }
+}
+
+hipError_t p16_jobs_build(const P16Conv* jobs, int n, hipStream_t st, P16Jobs* out, uint32_t* wgs_out);
+
+hipError_t loss_grad_p16(const int8_t* logits, int batch, int classes, int ld, const int8_t* ascale,
+                         const int32_t* labels, int8_t* out, const P16Conv* jobs, int n, hipStream_t st) {
+    if (classes > LOSS_MAXC || ld > LOSS_WIDE_MAXC || classes > ld) {
+        hipError_t e = loss_grad(logits, batch, classes, ld, ascale, labels, out, st);
+        return e != hipSuccess ? e : nhwc16_to_p16_many(jobs, n, st);
+    }
+    P16Jobs J;
+    uint32_t wg = 0;
+    hipError_t e = p16_jobs_build(jobs, n, st, &J, &wg);
+    if (e != hipSuccess) return e;
+    const int lw = (batch + 15) / 16;
+    if (J.n == 0) wg = 0;
+    hipLaunchKernelGGL(loss_grad_p16_kernel, dim3((unsigned)lw + wg), dim3(256), 0, st, logits, batch, classes, ld,
+                       ascale, labels, out, lw, J);
+    return hipGetLastError();
 }
 
 hipError_t loss_grad(const int8_t* logits, int batch, int classes, int ld, const int8_t* ascale, const int32_t* labels,

@@ -133,6 +133,9 @@ struct P16Conv {
 };
 constexpr int P16_MAX_JOBS = 16;
 hipError_t nhwc16_to_p16_many(const P16Conv* jobs, int n, hipStream_t st);
+// loss_grad and nhwc16_to_p16_many(jobs, n) in one launch (two launches for wide class rows)
+hipError_t loss_grad_p16(const int8_t* logits, int batch, int classes, int ld, const int8_t* ascale,
+                         const int32_t* labels, int8_t* out, const P16Conv* jobs, int n, hipStream_t st);
 bool conv_wgrad_p16_ok(const ConvGeom& g);
 // diagnostic builds (NITI_WG_STAMPS): per-block stamps of the following launches, 8 u64 per block
 void wgrad_stamps_arm(unsigned long long* buf);

@@ -379,6 +379,17 @@ struct Model {
         }
         return NITI_NO_ERROR;
     }
+    // every P16 input copy of the backward pass as one job list (false: more than one launch holds)
+    bool p16_input_jobs(P16Conv* jobs, int* n) {
+        *n = 0;
+        for (int j = 0; j < (int)L.size(); ++j)
+            if (wgrad_p16_splits(j)) {
+                if (*n == P16_MAX_JOBS) return false;
+                const ConvGeom& g = L[j].g;
+                jobs[(*n)++] = P16Conv{L[j].in, (int64_t)g.n * g.h * g.w, g.cip, xp16[j]};
+            }
+        return true;
+    }
     int convert_p16_inputs(hipStream_t st) {
         P16Conv jobs[P16_MAX_JOBS];
         int n = 0;
@@ -1385,13 +1396,26 @@ int Model::run(const int8_t* x_nchw, int exp_in, const uint8_t* images, const in
         const int rc = fwd_layer(i, st);
         if (rc != NITI_NO_ERROR) return rc;
     }
-    {
-        Layer& t = L[nl - 1];
-        MTRY(loss_grad(t.r, n, t.g.c_out, t.g.cop, t.exp, labels, t.dy, st));
-        dp16_valid[nl - 1] = 0;
-    }
     // weight gradients on the side stream (not inside a graph capture)
     const bool ov = overlap && !capturing && !(dp && shared_comm);  // one communicator: one stream
+    bool p16_done = false;
+    {
+        Layer& t = L[nl - 1];
+        P16Conv jobs[P16_MAX_JOBS];
+        int nj = 0;
+        if (!ov && p16_input_jobs(jobs, &nj) && nj > 0) {
+            // one stream: the loss gradient and every P16 input copy in one launch (the copies read
+            // forward activations only); A/B on one box, 8 alternating 200-step runs: median step
+            // 0.395 vs 0.400 ms (profiles/r03_lossp16_ab.txt)
+            MTRY(loss_grad_p16(t.r, n, t.g.c_out, t.g.cop, t.exp, labels, t.dy, jobs, nj, st));
+            for (int j = 0; j < nl; ++j)
+                if (wgrad_p16_splits(j)) xp16_valid[j] = 1;
+            p16_done = true;
+        } else {
+            MTRY(loss_grad(t.r, n, t.g.c_out, t.g.cop, t.exp, labels, t.dy, st));
+        }
+        dp16_valid[nl - 1] = 0;
+    }
     if (ov) {
         const int rc = ensure_streams();
         if (rc != NITI_NO_ERROR) return rc;
@@ -1404,7 +1428,7 @@ int Model::run(const int8_t* x_nchw, int exp_in, const uint8_t* images, const in
             MTRY(hipEventRecord(ev_dy[i], st));
             MTRY(hipStreamWaitEvent(side, ev_dy[i], 0));
         }
-        if (i == nl - 1) {  // the forward outputs are final: every P16 input copy in one go
+        if (i == nl - 1 && !p16_done) {  // the forward outputs are final: every P16 input copy in one go
             const int rc = convert_p16_inputs(wst);
             if (rc != NITI_NO_ERROR) return rc;
         }

@@ -545,46 +545,9 @@ __global__ void __launch_bounds__(NW * 64) wgrad_p16_kernel(WgP16 g) {
 // one 16-byte chunk, consecutive lanes consecutive chunks.  CP is a power of two from 32 to 1024:
 // a workgroup takes 256 / CP blocks (CP <= 256) or one block (CP > 256).  One launch serves up to
 // P16_MAX_JOBS tensors, each owning a contiguous range of workgroups.
-struct P16Job {
-    const int8_t* in;
-    int8_t* out;
-    int64_t blocks;
-    int lg;       // log2 CP
-    uint32_t wg0; // first workgroup
-};
-struct P16Jobs {
-    P16Job j[P16_MAX_JOBS];
-    int n;
-};
-
 __global__ void __launch_bounds__(256) nhwc16_to_p16_kernel(P16Jobs J) {
     __shared__ __attribute__((aligned(16))) int8_t tile[16 * 1024];
-    const uint32_t wg = blockIdx.x;
-    int k = 0;
-    while (k + 1 < J.n && wg >= J.j[k + 1].wg0) ++k;
-    const P16Job jb = J.j[k];
-    const int lg = jb.lg, cp = 1 << lg;
-    const int bpw = lg < 8 ? 1 << (8 - lg) : 1;
-    const int64_t b0 = (int64_t)(wg - jb.wg0) * bpw;
-    const int nb = (int)(jb.blocks - b0 < bpw ? jb.blocks - b0 : bpw);
-    const int bytes = nb * 16 * cp;
-    const int8_t* src = jb.in + b0 * 16 * cp;
-    for (int o = threadIdx.x * 16; o < bytes; o += 256 * 16) *(v4i*)(tile + o) = *(const v4i*)(src + o);
-    __syncthreads();
-    int8_t* dst = jb.out + b0 * 16 * cp;
-    for (int t = threadIdx.x; t < (nb << lg); t += 256) {
-        const int bl = t >> lg, c = t & (cp - 1);
-        const uint8_t* s = (const uint8_t*)tile + (bl << (lg + 4)) + c;
-        v4i o;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            uint32_t w = 0;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) w |= (uint32_t)s[(4 * q + e) << lg] << (8 * e);
-            o[q] = (int)w;
-        }
-        *(v4i*)(dst + (int64_t)t * 16) = o;
-    }
+    p16_convert_block(J, blockIdx.x, tile);
 }
 
 // any CP % 16 == 0: one thread per (16-pixel block, 16-channel chunk), a 16 x 16 byte transpose
@@ -608,9 +571,12 @@ __global__ void nhwc16_to_p16_any_kernel(const int8_t* __restrict__ in, int64_t 
     }
 }
 
-hipError_t nhwc16_to_p16_many(const P16Conv* jobs, int n, hipStream_t st) {
+// the power-of-two-CP jobs as one P16Jobs launch of *wgs workgroups; any other CP runs its own
+// generic launch here
+hipError_t p16_jobs_build(const P16Conv* jobs, int n, hipStream_t st, P16Jobs* out, uint32_t* wgs_out) {
     if (n < 0 || n > P16_MAX_JOBS) return hipErrorInvalidValue;
-    P16Jobs J{};
+    P16Jobs& J = *out;
+    J = P16Jobs{};
     uint32_t wg = 0;
     for (int i = 0; i < n; ++i) {
         const P16Conv& c = jobs[i];
@@ -631,6 +597,15 @@ hipError_t nhwc16_to_p16_many(const P16Conv* jobs, int n, hipStream_t st) {
         J.j[J.n++] = P16Job{c.in, c.out, blocks, lg, wg};
         wg += (uint32_t)wgs;
     }
+    *wgs_out = wg;
+    return hipGetLastError();
+}
+
+hipError_t nhwc16_to_p16_many(const P16Conv* jobs, int n, hipStream_t st) {
+    P16Jobs J;
+    uint32_t wg = 0;
+    hipError_t e = p16_jobs_build(jobs, n, st, &J, &wg);
+    if (e != hipSuccess) return e;
     if (J.n > 0) hipLaunchKernelGGL(nhwc16_to_p16_kernel, dim3(wg), dim3(256), 0, st, J);
     return hipGetLastError();
 }
