@@ -19,9 +19,12 @@
 //     range = max(|float(xmax - mean)|, |float(xmin - mean)|) / std   (the max of |Y| sits at
 //             an extreme pixel: fl(x - mean) and fl(./std) are monotonic in x)
 // and the per-pixel formula is evaluated in float in the reference's operation order.  The
-// oracle (oracle/niti_oracle.c niti_ref_quantize_images) states the same contract; its
-// float-sequential restatement (niti_ref_quantize_input) agrees wherever the float sums are
-// exact.  Because the statistics are integers, data-parallel ranks all-reduce them (SUM S1, S2;
+// oracle (oracle/niti_oracle.c niti_ref_image_quantize) states the same contract.  This is an
+// EXACT-STATISTICS CONTRACT, not a float-order match: the reference's float sums have no fixed
+// order under -ffast-math (CMakeLists.txt:429-430; sequential in the C source, vector lanes when
+// compiled), and its float readings (niti_ref_quantize_input_lanes, 1 / 4 / 8 / 16 lanes) move
+// 0-4 of the 256 pixel-value codes by one at the per-GPU BASELINE shapes and agree on ascale
+// (DESIGN.md "Input quantiser", profiles/r04_quant_parity.txt, tests/test_quant.py).  Because the statistics are integers, data-parallel ranks all-reduce them (SUM S1, S2;
 // MAX xmax, 255 - xmin) and quantise their shard exactly as one device would the global batch.
 // ascale is computed in float as the graph does (_Ceil(_Log(range)) on float tensors, :89-91),
 // logf taken as the correctly rounded float natural log, (float)log((double)range), so host and

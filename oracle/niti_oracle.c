@@ -805,16 +805,33 @@ void niti_ref_sgd_update(int8_t* w, const int8_t* g, int64_t n) {
     for (int64_t i = 0; i < n; ++i) w[i] = (int8_t)niti_ref_int8_clip((int32_t)w[i] - (int32_t)g[i]);
 }
 
-/* MnistUtils.cpp:83-93 (float math in the order the expression graph states it).  The variance
- * divisor is the reference's literal `batchSize * 28 * 28` (:86): var_n = images * 784 whatever the
- * image size (for MNIST it equals the pixel count); the mean is ReduceMean over all n values.
+/* MnistUtils.cpp:83-93 in float, in the operation order the expression graph states it, with the
+ * two full reductions (_ReduceMean, _ReduceSum: one axis of n values, OpCommonUtils.cpp:332-333,
+ * summed by CPUReduction.cpp:86-95 `summer += src[a]`) accumulated in `lanes` interleaved partial
+ * sums (value i into partial i % lanes, partials then added in order).  lanes = 1 is the C source's
+ * sequential loop; the engine is compiled with -ffast-math (CMakeLists.txt:429-430), which lets the
+ * compiler reassociate that loop into vector lanes (4-wide NEON / SSE, x2-x4 interleaved), so
+ * lanes = 4 / 8 / 16 are orders the reference binary may equally execute.  The variance divisor is
+ * the reference's literal `batchSize * 28 * 28` (:86): var_n = images * 784 whatever the image size.
  * _Log on a float is taken as the correctly rounded float natural log, (float)log((double)r). */
-int32_t niti_ref_quantize_input(const float* x, int64_t n, int64_t var_n, int8_t* out) {
-    float sum = 0.f;
-    for (int64_t i = 0; i < n; ++i) sum += x[i];
+static float sum_lanes(const float* x, int64_t n, int lanes, float mean, int sq) {
+    float part[64];
+    if (lanes < 1) lanes = 1;
+    if (lanes > 64) lanes = 64;
+    for (int l = 0; l < lanes; ++l) part[l] = 0.f;
+    for (int64_t i = 0; i < n; ++i) {
+        const float v = sq ? (x[i] - mean) * (x[i] - mean) : x[i];
+        part[i % lanes] += v;
+    }
+    float s = part[0];
+    for (int l = 1; l < lanes; ++l) s += part[l];
+    return s;
+}
+
+int32_t niti_ref_quantize_input_lanes(const float* x, int64_t n, int64_t var_n, int lanes, int8_t* out) {
+    const float sum = sum_lanes(x, n, lanes, 0.f, 0);
     const float mean = sum / (float)n;
-    float ss = 0.f;
-    for (int64_t i = 0; i < n; ++i) ss += (x[i] - mean) * (x[i] - mean);
+    const float ss = sum_lanes(x, n, lanes, mean, 1);
     const float sd = sqrtf(ss / (float)var_n);
     float range = 0.f;
     for (int64_t i = 0; i < n; ++i) {
@@ -824,6 +841,10 @@ int32_t niti_ref_quantize_input(const float* x, int64_t n, int64_t var_n, int8_t
     const float bw = ceilf((float)log((double)range));
     for (int64_t i = 0; i < n; ++i) out[i] = (int8_t)roundf((x[i] - mean) / sd / range * 127.0f);
     return (int32_t)(int8_t)(bw - 7.0f);
+}
+
+int32_t niti_ref_quantize_input(const float* x, int64_t n, int64_t var_n, int8_t* out) {
+    return niti_ref_quantize_input_lanes(x, n, var_n, 1, out);
 }
 
 /* MnistUtils.cpp:83-93 stated over exact integer statistics of the uint8 pixels (the

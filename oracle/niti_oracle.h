@@ -141,6 +141,7 @@ void niti_ref_image_stats(const uint8_t* img, int64_t n, uint64_t stats[4]);
 int32_t niti_ref_image_quantize(const uint8_t* img, int64_t n, const uint64_t stats[4], int64_t count,
                                 int64_t var_count, int8_t* out);
 int32_t niti_ref_quantize_input(const float* x, int64_t n, int64_t var_n, int8_t* out);
+int32_t niti_ref_quantize_input_lanes(const float* x, int64_t n, int64_t var_n, int lanes, int8_t* out);
 
 /* ---------------- CPU baseline ---------------- */
 /* One NITI_Conv_Int8 + NITI_GradientConv_Int8 + NITI_DeConv_Int8 pass in the reference's

@@ -85,6 +85,7 @@ def _declare(L):
         "niti_ref_loss_grad": (None, [vp, C.c_int, C.c_int, i32, vp, C.c_int, vp]),
         "niti_ref_sgd_update": (None, [vp, vp, i64]),
         "niti_ref_quantize_input": (i32, [vp, i64, i64, vp]),
+        "niti_ref_quantize_input_lanes": (i32, [vp, i64, i64, C.c_int, vp]),
         "niti_ref_image_stats": (None, [vp, i64, vp]),
         "niti_ref_set_threads": (None, [C.c_int]),
         "niti_ref_image_quantize": (i32, [vp, i64, vp, i64, i64, vp]),
@@ -344,11 +345,13 @@ def sgd_update(w, g):
 MNIST_VAR_PIXELS = 28 * 28  # MnistUtils.cpp:86 divides the variance by batchSize * 28 * 28, literally
 
 
-def quantize_input(x):
-    """x float [n][...]: the float-sequential restatement of MnistUtils.cpp:83-93."""
+def quantize_input(x, lanes=1):
+    """x float [n][...]: the float restatement of MnistUtils.cpp:83-93, its two full reductions
+    summed in `lanes` interleaved partials (1 = the C source's sequential loop; 4 / 8 / 16 = the
+    vector orders -ffast-math lets the compiler choose, niti_ref_quantize_input_lanes)."""
     x = _c(x, np.float32)
     out = np.empty(x.shape, np.int8)
-    a = lib().niti_ref_quantize_input(_p(x), x.size, x.shape[0] * MNIST_VAR_PIXELS, _p(out))
+    a = lib().niti_ref_quantize_input_lanes(_p(x), x.size, x.shape[0] * MNIST_VAR_PIXELS, int(lanes), _p(out))
     return out, int(a)
 
 

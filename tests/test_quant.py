@@ -1,8 +1,9 @@
 """NITIInt8Train's input quantiser (execution-engine/tools/train/source/demo/MnistUtils.cpp:83-93).
 
 CPU: the oracle's exact-statistics contract (niti_ref_image_quantize) against a hand-derived
-known answer and against the float-sequential restatement of the reference expression
-(niti_ref_quantize_input), which it must equal wherever the float sums are exact.
+known answer; against the float restatement of the reference expression (niti_ref_quantize_input_lanes),
+which it equals wherever the float sums are exact; and the documented number of codes the float
+readings (sequential, 4 / 8 / 16 lanes) change at the BASELINE input shapes.
 GPU: the device quantiser (niti_image_stats / niti_image_quantize, and inside the model step)
 bit-exact against the oracle, including statistics all-reduced over two half batches.
 """
@@ -37,17 +38,49 @@ def test_quant_constant_batch_is_zero():
 
 
 @pytest.mark.parametrize("shape", [(64, 1, 28, 28), (20, 1, 28, 28), (16, 3, 32, 32), (2, 3, 7, 5)])
-def test_quant_matches_float_sequential(shape):
-    """While S1 < 2^24 the reference's float sequential mean is exact; the variance sum is the
-    only float accumulation, and the two restatements agree on MNIST / CIFAR-shaped batches."""
+def test_quant_matches_float_sequential_small(shape):
+    """While every float partial sum is exact (S1 < 2^24 and few variance terms) the sequential float
+    reading of MnistUtils.cpp:83-93 and the exact-statistics contract give the same codes."""
     rng = np.random.default_rng(sum(shape))
     img = rng.integers(0, 256, shape).astype(np.uint8)
     x, a = O.quantize_images(img)
     xf, af = O.quantize_input(img.astype(np.float32))
-    assert a == af
-    d = np.abs(x.astype(np.int32) - xf.astype(np.int32))
-    assert d.max() <= 1 and (d > 0).mean() < 1e-3  # tolerance: rounding-boundary flips only
+    assert a == af and np.array_equal(x, xf)
     assert x.min() >= -127 and x.max() <= 127
+
+
+# The documented contract (DESIGN.md "Input quantiser", profiles/r04_quant_parity.txt): the device
+# computes MnistUtils.cpp:83-93 over exact integer statistics; the reference sums in float in an
+# order -ffast-math leaves to the compiler.  Per seed, BASELINE input shape and float order (lanes
+# = interleaved partial sums, 1 = the C loop's sequential order): (differing int8 inputs, pixel
+# values of 256 whose code differs).  Seeded uniform uint8 images, as tools/quant_parity.py.
+QUANT_FLIPS = {
+    (1, (256, 3, 32, 32)): {1: (0, 0), 4: (0, 0), 8: (0, 0), 16: (0, 0)},
+    (5, (256, 3, 32, 32)): {1: (3018, 1), 4: (0, 0), 8: (0, 0), 16: (0, 0)},
+    (1, (64, 1, 28, 28)): {1: (0, 0), 4: (0, 0), 8: (0, 0), 16: (0, 0)},
+    (1, (64, 3, 224, 224)): {1: (0, 0), 4: (37728, 1), 8: (0, 0), 16: (0, 0)},
+    (5, (64, 3, 224, 224)): {1: (37582, 1), 4: (0, 0), 8: (0, 0), 16: (0, 0)},
+    (5, (128, 3, 224, 224)): {1: (300076, 4), 4: (0, 0), 8: (0, 0), 16: (74998, 1)},
+}
+
+
+@pytest.mark.parametrize("key", list(QUANT_FLIPS), ids=lambda k: f"seed{k[0]}-{'x'.join(map(str, k[1]))}")
+def test_quant_contract_flip_counts(key):
+    """Exact-statistics contract vs the float readings: the documented flip counts, each flip a
+    whole pixel-value class moved by one code, the exponent (ascale) equal in every order."""
+    seed, shape = key
+    img = np.random.default_rng(seed).integers(0, 256, shape, dtype=np.uint8)
+    x, a = O.quantize_images(img)
+    f = img.astype(np.float32)
+    for lanes, (flips, classes) in QUANT_FLIPS[key].items():
+        xf, af = O.quantize_input(f, lanes)
+        assert af == a, lanes
+        d = x.astype(np.int16) - xf.astype(np.int16)
+        assert np.abs(d).max() <= 1, lanes
+        moved = np.unique(img[d != 0])
+        assert (int((d != 0).sum()), int(moved.size)) == (flips, classes), lanes
+        # the quantiser is a per-batch map of the 256 pixel values: a flip moves every pixel of a value
+        assert int((d != 0).sum()) == int(np.isin(img, moved).sum()), lanes
 
 
 def test_quant_split_statistics():
