@@ -226,7 +226,9 @@ def bench_resnet18(args):
     k_ops = 2 * batch * g.oh * g.ow * c["co"] * c["ci"] * c["k"] * c["k"]
     roof = {"kernel": f"ResNet-18 {c['name']} forward GEMM (gemm_kernel, implicit im2col, int32 accumulate + range; "
                       "re-run alone after the timed region)",
-            "bound": "mfma", "achieved": round(k_ops / k_us / 1e6, 2), "peak": round(PEAK_INT8_TOPS, 1),
+            "bound": bound,
+            "hbm_frac": round(hbm_frac, 4) if hbm_frac is not None else None,
+            "hbm_bytes_basis": "pmc traffic" if traffic else "algorithmic", "achieved": round(k_ops / k_us / 1e6, 2), "peak": round(PEAK_INT8_TOPS, 1),
             "unit": "TFLOP/s", "frac": round(k_ops / k_us / 1e6 / PEAK_INT8_TOPS, 4), "traffic": None,
             "avg_launch_us": round(k_us, 2), "timing": "HIP events around 20 back-to-back launches on one stream",
             "ops_per_launch": k_ops}
@@ -426,6 +428,9 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    # a fused row-kernel launch whose grid barrier timed out computed garbage: no number from it
+    if model.rowconv_error() != 0:
+        raise RuntimeError("a fused row-kernel grid barrier timed out in the timed region: results invalid")
     probe_ms, probe_n = model.probe_read()
     span_ms, span_n = model.probe_read_span()
     # the same launch alone (after the timed region, nothing else on the GPU): in the step the
@@ -435,6 +440,8 @@ def main():
     for _ in range(iso_reps):
         model.run_phase(probe_layer, args.probe_phase)
     torch.cuda.synchronize()
+    if model.rowconv_error() != 0:
+        raise RuntimeError("a fused row-kernel grid barrier timed out in the isolated re-runs: results invalid")
     iso_ms, iso_n = model.probe_read()
     iso_span_ms, iso_span_n = model.probe_read_span()
     model.set_probe(-1, 0, 0)
@@ -469,6 +476,16 @@ def main():
                 traffic = ent.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
+
+    # which roof bounds the probed launch: the larger of its MFMA fraction and its HBM fraction
+    # (PMC traffic when counted, else the algorithmic bytes: x + dy / w + the int8 output)
+    # (forward: x + w + y; weight gradient: x + dy + dw -- the same three sizes)
+    alg_bytes = args.batch * (pl["h"] * pl["w"] * pl["c_in"] + pl["oh"] * pl["ow"] * pl["c_out"]) + \
+        pl["c_out"] * pl["c_in"] * pl["kh"] * pl["kw"]
+    hbm_bytes = traffic if traffic else alg_bytes
+    mfma_frac = achieved / PEAK_INT8_TOPS if achieved else None
+    hbm_frac = hbm_bytes / k_avg_s / (PEAK_HBM_GBS * 1e9) if probe_n else None
+    bound = "hbm" if (hbm_frac is not None and mfma_frac is not None and hbm_frac > mfma_frac) else "mfma"
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_sample > 0 and args.arch in ("vgg11", "lenet", "vgg16"):
@@ -526,7 +543,9 @@ def main():
         "int8_mfma_frac_of_peak": round(tops / PEAK_INT8_TOPS, 4),
         "roofline": {
             "kernel": f"{args.arch.upper()} conv{probe_layer + 1} {phase_name} launch ({kname}; layer index {probe_layer})",
-            "bound": "mfma",
+            "bound": bound,
+            "hbm_frac": round(hbm_frac, 4) if hbm_frac is not None else None,
+            "hbm_bytes_basis": "pmc traffic" if traffic else "algorithmic",
             "achieved": round(achieved, 2) if achieved else None,
             "peak": round(PEAK_INT8_TOPS, 1),
             "unit": "TFLOP/s",

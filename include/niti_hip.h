@@ -167,9 +167,16 @@ int niti_create_execution(int op_type, const niti_conv2d_common* common, niti_ex
  * int32 accumulator N*C*H*W but its GEMM writes ceil(C/4)*4 channels): NITI_NOT_SUPPORT. */
 int niti_execution_resize(niti_execution_t e, const niti_tensor* inputs, int n_in, const niti_tensor* outputs,
                           int n_out);
-/* Execution::onExecute on `stream` (asynchronous). */
+/* Execution::onExecute on `stream`: asynchronous for device tensors; with any host tensor it stages
+ * them and returns when the host outputs are written, and then also returns NITI_NO_EXECUTION if a
+ * launch flagged its results invalid (the fused row kernel's grid barrier timed out: the grid was
+ * not resident).  Replaces Execution::onExecute (execution-engine/source/core/Execution.hpp:24-82),
+ * codes as ErrorCode.hpp:17-30. */
 int niti_execution_execute(niti_execution_t e, const niti_tensor* inputs, int n_in, const niti_tensor* outputs,
                            int n_out, void* stream);
+/* the asynchronous path's status: synchronizes `stream`, then NITI_NO_EXECUTION (and the flag
+ * cleared) if a launch since the last check flagged invalid results, else NITI_NO_ERROR */
+int niti_execution_status(niti_execution_t e, void* stream);
 void niti_destroy_execution(niti_execution_t e);
 /* bytes of device workspace the handle holds after resize */
 size_t niti_execution_workspace_bytes(niti_execution_t e);
@@ -282,6 +289,9 @@ int niti_conv_wgrad_p16_workspace(const niti_geom* g, int splits, size_t* bytes)
 void niti_diag_wgrad_stamps(void* buf);
 /* diagnostics: device buffer (8 u64 per wave) for the register-fed conv's per-wave stamps; NULL disarms */
 void niti_diag_rowconv_stamps(void* buf);
+/* diagnostics: the fused row kernel's barrier poll limit (0 = default) and a number of arrivals it
+ * waits for that never come (> 0 forces a timeout, to test the error plumbing) for later launches */
+void niti_diag_rowconv_barrier(uint32_t spin_limit, uint32_t expect_extra);
 int niti_conv_wgrad_p16_acc(const niti_geom* g, const int8_t* x_p16, const int8_t* dy_p16, int32_t* acc,
                             uint32_t* amax, void* workspace, size_t workspace_bytes, int splits, void* stream);
 /* acc[m][ldc] = sum_k B[m][k] A[o][k] (columns o..ldc = 0); K zero padded to k16; ldb/lda bytes */

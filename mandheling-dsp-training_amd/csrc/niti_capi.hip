@@ -15,10 +15,12 @@ struct niti_execution {
     int op = 0;
     std::vector<void*> stage;
     std::vector<size_t> stage_bytes;
+    uint32_t* err_host = nullptr;  // pinned copy of the Execution's error word (synchronous calls)
     ~niti_execution() {
         delete impl;
         for (void* p : stage)
             if (p) (void)hipFree(p);
+        if (err_host) (void)hipHostFree(err_host);
     }
 };
 
@@ -76,6 +78,24 @@ size_t tensor_bytes(int op, bool is_out, int idx, const niti_tensor& t) {
     if (!is_out && idx == 1 && op == NITI_OP_DSP_TRANSPOSE_INT8) return 4 * sizeof(int32_t);
     if (t.format == NITI_FORMAT_NC4HW4) return (size_t)(d[0] * ((d[1] + 3) / 4) * 4 * d[2] * d[3]);
     return (size_t)(d[0] * d[1] * d[2] * d[3]);
+}
+
+// The Execution's error word after `st` completes: NITI_NO_EXECUTION (and the word cleared) if a
+// launch flagged invalid results, else NITI_NO_ERROR.  copied: the word was already copied into
+// err_host on `st` (the staged path enqueues that copy before its synchronize).
+int take_error(niti_execution* e, hipStream_t st, bool copied) {
+    uint32_t* dev = e->impl->errorFlag();
+    if (dev == nullptr) return NITI_NO_ERROR;
+    uint32_t v = 0;
+    if (copied) {
+        v = *e->err_host;
+    } else if (hipStreamSynchronize(st) != hipSuccess || hipMemcpy(&v, dev, 4, hipMemcpyDeviceToHost) != hipSuccess) {
+        return NITI_NO_EXECUTION;
+    }
+    if (v == 0) return NITI_NO_ERROR;
+    (void)hipMemsetAsync(dev, 0, 4, st);
+    (void)hipStreamSynchronize(st);
+    return NITI_NO_EXECUTION;
 }
 }  // namespace
 
@@ -142,7 +162,23 @@ int niti_execution_execute(niti_execution_t e, const niti_tensor* in, int nin, c
             hipMemcpyAsync(out[k].data, dout[k].data, tensor_bytes(e->op, true, k, out[k]), hipMemcpyDeviceToHost,
                            st) != hipSuccess)
             return NITI_NO_EXECUTION;
-    return hipStreamSynchronize(st) == hipSuccess ? NITI_NO_ERROR : NITI_NO_EXECUTION;
+    // a synchronous call returns its ErrorCode (ErrorCode.hpp:17-30): a launch that flagged its
+    // results invalid (the fused barrier's timeout) is NO_EXECUTION, not NO_ERROR
+    uint32_t* flag = e->impl->errorFlag();
+    if (flag != nullptr) {
+        if (e->err_host == nullptr && hipHostMalloc((void**)&e->err_host, sizeof(uint32_t)) != hipSuccess) {
+            e->err_host = nullptr;
+            return NITI_OUT_OF_MEMORY;
+        }
+        if (hipMemcpyAsync(e->err_host, flag, 4, hipMemcpyDeviceToHost, st) != hipSuccess) return NITI_NO_EXECUTION;
+    }
+    if (hipStreamSynchronize(st) != hipSuccess) return NITI_NO_EXECUTION;
+    return take_error(e, st, flag != nullptr);
+}
+
+int niti_execution_status(niti_execution_t e, void* stream) {
+    if (!e) return NITI_INVALID_VALUE;
+    return take_error(e, S(stream), false);
 }
 
 void niti_destroy_execution(niti_execution_t e) { delete e; }
@@ -358,6 +394,9 @@ int niti_nhwc16_to_p16(const int8_t* in, int64_t pixels, int cp, int8_t* out, vo
 
 void niti_diag_wgrad_stamps(void* buf) { niti::wgrad_stamps_arm((unsigned long long*)buf); }
 void niti_diag_rowconv_stamps(void* buf) { niti::rowconv_stamps_arm((unsigned long long*)buf); }
+void niti_diag_rowconv_barrier(uint32_t spin_limit, uint32_t expect_extra) {
+    niti::rowconv_barrier_diag(spin_limit, expect_extra);
+}
 
 int niti_conv_wgrad_p16_workspace(const niti_geom* g, int splits, size_t* bytes) {
     if (!g || !bytes) return NITI_INVALID_VALUE;

@@ -111,18 +111,28 @@ struct RowPath {
         epoch = 0;
         return NITI_NO_ERROR;
     }
-    // x16 / w16: the Execution's NHWC16 input and OHWI16 weights (already converted)
+    // x16 / w16: the Execution's NHWC16 input and OHWI16 weights (already converted); amax zeroed.
+    // Under stream capture the fused launch's barrier parity (epoch, a kernel argument) would be
+    // replayed unchanged with counts nobody resets, so a captured call takes the two-launch form
+    // (range launch, then recompute + requantise with the published max): same results.
     hipError_t run(const ConvGeom& g, const int8_t* x16, const int8_t* w16, uint32_t* amax, const int8_t* exp_in,
                    const int8_t* wscale, int8_t* exp_out, int8_t* out_c4, hipStream_t st) {
         hipError_t e = nhwc16_to_c32(x16, g.n, g.h * g.w, g.cip, g.c_in, xc32, st);
         if (e == hipSuccess) e = weights_to_wf(w16, g.c_out, g.c_in, g.cip, false, wf, st);
         if (e != hipSuccess) return e;
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        if (hipStreamIsCapturing(st, &cs) != hipSuccess) return hipErrorInvalidValue;
         RowConvOut o;
         o.out = y16;
         o.exp_in = exp_in;
         o.wscale = wscale;
         o.exp_out = exp_out;
-        e = rowconv_fwd(g, xc32, wf, o, 0, amax, bar, ++epoch, err, st);
+        if (cs == hipStreamCaptureStatusNone) {
+            e = rowconv_fwd(g, xc32, wf, o, 0, amax, bar, ++epoch, err, st);
+        } else {
+            e = rowconv_fwd(g, xc32, wf, o, 1, amax, nullptr, 0, nullptr, st);
+            if (e == hipSuccess) e = rowconv_fwd(g, xc32, wf, o, 2, amax, nullptr, 0, nullptr, st);
+        }
         if (e != hipSuccess) return e;
         const int cq = (g.c_out + 3) / 4;
         return launch_map((int64_t)cq * g.n * g.oh * g.ow, Nhwc16ToC4{y16, g.n, g.c_out, g.oh * g.ow, g.cop, out_c4}, st);
@@ -322,6 +332,7 @@ class ConvInt8Execution : public Execution {
         if (!(x16_ && w16_ && acc_ && amax_)) return NITI_OUT_OF_MEMORY;
         return rows_.resize(g_);
     }
+    uint32_t* errorFlag() override { return rows_.on ? rows_.err : nullptr; }
     int onExecute(const niti_tensor* in, int nin, const niti_tensor* out, int nout, hipStream_t st) override {
         if (!acc_) return NITI_NO_EXECUTION;
         NITI_TRY(c4_to_nhwc16((const int8_t*)in[0].data, g_.n, g_.c_in, g_.h * g_.w, g_.cip, x16_, st));
@@ -390,6 +401,7 @@ class DeconvInt8Execution : public Execution {
         if (!(x16_ && w16_ && acc_ && amax_)) return NITI_OUT_OF_MEMORY;
         return rows_.resize(g_);
     }
+    uint32_t* errorFlag() override { return rows_.on ? rows_.err : nullptr; }
     int onExecute(const niti_tensor* in, int nin, const niti_tensor* out, int nout, hipStream_t st) override {
         if (!acc_) return NITI_NO_EXECUTION;
         NITI_TRY(c4_to_nhwc16((const int8_t*)in[0].data, g_.n, g_.c_in, g_.h * g_.w, g_.cip, x16_, st));

@@ -29,6 +29,10 @@ class Execution {
     virtual int onExecute(const niti_tensor* inputs, int nin, const niti_tensor* outputs, int nout,
                           hipStream_t st) = 0;
     size_t workspaceBytes() const { return ws_.total; }
+    // a device word a launch of this Execution sets when it could not complete (the fused row
+    // kernel's grid barrier timed out: results invalid), or null.  niti_execution_execute checks it
+    // before a synchronous (host-tensor) call returns, niti_execution_status for device tensors.
+    virtual uint32_t* errorFlag() { return nullptr; }
 
    protected:
     Workspace ws_;

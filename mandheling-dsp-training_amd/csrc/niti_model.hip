@@ -1846,9 +1846,31 @@ int niti_model_attach_comm(niti_model_t m, const char id[NITI_UNIQUE_ID_BYTES], 
     // the gradient communicator: split off the first (collective over the ranks), its own
     // resources, so its SUMs and the ranges' MAXes are not serialised against each other
     auto cg = std::make_unique<niti::RcclCollective>();
+    const bool split_ok = ncclCommSplit(c->comm, 0, rank, &cg->comm, nullptr) == ncclSuccess;
+    // every rank must pick the same mode (the SUMs run on different communicators and streams in
+    // the two modes): agree on the split's success with a MIN over the range communicator
+    int32_t* flag = nullptr;
+    int32_t ok = split_ok ? 1 : 0;
+    hipStream_t ast = nullptr;
+    bool agreed = hipMalloc(&flag, sizeof(int32_t)) == hipSuccess && hipStreamCreate(&ast) == hipSuccess &&
+                  hipMemcpyAsync(flag, &ok, sizeof(ok), hipMemcpyHostToDevice, ast) == hipSuccess &&
+                  ncclAllReduce(flag, flag, 1, ncclInt32, ncclMin, c->comm, ast) == ncclSuccess &&
+                  hipMemcpyAsync(&ok, flag, sizeof(ok), hipMemcpyDeviceToHost, ast) == hipSuccess &&
+                  hipStreamSynchronize(ast) == hipSuccess;
+    if (flag) (void)hipFree(flag);
+    if (ast) (void)hipStreamDestroy(ast);
+    if (!agreed) {
+        if (split_ok) (void)ncclCommDestroy(cg->comm);
+        cg->comm = nullptr;
+        (void)ncclCommDestroy(c->comm);
+        c->comm = nullptr;
+        return NITI_NO_EXECUTION;
+    }
     bool shared = false;
-    if (ncclCommSplit(c->comm, 0, rank, &cg->comm, nullptr) != ncclSuccess) {
-        // no split: the gradient SUMs use the range communicator, in the step's program order
+    if (ok == 0) {
+        // some rank has no split: every rank's gradient SUMs use the range communicator, in the
+        // step's program order
+        if (split_ok) (void)ncclCommDestroy(cg->comm);
         cg->comm = c->comm;
         cg->owns = false;
         shared = true;

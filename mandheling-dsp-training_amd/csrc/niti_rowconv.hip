@@ -28,6 +28,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <map>
+#include <mutex>
 
 #include "niti_device.hpp"
 #include "niti_kernels.hpp"
@@ -94,7 +96,7 @@ __device__ __forceinline__ v4i shift_in_right(v4i v, bool row_end) {
 constexpr int BAR_LINE = 32;                         // words per 128-byte line
 constexpr int BAR_WORDS = 19 * BAR_LINE;             // one parity (8 shard lines used)
 static_assert(2 * BAR_WORDS == ROWCONV_BAR_WORDS, "barrier state size");
-constexpr uint32_t BAR_SPIN_LIMIT = 1u << 22;
+constexpr uint32_t BAR_SPIN_LIMIT = 1u << 22;  // ~seconds of polling: only a non-resident grid reaches it
 
 __device__ __forceinline__ unsigned long long* bar_shard(uint32_t* base, int s) {
     return (unsigned long long*)(base + s * BAR_LINE);
@@ -116,19 +118,23 @@ __device__ void grid_bw_arrive(uint32_t* state, uint32_t epoch, int bw, int lane
     }
 }
 
-__device__ int grid_bw_wait(uint32_t* state, uint32_t epoch, uint32_t* err, int lane) {
+// A workgroup that is not resident never arrives: after spin_limit polls the waiters set *err
+// (the Executions return NITI_NO_EXECUTION, the model step reports it: niti_model_rowconv_error)
+// and go on with bw = 31 instead of hanging the GPU.
+__device__ int grid_bw_wait(uint32_t* state, uint32_t epoch, uint32_t* err, uint32_t spin_limit, uint32_t extra,
+                            int lane) {
     uint32_t* S = state + (epoch & 1) * BAR_WORDS;
     const int nwg = gridDim.x;
     const int nsh = nwg < 8 ? nwg : 8;
     // lane s < nsh polls shard s until its count is complete
-    const uint32_t expect = lane < nsh ? (uint32_t)((nwg - lane + nsh - 1) / nsh) : 0u;
+    const uint32_t expect = lane < nsh ? (uint32_t)((nwg - lane + nsh - 1) / nsh) + (lane == 0 ? extra : 0u) : 0u;
     uint32_t spins = 0;
     unsigned long long v = 0;
     for (;;) {
         v = lane < nsh ? __hip_atomic_load(bar_shard(S, lane), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
         const bool done = (uint32_t)(v >> 32) >= expect;
         if (__all(done)) break;
-        if (++spins > BAR_SPIN_LIMIT) {  // never hang the GPU: flag it and go on (results invalid)
+        if (++spins > spin_limit) {  // never hang the GPU: flag it and go on (results invalid)
             if (lane == 0) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             return 31;
         }
@@ -160,6 +166,8 @@ struct RowConvArgs {
     uint32_t* bar;    // FUSED: barrier state
     uint32_t epoch;
     uint32_t* err;
+    uint32_t spin_limit;         // FUSED: polls before the barrier gives up and sets *err
+    uint32_t expect_extra;       // diagnostics (niti_diag_rowconv_barrier): arrivals that never come
     unsigned long long* stamps;  // diagnostics (niti_diag_rowconv_stamps): 8 per wave, or null
     const int8_t* relu_mask;     // input gradient: RowConvOut's relu / pool gradients
     const int8_t* pool_x;
@@ -835,7 +843,7 @@ __global__ void __launch_bounds__(256, (RC_EXP & 16) ? 2 : 1) rowconv_fwd_kernel
         if constexpr (DG)
             if (owner) epi_masks<R>(a, ein);  // while the barrier completes
         if (wid == 0) {
-            const int gbw = grid_bw_wait(a.bar, a.epoch, a.err, lane);
+            const int gbw = grid_bw_wait(a.bar, a.epoch, a.err, a.spin_limit, a.expect_extra, lane);
             if (a.stamps != nullptr && lane == 0) a.stamps[blockIdx.x * 64 + 9] = __builtin_amdgcn_s_memrealtime();
             // the rule only needs bw: 2^bw stands for the max (bitwidth_rc(2^bw) == bw)
             const uint32_t g = gbw == 0 ? 0u : 1u << gbw;
@@ -1040,28 +1048,19 @@ int rowconv_units(const ConvGeom& g, bool dg) {
     return u;
 }
 
-// FUSED needs every workgroup resident: one per CU (K-split: 144 KiB of LDS each)
-bool rowconv_fused_ok(const ConvGeom& g, bool dg) {
-    return rowconv_ok(g) && rowconv_units(g, dg) <= ((RC_EXP & 16) ? 8 : 4) * 256;
-}
-
+// the instantiation a launch runs (ks > 0: the K-split form, W = R = 2)
 template <int MODE, bool DG>
-static hipError_t launch_rc(int W, int R, int grid, const RowConvArgs& a, hipStream_t st, int ks = 0) {
-    if (ks > 0) {  // rowconv_ks: W = R = 2
-        if (ks == 4) hipLaunchKernelGGL((rowconv_fwd_kernel<2, 2, MODE, DG, false, 4>), dim3((unsigned)grid), dim3(256), 0, st, a);
-        else if (ks == 2) hipLaunchKernelGGL((rowconv_fwd_kernel<2, 2, MODE, DG, false, 2>), dim3((unsigned)grid), dim3(256), 0, st, a);
-        else if (ks == 1) hipLaunchKernelGGL((rowconv_fwd_kernel<2, 2, MODE, DG, false, 1>), dim3((unsigned)grid), dim3(256), 0, st, a);
-        else return hipErrorInvalidValue;
-        return hipGetLastError();
+static const void* rc_kernel(int W, int R, bool unc, int ks) {
+    if (ks > 0) {
+        if (ks == 4) return reinterpret_cast<const void*>(&rowconv_fwd_kernel<2, 2, MODE, DG, false, 4>);
+        if (ks == 2) return reinterpret_cast<const void*>(&rowconv_fwd_kernel<2, 2, MODE, DG, false, 2>);
+        if (ks == 1) return reinterpret_cast<const void*>(&rowconv_fwd_kernel<2, 2, MODE, DG, false, 1>);
+        return nullptr;
     }
-#define RC_CASE(WW, RR)                                                                                              \
-    if (W == WW && R == RR) {                                                                                        \
-        if (WW > 1 && a.CB % 4 == 0)                                                                                 \
-            hipLaunchKernelGGL((rowconv_fwd_kernel<WW, RR, MODE, DG, true, 0>), dim3((unsigned)grid), dim3(256), 0, st, a); \
-        else                                                                                                         \
-            hipLaunchKernelGGL((rowconv_fwd_kernel<WW, RR, MODE, DG, false, 0>), dim3((unsigned)grid), dim3(256), 0, st, a); \
-        return hipGetLastError();                                                                                    \
-    }
+#define RC_CASE(WW, RR)                                                                                 \
+    if (W == WW && R == RR)                                                                             \
+        return (WW > 1 && unc) ? reinterpret_cast<const void*>(&rowconv_fwd_kernel<WW, RR, MODE, DG, true, 0>) \
+                               : reinterpret_cast<const void*>(&rowconv_fwd_kernel<WW, RR, MODE, DG, false, 0>);
     if constexpr (!DG) RC_CASE(16, 8)
     RC_CASE(16, 4)
     RC_CASE(16, 2)
@@ -1072,7 +1071,67 @@ static hipError_t launch_rc(int W, int R, int grid, const RowConvArgs& a, hipStr
     RC_CASE(2, 2)
     RC_CASE(1, 1)
 #undef RC_CASE
-    return hipErrorInvalidValue;
+    return nullptr;
+}
+
+template <int MODE, bool DG>
+static hipError_t launch_rc(int W, int R, int grid, RowConvArgs a, hipStream_t st, int ks = 0) {
+    const void* f = rc_kernel<MODE, DG>(W, R, W > 1 && a.CB % 4 == 0, ks);
+    if (f == nullptr) return hipErrorInvalidValue;
+    void* args[] = {&a};
+    return hipLaunchKernel(f, dim3((unsigned)grid), dim3(256), args, 0, st);
+}
+
+// Workgroups of kernel f the current device holds at once: CUs x the kernel's occupancy per CU
+// (hipOccupancyMaxActiveBlocksPerMultiprocessor over its LDS and registers), cached per (device,
+// kernel); 0 without a device.  The fused mode's grid barrier needs the whole grid resident, so a
+// smaller or partitioned device takes the two-launch form instead.
+static int resident_wgs(const void* f) {
+    static std::mutex mu;
+    static std::map<std::pair<int, const void*>, int> cache;
+    int dev = -1;
+    if (f == nullptr || hipGetDevice(&dev) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    std::lock_guard<std::mutex> lk(mu);
+    const auto key = std::make_pair(dev, f);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+    int cus = 0, occ = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, f, 256, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return cache[key] = cus * occ;
+}
+
+// workgroups of a launch (K-split: one unit each; else four units)
+static int rowconv_wgs(const ConvGeom& g, bool dg, int* R_out, int* ks_out) {
+    int u = 0;
+    const int R = rowconv_rows(g, dg, &u);
+    const int ks = rowconv_ks(g, dg);
+    const int G = 32 / g.w, ngb = ((g.n + G - 1) / G) * (g.h / R), ngb4 = (ngb + 3) / 4 * 4, COB = g.cop / 32;
+    *R_out = R;
+    *ks_out = ks;
+    return ks > 0 ? COB * ngb : COB * ngb4 / 4;
+}
+
+// FUSED needs every workgroup resident (one unit per wave, the grid barrier inside the kernel)
+bool rowconv_fused_ok(const ConvGeom& g, bool dg) {
+    if (!rowconv_ok(g)) return false;
+    int R = 0, ks = 0;
+    const int wgs = rowconv_wgs(g, dg, &R, &ks);
+    const bool unc = (g.c_in + 31) / 32 % 4 == 0;
+    const void* f = dg ? rc_kernel<RC_FUSED, true>(g.w, R, unc, ks) : rc_kernel<RC_FUSED, false>(g.w, R, unc, ks);
+    return wgs <= resident_wgs(f);
+}
+
+static uint32_t g_rc_spin_limit = BAR_SPIN_LIMIT, g_rc_expect_extra = 0;
+void rowconv_barrier_diag(uint32_t spin_limit, uint32_t expect_extra) {
+    g_rc_spin_limit = spin_limit ? spin_limit : BAR_SPIN_LIMIT;
+    g_rc_expect_extra = expect_extra;
 }
 
 static unsigned long long* g_rc_stamps = nullptr;
@@ -1118,6 +1177,8 @@ hipError_t rowconv_fwd(const ConvGeom& g, const int8_t* x_c32, const int8_t* wf,
     a.bar = bar;
     a.epoch = epoch;
     a.err = err;
+    a.spin_limit = g_rc_spin_limit;
+    a.expect_extra = g_rc_expect_extra;
     a.stamps = g_rc_stamps;
     a.relu_mask = o.relu_mask;
     a.pool_x = o.pool_x;
@@ -1209,8 +1270,12 @@ hipError_t head_wgrad(int n, int c_out, int cip, const int8_t* x, int xld, const
 // the input gradient's epilogues) = requant(Σ_k x[n][k] w[row][k]) for rows = cop channels.
 bool rowconv_fc_ok(int n, int K, int rows, bool fused) {
     if (n <= 0 || K <= 0 || rows <= 0) return false;
-    const int64_t units = (int64_t)((n + 31) / 32 + 3) / 4 * 4 * ((rows + 31) / 32);
-    return !fused || units <= 4 * 256;
+    const int64_t wgs = (int64_t)((n + 31) / 32 + 3) / 4 * ((rows + 31) / 32);
+    if (!fused) return true;
+    // either epilogue form: the resident limit of the smaller-occupancy instantiation
+    const int cap = std::min(resident_wgs(rc_kernel<RC_FUSED, false>(1, 1, false, 0)),
+                             resident_wgs(rc_kernel<RC_FUSED, true>(1, 1, false, 0)));
+    return wgs <= cap;
 }
 
 hipError_t rowconv_fc(int n, int K, int rows, const int8_t* x, int xld, const int8_t* w, int wld,
@@ -1251,6 +1316,8 @@ hipError_t rowconv_fc(int n, int K, int rows, const int8_t* x, int xld, const in
     a.bar = bar;
     a.epoch = epoch;
     a.err = err;
+    a.spin_limit = g_rc_spin_limit;
+    a.expect_extra = g_rc_expect_extra;
     a.stamps = nullptr;
     a.relu_mask = o.relu_mask;
     a.pool_x = o.pool_x;

@@ -79,6 +79,11 @@ class NITIExecution:
         o, no = self._arr(outputs)
         return self._lib.niti_execution_execute(self._h, i, ni, o, no, _stream(stream))
 
+    def status(self, stream=None):
+        """The asynchronous path's ErrorCode (niti_execution_status): synchronizes `stream`, then
+        NO_EXECUTION if a launch since the last check flagged invalid results."""
+        return self._lib.niti_execution_status(self._h, _stream(stream))
+
     @property
     def workspace_bytes(self):
         return int(self._lib.niti_execution_workspace_bytes(self._h))

@@ -100,3 +100,22 @@ def test_asm_ring_kernels_no_inflight_register_reuse(tmp_path, unit):
                        capture_output=True, text=True)
     assert r.returncode == 0, r.stdout
     assert " 0 asm-ring kernels" not in r.stdout, r.stdout
+
+
+def test_execution_status_plumbing(L):
+    """The error-status entry point without a device: a NULL handle is INVALID_VALUE, and an
+    Execution whose launches carry no error word (not resized, so no fused row path) reports
+    NO_ERROR without touching the GPU.  The forced-timeout path is tests/test_gpu_exec_host.py."""
+    lib = L.lib()
+    assert lib.niti_execution_status(None, None) == 5
+    h = C.c_void_p()
+    c = lib.niti_create_execution.argtypes[1]._type_()  # the ConvCommon class the loaded library binds
+    c.kernel_x = c.kernel_y = 3
+    c.stride_x = c.stride_y = c.dilate_x = c.dilate_y = 1
+    c.pad_x = c.pad_y = 1
+    c.group = 1
+    for op in (700, 701, 715):
+        assert lib.niti_create_execution(op, C.byref(c), C.byref(h)) == 0
+        assert lib.niti_execution_status(h, None) == 0
+        lib.niti_destroy_execution(h)
+    lib.niti_diag_rowconv_barrier(0, 0)  # host-side setter: no device call

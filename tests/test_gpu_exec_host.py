@@ -193,3 +193,77 @@ def test_dsp_maxpool_grad_ref_806_rejects_overlap(T, ops):
     ex = ops.NITIExecution(806, ops.conv_common(3, stride=2))
     t = ops.tensor(x, (2, 128, 4, 4), 1)
     assert ex.resize([t, t, t], [t]) == 2  # NOT_SUPPORT: stride < kernel (order-dependent in the reference)
+
+
+@pytest.mark.parametrize("op_name", ["conv", "deconv"])
+def test_fused_barrier_timeout_returns_no_execution(T, ops, oracle, op_name):
+    """A fused row-kernel launch whose grid barrier times out (forced: the barrier waits for one
+    arrival that never comes, with a short poll limit) flags its results invalid: a synchronous
+    host-tensor call returns NITI_NO_EXECUTION (ErrorCode.hpp:17-30) instead of NO_ERROR, the
+    asynchronous device-tensor path reports it through niti_execution_status, and once the knob is
+    reset the same handle computes the oracle's result again."""
+    import niti_amd
+    from niti_amd import _lib as L
+    n, ci, h, co, k = 16, 64, 8, 64, 3
+    rng = np.random.default_rng(311)
+    g = oracle.geom(n, ci, h, h, co, k, stride=1, pad=1)
+    x = oracle.synth_x(rng, (n, ci, h, h))
+    wt, ws = oracle.synth_w(rng, (co, ci, k, k))
+    _, e_ref, y4_ref = oracle.mnn_conv_fwd(g, x, wt, -7, ws)
+    op = niti_amd.OP_CONV_INT8 if op_name == "conv" else niti_amd.OP_DECONV_INT8
+    ex = ops.NITIExecution(op, ops.conv_common(k, stride=1, pad=1, input_count=ci, output_count=co))
+
+    def io(dev):
+        mk = (lambda a: T.from_numpy(np.ascontiguousarray(a)).cuda()) if dev else (lambda a: host(T, a))
+        y4 = T.zeros(y4_ref.shape, dtype=T.int8, device="cuda" if dev else "cpu")
+        ins = [ops.tensor(mk(oracle.nchw_to_c4(x)), (n, ci, h, h), niti_amd.FORMAT_NC4HW4),
+               ops.tensor(mk(wt), (co, ci, k, k))]
+        outs = [ops.tensor(y4, (n, co, h, h), niti_amd.FORMAT_NC4HW4)]
+        if op_name == "conv":
+            e_out = T.zeros(1, dtype=T.int8, device=y4.device)
+            ins += [ops.tensor(mk(np.array([-7], np.int8)), (1, 1, 1, 1)), ops.tensor(mk(np.array([ws], np.int8)), (1, 1, 1, 1))]
+            outs.append(ops.tensor(e_out, (1, 1, 1, 1)))
+        return ins, outs, y4
+
+    ins, outs, y4 = io(False)
+    assert ex.resize(ins, outs) == 0
+    lib = L.lib()
+    try:
+        lib.niti_diag_rowconv_barrier(2000, 1)
+        assert ex.execute(ins, outs) == 4            # host tensors: synchronous, NO_EXECUTION
+        ins_d, outs_d, _ = io(True)
+        assert ex.execute(ins_d, outs_d) == 0         # device tensors: asynchronous launch
+        assert ex.status() == 4                       # ... and its status
+        assert ex.status() == 0                       # the flag was cleared
+    finally:
+        lib.niti_diag_rowconv_barrier(0, 0)
+    assert ex.execute(ins, outs) == 0
+    if op_name == "conv":
+        assert np.array_equal(y4.numpy(), y4_ref)
+
+
+def test_model_step_reports_barrier_timeout(T):
+    """The whole-step driver: a forced barrier timeout in the fused row kernels is visible through
+    niti_model_rowconv_error (bench.py asserts it is 0 after its timed and isolated regions)."""
+    import niti_amd
+    import niti_model_ref as R
+    from niti_amd import _lib as L
+    from niti_amd.model import NitiModel
+    layers = R.vgg11_layers()
+    W, S = R.init_weights(layers, seed=5)
+    m = NitiModel(niti_amd.ARCH_VGG11, 32)
+    for i, (w, s) in enumerate(zip(W, S)):
+        m.set_weight(i, w, s)
+    rng = np.random.default_rng(5)
+    img = T.from_numpy(rng.integers(0, 256, (32, 3, 32, 32)).astype(np.uint8)).cuda()
+    lab = T.from_numpy(rng.integers(0, 10, 32).astype(np.int32)).cuda()
+    m.train_step_images(img, lab)
+    assert m.rowconv_error() == 0
+    lib = L.lib()
+    try:
+        lib.niti_diag_rowconv_barrier(2000, 1)
+        m.train_step_images(img, lab)
+        T.cuda.synchronize()
+    finally:
+        lib.niti_diag_rowconv_barrier(0, 0)
+    assert m.rowconv_error() == 1
