@@ -27,6 +27,8 @@
 // the NHWC16 output, the fused 2x2 max pool and the next layer's C32 input.
 #include <hip/hip_runtime.h>
 
+#include <stdlib.h>
+
 #include <algorithm>
 #include <map>
 #include <mutex>
@@ -154,6 +156,9 @@ struct RowConvArgs {
     int ngb, ngb4;    // (image group, band) pairs; rounded up to whole workgroups of 4
     int nbands;
     int wgs;          // workgroup tiles: COB * ngb4 / 4
+    int wmajor;       // 1: consecutive tiles (one co block) on one XCD (xcd_remap), so a co block's
+                      // weight panel is fetched into one L2; 0: dispatch order, which deals every
+                      // co block's image groups over the 8 XCDs alike, so each XCD reads 1/8 of x
     int8_t* out;      // NHWC16 [n][H][W][cop]
     int cop;
     int8_t* pool_out; // NHWC16 [n][H/2][W/2][cop] or null
@@ -823,7 +828,7 @@ __global__ void __launch_bounds__(256, (RC_EXP & 16) ? 2 : 1) rowconv_fwd_kernel
     const bool owner = KS == 0 || wid == 0;
     RC_STAMP(0);
     if constexpr (MODE == RC_FUSED) {
-        const RowUnit<W, R> U(a, blockIdx.x, wid, c, KS > 0);
+        const RowUnit<W, R> U(a, a.wmajor ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x, wid, c, KS > 0);
         uint32_t m = 0;
         compute_unit<W, R, UNC, KS>(a, U, lane, wid, smem, acc);
         EpiIn<DG ? R : 1> ein = {};
@@ -858,7 +863,8 @@ __global__ void __launch_bounds__(256, (RC_EXP & 16) ? 2 : 1) rowconv_fwd_kernel
         RC_STAMP(5);
     } else if constexpr (MODE == RC_RANGE) {
         uint32_t m = 0;
-        for (int wg = blockIdx.x; wg < a.wgs; wg += gridDim.x) {
+        for (int b = blockIdx.x; b < a.wgs; b += gridDim.x) {
+            const int wg = a.wmajor && (int)gridDim.x == a.wgs ? xcd_remap(b, gridDim.x) : b;
             const RowUnit<W, R> U(a, wg, wid, c, KS > 0);
             compute_unit<W, R, UNC, KS>(a, U, lane, wid, smem, acc);
             if (owner) {
@@ -875,7 +881,8 @@ __global__ void __launch_bounds__(256, (RC_EXP & 16) ? 2 : 1) rowconv_fwd_kernel
     } else {
         const uint32_t g = read_max(a.amax);
         if (blockIdx.x == 0 && threadIdx.x == 0) write_exponent(a, g);
-        for (int wg = blockIdx.x; wg < a.wgs; wg += gridDim.x) {
+        for (int b = blockIdx.x; b < a.wgs; b += gridDim.x) {
+            const int wg = a.wmajor && (int)gridDim.x == a.wgs ? xcd_remap(b, gridDim.x) : b;
             const RowUnit<W, R> U(a, wg, wid, c, KS > 0);
             if (a.acc_store != nullptr) {  // the range launch's accumulators (uniform branch)
                 if (owner) acc_get<R>(a, wg, wid, lane, acc);
@@ -1134,6 +1141,16 @@ void rowconv_barrier_diag(uint32_t spin_limit, uint32_t expect_extra) {
     g_rc_expect_extra = expect_extra;
 }
 
+// Tile order over the XCDs: weight-major when the layer's weights outweigh its input (VGG-11's
+// 4x4 / 2x2 layers: 16 image groups re-read each co block's 147 KiB panel), else dispatch order.
+// NITI_RC_MAP=x / w forces one (A/B diagnostics).
+static int rowconv_wmajor(int64_t xbytes, int64_t wbytes) {
+    static const char* env = getenv("NITI_RC_MAP");
+    if (env != nullptr && env[0] == 'x') return 0;
+    if (env != nullptr && env[0] == 'w') return 1;
+    return wbytes > xbytes ? 1 : 0;
+}
+
 static unsigned long long* g_rc_stamps = nullptr;
 void rowconv_stamps_arm(unsigned long long* buf) { g_rc_stamps = buf; }
 
@@ -1165,6 +1182,7 @@ hipError_t rowconv_fwd(const ConvGeom& g, const int8_t* x_c32, const int8_t* wf,
     a.ngb4 = (a.ngb + 3) / 4 * 4;
     const int ks = rowconv_ks(g, dg);
     a.wgs = ks > 0 ? COB * a.ngb : COB * a.ngb4 / 4;
+    a.wmajor = rowconv_wmajor(xb, wb);
     a.out = o.out;
     a.cop = g.cop;
     a.pool_out = o.pool_out;

@@ -219,3 +219,35 @@ def test_vgg16_224_step_layer_parity(T):
     logits, e = m.logits()
     want = O.loss_grad(logits, e, R.onehot(labels, 1000))
     assert np.array_equal(m.tap(15, 2).reshape(2, 1000), want)
+
+
+def test_vgg16_224_step_matches_oracle(T):
+    """BASELINE cfg 4's per-GPU workload at ImageNet size: one whole VGG-16 step at 224x224 (batch 2,
+    1000-class loss): every forward output, exponent, input gradient, int8 weight gradient and
+    updated weight of all 16 layers against the oracle (its reference-structured restatement,
+    exact accumulation, on every core the box gives the process).  NITI_Conv_Int8.cpp:162-310,
+    NITI_GradientConv_Int8.cpp:165-298, NITI_DeConv_Int8.cpp:187-332, NITI_SGD.hpp:20-54."""
+    import os
+
+    import niti_amd
+    import niti_model_ref as R
+    from niti_amd.model import NitiModel
+    layers = R.vgg16_layers(224)
+    W, S = R.init_weights(layers, seed=29)
+    rng = np.random.default_rng(29)
+    m = NitiModel(niti_amd.ARCH_VGG16, 2)
+    for i, (w, s) in enumerate(zip(W, S)):
+        m.set_weight(i, w, s)
+    x = rng.integers(-127, 128, (2, 3, 224, 224)).astype(np.int8)
+    labels = rng.integers(0, 1000, 2).astype(np.int32)
+    m.train_step(T.from_numpy(x).cuda(), -3, T.from_numpy(labels).cuda())
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    newW, rec = R.train_step(layers, W, S, x, -3, labels, classes=1000, impl="mnn", threads=threads)
+    logits, e = m.logits()
+    assert e == rec["exp"][-1] and np.array_equal(logits, rec["logits"])
+    for i in range(len(layers)):
+        assert np.array_equal(m.tap(i, 0), rec["r"][i]), ("fwd", i)
+        assert np.array_equal(m.tap(i, 2), rec["dy"][i]), ("dy", i)
+        assert np.array_equal(m.tap(i, 1), rec["dw"][i]), ("dw", i)
+        assert np.array_equal(m.get_weight(i), newW[i]), ("w", i)
+    assert m.rowconv_error() == 0
