@@ -317,6 +317,9 @@ def main():
     ap.add_argument("--wgrad-p16", type=int, default=-1, help="force the P16 weight gradient on every layer it "
                                                               "takes with this many K splits (0: its default; "
                                                               "-1: the autotuner's choice)")
+    ap.add_argument("--rc-spec", type=int, default=1, choices=[0, 1, 2],
+                    help="fused row kernels' speculative epilogue: 1 on (default), 0 off, 2 always redone "
+                         "(results identical; A/B diagnostics)")
     args = ap.parse_args()
     if args.gpus is not None and args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return spawn_ranks(args.gpus, sys.argv[1:])
@@ -336,6 +339,7 @@ def main():
         dist.init_process_group("gloo")  # control plane only; the data path is RCCL in C++
 
     import niti_amd
+    niti_amd._lib.lib().niti_diag_rowconv_speculate(args.rc_spec)
     from niti_amd.model import NitiModel
 
     arch = {"vgg11": niti_amd.ARCH_VGG11, "lenet": niti_amd.ARCH_LENET, "vgg16": niti_amd.ARCH_VGG16}[args.arch]

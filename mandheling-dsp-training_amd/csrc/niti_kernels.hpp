@@ -254,6 +254,9 @@ void rowconv_stamps_arm(unsigned long long* buf);
 // diagnostics: the fused barrier's poll limit (0 = the default) and arrivals it waits for that never
 // come (> 0 forces a timeout: the launch sets its err word), for the launches that follow
 void rowconv_barrier_diag(uint32_t spin_limit, uint32_t expect_extra);
+// the fused mode's speculative epilogue (the previous launch's bit width applied while the barrier
+// completes): 1 on (default), 0 off, 2 always guess wrong (diagnostics: every launch redoes it)
+void rowconv_speculate(int mode);
 hipError_t rowconv_fwd(const ConvGeom& g, const int8_t* x_c32, const int8_t* wf, const RowConvOut& o, int mode,
                        uint32_t* amax, uint32_t* bar, uint32_t epoch, uint32_t* err, hipStream_t st);
 // A 1x1 layer over 1x1 maps (the classifier head) on the same kernel: rows output channels of

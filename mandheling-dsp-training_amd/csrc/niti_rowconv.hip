@@ -104,6 +104,14 @@ __device__ __forceinline__ unsigned long long* bar_shard(uint32_t* base, int s) 
     return (unsigned long long*)(base + s * BAR_LINE);
 }
 
+// Speculative epilogue: the bit width a layer's output had at this state's previous fused launch
+// (forward and input-gradient launches keep separate slots: lines 16 / 17 of the parity-0 word
+// set, which the shard resets never touch), stored as bw + 1 (0: none yet).  A launch requantises
+// with it while its grid barrier completes and redoes the epilogue only if the barrier's bw
+// differs: per layer the bit width is stable from step to step, so the barrier's release latency
+// overlaps the epilogue instead of preceding it.  The results are the rule's whatever the guess.
+__device__ __forceinline__ uint32_t* bar_hint(uint32_t* state, bool dg) { return state + (16 + (dg ? 1 : 0)) * BAR_LINE; }
+
 // Called by one whole wave of each workgroup (lane 0's bw): the arrival, then -- after whatever
 // work the workgroup can do meanwhile -- the wait, which returns the grid's bw to every lane.
 __device__ void grid_bw_arrive(uint32_t* state, uint32_t epoch, int bw, int lane) {
@@ -173,6 +181,8 @@ struct RowConvArgs {
     uint32_t* err;
     uint32_t spin_limit;         // FUSED: polls before the barrier gives up and sets *err
     uint32_t expect_extra;       // diagnostics (niti_diag_rowconv_barrier): arrivals that never come
+    int spec;                    // FUSED: 1 speculative epilogue (bar_hint), 0 off, 2 diagnostics:
+                                 // guess one bit wide of the hint (every launch redoes its epilogue)
     unsigned long long* stamps;  // diagnostics (niti_diag_rowconv_stamps): 8 per wave, or null
     const int8_t* relu_mask;     // input gradient: RowConvOut's relu / pool gradients
     const int8_t* pool_x;
@@ -829,6 +839,16 @@ __global__ void __launch_bounds__(256, (RC_EXP & 16) ? 2 : 1) rowconv_fwd_kernel
     RC_STAMP(0);
     if constexpr (MODE == RC_FUSED) {
         const RowUnit<W, R> U(a, a.wmajor ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x, wid, c, KS > 0);
+        uint32_t* hint_p = bar_hint(a.bar, DG);
+        // the guess: the previous launch's bit width (written by block 0 after its barrier; the launch
+        // boundary orders it before this read)
+        int guess = -1;
+        if (a.spec != 0) {
+            const uint32_t h = __hip_atomic_load(hint_p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            guess = __builtin_amdgcn_readfirstlane((int)h) - 1;
+            if (guess >= 0 && a.spec == 2) guess = guess < 31 ? guess + 1 : guess - 1;
+        }
+        const uint32_t g_guess = guess <= 0 ? 0u : 1u << guess;
         uint32_t m = 0;
         compute_unit<W, R, UNC, KS>(a, U, lane, wid, smem, acc);
         EpiIn<DG ? R : 1> ein = {};
@@ -847,6 +867,11 @@ __global__ void __launch_bounds__(256, (RC_EXP & 16) ? 2 : 1) rowconv_fwd_kernel
         }
         if constexpr (DG)
             if (owner) epi_masks<R>(a, ein);  // while the barrier completes
+        int8_t* tile = smem + wid * RC_P16_WAVE_BYTES;
+        // the speculative epilogue, while the barrier completes (the guess cannot be below this
+        // workgroup's own bit width, so such a guess is not tried)
+        const bool spec = guess >= 0 && guess >= bitwidth_rc(max(max(red[0], red[1]), max(red[2], red[3])));
+        if (spec && U.valid && owner) rowconv_epilogue<W, R, DG>(a, U, lane, acc, g_guess, ein, tile);
         if (wid == 0) {
             const int gbw = grid_bw_wait(a.bar, a.epoch, a.err, a.spin_limit, a.expect_extra, lane);
             if (a.stamps != nullptr && lane == 0) a.stamps[blockIdx.x * 64 + 9] = __builtin_amdgcn_s_memrealtime();
@@ -854,12 +879,15 @@ __global__ void __launch_bounds__(256, (RC_EXP & 16) ? 2 : 1) rowconv_fwd_kernel
             const uint32_t g = gbw == 0 ? 0u : 1u << gbw;
             if (lane == 0) {
                 gm = g;
-                if (blockIdx.x == 0) write_exponent(a, g);
+                if (blockIdx.x == 0) {
+                    write_exponent(a, g);
+                    if (a.spec != 0) __hip_atomic_store(hint_p, (uint32_t)gbw + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
             }
         }
         __syncthreads();
         RC_STAMP(4);
-        if (U.valid && owner) rowconv_epilogue<W, R, DG>(a, U, lane, acc, gm, ein, smem + wid * RC_P16_WAVE_BYTES);
+        if (U.valid && owner && (!spec || gm != g_guess)) rowconv_epilogue<W, R, DG>(a, U, lane, acc, gm, ein, tile);
         RC_STAMP(5);
     } else if constexpr (MODE == RC_RANGE) {
         uint32_t m = 0;
@@ -1136,10 +1164,12 @@ bool rowconv_fused_ok(const ConvGeom& g, bool dg) {
 }
 
 static uint32_t g_rc_spin_limit = BAR_SPIN_LIMIT, g_rc_expect_extra = 0;
+static int g_rc_spec = 1;
 void rowconv_barrier_diag(uint32_t spin_limit, uint32_t expect_extra) {
     g_rc_spin_limit = spin_limit ? spin_limit : BAR_SPIN_LIMIT;
     g_rc_expect_extra = expect_extra;
 }
+void rowconv_speculate(int mode) { g_rc_spec = mode; }
 
 // Tile order over the XCDs: weight-major when the layer's weights outweigh its input (VGG-11's
 // 4x4 / 2x2 layers: 16 image groups re-read each co block's 147 KiB panel), else dispatch order.
@@ -1197,6 +1227,7 @@ hipError_t rowconv_fwd(const ConvGeom& g, const int8_t* x_c32, const int8_t* wf,
     a.err = err;
     a.spin_limit = g_rc_spin_limit;
     a.expect_extra = g_rc_expect_extra;
+    a.spec = g_rc_spec;
     a.stamps = g_rc_stamps;
     a.relu_mask = o.relu_mask;
     a.pool_x = o.pool_x;
@@ -1336,6 +1367,7 @@ hipError_t rowconv_fc(int n, int K, int rows, const int8_t* x, int xld, const in
     a.err = err;
     a.spin_limit = g_rc_spin_limit;
     a.expect_extra = g_rc_expect_extra;
+    a.spec = g_rc_spec;
     a.stamps = nullptr;
     a.relu_mask = o.relu_mask;
     a.pool_x = o.pool_x;

@@ -135,6 +135,7 @@ class ResNet18:
         y = y.view(self.batch, l["oh"], l["oh"], -1)
         if self.record:
             self.rec.setdefault("fwd", {})[i] = (y, relu)
+            self.rec.setdefault("in", {})[i] = x16
         return y, e_out
 
     def _dgrad(self, i, dy16, e_dy):
@@ -270,6 +271,11 @@ class ResNet18:
             out["logits"] = self.rec["logits"].cpu().numpy()[:, :self.classes].copy()
             out["exp_logits"] = int(self.rec["exp_logits"].item())
         return out
+
+    def input_tap(self, i):
+        """Host copy (NCHW) of parameter layer i's input in the last recorded step."""
+        x16 = self.rec["in"][i]
+        return self._nchw(x16.view(self.batch, self.convs[i]["h"], self.convs[i]["h"], -1), self.convs[i]["ci"])
 
     def step_macs(self) -> int:
         """MACs of one step, counted as the VGG driver counts them (niti_model_step_macs): every

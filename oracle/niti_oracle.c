@@ -916,3 +916,80 @@ int niti_ref_layer_step(const niti_ref_geom* g, const int8_t* x_nchw, const int8
     free(x_c4);
     return 0;
 }
+
+/* ---------------------------------------------------------------------------- */
+/* Sampled accumulation statistics (tools/guard_sample.py): for chosen outputs of a   */
+/* forward (kind 0), weight-gradient (1) or stride-1 input-gradient (2) conv, the      */
+/* exact integer sum, sum|p| (the 2^24 guard) and the sum accumulated product by      */
+/* product in float32 in the order the reference's 16x4 unit walks K                  */
+/* (Int8FunctionsOpt.cpp:211-226; K = ((tap) * ceil(C/4) + c/4) * 4 + c % 4, i.e. tap- */
+/* major then channel ascending, NITI_Conv_Int8.cpp:19-64 / the grad graph's convs),   */
+/* cast to int32 as the reference does.  NCHW activations, OIHW weights.               */
+/* ---------------------------------------------------------------------------- */
+void niti_ref_sample_stats(const niti_ref_geom* g, int kind, const int8_t* a, const int8_t* b, const int64_t* idx,
+                           int64_t ns, int64_t* exact, uint64_t* sabs, int32_t* f32) {
+    const int N = g->n, CI = g->c_in, H = g->h, W = g->w, CO = g->c_out, KH = g->kh, KW = g->kw;
+    const int OH = g->oh, OW = g->ow, SH = g->stride_h, SW = g->stride_w, PT = g->pad_t, PL = g->pad_l;
+    for (int64_t s = 0; s < ns; ++s) {
+        int64_t e = 0;
+        uint64_t sa = 0;
+        float f = 0.f;
+        int64_t q = idx[s];
+        if (kind == 0) { /* y[n][co][oy][ox], a = x, b = w */
+            const int ox = (int)(q % OW); q /= OW;
+            const int oy = (int)(q % OH); q /= OH;
+            const int co = (int)(q % CO);
+            const int n = (int)(q / CO);
+            for (int ky = 0; ky < KH; ++ky)
+                for (int kx = 0; kx < KW; ++kx) {
+                    const int iy = oy * SH - PT + ky * g->dilate_h, ix = ox * SW - PL + kx * g->dilate_w;
+                    if (iy < 0 || iy >= H || ix < 0 || ix >= W) continue;
+                    for (int c = 0; c < CI; ++c) {
+                        const int32_t p = (int32_t)a[(((int64_t)n * CI + c) * H + iy) * W + ix] *
+                                          (int32_t)b[(((int64_t)co * CI + c) * KH + ky) * KW + kx];
+                        e += p;
+                        sa += (uint64_t)(p < 0 ? -p : p);
+                        f += (float)p;
+                    }
+                }
+        } else if (kind == 1) { /* dw[co][ci][ky][kx], a = x, b = dy; K = (oy, ox) then n */
+            const int kx = (int)(q % KW); q /= KW;
+            const int ky = (int)(q % KH); q /= KH;
+            const int ci = (int)(q % CI);
+            const int co = (int)(q / CI);
+            for (int oy = 0; oy < OH; ++oy)
+                for (int ox = 0; ox < OW; ++ox) {
+                    const int iy = oy * SH - PT + ky * g->dilate_h, ix = ox * SW - PL + kx * g->dilate_w;
+                    if (iy < 0 || iy >= H || ix < 0 || ix >= W) continue;
+                    for (int n = 0; n < N; ++n) {
+                        const int32_t p = (int32_t)a[(((int64_t)n * CI + ci) * H + iy) * W + ix] *
+                                          (int32_t)b[(((int64_t)n * CO + co) * OH + oy) * OW + ox];
+                        e += p;
+                        sa += (uint64_t)(p < 0 ? -p : p);
+                        f += (float)p;
+                    }
+                }
+        } else { /* stride 1: dx[n][ci][y][x], a = dy, b = w; rotated taps ky' kx', then co */
+            const int x = (int)(q % W); q /= W;
+            const int y = (int)(q % H); q /= H;
+            const int ci = (int)(q % CI);
+            const int n = (int)(q / CI);
+            for (int kyr = 0; kyr < KH; ++kyr)
+                for (int kxr = 0; kxr < KW; ++kxr) {
+                    const int ky = KH - 1 - kyr, kx = KW - 1 - kxr;
+                    const int oy = y + PT - ky, ox = x + PL - kx;
+                    if (oy < 0 || oy >= OH || ox < 0 || ox >= OW) continue;
+                    for (int co = 0; co < CO; ++co) {
+                        const int32_t p = (int32_t)a[(((int64_t)n * CO + co) * OH + oy) * OW + ox] *
+                                          (int32_t)b[(((int64_t)co * CI + ci) * KH + ky) * KW + kx];
+                        e += p;
+                        sa += (uint64_t)(p < 0 ? -p : p);
+                        f += (float)p;
+                    }
+                }
+        }
+        exact[s] = e;
+        sabs[s] = sa;
+        f32[s] = (int32_t)f;
+    }
+}

@@ -141,6 +141,11 @@ void niti_ref_image_stats(const uint8_t* img, int64_t n, uint64_t stats[4]);
 int32_t niti_ref_image_quantize(const uint8_t* img, int64_t n, const uint64_t stats[4], int64_t count,
                                 int64_t var_count, int8_t* out);
 int32_t niti_ref_quantize_input(const float* x, int64_t n, int64_t var_n, int8_t* out);
+/* sampled accumulation statistics: kind 0 forward (a = x, b = w, idx into [n][co][oy][ox]), 1 weight
+ * gradient (a = x, b = dy, idx into [co][ci][ky][kx]), 2 stride-1 input gradient (a = dy, b = w, idx
+ * into [n][ci][y][x]): exact sum, sum|p| and the reference-order float32 sum cast to int32 */
+void niti_ref_sample_stats(const niti_ref_geom* g, int kind, const int8_t* a, const int8_t* b, const int64_t* idx,
+                           int64_t ns, int64_t* exact, uint64_t* sabs, int32_t* f32);
 int32_t niti_ref_quantize_input_lanes(const float* x, int64_t n, int64_t var_n, int lanes, int8_t* out);
 
 /* ---------------- CPU baseline ---------------- */

@@ -86,6 +86,7 @@ def _declare(L):
         "niti_ref_sgd_update": (None, [vp, vp, i64]),
         "niti_ref_quantize_input": (i32, [vp, i64, i64, vp]),
         "niti_ref_quantize_input_lanes": (i32, [vp, i64, i64, C.c_int, vp]),
+        "niti_ref_sample_stats": (None, [gp, C.c_int, vp, vp, vp, i64, vp, vp, vp]),
         "niti_ref_image_stats": (None, [vp, i64, vp]),
         "niti_ref_set_threads": (None, [C.c_int]),
         "niti_ref_image_quantize": (i32, [vp, i64, vp, i64, i64, vp]),
@@ -353,6 +354,19 @@ def quantize_input(x, lanes=1):
     out = np.empty(x.shape, np.int8)
     a = lib().niti_ref_quantize_input_lanes(_p(x), x.size, x.shape[0] * MNIST_VAR_PIXELS, int(lanes), _p(out))
     return out, int(a)
+
+
+def sample_stats(g, kind, a, b, idx):
+    """Per sampled output (flat indices idx): exact sum, sum|p|, reference-order float32 sum as int32
+    (niti_ref_sample_stats; kind 0 forward (x, w), 1 weight gradient (x, dy), 2 stride-1 input
+    gradient (dy, w); NCHW / OIHW int8)."""
+    a, b = _c(a, np.int8), _c(b, np.int8)
+    idx = np.ascontiguousarray(idx, np.int64)
+    ex = np.empty(idx.size, np.int64)
+    sa = np.empty(idx.size, np.uint64)
+    f = np.empty(idx.size, np.int32)
+    lib().niti_ref_sample_stats(C.byref(g), int(kind), _p(a), _p(b), _p(idx), idx.size, _p(ex), _p(sa), _p(f))
+    return ex, sa, f
 
 
 def image_stats(images):

@@ -251,3 +251,20 @@ def test_vgg16_224_step_matches_oracle(T):
         assert np.array_equal(m.tap(i, 1), rec["dw"][i]), ("dw", i)
         assert np.array_equal(m.get_weight(i), newW[i]), ("w", i)
     assert m.rowconv_error() == 0
+
+
+@pytest.mark.parametrize("mode", [0, 2])
+def test_vgg11_step_speculative_epilogue_modes(T, mode):
+    """The fused row kernels' speculative epilogue (the previous launch's bit width applied while
+    the grid barrier completes) must not change any result: off (0), and forced wrong on every
+    launch (2: every epilogue redone with the barrier's bit width), two steps each against the
+    oracle.  The default (1) is what every other test runs."""
+    import niti_amd
+    import niti_model_ref as R
+    from niti_amd import _lib as L
+    lib = L.lib()
+    try:
+        lib.niti_diag_rowconv_speculate(mode)
+        _run(T, niti_amd.ARCH_VGG11, R.vgg11_layers(), batch=32, steps=2, seed=17 + mode)
+    finally:
+        lib.niti_diag_rowconv_speculate(1)
