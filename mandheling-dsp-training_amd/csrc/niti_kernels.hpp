@@ -221,6 +221,10 @@ struct RowConvOut {
     int8_t* pool_dx = nullptr;
     int8_t* pool_dx_next = nullptr;
     int pool_relu = 0;
+    // 0: pool_dx (NHWC16) is not written, only its C32 (pool_dx_next) / P16 copies; the pool
+    // gradient's routing still needs pool_dx non-null.  Likewise out may be null in the input
+    // gradient when its consumers read the C32 (next) and P16 copies.
+    int pool_dx_nhwc = 1;
     // input gradient: the same gradient in the weight gradient's P16 layout (rowconv_p16_ok)
     int8_t* p16 = nullptr;
     // modes RANGE + REQUANT (data parallel: the MAX all-reduce sits between them): the range
@@ -247,6 +251,8 @@ bool rowconv_fused_ok(const ConvGeom& g, bool dg = false);
 int rowconv_units(const ConvGeom& g, bool dg = false);
 size_t rowconv_wf_bytes(int co, int ci);
 hipError_t nhwc16_to_c32(const int8_t* in, int n, int hw, int cp, int c, int8_t* out, hipStream_t st);
+// C32 [n][cb][hw][32] -> NHWC16 [n][hw][cp] (channels >= c written as zero)
+hipError_t c32_to_nhwc16(const int8_t* in, int n, int hw, int cp, int c, int8_t* out, hipStream_t st);
 // OHWI16 [co][9][cip] -> WF; transpose: the input-gradient conv's WF (rotate180, ci <-> co)
 hipError_t weights_to_wf(const int8_t* w_ohwi16, int co, int ci, int cip, bool transpose, int8_t* out,
                          hipStream_t st);

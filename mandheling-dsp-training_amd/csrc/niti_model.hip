@@ -343,6 +343,10 @@ struct Model {
     // dyc32_valid[i]: L[i].dyc32 holds L[i].dy as it is now (written by the next layer's input
     // gradient epilogue, else converted)
     std::vector<char> dyc32_valid;
+    // dy16_valid[i]: L[i].dy (NHWC16) was written this step; a row-kernel input gradient leaves it
+    // out when the layer's own consumers read its C32 (input gradient) and P16 (weight gradient)
+    // copies (niti_model_get_tap rebuilds it from the C32 copy)
+    std::vector<char> dy16_valid;
     bool rowconv_dgrad_layer(int i) const { return use_rowconv && L[i].rcd; }
     // the classifier head (a 1x1 conv over 1x1 maps, at most 64 outputs) on the row kernel's
     // W = 1 path: forward, and its input gradient into the previous layer's relu / 2x2 pool
@@ -587,6 +591,13 @@ struct Model {
     // it while its grid barrier completes (side_sgd_used: it did)
     const SgdJob* side_sgd = nullptr;
     bool side_sgd_used = false;
+    // the input gradient of layer i need not write L[i - 1].dy in NHWC16: its weight gradient reads
+    // the P16 copy (p16) and its input gradient the C32 copy (next) this same launch writes (layer 0's
+    // GEMM weight gradient reads NHWC16).  NITI_DY16=1 keeps the copy (A/B diagnostics).
+    bool skip_dy16(int i, const int8_t* next, const int8_t* p16) const {
+        static const bool keep = getenv("NITI_DY16") != nullptr && getenv("NITI_DY16")[0] == '1';
+        return !keep && i - 1 >= 1 && next != nullptr && p16 != nullptr && wgrad_p16_splits(i - 1) > 0;
+    }
     int autotune(hipStream_t st, int reps);
     // grow a split-K workspace (the old one stays owned by ws until the model is destroyed)
     bool ensure_slab(size_t bytes, bool wgrad) {
@@ -738,6 +749,7 @@ int Model::build(int arch_, int batch_, int in_hw) {
     dp16_valid.assign(nl, 0);
     xc32_valid.assign(nl, 0);
     dyc32_valid.assign(nl, 0);
+    dy16_valid.assign(nl, 1);
     rc_err = (uint32_t*)ws.alloc(64);
     if (!rc_err || hipMemset(rc_err, 0, 64) != hipSuccess) return NITI_OUT_OF_MEMORY;
     for (int i = 0; i < nl; ++i) {
@@ -1092,11 +1104,13 @@ int Model::dgrad_layer(int i, hipStream_t st) {
             o.pool_dx_next = next;
             o.pool_relu = pv.relu;
             o.p16 = fuse_dp16 && wgrad_p16_splits(i - 1) > 0 && (4 * n) % 16 == 0 ? dp16[i - 1] : nullptr;
+            o.pool_dx_nhwc = skip_dy16(i, next, o.p16) ? 0 : 1;
         } else {
             o.out = pv.dy;
             o.relu_mask = pv.relu ? pv.r : nullptr;
             next = nullptr;  // a 1x1 previous layer has no row-kernel input gradient
         }
+        dy16_valid[i - 1] = !(pv.pool && o.pool_dx_nhwc == 0);
         const int K = g.c_out, rows = g.c_in;
         if (!dp && !capturing && rowconv_fc_ok(n, K, rows, true)) {
             o.sgd = side_sgd;
@@ -1124,17 +1138,20 @@ int Model::dgrad_layer(int i, hipStream_t st) {
         // the previous layer's P16 dy for its weight gradient, when the launch's pixels make whole
         // 16-pixel blocks; else wgrad_layer converts
         o.p16 = fuse_dp16 && wgrad_p16_splits(i - 1) > 0 && rowconv_p16_ok(l.dg, pv.pool) ? dp16[i - 1] : nullptr;
+        const bool skip16 = skip_dy16(i, next, o.p16);
         if (pv.pool) {
             o.pool_x = pv.r;
             o.pool_y = pv.p;
             o.pool_dx = pv.dy;
             o.pool_dx_next = next;
             o.pool_relu = pv.relu;
+            o.pool_dx_nhwc = skip16 ? 0 : 1;
         } else {
-            o.out = pv.dy;
+            o.out = skip16 ? nullptr : pv.dy;
             o.next = next;
             o.relu_mask = pv.relu ? pv.r : nullptr;
         }
+        dy16_valid[i - 1] = !skip16;
         const ConvGeom& d = l.dg;
         if (!dp && !capturing && rowconv_fused_ok(d, true)) {
             o.sgd = side_sgd;
@@ -1151,6 +1168,7 @@ int Model::dgrad_layer(int i, hipStream_t st) {
         dyc32_valid[i - 1] = next != nullptr ? 1 : 0;
         return NITI_NO_ERROR;
     }
+    dy16_valid[i - 1] = 1;
     MTRY(conv_dgrad_phase1(g, l.dy, l.wT, acc, rng(i, 1), slab, slab_bytes, st));
     if (dp && exact) CTRY(coll->allreduce(rng(i, 1), MAX_WORDS, COLL_MAX_U32, st));
     const ConvGeom& pg = pv.g;
@@ -1647,7 +1665,14 @@ int niti_model_get_tap(niti_model_t m, int layer, int which, int8_t* host, size_
     hipError_t e;
     if (which == 0)
         e = niti::nhwc16_to_nchw(l.r, n, g.c_out, g.oh * g.ow, g.cop, tmp, nullptr);
-    else if (which == 2)
+    else if (which == 2 && !m->m.dy16_valid[layer]) {  // rebuilt from the C32 copy the step wrote
+        int8_t* d16 = nullptr;
+        e = hipMalloc(&d16, (size_t)n * g.oh * g.ow * g.cop);
+        if (e == hipSuccess) e = niti::c32_to_nhwc16(l.dyc32, n, g.oh * g.ow, g.cop, g.c_out, d16, nullptr);
+        if (e == hipSuccess) e = niti::nhwc16_to_nchw(d16, n, g.c_out, g.oh * g.ow, g.cop, tmp, nullptr);
+        if (e == hipSuccess) e = hipDeviceSynchronize();
+        if (d16) (void)hipFree(d16);
+    } else if (which == 2)
         e = niti::nhwc16_to_nchw(l.dy, n, g.c_out, g.oh * g.ow, g.cop, tmp, nullptr);
     else
         e = niti::ohwi16_to_oihw(l.g8, g.c_out, g.c_in, g.kh * g.kw, g.cip, tmp, nullptr);

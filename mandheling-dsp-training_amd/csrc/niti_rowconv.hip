@@ -193,6 +193,7 @@ struct RowConvArgs {
     int8_t* pool_dx;
     int8_t* pool_dx_next;
     int pool_relu;
+    int pool_dx_nhwc;            // 0: the NHWC16 pool_dx is not written (its consumers read the C32 / P16 copies)
     int8_t* p16;                 // P16 [pixels/16][cop][16] copy of out / pool_dx, or null
     int64_t p16_pixels;          // pixels of that tensor
     int32_t* acc_store;          // RANGE writes / REQUANT reads every unit's accumulators, or null
@@ -719,7 +720,7 @@ __device__ __forceinline__ void rowconv_epilogue(const RowConvArgs& a, const Row
             for (int t = 0; t < 4; ++t) {
                 const int iy = 2 * oy + (t >> 1), ix = 2 * ox + (t & 1);
                 const v4i d = v & e.x[DG ? r : 0][t];  // the routing mask (epi_masks)
-                *(v4i*)(a.pool_dx + ((img * H2 + iy) * W2 + ix) * a.cop + cb16) = d;
+                if (a.pool_dx_nhwc) *(v4i*)(a.pool_dx + ((img * H2 + iy) * W2 + ix) * a.cop + cb16) = d;
                 if (a.pool_dx_next != nullptr)
                     *(v4i*)(a.pool_dx_next + (((img * a.COB + U.cob) * H2 + iy) * W2 + ix) * 32 + 16 * h) = d;
                 if (a.p16 != nullptr)
@@ -737,7 +738,7 @@ __device__ __forceinline__ void rowconv_epilogue(const RowConvArgs& a, const Row
         if (U.img_ok) {
             const int64_t po = ((img * H + oy) * W + ox) * a.cop + cb16;
             if (DG && a.relu_mask != nullptr) v &= e.y[DG ? r : 0];
-            if (W > 1 || cb16 < a.cop) *(v4i*)(a.out + po) = v;  // a 1x1 head's 16 channels
+            if (a.out != nullptr && (W > 1 || cb16 < a.cop)) *(v4i*)(a.out + po) = v;  // (a 1x1 head: 16 channels)
             if (a.next != nullptr && a.pool_out == nullptr)
                 *(v4i*)(a.next + (((img * a.COB + U.cob) * H + oy) * W + ox) * 32 + 16 * h) = v;
             if (DG && a.p16 != nullptr) *(v4i*)(tile + (((c / W) * R + r) * W + ox) * 32 + 16 * h) = v;
@@ -1015,6 +1016,27 @@ hipError_t nhwc16_to_c32(const int8_t* in, int n, int hw, int cp, int c, int8_t*
     return launch_map((int64_t)n * cb * hw * 2, Nhwc16ToC32{in, hw, cp, cb, out}, st);
 }
 
+// C32 [n][cb][hw][32] -> NHWC16 [n][hw][cp], one 16-byte chunk per thread
+struct C32ToNhwc16 {
+    const int8_t* in;
+    int hw, cp, c, cb;
+    int8_t* out;
+    __device__ void operator()(int64_t i) const {  // i over 16-byte chunks of out
+        const int cc = (int)(i % (cp / 16)) * 16;
+        const int64_t q = i / (cp / 16);  // (img, p)
+        const int p = (int)(q % hw);
+        const int64_t img = q / hw;
+        v16c v = {};
+        if (cc < c) v = *(const v16c*)(in + (((img * cb + cc / 32) * hw + p) * 32 + (cc & 31)));
+        *(v16c*)(out + i * 16) = v;
+    }
+};
+
+hipError_t c32_to_nhwc16(const int8_t* in, int n, int hw, int cp, int c, int8_t* out, hipStream_t st) {
+    const int cb = (c + 31) / 32;
+    return launch_map((int64_t)n * hw * (cp / 16), C32ToNhwc16{in, hw, cp, c, cb, out}, st);
+}
+
 hipError_t weights_to_wf(const int8_t* w_ohwi16, int co, int ci, int cip, bool transpose, int8_t* out,
                          hipStream_t st) {
     const int COB = transpose ? (ci + 31) / 32 : (co + 31) / 32;
@@ -1258,6 +1280,7 @@ hipError_t rowconv_fwd(const ConvGeom& g, const int8_t* x_c32, const int8_t* wf,
     a.pool_dx = o.pool_dx;
     a.pool_dx_next = o.pool_dx_next;
     a.pool_relu = o.pool_relu;
+    a.pool_dx_nhwc = o.pool_dx_nhwc;
     a.p16 = o.p16;
     a.p16_pixels = (int64_t)g.n * g.h * g.w * (o.pool_dx != nullptr ? 4 : 1);
     a.acc_store = mode == RC_FUSED ? nullptr : o.acc_store;
@@ -1402,6 +1425,7 @@ hipError_t rowconv_fc(int n, int K, int rows, const int8_t* x, int xld, const in
     a.pool_dx = o.pool_dx;
     a.pool_dx_next = o.pool_dx_next;
     a.pool_relu = o.pool_relu;
+    a.pool_dx_nhwc = o.pool_dx_nhwc;
     a.p16 = o.p16;
     a.p16_pixels = (int64_t)n * (o.pool_dx != nullptr ? 4 : 1);
     const bool dg = o.relu_mask != nullptr || o.pool_dx != nullptr || o.p16 != nullptr;

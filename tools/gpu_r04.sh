@@ -12,10 +12,15 @@ if [ "${SKIP_TESTS:-0}" != 1 ]; then
   rc=$?; tail -2 gpurun_out/smoke_$TAG.log; echo "smoke rc=$rc"
   [ $rc -eq 0 ] || exit $rc
 fi
-for spec in 1 0 1 0; do
-  timeout -k 10 300 python3 bench.py --cpu-sample 0 --rc-spec $spec > gpurun_out/bench_${TAG}_s$spec.log 2>&1
-  rc=$?; [ $rc -eq 0 ] || { tail -5 gpurun_out/bench_${TAG}_s$spec.log; exit $rc; }
-  echo "spec=$spec $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/bench_${TAG}_s$spec.log)"
+# A/B, alternating: all on; speculation off; side SGD off; NHWC16 dy kept
+for rep in 1 2; do
+  for v in "on:" "spec0:--rc-spec 0" "side0:NITI_SIDE_SGD=0" "dy16:NITI_DY16=1"; do
+    name=${v%%:*}; opt=${v#*:}; envs=""; flags=""
+    case "$opt" in *=*) envs=$opt;; *) flags=$opt;; esac
+    env $envs timeout -k 10 300 python3 bench.py --cpu-sample 0 $flags > gpurun_out/bench_${TAG}_$name.log 2>&1
+    rc=$?; [ $rc -eq 0 ] || { tail -5 gpurun_out/bench_${TAG}_$name.log; exit $rc; }
+    echo "$name rep$rep $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/bench_${TAG}_$name.log)"
+  done
 done
 for m in x w; do
   for d in "" "--dgrad fused"; do
