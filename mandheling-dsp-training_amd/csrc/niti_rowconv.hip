@@ -1228,7 +1228,9 @@ void rowconv_stamps_arm(unsigned long long* buf) { g_rc_stamps = buf; }
 hipError_t rowconv_fwd(const ConvGeom& g, const int8_t* x_c32, const int8_t* wf, const RowConvOut& o, int mode,
                        uint32_t* amax, uint32_t* bar, uint32_t epoch, uint32_t* err, hipStream_t st) {
     if (!rowconv_ok(g) || x_c32 == nullptr || wf == nullptr || amax == nullptr) return hipErrorInvalidValue;
-    if (mode != RC_RANGE && o.out == nullptr && o.pool_dx == nullptr) return hipErrorInvalidValue;
+    // an output: NHWC16 out, the pool gradient, or (input gradient) only the C32 / P16 copies
+    if (mode != RC_RANGE && o.out == nullptr && o.pool_dx == nullptr && o.next == nullptr && o.p16 == nullptr)
+        return hipErrorInvalidValue;
     if (o.pool_dx != nullptr && (o.pool_x == nullptr || o.pool_y == nullptr || o.out != nullptr || o.pool_out != nullptr ||
                                  o.relu_mask != nullptr || o.next != nullptr))
         return hipErrorInvalidValue;
@@ -1379,7 +1381,9 @@ hipError_t rowconv_fc(int n, int K, int rows, const int8_t* x, int xld, const in
     if (!rowconv_fc_ok(n, K, rows, mode == RC_FUSED) || x == nullptr || w == nullptr || amax == nullptr)
         return hipErrorInvalidValue;
     if (xld % 16 != 0 || wld % 16 != 0 || xld < K || wld < K) return hipErrorInvalidValue;
-    if (mode != RC_RANGE && o.out == nullptr && o.pool_dx == nullptr) return hipErrorInvalidValue;
+    // an output: NHWC16 out, the pool gradient, or (input gradient) only the C32 / P16 copies
+    if (mode != RC_RANGE && o.out == nullptr && o.pool_dx == nullptr && o.next == nullptr && o.p16 == nullptr)
+        return hipErrorInvalidValue;
     if (o.pool_out != nullptr || (o.pool_dx != nullptr && (o.pool_x == nullptr || o.pool_y == nullptr)))
         return hipErrorInvalidValue;
     const int64_t xb = (int64_t)n * xld, wb = (int64_t)rows * wld;
