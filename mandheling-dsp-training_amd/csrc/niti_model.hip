@@ -972,7 +972,7 @@ int Model::fwd_layer(int i, hipStream_t st) {
         if (!dp && !capturing && rowconv_fused_ok(g)) {
             MTRY(rowconv_fwd(g, l.xc32, l.wf, o, 0, rng(i, 0), l.bar, ++l.epoch, rc_err, st));
         } else {
-            o.acc_store = rc_acc;
+            o.acc_store = rowconv_acc_bytes(g, false) ? rc_acc : nullptr;  // else the requantise launch recomputes
             MTRY(rowconv_fwd(g, l.xc32, l.wf, o, 1, rng(i, 0), nullptr, 0, nullptr, st));
             if (dp && exact) CTRY(coll->allreduce(rng(i, 0), MAX_WORDS, COLL_MAX_U32, st));
             MTRY(rowconv_fwd(g, l.xc32, l.wf, o, 2, rng(i, 0), nullptr, 0, nullptr, st));
@@ -1158,7 +1158,7 @@ int Model::dgrad_layer(int i, hipStream_t st) {
             MTRY(rowconv_fwd(d, l.dyc32, l.wft, o, 0, rng(i, 1), l.bar, ++l.epoch, rc_err, st));
             side_sgd_used = side_sgd != nullptr;
         } else {
-            o.acc_store = rc_acc;
+            o.acc_store = rowconv_acc_bytes(d, true) ? rc_acc : nullptr;
             MTRY(rowconv_fwd(d, l.dyc32, l.wft, o, 1, rng(i, 1), nullptr, 0, nullptr, st));
             if (dp && exact) CTRY(coll->allreduce(rng(i, 1), MAX_WORDS, COLL_MAX_U32, st));
             MTRY(rowconv_fwd(d, l.dyc32, l.wft, o, 2, rng(i, 1), nullptr, 0, nullptr, st));

@@ -200,6 +200,11 @@ struct RowConvArgs {
     // W = 1 (1x1 maps, the classifier head): x is row-major [n][xld], the weights row-major
     // [rows][wld] (OHWI16 forward, IHWO16 input gradient), K the reduced channels
     int xld, wld, K, rows;
+    // W = 0, the row-segment form (maps of 224 / 112 / 56 / 28 / 14 / 7 px): hw the map's side,
+    // gw images per unit (1: two 14-px segments of one row, 2: one 14-px row of two images, 4: two
+    // 7-px rows of two images per 16 lanes), nsp segment pairs per row, upc4 units per co block
+    // rounded up to whole workgroups of 4
+    int hw, gw, nsp, upc4;
 };
 
 // diagnostic stamps, 16 per wave: [0] start, [1] prologue issued, [2] cycles issuing loads, [3] K
@@ -219,11 +224,45 @@ enum RowMode { RC_FUSED = 0, RC_RANGE = 1, RC_REQUANT = 2 };
 // per 32-channel chunk (a 9 KiB contiguous run of WF) instead of each wave loading them.
 template <int W, int R>
 struct RowUnit {
-    static constexpr int G = 32 / W, H = W, NR = R + 2;
+    static constexpr int G = W > 0 ? 32 / W : 1, H = W, NR = R + 2;
     int cob, b, img;
     bool valid, img_ok;
+    // the row-segment form (W = 0): the lane's input column x (-1 / hw: a zero halo), whether x is
+    // in the map, and whether the lane's MFMA column is an output pixel (not a halo lane)
+    int x = 0;
+    bool x_ok = true, out_ok = true;
     // ks: the K-split form -- one unit per workgroup, its four waves splitting the channel chunks
     __device__ RowUnit(const RowConvArgs& a, int wg, int wid, int c, bool ks = false) {
+        if constexpr (W == 0) {
+            // units of a co block: ((image group, band), segment pair), whole workgroups of four
+            const int per = a.upc4 / 4;
+            cob = wg / per;
+            const int u = (wg - cob * per) * 4 + wid;
+            const int nu = a.ngb * a.nsp;  // ngb = image groups x bands
+            valid = u < nu;
+            const int uc = valid ? u : 0;
+            const int sp = uc % a.nsp, gb = uc / a.nsp;
+            b = gb % a.nbands;
+            const int ig = gb / a.nbands;
+            const int sgi = c >> 4, q = c & 15;
+            if (a.gw == 1) {  // two 14-px segments of one row: lanes 0 / 15 (16 / 31) are halos
+                img = ig;
+                x = 28 * sp + 14 * sgi + q - 1;
+                out_ok = q >= 1 && q <= 14;
+            } else if (a.gw == 2) {  // one 14-px row per 16 lanes, two images
+                img = 2 * ig + sgi;
+                x = q - 1;
+                out_ok = q >= 1 && q <= 14;
+            } else {  // two 7-px rows per 16 lanes (lanes 0 and 8 zero halos), four images
+                img = 4 * ig + 2 * sgi + (q >> 3);
+                x = (q & 7) - 1;
+                out_ok = (q & 7) >= 1;
+            }
+            x_ok = x >= 0 && x < a.hw;
+            img_ok = valid && img < a.n;
+            out_ok = out_ok && img_ok;
+            return;
+        }
         const int per = ks ? a.ngb : a.ngb4 / 4;
         cob = wg / per;
         const int gb = ks ? wg - cob * per : (wg - cob * per) * 4 + wid;
@@ -264,7 +303,10 @@ static_assert(RC_KS_BYTES >= 4 * RC_P16_WAVE_BYTES, "the P16 tile fits the K-spl
 template <int W, int R, bool UNC>
 __device__ __forceinline__ void rowconv_compute(const RowConvArgs& a, const RowUnit<W, R>& U, int lane, int wid,
                                                 int8_t* smem, v16i (&acc)[R]) {
-    constexpr int H = W, NR = R + 2;
+    // W = 0: the row-segment form, its side a.hw at run time; halo lanes supply the kx neighbours,
+    // so the DPP shifts need no row-end masks (as W = 16)
+    constexpr int NR = R + 2, WS = W == 0 ? 16 : W;
+    const int H = W == 0 ? a.hw : W, WR = W == 0 ? a.hw : W;
     // kx shifts: DPP row shifts of the centre column (zero fill at the 16-lane DPP row ends, a
     // mask where a narrower image row ends inside a DPP row) -- one load per row: each 16-byte
     // wave load costs the CU's texture addresser ~16 cycles, and three loads per row (the
@@ -274,11 +316,12 @@ __device__ __forceinline__ void rowconv_compute(const RowConvArgs& a, const RowU
     constexpr int KXL = DPPX ? 1 : 3;        // loads per row and chunk
     constexpr int S = 4;                     // ring stages: chunk c computes, c + 1 .. c + 3 in flight
     constexpr int L = KXL * NR + 3;          // vector-memory instructions per wave per chunk
-    const int h = lane >> 5, c = lane & 31, ox = c % W;
+    const int h = lane >> 5, c = lane & 31, ox = W == 0 ? U.x : c % WS;
     const __amdgpu_buffer_rsrc_t rX = make_rsrc(a.x, a.xbytes);
     const __amdgpu_buffer_rsrc_t rW = make_rsrc(a.wf, a.wbytes);
-    const uint32_t xl = U.img_ok ? (uint32_t)((((int64_t)U.img * a.CB * H) * W + ox) * 32 + 16 * h) : OOB;
-    constexpr uint32_t CHUNK = (uint32_t)H * W * 32;
+    const uint32_t xl =
+        U.img_ok && U.x_ok ? (uint32_t)((((int64_t)U.img * a.CB * H) * WR + ox) * 32 + 16 * h) : OOB;
+    const uint32_t CHUNK = (uint32_t)H * WR * 32;
     const int y0 = U.b * R - 1;
 #pragma unroll
     for (int r = 0; r < R; ++r)
@@ -290,10 +333,10 @@ __device__ __forceinline__ void rowconv_compute(const RowConvArgs& a, const RowU
     for (int j = 0; j < NR; ++j) {
         const int iy = y0 + j;
         const bool row_ok = iy >= 0 && iy < H && xl != OOB;
-        const uint32_t base = xl + (uint32_t)iy * W * 32;
+        const uint32_t base = xl + (uint32_t)iy * WR * 32;
         off[0][j] = row_ok && ox > 0 ? base - 32u : OOB;
         off[1][j] = row_ok ? base : OOB;
-        off[2][j] = row_ok && ox < W - 1 ? base + 32u : OOB;
+        off[2][j] = row_ok && ox < WR - 1 ? base + 32u : OOB;
     }
     // this wave's three DMA pieces of a chunk's 9 fragments (pieces 9..11 are dummies: OOB source)
     const uint32_t dv2 = wid == 0 ? (uint32_t)lane * 16u : OOB;
@@ -358,8 +401,8 @@ __device__ __forceinline__ void rowconv_compute(const RowConvArgs& a, const RowU
             v4i XL[NR], XR[NR];
 #pragma unroll
             for (int j = 0; j < NR; ++j) {
-                XL[j] = (RC_EXP & 1) ? X[ST][0][j] : shift_in_left<W>(X[ST][0][j], ox == 0);
-                XR[j] = (RC_EXP & 1) ? X[ST][0][j] : shift_in_right<W>(X[ST][0][j], ox == W - 1);
+                XL[j] = (RC_EXP & 1) ? X[ST][0][j] : shift_in_left<WS>(X[ST][0][j], ox == 0);
+                XR[j] = (RC_EXP & 1) ? X[ST][0][j] : shift_in_right<WS>(X[ST][0][j], ox == WS - 1);
             }
 #pragma unroll
             for (int r = 0; r < R; ++r)
@@ -768,6 +811,163 @@ __device__ __forceinline__ void rowconv_epilogue(const RowConvArgs& a, const Row
     }
 }
 
+__device__ __forceinline__ uint32_t max_abs16(const v16i& v, uint32_t m) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const uint32_t u = uabs32(v[i]);
+        m = m > u ? m : u;
+    }
+    return m;
+}
+
+// ---- the row-segment form's epilogue (W = 0) ---------------------------------------------------
+// Its MFMA columns are 14-px segments (or 7-px rows) with halo lanes, so a lane's output pixel is
+// (U.img, row, U.x) where U.out_ok; the halo lanes' accumulators are partial sums and are neither
+// ranged nor stored.  Same rule, relu / pool / pool-gradient epilogues and layouts as the W > 0 form.
+template <int R>
+__device__ __forceinline__ void seg_prefetch(const RowConvArgs& a, const RowUnit<0, R>& U, int lane, EpiIn<R>& e) {
+    const int h = lane >> 5, W = a.hw, H = a.hw;
+    const int64_t img = U.img_ok ? U.img : 0;
+    const int xs = U.x < 0 ? 0 : (U.x >= W ? W - 1 : U.x);  // a halo lane reads a real pixel (unused)
+    const int cb16 = U.cob * 32 + 16 * h;
+    uint32_t z = 0;
+    asm volatile("" : "+s"(z));
+    const bool pool = a.pool_dx != nullptr;
+    const int8_t* ps = (pool ? a.pool_y : a.relu_mask) + z;
+    const int8_t* px = a.pool_x + z;
+    if (!pool && a.relu_mask == nullptr) return;
+#pragma unroll
+    for (int r = 0; r < R; ++r) e.y[r] = *(const v4i*)(ps + ((img * H + U.b * R + r) * W + xs) * a.cop + cb16);
+    if (pool) {
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+                e.x[r][t] = *(const v4i*)(px + ((img * 2 * H + 2 * (U.b * R + r) + (t >> 1)) * 2 * W + 2 * xs + (t & 1)) *
+                                                   a.cop + cb16);
+    }
+}
+
+template <int R, bool DG>
+__device__ __forceinline__ void seg_epilogue(const RowConvArgs& a, const RowUnit<0, R>& U, int lane,
+                                             const v16i (&acc)[R], uint32_t gmax, const EpiIn<DG ? R : 1>& e) {
+    const int h = lane >> 5, W = a.hw, H = a.hw;
+    const int shift = __builtin_amdgcn_readfirstlane(bitwidth_rc(gmax) - 7);
+    int8_t q[R][16];
+    if (shift <= 0) {
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int32_t v = (int32_t)(int8_t)acc[r][i];
+                q[r][i] = (int8_t)(a.relu && v < 0 ? 0 : v);
+            }
+    } else {
+        const uint32_t s = shift > 1 ? shift : 2, hh = s >> 1, odd = s & 1;
+        auto pos = [&](uint32_t u) -> uint32_t {  // PSTO of u >= 0
+            const uint32_t qv = u >> s;
+            const uint32_t hi = __builtin_amdgcn_ubfe(u, hh, s - hh);
+            const uint32_t lo = __builtin_amdgcn_ubfe(u, 0, hh) << odd;
+            const uint32_t rr = qv + (hi > lo ? 1u : 0u);
+            return rr < 127u ? rr : 127u;
+        };
+        if (a.relu) {
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) q[r][i] = (int8_t)pos((uint32_t)max(acc[r][i], 0));
+        } else {
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const int32_t v = acc[r][i];
+                    const int32_t p = (int32_t)pos(uabs32(v));
+                    q[r][i] = (int8_t)(v < 0 ? -p : p);
+                }
+        }
+    }
+    const int64_t img = U.img;
+    const int x = U.x;
+    const int cb16 = U.cob * 32 + 16 * h;
+    if (DG && a.pool_dx != nullptr) {  // through the previous layer's 2x2 max pool
+        const int H2 = 2 * H, W2 = 2 * W;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const v4i v = pack_cols(q[r]);
+            const int oy = U.b * R + r;
+            if (!U.out_ok) continue;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const int iy = 2 * oy + (t >> 1), ix = 2 * x + (t & 1);
+                const v4i d = v & e.x[DG ? r : 0][t];
+                if (a.pool_dx_nhwc) *(v4i*)(a.pool_dx + ((img * H2 + iy) * W2 + ix) * a.cop + cb16) = d;
+                if (a.pool_dx_next != nullptr)
+                    *(v4i*)(a.pool_dx_next + (((img * a.COB + U.cob) * H2 + iy) * W2 + ix) * 32 + 16 * h) = d;
+            }
+        }
+        return;
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        v4i v = pack_cols(q[r]);
+        const int oy = U.b * R + r;
+        if (U.out_ok) {
+            if (DG && a.relu_mask != nullptr) v &= e.y[DG ? r : 0];
+            if (a.out != nullptr) *(v4i*)(a.out + ((img * H + oy) * W + x) * a.cop + cb16) = v;
+            if (a.next != nullptr && a.pool_out == nullptr)
+                *(v4i*)(a.next + (((img * a.COB + U.cob) * H + oy) * W + x) * 32 + 16 * h) = v;
+        }
+    }
+    if (a.pool_out != nullptr) {  // pairs (x, x + 1), x even, never straddle a segment (14 even)
+        const int HO = H / 2, WO = W / 2;
+#pragma unroll
+        for (int r = 0; r + 1 < R; r += 2) {
+            int8_t pm[16];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int v0 = q[r][i] > q[r + 1][i] ? q[r][i] : q[r + 1][i];
+                const int v1 = __builtin_amdgcn_update_dpp(0, v0, 0x101, 0xF, 0xF, true);  // row_shl:1: lane + 1
+                pm[i] = (int8_t)(v0 > v1 ? v0 : v1);
+            }
+            const v4i v = pack_cols(pm);
+            if (U.out_ok && (x & 1) == 0) {
+                const int py = (U.b * R + r) / 2, pxo = x / 2;
+                *(v4i*)(a.pool_out + ((img * HO + py) * WO + pxo) * a.cop + cb16) = v;
+                if (a.next != nullptr)
+                    *(v4i*)(a.next + (((img * a.COB + U.cob) * HO + py) * WO + pxo) * 32 + 16 * h) = v;
+            }
+        }
+    }
+}
+
+template <int W, int R>
+__device__ __forceinline__ void unit_prefetch(const RowConvArgs& a, const RowUnit<W, R>& U, int lane, EpiIn<R>& e) {
+    if constexpr (W == 0)
+        seg_prefetch<R>(a, U, lane, e);
+    else
+        epi_prefetch<W, R>(a, U, lane, e);
+}
+
+template <int W, int R, bool DG>
+__device__ __forceinline__ void unit_epilogue(const RowConvArgs& a, const RowUnit<W, R>& U, int lane,
+                                              const v16i (&acc)[R], uint32_t gmax, const EpiIn<DG ? R : 1>& e,
+                                              int8_t* tile) {
+    if constexpr (W == 0)
+        seg_epilogue<R, DG>(a, U, lane, acc, gmax, e);
+    else
+        rowconv_epilogue<W, R, DG>(a, U, lane, acc, gmax, e, tile);
+}
+
+// max |acc| over the unit's output columns (the row-segment form's halo lanes hold partial sums)
+template <int W, int R>
+__device__ __forceinline__ uint32_t unit_max(const RowUnit<W, R>& U, const v16i (&acc)[R], uint32_t m) {
+    if (W == 0 && !U.out_ok) return m;
+#pragma unroll
+    for (int r = 0; r < R; ++r) m = max_abs16(acc[r], m);
+    return m;
+}
+
 // a unit's accumulators in acc_store: [unit][r][i / 4][lane][4] -- one 1 KiB wave store / load per
 // 4 registers (unit = workgroup tile x 4 + wave; a K-split workgroup's unit is its wave 0's)
 template <int R>
@@ -819,14 +1019,6 @@ __device__ __forceinline__ void write_exponent(const RowConvArgs& a, uint32_t gm
     *a.exp_out = (int8_t)((a.exp_in ? (int)*a.exp_in : 0) + (a.wscale ? (int)*a.wscale : 0) + inc);
 }
 
-__device__ __forceinline__ uint32_t max_abs16(const v16i& v, uint32_t m) {
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        const uint32_t u = uabs32(v[i]);
-        m = m > u ? m : u;
-    }
-    return m;
-}
 
 // KS = 0: four units per workgroup; KS = NS: one unit, K split over the waves (wave 0 holds the sum)
 template <int W, int R, bool UNC, int KS>
@@ -872,10 +1064,8 @@ __global__ void __launch_bounds__(256, (RC_EXP & 16) ? 2 : 1) rowconv_fwd_kernel
         compute_unit<W, R, UNC, KS>(a, U, lane, wid, smem, acc);
         EpiIn<DG ? R : 1> ein = {};
         if constexpr (DG)
-            if (owner) epi_prefetch<W, R>(a, U, lane, ein);
-        if (owner)
-#pragma unroll
-            for (int r = 0; r < R; ++r) m = max_abs16(acc[r], m);
+            if (owner) unit_prefetch<W, R>(a, U, lane, ein);
+        if (owner) m = unit_max<W, R>(U, acc, m);
         m = wave_max(m);
         if (lane == 0) red[wid] = m;
         __syncthreads();
@@ -890,7 +1080,7 @@ __global__ void __launch_bounds__(256, (RC_EXP & 16) ? 2 : 1) rowconv_fwd_kernel
         // the speculative epilogue, while the barrier completes (the guess cannot be below this
         // workgroup's own bit width, so such a guess is not tried)
         const bool spec = guess >= 0 && guess >= bitwidth_rc(max(max(red[0], red[1]), max(red[2], red[3])));
-        if (spec && U.valid && owner) rowconv_epilogue<W, R, DG>(a, U, lane, acc, g_guess, ein, tile);
+        if (spec && U.valid && owner) unit_epilogue<W, R, DG>(a, U, lane, acc, g_guess, ein, tile);
         if (a.sgd_tiles > 0) sgd_side(a, sgd_T);  // every wave, before wave 0 waits
         if (wid == 0) {
             const int gbw = grid_bw_wait(a.bar, a.epoch, a.err, a.spin_limit, a.expect_extra, lane);
@@ -907,7 +1097,7 @@ __global__ void __launch_bounds__(256, (RC_EXP & 16) ? 2 : 1) rowconv_fwd_kernel
         }
         __syncthreads();
         RC_STAMP(4);
-        if (U.valid && owner && (!spec || gm != g_guess)) rowconv_epilogue<W, R, DG>(a, U, lane, acc, gm, ein, tile);
+        if (U.valid && owner && (!spec || gm != g_guess)) unit_epilogue<W, R, DG>(a, U, lane, acc, gm, ein, tile);
         RC_STAMP(5);
     } else if constexpr (MODE == RC_RANGE) {
         uint32_t m = 0;
@@ -916,8 +1106,7 @@ __global__ void __launch_bounds__(256, (RC_EXP & 16) ? 2 : 1) rowconv_fwd_kernel
             const RowUnit<W, R> U(a, wg, wid, c, KS > 0);
             compute_unit<W, R, UNC, KS>(a, U, lane, wid, smem, acc);
             if (owner) {
-#pragma unroll
-                for (int r = 0; r < R; ++r) m = max_abs16(acc[r], m);
+                m = unit_max<W, R>(U, acc, m);
                 if (a.acc_store != nullptr) acc_put<R>(a, wg, wid, lane, acc);
             }
         }
@@ -940,11 +1129,11 @@ __global__ void __launch_bounds__(256, (RC_EXP & 16) ? 2 : 1) rowconv_fwd_kernel
             EpiIn<DG ? R : 1> ein = {};
             if constexpr (DG) {
                 if (owner) {
-                    epi_prefetch<W, R>(a, U, lane, ein);
+                    unit_prefetch<W, R>(a, U, lane, ein);
                     epi_masks<R>(a, ein);
                 }
             }
-            if (U.valid && owner) rowconv_epilogue<W, R, DG>(a, U, lane, acc, g, ein, smem + wid * RC_P16_WAVE_BYTES);
+            if (U.valid && owner) unit_epilogue<W, R, DG>(a, U, lane, acc, g, ein, smem + wid * RC_P16_WAVE_BYTES);
             if (DG && a.p16 != nullptr) __syncthreads();  // the P16 tiles sit in the next unit's ring
         }
     }
@@ -1051,10 +1240,37 @@ bool rowconv_ok(const ConvGeom& g) {
     if (g.kh != 3 || g.kw != 3 || g.sh != 1 || g.sw != 1 || g.dh != 1 || g.dw != 1) return false;
     if (g.pt != 1 || g.pl != 1 || g.pb != 1 || g.pr != 1) return false;
     if (g.h != g.w || g.oh != g.h || g.ow != g.w) return false;
-    if (!(g.w == 2 || g.w == 4 || g.w == 8 || g.w == 16)) return false;
+    // W > 0 form: 2 / 4 / 8 / 16 px; the row-segment form (W = 0): 14-px segments of 224 / 112 / 56 /
+    // 28 / 14 px maps
+    const bool seg = g.w > 16 ? g.w % 28 == 0 : g.w == 14;
+    if (!(g.w == 2 || g.w == 4 || g.w == 8 || g.w == 16 || seg)) return false;
     if (g.cop % 32 != 0) return false;
     return true;
 }
+
+static bool rowconv_seg(const ConvGeom& g) { return g.w > 16 || g.w == 14; }
+
+// the row-segment form's launch shape: 4 rows per band (2 at 14 px), units of 28 px (two 14-px
+// segments of one row, or one 14-px row of two images), whole workgroups of 4 units per co block
+struct SegPlan {
+    int R, gw, nsp, nbands, ngb, upc4, wgs;
+};
+static SegPlan seg_plan(const ConvGeom& g) {
+    SegPlan p{};
+    p.R = g.h % 4 == 0 ? 4 : 2;
+    p.gw = g.w == 14 ? 2 : 1;
+    p.nsp = g.w >= 28 ? g.w / 28 : 1;
+    p.nbands = g.h / p.R;
+    p.ngb = ((g.n + p.gw - 1) / p.gw) * p.nbands;
+    p.upc4 = (p.ngb * p.nsp + 3) / 4 * 4;
+    p.wgs = (g.cop / 32) * p.upc4 / 4;
+    return p;
+}
+
+// the row-segment form keeps its int32 accumulators between the range and requantise launches
+// only where the GEMM is deep (K = 9 c_in >= 2304): recomputing 2 M N K ops costs more there than
+// the 8 bytes per output of an int32 round trip; shallower layers recompute (no int32 tensor)
+static bool seg_store_acc(const ConvGeom& g) { return g.c_in >= 256; }
 
 bool rowconv_dgrad_geom(const ConvGeom& l, ConvGeom* d) {
     if (!rowconv_ok(l)) return false;
@@ -1070,6 +1286,11 @@ bool rowconv_dgrad_geom(const ConvGeom& l, ConvGeom* d) {
 // count fills the chip (>= 768 waves), else R = 2, the most units; FUSED needs one unit per wave
 // and every workgroup resident (units <= 1024)
 static int rowconv_rows(const ConvGeom& g, bool dg, int* units_out) {
+    if (rowconv_seg(g)) {
+        const SegPlan p = seg_plan(g);
+        *units_out = p.wgs * 4;
+        return p.R;
+    }
     const int W = g.w, G = 32 / W;
     const int64_t groups = (g.n + G - 1) / G, cob = g.cop / 32;
     // register budget: 8 rows at W = 16 (DPP shifts), else 4; the input-gradient epilogue's
@@ -1087,6 +1308,10 @@ static int rowconv_ks(const ConvGeom& g, bool dg);
 // the accumulator store of modes RANGE + REQUANT: every wave slot of the launch, R x 1 KiB x 4
 size_t rowconv_acc_bytes(const ConvGeom& g, bool dg) {
     if (!rowconv_ok(g)) return 0;
+    if (rowconv_seg(g)) {
+        const SegPlan p = seg_plan(g);
+        return seg_store_acc(g) ? (size_t)p.wgs * 4 * p.R * 1024 * sizeof(int32_t) : 0;
+    }
     int u = 0;
     const int R = rowconv_rows(g, dg, &u);
     const int G = 32 / g.w, ngb = ((g.n + G - 1) / G) * (g.h / R), ngb4 = (ngb + 3) / 4 * 4, COB = g.cop / 32;
@@ -1095,7 +1320,7 @@ size_t rowconv_acc_bytes(const ConvGeom& g, bool dg) {
 }
 
 bool rowconv_p16_ok(const ConvGeom& d, bool pool) {
-    if (!rowconv_ok(d)) return false;
+    if (!rowconv_ok(d) || rowconv_seg(d)) return false;
     int u = 0;
     const int R = rowconv_rows(d, true, &u), W = d.w;
     const int64_t px = (int64_t)d.n * d.h * d.w * (pool ? 4 : 1);
@@ -1115,6 +1340,7 @@ static int rowconv_ks(const ConvGeom& g, bool dg) {
 
 // waves of the launch (K-split: four per unit)
 int rowconv_units(const ConvGeom& g, bool dg) {
+    if (rowconv_seg(g)) return seg_plan(g).wgs * 4;
     int u = 0;
     (void)rowconv_rows(g, dg, &u);
     if (rowconv_ks(g, dg) > 0) {
@@ -1133,10 +1359,10 @@ static const void* rc_kernel(int W, int R, bool unc, int ks) {
         if (ks == 1) return reinterpret_cast<const void*>(&rowconv_fwd_kernel<2, 2, MODE, DG, false, 1>);
         return nullptr;
     }
-#define RC_CASE(WW, RR)                                                                                 \
-    if (W == WW && R == RR)                                                                             \
-        return (WW > 1 && unc) ? reinterpret_cast<const void*>(&rowconv_fwd_kernel<WW, RR, MODE, DG, true, 0>) \
-                               : reinterpret_cast<const void*>(&rowconv_fwd_kernel<WW, RR, MODE, DG, false, 0>);
+#define RC_CASE(WW, RR)                                                                                  \
+    if (W == WW && R == RR)                                                                              \
+        return (WW != 1 && unc) ? reinterpret_cast<const void*>(&rowconv_fwd_kernel<WW, RR, MODE, DG, true, 0>) \
+                                : reinterpret_cast<const void*>(&rowconv_fwd_kernel<WW, RR, MODE, DG, false, 0>);
     if constexpr (!DG) RC_CASE(16, 8)
     RC_CASE(16, 4)
     RC_CASE(16, 2)
@@ -1146,13 +1372,15 @@ static const void* rc_kernel(int W, int R, bool unc, int ks) {
     RC_CASE(4, 2)
     RC_CASE(2, 2)
     RC_CASE(1, 1)
+    RC_CASE(0, 4)  // the row-segment form
+    RC_CASE(0, 2)
 #undef RC_CASE
     return nullptr;
 }
 
 template <int MODE, bool DG>
 static hipError_t launch_rc(int W, int R, int grid, RowConvArgs a, hipStream_t st, int ks = 0) {
-    const void* f = rc_kernel<MODE, DG>(W, R, W > 1 && a.CB % 4 == 0, ks);
+    const void* f = rc_kernel<MODE, DG>(W, R, W != 1 && a.CB % 4 == 0, ks);
     if (f == nullptr) return hipErrorInvalidValue;
     void* args[] = {&a};
     return hipLaunchKernel(f, dim3((unsigned)grid), dim3(256), args, 0, st);
@@ -1185,6 +1413,12 @@ static int resident_wgs(const void* f) {
 
 // workgroups of a launch (K-split: one unit each; else four units)
 static int rowconv_wgs(const ConvGeom& g, bool dg, int* R_out, int* ks_out) {
+    if (rowconv_seg(g)) {
+        const SegPlan p = seg_plan(g);
+        *R_out = p.R;
+        *ks_out = 0;
+        return p.wgs;
+    }
     int u = 0;
     const int R = rowconv_rows(g, dg, &u);
     const int ks = rowconv_ks(g, dg);
@@ -1200,7 +1434,8 @@ bool rowconv_fused_ok(const ConvGeom& g, bool dg) {
     int R = 0, ks = 0;
     const int wgs = rowconv_wgs(g, dg, &R, &ks);
     const bool unc = (g.c_in + 31) / 32 % 4 == 0;
-    const void* f = dg ? rc_kernel<RC_FUSED, true>(g.w, R, unc, ks) : rc_kernel<RC_FUSED, false>(g.w, R, unc, ks);
+    const int W = rowconv_seg(g) ? 0 : g.w;
+    const void* f = dg ? rc_kernel<RC_FUSED, true>(W, R, unc, ks) : rc_kernel<RC_FUSED, false>(W, R, unc, ks);
     return wgs <= resident_wgs(f);
 }
 
@@ -1249,12 +1484,26 @@ hipError_t rowconv_fwd(const ConvGeom& g, const int8_t* x_c32, const int8_t* wf,
     const bool dg = o.relu_mask != nullptr || o.pool_dx != nullptr || o.p16 != nullptr;
     int units = 0;
     const int R = rowconv_rows(g, dg, &units);
-    const int G = 32 / g.w;
-    a.nbands = g.h / R;
-    a.ngb = ((g.n + G - 1) / G) * a.nbands;
-    a.ngb4 = (a.ngb + 3) / 4 * 4;
-    const int ks = rowconv_ks(g, dg);
-    a.wgs = ks > 0 ? COB * a.ngb : COB * a.ngb4 / 4;
+    const bool seg = rowconv_seg(g);
+    const int Wk = seg ? 0 : g.w;  // the kernel's W (0: the row-segment form)
+    int ks = 0;
+    if (seg) {
+        const SegPlan p = seg_plan(g);
+        a.hw = g.w;
+        a.gw = p.gw;
+        a.nsp = p.nsp;
+        a.nbands = p.nbands;
+        a.ngb = p.ngb;
+        a.upc4 = p.upc4;
+        a.wgs = p.wgs;
+    } else {
+        const int G = 32 / g.w;
+        a.nbands = g.h / R;
+        a.ngb = ((g.n + G - 1) / G) * a.nbands;
+        a.ngb4 = (a.ngb + 3) / 4 * 4;
+        ks = rowconv_ks(g, dg);
+        a.wgs = ks > 0 ? COB * a.ngb : COB * a.ngb4 / 4;
+    }
     a.wmajor = rowconv_wmajor(xb, wb);
     a.out = o.out;
     a.cop = g.cop;
@@ -1290,12 +1539,12 @@ hipError_t rowconv_fwd(const ConvGeom& g, const int8_t* x_c32, const int8_t* wf,
     if (o.pool_out != nullptr && (R % 2 != 0 || g.h % 2 != 0)) return hipErrorInvalidValue;
     if (mode == RC_FUSED) {
         if (bar == nullptr || err == nullptr || epoch == 0 || !rowconv_fused_ok(g, dg)) return hipErrorInvalidValue;
-        return dg ? launch_rc<RC_FUSED, true>(g.w, R, a.wgs, a, st, ks) : launch_rc<RC_FUSED, false>(g.w, R, a.wgs, a, st, ks);
+        return dg ? launch_rc<RC_FUSED, true>(Wk, R, a.wgs, a, st, ks) : launch_rc<RC_FUSED, false>(Wk, R, a.wgs, a, st, ks);
     }
     int grid = a.wgs;
     grid = grid > 1024 ? 1024 : grid;
-    if (mode == RC_RANGE) return launch_rc<RC_RANGE, false>(g.w, R, grid, a, st, ks);
-    return dg ? launch_rc<RC_REQUANT, true>(g.w, R, grid, a, st, ks) : launch_rc<RC_REQUANT, false>(g.w, R, grid, a, st, ks);
+    if (mode == RC_RANGE) return launch_rc<RC_RANGE, false>(Wk, R, grid, a, st, ks);
+    return dg ? launch_rc<RC_REQUANT, true>(Wk, R, grid, a, st, ks) : launch_rc<RC_REQUANT, false>(Wk, R, grid, a, st, ks);
 }
 
 // ---- the classifier head's weight gradient ------------------------------------------------------

@@ -88,7 +88,7 @@ def test_rows_fwd_vgg11_conv4_shape(T):
     _case(T, 32, 256, 8, 256, True, True, 0, seed=4)
 
 
-def _dgrad_case(T, n, ci, h, co, pool, relu, mode, seed, wmax=127, dmax=127):
+def _dgrad_case(T, n, ci, h, co, pool, relu, mode, seed, wmax=127, dmax=127, p16=True):
     """The layer (ci -> co at h x h) input gradient on the row kernel against NITI's dgrad
     (NITI_DeConv_Int8.cpp:294-329 requantised by the forward rule) followed by the previous
     layer's relu gradient (NITI_ReluGrad_Int8) or its 2x2 max-pool + relu gradient
@@ -118,7 +118,7 @@ def _dgrad_case(T, n, ci, h, co, pool, relu, mode, seed, wmax=127, dmax=127):
     wft = ops.weights_to_wf(ops.oihw_to_ohwi16(dev(w)), ci, transpose=True)
     amax = ops.new_range()
     st = ops.RowConvState()
-    kw = dict(dx_c32=True, dx_p16=True)
+    kw = dict(dx_c32=True, dx_p16=p16)
     if pool:
         kw.update(pool_x=nhwc(px), pool_y=nhwc(py), pool_relu=relu)
     elif relu:
@@ -190,3 +190,43 @@ def test_rows_ks_vgg11_2x2_b256(T):
     conv7's relu."""
     _case(T, 256, 512, 2, 512, True, True, 0, seed=31)
     _dgrad_case(T, 256, 512, 2, 512, False, True, 0, seed=32)
+
+
+# ---- the row-segment form (W = 0): maps of 14 / 28 / 56 / 112 / 224 px as 14-px segments with halo
+# lanes (one 14-px row of two images at 14 px) -- VGG-16's and ResNet-18's stride-1 3x3 layers
+
+
+@pytest.mark.parametrize("h", [14, 28, 56])
+@pytest.mark.parametrize("mode", [0, 2])
+def test_rows_seg_fwd(T, h, mode):
+    """Forward with the rescale (fused launch, or range then recompute-and-requantise), relu, the
+    2x2 pool (pairs inside a segment) and the C32 copy, ragged image pairs at 14 px."""
+    for k, (n, ci, co, relu, pool) in enumerate([(2, 32, 32, True, True), (3, 64, 96, False, False),
+                                                  (1, 96, 64, True, True)]):
+        _case(T, n, ci, h, co, relu, pool, mode, seed=2000 + 100 * h + 10 * mode + k)
+
+
+@pytest.mark.parametrize("h", [112, 224])
+def test_rows_seg_fwd_large(T, h):
+    _case(T, 1, 32, h, 32, True, True, 2, seed=3000 + h)
+    _case(T, 2, 64, h, 32, False, False, 0, seed=3001 + h)
+
+
+@pytest.mark.parametrize("h", [14, 28, 56])
+@pytest.mark.parametrize("mode", [0, 2])
+def test_rows_seg_dgrad(T, h, mode):
+    """Input gradient on the row-segment form with the previous layer's relu gradient or its 2x2
+    max-pool (+ relu) gradient routed into the full-resolution map, NHWC16 and C32 outputs."""
+    for k, (n, ci, co, pool, relu) in enumerate([(2, 32, 32, True, True), (3, 64, 96, False, True),
+                                                  (1, 96, 64, True, False), (2, 32, 64, False, False)]):
+        _dgrad_case(T, n, ci, h, co, pool, relu, mode, seed=4000 + 100 * h + 10 * mode + k, p16=False)
+
+
+def test_rows_seg_shift_branches(T):
+    seen = set()
+    for seed, (wmax, xmax) in enumerate([(1, 1), (1, 2), (1, 3), (2, 3), (3, 4), (127, 127)]):
+        for mode in (0, 2):
+            m = _case(T, 2, 32, 28, 32, False, False, mode, seed=5000 + seed, wmax=wmax, xmax=xmax)
+            bw = 0 if m <= 1 else int(np.ceil(np.log2(m)))
+            seen.add("raw" if bw <= 7 else "one" if bw == 8 else "psto")
+    assert seen == {"raw", "one", "psto"}
