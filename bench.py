@@ -207,29 +207,43 @@ def bench_resnet18(args):
     if rank != 0:
         comm.dist.destroy_process_group()
         return
-    # roofline: the first 56x56 stage conv's forward GEMM (layer1.0.a, 64 -> 64, 3x3) re-run alone
-    # after the timed region, HIP events on the launch stream around 20 back-to-back launches
+    # roofline: the first 56x56 stage conv's forward (layer1.0.a, 64 -> 64, 3x3) re-run alone after the
+    # timed region, HIP events on the launch stream around 20 back-to-back launches: the row-segment
+    # kernel's requantise launch (the GEMM recomputed with the range given, relu, int8 out) as the step
+    # runs it, or the implicit GEMM where the layer is not on the row kernel
     c = m.convs[1]
     g = ops.geom(batch, c["ci"], c["h"], c["h"], c["co"], c["k"], stride=c["stride"], pad=c["pad"])
     xr = ops.nchw_to_nhwc16(torch.from_numpy(rng.integers(-127, 128, (batch, c["ci"], c["h"], c["h"])).astype(np.int8)).cuda())
     wr = ops.oihw_to_ohwi16(torch.from_numpy(rng.integers(-127, 128, (c["co"], c["ci"], c["k"], c["k"])).astype(np.int8)).cuda())
     amax = ops.new_range()
-    ops.conv_fwd_acc(g, xr, wr, amax)
+    rows = m.use_rows and m.rows[1]
+    if rows:
+        xc = ops.nhwc16_to_c32(xr, c["ci"])
+        wf = ops.weights_to_wf(wr, c["ci"])
+        ops.conv_fwd_rows(g, xc, wf, amax, mode=1, relu=True)
+        launch = lambda: ops.conv_fwd_rows(g, xc, wf, amax, mode=2, relu=True)  # noqa: E731
+        kname = (f"ResNet-18 {c['name']} forward, row-segment register-fed kernel, requantise launch (GEMM "
+                 "recomputed with the range given, relu, int8 out; re-run alone after the timed region)")
+    else:
+        launch = lambda: ops.conv_fwd_acc(g, xr, wr, amax)  # noqa: E731
+        kname = (f"ResNet-18 {c['name']} forward GEMM (gemm_kernel, implicit im2col, int32 accumulate + range; "
+                 "re-run alone after the timed region)")
+    launch()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     reps = 20
     e0.record()
     for _ in range(reps):
-        ops.conv_fwd_acc(g, xr, wr, amax)
+        launch()
     e1.record()
     torch.cuda.synchronize()
     k_us = e0.elapsed_time(e1) * 1e3 / reps
     k_ops = 2 * batch * g.oh * g.ow * c["co"] * c["ci"] * c["k"] * c["k"]
-    roof = {"kernel": f"ResNet-18 {c['name']} forward GEMM (gemm_kernel, implicit im2col, int32 accumulate + range; "
-                      "re-run alone after the timed region)",
-            "bound": bound,
-            "hbm_frac": round(hbm_frac, 4) if hbm_frac is not None else None,
-            "hbm_bytes_basis": "pmc traffic" if traffic else "algorithmic", "achieved": round(k_ops / k_us / 1e6, 2), "peak": round(PEAK_INT8_TOPS, 1),
-            "unit": "TFLOP/s", "frac": round(k_ops / k_us / 1e6 / PEAK_INT8_TOPS, 4), "traffic": None,
+    alg_bytes = batch * (c["h"] * c["h"] * c["ci"] + g.oh * g.ow * c["co"]) + c["co"] * c["ci"] * c["k"] * c["k"]
+    mfma_frac = k_ops / k_us / 1e6 / PEAK_INT8_TOPS
+    hbm_frac = alg_bytes / (k_us * 1e-6) / (PEAK_HBM_GBS * 1e9)
+    roof = {"kernel": kname, "bound": "hbm" if hbm_frac > mfma_frac else "mfma", "hbm_frac": round(hbm_frac, 4),
+            "hbm_bytes_basis": "algorithmic", "achieved": round(k_ops / k_us / 1e6, 2), "peak": round(PEAK_INT8_TOPS, 1),
+            "unit": "TFLOP/s", "frac": round(mfma_frac, 4), "traffic": None,
             "avg_launch_us": round(k_us, 2), "timing": "HIP events around 20 back-to-back launches on one stream",
             "ops_per_launch": k_ops}
     cpu = None

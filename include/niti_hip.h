@@ -265,12 +265,14 @@ int niti_conv_fwd_rows(const niti_geom* g, const int8_t* x_c32, const int8_t* wf
  * pool_y [n][H][W][cip] its output; pool_relu: zero where pool_x <= 0) into dx_nhwc16 at 2H x 2W.
  * dx_c32 (may be NULL) is the same gradient in C32 (the previous layer's dy_c32), dx_p16 (may be NULL)
  * in the weight gradient's P16 layout [pixels/16][cip][16] (NITI_NOT_SUPPORT where a launch's pixels
- * do not make whole 16-pixel blocks: 4x4 images without the pool at small batches).  mode, amax,
+ * do not make whole 16-pixel blocks: 4x4 images without the pool at small batches).  exp_out (may be
+ * NULL) = exp_in + wscale + the rule's increment, as the forward (NITI_DeConv_Int8 has no exponent
+ * output; callers that track gradient exponents, e.g. a residual network, read it here).  mode, amax,
  * state, epoch and err as niti_conv_fwd_rows. */
 int niti_conv_dgrad_rows(const niti_geom* g, const int8_t* dy_c32, const int8_t* wft, const int8_t* relu_mask,
                          const int8_t* pool_x, const int8_t* pool_y, int pool_relu, int8_t* dx_nhwc16, int8_t* dx_c32,
-                         int8_t* dx_p16, int mode, uint32_t* amax, uint32_t* state, uint32_t epoch, uint32_t* err,
-                         void* stream);
+                         int8_t* dx_p16, const int8_t* exp_in, const int8_t* wscale, int8_t* exp_out, int mode,
+                         uint32_t* amax, uint32_t* state, uint32_t epoch, uint32_t* err, void* stream);
 /* acc[co][kh][kw][cip] int32 = weight gradient for x (NHWC16) and dy (NHWC16): a K-major GEMM
  * over the pixels whose operand tiles are transposed in LDS (ds_read_b64_tr_b8) */
 int niti_conv_wgrad_acc(const niti_geom* g, const int8_t* x_nhwc16, const int8_t* dy_nhwc16, int32_t* acc,

@@ -317,8 +317,8 @@ int niti_conv_fwd_rows(const niti_geom* g, const int8_t* x_c32, const int8_t* wf
 
 int niti_conv_dgrad_rows(const niti_geom* g, const int8_t* dy_c32, const int8_t* wft, const int8_t* relu_mask,
                          const int8_t* pool_x, const int8_t* pool_y, int pool_relu, int8_t* dx, int8_t* dx_c32,
-                         int8_t* dx_p16, int mode, uint32_t* amax, uint32_t* state, uint32_t epoch, uint32_t* err,
-                         void* stream) {
+                         int8_t* dx_p16, const int8_t* exp_in, const int8_t* wscale, int8_t* exp_out, int mode,
+                         uint32_t* amax, uint32_t* state, uint32_t epoch, uint32_t* err, void* stream) {
     if (!g || !dy_c32 || !wft || !amax || mode < 0 || mode > 2) return NITI_INVALID_VALUE;
     if ((pool_x == nullptr) != (pool_y == nullptr) || (pool_x && relu_mask)) return NITI_INVALID_VALUE;
     if (mode != 1 && dx == nullptr) return NITI_INVALID_VALUE;
@@ -329,6 +329,9 @@ int niti_conv_dgrad_rows(const niti_geom* g, const int8_t* dy_c32, const int8_t*
     if (dx_p16 != nullptr && !niti::rowconv_p16_ok(d, pool_x != nullptr)) return NITI_NOT_SUPPORT;
     niti::RowConvOut o;
     o.p16 = dx_p16;
+    o.exp_in = exp_in;
+    o.wscale = wscale;
+    o.exp_out = exp_out;
     if (pool_x != nullptr) {
         o.pool_x = pool_x;
         o.pool_y = pool_y;

@@ -122,8 +122,7 @@ def lib():
         "niti_weights_to_wf": (ci, [vp, ci, ci, ci, ci, vp, vp]),
         "niti_conv_fwd_rows": (ci, [C.POINTER(Geom), vp, vp, vp, vp, vp, ci, vp, vp, vp, ci, vp, vp, C.c_uint32, vp,
                                     vp]),
-        "niti_conv_dgrad_rows": (ci, [C.POINTER(Geom), vp, vp, vp, vp, vp, ci, vp, vp, vp, ci, vp, vp, C.c_uint32, vp,
-                                      vp]),
+        "niti_conv_dgrad_rows": (ci, [C.POINTER(Geom), vp, vp, vp, vp, vp, ci, vp, vp, vp, vp, vp, vp, ci, vp, vp, C.c_uint32, vp, vp]),
         "niti_conv_fwd_phase2": (ci, [C.POINTER(Geom), vp, vp, vp, vp, vp, vp, vp, ci, vp, vp, C.c_size_t, vp]),
         "niti_conv_dgrad_phase1": (ci, [C.POINTER(Geom), vp, vp, vp, vp, vp, C.c_size_t, vp]),
         "niti_conv_dgrad_phase2": (ci, [C.POINTER(Geom), vp, vp, vp, vp, vp, vp, vp, ci, vp, vp, C.c_size_t, vp]),

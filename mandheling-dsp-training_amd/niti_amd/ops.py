@@ -205,20 +205,23 @@ def conv_rows_ok(g: L.Geom) -> bool:
     return bool(L.lib().niti_conv_rows_ok(C.byref(g)))
 
 
-def nhwc16_to_c32(x16: torch.Tensor, c: int, stream=None):
+def nhwc16_to_c32(x16: torch.Tensor, c: int, stream=None, out=None):
     """NHWC16 [n][h][w][cp] -> C32 [n][ceil(c/32)][h][w][32] (the register-fed conv's activations)."""
     n, h, w, cp = x16.shape
     cb = (c + 31) // 32
-    out = torch.empty((n, cb, h, w, 32), dtype=torch.int8, device=x16.device)
+    if out is None:
+        out = torch.empty((n, cb, h, w, 32), dtype=torch.int8, device=x16.device)
     check(L.lib().niti_nhwc16_to_c32(_ptr(x16), n, h * w, cp, c, _ptr(out), _stream(stream)), "nhwc16->c32")
     return out
 
 
-def weights_to_wf(w16: torch.Tensor, ci: int, transpose=False, stream=None):
-    """OHWI16 [co][kh][kw][cip] (3x3) -> WF fragment-major weights (transpose: the input gradient's)."""
+def weights_to_wf(w16: torch.Tensor, ci: int, transpose=False, stream=None, out=None):
+    """OHWI16 [co][kh][kw][cip] (3x3) -> WF fragment-major weights (transpose: the input gradient's);
+    out: a persistent buffer to rewrite in place."""
     co, cip = w16.shape[0], w16.shape[-1]
     ob, ib = ((ci if transpose else co) + 31) // 32, ((co if transpose else ci) + 31) // 32
-    out = torch.empty(ob * ib * 9 * 1024, dtype=torch.int8, device=w16.device)
+    if out is None:
+        out = torch.empty(ob * ib * 9 * 1024, dtype=torch.int8, device=w16.device)
     check(L.lib().niti_weights_to_wf(_ptr(w16), co, ci, cip, int(transpose), _ptr(out), _stream(stream)), "wf")
     return out
 
@@ -255,7 +258,8 @@ def conv_fwd_rows(g: L.Geom, xc32, wf, amax, mode=0, state: RowConvState | None 
 
 
 def conv_dgrad_rows(g: L.Geom, dyc32, wft, amax, mode=0, state: RowConvState | None = None, relu_mask=None,
-                    pool_x=None, pool_y=None, pool_relu=False, dx_c32=False, dx_p16=False, stream=None):
+                    pool_x=None, pool_y=None, pool_relu=False, dx_c32=False, dx_p16=False, exp_in=None, wscale=None,
+                    exp_out=None, stream=None):
     """The input gradient on the register-fed kernel (niti_conv_dgrad_rows) for the layer of
     geometry g: (dx NHWC16, dx C32 or None, dx P16 or None).  dx is [n][h][w][cip], or
     [n][2h][2w][cip] routed through the previous layer's 2x2 max pool when pool_x / pool_y are
@@ -271,7 +275,8 @@ def conv_dgrad_rows(g: L.Geom, dyc32, wft, amax, mode=0, state: RowConvState | N
         state.epoch += 1
         epoch, st_ptr, err_ptr = state.epoch, _ptr(state.state), _ptr(state.err)
     check(L.lib().niti_conv_dgrad_rows(C.byref(g), _ptr(dyc32), _ptr(wft), _ptr(relu_mask), _ptr(pool_x),
-                                       _ptr(pool_y), 1 if pool_relu else 0, _ptr(dx), _ptr(nxt), _ptr(p16), mode,
+                                       _ptr(pool_y), 1 if pool_relu else 0, _ptr(dx), _ptr(nxt), _ptr(p16),
+                                       _ptr(exp_in), _ptr(wscale), _ptr(exp_out), mode,
                                        _ptr(amax), st_ptr, epoch, err_ptr, _stream(stream)), "conv_dgrad_rows")
     return dx, nxt, p16
 

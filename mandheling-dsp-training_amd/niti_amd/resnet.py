@@ -18,6 +18,7 @@ import numpy as np
 import torch
 
 from . import ops
+from ._lib import NitiError
 
 
 def resnet18_convs(hw=224, classes=1000):
@@ -67,6 +68,15 @@ class ResNet18:
         self.wT = [None] * len(self.convs)
         self.wscale = [None] * len(self.convs)
         self.ws_dev = [None] * len(self.convs)
+        # stride-1 3x3 layers over 56 / 28 / 14-px maps run on the register-fed row-segment kernels
+        # (csrc/niti_rowconv.hip: range + requantise launches, or one fused launch where the grid is
+        # resident; no int32 tensor where the GEMM is shallow), their fragment-major weight copies
+        # rewritten after every update; use_rows = False keeps every conv on the GEMM path
+        self.rows = [ops.conv_rows_ok(g) for g in self.geoms]
+        self.use_rows = True
+        self.wf = [None] * len(self.convs)
+        self.wft = [None] * len(self.convs)
+        self.rstate = [ops.RowConvState(device) if r else None for r in self.rows]
         self.record = False
         self.rec = {}
         # range buffers and exponent scalars of one step, allocated once and handed out in order
@@ -108,11 +118,33 @@ class ResNet18:
         else:  # in place: a captured step holds these addresses
             self.w16[i].copy_(w16)
             self.wT[i].copy_(wT)
+        self._refresh_wf(i)
         self.wscale[i] = int(wscale)
         if self.ws_dev[i] is None:
             self.ws_dev[i] = torch.tensor([wscale], dtype=torch.int8, device=self.dev)
         else:
             self.ws_dev[i].fill_(int(wscale))
+
+    def _refresh_wf(self, i):
+        if self.rows[i]:
+            ci = self.convs[i]["ci"]
+            self.wf[i] = ops.weights_to_wf(self.w16[i], ci, out=self.wf[i])
+            self.wft[i] = ops.weights_to_wf(self.w16[i], ci, transpose=True, out=self.wft[i])
+
+    def _rows(self, fwd, i, xc, amax, **kw):
+        """One row-kernel conv: the fused launch where it is possible (one device, not capturing, the
+        grid resident), else range, [global MAX], recompute-or-stored requantise."""
+        f = ops.conv_fwd_rows if fwd else ops.conv_dgrad_rows
+        g, wf = self.geoms[i], self.wf[i] if fwd else self.wft[i]
+        if self.comm is None and not torch.cuda.is_current_stream_capturing():
+            try:
+                return f(g, xc, wf, amax, mode=0, state=self.rstate[i], **kw)[0]
+            except NitiError as e:
+                if e.code != 2:  # NOT_SUPPORT: the grid is not resident
+                    raise
+        f(g, xc, wf, amax, mode=1, **kw)
+        self._global_range(amax)
+        return f(g, xc, wf, amax, mode=2, **kw)[0]
 
     def get_weight(self, i) -> np.ndarray:
         return ops.ohwi16_to_oihw(self.w16[i], self.convs[i]["ci"]).cpu().numpy()
@@ -128,24 +160,39 @@ class ResNet18:
     def _fwd(self, i, x16, e_in, relu):
         l, g = self.convs[i], self.geoms[i]
         amax = self._range()
-        acc = ops.conv_fwd_acc(g, x16, self.w16[i], amax)
-        self._global_range(amax)
-        e_out = self._exp()
-        y = ops.requant_act(acc, amax, exp_in=e_in, wscale=self.ws_dev[i], exp_out=e_out, relu=relu)
+        if self.use_rows and self.rows[i]:
+            xc = ops.nhwc16_to_c32(x16.view(self.batch, l["h"], l["h"], -1), l["ci"])
+            e_out = self._exp()
+            y = self._rows(True, i, xc, amax, exp_in=e_in, wscale=self.ws_dev[i], exp_out=e_out, relu=relu)
+        else:
+            acc = ops.conv_fwd_acc(g, x16, self.w16[i], amax)
+            self._global_range(amax)
+            e_out = self._exp()
+            y = ops.requant_act(acc, amax, exp_in=e_in, wscale=self.ws_dev[i], exp_out=e_out, relu=relu)
         y = y.view(self.batch, l["oh"], l["oh"], -1)
         if self.record:
             self.rec.setdefault("fwd", {})[i] = (y, relu)
             self.rec.setdefault("in", {})[i] = x16
         return y, e_out
 
-    def _dgrad(self, i, dy16, e_dy):
+    def _dgrad(self, i, dy16, e_dy, relu_mask=None):
+        """The input gradient (exponent e_dy + wscale + inc), then the previous op's relu gradient
+        where relu_mask (its output) is given -- fused into the row kernel's epilogue there."""
         l, g = self.convs[i], self.geoms[i]
         amax = self._range()
+        e_dx = self._exp()
+        if self.use_rows and self.rows[i]:
+            dyc = ops.nhwc16_to_c32(dy16.view(self.batch, l["oh"], l["oh"], -1), l["co"])
+            m = None if relu_mask is None else relu_mask.view(self.batch, l["h"], l["h"], -1)
+            dx = self._rows(False, i, dyc, amax, relu_mask=m, exp_in=e_dy, wscale=self.ws_dev[i], exp_out=e_dx)
+            return dx.view(self.batch, l["h"], l["h"], -1), e_dx
         acc = ops.conv_dgrad_acc(g, dy16, self.wT[i], amax)
         self._global_range(amax)
-        e_dx = self._exp()
         dx = ops.requant_act(acc, amax, exp_in=e_dy, wscale=self.ws_dev[i], exp_out=e_dx)
-        return dx.view(self.batch, l["h"], l["h"], -1), e_dx
+        dx = dx.view(self.batch, l["h"], l["h"], -1)
+        if relu_mask is not None:
+            dx = ops.relu_grad(relu_mask, dx)
+        return dx, e_dx
 
     def _wgrad_update(self, i, x16, dy16):
         amax = self._range()
@@ -157,6 +204,7 @@ class ResNet18:
         # the transposed copy is rewritten in place (its input gradient above read it first), so a
         # captured step keeps reading the same buffer
         _, g8 = ops.sgd_update(acc, amax, self.w16[i], self.convs[i]["ci"], rule=2, wT=self.wT[i])
+        self._refresh_wf(i)
         if self.record:
             self.rec.setdefault("dy", {})[i] = dy16
             self.rec.setdefault("dw", {})[i] = g8
@@ -229,9 +277,8 @@ class ResNet18:
             ia, ib, ip = self.blocks[k]
             h, out = saved[k]
             dz = ops.relu_grad(out, du)
-            dh, edh = self._dgrad(ib, dz, edu)
+            dh, edh = self._dgrad(ib, dz, edu, relu_mask=h)  # conv a's relu gradient rides along
             self._wgrad_update(ib, h, dz)
-            dh = ops.relu_grad(h, dh)
             dua, edua = self._dgrad(ia, dh, edh)
             self._wgrad_update(ia, saved_in[ia], dh)
             if ip is not None:
