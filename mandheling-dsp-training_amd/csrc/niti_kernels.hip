@@ -2754,6 +2754,7 @@ struct Conv0 {
     int8_t* out;      // NHWC16 [P][cop]
     int8_t* pool_out; // [P / 4][cop] or null
     int8_t* pool_c32; // the pooled output as the next layer's C32 input [n][cop/32][oh/2][ow/2][32], or null
+    int8_t* out_c32;  // the (unpooled) output as the next layer's C32 input [n][cop/32][oh][ow][32], or null
     const int8_t *exp_in, *wscale;
     int8_t* exp_out;
     int relu;
@@ -2832,6 +2833,9 @@ __global__ void __launch_bounds__(256) conv0_kernel(Conv0 g) {
                 for (int r = 0; r < 2; ++r) {
                     const v4i v = pack(q[r]);
                     *(v4i*)(g.out + (p0 + (int64_t)r * g.ow + c) * g.cop + t * 32 + 16 * h) = v;
+                    if (g.out_c32 != nullptr)
+                        *(v4i*)(g.out_c32 + (((img * tiles + t) * g.oh + 2 * pr + r) * (int64_t)g.ow + seg * 32 + c) * 32 +
+                                16 * h) = v;
                 }
                 if (g.pool_out != nullptr) {
                     // vertical max in the lane, horizontal with the neighbour pixel (lane c ^ 1);
@@ -2871,7 +2875,7 @@ bool conv0_ok(const ConvGeom& g) {
 }
 
 hipError_t conv0_fwd(const ConvGeom& g, const int8_t* xcol, const int8_t* w, uint32_t* amax, const ActOut& o,
-                     int pass, hipStream_t st, int8_t* pool_c32) {
+                     int pass, hipStream_t st, int8_t* pool_c32, int8_t* out_c32) {
     if (!conv0_ok(g) || o.out == nullptr || o.relu_mask != nullptr) return hipErrorInvalidValue;
     if (pool_c32 != nullptr && o.pool.pool_out == nullptr) return hipErrorInvalidValue;
     Conv0 k{};
@@ -2887,6 +2891,7 @@ hipError_t conv0_fwd(const ConvGeom& g, const int8_t* xcol, const int8_t* w, uin
     k.out = o.out;
     k.pool_out = o.pool.pool_out;
     k.pool_c32 = pool_c32;
+    k.out_c32 = out_c32;
     k.exp_in = o.exp_in;
     k.wscale = o.wscale;
     k.exp_out = o.exp_out;

@@ -188,7 +188,7 @@ bool conv0_ok(const ConvGeom& g);
 // pass 0: range into amax; pass 1: requantise with it (a MAX all-reduce may sit between them)
 hipError_t conv0_fwd(const ConvGeom& g, const int8_t* xcol, const int8_t* w, uint32_t* amax, const ActOut& o,
                      int pass, hipStream_t st,
-                     int8_t* pool_c32 = nullptr);
+                     int8_t* pool_c32 = nullptr, int8_t* out_c32 = nullptr);
 bool conv_dgrad_phase2_separate(const ConvGeom& g, size_t ws_bytes);
 hipError_t conv_fwd_phase1(const ConvGeom& g, const int8_t* x, const int8_t* w, int32_t* acc, uint32_t* amax,
                            void* ws, size_t ws_bytes, hipStream_t st);

@@ -923,12 +923,13 @@ int Model::fwd_layer(int i, hipStream_t st) {
         o.wscale = l.ws_dev;
         o.exp_out = l.exp;
         o.pool.pool_out = l.pool ? l.p : nullptr;
-        // the pooled output also as the next layer's C32 input when it runs on the row kernel
-        const bool next_c32 = l.pool && i + 1 < (int)L.size() && rowconv_layer(i + 1);
+        // the (pooled) output also as the next layer's C32 input when it runs on the row kernel
+        const bool next_c32 = i + 1 < (int)L.size() && rowconv_layer(i + 1);
         if (!conv0_ranged) MTRY(conv0_fwd(g, l.in, l.w, rng(i, 0), o, 0, st));
         conv0_ranged = false;
         if (dp && exact) CTRY(coll->allreduce(rng(i, 0), MAX_WORDS, COLL_MAX_U32, st));
-        MTRY(conv0_fwd(g, l.in, l.w, rng(i, 0), o, 1, st, next_c32 ? L[i + 1].xc32 : nullptr));
+        MTRY(conv0_fwd(g, l.in, l.w, rng(i, 0), o, 1, st, next_c32 && l.pool ? L[i + 1].xc32 : nullptr,
+                       next_c32 && !l.pool ? L[i + 1].xc32 : nullptr));
         if (next_c32) xc32_valid[i + 1] = 1;
         probe(i, 0, false, st);
         return NITI_NO_ERROR;
