@@ -231,9 +231,6 @@ struct RowConvOut {
     // launch also stores every unit's int32 accumulators here (rowconv_acc_bytes) and the
     // requantise launch reads them back instead of recomputing the GEMM
     int32_t* acc_store = nullptr;
-    // mode FUSED: another layer's NITI_SGD update (its weight gradient and range complete) done by
-    // the launch's workgroups while the grid barrier completes, or null (SgdJob below)
-    const struct SgdJob* sgd = nullptr;
 };
 size_t rowconv_acc_bytes(const ConvGeom& g, bool dg);
 constexpr int ROWCONV_BAR_WORDS = 2 * 19 * 32;  // grid-barrier state (both parities)

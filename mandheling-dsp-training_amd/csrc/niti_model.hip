@@ -587,10 +587,6 @@ struct Model {
     int fwd_layer(int i, hipStream_t st);
     int wgrad_layer(int i, hipStream_t st);
     int dgrad_layer(int i, hipStream_t st);
-    // a completed layer's NITI_SGD update handed to the next fused input-gradient launch, which runs
-    // it while its grid barrier completes (side_sgd_used: it did)
-    const SgdJob* side_sgd = nullptr;
-    bool side_sgd_used = false;
     // the input gradient of layer i need not write L[i - 1].dy in NHWC16: its weight gradient reads
     // the P16 copy (p16) and its input gradient the C32 copy (next) this same launch writes (layer 0's
     // GEMM weight gradient reads NHWC16).  NITI_DY16=1 keeps the copy (A/B diagnostics).
@@ -1114,9 +1110,7 @@ int Model::dgrad_layer(int i, hipStream_t st) {
         dy16_valid[i - 1] = !(pv.pool && o.pool_dx_nhwc == 0);
         const int K = g.c_out, rows = g.c_in;
         if (!dp && !capturing && rowconv_fc_ok(n, K, rows, true)) {
-            o.sgd = side_sgd;
             MTRY(rowconv_fc(n, K, rows, l.dy, g.cop, l.wT, g.cop, o, 0, rng(i, 1), l.bar, ++l.epoch, rc_err, st));
-            side_sgd_used = side_sgd != nullptr;
         } else {
             MTRY(rowconv_fc(n, K, rows, l.dy, g.cop, l.wT, g.cop, o, 1, rng(i, 1), nullptr, 0, nullptr, st));
             if (dp && exact) CTRY(coll->allreduce(rng(i, 1), MAX_WORDS, COLL_MAX_U32, st));
@@ -1155,9 +1149,7 @@ int Model::dgrad_layer(int i, hipStream_t st) {
         dy16_valid[i - 1] = !skip16;
         const ConvGeom& d = l.dg;
         if (!dp && !capturing && rowconv_fused_ok(d, true)) {
-            o.sgd = side_sgd;
             MTRY(rowconv_fwd(d, l.dyc32, l.wft, o, 0, rng(i, 1), l.bar, ++l.epoch, rc_err, st));
-            side_sgd_used = side_sgd != nullptr;
         } else {
             o.acc_store = rowconv_acc_bytes(d, true) ? rc_acc : nullptr;
             MTRY(rowconv_fwd(d, l.dyc32, l.wft, o, 1, rng(i, 1), nullptr, 0, nullptr, st));
@@ -1448,11 +1440,6 @@ int Model::run(const int8_t* x_nchw, int exp_in, const uint8_t* images, const in
         if (rc != NITI_NO_ERROR) return rc;
     }
     hipStream_t wst = ov ? side : st;
-    // side updates: single device, one stream, the fused input-gradient launches (NITI_SIDE_SGD=0: off)
-    static const bool side_env = getenv("NITI_SIDE_SGD") == nullptr || getenv("NITI_SIDE_SGD")[0] != '0';
-    const bool side_upd = side_env && !dp && !ov && !capturing;
-    int pending = -1;
-    char updated[SGD_MAX_JOBS] = {};
     for (int i = nl - 1; i >= 0; --i) {
         // (an event record leaves a ~6.5 us bubble before the next launch on the step stream;
         // hipStreamWriteValue64 / WaitValue64 run as blit kernels here and cost more)
@@ -1466,34 +1453,19 @@ int Model::run(const int8_t* x_nchw, int exp_in, const uint8_t* images, const in
         }
         Layer& l = L[i];
         const ConvGeom& g = l.g;
-        int rc = NITI_NO_ERROR;
-        if (side_upd) {
-            // one stream, single device: the input gradient first (it reads the old weights), carrying
-            // the previous layer's NITI_SGD update through its barrier wait; then the weight gradient
-            if (i > 0) {
-                side_sgd = pending >= 0 ? &jobs[pending] : nullptr;
-                side_sgd_used = false;
-                rc = dgrad_layer(i, st);
-                if (side_sgd_used) updated[pending] = 1;
-                side_sgd = nullptr;
-            }
-            if (rc == NITI_NO_ERROR) rc = wgrad_layer(i, wst);
-        } else {
-            rc = wgrad_layer(i, wst);
-            // data parallel: a completed gradient bucket goes to the comm stream right away
-            if (rc == NITI_NO_ERROR && dp && closes_bucket[i]) rc = sum_bucket(i, wst);
-            if (rc == NITI_NO_ERROR && i > 0) rc = dgrad_layer(i, st);
-        }
+        int rc = wgrad_layer(i, wst);
+        // data parallel: a completed gradient bucket goes to the comm stream right away
+        if (rc == NITI_NO_ERROR && dp && closes_bucket[i]) rc = sum_bucket(i, wst);
+        if (rc == NITI_NO_ERROR && i > 0) rc = dgrad_layer(i, st);
         if (rc != NITI_NO_ERROR) return rc;
-        // NITI_SGD (NITI_SGD.hpp:20-54) for this layer runs after every read of its old weights: in
-        // the next fused input-gradient launch (side), else in one launch after the backward pass
-        // the IHWO16 transpose feeds only the GEMM input gradient, the int8 gradient only the
+        // NITI_SGD (NITI_SGD.hpp:20-54) for this layer is deferred: every layer's update runs in one
+        // launch after the backward pass (the input gradients above read the old weights); the IHWO16
+        // transpose feeds only the GEMM input gradient, the int8 gradient only the
         // niti_model_get tap (keep_grads)
         jobs[i] = SgdJob{l.dwacc, rng(i, 2), RULE_WGRAD_BW2, g.c_out, g.c_in, g.kh * g.kw, g.cip, g.cop, l.w,
                          i > 0 && !rowconv_dgrad_layer(i) ? l.wT : nullptr, keep_grads ? l.g8 : nullptr};
         jobs[i].wf = l.rc ? l.wf : nullptr;
         jobs[i].wft = l.rcd ? l.wft : nullptr;
-        pending = i;
     }
     if (dp) {  // every bucket summed and ranged on the comm stream before the update
         MTRY(hipEventRecord(ev_grads, cst));
@@ -1502,13 +1474,7 @@ int Model::run(const int8_t* x_nchw, int exp_in, const uint8_t* images, const in
         MTRY(hipEventRecord(ev_side, side));
         MTRY(hipStreamWaitEvent(st, ev_side, 0));
     }
-    {  // the updates no input-gradient launch carried (also rewrite the fragment-major weight copies)
-        SgdJob rest[SGD_MAX_JOBS];
-        int nr = 0;
-        for (int i = 0; i < nl; ++i)
-            if (!updated[i]) rest[nr++] = jobs[i];
-        MTRY(sgd_update_many(rest, nr, st));
-    }
+    MTRY(sgd_update_many(jobs, nl, st));  // also rewrites the fragment-major weight copies
     return NITI_NO_ERROR;
 }
 

@@ -36,7 +36,6 @@
 #include "niti_device.hpp"
 #include "niti_kernels.hpp"
 #include "niti_map.hpp"
-#include "niti_sgd.hpp"
 
 #ifndef RC_EXP
 #define RC_EXP 0
@@ -184,8 +183,6 @@ struct RowConvArgs {
     uint32_t expect_extra;       // diagnostics (niti_diag_rowconv_barrier): arrivals that never come
     int spec;                    // FUSED: 1 speculative epilogue (bar_hint), 0 off, 2 diagnostics:
                                  // guess one bit wide of the hint (every launch redoes its epilogue)
-    int sgd_tiles;               // FUSED: tiles of `sgd` updated while the barrier completes (0: none)
-    SgdJob sgd;
     unsigned long long* stamps;  // diagnostics (niti_diag_rowconv_stamps): 8 per wave, or null
     const int8_t* relu_mask;     // input gradient: RowConvOut's relu / pool gradients
     const int8_t* pool_x;
@@ -998,20 +995,6 @@ __device__ __forceinline__ void acc_get(const RowConvArgs& a, int wg, int wid, i
         }
 }
 
-// Another layer's NITI_SGD update by this launch's workgroups while its grid barrier completes:
-// tile b of the job (64 co x 64 ci of one tap, as sgd_update_kernel) on workgroup b % grid.  The job's
-// int32 gradient and range were completed by earlier launches on the stream.
-__device__ __forceinline__ void sgd_side(const RowConvArgs& a, int8_t (*T)[64 + 4]) {
-    const SgdJob& J = a.sgd;
-    const int bw = bitwidth_of(read_max(J.amax));
-    const int tx = (J.cip + 63) / 64, ty = (J.cop + 63) / 64;
-    for (int b = blockIdx.x; b < a.sgd_tiles; b += gridDim.x) {
-        const int k = b / (tx * ty), rem = b - k * tx * ty;
-        __syncthreads();  // T is free (the previous tile's transposed reads are done)
-        sgd_tile(J, bw, (rem % tx) * 64, (rem / tx) * 64, k, T);
-    }
-}
-
 __device__ __forceinline__ void write_exponent(const RowConvArgs& a, uint32_t gmax) {
     if (a.exp_out == nullptr) return;
     const int shift = bitwidth_rc(gmax) - 7;
@@ -1043,7 +1026,6 @@ __global__ void __launch_bounds__(256, (RC_EXP & 16) ? 2 : 1) rowconv_fwd_kernel
     __shared__ __attribute__((aligned(16))) int8_t smem[KS > 0 ? RC_KS_BYTES : RC_SMEM_BYTES];
     __shared__ uint32_t red[4];
     __shared__ uint32_t gm;
-    __shared__ int8_t sgd_T[MODE == RC_FUSED ? 64 : 1][64 + 4];
     v16i acc[R];
     // the waves that own a unit's result: all four, or wave 0 of a K-split workgroup
     const bool owner = KS == 0 || wid == 0;
@@ -1081,7 +1063,6 @@ __global__ void __launch_bounds__(256, (RC_EXP & 16) ? 2 : 1) rowconv_fwd_kernel
         // workgroup's own bit width, so such a guess is not tried)
         const bool spec = guess >= 0 && guess >= bitwidth_rc(max(max(red[0], red[1]), max(red[2], red[3])));
         if (spec && U.valid && owner) unit_epilogue<W, R, DG>(a, U, lane, acc, g_guess, ein, tile);
-        if (a.sgd_tiles > 0) sgd_side(a, sgd_T);  // every wave, before wave 0 waits
         if (wid == 0) {
             const int gbw = grid_bw_wait(a.bar, a.epoch, a.err, a.spin_limit, a.expect_extra, lane);
             if (a.stamps != nullptr && lane == 0) a.stamps[blockIdx.x * 64 + 9] = __builtin_amdgcn_s_memrealtime();
@@ -1520,10 +1501,6 @@ hipError_t rowconv_fwd(const ConvGeom& g, const int8_t* x_c32, const int8_t* wf,
     a.spin_limit = g_rc_spin_limit;
     a.expect_extra = g_rc_expect_extra;
     a.spec = g_rc_spec;
-    if (o.sgd != nullptr && mode == RC_FUSED) {
-        a.sgd = *o.sgd;
-        a.sgd_tiles = ((o.sgd->cip + 63) / 64) * ((o.sgd->cop + 63) / 64) * o.sgd->kk;
-    }
     a.stamps = g_rc_stamps;
     a.relu_mask = o.relu_mask;
     a.pool_x = o.pool_x;
@@ -1667,10 +1644,6 @@ hipError_t rowconv_fc(int n, int K, int rows, const int8_t* x, int xld, const in
     a.spin_limit = g_rc_spin_limit;
     a.expect_extra = g_rc_expect_extra;
     a.spec = g_rc_spec;
-    if (o.sgd != nullptr && mode == RC_FUSED) {
-        a.sgd = *o.sgd;
-        a.sgd_tiles = ((o.sgd->cip + 63) / 64) * ((o.sgd->cop + 63) / 64) * o.sgd->kk;
-    }
     a.stamps = nullptr;
     a.relu_mask = o.relu_mask;
     a.pool_x = o.pool_x;
