@@ -331,8 +331,8 @@ def main():
     ap.add_argument("--wgrad-p16", type=int, default=-1, help="force the P16 weight gradient on every layer it "
                                                               "takes with this many K splits (0: its default; "
                                                               "-1: the autotuner's choice)")
-    ap.add_argument("--rc-spec", type=int, default=1, choices=[0, 1, 2],
-                    help="fused row kernels' speculative epilogue: 1 on (default), 0 off, 2 always redone "
+    ap.add_argument("--rc-spec", type=int, default=0, choices=[0, 1, 2],
+                    help="fused row kernels' speculative epilogue: 0 off (default), 1 on, 2 always redone "
                          "(results identical; A/B diagnostics)")
     args = ap.parse_args()
     if args.gpus is not None and args.gpus > 1 and "WORLD_SIZE" not in os.environ:

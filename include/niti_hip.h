@@ -294,9 +294,10 @@ void niti_diag_rowconv_stamps(void* buf);
 /* diagnostics: the fused row kernel's barrier poll limit (0 = default) and a number of arrivals it
  * waits for that never come (> 0 forces a timeout, to test the error plumbing) for later launches */
 void niti_diag_rowconv_barrier(uint32_t spin_limit, uint32_t expect_extra);
-/* the fused row kernel's speculative epilogue for later launches: 1 on (default; the previous launch's
- * bit width is applied while the grid barrier completes, the epilogue redone if it differs), 0 off,
- * 2 always guess wrong (every launch redoes its epilogue).  Results are identical in every mode. */
+/* the fused row kernel's speculative epilogue for later launches: 1 on (the previous launch's bit width
+ * is applied while the grid barrier completes, the epilogue redone if it differs), 0 off (default:
+ * measured slower), 2 always guess wrong (every launch redoes its epilogue).  Results are identical
+ * in every mode. */
 void niti_diag_rowconv_speculate(int mode);
 int niti_conv_wgrad_p16_acc(const niti_geom* g, const int8_t* x_p16, const int8_t* dy_p16, int32_t* acc,
                             uint32_t* amax, void* workspace, size_t workspace_bytes, int splits, void* stream);

@@ -1421,7 +1421,10 @@ bool rowconv_fused_ok(const ConvGeom& g, bool dg) {
 }
 
 static uint32_t g_rc_spin_limit = BAR_SPIN_LIMIT, g_rc_expect_extra = 0;
-static int g_rc_spec = 1;
+// the speculative epilogue is off by default: VGG-11 batch 256, 3 alternating runs each on one box,
+// 0.4115 ms per step with it against 0.3988 without (profiles/r04_ab.txt) -- the early epilogues'
+// stores compete with the slowest workgroups' K loops, which set the launch's end
+static int g_rc_spec = 0;
 void rowconv_barrier_diag(uint32_t spin_limit, uint32_t expect_extra) {
     g_rc_spin_limit = spin_limit ? spin_limit : BAR_SPIN_LIMIT;
     g_rc_expect_extra = expect_extra;

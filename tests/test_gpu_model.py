@@ -253,12 +253,12 @@ def test_vgg16_224_step_matches_oracle(T):
     assert m.rowconv_error() == 0
 
 
-@pytest.mark.parametrize("mode", [0, 2])
+@pytest.mark.parametrize("mode", [1, 2])
 def test_vgg11_step_speculative_epilogue_modes(T, mode):
     """The fused row kernels' speculative epilogue (the previous launch's bit width applied while
-    the grid barrier completes) must not change any result: off (0), and forced wrong on every
+    the grid barrier completes) must not change any result: on (1), and forced wrong on every
     launch (2: every epilogue redone with the barrier's bit width), two steps each against the
-    oracle.  The default (1) is what every other test runs."""
+    oracle.  Off (0, the default) is what every other test runs."""
     import niti_amd
     import niti_model_ref as R
     from niti_amd import _lib as L
@@ -267,4 +267,4 @@ def test_vgg11_step_speculative_epilogue_modes(T, mode):
         lib.niti_diag_rowconv_speculate(mode)
         _run(T, niti_amd.ARCH_VGG11, R.vgg11_layers(), batch=32, steps=2, seed=17 + mode)
     finally:
-        lib.niti_diag_rowconv_speculate(1)
+        lib.niti_diag_rowconv_speculate(0)
