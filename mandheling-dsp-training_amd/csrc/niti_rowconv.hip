@@ -1217,13 +1217,20 @@ hipError_t weights_to_wf(const int8_t* w_ohwi16, int co, int ci, int cip, bool t
 size_t rowconv_wf_bytes(int co, int ci) { return (size_t)((co + 31) / 32) * ((ci + 31) / 32) * 9 * 1024; }
 
 // ---- host side ---------------------------------------------------------------------------------
+// the deepest conv (input channels) the row-segment form takes; NITI_SEG_MAX_CIN overrides (A/B)
+static int seg_max_cin() {
+    static const int v = getenv("NITI_SEG_MAX_CIN") ? atoi(getenv("NITI_SEG_MAX_CIN")) : 128;
+    return v;
+}
+
 bool rowconv_ok(const ConvGeom& g) {
     if (g.kh != 3 || g.kw != 3 || g.sh != 1 || g.sw != 1 || g.dh != 1 || g.dw != 1) return false;
     if (g.pt != 1 || g.pl != 1 || g.pb != 1 || g.pr != 1) return false;
     if (g.h != g.w || g.oh != g.h || g.ow != g.w) return false;
     // W > 0 form: 2 / 4 / 8 / 16 px; the row-segment form (W = 0): 14-px segments of 224 / 112 / 56 /
-    // 28 / 14 px maps
-    const bool seg = g.w > 16 ? g.w % 28 == 0 : g.w == 14;
+    // 28 / 14 px maps, where it beats the implicit GEMM: shallow convs (c_in <= 128; per layer on
+    // MI355X, tools/seg_bench.py, profiles/r04_seg_bench.txt)
+    const bool seg = (g.w > 16 ? g.w % 28 == 0 : g.w == 14) && g.c_in <= seg_max_cin();
     if (!(g.w == 2 || g.w == 4 || g.w == 8 || g.w == 16 || seg)) return false;
     if (g.cop % 32 != 0) return false;
     return true;
