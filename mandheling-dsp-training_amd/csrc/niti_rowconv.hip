@@ -1017,6 +1017,157 @@ __device__ __forceinline__ void compute_unit(const RowConvArgs& a, const RowUnit
     }
 }
 
+// The row-segment form's persistent modes (RANGE, REQUANT) as ONE software-pipelined stream of
+// (tile, chunk) steps over the block's tiles t = blockIdx.x, + gridDim.x, ...: the next tile's first
+// chunks load while this tile's last ones compute (the per-unit prologue of rowconv_compute left a
+// shallow conv -- 2 to 4 chunks per unit -- waiting for memory once per unit).  Same ring as
+// rowconv_compute: 4 stages, the R + 2 input rows of a chunk in registers, its 9 weight fragments
+// LDS-DMA'd by the four waves; steps past the last tile load out of range (zeros) and feed nothing.
+// A tile's epilogue (the max, or the requantised outputs) runs after its last chunk; its memory
+// operations are drained there (s_waitcnt vmcnt(0)), with the next tile's loads already in flight.
+template <int R, int MODE, bool DG>
+__device__ __forceinline__ void seg_run(const RowConvArgs& a, int lane, int wid, int8_t* smem, uint32_t& m,
+                                        uint32_t g) {
+    constexpr int NR = R + 2, S = 4, L = NR + 3;
+    const int H = a.hw, W = a.hw, CB = a.CB;
+    const int h = lane >> 5, c = lane & 31;
+    const __amdgpu_buffer_rsrc_t rX = make_rsrc(a.x, a.xbytes);
+    const __amdgpu_buffer_rsrc_t rW = make_rsrc(a.wf, a.wbytes);
+    const uint32_t CHUNK = (uint32_t)H * W * 32;
+    const int ntiles = (int)blockIdx.x < a.wgs ? (a.wgs - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+    const int total = ntiles * CB;
+    const int steps = (total + S - 1) / S * S;  // whole ring turns: straight-line steps
+    auto tile_wg = [&](int k) {
+        const int b = (int)blockIdx.x + k * (int)gridDim.x;
+        return a.wmajor && (int)gridDim.x == a.wgs ? xcd_remap(b, gridDim.x) : b;
+    };
+    // issue side: the tile whose chunks are being loaded, its rows' lane offsets and weight base
+    int ik = 0, icc = 0;
+    uint32_t ioff[NR], iwb = 0;
+    auto set_issue = [&](int k) {
+        if (k >= ntiles) {
+#pragma unroll
+            for (int j = 0; j < NR; ++j) ioff[j] = OOB;
+            iwb = 0;
+            return;
+        }
+        const RowUnit<0, R> U(a, tile_wg(k), wid, c, false);
+        const uint32_t xl = U.img_ok && U.x_ok ? (uint32_t)((((int64_t)U.img * CB * H) * W + U.x) * 32 + 16 * h) : OOB;
+#pragma unroll
+        for (int j = 0; j < NR; ++j) {
+            const int iy = U.b * R - 1 + j;
+            ioff[j] = xl != OOB && iy >= 0 && iy < H ? xl + (uint32_t)iy * W * 32 : OOB;
+        }
+        iwb = (uint32_t)(U.cob * CB * 9) * 1024u;
+    };
+    const uint32_t dv2 = wid == 0 ? (uint32_t)lane * 16u : OOB;
+    v4i X[S][NR];
+    auto issue = [&](auto st_c) {
+        constexpr int ST = decltype(st_c)::value;
+        int8_t* lds = smem + ST * RC_STAGE_BYTES;
+        const bool real = ik < ntiles;
+        const uint32_t wo = iwb + (uint32_t)icc * 9216u;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const int piece = wid + 4 * k;
+            dma16(rW, lds + piece * 1024, real ? (k < 2 ? (uint32_t)lane * 16u : dv2) : OOB,
+                  wo + (uint32_t)(piece < 9 ? piece : 0) * 1024u);
+        }
+#pragma unroll
+        for (int j = 0; j < NR; ++j) X[ST][j] = buf_load16(rX, ioff[j] == OOB ? OOB : ioff[j] + (uint32_t)icc * CHUNK);
+        if (++icc == CB) {  // the next tile
+            icc = 0;
+            set_issue(++ik);
+        }
+    };
+    const uint32_t lds_lane = lds_addr(smem) + (uint32_t)lane * 16u;
+    v4i wreg[2][9];
+    auto read_w = [&](auto st_c, v4i (&w)[9]) {
+        constexpr int ST = decltype(st_c)::value;
+#pragma unroll
+        for (int t = 0; t < 9; ++t) w[t] = lds_b128(lds_lane + (uint32_t)(ST * RC_STAGE_BYTES + t * 1024));
+    };
+    auto fence_w = [&](v4i (&w)[9]) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int t = 0; t < 9; ++t) reg_fence(w[t]);
+    };
+    // compute side: the tile whose chunks are being multiplied
+    int ck = 0, ccc = 0;
+    v16i acc[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[r][i] = 0;
+    auto finish = [&]() {  // tile ck's last chunk is in acc
+        const RowUnit<0, R> U(a, tile_wg(ck), wid, c, false);
+        if constexpr (MODE == RC_RANGE) {
+            m = unit_max<0, R>(U, acc, m);
+            if (a.acc_store != nullptr) acc_put<R>(a, tile_wg(ck), wid, lane, acc);
+        } else {
+            EpiIn<DG ? R : 1> ein = {};
+            if constexpr (DG) {
+                seg_prefetch<R>(a, U, lane, ein);
+                epi_masks<R>(a, ein);
+            }
+            if (U.valid) seg_epilogue<R, DG>(a, U, lane, acc, g, ein);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) acc[r][i] = 0;
+    };
+    auto step = [&](auto st_c, int s) {
+        constexpr int ST = decltype(st_c)::value, WB = ST & 1;
+        // chunk s + 1 has landed (s + 2 may still be in flight) and chunk s - 1's stage is free
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(L) : "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        issue(std::integral_constant<int, (ST + 3) % S>());
+        read_w(std::integral_constant<int, (ST + 1) % S>(), wreg[1 - WB]);
+        const v4i (&w)[9] = wreg[WB];
+        v4i XL[NR], XR[NR];
+#pragma unroll
+        for (int j = 0; j < NR; ++j) {
+            XL[j] = shift_in_left<16>(X[ST][j], false);
+            XR[j] = shift_in_right<16>(X[ST][j], false);
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int ky = 0; ky < 3; ++ky) {
+                acc[r] = __builtin_amdgcn_mfma_i32_32x32x32_i8(w[3 * ky], XL[r + ky], acc[r], 0, 0, 0);
+                acc[r] = __builtin_amdgcn_mfma_i32_32x32x32_i8(w[3 * ky + 1], X[ST][r + ky], acc[r], 0, 0, 0);
+                acc[r] = __builtin_amdgcn_mfma_i32_32x32x32_i8(w[3 * ky + 2], XR[r + ky], acc[r], 0, 0, 0);
+            }
+        fence_w(wreg[1 - WB]);
+        if (s < total && ++ccc == CB) {  // uniform: the tile's last chunk is in
+            finish();
+            ccc = 0;
+            ++ck;
+        }
+    };
+    set_issue(0);
+    issue(std::integral_constant<int, 0>());
+    issue(std::integral_constant<int, 1>());
+    issue(std::integral_constant<int, 2>());
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(L) : "memory");  // step 0 (and 1) landed
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    read_w(std::integral_constant<int, 0>(), wreg[0]);
+    fence_w(wreg[0]);
+    for (int s = 0; s < steps; s += S) {
+        step(std::integral_constant<int, 0>(), s);
+        step(std::integral_constant<int, 1>(), s + 1);
+        step(std::integral_constant<int, 2>(), s + 2);
+        step(std::integral_constant<int, 3>(), s + 3);
+    }
+    // the look-ahead loads (LDS-DMA into the ring) land before the workgroup's LDS is reused
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+}
+
 // DG: the input-gradient epilogues (relu mask / pool gradient), their operands prefetched
 template <int W, int R, int MODE, bool DG, bool UNC, int KS>
 __global__ void __launch_bounds__(256, (RC_EXP & 16) ? 2 : 1) rowconv_fwd_kernel(RowConvArgs a) {
@@ -1080,6 +1231,18 @@ __global__ void __launch_bounds__(256, (RC_EXP & 16) ? 2 : 1) rowconv_fwd_kernel
         RC_STAMP(4);
         if (U.valid && owner && (!spec || gm != g_guess)) unit_epilogue<W, R, DG>(a, U, lane, acc, gm, ein, tile);
         RC_STAMP(5);
+    } else if constexpr (MODE == RC_RANGE && W == 0) {
+        uint32_t m = 0;
+        seg_run<R, RC_RANGE, false>(a, lane, wid, smem, m, 0u);
+        m = wave_max(m);
+        if (lane == 0) red[wid] = m;
+        __syncthreads();
+        if (threadIdx.x == 0) publish_max(a.amax, max(max(red[0], red[1]), max(red[2], red[3])));
+    } else if constexpr (MODE == RC_REQUANT && W == 0) {
+        const uint32_t g = read_max(a.amax);
+        if (blockIdx.x == 0 && threadIdx.x == 0) write_exponent(a, g);
+        uint32_t m = 0;
+        seg_run<R, RC_REQUANT, DG>(a, lane, wid, smem, m, g);
     } else if constexpr (MODE == RC_RANGE) {
         uint32_t m = 0;
         for (int b = blockIdx.x; b < a.wgs; b += gridDim.x) {
@@ -1530,6 +1693,13 @@ hipError_t rowconv_fwd(const ConvGeom& g, const int8_t* x_c32, const int8_t* wf,
     }
     int grid = a.wgs;
     grid = grid > 1024 ? 1024 : grid;
+    if (seg) {  // one resident wave of blocks, each streaming its tiles through one pipeline (seg_run)
+        const void* f = mode == RC_RANGE ? rc_kernel<RC_RANGE, false>(0, R, false, 0)
+                                         : (dg ? rc_kernel<RC_REQUANT, true>(0, R, false, 0)
+                                               : rc_kernel<RC_REQUANT, false>(0, R, false, 0));
+        const int res = resident_wgs(f);
+        if (res > 0 && grid > res) grid = res;
+    }
     if (mode == RC_RANGE) return launch_rc<RC_RANGE, false>(Wk, R, grid, a, st, ks);
     return dg ? launch_rc<RC_REQUANT, true>(Wk, R, grid, a, st, ks) : launch_rc<RC_REQUANT, false>(Wk, R, grid, a, st, ks);
 }
