@@ -231,10 +231,11 @@ struct RowUnit {
     // ks: the K-split form -- one unit per workgroup, its four waves splitting the channel chunks
     __device__ RowUnit(const RowConvArgs& a, int wg, int wid, int c, bool ks = false) {
         if constexpr (W == 0) {
-            // units of a co block: ((image group, band), segment pair), whole workgroups of four
-            const int per = a.upc4 / 4;
-            cob = wg / per;
-            const int u = (wg - cob * per) * 4 + wid;
+            // units of a co block: ((image group, band), segment pair), whole workgroups of four; the
+            // co block varies fastest, so the co blocks of one pixel tile run side by side and its
+            // input rows (tens to hundreds of MB per layer) come from HBM once, not once per co block
+            cob = wg % a.COB;
+            const int u = (wg / a.COB) * 4 + wid;
             const int nu = a.ngb * a.nsp;  // ngb = image groups x bands
             valid = u < nu;
             const int uc = valid ? u : 0;
@@ -1408,7 +1409,8 @@ struct SegPlan {
 };
 static SegPlan seg_plan(const ConvGeom& g) {
     SegPlan p{};
-    p.R = g.h % 4 == 0 ? 4 : 2;
+    static const int r_env = getenv("NITI_SEG_R") ? atoi(getenv("NITI_SEG_R")) : 4;  // A/B diagnostics
+    p.R = g.h % 4 == 0 && r_env == 4 ? 4 : 2;
     p.gw = g.w == 14 ? 2 : 1;
     p.nsp = g.w >= 28 ? g.w / 28 : 1;
     p.nbands = g.h / p.R;

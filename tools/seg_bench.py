@@ -12,6 +12,7 @@ import sys
 import numpy as np
 import torch
 
+os.environ.setdefault("NITI_SEG_MAX_CIN", "1024")  # every width on the row-segment form, for the A/B
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "mandheling-dsp-training_amd"))
 from niti_amd import ops  # noqa: E402
