@@ -299,6 +299,9 @@ void niti_diag_rowconv_barrier(uint32_t spin_limit, uint32_t expect_extra);
  * measured slower), 2 always guess wrong (every launch redoes its epilogue).  Results are identical
  * in every mode. */
 void niti_diag_rowconv_speculate(int mode);
+/* jobs per P16 input-copy launch of a model step for later steps (<= 0: the default 16); a small
+ * cap sends a step down its more-than-one-launch branches.  Results are identical for every cap. */
+void niti_diag_p16_jobs_cap(int cap);
 int niti_conv_wgrad_p16_acc(const niti_geom* g, const int8_t* x_p16, const int8_t* dy_p16, int32_t* acc,
                             uint32_t* amax, void* workspace, size_t workspace_bytes, int splits, void* stream);
 /* acc[m][ldc] = sum_k B[m][k] A[o][k] (columns o..ldc = 0); K zero padded to k16; ldb/lda bytes */

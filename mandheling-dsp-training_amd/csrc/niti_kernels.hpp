@@ -263,6 +263,7 @@ void rowconv_barrier_diag(uint32_t spin_limit, uint32_t expect_extra);
 // the fused mode's speculative epilogue (the previous launch's bit width applied while the barrier
 // completes): 1 on (default), 0 off, 2 always guess wrong (diagnostics: every launch redoes it)
 void rowconv_speculate(int mode);
+void model_p16_jobs_cap(int cap);  // niti_model.hip, diagnostic
 hipError_t rowconv_fwd(const ConvGeom& g, const int8_t* x_c32, const int8_t* wf, const RowConvOut& o, int mode,
                        uint32_t* amax, uint32_t* bar, uint32_t epoch, uint32_t* err, hipStream_t st);
 // A 1x1 layer over 1x1 maps (the classifier head) on the same kernel: rows output channels of

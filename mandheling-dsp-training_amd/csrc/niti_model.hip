@@ -30,6 +30,11 @@
 namespace niti {
 
 namespace {
+extern int g_p16_jobs_cap;
+}
+void model_p16_jobs_cap(int cap) { g_p16_jobs_cap = cap <= 0 ? P16_MAX_JOBS : cap; }
+
+namespace {
 
 // im2col of the first layer: xcol[p][(ky * KW + kx) * C + c] = x[n][oy * sh + ky - pt][ox * sw + kx - pl][c]
 // (NHWC16 input, zero outside the image and for k >= C * KH * KW), one output pixel (32 bytes) per
@@ -77,6 +82,9 @@ struct Im2Col32 {
         }
     }
 };
+
+// diagnostic: jobs per P16 conversion launch (niti_diag_p16_jobs_cap)
+int g_p16_jobs_cap = P16_MAX_JOBS;
 
 static hipError_t im2col32(const ConvGeom& o, const int8_t* x16, int8_t* out, hipStream_t st) {
     const int64_t px = (int64_t)o.n * o.oh * o.ow;
@@ -383,12 +391,15 @@ struct Model {
         }
         return NITI_NO_ERROR;
     }
+    // jobs per P16 conversion launch: P16_MAX_JOBS, lowered only by niti_diag_p16_jobs_cap (tests
+    // reach the more-than-one-launch branches with a small net)
+    static int p16_jobs_cap() { return std::min(std::max(g_p16_jobs_cap, 1), P16_MAX_JOBS); }
     // every P16 input copy of the backward pass as one job list (false: more than one launch holds)
     bool p16_input_jobs(P16Conv* jobs, int* n) {
         *n = 0;
         for (int j = 0; j < (int)L.size(); ++j)
             if (wgrad_p16_splits(j)) {
-                if (*n == P16_MAX_JOBS) return false;
+                if (*n == p16_jobs_cap()) return false;
                 const ConvGeom& g = L[j].g;
                 jobs[(*n)++] = P16Conv{L[j].in, (int64_t)g.n * g.h * g.w, g.cip, xp16[j]};
             }
@@ -402,7 +413,7 @@ struct Model {
                 const ConvGeom& g = L[j].g;
                 jobs[n++] = P16Conv{L[j].in, (int64_t)g.n * g.h * g.w, g.cip, xp16[j]};
                 xp16_valid[j] = 1;
-                if (n == P16_MAX_JOBS || j + 1 == (int)L.size()) {
+                if (n == p16_jobs_cap() || j + 1 == (int)L.size()) {
                     if (nhwc16_to_p16_many(jobs, n, st) != hipSuccess) return NITI_NO_EXECUTION;
                     n = 0;
                 }

@@ -601,9 +601,10 @@ __device__ __forceinline__ v4i pack_cols(const int8_t* q) {
 // The input-gradient epilogue's operands (the relu mask, or the pool's input window and output),
 // loaded before the grid barrier and turned into byte masks while the barrier completes: the
 // epilogue then only ANDs the requantised gradient with them
-template <int R>
+// PX false: no pool window (an input-gradient launch without a pool gradient -- 8 R fewer VGPRs)
+template <int R, bool PX = true>
 struct EpiIn {
-    v4i x[R][4];  // pool: the 2x2 window of pool_x per row, then its routing masks
+    v4i x[PX ? R : 1][4];  // pool: the 2x2 window of pool_x per row, then its routing masks
     v4i y[R];     // pool: pool_y; relu: relu_mask, then its byte mask (one member for the tensors
                   // at the output's own pixels: hipcc merges the two branches' loads into one)
 };
@@ -622,9 +623,9 @@ __device__ __forceinline__ uint32_t sw_pos_hi(uint32_t x) {  // signed x > 0
 }
 __device__ __forceinline__ uint32_t sw_expand(uint32_t hb) { return hb | (hb - (hb >> 7)); }
 
-template <int R>
-__device__ __forceinline__ void epi_masks(const RowConvArgs& a, EpiIn<R>& e) {
-    if (a.pool_dx != nullptr) {
+template <int R, bool PX = true>
+__device__ __forceinline__ void epi_masks(const RowConvArgs& a, EpiIn<R, PX>& e) {
+    if (PX && a.pool_dx != nullptr) {
         // NITI_CPUPoolGrad_Int8's scan: the first window element >= the pool output takes it
 #pragma unroll
         for (int r = 0; r < R; ++r)
@@ -634,11 +635,11 @@ __device__ __forceinline__ void epi_masks(const RowConvArgs& a, EpiIn<R>& e) {
                 uint32_t done = 0;
 #pragma unroll
                 for (int t = 0; t < 4; ++t) {
-                    const uint32_t x = (uint32_t)e.x[r][t][k];
+                    const uint32_t x = (uint32_t)e.x[PX ? r : 0][t][k];
                     uint32_t take = sw_ge_hi(x, m) & ~done;
                     done |= take;
                     if (a.pool_relu) take &= sw_pos_hi(x);
-                    e.x[r][t][k] = (int)sw_expand(take);
+                    e.x[PX ? r : 0][t][k] = (int)sw_expand(take);
                 }
             }
     } else if (a.relu_mask != nullptr) {
@@ -822,20 +823,21 @@ __device__ __forceinline__ uint32_t max_abs16(const v16i& v, uint32_t m) {
 // Its MFMA columns are 14-px segments (or 7-px rows) with halo lanes, so a lane's output pixel is
 // (U.img, row, U.x) where U.out_ok; the halo lanes' accumulators are partial sums and are neither
 // ranged nor stored.  Same rule, relu / pool / pool-gradient epilogues and layouts as the W > 0 form.
-template <int R>
-__device__ __forceinline__ void seg_prefetch(const RowConvArgs& a, const RowUnit<0, R>& U, int lane, EpiIn<R>& e) {
+template <int R, bool PX = true>
+__device__ __forceinline__ void seg_prefetch(const RowConvArgs& a, const RowUnit<0, R>& U, int lane, EpiIn<R, PX>& e) {
     const int h = lane >> 5, W = a.hw, H = a.hw;
     const int64_t img = U.img_ok ? U.img : 0;
     const int xs = U.x < 0 ? 0 : (U.x >= W ? W - 1 : U.x);  // a halo lane reads a real pixel (unused)
     const int cb16 = U.cob * 32 + 16 * h;
     uint32_t z = 0;
     asm volatile("" : "+s"(z));
-    const bool pool = a.pool_dx != nullptr;
+    const bool pool = PX && a.pool_dx != nullptr;
     const int8_t* ps = (pool ? a.pool_y : a.relu_mask) + z;
     const int8_t* px = a.pool_x + z;
     if (!pool && a.relu_mask == nullptr) return;
 #pragma unroll
     for (int r = 0; r < R; ++r) e.y[r] = *(const v4i*)(ps + ((img * H + U.b * R + r) * W + xs) * a.cop + cb16);
+    if constexpr (PX)
     if (pool) {
 #pragma unroll
         for (int r = 0; r < R; ++r)
@@ -846,9 +848,9 @@ __device__ __forceinline__ void seg_prefetch(const RowConvArgs& a, const RowUnit
     }
 }
 
-template <int R, bool DG>
+template <int R, bool DG, bool PX = true>
 __device__ __forceinline__ void seg_epilogue(const RowConvArgs& a, const RowUnit<0, R>& U, int lane,
-                                             const v16i (&acc)[R], uint32_t gmax, const EpiIn<DG ? R : 1>& e) {
+                                             const v16i (&acc)[R], uint32_t gmax, const EpiIn<DG ? R : 1, PX>& e) {
     const int h = lane >> 5, W = a.hw, H = a.hw;
     const int shift = __builtin_amdgcn_readfirstlane(bitwidth_rc(gmax) - 7);
     int8_t q[R][16];
@@ -888,7 +890,7 @@ __device__ __forceinline__ void seg_epilogue(const RowConvArgs& a, const RowUnit
     const int64_t img = U.img;
     const int x = U.x;
     const int cb16 = U.cob * 32 + 16 * h;
-    if (DG && a.pool_dx != nullptr) {  // through the previous layer's 2x2 max pool
+    if (DG && PX && a.pool_dx != nullptr) {  // through the previous layer's 2x2 max pool
         const int H2 = 2 * H, W2 = 2 * W;
 #pragma unroll
         for (int r = 0; r < R; ++r) {
@@ -898,7 +900,7 @@ __device__ __forceinline__ void seg_epilogue(const RowConvArgs& a, const RowUnit
 #pragma unroll
             for (int t = 0; t < 4; ++t) {
                 const int iy = 2 * oy + (t >> 1), ix = 2 * x + (t & 1);
-                const v4i d = v & e.x[DG ? r : 0][t];
+                const v4i d = v & e.x[DG && PX ? r : 0][t];
                 if (a.pool_dx_nhwc) *(v4i*)(a.pool_dx + ((img * H2 + iy) * W2 + ix) * a.cop + cb16) = d;
                 if (a.pool_dx_next != nullptr)
                     *(v4i*)(a.pool_dx_next + (((img * a.COB + U.cob) * H2 + iy) * W2 + ix) * 32 + 16 * h) = d;
@@ -1018,15 +1020,43 @@ __device__ __forceinline__ void compute_unit(const RowConvArgs& a, const RowUnit
     }
 }
 
+// s_waitcnt vmcnt(n) for a run-time, wave-uniform n in [LO, HI] (a binary search of scalar
+// branches down to the immediate; n above HI waits for HI, which only waits longer)
+template <int LO, int HI>
+__device__ __forceinline__ void vm_wait_dyn(int n) {
+    if constexpr (LO == HI) {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LO) : "memory");
+    } else {
+        constexpr int MID = (LO + HI) / 2;
+        if (n <= MID)
+            vm_wait_dyn<LO, MID>(n);
+        else
+            vm_wait_dyn<MID + 1, HI>(n);
+    }
+}
+
+// VMEM stores a valid unit's seg_epilogue issues -- a lower bound (a store split in two only makes
+// the counted waits below wait longer; a count above the real one would let them pass early)
+template <int R, bool DG>
+__device__ __forceinline__ int seg_epi_stores(const RowConvArgs& a) {
+    if (DG && a.pool_dx != nullptr) return 4 * R * ((a.pool_dx_nhwc ? 1 : 0) + (a.pool_dx_next != nullptr ? 1 : 0));
+    int e = R * ((a.out != nullptr ? 1 : 0) + (a.next != nullptr && a.pool_out == nullptr ? 1 : 0));
+    if (a.pool_out != nullptr) e += (R / 2) * (1 + (a.next != nullptr ? 1 : 0));
+    return e;
+}
+
 // The row-segment form's persistent modes (RANGE, REQUANT) as ONE software-pipelined stream of
 // (tile, chunk) steps over the block's tiles t = blockIdx.x, + gridDim.x, ...: the next tile's first
 // chunks load while this tile's last ones compute (the per-unit prologue of rowconv_compute left a
 // shallow conv -- 2 to 4 chunks per unit -- waiting for memory once per unit).  Same ring as
 // rowconv_compute: 4 stages, the R + 2 input rows of a chunk in registers, its 9 weight fragments
 // LDS-DMA'd by the four waves; steps past the last tile load out of range (zeros) and feed nothing.
-// A tile's epilogue (the max, or the requantised outputs) runs after its last chunk; its memory
-// operations are drained there (s_waitcnt vmcnt(0)), with the next tile's loads already in flight.
-template <int R, int MODE, bool DG>
+// A tile's epilogue (the max, or the requantised outputs) runs after its last chunk, with the next
+// tile's loads in flight.  Its stores (and the input gradient's operand prefetch) are VMEM operations
+// the ring's counted waits must allow for: a step waits for vmcnt(L + the extra operations issued
+// after the stage it needs) instead of draining the queue after every tile (a full memory round trip
+// per tile: ~30 % of a shallow layer's launch).
+template <int R, int MODE, bool DG, bool PX = true>
 __device__ __forceinline__ void seg_run(const RowConvArgs& a, int lane, int wid, int8_t* smem, uint32_t& m,
                                         uint32_t g) {
     constexpr int NR = R + 2, S = 4, L = NR + 3;
@@ -1095,6 +1125,18 @@ __device__ __forceinline__ void seg_run(const RowConvArgs& a, int lane, int wid,
     };
     // compute side: the tile whose chunks are being multiplied
     int ck = 0, ccc = 0;
+    // the input-gradient epilogue's operands (relu mask / pool window) load with the tile's first
+    // chunk and land while its chunks multiply (loaded after the last one, they stalled every tile
+    // for a memory round trip: the requantise launch ran 2-3x its range launch in the VGG-16 step);
+    // the step after such a prefetch allows its pf loads in flight beside the ring's
+    EpiIn<DG ? R : 1, PX> ein = {};
+    // extra VMEM operations (outside the ring) of step s - 2 after its ring issue (xa2), and of step
+    // s - 1 before / after it (xb1, xa1): everything issued after the stage step s waits for
+    int xa2 = 0, xb1 = 0, xa1 = 0, xb = 0, xa = 0;
+    const int pf_n = __builtin_amdgcn_readfirstlane(
+        DG && MODE != RC_RANGE ? (PX && a.pool_dx != nullptr ? 5 * R : (a.relu_mask != nullptr ? R : 0)) : 0);
+    const int st_n = __builtin_amdgcn_readfirstlane(MODE == RC_RANGE ? (a.acc_store != nullptr ? 4 * R : 0)
+                                                                      : seg_epi_stores<R, DG>(a));
     v16i acc[R];
 #pragma unroll
     for (int r = 0; r < R; ++r)
@@ -1106,14 +1148,11 @@ __device__ __forceinline__ void seg_run(const RowConvArgs& a, int lane, int wid,
             m = unit_max<0, R>(U, acc, m);
             if (a.acc_store != nullptr) acc_put<R>(a, tile_wg(ck), wid, lane, acc);
         } else {
-            EpiIn<DG ? R : 1> ein = {};
-            if constexpr (DG) {
-                seg_prefetch<R>(a, U, lane, ein);
-                epi_masks<R>(a, ein);
-            }
-            if (U.valid) seg_epilogue<R, DG>(a, U, lane, acc, g, ein);
+            if constexpr (DG) epi_masks<R, PX>(a, ein);
+            if (U.valid) seg_epilogue<R, DG, PX>(a, U, lane, acc, g, ein);
+            xa = __builtin_amdgcn_readfirstlane(U.valid ? st_n : 0);
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if constexpr (MODE == RC_RANGE) xa = st_n;
 #pragma unroll
         for (int r = 0; r < R; ++r)
 #pragma unroll
@@ -1122,9 +1161,24 @@ __device__ __forceinline__ void seg_run(const RowConvArgs& a, int lane, int wid,
     auto step = [&](auto st_c, int s) {
         constexpr int ST = decltype(st_c)::value, WB = ST & 1;
         // chunk s + 1 has landed (s + 2 may still be in flight) and chunk s - 1's stage is free
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(L) : "memory");
+        {
+            const int ex = xa2 + xb1 + xa1;
+            if (ex == 0)
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(L) : "memory");
+            else
+                vm_wait_dyn<L, 63>(L + ex);
+            xa2 = xa1;
+            xb = xa = 0;
+        }
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
+        if constexpr (DG && MODE != RC_RANGE) {
+            if (s < total && ccc == 0) {
+                const RowUnit<0, R> U(a, tile_wg(ck), wid, c, false);
+                seg_prefetch<R, PX>(a, U, lane, ein);
+                xb = pf_n;
+            }
+        }
         issue(std::integral_constant<int, (ST + 3) % S>());
         read_w(std::integral_constant<int, (ST + 1) % S>(), wreg[1 - WB]);
         const v4i (&w)[9] = wreg[WB];
@@ -1148,6 +1202,8 @@ __device__ __forceinline__ void seg_run(const RowConvArgs& a, int lane, int wid,
             ccc = 0;
             ++ck;
         }
+        xb1 = xb;
+        xa1 = xa;
     };
     set_issue(0);
     issue(std::integral_constant<int, 0>());
@@ -1243,7 +1299,8 @@ __global__ void __launch_bounds__(256, (RC_EXP & 16) ? 2 : 1) rowconv_fwd_kernel
         const uint32_t g = read_max(a.amax);
         if (blockIdx.x == 0 && threadIdx.x == 0) write_exponent(a, g);
         uint32_t m = 0;
-        seg_run<R, RC_REQUANT, DG>(a, lane, wid, smem, m, g);
+        // the row-segment form's KS: 1 = an input gradient through a pool (its window operands)
+        seg_run<R, RC_REQUANT, DG, KS != 0>(a, lane, wid, smem, m, g);
     } else if constexpr (MODE == RC_RANGE) {
         uint32_t m = 0;
         for (int b = blockIdx.x; b < a.wgs; b += gridDim.x) {
@@ -1409,7 +1466,9 @@ struct SegPlan {
 };
 static SegPlan seg_plan(const ConvGeom& g) {
     SegPlan p{};
-    static const int r_env = getenv("NITI_SEG_R") ? atoi(getenv("NITI_SEG_R")) : 4;  // A/B diagnostics
+    // R = 2 (two blocks per CU: one wave's loads wait while the other's MFMAs run) measured faster
+    // than R = 4 at every row-segment layer (profiles/r04_seg_bench.txt); NITI_SEG_R=4 for A/B
+    static const int r_env = getenv("NITI_SEG_R") ? atoi(getenv("NITI_SEG_R")) : 2;
     p.R = g.h % 4 == 0 && r_env == 4 ? 4 : 2;
     p.gw = g.w == 14 ? 2 : 1;
     p.nsp = g.w >= 28 ? g.w / 28 : 1;
@@ -1506,6 +1565,11 @@ int rowconv_units(const ConvGeom& g, bool dg) {
 // the instantiation a launch runs (ks > 0: the K-split form, W = R = 2)
 template <int MODE, bool DG>
 static const void* rc_kernel(int W, int R, bool unc, int ks) {
+    if constexpr (MODE == RC_REQUANT && DG) {  // row-segment input gradients: ks = 1 through a pool
+        if (W == 0 && ks == 1 && R == 4) return reinterpret_cast<const void*>(&rowconv_fwd_kernel<0, 4, MODE, DG, false, 1>);
+        if (W == 0 && ks == 1 && R == 2) return reinterpret_cast<const void*>(&rowconv_fwd_kernel<0, 2, MODE, DG, false, 1>);
+    }
+    if (W == 0 && ks != 0) return nullptr;
     if (ks > 0) {
         if (ks == 4) return reinterpret_cast<const void*>(&rowconv_fwd_kernel<2, 2, MODE, DG, false, 4>);
         if (ks == 2) return reinterpret_cast<const void*>(&rowconv_fwd_kernel<2, 2, MODE, DG, false, 2>);
@@ -1696,8 +1760,11 @@ hipError_t rowconv_fwd(const ConvGeom& g, const int8_t* x_c32, const int8_t* wf,
     int grid = a.wgs;
     grid = grid > 1024 ? 1024 : grid;
     if (seg) {  // one resident wave of blocks, each streaming its tiles through one pipeline (seg_run)
+        // an input gradient without a pool gradient takes the instantiation without the pool window's
+        // registers (252 VGPRs at R = 2: two blocks per CU instead of one)
+        ks = mode == RC_REQUANT && dg && o.pool_dx != nullptr ? 1 : 0;
         const void* f = mode == RC_RANGE ? rc_kernel<RC_RANGE, false>(0, R, false, 0)
-                                         : (dg ? rc_kernel<RC_REQUANT, true>(0, R, false, 0)
+                                         : (dg ? rc_kernel<RC_REQUANT, true>(0, R, false, ks)
                                                : rc_kernel<RC_REQUANT, false>(0, R, false, 0));
         const int res = resident_wgs(f);
         if (res > 0 && grid > res) grid = res;

@@ -268,3 +268,20 @@ def test_vgg11_step_speculative_epilogue_modes(T, mode):
         _run(T, niti_amd.ARCH_VGG11, R.vgg11_layers(), batch=32, steps=2, seed=17 + mode)
     finally:
         lib.niti_diag_rowconv_speculate(0)
+
+
+@pytest.mark.parametrize("cap", [1, 3])
+def test_vgg11_step_p16_copies_over_several_launches(T, cap):
+    """More P16 input copies than one launch takes (the model's job cap lowered to 1 or 3): the
+    step then runs the plain loss gradient and converts the inputs in several launches ahead of the
+    last layer's weight gradient, instead of the fused loss + P16 launch -- two steps against the
+    oracle (overlap off, the default)."""
+    import niti_amd
+    import niti_model_ref as R
+    from niti_amd import _lib as L
+    lib = L.lib()
+    try:
+        lib.niti_diag_p16_jobs_cap(cap)
+        _run(T, niti_amd.ARCH_VGG11, R.vgg11_layers(), batch=32, steps=2, seed=41 + cap)
+    finally:
+        lib.niti_diag_p16_jobs_cap(0)
