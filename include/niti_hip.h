@@ -252,6 +252,13 @@ int niti_conv_rows_ok(const niti_geom* g);
 int niti_nhwc16_to_c32(const int8_t* in_nhwc16, int n, int hw, int cp, int c, int8_t* out_c32, void* stream);
 int niti_weights_to_wf(const int8_t* w_ohwi16, int co, int ci, int cip, int transpose, int8_t* out_wf,
                        void* stream);
+/* mode | NITI_ROWS_X_NHWC16 (niti_conv_fwd_rows / niti_conv_dgrad_rows): the input (x, or dy) is NHWC16
+ * [n][H][W][cip] instead of C32 -- the row-segment maps (niti_conv_rows_nhwc_ok: 14-px multiples
+ * above 16 px, or 14 px; cip % 32 == 0) read it in place, with no C32 copy */
+#define NITI_ROWS_X_NHWC16 0x100
+/* flags bit 0: the input gradient's input (dy) instead of the forward's x; bit 1: whether the
+ * library's own step prefers it over a C32 copy (64-channel inputs), not only whether it works */
+int niti_conv_rows_nhwc_ok(const niti_geom* g, int flags);
 int niti_conv_fwd_rows(const niti_geom* g, const int8_t* x_c32, const int8_t* wf, const int8_t* exp_in,
                        const int8_t* wscale, int8_t* exp_out, int relu, int8_t* out_nhwc16, int8_t* pool_out_nhwc16,
                        int8_t* next_c32, int mode, uint32_t* amax, uint32_t* state, uint32_t epoch, uint32_t* err,
@@ -344,10 +351,19 @@ int niti_residual_add(const int8_t* a, const int8_t* ea, const int8_t* b, const 
  * on the stored z; *ez = e_hi - d and *exp_out = *ez + inc (either may be NULL). */
 int niti_residual_requant(const int8_t* a, const int8_t* ea, const int8_t* b, const int8_t* eb, int64_t n,
                           const uint32_t* amax, int8_t* ez, int8_t* exp_out, int relu, int8_t* out, void* stream);
+/* the same (no relu), followed by the next op's relu gradient: out = relu_mask > 0 ? q : 0 (the
+ * backward residual sum of a block, masked by the previous block's output, NITI_ReluGrad_Int8) */
+int niti_residual_requant_relu_grad(const int8_t* a, const int8_t* ea, const int8_t* b, const int8_t* eb, int64_t n,
+                                    const uint32_t* amax, int8_t* ez, int8_t* exp_out, const int8_t* relu_mask,
+                                    int8_t* out, void* stream);
 /* global sum pool: acc[img][c] = sum over hw pixels of x NHWC16 [n][hw][cp] (+ max into amax) */
 int niti_sum_pool(const int8_t* x, int n, int hw, int cp, int32_t* acc, uint32_t* amax, void* stream);
 /* its gradient: dx[img][p][c] = dy[img][c] */
 int niti_sum_pool_grad(const int8_t* dy, int n, int hw, int cp, int8_t* dx, void* stream);
+/* im2col of a shallow NHWC16 input (c_in <= 4; the ResNet-18 stem) for a conv run as a 1x1 conv over
+ * kp columns (kp % 16 == 0, kp >= kh * kw * c_in): xcol [n * oh * ow][kp], column k = (ky * kw + kx) *
+ * c_in + c, zero beyond kh * kw * c_in and outside the image (the weight [co][kp] in the same order). */
+int niti_im2col(const niti_geom* g, const int8_t* x, int kp, int8_t* xcol, void* stream);
 int niti_maxpool(const int8_t* x, int n, int h, int w, int cp, int k, int s, int p, int8_t* y, int oh, int ow,
                  void* stream);
 int niti_maxpool_grad(const int8_t* x, const int8_t* y, const int8_t* dy, int n, int h, int w, int cp, int k,

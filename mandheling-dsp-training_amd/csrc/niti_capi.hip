@@ -295,16 +295,30 @@ int niti_weights_to_wf(const int8_t* w, int co, int ci, int cip, int transpose, 
     return code(niti::weights_to_wf(w, co, ci, cip, transpose != 0, out, S(stream)));
 }
 
+int niti_conv_rows_nhwc_ok(const niti_geom* g, int dgrad) {
+    if (!g) return 0;
+    niti::ConvGeom r, d;
+    if (!to_geom(g, &r)) return 0;
+    const bool pd = dgrad & 2;  // bit 1: whether the model prefers it (not just whether it can)
+    if (!(dgrad & 1)) return (pd ? niti::rowconv_nhwc_pref(r) : niti::rowconv_nhwc_ok(r)) ? 1 : 0;
+    if (!niti::rowconv_dgrad_geom(r, &d)) return 0;
+    return (pd ? niti::rowconv_nhwc_pref(d) : niti::rowconv_nhwc_ok(d)) ? 1 : 0;
+}
+
 int niti_conv_fwd_rows(const niti_geom* g, const int8_t* x_c32, const int8_t* wf, const int8_t* exp_in,
                        const int8_t* wscale, int8_t* exp_out, int relu, int8_t* out, int8_t* pool_out,
                        int8_t* next_c32, int mode, uint32_t* amax, uint32_t* state, uint32_t epoch, uint32_t* err,
                        void* stream) {
+    const int x_nhwc = (mode & NITI_ROWS_X_NHWC16) ? 1 : 0;
+    mode &= ~NITI_ROWS_X_NHWC16;
     if (!g || !x_c32 || !wf || !amax || mode < 0 || mode > 2) return NITI_INVALID_VALUE;
     niti::ConvGeom r;
     if (!to_geom(g, &r)) return NITI_COMPUTE_SIZE_ERROR;
     if (!niti::rowconv_ok(r)) return NITI_NOT_SUPPORT;
+    if (x_nhwc && !niti::rowconv_nhwc_ok(r)) return NITI_NOT_SUPPORT;
     if (mode == 0 && !niti::rowconv_fused_ok(r)) return NITI_NOT_SUPPORT;
     niti::RowConvOut o;
+    o.x_nhwc = x_nhwc;
     o.out = out;
     o.pool_out = pool_out;
     o.next = next_c32;
@@ -319,6 +333,8 @@ int niti_conv_dgrad_rows(const niti_geom* g, const int8_t* dy_c32, const int8_t*
                          const int8_t* pool_x, const int8_t* pool_y, int pool_relu, int8_t* dx, int8_t* dx_c32,
                          int8_t* dx_p16, const int8_t* exp_in, const int8_t* wscale, int8_t* exp_out, int mode,
                          uint32_t* amax, uint32_t* state, uint32_t epoch, uint32_t* err, void* stream) {
+    const int x_nhwc = (mode & NITI_ROWS_X_NHWC16) ? 1 : 0;
+    mode &= ~NITI_ROWS_X_NHWC16;
     if (!g || !dy_c32 || !wft || !amax || mode < 0 || mode > 2) return NITI_INVALID_VALUE;
     if ((pool_x == nullptr) != (pool_y == nullptr) || (pool_x && relu_mask)) return NITI_INVALID_VALUE;
     if (mode != 1 && dx == nullptr) return NITI_INVALID_VALUE;
@@ -327,7 +343,9 @@ int niti_conv_dgrad_rows(const niti_geom* g, const int8_t* dy_c32, const int8_t*
     if (!niti::rowconv_dgrad_geom(r, &d)) return NITI_NOT_SUPPORT;
     if (mode == 0 && !niti::rowconv_fused_ok(d, true)) return NITI_NOT_SUPPORT;
     if (dx_p16 != nullptr && !niti::rowconv_p16_ok(d, pool_x != nullptr)) return NITI_NOT_SUPPORT;
+    if (x_nhwc && !niti::rowconv_nhwc_ok(d)) return NITI_NOT_SUPPORT;
     niti::RowConvOut o;
+    o.x_nhwc = x_nhwc;
     o.p16 = dx_p16;
     o.exp_in = exp_in;
     o.wscale = wscale;
@@ -344,6 +362,14 @@ int niti_conv_dgrad_rows(const niti_geom* g, const int8_t* dy_c32, const int8_t*
         o.relu_mask = relu_mask;
     }
     return code(niti::rowconv_fwd(d, dy_c32, wft, o, mode, amax, state, epoch, err, S(stream)));
+}
+
+int niti_im2col(const niti_geom* g, const int8_t* x, int kp, int8_t* xcol, void* stream) {
+    if (!g || !x || !xcol) return NITI_INVALID_VALUE;
+    niti::ConvGeom r;
+    if (!to_geom(g, &r)) return NITI_COMPUTE_SIZE_ERROR;
+    if (r.cip > 16 || r.c_in > 4 || kp % 16 != 0 || kp < r.kh * r.kw * r.c_in) return NITI_NOT_SUPPORT;
+    return code(niti::im2col_small(r, x, kp, xcol, S(stream)));
 }
 
 int niti_conv_fwd_phase1(const niti_geom* g, const int8_t* x, const int8_t* w, int32_t* acc, uint32_t* amax,
@@ -490,6 +516,12 @@ int niti_residual_add(const int8_t* a, const int8_t* ea, const int8_t* b, const 
 int niti_residual_requant(const int8_t* a, const int8_t* ea, const int8_t* b, const int8_t* eb, int64_t n,
                           const uint32_t* amax, int8_t* ez, int8_t* exp_out, int relu, int8_t* out, void* stream) {
     return code(niti::residual_requant(a, ea, b, eb, n, amax, ez, exp_out, relu, out, S(stream)));
+}
+int niti_residual_requant_relu_grad(const int8_t* a, const int8_t* ea, const int8_t* b, const int8_t* eb, int64_t n,
+                                    const uint32_t* amax, int8_t* ez, int8_t* exp_out, const int8_t* relu_mask,
+                                    int8_t* out, void* stream) {
+    if (!relu_mask) return NITI_INVALID_VALUE;
+    return code(niti::residual_requant(a, ea, b, eb, n, amax, ez, exp_out, 0, out, S(stream), relu_mask));
 }
 int niti_sum_pool(const int8_t* x, int n, int hw, int cp, int32_t* acc, uint32_t* amax, void* stream) {
     return code(niti::sum_pool(x, n, hw, cp, acc, amax, S(stream)));

@@ -1049,6 +1049,12 @@ struct WgTaps {
     int steps_total, steps_per_split;  // K steps of two region steps
     int tiles_ci, tiles;  // 32-channel input tiles; tiles per K split
     FastDiv fRW, fRPI, fPPI, fOW, fOHW, fTiles, fTci, fBPI;
+    // segment mode (maps whose rows are not whole 64-pixel steps: 224 / 112 / 56 / 28 / 14 px): a
+    // region step is 4 row segments of SW = 16 (or 14: two zero pixel slots) output pixels, each a
+    // 1 x 16 region image of 3 x 18 input pixels; segment gs = 4 step + s is row gs / NS (of all
+    // N * H rows), columns (gs % NS) * SW ...
+    int seg, SW, NS, nseg;  // NS segments per row, nseg = N * H * NS
+    FastDiv fNS, fH;
     unsigned long long* stamps;  // diagnostic builds (NITI_STAMPS): per-block s_memtime marks
     unsigned long long* span;    // kernel-span probe slot (probe_span_arm)
 };
@@ -1145,7 +1151,7 @@ __global__ void __launch_bounds__(TAPS_THREADS) wgrad_taps_kernel(WgTaps g, Epi 
     const int rpi = g.RH * g.RW;
     const bool xw = XPW == 2 || wid < 4;  // this wave's first DMA is a region chunk block
     const int xblk = XPW == 2 ? wid : (wid & 3);
-    int xrel = 0, xry = 0;
+    int xrel = 0, xry = 0, xseg = 0, xrx = 0;
     bool xok = false;
     {
         const int c = xblk * 64 + lane;
@@ -1153,13 +1159,19 @@ __global__ void __launch_bounds__(TAPS_THREADS) wgrad_taps_kernel(WgTaps g, Epi 
         const int img = (int)fdiv(g.fRPI, (uint32_t)q), rr = q - img * rpi;
         const int ry = (int)fdiv(g.fRW, (uint32_t)rr), rx = rr - ry * g.RW;
         const int ix = rx - g.pl;
-        xok = q < g.imgs * rpi && (unsigned)ix < (unsigned)g.W;
+        xok = q < g.imgs * rpi && (g.seg || (unsigned)ix < (unsigned)g.W);
         xry = ry;
-        xrel = ((img * g.H + ry) * g.W + ix) * g.CIP + 16 * (c & 1) + ci0;
+        xrel = g.seg ? 16 * (c & 1) + ci0 : ((img * g.H + ry) * g.W + ix) * g.CIP + 16 * (c & 1) + ci0;
+        xseg = img;
+        xrx = rx;
     }
     const int dch = (wid & 3) * 64 + lane;
     const int drow = dch >> 2;
-    const uint32_t dvo = (uint32_t)(drow * g.COP + co0 + 16 * ((dch & 3) ^ kt_swz<64>(drow)));
+    // segment mode, SW = 14: slot drow is pixel 14 (drow / 16) + drow % 16 of the step (slots 14 and
+    // 15 of a segment read zeros); SW = 16 is the plain 64-pixel run
+    const int dpx = g.seg && g.SW == 14 ? ((drow & 15) < 14 ? 14 * (drow >> 4) + (drow & 15) : -1) : drow;
+    const uint32_t dvo = dpx < 0 ? OOB : (uint32_t)(dpx * g.COP + co0 + 16 * ((dch & 3) ^ kt_swz<64>(drow)));
+    const uint32_t dstep = (uint32_t)(g.seg ? 4 * g.SW : 64) * (uint32_t)g.COP;  // dy bytes per region step
     const bool dw = XPW == 1 ? !xw : wid < 4;  // this wave loads a dy chunk block
 
     // LDS-DMA of region step `step` (block-relative) into `stage`; wave-uniform offsets from the
@@ -1167,15 +1179,26 @@ __global__ void __launch_bounds__(TAPS_THREADS) wgrad_taps_kernel(WgTaps g, Epi 
     auto issue = [&](int stage, int step) {
         int8_t* st0 = smem + stage * SB;
         const int r = s_begin + step;
-        const int q = (int)fdiv(g.fBPI, (uint32_t)r);
-        const int ybase = (r - q * g.BPI) * g.rows_per_step - g.pt;
-        const int ub = (q * g.imgs * g.H + ybase) * g.W * g.CIP;
-        if (xw) {
+        if (xw && g.seg) {
+            // the chunk's segment gs: image row `row` (of all N * H), columns from (gs % NS) * SW;
+            // region pixel (xry, xrx) is input (row + xry - 1, (gs % NS) * SW + xrx - 1), zero
+            // outside the image (pad 1, stride 1: output and input rows coincide)
+            const int gs = 4 * r + xseg;
+            const int row = (int)fdiv(g.fNS, (uint32_t)gs);
+            const int ix = (gs - row * g.NS) * g.SW + xrx - 1;
+            const int iy = row - (int)fdiv(g.fH, (uint32_t)row) * g.H + xry - 1;
+            const bool v = xok && gs < g.nseg && (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W;
+            const int a = ((row + xry - 1) * g.W + ix) * g.CIP + xrel;
+            if (NITI_ABLATE != 1 && NITI_ABLATE != 7) dma16(rX, st0 + xblk * 1024, v ? (uint32_t)a : OOB, 0u);
+        } else if (xw) {
+            const int q = (int)fdiv(g.fBPI, (uint32_t)r);
+            const int ybase = (r - q * g.BPI) * g.rows_per_step - g.pt;
+            const int ub = (q * g.imgs * g.H + ybase) * g.W * g.CIP;
             const bool v = xok && (unsigned)(ybase + xry) < (unsigned)g.H;
             if (NITI_ABLATE != 1 && NITI_ABLATE != 7) dma16(rX, st0 + xblk * 1024, v ? (uint32_t)(ub + xrel) : OOB, 0u);
         }
         if (dw) {
-            if (NITI_ABLATE != 1 && NITI_ABLATE != 7) dma16(rD, st0 + XB + (wid & 3) * 1024, dvo, (uint32_t)r * 64u * (uint32_t)g.COP);
+            if (NITI_ABLATE != 1 && NITI_ABLATE != 7) dma16(rD, st0 + XB + (wid & 3) * 1024, dvo, (uint32_t)r * dstep);
         } else if (XPW == 2) {
             if (NITI_ABLATE != 1 && NITI_ABLATE != 7) dma16(rD, st0 + XB + DB + (wid & 3) * 1024, OOB, 0u);
         }
@@ -1857,24 +1880,41 @@ static bool wgrad_taps_geom(const ConvGeom& g, const int8_t* x, const int8_t* dy
     const int64_t ohw = (int64_t)g.oh * g.ow;
     const int64_t K = (int64_t)g.n * ohw;
     const int64_t xbytes = (int64_t)g.n * g.h * g.w * g.cip, dybytes = K * g.cop;
-    if (K % 64 != 0 || xbytes >= (int64_t)OOB || dybytes >= (int64_t)OOB) return false;
+    if (xbytes >= (int64_t)OOB || dybytes >= (int64_t)OOB) return false;
     WgTaps w{};
+    // segment mode: rows of 16-pixel (or 14-pixel) segments, pad 1 (output rows = input rows); only
+    // shallow inputs (cip <= 64), where it measured faster in the VGG-16 step than the K-major GEMM
+    // (conv1_2 180 vs 378 us, conv2_1 93 vs 106 us; at cip 128 - 512 it was 13 - 40 % slower with
+    // cold operands, tools/gpu_r04g.sh)
+    const int sw = g.ow % 16 == 0 ? 16 : (g.ow % 14 == 0 ? 14 : 0);
+    const bool seg_ok = sw > 0 && g.cip <= 64 && g.oh == g.h && g.ow == g.w && g.pt == 1 && g.pl == 1 && g.pb == 1 && g.pr == 1 &&
+                        g.kh == 3 && g.kw == 3 && !getenv("NITI_DIAG_NO_TAPS_SEG");
     if (64 % g.ow == 0 && ohw % 64 == 0) {
         w.band = 1;
         w.rows_per_step = 64 / g.ow;
         w.RH = w.rows_per_step + g.kh - 1;
         w.imgs = 1;
         w.PPI = 64;
-    } else if (64 % ohw == 0) {
+    } else if (64 % ohw == 0 && K % 64 == 0) {
         w.band = 0;
         w.rows_per_step = 0;
         w.RH = g.oh + g.kh - 1;
         w.imgs = (int)(64 / ohw);
         w.PPI = (int)ohw;
+    } else if (seg_ok) {
+        w.seg = 1;
+        w.SW = sw;
+        w.NS = g.ow / sw;
+        w.nseg = g.n * g.oh * w.NS;
+        w.band = 0;
+        w.rows_per_step = 0;
+        w.RH = 3;
+        w.imgs = 4;
+        w.PPI = 16;
     } else {
         return false;
     }
-    w.RW = g.ow + g.kw - 1;
+    w.RW = (w.seg ? 16 : g.ow) + g.kw - 1;
     if (w.imgs * w.RH * w.RW > 256) return false;  // region rows (XPW <= 2)
     w.x = x;
     w.dy = dy;
@@ -1890,7 +1930,7 @@ static bool wgrad_taps_geom(const ConvGeom& g, const int8_t* x, const int8_t* dy
     w.pt = g.pt;
     w.pl = g.pl;
     w.c_out = g.c_out;
-    w.rs_total = (int)(K / 64);
+    w.rs_total = w.seg ? (w.nseg + 3) / 4 : (int)(K / 64);
     w.steps_total = w.rs_total;
     w.steps_per_split = w.steps_total;
     w.tiles_ci = g.cip / 32;
@@ -1898,7 +1938,12 @@ static bool wgrad_taps_geom(const ConvGeom& g, const int8_t* x, const int8_t* dy
     w.fRW = make_fastdiv((uint32_t)w.RW);
     w.fRPI = make_fastdiv((uint32_t)(w.RH * w.RW));
     w.fPPI = make_fastdiv((uint32_t)w.PPI);
-    w.fOW = make_fastdiv((uint32_t)g.ow);
+    w.fOW = make_fastdiv((uint32_t)(w.seg ? 16 : g.ow));
+    if (w.seg) {  // a region image is one 16-slot segment
+        w.OW = 16;
+        w.fNS = make_fastdiv((uint32_t)w.NS);
+        w.fH = make_fastdiv((uint32_t)g.h);
+    }
     w.fOHW = make_fastdiv((uint32_t)ohw);
     w.fTiles = make_fastdiv((uint32_t)w.tiles);
     w.fTci = make_fastdiv((uint32_t)w.tiles_ci);
@@ -2696,7 +2741,8 @@ __global__ void __launch_bounds__(256) residual_requant_kernel(const int8_t* __r
                                                                const int8_t* __restrict__ b, const int8_t* __restrict__ eb,
                                                                int64_t n16, const uint32_t* __restrict__ amax,
                                                                int8_t* __restrict__ ez, int8_t* __restrict__ exp_out,
-                                                               int relu, int8_t* __restrict__ out) {
+                                                               int relu, const int8_t* __restrict__ relu_mask,
+                                                               int8_t* __restrict__ out) {
     const int xa = *ea, xb = *eb;
     const bool a_hi = xa >= xb;
     const int diff = a_hi ? xa - xb : xb - xa;
@@ -2712,12 +2758,15 @@ __global__ void __launch_bounds__(256) residual_requant_kernel(const int8_t* __r
     }
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += (int64_t)gridDim.x * 256) {
         const v16c va = ((const v16c*)a)[i], vb = ((const v16c*)b)[i];
+        v16c mk;
+        if (relu_mask != nullptr) mk = ((const v16c*)relu_mask)[i];
         v16c q;
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
             const int32_t z = residual_z(a_hi ? va[e] : vb[e], a_hi ? vb[e] : va[e], d, r);
             int32_t o = raw ? (int32_t)(int8_t)z : psto_fast(z, s);
             if (relu && o < 0) o = 0;
+            if (relu_mask != nullptr && mk[e] <= 0) o = 0;  // the next op's NITI_ReluGrad_Int8, fused
             q[e] = (signed char)o;
         }
         ((v16c*)out)[i] = q;
@@ -2725,13 +2774,14 @@ __global__ void __launch_bounds__(256) residual_requant_kernel(const int8_t* __r
 }
 
 hipError_t residual_requant(const int8_t* a, const int8_t* ea, const int8_t* b, const int8_t* eb, int64_t n,
-                            const uint32_t* amax, int8_t* ez, int8_t* exp_out, int relu, int8_t* out, hipStream_t st) {
+                            const uint32_t* amax, int8_t* ez, int8_t* exp_out, int relu, int8_t* out, hipStream_t st,
+                            const int8_t* relu_mask) {
     if (n < 0 || n % 16 != 0 || !a || !b || !ea || !eb || !amax || !out) return hipErrorInvalidValue;
     const int64_t n16 = n / 16;
     int64_t blocks = (n16 + 255) / 256;
     blocks = blocks < 1 ? 1 : blocks > 2048 ? 2048 : blocks;
     hipLaunchKernelGGL(residual_requant_kernel, dim3((unsigned)blocks), dim3(256), 0, st, a, ea, b, eb, n16, amax, ez,
-                       exp_out, relu, out);
+                       exp_out, relu, relu_mask, out);
     return hipGetLastError();
 }
 

@@ -117,10 +117,12 @@ hipError_t residual_add(const int8_t* a, const int8_t* ea, const int8_t* b, cons
 // the fused form: z recomputed from a, b and requantised with the range in amax (from residual_add
 // with z = null); out int8 (n elements), *ez and *exp_out = *ez + inc (either may be null)
 hipError_t residual_requant(const int8_t* a, const int8_t* ea, const int8_t* b, const int8_t* eb, int64_t n,
-                            const uint32_t* amax, int8_t* ez, int8_t* exp_out, int relu, int8_t* out, hipStream_t st);
+                            const uint32_t* amax, int8_t* ez, int8_t* exp_out, int relu, int8_t* out, hipStream_t st,
+                            const int8_t* relu_mask = nullptr);
 // acc[n][cp] = sum over hw pixels of x NHWC16 (+ max into amax); its gradient: dy broadcast
 hipError_t sum_pool(const int8_t* x, int n, int hw, int cp, int32_t* acc, uint32_t* amax, hipStream_t st);
 hipError_t sum_pool_grad(const int8_t* dy, int n, int hw, int cp, int8_t* dx, hipStream_t st);
+hipError_t im2col_small(const ConvGeom& g, const int8_t* x, int kp, int8_t* xcol, hipStream_t st);
 // ---- weight gradient on P16 pixel blocks (niti_wgrad.hip) --------------------------------
 // P16: [pixels/16][Cp][16] int8 (Cp % 16 == 0, pixels % 16 == 0)
 hipError_t nhwc16_to_p16(const int8_t* in, int64_t pixels, int cp, int8_t* out, hipStream_t st);
@@ -231,8 +233,13 @@ struct RowConvOut {
     // launch also stores every unit's int32 accumulators here (rowconv_acc_bytes) and the
     // requantise launch reads them back instead of recomputing the GEMM
     int32_t* acc_store = nullptr;
+    // input layout: 0 C32 [n][C/32][H][W][32]; 1 NHWC16 [n][H][W][cip] (row-segment maps, cip % 32
+    // == 0: read in place, no C32 copy)
+    int x_nhwc = 0;
 };
 size_t rowconv_acc_bytes(const ConvGeom& g, bool dg);
+bool rowconv_nhwc_ok(const ConvGeom& g);
+bool rowconv_nhwc_pref(const ConvGeom& g);
 constexpr int ROWCONV_BAR_WORDS = 2 * 19 * 32;  // grid-barrier state (both parities)
 static_assert(ROWCONV_BAR_WORDS == NITI_ROWCONV_STATE_WORDS, "header constant");
 bool rowconv_ok(const ConvGeom& g);

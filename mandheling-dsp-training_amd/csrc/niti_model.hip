@@ -931,7 +931,7 @@ int Model::fwd_layer(int i, hipStream_t st) {
         o.exp_out = l.exp;
         o.pool.pool_out = l.pool ? l.p : nullptr;
         // the (pooled) output also as the next layer's C32 input when it runs on the row kernel
-        const bool next_c32 = i + 1 < (int)L.size() && rowconv_layer(i + 1);
+        const bool next_c32 = i + 1 < (int)L.size() && rowconv_layer(i + 1) && !rowconv_nhwc_pref(L[i + 1].g);
         if (!conv0_ranged) MTRY(conv0_fwd(g, l.in, l.w, rng(i, 0), o, 0, st));
         conv0_ranged = false;
         if (dp && exact) CTRY(coll->allreduce(rng(i, 0), MAX_WORDS, COLL_MAX_U32, st));
@@ -964,26 +964,31 @@ int Model::fwd_layer(int i, hipStream_t st) {
         // register-fed forward, rescale fused: one launch with an in-kernel grid barrier (single
         // device, every workgroup resident, not inside a graph capture), else a range launch,
         // [all-reduce MAX], and a recompute-and-requantise launch
-        if (!xc32_valid[i]) {
+        // a row-segment layer reads its NHWC16 input in place; the others their C32 copy
+        const bool xn = rowconv_nhwc_pref(g);
+        if (!xn && !xc32_valid[i]) {
             MTRY(nhwc16_to_c32(l.in, n, g.h * g.w, g.cip, g.c_in, l.xc32, st));
             xc32_valid[i] = 1;
         }
+        const int8_t* xin = xn ? l.in : l.xc32;
         RowConvOut o;
+        o.x_nhwc = xn ? 1 : 0;
         o.out = l.r;
         o.pool_out = l.pool ? l.p : nullptr;
-        const bool feeds_next = i + 1 < (int)L.size() && rowconv_layer(i + 1) && !l.flatten;
+        const bool feeds_next = i + 1 < (int)L.size() && rowconv_layer(i + 1) && !l.flatten &&
+                                !rowconv_nhwc_pref(L[i + 1].g);
         o.next = feeds_next ? L[i + 1].xc32 : nullptr;
         o.exp_in = i == 0 ? exp0 : L[i - 1].exp;
         o.wscale = l.ws_dev;
         o.exp_out = l.exp;
         o.relu = l.relu;
         if (!dp && !capturing && rowconv_fused_ok(g)) {
-            MTRY(rowconv_fwd(g, l.xc32, l.wf, o, 0, rng(i, 0), l.bar, ++l.epoch, rc_err, st));
+            MTRY(rowconv_fwd(g, xin, l.wf, o, 0, rng(i, 0), l.bar, ++l.epoch, rc_err, st));
         } else {
             o.acc_store = rowconv_acc_bytes(g, false) ? rc_acc : nullptr;  // else the requantise launch recomputes
-            MTRY(rowconv_fwd(g, l.xc32, l.wf, o, 1, rng(i, 0), nullptr, 0, nullptr, st));
+            MTRY(rowconv_fwd(g, xin, l.wf, o, 1, rng(i, 0), nullptr, 0, nullptr, st));
             if (dp && exact) CTRY(coll->allreduce(rng(i, 0), MAX_WORDS, COLL_MAX_U32, st));
-            MTRY(rowconv_fwd(g, l.xc32, l.wf, o, 2, rng(i, 0), nullptr, 0, nullptr, st));
+            MTRY(rowconv_fwd(g, xin, l.wf, o, 2, rng(i, 0), nullptr, 0, nullptr, st));
         }
         if (feeds_next) xc32_valid[i + 1] = 1;
         probe(i, 0, false, st);
@@ -1104,7 +1109,7 @@ int Model::dgrad_layer(int i, hipStream_t st) {
         // the head's input gradient on the row kernel (W = 1), into the previous layer's relu or
         // 2x2-pool gradient (+ its C32 / P16 copies)
         RowConvOut o;
-        int8_t* next = rowconv_dgrad_layer(i - 1) ? pv.dyc32 : nullptr;
+        int8_t* next = rowconv_dgrad_layer(i - 1) && !rowconv_nhwc_pref(pv.dg) ? pv.dyc32 : nullptr;
         if (pv.pool) {
             o.pool_x = pv.r;
             o.pool_y = pv.p;
@@ -1135,12 +1140,18 @@ int Model::dgrad_layer(int i, hipStream_t st) {
     if (rowconv_dgrad_layer(i)) {
         // register-fed input gradient, its requantisation and the previous layer's relu / pool
         // gradient fused; the previous layer's dy also in C32 when its own input gradient runs here
-        if (!dyc32_valid[i]) {
+        const ConvGeom& d = l.dg;
+        // a row-segment input gradient reads dy (NHWC16) in place; the others its C32 copy
+        const bool xn = rowconv_nhwc_pref(d);
+        if (xn && !dy16_valid[i]) MTRY(c32_to_nhwc16(l.dyc32, n, g.oh * g.ow, g.cop, g.c_out, l.dy, st));
+        if (!xn && !dyc32_valid[i]) {
             MTRY(nhwc16_to_c32(l.dy, n, g.oh * g.ow, g.cop, g.c_out, l.dyc32, st));
             dyc32_valid[i] = 1;
         }
+        const int8_t* dyin = xn ? l.dy : l.dyc32;
         RowConvOut o;
-        int8_t* next = rowconv_dgrad_layer(i - 1) ? pv.dyc32 : nullptr;
+        o.x_nhwc = xn ? 1 : 0;
+        int8_t* next = rowconv_dgrad_layer(i - 1) && !rowconv_nhwc_pref(pv.dg) ? pv.dyc32 : nullptr;
         // the previous layer's P16 dy for its weight gradient, when the launch's pixels make whole
         // 16-pixel blocks; else wgrad_layer converts
         o.p16 = fuse_dp16 && wgrad_p16_splits(i - 1) > 0 && rowconv_p16_ok(l.dg, pv.pool) ? dp16[i - 1] : nullptr;
@@ -1158,14 +1169,13 @@ int Model::dgrad_layer(int i, hipStream_t st) {
             o.relu_mask = pv.relu ? pv.r : nullptr;
         }
         dy16_valid[i - 1] = !skip16;
-        const ConvGeom& d = l.dg;
         if (!dp && !capturing && rowconv_fused_ok(d, true)) {
-            MTRY(rowconv_fwd(d, l.dyc32, l.wft, o, 0, rng(i, 1), l.bar, ++l.epoch, rc_err, st));
+            MTRY(rowconv_fwd(d, dyin, l.wft, o, 0, rng(i, 1), l.bar, ++l.epoch, rc_err, st));
         } else {
             o.acc_store = rowconv_acc_bytes(d, true) ? rc_acc : nullptr;
-            MTRY(rowconv_fwd(d, l.dyc32, l.wft, o, 1, rng(i, 1), nullptr, 0, nullptr, st));
+            MTRY(rowconv_fwd(d, dyin, l.wft, o, 1, rng(i, 1), nullptr, 0, nullptr, st));
             if (dp && exact) CTRY(coll->allreduce(rng(i, 1), MAX_WORDS, COLL_MAX_U32, st));
-            MTRY(rowconv_fwd(d, l.dyc32, l.wft, o, 2, rng(i, 1), nullptr, 0, nullptr, st));
+            MTRY(rowconv_fwd(d, dyin, l.wft, o, 2, rng(i, 1), nullptr, 0, nullptr, st));
         }
         probe(i, 1, false, st);
         dp16_valid[i - 1] = o.p16 != nullptr ? 1 : 0;

@@ -113,4 +113,61 @@ hipError_t sum_pool_grad(const int8_t* dy, int n, int hw, int cp, int8_t* dx, hi
     return hipGetLastError();
 }
 
+// im2col of a shallow input (NHWC16, c_in <= 4: the ResNet stem's 3 channels) for a conv that
+// then runs as a 1x1 conv over kp columns: xcol[p][k], k = (ky * KW + kx) * c_in + c for
+// k < KH * KW * c_in, zero beyond and outside the image.  One workgroup per output row: the KH
+// input rows it reads are staged once in LDS as packed c_in-byte pixels (a dword load per input
+// pixel: 4 of its 16 bytes), then every thread builds 16-byte output chunks from LDS bytes (a
+// byte gather straight from HBM / L2 per output byte ran ~9x slower).  KH, KW, C as template
+// arguments (the stem's 7, 7, 3) make the byte -> (tap, channel) map compile-time; 0 = run time.
+constexpr int IM2COL_LDS = 16384;
+template <int KH_, int KW_, int C_>
+__global__ void __launch_bounds__(256) im2col_small_kernel(const int8_t* __restrict__ x, ConvGeom g, int kp,
+                                                           int8_t* __restrict__ xcol) {
+    __shared__ int8_t tile[IM2COL_LDS];
+    const int KH = KH_ ? KH_ : g.kh, KW = KW_ ? KW_ : g.kw, C = C_ ? C_ : g.c_in;
+    const int row = blockIdx.x;  // n * oh + oy
+    const int n = row / g.oh, oy = row - n * g.oh;
+    const int cols = (g.ow - 1) * g.sw + (KW - 1) * g.dw + 1;  // input columns the row reads
+    for (int e = threadIdx.x; e < KH * cols; e += 256) {
+        const int ky = e / cols, cx = e - ky * cols;
+        const int iy = oy * g.sh + ky * g.dh - g.pt, ix = cx - g.pl;
+        uint32_t v = 0;
+        if ((unsigned)iy < (unsigned)g.h && (unsigned)ix < (unsigned)g.w)
+            v = *(const uint32_t*)(x + (((int64_t)n * g.h + iy) * g.w + ix) * g.cip);
+#pragma unroll
+        for (int c = 0; c < (C_ ? C_ : 4); ++c)
+            if (C_ || c < C) tile[e * C + c] = (int8_t)(v >> (8 * c));
+    }
+    __syncthreads();
+    const int kc = kp / 16, kt = KH * KW * C;
+    int8_t* out = xcol + (int64_t)row * g.ow * kp;
+    for (int e = threadIdx.x; e < g.ow * kc; e += 256) {
+        const int ox = e / kc, j = e - ox * kc;
+        v16c o;
+#pragma unroll
+        for (int b = 0; b < 16; ++b) {
+            const int k = 16 * j + b;
+            const int tap = k / C, c = k - tap * C;
+            const int ky = tap / KW, kx = tap - ky * KW;
+            o[b] = k < kt ? tile[(ky * cols + ox * g.sw + kx * g.dw) * C + c] : (int8_t)0;
+        }
+        *(v16c*)(out + (int64_t)ox * kp + 16 * j) = o;
+    }
+}
+
+hipError_t im2col_small(const ConvGeom& g, const int8_t* x, int kp, int8_t* xcol, hipStream_t st) {
+    if (kp % 16 != 0 || kp < g.kh * g.kw * g.c_in || g.c_in > 4 || g.cip > 16) return hipErrorInvalidValue;
+    const int cols = (g.ow - 1) * g.sw + (g.kw - 1) * g.dw + 1;
+    if ((int64_t)g.kh * cols * g.c_in > IM2COL_LDS) return hipErrorInvalidValue;
+    const int64_t rows = (int64_t)g.n * g.oh;
+    if (rows == 0) return hipSuccess;
+    if (rows > 0x7fffffff) return hipErrorInvalidValue;
+    if (g.kh == 7 && g.kw == 7 && g.c_in == 3)
+        hipLaunchKernelGGL((im2col_small_kernel<7, 7, 3>), dim3((unsigned)rows), dim3(256), 0, st, x, g, kp, xcol);
+    else
+        hipLaunchKernelGGL((im2col_small_kernel<0, 0, 0>), dim3((unsigned)rows), dim3(256), 0, st, x, g, kp, xcol);
+    return hipGetLastError();
+}
+
 }  // namespace niti

@@ -202,6 +202,10 @@ struct RowConvArgs {
     // 7-px rows of two images per 16 lanes), nsp segment pairs per row, upc4 units per co block
     // rounded up to whole workgroups of 4
     int hw, gw, nsp, upc4;
+    // the row-segment form's input layout as byte strides: pixel, image row, image, 32-channel
+    // chunk -- C32 (32, W*32, CB*H*W*32, H*W*32) or NHWC16 with cip % 32 == 0 (cip, W*cip,
+    // H*W*cip, 32: a lane's 16 bytes are still one pixel's 16 channels, so no C32 copy is needed)
+    uint32_t xps, xrs, xis, xcs;
 };
 
 // diagnostic stamps, 16 per wave: [0] start, [1] prologue issued, [2] cycles issuing loads, [3] K
@@ -317,9 +321,11 @@ __device__ __forceinline__ void rowconv_compute(const RowConvArgs& a, const RowU
     const int h = lane >> 5, c = lane & 31, ox = W == 0 ? U.x : c % WS;
     const __amdgpu_buffer_rsrc_t rX = make_rsrc(a.x, a.xbytes);
     const __amdgpu_buffer_rsrc_t rW = make_rsrc(a.wf, a.wbytes);
-    const uint32_t xl =
-        U.img_ok && U.x_ok ? (uint32_t)((((int64_t)U.img * a.CB * H) * WR + ox) * 32 + 16 * h) : OOB;
-    const uint32_t CHUNK = (uint32_t)H * WR * 32;
+    const uint32_t xl = !(U.img_ok && U.x_ok) ? OOB
+                        : W == 0 ? (uint32_t)U.img * a.xis + (uint32_t)ox * a.xps + 16u * h
+                                 : (uint32_t)((((int64_t)U.img * a.CB * H) * WR + ox) * 32 + 16 * h);
+    const uint32_t CHUNK = W == 0 ? a.xcs : (uint32_t)H * WR * 32;
+    const uint32_t XROW = W == 0 ? a.xrs : (uint32_t)WR * 32;
     const int y0 = U.b * R - 1;
 #pragma unroll
     for (int r = 0; r < R; ++r)
@@ -331,8 +337,8 @@ __device__ __forceinline__ void rowconv_compute(const RowConvArgs& a, const RowU
     for (int j = 0; j < NR; ++j) {
         const int iy = y0 + j;
         const bool row_ok = iy >= 0 && iy < H && xl != OOB;
-        const uint32_t base = xl + (uint32_t)iy * WR * 32;
-        off[0][j] = row_ok && ox > 0 ? base - 32u : OOB;
+        const uint32_t base = xl + (uint32_t)iy * XROW;
+        off[0][j] = row_ok && ox > 0 ? base - 32u : OOB;  // (unused: DPPX)
         off[1][j] = row_ok ? base : OOB;
         off[2][j] = row_ok && ox < WR - 1 ? base + 32u : OOB;
     }
@@ -1064,7 +1070,7 @@ __device__ __forceinline__ void seg_run(const RowConvArgs& a, int lane, int wid,
     const int h = lane >> 5, c = lane & 31;
     const __amdgpu_buffer_rsrc_t rX = make_rsrc(a.x, a.xbytes);
     const __amdgpu_buffer_rsrc_t rW = make_rsrc(a.wf, a.wbytes);
-    const uint32_t CHUNK = (uint32_t)H * W * 32;
+    const uint32_t CHUNK = a.xcs;
     const int ntiles = (int)blockIdx.x < a.wgs ? (a.wgs - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
     const int total = ntiles * CB;
     const int steps = (total + S - 1) / S * S;  // whole ring turns: straight-line steps
@@ -1083,11 +1089,11 @@ __device__ __forceinline__ void seg_run(const RowConvArgs& a, int lane, int wid,
             return;
         }
         const RowUnit<0, R> U(a, tile_wg(k), wid, c, false);
-        const uint32_t xl = U.img_ok && U.x_ok ? (uint32_t)((((int64_t)U.img * CB * H) * W + U.x) * 32 + 16 * h) : OOB;
+        const uint32_t xl = U.img_ok && U.x_ok ? (uint32_t)U.img * a.xis + (uint32_t)U.x * a.xps + 16u * h : OOB;
 #pragma unroll
         for (int j = 0; j < NR; ++j) {
             const int iy = U.b * R - 1 + j;
-            ioff[j] = xl != OOB && iy >= 0 && iy < H ? xl + (uint32_t)iy * W * 32 : OOB;
+            ioff[j] = xl != OOB && iy >= 0 && iy < H ? xl + (uint32_t)iy * a.xrs : OOB;
         }
         iwb = (uint32_t)(U.cob * CB * 9) * 1024u;
     };
@@ -1459,6 +1465,17 @@ bool rowconv_ok(const ConvGeom& g) {
 
 static bool rowconv_seg(const ConvGeom& g) { return g.w > 16 || g.w == 14; }
 
+// the row-segment form can read its input as NHWC16 in place (RowConvOut::x_nhwc) ...
+bool rowconv_nhwc_ok(const ConvGeom& g) { return rowconv_ok(g) && rowconv_seg(g) && g.cip % 32 == 0; }
+// ... and the model does where that is not slower than a C32 copy: 64 channels (a wave load then
+// spans whole 128-byte lines, half used per chunk; VGG-16 conv1_2 / conv2_1 as fast as from C32,
+// conv0's C32 copy and a layout pass saved), not 128 (conv2_2 1.3-1.4x slower, tools/gpu_r04k.sh);
+// NITI_SEG_NHWC_MAX_CIP overrides (A/B)
+bool rowconv_nhwc_pref(const ConvGeom& g) {
+    static const int v = getenv("NITI_SEG_NHWC_MAX_CIP") ? atoi(getenv("NITI_SEG_NHWC_MAX_CIP")) : 64;
+    return rowconv_nhwc_ok(g) && g.cip <= v;
+}
+
 // the row-segment form's launch shape: 4 rows per band (2 at 14 px), units of 28 px (two 14-px
 // segments of one row, or one 14-px row of two images), whole workgroups of 4 units per co block
 struct SegPlan {
@@ -1482,7 +1499,11 @@ static SegPlan seg_plan(const ConvGeom& g) {
 // the row-segment form keeps its int32 accumulators between the range and requantise launches
 // only where the GEMM is deep (K = 9 c_in >= 2304): recomputing 2 M N K ops costs more there than
 // the 8 bytes per output of an int32 round trip; shallower layers recompute (no int32 tensor)
-static bool seg_store_acc(const ConvGeom& g) { return g.c_in >= 256; }
+static int acc_min_cin() {  // NITI_RC_ACC_MIN_CIN overrides (A/B diagnostics)
+    static const int v = getenv("NITI_RC_ACC_MIN_CIN") ? atoi(getenv("NITI_RC_ACC_MIN_CIN")) : 256;
+    return v;
+}
+static bool seg_store_acc(const ConvGeom& g) { return g.c_in >= acc_min_cin(); }
 
 bool rowconv_dgrad_geom(const ConvGeom& l, ConvGeom* d) {
     if (!rowconv_ok(l)) return false;
@@ -1524,6 +1545,10 @@ size_t rowconv_acc_bytes(const ConvGeom& g, bool dg) {
         const SegPlan p = seg_plan(g);
         return seg_store_acc(g) ? (size_t)p.wgs * 4 * p.R * 1024 * sizeof(int32_t) : 0;
     }
+    // the W > 0 forms (VGG-11's data-parallel path) store at every depth: recomputing VGG-11's
+    // conv1 / conv2 (c_in 64 / 128) in the requantise launch measured no faster (--dp-path 0.578 vs
+    // 0.575 ms per step); NITI_RC_ACC_MIN_CIN applies the row-segment rule here too (A/B)
+    if (getenv("NITI_RC_ACC_MIN_CIN") != nullptr && g.c_in < acc_min_cin()) return 0;
     int u = 0;
     const int R = rowconv_rows(g, dg, &u);
     const int G = 32 / g.w, ngb = ((g.n + G - 1) / G) * (g.h / R), ngb4 = (ngb + 3) / 4 * 4, COB = g.cop / 32;
@@ -1691,9 +1716,22 @@ hipError_t rowconv_fwd(const ConvGeom& g, const int8_t* x_c32, const int8_t* wf,
         return hipErrorInvalidValue;
     RowConvArgs a{};
     const int CB = (g.c_in + 31) / 32, COB = g.cop / 32;
-    const int64_t xb = (int64_t)g.n * CB * g.h * g.w * 32;
+    // the row-segment form may read x as NHWC16 (o.x_nhwc; cip a multiple of 32)
+    if (o.x_nhwc && (!rowconv_seg(g) || g.cip % 32 != 0)) return hipErrorInvalidValue;
+    const int64_t xb = o.x_nhwc ? (int64_t)g.n * g.h * g.w * g.cip : (int64_t)g.n * CB * g.h * g.w * 32;
     const int64_t wb = (int64_t)COB * CB * 9 * 1024;
     if (xb > 0x7fffffff || wb > 0x7fffffff) return hipErrorInvalidValue;
+    if (o.x_nhwc) {
+        a.xps = (uint32_t)g.cip;
+        a.xrs = (uint32_t)(g.w * g.cip);
+        a.xis = (uint32_t)(g.h * g.w * g.cip);
+        a.xcs = 32u;
+    } else {
+        a.xps = 32u;
+        a.xrs = (uint32_t)(g.w * 32);
+        a.xis = (uint32_t)(CB * g.h * g.w * 32);
+        a.xcs = (uint32_t)(g.h * g.w * 32);
+    }
     a.x = x_c32;
     a.wf = wf;
     a.xbytes = (uint32_t)xb;

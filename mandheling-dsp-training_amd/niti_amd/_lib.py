@@ -146,8 +146,11 @@ def lib():
         "niti_ohwi16_to_oihw": (ci, [vp, ci, ci, ci, ci, vp, vp]),
         "niti_residual_add": (ci, [vp, vp, vp, vp, i64, vp, vp, vp, vp]),
         "niti_residual_requant": (ci, [vp, vp, vp, vp, i64, vp, vp, vp, ci, vp, vp]),
+        "niti_residual_requant_relu_grad": (ci, [vp, vp, vp, vp, i64, vp, vp, vp, vp, vp, vp]),
         "niti_sum_pool": (ci, [vp, ci, ci, ci, vp, vp, vp]),
         "niti_sum_pool_grad": (ci, [vp, ci, ci, ci, vp, vp]),
+        "niti_im2col": (ci, [C.POINTER(Geom), vp, ci, vp, vp]),
+        "niti_conv_rows_nhwc_ok": (ci, [C.POINTER(Geom), ci]),
         "niti_maxpool": (ci, [vp] + [ci] * 7 + [vp, ci, ci, vp]),
         "niti_maxpool_grad": (ci, [vp, vp, vp] + [ci] * 10 + [vp, vp]),
         "niti_maxpool_grad_ws": (ci, [vp, vp, vp] + [ci] * 10 + [vp, vp, vp]),

@@ -235,10 +235,20 @@ class RowConvState:
         self.epoch = 0
 
 
+ROWS_X_NHWC16 = 0x100  # NITI_ROWS_X_NHWC16
+
+
+def rows_nhwc_ok(g: L.Geom, dgrad=False, preferred=False) -> bool:
+    """Whether the row kernel takes its input as NHWC16 in place (row-segment maps, cip % 32 == 0);
+    preferred: whether that is the faster choice too (64-channel inputs)."""
+    return bool(L.lib().niti_conv_rows_nhwc_ok(C.byref(g), (1 if dgrad else 0) | (2 if preferred else 0)))
+
+
 def conv_fwd_rows(g: L.Geom, xc32, wf, amax, mode=0, state: RowConvState | None = None, exp_in=None, wscale=None,
-                  exp_out=None, relu=False, pool=False, next_c32=False, stream=None):
+                  exp_out=None, relu=False, pool=False, next_c32=False, x_nhwc=False, stream=None):
     """The register-fed forward (niti_conv_fwd_rows): (out NHWC16, pooled NHWC16 or None,
-    next C32 or None).  mode 0 fused (state required), 1 range only, 2 requantise with amax."""
+    next C32 or None).  mode 0 fused (state required), 1 range only, 2 requantise with amax.
+    x_nhwc: xc32 is the NHWC16 input itself (rows_nhwc_ok)."""
     dev = xc32.device
     out = None if mode == 1 else torch.empty((g.n, g.oh, g.ow, g.cop), dtype=torch.int8, device=dev)
     pout = torch.empty((g.n, g.oh // 2, g.ow // 2, g.cop), dtype=torch.int8, device=dev) if pool and mode != 1 else None
@@ -252,14 +262,15 @@ def conv_fwd_rows(g: L.Geom, xc32, wf, amax, mode=0, state: RowConvState | None 
         state.epoch += 1
         epoch, st_ptr, err_ptr = state.epoch, _ptr(state.state), _ptr(state.err)
     check(L.lib().niti_conv_fwd_rows(C.byref(g), _ptr(xc32), _ptr(wf), _ptr(exp_in), _ptr(wscale), _ptr(exp_out),
-                                     1 if relu else 0, _ptr(out), _ptr(pout), _ptr(nxt), mode, _ptr(amax), st_ptr,
+                                     1 if relu else 0, _ptr(out), _ptr(pout), _ptr(nxt),
+                                     mode | (ROWS_X_NHWC16 if x_nhwc else 0), _ptr(amax), st_ptr,
                                      epoch, err_ptr, _stream(stream)), "conv_fwd_rows")
     return out, pout, nxt
 
 
 def conv_dgrad_rows(g: L.Geom, dyc32, wft, amax, mode=0, state: RowConvState | None = None, relu_mask=None,
                     pool_x=None, pool_y=None, pool_relu=False, dx_c32=False, dx_p16=False, exp_in=None, wscale=None,
-                    exp_out=None, stream=None):
+                    exp_out=None, x_nhwc=False, stream=None):
     """The input gradient on the register-fed kernel (niti_conv_dgrad_rows) for the layer of
     geometry g: (dx NHWC16, dx C32 or None, dx P16 or None).  dx is [n][h][w][cip], or
     [n][2h][2w][cip] routed through the previous layer's 2x2 max pool when pool_x / pool_y are
@@ -276,7 +287,8 @@ def conv_dgrad_rows(g: L.Geom, dyc32, wft, amax, mode=0, state: RowConvState | N
         epoch, st_ptr, err_ptr = state.epoch, _ptr(state.state), _ptr(state.err)
     check(L.lib().niti_conv_dgrad_rows(C.byref(g), _ptr(dyc32), _ptr(wft), _ptr(relu_mask), _ptr(pool_x),
                                        _ptr(pool_y), 1 if pool_relu else 0, _ptr(dx), _ptr(nxt), _ptr(p16),
-                                       _ptr(exp_in), _ptr(wscale), _ptr(exp_out), mode,
+                                       _ptr(exp_in), _ptr(wscale), _ptr(exp_out),
+                                       mode | (ROWS_X_NHWC16 if x_nhwc else 0),
                                        _ptr(amax), st_ptr, epoch, err_ptr, _stream(stream)), "conv_dgrad_rows")
     return dx, nxt, p16
 
@@ -423,15 +435,22 @@ def residual_range(a, ea, b, eb, amax, stream=None):
                                     _stream(stream)), "residual_range")
 
 
-def residual_requant(a, ea, b, eb, amax, ez=None, exp_out=None, relu=False, stream=None):
+def residual_requant(a, ea, b, eb, amax, ez=None, exp_out=None, relu=False, relu_mask=None, stream=None):
     """int8 requant(aligned a + b) with the range in amax; the residual and output exponents into ez /
-    exp_out (device int8 [1], created when None) -> (out, ez, exp_out)."""
+    exp_out (device int8 [1], created when None) -> (out, ez, exp_out).  relu_mask (same shape):
+    then the next op's relu gradient, out = relu_mask > 0 ? q : 0 (no relu)."""
     assert a.shape == b.shape and a.dtype == b.dtype == torch.int8
     out = torch.empty(a.shape, dtype=torch.int8, device=a.device)
     if ez is None:
         ez = torch.zeros(1, dtype=torch.int8, device=a.device)
     if exp_out is None:
         exp_out = torch.zeros(1, dtype=torch.int8, device=a.device)
+    if relu_mask is not None:
+        assert not relu and relu_mask.numel() == a.numel() and relu_mask.dtype == torch.int8
+        check(L.lib().niti_residual_requant_relu_grad(_ptr(a), _ptr(ea), _ptr(b), _ptr(eb), a.numel(), _ptr(amax),
+                                                      _ptr(ez), _ptr(exp_out), _ptr(relu_mask), _ptr(out),
+                                                      _stream(stream)), "residual_requant_relu_grad")
+        return out, ez, exp_out
     check(L.lib().niti_residual_requant(_ptr(a), _ptr(ea), _ptr(b), _ptr(eb), a.numel(), _ptr(amax), _ptr(ez),
                                         _ptr(exp_out), 1 if relu else 0, _ptr(out), _stream(stream)),
           "residual_requant")
@@ -444,6 +463,14 @@ def sum_pool(x16, amax, stream=None):
     acc = torch.empty((n, cp), dtype=torch.int32, device=x16.device)
     check(L.lib().niti_sum_pool(_ptr(x16), n, h * w, cp, _ptr(acc), _ptr(amax), _stream(stream)), "sum_pool")
     return acc
+
+
+def im2col(g: L.Geom, x16, kp, stream=None):
+    """im2col of a shallow NHWC16 input (c_in <= 4) -> xcol int8 [n * oh * ow][kp], column
+    (ky * kw + kx) * c_in + c (niti_im2col)."""
+    xcol = torch.empty((g.n * g.oh * g.ow, kp), dtype=torch.int8, device=x16.device)
+    check(L.lib().niti_im2col(C.byref(g), _ptr(x16), kp, _ptr(xcol), _stream(stream)), "im2col")
+    return xcol
 
 
 def sum_pool_grad(dy16, h, w, stream=None):

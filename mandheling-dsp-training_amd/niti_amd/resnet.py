@@ -53,6 +53,8 @@ def _blocks(convs):
 
 
 class ResNet18:
+    STEM_KP = 160  # the stem's im2col columns: 7 * 7 * 3 = 147, padded to whole 32-byte chunks
+
     def __init__(self, batch: int, in_hw: int = 224, classes: int = 1000, device="cuda", comm=None):
         """batch: images per rank; comm: data-parallel collectives (niti_amd.dp), None for one device."""
         if in_hw % 32 or in_hw < 32:
@@ -64,6 +66,14 @@ class ResNet18:
         n = batch
         self.geoms = [ops.geom(n, l["ci"], l["h"], l["h"], l["co"], l["k"], stride=l["stride"], pad=l["pad"])
                       for l in self.convs]
+        # the 7x7 / 2 stem runs as a 1x1 conv over its im2col (STEM_KP columns, k = (ky * 7 + kx) * 3
+        # + c; ops.im2col): the implicit-GEMM forms gather 3 useful bytes of every 16-byte input pixel
+        # per tap and ran the stem's forward + weight gradient at ~2 % of peak.  Its weight is kept
+        # in that column order ([64][1][1][STEM_KP]); get_weight / set_weight / taps map OIHW.
+        s0 = self.convs[0]
+        self.stem_geom = self.geoms[0]
+        self.geoms[0] = ops.geom(n, self.STEM_KP, s0["oh"], s0["oh"], s0["co"], 1, stride=1, pad=0)
+        self._xcol = None
         self.w16 = [None] * len(self.convs)
         self.wT = [None] * len(self.convs)
         self.wscale = [None] * len(self.convs)
@@ -73,6 +83,8 @@ class ResNet18:
         # resident; no int32 tensor where the GEMM is shallow), their fragment-major weight copies
         # rewritten after every update; use_rows = False keeps every conv on the GEMM path
         self.rows = [ops.conv_rows_ok(g) for g in self.geoms]
+        self.rows_nhwc = [(r and ops.rows_nhwc_ok(g, preferred=True), r and ops.rows_nhwc_ok(g, dgrad=True, preferred=True))
+                          for r, g in zip(self.rows, self.geoms)]
         self.use_rows = True
         self.wf = [None] * len(self.convs)
         self.wft = [None] * len(self.convs)
@@ -103,6 +115,20 @@ class ResNet18:
     def layers(self):
         return self.convs
 
+    def _ci(self, i):  # input channels of the conv as it runs (the stem: its im2col columns)
+        return self.STEM_KP if i == 0 else self.convs[i]["ci"]
+
+    def _stem_cols(self, w):  # OIHW [co][3][7][7] -> [co][STEM_KP][1][1], column (ky * 7 + kx) * 3 + c
+        co, ci, k, _ = w.shape
+        wc = np.zeros((co, self.STEM_KP), dtype=np.int8)
+        wc[:, :k * k * ci] = w.transpose(0, 2, 3, 1).reshape(co, k * k * ci)
+        return wc.reshape(co, self.STEM_KP, 1, 1)
+
+    def _stem_oihw(self, wc):  # [co][STEM_KP] (any int dtype) -> OIHW [co][3][7][7]
+        l = self.convs[0]
+        k, ci = l["k"], l["ci"]
+        return wc[:, :k * k * ci].reshape(-1, k, k, ci).transpose(0, 3, 1, 2).copy()
+
     def weight_shape(self, i):
         l = self.convs[i]
         return (l["co"], l["ci"], l["k"], l["k"])
@@ -111,8 +137,10 @@ class ResNet18:
         w = np.asarray(w)
         if w.dtype != np.int8 or tuple(w.shape) != self.weight_shape(i):
             raise ValueError(f"layer {i}: weight {w.dtype} {tuple(w.shape)}, want int8 {self.weight_shape(i)}")
+        if i == 0:
+            w = self._stem_cols(w)
         w16 = ops.oihw_to_ohwi16(torch.from_numpy(np.ascontiguousarray(w)).to(self.dev))
-        wT = ops.ohwi16_to_ihwo16(w16, self.convs[i]["ci"])
+        wT = ops.ohwi16_to_ihwo16(w16, self._ci(i))
         if self.w16[i] is None:
             self.w16[i], self.wT[i] = w16, wT
         else:  # in place: a captured step holds these addresses
@@ -147,7 +175,8 @@ class ResNet18:
         return f(g, xc, wf, amax, mode=2, **kw)[0]
 
     def get_weight(self, i) -> np.ndarray:
-        return ops.ohwi16_to_oihw(self.w16[i], self.convs[i]["ci"]).cpu().numpy()
+        w = ops.ohwi16_to_oihw(self.w16[i], self._ci(i)).cpu().numpy()
+        return self._stem_oihw(w[:, :, 0, 0]) if i == 0 else w
 
     # ---------------------------------------------------------------- pieces
     def _nchw(self, t16, c):  # [n, h, w, cp] NHWC16 -> NCHW int8 (host, records only)
@@ -161,11 +190,17 @@ class ResNet18:
         l, g = self.convs[i], self.geoms[i]
         amax = self._range()
         if self.use_rows and self.rows[i]:
-            xc = ops.nhwc16_to_c32(x16.view(self.batch, l["h"], l["h"], -1), l["ci"])
+            # the row-segment maps read NHWC16 in place, the others a C32 copy
+            xn = self.rows_nhwc[i][0]
+            xc = x16 if xn else ops.nhwc16_to_c32(x16.view(self.batch, l["h"], l["h"], -1), l["ci"])
             e_out = self._exp()
-            y = self._rows(True, i, xc, amax, exp_in=e_in, wscale=self.ws_dev[i], exp_out=e_out, relu=relu)
+            y = self._rows(True, i, xc, amax, exp_in=e_in, wscale=self.ws_dev[i], exp_out=e_out, relu=relu, x_nhwc=xn)
         else:
-            acc = ops.conv_fwd_acc(g, x16, self.w16[i], amax)
+            xg = x16
+            if i == 0:  # the stem: its im2col, kept for the weight gradient
+                self._xcol = ops.im2col(self.stem_geom, x16, self.STEM_KP)
+                xg = self._xcol
+            acc = ops.conv_fwd_acc(g, xg, self.w16[i], amax)
             self._global_range(amax)
             e_out = self._exp()
             y = ops.requant_act(acc, amax, exp_in=e_in, wscale=self.ws_dev[i], exp_out=e_out, relu=relu)
@@ -182,9 +217,11 @@ class ResNet18:
         amax = self._range()
         e_dx = self._exp()
         if self.use_rows and self.rows[i]:
-            dyc = ops.nhwc16_to_c32(dy16.view(self.batch, l["oh"], l["oh"], -1), l["co"])
+            xn = self.rows_nhwc[i][1]
+            dyc = dy16 if xn else ops.nhwc16_to_c32(dy16.view(self.batch, l["oh"], l["oh"], -1), l["co"])
             m = None if relu_mask is None else relu_mask.view(self.batch, l["h"], l["h"], -1)
-            dx = self._rows(False, i, dyc, amax, relu_mask=m, exp_in=e_dy, wscale=self.ws_dev[i], exp_out=e_dx)
+            dx = self._rows(False, i, dyc, amax, relu_mask=m, exp_in=e_dy, wscale=self.ws_dev[i], exp_out=e_dx,
+                            x_nhwc=xn)
             return dx.view(self.batch, l["h"], l["h"], -1), e_dx
         acc = ops.conv_dgrad_acc(g, dy16, self.wT[i], amax)
         self._global_range(amax)
@@ -196,27 +233,28 @@ class ResNet18:
 
     def _wgrad_update(self, i, x16, dy16):
         amax = self._range()
-        acc = ops.conv_wgrad_acc(self.geoms[i], x16, dy16, amax)
+        acc = ops.conv_wgrad_acc(self.geoms[i], self._xcol if i == 0 else x16, dy16, amax)
         if self.comm is not None:  # the global batch's gradient, then its range
             self.comm.all_sum(acc)
             amax.zero_()
             ops.absmax(acc, amax)
         # the transposed copy is rewritten in place (its input gradient above read it first), so a
         # captured step keeps reading the same buffer
-        _, g8 = ops.sgd_update(acc, amax, self.w16[i], self.convs[i]["ci"], rule=2, wT=self.wT[i])
+        _, g8 = ops.sgd_update(acc, amax, self.w16[i], self._ci(i), rule=2, wT=self.wT[i])
         self._refresh_wf(i)
         if self.record:
             self.rec.setdefault("dy", {})[i] = dy16
             self.rec.setdefault("dw", {})[i] = g8
 
-    def _add(self, a, ea, b, eb, relu):
+    def _add(self, a, ea, b, eb, relu, relu_mask=None):
         # fused residual requantisation: a range pass without the int32 z, then z recomputed from
-        # the int8 operands while requantising (2 x 2 int8 reads instead of an int32 write + read)
+        # the int8 operands while requantising (2 x 2 int8 reads instead of an int32 write + read);
+        # relu_mask: the next op's relu gradient applied in the same pass (backward)
         amax = self._range()
         ops.residual_range(a, ea, b, eb, amax)
         self._global_range(amax)
         ez, e_out = self._exp(), self._exp()
-        q, _, _ = ops.residual_requant(a, ea, b, eb, amax, ez=ez, exp_out=e_out, relu=relu)
+        q, _, _ = ops.residual_requant(a, ea, b, eb, amax, ez=ez, exp_out=e_out, relu=relu, relu_mask=relu_mask)
         return q, e_out
 
     # ---------------------------------------------------------------- step
@@ -276,7 +314,9 @@ class ResNet18:
         for k in range(len(self.blocks) - 1, -1, -1):
             ia, ib, ip = self.blocks[k]
             h, out = saved[k]
-            dz = ops.relu_grad(out, du)
+            # block k's output relu gradient: fused into block k + 1's backward residual sum, except
+            # for the last block (after the sum pool's gradient)
+            dz = ops.relu_grad(out, du) if k == len(self.blocks) - 1 else du
             dh, edh = self._dgrad(ib, dz, edu, relu_mask=h)  # conv a's relu gradient rides along
             self._wgrad_update(ib, h, dz)
             dua, edua = self._dgrad(ia, dh, edh)
@@ -286,7 +326,8 @@ class ResNet18:
                 self._wgrad_update(ip, saved_in[ip], dz)
             else:
                 dus, edus = dz, edu
-            du, edu = self._add(dua, edua, dus, edus, relu=False)
+            du, edu = self._add(dua, edua, dus, edus, relu=False,
+                                relu_mask=saved[k - 1][1].view(dua.shape) if k > 0 else None)
         dp = ops.maxpool_grad(r0, p0, du, 3, 2, 1)
         d0 = ops.relu_grad(r0, dp)
         self._wgrad_update(0, x0, d0)
@@ -313,7 +354,9 @@ class ResNet18:
         for i, dy in self.rec.get("dy", {}).items():
             out["dy"][i] = self._nchw(dy, self.convs[i]["co"])
         for i, g8 in self.rec.get("dw", {}).items():
-            out["dw"][i] = g8.cpu().numpy()[..., :self.convs[i]["ci"]].transpose(0, 3, 1, 2).copy()
+            g = g8.cpu().numpy()
+            out["dw"][i] = (self._stem_oihw(g[:, 0, 0, :]) if i == 0
+                            else g[..., :self.convs[i]["ci"]].transpose(0, 3, 1, 2).copy())
         if "logits" in self.rec:
             out["logits"] = self.rec["logits"].cpu().numpy()[:, :self.classes].copy()
             out["exp_logits"] = int(self.rec["exp_logits"].item())

@@ -176,6 +176,14 @@ TAPS_GEOMS = [
     (16, 32, 2, 2, 128, 1),    # whole images: 16 per step
     (2, 32, 10, 10, 50, 0),    # no padding (10x10 -> 8x8), c_out not a multiple of 64
     (4, 96, 8, 8, 64, 1),      # 3 input-channel tiles
+    # segment mode (rows that are not whole 64-pixel steps): 16-pixel segments ...
+    (2, 32, 48, 48, 64, 1),    # 3 per row
+    (1, 32, 112, 112, 64, 1),  # 7 per row (VGG-16 conv2 maps)
+    # ... and 14-pixel segments (two zero slots of 16)
+    (3, 32, 28, 28, 64, 1),    # 2 per row
+    (1, 64, 56, 56, 64, 1),    # 4 per row (VGG-16 conv3 / ResNet-18 layer1 maps)
+    (5, 64, 14, 14, 128, 1),   # 1 per row, 70 segments: a partial last step
+    (2, 32, 28, 28, 50, 1),    # c_out not a multiple of 64
 ]
 
 
@@ -874,3 +882,24 @@ def test_maxpool_grad_two_pass(T, ops, oracle, geo, relu):
     T.cuda.synchronize()
     assert T.equal(got1, got2)
     assert np.array_equal(ops.nhwc16_to_nchw(got2, c).cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("geo", [(2, 3, 20, 20, 7, 2, 3, 160), (1, 3, 15, 17, 3, 1, 1, 32), (3, 4, 8, 8, 3, 2, 1, 48),
+                                 (2, 1, 9, 9, 5, 1, 2, 32)])
+def test_im2col_small(T, ops, geo):
+    """niti_im2col (the ResNet-18 stem's 1x1-over-im2col form) against a numpy im2col: column
+    (ky * kw + kx) * c_in + c, zero past kh * kw * c_in and outside the image."""
+    n, ci, h, w, k, s, p, kp = geo
+    rng = np.random.default_rng(5)
+    x = rng.integers(-127, 128, (n, ci, h, w)).astype(np.int8)
+    g = ops.geom(n, ci, h, w, 8, k, stride=s, pad=p)
+    got = ops.im2col(g, ops.nchw_to_nhwc16(dev(T, x)), kp).cpu().numpy()
+    oh, ow = (h + 2 * p - k) // s + 1, (w + 2 * p - k) // s + 1
+    xp = np.zeros((n, ci, h + 2 * p + k, w + 2 * p + k), np.int8)
+    xp[:, :, p:p + h, p:p + w] = x
+    ref = np.zeros((n, oh, ow, kp), np.int8)
+    for ky in range(k):
+        for kx in range(k):
+            win = xp[:, :, ky:ky + s * oh:s, kx:kx + s * ow:s]  # [n][ci][oh][ow]
+            ref[..., (ky * k + kx) * ci:(ky * k + kx + 1) * ci] = win.transpose(0, 2, 3, 1)
+    assert np.array_equal(got, ref.reshape(n * oh * ow, kp))

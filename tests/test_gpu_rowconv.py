@@ -19,7 +19,7 @@ def T():
     return torch
 
 
-def _case(T, n, ci, h, co, relu, pool, mode, seed, wmax=127, xmax=127):
+def _case(T, n, ci, h, co, relu, pool, mode, seed, wmax=127, xmax=127, x_nhwc=False):
     import niti_oracle as O
     from niti_amd import ops
     rng = np.random.default_rng(seed)
@@ -39,6 +39,10 @@ def _case(T, n, ci, h, co, relu, pool, mode, seed, wmax=127, xmax=127):
     amax = ops.new_range()
     st = ops.RowConvState()
     kw = dict(exp_in=ein, wscale=ws, exp_out=eo, relu=relu, pool=pool, next_c32=True)
+    if x_nhwc:  # the row-segment form reading its NHWC16 input in place
+        assert ops.rows_nhwc_ok(gg)
+        xc = x16
+        kw["x_nhwc"] = True
     if mode == 0:
         out, pout, nxt = ops.conv_fwd_rows(gg, xc, wf, amax, mode=0, state=st, **kw)
     else:
@@ -88,7 +92,7 @@ def test_rows_fwd_vgg11_conv4_shape(T):
     _case(T, 32, 256, 8, 256, True, True, 0, seed=4)
 
 
-def _dgrad_case(T, n, ci, h, co, pool, relu, mode, seed, wmax=127, dmax=127, p16=True):
+def _dgrad_case(T, n, ci, h, co, pool, relu, mode, seed, wmax=127, dmax=127, p16=True, x_nhwc=False):
     """The layer (ci -> co at h x h) input gradient on the row kernel against NITI's dgrad
     (NITI_DeConv_Int8.cpp:294-329 requantised by the forward rule) followed by the previous
     layer's relu gradient (NITI_ReluGrad_Int8) or its 2x2 max-pool + relu gradient
@@ -119,6 +123,10 @@ def _dgrad_case(T, n, ci, h, co, pool, relu, mode, seed, wmax=127, dmax=127, p16
     amax = ops.new_range()
     st = ops.RowConvState()
     kw = dict(dx_c32=True, dx_p16=p16)
+    if x_nhwc:  # dy NHWC16 read in place
+        assert ops.rows_nhwc_ok(gg, dgrad=True)
+        dyc = nhwc(dy)
+        kw["x_nhwc"] = True
     if pool:
         kw.update(pool_x=nhwc(px), pool_y=nhwc(py), pool_relu=relu)
     elif relu:
@@ -230,3 +238,21 @@ def test_rows_seg_shift_branches(T):
             bw = 0 if m <= 1 else int(np.ceil(np.log2(m)))
             seen.add("raw" if bw <= 7 else "one" if bw == 8 else "psto")
     assert seen == {"raw", "one", "psto"}
+
+
+@pytest.mark.parametrize("h", [14, 28, 56])
+@pytest.mark.parametrize("mode", [0, 2])
+def test_rows_seg_nhwc_input(T, h, mode):
+    """The row-segment form reading its input (x, or dy) as NHWC16 in place (NITI_ROWS_X_NHWC16):
+    the same outputs as from the C32 copy, forward and input gradient."""
+    for k, (n, ci, co, relu, pool) in enumerate([(2, 32, 32, True, True), (3, 64, 96, False, False),
+                                                  (1, 96, 64, True, True)]):
+        _case(T, n, ci, h, co, relu, pool, mode, seed=6000 + 100 * h + 10 * mode + k, x_nhwc=True)
+    for k, (n, ci, co, pool, relu) in enumerate([(2, 32, 32, True, True), (3, 64, 96, False, True),
+                                                  (1, 96, 64, True, False)]):
+        _dgrad_case(T, n, ci, h, co, pool, relu, mode, seed=6500 + 100 * h + 10 * mode + k, p16=False, x_nhwc=True)
+
+
+def test_rows_seg_nhwc_input_large(T):
+    _case(T, 2, 64, 112, 64, True, True, 2, seed=6901, x_nhwc=True)
+    _dgrad_case(T, 1, 64, 224, 64, False, True, 2, seed=6902, p16=False, x_nhwc=True)
