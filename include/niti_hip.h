@@ -364,6 +364,8 @@ int niti_sum_pool_grad(const int8_t* dy, int n, int hw, int cp, int8_t* dx, void
  * kp columns (kp % 16 == 0, kp >= kh * kw * c_in): xcol [n * oh * ow][kp], column k = (ky * kw + kx) *
  * c_in + c, zero beyond kh * kw * c_in and outside the image (the weight [co][kp] in the same order). */
 int niti_im2col(const niti_geom* g, const int8_t* x, int kp, int8_t* xcol, void* stream);
+/* the same from an int8 NCHW input [n][c_in][h][w] (niti_image_quantize's output) */
+int niti_im2col_nchw(const niti_geom* g, const int8_t* x_nchw, int kp, int8_t* xcol, void* stream);
 int niti_maxpool(const int8_t* x, int n, int h, int w, int cp, int k, int s, int p, int8_t* y, int oh, int ow,
                  void* stream);
 int niti_maxpool_grad(const int8_t* x, const int8_t* y, const int8_t* dy, int n, int h, int w, int cp, int k,

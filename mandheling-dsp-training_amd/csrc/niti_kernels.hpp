@@ -122,7 +122,7 @@ hipError_t residual_requant(const int8_t* a, const int8_t* ea, const int8_t* b, 
 // acc[n][cp] = sum over hw pixels of x NHWC16 (+ max into amax); its gradient: dy broadcast
 hipError_t sum_pool(const int8_t* x, int n, int hw, int cp, int32_t* acc, uint32_t* amax, hipStream_t st);
 hipError_t sum_pool_grad(const int8_t* dy, int n, int hw, int cp, int8_t* dx, hipStream_t st);
-hipError_t im2col_small(const ConvGeom& g, const int8_t* x, int kp, int8_t* xcol, hipStream_t st);
+hipError_t im2col_small(const ConvGeom& g, const int8_t* x, int kp, int8_t* xcol, hipStream_t st, bool nchw = false);
 // ---- weight gradient on P16 pixel blocks (niti_wgrad.hip) --------------------------------
 // P16: [pixels/16][Cp][16] int8 (Cp % 16 == 0, pixels % 16 == 0)
 hipError_t nhwc16_to_p16(const int8_t* in, int64_t pixels, int cp, int8_t* out, hipStream_t st);
@@ -144,9 +144,11 @@ void wgrad_stamps_arm(unsigned long long* buf);
 int conv_wgrad_p16_splits(const ConvGeom& g);
 // workspace: the split-K partial slabs (0 bytes when the plan does not split)
 size_t conv_wgrad_p16_workspace(const ConvGeom& g, int splits);
+struct SgdJob;
 hipError_t conv_wgrad_p16(const ConvGeom& g, const int8_t* x_p16, const int8_t* dy_p16, int32_t* acc,
                           uint32_t* amax, void* ws, size_t ws_bytes, int splits, hipStream_t st,
-                          hipEvent_t ev_b = nullptr, hipEvent_t ev_e = nullptr, unsigned long long* span = nullptr);
+                          hipEvent_t ev_b = nullptr, hipEvent_t ev_e = nullptr, unsigned long long* span = nullptr,
+                          SgdJob* defer = nullptr);
 // acc[m][o] = sum_k B[m][k] * A[o][k] (NITI_Matmul_Int8); k16 multiple of 16 (zero padded rows),
 // ldb/lda bytes, ldc elements (multiple of 16; columns o..ldc come out 0)
 hipError_t matmul_acc(int M, int O, int k16, const int8_t* B, int64_t ldb, const int8_t* A, int64_t lda,
@@ -346,11 +348,18 @@ struct SgdJob {
     // forward's and the input gradient's fragment-major copies (may be null; kk == 9)
     int8_t* wf = nullptr;
     int8_t* wft = nullptr;
+    // a deferred split-K combine (the P16 weight gradient's slabs, conv_wgrad_p16 with defer):
+    // sgd_update_many first sums `splits` C-shaped slabs `slab_stride` elements apart into acc
+    // (slab_n elements) with its range into amax, for every such job in one launch
+    const int32_t* slab = nullptr;
+    int splits = 0;
+    int64_t slab_stride = 0, slab_n = 0;
 };
 constexpr int SGD_MAX_JOBS = 24;
 struct SgdJobs {
     SgdJob job[SGD_MAX_JOBS];
     int start[SGD_MAX_JOBS];
+    int cstart[SGD_MAX_JOBS + 1];  // combine chunks (1024 elements) per job, prefix sums
     int n;
 };
 hipError_t sgd_update_many(const SgdJob* jobs, int n, hipStream_t st);

@@ -286,6 +286,11 @@ struct Layer {
     int8_t* dtmp = nullptr;  // gradient wrt the pooled / flattened output
     int8_t* dflat = nullptr;
     int32_t* dwacc = nullptr;  // [co][kk][cip]
+    // the P16 weight gradient's own split-K slabs when its combine is deferred to the NITI_SGD
+    // launch (sgd_update_many), and this step's deferred combine (slab == null: none)
+    int32_t* slab16 = nullptr;
+    size_t slab16_bytes = 0;
+    SgdJob defer{};
     int8_t* g8 = nullptr;    // int8 weight gradient OHWI16
     int8_t* exp = nullptr;   // exponent of this layer's output
     const int8_t* in = nullptr;  // NHWC16 input (previous output or x0)
@@ -341,6 +346,11 @@ struct Model {
     bool use_rowconv = true;
     std::vector<char> xc32_valid;
     uint32_t* rc_err = nullptr;
+    bool in_step = false;  // run(): weight gradients may defer their combine to the update launch
+    bool defer_combine() const {
+        static const bool off = getenv("NITI_DIAG_SGD_COMBINE") && atoi(getenv("NITI_DIAG_SGD_COMBINE")) == 0;
+        return in_step && !off && !dp() && !capturing && !tuning;
+    }
     // the row kernels' accumulator store for their two-launch form (data parallel, graph capture):
     // the range launch keeps its int32 accumulators here, the requantise launch reads them back
     int32_t* rc_acc = nullptr;
@@ -822,6 +832,9 @@ int Model::build(int arch_, int batch_, int in_hw) {
         if (conv_wgrad_p16_ok(g)) {
             slab_w_bytes = std::max(slab_w_bytes, conv_wgrad_p16_workspace(g, 8));
             xp16[i] = (int8_t*)ws.alloc((size_t)n * g.h * g.w * g.cip);
+            l.slab16_bytes = conv_wgrad_p16_workspace(g, 8);
+            l.slab16 = l.slab16_bytes ? (int32_t*)ws.alloc(l.slab16_bytes) : nullptr;
+            if (l.slab16_bytes && !l.slab16) return NITI_OUT_OF_MEMORY;
             dp16[i] = (int8_t*)ws.alloc(out_px * g.cop);
             if (!xp16[i] || !dp16[i]) return NITI_OUT_OF_MEMORY;
         }
@@ -1051,7 +1064,14 @@ int Model::wgrad_layer(int i, hipStream_t st) {
         hipEvent_t eb, ee;
         unsigned long long* sp;
         probe_launch(i, 2, &eb, &ee, &sp);
-        MTRY(conv_wgrad_p16(g, xp16[i], dp16[i], l.dwacc, dp ? nullptr : rng(i, 2), slab_w, slab_w_bytes, s, st, eb, ee, sp));
+        // single device: the split-K combine (+ range) runs with every other layer's in one launch
+        // ahead of NITI_SGD, over this layer's own slabs (the shared workspace is reused by the
+        // next layer)
+        const bool defer = defer_combine() && s > 1 && l.slab16 != nullptr &&
+                           conv_wgrad_p16_workspace(g, s) <= l.slab16_bytes;
+        l.defer = SgdJob{};
+        MTRY(conv_wgrad_p16(g, xp16[i], dp16[i], l.dwacc, dp ? nullptr : rng(i, 2), defer ? l.slab16 : slab_w,
+                            defer ? l.slab16_bytes : slab_w_bytes, s, st, eb, ee, sp, defer ? &l.defer : nullptr));
         return NITI_NO_ERROR;
     }
     // the weight-gradient probe brackets the GEMM launch alone (not its split-K reduce)
@@ -1379,6 +1399,12 @@ int Model::run(const int8_t* x_nchw, int exp_in, const uint8_t* images, const in
     const bool dp = this->dp();
     SgdJob jobs[SGD_MAX_JOBS];
     if (nl > SGD_MAX_JOBS) return NITI_NOT_SUPPORT;
+    struct InStep {  // weight gradients inside this step may defer their combine (defer_combine)
+        bool& f;
+        explicit InStep(bool& x) : f(x) { f = true; }
+        ~InStep() { f = false; }
+    } in_step_guard(in_step);
+    for (auto& l : L) l.defer = SgdJob{};
     if (dp) {
         const int rc = ensure_comm_stream();
         if (rc != NITI_NO_ERROR) return rc;
@@ -1487,6 +1513,12 @@ int Model::run(const int8_t* x_nchw, int exp_in, const uint8_t* images, const in
                          i > 0 && !rowconv_dgrad_layer(i) ? l.wT : nullptr, keep_grads ? l.g8 : nullptr};
         jobs[i].wf = l.rc ? l.wf : nullptr;
         jobs[i].wft = l.rcd ? l.wft : nullptr;
+        if (l.defer.slab != nullptr) {  // the combine of this layer's split-K slabs, in the update launch
+            jobs[i].slab = l.defer.slab;
+            jobs[i].splits = l.defer.splits;
+            jobs[i].slab_stride = l.defer.slab_stride;
+            jobs[i].slab_n = l.defer.slab_n;
+        }
     }
     if (dp) {  // every bucket summed and ranged on the comm stream before the update
         MTRY(hipEventRecord(ev_grads, cst));
@@ -1495,7 +1527,7 @@ int Model::run(const int8_t* x_nchw, int exp_in, const uint8_t* images, const in
         MTRY(hipEventRecord(ev_side, side));
         MTRY(hipStreamWaitEvent(st, ev_side, 0));
     }
-    MTRY(sgd_update_many(jobs, nl, st));  // also rewrites the fragment-major weight copies
+    MTRY(sgd_update_many(jobs, nl, st));  // (+ the deferred combines) also rewrites the fragment-major weight copies
     return NITI_NO_ERROR;
 }
 

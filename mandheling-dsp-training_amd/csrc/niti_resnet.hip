@@ -121,7 +121,10 @@ hipError_t sum_pool_grad(const int8_t* dy, int n, int hw, int cp, int8_t* dx, hi
 // byte gather straight from HBM / L2 per output byte ran ~9x slower).  KH, KW, C as template
 // arguments (the stem's 7, 7, 3) make the byte -> (tap, channel) map compile-time; 0 = run time.
 constexpr int IM2COL_LDS = 16384;
-template <int KH_, int KW_, int C_>
+// NCHW: x is int8 NCHW [n][c_in][h][w] (the input quantiser's planar output): each input row of
+// each channel is a contiguous run, loaded bytewise (coalesced) -- a 16-byte NHWC16 pixel carries
+// 3 useful bytes, so the NCHW source reads ~5x fewer lines.
+template <int KH_, int KW_, int C_, bool NCHW>
 __global__ void __launch_bounds__(256) im2col_small_kernel(const int8_t* __restrict__ x, ConvGeom g, int kp,
                                                            int8_t* __restrict__ xcol) {
     __shared__ int8_t tile[IM2COL_LDS];
@@ -129,15 +132,27 @@ __global__ void __launch_bounds__(256) im2col_small_kernel(const int8_t* __restr
     const int row = blockIdx.x;  // n * oh + oy
     const int n = row / g.oh, oy = row - n * g.oh;
     const int cols = (g.ow - 1) * g.sw + (KW - 1) * g.dw + 1;  // input columns the row reads
-    for (int e = threadIdx.x; e < KH * cols; e += 256) {
-        const int ky = e / cols, cx = e - ky * cols;
-        const int iy = oy * g.sh + ky * g.dh - g.pt, ix = cx - g.pl;
-        uint32_t v = 0;
-        if ((unsigned)iy < (unsigned)g.h && (unsigned)ix < (unsigned)g.w)
-            v = *(const uint32_t*)(x + (((int64_t)n * g.h + iy) * g.w + ix) * g.cip);
+    if constexpr (NCHW) {
+        for (int e = threadIdx.x; e < KH * C * cols; e += 256) {
+            const int kc = e / cols, cx = e - kc * cols;
+            const int ky = kc / C, c = kc - ky * C;
+            const int iy = oy * g.sh + ky * g.dh - g.pt, ix = cx - g.pl;
+            int8_t v = 0;
+            if ((unsigned)iy < (unsigned)g.h && (unsigned)ix < (unsigned)g.w)
+                v = x[(((int64_t)n * g.c_in + c) * g.h + iy) * g.w + ix];
+            tile[(ky * cols + cx) * C + c] = v;
+        }
+    } else {
+        for (int e = threadIdx.x; e < KH * cols; e += 256) {
+            const int ky = e / cols, cx = e - ky * cols;
+            const int iy = oy * g.sh + ky * g.dh - g.pt, ix = cx - g.pl;
+            uint32_t v = 0;
+            if ((unsigned)iy < (unsigned)g.h && (unsigned)ix < (unsigned)g.w)
+                v = *(const uint32_t*)(x + (((int64_t)n * g.h + iy) * g.w + ix) * g.cip);
 #pragma unroll
-        for (int c = 0; c < (C_ ? C_ : 4); ++c)
-            if (C_ || c < C) tile[e * C + c] = (int8_t)(v >> (8 * c));
+            for (int c = 0; c < (C_ ? C_ : 4); ++c)
+                if (C_ || c < C) tile[e * C + c] = (int8_t)(v >> (8 * c));
+        }
     }
     __syncthreads();
     const int kc = kp / 16, kt = KH * KW * C;
@@ -156,17 +171,24 @@ __global__ void __launch_bounds__(256) im2col_small_kernel(const int8_t* __restr
     }
 }
 
-hipError_t im2col_small(const ConvGeom& g, const int8_t* x, int kp, int8_t* xcol, hipStream_t st) {
+hipError_t im2col_small(const ConvGeom& g, const int8_t* x, int kp, int8_t* xcol, hipStream_t st, bool nchw) {
     if (kp % 16 != 0 || kp < g.kh * g.kw * g.c_in || g.c_in > 4 || g.cip > 16) return hipErrorInvalidValue;
     const int cols = (g.ow - 1) * g.sw + (g.kw - 1) * g.dw + 1;
     if ((int64_t)g.kh * cols * g.c_in > IM2COL_LDS) return hipErrorInvalidValue;
     const int64_t rows = (int64_t)g.n * g.oh;
     if (rows == 0) return hipSuccess;
     if (rows > 0x7fffffff) return hipErrorInvalidValue;
-    if (g.kh == 7 && g.kw == 7 && g.c_in == 3)
-        hipLaunchKernelGGL((im2col_small_kernel<7, 7, 3>), dim3((unsigned)rows), dim3(256), 0, st, x, g, kp, xcol);
-    else
-        hipLaunchKernelGGL((im2col_small_kernel<0, 0, 0>), dim3((unsigned)rows), dim3(256), 0, st, x, g, kp, xcol);
+    const dim3 grid((unsigned)rows);
+    if (g.kh == 7 && g.kw == 7 && g.c_in == 3) {
+        if (nchw)
+            hipLaunchKernelGGL((im2col_small_kernel<7, 7, 3, true>), grid, dim3(256), 0, st, x, g, kp, xcol);
+        else
+            hipLaunchKernelGGL((im2col_small_kernel<7, 7, 3, false>), grid, dim3(256), 0, st, x, g, kp, xcol);
+    } else if (nchw) {
+        hipLaunchKernelGGL((im2col_small_kernel<0, 0, 0, true>), grid, dim3(256), 0, st, x, g, kp, xcol);
+    } else {
+        hipLaunchKernelGGL((im2col_small_kernel<0, 0, 0, false>), grid, dim3(256), 0, st, x, g, kp, xcol);
+    }
     return hipGetLastError();
 }
 

@@ -677,7 +677,7 @@ size_t conv_wgrad_p16_workspace(const ConvGeom& g, int splits) {
 
 hipError_t conv_wgrad_p16(const ConvGeom& g, const int8_t* x_p16, const int8_t* dy_p16, int32_t* acc,
                           uint32_t* amax, void* ws, size_t ws_bytes, int splits, hipStream_t st, hipEvent_t ev_b,
-                          hipEvent_t ev_e, unsigned long long* span) {
+                          hipEvent_t ev_e, unsigned long long* span, SgdJob* defer) {
     WgP16 t;
     if (!p16_geom(g, &t)) return hipErrorInvalidValue;
     if (splits <= 0) splits = conv_wgrad_p16_splits(g);
@@ -714,8 +714,17 @@ hipError_t conv_wgrad_p16(const ConvGeom& g, const int8_t* x_p16, const int8_t* 
         default: launch(wgrad_p16_kernel<2, NW, NITI_WG_D4>); break;
     }
     hipError_t e = hipGetLastError();
-    if (e == hipSuccess && t.splits > 1)
-        e = splitk_reduce_linear(t.slab, t.splits, (int64_t)g.c_out * 9 * g.cip, t.slab_stride, acc, amax, st);
+    if (e == hipSuccess && t.splits > 1) {
+        const int64_t n = (int64_t)g.c_out * 9 * g.cip;
+        if (defer != nullptr) {  // the NITI_SGD launch combines the slabs (sgd_update_many)
+            defer->slab = t.slab;
+            defer->splits = t.splits;
+            defer->slab_stride = t.slab_stride;
+            defer->slab_n = n;
+        } else {
+            e = splitk_reduce_linear(t.slab, t.splits, n, t.slab_stride, acc, amax, st);
+        }
+    }
     return e;
 }
 

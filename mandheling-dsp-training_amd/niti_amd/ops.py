@@ -465,11 +465,12 @@ def sum_pool(x16, amax, stream=None):
     return acc
 
 
-def im2col(g: L.Geom, x16, kp, stream=None):
-    """im2col of a shallow NHWC16 input (c_in <= 4) -> xcol int8 [n * oh * ow][kp], column
-    (ky * kw + kx) * c_in + c (niti_im2col)."""
+def im2col(g: L.Geom, x16, kp, stream=None, nchw=False):
+    """im2col of a shallow NHWC16 input (c_in <= 4; nchw: an int8 NCHW input) -> xcol int8
+    [n * oh * ow][kp], column (ky * kw + kx) * c_in + c (niti_im2col / niti_im2col_nchw)."""
     xcol = torch.empty((g.n * g.oh * g.ow, kp), dtype=torch.int8, device=x16.device)
-    check(L.lib().niti_im2col(C.byref(g), _ptr(x16), kp, _ptr(xcol), _stream(stream)), "im2col")
+    f = L.lib().niti_im2col_nchw if nchw else L.lib().niti_im2col
+    check(f(C.byref(g), _ptr(x16), kp, _ptr(xcol), _stream(stream)), "im2col")
     return xcol
 
 

@@ -197,8 +197,8 @@ class ResNet18:
             y = self._rows(True, i, xc, amax, exp_in=e_in, wscale=self.ws_dev[i], exp_out=e_out, relu=relu, x_nhwc=xn)
         else:
             xg = x16
-            if i == 0:  # the stem: its im2col, kept for the weight gradient
-                self._xcol = ops.im2col(self.stem_geom, x16, self.STEM_KP)
+            if i == 0:  # the stem: its im2col (from NCHW or NHWC16), kept for the weight gradient
+                self._xcol = ops.im2col(self.stem_geom, x16, self.STEM_KP, nchw=x16.dim() == 4 and x16.shape[1] == 3)
                 xg = self._xcol
             acc = ops.conv_fwd_acc(g, xg, self.w16[i], amax)
             self._global_range(amax)
@@ -270,7 +270,7 @@ class ResNet18:
         self.rec = {}
         self._ranges.zero_()
         self._ri = self._ei = 0
-        x0 = ops.nchw_to_nhwc16(x) if x.shape[1] == 3 else x
+        x0 = x  # NCHW int8 or NHWC16: only the stem's im2col reads it
         e0 = exp_in if isinstance(exp_in, torch.Tensor) else torch.tensor([exp_in], dtype=torch.int8, device=self.dev)
         saved_in = {}
         # stem
@@ -341,7 +341,7 @@ class ResNet18:
             self.comm.all_sum(stats[:2])
             self.comm.all_max(stats[2:])
             count *= self.comm.world
-        x, a = ops.image_quantize_nhwc16(images, stats, count)
+        x, a = ops.image_quantize(images, stats, count)  # NCHW: the stem's im2col reads its planes
         self.train_step(x, a, labels)
 
     def taps(self):
@@ -365,6 +365,8 @@ class ResNet18:
     def input_tap(self, i):
         """Host copy (NCHW) of parameter layer i's input in the last recorded step."""
         x16 = self.rec["in"][i]
+        if x16.dim() == 4 and x16.shape[1] == 3 and i == 0:  # the stem's NCHW input
+            return x16.cpu().numpy().copy()
         return self._nchw(x16.view(self.batch, self.convs[i]["h"], self.convs[i]["h"], -1), self.convs[i]["ci"])
 
     def step_macs(self) -> int:

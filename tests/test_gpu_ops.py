@@ -903,3 +903,5 @@ def test_im2col_small(T, ops, geo):
             win = xp[:, :, ky:ky + s * oh:s, kx:kx + s * ow:s]  # [n][ci][oh][ow]
             ref[..., (ky * k + kx) * ci:(ky * k + kx + 1) * ci] = win.transpose(0, 2, 3, 1)
     assert np.array_equal(got, ref.reshape(n * oh * ow, kp))
+    # the planar source (niti_im2col_nchw: the input quantiser's NCHW output)
+    assert np.array_equal(ops.im2col(g, dev(T, x), kp, nchw=True).cpu().numpy(), ref.reshape(n * oh * ow, kp))
