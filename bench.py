@@ -525,7 +525,7 @@ def main():
     if args.probe_phase == 2 and pplan[0] == 16:
         kname = ("wgrad_p16_kernel: P16 pixel-block operands loaded straight into the MFMA fragments, taps as "
                  f"dy row shifts and x row selection, {pplan[2]} K split(s)"
-                 + (" + splitk_reduce_linear launch, not in this time" if pplan[2] > 1 else ""))
+                 + ("; the slabs summed in the step's sgd_combine launch, not in this time" if pplan[2] > 1 else ""))
     elif args.probe_phase == 2 and pplan[0] == 32:
         kname = ("wgrad_taps_kernel: tap-sharing weight gradient, one padded input region per 64-pixel step "
                  f"for all 9 taps, {pplan[2]} K splits")

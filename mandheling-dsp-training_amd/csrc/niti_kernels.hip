@@ -1055,6 +1055,11 @@ struct WgTaps {
     // N * H rows), columns (gs % NS) * SW ...
     int seg, SW, NS, nseg;  // NS segments per row, nseg = N * H * NS
     FastDiv fNS, fH;
+    // tile mode (seg == 2): a step is one 4-row x 16-slot tile (SW real columns) of one image, a
+    // 6 x 18 region: the halo rows are shared by the tile's 4 rows (segment mode stages 3 rows per
+    // row); tile t = strip (t % NS), band ((t / NS) % NB), image (t / NS / NB); nseg = tiles
+    int NB;
+    FastDiv fNB;
     unsigned long long* stamps;  // diagnostic builds (NITI_STAMPS): per-block s_memtime marks
     unsigned long long* span;    // kernel-span probe slot (probe_span_arm)
 };
@@ -1169,7 +1174,10 @@ __global__ void __launch_bounds__(TAPS_THREADS) wgrad_taps_kernel(WgTaps g, Epi 
     const int drow = dch >> 2;
     // segment mode, SW = 14: slot drow is pixel 14 (drow / 16) + drow % 16 of the step (slots 14 and
     // 15 of a segment read zeros); SW = 16 is the plain 64-pixel run
-    const int dpx = g.seg && g.SW == 14 ? ((drow & 15) < 14 ? 14 * (drow >> 4) + (drow & 15) : -1) : drow;
+    // tile mode: slot drow is pixel (drow / 16, drow % 16) of the tile, relative to its first
+    // pixel (the step's soffset); columns past SW read zeros
+    const int dpx = g.seg == 2 ? ((drow & 15) < g.SW ? (drow >> 4) * g.W + (drow & 15) : -1)
+                  : g.seg && g.SW == 14 ? ((drow & 15) < 14 ? 14 * (drow >> 4) + (drow & 15) : -1) : drow;
     const uint32_t dvo = dpx < 0 ? OOB : (uint32_t)(dpx * g.COP + co0 + 16 * ((dch & 3) ^ kt_swz<64>(drow)));
     const uint32_t dstep = (uint32_t)(g.seg ? 4 * g.SW : 64) * (uint32_t)g.COP;  // dy bytes per region step
     const bool dw = XPW == 1 ? !xw : wid < 4;  // this wave loads a dy chunk block
@@ -1179,7 +1187,21 @@ __global__ void __launch_bounds__(TAPS_THREADS) wgrad_taps_kernel(WgTaps g, Epi 
     auto issue = [&](int stage, int step) {
         int8_t* st0 = smem + stage * SB;
         const int r = s_begin + step;
-        if (xw && g.seg) {
+        // tile mode: the step's tile (image, first row, first column), uniform
+        int t_img = 0, t_y0 = 0, t_x0 = 0;
+        if (g.seg == 2) {
+            const int rest = (int)fdiv(g.fNS, (uint32_t)r);
+            t_x0 = (r - rest * g.NS) * g.SW;
+            t_img = (int)fdiv(g.fNB, (uint32_t)rest);
+            t_y0 = (rest - t_img * g.NB) * 4;
+        }
+        if (xw && g.seg == 2) {
+            // region pixel (xry, xrx) = input (t_y0 + xry - 1, t_x0 + xrx - 1), zero outside
+            const int iy = t_y0 + xry - 1, ix = t_x0 + xrx - 1;
+            const bool v = xok && r < g.nseg && (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W;
+            const int a = ((t_img * g.H + iy) * g.W + ix) * g.CIP + xrel;
+            if (NITI_ABLATE != 1 && NITI_ABLATE != 7) dma16(rX, st0 + xblk * 1024, v ? (uint32_t)a : OOB, 0u);
+        } else if (xw && g.seg) {
             // the chunk's segment gs: image row `row` (of all N * H), columns from (gs % NS) * SW;
             // region pixel (xry, xrx) is input (row + xry - 1, (gs % NS) * SW + xrx - 1), zero
             // outside the image (pad 1, stride 1: output and input rows coincide)
@@ -1198,7 +1220,9 @@ __global__ void __launch_bounds__(TAPS_THREADS) wgrad_taps_kernel(WgTaps g, Epi 
             if (NITI_ABLATE != 1 && NITI_ABLATE != 7) dma16(rX, st0 + xblk * 1024, v ? (uint32_t)(ub + xrel) : OOB, 0u);
         }
         if (dw) {
-            if (NITI_ABLATE != 1 && NITI_ABLATE != 7) dma16(rD, st0 + XB + (wid & 3) * 1024, dvo, (uint32_t)r * dstep);
+            const uint32_t so = g.seg == 2 ? (r < g.nseg ? (uint32_t)((t_img * g.H + t_y0) * g.W + t_x0) * (uint32_t)g.COP : OOB)
+                                           : (uint32_t)r * dstep;
+            if (NITI_ABLATE != 1 && NITI_ABLATE != 7) dma16(rD, st0 + XB + (wid & 3) * 1024, dvo, so);
         } else if (XPW == 2) {
             if (NITI_ABLATE != 1 && NITI_ABLATE != 7) dma16(rD, st0 + XB + DB + (wid & 3) * 1024, OOB, 0u);
         }
@@ -1870,6 +1894,17 @@ static void wgrad_operands(const ConvGeom& g, const int8_t* x, const int8_t* dy,
 }
 
 // ------------------------------------------------------------------------------ tap-sharing wgrad
+// NITI_TAPS_TILE=0: segment mode instead of 4-row tiles (A/B); NITI_TAPS_SEG_MAX_CIP: the widest input
+// the segment / tile modes take
+static bool taps_tile_mode() {
+    static const bool on = !(getenv("NITI_TAPS_TILE") && atoi(getenv("NITI_TAPS_TILE")) == 0);
+    return on;
+}
+static int taps_seg_max_cip() {
+    static const int v = getenv("NITI_TAPS_SEG_MAX_CIP") ? atoi(getenv("NITI_TAPS_SEG_MAX_CIP")) : 128;
+    return v;
+}
+
 // Geometry of wgrad_taps_kernel, or false where it does not apply (the generic KT GEMM runs).
 static bool wgrad_taps_geom(const ConvGeom& g, const int8_t* x, const int8_t* dy, WgTaps* t) {
     if (const char* f = getenv("NITI_DIAG_NO_TAPS")) {  // diagnostics / tests: generic KT GEMM only
@@ -1882,12 +1917,13 @@ static bool wgrad_taps_geom(const ConvGeom& g, const int8_t* x, const int8_t* dy
     const int64_t xbytes = (int64_t)g.n * g.h * g.w * g.cip, dybytes = K * g.cop;
     if (xbytes >= (int64_t)OOB || dybytes >= (int64_t)OOB) return false;
     WgTaps w{};
-    // segment mode: rows of 16-pixel (or 14-pixel) segments, pad 1 (output rows = input rows); only
-    // shallow inputs (cip <= 64), where it measured faster in the VGG-16 step than the K-major GEMM
-    // (conv1_2 180 vs 378 us, conv2_1 93 vs 106 us; at cip 128 - 512 it was 13 - 40 % slower with
-    // cold operands, tools/gpu_r04g.sh)
+    // segment / tile modes: rows of 16-pixel (or 14-pixel) segments, pad 1 (output rows = input
+    // rows), inputs up to 128 channels: faster than the K-major GEMM at 64 (VGG-16 conv1_2 180 vs
+    // 378 us, conv2_1 93 vs 106 us), level with it at 128 (conv2_2 in tile mode 171.5 vs 166-169 us,
+    // with a fraction of its traffic: the GEMM fetches x once per tap), 13 - 40 % slower at 256 - 512
+    // in segment mode (tools/gpu_r04g.sh, gpu_r04p.sh); the autotuner picks per layer
     const int sw = g.ow % 16 == 0 ? 16 : (g.ow % 14 == 0 ? 14 : 0);
-    const bool seg_ok = sw > 0 && g.cip <= 64 && g.oh == g.h && g.ow == g.w && g.pt == 1 && g.pl == 1 && g.pb == 1 && g.pr == 1 &&
+    const bool seg_ok = sw > 0 && g.cip <= taps_seg_max_cip() && g.oh == g.h && g.ow == g.w && g.pt == 1 && g.pl == 1 && g.pb == 1 && g.pr == 1 &&
                         g.kh == 3 && g.kw == 3 && !getenv("NITI_DIAG_NO_TAPS_SEG");
     if (64 % g.ow == 0 && ohw % 64 == 0) {
         w.band = 1;
@@ -1901,6 +1937,17 @@ static bool wgrad_taps_geom(const ConvGeom& g, const int8_t* x, const int8_t* dy
         w.RH = g.oh + g.kh - 1;
         w.imgs = (int)(64 / ohw);
         w.PPI = (int)ohw;
+    } else if (seg_ok && g.oh % 4 == 0 && taps_tile_mode()) {  // 4-row tiles
+        w.seg = 2;
+        w.SW = sw;
+        w.NS = g.ow / sw;
+        w.NB = g.oh / 4;
+        w.nseg = g.n * w.NB * w.NS;
+        w.band = 0;
+        w.rows_per_step = 0;
+        w.RH = 6;
+        w.imgs = 1;
+        w.PPI = 64;
     } else if (seg_ok) {
         w.seg = 1;
         w.SW = sw;
@@ -1930,7 +1977,7 @@ static bool wgrad_taps_geom(const ConvGeom& g, const int8_t* x, const int8_t* dy
     w.pt = g.pt;
     w.pl = g.pl;
     w.c_out = g.c_out;
-    w.rs_total = w.seg ? (w.nseg + 3) / 4 : (int)(K / 64);
+    w.rs_total = w.seg == 2 ? w.nseg : w.seg ? (w.nseg + 3) / 4 : (int)(K / 64);
     w.steps_total = w.rs_total;
     w.steps_per_split = w.steps_total;
     w.tiles_ci = g.cip / 32;
@@ -1939,10 +1986,11 @@ static bool wgrad_taps_geom(const ConvGeom& g, const int8_t* x, const int8_t* dy
     w.fRPI = make_fastdiv((uint32_t)(w.RH * w.RW));
     w.fPPI = make_fastdiv((uint32_t)w.PPI);
     w.fOW = make_fastdiv((uint32_t)(w.seg ? 16 : g.ow));
-    if (w.seg) {  // a region image is one 16-slot segment
+    if (w.seg) {  // a region image is one 16-slot segment (tile mode: 4 of them stacked)
         w.OW = 16;
         w.fNS = make_fastdiv((uint32_t)w.NS);
         w.fH = make_fastdiv((uint32_t)g.h);
+        if (w.seg == 2) w.fNB = make_fastdiv((uint32_t)w.NB);
     }
     w.fOHW = make_fastdiv((uint32_t)ohw);
     w.fTiles = make_fastdiv((uint32_t)w.tiles);

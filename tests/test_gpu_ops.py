@@ -176,7 +176,8 @@ TAPS_GEOMS = [
     (16, 32, 2, 2, 128, 1),    # whole images: 16 per step
     (2, 32, 10, 10, 50, 0),    # no padding (10x10 -> 8x8), c_out not a multiple of 64
     (4, 96, 8, 8, 64, 1),      # 3 input-channel tiles
-    # segment mode (rows that are not whole 64-pixel steps): 16-pixel segments ...
+    # segment / 4-row tile modes (rows that are not whole 64-pixel steps; tiles where H % 4 == 0):
+    # 16-pixel segments ...
     (2, 32, 48, 48, 64, 1),    # 3 per row
     (1, 32, 112, 112, 64, 1),  # 7 per row (VGG-16 conv2 maps)
     # ... and 14-pixel segments (two zero slots of 16)
@@ -184,6 +185,7 @@ TAPS_GEOMS = [
     (1, 64, 56, 56, 64, 1),    # 4 per row (VGG-16 conv3 / ResNet-18 layer1 maps)
     (5, 64, 14, 14, 128, 1),   # 1 per row, 70 segments: a partial last step
     (2, 32, 28, 28, 50, 1),    # c_out not a multiple of 64
+    (1, 128, 56, 56, 64, 1),   # 4-row tiles at 128 input channels (four ci tiles)
 ]
 
 
