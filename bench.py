@@ -173,6 +173,11 @@ def bench_resnet18(args):
     def step():
         m.train_step_images(img, labels)
 
+    tune_s = 0.0
+    if not args.no_autotune:  # per-shape GEMM plans of the GEMM-path convs, timed on this batch
+        t_tune = time.perf_counter()
+        m.autotune()
+        tune_s = time.perf_counter() - t_tune
     for _ in range(max(args.warmup, 1)):
         step()
     torch.cuda.synchronize()
@@ -286,7 +291,7 @@ def bench_resnet18(args):
                    "driver": "host-driven op sequence (niti_amd.resnet)",
                    "launch": "hipGraph replay of the captured step" if graph is not None else "direct launches"},
         "int8_mfma_tops": round(tops, 2), "int8_mfma_frac_of_peak": round(tops / PEAK_INT8_TOPS, 4),
-        "roofline": roof, "cpu_baseline": cpu}))
+        "roofline": roof, "autotune_s": round(tune_s, 2), "cpu_baseline": cpu}))
     if comm is not None:
         comm.dist.destroy_process_group()
 

@@ -213,6 +213,11 @@ int niti_conv_workspace_bytes(const niti_geom* g, int op, size_t* bytes);
  * 1 input gradient, 2 weight gradient): info = {bm, bn, splits, strategy}; bm = bn = 32 is the
  * tap-sharing weight-gradient kernel (stride-1 3x3, Cip % 32 == 0, Cop % 64 == 0). */
 int niti_conv_plan_info(const niti_geom* g, int op, size_t ws_bytes, int info[4]);
+/* Force the plan a conv GEMM of geometry g runs with (op 0 forward, 1 input gradient, 2 weight
+ * gradient; plan as niti_model_plan_set, NULL restores the default); niti_conv_workspace_bytes then
+ * reports the workspace the forced plan needs.  Per process, keyed by GEMM shape (what the host-
+ * driven ResNet-18 step's autotuner uses). */
+int niti_conv_plan_set(const niti_geom* g, int op, const int plan[4]);
 int niti_matmul_workspace_bytes(int m, int ldc, int k16, size_t* bytes);
 /* acc[n*oh*ow][cop] int32 = conv(x, w); if amax (NITI_MAX_WORDS words): range max-ed in */
 int niti_conv_fwd_acc(const niti_geom* g, const int8_t* x_nhwc16, const int8_t* w_ohwi16, int32_t* acc,
@@ -331,6 +336,11 @@ int niti_requant_grad(const int32_t* acc, int64_t n, const uint32_t* amax, int r
  * g_out (OHWI16, may be NULL). */
 int niti_sgd_update(const int32_t* acc, const uint32_t* amax, int rule, int co, int ci, int kk, int cip, int cop,
                     int8_t* w_ohwi16, int8_t* wt_ihwo16, int8_t* g_out, void* stream);
+/* the same, also rewriting the row kernels' fragment-major copies of a 3x3 layer (niti_weights_to_wf:
+ * wf the forward's, wft the input gradient's; either may be NULL; ci, co multiples of 32) in the same
+ * pass -- no separate weights_to_wf launches after the update */
+int niti_sgd_update_wf(const int32_t* acc, const uint32_t* amax, int rule, int co, int ci, int kk, int cip, int cop,
+                       int8_t* w_ohwi16, int8_t* wt_ihwo16, int8_t* g_out, int8_t* wf, int8_t* wft, void* stream);
 /* layout helpers */
 int niti_nhwc16_to_chwn16(const int8_t* in, int n, int hw, int cp, int np, int8_t* out, void* stream);
 int niti_ohwi16_to_ihwo16(const int8_t* w, int co, int ci, int kk, int cip, int cop, int8_t* wt, void* stream);

@@ -233,6 +233,31 @@ int niti_conv_workspace_bytes(const niti_geom* g, int op, size_t* bytes) {
     return NITI_NO_ERROR;
 }
 
+int niti_conv_plan_set(const niti_geom* g, int op, const int plan[4]) {
+    if (!g || op < 0 || op > 2) return NITI_INVALID_VALUE;
+    niti::ConvGeom r;
+    if (!to_geom(g, &r)) return NITI_COMPUTE_SIZE_ERROR;
+    const int pop = op == 0 ? niti::PLAN_FWD : op == 1 ? niti::PLAN_DGRAD : niti::PLAN_WGRAD;
+    const niti::PlanKey k = niti::conv_plan_key(pop, r);
+    if (plan == nullptr) {
+        niti::plan_override_clear(k);
+        return NITI_NO_ERROR;
+    }
+    auto tile_ok = [](int t) { return t == 64 || t == 128 || t == 256; };
+    const bool taps = plan[0] == niti::PLAN_TAPS_TILE && plan[1] == niti::PLAN_TAPS_TILE && pop == niti::PLAN_WGRAD &&
+                      niti::conv_wgrad_taps_ok(r);
+    if ((!taps && (!tile_ok(plan[0]) || !tile_ok(plan[1]))) || plan[2] < 1 || plan[2] > 64 || plan[3] < 0 ||
+        plan[3] > 2 || (taps && plan[3] == 1))
+        return NITI_INVALID_VALUE;
+    niti::PlanChoice c;
+    c.bm = plan[0];
+    c.bn = plan[1];
+    c.splits = plan[2];
+    c.strat = plan[3];
+    niti::plan_override_set(k, c);
+    return NITI_NO_ERROR;
+}
+
 int niti_conv_plan_info(const niti_geom* g, int op, size_t ws_bytes, int info[4]) {
     if (!g || !info || op < 0 || op > 2) return NITI_INVALID_VALUE;
     niti::ConvGeom r;
@@ -493,6 +518,15 @@ int niti_sgd_update(const int32_t* acc, const uint32_t* amax, int rule, int co, 
                     int8_t* w, int8_t* wt, int8_t* g_out, void* stream) {
     if (rule != 2 && rule != 3) return NITI_INVALID_VALUE;
     return code(niti::sgd_update(acc, amax, rule, co, ci, kk, cip, cop, w, wt, g_out, S(stream)));
+}
+int niti_sgd_update_wf(const int32_t* acc, const uint32_t* amax, int rule, int co, int ci, int kk, int cip, int cop,
+                       int8_t* w, int8_t* wt, int8_t* g_out, int8_t* wf, int8_t* wft, void* stream) {
+    if (rule != 2 && rule != 3) return NITI_INVALID_VALUE;
+    if ((wf || wft) && (kk != 9 || ci % 32 != 0 || co % 32 != 0)) return NITI_NOT_SUPPORT;
+    niti::SgdJob j{acc, amax, rule, co, ci, kk, cip, cop, w, wt, g_out};
+    j.wf = wf;
+    j.wft = wft;
+    return code(niti::sgd_update_many(&j, 1, S(stream)));
 }
 
 int niti_nhwc16_to_chwn16(const int8_t* in, int n, int hw, int cp, int np, int8_t* out, void* stream) {

@@ -1353,6 +1353,16 @@ __global__ void __launch_bounds__(TAPS_THREADS) wgrad_taps_kernel(WgTaps g, Epi 
             }(std::make_integer_sequence<int, STAGES>());
         }
         lgkm_wait<0>();
+        // hipcc cannot prove the tail runs at least once after the steady-state loop, so on its
+        // (dead) steady-exit path the look-ahead fragments are in flight; keep every fragment
+        // register live through the drain so none is reused ahead of it
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            reg_fence(fd[b][0]);
+            reg_fence(fd[b][1]);
+#pragma unroll
+            for (int i = 0; i < NX; ++i) reg_fence(fx[b][i]);
+        }
         if (NITI_TAPS_PRIO && wid >= 4) __builtin_amdgcn_s_setprio(0);
         __syncthreads();
         TAPS_STAMP(2);
@@ -1613,9 +1623,16 @@ PlanChoice plan_query(const PlanKey& k, int k_step, bool recompute_ok, size_t ws
 
 size_t plan_slab_bytes(int M, int N, int splits) { return (size_t)splits * slab_stride_elems(M, N) * 4; }
 
-static size_t plan_ws_elems(int M, int N, int k_total, int k_step) {
+// the workspace of the default plan, or of a forced one (op >= 0: plan_override_set, e.g. autotuned
+// plans of a caller that sizes its workspace per call) when that needs more
+static size_t plan_ws_elems(int M, int N, int k_total, int k_step, int op = -1) {
     GemmPlan p = plan_gemm(M, N, k_total, k_step, 1 << 30, false, (size_t)-1);
-    return p.strat == STRAT_SLAB ? (size_t)p.splits * slab_stride_elems(M, N) : 0;
+    size_t e = p.strat == STRAT_SLAB ? (size_t)p.splits * slab_stride_elems(M, N) : 0;
+    if (op >= 0) {
+        const GemmPlan q = plan_gemm(M, N, k_total, k_step, 1 << 30, false, (size_t)-1, op);
+        if (q.strat == STRAT_SLAB) e = std::max(e, (size_t)q.splits * slab_stride_elems(M, N));
+    }
+    return e;
 }
 
 template <class LA, class LB, int MODE, bool KT>
@@ -2149,15 +2166,15 @@ int conv_plan_k_step(int op, const ConvGeom& g) {
 
 size_t conv_fwd_workspace(const ConvGeom& g) {
     const int bk = fwd_taps_bk(g) ? fwd_taps_bk(g) : 64;
-    return plan_ws_elems(g.n * g.oh * g.ow, g.cop, g.kh * g.kw * g.cip / 16, bk / 16) * sizeof(int32_t);
+    return plan_ws_elems(g.n * g.oh * g.ow, g.cop, g.kh * g.kw * g.cip / 16, bk / 16, PLAN_FWD) * sizeof(int32_t);
 }
 size_t conv_dgrad_workspace(const ConvGeom& g) {
     const int bk = dgrad_taps_bk(g) ? dgrad_taps_bk(g) : 64;
-    return plan_ws_elems(g.n * g.h * g.w, g.cip, g.kh * g.kw * g.cop / 16, bk / 16) * sizeof(int32_t);
+    return plan_ws_elems(g.n * g.h * g.w, g.cip, g.kh * g.kw * g.cop / 16, bk / 16, PLAN_DGRAD) * sizeof(int32_t);
 }
 size_t conv_wgrad_workspace(const ConvGeom& g) {
     const int M = g.c_out, N = g.kh * g.kw * g.cip;
-    size_t e = plan_ws_elems(M, N, g.n * g.oh * g.ow, KT_BK);
+    size_t e = plan_ws_elems(M, N, g.n * g.oh * g.ow, KT_BK, PLAN_WGRAD);
     WgTaps t;
     if (wgrad_taps_geom(g, nullptr, nullptr, &t)) {
         const GemmPlan p = plan_taps(t, M, N, (size_t)-1, nullptr);

@@ -133,14 +133,37 @@ __global__ void __launch_bounds__(256) im2col_small_kernel(const int8_t* __restr
     const int n = row / g.oh, oy = row - n * g.oh;
     const int cols = (g.ow - 1) * g.sw + (KW - 1) * g.dw + 1;  // input columns the row reads
     if constexpr (NCHW) {
-        for (int e = threadIdx.x; e < KH * C * cols; e += 256) {
-            const int kc = e / cols, cx = e - kc * cols;
+        // dword loads over each (ky, c) input row's span [ix0, ix0 + cols), aligned down to 4 bytes
+        // when the plane rows are (w % 4 == 0; else bytewise), 4 bytes scattered into the tile
+        const int ix0 = -g.pl;
+        const bool al = (g.w & 3) == 0;
+        const int lead = al ? (ix0 & 3) : 0;  // bytes of the first dword before ix0
+        const int nd = al ? (lead + cols + 3) / 4 : cols;
+        for (int e = threadIdx.x; e < KH * C * nd; e += 256) {
+            const int kc = e / nd, d = e - kc * nd;
             const int ky = kc / C, c = kc - ky * C;
-            const int iy = oy * g.sh + ky * g.dh - g.pt, ix = cx - g.pl;
-            int8_t v = 0;
-            if ((unsigned)iy < (unsigned)g.h && (unsigned)ix < (unsigned)g.w)
-                v = x[(((int64_t)n * g.c_in + c) * g.h + iy) * g.w + ix];
-            tile[(ky * cols + cx) * C + c] = v;
+            const int iy = oy * g.sh + ky * g.dh - g.pt;
+            const bool row_ok = (unsigned)iy < (unsigned)g.h;
+            const int8_t* rowp = x + (((int64_t)n * g.c_in + c) * g.h + (row_ok ? iy : 0)) * g.w;
+            if (al) {
+                const int ixa = ix0 - lead + 4 * d;  // first input column of this dword
+                uint32_t v = 0;
+                if (row_ok && ixa >= 0 && ixa + 3 < g.w) {
+                    v = *(const uint32_t*)(rowp + ixa);
+                } else if (row_ok) {
+#pragma unroll
+                    for (int b = 0; b < 4; ++b)
+                        if ((unsigned)(ixa + b) < (unsigned)g.w) v |= (uint32_t)(uint8_t)rowp[ixa + b] << (8 * b);
+                }
+#pragma unroll
+                for (int b = 0; b < 4; ++b) {
+                    const int cx = ixa + b - ix0;
+                    if (cx >= 0 && cx < cols) tile[(ky * cols + cx) * C + c] = (int8_t)(v >> (8 * b));
+                }
+            } else {
+                const int ix = ix0 + d;
+                tile[(ky * cols + d) * C + c] = row_ok && (unsigned)ix < (unsigned)g.w ? rowp[ix] : (int8_t)0;
+            }
         }
     } else {
         for (int e = threadIdx.x; e < KH * cols; e += 256) {

@@ -1469,11 +1469,14 @@ static bool rowconv_seg(const ConvGeom& g) { return g.w > 16 || g.w == 14; }
 bool rowconv_nhwc_ok(const ConvGeom& g) { return rowconv_ok(g) && rowconv_seg(g) && g.cip % 32 == 0; }
 // ... and the model does where that is not slower than a C32 copy: 64 channels (a wave load then
 // spans whole 128-byte lines, half used per chunk; VGG-16 conv1_2 / conv2_1 as fast as from C32,
-// conv0's C32 copy and a layout pass saved), not 128 (conv2_2 1.3-1.4x slower, tools/gpu_r04k.sh);
-// NITI_SEG_NHWC_MAX_CIP overrides (A/B)
+// conv0's C32 copy and a layout pass saved), and 128 channels on maps up to 28 px (ResNet-18's
+// layer2: step 4.06 vs 4.12 ms), not on wider ones (VGG-16 conv2_2 @112 1.3-1.4x slower, conv3_1
+// @56 1.2x; tools/gpu_r04k.sh, gpu_r04r.sh); NITI_SEG_NHWC_MAX_CIP sets one channel cap for every
+// map (A/B)
 bool rowconv_nhwc_pref(const ConvGeom& g) {
-    static const int v = getenv("NITI_SEG_NHWC_MAX_CIP") ? atoi(getenv("NITI_SEG_NHWC_MAX_CIP")) : 64;
-    return rowconv_nhwc_ok(g) && g.cip <= v;
+    if (!rowconv_nhwc_ok(g)) return false;
+    if (const char* e = getenv("NITI_SEG_NHWC_MAX_CIP")) return g.cip <= atoi(e);
+    return g.cip <= 64 || (g.cip <= 128 && g.w <= 28);
 }
 
 // the row-segment form's launch shape: 4 rows per band (2 at 14 px), units of 28 px (two 14-px

@@ -151,7 +151,9 @@ def lib():
         "niti_sum_pool_grad": (ci, [vp, ci, ci, ci, vp, vp]),
         "niti_im2col": (ci, [C.POINTER(Geom), vp, ci, vp, vp]),
         "niti_im2col_nchw": (ci, [C.POINTER(Geom), vp, ci, vp, vp]),
+        "niti_sgd_update_wf": (ci, [vp, vp, ci, ci, ci, ci, ci, ci, vp, vp, vp, vp, vp, vp]),
         "niti_conv_rows_nhwc_ok": (ci, [C.POINTER(Geom), ci]),
+        "niti_conv_plan_set": (ci, [C.POINTER(Geom), ci, vp]),
         "niti_maxpool": (ci, [vp] + [ci] * 7 + [vp, ci, ci, vp]),
         "niti_maxpool_grad": (ci, [vp, vp, vp] + [ci] * 10 + [vp, vp]),
         "niti_maxpool_grad_ws": (ci, [vp, vp, vp] + [ci] * 10 + [vp, vp, vp]),

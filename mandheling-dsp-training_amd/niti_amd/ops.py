@@ -160,6 +160,12 @@ def nhwc16_to_chwn16(x16: torch.Tensor, stream=None):
     return out
 
 
+def conv_plan_set(g: L.Geom, op: int, plan=None):
+    """Force the GEMM plan (bm, bn, splits, strategy) of a conv phase (op 0 / 1 / 2); None: default."""
+    arr = (C.c_int * 4)(*plan) if plan is not None else None
+    check(L.lib().niti_conv_plan_set(C.byref(g), op, arr), "conv_plan_set")
+
+
 def conv_workspace(g: L.Geom, op: int, device="cuda"):
     n = C.c_size_t()
     check(L.lib().niti_conv_workspace_bytes(C.byref(g), op, C.byref(n)), "workspace")
@@ -402,7 +408,7 @@ def requant_grad(acc, amax, rule=2, w_update=None, stream=None):
     return g
 
 
-def sgd_update(acc, amax, w16, ci, rule=2, stream=None, wT=None, g=None):
+def sgd_update(acc, amax, w16, ci, rule=2, stream=None, wT=None, g=None, wf=None, wft=None):
     """acc [co][kh][kw][cip] int32, w16 OHWI16 int8 (updated in place) -> (wT IHWO16, g OHWI16);
     wT / g may be given (written in place, e.g. persistent buffers of a captured step)."""
     co, kh, kw, cip = acc.shape
@@ -412,6 +418,10 @@ def sgd_update(acc, amax, w16, ci, rule=2, stream=None, wT=None, g=None):
     if g is None:
         g = torch.empty(acc.shape, dtype=torch.int8, device=acc.device)
     assert wT.shape == (ci, kh, kw, cop) and g.shape == acc.shape
+    if wf is not None or wft is not None:  # the row kernels' fragment-major copies in the same pass
+        check(L.lib().niti_sgd_update_wf(_ptr(acc), _ptr(amax), rule, co, ci, kh * kw, cip, cop, _ptr(w16), _ptr(wT),
+                                         _ptr(g), _ptr(wf), _ptr(wft), _stream(stream)), "sgd_update_wf")
+        return wT, g
     check(L.lib().niti_sgd_update(_ptr(acc), _ptr(amax), rule, co, ci, kh * kw, cip, cop, _ptr(w16), _ptr(wT), _ptr(g),
                                   _stream(stream)), "sgd_update")
     return wT, g

@@ -240,8 +240,12 @@ class ResNet18:
             ops.absmax(acc, amax)
         # the transposed copy is rewritten in place (its input gradient above read it first), so a
         # captured step keeps reading the same buffer
-        _, g8 = ops.sgd_update(acc, amax, self.w16[i], self._ci(i), rule=2, wT=self.wT[i])
-        self._refresh_wf(i)
+        # the row kernels' fragment-major copies are rewritten by the update itself
+        rw = self.rows[i] and self.wf[i] is not None and self.convs[i]["ci"] % 32 == 0 and self.convs[i]["co"] % 32 == 0
+        _, g8 = ops.sgd_update(acc, amax, self.w16[i], self._ci(i), rule=2, wT=self.wT[i],
+                               wf=self.wf[i] if rw else None, wft=self.wft[i] if rw else None)
+        if not rw:
+            self._refresh_wf(i)
         if self.record:
             self.rec.setdefault("dy", {})[i] = dy16
             self.rec.setdefault("dw", {})[i] = g8
@@ -256,6 +260,71 @@ class ResNet18:
         ez, e_out = self._exp(), self._exp()
         q, _, _ = ops.residual_requant(a, ea, b, eb, amax, ez=ez, exp_out=e_out, relu=relu, relu_mask=relu_mask)
         return q, e_out
+
+    # ---------------------------------------------------------------- plans
+    def autotune(self, reps=3):
+        """Per-shape plan autotuning of the GEMM-path convs (what niti_model_autotune does for the C++
+        Model): every candidate tile / K-split plan of each forward, input-gradient and weight-gradient
+        GEMM (and the tap-sharing weight gradient where it applies) timed on this batch's shapes with
+        dummy operands, the fastest forced (ops.conv_plan_set: per process, keyed by GEMM shape; the
+        results are plan-independent).  Returns {(layer, op): (plan, us)}."""
+        dev, n = self.dev, self.batch
+        tiles = [(128, 128), (128, 64), (64, 128), (64, 64), (256, 128), (128, 256)]
+        splits = [2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64]
+        done, out = set(), {}
+        amax = torch.zeros(ops.MAX_WORDS, dtype=torch.int32, device=dev)
+
+        def timed(f):
+            f()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            best = float("inf")
+            for _ in range(reps):
+                e0.record()
+                f()
+                e1.record()
+                e1.synchronize()
+                best = min(best, e0.elapsed_time(e1) * 1000.0)
+            return best
+
+        for i, l in enumerate(self.convs):
+            g = self.geoms[i]
+            rows = self.use_rows and self.rows[i]
+            phases = ([] if rows else [0]) + ([1] if i > 0 and not rows else []) + [2]
+            x16 = torch.randint(-8, 8, (g.n * g.h * g.w, g.cip), dtype=torch.int8, device=dev)
+            dy16 = torch.randint(-8, 8, (g.n * g.oh * g.ow, g.cop), dtype=torch.int8, device=dev)
+            w16 = torch.randint(-8, 8, (g.c_out, g.kh, g.kw, g.cip), dtype=torch.int8, device=dev)
+            wT = torch.randint(-8, 8, (g.c_in, g.kh, g.kw, g.cop), dtype=torch.int8, device=dev)
+            for op in phases:
+                key = (op, g.n, g.c_in, g.h, g.w, g.c_out, g.kh, g.stride_h if hasattr(g, "stride_h") else 0,
+                       g.oh, g.ow)
+                if key in done:
+                    continue
+                done.add(key)
+                run = {0: lambda: ops.conv_fwd_acc(g, x16, w16, amax),
+                       1: lambda: ops.conv_dgrad_acc(g, dy16, wT, amax),
+                       2: lambda: ops.conv_wgrad_acc(g, x16, dy16, amax)}[op]
+                ops.conv_plan_set(g, op, None)
+                best_plan, best_us = None, timed(run)
+                M, N = {0: (g.n * g.oh * g.ow, g.cop), 1: (g.n * g.h * g.w, g.cip),
+                        2: (g.c_out, g.kh * g.kw * g.cip)}[op]
+                # K splits only where the tiles alone leave the chip idle (their int32 slabs are M x N each)
+                cands = [(bm, bn, 1, 0) for bm, bn in tiles] + [
+                    (bm, bn, sp, 2) for bm, bn in tiles for sp in splits
+                    if -(-M // bm) * -(-N // bn) < 256 and -(-M // bm) * -(-N // bn) * sp <= 4096]
+                if op == 2 and ops.wgrad_taps_ok(g):
+                    cands += [(32, 32, 1, 0)] + [(32, 32, sp, 2) for sp in splits]
+                for plan in cands:
+                    try:
+                        ops.conv_plan_set(g, op, plan)
+                        us = timed(run)
+                    except NitiError:
+                        continue
+                    if us < best_us:
+                        best_plan, best_us = plan, us
+                ops.conv_plan_set(g, op, best_plan)
+                out[(i, op)] = (best_plan, best_us)
+        return out
 
     # ---------------------------------------------------------------- step
     def train_step(self, x: torch.Tensor, exp_in: int, labels: torch.Tensor):

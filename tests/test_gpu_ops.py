@@ -907,3 +907,29 @@ def test_im2col_small(T, ops, geo):
     assert np.array_equal(got, ref.reshape(n * oh * ow, kp))
     # the planar source (niti_im2col_nchw: the input quantiser's NCHW output)
     assert np.array_equal(ops.im2col(g, dev(T, x), kp, nchw=True).cpu().numpy(), ref.reshape(n * oh * ow, kp))
+
+
+def test_conv_plan_set_forced_plans_agree(T, ops):
+    """niti_conv_plan_set (the host-driven ResNet-18 step's autotuner): forced tile / K-split plans of
+    the forward, input-gradient and weight-gradient GEMMs give the default plan's int32 results, with
+    the workspace niti_conv_workspace_bytes reports for the forced plan."""
+    rng = np.random.default_rng(8)
+    n, ci, h, co = 4, 64, 14, 128
+    g = ops.geom(n, ci, h, h, co, 3, stride=2, pad=1)
+    x = ops.nchw_to_nhwc16(dev(T, rng.integers(-127, 128, (n, ci, h, h)).astype(np.int8)))
+    dy = ops.nchw_to_nhwc16(dev(T, rng.integers(-127, 128, (n, co, g.oh, g.ow)).astype(np.int8)))
+    w16 = ops.oihw_to_ohwi16(dev(T, rng.integers(-127, 128, (co, ci, 3, 3)).astype(np.int8)))
+    wT = ops.ohwi16_to_ihwo16(w16, ci)
+    runs = {0: lambda: ops.conv_fwd_acc(g, x, w16, zeros_u32(T)),
+            1: lambda: ops.conv_dgrad_acc(g, dy, wT, zeros_u32(T)),
+            2: lambda: ops.conv_wgrad_acc(g, x, dy, zeros_u32(T))}
+    try:
+        for op, f in runs.items():
+            ops.conv_plan_set(g, op, None)
+            ref = f().cpu().numpy()
+            for plan in [(64, 64, 1, 0), (128, 64, 3, 2), (64, 128, 8, 2), (256, 128, 2, 2)]:
+                ops.conv_plan_set(g, op, plan)
+                assert np.array_equal(f().cpu().numpy(), ref), (op, plan)
+    finally:
+        for op in runs:
+            ops.conv_plan_set(g, op, None)

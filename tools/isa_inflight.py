@@ -9,9 +9,14 @@ in round 2.  The scan tracks every load in issue order: loads between hipcc's ;;
 buffer / global loads, lgkmcnt for ds_read, in order); compiler-issued loads only take a place in
 the counters.  Any other instruction naming a held register is a hit.
 
-A linear scan: it follows the instruction order of the file, not the control flow, so a hit at a
-loop head may be a false alarm, and SMEM loads (which retire lgkmcnt out of order) are not
-modelled.  A clean scan is what every asm-ring kernel must show.
+The scan follows the instruction order of the file, except that a block only entered by
+forward branches (the previous instruction is an unconditional s_branch) starts from the merged
+state of those branches rather than from the unrelated code above it.  A block with a
+fall-through keeps the fall-through state: the waits of an if/else wait ladder (a dynamic
+count) are all taken as executed, so the scan is optimistic there.  Back edges are not
+followed, so a hit at a loop head may be a false alarm, and SMEM loads (which retire lgkmcnt
+out of order) are not modelled.  A clean
+scan is what every asm-ring kernel must show.
 """
 import re
 import sys
@@ -33,13 +38,30 @@ def _retire(pending, l, counter):
     return pending[len(pending) - n:] if 0 < n < len(pending) else ([] if n == 0 else pending)
 
 
+def _merge(a, b):
+    """Two pending lists aligned at their most recent load; a waitcnt(n) keeps the last n of each."""
+    n = max(len(a), len(b))
+    a = [set()] * (n - len(a)) + a
+    b = [set()] * (n - len(b)) + b
+    return [x | y for x, y in zip(a, b)]
+
+
 def scan(asm, name):
     i = asm.index(name + ':')
     j = asm.index('.Lfunc_end', i)
     vm, lgkm, hits = [], [], []
     in_asm = False
+    at_label = {}           # label -> (vm, lgkm) merged over the forward branches seen so far
+    no_fall = False         # the previous instruction never falls through
     for l in asm[i:j].split('\n'):
         l = l.strip()
+        m = re.match(r'(\.LBB\w+):', l)
+        if m:
+            got = at_label.pop(m.group(1), None)
+            if got is not None and no_fall:
+                vm, lgkm = list(got[0]), list(got[1])
+            no_fall = False
+            continue
         if l.startswith(';;#ASMSTART'):
             in_asm = True
             continue
@@ -52,6 +74,13 @@ def scan(asm, name):
         if not ops:
             continue
         op = ops[0]
+        if op.startswith(('s_branch', 's_cbranch')) and len(ops) > 1 and ops[1].startswith('.LBB'):
+            old = at_label.get(ops[1])
+            at_label[ops[1]] = (list(vm), list(lgkm)) if old is None else \
+                (_merge(old[0], vm), _merge(old[1], lgkm))
+            no_fall = op == 's_branch'
+            continue
+        no_fall = op in ('s_endpgm', 's_setpc_b64')
         if op == 's_waitcnt':
             vm = _retire(vm, l, 'vmcnt')
             lgkm = _retire(lgkm, l, 'lgkmcnt')
