@@ -454,6 +454,11 @@ def main():
     # a fused row-kernel launch whose grid barrier timed out computed garbage: no number from it
     if model.rowconv_error() != 0:
         raise RuntimeError("a fused row-kernel grid barrier timed out in the timed region: results invalid")
+    # the speculative row-kernel pairs (two-launch form): launches redone / pairs in store mode per
+    # layer over warmup + timed steps (per layer: fwd redone, fwd stored, dgrad redone, dgrad stored)
+    spec = [(s[1], s[2], s[4], s[5]) for s in model.spec_stats()]
+    spec = {"redone": sum(a + c for a, _, c, _ in spec), "stored": sum(b + d for _, b, _, d in spec),
+            "per_layer": [list(v) for v in spec if any(v)]}
     probe_ms, probe_n = model.probe_read()
     span_ms, span_n = model.probe_read_span()
     # the same launch alone (after the timed region, nothing else on the GPU): in the step the
@@ -588,6 +593,7 @@ def main():
                          "note": "same launch re-run alone after the timed region (no side-stream overlap)"},
         },
         "autotune_s": round(tune_s, 2) if not (args.no_autotune or args.load_plans) else None,
+        "rowconv_spec": spec,
         "cpu_baseline": cpu,
     }
     if rank == 0:

@@ -251,8 +251,16 @@ int niti_conv_dgrad_phase2(const niti_geom* g, const int8_t* dy_nhwc16, const in
  * (zeroed by the caller); mode 2: recompute and requantise with amax (a data-parallel caller
  * all-reduces amax between modes 1 and 2).  Outputs: out_nhwc16 [n][H][W][cop] = relu?(requant(y)),
  * pool_out_nhwc16 (may be NULL) its 2x2 max pool, next_c32 (may be NULL) the (pooled) output as the
- * next layer's C32 input; exp_out = exp_in + wscale + inc. */
+ * next layer's C32 input; exp_out = exp_in + wscale + inc.  Modes 3 and 4, the speculative pair
+ * (state required; both calls with the same outputs and amax): mode 3 multiplies, requantises with
+ * the bit width this state's layer had at its previous mode-4 call and publishes max|y| into amax;
+ * mode 4 (after the caller's all-reduce of amax, if any) writes exp_out and redoes the launch only
+ * if max|y|'s bit width differs from that guess -- the results are modes 1 + 2's, at one GEMM pass
+ * when the bit width holds from step to step. */
 #define NITI_ROWCONV_STATE_WORDS 1216
+/* the speculative pair's slot of a state (dgrad 0 forward, 1 input gradient): u32 [0] the hint (bit
+ * width + 1, 0 none), [1] the guess the last mode-3 call used, [2] the mode-4 calls that redid */
+uint32_t* niti_rows_spec_slot(uint32_t* state, int dgrad);
 int niti_conv_rows_ok(const niti_geom* g);
 int niti_nhwc16_to_c32(const int8_t* in_nhwc16, int n, int hw, int cp, int c, int8_t* out_c32, void* stream);
 int niti_weights_to_wf(const int8_t* w_ohwi16, int co, int ci, int cip, int transpose, int8_t* out_wf,
@@ -450,6 +458,10 @@ int niti_model_keep_grads(niti_model_t m, int enable);
  * ever timed out (synchronises). */
 int niti_model_set_rowconv(niti_model_t m, int enable);
 int niti_model_rowconv_error(niti_model_t m);
+/* the speculative row-kernel pairs' counters per layer (max_layers x 6 u32): forward hint (bit
+ * width + 1), forward launches redone, forward pairs in store mode, then the same for the input
+ * gradient (niti_rows_spec_slot; synchronises) */
+int niti_model_spec_stats(niti_model_t m, uint32_t* out, int max_layers);
 /* Replay the step as a hipGraph (single device only -- with a communicator attached the step
  * always runs as direct launches).  Default 0 (direct launches: measured faster on ROCm 7.2). */
 int niti_model_set_graph(niti_model_t m, int enable);

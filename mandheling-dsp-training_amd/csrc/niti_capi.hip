@@ -336,7 +336,8 @@ int niti_conv_fwd_rows(const niti_geom* g, const int8_t* x_c32, const int8_t* wf
                        void* stream) {
     const int x_nhwc = (mode & NITI_ROWS_X_NHWC16) ? 1 : 0;
     mode &= ~NITI_ROWS_X_NHWC16;
-    if (!g || !x_c32 || !wf || !amax || mode < 0 || mode > 2) return NITI_INVALID_VALUE;
+    if (!g || !x_c32 || !wf || !amax || mode < 0 || mode > 4) return NITI_INVALID_VALUE;
+    if (mode >= 3 && state == nullptr) return NITI_INVALID_VALUE;
     niti::ConvGeom r;
     if (!to_geom(g, &r)) return NITI_COMPUTE_SIZE_ERROR;
     if (!niti::rowconv_ok(r)) return NITI_NOT_SUPPORT;
@@ -360,7 +361,8 @@ int niti_conv_dgrad_rows(const niti_geom* g, const int8_t* dy_c32, const int8_t*
                          uint32_t* amax, uint32_t* state, uint32_t epoch, uint32_t* err, void* stream) {
     const int x_nhwc = (mode & NITI_ROWS_X_NHWC16) ? 1 : 0;
     mode &= ~NITI_ROWS_X_NHWC16;
-    if (!g || !dy_c32 || !wft || !amax || mode < 0 || mode > 2) return NITI_INVALID_VALUE;
+    if (!g || !dy_c32 || !wft || !amax || mode < 0 || mode > 4) return NITI_INVALID_VALUE;
+    if (mode >= 3 && state == nullptr) return NITI_INVALID_VALUE;
     if ((pool_x == nullptr) != (pool_y == nullptr) || (pool_x && relu_mask)) return NITI_INVALID_VALUE;
     if (mode != 1 && dx == nullptr) return NITI_INVALID_VALUE;
     niti::ConvGeom r, d;
@@ -375,6 +377,7 @@ int niti_conv_dgrad_rows(const niti_geom* g, const int8_t* dy_c32, const int8_t*
     o.exp_in = exp_in;
     o.wscale = wscale;
     o.exp_out = exp_out;
+    o.dgrad_slot = 1;
     if (pool_x != nullptr) {
         o.pool_x = pool_x;
         o.pool_y = pool_y;
@@ -455,6 +458,10 @@ int niti_nhwc16_to_p16(const int8_t* in, int64_t pixels, int cp, int8_t* out, vo
 
 void niti_diag_wgrad_stamps(void* buf) { niti::wgrad_stamps_arm((unsigned long long*)buf); }
 void niti_diag_rowconv_stamps(void* buf) { niti::rowconv_stamps_arm((unsigned long long*)buf); }
+uint32_t* niti_rows_spec_slot(uint32_t* state, int dgrad) {
+    return state ? niti::rowconv_spec_slot(state, dgrad != 0) : nullptr;
+}
+
 void niti_diag_rowconv_barrier(uint32_t spin_limit, uint32_t expect_extra) {
     niti::rowconv_barrier_diag(spin_limit, expect_extra);
 }

@@ -235,6 +235,9 @@ struct RowConvOut {
     // launch also stores every unit's int32 accumulators here (rowconv_acc_bytes) and the
     // requantise launch reads them back instead of recomputing the GEMM
     int32_t* acc_store = nullptr;
+    // the speculative pair's hint slot: 0 forward, 1 input gradient (set by input-gradient callers
+    // whose call has no relu / pool / P16 operand, so the two directions never share a slot)
+    int dgrad_slot = 0;
     // input layout: 0 C32 [n][C/32][H][W][32]; 1 NHWC16 [n][H][W][cip] (row-segment maps, cip % 32
     // == 0: read in place, no C32 copy)
     int x_nhwc = 0;
@@ -263,7 +266,14 @@ hipError_t c32_to_nhwc16(const int8_t* in, int n, int hw, int cp, int c, int8_t*
 hipError_t weights_to_wf(const int8_t* w_ohwi16, int co, int ci, int cip, bool transpose, int8_t* out,
                          hipStream_t st);
 // mode 0 FUSED (bar, err, epoch != 0 required; epoch + 1 per launch), 1 RANGE (max|y| into amax),
-// 2 REQUANT (recompute with the max in amax, requantise, store)
+// 2 REQUANT (recompute with the max in amax, requantise, store); 3 / 4 the speculative pair (bar
+// required, the same outputs and amax for both): 3 multiplies, requantises with the bit width the
+// layer had last time and publishes max|y| into amax; 4 (after any all-reduce of amax) writes the
+// exponent and redoes the launch only where the bit width differs -- the results are mode 1 + 2's
+constexpr int RC_SPEC_A = 3, RC_SPEC_B = 4;
+// whether the model's two-launch row convs take the speculative pair (NITI_RC_SPEC2=0: range +
+// recompute-or-stored requantise, A/B diagnostics)
+bool rowconv_spec2_on();
 // diagnostics: 8 u64 per wave of the following launches (niti_diag_rowconv_stamps), null disarms
 void rowconv_stamps_arm(unsigned long long* buf);
 // diagnostics: the fused barrier's poll limit (0 = the default) and arrivals it waits for that never
@@ -272,6 +282,8 @@ void rowconv_barrier_diag(uint32_t spin_limit, uint32_t expect_extra);
 // the fused mode's speculative epilogue (the previous launch's bit width applied while the barrier
 // completes): 1 on (default), 0 off, 2 always guess wrong (diagnostics: every launch redoes it)
 void rowconv_speculate(int mode);
+// the speculative pair's miss count of a state buffer (forward / input-gradient slot), device words
+uint32_t* rowconv_spec_slot(uint32_t* bar, bool dg);
 void model_p16_jobs_cap(int cap);  // niti_model.hip, diagnostic
 hipError_t rowconv_fwd(const ConvGeom& g, const int8_t* x_c32, const int8_t* wf, const RowConvOut& o, int mode,
                        uint32_t* amax, uint32_t* bar, uint32_t epoch, uint32_t* err, hipStream_t st);

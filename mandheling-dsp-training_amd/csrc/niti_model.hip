@@ -965,6 +965,10 @@ int Model::fwd_layer(int i, hipStream_t st) {
         const int K = g.c_in, rows = g.c_out;
         if (!dp && !capturing && rowconv_fc_ok(n, K, rows, true)) {
             MTRY(rowconv_fc(n, K, rows, l.in, g.cip, l.w, g.cip, o, 0, rng(i, 0), l.bar, ++l.epoch, rc_err, st));
+        } else if (rowconv_spec2_on()) {  // the speculative pair: one GEMM pass while the bit width holds
+            MTRY(rowconv_fc(n, K, rows, l.in, g.cip, l.w, g.cip, o, RC_SPEC_A, rng(i, 0), l.bar, 0, nullptr, st));
+            if (dp && exact) CTRY(coll->allreduce(rng(i, 0), MAX_WORDS, COLL_MAX_U32, st));
+            MTRY(rowconv_fc(n, K, rows, l.in, g.cip, l.w, g.cip, o, RC_SPEC_B, rng(i, 0), l.bar, 0, nullptr, st));
         } else {
             MTRY(rowconv_fc(n, K, rows, l.in, g.cip, l.w, g.cip, o, 1, rng(i, 0), nullptr, 0, nullptr, st));
             if (dp && exact) CTRY(coll->allreduce(rng(i, 0), MAX_WORDS, COLL_MAX_U32, st));
@@ -997,6 +1001,11 @@ int Model::fwd_layer(int i, hipStream_t st) {
         o.relu = l.relu;
         if (!dp && !capturing && rowconv_fused_ok(g)) {
             MTRY(rowconv_fwd(g, xin, l.wf, o, 0, rng(i, 0), l.bar, ++l.epoch, rc_err, st));
+        } else if (rowconv_spec2_on()) {  // the speculative pair: one GEMM pass while the bit width holds
+            o.acc_store = rowconv_acc_bytes(g, false) ? rc_acc : nullptr;  // its store mode after a change
+            MTRY(rowconv_fwd(g, xin, l.wf, o, RC_SPEC_A, rng(i, 0), l.bar, 0, nullptr, st));
+            if (dp && exact) CTRY(coll->allreduce(rng(i, 0), MAX_WORDS, COLL_MAX_U32, st));
+            MTRY(rowconv_fwd(g, xin, l.wf, o, RC_SPEC_B, rng(i, 0), l.bar, 0, nullptr, st));
         } else {
             o.acc_store = rowconv_acc_bytes(g, false) ? rc_acc : nullptr;  // else the requantise launch recomputes
             MTRY(rowconv_fwd(g, xin, l.wf, o, 1, rng(i, 0), nullptr, 0, nullptr, st));
@@ -1147,6 +1156,11 @@ int Model::dgrad_layer(int i, hipStream_t st) {
         const int K = g.c_out, rows = g.c_in;
         if (!dp && !capturing && rowconv_fc_ok(n, K, rows, true)) {
             MTRY(rowconv_fc(n, K, rows, l.dy, g.cop, l.wT, g.cop, o, 0, rng(i, 1), l.bar, ++l.epoch, rc_err, st));
+        } else if (rowconv_spec2_on()) {
+            o.dgrad_slot = 1;
+            MTRY(rowconv_fc(n, K, rows, l.dy, g.cop, l.wT, g.cop, o, RC_SPEC_A, rng(i, 1), l.bar, 0, nullptr, st));
+            if (dp && exact) CTRY(coll->allreduce(rng(i, 1), MAX_WORDS, COLL_MAX_U32, st));
+            MTRY(rowconv_fc(n, K, rows, l.dy, g.cop, l.wT, g.cop, o, RC_SPEC_B, rng(i, 1), l.bar, 0, nullptr, st));
         } else {
             MTRY(rowconv_fc(n, K, rows, l.dy, g.cop, l.wT, g.cop, o, 1, rng(i, 1), nullptr, 0, nullptr, st));
             if (dp && exact) CTRY(coll->allreduce(rng(i, 1), MAX_WORDS, COLL_MAX_U32, st));
@@ -1191,6 +1205,12 @@ int Model::dgrad_layer(int i, hipStream_t st) {
         dy16_valid[i - 1] = !skip16;
         if (!dp && !capturing && rowconv_fused_ok(d, true)) {
             MTRY(rowconv_fwd(d, dyin, l.wft, o, 0, rng(i, 1), l.bar, ++l.epoch, rc_err, st));
+        } else if (rowconv_spec2_on()) {
+            o.dgrad_slot = 1;
+            o.acc_store = rowconv_acc_bytes(d, true) ? rc_acc : nullptr;
+            MTRY(rowconv_fwd(d, dyin, l.wft, o, RC_SPEC_A, rng(i, 1), l.bar, 0, nullptr, st));
+            if (dp && exact) CTRY(coll->allreduce(rng(i, 1), MAX_WORDS, COLL_MAX_U32, st));
+            MTRY(rowconv_fwd(d, dyin, l.wft, o, RC_SPEC_B, rng(i, 1), l.bar, 0, nullptr, st));
         } else {
             o.acc_store = rowconv_acc_bytes(d, true) ? rc_acc : nullptr;
             MTRY(rowconv_fwd(d, dyin, l.wft, o, 1, rng(i, 1), nullptr, 0, nullptr, st));
@@ -1742,6 +1762,26 @@ int niti_model_set_rowconv(niti_model_t m, int enable) {
     }
     m->m.use_rowconv = enable != 0;
     m->m.drop_graph();
+    return NITI_NO_ERROR;
+}
+
+int niti_model_spec_stats(niti_model_t m, uint32_t* out, int max_layers) {
+    if (!m || !out || max_layers < 0) return NITI_INVALID_VALUE;
+    const int nl = std::min(max_layers, (int)m->m.L.size());
+    std::fill(out, out + (size_t)nl * 6, 0u);
+    for (int i = 0; i < nl; ++i) {
+        const uint32_t* bar = m->m.L[i].bar;
+        if (bar == nullptr) continue;
+        for (int d = 0; d < 2; ++d) {  // forward / input-gradient slot: hint, redone launches, stored pairs
+            uint32_t w[5];
+            if (hipMemcpy(w, niti::rowconv_spec_slot(const_cast<uint32_t*>(bar), d != 0), sizeof(w), hipMemcpyDeviceToHost) !=
+                hipSuccess)
+                return NITI_INVALID_VALUE;
+            out[i * 6 + d * 3] = w[0];
+            out[i * 6 + d * 3 + 1] = w[2];
+            out[i * 6 + d * 3 + 2] = w[4];
+        }
+    }
     return NITI_NO_ERROR;
 }
 

@@ -112,6 +112,7 @@ __device__ __forceinline__ unsigned long long* bar_shard(uint32_t* base, int s) 
 // overlaps the epilogue instead of preceding it.  The results are the rule's whatever the guess.
 __device__ __forceinline__ uint32_t* bar_hint(uint32_t* state, bool dg) { return state + (16 + (dg ? 1 : 0)) * BAR_LINE; }
 
+
 // Called by one whole wave of each workgroup (lane 0's bw): the arrival, then -- after whatever
 // work the workgroup can do meanwhile -- the wait, which returns the grid's bw to every lane.
 __device__ void grid_bw_arrive(uint32_t* state, uint32_t epoch, int bw, int lane) {
@@ -194,6 +195,10 @@ struct RowConvArgs {
     int8_t* p16;                 // P16 [pixels/16][cop][16] copy of out / pool_dx, or null
     int64_t p16_pixels;          // pixels of that tensor
     int32_t* acc_store;          // RANGE writes / REQUANT reads every unit's accumulators, or null
+    // REQUANT as a speculative pair (spec_hint, below): 1 = launch A, requantise with the hinted bit
+    // width and publish the max; 2 = launch B, redo only if the (all-reduced) max's bit width differs
+    int spec2;
+    uint32_t* hint;              // spec2: the slot (spec_hint); its word 0 the hint, 1 the guess A used, 2 misses
     // W = 1 (1x1 maps, the classifier head): x is row-major [n][xld], the weights row-major
     // [rows][wld] (OHWI16 forward, IHWO16 input gradient), K the reduced channels
     int xld, wld, K, rows;
@@ -219,6 +224,8 @@ struct RowConvArgs {
     } while (0)
 
 enum RowMode { RC_FUSED = 0, RC_RANGE = 1, RC_REQUANT = 2 };
+// host modes RC_SPEC_A / RC_SPEC_B of rowconv_fwd / rowconv_fc (niti_kernels.hpp): the speculative
+// two-launch pair (spec_guess), both on the RC_REQUANT instantiation
 
 // A workgroup tile is one co block x 4 consecutive (image group, band) pairs, one per wave: the
 // four waves share the co block's weight fragments, which the workgroup stages through LDS once
@@ -1011,6 +1018,55 @@ __device__ __forceinline__ void write_exponent(const RowConvArgs& a, uint32_t gm
     *a.exp_out = (int8_t)((a.exp_in ? (int)*a.exp_in : 0) + (a.wscale ? (int)*a.wscale : 0) + inc);
 }
 
+// The same speculation for the two-launch form (several devices, graph capture, and the
+// row-segment maps, which have no fused form): launch A multiplies, requantises with the hint and
+// publishes its max; launch B (after the all-reduce MAX, when there is one) compares the max's bit
+// width with the guess A used and redoes the launch only when they differ -- otherwise every
+// workgroup exits at once, so a hit costs one GEMM pass instead of two (or a pass plus an int32
+// accumulator round trip).  A layer whose bit width has just changed may flip again (gradients
+// near a power of two): after a change, where the caller gave an accumulator store (the W > 0
+// forms), the next pairs store the accumulators in A instead of requantising and B requantises
+// them -- the range + stored-requantise cost -- until SPEC_COOLDOWN pairs in a row see the bit
+// width hold.  Slot words:
+// [0] the hint (bw + 1, 0 none; written by B's block 0, read by A), [1] what A did (the hint it
+// used, bit 31 set when it stored instead; written by A's block 0, read by B), [2] redone launches,
+// [3] pairs left in store mode (read and written by B's thread 0, read by A), [4] stored pairs.
+// Every other reader of a word runs in the other launch, so no launch's blocks race on a word.
+constexpr uint32_t SPEC_COOLDOWN = 4;
+__device__ __forceinline__ int spec_guess(const RowConvArgs& a, bool can_store, bool& store) {
+    const uint32_t h = __hip_atomic_load(a.hint, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t f = __hip_atomic_load(a.hint + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    store = can_store && a.acc_store != nullptr && __builtin_amdgcn_readfirstlane((int)f) != 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+        __hip_atomic_store(a.hint + 1, h | (store ? 0x80000000u : 0u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return __builtin_amdgcn_readfirstlane((int)h) - 1;
+}
+
+// launch B: g = the rule's max word; returns whether this launch has work (A stored the
+// accumulators -- `stored` -- or guessed a different bit width), else every block returns; block 0
+// writes the exponent, the next hint and store flag, and the counts
+__device__ __forceinline__ bool spec_settle(const RowConvArgs& a, uint32_t& g, bool& stored) {
+    g = read_max(a.amax);
+    const int bw = bitwidth_rc(g);
+    const uint32_t w1 = (uint32_t)__builtin_amdgcn_readfirstlane(
+        (int)__hip_atomic_load(a.hint + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    stored = (w1 >> 31) != 0;
+    const bool changed = bw != (int)(w1 & 0x7fffffffu) - 1;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        write_exponent(a, g);
+        __hip_atomic_store(a.hint, (uint32_t)bw + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // store mode for the next SPEC_COOLDOWN pairs after a change (a layer whose bit width flips
+        // from step to step, gradients near a power of two, stays there; block 0 of B is the only
+        // reader-writer of this word within a launch)
+        const uint32_t cd = __hip_atomic_load(a.hint + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(a.hint + 3, changed ? SPEC_COOLDOWN : (cd > 0u ? cd - 1u : 0u), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        if (stored) __hip_atomic_fetch_add(a.hint + 4, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else if (changed) __hip_atomic_fetch_add(a.hint + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return stored || changed;
+}
+
 
 // KS = 0: four units per workgroup; KS = NS: one unit, K split over the waves (wave 0 holds the sum)
 template <int W, int R, bool UNC, int KS>
@@ -1154,6 +1210,7 @@ __device__ __forceinline__ void seg_run(const RowConvArgs& a, int lane, int wid,
             m = unit_max<0, R>(U, acc, m);
             if (a.acc_store != nullptr) acc_put<R>(a, tile_wg(ck), wid, lane, acc);
         } else {
+            if (a.spec2 == 1) m = unit_max<0, R>(U, acc, m);  // speculative launch A publishes the max too
             if constexpr (DG) epi_masks<R, PX>(a, ein);
             if (U.valid) seg_epilogue<R, DG, PX>(a, U, lane, acc, g, ein);
             xa = __builtin_amdgcn_readfirstlane(U.valid ? st_n : 0);
@@ -1302,11 +1359,26 @@ __global__ void __launch_bounds__(256, (RC_EXP & 16) ? 2 : 1) rowconv_fwd_kernel
         __syncthreads();
         if (threadIdx.x == 0) publish_max(a.amax, max(max(red[0], red[1]), max(red[2], red[3])));
     } else if constexpr (MODE == RC_REQUANT && W == 0) {
-        const uint32_t g = read_max(a.amax);
-        if (blockIdx.x == 0 && threadIdx.x == 0) write_exponent(a, g);
+        uint32_t g = 0;
+        bool store = false;
+        if (a.spec2 == 1) {  // (the row-segment form stores no accumulators: always the guess)
+            const int guess = spec_guess(a, false, store);
+            g = guess <= 0 ? 0u : 1u << guess;
+        } else if (a.spec2 == 2) {
+            if (!spec_settle(a, g, store)) return;
+        } else {
+            g = read_max(a.amax);
+            if (blockIdx.x == 0 && threadIdx.x == 0) write_exponent(a, g);
+        }
         uint32_t m = 0;
         // the row-segment form's KS: 1 = an input gradient through a pool (its window operands)
         seg_run<R, RC_REQUANT, DG, KS != 0>(a, lane, wid, smem, m, g);
+        if (a.spec2 == 1) {
+            m = wave_max(m);
+            if (lane == 0) red[wid] = m;
+            __syncthreads();
+            if (threadIdx.x == 0) publish_max(a.amax, max(max(red[0], red[1]), max(red[2], red[3])));
+        }
     } else if constexpr (MODE == RC_RANGE) {
         uint32_t m = 0;
         for (int b = blockIdx.x; b < a.wgs; b += gridDim.x) {
@@ -1324,15 +1396,32 @@ __global__ void __launch_bounds__(256, (RC_EXP & 16) ? 2 : 1) rowconv_fwd_kernel
         if (threadIdx.x == 0) publish_max(a.amax, max(max(red[0], red[1]), max(red[2], red[3])));
         RC_STAMP(5);
     } else {
-        const uint32_t g = read_max(a.amax);
-        if (blockIdx.x == 0 && threadIdx.x == 0) write_exponent(a, g);
+        uint32_t g = 0, m = 0;
+        // load: the accumulators come from acc_store (the range launch's, or a storing launch A's);
+        // store: this launch A stores them instead of requantising (spec_guess)
+        bool load = a.acc_store != nullptr, store = false;
+        if (a.spec2 == 1) {
+            const int guess = spec_guess(a, true, store);
+            g = guess <= 0 ? 0u : 1u << guess;
+            load = false;
+        } else if (a.spec2 == 2) {
+            if (!spec_settle(a, g, load)) return;
+        } else {
+            g = read_max(a.amax);
+            if (blockIdx.x == 0 && threadIdx.x == 0) write_exponent(a, g);
+        }
         for (int b = blockIdx.x; b < a.wgs; b += gridDim.x) {
             const int wg = a.wmajor && (int)gridDim.x == a.wgs ? xcd_remap(b, gridDim.x) : b;
             const RowUnit<W, R> U(a, wg, wid, c, KS > 0);
-            if (a.acc_store != nullptr) {  // the range launch's accumulators (uniform branch)
+            if (load) {  // uniform branch
                 if (owner) acc_get<R>(a, wg, wid, lane, acc);
             } else {
                 compute_unit<W, R, UNC, KS>(a, U, lane, wid, smem, acc);
+            }
+            if (a.spec2 == 1 && owner) m = unit_max<W, R>(U, acc, m);
+            if (store) {
+                if (owner) acc_put<R>(a, wg, wid, lane, acc);
+                continue;
             }
             EpiIn<DG ? R : 1> ein = {};
             if constexpr (DG) {
@@ -1343,6 +1432,12 @@ __global__ void __launch_bounds__(256, (RC_EXP & 16) ? 2 : 1) rowconv_fwd_kernel
             }
             if (U.valid && owner) unit_epilogue<W, R, DG>(a, U, lane, acc, g, ein, smem + wid * RC_P16_WAVE_BYTES);
             if (DG && a.p16 != nullptr) __syncthreads();  // the P16 tiles sit in the next unit's ring
+        }
+        if (a.spec2 == 1) {
+            m = wave_max(m);
+            if (lane == 0) red[wid] = m;
+            __syncthreads();
+            if (threadIdx.x == 0) publish_max(a.amax, max(max(red[0], red[1]), max(red[2], red[3])));
         }
     }
 }
@@ -1694,6 +1789,11 @@ void rowconv_barrier_diag(uint32_t spin_limit, uint32_t expect_extra) {
     g_rc_expect_extra = expect_extra;
 }
 void rowconv_speculate(int mode) { g_rc_spec = mode; }
+uint32_t* rowconv_spec_slot(uint32_t* bar, bool dg) { return bar + (16 + (dg ? 1 : 0)) * BAR_LINE; }
+bool rowconv_spec2_on() {
+    static const char* env = getenv("NITI_RC_SPEC2");
+    return env == nullptr || env[0] != '0';
+}
 
 // Tile order over the XCDs: weight-major when the layer's weights outweigh its input (VGG-11's
 // 4x4 / 2x2 layers: 16 image groups re-read each co block's 147 KiB panel), else dispatch order.
@@ -1711,6 +1811,11 @@ void rowconv_stamps_arm(unsigned long long* buf) { g_rc_stamps = buf; }
 hipError_t rowconv_fwd(const ConvGeom& g, const int8_t* x_c32, const int8_t* wf, const RowConvOut& o, int mode,
                        uint32_t* amax, uint32_t* bar, uint32_t epoch, uint32_t* err, hipStream_t st) {
     if (!rowconv_ok(g) || x_c32 == nullptr || wf == nullptr || amax == nullptr) return hipErrorInvalidValue;
+    // modes RC_SPEC_A / RC_SPEC_B: the requantise instantiation as a speculative pair (spec_guess)
+    const bool spec = mode == RC_SPEC_A || mode == RC_SPEC_B;
+    if (spec && bar == nullptr) return hipErrorInvalidValue;
+    const int spec2 = spec ? mode - RC_SPEC_A + 1 : 0;
+    if (spec) mode = RC_REQUANT;
     // an output: NHWC16 out, the pool gradient, or (input gradient) only the C32 / P16 copies
     if (mode != RC_RANGE && o.out == nullptr && o.pool_dx == nullptr && o.next == nullptr && o.p16 == nullptr)
         return hipErrorInvalidValue;
@@ -1792,6 +1897,8 @@ hipError_t rowconv_fwd(const ConvGeom& g, const int8_t* x_c32, const int8_t* wf,
     a.p16 = o.p16;
     a.p16_pixels = (int64_t)g.n * g.h * g.w * (o.pool_dx != nullptr ? 4 : 1);
     a.acc_store = mode == RC_FUSED ? nullptr : o.acc_store;
+    a.spec2 = spec2;
+    a.hint = spec ? bar + (16 + (dg || o.dgrad_slot ? 1 : 0)) * BAR_LINE : nullptr;
     if (o.p16 != nullptr && (!dg || !rowconv_p16_ok(g, o.pool_dx != nullptr))) return hipErrorInvalidValue;
     if (o.pool_out != nullptr && (R % 2 != 0 || g.h % 2 != 0)) return hipErrorInvalidValue;
     if (mode == RC_FUSED) {
@@ -1896,6 +2003,10 @@ hipError_t rowconv_fc(int n, int K, int rows, const int8_t* x, int xld, const in
                       hipStream_t st) {
     if (!rowconv_fc_ok(n, K, rows, mode == RC_FUSED) || x == nullptr || w == nullptr || amax == nullptr)
         return hipErrorInvalidValue;
+    const bool spec = mode == RC_SPEC_A || mode == RC_SPEC_B;
+    if (spec && bar == nullptr) return hipErrorInvalidValue;
+    const int spec2 = spec ? mode - RC_SPEC_A + 1 : 0;
+    if (spec) mode = RC_REQUANT;
     if (xld % 16 != 0 || wld % 16 != 0 || xld < K || wld < K) return hipErrorInvalidValue;
     // an output: NHWC16 out, the pool gradient, or (input gradient) only the C32 / P16 copies
     if (mode != RC_RANGE && o.out == nullptr && o.pool_dx == nullptr && o.next == nullptr && o.p16 == nullptr)
@@ -1945,6 +2056,8 @@ hipError_t rowconv_fc(int n, int K, int rows, const int8_t* x, int xld, const in
     a.p16 = o.p16;
     a.p16_pixels = (int64_t)n * (o.pool_dx != nullptr ? 4 : 1);
     const bool dg = o.relu_mask != nullptr || o.pool_dx != nullptr || o.p16 != nullptr;
+    a.spec2 = spec2;
+    a.hint = spec ? bar + (16 + (dg || o.dgrad_slot ? 1 : 0)) * BAR_LINE : nullptr;
     if (o.p16 != nullptr && (o.pool_dx == nullptr || a.p16_pixels % 16 != 0)) return hipErrorInvalidValue;
     if (o.next != nullptr && a.cop % 32 != 0) return hipErrorInvalidValue;
     if (mode == RC_FUSED) {

@@ -124,6 +124,7 @@ def lib():
         "niti_conv_fwd_rows": (ci, [C.POINTER(Geom), vp, vp, vp, vp, vp, ci, vp, vp, vp, ci, vp, vp, C.c_uint32, vp,
                                     vp]),
         "niti_conv_dgrad_rows": (ci, [C.POINTER(Geom), vp, vp, vp, vp, vp, ci, vp, vp, vp, vp, vp, vp, ci, vp, vp, C.c_uint32, vp, vp]),
+        "niti_rows_spec_slot": (vp, [vp, ci]),
         "niti_conv_fwd_phase2": (ci, [C.POINTER(Geom), vp, vp, vp, vp, vp, vp, vp, ci, vp, vp, C.c_size_t, vp]),
         "niti_conv_dgrad_phase1": (ci, [C.POINTER(Geom), vp, vp, vp, vp, vp, C.c_size_t, vp]),
         "niti_conv_dgrad_phase2": (ci, [C.POINTER(Geom), vp, vp, vp, vp, vp, vp, vp, ci, vp, vp, C.c_size_t, vp]),
@@ -174,6 +175,7 @@ def lib():
         "niti_model_set_rowconv": (ci, [vp, ci]),
         "niti_model_keep_grads": (ci, [vp, ci]),
         "niti_model_rowconv_error": (ci, [vp]),
+        "niti_model_spec_stats": (ci, [vp, vp, ci]),
         "niti_model_autotune": (ci, [vp, ci, vp]),
         "niti_model_set_overlap": (ci, [vp, ci]),
         "niti_model_plan_info": (ci, [vp, ci, ci, C.POINTER(ci)]),

@@ -198,6 +198,14 @@ class NitiModel:
         """1 if an in-kernel grid barrier of the register-fed forward ever timed out."""
         return int(self._lib.niti_model_rowconv_error(self._h))
 
+    def spec_stats(self):
+        """Per layer: (fwd hint, fwd launches redone, fwd pairs stored, dgrad hint, dgrad redone,
+        dgrad stored) of the speculative row-kernel pairs (niti_model_spec_stats)."""
+        n = len(self.layers)
+        buf = (C.c_uint32 * (6 * n))()
+        check(self._lib.niti_model_spec_stats(self._h, buf, n), "spec_stats")
+        return [tuple(buf[6 * i:6 * i + 6]) for i in range(n)]
+
     def set_probe(self, layer: int, phase: int, max_launches: int = 256):
         check(self._lib.niti_model_set_probe(self._h, layer, phase, max_launches), "set_probe")
 

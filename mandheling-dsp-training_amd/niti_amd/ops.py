@@ -233,12 +233,22 @@ def weights_to_wf(w16: torch.Tensor, ci: int, transpose=False, stream=None, out=
 
 
 class RowConvState:
-    """Grid-barrier state of the fused register-fed conv (mode 0) and its epoch counter."""
+    """Grid-barrier state of the fused register-fed conv (mode 0) and its epoch counter; the
+    speculative pair's (modes 3 / 4) hint slots live in it too."""
 
     def __init__(self, device="cuda"):
         self.state = torch.zeros(ROWCONV_STATE_WORDS, dtype=torch.int32, device=device)
         self.err = torch.zeros(1, dtype=torch.int32, device=device)
         self.epoch = 0
+
+    def spec_offset(self, dgrad=False):
+        """Word offset in `state` of the speculative pair's forward / input-gradient slot."""
+        return (L.lib().niti_rows_spec_slot(_ptr(self.state), 1 if dgrad else 0) - self.state.data_ptr()) // 4
+
+    def spec_slot(self, dgrad=False):
+        """(hint, guess used, misses) of the speculative pair's forward / input-gradient slot."""
+        off = self.spec_offset(dgrad)
+        return tuple(int(v) for v in self.state[off:off + 3].cpu())
 
 
 ROWS_X_NHWC16 = 0x100  # NITI_ROWS_X_NHWC16
@@ -251,22 +261,28 @@ def rows_nhwc_ok(g: L.Geom, dgrad=False, preferred=False) -> bool:
 
 
 def conv_fwd_rows(g: L.Geom, xc32, wf, amax, mode=0, state: RowConvState | None = None, exp_in=None, wscale=None,
-                  exp_out=None, relu=False, pool=False, next_c32=False, x_nhwc=False, stream=None):
+                  exp_out=None, relu=False, pool=False, next_c32=False, x_nhwc=False, stream=None, outs=None):
     """The register-fed forward (niti_conv_fwd_rows): (out NHWC16, pooled NHWC16 or None,
-    next C32 or None).  mode 0 fused (state required), 1 range only, 2 requantise with amax.
+    next C32 or None).  mode 0 fused (state required), 1 range only, 2 requantise with amax;
+    3 / 4 the speculative pair (state required; mode 4 takes mode 3's outputs as `outs`).
     x_nhwc: xc32 is the NHWC16 input itself (rows_nhwc_ok)."""
     dev = xc32.device
-    out = None if mode == 1 else torch.empty((g.n, g.oh, g.ow, g.cop), dtype=torch.int8, device=dev)
-    pout = torch.empty((g.n, g.oh // 2, g.ow // 2, g.cop), dtype=torch.int8, device=dev) if pool and mode != 1 else None
-    nxt = None
-    if next_c32 and mode != 1:
-        hh, ww = (g.oh // 2, g.ow // 2) if pool else (g.oh, g.ow)
-        nxt = torch.empty((g.n, g.cop // 32, hh, ww, 32), dtype=torch.int8, device=dev)
+    if outs is not None:
+        out, pout, nxt = outs
+    else:
+        out = None if mode == 1 else torch.empty((g.n, g.oh, g.ow, g.cop), dtype=torch.int8, device=dev)
+        pout = torch.empty((g.n, g.oh // 2, g.ow // 2, g.cop), dtype=torch.int8, device=dev) if pool and mode != 1 else None
+        nxt = None
+        if next_c32 and mode != 1:
+            hh, ww = (g.oh // 2, g.ow // 2) if pool else (g.oh, g.ow)
+            nxt = torch.empty((g.n, g.cop // 32, hh, ww, 32), dtype=torch.int8, device=dev)
     st_ptr = err_ptr = None
     epoch = 0
     if mode == 0:
         state.epoch += 1
         epoch, st_ptr, err_ptr = state.epoch, _ptr(state.state), _ptr(state.err)
+    elif mode >= 3:
+        st_ptr = _ptr(state.state)
     check(L.lib().niti_conv_fwd_rows(C.byref(g), _ptr(xc32), _ptr(wf), _ptr(exp_in), _ptr(wscale), _ptr(exp_out),
                                      1 if relu else 0, _ptr(out), _ptr(pout), _ptr(nxt),
                                      mode | (ROWS_X_NHWC16 if x_nhwc else 0), _ptr(amax), st_ptr,
@@ -276,21 +292,26 @@ def conv_fwd_rows(g: L.Geom, xc32, wf, amax, mode=0, state: RowConvState | None 
 
 def conv_dgrad_rows(g: L.Geom, dyc32, wft, amax, mode=0, state: RowConvState | None = None, relu_mask=None,
                     pool_x=None, pool_y=None, pool_relu=False, dx_c32=False, dx_p16=False, exp_in=None, wscale=None,
-                    exp_out=None, x_nhwc=False, stream=None):
+                    exp_out=None, x_nhwc=False, stream=None, outs=None):
     """The input gradient on the register-fed kernel (niti_conv_dgrad_rows) for the layer of
     geometry g: (dx NHWC16, dx C32 or None, dx P16 or None).  dx is [n][h][w][cip], or
     [n][2h][2w][cip] routed through the previous layer's 2x2 max pool when pool_x / pool_y are
-    given."""
+    given.  Modes as conv_fwd_rows."""
     dev = dyc32.device
     hh, ww = (2 * g.h, 2 * g.w) if pool_x is not None else (g.h, g.w)
-    dx = None if mode == 1 else torch.empty((g.n, hh, ww, g.cip), dtype=torch.int8, device=dev)
-    nxt = torch.empty((g.n, g.cip // 32, hh, ww, 32), dtype=torch.int8, device=dev) if dx_c32 and mode != 1 else None
-    p16 = torch.empty((g.n * hh * ww // 16, g.cip, 16), dtype=torch.int8, device=dev) if dx_p16 and mode != 1 else None
+    if outs is not None:
+        dx, nxt, p16 = outs
+    else:
+        dx = None if mode == 1 else torch.empty((g.n, hh, ww, g.cip), dtype=torch.int8, device=dev)
+        nxt = torch.empty((g.n, g.cip // 32, hh, ww, 32), dtype=torch.int8, device=dev) if dx_c32 and mode != 1 else None
+        p16 = torch.empty((g.n * hh * ww // 16, g.cip, 16), dtype=torch.int8, device=dev) if dx_p16 and mode != 1 else None
     st_ptr = err_ptr = None
     epoch = 0
     if mode == 0:
         state.epoch += 1
         epoch, st_ptr, err_ptr = state.epoch, _ptr(state.state), _ptr(state.err)
+    elif mode >= 3:
+        st_ptr = _ptr(state.state)
     check(L.lib().niti_conv_dgrad_rows(C.byref(g), _ptr(dyc32), _ptr(wft), _ptr(relu_mask), _ptr(pool_x),
                                        _ptr(pool_y), 1 if pool_relu else 0, _ptr(dx), _ptr(nxt), _ptr(p16),
                                        _ptr(exp_in), _ptr(wscale), _ptr(exp_out),

@@ -14,6 +14,8 @@ SUM / MAX-reduced -- so each rank is bit-identical to one device running the glo
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 
@@ -161,7 +163,8 @@ class ResNet18:
 
     def _rows(self, fwd, i, xc, amax, **kw):
         """One row-kernel conv: the fused launch where it is possible (one device, not capturing, the
-        grid resident), else range, [global MAX], recompute-or-stored requantise."""
+        grid resident), else the speculative pair (modes 3, [global MAX], 4) or range, [global
+        MAX], recompute-or-stored requantise."""
         f = ops.conv_fwd_rows if fwd else ops.conv_dgrad_rows
         g, wf = self.geoms[i], self.wf[i] if fwd else self.wft[i]
         if self.comm is None and not torch.cuda.is_current_stream_capturing():
@@ -170,6 +173,12 @@ class ResNet18:
             except NitiError as e:
                 if e.code != 2:  # NOT_SUPPORT: the grid is not resident
                     raise
+        if os.environ.get("NITI_RC_SPEC2", "1") != "0":
+            # the speculative pair: requantised with the layer's previous bit width, redone only
+            # where the (global) max's bit width differs
+            outs = f(g, xc, wf, amax, mode=3, state=self.rstate[i], **kw)
+            self._global_range(amax)
+            return f(g, xc, wf, amax, mode=4, state=self.rstate[i], outs=outs, **kw)[0]
         f(g, xc, wf, amax, mode=1, **kw)
         self._global_range(amax)
         return f(g, xc, wf, amax, mode=2, **kw)[0]

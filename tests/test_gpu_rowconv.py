@@ -43,30 +43,53 @@ def _case(T, n, ci, h, co, relu, pool, mode, seed, wmax=127, xmax=127, x_nhwc=Fa
         assert ops.rows_nhwc_ok(gg)
         xc = x16
         kw["x_nhwc"] = True
+    def check(out, pout, nxt):
+        T.cuda.synchronize()
+        assert int(st.err.item()) == 0
+        got = out.cpu().numpy()[..., :co].transpose(0, 3, 1, 2)
+        assert np.array_equal(got, r_ref)
+        assert int(eo.item()) == e_ref
+        if pool:
+            p_ref = O.maxpool(r_ref)
+            assert np.array_equal(pout.cpu().numpy()[..., :co].transpose(0, 3, 1, 2), p_ref)
+            want_next = p_ref
+        else:
+            want_next = r_ref
+        nx = nxt.cpu().numpy()  # [n][cb][h][w][32]
+        nx = nx.transpose(0, 1, 4, 2, 3).reshape(n, -1, nx.shape[2], nx.shape[3])[:, :co]
+        assert np.array_equal(nx, want_next)
+
     if mode == 0:
-        out, pout, nxt = ops.conv_fwd_rows(gg, xc, wf, amax, mode=0, state=st, **kw)
+        check(*ops.conv_fwd_rows(gg, xc, wf, amax, mode=0, state=st, **kw))
+    elif mode == 4:
+        _spec_pairs(T, st, False, amax, eo, lambda m, outs: ops.conv_fwd_rows(gg, xc, wf, amax, mode=m, state=st,
+                                                                              outs=outs, **kw), check)
     else:
         ops.conv_fwd_rows(gg, xc, wf, amax, mode=1, **kw)
-        out, pout, nxt = ops.conv_fwd_rows(gg, xc, wf, amax, mode=2, **kw)
-    T.cuda.synchronize()
-    assert int(st.err.item()) == 0
-    got = out.cpu().numpy()[..., :co].transpose(0, 3, 1, 2)
-    assert np.array_equal(got, r_ref)
-    assert int(eo.item()) == e_ref
-    if pool:
-        p_ref = O.maxpool(r_ref)
-        assert np.array_equal(pout.cpu().numpy()[..., :co].transpose(0, 3, 1, 2), p_ref)
-        want_next = p_ref
-    else:
-        want_next = r_ref
-    nx = nxt.cpu().numpy()  # [n][cb][h][w][32]
-    nx = nx.transpose(0, 1, 4, 2, 3).reshape(n, -1, nx.shape[2], nx.shape[3])[:, :co]
-    assert np.array_equal(nx, want_next)
+        check(*ops.conv_fwd_rows(gg, xc, wf, amax, mode=2, **kw))
     return int(np.abs(acc).max())
 
 
+def _spec_pairs(T, st, dgrad, amax, eo, launch, check):
+    """The speculative pair (modes 3 + 4) three times on one state: no hint yet (launch 4 redoes),
+    the hint of the first pair (a hit: launch 4 exits at once), and a hint forced one bit wide
+    (launch 4 redoes); every pair's outputs are the rule's, and the slot counts the two misses."""
+    off = st.spec_offset(dgrad)
+    for rep in range(3):
+        if rep == 2:
+            hint = int(st.state[off].item())
+            st.state[off] = hint + 1 if hint < 20 else hint - 1
+        amax.zero_()
+        if eo is not None:
+            eo.zero_()
+        outs = launch(3, None)
+        outs = launch(4, outs)
+        check(*outs)
+        assert st.spec_slot(dgrad)[2] == (1 if rep < 2 else 2), (rep, st.spec_slot(dgrad))
+
+
 @pytest.mark.parametrize("h", [2, 4, 8, 16])
-@pytest.mark.parametrize("mode", [0, 2])
+@pytest.mark.parametrize("mode", [0, 2, 4])
 def test_rows_fwd_widths(T, h, mode):
     for k, (n, ci, co, relu, pool) in enumerate([(3, 32, 32, True, True), (17, 64, 64, False, False),
                                                   (1, 96, 32, True, False), (8, 32, 96, False, True)]):
@@ -80,7 +103,7 @@ def test_rows_fwd_shift_branches(T):
     shift > 1 branches of the rule (NITI_Conv_Int8.cpp:266-307)."""
     seen = set()
     for seed, (wmax, xmax) in enumerate([(1, 1), (1, 2), (1, 3), (2, 2), (2, 3), (3, 4), (127, 127)]):
-        for mode in (0, 2):
+        for mode in (0, 2, 4):
             m = _case(T, 4, 32, 4, 32, False, False, mode, seed=900 + seed, wmax=wmax, xmax=xmax)
             bw = 0 if m <= 1 else int(np.ceil(np.log2(m)))
             seen.add("raw" if bw <= 7 else "one" if bw == 8 else "psto")
@@ -136,27 +159,39 @@ def _dgrad_case(T, n, ci, h, co, pool, relu, mode, seed, wmax=127, dmax=127, p16
     def launch(**k):
         if mode == 0:
             return ops.conv_dgrad_rows(gg, dyc, wft, amax, mode=0, state=st, **k)
+        if mode == 4:  # the pair's first call here (the NOT_SUPPORT probe); _spec_pairs repeats it
+            outs = ops.conv_dgrad_rows(gg, dyc, wft, amax, mode=3, state=st, **k)
+            return ops.conv_dgrad_rows(gg, dyc, wft, amax, mode=4, state=st, outs=outs, **k)
         ops.conv_dgrad_rows(gg, dyc, wft, amax, mode=1, **k)
         return ops.conv_dgrad_rows(gg, dyc, wft, amax, mode=2, **k)
+
+    def check(dx, dxc, p16):
+        T.cuda.synchronize()
+        assert int(st.err.item()) == 0
+        assert np.array_equal(dx.cpu().numpy()[..., :ci].transpose(0, 3, 1, 2), want)
+        nx = dxc.cpu().numpy()
+        nx = nx.transpose(0, 1, 4, 2, 3).reshape(n, -1, nx.shape[2], nx.shape[3])[:, :ci]
+        assert np.array_equal(nx, want)
+        if p16 is not None:  # the weight gradient's pixel blocks, as niti_nhwc16_to_p16 lays them out
+            assert np.array_equal(p16.cpu().numpy(), ops.nhwc16_to_p16(dx).cpu().numpy())
+
     try:
-        dx, dxc, p16 = launch(**kw)
+        res = launch(**kw)
     except NitiError as e:  # no whole 16-pixel blocks per wave (4x4 images, no pool, small batch) or tensor
         assert e.code == 2 and not pool and (h == 4 or n * h * h % 16 != 0), (e, h, pool)
         kw["dx_p16"] = False
-        dx, dxc, p16 = launch(**kw)
-    T.cuda.synchronize()
-    assert int(st.err.item()) == 0
-    assert np.array_equal(dx.cpu().numpy()[..., :ci].transpose(0, 3, 1, 2), want)
-    nx = dxc.cpu().numpy()
-    nx = nx.transpose(0, 1, 4, 2, 3).reshape(n, -1, nx.shape[2], nx.shape[3])[:, :ci]
-    assert np.array_equal(nx, want)
-    if p16 is not None:  # the weight gradient's pixel blocks, as niti_nhwc16_to_p16 lays them out
-        assert np.array_equal(p16.cpu().numpy(), ops.nhwc16_to_p16(dx).cpu().numpy())
+        res = launch(**kw)
+    if mode == 4:
+        st.state.zero_()  # a fresh slot for the three pairs
+        _spec_pairs(T, st, True, amax, None, lambda m, outs: ops.conv_dgrad_rows(gg, dyc, wft, amax, mode=m, state=st,
+                                                                                 outs=outs, **kw), check)
+    else:
+        check(*res)
     return int(np.abs(acc).max())
 
 
 @pytest.mark.parametrize("h", [2, 4, 8, 16])
-@pytest.mark.parametrize("mode", [0, 2])
+@pytest.mark.parametrize("mode", [0, 2, 4])
 def test_rows_dgrad_widths(T, h, mode):
     for k, (n, ci, co, pool, relu) in enumerate([(3, 32, 32, True, True), (17, 64, 64, False, True),
                                                   (1, 96, 32, True, False), (8, 32, 96, False, False)]):
@@ -179,7 +214,7 @@ def test_rows_dgrad_vgg11_shapes(T):
     _dgrad_case(T, 32, 256, 8, 256, False, True, 0, seed=42)
 
 
-@pytest.mark.parametrize("mode", [0, 2])
+@pytest.mark.parametrize("mode", [0, 2, 4])
 def test_rows_ks_2x2(T, mode):
     """The K-split form (rowconv_compute_ks: 2x2 maps whose conv input channels are a multiple of
     128 -- one unit per workgroup, the four waves splitting the channel chunks, partial tiles summed
@@ -205,7 +240,7 @@ def test_rows_ks_vgg11_2x2_b256(T):
 
 
 @pytest.mark.parametrize("h", [14, 28, 56])
-@pytest.mark.parametrize("mode", [0, 2])
+@pytest.mark.parametrize("mode", [0, 2, 4])
 def test_rows_seg_fwd(T, h, mode):
     """Forward with the rescale (fused launch, or range then recompute-and-requantise), relu, the
     2x2 pool (pairs inside a segment) and the C32 copy, ragged image pairs at 14 px."""
@@ -221,7 +256,7 @@ def test_rows_seg_fwd_large(T, h):
 
 
 @pytest.mark.parametrize("h", [14, 28, 56])
-@pytest.mark.parametrize("mode", [0, 2])
+@pytest.mark.parametrize("mode", [0, 2, 4])
 def test_rows_seg_dgrad(T, h, mode):
     """Input gradient on the row-segment form with the previous layer's relu gradient or its 2x2
     max-pool (+ relu) gradient routed into the full-resolution map, NHWC16 and C32 outputs."""
@@ -233,7 +268,7 @@ def test_rows_seg_dgrad(T, h, mode):
 def test_rows_seg_shift_branches(T):
     seen = set()
     for seed, (wmax, xmax) in enumerate([(1, 1), (1, 2), (1, 3), (2, 3), (3, 4), (127, 127)]):
-        for mode in (0, 2):
+        for mode in (0, 2, 4):
             m = _case(T, 2, 32, 28, 32, False, False, mode, seed=5000 + seed, wmax=wmax, xmax=xmax)
             bw = 0 if m <= 1 else int(np.ceil(np.log2(m)))
             seen.add("raw" if bw <= 7 else "one" if bw == 8 else "psto")
@@ -241,7 +276,7 @@ def test_rows_seg_shift_branches(T):
 
 
 @pytest.mark.parametrize("h", [14, 28, 56])
-@pytest.mark.parametrize("mode", [0, 2])
+@pytest.mark.parametrize("mode", [0, 2, 4])
 def test_rows_seg_nhwc_input(T, h, mode):
     """The row-segment form reading its input (x, or dy) as NHWC16 in place (NITI_ROWS_X_NHWC16):
     the same outputs as from the C32 copy, forward and input gradient."""
