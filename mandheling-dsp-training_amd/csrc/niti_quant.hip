@@ -194,6 +194,14 @@ __device__ __forceinline__ int8_t quant_pixel(uint32_t p, const QuantParams& q) 
     return (int8_t)(int)roundf(y / q.range * 127.0f);
 }
 
+// A pixel is a uint8, so the whole map is 256 entries: each block evaluates quant_pixel once per
+// value into LDS (the same float sequence, so the same bytes) and the per-pixel work is a lookup
+// instead of two float divisions.  Call with all threads of a 256-thread block after q is set.
+__device__ __forceinline__ void quant_lut_fill(int8_t* lut, const QuantParams& q) {
+    if (threadIdx.x < 256) lut[threadIdx.x] = quant_pixel(threadIdx.x, q);
+    __syncthreads();
+}
+
 // out: NHWC16 [n][hw][cp] (nhwc = true, the step's layer-0 input: one thread per pixel, its c
 // channels packed into 16-byte stores) or NCHW [n][c][hw] (one thread per element).  Thread 0 of
 // each block derives the parameters (double log / sqrt), so the grid is kept to a few blocks per
@@ -204,12 +212,13 @@ __global__ void __launch_bounds__(256) image_quant_kernel(const uint8_t* __restr
                                                           int64_t count, int64_t var_count,
                                                           int8_t* __restrict__ out, int8_t* __restrict__ ascale) {
     __shared__ QuantParams sq;
+    __shared__ int8_t lut[256];
     if (threadIdx.x == 0) {
         sq = quant_params(stats, count, var_count);
         if (blockIdx.x == 0 && ascale != nullptr) *ascale = (int8_t)sq.ascale;
     }
     __syncthreads();
-    const QuantParams q = sq;
+    quant_lut_fill(lut, sq);
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     if (NHWC) {
         const int64_t pixels = (int64_t)n * hw;
@@ -223,15 +232,31 @@ __global__ void __launch_bounds__(256) image_quant_kernel(const uint8_t* __restr
 #pragma unroll
                 for (int j = 0; j < 16; ++j) {
                     const int ch = 16 * k + j;
-                    v[j] = ch < c ? quant_pixel(src[(int64_t)ch * hw], q) : (int8_t)0;
+                    v[j] = ch < c ? lut[src[(int64_t)ch * hw]] : (int8_t)0;
                 }
                 *(v16c*)(dst + 16 * k) = v;
             }
         }
     } else {
-        const int64_t total = (int64_t)n * c * hw;
-        for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += stride)
-            out[i] = quant_pixel(img[i], q);
+        // 16 pixels per thread and step (16-byte loads and stores), the tail one by one
+        const int64_t total = (int64_t)n * c * hw, n16 = total / 16;
+        const uint4* in16 = reinterpret_cast<const uint4*>(img);
+        uint4* out16 = reinterpret_cast<uint4*>(out);
+        for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n16; i += stride) {
+            const uint4 v = in16[i];
+            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+            uint32_t o[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                uint32_t r = 0;
+#pragma unroll
+                for (int b = 0; b < 4; ++b) r |= (uint32_t)(uint8_t)lut[(w[j] >> (8 * b)) & 255u] << (8 * b);
+                o[j] = r;
+            }
+            out16[i] = uint4{o[0], o[1], o[2], o[3]};
+        }
+        for (int64_t i = n16 * 16 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += stride)
+            out[i] = lut[img[i]];
     }
 }
 
@@ -265,7 +290,8 @@ __global__ void __launch_bounds__(256) input_im2col_kernel(const void* __restric
         }
         __syncthreads();
     }
-    const QuantParams q = sq;
+    __shared__ int8_t lut[256];
+    if constexpr (QUANT) quant_lut_fill(lut, sq);
     // input rows this band writes to the tap: [oy0, oy0 + band), the last band through h
     const bool last = blockIdx.x % bands == bands - 1;
     const int own0 = oy0, own1 = last ? h : oy0 + band;
@@ -280,7 +306,7 @@ __global__ void __launch_bounds__(256) input_im2col_kernel(const void* __restric
                 const int64_t e = (((int64_t)img * C + c) * h + iy) * w + ix;
                 int8_t qv;
                 if constexpr (QUANT)
-                    qv = quant_pixel(((const uint8_t*)in)[e], q);
+                    qv = lut[((const uint8_t*)in)[e]];
                 else
                     qv = ((const int8_t*)in)[e];
                 v |= (uint32_t)(uint8_t)qv << (8 * c);
@@ -414,11 +440,13 @@ hipError_t input_im2col(const void* in, bool quant, int n, int c, int h, int w, 
 }
 
 hipError_t image_stats(const uint8_t* img, int64_t n, unsigned long long* stats, hipStream_t st) {
-    // the standalone op: up to 64 blocks' atomics into the zeroed stats (the step spreads the
-    // pixels over IMAGE_STATS_SLOTS blocks and sums their slots where it uses them)
+    // the standalone op: up to 512 blocks' atomics into the zeroed stats (the step spreads the
+    // pixels over IMAGE_STATS_SLOTS blocks and sums their slots where it uses them).  64 blocks
+    // (one wave per CU) took 43 us over a 128 x 224 x 224 batch: latency-bound loads, not the
+    // atomics
     if (n <= 0) return hipErrorInvalidValue;
     int64_t blocks = (n / 16 + 255) / 256;
-    blocks = blocks < 1 ? 1 : blocks > 64 ? 64 : blocks;
+    blocks = blocks < 1 ? 1 : blocks > 512 ? 512 : blocks;
     const hipError_t e = hipMemsetAsync(stats, 0, 4 * sizeof(unsigned long long), st);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(image_stats_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, st, img, n, stats);
@@ -432,8 +460,9 @@ hipError_t image_quantize(const uint8_t* img, int n, int c, int hw, int cp, cons
     const int64_t total = nhwc16 ? (int64_t)n * hw : (int64_t)n * c * hw;
     // MnistUtils.cpp:86: the variance over batchSize * 28 * 28, batchSize = the images `count` covers
     const int64_t var_count = count / ((int64_t)c * hw) * 784;
-    int64_t blocks = (total + 255) / 256;
-    blocks = blocks > 512 ? 512 : blocks;
+    const int64_t work = nhwc16 ? total : total / 16 + 1;  // NCHW: 16 pixels per thread
+    int64_t blocks = (work + 255) / 256;
+    blocks = blocks > 2048 ? 2048 : blocks;
     if (nhwc16)
         hipLaunchKernelGGL(image_quant_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, st, img, n, c, hw, cp,
                            stats, count, var_count, out, ascale);

@@ -180,16 +180,25 @@ __global__ void __launch_bounds__(256) im2col_small_kernel(const int8_t* __restr
     __syncthreads();
     const int kc = kp / 16, kt = KH * KW * C;
     int8_t* out = xcol + (int64_t)row * g.ow * kp;
-    for (int e = threadIdx.x; e < g.ow * kc; e += 256) {
-        const int ox = e / kc, j = e - ox * kc;
+    // a thread keeps one 16-byte column chunk j of every output pixel it writes (ox steps by
+    // 256 / kc), so the chunk's 16 tile offsets (tap and channel, without the pixel's column) are
+    // computed once into registers; -1: a padding column k >= KH KW C
+    const int per = 256 / kc;  // pixels per pass
+    if ((int)threadIdx.x >= per * kc) return;
+    const int j = threadIdx.x % kc;
+    int koff[16];
+#pragma unroll
+    for (int b = 0; b < 16; ++b) {
+        const int k = 16 * j + b;
+        const int tap = k / C, c = k - tap * C;
+        const int ky = tap / KW, kx = tap - ky * KW;
+        koff[b] = k < kt ? (ky * cols + kx * g.dw) * C + c : -1;
+    }
+    for (int ox = threadIdx.x / kc; ox < g.ow; ox += per) {
+        const int xo = ox * g.sw * C;
         v16c o;
 #pragma unroll
-        for (int b = 0; b < 16; ++b) {
-            const int k = 16 * j + b;
-            const int tap = k / C, c = k - tap * C;
-            const int ky = tap / KW, kx = tap - ky * KW;
-            o[b] = k < kt ? tile[(ky * cols + ox * g.sw + kx * g.dw) * C + c] : (int8_t)0;
-        }
+        for (int b = 0; b < 16; ++b) o[b] = koff[b] >= 0 ? tile[xo + koff[b]] : (int8_t)0;
         *(v16c*)(out + (int64_t)ox * kp + 16 * j) = o;
     }
 }
