@@ -91,6 +91,7 @@ class ResNet18:
         self.wf = [None] * len(self.convs)
         self.wft = [None] * len(self.convs)
         self.rstate = [ops.RowConvState(device) if r else None for r in self.rows]
+        self.fwd_recompute = set()  # forward GEMM shapes the autotuner put on the two-phase recompute form
         self.record = False
         self.rec = {}
         # range buffers and exponent scalars of one step, allocated once and handed out in order
@@ -209,10 +210,14 @@ class ResNet18:
             if i == 0:  # the stem: its im2col (from NCHW or NHWC16), kept for the weight gradient
                 self._xcol = ops.im2col(self.stem_geom, x16, self.STEM_KP, nchw=x16.dim() == 4 and x16.shape[1] == 3)
                 xg = self._xcol
-            acc = ops.conv_fwd_acc(g, xg, self.w16[i], amax)
-            self._global_range(amax)
             e_out = self._exp()
-            y = ops.requant_act(acc, amax, exp_in=e_in, wscale=self.ws_dev[i], exp_out=e_out, relu=relu)
+            if self._fwd_key(i) in self.fwd_recompute:  # autotune: the two-phase recompute form is faster
+                y = ops.conv_fwd_requant(g, xg, self.w16[i], amax, exp_in=e_in, wscale=self.ws_dev[i], exp_out=e_out,
+                                         relu=relu, between=self._global_range)
+            else:
+                acc = ops.conv_fwd_acc(g, xg, self.w16[i], amax)
+                self._global_range(amax)
+                y = ops.requant_act(acc, amax, exp_in=e_in, wscale=self.ws_dev[i], exp_out=e_out, relu=relu)
         y = y.view(self.batch, l["oh"], l["oh"], -1)
         if self.record:
             self.rec.setdefault("fwd", {})[i] = (y, relu)
@@ -271,6 +276,10 @@ class ResNet18:
         return q, e_out
 
     # ---------------------------------------------------------------- plans
+    def _fwd_key(self, i, op=0):  # the autotuner's per-shape key of layer i's GEMM `op`
+        g = self.geoms[i]
+        return (op, g.n, g.c_in, g.h, g.w, g.c_out, g.kh, g.stride_h if hasattr(g, "stride_h") else 0, g.oh, g.ow)
+
     def autotune(self, reps=3):
         """Per-shape plan autotuning of the GEMM-path convs (what niti_model_autotune does for the C++
         Model): every candidate tile / K-split plan of each forward, input-gradient and weight-gradient
@@ -305,8 +314,7 @@ class ResNet18:
             w16 = torch.randint(-8, 8, (g.c_out, g.kh, g.kw, g.cip), dtype=torch.int8, device=dev)
             wT = torch.randint(-8, 8, (g.c_in, g.kh, g.kw, g.cop), dtype=torch.int8, device=dev)
             for op in phases:
-                key = (op, g.n, g.c_in, g.h, g.w, g.c_out, g.kh, g.stride_h if hasattr(g, "stride_h") else 0,
-                       g.oh, g.ow)
+                key = self._fwd_key(i, op)
                 if key in done:
                     continue
                 done.add(key)
@@ -333,6 +341,23 @@ class ResNet18:
                         best_plan, best_us = plan, us
                 ops.conv_plan_set(g, op, best_plan)
                 out[(i, op)] = (best_plan, best_us)
+                if op == 0:
+                    # the forward with its requantisation: int32 stored + requant_act, or the two-phase
+                    # form recomputing the GEMM (strategy 1: no int32 round trip; the stem's K = 160
+                    # GEMM moves 257 MB of im2col against 411 MB of int32 out and back)
+                    bm, bn = best_plan[:2] if best_plan else ops.conv_plan(g, 0)[:2]
+                    e8 = torch.zeros(1, dtype=torch.int8, device=dev)
+                    t_acc = timed(lambda: ops.requant_act(run(), amax, exp_in=e8, wscale=e8, exp_out=e8))
+                    try:
+                        ops.conv_plan_set(g, 0, (bm, bn, 1, 1))
+                        t_rc = timed(lambda: ops.conv_fwd_requant(g, x16, w16, amax, exp_in=e8, wscale=e8, exp_out=e8))
+                    except NitiError:
+                        t_rc = float("inf")
+                    if t_rc < t_acc:
+                        self.fwd_recompute.add(key)
+                        out[(i, "fwd_recompute")] = ((bm, bn, 1, 1), t_rc)
+                    else:
+                        ops.conv_plan_set(g, 0, best_plan)
         return out
 
     # ---------------------------------------------------------------- step

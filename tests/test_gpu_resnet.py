@@ -52,6 +52,49 @@ def test_resnet18_step_matches_oracle(T, hw, batch, classes):
         W = newW
 
 
+def test_resnet18_autotuned_and_recompute_forwards_match_oracle(T):
+    """The autotuner's per-shape plans, then every GEMM-path forward forced onto the two-phase
+    recompute form (strategy 1: range pass, GEMM recomputed and requantised -- what the autotuner
+    picks for the stem), two steps against the oracle; the plans are cleared afterwards."""
+    import niti_oracle as O
+    import niti_resnet_ref as RR
+    from niti_amd import ops
+    from niti_amd.resnet import ResNet18
+    hw, batch, classes = 64, 3, 1000
+    convs = RR.resnet18_convs(hw, classes)
+    W, S = RR.init_weights(convs, seed=77)
+    rng = np.random.default_rng(77)
+    m = ResNet18(batch, hw, classes)
+    for i, (w, s) in enumerate(zip(W, S)):
+        m.set_weight(i, w, s)
+    try:
+        m.autotune(reps=1)
+        for i in range(len(m.convs)):
+            if not (m.use_rows and m.rows[i]):
+                ops.conv_plan_set(m.geoms[i], 0, (128, 128, 1, 1))
+                m.fwd_recompute.add(m._fwd_key(i))
+        m.record = True
+        for step in range(2):
+            x = rng.integers(-127, 128, (batch, 3, hw, hw)).astype(np.int8)
+            labels = rng.integers(0, classes, batch).astype(np.int32)
+            newW, rec = RR.train_step(convs, W, S, x, -2, labels, classes=classes)
+            m.train_step(T.from_numpy(x).cuda(), -2, T.from_numpy(labels).cuda())
+            t = m.taps()
+            assert t["exp_logits"] == rec["exp_logits"] and np.array_equal(t["logits"], rec["logits"]), step
+            for i, c in enumerate(convs):
+                relu = m.rec["fwd"][i][1]
+                want = O.relu(rec["fwd"][i]) if relu else rec["fwd"][i]
+                assert np.array_equal(t["fwd"][i], want), ("fwd", step, c["name"])
+                assert np.array_equal(t["dy"][i], rec["dy"][i]), ("dy", step, c["name"])
+                assert np.array_equal(t["dw"][i], rec["dw"][i]), ("dw", step, c["name"])
+                assert np.array_equal(m.get_weight(i), newW[i]), ("w", step, c["name"])
+            W = newW
+    finally:
+        for g in m.geoms:
+            for op in (0, 1, 2):
+                ops.conv_plan_set(g, op, None)
+
+
 def test_resnet18_224_step_matches_oracle(T):
     """BASELINE config 5's input size (224x224, batch 2, 1000 classes), one whole step against the
     oracle: the 7x7 / 2 stem and its weight gradient over the 224-px input, the overlapping 3x3 / 2
