@@ -66,6 +66,27 @@ def test_geometry(L):
     assert lib.niti_geom_finalize(C.byref(g)) == 3  # COMPUTE_SIZE_ERROR
 
 
+def test_row_conv_speculative_modes_validation(L):
+    """Modes 3 / 4 (the speculative pair) need the state buffer that holds the layer's hint slot;
+    modes past 4 are refused; the slot accessor is pure pointer arithmetic (no device access)."""
+    lib = L.lib()
+    g = L.Geom(2, 64, 56, 56, 64, 3, 3, 1, 1, 1, 1, 1, 1, 1, 1, 0, 0, 0, 0, 0)
+    assert lib.niti_geom_finalize(C.byref(g)) == 0
+    dummy = C.c_void_p(16)  # never dereferenced: the calls fail validation first
+    for mode in (3, 4):
+        assert lib.niti_conv_fwd_rows(C.byref(g), dummy, dummy, None, None, None, 0, dummy, None, None, mode, dummy,
+                                      None, 0, None, None) == 5  # INVALID_VALUE: no state
+        assert lib.niti_conv_dgrad_rows(C.byref(g), dummy, dummy, None, None, None, 0, dummy, None, None, None,
+                                        None, None, mode, dummy, None, 0, None, None) == 5
+    assert lib.niti_conv_fwd_rows(C.byref(g), dummy, dummy, None, None, None, 0, dummy, None, None, 5, dummy, dummy, 0,
+                                  None, None) == 5
+    base = 4096
+    fwd, dg = lib.niti_rows_spec_slot(C.c_void_p(base), 0), lib.niti_rows_spec_slot(C.c_void_p(base), 1)
+    assert fwd is not None and dg is not None and dg - fwd == 128  # one 128-byte line per direction
+    assert (fwd - base) // 4 + 5 <= 1216  # inside NITI_ROWCONV_STATE_WORDS
+    assert lib.niti_rows_spec_slot(None, 0) is None
+
+
 def test_no_fallback_when_library_missing(tmp_path, monkeypatch):
     import importlib
 
