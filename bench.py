@@ -104,6 +104,21 @@ def synth_weights(layers, seed):
     return out
 
 
+RIDGE_OPS_PER_BYTE = PEAK_INT8_TOPS * 1e12 / (PEAK_HBM_GBS * 1e9)  # ~629 int8 op per HBM byte
+
+
+def roof_labels(ops, alg_bytes, mfma_frac, hbm_frac):
+    """(bound, limiter) of a probed launch.  bound: the roof its arithmetic intensity puts it under
+    (algorithmic ops / algorithmic bytes against the ridge point) -- the roof `frac` is priced
+    against.  limiter: what the two measured fractions say holds it back -- "mfma" or "hbm" when
+    that fraction reaches 0.5, else "latency/issue" (neither roof is close: launch ramp, barriers,
+    instruction issue)."""
+    bound = "mfma" if ops / max(alg_bytes, 1) >= RIDGE_OPS_PER_BYTE else "hbm"
+    fr = {"mfma": mfma_frac or 0.0, "hbm": hbm_frac or 0.0}
+    top = max(fr, key=fr.get)
+    return bound, (top if fr[top] >= 0.5 else "latency/issue")
+
+
 def cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -204,6 +219,8 @@ def bench_resnet18(args):
     if comm is not None:
         comm.dist.barrier()
     el = time.perf_counter() - t0
+    if m.rowconv_error() != 0:  # a fused row-kernel grid barrier timed out: no number from it
+        raise RuntimeError("a fused row-kernel grid barrier timed out in the timed region: results invalid")
     if comm is not None:  # the slowest rank's time
         t = torch.tensor([el], dtype=torch.float64, device="cuda")
         comm.dist.all_reduce(t, op=comm.dist.ReduceOp.MAX)
@@ -262,7 +279,8 @@ def bench_resnet18(args):
             traffic = ent.get("hbm_bytes_per_launch")
     # the HBM roof from the PMC bytes where they were counted, else the algorithmic x + w + y
     hbm_frac = (traffic or alg_bytes) / (k_us * 1e-6) / (PEAK_HBM_GBS * 1e9)
-    roof = {"kernel": kname, "bound": "hbm" if hbm_frac > mfma_frac else "mfma", "hbm_frac": round(hbm_frac, 4),
+    bound, limiter = roof_labels(k_ops, alg_bytes, mfma_frac, hbm_frac)
+    roof = {"kernel": kname, "bound": bound, "limiter": limiter, "hbm_frac": round(hbm_frac, 4),
             "hbm_bytes_basis": "pmc traffic" if traffic else "algorithmic", "achieved": round(k_ops / k_us / 1e6, 2), "peak": round(PEAK_INT8_TOPS, 1),
             "unit": "TFLOP/s", "frac": round(mfma_frac, 4), "traffic": traffic,
             "avg_launch_us": round(k_us, 2), "timing": "HIP events around 20 back-to-back launches on one stream",
@@ -521,15 +539,15 @@ def main():
         except Exception:
             traffic = None
 
-    # which roof bounds the probed launch: the larger of its MFMA fraction and its HBM fraction
-    # (PMC traffic when counted, else the algorithmic bytes: x + dy / w + the int8 output)
-    # (forward: x + w + y; weight gradient: x + dy + dw -- the same three sizes)
+    # the probed launch's HBM fraction (PMC traffic when counted, else the algorithmic bytes: x + dy /
+    # w + the int8 output -- forward: x + w + y; weight gradient: x + dy + dw, the same three sizes);
+    # its roof by arithmetic intensity and what limits it (roof_labels)
     alg_bytes = args.batch * (pl["h"] * pl["w"] * pl["c_in"] + pl["oh"] * pl["ow"] * pl["c_out"]) + \
         pl["c_out"] * pl["c_in"] * pl["kh"] * pl["kw"]
     hbm_bytes = traffic if traffic else alg_bytes
     mfma_frac = achieved / PEAK_INT8_TOPS if achieved else None
     hbm_frac = hbm_bytes / k_avg_s / (PEAK_HBM_GBS * 1e9) if probe_n else None
-    bound = "hbm" if (hbm_frac is not None and mfma_frac is not None and hbm_frac > mfma_frac) else "mfma"
+    bound, limiter = roof_labels(k_ops, alg_bytes, mfma_frac, hbm_frac)
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_sample > 0 and args.arch in ("vgg11", "lenet", "vgg16"):
@@ -588,6 +606,7 @@ def main():
         "roofline": {
             "kernel": f"{args.arch.upper()} conv{probe_layer + 1} {phase_name} launch ({kname}; layer index {probe_layer})",
             "bound": bound,
+            "limiter": limiter,
             "hbm_frac": round(hbm_frac, 4) if hbm_frac is not None else None,
             "hbm_bytes_basis": "pmc traffic" if traffic else "algorithmic",
             "achieved": round(achieved, 2) if achieved else None,

@@ -396,14 +396,14 @@ int niti_im2col(const niti_geom* g, const int8_t* x, int kp, int8_t* xcol, void*
     if (!g || !x || !xcol) return NITI_INVALID_VALUE;
     niti::ConvGeom r;
     if (!to_geom(g, &r)) return NITI_COMPUTE_SIZE_ERROR;
-    if (r.cip > 16 || r.c_in > 4 || kp % 16 != 0 || kp < r.kh * r.kw * r.c_in) return NITI_NOT_SUPPORT;
+    if (r.cip > 16 || r.c_in > 4 || kp % 16 != 0 || kp > 4096 || kp < r.kh * r.kw * r.c_in) return NITI_NOT_SUPPORT;
     return code(niti::im2col_small(r, x, kp, xcol, S(stream)));
 }
 int niti_im2col_nchw(const niti_geom* g, const int8_t* x_nchw, int kp, int8_t* xcol, void* stream) {
     if (!g || !x_nchw || !xcol) return NITI_INVALID_VALUE;
     niti::ConvGeom r;
     if (!to_geom(g, &r)) return NITI_COMPUTE_SIZE_ERROR;
-    if (r.c_in > 4 || kp % 16 != 0 || kp < r.kh * r.kw * r.c_in) return NITI_NOT_SUPPORT;
+    if (r.c_in > 4 || kp % 16 != 0 || kp > 4096 || kp < r.kh * r.kw * r.c_in) return NITI_NOT_SUPPORT;
     return code(niti::im2col_small(r, x_nchw, kp, xcol, S(stream), true));
 }
 

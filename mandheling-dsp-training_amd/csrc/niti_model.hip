@@ -1959,25 +1959,35 @@ int niti_model_attach_comm(niti_model_t m, const char id[NITI_UNIQUE_ID_BYTES], 
     if (!m || !id || world < 1 || rank < 0 || rank >= world) return NITI_INVALID_VALUE;
     ncclUniqueId u;
     memcpy(&u, id, sizeof(u));
+    // the split-agreement flag and stream first: a local allocation failure then returns before any
+    // collective call, instead of leaving the peers blocked in one this rank never enters
+    int32_t* flag = nullptr;
+    hipStream_t ast = nullptr;
+    if (hipMalloc(&flag, sizeof(int32_t)) != hipSuccess || hipStreamCreate(&ast) != hipSuccess) {
+        if (flag) (void)hipFree(flag);
+        return NITI_OUT_OF_MEMORY;
+    }
     auto c = std::make_unique<niti::RcclCollective>();
-    if (ncclCommInitRank(&c->comm, world, u, rank) != ncclSuccess) return NITI_NO_EXECUTION;
+    if (ncclCommInitRank(&c->comm, world, u, rank) != ncclSuccess) {
+        (void)hipFree(flag);
+        (void)hipStreamDestroy(ast);
+        return NITI_NO_EXECUTION;
+    }
     c->world = world;
     // the gradient communicator: split off the first (collective over the ranks), its own
     // resources, so its SUMs and the ranges' MAXes are not serialised against each other
     auto cg = std::make_unique<niti::RcclCollective>();
     const bool split_ok = ncclCommSplit(c->comm, 0, rank, &cg->comm, nullptr) == ncclSuccess;
     // every rank must pick the same mode (the SUMs run on different communicators and streams in
-    // the two modes): agree on the split's success with a MIN over the range communicator
-    int32_t* flag = nullptr;
+    // the two modes): agree on the split's success with a MIN over the range communicator, which
+    // every rank enters whatever its own split did
     int32_t ok = split_ok ? 1 : 0;
-    hipStream_t ast = nullptr;
-    bool agreed = hipMalloc(&flag, sizeof(int32_t)) == hipSuccess && hipStreamCreate(&ast) == hipSuccess &&
-                  hipMemcpyAsync(flag, &ok, sizeof(ok), hipMemcpyHostToDevice, ast) == hipSuccess &&
-                  ncclAllReduce(flag, flag, 1, ncclInt32, ncclMin, c->comm, ast) == ncclSuccess &&
-                  hipMemcpyAsync(&ok, flag, sizeof(ok), hipMemcpyDeviceToHost, ast) == hipSuccess &&
-                  hipStreamSynchronize(ast) == hipSuccess;
-    if (flag) (void)hipFree(flag);
-    if (ast) (void)hipStreamDestroy(ast);
+    const bool agreed = hipMemcpyAsync(flag, &ok, sizeof(ok), hipMemcpyHostToDevice, ast) == hipSuccess &&
+                        ncclAllReduce(flag, flag, 1, ncclInt32, ncclMin, c->comm, ast) == ncclSuccess &&
+                        hipMemcpyAsync(&ok, flag, sizeof(ok), hipMemcpyDeviceToHost, ast) == hipSuccess &&
+                        hipStreamSynchronize(ast) == hipSuccess;
+    (void)hipFree(flag);
+    (void)hipStreamDestroy(ast);
     if (!agreed) {
         if (split_ok) (void)ncclCommDestroy(cg->comm);
         cg->comm = nullptr;

@@ -204,7 +204,8 @@ __global__ void __launch_bounds__(256) im2col_small_kernel(const int8_t* __restr
 }
 
 hipError_t im2col_small(const ConvGeom& g, const int8_t* x, int kp, int8_t* xcol, hipStream_t st, bool nchw) {
-    if (kp % 16 != 0 || kp < g.kh * g.kw * g.c_in || g.c_in > 4 || g.cip > 16) return hipErrorInvalidValue;
+    // kp <= 4096: a thread keeps one 16-byte column chunk, so 256 threads cover at most 256 chunks
+    if (kp % 16 != 0 || kp > 4096 || kp < g.kh * g.kw * g.c_in || g.c_in > 4 || g.cip > 16) return hipErrorInvalidValue;
     const int cols = (g.ow - 1) * g.sw + (g.kw - 1) * g.dw + 1;
     if ((int64_t)g.kh * cols * g.c_in > IM2COL_LDS) return hipErrorInvalidValue;
     const int64_t rows = (int64_t)g.n * g.oh;

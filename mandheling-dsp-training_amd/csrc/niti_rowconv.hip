@@ -110,7 +110,6 @@ __device__ __forceinline__ unsigned long long* bar_shard(uint32_t* base, int s) 
 // with it while its grid barrier completes and redoes the epilogue only if the barrier's bw
 // differs: per layer the bit width is stable from step to step, so the barrier's release latency
 // overlaps the epilogue instead of preceding it.  The results are the rule's whatever the guess.
-__device__ __forceinline__ uint32_t* bar_hint(uint32_t* state, bool dg) { return state + (16 + (dg ? 1 : 0)) * BAR_LINE; }
 
 
 // Called by one whole wave of each workgroup (lane 0's bw): the arrival, then -- after whatever
@@ -182,7 +181,7 @@ struct RowConvArgs {
     uint32_t* err;
     uint32_t spin_limit;         // FUSED: polls before the barrier gives up and sets *err
     uint32_t expect_extra;       // diagnostics (niti_diag_rowconv_barrier): arrivals that never come
-    int spec;                    // FUSED: 1 speculative epilogue (bar_hint), 0 off, 2 diagnostics:
+    int spec;                    // FUSED: 1 speculative epilogue (hint slot), 0 off, 2 diagnostics:
                                  // guess one bit wide of the hint (every launch redoes its epilogue)
     unsigned long long* stamps;  // diagnostics (niti_diag_rowconv_stamps): 8 per wave, or null
     const int8_t* relu_mask;     // input gradient: RowConvOut's relu / pool gradients
@@ -1303,7 +1302,7 @@ __global__ void __launch_bounds__(256, (RC_EXP & 16) ? 2 : 1) rowconv_fwd_kernel
     RC_STAMP(0);
     if constexpr (MODE == RC_FUSED) {
         const RowUnit<W, R> U(a, a.wmajor ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x, wid, c, KS > 0);
-        uint32_t* hint_p = bar_hint(a.bar, DG);
+        uint32_t* hint_p = a.hint;  // the host's slot choice (DG or the caller's dgrad_slot)
         // the guess: the previous launch's bit width (written by block 0 after its barrier; the launch
         // boundary orders it before this read)
         int guess = -1;
@@ -1898,7 +1897,9 @@ hipError_t rowconv_fwd(const ConvGeom& g, const int8_t* x_c32, const int8_t* wf,
     a.p16_pixels = (int64_t)g.n * g.h * g.w * (o.pool_dx != nullptr ? 4 : 1);
     a.acc_store = mode == RC_FUSED ? nullptr : o.acc_store;
     a.spec2 = spec2;
-    a.hint = spec ? bar + (16 + (dg || o.dgrad_slot ? 1 : 0)) * BAR_LINE : nullptr;
+    // the hint slot (the speculative pair's, and the fused mode's speculative epilogue): forward or
+    // input gradient, by the operands or the caller's dgrad_slot, so the two directions never share it
+    a.hint = (spec || mode == RC_FUSED) && bar != nullptr ? bar + (16 + (dg || o.dgrad_slot ? 1 : 0)) * BAR_LINE : nullptr;
     if (o.p16 != nullptr && (!dg || !rowconv_p16_ok(g, o.pool_dx != nullptr))) return hipErrorInvalidValue;
     if (o.pool_out != nullptr && (R % 2 != 0 || g.h % 2 != 0)) return hipErrorInvalidValue;
     if (mode == RC_FUSED) {
@@ -2057,7 +2058,9 @@ hipError_t rowconv_fc(int n, int K, int rows, const int8_t* x, int xld, const in
     a.p16_pixels = (int64_t)n * (o.pool_dx != nullptr ? 4 : 1);
     const bool dg = o.relu_mask != nullptr || o.pool_dx != nullptr || o.p16 != nullptr;
     a.spec2 = spec2;
-    a.hint = spec ? bar + (16 + (dg || o.dgrad_slot ? 1 : 0)) * BAR_LINE : nullptr;
+    // the hint slot (the speculative pair's, and the fused mode's speculative epilogue): forward or
+    // input gradient, by the operands or the caller's dgrad_slot, so the two directions never share it
+    a.hint = (spec || mode == RC_FUSED) && bar != nullptr ? bar + (16 + (dg || o.dgrad_slot ? 1 : 0)) * BAR_LINE : nullptr;
     if (o.p16 != nullptr && (o.pool_dx == nullptr || a.p16_pixels % 16 != 0)) return hipErrorInvalidValue;
     if (o.next != nullptr && a.cop % 32 != 0) return hipErrorInvalidValue;
     if (mode == RC_FUSED) {

@@ -279,14 +279,17 @@ def conv_fwd_rows(g: L.Geom, xc32, wf, amax, mode=0, state: RowConvState | None 
     st_ptr = err_ptr = None
     epoch = 0
     if mode == 0:
-        state.epoch += 1
-        epoch, st_ptr, err_ptr = state.epoch, _ptr(state.state), _ptr(state.err)
+        # the launch's epoch; state.epoch advances only when the launch happened (a NOT_SUPPORT
+        # return launches nothing, and a skipped epoch would reuse the previous launch's barrier words)
+        epoch, st_ptr, err_ptr = state.epoch + 1, _ptr(state.state), _ptr(state.err)
     elif mode >= 3:
         st_ptr = _ptr(state.state)
     check(L.lib().niti_conv_fwd_rows(C.byref(g), _ptr(xc32), _ptr(wf), _ptr(exp_in), _ptr(wscale), _ptr(exp_out),
                                      1 if relu else 0, _ptr(out), _ptr(pout), _ptr(nxt),
                                      mode | (ROWS_X_NHWC16 if x_nhwc else 0), _ptr(amax), st_ptr,
                                      epoch, err_ptr, _stream(stream)), "conv_fwd_rows")
+    if mode == 0:
+        state.epoch = epoch
     return out, pout, nxt
 
 
@@ -308,8 +311,9 @@ def conv_dgrad_rows(g: L.Geom, dyc32, wft, amax, mode=0, state: RowConvState | N
     st_ptr = err_ptr = None
     epoch = 0
     if mode == 0:
-        state.epoch += 1
-        epoch, st_ptr, err_ptr = state.epoch, _ptr(state.state), _ptr(state.err)
+        # the launch's epoch; state.epoch advances only when the launch happened (a NOT_SUPPORT
+        # return launches nothing, and a skipped epoch would reuse the previous launch's barrier words)
+        epoch, st_ptr, err_ptr = state.epoch + 1, _ptr(state.state), _ptr(state.err)
     elif mode >= 3:
         st_ptr = _ptr(state.state)
     check(L.lib().niti_conv_dgrad_rows(C.byref(g), _ptr(dyc32), _ptr(wft), _ptr(relu_mask), _ptr(pool_x),
@@ -317,6 +321,8 @@ def conv_dgrad_rows(g: L.Geom, dyc32, wft, amax, mode=0, state: RowConvState | N
                                        _ptr(exp_in), _ptr(wscale), _ptr(exp_out),
                                        mode | (ROWS_X_NHWC16 if x_nhwc else 0),
                                        _ptr(amax), st_ptr, epoch, err_ptr, _stream(stream)), "conv_dgrad_rows")
+    if mode == 0:
+        state.epoch = epoch
     return dx, nxt, p16
 
 

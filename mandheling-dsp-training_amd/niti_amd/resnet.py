@@ -184,6 +184,12 @@ class ResNet18:
         self._global_range(amax)
         return f(g, xc, wf, amax, mode=2, **kw)[0]
 
+    def rowconv_error(self) -> int:
+        """1 if a fused row-kernel launch's grid barrier timed out (its results are invalid): the OR
+        of every row layer's error word."""
+        errs = [s.err for s in self.rstate if s is not None]
+        return int(torch.stack(errs).max().item()) if errs else 0
+
     def get_weight(self, i) -> np.ndarray:
         w = ops.ohwi16_to_oihw(self.w16[i], self._ci(i)).cpu().numpy()
         return self._stem_oihw(w[:, :, 0, 0]) if i == 0 else w
