@@ -158,176 +158,29 @@ def cpu_baseline(arch, sample, threads_list, in_hw=0):
     return legs
 
 
-def bench_resnet18(args):
-    """BASELINE config 5's network: ResNet-18 at 224x224, 1000 classes.  A step: uint8 images
-    through the device input quantiser, then the whole NITI_SGD step on the HIP ops
-    (niti_amd.resnet).  Under torchrun (WORLD_SIZE > 1) every rank steps its own batch and the
-    exact data-parallel protocol runs over RCCL (niti_amd.dp.TorchComm, backend "nccl")."""
+def cpu_baseline_resnet18(sample, threads_list, hw):
+    """The oracle's exact C restatement of the whole ResNet-18 step (oracle/niti_resnet_ref.py:
+    input quantiser, convs with the shift rule, relu / max pool, the residual rules, sum pool, loss
+    gradient, weight and input gradients, NITI_SGD) on `sample` images, once per thread count.
+    Test infrastructure, never the product."""
     import numpy as np
-    import torch
-    from niti_amd import ops
-    from niti_amd.resnet import ResNet18
-    world, rank, local = resolve_world(args)
-    torch.cuda.set_device(local)
-    comm = None
-    if world > 1:
-        import torch.distributed as dist
-        from niti_amd.dp import TorchComm
-        dist.init_process_group("nccl", device_id=torch.device("cuda", torch.cuda.current_device()))
-        comm = TorchComm()
-    hw = args.in_hw or 224
-    batch, scaling = per_gpu_batch(args, world, 128)
-    m = ResNet18(batch, hw, 1000, comm=comm)
-    layers = [dict(c_out=l["co"], c_in=l["ci"], kh=l["k"], kw=l["k"]) for l in m.convs]
-    for i, (w, s) in enumerate(synth_weights(layers, seed=17)):
-        m.set_weight(i, w, s)
-    rng = np.random.default_rng(100 + rank)
-    img = torch.from_numpy(rng.integers(0, 256, (batch, 3, hw, hw)).astype(np.uint8)).cuda()
-    labels = torch.from_numpy(rng.integers(0, 1000, batch).astype(np.int32)).cuda()
-
-    def step():
-        m.train_step_images(img, labels)
-
-    tune_s = 0.0
-    if not args.no_autotune:  # per-shape GEMM plans of the GEMM-path convs, timed on this batch
-        t_tune = time.perf_counter()
-        m.autotune()
-        tune_s = time.perf_counter() - t_tune
-    for _ in range(max(args.warmup, 1)):
-        step()
-    torch.cuda.synchronize()
-    run = step
-    graph = None
-    if args.graph and comm is None:  # the whole step (~450 launches) captured once, replayed as one graph
-        try:
-            graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph):
-                step()
-            run = graph.replay
-            run()
-            torch.cuda.synchronize()
-        except RuntimeError as e:  # not capturable here: direct launches
-            print(f"graph capture failed ({e}); direct launches", file=sys.stderr)
-            graph, run = None, step
-    if comm is not None:
-        comm.dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        run()
-    torch.cuda.synchronize()
-    if comm is not None:
-        comm.dist.barrier()
-    el = time.perf_counter() - t0
-    if m.rowconv_error() != 0:  # a fused row-kernel grid barrier timed out: no number from it
-        raise RuntimeError("a fused row-kernel grid barrier timed out in the timed region: results invalid")
-    if comm is not None:  # the slowest rank's time
-        t = torch.tensor([el], dtype=torch.float64, device="cuda")
-        comm.dist.all_reduce(t, op=comm.dist.ReduceOp.MAX)
-        el = float(t.item())
-    tops = 2 * m.step_macs() * world * args.steps / el / 1e12
-    if rank != 0:
-        comm.dist.destroy_process_group()
-        return
-    # roofline: the first 56x56 stage conv's forward (layer1.0.a, 64 -> 64, 3x3) re-run alone after the
-    # timed region, HIP events on the launch stream around 20 back-to-back launches: the row-segment
-    # kernel's requantise launch (the GEMM recomputed with the range given, relu, int8 out) as the step
-    # runs it, or the implicit GEMM where the layer is not on the row kernel
-    c = m.convs[1]
-    g = ops.geom(batch, c["ci"], c["h"], c["h"], c["co"], c["k"], stride=c["stride"], pad=c["pad"])
-    xr = ops.nchw_to_nhwc16(torch.from_numpy(rng.integers(-127, 128, (batch, c["ci"], c["h"], c["h"])).astype(np.int8)).cuda())
-    wr = ops.oihw_to_ohwi16(torch.from_numpy(rng.integers(-127, 128, (c["co"], c["ci"], c["k"], c["k"])).astype(np.int8)).cuda())
-    amax = ops.new_range()
-    rows = m.use_rows and m.rows[1]
-    probe_plan = None
-    if rows:
-        # the step's form: the speculative pair's launch A (the pair's B exits at once while the bit
-        # width holds); one pair first so A has the layer's hint
-        xn = ops.rows_nhwc_ok(g, preferred=True)
-        xc = xr if xn else ops.nhwc16_to_c32(xr, c["ci"])
-        wf = ops.weights_to_wf(wr, c["ci"])
-        rst = ops.RowConvState()
-        outs = ops.conv_fwd_rows(g, xc, wf, amax, mode=3, state=rst, relu=True, x_nhwc=xn)
-        ops.conv_fwd_rows(g, xc, wf, amax, mode=4, state=rst, relu=True, x_nhwc=xn, outs=outs)
-        launch = lambda: ops.conv_fwd_rows(g, xc, wf, amax, mode=3, state=rst, relu=True,  # noqa: E731
-                                           x_nhwc=xn, outs=outs)
-        kname = (f"ResNet-18 {c['name']} forward, row-segment register-fed kernel, speculative launch A (GEMM, "
-                 "requantised with the layer's previous bit width, relu, int8 out, range published; the pair's "
-                 "launch B exits at once when the bit width holds; re-run alone after the timed region)")
-        probe_plan = [0, 0, 0, 3]
-    else:
-        launch = lambda: ops.conv_fwd_acc(g, xr, wr, amax)  # noqa: E731
-        kname = (f"ResNet-18 {c['name']} forward GEMM (gemm_kernel, implicit im2col, int32 accumulate + range; "
-                 "re-run alone after the timed region)")
-    launch()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    reps = 20
-    e0.record()
-    for _ in range(reps):
-        launch()
-    e1.record()
-    torch.cuda.synchronize()
-    k_us = e0.elapsed_time(e1) * 1e3 / reps
-    k_ops = 2 * batch * g.oh * g.ow * c["co"] * c["ci"] * c["k"] * c["k"]
-    alg_bytes = batch * (c["h"] * c["h"] * c["ci"] + g.oh * g.ow * c["co"]) + c["co"] * c["ci"] * c["k"] * c["k"]
-    mfma_frac = k_ops / k_us / 1e6 / PEAK_INT8_TOPS
-    traffic = None  # PMC bytes of this probe (tools/traffic.py, key resnet18_b{batch}_L1_p0, plan 0,0,0,3)
-    tfile = os.path.join(ROOT, "profiles", "traffic.json")
-    if probe_plan is not None and os.path.exists(tfile):
-        ent = json.load(open(tfile)).get(f"resnet18_b{batch}_L1_p0", {})
-        if list(ent.get("plan", [])) == probe_plan:
-            traffic = ent.get("hbm_bytes_per_launch")
-    # the HBM roof from the PMC bytes where they were counted, else the algorithmic x + w + y
-    hbm_frac = (traffic or alg_bytes) / (k_us * 1e-6) / (PEAK_HBM_GBS * 1e9)
-    bound, limiter = roof_labels(k_ops, alg_bytes, mfma_frac, hbm_frac)
-    roof = {"kernel": kname, "bound": bound, "limiter": limiter, "hbm_frac": round(hbm_frac, 4),
-            "hbm_bytes_basis": "pmc traffic" if traffic else "algorithmic", "achieved": round(k_ops / k_us / 1e6, 2), "peak": round(PEAK_INT8_TOPS, 1),
-            "unit": "TFLOP/s", "frac": round(mfma_frac, 4), "traffic": traffic,
-            "avg_launch_us": round(k_us, 2), "timing": "HIP events around 20 back-to-back launches on one stream",
-            "ops_per_launch": k_ops}
-    cpu = None
-    if world == 1 and args.cpu_sample != 0:
-        # the oracle's ResNet-18 restatement (oracle/niti_resnet_ref.py) of the whole step
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import niti_oracle as O
-        import niti_resnet_ref as RR
-        sample = args.cpu_sample if args.cpu_sample > 0 else 1
-        convs = RR.resnet18_convs(hw, 1000)
-        W, S = RR.init_weights(convs, seed=17)
-        crng = np.random.default_rng(1)
-        cimg = crng.integers(0, 256, (sample, 3, hw, hw)).astype(np.uint8)
-        clab = crng.integers(0, 1000, sample).astype(np.int32)
-        all_cores = len(os.sched_getaffinity(0))
-        if os.environ.get("OMP_NUM_THREADS", "").isdigit():
-            all_cores = max(1, min(all_cores, int(os.environ["OMP_NUM_THREADS"])))
-        legs = []
-        for t in sorted({args.cpu_threads, all_cores}):
-            O.set_threads(t)
-            t0 = time.perf_counter()
-            x, a = O.quantize_images(cimg)
-            RR.train_step(convs, W, S, x, a, clab, classes=1000)
-            secs = time.perf_counter() - t0
-            legs.append({"threads": t, "value": round(sample / secs, 3), "seconds": round(secs, 2)})
-        best = max(legs, key=lambda l: l["value"])
-        cpu = {"value": best["value"], "unit": "images/s", "cores": best["threads"], "kind": "port",
-               "sample": f"{sample} image(s) at {hw}x{hw} through the whole ResNet-18 step in the oracle's exact C "
-                         f"restatement (oracle/niti_resnet_ref.py; conv threads split the batch/channels)",
-               "legs": legs, "cpu_model": cpu_model()}
-    print(json.dumps({
-        "metric": "training images/sec + int8 MFMA TOPS, ResNet-18 ImageNet-224 (BASELINE config 5 network)",
-        "value": round(batch * world * args.steps / el, 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True,
-        "scaling": scaling, "vs_baseline": None, "dtype": "int8",
-        "data": "synthetic (random uint8 images through the on-device input quantiser; random labels; seeded weights)",
-        "config": {"workload": f"ResNet-18 NITI int8 training step, 3x{hw}x{hw}, 1000 classes",
-                   "global_batch": batch * world, "per_gpu_batch": batch,
-                   "parallelism": parallelism_label(world, "RCCL all-reduce MAX ranges + SUM int32 grads, niti_amd.dp"),
-                   "driver": "host-driven op sequence (niti_amd.resnet)",
-                   "launch": "hipGraph replay of the captured step" if graph is not None else "direct launches"},
-        "int8_mfma_tops": round(tops, 2), "int8_mfma_frac_of_peak": round(tops / PEAK_INT8_TOPS, 4),
-        "roofline": roof, "autotune_s": round(tune_s, 2), "cpu_baseline": cpu}))
-    if comm is not None:
-        comm.dist.destroy_process_group()
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import niti_oracle as O
+    import niti_resnet_ref as RR
+    convs = RR.resnet18_convs(hw, 1000)
+    W, S = RR.init_weights(convs, seed=17)
+    crng = np.random.default_rng(1)
+    cimg = crng.integers(0, 256, (sample, 3, hw, hw)).astype(np.uint8)
+    clab = crng.integers(0, 1000, sample).astype(np.int32)
+    legs = []
+    for t in threads_list:
+        O.set_threads(t)
+        t0 = time.perf_counter()
+        x, a = O.quantize_images(cimg)
+        RR.train_step(convs, W, S, x, a, clab, classes=1000)
+        secs = time.perf_counter() - t0
+        legs.append({"threads": t, "value": round(sample / secs, 3), "seconds": round(secs, 2)})
+    return legs
 
 
 def main():
@@ -351,8 +204,8 @@ def main():
                                                               "instead of uint8 images through the device quantiser")
     ap.add_argument("--probe-layer", type=int, default=-1, help="layer whose GEMM is timed for the roofline (default: "
                                                                 "3, VGG-11 / VGG-16 conv4; LeNet: 1, its 5x5 conv2)")
-    ap.add_argument("--probe-phase", type=int, default=2, help="0 fwd, 1 input grad, 2 weight grad")
-    ap.add_argument("--graph", action="store_true", help="replay the step as a hipGraph (slower on ROCm 7.2)")
+    ap.add_argument("--probe-phase", type=int, default=-1, help="0 fwd, 1 input grad, 2 weight grad (-1: 2, ResNet-18 0)")
+    ap.add_argument("--graph", action="store_true", help="replay the step as a hipGraph")
     ap.add_argument("--no-autotune", action="store_true", help="keep the fixed default GEMM plans")
     ap.add_argument("--overlap", action="store_true",
                     help="weight gradients on a second stream beside the input-gradient chain (measured within 1 %% "
@@ -378,9 +231,6 @@ def main():
         return spawn_ranks(args.gpus, sys.argv[1:])
     if args.spawn_check:
         return spawn_check(args)
-    if args.arch == "resnet18":
-        return bench_resnet18(args)
-
     import numpy as np
     import torch
 
@@ -395,10 +245,14 @@ def main():
     niti_amd._lib.lib().niti_diag_rowconv_speculate(args.rc_spec)
     from niti_amd.model import NitiModel
 
-    arch = {"vgg11": niti_amd.ARCH_VGG11, "lenet": niti_amd.ARCH_LENET, "vgg16": niti_amd.ARCH_VGG16}[args.arch]
-    args.batch, scaling = per_gpu_batch(args, world, 64 if arch == niti_amd.ARCH_VGG16 else 256)
+    arch = {"vgg11": niti_amd.ARCH_VGG11, "lenet": niti_amd.ARCH_LENET, "vgg16": niti_amd.ARCH_VGG16,
+            "resnet18": niti_amd.ARCH_RESNET18}[args.arch]
+    imagenet = arch in (niti_amd.ARCH_VGG16, niti_amd.ARCH_RESNET18)
+    args.batch, scaling = per_gpu_batch(args, world, {niti_amd.ARCH_VGG16: 64, niti_amd.ARCH_RESNET18: 128}.get(arch, 256))
     if args.cpu_sample < 0:
-        args.cpu_sample = {niti_amd.ARCH_VGG16: 2, niti_amd.ARCH_LENET: 512}.get(arch, 128)
+        args.cpu_sample = {niti_amd.ARCH_VGG16: 2, niti_amd.ARCH_LENET: 512, niti_amd.ARCH_RESNET18: 1}.get(arch, 128)
+    if args.probe_phase < 0:  # ResNet-18: layer1.0.a's forward (a row-segment conv); the others: conv4's wgrad
+        args.probe_phase = 0 if arch == niti_amd.ARCH_RESNET18 else 2
     model = NitiModel(arch, args.batch, args.in_hw)
     model.set_graph(args.graph)
     # (data parallel keeps the default too: a third stream beside the step stream and the gradient
@@ -425,7 +279,7 @@ def main():
         x = torch.from_numpy(rng.integers(-127, 128, shape).astype(np.int8)).cuda()
     else:  # uint8 images: the on-device input quantiser is part of every timed step
         x = torch.from_numpy(rng.integers(0, 256, shape).astype(np.uint8)).cuda()
-    labels = torch.from_numpy(rng.integers(0, 1000 if arch == niti_amd.ARCH_VGG16 else 10,
+    labels = torch.from_numpy(rng.integers(0, 1000 if imagenet else 10,
                                            args.batch).astype(np.int32)).cuda()
 
     def step():
@@ -454,7 +308,7 @@ def main():
             sp = args.wgrad_p16 or p[2]
             model.set_plan(i, 2, (16, 16, sp, 2 if sp > 1 else 0))
     if args.probe_layer < 0:
-        args.probe_layer = 1 if arch == niti_amd.ARCH_LENET else 3
+        args.probe_layer = 1 if arch in (niti_amd.ARCH_LENET, niti_amd.ARCH_RESNET18) else 3
     probe_layer = args.probe_layer if args.probe_layer < len(model.layers) else len(model.layers) - 1
     if args.probe_plan:
         model.set_plan(probe_layer, args.probe_phase, [int(v) for v in args.probe_plan.split(",")])
@@ -550,6 +404,17 @@ def main():
     bound, limiter = roof_labels(k_ops, alg_bytes, mfma_frac, hbm_frac)
 
     cpu = None
+    if rank == 0 and world == 1 and args.cpu_sample > 0 and args.arch == "resnet18":
+        all_cores = len(os.sched_getaffinity(0))
+        if os.environ.get("OMP_NUM_THREADS", "").isdigit():
+            all_cores = max(1, min(all_cores, int(os.environ["OMP_NUM_THREADS"])))
+        hw = args.in_hw or 224
+        legs = cpu_baseline_resnet18(args.cpu_sample, sorted({args.cpu_threads, all_cores}), hw)
+        best = max(legs, key=lambda l: l["value"])
+        cpu = {"value": best["value"], "unit": "images/s", "cores": best["threads"], "kind": "port",
+               "sample": f"{args.cpu_sample} image(s) at {hw}x{hw} through the whole ResNet-18 step in the oracle's exact "
+                         f"C restatement (oracle/niti_resnet_ref.py; conv threads split the batch/channels)",
+               "legs": legs, "cpu_model": cpu_model()}
     if rank == 0 and world == 1 and args.cpu_sample > 0 and args.arch in ("vgg11", "lenet", "vgg16"):
         # every core this process may use: the affinity set, capped by the box's CPU share
         # (OMP_NUM_THREADS, 16 per GPU on the pool) -- the thread count is reported as `cores`
@@ -575,6 +440,10 @@ def main():
                  f"for all 9 taps, {pplan[2]} K splits")
     elif args.probe_phase == 2:
         kname = f"gemm_kernel {pplan[0]}x{pplan[1]}, K-major over pixels, {pplan[2]} K splits"
+    elif arch == niti_amd.ARCH_RESNET18 and model.layers[probe_layer]["kh"] == 3 and model.layers[probe_layer]["stride"] == 1:
+        kname = ("rowconv_fwd_kernel, row-segment register-fed conv with the rescale fused: the speculative pair "
+                 "(launch A multiplies and requantises with the layer's previous bit width, launch B exits at once "
+                 "while it holds), both launches in the time")
     else:
         kname = f"gemm_kernel {pplan[0]}x{pplan[1]}, implicit im2col"
     line = {
@@ -593,10 +462,13 @@ def main():
         "data": ("synthetic (random int8 x, fixed exponent" if args.int8_input else
                  "synthetic (random uint8 images through the on-device input quantiser") +
                 "; random labels; seeded niti_normal_int8 weights)",
-        "config": {"workload": f"{args.arch.upper()} NITI int8 training step (fwd+relu+pool, loss grad, "
-                               f"weight grad, input grad, SGD), {l0['c_in']}x{l0['h']}x{l0['w']}"
-                               + (", 4096-4096-1000 head" if arch == niti_amd.ARCH_VGG16 else "")
-                               if arch != niti_amd.ARCH_LENET else "LeNet NITI int8 training step, 1x28x28",
+        "config": {"workload": (f"{args.arch.upper()} NITI int8 training step (fwd+relu+pool, loss grad, "
+                                f"weight grad, input grad, SGD), {l0['c_in']}x{l0['h']}x{l0['w']}"
+                                + (", 4096-4096-1000 head" if arch == niti_amd.ARCH_VGG16 else "")
+                                if arch not in (niti_amd.ARCH_LENET, niti_amd.ARCH_RESNET18) else
+                                "LeNet NITI int8 training step, 1x28x28" if arch == niti_amd.ARCH_LENET else
+                                f"ResNet-18 NITI int8 training step (C++ step driver: convs, residual sums, sum pool, "
+                                f"1000-class loss grad, weight + input grads, SGD), 3x{l0['h']}x{l0['w']}"),
                    "global_batch": args.batch * world, "per_gpu_batch": args.batch,
                    "parallelism": parallelism_label(world, "RCCL all-reduce MAX ranges + SUM int32 grads"),
                    "streams": "weight gradients beside the input-gradient chain on a second stream" if overlap

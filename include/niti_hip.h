@@ -414,8 +414,11 @@ int niti_image_quantize_nhwc16(const uint8_t* images_nchw, int n, int c, int hw,
 /* ============================ 3. device-resident training step ========================= */
 /* LeNet on MNIST 1x28x28 (cfg 1/2); VGG-11 on CIFAR 3x32x32 (cfg 3); VGG-16 on ImageNet 3x224x224
  * with the 4096-4096-1000 head (cfg 4; niti_model_create2 takes another input size, a multiple
- * of 32, e.g. 32 for the oracle-checked tests) */
-enum niti_arch { NITI_ARCH_LENET = 1, NITI_ARCH_VGG11 = 2, NITI_ARCH_VGG16 = 3 };
+ * of 32, e.g. 32 for the oracle-checked tests); ResNet-18 on ImageNet 3x224x224 (cfg 5: 21
+ * parameter layers in the order conv1, per basic block conv a / conv b / [1x1 projection], fc; the
+ * residual and global-pool rules are this library's -- the reference's NITI_Eltwise_Int8 is a stub,
+ * NITI_Eltwise_Int8.cpp:20-28 -- stated in csrc/niti_resnet.hip and oracle/niti_resnet_ref.py). */
+enum niti_arch { NITI_ARCH_LENET = 1, NITI_ARCH_VGG11 = 2, NITI_ARCH_VGG16 = 3, NITI_ARCH_RESNET18 = 4 };
 typedef struct niti_model* niti_model_t;
 
 /* batch = this rank's images per step.  Weights start zero; load them with
@@ -424,6 +427,9 @@ typedef struct niti_model* niti_model_t;
 int niti_model_create(int arch, int batch, niti_model_t* out);
 /* The same with the input resolution (in_hw x in_hw; 0 = the architecture's default). */
 int niti_model_create2(int arch, int batch, int in_hw, niti_model_t* out);
+/* ... and the class count of the head (0 = the architecture's: 10 LeNet / VGG-11, 1000 VGG-16 /
+ * ResNet-18; only ResNet-18 takes another, <= 2048) */
+int niti_model_create3(int arch, int batch, int in_hw, int classes, niti_model_t* out);
 void niti_model_destroy(niti_model_t m);
 int niti_model_num_layers(niti_model_t m);
 /* per layer: {c_in, c_out, kh, kw, h_in, w_in, oh, ow, pad, stride, relu, pool} */

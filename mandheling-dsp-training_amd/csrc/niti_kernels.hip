@@ -204,7 +204,36 @@ struct Epi {
     const int8_t* wscale = nullptr;
     int8_t* exp_out = nullptr;
     unsigned long long* span = nullptr;  // kernel-span probe slot (probe_span_arm)
+    // the speculative pair (plan strategy STRAT_SPEC, EPI_REQUANT only): spec 1 = launch A --
+    // requantise with the bit width in hint[0] (the layer's previous one, bw + 1; 0 none) and publish
+    // max|C| into amax; spec 2 = launch B -- every block exits at once unless the max's bit width
+    // differs from the one A used (hint[1]), and otherwise requantises with it.  Slot words as the
+    // row kernels' (niti_rowconv.hip spec_guess / spec_settle): [0] hint (written by B), [1] the guess
+    // A used (written by A), [2] launches B redid.
+    int spec = 0;
+    uint32_t* hint = nullptr;
 };
+
+// launch B of the pair: the rule's bit width of the (all-reduced) max against the guess A used;
+// block 0 writes the exponent and the next hint.  Returns true when A's output stands (every block
+// of B then exits).  Called by whole waves (read_max: one slot per lane).
+__device__ __forceinline__ bool gemm_spec_hit(const Epi& epi) {
+    const uint32_t g = read_max(epi.amax);
+    const int bw = bitwidth_of(g);
+    const int used = __builtin_amdgcn_readfirstlane(
+                         (int)__hip_atomic_load(epi.hint + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) - 1;
+    const bool hit = bw == used;
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
+        if (hit && epi.exp_out != nullptr) {  // (a miss writes it in the redone epilogue)
+            const int shift = bw - 7;
+            const int inc = shift > 1 ? shift : (shift == 1 ? 2 : 0);
+            *epi.exp_out = (int8_t)((epi.exp_in ? (int)*epi.exp_in : 0) + (epi.wscale ? (int)*epi.wscale : 0) + inc);
+        }
+        __hip_atomic_store(epi.hint, (uint32_t)bw + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (!hit) __hip_atomic_fetch_add(epi.hint + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return hit;
+}
 
 
 
@@ -226,11 +255,23 @@ __device__ __forceinline__ void gemm_epilogue(v16i (&acc)[TM][TN], int r0, int c
     const int wid = tid >> 6;
     int rq_shift = 2;
     bool rq_raw = false;
+    // launch A of the speculative pair: requantise with the hinted bit width, publish the max
+    const bool spec_a = MODE == EPI_REQUANT && epi.spec == 1;
     if (MODE == EPI_REQUANT) {
-        const int shift = bitwidth_of(read_max(epi.amax)) - 7;  // NITI_Conv_Int8.cpp:262-307
+        int bw;
+        if (spec_a) {
+            const uint32_t h = __hip_atomic_load(epi.hint, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            bw = __builtin_amdgcn_readfirstlane((int)h) - 1;  // -1: no hint yet (B redoes the launch)
+            if (bw < 0) bw = 0;
+            if (blockIdx.x == 0 && blockIdx.y == 0 && tid == 0)
+                __hip_atomic_store(epi.hint + 1, h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            bw = bitwidth_of(read_max(epi.amax));
+        }
+        const int shift = bw - 7;  // NITI_Conv_Int8.cpp:262-307
         rq_shift = shift > 1 ? shift : 2;
         rq_raw = shift <= 0;
-        if (blockIdx.x == 0 && blockIdx.y == 0 && tid == 0 && epi.exp_out != nullptr) {
+        if (!spec_a && blockIdx.x == 0 && blockIdx.y == 0 && tid == 0 && epi.exp_out != nullptr) {
             const int inc = shift > 1 ? shift : (shift == 1 ? 2 : 0);
             const int ein = epi.exp_in ? (int)*epi.exp_in : 0;
             const int ws = epi.wscale ? (int)*epi.wscale : 0;
@@ -254,7 +295,7 @@ __device__ __forceinline__ void gemm_epilogue(v16i (&acc)[TM][TN], int r0, int c
                 if (STAGE_C) ctile[(row - m0) * LDT + (col - n0)] = v;
                 if (row < M && col < N) {
                     if (!STAGE_C && (MODE == EPI_STORE || MODE == EPI_SLAB)) Cs[(int64_t)row * epi.ldc + col] = v;
-                    if (MODE == EPI_STORE || MODE == EPI_AMAX) {
+                    if (MODE == EPI_STORE || MODE == EPI_AMAX || spec_a) {
                         const uint32_t u = uabs32(v);
                         lmax = lmax > u ? lmax : u;
                     }
@@ -296,7 +337,7 @@ __device__ __forceinline__ void gemm_epilogue(v16i (&acc)[TM][TN], int r0, int c
                 *(v4i*)(Cs + (int64_t)row * epi.ldc + col) = *(const v4i*)(ctile + rl * LDT + cl);
         }
     }
-    if (MODE == EPI_STORE || MODE == EPI_AMAX) {
+    if (MODE == EPI_STORE || MODE == EPI_AMAX || spec_a) {
         lmax = wave_max(lmax);
         __syncthreads();  // LDS reads of the staged tile / the last K step are finished
         uint32_t* red = (uint32_t*)smem;
@@ -704,6 +745,9 @@ __global__ void __launch_bounds__(NW * 64) gemm_kernel(LA la, LB lb, int M, int 
     static_assert(SMEM >= BM * (BN + 16), "requant epilogue staging fits in the pipeline's LDS");
     __shared__ __attribute__((aligned(16))) int8_t smem[SMEM];
 
+    if constexpr (MODE == EPI_REQUANT) {
+        if (epi.spec == 2 && gemm_spec_hit(epi)) return;  // launch B of the pair: A's output stands
+    }
     const unsigned long long span_t0 = span_begin(epi.span);
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -1494,7 +1538,11 @@ static unsigned long long* take_span() {
 }
 
 // ------------------------------------------------------------------------------ planning
-enum Strategy { STRAT_STORE = 0, STRAT_RECOMPUTE = 1, STRAT_SLAB = 2 };
+// STRAT_SPEC: the speculative pair (forward / input gradient, no K split): launch A requantises
+// with the layer's previous bit width and publishes the max, launch B redoes the GEMM only when
+// the (all-reduced) max's bit width differs -- one GEMM pass on a hit, no int32 tensor.  Callers
+// that run the two-phase entry points take it as STRAT_RECOMPUTE (same results).
+enum Strategy { STRAT_STORE = 0, STRAT_RECOMPUTE = 1, STRAT_SLAB = 2, STRAT_SPEC = 3 };
 
 struct GemmPlan {
     int bm = 128, bn = 128, tiles = 1, splits = 1, kc_per_split = 0;
@@ -1574,6 +1622,8 @@ static GemmPlan plan_gemm(int M, int N, int k_total, int k_step, int k_bytes, bo
         p.tiles = ((M + p.bm - 1) / p.bm) * ((N + p.bn - 1) / p.bn);
         if (c.strat == STRAT_SLAB) {
             plan_slab(p, c.splits, k_total, k_step, steps, false, M, N, ws_elems);
+        } else if (c.strat == STRAT_SPEC) {
+            p.strat = recompute_ok ? STRAT_SPEC : STRAT_STORE;
         } else {
             p.strat = c.strat == STRAT_RECOMPUTE && recompute_ok ? STRAT_RECOMPUTE : STRAT_STORE;
         }
@@ -1735,7 +1785,7 @@ static hipError_t act_phase1(int op, const LA& la, const LB& lb, int M, int N, i
                              uint32_t* amax, int32_t* ws, size_t ws_elems, hipStream_t st) {
     if (M <= 0 || N <= 0) return hipSuccess;
     const GemmPlan p = plan_gemm(M, N, kc_total, LA::BK / 16, kc_total * 16, true, ws ? ws_elems : 0, op);
-    if (p.strat == STRAT_RECOMPUTE) {
+    if (p.strat == STRAT_RECOMPUTE || p.strat == STRAT_SPEC) {
         Epi e;
         e.amax = amax;
         return launch_mode<LA, LB, EPI_AMAX, false>(p, la, lb, M, N, kc_total, e, st);
@@ -1747,7 +1797,7 @@ template <class LA, class LB>
 static hipError_t act_phase2(int op, const LA& la, const LB& lb, int M, int N, int kc_total, const int32_t* acc,
                              const uint32_t* amax, const ActOut& o, size_t ws_elems, hipStream_t st) {
     const GemmPlan p = plan_gemm(M, N, kc_total, LA::BK / 16, kc_total * 16, true, ws_elems, op);
-    if (p.strat == STRAT_RECOMPUTE) {
+    if (p.strat == STRAT_RECOMPUTE || p.strat == STRAT_SPEC) {
         if (o.pool.pool_out != nullptr || o.pool.dx != nullptr || o.out_p16 != nullptr) return hipErrorInvalidValue;
         Epi e;
         e.amax = const_cast<uint32_t*>(amax);
@@ -1776,7 +1826,37 @@ static hipError_t act_phase2(int op, const LA& la, const LB& lb, int M, int N, i
     return requant_act(r, st);
 }
 
+// The speculative pair (STRAT_SPEC): pass 0 = launch A, pass 1 = launch B (see Epi::spec)
+template <class LA, class LB>
+static hipError_t act_spec(int op, const LA& la, const LB& lb, int M, int N, int kc_total, uint32_t* amax,
+                           const ActOut& o, uint32_t* hint, int pass, hipStream_t st) {
+    if (M <= 0 || N <= 0) return hipSuccess;
+    if (o.pool.pool_out != nullptr || o.pool.dx != nullptr || o.out_p16 != nullptr || hint == nullptr || o.out == nullptr)
+        return hipErrorInvalidValue;
+    const GemmPlan p = plan_gemm(M, N, kc_total, LA::BK / 16, kc_total * 16, true, 0, op);
+    Epi e;
+    e.amax = amax;
+    e.out = o.out;
+    e.ldo = N;
+    e.relu = o.relu;
+    e.relu_mask = o.relu_mask;
+    e.exp_in = o.exp_in;
+    e.wscale = o.wscale;
+    e.exp_out = o.exp_out;
+    e.spec = pass == 0 ? 1 : 2;
+    e.hint = hint;
+    return launch_mode<LA, LB, EPI_REQUANT, false>(p, la, lb, M, N, kc_total, e, st);
+}
+
 // ------------------------------------------------------------------------------ per-op wrappers
+bool conv_fwd_spec_ok(const ConvGeom& g) {
+    const int kc = g.kh * g.kw * g.cip / 16;
+    return plan_gemm(g.n * g.oh * g.ow, g.cop, kc, 64 / 16, kc * 16, true, 0, PLAN_FWD).strat == STRAT_SPEC;
+}
+bool conv_dgrad_spec_ok(const ConvGeom& g) {
+    const int kc = g.kh * g.kw * g.cop / 16;
+    return plan_gemm(g.n * g.h * g.w, g.cip, kc, 64 / 16, kc * 16, true, 0, PLAN_DGRAD).strat == STRAT_SPEC;
+}
 bool conv_fwd_phase2_separate(const ConvGeom& g, size_t ws_bytes) {
     const int kc = g.kh * g.kw * g.cip / 16;  // every forward operand loader steps 64 bytes
     return plan_gemm(g.n * g.oh * g.ow, g.cop, kc, 64 / 16, kc * 16, true, ws_bytes / 4, PLAN_FWD).strat !=
@@ -2269,6 +2349,22 @@ hipError_t conv_fwd_phase2(const ConvGeom& g, const int8_t* x, const int8_t* w, 
     const RowsK lb = rows_k(w, (int64_t)g.kh * g.kw * g.cip, g.c_out, kc_total);
     return with_fwd_operand(g, x, [&](const auto& la) {
         return act_phase2(PLAN_FWD, la, lb, g.n * g.oh * g.ow, g.cop, kc_total, acc, amax, o, ws_bytes / 4, st);
+    });
+}
+hipError_t conv_fwd_spec(const ConvGeom& g, const int8_t* x, const int8_t* w, uint32_t* amax, const ActOut& o,
+                         uint32_t* slot, int pass, hipStream_t st) {
+    const int kc_total = g.kh * g.kw * g.cip / 16;
+    const RowsK lb = rows_k(w, (int64_t)g.kh * g.kw * g.cip, g.c_out, kc_total);
+    return with_fwd_operand(g, x, [&](const auto& la) {
+        return act_spec(PLAN_FWD, la, lb, g.n * g.oh * g.ow, g.cop, kc_total, amax, o, slot, pass, st);
+    });
+}
+hipError_t conv_dgrad_spec(const ConvGeom& g, const int8_t* dy, const int8_t* wt, uint32_t* amax, const ActOut& o,
+                           uint32_t* slot, int pass, hipStream_t st) {
+    const int kc_total = g.kh * g.kw * g.cop / 16;
+    const RowsK lb = rows_k(wt, (int64_t)g.kh * g.kw * g.cop, g.c_in, kc_total);
+    return with_dgrad_operand(g, dy, [&](const auto& la) {
+        return act_spec(PLAN_DGRAD, la, lb, g.n * g.h * g.w, g.cip, kc_total, amax, o, slot, pass, st);
     });
 }
 hipError_t conv_dgrad_phase1(const ConvGeom& g, const int8_t* dy, const int8_t* wt, int32_t* acc, uint32_t* amax,

@@ -121,7 +121,9 @@ hipError_t residual_requant(const int8_t* a, const int8_t* ea, const int8_t* b, 
                             const int8_t* relu_mask = nullptr);
 // acc[n][cp] = sum over hw pixels of x NHWC16 (+ max into amax); its gradient: dy broadcast
 hipError_t sum_pool(const int8_t* x, int n, int hw, int cp, int32_t* acc, uint32_t* amax, hipStream_t st);
-hipError_t sum_pool_grad(const int8_t* dy, int n, int hw, int cp, int8_t* dx, hipStream_t st);
+// (relu_mask: the pooled map, NHWC16 -- its relu gradient applied too, dx = mask > 0 ? dy : 0)
+hipError_t sum_pool_grad(const int8_t* dy, int n, int hw, int cp, int8_t* dx, hipStream_t st,
+                         const int8_t* relu_mask = nullptr);
 hipError_t im2col_small(const ConvGeom& g, const int8_t* x, int kp, int8_t* xcol, hipStream_t st, bool nchw = false);
 // ---- weight gradient on P16 pixel blocks (niti_wgrad.hip) --------------------------------
 // P16: [pixels/16][Cp][16] int8 (Cp % 16 == 0, pixels % 16 == 0)
@@ -194,6 +196,21 @@ hipError_t conv0_fwd(const ConvGeom& g, const int8_t* xcol, const int8_t* w, uin
                      int pass, hipStream_t st,
                      int8_t* pool_c32 = nullptr, int8_t* out_c32 = nullptr);
 bool conv_dgrad_phase2_separate(const ConvGeom& g, size_t ws_bytes);
+// The speculative pair on the implicit GEMM (plan strategy 3 = STRAT_SPEC, forward / input
+// gradient, no K split; NITI_Conv_Int8.cpp:260-307, NITI_DeConv_Int8.cpp:294-329): pass 0 (launch A)
+// multiplies, requantises with the bit width the layer had last time and publishes max|acc| into
+// amax (zeroed by the caller); pass 1 (launch B, after any MAX all-reduce of amax) writes the
+// exponent and redoes the GEMM, requantised with the max, only when its bit width differs -- on a
+// hit every block of B exits at once: one GEMM pass and no int32 tensor.  slot: the layer phase's
+// own GEMM_SPEC_SLOT_WORDS zeroed device words ([0] hint, [1] the guess A used, [2] launches B
+// redid).  ActOut without pool / P16 fusion.  Results equal phase 1 + phase 2's.
+constexpr int GEMM_SPEC_SLOT_WORDS = 32;  // one 128-byte line per slot
+bool conv_fwd_spec_ok(const ConvGeom& g);    // the plan (autotuned / forced) is STRAT_SPEC
+bool conv_dgrad_spec_ok(const ConvGeom& g);
+hipError_t conv_fwd_spec(const ConvGeom& g, const int8_t* x, const int8_t* w, uint32_t* amax, const ActOut& o,
+                         uint32_t* slot, int pass, hipStream_t st);
+hipError_t conv_dgrad_spec(const ConvGeom& g, const int8_t* dy, const int8_t* wt, uint32_t* amax, const ActOut& o,
+                           uint32_t* slot, int pass, hipStream_t st);
 hipError_t conv_fwd_phase1(const ConvGeom& g, const int8_t* x, const int8_t* w, int32_t* acc, uint32_t* amax,
                            void* ws, size_t ws_bytes, hipStream_t st);
 hipError_t conv_fwd_phase2(const ConvGeom& g, const int8_t* x, const int8_t* w, const int32_t* acc,

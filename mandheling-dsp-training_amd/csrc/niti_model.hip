@@ -25,7 +25,9 @@
 #include "../../include/niti_hip.h"
 #include "niti_internal.hpp"
 #include "niti_kernels.hpp"
+#include "niti_coll.hpp"
 #include "niti_map.hpp"
+#include "niti_resnet_model.hpp"
 
 namespace niti {
 
@@ -126,149 +128,6 @@ struct FlattenBwd {
 
 }  // namespace
 
-// ---------------------------------------------------------------------------- collectives
-// The data-parallel step's collectives run on two communicators, each used in one fixed program
-// order on every rank:
-//   ranges (`coll`, the step stream): the input quantiser's statistics and every forward /
-//     input-gradient range (MAX), each needed by the very next launch on the step stream;
-//   gradients (`coll_grad`, the comm stream `cst`): one SUM per gradient bucket (consecutive
-//     layers in backward order, ~8 MB or more), issued as soon as the bucket's weight gradients
-//     are in and followed on cst by those layers' ranges, so the SUMs overlap the rest of the
-//     backward pass.
-// RCCL serialises the operations of ONE communicator in issue order whatever stream they are on
-// (each launch waits for the communicator's previous one), so a range MAX on the same
-// communicator as a large SUM would wait for that SUM and stall the input-gradient chain behind
-// it.  With two communicators the step stream's MAXes never wait for a SUM; no operation of one
-// communicator waits for an operation of the other (the SUMs wait only for weight-gradient
-// kernels, the step stream for the SUMs only at the NITI_SGD join), and each communicator's
-// operations are issued in the same order on every rank, so the two cannot deadlock.
-enum CollOp { COLL_MAX_U32 = 0, COLL_SUM_I32 = 1, COLL_SUM_U64 = 2, COLL_MAX_U64 = 3 };
-
-struct Collective {
-    virtual ~Collective() = default;
-    virtual int size() const = 0;
-    // in place, on stream st, asynchronous where the transport allows
-    virtual hipError_t allreduce(void* p, size_t n, CollOp op, hipStream_t st) = 0;
-};
-
-struct RcclCollective final : Collective {
-    ncclComm_t comm = nullptr;
-    int world = 1;
-    bool owns = true;  // false: another RcclCollective's communicator (the no-split fallback)
-    ~RcclCollective() override {
-        if (comm && owns) (void)ncclCommDestroy(comm);
-    }
-    int size() const override { return world; }
-    hipError_t allreduce(void* p, size_t n, CollOp op, hipStream_t st) override {
-        static const ncclDataType_t ty[4] = {ncclUint32, ncclInt32, ncclUint64, ncclUint64};
-        static const ncclRedOp_t ro[4] = {ncclMax, ncclSum, ncclSum, ncclMax};
-        return ncclAllReduce(p, p, n, ty[op], ro[op], comm, st) == ncclSuccess ? hipSuccess : hipErrorUnknown;
-    }
-};
-
-// In-process group of `world` ranks on ONE device, one host thread per rank (tests): each
-// collective synchronises the caller's stream, the last rank to arrive reduces every rank's
-// buffer on the device and writes the result back to all of them.  It runs the model's exact
-// data-parallel protocol -- the same calls, in the same order, on the same streams -- with a
-// transport that needs no second GPU.  A group has one channel per communicator (ranges,
-// gradients), each its own rendezvous.
-struct LocalChannel {
-    std::mutex mu;
-    std::condition_variable cv;
-    int arrived = 0;
-    unsigned long long gen = 0;
-    void* ptr[16] = {};
-    size_t n = 0;
-    int op = -1;
-    bool mismatch = false;
-    hipError_t err = hipSuccess;
-    // the result of generation g, published before the waiters are released: a waiter reads
-    // its own generation's slot, which a faster rank entering generation g + 1 cannot reset
-    // (generation g + 2 needs this waiter's arrival first)
-    hipError_t result[2] = {hipSuccess, hipSuccess};
-};
-
-struct LocalGroup {
-    static constexpr int MAX_RANKS = 16;
-    int world = 1;
-    LocalChannel ch[2];
-    hipStream_t rst = nullptr;
-    ~LocalGroup() {
-        if (rst) (void)hipStreamDestroy(rst);
-    }
-};
-
-namespace {
-struct RankPtrs {
-    void* p[LocalGroup::MAX_RANKS];
-    int world;
-};
-template <class T, bool MAX>
-__global__ void local_reduce_kernel(RankPtrs r, size_t n) {
-    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
-        T v = static_cast<T*>(r.p[0])[i];
-        for (int k = 1; k < r.world; ++k) {
-            const T t = static_cast<T*>(r.p[k])[i];
-            v = MAX ? (t > v ? t : v) : (T)(v + t);
-        }
-        for (int k = 0; k < r.world; ++k) static_cast<T*>(r.p[k])[i] = v;
-    }
-}
-}  // namespace
-
-struct LocalCollective final : Collective {
-    std::shared_ptr<LocalGroup> g;
-    int rank = 0, chan = 0;
-    int size() const override { return g->world; }
-    hipError_t allreduce(void* p, size_t n, CollOp op, hipStream_t st) override {
-        if (g->world == 1) return hipSuccess;  // one rank: the all-reduce is the identity
-        LocalChannel& c = g->ch[chan];
-        hipError_t e = hipStreamSynchronize(st);
-        std::unique_lock<std::mutex> lk(c.mu);
-        const unsigned long long my_gen = c.gen;
-        if (c.arrived == 0) {
-            c.n = n;
-            c.op = op;
-            c.mismatch = false;
-            c.err = hipSuccess;
-        } else if (c.n != n || c.op != op) {
-            c.mismatch = true;  // ranks disagree on the sequence: a protocol bug
-        }
-        c.ptr[rank] = p;
-        if (e != hipSuccess) c.err = e;
-        if (++c.arrived == g->world) {
-            if (!c.mismatch && c.err == hipSuccess) {
-                RankPtrs r{};
-                for (int k = 0; k < g->world; ++k) r.p[k] = c.ptr[k];
-                r.world = g->world;
-                const unsigned blocks = (unsigned)std::min<size_t>((n + 255) / 256, 1024);
-                if (blocks > 0) {
-                    if (op == COLL_MAX_U32)
-                        hipLaunchKernelGGL((local_reduce_kernel<uint32_t, true>), dim3(blocks), dim3(256), 0, g->rst, r, n);
-                    else if (op == COLL_SUM_I32)
-                        hipLaunchKernelGGL((local_reduce_kernel<int32_t, false>), dim3(blocks), dim3(256), 0, g->rst, r, n);
-                    else if (op == COLL_SUM_U64)
-                        hipLaunchKernelGGL((local_reduce_kernel<unsigned long long, false>), dim3(blocks), dim3(256), 0,
-                                           g->rst, r, n);
-                    else
-                        hipLaunchKernelGGL((local_reduce_kernel<unsigned long long, true>), dim3(blocks), dim3(256), 0,
-                                           g->rst, r, n);
-                    c.err = hipGetLastError();
-                    if (c.err == hipSuccess) c.err = hipStreamSynchronize(g->rst);
-                }
-            }
-            if (c.mismatch) c.err = hipErrorInvalidValue;
-            c.result[my_gen & 1] = c.err;
-            c.arrived = 0;
-            ++c.gen;
-            c.cv.notify_all();
-        } else {
-            c.cv.wait(lk, [&] { return c.gen != my_gen; });
-        }
-        return c.result[my_gen & 1];
-    }
-};
-
 struct Layer {
     ConvGeom g{};
     int relu = 0, pool = 0, flatten = 0;
@@ -313,6 +172,8 @@ struct Layer {
     // previous layer's relu / pool gradient in the epilogue); dg = that conv's geometry
     int rcd = 0;
     ConvGeom dg{};
+    // the GEMM path's speculative pair (plan strategy 3): hint slots, forward and input gradient
+    uint32_t* gspec = nullptr;  // 2 x GEMM_SPEC_SLOT_WORDS
     int8_t* wft = nullptr;
     int8_t* dyc32 = nullptr;
     int64_t w_elems() const { return (int64_t)g.c_out * g.kh * g.kw * g.cip; }
@@ -791,8 +652,10 @@ int Model::build(int arch_, int batch_, int in_hw) {
         grad_off += (size_t)l.w_elems();
         l.g8 = (int8_t*)ws.alloc(l.w_elems());
         l.exp = (int8_t*)ws.alloc(16);
-        if (!l.w || !l.ws_dev || !l.wT || !l.r || !l.dy || !l.dwacc || !l.g8 || !l.exp)
+        l.gspec = (uint32_t*)ws.alloc(2 * GEMM_SPEC_SLOT_WORDS * 4);
+        if (!l.w || !l.ws_dev || !l.wT || !l.r || !l.dy || !l.dwacc || !l.g8 || !l.exp || !l.gspec)
             return NITI_OUT_OF_MEMORY;
+        if (hipMemset(l.gspec, 0, 2 * GEMM_SPEC_SLOT_WORDS * 4) != hipSuccess) return NITI_NO_EXECUTION;
         if (hipMemset(l.w, 0, l.w_elems()) != hipSuccess) return NITI_NO_EXECUTION;
         if (hipMemset(l.ws_dev, 0, 16) != hipSuccess) return NITI_NO_EXECUTION;
         acc_elems = std::max(acc_elems, out_px * g.cop);
@@ -1020,22 +883,29 @@ int Model::fwd_layer(int i, hipStream_t st) {
         }
         return NITI_NO_ERROR;
     }
-    MTRY(conv_fwd_phase1(g, l.in, l.w, acc, rng(i, 0), slab, slab_bytes, st));
-    if (dp && exact) CTRY(coll->allreduce(rng(i, 0), MAX_WORDS, COLL_MAX_U32, st));
     ActOut o;
     o.out = l.r;
     o.relu = l.relu;
     o.exp_in = i == 0 ? exp0 : L[i - 1].exp;
     o.wscale = l.ws_dev;
     o.exp_out = l.exp;
+    const bool spec = conv_fwd_spec_ok(g);
     // the 2x2 pool rides along the separate requant pass when there is one
-    const bool fuse_pool = l.pool && g.oh % 2 == 0 && g.ow % 2 == 0 && conv_fwd_phase2_separate(g, slab_bytes);
+    const bool fuse_pool = !spec && l.pool && g.oh % 2 == 0 && g.ow % 2 == 0 && conv_fwd_phase2_separate(g, slab_bytes);
     if (fuse_pool) {
         o.pool.pool_out = l.p;
         o.pool.H = g.oh;
         o.pool.W = g.ow;
     }
-    MTRY(conv_fwd_phase2(g, l.in, l.w, acc, rng(i, 0), o, slab_bytes, st));
+    if (spec) {  // the speculative pair: one GEMM pass while the bit width holds, no int32 tensor
+        MTRY(conv_fwd_spec(g, l.in, l.w, rng(i, 0), o, l.gspec, 0, st));
+        if (dp && exact) CTRY(coll->allreduce(rng(i, 0), MAX_WORDS, COLL_MAX_U32, st));
+        MTRY(conv_fwd_spec(g, l.in, l.w, rng(i, 0), o, l.gspec, 1, st));
+    } else {
+        MTRY(conv_fwd_phase1(g, l.in, l.w, acc, rng(i, 0), slab, slab_bytes, st));
+        if (dp && exact) CTRY(coll->allreduce(rng(i, 0), MAX_WORDS, COLL_MAX_U32, st));
+        MTRY(conv_fwd_phase2(g, l.in, l.w, acc, rng(i, 0), o, slab_bytes, st));
+    }
     probe(i, 0, false, st);
     if (l.pool && !fuse_pool) MTRY(maxpool_nhwc16(l.r, n, g.oh, g.ow, g.cop, 2, 2, 0, l.p, l.ph, l.pw, st));
     if (l.flatten) {
@@ -1223,25 +1093,18 @@ int Model::dgrad_layer(int i, hipStream_t st) {
         return NITI_NO_ERROR;
     }
     dy16_valid[i - 1] = 1;
-    MTRY(conv_dgrad_phase1(g, l.dy, l.wT, acc, rng(i, 1), slab, slab_bytes, st));
-    if (dp && exact) CTRY(coll->allreduce(rng(i, 1), MAX_WORDS, COLL_MAX_U32, st));
     const ConvGeom& pg = pv.g;
+    const bool spec = conv_dgrad_spec_ok(g);
     // dy of layer i - 1 is rewritten here; its P16 copy comes along where the requant pass can
     // write it (the plain and the fused pool-gradient passes), else wgrad_layer converts it
-    int8_t* p16_out = fuse_dp16 && wgrad_p16_splits(i - 1) > 0 ? dp16[i - 1] : nullptr;
+    int8_t* p16_out = !spec && fuse_dp16 && wgrad_p16_splits(i - 1) > 0 ? dp16[i - 1] : nullptr;
     dp16_valid[i - 1] = 0;
     ActOut o;
+    bool fuse = false;
     if (pv.flatten) {
         o.out = pv.dflat;
-        MTRY(conv_dgrad_phase2(g, l.dy, l.wT, acc, rng(i, 1), o, slab_bytes, st));
-        probe(i, 1, false, st);
-        const int fc = pg.c_out * pv.ph * pv.pw, ld = round_up(fc, 16);
-        MTRY(launch_map((int64_t)n * pv.ph * pv.pw * pg.cop,
-                        FlattenBwd{pv.dflat, pv.ph * pv.pw, pg.c_out, pg.cop, ld, pv.dtmp}, st));
-        MTRY(maxpool_relu_grad_nhwc16(pv.r, pv.p, pv.dtmp, n, pg.oh, pg.ow, pg.cop, 2, 2, 0, pv.ph, pv.pw, pv.relu,
-                                      pv.dy, st));
     } else if (pv.pool) {
-        const bool fuse = pg.oh % 2 == 0 && pg.ow % 2 == 0 && conv_dgrad_phase2_separate(g, slab_bytes);
+        fuse = !spec && pg.oh % 2 == 0 && pg.ow % 2 == 0 && conv_dgrad_phase2_separate(g, slab_bytes);
         if (fuse) {  // pool gradient + relu gradient ride along the requant pass
             o.out = nullptr;
             o.pool.x = pv.r;
@@ -1254,17 +1117,30 @@ int Model::dgrad_layer(int i, hipStream_t st) {
         } else {
             o.out = pv.dtmp;
         }
-        MTRY(conv_dgrad_phase2(g, l.dy, l.wT, acc, rng(i, 1), o, slab_bytes, st));
-        probe(i, 1, false, st);
-        if (!fuse)
-            MTRY(maxpool_relu_grad_nhwc16(pv.r, pv.p, pv.dtmp, n, pg.oh, pg.ow, pg.cop, 2, 2, 0, pv.ph, pv.pw,
-                                          pv.relu, pv.dy, st));
     } else {
         o.relu_mask = pv.relu ? pv.r : nullptr;
         o.out = pv.dy;
         if (conv_dgrad_phase2_separate(g, slab_bytes)) o.out_p16 = p16_out;
+    }
+    if (spec) {  // the speculative pair (no int32 tensor while the bit width holds)
+        MTRY(conv_dgrad_spec(g, l.dy, l.wT, rng(i, 1), o, l.gspec + GEMM_SPEC_SLOT_WORDS, 0, st));
+        if (dp && exact) CTRY(coll->allreduce(rng(i, 1), MAX_WORDS, COLL_MAX_U32, st));
+        MTRY(conv_dgrad_spec(g, l.dy, l.wT, rng(i, 1), o, l.gspec + GEMM_SPEC_SLOT_WORDS, 1, st));
+    } else {
+        MTRY(conv_dgrad_phase1(g, l.dy, l.wT, acc, rng(i, 1), slab, slab_bytes, st));
+        if (dp && exact) CTRY(coll->allreduce(rng(i, 1), MAX_WORDS, COLL_MAX_U32, st));
         MTRY(conv_dgrad_phase2(g, l.dy, l.wT, acc, rng(i, 1), o, slab_bytes, st));
-        probe(i, 1, false, st);
+    }
+    probe(i, 1, false, st);
+    if (pv.flatten) {
+        const int fc = pg.c_out * pv.ph * pv.pw, ld = round_up(fc, 16);
+        MTRY(launch_map((int64_t)n * pv.ph * pv.pw * pg.cop,
+                        FlattenBwd{pv.dflat, pv.ph * pv.pw, pg.c_out, pg.cop, ld, pv.dtmp}, st));
+        MTRY(maxpool_relu_grad_nhwc16(pv.r, pv.p, pv.dtmp, n, pg.oh, pg.ow, pg.cop, 2, 2, 0, pv.ph, pv.pw, pv.relu,
+                                      pv.dy, st));
+    } else if (pv.pool && !fuse) {
+        MTRY(maxpool_relu_grad_nhwc16(pv.r, pv.p, pv.dtmp, n, pg.oh, pg.ow, pg.cop, 2, 2, 0, pv.ph, pv.pw, pv.relu,
+                                      pv.dy, st));
     }
     if (o.out_p16 != nullptr) dp16_valid[i - 1] = 1;
     return NITI_NO_ERROR;
@@ -1381,6 +1257,8 @@ int Model::autotune(hipStream_t st, int reps) {
                 cands.push_back(c);
                 if (act) {
                     c.strat = 1;
+                    cands.push_back(c);
+                    c.strat = 3;  // the speculative pair
                     cands.push_back(c);
                 }
                 for (int s : split_opts) {
@@ -1555,7 +1433,8 @@ int Model::run(const int8_t* x_nchw, int exp_in, const uint8_t* images, const in
 
 // =========================================================================== C ABI (section 3)
 struct niti_model {
-    niti::Model m;
+    niti::Model m;                         // LeNet / VGG-11 / VGG-16
+    std::unique_ptr<niti::ResNetModel> r;  // ResNet-18 (niti_resnet_model.hip); m unused then
 };
 
 extern "C" {
@@ -1563,9 +1442,23 @@ extern "C" {
 int niti_model_create(int arch, int batch, niti_model_t* out) { return niti_model_create2(arch, batch, 0, out); }
 
 int niti_model_create2(int arch, int batch, int in_hw, niti_model_t* out) {
-    if (!out || batch <= 0 || in_hw < 0) return NITI_INVALID_VALUE;
+    return niti_model_create3(arch, batch, in_hw, 0, out);
+}
+
+int niti_model_create3(int arch, int batch, int in_hw, int classes, niti_model_t* out) {
+    if (!out || batch <= 0 || in_hw < 0 || classes < 0) return NITI_INVALID_VALUE;
     auto* h = new niti_model();
-    const int rc = h->m.build(arch, batch, in_hw);
+    int rc;
+    if (arch == NITI_ARCH_RESNET18) {
+        h->r = std::make_unique<niti::ResNetModel>();
+        rc = h->r->build(batch, in_hw, classes);
+    } else {
+        if (classes != 0) {  // the LeNet / VGG heads are fixed (10 or 1000 classes)
+            delete h;
+            return NITI_NOT_SUPPORT;
+        }
+        rc = h->m.build(arch, batch, in_hw);
+    }
     if (rc != NITI_NO_ERROR) {
         delete h;
         return rc;
@@ -1576,9 +1469,17 @@ int niti_model_create2(int arch, int batch, int in_hw, niti_model_t* out) {
 
 void niti_model_destroy(niti_model_t m) { delete m; }
 
-int niti_model_num_layers(niti_model_t m) { return m ? (int)m->m.L.size() : 0; }
+int niti_model_num_layers(niti_model_t m) { return !m ? 0 : m->r ? (int)m->r->C.size() : (int)m->m.L.size(); }
 
 int niti_model_layer_info(niti_model_t m, int layer, int info[12]) {
+    if (m && m->r) {
+        if (layer < 0 || layer >= (int)m->r->C.size() || !info) return NITI_INVALID_VALUE;
+        const niti::RConv& c = m->r->C[layer];
+        const niti::ConvGeom& g = c.og;
+        const int v[12] = {g.c_in, g.c_out, g.kh, g.kw, g.h, g.w, g.oh, g.ow, g.pt, g.sh, c.relu, 0};
+        memcpy(info, v, sizeof(v));
+        return NITI_NO_ERROR;
+    }
     if (!m || layer < 0 || layer >= (int)m->m.L.size()) return NITI_INVALID_VALUE;
     const niti::Layer& l = m->m.L[layer];
     const niti::ConvGeom& g = l.og;  // the layer as the network defines it
@@ -1601,6 +1502,7 @@ static void oihw_from_col(const niti::ConvGeom& o, const int8_t* wc, int8_t* w) 
 }
 
 int niti_model_set_weight(niti_model_t m, int layer, const int8_t* w_host, int wscale) {
+    if (m && m->r) return m->r->set_weight(layer, w_host, wscale);
     if (!m || layer < 0 || layer >= (int)m->m.L.size() || !w_host) return NITI_INVALID_VALUE;
     niti::Layer& l = m->m.L[layer];
     std::vector<int8_t> colw;
@@ -1627,6 +1529,7 @@ int niti_model_set_weight(niti_model_t m, int layer, const int8_t* w_host, int w
 }
 
 int niti_model_get_weight(niti_model_t m, int layer, int8_t* w_host) {
+    if (m && m->r) return m->r->get_weight(layer, w_host);
     if (!m || layer < 0 || layer >= (int)m->m.L.size() || !w_host) return NITI_INVALID_VALUE;
     niti::Layer& l = m->m.L[layer];
     const size_t n = (size_t)l.g.c_out * l.g.c_in * l.g.kh * l.g.kw;
@@ -1643,16 +1546,19 @@ int niti_model_get_weight(niti_model_t m, int layer, int8_t* w_host) {
 }
 
 int niti_model_train_step(niti_model_t m, const int8_t* x_nchw, int exp_in, const int32_t* labels, void* stream) {
+    if (m && m->r) return x_nchw && labels ? m->r->step(x_nchw, exp_in, nullptr, labels, (hipStream_t)stream) : NITI_INVALID_VALUE;
     if (!m || !x_nchw || !labels) return NITI_INVALID_VALUE;
     return m->m.step(x_nchw, exp_in, nullptr, labels, (hipStream_t)stream);
 }
 
 int niti_model_train_step_images(niti_model_t m, const uint8_t* images_nchw, const int32_t* labels, void* stream) {
+    if (m && m->r) return images_nchw && labels ? m->r->step(nullptr, 0, images_nchw, labels, (hipStream_t)stream) : NITI_INVALID_VALUE;
     if (!m || !images_nchw || !labels) return NITI_INVALID_VALUE;
     return m->m.step(nullptr, 0, images_nchw, labels, (hipStream_t)stream);
 }
 
 int niti_model_get_input(niti_model_t m, int8_t* x_nchw_host, int* ascale, void* stream) {
+    if (m && m->r) return x_nchw_host ? m->r->get_input(x_nchw_host, ascale, (hipStream_t)stream) : NITI_INVALID_VALUE;
     if (!m || !x_nchw_host) return NITI_INVALID_VALUE;
     niti::Model& mm = m->m;
     const int n = mm.batch, hw = mm.in_h * mm.in_w;
@@ -1671,6 +1577,7 @@ int niti_model_get_input(niti_model_t m, int8_t* x_nchw_host, int* ascale, void*
 }
 
 int niti_model_get_logits(niti_model_t m, int8_t* logits_host, int* exp_out, void* stream) {
+    if (m && m->r) return logits_host ? m->r->get_logits(logits_host, exp_out, (hipStream_t)stream) : NITI_INVALID_VALUE;
     if (!m) return NITI_INVALID_VALUE;
     niti::Layer& t = m->m.L.back();
     const int n = m->m.batch;
@@ -1686,6 +1593,7 @@ int niti_model_get_logits(niti_model_t m, int8_t* logits_host, int* exp_out, voi
 }
 
 int niti_model_get_tap(niti_model_t m, int layer, int which, int8_t* host, size_t bytes, void* stream) {
+    if (m && m->r) return host ? m->r->get_tap(layer, which, host, bytes, (hipStream_t)stream) : NITI_INVALID_VALUE;
     if (!m || layer < 0 || layer >= (int)m->m.L.size()) return NITI_INVALID_VALUE;
     niti::Layer& l = m->m.L[layer];
     const niti::ConvGeom& g = l.g;
@@ -1728,6 +1636,7 @@ int niti_model_get_tap(niti_model_t m, int layer, int which, int8_t* host, size_
 }
 
 int64_t niti_model_step_macs(niti_model_t m) {
+    if (m && m->r) return m->r->step_macs();
     if (!m) return 0;
     int64_t s = 0;
     const int world = m->m.world > 0 ? m->m.world : 1;
@@ -1742,12 +1651,18 @@ int64_t niti_model_step_macs(niti_model_t m) {
 }
 
 int niti_model_set_overlap(niti_model_t m, int enable) {
+    if (m && m->r) return NITI_NO_ERROR;  // one stream (the weight gradients interleave with the input gradients)
     if (!m) return NITI_INVALID_VALUE;
     m->m.overlap = enable != 0;
     return NITI_NO_ERROR;
 }
 
 int niti_model_keep_grads(niti_model_t m, int enable) {
+    if (m && m->r) {
+        m->r->keep_grads = enable != 0;
+        m->r->drop_graph();
+        return NITI_NO_ERROR;
+    }
     if (!m) return NITI_INVALID_VALUE;
     m->m.keep_grads = enable != 0;
     m->m.drop_graph();
@@ -1755,6 +1670,17 @@ int niti_model_keep_grads(niti_model_t m, int enable) {
 }
 
 int niti_model_set_rowconv(niti_model_t m, int enable) {
+    if (m && m->r) {
+        niti::ResNetModel& r = *m->r;
+        if (r.use_rowconv && enable == 0) {  // the GEMM input gradients read IHWO16 copies the update skipped
+            for (int i = 0; i < (int)r.C.size(); ++i)
+                if (r.refresh_copies(i, nullptr) != NITI_NO_ERROR) return NITI_NO_EXECUTION;
+            if (hipDeviceSynchronize() != hipSuccess) return NITI_NO_EXECUTION;
+        }
+        r.use_rowconv = enable != 0;
+        r.drop_graph();
+        return NITI_NO_ERROR;
+    }
     if (!m) return NITI_INVALID_VALUE;
     if (m->m.use_rowconv && enable == 0) {
         const int rc = m->m.refresh_wt(nullptr);
@@ -1766,6 +1692,7 @@ int niti_model_set_rowconv(niti_model_t m, int enable) {
 }
 
 int niti_model_spec_stats(niti_model_t m, uint32_t* out, int max_layers) {
+    if (m && m->r) return out && max_layers >= 0 ? m->r->spec_stats(out, max_layers) : NITI_INVALID_VALUE;
     if (!m || !out || max_layers < 0) return NITI_INVALID_VALUE;
     const int nl = std::min(max_layers, (int)m->m.L.size());
     std::fill(out, out + (size_t)nl * 6, 0u);
@@ -1786,6 +1713,7 @@ int niti_model_spec_stats(niti_model_t m, uint32_t* out, int max_layers) {
 }
 
 int niti_model_rowconv_error(niti_model_t m) {
+    if (m && m->r) return m->r->rowconv_error();
     if (!m) return NITI_INVALID_VALUE;
     uint32_t e = 0;
     if (hipDeviceSynchronize() != hipSuccess || hipMemcpy(&e, m->m.rc_err, 4, hipMemcpyDeviceToHost) != hipSuccess)
@@ -1794,6 +1722,11 @@ int niti_model_rowconv_error(niti_model_t m) {
 }
 
 int niti_model_set_graph(niti_model_t m, int enable) {
+    if (m && m->r) {
+        m->r->drop_graph();
+        m->r->use_graph = enable != 0;
+        return NITI_NO_ERROR;
+    }
     if (!m) return NITI_INVALID_VALUE;
     m->m.drop_graph();
     m->m.use_graph = enable != 0;
@@ -1801,11 +1734,13 @@ int niti_model_set_graph(niti_model_t m, int enable) {
 }
 
 int niti_model_autotune(niti_model_t m, int reps, void* stream) {
+    if (m && m->r) return m->r->autotune((hipStream_t)stream, reps);
     if (!m) return NITI_INVALID_VALUE;
     return m->m.autotune((hipStream_t)stream, reps);
 }
 
 int niti_model_run_phase(niti_model_t m, int layer, int phase, void* stream) {
+    if (m && m->r) return m->r->run_phase(layer, phase, (hipStream_t)stream);
     if (!m || layer < 0 || layer >= (int)m->m.L.size() || phase < 0 || phase > 2 || (phase == 1 && layer == 0))
         return NITI_INVALID_VALUE;
     const bool t = m->m.tuning;
@@ -1820,6 +1755,17 @@ int niti_model_run_phase(niti_model_t m, int layer, int phase, void* stream) {
 }
 
 int niti_model_plan_info(niti_model_t m, int layer, int phase, int info[4]) {
+    if (m && m->r) {
+        if (!info || layer < 0 || layer >= (int)m->r->C.size() || phase < 0 || phase > 2) return NITI_INVALID_VALUE;
+        const int op = phase == 0 ? niti::PLAN_FWD : phase == 1 ? niti::PLAN_DGRAD : niti::PLAN_WGRAD;
+        const niti::PlanChoice c = niti::conv_plan_query(op, m->r->C[layer].g, phase != 2,
+                                                         phase == 2 ? m->r->slab_w_bytes : m->r->slab_bytes);
+        info[0] = c.bm;
+        info[1] = c.bn;
+        info[2] = c.splits;
+        info[3] = c.strat;
+        return NITI_NO_ERROR;
+    }
     if (!m || !info || layer < 0 || layer >= (int)m->m.L.size() || phase < 0 || phase > 2)
         return NITI_INVALID_VALUE;
     const niti::ConvGeom& g = m->m.L[layer].g;
@@ -1838,6 +1784,33 @@ int niti_model_plan_info(niti_model_t m, int layer, int phase, int info[4]) {
 }
 
 int niti_model_plan_set(niti_model_t m, int layer, int phase, const int plan[4]) {
+    if (m && m->r) {
+        if (layer < 0 || layer >= (int)m->r->C.size() || phase < 0 || phase > 2) return NITI_INVALID_VALUE;
+        const int op = phase == 0 ? niti::PLAN_FWD : phase == 1 ? niti::PLAN_DGRAD : niti::PLAN_WGRAD;
+        const niti::ConvGeom& g = m->r->C[layer].g;
+        const niti::PlanKey k = niti::conv_plan_key(op, g);
+        m->r->drop_graph();
+        if (plan == nullptr) {
+            niti::plan_override_clear(k);
+            return NITI_NO_ERROR;
+        }
+        auto tile_ok = [](int t) { return t == 64 || t == 128 || t == 256; };
+        const bool taps = plan[0] == niti::PLAN_TAPS_TILE && plan[1] == niti::PLAN_TAPS_TILE && op == niti::PLAN_WGRAD &&
+                          niti::conv_wgrad_taps_ok(g);
+        if ((!taps && (!tile_ok(plan[0]) || !tile_ok(plan[1]))) || plan[2] < 1 || plan[2] > 64 || plan[3] < 0 ||
+            plan[3] > 3 || (taps && plan[3] == 1) || (plan[3] == 3 && (op == niti::PLAN_WGRAD || plan[2] != 1)))
+            return NITI_INVALID_VALUE;
+        niti::PlanChoice c;
+        c.bm = plan[0];
+        c.bn = plan[1];
+        c.splits = plan[2];
+        c.strat = plan[3];
+        if (c.strat == 2 &&
+            !m->r->ensure_slab(std::min(niti::plan_slab_bytes(k.M, k.N, c.splits), size_t(1) << 30), op == niti::PLAN_WGRAD))
+            return NITI_OUT_OF_MEMORY;
+        niti::plan_override_set(k, c);
+        return NITI_NO_ERROR;
+    }
     if (!m || layer < 0 || layer >= (int)m->m.L.size() || phase < 0 || phase > 2) return NITI_INVALID_VALUE;
     const int op = phase == 0 ? niti::PLAN_FWD : phase == 1 ? niti::PLAN_DGRAD : niti::PLAN_WGRAD;
     const niti::PlanKey k = niti::conv_plan_key(op, m->m.L[layer].g);
@@ -1851,7 +1824,7 @@ int niti_model_plan_set(niti_model_t m, int layer, int phase, const int plan[4])
         const bool p16 = plan[0] == niti::PLAN_P16_TILE && plan[1] == niti::PLAN_P16_TILE &&
                          op == niti::PLAN_WGRAD && niti::conv_wgrad_p16_ok(g);
         if ((!taps && !p16 && (!tile_ok(plan[0]) || !tile_ok(plan[1]))) || plan[2] < 1 || plan[3] < 0 ||
-            plan[3] > 2 || ((taps || p16) && plan[3] == 1))
+            plan[3] > 3 || ((taps || p16) && plan[3] == 1) || (plan[3] == 3 && (op == niti::PLAN_WGRAD || plan[2] != 1)))
             return NITI_INVALID_VALUE;
         if (p16) {
             if (plan[2] > 64) return NITI_INVALID_VALUE;
@@ -1874,6 +1847,21 @@ int niti_model_plan_set(niti_model_t m, int layer, int phase, const int plan[4])
 void niti_plan_reset(void) { niti::plan_override_clear_all(); }
 
 int niti_model_set_probe(niti_model_t m, int layer, int phase, int max_launches) {
+    if (m && m->r) {
+        if (max_launches < 0) return NITI_INVALID_VALUE;
+        niti::ResNetModel& r = *m->r;
+        r.clear_probe();
+        if (layer < 0) return NITI_NO_ERROR;
+        r.probe_layer = layer;
+        r.probe_phase = phase;
+        r.ev0.resize(max_launches);
+        r.ev1.resize(max_launches);
+        for (int i = 0; i < max_launches; ++i)
+            if (hipEventCreateWithFlags(&r.ev0[i], hipEventDisableSystemFence) != hipSuccess ||
+                hipEventCreateWithFlags(&r.ev1[i], hipEventDisableSystemFence) != hipSuccess)
+                return NITI_OUT_OF_MEMORY;
+        return NITI_NO_ERROR;
+    }
     if (!m || max_launches < 0) return NITI_INVALID_VALUE;
     m->m.clear_probe();
     if (layer < 0) return NITI_NO_ERROR;
@@ -1897,6 +1885,12 @@ int niti_model_set_probe(niti_model_t m, int layer, int phase, int max_launches)
 }
 
 int niti_model_probe_read_span(niti_model_t m, double* total_ms, int* count) {
+    if (m && m->r) {
+        if (!total_ms || !count) return NITI_INVALID_VALUE;
+        *total_ms = 0;  // no in-kernel span probe on this driver
+        *count = 0;
+        return NITI_NO_ERROR;
+    }
     if (!m || !total_ms || !count) return NITI_INVALID_VALUE;
     *total_ms = 0;
     *count = 0;
@@ -1932,6 +1926,21 @@ int niti_model_probe_read_span(niti_model_t m, double* total_ms, int* count) {
 }
 
 int niti_model_probe_read(niti_model_t m, double* total_ms, int* count) {
+    if (m && m->r) {
+        if (!total_ms || !count) return NITI_INVALID_VALUE;
+        niti::ResNetModel& r = *m->r;
+        double t = 0;
+        for (int i = 0; i < r.probe_count; ++i) {
+            float ms = 0.f;
+            if (hipEventSynchronize(r.ev1[i]) != hipSuccess || hipEventElapsedTime(&ms, r.ev0[i], r.ev1[i]) != hipSuccess)
+                return NITI_NO_EXECUTION;
+            t += ms;
+        }
+        *total_ms = t;
+        *count = r.probe_count;
+        r.probe_count = 0;
+        return NITI_NO_ERROR;
+    }
     if (!m || !total_ms || !count) return NITI_INVALID_VALUE;
     double t = 0;
     for (int i = 0; i < m->m.probe_count; ++i) {
@@ -1946,6 +1955,28 @@ int niti_model_probe_read(niti_model_t m, double* total_ms, int* count) {
     m->m.probe_count = 0;
     return NITI_NO_ERROR;
 }
+
+extern "C++" {
+// hand a communicator pair to whichever step driver the handle holds
+template <class M>
+static void attach_to(M& d, std::unique_ptr<niti::Collective> c, std::unique_ptr<niti::Collective> cg, bool shared,
+                      int world, int rank, int exact) {
+    d.drop_graph();
+    d.coll = std::move(c);
+    d.coll_grad = std::move(cg);
+    d.shared_comm = shared;
+    d.world = world;
+    d.rank = rank;
+    d.exact = exact ? 1 : 0;
+}
+static void attach(niti_model_t m, std::unique_ptr<niti::Collective> c, std::unique_ptr<niti::Collective> cg,
+                   bool shared, int world, int rank, int exact) {
+    if (m->r)
+        attach_to(*m->r, std::move(c), std::move(cg), shared, world, rank, exact);
+    else
+        attach_to(m->m, std::move(c), std::move(cg), shared, world, rank, exact);
+}
+}  // extern "C++"
 
 int niti_dp_get_unique_id(char id[NITI_UNIQUE_ID_BYTES]) {
     static_assert(sizeof(ncclUniqueId) == NITI_UNIQUE_ID_BYTES, "ncclUniqueId size");
@@ -2005,13 +2036,7 @@ int niti_model_attach_comm(niti_model_t m, const char id[NITI_UNIQUE_ID_BYTES], 
         shared = true;
     }
     cg->world = world;
-    m->m.shared_comm = shared;
-    m->m.drop_graph();
-    m->m.coll = std::move(c);
-    m->m.coll_grad = std::move(cg);
-    m->m.world = world;
-    m->m.rank = rank;
-    m->m.exact = exact ? 1 : 0;
+    attach(m, std::move(c), std::move(cg), shared, world, rank, exact);
     return NITI_NO_ERROR;
 }
 
@@ -2047,13 +2072,7 @@ int niti_model_attach_local(niti_model_t m, niti_local_group_t g, int rank, int 
     // no-split fallback runs them on one RCCL communicator
     const bool shared = getenv("NITI_DIAG_SHARED_COMM") != nullptr;
     cg->chan = shared ? 0 : 1;
-    m->m.drop_graph();
-    m->m.coll = std::move(c);
-    m->m.shared_comm = shared;
-    m->m.coll_grad = std::move(cg);
-    m->m.world = g->g->world;
-    m->m.rank = rank;
-    m->m.exact = exact ? 1 : 0;
+    attach(m, std::move(c), std::move(cg), shared, g->g->world, rank, exact);
     return NITI_NO_ERROR;
 }
 

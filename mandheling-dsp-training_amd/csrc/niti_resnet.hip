@@ -94,22 +94,31 @@ hipError_t sum_pool(const int8_t* x, int n, int hw, int cp, int32_t* acc, uint32
     return hipGetLastError();
 }
 
-// dx[img][p][c] = dy[img][c] for every pixel p (16-byte chunks)
+// dx[img][p][c] = dy[img][c] for every pixel p (16-byte chunks); with relu_mask (NHWC16, the pooled
+// map -- the last block's output) the relu gradient too: dx = mask > 0 ? dy : 0
 __global__ void __launch_bounds__(256) sum_pool_grad_kernel(const int8_t* __restrict__ dy, int64_t total16, int hw,
-                                                            int c16, int8_t* __restrict__ dx) {
+                                                            int c16, const int8_t* __restrict__ relu_mask,
+                                                            int8_t* __restrict__ dx) {
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total16; i += (int64_t)gridDim.x * 256) {
         const int64_t img = i / ((int64_t)hw * c16);
         const int ch = (int)(i % c16);
-        ((v4i*)dx)[i] = ((const v4i*)dy)[img * c16 + ch];
+        v16c v = ((const v16c*)dy)[img * c16 + ch];
+        if (relu_mask != nullptr) {
+            const v16c m = ((const v16c*)relu_mask)[i];
+#pragma unroll
+            for (int e = 0; e < 16; ++e) v[e] = m[e] > 0 ? v[e] : (int8_t)0;
+        }
+        ((v16c*)dx)[i] = v;
     }
 }
 
-hipError_t sum_pool_grad(const int8_t* dy, int n, int hw, int cp, int8_t* dx, hipStream_t st) {
+hipError_t sum_pool_grad(const int8_t* dy, int n, int hw, int cp, int8_t* dx, hipStream_t st, const int8_t* relu_mask) {
     if (n <= 0 || hw <= 0 || cp <= 0 || cp % 16 != 0) return hipErrorInvalidValue;
     const int64_t total16 = (int64_t)n * hw * (cp / 16);
     int64_t blocks = (total16 + 255) / 256;
     blocks = blocks > 4096 ? 4096 : blocks;
-    hipLaunchKernelGGL(sum_pool_grad_kernel, dim3((unsigned)blocks), dim3(256), 0, st, dy, total16, hw, cp / 16, dx);
+    hipLaunchKernelGGL(sum_pool_grad_kernel, dim3((unsigned)blocks), dim3(256), 0, st, dy, total16, hw, cp / 16,
+                       relu_mask, dx);
     return hipGetLastError();
 }
 

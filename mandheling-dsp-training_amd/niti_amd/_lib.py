@@ -48,7 +48,7 @@ OP_DSP_GRADIENT_SPLITBATCHCONV_INT8 = 821
 OP_DSP_TRANSPOSEGRADIENT_CONV_INT8 = 822
 FORMAT_NCHW, FORMAT_NHWC, FORMAT_NC4HW4 = 0, 1, 2
 PAD_CAFFE, PAD_VALID, PAD_SAME = 0, 1, 2
-ARCH_LENET, ARCH_VGG11, ARCH_VGG16 = 1, 2, 3
+ARCH_LENET, ARCH_VGG11, ARCH_VGG16, ARCH_RESNET18 = 1, 2, 3, 4
 
 
 class NitiError(RuntimeError):
@@ -162,6 +162,7 @@ def lib():
         "niti_loss_grad": (ci, [vp, ci, ci, ci, vp, vp, vp, vp]),
         "niti_model_create": (ci, [ci, ci, C.POINTER(vp)]),
         "niti_model_create2": (ci, [ci, ci, ci, C.POINTER(vp)]),
+        "niti_model_create3": (ci, [ci, ci, ci, ci, C.POINTER(vp)]),
         "niti_model_destroy": (None, [vp]),
         "niti_model_num_layers": (ci, [vp]),
         "niti_model_layer_info": (ci, [vp, ci, C.POINTER(ci)]),

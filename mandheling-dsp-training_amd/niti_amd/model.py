@@ -14,10 +14,12 @@ from .ops import _stream
 class NitiModel:
     """NITIInt8Train's model + NITI_SGD step, on one GPU (optionally one rank of a DP group)."""
 
-    def __init__(self, arch: int, batch: int, in_hw: int = 0):
+    def __init__(self, arch: int, batch: int, in_hw: int = 0, classes: int = 0):
+        """arch: niti_amd.ARCH_*; in_hw: the input size (0: the architecture's); classes: the head's
+        class count (0: the architecture's; ResNet-18 only)."""
         self._lib = L.lib()
         h = C.c_void_p()
-        check(self._lib.niti_model_create2(arch, batch, int(in_hw), C.byref(h)), "model_create")
+        check(self._lib.niti_model_create3(arch, batch, int(in_hw), int(classes), C.byref(h)), "model_create")
         self._h = h
         self.arch, self.batch = arch, batch
         self._wscale = {}

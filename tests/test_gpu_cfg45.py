@@ -9,7 +9,7 @@
   tile-mode tap-sharing weight gradient with 128 / 64 / 32 / 16 K splits on conv1_2 .. conv3_1, and
   split-K GEMMs on the deeper layers.  Every tap of a whole step is compared with the oracle.
 - Exact data parallelism where the row-segment speculative pair runs under the cross-rank MAX:
-  VGG-16 at 112 px, one image per rank through the C++ in-process group, and ResNet-18 at 112 px
+  VGG-16 at 224 px, one image per rank through the C++ in-process group, and ResNet-18 at 112 px
   through ThreadComm.  One rank gets an all-zero image, so its local bit width is 0 in every forward
   layer while the global one is not.  The first step has no hint, so every pair's launch B redoes
   its launch against the all-reduced max.  Every rank must equal one device stepping the whole batch.
@@ -110,10 +110,12 @@ VGG16_BENCH_PLANS = {
 }
 
 
-@pytest.mark.parametrize("plans", ["autotuned", "bench"])
+@pytest.mark.parametrize("plans", ["autotuned", "bench", "spec"])
 def test_vgg16_224_tuned_plans_step_matches_oracle(T, plans):
-    """A whole VGG-16 224-px step (batch 2) under the autotuner's plans, or under the bench's batch-64
-    kernel choices forced on, every tap against the oracle; the plans are dropped afterwards."""
+    """A whole VGG-16 224-px step (batch 2) under the autotuner's plans, under the bench's batch-64
+    kernel choices forced on, or with every GEMM-path forward and input gradient on the speculative
+    pair (plan strategy 3: launch A requantises with the previous bit width, launch B redoes it on a
+    change -- no int32 tensor), every tap against the oracle over two steps; plans dropped after."""
     import niti_amd
     import niti_model_ref as R
     from niti_amd.model import NitiModel
@@ -129,11 +131,16 @@ def test_vgg16_224_tuned_plans_step_matches_oracle(T, plans):
         m.train_step(T.from_numpy(x).cuda(), -3, T.from_numpy(labels).cuda())  # fills the buffers
         if plans == "autotuned":
             m.autotune(reps=1)
-        else:
+        elif plans == "bench":
             for (layer, phase), p in VGG16_BENCH_PLANS.items():
                 m.set_plan(layer, phase, p)
             for layer in range(1, 5):
                 assert m.plan(layer, 2)[:2] == (32, 32), layer
+        else:
+            for layer in range(5, len(layers)):
+                for phase in (0, 1):
+                    m.set_plan(layer, phase, (128, 128, 1, 3))
+                    assert m.plan(layer, phase)[3] == 3, (layer, phase)
         for i, (w, s) in enumerate(zip(W, S)):
             m.set_weight(i, w, s)
         for step in range(2):
@@ -186,14 +193,15 @@ def _batches(rng, steps, world, per, shape, classes):
     return out
 
 
-def test_vgg16_112_local_dp_row_segment_pair(T):
-    """VGG-16 at 112 px, world 2, one image per rank, the C++ in-process group (the RCCL protocol's
+def test_vgg16_224_local_dp_row_segment_pair(T):
+    """VGG-16 at 224 px (the row-segment maps are 224 / 112 / 56 / 28 / 14 px, and VGG-16 inputs are
+    multiples of 32), world 2, one image per rank, the C++ in-process group (the RCCL protocol's
     calls and streams): conv1_2 .. conv3_1 run the row-segment speculative pair with the MAX between
     launches A and B.  Every rank equals one full-batch device, which equals the oracle."""
     import niti_amd
     import niti_model_ref as R
     from niti_amd.model import LocalGroup, NitiModel
-    world, per, hw = 2, 1, 112
+    world, per, hw = 2, 1, 224
     layers = R.vgg16_layers(hw)
     W, S = R.init_weights(layers, seed=112)
     full = NitiModel(niti_amd.ARCH_VGG16, world * per, hw)
