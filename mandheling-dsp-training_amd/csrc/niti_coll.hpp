@@ -3,6 +3,7 @@
 #pragma once
 
 #include <rccl/rccl.h>
+#include <stdlib.h>
 
 #include <condition_variable>
 #include <memory>
@@ -28,6 +29,14 @@ namespace niti {
 // communicator waits for an operation of the other (the SUMs wait only for weight-gradient
 // kernels, the step stream for the SUMs only at the NITI_SGD join), and each communicator's
 // operations are issued in the same order on every rank, so the two cannot deadlock.
+// Gradient buckets close once they hold this many int32 gradient bytes (backward order).  Each
+// bucket costs one event record on the step stream (a ~6.5 us bubble before the next launch), so
+// fewer, larger buckets; NITI_BUCKET_MB overrides (A/B).
+inline size_t grad_bucket_bytes() {
+    static const long mb = getenv("NITI_BUCKET_MB") ? atol(getenv("NITI_BUCKET_MB")) : 8;
+    return (size_t)(mb > 0 ? mb : 1) << 20;
+}
+
 enum CollOp { COLL_MAX_U32 = 0, COLL_SUM_I32 = 1, COLL_SUM_U64 = 2, COLL_MAX_U64 = 3 };
 
 struct Collective {

@@ -1748,7 +1748,8 @@ hipError_t splitk_reduce_linear(const int32_t* slab, int splits, int64_t n, int6
 // Materialise C [M][N] int32 (+ max|C| if amax) under plan p: STORE, or SLAB + reduce.
 template <class LA, class LB, bool KT = false>
 static hipError_t gemm_acc_plan(const GemmPlan& p, const LA& la, const LB& lb, int M, int N, int kc_total, int32_t* C,
-                                uint32_t* amax, int32_t* ws, hipStream_t st, hipEvent_t after_gemm = nullptr) {
+                                uint32_t* amax, int32_t* ws, hipStream_t st, hipEvent_t after_gemm = nullptr,
+                                SgdJob* defer = nullptr) {
     Epi e;
     if (KT) e.span = take_span();  // weight gradient: the kernel-span probe slot, if armed
     if (p.strat == STRAT_SLAB) {
@@ -1759,6 +1760,13 @@ static hipError_t gemm_acc_plan(const GemmPlan& p, const LA& la, const LB& lb, i
         hipError_t r = launch_mode<LA, LB, EPI_SLAB, KT>(p, la, lb, M, N, kc_total, e, st);
         if (r == hipSuccess && after_gemm != nullptr) r = hipEventRecord(after_gemm, st);
         if (r != hipSuccess) return r;
+        if (defer != nullptr && ((int64_t)M * N) % 4 == 0) {  // the NITI_SGD launch combines the slabs
+            defer->slab = ws;
+            defer->splits = p.splits;
+            defer->slab_stride = e.slab_stride;
+            defer->slab_n = (int64_t)M * N;
+            return hipSuccess;
+        }
         return splitk_reduce(p, ws, (int64_t)M * N, e.slab_stride, C, amax, st);
     }
     e.C = C;
@@ -1771,11 +1779,12 @@ static hipError_t gemm_acc_plan(const GemmPlan& p, const LA& la, const LB& lb, i
 
 template <class LA, class LB, bool KT = false>
 static hipError_t gemm_acc(int op, const LA& la, const LB& lb, int M, int N, int kc_total, int32_t* C, uint32_t* amax,
-                           int32_t* ws, size_t ws_elems, hipStream_t st, hipEvent_t after_gemm = nullptr) {
+                           int32_t* ws, size_t ws_elems, hipStream_t st, hipEvent_t after_gemm = nullptr,
+                           SgdJob* defer = nullptr) {
     if (M <= 0 || N <= 0) return hipSuccess;
     const int k_step = KT ? KT_BK : LA::BK / 16;
     const GemmPlan p = plan_gemm(M, N, kc_total, k_step, 1 << 30, false, ws ? ws_elems : 0, op);
-    return gemm_acc_plan<LA, LB, KT>(p, la, lb, M, N, kc_total, C, amax, ws, st, after_gemm);
+    return gemm_acc_plan<LA, LB, KT>(p, la, lb, M, N, kc_total, C, amax, ws, st, after_gemm, defer);
 }
 
 // Two-phase activation GEMM (forward / input gradient): phase 1 establishes max|acc| (and
@@ -2285,7 +2294,7 @@ hipError_t conv_dgrad_acc(const ConvGeom& g, const int8_t* dy, const int8_t* wt,
 }
 
 hipError_t conv_wgrad_acc(const ConvGeom& g, const int8_t* x, const int8_t* dy, int32_t* acc, uint32_t* amax,
-                          void* ws, size_t ws_bytes, hipStream_t st, hipEvent_t after_gemm) {
+                          void* ws, size_t ws_bytes, hipStream_t st, hipEvent_t after_gemm, SgdJob* defer) {
     WgTaps tg;
     if (wgrad_taps_geom(g, x, dy, &tg)) {
         const int M = g.c_out, N = g.kh * g.kw * g.cip;
@@ -2321,10 +2330,10 @@ hipError_t conv_wgrad_acc(const ConvGeom& g, const int8_t* x, const int8_t* dy, 
         lb.K = lg.K;
         lb.rows_mode = rows_mode;
         return gemm_acc<KtRowsU, KtIm2colU, true>(PLAN_WGRAD, la, lb, g.c_out, lg.ncols, lg.K, acc, amax, (int32_t*)ws,
-                                                  ws_bytes / 4, st, after_gemm);
+                                                  ws_bytes / 4, st, after_gemm, defer);
     }
     return gemm_acc<KtRowsU, PerLane<KtIm2col, true>, true>(PLAN_WGRAD, la, per_lane<KtIm2col, true>(lg), g.c_out, lg.ncols, lg.K,
-                                                            acc, amax, (int32_t*)ws, ws_bytes / 4, st, after_gemm);
+                                                            acc, amax, (int32_t*)ws, ws_bytes / 4, st, after_gemm, defer);
 }
 
 hipError_t matmul_acc(int M, int O, int k16, const int8_t* B, int64_t ldb, const int8_t* A, int64_t lda, int32_t* acc,

@@ -104,9 +104,16 @@ constexpr int SPAN_MAX_BLOCKS = 4096;
 // own dispatch (hipExtLaunchKernel: the kernel's begin and end, as rocprofv3 times it).
 void probe_events_arm(hipEvent_t begin, hipEvent_t end);
 // acc[co][kh][kw][cip] = sum over (n, oy, ox) of dy * x (x, dy NHWC16): the weight gradient,
-// a K-major GEMM over pixels whose operand tiles are transposed in LDS (ds_read_b64_tr_b8)
+// a K-major GEMM over pixels whose operand tiles are transposed in LDS (ds_read_b64_tr_b8).
+// defer (may be null): where the plan splits K into C-shaped slabs (the GEMM path; not the
+// tap-sharing kernel's tile-blocked slabs), leave the slabs in ws unreduced and describe them in
+// *defer (slab, splits, stride, n) for sgd_update_many's combine, which sums them into acc and
+// takes the range -- one launch and an int32 round trip less per layer.  ws must then stay the
+// layer's own until the update; *defer.slab stays null when the launch reduced itself.
+struct SgdJob;
 hipError_t conv_wgrad_acc(const ConvGeom& g, const int8_t* x_nhwc16, const int8_t* dy_nhwc16, int32_t* acc,
-                          uint32_t* amax, void* ws, size_t ws_bytes, hipStream_t st, hipEvent_t after_gemm = nullptr);
+                          uint32_t* amax, void* ws, size_t ws_bytes, hipStream_t st, hipEvent_t after_gemm = nullptr,
+                          SgdJob* defer = nullptr);
 // C[i] = sum over z < splits of slab[z * stride + i] (+ max|C| into amax); n % 4 == 0
 hipError_t splitk_reduce_linear(const int32_t* slab, int splits, int64_t n, int64_t stride, int32_t* C,
                                 uint32_t* amax, hipStream_t st);

@@ -149,6 +149,10 @@ struct Layer {
     // launch (sgd_update_many), and this step's deferred combine (slab == null: none)
     int32_t* slab16 = nullptr;
     size_t slab16_bytes = 0;
+    // the GEMM-path weight gradient's own split-K slabs when its combine is deferred the same way
+    // (grown to the plan's need on the first step that defers, ensure_wslab)
+    int32_t* wslab = nullptr;
+    size_t wslab_bytes = 0;
     SgdJob defer{};
     int8_t* g8 = nullptr;    // int8 weight gradient OHWI16
     int8_t* exp = nullptr;   // exponent of this layer's output
@@ -337,7 +341,7 @@ struct Model {
     bool shared_comm = false;
     std::vector<hipEvent_t> ev_bucket;  // per layer: the bucket closed after this layer's weight gradient
     hipEvent_t ev_grads = nullptr;      // every bucket summed and ranged (the NITI_SGD join)
-    size_t bucket_min_bytes = size_t(8) << 20;
+    size_t bucket_min_bytes = grad_bucket_bytes();
     // the bucket a layer's gradient SUM rides in: layers (backward order) accumulate until the
     // bucket holds bucket_min_bytes; closes_bucket[i] marks the layer whose weight gradient
     // completes one (its first layer in memory order is bucket_lo[i])
@@ -490,6 +494,22 @@ struct Model {
         return true;
     }
     size_t ws_bytes_for(int op) const { return op == PLAN_WGRAD ? slab_w_bytes : slab_bytes; }
+    // layer i's own slab buffer for a deferred GEMM weight-gradient combine, sized to the plan it runs
+    // with (false: its plan does not split K into C-shaped slabs, or no memory)
+    bool ensure_wslab(int i) {
+        Layer& l = L[i];
+        const PlanChoice c = conv_plan_query(PLAN_WGRAD, l.g, false, slab_w_bytes);
+        if (c.strat != 2 || c.splits < 2 || c.bm == PLAN_TAPS_TILE || c.bm == PLAN_P16_TILE) return false;
+        const PlanKey k = conv_plan_key(PLAN_WGRAD, l.g);
+        const size_t need = plan_slab_bytes(k.M, k.N, c.splits);
+        if (l.wslab_bytes >= need) return true;
+        if (hipDeviceSynchronize() != hipSuccess) return false;
+        void* p = ws.alloc(need);
+        if (!p) return false;
+        l.wslab = (int32_t*)p;
+        l.wslab_bytes = need;
+        return true;
+    }
     int ensure_streams() {
         if (side) return NITI_NO_ERROR;
         if (hipStreamCreateWithFlags(&side, hipStreamNonBlocking) != hipSuccess) return NITI_NO_EXECUTION;
@@ -953,15 +973,19 @@ int Model::wgrad_layer(int i, hipStream_t st) {
                             defer ? l.slab16_bytes : slab_w_bytes, s, st, eb, ee, sp, defer ? &l.defer : nullptr));
         return NITI_NO_ERROR;
     }
-    // the weight-gradient probe brackets the GEMM launch alone (not its split-K reduce)
     // the weight-gradient probe is the GEMM launch's own begin / end (its split-K reduce excluded)
     if (capturing)
         probe(i, 2, true, st);
     else
         arm_kernel_events(i, 2);
     arm_span(i, 2);
-    MTRY(conv_wgrad_acc(g, l.in, l.dy, l.dwacc, dp ? nullptr : rng(i, 2), slab_w, slab_w_bytes, st,
-                        capturing ? probe_end_event(i, 2) : nullptr));
+    // single device: a split-K plan leaves its slabs (this layer's own) to the NITI_SGD launch's
+    // combine, which sums them and takes the range (no reduce launch, no int32 round trip)
+    const bool defer = defer_combine() && ensure_wslab(i);
+    l.defer = SgdJob{};
+    MTRY(conv_wgrad_acc(g, l.in, l.dy, l.dwacc, dp ? nullptr : rng(i, 2), defer ? l.wslab : slab_w,
+                        defer ? l.wslab_bytes : slab_w_bytes, st, capturing ? probe_end_event(i, 2) : nullptr,
+                        defer ? &l.defer : nullptr));
     return NITI_NO_ERROR;
 }
 

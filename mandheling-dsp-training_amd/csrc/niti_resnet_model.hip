@@ -403,9 +403,30 @@ int ResNetModel::dgrad_conv(int i, hipStream_t st) {
 int ResNetModel::wgrad_conv(int i, hipStream_t st) {
     RConv& c = C[i];
     probe(i, 2, true, st);
-    RTRY(conv_wgrad_acc(c.g, c.in, c.dy, c.dwacc, dp() ? nullptr : rng(i, 2), slab_w, slab_w_bytes, st));
+    // single device, in the step: a split-K plan leaves its (own) slabs to the update's combine
+    const bool defer = in_step && !dp() && !capturing && !tuning && ensure_wslab(i);
+    c.defer = SgdJob{};
+    RTRY(conv_wgrad_acc(c.g, c.in, c.dy, c.dwacc, dp() ? nullptr : rng(i, 2), defer ? c.wslab : slab_w,
+                        defer ? c.wslab_bytes : slab_w_bytes, st, nullptr, defer ? &c.defer : nullptr));
     probe(i, 2, false, st);
     return NITI_NO_ERROR;
+}
+
+// conv i's own slab buffer for a deferred weight-gradient combine, sized to the plan it runs with
+// (false: the plan does not split K into C-shaped slabs, or no memory)
+bool ResNetModel::ensure_wslab(int i) {
+    RConv& c = C[i];
+    const PlanChoice p = conv_plan_query(PLAN_WGRAD, c.g, false, slab_w_bytes);
+    if (p.strat != 2 || p.splits < 2 || p.bm == PLAN_TAPS_TILE || p.bm == PLAN_P16_TILE) return false;
+    const PlanKey k = conv_plan_key(PLAN_WGRAD, c.g);
+    const size_t need = plan_slab_bytes(k.M, k.N, p.splits);
+    if (c.wslab_bytes >= need) return true;
+    if (hipDeviceSynchronize() != hipSuccess) return false;
+    void* q = ws.alloc(need);
+    if (!q) return false;
+    c.wslab = (int32_t*)q;
+    c.wslab_bytes = need;
+    return true;
 }
 
 // Block k's output: relu(requant(aligned y_b + shortcut)) -- range pass (the sum not stored),
@@ -497,6 +518,12 @@ int ResNetModel::run(const int8_t* x_nchw, int exp_in, const uint8_t* images, co
         const int rc = ensure_comm_stream();
         if (rc != NITI_NO_ERROR) return rc;
     }
+    struct InStep {  // weight gradients inside this step may defer their combine
+        bool& f;
+        explicit InStep(bool& x) : f(x) { f = true; }
+        ~InStep() { f = false; }
+    } in_step_guard(in_step);
+    for (RConv& c : C) c.defer = SgdJob{};
     RTRY(hipMemsetAsync(amax, 0, amax_bytes, st));
     // input: NITIInt8Train's quantiser (MnistUtils.cpp:83-93) on uint8 images, or int8 x as given
     const int64_t px = (int64_t)n * 3 * in_hw * in_hw;
@@ -585,6 +612,12 @@ int ResNetModel::run(const int8_t* x_nchw, int exp_in, const uint8_t* images, co
                          i > 0 && !rows_dg_on(i) ? c.wT : nullptr, keep_grads ? c.g8 : nullptr};
         jobs[i].wf = c.rows ? c.wf : nullptr;
         jobs[i].wft = c.rows_dg ? c.wft : nullptr;
+        if (c.defer.slab != nullptr) {  // this conv's split-K slabs, combined in the update launch
+            jobs[i].slab = c.defer.slab;
+            jobs[i].splits = c.defer.splits;
+            jobs[i].slab_stride = c.defer.slab_stride;
+            jobs[i].slab_n = c.defer.slab_n;
+        }
     }
     RTRY(sgd_update_many(jobs, nl, st));
     return NITI_NO_ERROR;

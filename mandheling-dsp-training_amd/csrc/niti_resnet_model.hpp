@@ -48,6 +48,10 @@ struct RConv {
     int8_t* dx_exp = nullptr;
     const int8_t* dx_mask = nullptr; // the previous op's relu gradient fused into the input gradient
     int32_t* dwacc = nullptr;        // int32 weight gradient (in the contiguous gradient bucket)
+    // single device: a split-K weight gradient's own slabs, combined by the NITI_SGD launch
+    int32_t* wslab = nullptr;
+    size_t wslab_bytes = 0;
+    SgdJob defer{};
     int64_t w_elems() const { return (int64_t)g.c_out * g.kh * g.kw * g.cip; }
     int64_t macs() const { return (int64_t)og.n * og.oh * og.ow * og.c_out * og.c_in * og.kh * og.kw; }
 };
@@ -121,7 +125,7 @@ struct ResNetModel {
     hipEvent_t ev_grads = nullptr;
     std::vector<int> bucket_lo;
     std::vector<char> closes_bucket;
-    size_t bucket_min_bytes = size_t(8) << 20;
+    size_t bucket_min_bytes = grad_bucket_bytes();
     // kernel probe: HIP events on the step stream around one conv phase (both launches of a
     // two-launch form), up to ev0.size() launches
     int probe_layer = -1, probe_phase = -1, probe_count = 0;
@@ -141,6 +145,8 @@ struct ResNetModel {
     int fwd_conv(int i, hipStream_t st);
     int dgrad_conv(int i, hipStream_t st);
     int wgrad_conv(int i, hipStream_t st);
+    bool in_step = false;  // run(): weight gradients may leave their split-K combine to the update
+    bool ensure_wslab(int i);
     int residual_fwd(int k, hipStream_t st);
     int residual_bwd(int k, hipStream_t st);
     int run(const int8_t* x_nchw, int exp_in, const uint8_t* images, const int32_t* labels, hipStream_t st);

@@ -197,6 +197,7 @@ struct RowConvArgs {
     // REQUANT as a speculative pair (spec_hint, below): 1 = launch A, requantise with the hinted bit
     // width and publish the max; 2 = launch B, redo only if the (all-reduced) max's bit width differs
     int spec2;
+    uint32_t spec_cooldown;      // spec2: pairs in store mode after a change (spec_cooldown())
     uint32_t* hint;              // spec2: the slot (spec_hint); its word 0 the hint, 1 the guess A used, 2 misses
     // W = 1 (1x1 maps, the classifier head): x is row-major [n][xld], the weights row-major
     // [rows][wld] (OHWI16 forward, IHWO16 input gradient), K the reduced channels
@@ -1031,7 +1032,7 @@ __device__ __forceinline__ void write_exponent(const RowConvArgs& a, uint32_t gm
 // used, bit 31 set when it stored instead; written by A's block 0, read by B), [2] redone launches,
 // [3] pairs left in store mode (read and written by B's thread 0, read by A), [4] stored pairs.
 // Every other reader of a word runs in the other launch, so no launch's blocks race on a word.
-constexpr uint32_t SPEC_COOLDOWN = 4;
+constexpr uint32_t SPEC_COOLDOWN = 4;  // the default of spec_cooldown() (NITI_SPEC_COOLDOWN overrides)
 __device__ __forceinline__ int spec_guess(const RowConvArgs& a, bool can_store, bool& store) {
     const uint32_t h = __hip_atomic_load(a.hint, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint32_t f = __hip_atomic_load(a.hint + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1058,7 +1059,7 @@ __device__ __forceinline__ bool spec_settle(const RowConvArgs& a, uint32_t& g, b
         // from step to step, gradients near a power of two, stays there; block 0 of B is the only
         // reader-writer of this word within a launch)
         const uint32_t cd = __hip_atomic_load(a.hint + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(a.hint + 3, changed ? SPEC_COOLDOWN : (cd > 0u ? cd - 1u : 0u), __ATOMIC_RELAXED,
+        __hip_atomic_store(a.hint + 3, changed ? a.spec_cooldown : (cd > 0u ? cd - 1u : 0u), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
         if (stored) __hip_atomic_fetch_add(a.hint + 4, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         else if (changed) __hip_atomic_fetch_add(a.hint + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1789,6 +1790,13 @@ void rowconv_barrier_diag(uint32_t spin_limit, uint32_t expect_extra) {
 }
 void rowconv_speculate(int mode) { g_rc_spec = mode; }
 uint32_t* rowconv_spec_slot(uint32_t* bar, bool dg) { return bar + (16 + (dg ? 1 : 0)) * BAR_LINE; }
+// pairs a layer stays in store mode after its bit width changed (A/B knob NITI_SPEC_COOLDOWN; 0 never
+// stores: a miss then redoes the GEMM instead of reading back stored accumulators)
+static uint32_t spec_cooldown() {
+    static const int v = getenv("NITI_SPEC_COOLDOWN") ? atoi(getenv("NITI_SPEC_COOLDOWN")) : (int)SPEC_COOLDOWN;
+    return v < 0 ? 0u : (uint32_t)v;
+}
+
 bool rowconv_spec2_on() {
     static const char* env = getenv("NITI_RC_SPEC2");
     return env == nullptr || env[0] != '0';
@@ -1897,6 +1905,7 @@ hipError_t rowconv_fwd(const ConvGeom& g, const int8_t* x_c32, const int8_t* wf,
     a.p16_pixels = (int64_t)g.n * g.h * g.w * (o.pool_dx != nullptr ? 4 : 1);
     a.acc_store = mode == RC_FUSED ? nullptr : o.acc_store;
     a.spec2 = spec2;
+    a.spec_cooldown = spec_cooldown();
     // the hint slot (the speculative pair's, and the fused mode's speculative epilogue): forward or
     // input gradient, by the operands or the caller's dgrad_slot, so the two directions never share it
     a.hint = (spec || mode == RC_FUSED) && bar != nullptr ? bar + (16 + (dg || o.dgrad_slot ? 1 : 0)) * BAR_LINE : nullptr;
@@ -2058,6 +2067,7 @@ hipError_t rowconv_fc(int n, int K, int rows, const int8_t* x, int xld, const in
     a.p16_pixels = (int64_t)n * (o.pool_dx != nullptr ? 4 : 1);
     const bool dg = o.relu_mask != nullptr || o.pool_dx != nullptr || o.p16 != nullptr;
     a.spec2 = spec2;
+    a.spec_cooldown = spec_cooldown();
     // the hint slot (the speculative pair's, and the fused mode's speculative epilogue): forward or
     // input gradient, by the operands or the caller's dgrad_slot, so the two directions never share it
     a.hint = (spec || mode == RC_FUSED) && bar != nullptr ? bar + (16 + (dg || o.dgrad_slot ? 1 : 0)) * BAR_LINE : nullptr;

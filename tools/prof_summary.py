@@ -1,47 +1,66 @@
-"""Summarise a rocprofv3 --kernel-trace CSV: per-kernel totals per step and the last step's launches."""
+"""Summarise a rocprofv3 --kernel-trace CSV of a bench run: per-kernel time per training step over the
+last timed steps (each step from its input quantiser's first launch to its NITI_SGD update launch),
+then the last step's launches as a timeline.  Launches outside those steps (autotuning, warmup, the
+isolated probe re-runs after the timed region) are not counted.
+
+usage: prof_summary.py kernel_trace.csv [steps]   (steps: how many of the last steps to average)
+"""
 import collections
 import csv
 import sys
 
 path = sys.argv[1]
-steps = int(sys.argv[2]) if len(sys.argv) > 2 else 13
+want = int(sys.argv[2]) if len(sys.argv) > 2 else 5
 rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
 dur = lambda r: (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3  # noqa: E731
 
 
 def short(n):
-    n = n.split("(")[0].replace("void niti::", "").replace("niti::", "")
-    return n.replace("gemm_i8_kernel", "gemm").replace("Load", "")[:70]
+    n = n.replace("(anonymous namespace)::", "").split("(")[0].replace("void niti::", "").replace("niti::", "")
+    return n.replace("gemm_i8_kernel", "gemm").replace("Load", "")[:80]
 
 
+def is_start(r):  # a step's first kernel: the input statistics or the int8 input's relayout / im2col
+    k = r["Kernel_Name"]
+    return "image_stats" in k or "NchwToNhwc16" in k or "input_im2col" in k
+
+
+# steps: [start index, index of the sgd_update launch]; the stats launch may be preceded by a memset
+ends = [i for i, r in enumerate(rows) if "sgd_update_kernel" in r["Kernel_Name"]]
+steps = []
+prev = -1
+for e in ends:
+    s = min((i for i in range(prev + 1, e) if is_start(rows[i])), default=None)
+    prev = e
+    if s is None:
+        continue
+    steps.append((s, e))
+steps = steps[-want:]
+if not steps:
+    sys.exit("no complete step in the trace")
 tot = collections.defaultdict(float)
 cnt = collections.Counter()
-for r in rows:
-    tot[short(r["Kernel_Name"])] += dur(r)
-    cnt[short(r["Kernel_Name"])] += 1
+for s, e in steps:
+    for r in rows[s:e + 1]:
+        tot[short(r["Kernel_Name"])] += dur(r)
+        cnt[short(r["Kernel_Name"])] += 1
+n = len(steps)
+print(f"per-kernel time per step, averaged over the last {n} steps")
 print(f"{'us/step':>9} {'calls/step':>10}  kernel")
 for k, v in sorted(tot.items(), key=lambda x: -x[1]):
-    print(f"{v / steps:9.1f} {cnt[k] / steps:10.1f}  {k}")
-print("total busy us/step", sum(tot.values()) / steps)
-# last step: from the last loss_grad to the end
-def is_start(r):  # a step's first kernel: the input quantiser or the int8 input's relayout
-    return "image_stats" in r["Kernel_Name"] or "NchwToNhwc16" in r["Kernel_Name"]
-
-
-idx = max(i for i, r in enumerate(rows) if "loss_grad" in r["Kernel_Name"])
-first = max(i for i, r in enumerate(rows[:idx]) if is_start(r))
-print("\nlast step launches (from the forward of the step):")
-seg = rows[first:]
-span = (int(seg[-1]["End_Timestamp"]) - int(seg[0]["Start_Timestamp"])) / 1e3
+    print(f"{v / n:9.1f} {cnt[k] / n:10.1f}  {k}")
+busy = sum(tot.values()) / n
+span = sum((int(rows[e]["End_Timestamp"]) - int(rows[s]["Start_Timestamp"])) / 1e3 for s, e in steps) / n
+print(f"busy us/step {busy:.1f}   first launch -> update end us/step {span:.1f}   launches/step "
+      f"{sum(cnt.values()) / n:.1f}")
+s, e = steps[-1]
+seg = rows[s:e + 1]
 t0 = int(seg[0]["Start_Timestamp"])
-qcol = "Queue_Id" if "Queue_Id" in seg[0] else ("Stream_Id" if "Stream_Id" in seg[0] else None)
-last_end = {}
-print(f"{'start':>8} {'dur':>7} {'gap':>6}  q  grid        kernel")
+print("\nlast step's launches:")
+print(f"{'start':>8} {'dur':>7} {'gap':>6}  grid        kernel")
+prev_end = t0
 for r in seg:
-    g = f"{int(r['Grid_Size_X']) // int(r['Workgroup_Size_X'])}x{r['Grid_Size_Y']}"
-    q = r[qcol] if qcol else "-"
-    s0, e0 = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
-    gap = (s0 - last_end[q]) / 1e3 if q in last_end else 0.0
-    last_end[q] = e0
-    print(f"{(s0 - t0) / 1e3:8.2f} {dur(r):7.2f} {gap:6.2f} {q:>2}  {g:>10}  {short(r['Kernel_Name'])}")
-print("step span us", span, "busy", sum(dur(r) for r in seg), "launches", len(seg))
+    st = int(r["Start_Timestamp"])
+    grid = f"{r.get('Grid_Size_X', r.get('Grid_Size', '?'))}"
+    print(f"{(st - t0) / 1e3:8.2f} {dur(r):7.2f} {max(0, st - prev_end) / 1e3:6.2f}  {grid:<10}  {short(r['Kernel_Name'])}")
+    prev_end = max(prev_end, int(r["End_Timestamp"]))
