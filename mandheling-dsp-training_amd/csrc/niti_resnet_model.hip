@@ -51,7 +51,8 @@ int ResNetModel::build(int batch_, int in_hw_, int classes_) {
     batch = batch_;
     in_hw = in_hw_ > 0 ? in_hw_ : 224;
     classes = classes_ > 0 ? classes_ : 1000;
-    if (in_hw % 32 != 0 || classes > 2048) return NITI_INVALID_VALUE;
+    // every stage halves the map (stride-2 convs and the 1x1 projections agree on odd sizes too)
+    if (in_hw % 16 != 0 || classes > 2048) return NITI_INVALID_VALUE;
     const int n = batch;
     // the 21 parameter layers in parameter order (oracle/niti_resnet_ref.py resnet18_convs)
     auto add = [&](int ci, int co, int k, int s, int p, int h, int relu) {

@@ -59,8 +59,8 @@ class ResNet18:
 
     def __init__(self, batch: int, in_hw: int = 224, classes: int = 1000, device="cuda", comm=None):
         """batch: images per rank; comm: data-parallel collectives (niti_amd.dp), None for one device."""
-        if in_hw % 32 or in_hw < 32:
-            raise ValueError("in_hw must be a multiple of 32")
+        if in_hw % 16 or in_hw < 32:
+            raise ValueError("in_hw must be a multiple of 16, at least 32")
         self.batch, self.in_hw, self.classes, self.dev = batch, in_hw, classes, device
         self.comm = comm
         self.convs = resnet18_convs(in_hw, classes)
