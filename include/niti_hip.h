@@ -482,7 +482,9 @@ int niti_model_set_overlap(niti_model_t m, int enable);
  * buffers); weights are not touched.  reps <= 0 uses 5.  Synchronises `stream`. */
 int niti_model_autotune(niti_model_t m, int reps, void* stream);
 /* The plan a layer phase (0 forward, 1 input gradient, 2 weight gradient) runs with:
- * {bm, bn, splits, strategy 0 store / 1 recompute / 2 split-K}. */
+ * {bm, bn, splits, strategy 0 store / 1 recompute / 2 split-K / 3 the speculative pair (forward and
+ * input gradient, unsplit: launch A requantises with the layer's previous bit width and publishes the
+ * range, launch B redoes the GEMM only when the range's bit width differs)}. */
 int niti_model_plan_info(niti_model_t m, int layer, int phase, int info[4]);
 /* Force a plan for a layer phase ({bm 64|128, bn 64|128, splits >= 1, strategy}; split counts
  * beyond the K steps or the workspace are clamped; recompute on the weight gradient means
