@@ -1821,7 +1821,7 @@ int niti_model_plan_set(niti_model_t m, int layer, int phase, const int plan[4])
         auto tile_ok = [](int t) { return t == 64 || t == 128 || t == 256; };
         const bool taps = plan[0] == niti::PLAN_TAPS_TILE && plan[1] == niti::PLAN_TAPS_TILE && op == niti::PLAN_WGRAD &&
                           niti::conv_wgrad_taps_ok(g);
-        if ((!taps && (!tile_ok(plan[0]) || !tile_ok(plan[1]))) || plan[2] < 1 || plan[2] > 64 || plan[3] < 0 ||
+        if ((!taps && (!tile_ok(plan[0]) || !tile_ok(plan[1]))) || plan[2] < 1 || plan[2] > 4096 || plan[3] < 0 ||
             plan[3] > 3 || (taps && plan[3] == 1) || (plan[3] == 3 && (op == niti::PLAN_WGRAD || plan[2] != 1)))
             return NITI_INVALID_VALUE;
         niti::PlanChoice c;
