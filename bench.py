@@ -342,10 +342,12 @@ def main():
     # a fused row-kernel launch whose grid barrier timed out computed garbage: no number from it
     if model.rowconv_error() != 0:
         raise RuntimeError("a fused row-kernel grid barrier timed out in the timed region: results invalid")
-    # the speculative row-kernel pairs (two-launch form): launches redone / pairs in store mode per
-    # layer over warmup + timed steps (per layer: fwd redone, fwd stored, dgrad redone, dgrad stored)
+    # the speculative pairs (the row kernels' two-launch form and the GEMM path's plan strategy 3):
+    # launches B redid, and pairs the row kernels ran in store mode or the GEMM pair settled from an
+    # alternate, per layer over warmup + timed steps (fwd redone, fwd stored/alt, dgrad redone, dgrad
+    # stored/alt)
     spec = [(s[1], s[2], s[4], s[5]) for s in model.spec_stats()]
-    spec = {"redone": sum(a + c for a, _, c, _ in spec), "stored": sum(b + d for _, b, _, d in spec),
+    spec = {"redone": sum(a + c for a, _, c, _ in spec), "stored_or_alternate": sum(b + d for _, b, _, d in spec),
             "per_layer": [list(v) for v in spec if any(v)]}
     probe_ms, probe_n = model.probe_read()
     span_ms, span_n = model.probe_read_span()

@@ -319,6 +319,10 @@ void niti_diag_rowconv_barrier(uint32_t spin_limit, uint32_t expect_extra);
  * measured slower), 2 always guess wrong (every launch redoes its epilogue).  Results are identical
  * in every mode. */
 void niti_diag_rowconv_speculate(int mode);
+/* diagnostics: launch A of every GEMM speculative pair (plan strategy 3) guesses the layer's previous
+ * bit width + bias: +-1 makes launch B settle from an alternate, 2 makes it redo the GEMM (tests);
+ * 0 (default) off.  Results are the rule's whatever the bias. */
+void niti_diag_gemm_speculate(int bias);
 /* jobs per P16 input-copy launch of a model step for later steps (<= 0: the default 16); a small
  * cap sends a step down its more-than-one-launch branches.  Results are identical for every cap. */
 void niti_diag_p16_jobs_cap(int cap);

@@ -212,27 +212,35 @@ struct Epi {
     // A used (written by A), [2] launches B redid.
     int spec = 0;
     uint32_t* hint = nullptr;
+    // launch A also writes the output requantised one bit width below and above its guess into
+    // alt[0 .. M*ldo) / alt[M*ldo .. 2*M*ldo) (may be null): launch B then settles a +-1 change --
+    // the common miss, a max near a power of two -- by copying instead of redoing the GEMM
+    int8_t* alt = nullptr;
+    int spec_bias = 0;  // diagnostics (niti_diag_gemm_speculate): launch A guesses hint + bias
 };
 
-// launch B of the pair: the rule's bit width of the (all-reduced) max against the guess A used;
-// block 0 writes the exponent and the next hint.  Returns true when A's output stands (every block
-// of B then exits).  Called by whole waves (read_max: one slot per lane).
-__device__ __forceinline__ bool gemm_spec_hit(const Epi& epi) {
+// launch B of the pair: the rule's bit width of the (all-reduced) max against the one A used
+// (hint[1] = bw + 1); block 0 writes the exponent and the next hint.  Returns 0 when A's output
+// stands (every block of B then exits), 1 / 2 when A's alternate one bit width below / above holds
+// it (B copies it over the output), -1 when the GEMM must be redone.  Called by whole waves
+// (read_max: one slot per lane).
+__device__ __forceinline__ int gemm_spec_settle(const Epi& epi) {
     const uint32_t g = read_max(epi.amax);
     const int bw = bitwidth_of(g);
     const int used = __builtin_amdgcn_readfirstlane(
                          (int)__hip_atomic_load(epi.hint + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) - 1;
-    const bool hit = bw == used;
+    const int act = bw == used ? 0 : epi.alt == nullptr ? -1 : (bw == used - 1 && used >= 1) ? 1 : bw == used + 1 ? 2 : -1;
     if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
-        if (hit && epi.exp_out != nullptr) {  // (a miss writes it in the redone epilogue)
+        if (act >= 0 && epi.exp_out != nullptr) {  // (a redo writes it in its epilogue)
             const int shift = bw - 7;
             const int inc = shift > 1 ? shift : (shift == 1 ? 2 : 0);
             *epi.exp_out = (int8_t)((epi.exp_in ? (int)*epi.exp_in : 0) + (epi.wscale ? (int)*epi.wscale : 0) + inc);
         }
         __hip_atomic_store(epi.hint, (uint32_t)bw + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (!hit) __hip_atomic_fetch_add(epi.hint + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (act < 0) __hip_atomic_fetch_add(epi.hint + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (act > 0) __hip_atomic_fetch_add(epi.hint + 3, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    return hit;
+    return act;
 }
 
 
@@ -257,14 +265,17 @@ __device__ __forceinline__ void gemm_epilogue(v16i (&acc)[TM][TN], int r0, int c
     bool rq_raw = false;
     // launch A of the speculative pair: requantise with the hinted bit width, publish the max
     const bool spec_a = MODE == EPI_REQUANT && epi.spec == 1;
+    int abw = 0;  // the bit width launch A requantises with
     if (MODE == EPI_REQUANT) {
         int bw;
         if (spec_a) {
             const uint32_t h = __hip_atomic_load(epi.hint, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            bw = __builtin_amdgcn_readfirstlane((int)h) - 1;  // -1: no hint yet (B redoes the launch)
+            bw = __builtin_amdgcn_readfirstlane((int)h) - 1;  // no hint yet: 0 (B redoes unless the max is 0)
+            if (h != 0u) bw += epi.spec_bias;
             if (bw < 0) bw = 0;
+            abw = bw;
             if (blockIdx.x == 0 && blockIdx.y == 0 && tid == 0)
-                __hip_atomic_store(epi.hint + 1, h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(epi.hint + 1, (uint32_t)bw + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else {
             bw = bitwidth_of(read_max(epi.amax));
         }
@@ -322,6 +333,46 @@ __device__ __forceinline__ void gemm_epilogue(v16i (&acc)[TM][TN], int r0, int c
                     for (int j = 0; j < 16; ++j) q[j] = mk[j] > 0 ? q[j] : (signed char)0;
                 }
                 *(v16c*)(epi.out + o) = q;
+            }
+        }
+        if (spec_a && epi.alt != nullptr) {
+            // the alternates: the same tile requantised one bit width below / above the guess
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const int sh = (k == 0 ? (abw > 0 ? abw - 1 : 0) : abw + 1) - 7;
+                const int s2 = sh > 1 ? sh : 2;
+                const bool raw = sh <= 0;
+                __syncthreads();  // the previous round's LDS reads are done
+#pragma unroll
+                for (int a = 0; a < TM; ++a)
+#pragma unroll
+                    for (int b = 0; b < TN; ++b) {
+                        const int col = c0 + b * 32 + (lane & 31);
+#pragma unroll
+                        for (int i = 0; i < 16; ++i) {
+                            const int row = r0 + a * 32 + (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
+                            const int v = acc[a][b][i];
+                            int32_t q = raw ? (int32_t)(int8_t)v : psto_any(v, s2);
+                            if (epi.relu && q < 0) q = 0;
+                            smem[(row - m0) * (BN + 16) + (col - n0)] = (int8_t)q;
+                        }
+                    }
+                __syncthreads();
+                int8_t* dst = epi.alt + (int64_t)k * M * epi.ldo;
+                for (int t = tid; t < BM * CPR; t += NW * 64) {
+                    const int rl = t / CPR, cl = (t - rl * CPR) * 16;
+                    const int row = m0 + rl, col = n0 + cl;
+                    if (row < M && col < N) {
+                        v16c q = *(const v16c*)(smem + rl * (BN + 16) + cl);
+                        const int64_t o = (int64_t)row * epi.ldo + col;
+                        if (epi.relu_mask != nullptr) {
+                            const v16c mk = *(const v16c*)(epi.relu_mask + o);
+#pragma unroll
+                            for (int j = 0; j < 16; ++j) q[j] = mk[j] > 0 ? q[j] : (signed char)0;
+                        }
+                        *(v16c*)(dst + o) = q;
+                    }
+                }
             }
         }
     }
@@ -746,7 +797,19 @@ __global__ void __launch_bounds__(NW * 64) gemm_kernel(LA la, LB lb, int M, int 
     __shared__ __attribute__((aligned(16))) int8_t smem[SMEM];
 
     if constexpr (MODE == EPI_REQUANT) {
-        if (epi.spec == 2 && gemm_spec_hit(epi)) return;  // launch B of the pair: A's output stands
+        if (epi.spec == 2) {  // launch B of the pair
+            const int act = gemm_spec_settle(epi);
+            if (act == 0) return;  // A's output stands
+            if (act > 0) {         // one bit width off: A's alternate is the output
+                const int64_t n16 = (int64_t)M * epi.ldo / 16;
+                const v16c* src = (const v16c*)(epi.alt + (int64_t)(act - 1) * M * epi.ldo);
+                const int64_t nb = (int64_t)gridDim.x * gridDim.y;
+                for (int64_t i = ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * blockDim.x + threadIdx.x; i < n16;
+                     i += nb * blockDim.x)
+                    ((v16c*)epi.out)[i] = src[i];
+                return;
+            }
+        }
     }
     const unsigned long long span_t0 = span_begin(epi.span);
     const int tid = threadIdx.x;
@@ -1835,10 +1898,15 @@ static hipError_t act_phase2(int op, const LA& la, const LB& lb, int M, int N, i
     return requant_act(r, st);
 }
 
+// diagnostics: launch A of every GEMM pair guesses the hint + this bias (tests: +-1 exercises the
+// alternates, 2 the redone launch)
+static int g_gemm_spec_bias = 0;
+void gemm_speculate_bias(int bias) { g_gemm_spec_bias = bias; }
+
 // The speculative pair (STRAT_SPEC): pass 0 = launch A, pass 1 = launch B (see Epi::spec)
 template <class LA, class LB>
 static hipError_t act_spec(int op, const LA& la, const LB& lb, int M, int N, int kc_total, uint32_t* amax,
-                           const ActOut& o, uint32_t* hint, int pass, hipStream_t st) {
+                           const ActOut& o, uint32_t* hint, int pass, int8_t* alt, hipStream_t st) {
     if (M <= 0 || N <= 0) return hipSuccess;
     if (o.pool.pool_out != nullptr || o.pool.dx != nullptr || o.out_p16 != nullptr || hint == nullptr || o.out == nullptr)
         return hipErrorInvalidValue;
@@ -1854,6 +1922,8 @@ static hipError_t act_spec(int op, const LA& la, const LB& lb, int M, int N, int
     e.exp_out = o.exp_out;
     e.spec = pass == 0 ? 1 : 2;
     e.hint = hint;
+    e.alt = alt;
+    e.spec_bias = g_gemm_spec_bias;
     return launch_mode<LA, LB, EPI_REQUANT, false>(p, la, lb, M, N, kc_total, e, st);
 }
 
@@ -1960,14 +2030,25 @@ static int dgrad_taps_bk(const ConvGeom& g) {
     if (g.kh * g.kw > 32 || g.sh != 1 || g.sw != 1) return 0;
     return g.cop % 64 == 0 ? 64 : 0;
 }
+// a 1x1, stride-1, unpadded conv is a plain GEMM over the activation rows: x [pixels][cip] (forward),
+// dy [pixels][cop] (input gradient) and, K-major, x again (weight gradient) -- the row-major
+// loaders with no per-lane address arithmetic (ResNet-18's stem over its 160-column im2col, the fc
+// heads); a per-lane conv loader gathered those rows at ~2 TB/s
+static bool plain_1x1(const ConvGeom& g) {
+    return g.kh == 1 && g.kw == 1 && g.sh == 1 && g.sw == 1 && g.dh == 1 && g.dw == 1 && g.pt == 0 && g.pl == 0 &&
+           g.pb == 0 && g.pr == 0 && g.oh == g.h && g.ow == g.w &&
+           (int64_t)g.n * g.h * g.w * (g.cip > g.cop ? g.cip : g.cop) < ((int64_t)1 << 31);
+}
 template <class F>
 static hipError_t with_fwd_operand(const ConvGeom& g, const int8_t* x, F&& f) {
+    if (plain_1x1(g)) return f(rows_k(x, g.cip, g.n * g.h * g.w, g.cip / 16));
     const int bk = fwd_taps_bk(g);
     if (bk == 64) return f(conv_taps<64>(g, x, true));
     return f(per_lane<LoadConvFwd, false>(fwd_loader(g, x)));
 }
 template <class F>
 static hipError_t with_dgrad_operand(const ConvGeom& g, const int8_t* dy, F&& f) {
+    if (plain_1x1(g)) return f(rows_k(dy, g.cop, g.n * g.h * g.w, g.cop / 16));
     const int bk = dgrad_taps_bk(g);
     if (bk == 64) return f(conv_taps<64>(g, dy, false));
     return f(per_lane<LoadConvDgrad, false>(dgrad_loader(g, dy)));
@@ -2308,6 +2389,16 @@ hipError_t conv_wgrad_acc(const ConvGeom& g, const int8_t* x, const int8_t* dy, 
     KtRowsU la;
     KtIm2col lg;
     wgrad_operands(g, x, dy, &la, &lg);
+    if (plain_1x1(g)) {  // the im2col is x itself: K-major rows of [pixels][cip]
+        KtRowsU lx;
+        lx.p = x;
+        lx.ld = g.cip;
+        lx.cols = g.cip;
+        lx.K = lg.K;
+        lx.bytes = lg.bytes;
+        return gemm_acc<KtRowsU, KtRowsU, true>(PLAN_WGRAD, la, lx, g.c_out, lg.ncols, lg.K, acc, amax, (int32_t*)ws,
+                                                ws_bytes / 4, st, after_gemm, defer);
+    }
     const int ohw = g.oh * g.ow;
     const bool rows_mode = ohw % KT_BK == 0 && KT_BK % g.ow == 0;
     if (rows_mode || KT_BK % ohw == 0) {
@@ -2361,21 +2452,23 @@ hipError_t conv_fwd_phase2(const ConvGeom& g, const int8_t* x, const int8_t* w, 
     });
 }
 hipError_t conv_fwd_spec(const ConvGeom& g, const int8_t* x, const int8_t* w, uint32_t* amax, const ActOut& o,
-                         uint32_t* slot, int pass, hipStream_t st) {
+                         uint32_t* slot, int pass, hipStream_t st, int8_t* alt) {
     const int kc_total = g.kh * g.kw * g.cip / 16;
     const RowsK lb = rows_k(w, (int64_t)g.kh * g.kw * g.cip, g.c_out, kc_total);
     return with_fwd_operand(g, x, [&](const auto& la) {
-        return act_spec(PLAN_FWD, la, lb, g.n * g.oh * g.ow, g.cop, kc_total, amax, o, slot, pass, st);
+        return act_spec(PLAN_FWD, la, lb, g.n * g.oh * g.ow, g.cop, kc_total, amax, o, slot, pass, alt, st);
     });
 }
 hipError_t conv_dgrad_spec(const ConvGeom& g, const int8_t* dy, const int8_t* wt, uint32_t* amax, const ActOut& o,
-                           uint32_t* slot, int pass, hipStream_t st) {
+                           uint32_t* slot, int pass, hipStream_t st, int8_t* alt) {
     const int kc_total = g.kh * g.kw * g.cop / 16;
     const RowsK lb = rows_k(wt, (int64_t)g.kh * g.kw * g.cop, g.c_in, kc_total);
     return with_dgrad_operand(g, dy, [&](const auto& la) {
-        return act_spec(PLAN_DGRAD, la, lb, g.n * g.h * g.w, g.cip, kc_total, amax, o, slot, pass, st);
+        return act_spec(PLAN_DGRAD, la, lb, g.n * g.h * g.w, g.cip, kc_total, amax, o, slot, pass, alt, st);
     });
 }
+size_t conv_fwd_spec_alt_bytes(const ConvGeom& g) { return (size_t)2 * g.n * g.oh * g.ow * g.cop; }
+size_t conv_dgrad_spec_alt_bytes(const ConvGeom& g) { return (size_t)2 * g.n * g.h * g.w * g.cip; }
 hipError_t conv_dgrad_phase1(const ConvGeom& g, const int8_t* dy, const int8_t* wt, int32_t* acc, uint32_t* amax,
                              void* ws, size_t ws_bytes, hipStream_t st) {
     const int kc_total = g.kh * g.kw * g.cop / 16;

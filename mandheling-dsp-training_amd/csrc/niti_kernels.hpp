@@ -209,15 +209,21 @@ bool conv_dgrad_phase2_separate(const ConvGeom& g, size_t ws_bytes);
 // amax (zeroed by the caller); pass 1 (launch B, after any MAX all-reduce of amax) writes the
 // exponent and redoes the GEMM, requantised with the max, only when its bit width differs -- on a
 // hit every block of B exits at once: one GEMM pass and no int32 tensor.  slot: the layer phase's
-// own GEMM_SPEC_SLOT_WORDS zeroed device words ([0] hint, [1] the guess A used, [2] launches B
-// redid).  ActOut without pool / P16 fusion.  Results equal phase 1 + phase 2's.
+// own GEMM_SPEC_SLOT_WORDS zeroed device words ([0] hint, [1] the bit width A used, [2] launches B
+// redid, [3] misses B settled from an alternate).  alt (may be null; the same scratch for both
+// passes, *_alt_bytes): launch A also writes the output requantised one bit width below and above
+// its guess, and launch B settles a +-1 change by copying one instead of redoing the GEMM.  ActOut
+// without pool / P16 fusion.  Results equal phase 1 + phase 2's.
 constexpr int GEMM_SPEC_SLOT_WORDS = 32;  // one 128-byte line per slot
 bool conv_fwd_spec_ok(const ConvGeom& g);    // the plan (autotuned / forced) is STRAT_SPEC
 bool conv_dgrad_spec_ok(const ConvGeom& g);
+void gemm_speculate_bias(int bias);  // diagnostics: A guesses the hint + bias (niti_diag_gemm_speculate)
+size_t conv_fwd_spec_alt_bytes(const ConvGeom& g);
+size_t conv_dgrad_spec_alt_bytes(const ConvGeom& g);
 hipError_t conv_fwd_spec(const ConvGeom& g, const int8_t* x, const int8_t* w, uint32_t* amax, const ActOut& o,
-                         uint32_t* slot, int pass, hipStream_t st);
+                         uint32_t* slot, int pass, hipStream_t st, int8_t* alt = nullptr);
 hipError_t conv_dgrad_spec(const ConvGeom& g, const int8_t* dy, const int8_t* wt, uint32_t* amax, const ActOut& o,
-                           uint32_t* slot, int pass, hipStream_t st);
+                           uint32_t* slot, int pass, hipStream_t st, int8_t* alt = nullptr);
 hipError_t conv_fwd_phase1(const ConvGeom& g, const int8_t* x, const int8_t* w, int32_t* acc, uint32_t* amax,
                            void* ws, size_t ws_bytes, hipStream_t st);
 hipError_t conv_fwd_phase2(const ConvGeom& g, const int8_t* x, const int8_t* w, const int32_t* acc,

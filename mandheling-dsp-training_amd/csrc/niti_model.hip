@@ -220,6 +220,10 @@ struct Model {
     // the range launch keeps its int32 accumulators here, the requantise launch reads them back
     int32_t* rc_acc = nullptr;
     size_t rc_acc_size = 0;
+    // the GEMM speculative pairs' alternates (one bit width below / above A's guess), shared by every
+    // layer phase: a pair's B consumes them before the next pair's A writes them
+    int8_t* gspec_alt = nullptr;
+    size_t gspec_alt_bytes = 0;
     // the first layer's range came with its im2col copy (input_im2col's Conv0Range) this step
     bool conv0_ranged = false;
     bool rowconv_layer(int i) const { return use_rowconv && L[i].rc; }
@@ -746,6 +750,12 @@ int Model::build(int arch_, int batch_, int in_hw) {
         rc_acc = (int32_t*)ws.alloc(rc_acc_size);
         if (!rc_acc) return NITI_OUT_OF_MEMORY;
     }
+    for (int i = 0; i < nl; ++i) {  // the GEMM-path phases that may run the speculative pair
+        const Layer& l = L[i];
+        if (!(l.col && conv0_ok(l.g)) && !l.rc) gspec_alt_bytes = std::max(gspec_alt_bytes, conv_fwd_spec_alt_bytes(l.g));
+        if (i > 0 && !l.rcd) gspec_alt_bytes = std::max(gspec_alt_bytes, conv_dgrad_spec_alt_bytes(l.g));
+    }
+    if (gspec_alt_bytes && !(gspec_alt = (int8_t*)ws.alloc(gspec_alt_bytes))) return NITI_OUT_OF_MEMORY;
     amax_bytes = (size_t)3 * nl * MAX_BYTES;
     amax = (uint32_t*)ws.alloc(amax_bytes);
     if (!x0 || !exp0 || !acc || !amax) return NITI_OUT_OF_MEMORY;
@@ -918,9 +928,10 @@ int Model::fwd_layer(int i, hipStream_t st) {
         o.pool.W = g.ow;
     }
     if (spec) {  // the speculative pair: one GEMM pass while the bit width holds, no int32 tensor
-        MTRY(conv_fwd_spec(g, l.in, l.w, rng(i, 0), o, l.gspec, 0, st));
+        int8_t* alt = conv_fwd_spec_alt_bytes(g) <= gspec_alt_bytes ? gspec_alt : nullptr;
+        MTRY(conv_fwd_spec(g, l.in, l.w, rng(i, 0), o, l.gspec, 0, st, alt));
         if (dp && exact) CTRY(coll->allreduce(rng(i, 0), MAX_WORDS, COLL_MAX_U32, st));
-        MTRY(conv_fwd_spec(g, l.in, l.w, rng(i, 0), o, l.gspec, 1, st));
+        MTRY(conv_fwd_spec(g, l.in, l.w, rng(i, 0), o, l.gspec, 1, st, alt));
     } else {
         MTRY(conv_fwd_phase1(g, l.in, l.w, acc, rng(i, 0), slab, slab_bytes, st));
         if (dp && exact) CTRY(coll->allreduce(rng(i, 0), MAX_WORDS, COLL_MAX_U32, st));
@@ -1147,9 +1158,10 @@ int Model::dgrad_layer(int i, hipStream_t st) {
         if (conv_dgrad_phase2_separate(g, slab_bytes)) o.out_p16 = p16_out;
     }
     if (spec) {  // the speculative pair (no int32 tensor while the bit width holds)
-        MTRY(conv_dgrad_spec(g, l.dy, l.wT, rng(i, 1), o, l.gspec + GEMM_SPEC_SLOT_WORDS, 0, st));
+        int8_t* alt = conv_dgrad_spec_alt_bytes(g) <= gspec_alt_bytes ? gspec_alt : nullptr;
+        MTRY(conv_dgrad_spec(g, l.dy, l.wT, rng(i, 1), o, l.gspec + GEMM_SPEC_SLOT_WORDS, 0, st, alt));
         if (dp && exact) CTRY(coll->allreduce(rng(i, 1), MAX_WORDS, COLL_MAX_U32, st));
-        MTRY(conv_dgrad_spec(g, l.dy, l.wT, rng(i, 1), o, l.gspec + GEMM_SPEC_SLOT_WORDS, 1, st));
+        MTRY(conv_dgrad_spec(g, l.dy, l.wT, rng(i, 1), o, l.gspec + GEMM_SPEC_SLOT_WORDS, 1, st, alt));
     } else {
         MTRY(conv_dgrad_phase1(g, l.dy, l.wT, acc, rng(i, 1), slab, slab_bytes, st));
         if (dp && exact) CTRY(coll->allreduce(rng(i, 1), MAX_WORDS, COLL_MAX_U32, st));
@@ -1721,16 +1733,19 @@ int niti_model_spec_stats(niti_model_t m, uint32_t* out, int max_layers) {
     const int nl = std::min(max_layers, (int)m->m.L.size());
     std::fill(out, out + (size_t)nl * 6, 0u);
     for (int i = 0; i < nl; ++i) {
-        const uint32_t* bar = m->m.L[i].bar;
-        if (bar == nullptr) continue;
+        const niti::Layer& l = m->m.L[i];
         for (int d = 0; d < 2; ++d) {  // forward / input-gradient slot: hint, redone launches, stored pairs
-            uint32_t w[5];
-            if (hipMemcpy(w, niti::rowconv_spec_slot(const_cast<uint32_t*>(bar), d != 0), sizeof(w), hipMemcpyDeviceToHost) !=
-                hipSuccess)
+            uint32_t w[5] = {0, 0, 0, 0, 0}, gw[4] = {0, 0, 0, 0};
+            if (l.bar != nullptr && hipMemcpy(w, niti::rowconv_spec_slot(const_cast<uint32_t*>(l.bar), d != 0), sizeof(w),
+                                              hipMemcpyDeviceToHost) != hipSuccess)
                 return NITI_INVALID_VALUE;
-            out[i * 6 + d * 3] = w[0];
-            out[i * 6 + d * 3 + 1] = w[2];
-            out[i * 6 + d * 3 + 2] = w[4];
+            // the GEMM path's pair (plan strategy 3): its own slot, no store mode
+            if (l.gspec != nullptr && hipMemcpy(gw, l.gspec + d * niti::GEMM_SPEC_SLOT_WORDS, sizeof(gw),
+                                                hipMemcpyDeviceToHost) != hipSuccess)
+                return NITI_INVALID_VALUE;
+            out[i * 6 + d * 3] = std::max(w[0], gw[0]);
+            out[i * 6 + d * 3 + 1] = w[2] + gw[2];
+            out[i * 6 + d * 3 + 2] = w[4] + gw[3];  // the GEMM pair: misses settled from an alternate
         }
     }
     return NITI_NO_ERROR;

@@ -231,6 +231,11 @@ int ResNetModel::build(int batch_, int in_hw_, int classes_) {
     if (slab_bytes && !(slab = ws.alloc(slab_bytes))) return NITI_OUT_OF_MEMORY;
     if (slab_w_bytes && !(slab_w = ws.alloc(slab_w_bytes))) return NITI_OUT_OF_MEMORY;
     if (rc_acc_size && !(rc_acc = (int32_t*)ws.alloc(rc_acc_size))) return NITI_OUT_OF_MEMORY;
+    for (int i = 0; i < nl; ++i) {  // the GEMM-path phases that may run the speculative pair
+        if (!C[i].rows) gspec_alt_bytes = std::max(gspec_alt_bytes, conv_fwd_spec_alt_bytes(C[i].g));
+        if (C[i].dx != nullptr && !C[i].rows_dg) gspec_alt_bytes = std::max(gspec_alt_bytes, conv_dgrad_spec_alt_bytes(C[i].g));
+    }
+    if (gspec_alt_bytes && !(gspec_alt = (int8_t*)ws.alloc(gspec_alt_bytes))) return NITI_OUT_OF_MEMORY;
     amax_bytes = (3 * C.size() + 2 * B.size() + 1) * MAX_BYTES;
     amax = (uint32_t*)ws.alloc(amax_bytes);
     if (!amax) return NITI_OUT_OF_MEMORY;
@@ -330,9 +335,10 @@ int ResNetModel::fwd_conv(int i, hipStream_t st) {
     o.wscale = c.ws_dev;
     o.exp_out = c.y_exp;
     if (conv_fwd_spec_ok(g)) {  // the GEMM's speculative pair (plan strategy 3)
-        RTRY(conv_fwd_spec(g, c.in, c.w, rng(i, 0), o, c.gspec, 0, st));
+        int8_t* alt = conv_fwd_spec_alt_bytes(g) <= gspec_alt_bytes ? gspec_alt : nullptr;
+        RTRY(conv_fwd_spec(g, c.in, c.w, rng(i, 0), o, c.gspec, 0, st, alt));
         if (dp && exact) RTRY(coll->allreduce(rng(i, 0), MAX_WORDS, COLL_MAX_U32, st));
-        RTRY(conv_fwd_spec(g, c.in, c.w, rng(i, 0), o, c.gspec, 1, st));
+        RTRY(conv_fwd_spec(g, c.in, c.w, rng(i, 0), o, c.gspec, 1, st, alt));
     } else {
         RTRY(conv_fwd_phase1(g, c.in, c.w, acc, rng(i, 0), slab, slab_bytes, st));
         if (dp && exact) RTRY(coll->allreduce(rng(i, 0), MAX_WORDS, COLL_MAX_U32, st));
@@ -387,9 +393,10 @@ int ResNetModel::dgrad_conv(int i, hipStream_t st) {
     o.exp_out = c.dx_exp;
     uint32_t* slot = c.gspec + GEMM_SPEC_SLOT_WORDS;
     if (conv_dgrad_spec_ok(g)) {
-        RTRY(conv_dgrad_spec(g, c.dy, c.wT, rng(i, 1), o, slot, 0, st));
+        int8_t* alt = conv_dgrad_spec_alt_bytes(g) <= gspec_alt_bytes ? gspec_alt : nullptr;
+        RTRY(conv_dgrad_spec(g, c.dy, c.wT, rng(i, 1), o, slot, 0, st, alt));
         if (dp && exact) RTRY(coll->allreduce(rng(i, 1), MAX_WORDS, COLL_MAX_U32, st));
-        RTRY(conv_dgrad_spec(g, c.dy, c.wT, rng(i, 1), o, slot, 1, st));
+        RTRY(conv_dgrad_spec(g, c.dy, c.wT, rng(i, 1), o, slot, 1, st, alt));
     } else {
         RTRY(conv_dgrad_phase1(g, c.dy, c.wT, acc, rng(i, 1), slab, slab_bytes, st));
         if (dp && exact) RTRY(coll->allreduce(rng(i, 1), MAX_WORDS, COLL_MAX_U32, st));
@@ -913,14 +920,16 @@ int ResNetModel::spec_stats(uint32_t* out, int max_layers) {
     const int nl = std::min(max_layers, (int)C.size());
     std::fill(out, out + (size_t)nl * 6, 0u);
     for (int i = 0; i < nl; ++i) {
-        if (C[i].bar == nullptr) continue;
-        for (int d = 0; d < 2; ++d) {
-            uint32_t w[5];
-            if (hipMemcpy(w, rowconv_spec_slot(C[i].bar, d != 0), sizeof(w), hipMemcpyDeviceToHost) != hipSuccess)
+        for (int d = 0; d < 2; ++d) {  // the row kernels' pair and the GEMM's (its own slot, no store mode)
+            uint32_t w[5] = {0, 0, 0, 0, 0}, gw[4] = {0, 0, 0, 0};
+            if (C[i].bar != nullptr &&
+                hipMemcpy(w, rowconv_spec_slot(C[i].bar, d != 0), sizeof(w), hipMemcpyDeviceToHost) != hipSuccess)
                 return NITI_INVALID_VALUE;
-            out[i * 6 + d * 3] = w[0];
-            out[i * 6 + d * 3 + 1] = w[2];
-            out[i * 6 + d * 3 + 2] = w[4];
+            if (hipMemcpy(gw, C[i].gspec + d * GEMM_SPEC_SLOT_WORDS, sizeof(gw), hipMemcpyDeviceToHost) != hipSuccess)
+                return NITI_INVALID_VALUE;
+            out[i * 6 + d * 3] = std::max(w[0], gw[0]);
+            out[i * 6 + d * 3 + 1] = w[2] + gw[2];
+            out[i * 6 + d * 3 + 2] = w[4] + gw[3];  // the GEMM pair: misses settled from an alternate
         }
     }
     return NITI_NO_ERROR;

@@ -102,6 +102,8 @@ struct ResNetModel {
     size_t slab_w_bytes = 0;
     int32_t* rc_acc = nullptr;    // the row kernels' accumulator store (two-launch store mode)
     size_t rc_acc_size = 0;
+    int8_t* gspec_alt = nullptr;  // the GEMM speculative pairs' alternates (shared)
+    size_t gspec_alt_bytes = 0;
     uint32_t* rc_err = nullptr;
     unsigned long long* qstats = nullptr;
     unsigned long long* qslots = nullptr;

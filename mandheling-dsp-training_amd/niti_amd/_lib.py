@@ -108,6 +108,7 @@ def lib():
         "niti_execution_status": (ci, [vp, vp]),
         "niti_diag_rowconv_barrier": (None, [C.c_uint32, C.c_uint32]),
         "niti_diag_rowconv_speculate": (None, [C.c_int]),
+        "niti_diag_gemm_speculate": (None, [C.c_int]),
         "niti_diag_p16_jobs_cap": (None, [C.c_int]),
         "niti_tensor_convert": (ci, [tp, tp, vp]),
         "niti_geom_finalize": (ci, [C.POINTER(Geom)]),

@@ -256,3 +256,43 @@ def _dp_steps(T, full, ranks, streams, rng, world, per, hw, classes, images, con
                 assert np.array_equal(m.tap(i, 2), full.tap(i, 2)[sl]), ("dy", step, r, c["name"])
                 assert np.array_equal(m.tap(i, 1), full.tap(i, 1)), ("dw", step, r, c["name"])
                 assert np.array_equal(m.get_weight(i), full.get_weight(i)), ("w", step, r, c["name"])
+
+
+@pytest.mark.parametrize("bias", [1, -1, 2])
+def test_resnet18_cpp_gemm_pair_misses(T, bias):
+    """The GEMM speculative pair (plan strategy 3 on every GEMM-path forward and input gradient) with
+    launch A's guess forced off by `bias` (niti_diag_gemm_speculate): +1 / -1 make every launch B
+    settle from A's alternate one bit width below / above, 2 makes every launch B redo the GEMM.  Two
+    steps against the oracle each (NITI_Conv_Int8.cpp:260-307, NITI_DeConv_Int8.cpp:294-329)."""
+    import niti_resnet_ref as RR
+    from niti_amd import _lib as L
+    from niti_amd.model import NitiModel
+    hw, batch, classes = 64, 2, 10
+    convs = RR.resnet18_convs(hw, classes)
+    W, S = RR.init_weights(convs, seed=90 + bias)
+    rng = np.random.default_rng(90 + bias)
+    m = _model(batch, hw, classes, W, S)
+    lib = L.lib()
+    try:
+        for i in range(len(convs)):
+            for ph in (0, 1):
+                m.set_plan(i, ph, (128, 128, 1, 3))
+        lib.niti_diag_gemm_speculate(bias)
+        for step in range(3):
+            x = rng.integers(-127, 128, (batch, 3, hw, hw)).astype(np.int8)
+            lab = rng.integers(0, classes, batch).astype(np.int32)
+            newW, rec = RR.train_step(convs, W, S, x, -2, lab, classes=classes)
+            m.train_step(T.from_numpy(x).cuda(), -2, T.from_numpy(lab).cuda())
+            _check_step(m, convs, rec, newW, step)
+            W = newW
+        st = m.spec_stats()
+        settled = sum(s[2] + s[5] for s in st)  # GEMM pairs: misses settled from an alternate
+        redone = sum(s[1] + s[4] for s in st)
+        if bias == 2:
+            assert redone > 0, st
+        else:
+            assert settled > 0, st
+    finally:
+        lib.niti_diag_gemm_speculate(0)
+        NitiModel.reset_plans()
+
