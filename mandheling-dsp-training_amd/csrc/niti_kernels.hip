@@ -1823,7 +1823,10 @@ static hipError_t gemm_acc_plan(const GemmPlan& p, const LA& la, const LB& lb, i
         hipError_t r = launch_mode<LA, LB, EPI_SLAB, KT>(p, la, lb, M, N, kc_total, e, st);
         if (r == hipSuccess && after_gemm != nullptr) r = hipEventRecord(after_gemm, st);
         if (r != hipSuccess) return r;
-        if (defer != nullptr && ((int64_t)M * N) % 4 == 0) {  // the NITI_SGD launch combines the slabs
+        // the NITI_SGD launch combines the slabs -- where each split has a few 1024-element chunks;
+        // a small gradient over many splits (VGG-11 conv0: 2048 elements x 256 splits) reduces faster
+        // here, splitk_reduce spreading the splits over blocks (the combine sums them serially)
+        if (defer != nullptr && ((int64_t)M * N) % 4 == 0 && (int64_t)M * N >= (int64_t)p.splits * 4096) {
             defer->slab = ws;
             defer->splits = p.splits;
             defer->slab_stride = e.slab_stride;
