@@ -184,11 +184,26 @@ struct LoadConvDgrad {
 //   EPI_REQUANT  reads the max word, applies the NITI forward shift rule, writes int8
 //                (+ fused relu / relu-grad mask, + exponent)   (second pass)
 //   EPI_SLAB     int32 partial sums of one K split -> slab[split] (reduced later)
+//   EPI_SGD      reads the weight gradient's max word, applies NITI_SGD to the weights in place
+//                (the second pass of a fully connected layer's weight gradient)
 // =====================================================================================
 // K bytes per step (KT = false) is the A loader's BK: 128 (full 128-byte lines per row and
 // step) where the operand allows it, else 64.
 
-enum EpiMode { EPI_STORE = 0, EPI_AMAX = 1, EPI_REQUANT = 2, EPI_SLAB = 3 };
+enum EpiMode { EPI_STORE = 0, EPI_AMAX = 1, EPI_REQUANT = 2, EPI_SLAB = 3, EPI_SGD = 4 };
+
+// Output row map of a sub-pixel class GEMM (the stride-2 input gradient, conv_dgrad_phase1): GEMM
+// row m = (img, my, mx) of the class grid [n][hc][wc] is pixel (img, sy*my + py, sx*mx + px) of the
+// [n][h][w] output.  off: rows are output pixels as they stand.
+struct RowMap {
+    int on = 0;
+    int hc = 0, wc = 0, h = 0, w = 0, py = 0, px = 0, sy = 2, sx = 2;
+};
+__device__ __forceinline__ int64_t map_row(const RowMap& m, int row) {
+    if (!m.on) return row;
+    const int mx = row % m.wc, t = row / m.wc, my = t % m.hc, img = t / m.hc;
+    return ((int64_t)img * m.h + m.sy * my + m.py) * m.w + m.sx * mx + m.px;
+}
 
 struct Epi {
     int32_t* C = nullptr;  // STORE: C; SLAB: slab base
@@ -217,6 +232,14 @@ struct Epi {
     // the common miss, a max near a power of two -- by copying instead of redoing the GEMM
     int8_t* alt = nullptr;
     int spec_bias = 0;  // diagnostics (niti_diag_gemm_speculate): launch A guesses hint + bias
+    // EPI_SGD (the fully connected layers' weight gradient recomputed after its range pass): the
+    // update in the epilogue -- weights [M][ldo], their transpose [sgd_ci][sgd_ldt], int8 gradient
+    int8_t* sgd_w = nullptr;
+    int8_t* sgd_wT = nullptr;
+    int8_t* sgd_g = nullptr;
+    int sgd_rule = 0, sgd_ci = 0;
+    int64_t sgd_ldt = 0;
+    RowMap rmap;  // STORE / REQUANT: where GEMM row m lands (sub-pixel classes)
 };
 
 // launch B of the pair: the rule's bit width of the (all-reduced) max against the one A used
@@ -227,9 +250,11 @@ struct Epi {
 __device__ __forceinline__ int gemm_spec_settle(const Epi& epi) {
     const uint32_t g = read_max(epi.amax);
     const int bw = bitwidth_of(g);
-    const int used = __builtin_amdgcn_readfirstlane(
-                         (int)__hip_atomic_load(epi.hint + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) - 1;
-    const int act = bw == used ? 0 : epi.alt == nullptr ? -1 : (bw == used - 1 && used >= 1) ? 1 : bw == used + 1 ? 2 : -1;
+    const uint32_t h1 = (uint32_t)__builtin_amdgcn_readfirstlane(
+        (int)__hip_atomic_load(epi.hint + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    const int used = (int)(h1 & 0x7fffffffu) - 1;
+    const bool alts = (h1 >> 31) != 0u;  // A wrote the alternates
+    const int act = bw == used ? 0 : !alts ? -1 : (bw == used - 1 && used >= 1) ? 1 : bw == used + 1 ? 2 : -1;
     if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
         if (act >= 0 && epi.exp_out != nullptr) {  // (a redo writes it in its epilogue)
             const int shift = bw - 7;
@@ -239,6 +264,11 @@ __device__ __forceinline__ int gemm_spec_settle(const Epi& epi) {
         __hip_atomic_store(epi.hint, (uint32_t)bw + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (act < 0) __hip_atomic_fetch_add(epi.hint + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (act > 0) __hip_atomic_fetch_add(epi.hint + 3, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // the alternates' window: a miss opens it for the next GEMM_SPEC_ALT_PAIRS pairs, a hit
+        // narrows it (a layer whose bit width holds pays for one output only)
+        const uint32_t win = __hip_atomic_load(epi.hint + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(epi.hint + 4, act != 0 ? (uint32_t)GEMM_SPEC_ALT_PAIRS : (win > 0u ? win - 1u : 0u),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     return act;
 }
@@ -247,9 +277,17 @@ __device__ __forceinline__ int gemm_spec_settle(const Epi& epi) {
 
 // Shared epilogue: D[row][col] of the 32x32 MFMA tiles, row = (i&3) + 8*(i>>2) + 4*(lane>>5),
 // col = lane&31.  `smem` is reused for the block max (every LDS read finished at the last barrier).
-// REQUANT: the int8 tile is staged in LDS ([BM][BN + 16] bytes) and written out as 16-byte
-// row chunks (the MFMA C layout gives each lane one column of 16 rows, i.e. byte stores);
-// the relu-grad mask is applied in the same pass.
+// REQUANT: the int8 values leave as dwords of 4 columns of one row, packed in registers (see
+// below); the relu-grad mask is applied in the same pass.
+// 4 x 4 byte transpose inside a lane quad (j = lane & 3): byte r of lane k -> byte k of lane r.
+// Every lane of the wave must execute it (DPP reads the quad partners' registers).
+__device__ __forceinline__ uint32_t quad_transpose(uint32_t d, int j) {
+    const uint32_t y1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)d, 0xB1, 0xF, 0xF, false);  // lane ^ 1
+    d = __builtin_amdgcn_perm(y1, d, (j & 1) ? 0x03070105u : 0x06020400u);
+    const uint32_t y2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)d, 0x4E, 0xF, 0xF, false);  // lane ^ 2
+    return __builtin_amdgcn_perm(y2, d, (j & 2) ? 0x03020706u : 0x05040100u);
+}
+
 // whether the STORE / SLAB epilogue stages the int32 tile through LDS (tiles up to 128 x 128)
 constexpr bool epi_stage_c(int mode, int bm, int bn) {
     return (mode == EPI_STORE || mode == EPI_SLAB) && bm * (bn + 4) * 4 <= 72 * 1024;
@@ -265,7 +303,8 @@ __device__ __forceinline__ void gemm_epilogue(v16i (&acc)[TM][TN], int r0, int c
     bool rq_raw = false;
     // launch A of the speculative pair: requantise with the hinted bit width, publish the max
     const bool spec_a = MODE == EPI_REQUANT && epi.spec == 1;
-    int abw = 0;  // the bit width launch A requantises with
+    int abw = 0;             // the bit width launch A requantises with
+    bool spec_alts = false;  // and whether it writes the alternates
     if (MODE == EPI_REQUANT) {
         int bw;
         if (spec_a) {
@@ -274,8 +313,13 @@ __device__ __forceinline__ void gemm_epilogue(v16i (&acc)[TM][TN], int r0, int c
             if (h != 0u) bw += epi.spec_bias;
             if (bw < 0) bw = 0;
             abw = bw;
+            // the alternates only while the window a recent miss opened lasts (hint[4], written by B)
+            spec_alts = epi.alt != nullptr &&
+                        __builtin_amdgcn_readfirstlane((int)__hip_atomic_load(epi.hint + 4, __ATOMIC_RELAXED,
+                                                                              __HIP_MEMORY_SCOPE_AGENT)) != 0;
             if (blockIdx.x == 0 && blockIdx.y == 0 && tid == 0)
-                __hip_atomic_store(epi.hint + 1, (uint32_t)bw + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(epi.hint + 1, ((uint32_t)bw + 1u) | (spec_alts ? 0x80000000u : 0u), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
         } else {
             bw = bitwidth_of(read_max(epi.amax));
         }
@@ -294,85 +338,138 @@ __device__ __forceinline__ void gemm_epilogue(v16i (&acc)[TM][TN], int r0, int c
     constexpr int LDT = BN + 4;  // int32 row pitch of the staged C tile (STORE / SLAB)
     int32_t* ctile = (int32_t*)smem;
     uint32_t lmax = 0;
+    if (MODE != EPI_REQUANT || spec_a) {
 #pragma unroll
-    for (int a = 0; a < TM; ++a)
+        for (int a = 0; a < TM; ++a)
 #pragma unroll
-        for (int b = 0; b < TN; ++b) {
-            const int col = c0 + b * 32 + (lane & 31);
+            for (int b = 0; b < TN; ++b) {
+                const int col = c0 + b * 32 + (lane & 31);
 #pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const int row = r0 + a * 32 + (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
-                const int v = acc[a][b][i];
-                if (STAGE_C) ctile[(row - m0) * LDT + (col - n0)] = v;
-                if (row < M && col < N) {
-                    if (!STAGE_C && (MODE == EPI_STORE || MODE == EPI_SLAB)) Cs[(int64_t)row * epi.ldc + col] = v;
-                    if (MODE == EPI_STORE || MODE == EPI_AMAX || spec_a) {
-                        const uint32_t u = uabs32(v);
-                        lmax = lmax > u ? lmax : u;
+                for (int i = 0; i < 16; ++i) {
+                    const int row = r0 + a * 32 + (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
+                    const int v = acc[a][b][i];
+                    if (STAGE_C) ctile[(row - m0) * LDT + (col - n0)] = v;
+                    if (row < M && col < N) {
+                        if (!STAGE_C && (MODE == EPI_STORE || MODE == EPI_SLAB)) Cs[map_row(epi.rmap, row) * epi.ldc + col] = v;
+                        if (MODE == EPI_STORE || MODE == EPI_AMAX || spec_a) {
+                            const uint32_t u = uabs32(v);
+                            lmax = lmax > u ? lmax : u;
+                        }
                     }
                 }
-                if (MODE == EPI_REQUANT) {
-                    int32_t q = rq_raw ? (int32_t)(int8_t)v : psto_any(v, rq_shift);
-                    if (epi.relu && q < 0) q = 0;
-                    smem[(row - m0) * (BN + 16) + (col - n0)] = (int8_t)q;
-                }
             }
-        }
+    }
     if (MODE == EPI_REQUANT) {
-        __syncthreads();
-        constexpr int CPR = BN / 16;  // 16-byte chunks per tile row
-        for (int t = tid; t < BM * CPR; t += NW * 64) {
-            const int rl = t / CPR, cl = (t - rl * CPR) * 16;
-            const int row = m0 + rl, col = n0 + cl;
-            if (row < M && col < N) {  // N is a multiple of 16
-                v16c q = *(const v16c*)(smem + rl * (BN + 16) + cl);
-                const int64_t o = (int64_t)row * epi.ldo + col;
-                if (epi.relu_mask != nullptr) {
-                    const v16c mk = *(const v16c*)(epi.relu_mask + o);
+        // Straight from the accumulators, no LDS: a lane holds 4 consecutive rows of one column per
+        // 4 accumulator registers; a 4 x 4 byte transpose inside each lane quad (two DPP swaps, two
+        // byte permutes) gives it 4 consecutive columns of one row -- a dword store; the 8 quads of a
+        // half-wave write 32 contiguous bytes of each of 4 rows.
+        const int j = lane & 3;
+        const int col4 = c0 + 4 * ((lane & 31) >> 2);  // + b * 32: the dword's first column
+        auto put = [&](int sh, bool raw, int8_t* dst) {
 #pragma unroll
-                    for (int j = 0; j < 16; ++j) q[j] = mk[j] > 0 ? q[j] : (signed char)0;
-                }
-                *(v16c*)(epi.out + o) = q;
-            }
-        }
-        if (spec_a && epi.alt != nullptr) {
+            for (int a = 0; a < TM; ++a)
+#pragma unroll
+                for (int b = 0; b < TN; ++b)
+#pragma unroll
+                    for (int gq = 0; gq < 4; ++gq) {
+                        uint32_t d = 0;
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const int v = acc[a][b][4 * gq + r];
+                            int32_t q = raw ? (int32_t)(int8_t)v : psto_any(v, sh);
+                            if (epi.relu && q < 0) q = 0;
+                            d |= ((uint32_t)q & 0xffu) << (8 * r);
+                        }
+                        d = quad_transpose(d, j);  // byte r of lane k = (row r, column k) -> byte k of lane r
+                        const int row = r0 + a * 32 + 8 * gq + 4 * (lane >> 5) + j;
+                        const int col = col4 + b * 32;
+                        if (row < M && col < N) {  // N is a multiple of 16
+                            const int64_t o = map_row(epi.rmap, row) * epi.ldo + col;
+                            if (epi.relu_mask != nullptr) {
+                                const uint32_t mk = *(const uint32_t*)(epi.relu_mask + o);
+                                uint32_t keep = 0;
+#pragma unroll
+                                for (int k = 0; k < 4; ++k)
+                                    keep |= ((int8_t)(mk >> (8 * k)) > 0 ? 0xffu : 0u) << (8 * k);
+                                d &= keep;
+                            }
+                            *(uint32_t*)(dst + o) = d;
+                        }
+                    }
+        };
+        put(rq_shift, rq_raw, epi.out);
+        if (spec_a && spec_alts) {
             // the alternates: the same tile requantised one bit width below / above the guess
 #pragma unroll
             for (int k = 0; k < 2; ++k) {
                 const int sh = (k == 0 ? (abw > 0 ? abw - 1 : 0) : abw + 1) - 7;
-                const int s2 = sh > 1 ? sh : 2;
-                const bool raw = sh <= 0;
-                __syncthreads();  // the previous round's LDS reads are done
+                put(sh > 1 ? sh : 2, sh <= 0, epi.alt + (int64_t)k * M * epi.ldo);
+            }
+        }
+    }
+    if (MODE == EPI_SGD) {
+        // NITI_SGD on the weight-gradient tile (NITI_GradientConv_Int8.cpp:274-296, NITI_SGD.hpp:20-54):
+        // g = PSTO(C, bw - rule), w <- clip(w - g, +-127) with w [M][ldo] (OHWI16, one tap), the
+        // int8 gradient to sgd_g, and the new weights transposed into sgd_wT [sgd_ci][sgd_ldt] (IHWO16)
+        // through an LDS tile, leaving as 16-byte row chunks.  Every weight of the tile is loaded
+        // before the first store (the stores to w could alias later loads: issued in between, each
+        // load would wait for a memory round trip of its own).
+        const int bw = bitwidth_of(read_max(epi.amax));
+        const int sh = bw - epi.sgd_rule;
+        const int j = lane & 3;
+        const int col4 = c0 + 4 * ((lane & 31) >> 2);
+        uint32_t wv[TM][TN][4];
 #pragma unroll
-                for (int a = 0; a < TM; ++a)
+        for (int a = 0; a < TM; ++a)
 #pragma unroll
-                    for (int b = 0; b < TN; ++b) {
-                        const int col = c0 + b * 32 + (lane & 31);
+            for (int b = 0; b < TN; ++b)
 #pragma unroll
-                        for (int i = 0; i < 16; ++i) {
-                            const int row = r0 + a * 32 + (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
-                            const int v = acc[a][b][i];
-                            int32_t q = raw ? (int32_t)(int8_t)v : psto_any(v, s2);
-                            if (epi.relu && q < 0) q = 0;
-                            smem[(row - m0) * (BN + 16) + (col - n0)] = (int8_t)q;
-                        }
-                    }
-                __syncthreads();
-                int8_t* dst = epi.alt + (int64_t)k * M * epi.ldo;
-                for (int t = tid; t < BM * CPR; t += NW * 64) {
-                    const int rl = t / CPR, cl = (t - rl * CPR) * 16;
-                    const int row = m0 + rl, col = n0 + cl;
-                    if (row < M && col < N) {
-                        v16c q = *(const v16c*)(smem + rl * (BN + 16) + cl);
-                        const int64_t o = (int64_t)row * epi.ldo + col;
-                        if (epi.relu_mask != nullptr) {
-                            const v16c mk = *(const v16c*)(epi.relu_mask + o);
-#pragma unroll
-                            for (int j = 0; j < 16; ++j) q[j] = mk[j] > 0 ? q[j] : (signed char)0;
-                        }
-                        *(v16c*)(dst + o) = q;
-                    }
+                for (int gq = 0; gq < 4; ++gq) {
+                    const int row = r0 + a * 32 + 8 * gq + 4 * (lane >> 5) + j, col = col4 + b * 32;
+                    wv[a][b][gq] = row < M && col < N ? *(const uint32_t*)(epi.sgd_w + (int64_t)row * epi.ldo + col) : 0u;
                 }
+        __syncthreads();  // (LDS: every wave is past the main loop's last reads)
+        constexpr int TP = BM + 16;  // byte pitch of the transposed tile [BN][TP]
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+#pragma unroll
+            for (int b = 0; b < TN; ++b)
+#pragma unroll
+                for (int gq = 0; gq < 4; ++gq) {
+                    uint32_t gd = 0;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int32_t q = bw == 0 ? 0 : psto_any(acc[a][b][4 * gq + r], sh);
+                        gd |= ((uint32_t)q & 0xffu) << (8 * r);
+                    }
+                    gd = quad_transpose(gd, j);
+                    const int row = r0 + a * 32 + 8 * gq + 4 * (lane >> 5) + j;
+                    const int col = col4 + b * 32;
+                    uint32_t wn = 0;
+                    if (row < M && col < N) {
+                        const int64_t o = (int64_t)row * epi.ldo + col;
+                        const uint32_t wo = wv[a][b][gq];
+#pragma unroll
+                        for (int k = 0; k < 4; ++k)
+                            wn |= ((uint32_t)clip127((int32_t)(int8_t)(wo >> (8 * k)) - (int32_t)(int8_t)(gd >> (8 * k))) &
+                                   0xffu)
+                                  << (8 * k);
+                        *(uint32_t*)(epi.sgd_w + o) = wn;
+                        if (epi.sgd_g != nullptr) *(uint32_t*)(epi.sgd_g + o) = gd;
+                    }
+                    // back to 4 rows of one column: a dword of the transposed tile
+                    const uint32_t wt = quad_transpose(wn, j);
+                    const int trow = a * 32 + 8 * gq + 4 * (lane >> 5) + (r0 - m0), tcol = b * 32 + (lane & 31) + (c0 - n0);
+                    *(uint32_t*)(smem + tcol * TP + trow) = wt;
+                }
+        __syncthreads();
+        if (epi.sgd_wT != nullptr) {
+            constexpr int CPR = BM / 16;  // 16-byte chunks per transposed row
+            for (int t = tid; t < BN * CPR; t += NW * 64) {
+                const int cl = t / CPR, rl = (t - cl * CPR) * 16;
+                if (n0 + cl < epi.sgd_ci && m0 + rl < epi.sgd_ldt)
+                    *(v16c*)(epi.sgd_wT + (int64_t)(n0 + cl) * epi.sgd_ldt + m0 + rl) = *(const v16c*)(smem + cl * TP + rl);
             }
         }
     }
@@ -385,7 +482,7 @@ __device__ __forceinline__ void gemm_epilogue(v16i (&acc)[TM][TN], int r0, int c
             const int rl = t / CPR, cl = (t - rl * CPR) * 4;
             const int row = m0 + rl, col = n0 + cl;
             if (row < M && col < N)  // N is a multiple of 16
-                *(v4i*)(Cs + (int64_t)row * epi.ldc + col) = *(const v4i*)(ctile + rl * LDT + cl);
+                *(v4i*)(Cs + map_row(epi.rmap, row) * epi.ldc + col) = *(const v4i*)(ctile + rl * LDT + cl);
         }
     }
     if (MODE == EPI_STORE || MODE == EPI_AMAX || spec_a) {
@@ -794,6 +891,7 @@ __global__ void __launch_bounds__(NW * 64) gemm_kernel(LA la, LB lb, int M, int 
     constexpr int CT_BYTES = epi_stage_c(MODE, BM, BN) ? BM * (BN + 4) * 4 : 0;  // staged C tile
     constexpr int SMEM = SMEM0 > CT_BYTES ? SMEM0 : CT_BYTES;
     static_assert(SMEM >= BM * (BN + 16), "requant epilogue staging fits in the pipeline's LDS");
+    static_assert(MODE != EPI_SGD || SMEM >= BN * (BM + 16), "the NITI_SGD epilogue's transposed tile fits");
     __shared__ __attribute__((aligned(16))) int8_t smem[SMEM];
 
     if constexpr (MODE == EPI_REQUANT) {
@@ -1775,8 +1873,15 @@ static hipError_t launch_mode(const GemmPlan& p, const LA& la, const LB& lb, int
         NITI_LAUNCH(128, 64, 2, 2, 4);
     else if (p.bm == 64)
         NITI_LAUNCH(64, 128, 1, 4, 4);
-    else if (p.bm == 256 && p.bn == 256)
-        NITI_LAUNCH(256, 256, 2, 4, 8);
+    else if (p.bm == 256 && p.bn == 256) {
+        // (the fully connected layers' range / update passes take 128 x 256: at 256 x 256 their
+        // weight-gradient instantiations move registers an in-flight fragment read still writes,
+        // tools/isa_inflight.py)
+        if constexpr (KT && (MODE == EPI_AMAX || MODE == EPI_SGD))
+            NITI_LAUNCH(128, 256, 2, 4, 8);
+        else
+            NITI_LAUNCH(256, 256, 2, 4, 8);
+    }
     else if (p.bm == 256)
         NITI_LAUNCH(256, 128, 4, 2, 8);
     else if (p.bn == 256)
@@ -2430,6 +2535,43 @@ hipError_t conv_wgrad_acc(const ConvGeom& g, const int8_t* x, const int8_t* dy, 
                                                             acc, amax, (int32_t*)ws, ws_bytes / 4, st, after_gemm, defer);
 }
 
+// A fully connected layer's weight gradient in two GEMM passes with no int32 tensor: pass 0 takes
+// its range (EPI_AMAX), pass 1 recomputes it and applies NITI_SGD in the epilogue (EPI_SGD).  The
+// reduction is the batch, so the second pass costs a few microseconds against the gradient's
+// int32 write + read (411 MB for VGG-16's first FC layer).
+bool conv_wgrad_fc_sgd_ok(const ConvGeom& g) {
+    return g.kh == 1 && g.kw == 1 && g.h == 1 && g.w == 1 && g.oh == 1 && g.ow == 1 && plain_1x1(g);
+}
+hipError_t conv_wgrad_fc_sgd(const ConvGeom& g, const int8_t* x, const int8_t* dy, uint32_t* amax, const SgdJob& j,
+                             int pass, hipStream_t st) {
+    if (!conv_wgrad_fc_sgd_ok(g) || amax == nullptr || (pass == 1 && j.w == nullptr)) return hipErrorInvalidValue;
+    KtRowsU la;
+    KtIm2col lg;
+    wgrad_operands(g, x, dy, &la, &lg);
+    KtRowsU lx;
+    lx.p = x;
+    lx.ld = g.cip;
+    lx.cols = g.cip;
+    lx.K = lg.K;
+    lx.bytes = lg.bytes;
+    const int M = g.c_out, N = lg.ncols;
+    GemmPlan p = plan_gemm(M, N, lg.K, KT_BK, 1 << 30, false, 0, PLAN_WGRAD);
+    // diagnostics: the update pass's tile (NITI_DIAG_FC_SGD_TILE=64 / 128 / 256: bm = bn)
+    static const int tile = getenv("NITI_DIAG_FC_SGD_TILE") ? atoi(getenv("NITI_DIAG_FC_SGD_TILE")) : 0;
+    if (pass == 1 && (tile == 64 || tile == 128)) p.bm = p.bn = tile;
+    Epi e;
+    e.amax = amax;
+    if (pass == 0) return launch_mode<KtRowsU, KtRowsU, EPI_AMAX, true>(p, la, lx, M, N, lg.K, e, st);
+    e.ldo = N;
+    e.sgd_w = j.w;
+    e.sgd_wT = j.wT;
+    e.sgd_g = j.g_out;
+    e.sgd_rule = j.rule;
+    e.sgd_ci = j.ci;
+    e.sgd_ldt = j.cop;
+    return launch_mode<KtRowsU, KtRowsU, EPI_SGD, true>(p, la, lx, M, N, lg.K, e, st);
+}
+
 hipError_t matmul_acc(int M, int O, int k16, const int8_t* B, int64_t ldb, const int8_t* A, int64_t lda, int32_t* acc,
                       int64_t ldc, uint32_t* amax, void* ws, size_t ws_bytes, hipStream_t st) {
     const int kc_total = k16 / 16;
@@ -2472,17 +2614,178 @@ hipError_t conv_dgrad_spec(const ConvGeom& g, const int8_t* dy, const int8_t* wt
 }
 size_t conv_fwd_spec_alt_bytes(const ConvGeom& g) { return (size_t)2 * g.n * g.oh * g.ow * g.cop; }
 size_t conv_dgrad_spec_alt_bytes(const ConvGeom& g) { return (size_t)2 * g.n * g.h * g.w * g.cip; }
+// ---- the stride-2 input gradient as four sub-pixel classes ------------------------------------
+// dx[iy][ix] gathers dy[(iy + pt - ky) / 2][(ix + pl - kx) / 2] over the taps where both divisions
+// are exact: the taps of pixel (2 my + py, 2 mx + px) are ky = ky0(py), ky0 + 2, ... and kx alike,
+// the same for the whole class.  Each class is a stride-1 input gradient over dy with a 1- or 2-tap
+// kernel per axis (pad (py + pt - ky0) / 2), written into dx through a row map: the generic per-lane
+// loader instead walked all kh x kw taps for every pixel with 3/4 of them masked to zero.  The
+// class weights [class][ci][kh_c][kw_c][cop] are kept beside wT: built from it when the weights are
+// set (conv_dgrad_subpix_weights) and rewritten by NITI_SGD (SgdJob::subw, sgd_tile_finish).
+struct SubpixAxis {
+    int n, k0;  // taps of the class (k0, k0 + 2, ...), n may be 0
+    int pad;    // the class conv's pad: (p + parity - k0) / 2
+};
+static SubpixAxis subpix_axis(int k, int pad, int parity) {
+    SubpixAxis a;
+    a.k0 = ((parity + pad) % 2 + 2) % 2;
+    a.n = a.k0 < k ? (k - a.k0 + 1) / 2 : 0;
+    a.pad = (parity + pad - a.k0) / 2;
+    return a;
+}
+bool conv_dgrad_subpix_ok(const ConvGeom& g) {
+    return g.sh == 2 && g.sw == 2 && g.dh == 1 && g.dw == 1 && g.h % 2 == 0 && g.w % 2 == 0 && g.kh <= 8 &&
+           g.kw <= 8 && g.pt >= 0 && g.pl >= 0 && g.cop % 64 == 0 && g.cip % 16 == 0 &&
+           (int64_t)g.n * g.h * g.w * g.cip < ((int64_t)1 << 31) && (int64_t)g.n * g.oh * g.ow * g.cop < ((int64_t)1 << 31);
+}
+size_t conv_dgrad_subpix_bytes(const ConvGeom& g) { return (size_t)g.kh * g.kw * g.c_in * g.cop; }
+
+struct SubpixW {
+    const int8_t* wt;
+    int8_t* out;
+    int ci, kh, kw, cop16;  // cop16: 16-byte chunks per tap row
+    int ny[4], nx[4], ky0[4], kx0[4];
+    int64_t off[5];  // chunk offsets of the classes (prefix)
+};
+__global__ void subpix_weights_kernel(SubpixW p) {
+    const int64_t total = p.off[4];
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+        int c = 0;
+        while (c < 3 && t >= p.off[c + 1]) ++c;
+        int64_t r = t - p.off[c];
+        const int cc = (int)(r % p.cop16);
+        r /= p.cop16;
+        const int jx = (int)(r % p.nx[c]);
+        r /= p.nx[c];
+        const int jy = (int)(r % p.ny[c]);
+        const int ci = (int)(r / p.ny[c]);
+        const int ky = p.ky0[c] + 2 * jy, kx = p.kx0[c] + 2 * jx;
+        ((v4i*)p.out)[t] = ((const v4i*)p.wt)[((int64_t)(ci * p.kh + ky) * p.kw + kx) * p.cop16 + cc];
+    }
+}
+
+// the classes in order (py, px) = (0,0), (0,1), (1,0), (1,1): axes and weight offsets (bytes)
+struct SubpixPlan {
+    SubpixAxis ay[2], ax[2];
+    int64_t woff[4];
+};
+static SubpixPlan subpix_plan(const ConvGeom& g) {
+    SubpixPlan q;
+    for (int p = 0; p < 2; ++p) {
+        q.ay[p] = subpix_axis(g.kh, g.pt, p);
+        q.ax[p] = subpix_axis(g.kw, g.pl, p);
+    }
+    int64_t o = 0;
+    for (int c = 0; c < 4; ++c) {
+        q.woff[c] = o;
+        o += (int64_t)q.ay[c >> 1].n * q.ax[c & 1].n * g.c_in * g.cop;
+    }
+    return q;
+}
+hipError_t conv_dgrad_subpix_weights(const ConvGeom& g, const int8_t* wt, int8_t* out, hipStream_t st) {
+    if (!conv_dgrad_subpix_ok(g) || wt == nullptr || out == nullptr) return hipErrorInvalidValue;
+    const SubpixPlan q = subpix_plan(g);
+    SubpixW p;
+    p.wt = wt;
+    p.out = out;
+    p.ci = g.c_in;
+    p.kh = g.kh;
+    p.kw = g.kw;
+    p.cop16 = g.cop / 16;
+    p.off[0] = 0;
+    for (int c = 0; c < 4; ++c) {
+        p.ny[c] = q.ay[c >> 1].n;
+        p.nx[c] = q.ax[c & 1].n;
+        p.ky0[c] = q.ay[c >> 1].k0;
+        p.kx0[c] = q.ax[c & 1].k0;
+        p.off[c + 1] = p.off[c] + (int64_t)p.ny[c] * p.nx[c] * g.c_in * p.cop16;
+    }
+    if (p.off[4] == 0) return hipSuccess;
+    const int64_t blocks = std::min<int64_t>((p.off[4] + 255) / 256, 1024);
+    hipLaunchKernelGGL(subpix_weights_kernel, dim3((unsigned)blocks), dim3(256), 0, st, p);
+    return hipGetLastError();
+}
+
+// one pass over the four classes: MODE EPI_STORE (acc), EPI_AMAX (max only) or EPI_REQUANT (o)
+template <int MODE>
+static hipError_t subpix_pass(const ConvGeom& g, const GemmPlan& plan, const int8_t* dy, const int8_t* subw,
+                              int32_t* acc, uint32_t* amax, const ActOut* o, hipStream_t st) {
+    const SubpixPlan q = subpix_plan(g);
+    for (int c = 0; c < 4; ++c) {
+        const SubpixAxis& ay = q.ay[c >> 1];
+        const SubpixAxis& ax = q.ax[c & 1];
+        ConvGeom gc = g;
+        gc.h = g.h / 2;
+        gc.w = g.w / 2;
+        gc.kh = ay.n > 0 ? ay.n : 1;
+        gc.kw = ax.n > 0 ? ax.n : 1;
+        gc.sh = gc.sw = 1;
+        gc.pt = ay.pad;
+        gc.pl = ax.pad;
+        gc.dh = gc.dw = 1;
+        const int kc = ay.n * ax.n * g.cop / 16;  // 0: the class gets no tap (its dx is zero)
+        const int M = g.n * gc.h * gc.w;
+        GemmPlan p = plan;
+        p.splits = 1;
+        Epi e;
+        e.rmap.on = 1;
+        e.rmap.hc = gc.h;
+        e.rmap.wc = gc.w;
+        e.rmap.h = g.h;
+        e.rmap.w = g.w;
+        e.rmap.py = c >> 1;
+        e.rmap.px = c & 1;
+        e.amax = amax;
+        if (MODE == EPI_STORE) {
+            e.C = acc;
+            e.ldc = g.cip;
+        }
+        if (MODE == EPI_REQUANT) {
+            e.out = o->out;
+            e.ldo = g.cip;
+            e.relu = o->relu;
+            e.relu_mask = o->relu_mask;
+            e.exp_in = o->exp_in;
+            e.wscale = o->wscale;
+            e.exp_out = o->exp_out;
+        }
+        if (MODE == EPI_AMAX && kc == 0) continue;  // (a zero class adds nothing to the max)
+        const RowsK lb = rows_k(subw + q.woff[c], (int64_t)gc.kh * gc.kw * g.cop, g.c_in, kc);
+        const hipError_t r = launch_mode<ConvTaps<64>, RowsK, MODE, false>(p, conv_taps<64>(gc, dy, false), lb, M, g.cip,
+                                                                          kc, e, st);
+        if (r != hipSuccess) return r;
+    }
+    return hipSuccess;
+}
+
 hipError_t conv_dgrad_phase1(const ConvGeom& g, const int8_t* dy, const int8_t* wt, int32_t* acc, uint32_t* amax,
-                             void* ws, size_t ws_bytes, hipStream_t st) {
+                             void* ws, size_t ws_bytes, hipStream_t st, const int8_t* subw) {
     const int kc_total = g.kh * g.kw * g.cop / 16;
+    if (subw != nullptr && conv_dgrad_subpix_ok(g)) {  // (the strategy phase 2 will see: same workspace rule)
+        const GemmPlan p = plan_gemm(g.n * g.h * g.w, g.cip, kc_total, 64 / 16, kc_total * 16, true,
+                                     ws ? ws_bytes / 4 : 0, PLAN_DGRAD);
+        if (p.strat != STRAT_SPEC) {
+            if (p.strat == STRAT_RECOMPUTE) return subpix_pass<EPI_AMAX>(g, p, dy, subw, nullptr, amax, nullptr, st);
+            return subpix_pass<EPI_STORE>(g, p, dy, subw, acc, amax, nullptr, st);
+        }
+    }
     const RowsK lb = rows_k(wt, (int64_t)g.kh * g.kw * g.cop, g.c_in, kc_total);
     return with_dgrad_operand(g, dy, [&](const auto& la) {
         return act_phase1(PLAN_DGRAD, la, lb, g.n * g.h * g.w, g.cip, kc_total, acc, amax, (int32_t*)ws, ws_bytes / 4, st);
     });
 }
 hipError_t conv_dgrad_phase2(const ConvGeom& g, const int8_t* dy, const int8_t* wt, const int32_t* acc,
-                             const uint32_t* amax, const ActOut& o, size_t ws_bytes, hipStream_t st) {
+                             const uint32_t* amax, const ActOut& o, size_t ws_bytes, hipStream_t st,
+                             const int8_t* subw) {
     const int kc_total = g.kh * g.kw * g.cop / 16;
+    if (subw != nullptr && conv_dgrad_subpix_ok(g)) {
+        const GemmPlan p = plan_gemm(g.n * g.h * g.w, g.cip, kc_total, 64 / 16, kc_total * 16, true, ws_bytes / 4,
+                                     PLAN_DGRAD);
+        if (p.strat == STRAT_RECOMPUTE) {
+            if (o.pool.pool_out != nullptr || o.pool.dx != nullptr || o.out_p16 != nullptr) return hipErrorInvalidValue;
+            return subpix_pass<EPI_REQUANT>(g, p, dy, subw, nullptr, const_cast<uint32_t*>(amax), &o, st);
+        }
+    }
     const RowsK lb = rows_k(wt, (int64_t)g.kh * g.kw * g.cop, g.c_in, kc_total);
     return with_dgrad_operand(g, dy, [&](const auto& la) {
         return act_phase2(PLAN_DGRAD, la, lb, g.n * g.h * g.w, g.cip, kc_total, acc, amax, o, ws_bytes / 4, st);
@@ -3323,12 +3626,24 @@ hipError_t requant_grad(const int32_t* acc, int64_t n, const uint32_t* amax, int
 // launch instead measured +275 us per VGG-11 step: 1536-2048 arrivals on one counter.)
 __global__ void __launch_bounds__(256) sgd_combine_kernel(SgdJobs jobs) {
     const int chunks = jobs.cstart[jobs.n];
+    // a block's chunks ascend, so its jobs do too: the running max of the current job is
+    // published once when the block leaves it (one atomic per wave per job, not per chunk --
+    // ResNet-18's ~15 K chunks of per-chunk atomics on a few range words cost ~50 us)
+    uint32_t m = 0;
+    int cur = -1;
     for (int c = blockIdx.x; c < chunks; c += gridDim.x) {
         int j = 0;
         while (j + 1 < jobs.n && c >= jobs.cstart[j + 1]) ++j;
+        if (j != cur) {
+            if (cur >= 0) {
+                const uint32_t w = wave_max(m);
+                if ((threadIdx.x & 63) == 0) publish_max(const_cast<uint32_t*>(jobs.job[cur].amax), w);
+            }
+            cur = j;
+            m = 0;
+        }
         const SgdJob& J = jobs.job[j];
         const int64_t e = (int64_t)(c - jobs.cstart[j]) * 1024 + threadIdx.x * 4;
-        uint32_t m = 0;
         if (J.slab != nullptr && e < J.slab_n) {
             const v4i* base = (const v4i*)(J.slab + e);
             const int64_t st4 = J.slab_stride / 4;
@@ -3348,31 +3663,57 @@ __global__ void __launch_bounds__(256) sgd_combine_kernel(SgdJobs jobs) {
                 m = m > u ? m : u;
             }
         }
-        m = wave_max(m);
-        if ((threadIdx.x & 63) == 0) publish_max(const_cast<uint32_t*>(J.amax), m);
+    }
+    if (cur >= 0) {
+        const uint32_t w = wave_max(m);
+        if ((threadIdx.x & 63) == 0) publish_max(const_cast<uint32_t*>(jobs.job[cur].amax), w);
     }
 }
 
 __global__ void sgd_update_kernel(SgdJobs jobs, int total) {
     __shared__ int8_t T[64][64 + 4];
     // a block takes tiles b, b + gridDim, ...: one resident wave of blocks instead of a full
-    // wave plus a straggling partial one
-    // the range of a job's gradient is read once per job a block visits (a dependent global read
-    // and wave reduction per tile was a latency round trip of every iteration)
-    int last_j = -1, bw = 0;
-    for (int bb = blockIdx.x; bb < total; bb += gridDim.x) {
+    // wave plus a straggling partial one.  The next tile's operands are loaded before this one is
+    // finished, and a tile's loads are issued before its job's range is read (the range word's
+    // dependent read and wave reduction then overlap the operand fetch).
+    struct Tile {
+        int j, ci0, co0, k;
+    };
+    auto locate = [&](int bb) {
+        Tile t;
         int b = bb, j = 0;
         while (j + 1 < jobs.n && b >= jobs.start[j + 1]) ++j;
         const SgdJob& J = jobs.job[j];
-        if (j != last_j) {
-            bw = bitwidth_of(read_max(J.amax));
-            last_j = j;
-        }
         b -= jobs.start[j];
         const int tx = (J.cip + 63) / 64, ty = (J.cop + 63) / 64;
         const int k = b / (tx * ty), rem = b - k * tx * ty;
+        t.j = j;
+        t.ci0 = (rem % tx) * 64;
+        t.co0 = (rem / tx) * 64;
+        t.k = k;
+        return t;
+    };
+    int bb = blockIdx.x;
+    if (bb >= total) return;
+    Tile cur = locate(bb);
+    SgdTileIn cin, nin;  // (named, not an indexed pair: a dynamically indexed array would live in scratch)
+    sgd_tile_load(jobs.job[cur.j], cur.ci0, cur.co0, cur.k, cin);
+    int last_j = -1, bw = 0;
+    for (; bb < total; bb += gridDim.x) {
+        const int nb = bb + gridDim.x;
+        Tile nxt = cur;
+        if (nb < total) {
+            nxt = locate(nb);
+            sgd_tile_load(jobs.job[nxt.j], nxt.ci0, nxt.co0, nxt.k, nin);
+        }
+        if (cur.j != last_j) {
+            bw = bitwidth_of(read_max(jobs.job[cur.j].amax));
+            last_j = cur.j;
+        }
         if (bb != (int)blockIdx.x) __syncthreads();  // the previous tile's transposed reads are done
-        sgd_tile(J, bw, (rem % tx) * 64, (rem / tx) * 64, k, T);
+        sgd_tile_finish(jobs.job[cur.j], bw, cur.ci0, cur.co0, cur.k, cin, T);
+        cur = nxt;
+        cin = nin;
     }
 }
 
@@ -3412,41 +3753,54 @@ hipError_t sgd_update(const int32_t* acc, const uint32_t* amax, int rule, int co
 // The rest of the step: pool / relu-grad / loss-grad
 // =====================================================================================
 
-// NITI_Maxpool_Int8.cpp:24-72 (kernel clipped to the input); one thread per 16 channels.
+// NITI_Maxpool_Int8.cpp:24-72 (kernel clipped to the input); one thread per 16 channels (32-bit
+// index math: the host keeps the thread count below 2^31).  With `arg`, each window's first-max
+// position (ky * k + kx, in NITI_CPUPoolGrad_Int8.cpp:21-77's order) goes there too: the first
+// element equal to the max is the first one >= it, the backward pass's choice.
 __global__ void maxpool_kernel(const int8_t* __restrict__ x, int n, int h, int w, int cp, int k, int s, int p,
-                               int8_t* __restrict__ y, int oh, int ow) {
-    const int groups = cp / 16;
-    const int64_t total = (int64_t)n * oh * ow * groups;
+                               int8_t* __restrict__ y, int oh, int ow, int8_t* __restrict__ arg) {
+    const uint32_t groups = cp / 16;
+    const uint32_t total = (uint32_t)n * oh * ow * groups;
     const int kh = k < h ? k : h, kw = k < w ? k : w;
-    for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
-        int64_t r = t;
+    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
+        uint32_t r = t;
         const int gi = (int)(r % groups);
         r /= groups;
-        const int ox = (int)(r % ow);
-        r /= ow;
-        const int oy = (int)(r % oh);
-        const int b = (int)(r / oh);
+        const int ox = (int)(r % (uint32_t)ow);
+        r /= (uint32_t)ow;
+        const int oy = (int)(r % (uint32_t)oh);
+        const int b = (int)(r / (uint32_t)oh);
         const int sx0 = ox * s - p, sy0 = oy * s - p;
-        v16c m;
+        v16c m, a;
 #pragma unroll
-        for (int j = 0; j < 16; ++j) m[j] = (signed char)-128;
+        for (int j = 0; j < 16; ++j) {
+            m[j] = (signed char)-128;
+            a[j] = (signed char)-1;
+        }
         for (int yy = max(0, -sy0); yy < min(kh, h - sy0); ++yy)
             for (int xx = max(0, -sx0); xx < min(kw, w - sx0); ++xx) {
                 const v16c v = *(const v16c*)(x + (((int64_t)b * h + sy0 + yy) * w + sx0 + xx) * cp + gi * 16);
+                const signed char pos = (signed char)(yy * k + xx);
 #pragma unroll
-                for (int j = 0; j < 16; ++j) m[j] = v[j] > m[j] ? v[j] : m[j];
+                for (int j = 0; j < 16; ++j) {
+                    const bool take = a[j] < 0 || v[j] > m[j];
+                    m[j] = take ? v[j] : m[j];
+                    a[j] = take ? pos : a[j];
+                }
             }
-        *(v16c*)(y + (((int64_t)b * oh + oy) * ow + ox) * cp + gi * 16) = m;
+        *(v16c*)(y + (int64_t)t * 16) = m;
+        if (arg != nullptr) *(v16c*)(arg + (int64_t)t * 16) = a;
     }
 }
 
 hipError_t maxpool_nhwc16(const int8_t* x, int n, int h, int w, int cp, int k, int s, int p, int8_t* y, int oh, int ow,
-                          hipStream_t st) {
+                          hipStream_t st, int8_t* arg) {
     const int64_t total = (int64_t)n * oh * ow * (cp / 16);
+    if (total >= ((int64_t)1 << 31) || cp % 16 != 0) return hipErrorInvalidValue;
     int64_t blocks = (total + 255) / 256;
     if (blocks > 4096) blocks = 4096;
     if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL(maxpool_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, n, h, w, cp, k, s, p, y, oh, ow);
+    hipLaunchKernelGGL(maxpool_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, n, h, w, cp, k, s, p, y, oh, ow, arg);
     return hipGetLastError();
 }
 
@@ -3613,16 +3967,16 @@ __global__ void maxpool_argmax_kernel(const int8_t* __restrict__ x, const int8_t
 __global__ void maxpool_grad_gather_kernel(const int8_t* __restrict__ x, const int8_t* __restrict__ arg,
                                            const int8_t* __restrict__ dy, int n, int h, int w, int cp, int k, int s,
                                            int p, int oh, int ow, int relu, int8_t* __restrict__ dx) {
-    const int groups = cp / 16;
-    const int64_t total = (int64_t)n * h * w * groups;
-    for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
-        int64_t r = t;
+    const uint32_t groups = cp / 16;
+    const uint32_t total = (uint32_t)n * h * w * groups;  // < 2^31 (host)
+    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
+        uint32_t r = t;
         const int gi = (int)(r % groups);
         r /= groups;
-        const int ix = (int)(r % w);
-        r /= w;
-        const int iy = (int)(r % h);
-        const int b = (int)(r / h);
+        const int ix = (int)(r % (uint32_t)w);
+        r /= (uint32_t)w;
+        const int iy = (int)(r % (uint32_t)h);
+        const int b = (int)(r / (uint32_t)h);
         v16c acc;
 #pragma unroll
         for (int j = 0; j < 16; ++j) acc[j] = 0;
@@ -3641,11 +3995,11 @@ __global__ void maxpool_grad_gather_kernel(const int8_t* __restrict__ x, const i
                     if (av[j] == me) acc[j] = (signed char)(acc[j] + dv[j]);
             }
         if (relu) {
-            const v16c xv = *(const v16c*)(x + t * 16);
+            const v16c xv = *(const v16c*)(x + (int64_t)t * 16);
 #pragma unroll
             for (int j = 0; j < 16; ++j) acc[j] = xv[j] > 0 ? acc[j] : (signed char)0;
         }
-        *(v16c*)(dx + t * 16) = acc;
+        *(v16c*)(dx + (int64_t)t * 16) = acc;
     }
 }
 
@@ -3653,10 +4007,23 @@ hipError_t maxpool_relu_grad_ws(const int8_t* x, const int8_t* y, const int8_t* 
                                 int s, int p, int oh, int ow, int relu, int8_t* ws, int8_t* dx, hipStream_t st) {
     if (cp % 16 != 0 || k <= 0 || k > 11 || s <= 0 || ws == nullptr) return hipErrorInvalidValue;
     const int64_t tw = (int64_t)n * oh * ow * (cp / 16), tx = (int64_t)n * h * w * (cp / 16);
+    if (tx >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
     auto blocks = [](int64_t t) { return (unsigned)std::max<int64_t>(1, std::min<int64_t>((t + 255) / 256, 8192)); };
     hipLaunchKernelGGL(maxpool_argmax_kernel, dim3(blocks(tw)), dim3(256), 0, st, x, y, n, h, w, cp, k, s, p, oh, ow, ws);
     hipLaunchKernelGGL(maxpool_grad_gather_kernel, dim3(blocks(tx)), dim3(256), 0, st, x, ws, dy, n, h, w, cp, k, s, p,
                        oh, ow, relu, dx);
+    return hipGetLastError();
+}
+
+// the same gradient from the first-max positions the forward maxpool_nhwc16 wrote (`arg`): one pass
+hipError_t maxpool_relu_grad_arg(const int8_t* x, const int8_t* arg, const int8_t* dy, int n, int h, int w, int cp,
+                                 int k, int s, int p, int oh, int ow, int relu, int8_t* dx, hipStream_t st) {
+    if (cp % 16 != 0 || k <= 0 || k > 11 || s <= 0 || arg == nullptr) return hipErrorInvalidValue;
+    const int64_t tx = (int64_t)n * h * w * (cp / 16);
+    if (tx >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
+    const unsigned blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>((tx + 255) / 256, 8192));
+    hipLaunchKernelGGL(maxpool_grad_gather_kernel, dim3(blocks), dim3(256), 0, st, x, arg, dy, n, h, w, cp, k, s, p, oh,
+                       ow, relu, dx);
     return hipGetLastError();
 }
 

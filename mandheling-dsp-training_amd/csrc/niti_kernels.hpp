@@ -13,6 +13,7 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../../include/niti_hip.h"
 
@@ -118,6 +119,15 @@ hipError_t conv_wgrad_acc(const ConvGeom& g, const int8_t* x_nhwc16, const int8_
 hipError_t splitk_reduce_linear(const int32_t* slab, int splits, int64_t n, int64_t stride, int32_t* C,
                                 uint32_t* amax, hipStream_t st);
 // ---- residual add / global sum pool (niti_resnet.hip) ------------------------------------
+// residual_add (range) + residual_requant in one launch with an in-kernel grid barrier (single
+// device; bar: ROWCONV_BAR_WORDS zeroed words, epoch: this state's launch count, 1 on the first;
+// a barrier timeout sets *err).  hipErrorNotSupported when the grid cannot be resident at once
+// (the caller then takes the two launches)
+hipError_t residual_fused(const int8_t* a, const int8_t* ea, const int8_t* b, const int8_t* eb, int64_t n, int8_t* ez,
+                          int8_t* exp_out, int relu, int8_t* out, uint32_t* bar, uint32_t epoch, uint32_t* err,
+                          hipStream_t st, const int8_t* relu_mask = nullptr);
+// workgroups of 256 threads of kernel f the device holds at once (0 without a device)
+int resident_wgs(const void* f);
 // z = aligned a + b (int32, n % 16 == 0 elements), its exponent into ez, max|z| into amax
 hipError_t residual_add(const int8_t* a, const int8_t* ea, const int8_t* b, const int8_t* eb, int64_t n,
                         int32_t* z, int8_t* ez, uint32_t* amax, hipStream_t st);
@@ -210,11 +220,18 @@ bool conv_dgrad_phase2_separate(const ConvGeom& g, size_t ws_bytes);
 // exponent and redoes the GEMM, requantised with the max, only when its bit width differs -- on a
 // hit every block of B exits at once: one GEMM pass and no int32 tensor.  slot: the layer phase's
 // own GEMM_SPEC_SLOT_WORDS zeroed device words ([0] hint, [1] the bit width A used, [2] launches B
-// redid, [3] misses B settled from an alternate).  alt (may be null; the same scratch for both
+// redid, [3] misses B settled from an alternate, [4] the alternates' window: A writes them only
+// within GEMM_SPEC_ALT_PAIRS pairs of a miss).  alt (may be null; the same scratch for both
 // passes, *_alt_bytes): launch A also writes the output requantised one bit width below and above
 // its guess, and launch B settles a +-1 change by copying one instead of redoing the GEMM.  ActOut
 // without pool / P16 fusion.  Results equal phase 1 + phase 2's.
 constexpr int GEMM_SPEC_SLOT_WORDS = 32;  // one 128-byte line per slot
+constexpr int GEMM_SPEC_ALT_PAIRS = 8;
+// whether the model autotuners time the speculative pair (NITI_TUNE_SPEC=1)
+inline bool tune_spec() {
+    static const bool on = getenv("NITI_TUNE_SPEC") && atoi(getenv("NITI_TUNE_SPEC")) == 1;
+    return on;
+}
 bool conv_fwd_spec_ok(const ConvGeom& g);    // the plan (autotuned / forced) is STRAT_SPEC
 bool conv_dgrad_spec_ok(const ConvGeom& g);
 void gemm_speculate_bias(int bias);  // diagnostics: A guesses the hint + bias (niti_diag_gemm_speculate)
@@ -228,10 +245,17 @@ hipError_t conv_fwd_phase1(const ConvGeom& g, const int8_t* x, const int8_t* w, 
                            void* ws, size_t ws_bytes, hipStream_t st);
 hipError_t conv_fwd_phase2(const ConvGeom& g, const int8_t* x, const int8_t* w, const int32_t* acc,
                            const uint32_t* amax, const ActOut& o, size_t ws_bytes, hipStream_t st);
+// subw (may be null): the stride-2 sub-pixel form's class weights (conv_dgrad_subpix_weights, kept
+// current by NITI_SGD through SgdJob::subw) where conv_dgrad_subpix_ok: four class GEMMs over dy
 hipError_t conv_dgrad_phase1(const ConvGeom& g, const int8_t* dy, const int8_t* wt, int32_t* acc, uint32_t* amax,
-                             void* ws, size_t ws_bytes, hipStream_t st);
+                             void* ws, size_t ws_bytes, hipStream_t st, const int8_t* subw = nullptr);
 hipError_t conv_dgrad_phase2(const ConvGeom& g, const int8_t* dy, const int8_t* wt, const int32_t* acc,
-                             const uint32_t* amax, const ActOut& o, size_t ws_bytes, hipStream_t st);
+                             const uint32_t* amax, const ActOut& o, size_t ws_bytes, hipStream_t st,
+                             const int8_t* subw = nullptr);
+bool conv_dgrad_subpix_ok(const ConvGeom& g);
+size_t conv_dgrad_subpix_bytes(const ConvGeom& g);
+// the class weights [class (py, px)][ci][taps ky = ky0 + 2 j][taps kx][cop] from IHWO16 wT
+hipError_t conv_dgrad_subpix_weights(const ConvGeom& g, const int8_t* wt, int8_t* out, hipStream_t st);
 
 // ---- forward conv of stride-1 pad-1 3x3 layers with the rescale fused (niti_rowconv.hip) -------
 // Activations in C32 [n][ceil(C/32)][H][W][32], weights in WF [Co/32][Ci/32][9][2][32][16] (a 1 KiB
@@ -390,6 +414,10 @@ struct SgdJob {
     // forward's and the input gradient's fragment-major copies (may be null; kk == 9)
     int8_t* wf = nullptr;
     int8_t* wft = nullptr;
+    // a stride-2 layer's sub-pixel class weights (conv_dgrad_subpix_weights' layout), or null; pads
+    // of the conv (the class of tap (ky, kx) is ((ky - pt) & 1, (kx - pl) & 1)), kh / kw = kk split
+    int8_t* subw = nullptr;
+    int sub_kw = 0, sub_kh = 0, sub_pt = 0, sub_pl = 0;
     // a deferred split-K combine (the P16 weight gradient's slabs, conv_wgrad_p16 with defer):
     // sgd_update_many first sums `splits` C-shaped slabs `slab_stride` elements apart into acc
     // (slab_n elements) with its range into amax, for every such job in one launch
@@ -405,14 +433,21 @@ struct SgdJobs {
     int n;
 };
 hipError_t sgd_update_many(const SgdJob* jobs, int n, hipStream_t st);
+// a fully connected layer (1x1 map): its weight gradient's range (pass 0), then the gradient
+// recomputed with job j's NITI_SGD step in the GEMM epilogue (pass 1; j.acc, wf, wft and the
+// slab fields unused) -- no int32 gradient tensor
+bool conv_wgrad_fc_sgd_ok(const ConvGeom& g);
+hipError_t conv_wgrad_fc_sgd(const ConvGeom& g, const int8_t* x, const int8_t* dy, uint32_t* amax, const SgdJob& j,
+                             int pass, hipStream_t st);
 // exponent of a requantised weight gradient: bw - rule (0 for an all-zero gradient)
 hipError_t grad_exponent(const uint32_t* amax, int rule, int8_t* out, hipStream_t st);
 hipError_t sgd_update(const int32_t* acc, const uint32_t* amax, int rule, int co, int ci, int kk, int cip, int cop,
                       int8_t* w, int8_t* wT, int8_t* g_out, hipStream_t st);
 
 // ---- the rest of the NITI step -----------------------------------------
+// (arg: each window's first-max position too, [n][oh][ow][cp] bytes, for maxpool_relu_grad_arg)
 hipError_t maxpool_nhwc16(const int8_t* x, int n, int h, int w, int cp, int k, int s, int p, int8_t* y,
-                          int oh, int ow, hipStream_t st);
+                          int oh, int ow, hipStream_t st, int8_t* arg = nullptr);
 // dx = maxpool_grad(x, y, dy) then, if relu, dx = x > 0 ? dx : 0 (x is the relu output)
 hipError_t maxpool_relu_grad_nhwc16(const int8_t* x, const int8_t* y, const int8_t* dy, int n, int h,
                                     int w, int cp, int k, int s, int p, int oh, int ow, int relu,
@@ -422,6 +457,9 @@ hipError_t relu_grad_nhwc16(const int8_t* x, const int8_t* dy, int64_t n, int8_t
 // position, then a gather per input pixel): for overlapping windows (ResNet's 3x3 / 2 stem pool)
 hipError_t maxpool_relu_grad_ws(const int8_t* x, const int8_t* y, const int8_t* dy, int n, int h, int w, int cp, int k,
                                 int s, int p, int oh, int ow, int relu, int8_t* ws, int8_t* dx, hipStream_t st);
+// the same from the forward's first-max positions (maxpool_nhwc16 with arg): one pass
+hipError_t maxpool_relu_grad_arg(const int8_t* x, const int8_t* arg, const int8_t* dy, int n, int h, int w, int cp,
+                                 int k, int s, int p, int oh, int ow, int relu, int8_t* dx, hipStream_t st);
 // logits int8 [batch][ld] (first `classes` used), labels int32 [batch] (class index);
 // out int8 [batch][ld] (padded lanes zeroed).  classes <= 2048 (one thread per sample up to 16,
 // one block per sample above).  NITI_CPULossGrad_Int8.cpp:81-200.

@@ -154,6 +154,7 @@ struct Layer {
     int32_t* wslab = nullptr;
     size_t wslab_bytes = 0;
     SgdJob defer{};
+    bool fc_sgd = false;  // this step's weight gradient took the fused NITI_SGD form (pass 1 in run())
     int8_t* g8 = nullptr;    // int8 weight gradient OHWI16
     int8_t* exp = nullptr;   // exponent of this layer's output
     const int8_t* in = nullptr;  // NHWC16 input (previous output or x0)
@@ -212,6 +213,14 @@ struct Model {
     std::vector<char> xc32_valid;
     uint32_t* rc_err = nullptr;
     bool in_step = false;  // run(): weight gradients may defer their combine to the update launch
+    // a fully connected layer's weight gradient as a range pass plus a recompute that applies
+    // NITI_SGD in its epilogue (conv_wgrad_fc_sgd): single device, inside run() (NITI_FC_SGD=0: off)
+    bool fc_sgd_layer(int i) const {
+        static const bool off = getenv("NITI_FC_SGD") && atoi(getenv("NITI_FC_SGD")) == 0;
+        const ConvGeom& g = L[i].g;
+        return in_step && !off && !dp() && !tuning && conv_wgrad_fc_sgd_ok(g) &&
+               !(head_layer(i) && g.c_out <= 32 && g.cip % 32 == 0) && wgrad_p16_splits(i) == 0;
+    }
     bool defer_combine() const {
         static const bool off = getenv("NITI_DIAG_SGD_COMBINE") && atoi(getenv("NITI_DIAG_SGD_COMBINE")) == 0;
         return in_step && !off && !dp() && !capturing && !tuning;
@@ -959,6 +968,12 @@ int Model::wgrad_layer(int i, hipStream_t st) {
         probe(i, 2, false, st);
         return NITI_NO_ERROR;
     }
+    l.fc_sgd = fc_sgd_layer(i);
+    if (l.fc_sgd) {  // its range now; the recompute with the update after the backward pass
+        l.defer = SgdJob{};
+        MTRY(conv_wgrad_fc_sgd(g, l.in, l.dy, rng(i, 2), SgdJob{}, 0, st));
+        return NITI_NO_ERROR;
+    }
     if (const int s = wgrad_p16_splits(i)) {
         // P16 weight gradient: x (unless run() converted every input already) and dy to pixel
         // blocks, then the register-fed kernel (+ its split-K reduce); the probe times the kernel
@@ -1294,8 +1309,13 @@ int Model::autotune(hipStream_t st, int reps) {
                 if (act) {
                     c.strat = 1;
                     cands.push_back(c);
-                    c.strat = 3;  // the speculative pair
-                    cands.push_back(c);
+                    // the speculative pair only on request (NITI_TUNE_SPEC=1): timed here on one
+                    // batch its guess always holds, but over a run of batches 60-80 % of the deep
+                    // layers' pairs miss (profiles/r05_gemm_spec.txt) and then cost more than STORE
+                    if (tune_spec()) {
+                        c.strat = 3;
+                        cands.push_back(c);
+                    }
                 }
                 for (int s : split_opts) {
                     if (s > steps / 2 || plan_slab_bytes(key.M, key.N, s) > wsb) break;
@@ -1461,7 +1481,14 @@ int Model::run(const int8_t* x_nchw, int exp_in, const uint8_t* images, const in
         MTRY(hipEventRecord(ev_side, side));
         MTRY(hipStreamWaitEvent(st, ev_side, 0));
     }
-    MTRY(sgd_update_many(jobs, nl, st));  // (+ the deferred combines) also rewrites the fragment-major weight copies
+    // the fully connected layers that took the fused form update in their own recompute pass
+    SgdJob many[SGD_MAX_JOBS];
+    int n_many = 0;
+    for (int i = 0; i < nl; ++i)
+        if (!L[i].fc_sgd) many[n_many++] = jobs[i];
+    MTRY(sgd_update_many(many, n_many, st));  // (+ the deferred combines) also rewrites the fragment-major weight copies
+    for (int i = 0; i < nl; ++i)
+        if (L[i].fc_sgd) MTRY(conv_wgrad_fc_sgd(L[i].g, L[i].in, L[i].dy, rng(i, 2), jobs[i], 1, st));
     return NITI_NO_ERROR;
 }
 

@@ -15,7 +15,9 @@
 // (residual_requant in niti_kernels.hip) takes the range in a pass without z and recomputes z
 // from the int8 operands while requantising: 2 x 2 int8 reads instead of an int32 write + read.
 #include "niti_device.hpp"
+#include "niti_gridbar.hpp"
 #include "niti_kernels.hpp"
+#include "niti_sgd.hpp"
 
 namespace niti {
 
@@ -61,6 +63,126 @@ hipError_t residual_add(const int8_t* a, const int8_t* ea, const int8_t* b, cons
     blocks = blocks < 1 ? 1 : blocks > 2048 ? 2048 : blocks;
     hipLaunchKernelGGL(residual_add_kernel, dim3((unsigned)blocks), dim3(256), 0, st, a, ea, b, eb, n16, z, ez, amax);
     return hipGetLastError();
+}
+
+// The single-launch form of residual_add + residual_requant (single device): every thread keeps
+// its VPT 16-byte chunks of both operands in registers, the grid barrier of the fused row kernels
+// (niti_gridbar.hpp) folds the tensor's range into its arrival, and z is recomputed from the
+// registers and requantised -- one read of a and b, one write of the output, one launch.  Measured
+// slower than the two launches on MI355X (ResNet-18 batch 128: 17.5 vs 14.0 us at 401 K chunks,
+// 11-13 vs 9.9 us at 200 K; a kernel boundary costs ~1 us here, the grid barrier and the
+// register-bound occupancy more), so ResNetModel runs it only with NITI_RES_FUSED=1.
+struct ResFused {
+    const int8_t *a, *ea, *b, *eb;
+    int64_t n16;
+    int8_t *ez, *exp_out;
+    int relu;
+    const int8_t* relu_mask;
+    int8_t* out;
+    uint32_t* bar;
+    uint32_t epoch;
+    uint32_t* err;
+};
+
+// byte k of a packed word, sign-extended
+__device__ __forceinline__ int32_t sbyte(uint32_t w, int k) { return (int32_t)(w << (24 - 8 * k)) >> 24; }
+
+template <int VPT, bool MASK>
+__global__ void __launch_bounds__(256) residual_fused_kernel(ResFused p) {
+    const int xa = *p.ea, xb = *p.eb;
+    const bool a_hi = xa >= xb;
+    const int diff = a_hi ? xa - xb : xb - xa;
+    const int d = diff < 23 ? diff : 23, r = diff - d;
+    const int64_t stride = (int64_t)gridDim.x * 256, i0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    // the operands stay packed (4 words per 16 bytes: 12 VGPRs per chunk with the mask), so the grid
+    // that holds a ResNet-18 block output at batch 128 fits the GPU at once
+    v4i hi[VPT], lo[VPT], mk[MASK ? VPT : 1];
+    uint32_t m = 0;
+#pragma unroll
+    for (int v = 0; v < VPT; ++v) {
+        const int64_t i = i0 + v * stride;
+        if (i < p.n16) {
+            const v4i va = ((const v4i*)p.a)[i], vb = ((const v4i*)p.b)[i];
+            hi[v] = a_hi ? va : vb;
+            lo[v] = a_hi ? vb : va;
+            if (MASK) mk[MASK ? v : 0] = ((const v4i*)p.relu_mask)[i];  // lands during the barrier
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const uint32_t u = uabs32(residual_z(sbyte(hi[v][q], k), sbyte(lo[v][q], k), d, r));
+                    m = m > u ? m : u;
+                }
+        }
+    }
+    __shared__ uint32_t red[4];
+    __shared__ int gbw;
+    m = wave_max(m);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        const int lane = threadIdx.x;
+        const uint32_t bm = max(max(red[0], red[1]), max(red[2], red[3]));
+        grid_bw_arrive(p.bar, p.epoch, bitwidth_of(bm), lane);
+        const int g = grid_bw_wait(p.bar, p.epoch, p.err, BAR_SPIN_LIMIT, 0u, lane);
+        if (lane == 0) gbw = g;
+    }
+    __syncthreads();
+    const int shift = gbw - 7;  // as residual_requant_kernel (niti_kernels.hip)
+    const int s = shift > 1 ? shift : 2;
+    const bool raw = shift <= 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        const int e_z = (a_hi ? xa : xb) - d;
+        if (p.ez != nullptr) *p.ez = (int8_t)e_z;
+        if (p.exp_out != nullptr) *p.exp_out = (int8_t)(e_z + (shift > 1 ? shift : (shift == 1 ? 2 : 0)));
+    }
+#pragma unroll
+    for (int v = 0; v < VPT; ++v) {
+        const int64_t i = i0 + v * stride;
+        if (i < p.n16) {
+            v4i q;
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                uint32_t word = 0;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const int32_t z = residual_z(sbyte(hi[v][w], k), sbyte(lo[v][w], k), d, r);
+                    int32_t o = raw ? (int32_t)(int8_t)z : psto_fast(z, s);
+                    if (p.relu && o < 0) o = 0;
+                    if (MASK && sbyte(mk[MASK ? v : 0][w], k) <= 0) o = 0;
+                    word |= ((uint32_t)o & 0xffu) << (8 * k);
+                }
+                q[w] = (int)word;
+            }
+            ((v4i*)p.out)[i] = q;
+        }
+    }
+}
+
+hipError_t residual_fused(const int8_t* a, const int8_t* ea, const int8_t* b, const int8_t* eb, int64_t n, int8_t* ez,
+                          int8_t* exp_out, int relu, int8_t* out, uint32_t* bar, uint32_t epoch, uint32_t* err,
+                          hipStream_t st, const int8_t* relu_mask) {
+    if (n < 0 || n % 16 != 0 || !a || !b || !ea || !eb || !out || !bar || !err || epoch == 0) return hipErrorInvalidValue;
+    const int64_t n16 = n / 16;
+    ResFused p{a, ea, b, eb, n16, ez, exp_out, relu, relu_mask, out, bar, epoch, err};
+    // the smallest per-thread depth whose grid is resident at once (the barrier needs every block)
+    auto try_vpt = [&](auto vc, auto mc) -> hipError_t {
+        constexpr int V = decltype(vc)::value;
+        constexpr bool MK = decltype(mc)::value;
+        const void* f = (const void*)residual_fused_kernel<V, MK>;
+        const int64_t blocks = std::max<int64_t>(1, (n16 + 256 * V - 1) / (256 * V));
+        if (blocks > resident_wgs(f)) return hipErrorNotSupported;
+        hipLaunchKernelGGL((residual_fused_kernel<V, MK>), dim3((unsigned)blocks), dim3(256), 0, st, p);
+        return hipGetLastError();
+    };
+    auto over = [&](auto mc) -> hipError_t {
+        hipError_t r = try_vpt(std::integral_constant<int, 4>(), mc);
+        if (r == hipErrorNotSupported) r = try_vpt(std::integral_constant<int, 5>(), mc);
+        if (r == hipErrorNotSupported) r = try_vpt(std::integral_constant<int, 6>(), mc);
+        if (r == hipErrorNotSupported) r = try_vpt(std::integral_constant<int, 8>(), mc);
+        return r;
+    };
+    return relu_mask != nullptr ? over(std::true_type()) : over(std::false_type());
 }
 
 // acc[img][c] = sum over the image's hw pixels of x[img][p][c] (NHWC16, cp % 16 == 0): one thread

@@ -103,6 +103,8 @@ int ResNetModel::build(int batch_, int in_hw_, int classes_) {
     size_t acc_elems = 0, grad_elems = 0;
     rc_err = (uint32_t*)ws.alloc(64);
     if (!rc_err || hipMemset(rc_err, 0, 64) != hipSuccess) return NITI_OUT_OF_MEMORY;
+    res_bar = (uint32_t*)ws.alloc(ROWCONV_BAR_WORDS * 4);
+    if (!res_bar || hipMemset(res_bar, 0, ROWCONV_BAR_WORDS * 4) != hipSuccess) return NITI_OUT_OF_MEMORY;
     for (int i = 0; i < nl; ++i) {
         RConv& c = C[i];
         const ConvGeom& g = c.g;
@@ -120,6 +122,10 @@ int ResNetModel::build(int batch_, int in_hw_, int classes_) {
         if (i > 0) {
             c.wT = A8((size_t)g.c_in * g.kh * g.kw * g.cop);
             if (!c.wT) return NITI_OUT_OF_MEMORY;
+            if (conv_dgrad_subpix_ok(g)) {  // the stride-2 input gradient's class weights
+                c.subw = A8(conv_dgrad_subpix_bytes(g));
+                if (!c.subw) return NITI_OUT_OF_MEMORY;
+            }
         }
         grad_elems += (size_t)c.w_elems();
         acc_elems = std::max(acc_elems, (size_t)n * g.oh * g.ow * g.cop);
@@ -398,9 +404,10 @@ int ResNetModel::dgrad_conv(int i, hipStream_t st) {
         if (dp && exact) RTRY(coll->allreduce(rng(i, 1), MAX_WORDS, COLL_MAX_U32, st));
         RTRY(conv_dgrad_spec(g, c.dy, c.wT, rng(i, 1), o, slot, 1, st, alt));
     } else {
-        RTRY(conv_dgrad_phase1(g, c.dy, c.wT, acc, rng(i, 1), slab, slab_bytes, st));
+        const int8_t* subw = subpix_on() ? c.subw : nullptr;  // stride 2: four sub-pixel class GEMMs
+        RTRY(conv_dgrad_phase1(g, c.dy, c.wT, acc, rng(i, 1), slab, slab_bytes, st, subw));
         if (dp && exact) RTRY(coll->allreduce(rng(i, 1), MAX_WORDS, COLL_MAX_U32, st));
-        RTRY(conv_dgrad_phase2(g, c.dy, c.wT, acc, rng(i, 1), o, slab_bytes, st));
+        RTRY(conv_dgrad_phase2(g, c.dy, c.wT, acc, rng(i, 1), o, slab_bytes, st, subw));
     }
     probe(i, 1, false, st);
     return NITI_NO_ERROR;
@@ -444,6 +451,15 @@ int ResNetModel::residual_fwd(int k, hipStream_t st) {
     const RConv& cb = C[b.b];
     const int8_t* sc = b.p >= 0 ? C[b.p].y : b.u;
     const int8_t* es = b.p >= 0 ? C[b.p].y_exp : b.u_exp;
+    if (res_fused_on()) {  // one launch: the range through the in-kernel grid barrier
+        const hipError_t e = residual_fused(cb.y, cb.y_exp, sc, es, b.out_elems, b.ez, b.out_exp, 1, b.out, res_bar,
+                                            ++res_epoch, rc_err, st);
+        if (e != hipErrorNotSupported) {
+            RTRY(e);
+            return NITI_NO_ERROR;
+        }
+        --res_epoch;
+    }
     RTRY(residual_add(cb.y, cb.y_exp, sc, es, b.out_elems, nullptr, nullptr, rng_blk(k, 0), st));
     if (dp() && exact) RTRY(coll->allreduce(rng_blk(k, 0), MAX_WORDS, COLL_MAX_U32, st));
     RTRY(residual_requant(cb.y, cb.y_exp, sc, es, b.out_elems, rng_blk(k, 0), b.ez, b.out_exp, 1, b.out, st));
@@ -457,6 +473,15 @@ int ResNetModel::residual_bwd(int k, hipStream_t st) {
     const RConv& ca = C[b.a];
     const int8_t* s = b.p >= 0 ? b.dus : b.dz;
     const int8_t* es = b.p >= 0 ? C[b.p].dx_exp : b.dz_exp;
+    if (res_fused_on()) {
+        const hipError_t e = residual_fused(b.dua, ca.dx_exp, s, es, b.in_elems, b.ezb, b.du_exp, 0, b.du, res_bar,
+                                            ++res_epoch, rc_err, st, k > 0 ? B[k - 1].out : nullptr);
+        if (e != hipErrorNotSupported) {
+            RTRY(e);
+            return NITI_NO_ERROR;
+        }
+        --res_epoch;
+    }
     RTRY(residual_add(b.dua, ca.dx_exp, s, es, b.in_elems, nullptr, nullptr, rng_blk(k, 1), st));
     if (dp() && exact) RTRY(coll->allreduce(rng_blk(k, 1), MAX_WORDS, COLL_MAX_U32, st));
     RTRY(residual_requant(b.dua, ca.dx_exp, s, es, b.in_elems, rng_blk(k, 1), b.ezb, b.du_exp, 0, b.du, st,
@@ -555,7 +580,7 @@ int ResNetModel::run(const int8_t* x_nchw, int exp_in, const uint8_t* images, co
     int rc = fwd_conv(0, st);
     if (rc != NITI_NO_ERROR) return rc;
     const int ph = C[B[0].a].g.h;  // the stem's pooled size
-    RTRY(maxpool_nhwc16(C[0].y, n, stem.oh, stem.ow, 64, 3, 2, 1, p0, ph, ph, st));
+    RTRY(maxpool_nhwc16(C[0].y, n, stem.oh, stem.ow, 64, 3, 2, 1, p0, ph, ph, st, pool_ws));  // + first-max positions
     for (int k = 0; k < (int)B.size(); ++k) {
         const RBlock& b = B[k];
         if ((rc = fwd_conv(b.a, st)) != NITI_NO_ERROR) return rc;
@@ -600,7 +625,7 @@ int ResNetModel::run(const int8_t* x_nchw, int exp_in, const uint8_t* images, co
     }
     // the stem: overlapping 3x3 / 2 max-pool gradient (first max wins) with the relu gradient, then
     // its weight gradient over the im2col
-    RTRY(maxpool_relu_grad_ws(C[0].y, p0, B[0].du, n, stem.oh, stem.ow, 64, 3, 2, 1, ph, ph, 1, pool_ws, d0, st));
+    RTRY(maxpool_relu_grad_arg(C[0].y, pool_ws, B[0].du, n, stem.oh, stem.ow, 64, 3, 2, 1, ph, ph, 1, d0, st));
     if ((rc = wg(0)) != NITI_NO_ERROR) return rc;
     if (dp) {  // every bucket summed and ranged before the update
         if (!shared_comm) {
@@ -620,6 +645,13 @@ int ResNetModel::run(const int8_t* x_nchw, int exp_in, const uint8_t* images, co
                          i > 0 && !rows_dg_on(i) ? c.wT : nullptr, keep_grads ? c.g8 : nullptr};
         jobs[i].wf = c.rows ? c.wf : nullptr;
         jobs[i].wft = c.rows_dg ? c.wft : nullptr;
+        if (c.subw != nullptr) {  // the stride-2 input gradient's sub-pixel class weights
+            jobs[i].subw = c.subw;
+            jobs[i].sub_kh = g.kh;
+            jobs[i].sub_kw = g.kw;
+            jobs[i].sub_pt = g.pt;
+            jobs[i].sub_pl = g.pl;
+        }
         if (c.defer.slab != nullptr) {  // this conv's split-K slabs, combined in the update launch
             jobs[i].slab = c.defer.slab;
             jobs[i].splits = c.defer.splits;
@@ -739,8 +771,13 @@ int ResNetModel::autotune(hipStream_t st, int reps) {
                 if (act) {
                     c.strat = 1;
                     cands.push_back(c);
-                    c.strat = 3;  // the speculative pair
-                    cands.push_back(c);
+                    // the speculative pair only on request (NITI_TUNE_SPEC=1): timed here on one
+                    // batch its guess always holds, but over a run of batches 60-80 % of the deep
+                    // layers' pairs miss (profiles/r05_gemm_spec.txt) and then cost more than STORE
+                    if (tune_spec()) {
+                        c.strat = 3;
+                        cands.push_back(c);
+                    }
                 }
                 for (int s : split_opts) {
                     if (s > steps / 2 || plan_slab_bytes(key.M, key.N, s) > wsb) break;
@@ -804,6 +841,7 @@ int ResNetModel::refresh_copies(int i, hipStream_t st) {
         return NITI_NO_EXECUTION;
     if (c.rows && weights_to_wf(c.w, g.c_out, g.c_in, g.cip, false, c.wf, st) != hipSuccess) return NITI_NO_EXECUTION;
     if (c.rows_dg && weights_to_wf(c.w, g.c_out, g.c_in, g.cip, true, c.wft, st) != hipSuccess) return NITI_NO_EXECUTION;
+    if (c.subw && conv_dgrad_subpix_weights(g, c.wT, c.subw, st) != hipSuccess) return NITI_NO_EXECUTION;
     return NITI_NO_ERROR;
 }
 

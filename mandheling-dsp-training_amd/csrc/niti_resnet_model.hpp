@@ -29,6 +29,7 @@ struct RConv {
     int8_t wscale = 0;
     int8_t* w = nullptr;       // OHWI16
     int8_t* wT = nullptr;      // IHWO16 (GEMM input gradient)
+    int8_t* subw = nullptr;    // stride 2: the sub-pixel classes' weights (conv_dgrad_subpix_bytes)
     int8_t* wf = nullptr;      // fragment-major copies (row kernels)
     int8_t* wft = nullptr;
     int8_t* ws_dev = nullptr;  // wscale, device
@@ -105,6 +106,19 @@ struct ResNetModel {
     int8_t* gspec_alt = nullptr;  // the GEMM speculative pairs' alternates (shared)
     size_t gspec_alt_bytes = 0;
     uint32_t* rc_err = nullptr;
+    // the residual sums' single-launch form (residual_fused, NITI_RES_FUSED=1: measured slower than
+    // the two launches): one grid-barrier state for all of them (in order on the step stream)
+    // the stride-2 input gradients as sub-pixel classes (NITI_SUBPIX=0: the generic masked loader)
+    static bool subpix_on() {
+        static const bool off = getenv("NITI_SUBPIX") && atoi(getenv("NITI_SUBPIX")) == 0;
+        return !off;
+    }
+    uint32_t* res_bar = nullptr;
+    uint32_t res_epoch = 0;
+    bool res_fused_on() const {
+        static const bool on = getenv("NITI_RES_FUSED") && atoi(getenv("NITI_RES_FUSED")) == 1;
+        return on && !dp() && !capturing && res_bar != nullptr;
+    }
     unsigned long long* qstats = nullptr;
     unsigned long long* qslots = nullptr;
     int32_t* grad_bucket = nullptr;

@@ -49,7 +49,25 @@ __device__ __forceinline__ int32_t psto_any(int32_t a, int s) {
 // One 64 (co) x 64 (ci) tile of tap k of a layer's NITI_SGD step (NITI_SGD.hpp:20-54,
 // CPUBinary.cpp:424-426): g = PSTO(acc, bw - rule) (NITI_GradientConv_Int8.cpp:274-296), w <- clip(w - g,
 // +-127), and the weight copies the next step's kernels read.  256 threads; T: 64 x 68 bytes of LDS.
-__device__ __forceinline__ void sgd_tile(const SgdJob& J, int bw, int ci0, int co0, int k, int8_t (*T)[64 + 4]) {
+// Split in two so a caller can have a tile's operands in flight while it works on another (or
+// while it reads the gradient's range): sgd_tile_load issues the loads, sgd_tile_finish the rest.
+struct SgdTileIn {
+    v4i a[4];  // this thread's 16 gradient words
+    v16c w;    // and its 16 weights
+};
+__device__ __forceinline__ void sgd_tile_load(const SgdJob& J, int ci0, int co0, int k, SgdTileIn& in) {
+    const int t = threadIdx.x;
+    const int r = t >> 2, c = (t & 3) * 16;
+    if (co0 + r < J.co && ci0 + c < J.cip) {
+        const int64_t idx = ((int64_t)(co0 + r) * J.kk + k) * J.cip + ci0 + c;
+        const v4i* a4 = (const v4i*)(J.acc + idx);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) in.a[q] = __builtin_nontemporal_load(a4 + q);  // read once
+        in.w = *(const v16c*)(J.w + idx);
+    }
+}
+__device__ __forceinline__ void sgd_tile_finish(const SgdJob& J, int bw, int ci0, int co0, int k, const SgdTileIn& in,
+                                                int8_t (*T)[64 + 4]) {
     const int t = threadIdx.x;
     const int sh = bw - J.rule;
     {
@@ -59,17 +77,15 @@ __device__ __forceinline__ void sgd_tile(const SgdJob& J, int bw, int ci0, int c
         for (int j = 0; j < 16; ++j) wn[j] = 0;
         if (co0 + r < J.co && ci0 + c < J.cip) {
             const int64_t idx = ((int64_t)(co0 + r) * J.kk + k) * J.cip + ci0 + c;
-            const v4i* a4 = (const v4i*)(J.acc + idx);
-            const v16c wo = *(const v16c*)(J.w + idx);
             v16c g;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                const v4i v = a4[q];
+                const v4i v = in.a[q];
 #pragma unroll
                 for (int e = 0; e < 4; ++e) g[q * 4 + e] = (signed char)(bw == 0 ? 0 : psto_any(v[e], sh));
             }
 #pragma unroll
-            for (int j = 0; j < 16; ++j) wn[j] = (signed char)clip127((int32_t)wo[j] - (int32_t)g[j]);
+            for (int j = 0; j < 16; ++j) wn[j] = (signed char)clip127((int32_t)in.w[j] - (int32_t)g[j]);
             *(v16c*)(J.w + idx) = wn;
             if (J.g_out != nullptr) *(v16c*)(J.g_out + idx) = g;
             if (J.wf != nullptr) {  // WF [co/32][ci/32][9][2][32][16]: this row's 16 ci of one co
@@ -81,19 +97,37 @@ __device__ __forceinline__ void sgd_tile(const SgdJob& J, int bw, int ci0, int c
         for (int j = 0; j < 16; ++j) T[r][c + j] = wn[j];
     }
     __syncthreads();
-    if (J.wT != nullptr || J.wft != nullptr) {
+    if (J.wT != nullptr || J.wft != nullptr || J.subw != nullptr) {
         const int r = t >> 2, c = (t & 3) * 16;  // r: ci within the tile, c: co offset
         if (ci0 + r < J.ci && co0 + c < J.cop) {
             v16c o;
 #pragma unroll
             for (int j = 0; j < 16; ++j) o[j] = T[c + j][r];
             if (J.wT != nullptr) *(v16c*)(J.wT + ((int64_t)(ci0 + r) * J.kk + k) * J.cop + co0 + c) = o;
+            if (J.subw != nullptr) {  // the sub-pixel class copy: class of the tap, then [ci][jy][jx][cop]
+                const int ky = k / J.sub_kw, kx = k - ky * J.sub_kw;
+                const int py = (ky - J.sub_pt) & 1, px = (kx - J.sub_pl) & 1;
+                auto taps = [](int kn, int pad, int par) {
+                    const int k0 = (par + pad) & 1;
+                    return k0 < kn ? (kn - k0 + 1) / 2 : 0;
+                };
+                int64_t off = 0;
+                for (int cl = 0; cl < py * 2 + px; ++cl)
+                    off += (int64_t)taps(J.sub_kh, J.sub_pt, cl >> 1) * taps(J.sub_kw, J.sub_pl, cl & 1) * J.ci * J.cop;
+                const int ny = taps(J.sub_kh, J.sub_pt, py), nx = taps(J.sub_kw, J.sub_pl, px);
+                *(v16c*)(J.subw + off + (((int64_t)(ci0 + r) * ny + (ky >> 1)) * nx + (kx >> 1)) * J.cop + co0 + c) = o;
+            }
             if (J.wft != nullptr) {  // the input gradient's WF: output channel ci, k = 16 co, tap 8 - k
                 const int i = ci0 + r, o0 = co0 + c, ob = (J.co + 31) / 32;
                 *(v16c*)(J.wft + (((((int64_t)(i >> 5) * ob + (o0 >> 5)) * 9 + (8 - k)) * 2 + ((o0 >> 4) & 1)) * 32 + (i & 31)) * 16) = o;
             }
         }
     }
+}
+__device__ __forceinline__ void sgd_tile(const SgdJob& J, int bw, int ci0, int co0, int k, int8_t (*T)[64 + 4]) {
+    SgdTileIn in;
+    sgd_tile_load(J, ci0, co0, k, in);
+    sgd_tile_finish(J, bw, ci0, co0, k, in, T);
 }
 
 }  // namespace niti

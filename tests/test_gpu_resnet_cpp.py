@@ -262,8 +262,9 @@ def _dp_steps(T, full, ranks, streams, rng, world, per, hw, classes, images, con
 def test_resnet18_cpp_gemm_pair_misses(T, bias):
     """The GEMM speculative pair (plan strategy 3 on every GEMM-path forward and input gradient) with
     launch A's guess forced off by `bias` (niti_diag_gemm_speculate): +1 / -1 make every launch B
-    settle from A's alternate one bit width below / above, 2 makes every launch B redo the GEMM.  Two
-    steps against the oracle each (NITI_Conv_Int8.cpp:260-307, NITI_DeConv_Int8.cpp:294-329)."""
+    after the first miss (which opens the alternates' window) settle from A's alternate one bit width
+    below / above, 2 makes every launch B redo the GEMM.  Three steps against the oracle each
+    (NITI_Conv_Int8.cpp:260-307, NITI_DeConv_Int8.cpp:294-329)."""
     import niti_resnet_ref as RR
     from niti_amd import _lib as L
     from niti_amd.model import NitiModel
@@ -296,3 +297,31 @@ def test_resnet18_cpp_gemm_pair_misses(T, bias):
         lib.niti_diag_gemm_speculate(0)
         NitiModel.reset_plans()
 
+
+
+@pytest.mark.parametrize("plan", [(128, 128, 1, 0), (64, 64, 1, 1), (128, 64, 4, 2)])
+def test_resnet18_cpp_subpix_dgrad_plans(T, plan):
+    """The stride-2 input gradients (3x3 / 2 and 1x1 / 2 projections) as four sub-pixel class GEMMs
+    through a row map, under a forced store / recompute / split-K plan on every input gradient
+    (split-K falls back to one split per class), three steps against the oracle
+    (NITI_DeConv_Int8.cpp:187-332: the transposed conv over the dilated output gradient)."""
+    import niti_resnet_ref as RR
+    from niti_amd.model import NitiModel
+    hw, batch, classes = 64, 2, 10
+    convs = RR.resnet18_convs(hw, classes)
+    W, S = RR.init_weights(convs, seed=70 + plan[3])
+    rng = np.random.default_rng(70 + plan[3])
+    m = _model(batch, hw, classes, W, S)
+    assert any(c["stride"] == 2 and c["k"] == 3 for c in convs) and any(c["stride"] == 2 and c["k"] == 1 for c in convs)
+    try:
+        for i in range(1, len(convs)):
+            m.set_plan(i, 1, plan)
+        for step in range(3):
+            x = rng.integers(-127, 128, (batch, 3, hw, hw)).astype(np.int8)
+            lab = rng.integers(0, classes, batch).astype(np.int32)
+            newW, rec = RR.train_step(convs, W, S, x, -2, lab, classes=classes)
+            m.train_step(T.from_numpy(x).cuda(), -2, T.from_numpy(lab).cuda())
+            _check_step(m, convs, rec, newW, step)
+            W = newW
+    finally:
+        NitiModel.reset_plans()

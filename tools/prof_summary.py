@@ -1,5 +1,6 @@
 """Summarise a rocprofv3 --kernel-trace CSV of a bench run: per-kernel time per training step over the
-last timed steps (each step from its input quantiser's first launch to its NITI_SGD update launch),
+last timed steps (each step from its input quantiser's first launch to its NITI_SGD update launch and the fused
+fully connected updates after it),
 then the last step's launches as a timeline.  Launches outside those steps (autotuning, warmup, the
 isolated probe re-runs after the timed region) are not counted.
 
@@ -25,8 +26,18 @@ def is_start(r):  # a step's first kernel: the input statistics or the int8 inpu
     return "image_stats" in k or "NchwToNhwc16" in k or "input_im2col" in k
 
 
-# steps: [start index, index of the sgd_update launch]; the stats launch may be preceded by a memset
-ends = [i for i, r in enumerate(rows) if "sgd_update_kernel" in r["Kernel_Name"]]
+def is_update_tail(r):  # the fully connected layers' fused NITI_SGD passes follow the update launch
+    return "KtRowsU, niti::KtRowsU, 4, true" in r["Kernel_Name"]
+
+
+# steps: [start index, index of the sgd_update launch or the last fused-update pass after it]; the
+# stats launch may be preceded by a memset
+ends = []
+for i, r in enumerate(rows):
+    if "sgd_update_kernel" in r["Kernel_Name"]:
+        while i + 1 < len(rows) and is_update_tail(rows[i + 1]):
+            i += 1
+        ends.append(i)
 steps = []
 prev = -1
 for e in ends:
