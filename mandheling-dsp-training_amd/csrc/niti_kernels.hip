@@ -3695,6 +3695,19 @@ __global__ void sgd_update_kernel(SgdJobs jobs, int total) {
     };
     int bb = blockIdx.x;
     if (bb >= total) return;
+    if (!NITI_SGD_PREFETCH) {  // one tile at a time
+        int last_j = -1, bw = 0;
+        for (; bb < total; bb += gridDim.x) {
+            const Tile t = locate(bb);
+            if (t.j != last_j) {
+                bw = bitwidth_of(read_max(jobs.job[t.j].amax));
+                last_j = t.j;
+            }
+            if (bb != (int)blockIdx.x) __syncthreads();  // the previous tile's transposed reads are done
+            sgd_tile(jobs.job[t.j], bw, t.ci0, t.co0, t.k, T);
+        }
+        return;
+    }
     Tile cur = locate(bb);
     SgdTileIn cin, nin;  // (named, not an indexed pair: a dynamically indexed array would live in scratch)
     sgd_tile_load(jobs.job[cur.j], cur.ci0, cur.co0, cur.k, cin);

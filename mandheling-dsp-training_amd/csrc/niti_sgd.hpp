@@ -5,6 +5,13 @@
 #include "niti_device.hpp"
 #include "niti_kernels.hpp"
 
+#ifndef NITI_SGD_NT
+#define NITI_SGD_NT 0  // diagnostics: nontemporal loads of the int32 gradient in the update
+#endif
+#ifndef NITI_SGD_PREFETCH
+#define NITI_SGD_PREFETCH 0  // diagnostics: the update loads the next tile before finishing this one
+#endif
+
 namespace niti {
 
 // NITI_RangeEstimate on the max word: ceil(log2(m)), 0 for m <= 1.
@@ -62,7 +69,7 @@ __device__ __forceinline__ void sgd_tile_load(const SgdJob& J, int ci0, int co0,
         const int64_t idx = ((int64_t)(co0 + r) * J.kk + k) * J.cip + ci0 + c;
         const v4i* a4 = (const v4i*)(J.acc + idx);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) in.a[q] = __builtin_nontemporal_load(a4 + q);  // read once
+        for (int q = 0; q < 4; ++q) in.a[q] = NITI_SGD_NT ? __builtin_nontemporal_load(a4 + q) : a4[q];
         in.w = *(const v16c*)(J.w + idx);
     }
 }
