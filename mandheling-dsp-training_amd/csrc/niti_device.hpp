@@ -125,6 +125,15 @@ __device__ __forceinline__ void wait_steps(int later) {
         wait_vmcnt<0>();
 }
 
+// 4 x 4 byte transpose inside a lane quad (j = lane & 3): byte r of lane k -> byte k of lane r.
+// Every lane of the wave must execute it (DPP reads the quad partners' registers).
+__device__ __forceinline__ uint32_t quad_transpose(uint32_t d, int j) {
+    const uint32_t y1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)d, 0xB1, 0xF, 0xF, false);  // lane ^ 1
+    d = __builtin_amdgcn_perm(y1, d, (j & 1) ? 0x03070105u : 0x06020400u);
+    const uint32_t y2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)d, 0x4E, 0xF, 0xF, false);  // lane ^ 2
+    return __builtin_amdgcn_perm(y2, d, (j & 2) ? 0x03020706u : 0x05040100u);
+}
+
 __device__ __forceinline__ uint32_t lds_addr(const void* p) {
     return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
 }

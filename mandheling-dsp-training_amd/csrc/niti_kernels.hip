@@ -279,15 +279,6 @@ __device__ __forceinline__ int gemm_spec_settle(const Epi& epi) {
 // col = lane&31.  `smem` is reused for the block max (every LDS read finished at the last barrier).
 // REQUANT: the int8 values leave as dwords of 4 columns of one row, packed in registers (see
 // below); the relu-grad mask is applied in the same pass.
-// 4 x 4 byte transpose inside a lane quad (j = lane & 3): byte r of lane k -> byte k of lane r.
-// Every lane of the wave must execute it (DPP reads the quad partners' registers).
-__device__ __forceinline__ uint32_t quad_transpose(uint32_t d, int j) {
-    const uint32_t y1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)d, 0xB1, 0xF, 0xF, false);  // lane ^ 1
-    d = __builtin_amdgcn_perm(y1, d, (j & 1) ? 0x03070105u : 0x06020400u);
-    const uint32_t y2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)d, 0x4E, 0xF, 0xF, false);  // lane ^ 2
-    return __builtin_amdgcn_perm(y2, d, (j & 2) ? 0x03020706u : 0x05040100u);
-}
-
 // whether the STORE / SLAB epilogue stages the int32 tile through LDS (tiles up to 128 x 128)
 constexpr bool epi_stage_c(int mode, int bm, int bn) {
     return (mode == EPI_STORE || mode == EPI_SLAB) && bm * (bn + 4) * 4 <= 72 * 1024;
