@@ -3048,7 +3048,7 @@ __global__ void __launch_bounds__(256) requant_quad_kernel(ActRequant r, RqGeom 
         } else {
             // window rows of each unit
             int64_t wrow[RQ_U];
-            uint32_t pp_[RQ_U];
+            uint32_t pp_[RQ_U], img_[RQ_U];
             int cq_[RQ_U];
 #pragma unroll
             for (int j = 0; j < RQ_U; ++j) {
@@ -3062,6 +3062,7 @@ __global__ void __launch_bounds__(256) requant_quad_kernel(ActRequant r, RqGeom 
                 const int py = (int)(rest - b * g.fph.d);
                 wrow[j] = ((int64_t)b * (2 * g.fph.d) + 2 * py) * g.W + 2 * px;
                 pp_[j] = pp;
+                img_[j] = b;
             }
             if (MODE == RQ_POOL_FWD) {
                 v4i v[RQ_U][4];
@@ -3120,6 +3121,12 @@ __global__ void __launch_bounds__(256) requant_quad_kernel(ActRequant r, RqGeom 
                         }
                         const int64_t row = wrow[j] + (k & 1) + (k >> 1) * g.W;
                         ((uint32_t*)(r.pool.dx + row * ldc))[cq_[j]] = o;
+                        if (r.pool.dx_c32 != nullptr) {  // [img][c / 32][H][W][32]: 4 channels of one pixel
+                            const int64_t hw = (int64_t)(2 * g.fph.d) * g.W;
+                            const int64_t pix = row - (int64_t)img_[j] * hw;
+                            const int c = 4 * cq_[j];
+                            *(uint32_t*)(r.pool.dx_c32 + (((int64_t)img_[j] * (ldc / 32) + c / 32) * hw + pix) * 32 + (c & 31)) = o;
+                        }
                     }
                 }
             }
@@ -3525,6 +3532,8 @@ hipError_t requant_act(const ActRequant& r, hipStream_t st) {
                                      r.rows % ((int64_t)(r.pool.H / 2) * (r.pool.W / 2))))
             return hipErrorInvalidValue;
     }
+    if (r.pool.dx_c32 != nullptr && (r.pool.dx == nullptr || r.out_p16 != nullptr || r.ldc % 32 != 0))
+        return hipErrorInvalidValue;
     if (r.out_p16 != nullptr) {  // the output (dx with the pool gradient) also as its P16 copy
         if (!requant_p16_ok(r)) return hipErrorInvalidValue;
         RqGeom g{};

@@ -191,6 +191,9 @@ struct PoolFuse {
     int8_t* dx = nullptr;
     int relu = 0;
     int H = 0, W = 0;  // pre-pool image size
+    // the pool gradient dx also as the row kernels' C32 layout [n][ld/32][H][W][32] (the next input
+    // gradient's operand; separate requant pass without a P16 copy, ld % 32 == 0), or null
+    int8_t* dx_c32 = nullptr;
 };
 struct ActOut {
     int8_t* out = nullptr;             // NHWC16 [rows][ld] (may be null with pool.dx)

@@ -1164,6 +1164,10 @@ int Model::dgrad_layer(int i, hipStream_t st) {
             o.pool.H = pg.oh;
             o.pool.W = pg.ow;
             o.out_p16 = p16_out;
+            // the previous layer's row-kernel input gradient reads dy as C32: the same pass writes it
+            // (VGG-16 conv2_2 at 112 px: no 205 MB layout launch)
+            if (p16_out == nullptr && rowconv_dgrad_layer(i - 1) && !rowconv_nhwc_pref(pv.dg) && pg.cop % 32 == 0)
+                o.pool.dx_c32 = pv.dyc32;
         } else {
             o.out = pv.dtmp;
         }
@@ -1194,6 +1198,7 @@ int Model::dgrad_layer(int i, hipStream_t st) {
                                       pv.dy, st));
     }
     if (o.out_p16 != nullptr) dp16_valid[i - 1] = 1;
+    dyc32_valid[i - 1] = fuse && o.pool.dx_c32 != nullptr ? 1 : 0;
     return NITI_NO_ERROR;
 }
 

@@ -969,7 +969,7 @@ __device__ __forceinline__ void write_exponent(const RowConvArgs& a, uint32_t gm
 // used, bit 31 set when it stored instead; written by A's block 0, read by B), [2] redone launches,
 // [3] pairs left in store mode (read and written by B's thread 0, read by A), [4] stored pairs.
 // Every other reader of a word runs in the other launch, so no launch's blocks race on a word.
-constexpr uint32_t SPEC_COOLDOWN = 4;  // the default of spec_cooldown() (NITI_SPEC_COOLDOWN overrides)
+constexpr uint32_t SPEC_COOLDOWN = 8;  // the default of spec_cooldown() (NITI_SPEC_COOLDOWN overrides; profiles/r05_spec_cooldown_ab.txt)
 __device__ __forceinline__ int spec_guess(const RowConvArgs& a, bool can_store, bool& store) {
     const uint32_t h = __hip_atomic_load(a.hint, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint32_t f = __hip_atomic_load(a.hint + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -27,6 +27,9 @@ def load(d, name):
 
 def probe_rows(rows):
     last = max(k for k, r in enumerate(rows) if "sgd_update_kernel" in r["Kernel_Name"])
+    # (the fully connected layers' fused NITI_SGD passes follow the update launch: still the step)
+    while last + 1 < len(rows) and "KtRowsU, niti::KtRowsU, 4, true" in rows[last + 1]["Kernel_Name"]:
+        last += 1
     tail = rows[last + 1:]
     t = collections.defaultdict(float)
     for r in tail:
