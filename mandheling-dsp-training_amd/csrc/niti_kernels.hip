@@ -2375,7 +2375,7 @@ static hipError_t launch_taps(const GemmPlan& p, WgTaps t, const Epi& e, hipStre
 }
 
 static hipError_t wgrad_taps_run(const GemmPlan& p, const WgTaps& t, int M, int N, int32_t* C, uint32_t* amax,
-                                 int32_t* ws, hipStream_t st, hipEvent_t after_gemm) {
+                                 int32_t* ws, hipStream_t st, hipEvent_t after_gemm, SgdJob* defer = nullptr) {
     Epi e;
     e.span = take_span();
     if (p.strat == STRAT_SLAB) {
@@ -2395,6 +2395,20 @@ static hipError_t wgrad_taps_run(const GemmPlan& p, const WgTaps& t, int M, int 
         map.fRow = make_fastdiv(72);
         map.fPart = make_fastdiv(8);
         map.fTci = make_fastdiv((uint32_t)t.tiles_ci);
+        // the NITI_SGD launch's combine sums the tile-blocked slabs (as gemm_acc_plan's C-shaped ones)
+        if (defer != nullptr && (int64_t)mb * N >= (int64_t)p.splits * 4096 && (int64_t)mb * N < ((int64_t)1 << 32)) {
+            defer->slab = ws;
+            defer->splits = p.splits;
+            defer->slab_stride = e.slab_stride;
+            defer->slab_n = (int64_t)mb * N;
+            defer->slab_map = 1;
+            defer->tb_tiles_ci = map.tiles_ci;
+            defer->tb_cip4 = map.cip4;
+            defer->tb_ld4 = map.ld4;
+            defer->tb_m = map.fTci.m;
+            defer->tb_s = map.fTci.s;
+            return hipSuccess;
+        }
         return splitk_reduce(p, ws, (int64_t)mb * N, e.slab_stride, C, amax, st, map);
     }
     e.C = C;
@@ -2403,6 +2417,16 @@ static hipError_t wgrad_taps_run(const GemmPlan& p, const WgTaps& t, int M, int 
     hipError_t r = launch_taps<EPI_STORE>(p, t, e, st);
     if (r == hipSuccess && after_gemm != nullptr) r = hipEventRecord(after_gemm, st);
     return r;
+}
+
+// bytes of the K-split slabs a weight-gradient plan writes (the tap-sharing kernel's tile-blocked
+// slabs pad the output channels to whole 64-row tiles)
+size_t conv_wgrad_slab_bytes(const ConvGeom& g, const PlanChoice& c) {
+    const PlanKey k = conv_plan_key(PLAN_WGRAD, g);
+    WgTaps t;
+    if (c.bm == PLAN_TAPS_TILE && wgrad_taps_geom(g, nullptr, nullptr, &t))
+        return (size_t)c.splits * slab_stride_elems(taps_slab_rows(t), k.N) * 4;
+    return plan_slab_bytes(k.M, k.N, c.splits);
 }
 
 PlanChoice conv_plan_query(int op, const ConvGeom& g, bool recompute_ok, size_t ws_bytes) {
@@ -2482,7 +2506,7 @@ hipError_t conv_wgrad_acc(const ConvGeom& g, const int8_t* x, const int8_t* dy, 
         const bool has = plan_override_get(conv_plan_key(PLAN_WGRAD, g), &c);
         if (!has || c.bm == PLAN_TAPS_TILE) {
             const GemmPlan p = plan_taps(tg, M, N, ws ? ws_bytes / 4 : 0, has ? &c : nullptr);
-            return wgrad_taps_run(p, tg, M, N, acc, amax, (int32_t*)ws, st, after_gemm);
+            return wgrad_taps_run(p, tg, M, N, acc, amax, (int32_t*)ws, st, after_gemm, defer);
         }
     }
     KtRowsU la;
@@ -3644,7 +3668,22 @@ __global__ void __launch_bounds__(256) sgd_combine_kernel(SgdJobs jobs) {
         }
         const SgdJob& J = jobs.job[j];
         const int64_t e = (int64_t)(c - jobs.cstart[j]) * 1024 + threadIdx.x * 4;
-        if (J.slab != nullptr && e < J.slab_n) {
+        int64_t de = e;  // the acc element this slab element sums into
+        bool live = J.slab != nullptr && e < J.slab_n;
+        if (live && J.slab_map == 1) {  // SlabTapsBlocked (splitk_reduce's map), on 16-byte units
+            const uint32_t u = (uint32_t)(e >> 2);
+            const uint32_t tile = u / 4608u, rem = u - tile * 4608u;
+            const uint32_t row = rem / 72u, rc = rem - row * 72u;
+            const uint32_t t = rc / 8u, part = rc - t * 8u;
+            FastDiv ft;
+            ft.m = J.tb_m;
+            ft.s = J.tb_s;
+            const uint32_t tco = fdiv(ft, tile), tci = tile - tco * (uint32_t)J.tb_tiles_ci;
+            const int co = (int)(tco * 64u + row);
+            live = co < J.co;
+            de = ((int64_t)co * J.tb_ld4 + t * J.tb_cip4 + tci * 8u + part) * 4;
+        }
+        if (live) {
             const v4i* base = (const v4i*)(J.slab + e);
             const int64_t st4 = J.slab_stride / 4;
             v4i s = {0, 0, 0, 0};
@@ -3656,7 +3695,7 @@ __global__ void __launch_bounds__(256) sgd_combine_kernel(SgdJobs jobs) {
 #pragma unroll
                 for (int q = 0; q < 8; ++q) s += v[q];
             }
-            *(v4i*)(const_cast<int32_t*>(J.acc) + e) = s;
+            *(v4i*)(const_cast<int32_t*>(J.acc) + de) = s;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const uint32_t u = uabs32(s[q]);

@@ -89,6 +89,8 @@ void plan_override_clear_all();
 // the plan the GEMM of key k runs with now (override or default) under a workspace of ws_bytes
 PlanChoice plan_query(const PlanKey& k, int k_step, bool recompute_ok, size_t ws_bytes);
 size_t plan_slab_bytes(int M, int N, int splits);
+struct PlanChoice;
+size_t conv_wgrad_slab_bytes(const ConvGeom& g, const PlanChoice& c);
 // acc[M = n*oh*ow][cop] = conv(x NHWC16, w OHWI16)
 hipError_t conv_fwd_acc(const ConvGeom& g, const int8_t* x_nhwc16, const int8_t* w_ohwi16, int32_t* acc,
                         uint32_t* amax, void* ws, size_t ws_bytes, hipStream_t st);
@@ -427,6 +429,12 @@ struct SgdJob {
     const int32_t* slab = nullptr;
     int splits = 0;
     int64_t slab_stride = 0, slab_n = 0;
+    // slab layout: 0 = C-shaped (acc index = slab index); 1 = the tap-sharing weight gradient's
+    // tile-blocked slabs (wgrad_taps_kernel: 64-row tiles of 72 16-byte columns, mapped back to
+    // [co][tap][ci] with these fields; tb_m / tb_s: the magic division by tb_tiles_ci)
+    int slab_map = 0;
+    int tb_tiles_ci = 0, tb_cip4 = 0, tb_ld4 = 0;
+    uint32_t tb_m = 0, tb_s = 0;
 };
 constexpr int SGD_MAX_JOBS = 24;
 struct SgdJobs {
@@ -481,7 +489,9 @@ hipError_t image_quantize(const uint8_t* img, int n, int c, int hw, int cp, cons
 // atomics), summed by their consumer; stats_finalize sums them into stats[4] (data parallel:
 // before the all-reduce)
 constexpr int IMAGE_STATS_SLOTS = 256;
-hipError_t image_stats_slots(const uint8_t* img, int64_t n, unsigned long long* slots, int* nslots, hipStream_t st);
+// (zero / zero_bytes, multiple of 16: a buffer the same launch zeroes, e.g. the step's range words)
+hipError_t image_stats_slots(const uint8_t* img, int64_t n, unsigned long long* slots, int* nslots, hipStream_t st,
+                             void* zero = nullptr, size_t zero_bytes = 0);
 hipError_t stats_finalize(const unsigned long long* slots, int nslots, unsigned long long* stats, hipStream_t st);
 // the first layer's im2col copy (xcol [n*oh*ow][32]) straight from the NCHW batch: uint8 images
 // quantised with the statistics in `slots` (nslots partials over `count` pixels), or int8 pixels

@@ -512,9 +512,8 @@ struct Model {
     bool ensure_wslab(int i) {
         Layer& l = L[i];
         const PlanChoice c = conv_plan_query(PLAN_WGRAD, l.g, false, slab_w_bytes);
-        if (c.strat != 2 || c.splits < 2 || c.bm == PLAN_TAPS_TILE || c.bm == PLAN_P16_TILE) return false;
-        const PlanKey k = conv_plan_key(PLAN_WGRAD, l.g);
-        const size_t need = plan_slab_bytes(k.M, k.N, c.splits);
+        if (c.strat != 2 || c.splits < 2 || c.bm == PLAN_P16_TILE) return false;
+        const size_t need = conv_wgrad_slab_bytes(l.g, c);  // (GEMM or tap-sharing slabs)
         if (l.wslab_bytes >= need) return true;
         if (hipDeviceSynchronize() != hipSuccess) return false;
         void* p = ws.alloc(need);
@@ -1371,7 +1370,9 @@ int Model::run(const int8_t* x_nchw, int exp_in, const uint8_t* images, const in
     invalidate_xp16();  // the forward pass rewrites every layer input
     std::fill(xc32_valid.begin(), xc32_valid.end(), 0);
     std::fill(dyc32_valid.begin(), dyc32_valid.end(), 0);
-    MTRY(hipMemsetAsync(amax, 0, amax_bytes, st));
+    // the range words start each step at zero: zeroed by the input statistics launch (uint8
+    // images), else here
+    if (x_nchw != nullptr || amax_bytes % 16 != 0) MTRY(hipMemsetAsync(amax, 0, amax_bytes, st));
     // the first layer's im2col copy straight from the batch where the fused pass takes the layer
     const ConvGeom& o0 = L[0].og;
     const bool fused_in = L[0].col && input_im2col_ok(o0.c_in, o0.kh, o0.kw) && o0.sh == 1 && o0.sw == 1;
@@ -1398,7 +1399,8 @@ int Model::run(const int8_t* x_nchw, int exp_in, const uint8_t* images, const in
         // ascale straight into the layer-0 input
         const int64_t px = (int64_t)n * in_c * in_h * in_w;
         int ns = 0;
-        MTRY(image_stats_slots(images, px, qslots, &ns, st));
+        MTRY(image_stats_slots(images, px, qslots, &ns, st, amax_bytes % 16 == 0 ? amax : nullptr,
+                               amax_bytes % 16 == 0 ? amax_bytes : 0));
         const unsigned long long* slots = qslots;
         if ((dp && exact) || !fused_in) {
             MTRY(stats_finalize(qslots, ns, qstats, st));
@@ -1477,6 +1479,12 @@ int Model::run(const int8_t* x_nchw, int exp_in, const uint8_t* images, const in
             jobs[i].splits = l.defer.splits;
             jobs[i].slab_stride = l.defer.slab_stride;
             jobs[i].slab_n = l.defer.slab_n;
+            jobs[i].slab_map = l.defer.slab_map;  // (the tap-sharing kernel's tile-blocked slabs)
+            jobs[i].tb_tiles_ci = l.defer.tb_tiles_ci;
+            jobs[i].tb_cip4 = l.defer.tb_cip4;
+            jobs[i].tb_ld4 = l.defer.tb_ld4;
+            jobs[i].tb_m = l.defer.tb_m;
+            jobs[i].tb_s = l.defer.tb_s;
         }
     }
     if (dp) {  // every bucket summed and ranged on the comm stream before the update

@@ -432,9 +432,8 @@ int ResNetModel::wgrad_conv(int i, hipStream_t st) {
 bool ResNetModel::ensure_wslab(int i) {
     RConv& c = C[i];
     const PlanChoice p = conv_plan_query(PLAN_WGRAD, c.g, false, slab_w_bytes);
-    if (p.strat != 2 || p.splits < 2 || p.bm == PLAN_TAPS_TILE || p.bm == PLAN_P16_TILE) return false;
-    const PlanKey k = conv_plan_key(PLAN_WGRAD, c.g);
-    const size_t need = plan_slab_bytes(k.M, k.N, p.splits);
+    if (p.strat != 2 || p.splits < 2 || p.bm == PLAN_P16_TILE) return false;
+    const size_t need = conv_wgrad_slab_bytes(c.g, p);  // (GEMM or tap-sharing slabs)
     if (c.wslab_bytes >= need) return true;
     if (hipDeviceSynchronize() != hipSuccess) return false;
     void* q = ws.alloc(need);
@@ -557,13 +556,16 @@ int ResNetModel::run(const int8_t* x_nchw, int exp_in, const uint8_t* images, co
         ~InStep() { f = false; }
     } in_step_guard(in_step);
     for (RConv& c : C) c.defer = SgdJob{};
-    RTRY(hipMemsetAsync(amax, 0, amax_bytes, st));
+    // the range words start each step at zero: zeroed by the input statistics launch (uint8
+    // images), else here
+    if (images == nullptr || amax_bytes % 16 != 0) RTRY(hipMemsetAsync(amax, 0, amax_bytes, st));
     // input: NITIInt8Train's quantiser (MnistUtils.cpp:83-93) on uint8 images, or int8 x as given
     const int64_t px = (int64_t)n * 3 * in_hw * in_hw;
     const int8_t* xq = x_nchw;
     if (images != nullptr) {
         int ns = 0;
-        RTRY(image_stats_slots(images, px, qslots, &ns, st));
+        RTRY(image_stats_slots(images, px, qslots, &ns, st, amax_bytes % 16 == 0 ? amax : nullptr,
+                               amax_bytes % 16 == 0 ? amax_bytes : 0));
         RTRY(stats_finalize(qslots, ns, qstats, st));
         if (dp && exact) {
             RTRY(coll->allreduce(qstats, 2, COLL_SUM_U64, st));
@@ -657,6 +659,12 @@ int ResNetModel::run(const int8_t* x_nchw, int exp_in, const uint8_t* images, co
             jobs[i].splits = c.defer.splits;
             jobs[i].slab_stride = c.defer.slab_stride;
             jobs[i].slab_n = c.defer.slab_n;
+            jobs[i].slab_map = c.defer.slab_map;  // (the tap-sharing kernel's tile-blocked slabs)
+            jobs[i].tb_tiles_ci = c.defer.tb_tiles_ci;
+            jobs[i].tb_cip4 = c.defer.tb_cip4;
+            jobs[i].tb_ld4 = c.defer.tb_ld4;
+            jobs[i].tb_m = c.defer.tb_m;
+            jobs[i].tb_s = c.defer.tb_s;
         }
     }
     RTRY(sgd_update_many(jobs, nl, st));
