@@ -60,7 +60,12 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 // few dozen blocks' atomics, where one block over a 224x224 batch took 2.6 ms
 template <bool ATOMIC>
 __global__ void __launch_bounds__(256) image_stats_kernel(const uint8_t* __restrict__ img, int64_t n,
-                                                          unsigned long long* __restrict__ slots) {
+                                                          unsigned long long* __restrict__ slots,
+                                                          uint4* __restrict__ zero = nullptr, int64_t zero16 = 0) {
+    // a side job: the step's range words zeroed here, the step's first launch (a memset of its own
+    // was a ~5 us blit launch)
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < zero16; i += (int64_t)gridDim.x * blockDim.x)
+        zero[i] = uint4{0u, 0u, 0u, 0u};
     unsigned long long s1 = 0, s2 = 0;
     uint32_t mx = 0, mn = 0;  // mn holds 255 - min
     const int64_t nv = n / 16;
@@ -393,11 +398,13 @@ __global__ void __launch_bounds__(256) input_im2col_kernel(const void* __restric
 }  // namespace
 
 // slots: IMAGE_STATS_SLOTS x 4 u64 of per-block partials
-hipError_t image_stats_slots(const uint8_t* img, int64_t n, unsigned long long* slots, int* nslots, hipStream_t st) {
-    if (n <= 0) return hipErrorInvalidValue;
+hipError_t image_stats_slots(const uint8_t* img, int64_t n, unsigned long long* slots, int* nslots, hipStream_t st,
+                             void* zero, size_t zero_bytes) {
+    if (n <= 0 || zero_bytes % 16 != 0 || (zero_bytes != 0 && zero == nullptr)) return hipErrorInvalidValue;
     int64_t blocks = (n / 16 + 255) / 256;
     blocks = blocks < 1 ? 1 : blocks > IMAGE_STATS_SLOTS ? IMAGE_STATS_SLOTS : blocks;
-    hipLaunchKernelGGL(image_stats_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, st, img, n, slots);
+    hipLaunchKernelGGL(image_stats_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, st, img, n, slots, (uint4*)zero,
+                       (int64_t)(zero_bytes / 16));
     *nslots = (int)blocks;
     return hipGetLastError();
 }
