@@ -1994,6 +1994,9 @@ static hipError_t act_phase2(int op, const LA& la, const LB& lb, int M, int N, i
     r.out_nhwc16 = o.out;
     r.pool = o.pool;
     r.out_p16 = o.out_p16;
+    r.zero_cls = o.zero_cls;
+    r.zc_h = o.zc_h;
+    r.zc_w = o.zc_w;
     return requant_act(r, st);
 }
 
@@ -2724,9 +2727,10 @@ hipError_t conv_dgrad_subpix_weights(const ConvGeom& g, const int8_t* wt, int8_t
 // one pass over the four classes: MODE EPI_STORE (acc), EPI_AMAX (max only) or EPI_REQUANT (o)
 template <int MODE>
 static hipError_t subpix_pass(const ConvGeom& g, const GemmPlan& plan, const int8_t* dy, const int8_t* subw,
-                              int32_t* acc, uint32_t* amax, const ActOut* o, hipStream_t st) {
+                              int32_t* acc, uint32_t* amax, const ActOut* o, hipStream_t st, bool zero_fill = false) {
     const SubpixPlan q = subpix_plan(g);
     for (int c = 0; c < 4; ++c) {
+        if (zero_fill && q.ay[c >> 1].n * q.ax[c & 1].n != 0) continue;  // only the tap-less classes' zeros
         const SubpixAxis& ay = q.ay[c >> 1];
         const SubpixAxis& ax = q.ax[c & 1];
         ConvGeom gc = g;
@@ -2764,7 +2768,7 @@ static hipError_t subpix_pass(const ConvGeom& g, const GemmPlan& plan, const int
             e.wscale = o->wscale;
             e.exp_out = o->exp_out;
         }
-        if (MODE == EPI_AMAX && kc == 0) continue;  // (a zero class adds nothing to the max)
+        if ((MODE == EPI_AMAX || MODE == EPI_STORE) && kc == 0 && !zero_fill) continue;  // (requant: zero_cls)
         const RowsK lb = rows_k(subw + q.woff[c], (int64_t)gc.kh * gc.kw * g.cop, g.c_in, kc);
         const hipError_t r = launch_mode<ConvTaps<64>, RowsK, MODE, false>(p, conv_taps<64>(gc, dy, false), lb, M, g.cip,
                                                                           kc, e, st);
@@ -2799,6 +2803,26 @@ hipError_t conv_dgrad_phase2(const ConvGeom& g, const int8_t* dy, const int8_t* 
         if (p.strat == STRAT_RECOMPUTE) {
             if (o.pool.pool_out != nullptr || o.pool.dx != nullptr || o.out_p16 != nullptr) return hipErrorInvalidValue;
             return subpix_pass<EPI_REQUANT>(g, p, dy, subw, nullptr, const_cast<uint32_t*>(amax), &o, st);
+        }
+        // phase 1 left the tap-less classes' accumulators unwritten: the plain requantise pass
+        // writes their zeros without reading them, any other pass gets them zero-filled first
+        const SubpixPlan q = subpix_plan(g);
+        int zc = 0;
+        for (int c = 0; c < 4; ++c)
+            if (q.ay[c >> 1].n * q.ax[c & 1].n == 0) zc |= 1 << c;
+        if (zc != 0 && p.strat != STRAT_SPEC) {  // (a speculative plan runs phase 1 as one GEMM)
+            if (o.pool.pool_out == nullptr && o.pool.dx == nullptr && o.out_p16 == nullptr) {
+                ActOut oz = o;
+                oz.zero_cls = zc;
+                oz.zc_h = g.h;
+                oz.zc_w = g.w;
+                return with_dgrad_operand(g, dy, [&](const auto& la) {
+                    const RowsK lb = rows_k(wt, (int64_t)g.kh * g.kw * g.cop, g.c_in, kc_total);
+                    return act_phase2(PLAN_DGRAD, la, lb, g.n * g.h * g.w, g.cip, kc_total, acc, amax, oz, ws_bytes / 4, st);
+                });
+            }
+            const hipError_t r = subpix_pass<EPI_STORE>(g, p, dy, subw, const_cast<int32_t*>(acc), nullptr, nullptr, st, true);
+            if (r != hipSuccess) return r;
         }
     }
     const RowsK lb = rows_k(wt, (int64_t)g.kh * g.kw * g.cop, g.c_in, kc_total);
@@ -3009,6 +3033,7 @@ struct RqGeom {
     FastDiv fq, fpw, fph;  // by quads per row, pooled width, pooled height
     int qpr, W;            // quads per row, pre-pool width
     uint32_t units;
+    FastDiv fzw, fzh;      // ActRequant::zc_w / zc_h (zero_cls)
 };
 
 __device__ __forceinline__ uint32_t rq4(v4i v, bool raw, int s, int relu) {
@@ -3052,7 +3077,13 @@ __global__ void __launch_bounds__(256) requant_quad_kernel(ActRequant r, RqGeom 
 #pragma unroll
             for (int j = 0; j < RQ_U; ++j) {
                 const uint32_t u = u0 + j * stride;
-                v[j] = u < g.units ? __builtin_nontemporal_load((const v4i*)r.acc + u) : v4i{0, 0, 0, 0};
+                bool ld = u < g.units;
+                if (ld && r.zero_cls != 0) {  // a tap-less sub-pixel class: 0, its accumulators unread
+                    const uint32_t row = fdiv(g.fq, u), t = fdiv(g.fzw, row);
+                    const uint32_t x = row - t * g.fzw.d, y = t - fdiv(g.fzh, t) * g.fzh.d;
+                    ld = !((r.zero_cls >> (2 * (y & 1u) + (x & 1u))) & 1);
+                }
+                v[j] = ld ? __builtin_nontemporal_load((const v4i*)r.acc + u) : v4i{0, 0, 0, 0};
                 mk[j] = (r.relu_mask != nullptr && u < g.units) ? ((const uint32_t*)r.relu_mask)[u] : 0x01010101u;
             }
 #pragma unroll
@@ -3558,6 +3589,7 @@ hipError_t requant_act(const ActRequant& r, hipStream_t st) {
     }
     if (r.pool.dx_c32 != nullptr && (r.pool.dx == nullptr || r.out_p16 != nullptr || r.ldc % 32 != 0))
         return hipErrorInvalidValue;
+    if (r.zero_cls != 0 && (r.out_p16 != nullptr || r.out_c4 != nullptr)) return hipErrorInvalidValue;
     if (r.out_p16 != nullptr) {  // the output (dx with the pool gradient) also as its P16 copy
         if (!requant_p16_ok(r)) return hipErrorInvalidValue;
         RqGeom g{};
@@ -3592,6 +3624,11 @@ hipError_t requant_act(const ActRequant& r, hipStream_t st) {
         if (pf || pb) {
             g.fpw = make_fastdiv((uint32_t)(r.pool.W / 2));
             g.fph = make_fastdiv((uint32_t)(r.pool.H / 2));
+        }
+        if (r.zero_cls != 0) {
+            if (pf || pb || r.zc_h <= 0 || r.zc_w <= 0 || r.rows % ((int64_t)r.zc_h * r.zc_w)) return hipErrorInvalidValue;
+            g.fzw = make_fastdiv((uint32_t)r.zc_w);
+            g.fzh = make_fastdiv((uint32_t)r.zc_h);
         }
         int64_t blocks = (units + 256 * RQ_U - 1) / (256 * RQ_U);
         if (blocks > 2048) blocks = 2048;

@@ -206,6 +206,10 @@ struct ActOut {
     int8_t* exp_out = nullptr;
     PoolFuse pool;                     // only where the phase runs as a separate requant pass
     int8_t* out_p16 = nullptr;         // P16 copy of the output (of pool.dx), separate pass only
+    // rows = pixels [n][zc_h][zc_w]: pixels of the parity classes (y & 1, x & 1) whose bit
+    // 2 (y & 1) + (x & 1) is set in zero_cls are 0 and their accumulators are never read (a stride-2
+    // input gradient's tap-less sub-pixel classes; the plain requantise pass only)
+    int zero_cls = 0, zc_h = 0, zc_w = 0;
 };
 // whether phase 2 of the forward / input-gradient conv requantises in a separate pass (and so
 // can take ActOut::pool); otherwise it recomputes the GEMM with a requantising epilogue
@@ -393,6 +397,7 @@ struct ActRequant {
     // optional P16 copy [pixels/16][ldc][16] of out_nhwc16 (of pool.dx with the pool gradient):
     // the weight-gradient operand of niti_wgrad.hip, written by the same pass
     int8_t* out_p16 = nullptr;
+    int zero_cls = 0, zc_h = 0, zc_w = 0;  // as ActOut's (plain pass, no P16 copy)
 };
 hipError_t requant_act(const ActRequant& r, hipStream_t st);
 // whether requant_act can write out_p16 for this pass: plain (rows % 16 == 0) or the 2x2 pool
