@@ -460,7 +460,8 @@ int64_t niti_model_step_macs(niti_model_t m);
 
 /* Keep each step's int8 weight gradient for niti_model_get_tap(which = 1) (default 1).  With 0 the
  * SGD kernel updates the weights from the int32 gradient without storing the int8 copy, and the
- * tap returns NITI_INVALID_VALUE. */
+ * tap returns NITI_INVALID_VALUE; likewise ResNet-18's stem, whose requantise pass max-pools in
+ * the same pass, then writes no pre-pool output (its which = 0 tap returns NITI_INVALID_VALUE). */
 int niti_model_keep_grads(niti_model_t m, int enable);
 /* Forward convs and input gradients of the stride-1 pad-1 3x3 layers on the register-fed kernel
  * with the rescale fused (niti_rowconv.hip; default 1), or on the LDS-staged GEMM + requantisation

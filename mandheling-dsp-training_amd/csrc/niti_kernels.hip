@@ -1969,7 +1969,8 @@ static hipError_t act_phase2(int op, const LA& la, const LB& lb, int M, int N, i
                              const uint32_t* amax, const ActOut& o, size_t ws_elems, hipStream_t st) {
     const GemmPlan p = plan_gemm(M, N, kc_total, LA::BK / 16, kc_total * 16, true, ws_elems, op);
     if (p.strat == STRAT_RECOMPUTE || p.strat == STRAT_SPEC) {
-        if (o.pool.pool_out != nullptr || o.pool.dx != nullptr || o.out_p16 != nullptr) return hipErrorInvalidValue;
+        if (o.pool.pool_out != nullptr || o.pool.dx != nullptr || o.out_p16 != nullptr || o.pool3.out != nullptr)
+            return hipErrorInvalidValue;
         Epi e;
         e.amax = const_cast<uint32_t*>(amax);
         e.out = o.out;
@@ -1997,6 +1998,7 @@ static hipError_t act_phase2(int op, const LA& la, const LB& lb, int M, int N, i
     r.zero_cls = o.zero_cls;
     r.zc_h = o.zc_h;
     r.zc_w = o.zc_w;
+    r.pool3 = o.pool3;
     return requant_act(r, st);
 }
 
@@ -3577,6 +3579,165 @@ hipError_t conv0_fwd(const ConvGeom& g, const int8_t* xcol, const int8_t* w, uin
     return hipGetLastError();
 }
 
+// The requantisation with the 3x3 / 2 (pad 1) max pool fused (ActRequant::pool3, ResNet-18's
+// stem: NITI_Conv_Int8.cpp:266-307's rescale + relu, then NITI_Maxpool_Int8.cpp:24-72 over the
+// int8 result, first maximum in (ky, kx) order), so the pre-pool int8 image is neither written
+// (unless out_nhwc16) nor read back by a pool pass.  One thread per pooled column strip of
+// RQ3_ROWS pooled rows and 4 channels: each step requantises the two new input rows' three
+// columns and carries the last one down as the next window's top row, so the accumulators are
+// read once vertically (plus one row per strip); the horizontal overlap (the shared column of
+// neighbouring windows) is the neighbouring lanes' load of the same lines.  VALU-bound before
+// the relu forms below (~700 operations per pooled quad: 160 us for the batch-128 stem).
+constexpr int RQ3_ROWS = 8;
+struct Rq3Geom {
+    FastDiv fq, fow, fch;  // by quads per row, pooled width, strips per image
+    int qpr, H, W, OH, rows;  // rows: pooled rows per strip
+    uint32_t units;
+    int remap;  // one thread per unit, blocks XCD-remapped (else grid-stride)
+};
+__device__ __forceinline__ void pool3_take(uint32_t o, int k, uint32_t& m, uint32_t& a) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const int ov = (int8_t)(o >> (8 * e)), mv = (int8_t)(m >> (8 * e)), av = (int8_t)(a >> (8 * e));
+        if (av < 0 || ov > mv) {
+            m = (m & ~(0xffu << (8 * e))) | (o & (0xffu << (8 * e)));
+            a = (a & ~(0xffu << (8 * e))) | ((uint32_t)k << (8 * e));
+        }
+    }
+}
+// relu(PSTO(v, s)) of four accumulators, packed (rq4 with relu and s >= 2, in fewer VALU
+// operations: a <= 0 gives 0 either way, so the sign paths go; the pool is VALU-bound otherwise)
+__device__ __forceinline__ uint32_t rq4_relu(v4i v, int s) {
+    const int h = s >> 1, odd = s & 1;
+    uint32_t o = 0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const uint32_t x = (uint32_t)max(v[e], 0);
+        const uint32_t qp = __builtin_amdgcn_ubfe(x, h, s - h), pr = __builtin_amdgcn_ubfe(x, 0, h) << odd;
+        const uint32_t q = min((x >> s) + (qp > pr ? 1u : 0u), 127u);
+        o |= q << (8 * e);
+    }
+    return o;
+}
+// pool3_take for bytes in [0, 127] (relu outputs), four at once: where o > m (strict: the first
+// maximum stays), m = o and a = k
+__device__ __forceinline__ void pool3_take_u7(uint32_t o, uint32_t k4, uint32_t& m, uint32_t& a) {
+    const uint32_t gt = ((o | 0x80808080u) - m - 0x01010101u) & 0x80808080u;  // bytes: 127 + o - m >= 128
+    const uint32_t mask = (gt >> 7) * 0xffu;
+    m = (m & ~mask) | (o & mask);
+    a = (a & ~mask) | (k4 & mask);
+}
+
+template <bool RELU>
+__global__ void __launch_bounds__(256) requant_pool3_kernel(ActRequant r, Rq3Geom g) {
+    // (wave-uniform: scalar branches below)
+    const int bw = __builtin_amdgcn_readfirstlane(bitwidth_of(read_max(r.amax)));
+    const int shift = bw - 7;
+    const int s = shift > 1 ? shift : 2;
+    const bool raw = shift <= 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0 && r.exp_out != nullptr) {
+        const int inc = shift > 1 ? shift : (shift == 1 ? 2 : 0);
+        const int ein = r.exp_in ? (int)*r.exp_in : 0;
+        const int ws = r.wscale ? (int)*r.wscale : 0;
+        *r.exp_out = (int8_t)(ein + ws + inc);
+    }
+    const uint32_t qpr = (uint32_t)g.qpr;
+    const int OW = (int)g.fow.d;
+    const int64_t RS = (int64_t)g.W * qpr;  // input row stride, quads
+    const uint32_t bid = g.remap ? (uint32_t)xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+    auto rq = [&](const v4i& v) { return RELU && !raw ? rq4_relu(v, s) : rq4(v, raw, s, RELU); };
+    auto take = [&](uint32_t o, int k, uint32_t& m, uint32_t& a) {
+        if (RELU)
+            pool3_take_u7(o, 0x01010101u * (uint32_t)k, m, a);
+        else
+            pool3_take(o, k, m, a);
+    };
+    for (uint32_t u = bid * 256u + threadIdx.x; u < g.units; u += g.remap ? g.units : gridDim.x * 256u) {
+        const uint32_t pix = fdiv(g.fq, u), q = u - pix * qpr;
+        const uint32_t t = fdiv(g.fow, pix), ox = pix - t * g.fow.d;
+        const uint32_t b = fdiv(g.fch, t), ch = t - b * g.fch.d;
+        const int oy0 = (int)ch * g.rows, oy1 = min(g.OH, oy0 + g.rows);
+        const int x0 = 2 * (int)ox - 1;
+        const bool c0 = x0 >= 0, c2 = x0 + 2 < g.W;
+        // columns x0, x0 + 1, x0 + 2 of a row as offsets from column x0 + 1 (a column outside the
+        // image reads column x0 + 1 instead: loaded, never taken)
+        const int64_t o0 = c0 ? -(int64_t)qpr : 0, o2 = c2 ? (int64_t)qpr : 0;
+        const v4i* p = (const v4i*)r.acc + ((int64_t)b * g.H * g.W + 2 * oy0 * g.W + x0 + 1) * qpr + q;
+        uint32_t* y0 = r.out_nhwc16 ? (uint32_t*)r.out_nhwc16 + (p - (const v4i*)r.acc) : nullptr;
+        // the two input rows 2 oy, 2 oy + 1 at p (the second: the first again past the image)
+        auto load = [&](const v4i* p, int oy, v4i* a) {
+            const v4i* p1 = 2 * oy + 1 < g.H ? p + RS : p;
+            a[0] = p[o0];
+            a[1] = p[0];
+            a[2] = p[o2];
+            a[3] = p1[o0];
+            a[4] = p1[0];
+            a[5] = p1[o2];
+        };
+        uint32_t top[3] = {0, 0, 0};
+        if (oy0 > 0) {
+            const v4i* pt = p - RS;
+            top[0] = rq(pt[o0]);
+            top[1] = rq(pt[0]);
+            top[2] = rq(pt[o2]);
+        }
+        auto step = [&](const v4i* a, int oy) {
+            const bool r2 = 2 * oy + 1 < g.H;
+            uint32_t mid[3], bot[3];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                mid[k] = rq(a[k]);
+                bot[k] = rq(a[3 + k]);
+            }
+            // bytes: max, position.  With relu every value is >= 0: start from 0 at the window's
+            // first position, later positions taken where strictly greater (the first maximum)
+            uint32_t m = RELU ? 0u : 0x80808080u;
+            uint32_t am = RELU ? 0x01010101u * (uint32_t)((oy > 0 ? 0 : 3) + (c0 ? 0 : 1)) : 0xffffffffu;
+            if (oy > 0) {
+                if (c0) take(top[0], 0, m, am);
+                take(top[1], 1, m, am);
+                if (c2) take(top[2], 2, m, am);
+            }
+            if (c0) take(mid[0], 3, m, am);
+            take(mid[1], 4, m, am);
+            if (c2) take(mid[2], 5, m, am);
+            if (r2) {
+                if (c0) take(bot[0], 6, m, am);
+                take(bot[1], 7, m, am);
+                if (c2) take(bot[2], 8, m, am);
+            }
+            const int64_t po = (((int64_t)b * g.OH + oy) * OW + ox) * qpr + q;
+            ((uint32_t*)r.pool3.out)[po] = m;
+            ((uint32_t*)r.pool3.arg)[po] = am;
+            if (y0 != nullptr) {  // each pre-pool pixel once: rows 2 oy, 2 oy + 1 x columns x0 + 1, x0 + 2
+                uint32_t* d = y0 + (int64_t)(oy - oy0) * 2 * RS;
+                d[0] = mid[1];
+                if (c2) d[qpr] = mid[2];
+                if (r2) {
+                    d[RS] = bot[1];
+                    if (c2) d[RS + qpr] = bot[2];
+                }
+            }
+            top[0] = bot[0];
+            top[1] = bot[1];
+            top[2] = bot[2];
+        };
+        // two register sets, each step's rows loaded one step ahead
+        v4i A[6], B[6];
+        load(p, oy0, A);
+        for (int oy = oy0;;) {
+            if (oy + 1 < oy1) load(p + 2 * RS, oy + 1, B);
+            step(A, oy);
+            if (++oy >= oy1) break;
+            p += 2 * RS;
+            if (oy + 1 < oy1) load(p + 2 * RS, oy + 1, A);
+            step(B, oy);
+            if (++oy >= oy1) break;
+            p += 2 * RS;
+        }
+    }
+}
+
 hipError_t requant_act(const ActRequant& r, hipStream_t st) {
     if (r.ldc % 16 != 0 || r.acc == nullptr || r.amax == nullptr) return hipErrorInvalidValue;
     if (r.pool.pool_out != nullptr || r.pool.dx != nullptr) {
@@ -3590,6 +3751,37 @@ hipError_t requant_act(const ActRequant& r, hipStream_t st) {
     if (r.pool.dx_c32 != nullptr && (r.pool.dx == nullptr || r.out_p16 != nullptr || r.ldc % 32 != 0))
         return hipErrorInvalidValue;
     if (r.zero_cls != 0 && (r.out_p16 != nullptr || r.out_c4 != nullptr)) return hipErrorInvalidValue;
+    if (r.pool3.out != nullptr) {
+        const Pool3& p = r.pool3;
+        if (r.out_p16 != nullptr || r.out_c4 != nullptr || r.zero_cls != 0 || r.pool.pool_out != nullptr ||
+            r.pool.dx != nullptr || r.relu_mask != nullptr || p.arg == nullptr || r.ldc % 4 != 0 || p.H <= 0 ||
+            p.W <= 0 || p.OH != (p.H - 1) / 2 + 1 || p.OW != (p.W - 1) / 2 + 1 || r.rows % ((int64_t)p.H * p.W) != 0)
+            return hipErrorInvalidValue;
+        Rq3Geom g;
+        g.qpr = r.ldc / 4;
+        g.H = p.H;
+        g.W = p.W;
+        g.OH = p.OH;
+        static const int rows_env = getenv("NITI_RQ3_ROWS") ? atoi(getenv("NITI_RQ3_ROWS")) : RQ3_ROWS;
+        static const int remap_env = getenv("NITI_RQ3_REMAP") ? atoi(getenv("NITI_RQ3_REMAP")) : 1;
+        g.rows = rows_env > 0 ? rows_env : RQ3_ROWS;
+        const int strips = (p.OH + g.rows - 1) / g.rows;
+        const int64_t units = r.rows / ((int64_t)p.H * p.W) * strips * p.OW * g.qpr;
+        if (units >= (int64_t)1 << 31) return hipErrorInvalidValue;
+        g.units = (uint32_t)units;
+        g.fq = make_fastdiv((uint32_t)g.qpr);
+        g.fow = make_fastdiv((uint32_t)p.OW);
+        g.fch = make_fastdiv((uint32_t)strips);
+        int64_t blocks = (units + 255) / 256;
+        g.remap = remap_env != 0 && blocks <= ((int64_t)1 << 24);
+        if (!g.remap && blocks > 8192) blocks = 8192;
+        if (blocks < 1) blocks = 1;
+        if (r.relu)
+            hipLaunchKernelGGL(requant_pool3_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, st, r, g);
+        else
+            hipLaunchKernelGGL(requant_pool3_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, st, r, g);
+        return hipGetLastError();
+    }
     if (r.out_p16 != nullptr) {  // the output (dx with the pool gradient) also as its P16 copy
         if (!requant_p16_ok(r)) return hipErrorInvalidValue;
         RqGeom g{};
@@ -4055,7 +4247,9 @@ __global__ void maxpool_argmax_kernel(const int8_t* __restrict__ x, const int8_t
 
 __global__ void maxpool_grad_gather_kernel(const int8_t* __restrict__ x, const int8_t* __restrict__ arg,
                                            const int8_t* __restrict__ dy, int n, int h, int w, int cp, int k, int s,
-                                           int p, int oh, int ow, int relu, int8_t* __restrict__ dx) {
+                                           int p, int oh, int ow, int relu, int8_t* __restrict__ dx,
+                                           const int8_t* __restrict__ pooled) {
+    const bool ymask = relu && pooled != nullptr;  // the relu mask from the window's pooled value
     const uint32_t groups = cp / 16;
     const uint32_t total = (uint32_t)n * h * w * groups;  // < 2^31 (host)
     for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
@@ -4078,12 +4272,14 @@ __global__ void maxpool_grad_gather_kernel(const int8_t* __restrict__ x, const i
                 const int64_t po = (((int64_t)b * oh + oy) * ow + ox) * cp + gi * 16;
                 const v16c av = *(const v16c*)(arg + po);
                 const v16c dv = *(const v16c*)(dy + po);
+                v16c pv;
+                if (ymask) pv = *(const v16c*)(pooled + po);
                 const signed char me = (signed char)(ky * k + kx);
 #pragma unroll
                 for (int j = 0; j < 16; ++j)
-                    if (av[j] == me) acc[j] = (signed char)(acc[j] + dv[j]);
+                    if (av[j] == me && (!ymask || pv[j] > 0)) acc[j] = (signed char)(acc[j] + dv[j]);
             }
-        if (relu) {
+        if (relu && !ymask) {
             const v16c xv = *(const v16c*)(x + (int64_t)t * 16);
 #pragma unroll
             for (int j = 0; j < 16; ++j) acc[j] = xv[j] > 0 ? acc[j] : (signed char)0;
@@ -4100,19 +4296,21 @@ hipError_t maxpool_relu_grad_ws(const int8_t* x, const int8_t* y, const int8_t* 
     auto blocks = [](int64_t t) { return (unsigned)std::max<int64_t>(1, std::min<int64_t>((t + 255) / 256, 8192)); };
     hipLaunchKernelGGL(maxpool_argmax_kernel, dim3(blocks(tw)), dim3(256), 0, st, x, y, n, h, w, cp, k, s, p, oh, ow, ws);
     hipLaunchKernelGGL(maxpool_grad_gather_kernel, dim3(blocks(tx)), dim3(256), 0, st, x, ws, dy, n, h, w, cp, k, s, p,
-                       oh, ow, relu, dx);
+                       oh, ow, relu, dx, (const int8_t*)nullptr);
     return hipGetLastError();
 }
 
 // the same gradient from the first-max positions the forward maxpool_nhwc16 wrote (`arg`): one pass
 hipError_t maxpool_relu_grad_arg(const int8_t* x, const int8_t* arg, const int8_t* dy, int n, int h, int w, int cp,
-                                 int k, int s, int p, int oh, int ow, int relu, int8_t* dx, hipStream_t st) {
+                                 int k, int s, int p, int oh, int ow, int relu, int8_t* dx, hipStream_t st,
+                                 const int8_t* pooled) {
     if (cp % 16 != 0 || k <= 0 || k > 11 || s <= 0 || arg == nullptr) return hipErrorInvalidValue;
+    if (relu && pooled == nullptr && x == nullptr) return hipErrorInvalidValue;
     const int64_t tx = (int64_t)n * h * w * (cp / 16);
     if (tx >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
     const unsigned blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>((tx + 255) / 256, 8192));
     hipLaunchKernelGGL(maxpool_grad_gather_kernel, dim3(blocks), dim3(256), 0, st, x, arg, dy, n, h, w, cp, k, s, p, oh,
-                       ow, relu, dx);
+                       ow, relu, dx, pooled);
     return hipGetLastError();
 }
 

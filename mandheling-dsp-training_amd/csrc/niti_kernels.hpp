@@ -197,8 +197,17 @@ struct PoolFuse {
     // gradient's operand; separate requant pass without a P16 copy, ld % 32 == 0), or null
     int8_t* dx_c32 = nullptr;
 };
+// The 3x3 / 2 max pool (pad 1, NITI_Maxpool_Int8.cpp:24-72) over the requantised output: rows =
+// pixels [n][H][W]; out [n][OH][OW][ld] the pooled image, arg the same with each window's
+// first-max position ky * 3 + kx (maxpool_nhwc16's `arg`); the pre-pool output (ActOut::out) is
+// optional.  Separate plain requant pass only (ResNet-18's stem).
+struct Pool3 {
+    int8_t* out = nullptr;
+    int8_t* arg = nullptr;
+    int H = 0, W = 0, OH = 0, OW = 0;
+};
 struct ActOut {
-    int8_t* out = nullptr;             // NHWC16 [rows][ld] (may be null with pool.dx)
+    int8_t* out = nullptr;             // NHWC16 [rows][ld] (may be null with pool.dx or pool3)
     int relu = 0;                      // fused NITI_Relu_Int8
     const int8_t* relu_mask = nullptr; // fused NITI_ReluGrad_Int8 (out = mask > 0 ? q : 0)
     const int8_t* exp_in = nullptr;
@@ -210,6 +219,7 @@ struct ActOut {
     // 2 (y & 1) + (x & 1) is set in zero_cls are 0 and their accumulators are never read (a stride-2
     // input gradient's tap-less sub-pixel classes; the plain requantise pass only)
     int zero_cls = 0, zc_h = 0, zc_w = 0;
+    Pool3 pool3;
 };
 // whether phase 2 of the forward / input-gradient conv requantises in a separate pass (and so
 // can take ActOut::pool); otherwise it recomputes the GEMM with a requantising epilogue
@@ -398,6 +408,7 @@ struct ActRequant {
     // the weight-gradient operand of niti_wgrad.hip, written by the same pass
     int8_t* out_p16 = nullptr;
     int zero_cls = 0, zc_h = 0, zc_w = 0;  // as ActOut's (plain pass, no P16 copy)
+    Pool3 pool3;                           // as ActOut's (out_nhwc16 optional)
 };
 hipError_t requant_act(const ActRequant& r, hipStream_t st);
 // whether requant_act can write out_p16 for this pass: plain (rows % 16 == 0) or the 2x2 pool
@@ -473,9 +484,12 @@ hipError_t relu_grad_nhwc16(const int8_t* x, const int8_t* dy, int64_t n, int8_t
 // position, then a gather per input pixel): for overlapping windows (ResNet's 3x3 / 2 stem pool)
 hipError_t maxpool_relu_grad_ws(const int8_t* x, const int8_t* y, const int8_t* dy, int n, int h, int w, int cp, int k,
                                 int s, int p, int oh, int ow, int relu, int8_t* ws, int8_t* dx, hipStream_t st);
-// the same from the forward's first-max positions (maxpool_nhwc16 with arg): one pass
+// the same from the forward's first-max positions (maxpool_nhwc16 with arg): one pass.  With
+// `pooled` (the forward's pooled output y) the relu gradient's mask comes from y instead of x (x
+// may be null): a pixel gets a gradient only from windows whose first max it is, where y = x
 hipError_t maxpool_relu_grad_arg(const int8_t* x, const int8_t* arg, const int8_t* dy, int n, int h, int w, int cp,
-                                 int k, int s, int p, int oh, int ow, int relu, int8_t* dx, hipStream_t st);
+                                 int k, int s, int p, int oh, int ow, int relu, int8_t* dx, hipStream_t st,
+                                 const int8_t* pooled = nullptr);
 // logits int8 [batch][ld] (first `classes` used), labels int32 [batch] (class index);
 // out int8 [batch][ld] (padded lanes zeroed).  classes <= 2048 (one thread per sample up to 16,
 // one block per sample above).  NITI_CPULossGrad_Int8.cpp:81-200.

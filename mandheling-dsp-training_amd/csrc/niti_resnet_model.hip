@@ -340,6 +340,18 @@ int ResNetModel::fwd_conv(int i, hipStream_t st) {
     o.exp_in = c.in_exp;
     o.wscale = c.ws_dev;
     o.exp_out = c.y_exp;
+    if (i == 0) {  // the stem: its 3x3 / 2 max pool in the requantise pass when there is one
+        stem_pooled = !conv_fwd_spec_ok(g) && conv_fwd_phase2_separate(g, slab_bytes);
+        if (stem_pooled) {
+            const int ph = C[B[0].a].g.h;
+            o.pool3.out = p0;
+            o.pool3.arg = pool_ws;
+            o.pool3.H = g.oh;
+            o.pool3.W = g.ow;
+            o.pool3.OH = o.pool3.OW = ph;
+            if (!keep_grads) o.out = nullptr;  // (the pre-pool output: only its tap reads it)
+        }
+    }
     if (conv_fwd_spec_ok(g)) {  // the GEMM's speculative pair (plan strategy 3)
         int8_t* alt = conv_fwd_spec_alt_bytes(g) <= gspec_alt_bytes ? gspec_alt : nullptr;
         RTRY(conv_fwd_spec(g, c.in, c.w, rng(i, 0), o, c.gspec, 0, st, alt));
@@ -582,7 +594,8 @@ int ResNetModel::run(const int8_t* x_nchw, int exp_in, const uint8_t* images, co
     int rc = fwd_conv(0, st);
     if (rc != NITI_NO_ERROR) return rc;
     const int ph = C[B[0].a].g.h;  // the stem's pooled size
-    RTRY(maxpool_nhwc16(C[0].y, n, stem.oh, stem.ow, 64, 3, 2, 1, p0, ph, ph, st, pool_ws));  // + first-max positions
+    if (!stem_pooled)  // (else fused into the stem's requantise pass)
+        RTRY(maxpool_nhwc16(C[0].y, n, stem.oh, stem.ow, 64, 3, 2, 1, p0, ph, ph, st, pool_ws));  // + first-max positions
     for (int k = 0; k < (int)B.size(); ++k) {
         const RBlock& b = B[k];
         if ((rc = fwd_conv(b.a, st)) != NITI_NO_ERROR) return rc;
@@ -627,7 +640,8 @@ int ResNetModel::run(const int8_t* x_nchw, int exp_in, const uint8_t* images, co
     }
     // the stem: overlapping 3x3 / 2 max-pool gradient (first max wins) with the relu gradient, then
     // its weight gradient over the im2col
-    RTRY(maxpool_relu_grad_arg(C[0].y, pool_ws, B[0].du, n, stem.oh, stem.ow, 64, 3, 2, 1, ph, ph, 1, d0, st));
+    // (the relu mask from the pooled output: the pre-pool output may not exist)
+    RTRY(maxpool_relu_grad_arg(nullptr, pool_ws, B[0].du, n, stem.oh, stem.ow, 64, 3, 2, 1, ph, ph, 1, d0, st, p0));
     if ((rc = wg(0)) != NITI_NO_ERROR) return rc;
     if (dp) {  // every bucket summed and ranged before the update
         if (!shared_comm) {
@@ -730,6 +744,14 @@ int ResNetModel::autotune(hipStream_t st, int reps) {
     tuning = true;
     int rc = NITI_NO_ERROR;
     auto run_op = [&](int i, int op) {
+        if (op == PLAN_FWD && i == 0) {  // the stem with its max pool (fused into a separate requantise pass)
+            int r = fwd_conv(0, st);
+            if (r == NITI_NO_ERROR && !stem_pooled &&
+                maxpool_nhwc16(C[0].y, batch, stem.oh, stem.ow, 64, 3, 2, 1, p0, C[B[0].a].g.h, C[B[0].a].g.w, st,
+                               pool_ws) != hipSuccess)
+                r = NITI_NO_EXECUTION;
+            return r;
+        }
         return op == PLAN_FWD ? fwd_conv(i, st) : op == PLAN_WGRAD ? wgrad_conv(i, st) : dgrad_conv(i, st);
     };
     auto time_op = [&](int i, int op, float* us) -> int {
@@ -903,6 +925,7 @@ int ResNetModel::get_tap(int layer, int which, int8_t* host, size_t bytes, hipSt
     const int n = batch;
     if (hipStreamSynchronize(st) != hipSuccess) return NITI_NO_EXECUTION;
     size_t need = 0;
+    if (which == 0 && layer == 0 && stem_pooled && !keep_grads) return NITI_INVALID_VALUE;  // (never written)
     if (which == 0 || which == 2)
         need = (size_t)n * g.c_out * g.oh * g.ow;
     else if (which == 1 && keep_grads)

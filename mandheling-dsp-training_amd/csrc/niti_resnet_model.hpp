@@ -86,7 +86,10 @@ struct ResNetModel {
     int8_t* exp0 = nullptr;
     int8_t* xcol = nullptr;       // the stem's im2col [n * oh * ow][STEM_KP]
     int8_t* p0 = nullptr;         // 3x3 / 2 max pool of the stem output
-    int8_t* pool_ws = nullptr;    // the pool gradient's first-max workspace
+    int8_t* pool_ws = nullptr;    // each pool window's first-max position (the pool gradient's)
+    // the stem's requantise pass also max-pooled (Pool3) this step; with keep_grads off its pre-pool
+    // output is then never written (its forward tap is unavailable)
+    bool stem_pooled = false;
     int8_t* d0 = nullptr;         // the stem's output gradient
     int32_t* gsum = nullptr;      // global sum pool [n][512]
     int8_t* g8pool = nullptr;     // its requantisation (the fc input)

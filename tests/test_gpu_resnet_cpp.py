@@ -325,3 +325,52 @@ def test_resnet18_cpp_subpix_dgrad_plans(T, plan):
             W = newW
     finally:
         NitiModel.reset_plans()
+
+
+@pytest.mark.parametrize("hw,batch,stem_plan", [(64, 3, (128, 64, 1, 0)), (112, 2, (128, 64, 1, 0)),
+                                                (64, 3, (128, 64, 1, 1))])
+def test_resnet18_cpp_without_debug_taps(T, hw, batch, stem_plan):
+    """keep_grads(False), as bench.py steps: no int8 weight-gradient copies and, with a stem plan
+    that requantises in a separate pass (strategy 0), the stem's requantise pass max-pools without
+    writing its pre-pool output (Pool3); with the recompute plan (1) the pool stays its own pass.
+    Every other tap, the logits and the new weights still equal the oracle's; the weight-gradient
+    taps, and the stem's forward tap when fused, report NITI_INVALID_VALUE."""
+    import niti_resnet_ref as RR
+    import niti_oracle as O
+    from niti_amd._lib import NitiError
+    from niti_amd.model import NitiModel
+    convs = RR.resnet18_convs(hw, 1000)
+    W, S = RR.init_weights(convs, seed=hw + 7)
+    rng = np.random.default_rng(hw + 7)
+    m = _model(batch, hw, 1000, W, S)
+    m.keep_grads(False)
+    m.set_plan(0, 0, stem_plan)
+    try:
+        _steps_without_taps(T, m, RR, O, NitiError, convs, W, S, rng, batch, hw, stem_plan[3] == 0)
+    finally:
+        NitiModel.reset_plans()
+
+
+def _steps_without_taps(T, m, RR, O, NitiError, convs, W, S, rng, batch, hw, fused):
+    for step in range(2):
+        x = rng.integers(-127, 128, (batch, 3, hw, hw)).astype(np.int8)
+        lab = rng.integers(0, 1000, batch).astype(np.int32)
+        newW, rec = RR.train_step(convs, W, S, x, -2, lab, classes=1000)
+        m.train_step(T.from_numpy(x).cuda(), -2, T.from_numpy(lab).cuda())
+        lg, e = m.logits()
+        assert e == rec["exp_logits"] and np.array_equal(lg, rec["logits"]), step
+        for i, c in enumerate(convs):
+            if i > 0:
+                f = O.relu(rec["fwd"][i]) if m.layers[i]["relu"] else rec["fwd"][i]
+                assert np.array_equal(m.tap(i, 0), f), ("fwd", step, c["name"])
+            assert np.array_equal(m.tap(i, 2), rec["dy"][i]), ("dy", step, c["name"])
+            assert np.array_equal(m.get_weight(i), newW[i]), ("w", step, c["name"])
+        if fused:
+            with pytest.raises(NitiError):
+                m.tap(0, 0)
+        else:
+            assert np.array_equal(m.tap(0, 0), O.relu(rec["fwd"][0])), ("fwd", step, "stem")
+        with pytest.raises(NitiError):
+            m.tap(1, 1)
+        W = newW
+    assert m.rowconv_error() == 0
