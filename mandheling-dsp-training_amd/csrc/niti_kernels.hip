@@ -3588,7 +3588,7 @@ hipError_t conv0_fwd(const ConvGeom& g, const int8_t* xcol, const int8_t* w, uin
 // read once vertically (plus one row per strip); the horizontal overlap (the shared column of
 // neighbouring windows) is the neighbouring lanes' load of the same lines.  VALU-bound before
 // the relu forms below (~700 operations per pooled quad: 160 us for the batch-128 stem).
-constexpr int RQ3_ROWS = 8;
+constexpr int RQ3_ROWS = 4;  // (2-28 measured: 103-113 us, profiles/r05_stem_pool.txt)
 struct Rq3Geom {
     FastDiv fq, fow, fch;  // by quads per row, pooled width, strips per image
     int qpr, H, W, OH, rows;  // rows: pooled rows per strip
@@ -3763,7 +3763,7 @@ hipError_t requant_act(const ActRequant& r, hipStream_t st) {
         g.W = p.W;
         g.OH = p.OH;
         static const int rows_env = getenv("NITI_RQ3_ROWS") ? atoi(getenv("NITI_RQ3_ROWS")) : RQ3_ROWS;
-        static const int remap_env = getenv("NITI_RQ3_REMAP") ? atoi(getenv("NITI_RQ3_REMAP")) : 1;
+        static const int remap_env = getenv("NITI_RQ3_REMAP") ? atoi(getenv("NITI_RQ3_REMAP")) : 0;
         g.rows = rows_env > 0 ? rows_env : RQ3_ROWS;
         const int strips = (p.OH + g.rows - 1) / g.rows;
         const int64_t units = r.rows / ((int64_t)p.H * p.W) * strips * p.OW * g.qpr;
