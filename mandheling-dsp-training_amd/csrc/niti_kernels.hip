@@ -4288,6 +4288,46 @@ __global__ void maxpool_grad_gather_kernel(const int8_t* __restrict__ x, const i
     }
 }
 
+// The same gather for the 3x3 / 2 pad-1 pool with the relu mask from the pooled output (ResNet-18's
+// stem): four bytes at a time per 32-bit word (first-max match, pooled > 0, wrapping int8 sum)
+// instead of a byte loop -- the byte form is VALU-bound.  Pooled values are relu outputs (>= 0).
+struct PoolGradGeom {
+    FastDiv fg, fw, fh;  // by 16-channel groups, input width, input height
+    int oh, ow;
+    uint32_t total;
+};
+__global__ void __launch_bounds__(256) maxpool3_grad_pooled_kernel(const uint4* __restrict__ arg, const uint4* __restrict__ dy,
+                                                                   const uint4* __restrict__ pooled, PoolGradGeom g,
+                                                                   uint4* __restrict__ dx) {
+    const uint32_t groups = g.fg.d, w = g.fw.d, h = g.fh.d;
+    for (uint32_t t = blockIdx.x * 256u + threadIdx.x; t < g.total; t += gridDim.x * 256u) {
+        const uint32_t r0 = fdiv(g.fg, t), gi = t - r0 * groups;
+        const uint32_t r1 = fdiv(g.fw, r0), ix = r0 - r1 * w;
+        const uint32_t b = fdiv(g.fh, r1), iy = r1 - b * h;
+        uint32_t acc[4] = {0, 0, 0, 0};
+        // windows oy with 2 oy - 1 <= iy <= 2 oy + 1 (ky = iy + 1 - 2 oy), likewise ox
+        const int oy_lo = ((int)iy) >> 1, oy_hi = min(g.oh - 1, ((int)iy + 1) >> 1);
+        const int ox_lo = ((int)ix) >> 1, ox_hi = min(g.ow - 1, ((int)ix + 1) >> 1);
+        for (int oy = oy_lo; oy <= oy_hi; ++oy)
+            for (int ox = ox_lo; ox <= ox_hi; ++ox) {
+                const uint32_t me = (uint32_t)(((int)iy + 1 - 2 * oy) * 3 + ((int)ix + 1 - 2 * ox)) * 0x01010101u;
+                const int64_t po = (((int64_t)b * g.oh + oy) * g.ow + ox) * groups + gi;
+                const uint4 av = arg[po], dv = dy[po], pv = pooled[po];
+                const uint32_t aw[4] = {av.x, av.y, av.z, av.w}, dw[4] = {dv.x, dv.y, dv.z, dv.w},
+                               pw[4] = {pv.x, pv.y, pv.z, pv.w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const uint32_t d = aw[e] ^ me;  // 0 bytes: this pixel is the window's first max
+                    const uint32_t hit = ~(((d & 0x7f7f7f7fu) + 0x7f7f7f7fu) | d | 0x7f7f7f7fu);
+                    const uint32_t pos = ((pw[e] & 0x7f7f7f7fu) + 0x7f7f7f7fu) & ~pw[e] & 0x80808080u;  // pooled > 0
+                    const uint32_t c = dw[e] & (((hit & pos) >> 7) * 0xffu);
+                    acc[e] = ((acc[e] & 0x7f7f7f7fu) + (c & 0x7f7f7f7fu)) ^ ((acc[e] ^ c) & 0x80808080u);
+                }
+            }
+        dx[t] = uint4{acc[0], acc[1], acc[2], acc[3]};
+    }
+}
+
 hipError_t maxpool_relu_grad_ws(const int8_t* x, const int8_t* y, const int8_t* dy, int n, int h, int w, int cp, int k,
                                 int s, int p, int oh, int ow, int relu, int8_t* ws, int8_t* dx, hipStream_t st) {
     if (cp % 16 != 0 || k <= 0 || k > 11 || s <= 0 || ws == nullptr) return hipErrorInvalidValue;
@@ -4308,6 +4348,19 @@ hipError_t maxpool_relu_grad_arg(const int8_t* x, const int8_t* arg, const int8_
     if (relu && pooled == nullptr && x == nullptr) return hipErrorInvalidValue;
     const int64_t tx = (int64_t)n * h * w * (cp / 16);
     if (tx >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
+    if (relu && pooled != nullptr && k == 3 && s == 2 && p == 1 && oh == (h - 1) / 2 + 1 && ow == (w - 1) / 2 + 1) {
+        PoolGradGeom g;
+        g.fg = make_fastdiv((uint32_t)(cp / 16));
+        g.fw = make_fastdiv((uint32_t)w);
+        g.fh = make_fastdiv((uint32_t)h);
+        g.oh = oh;
+        g.ow = ow;
+        g.total = (uint32_t)tx;
+        const unsigned blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>((tx + 255) / 256, 8192));
+        hipLaunchKernelGGL(maxpool3_grad_pooled_kernel, dim3(blocks), dim3(256), 0, st, (const uint4*)arg,
+                           (const uint4*)dy, (const uint4*)pooled, g, (uint4*)dx);
+        return hipGetLastError();
+    }
     const unsigned blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>((tx + 255) / 256, 8192));
     hipLaunchKernelGGL(maxpool_grad_gather_kernel, dim3(blocks), dim3(256), 0, st, x, arg, dy, n, h, w, cp, k, s, p, oh,
                        ow, relu, dx, pooled);
