@@ -323,6 +323,9 @@ void niti_diag_rowconv_speculate(int mode);
  * bit width + bias: +-1 makes launch B settle from an alternate, 2 makes it redo the GEMM (tests);
  * 0 (default) off.  Results are the rule's whatever the bias. */
 void niti_diag_gemm_speculate(int bias);
+/* diagnostics: implicit-GEMM launches of this process that ran with the rescale fused behind the
+ * in-kernel grid barrier (plan strategy 4) */
+unsigned long long niti_diag_gemm_fused_launches(void);
 /* jobs per P16 input-copy launch of a model step for later steps (<= 0: the default 16); a small
  * cap sends a step down its more-than-one-launch branches.  Results are identical for every cap. */
 void niti_diag_p16_jobs_cap(int cap);
@@ -489,7 +492,11 @@ int niti_model_autotune(niti_model_t m, int reps, void* stream);
 /* The plan a layer phase (0 forward, 1 input gradient, 2 weight gradient) runs with:
  * {bm, bn, splits, strategy 0 store / 1 recompute / 2 split-K / 3 the speculative pair (forward and
  * input gradient, unsplit: launch A requantises with the layer's previous bit width and publishes the
- * range, launch B redoes the GEMM only when the range's bit width differs)}. */
+ * range, launch B redoes the GEMM only when the range's bit width differs) / 4 fused (forward and
+ * stride-1 input gradient, unsplit: one launch whose blocks keep their accumulators in registers
+ * across an in-kernel grid barrier carrying the tensor's bit width, then requantise -- where every
+ * tile is resident at once and no collective sits between range and requantisation; elsewhere it
+ * runs as 1)}. */
 int niti_model_plan_info(niti_model_t m, int layer, int phase, int info[4]);
 /* Force a plan for a layer phase ({bm 64|128, bn 64|128, splits >= 1, strategy}; split counts
  * beyond the K steps or the workspace are clamped; recompute on the weight gradient means

@@ -247,7 +247,7 @@ int niti_conv_plan_set(const niti_geom* g, int op, const int plan[4]) {
     const bool taps = plan[0] == niti::PLAN_TAPS_TILE && plan[1] == niti::PLAN_TAPS_TILE && pop == niti::PLAN_WGRAD &&
                       niti::conv_wgrad_taps_ok(r);
     if ((!taps && (!tile_ok(plan[0]) || !tile_ok(plan[1]))) || plan[2] < 1 || plan[2] > 4096 || plan[3] < 0 ||
-        plan[3] > 3 || (taps && plan[3] == 1) || (plan[3] == 3 && (pop == niti::PLAN_WGRAD || plan[2] != 1)))
+        plan[3] > 4 || (taps && plan[3] == 1) || (plan[3] >= 3 && (pop == niti::PLAN_WGRAD || plan[2] != 1)))
         return NITI_INVALID_VALUE;
     niti::PlanChoice c;
     c.bm = plan[0];
@@ -467,6 +467,7 @@ void niti_diag_rowconv_barrier(uint32_t spin_limit, uint32_t expect_extra) {
 }
 void niti_diag_rowconv_speculate(int mode) { niti::rowconv_speculate(mode); }
 void niti_diag_gemm_speculate(int bias) { niti::gemm_speculate_bias(bias); }
+unsigned long long niti_diag_gemm_fused_launches(void) { return niti::gemm_fused_launches(); }
 void niti_diag_p16_jobs_cap(int cap) { niti::model_p16_jobs_cap(cap); }
 
 int niti_conv_wgrad_p16_workspace(const niti_geom* g, int splits, size_t* bytes) {

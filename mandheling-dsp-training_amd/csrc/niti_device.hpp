@@ -70,6 +70,43 @@ __device__ __forceinline__ uint32_t read_max(const uint32_t* amax) {
     return wave_max(amax[(threadIdx.x & 63) * MAX_SLOT_STRIDE]);
 }
 
+// SWAR on 4 int8 lanes of a dword; a "hi" result is meaningful in bit 7 of each byte only
+constexpr uint32_t SW_H = 0x80808080u, SW_L = 0x7F7F7F7Fu;
+__device__ __forceinline__ uint32_t sw_ge_hi(uint32_t x, uint32_t m) {  // signed x >= m
+    const uint32_t ax = x ^ SW_H, bm = m ^ SW_H;  // as unsigned
+    const uint32_t t = (ax | SW_H) - (bm & SW_L);  // bit 7: low 7 bits of ax >= those of bm
+    const uint32_t d = ax ^ bm;                    // bit 7: the top bits differ -> ax's top bit decides
+    return ((d & ax) | (~d & t)) & SW_H;
+}
+__device__ __forceinline__ uint32_t sw_pos_hi(uint32_t x) {  // signed x > 0
+    const uint32_t nz = (((x & SW_L) + SW_L) | x) & SW_H;
+    return nz & ~x;
+}
+__device__ __forceinline__ uint32_t sw_expand(uint32_t hb) { return hb | (hb - (hb >> 7)); }
+
+// The 2x2 max pool's gradient route, decided by the forward pass that pools (NITI_CPUPoolGrad_Int8.cpp:
+// 21-77: the first window element -- (0,0), (0,1), (1,0), (1,1) -- that is >= the pooled value takes
+// the gradient): one code byte per pooled element and channel, bit t set when window element t
+// takes it and, for a relu layer, the pooled value (the routed element's own value) is > 0 -- the
+// relu gradient of NITI_ReluGrad_Int8 at that element.  4 channels per dword: t0..t3 the window's
+// elements, m their max.  The input-gradient pass reads one byte per pooled element instead of the
+// 4 window elements and the pooled value.
+__device__ __forceinline__ uint32_t pool_code4(uint32_t t0, uint32_t t1, uint32_t t2, uint32_t t3, uint32_t m,
+                                               bool relu) {
+    const uint32_t h0 = sw_ge_hi(t0, m);
+    const uint32_t h1 = sw_ge_hi(t1, m) & ~h0;
+    const uint32_t d1 = h0 | h1;
+    const uint32_t h2 = sw_ge_hi(t2, m) & ~d1;
+    const uint32_t h3 = SW_H & ~(d1 | h2);
+    uint32_t code = (h0 >> 7) | (h1 >> 6) | (h2 >> 5) | (h3 >> 4);
+    if (relu) code &= sw_expand(sw_pos_hi(m));
+    return code;
+}
+// the byte mask (0xff where it takes the gradient) of window element t from 4 code bytes
+__device__ __forceinline__ uint32_t pool_code_mask(uint32_t code, int t) {
+    return sw_expand(((code >> t) & 0x01010101u) << 7);
+}
+
 // The residual rule (niti_resnet.hip): z = hi * 2^d + (lo >> r), arithmetic shift
 __device__ __forceinline__ int32_t residual_z(int32_t hi, int32_t lo, int d, int r) {
     return hi * (1 << d) + (r >= 31 ? (lo < 0 ? -1 : 0) : lo >> r);

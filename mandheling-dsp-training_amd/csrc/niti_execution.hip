@@ -251,6 +251,17 @@ void* Workspace::alloc(size_t bytes) {
     total += bytes;
     return p;
 }
+void* Workspace::replace(void* old, size_t bytes) {
+    if (old != nullptr) {
+        for (size_t i = 0; i < ptrs.size(); ++i)
+            if (ptrs[i] == old) {
+                (void)hipFree(old);
+                ptrs.erase(ptrs.begin() + i);
+                break;
+            }
+    }
+    return alloc(bytes);
+}
 void Workspace::release() {
     for (void* p : ptrs) (void)hipFree(p);
     ptrs.clear();

@@ -17,6 +17,8 @@ struct Workspace {
     std::vector<void*> ptrs;
     size_t total = 0;
     void* alloc(size_t bytes);
+    // free `old` (one of ours, or null) and allocate `bytes` in its place
+    void* replace(void* old, size_t bytes);
     void release();
     ~Workspace() { release(); }
 };

@@ -13,6 +13,7 @@
 #include <stdlib.h>
 
 #include <map>
+#include <atomic>
 #include <mutex>
 #include <type_traits>
 #include <vector>
@@ -22,6 +23,7 @@
 #include <hip/hip_ext.h>
 
 #include "niti_device.hpp"
+#include "niti_gridbar.hpp"
 #include "niti_kernels.hpp"
 #include "niti_sgd.hpp"
 #include "niti_map.hpp"
@@ -240,6 +242,14 @@ struct Epi {
     int sgd_rule = 0, sgd_ci = 0;
     int64_t sgd_ldt = 0;
     RowMap rmap;  // STORE / REQUANT: where GEMM row m lands (sub-pixel classes)
+    // REQUANT with the rescale fused (plan strategy STRAT_FUSED, every tile resident): each block
+    // keeps its accumulators in registers across the row kernels' in-kernel grid barrier, which
+    // carries the tensor's bit width (niti_gridbar.hpp), then requantises -- no int32 tensor, no
+    // second pass.  bar: ROWCONV_BAR_WORDS words, epoch: this state's launch count (1 first).
+    uint32_t* bar = nullptr;
+    uint32_t epoch = 0;
+    uint32_t* err = nullptr;
+    uint32_t spin_limit = 0;
 };
 
 // launch B of the pair: the rule's bit width of the (all-reduced) max against the one A used
@@ -294,11 +304,46 @@ __device__ __forceinline__ void gemm_epilogue(v16i (&acc)[TM][TN], int r0, int c
     bool rq_raw = false;
     // launch A of the speculative pair: requantise with the hinted bit width, publish the max
     const bool spec_a = MODE == EPI_REQUANT && epi.spec == 1;
+    const bool fused = MODE == EPI_REQUANT && epi.bar != nullptr;
     int abw = 0;             // the bit width launch A requantises with
     bool spec_alts = false;  // and whether it writes the alternates
+    int fused_bw = 0;
+    if (fused) {
+        // NITI_RangeEstimate over the whole tensor (NITI_Conv_Int8.cpp:260) through the grid barrier:
+        // this block's max|acc| over its valid outputs, its bit width ORed in, the grid's read back
+        uint32_t m = 0;
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+#pragma unroll
+            for (int b = 0; b < TN; ++b) {
+                const int col = c0 + b * 32 + (lane & 31);
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const int row = r0 + a * 32 + (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
+                    const uint32_t u = row < M && col < N ? uabs32(acc[a][b][i]) : 0u;
+                    m = m > u ? m : u;
+                }
+            }
+        m = wave_max(m);
+        uint32_t* red = (uint32_t*)smem;  // (every LDS read of the K loop / exchange is finished)
+        if (lane == 0) red[wid] = m;
+        __syncthreads();
+        if (wid == 0) {
+            uint32_t bm = red[0];
+#pragma unroll
+            for (int i = 1; i < NW; ++i) bm = bm > red[i] ? bm : red[i];
+            grid_bw_arrive(epi.bar, epi.epoch, bitwidth_of(bm), lane);
+            const int gbw = grid_bw_wait(epi.bar, epi.epoch, epi.err, epi.spin_limit, 0u, lane);
+            if (lane == 0) red[NW] = (uint32_t)gbw;
+        }
+        __syncthreads();
+        fused_bw = __builtin_amdgcn_readfirstlane((int)red[NW]);
+    }
     if (MODE == EPI_REQUANT) {
         int bw;
-        if (spec_a) {
+        if (fused) {
+            bw = fused_bw;
+        } else if (spec_a) {
             const uint32_t h = __hip_atomic_load(epi.hint, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             bw = __builtin_amdgcn_readfirstlane((int)h) - 1;  // no hint yet: 0 (B redoes unless the max is 0)
             if (h != 0u) bw += epi.spec_bias;
@@ -1694,7 +1739,10 @@ static unsigned long long* take_span() {
 // with the layer's previous bit width and publishes the max, launch B redoes the GEMM only when
 // the (all-reduced) max's bit width differs -- one GEMM pass on a hit, no int32 tensor.  Callers
 // that run the two-phase entry points take it as STRAT_RECOMPUTE (same results).
-enum Strategy { STRAT_STORE = 0, STRAT_RECOMPUTE = 1, STRAT_SLAB = 2, STRAT_SPEC = 3 };
+// STRAT_FUSED: one launch with the rescale fused behind an in-kernel grid barrier (act_fused) where
+// every tile is resident and nothing spans ranks; elsewhere it runs as STRAT_RECOMPUTE
+enum Strategy { STRAT_STORE = 0, STRAT_RECOMPUTE = 1, STRAT_SLAB = 2, STRAT_SPEC = 3, STRAT_FUSED = 4 };
+static bool recomputes(int strat) { return strat == STRAT_RECOMPUTE || strat == STRAT_FUSED; }
 
 struct GemmPlan {
     int bm = 128, bn = 128, tiles = 1, splits = 1, kc_per_split = 0;
@@ -1720,20 +1768,25 @@ static size_t slab_stride_elems(int M, int N) {
 namespace {
 std::mutex g_plan_mu;
 std::map<PlanKey, PlanChoice> g_plan_tab;
+std::atomic<unsigned> g_plan_epoch{1};
 }  // namespace
 
 void plan_override_set(const PlanKey& k, const PlanChoice& c) {
     std::lock_guard<std::mutex> lk(g_plan_mu);
     g_plan_tab[k] = c;
+    g_plan_epoch.fetch_add(1);
 }
 void plan_override_clear(const PlanKey& k) {
     std::lock_guard<std::mutex> lk(g_plan_mu);
     g_plan_tab.erase(k);
+    g_plan_epoch.fetch_add(1);
 }
 void plan_override_clear_all() {
     std::lock_guard<std::mutex> lk(g_plan_mu);
     g_plan_tab.clear();
+    g_plan_epoch.fetch_add(1);
 }
+unsigned plan_override_epoch() { return g_plan_epoch.load(); }
 bool plan_override_lookup(const PlanKey& k, PlanChoice* c) {
     std::lock_guard<std::mutex> lk(g_plan_mu);
     auto it = g_plan_tab.find(k);
@@ -1776,6 +1829,8 @@ static GemmPlan plan_gemm(int M, int N, int k_total, int k_step, int k_bytes, bo
             plan_slab(p, c.splits, k_total, k_step, steps, false, M, N, ws_elems);
         } else if (c.strat == STRAT_SPEC) {
             p.strat = recompute_ok ? STRAT_SPEC : STRAT_STORE;
+        } else if (c.strat == STRAT_FUSED) {
+            p.strat = recompute_ok ? STRAT_FUSED : STRAT_STORE;
         } else {
             p.strat = c.strat == STRAT_RECOMPUTE && recompute_ok ? STRAT_RECOMPUTE : STRAT_STORE;
         }
@@ -1883,6 +1938,26 @@ static hipError_t launch_mode(const GemmPlan& p, const LA& la, const LB& lb, int
     return hipGetLastError();
 }
 
+// The kernel launch_mode would run for plan p (same dispatch), for the occupancy query
+template <class LA, class LB, int MODE, bool KT>
+static std::pair<const void*, int> gemm_fn(const GemmPlan& p) {
+#define NITI_FN(BM_, BN_, WM_, WN_, NW_) \
+    return {(const void*)&gemm_kernel<BM_, BN_, WM_, WN_, LA, LB, MODE, KT, NW_>, NW_ * 64}
+    if (p.bn == 64 && p.bm == 64) NITI_FN(64, 64, 2, 2, 4);
+    if (p.bn == 64) NITI_FN(128, 64, 2, 2, 4);
+    if (p.bm == 64) NITI_FN(64, 128, 1, 4, 4);
+    if (p.bm == 256 && p.bn == 256) {
+        if constexpr (KT && (MODE == EPI_AMAX || MODE == EPI_SGD))
+            NITI_FN(128, 256, 2, 4, 8);
+        else
+            NITI_FN(256, 256, 2, 4, 8);
+    }
+    if (p.bm == 256) NITI_FN(256, 128, 4, 2, 8);
+    if (p.bn == 256) NITI_FN(128, 256, 2, 4, 8);
+    NITI_FN(128, 128, 2, 2, 8);
+#undef NITI_FN
+}
+
 template <class MAP = SlabLinear>
 static hipError_t splitk_reduce(const GemmPlan& p, const int32_t* slab, int64_t n, int64_t stride, int32_t* C,
                                 uint32_t* amax, hipStream_t st, MAP map = MAP()) {
@@ -1956,7 +2031,7 @@ static hipError_t act_phase1(int op, const LA& la, const LB& lb, int M, int N, i
                              uint32_t* amax, int32_t* ws, size_t ws_elems, hipStream_t st) {
     if (M <= 0 || N <= 0) return hipSuccess;
     const GemmPlan p = plan_gemm(M, N, kc_total, LA::BK / 16, kc_total * 16, true, ws ? ws_elems : 0, op);
-    if (p.strat == STRAT_RECOMPUTE || p.strat == STRAT_SPEC) {
+    if (recomputes(p.strat) || p.strat == STRAT_SPEC) {
         Epi e;
         e.amax = amax;
         return launch_mode<LA, LB, EPI_AMAX, false>(p, la, lb, M, N, kc_total, e, st);
@@ -1968,7 +2043,7 @@ template <class LA, class LB>
 static hipError_t act_phase2(int op, const LA& la, const LB& lb, int M, int N, int kc_total, const int32_t* acc,
                              const uint32_t* amax, const ActOut& o, size_t ws_elems, hipStream_t st) {
     const GemmPlan p = plan_gemm(M, N, kc_total, LA::BK / 16, kc_total * 16, true, ws_elems, op);
-    if (p.strat == STRAT_RECOMPUTE || p.strat == STRAT_SPEC) {
+    if (recomputes(p.strat) || p.strat == STRAT_SPEC) {
         if (o.pool.pool_out != nullptr || o.pool.dx != nullptr || o.out_p16 != nullptr || o.pool3.out != nullptr)
             return hipErrorInvalidValue;
         Epi e;
@@ -2031,6 +2106,39 @@ static hipError_t act_spec(int op, const LA& la, const LB& lb, int M, int N, int
     return launch_mode<LA, LB, EPI_REQUANT, false>(p, la, lb, M, N, kc_total, e, st);
 }
 
+// STRAT_FUSED: one launch, the rescale fused behind the grid barrier (Epi::bar).  hipErrorNotSupported
+// (nothing launched) unless the plan is STRAT_FUSED and every tile is resident at once -- the
+// caller then runs the two-phase form, which treats the plan as STRAT_RECOMPUTE.
+static std::atomic<unsigned long long> g_fused_launches{0};
+unsigned long long gemm_fused_launches() { return g_fused_launches.load(); }
+
+template <class LA, class LB>
+static hipError_t act_fused(int op, const LA& la, const LB& lb, int M, int N, int kc_total, const ActOut& o,
+                            const FusedBar& fb, hipStream_t st) {
+    if (M <= 0 || N <= 0) return hipSuccess;
+    const GemmPlan p = plan_gemm(M, N, kc_total, LA::BK / 16, kc_total * 16, true, 0, op);
+    if (p.strat != STRAT_FUSED) return hipErrorNotSupported;
+    if (o.pool.pool_out != nullptr || o.pool.dx != nullptr || o.out_p16 != nullptr || o.pool3.out != nullptr ||
+        o.out == nullptr || fb.bar == nullptr || fb.err == nullptr)
+        return hipErrorInvalidValue;
+    const auto f = gemm_fn<LA, LB, EPI_REQUANT, false>(p);
+    if (p.tiles > resident_wgs(f.first, f.second)) return hipErrorNotSupported;
+    Epi e;
+    e.out = o.out;
+    e.ldo = N;
+    e.relu = o.relu;
+    e.relu_mask = o.relu_mask;
+    e.exp_in = o.exp_in;
+    e.wscale = o.wscale;
+    e.exp_out = o.exp_out;
+    e.bar = fb.bar;
+    e.epoch = fb.epoch;
+    e.err = fb.err;
+    e.spin_limit = fb.spin_limit ? fb.spin_limit : BAR_SPIN_LIMIT;
+    g_fused_launches.fetch_add(1);
+    return launch_mode<LA, LB, EPI_REQUANT, false>(p, la, lb, M, N, kc_total, e, st);
+}
+
 // ------------------------------------------------------------------------------ per-op wrappers
 bool conv_fwd_spec_ok(const ConvGeom& g) {
     const int kc = g.kh * g.kw * g.cip / 16;
@@ -2042,13 +2150,11 @@ bool conv_dgrad_spec_ok(const ConvGeom& g) {
 }
 bool conv_fwd_phase2_separate(const ConvGeom& g, size_t ws_bytes) {
     const int kc = g.kh * g.kw * g.cip / 16;  // every forward operand loader steps 64 bytes
-    return plan_gemm(g.n * g.oh * g.ow, g.cop, kc, 64 / 16, kc * 16, true, ws_bytes / 4, PLAN_FWD).strat !=
-           STRAT_RECOMPUTE;
+    return !recomputes(plan_gemm(g.n * g.oh * g.ow, g.cop, kc, 64 / 16, kc * 16, true, ws_bytes / 4, PLAN_FWD).strat);
 }
 bool conv_dgrad_phase2_separate(const ConvGeom& g, size_t ws_bytes) {
     const int kc = g.kh * g.kw * g.cop / 16;
-    return plan_gemm(g.n * g.h * g.w, g.cip, kc, 64 / 16, kc * 16, true, ws_bytes / 4, PLAN_DGRAD).strat !=
-           STRAT_RECOMPUTE;
+    return !recomputes(plan_gemm(g.n * g.h * g.w, g.cip, kc, 64 / 16, kc * 16, true, ws_bytes / 4, PLAN_DGRAD).strat);
 }
 static RowsK rows_k(const int8_t* p, int64_t ld, int rows, int kc_total) {
     RowsK r;
@@ -2565,6 +2671,10 @@ bool conv_wgrad_fc_sgd_ok(const ConvGeom& g) {
 hipError_t conv_wgrad_fc_sgd(const ConvGeom& g, const int8_t* x, const int8_t* dy, uint32_t* amax, const SgdJob& j,
                              int pass, hipStream_t st) {
     if (!conv_wgrad_fc_sgd_ok(g) || amax == nullptr || (pass == 1 && j.w == nullptr)) return hipErrorInvalidValue;
+    // the EPI_SGD epilogue writes w, wT and the int8 gradient only: a job carrying the row kernels'
+    // fragment-major copies, sub-pixel class weights or deferred slabs would leave them stale
+    if (pass == 1 && (j.wf != nullptr || j.wft != nullptr || j.subw != nullptr || j.slab != nullptr))
+        return hipErrorInvalidValue;
     KtRowsU la;
     KtIm2col lg;
     wgrad_operands(g, x, dy, &la, &lg);
@@ -2630,6 +2740,23 @@ hipError_t conv_dgrad_spec(const ConvGeom& g, const int8_t* dy, const int8_t* wt
     const RowsK lb = rows_k(wt, (int64_t)g.kh * g.kw * g.cop, g.c_in, kc_total);
     return with_dgrad_operand(g, dy, [&](const auto& la) {
         return act_spec(PLAN_DGRAD, la, lb, g.n * g.h * g.w, g.cip, kc_total, amax, o, slot, pass, alt, st);
+    });
+}
+hipError_t conv_fwd_fused(const ConvGeom& g, const int8_t* x, const int8_t* w, const ActOut& o, const FusedBar& fb,
+                          hipStream_t st) {
+    const int kc_total = g.kh * g.kw * g.cip / 16;
+    const RowsK lb = rows_k(w, (int64_t)g.kh * g.kw * g.cip, g.c_out, kc_total);
+    return with_fwd_operand(g, x, [&](const auto& la) {
+        return act_fused(PLAN_FWD, la, lb, g.n * g.oh * g.ow, g.cop, kc_total, o, fb, st);
+    });
+}
+hipError_t conv_dgrad_fused(const ConvGeom& g, const int8_t* dy, const int8_t* wt, const ActOut& o, const FusedBar& fb,
+                            hipStream_t st) {
+    if (g.sh != 1 || g.sw != 1) return hipErrorNotSupported;  // (strided: the sub-pixel class GEMMs)
+    const int kc_total = g.kh * g.kw * g.cop / 16;
+    const RowsK lb = rows_k(wt, (int64_t)g.kh * g.kw * g.cop, g.c_in, kc_total);
+    return with_dgrad_operand(g, dy, [&](const auto& la) {
+        return act_fused(PLAN_DGRAD, la, lb, g.n * g.h * g.w, g.cip, kc_total, o, fb, st);
     });
 }
 size_t conv_fwd_spec_alt_bytes(const ConvGeom& g) { return (size_t)2 * g.n * g.oh * g.ow * g.cop; }
@@ -2786,7 +2913,7 @@ hipError_t conv_dgrad_phase1(const ConvGeom& g, const int8_t* dy, const int8_t* 
         const GemmPlan p = plan_gemm(g.n * g.h * g.w, g.cip, kc_total, 64 / 16, kc_total * 16, true,
                                      ws ? ws_bytes / 4 : 0, PLAN_DGRAD);
         if (p.strat != STRAT_SPEC) {
-            if (p.strat == STRAT_RECOMPUTE) return subpix_pass<EPI_AMAX>(g, p, dy, subw, nullptr, amax, nullptr, st);
+            if (recomputes(p.strat)) return subpix_pass<EPI_AMAX>(g, p, dy, subw, nullptr, amax, nullptr, st);
             return subpix_pass<EPI_STORE>(g, p, dy, subw, acc, amax, nullptr, st);
         }
     }
@@ -2802,7 +2929,7 @@ hipError_t conv_dgrad_phase2(const ConvGeom& g, const int8_t* dy, const int8_t* 
     if (subw != nullptr && conv_dgrad_subpix_ok(g)) {
         const GemmPlan p = plan_gemm(g.n * g.h * g.w, g.cip, kc_total, 64 / 16, kc_total * 16, true, ws_bytes / 4,
                                      PLAN_DGRAD);
-        if (p.strat == STRAT_RECOMPUTE) {
+        if (recomputes(p.strat)) {
             if (o.pool.pool_out != nullptr || o.pool.dx != nullptr || o.out_p16 != nullptr) return hipErrorInvalidValue;
             return subpix_pass<EPI_REQUANT>(g, p, dy, subw, nullptr, const_cast<uint32_t*>(amax), &o, st);
         }
@@ -3429,6 +3556,7 @@ struct Conv0 {
     int8_t* pool_out; // [P / 4][cop] or null
     int8_t* pool_c32; // the pooled output as the next layer's C32 input [n][cop/32][oh/2][ow/2][32], or null
     int8_t* out_c32;  // the (unpooled) output as the next layer's C32 input [n][cop/32][oh][ow][32], or null
+    int8_t* pool_code; // the pool gradient's route (pool_code4) [P / 4][cop], or null
     const int8_t *exp_in, *wscale;
     int8_t* exp_out;
     int relu;
@@ -3503,10 +3631,12 @@ __global__ void __launch_bounds__(256) conv0_kernel(Conv0 g) {
                     const auto x13 = __builtin_amdgcn_permlane32_swap(d[1], d[3], false, false);
                     return v4i{(int)x02[0], (int)x02[1], (int)x13[0], (int)x13[1]};
                 };
+                v4i qv[2];
 #pragma unroll
                 for (int r = 0; r < 2; ++r) {
                     const v4i v = pack(q[r]);
-                    *(v4i*)(g.out + (p0 + (int64_t)r * g.ow + c) * g.cop + t * 32 + 16 * h) = v;
+                    qv[r] = v;
+                    if (g.out != nullptr) *(v4i*)(g.out + (p0 + (int64_t)r * g.ow + c) * g.cop + t * 32 + 16 * h) = v;
                     if (g.out_c32 != nullptr)
                         *(v4i*)(g.out_c32 + (((img * tiles + t) * g.oh + 2 * pr + r) * (int64_t)g.ow + seg * 32 + c) * 32 +
                                 16 * h) = v;
@@ -3522,9 +3652,20 @@ __global__ void __launch_bounds__(256) conv0_kernel(Conv0 g) {
                         pm[i] = (int8_t)(v0 > v1 ? v0 : v1);
                     }
                     const v4i v = pack(pm);
+                    v4i code{0, 0, 0, 0};
+                    if (g.pool_code != nullptr) {  // the window: (top, bottom) here, the odd neighbour's
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) {
+                            const uint32_t t1 = (uint32_t)__builtin_amdgcn_mov_dpp(qv[0][k], 0xB1, 0xF, 0xF, false);
+                            const uint32_t t3 = (uint32_t)__builtin_amdgcn_mov_dpp(qv[1][k], 0xB1, 0xF, 0xF, false);
+                            code[k] = (int)pool_code4((uint32_t)qv[0][k], t1, (uint32_t)qv[1][k], t3, (uint32_t)v[k],
+                                                      g.relu != 0);
+                        }
+                    }
                     if ((c & 1) == 0) {
                         const int64_t pp = (img * (g.oh / 2) + pr) * (g.ow / 2) + seg * 16 + (c >> 1);
                         *(v4i*)(g.pool_out + pp * g.cop + t * 32 + 16 * h) = v;
+                        if (g.pool_code != nullptr) *(v4i*)(g.pool_code + pp * g.cop + t * 32 + 16 * h) = code;
                         if (g.pool_c32 != nullptr) {
                             const int64_t hw2 = (int64_t)(g.oh / 2) * (g.ow / 2);
                             *(v4i*)(g.pool_c32 + ((img * tiles + t) * hw2 + pp - img * hw2) * 32 + 16 * h) = v;
@@ -3549,9 +3690,12 @@ bool conv0_ok(const ConvGeom& g) {
 }
 
 hipError_t conv0_fwd(const ConvGeom& g, const int8_t* xcol, const int8_t* w, uint32_t* amax, const ActOut& o,
-                     int pass, hipStream_t st, int8_t* pool_c32, int8_t* out_c32) {
-    if (!conv0_ok(g) || o.out == nullptr || o.relu_mask != nullptr) return hipErrorInvalidValue;
-    if (pool_c32 != nullptr && o.pool.pool_out == nullptr) return hipErrorInvalidValue;
+                     int pass, hipStream_t st, int8_t* pool_c32, int8_t* out_c32, int8_t* pool_code) {
+    // (out may be null when the pooled output is kept: pool_out + pool_code carry everything the
+    // backward pass reads)
+    if (!conv0_ok(g) || o.relu_mask != nullptr) return hipErrorInvalidValue;
+    if (o.out == nullptr && (pass == 1 && (o.pool.pool_out == nullptr || pool_code == nullptr))) return hipErrorInvalidValue;
+    if ((pool_c32 != nullptr || pool_code != nullptr) && o.pool.pool_out == nullptr) return hipErrorInvalidValue;
     Conv0 k{};
     k.x = xcol;
     k.w = w;
@@ -3566,6 +3710,7 @@ hipError_t conv0_fwd(const ConvGeom& g, const int8_t* xcol, const int8_t* w, uin
     k.pool_out = o.pool.pool_out;
     k.pool_c32 = pool_c32;
     k.out_c32 = out_c32;
+    k.pool_code = pool_code;
     k.exp_in = o.exp_in;
     k.wscale = o.wscale;
     k.exp_out = o.exp_out;

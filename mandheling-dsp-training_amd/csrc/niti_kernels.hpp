@@ -86,6 +86,8 @@ int conv_plan_k_step(int op, const ConvGeom& g);
 void plan_override_set(const PlanKey& k, const PlanChoice& c);
 void plan_override_clear(const PlanKey& k);
 void plan_override_clear_all();
+// bumped by every override change: callers that size buffers per plan re-check when it moves
+unsigned plan_override_epoch();
 // the plan the GEMM of key k runs with now (override or default) under a workspace of ws_bytes
 PlanChoice plan_query(const PlanKey& k, int k_step, bool recompute_ok, size_t ws_bytes);
 size_t plan_slab_bytes(int M, int N, int splits);
@@ -129,7 +131,7 @@ hipError_t residual_fused(const int8_t* a, const int8_t* ea, const int8_t* b, co
                           int8_t* exp_out, int relu, int8_t* out, uint32_t* bar, uint32_t epoch, uint32_t* err,
                           hipStream_t st, const int8_t* relu_mask = nullptr);
 // workgroups of 256 threads of kernel f the device holds at once (0 without a device)
-int resident_wgs(const void* f);
+int resident_wgs(const void* f, int threads = 256);
 // z = aligned a + b (int32, n % 16 == 0 elements), its exponent into ez, max|z| into amax
 hipError_t residual_add(const int8_t* a, const int8_t* ea, const int8_t* b, const int8_t* eb, int64_t n,
                         int32_t* z, int8_t* ez, uint32_t* amax, hipStream_t st);
@@ -230,7 +232,7 @@ bool conv0_ok(const ConvGeom& g);
 // pass 0: range into amax; pass 1: requantise with it (a MAX all-reduce may sit between them)
 hipError_t conv0_fwd(const ConvGeom& g, const int8_t* xcol, const int8_t* w, uint32_t* amax, const ActOut& o,
                      int pass, hipStream_t st,
-                     int8_t* pool_c32 = nullptr, int8_t* out_c32 = nullptr);
+                     int8_t* pool_c32 = nullptr, int8_t* out_c32 = nullptr, int8_t* pool_code = nullptr);
 bool conv_dgrad_phase2_separate(const ConvGeom& g, size_t ws_bytes);
 // The speculative pair on the implicit GEMM (plan strategy 3 = STRAT_SPEC, forward / input
 // gradient, no K split; NITI_Conv_Int8.cpp:260-307, NITI_DeConv_Int8.cpp:294-329): pass 0 (launch A)
@@ -260,6 +262,26 @@ hipError_t conv_fwd_spec(const ConvGeom& g, const int8_t* x, const int8_t* w, ui
                          uint32_t* slot, int pass, hipStream_t st, int8_t* alt = nullptr);
 hipError_t conv_dgrad_spec(const ConvGeom& g, const int8_t* dy, const int8_t* wt, uint32_t* amax, const ActOut& o,
                            uint32_t* slot, int pass, hipStream_t st, int8_t* alt = nullptr);
+// The implicit GEMM with the rescale fused (plan strategy 4 = STRAT_FUSED, forward / stride-1 input
+// gradient, no K split; NITI_Conv_Int8.cpp:260-307, NITI_DeConv_Int8.cpp:294-329): ONE launch whose
+// blocks keep their accumulators in registers across an in-kernel grid barrier carrying the tensor's
+// bit width (the row kernels' protocol, niti_gridbar.hpp), then requantise -- no int32 tensor and no
+// second GEMM pass.  Needs every tile resident at once (checked with the occupancy API) and no rank
+// boundary: hipErrorNotSupported (nothing launched) otherwise or when the plan is not STRAT_FUSED,
+// and the caller runs phase 1 + phase 2, which take the plan as STRAT_RECOMPUTE.  bar:
+// ROWCONV_BAR_WORDS zeroed words per layer phase, epoch its launch count (1 first), err set on a
+// barrier timeout.  ActOut without pool / P16 fusion.  Results equal phase 1 + phase 2's.
+struct FusedBar {
+    uint32_t* bar = nullptr;
+    uint32_t epoch = 0;
+    uint32_t* err = nullptr;
+    uint32_t spin_limit = 0;  // 0: the default
+};
+unsigned long long gemm_fused_launches();  // (diagnostics: launches that ran fused)
+hipError_t conv_fwd_fused(const ConvGeom& g, const int8_t* x, const int8_t* w, const ActOut& o, const FusedBar& fb,
+                          hipStream_t st);
+hipError_t conv_dgrad_fused(const ConvGeom& g, const int8_t* dy, const int8_t* wt, const ActOut& o, const FusedBar& fb,
+                            hipStream_t st);
 hipError_t conv_fwd_phase1(const ConvGeom& g, const int8_t* x, const int8_t* w, int32_t* acc, uint32_t* amax,
                            void* ws, size_t ws_bytes, hipStream_t st);
 hipError_t conv_fwd_phase2(const ConvGeom& g, const int8_t* x, const int8_t* w, const int32_t* acc,
@@ -298,6 +320,11 @@ struct RowConvOut {
     int8_t* pool_dx = nullptr;
     int8_t* pool_dx_next = nullptr;
     int pool_relu = 0;
+    // the route as the forward pass that pooled recorded it (pool_code4, NHWC16-shaped [n][H][W][cop]
+    // bytes): read instead of pool_x / pool_y, which may then be null (W > 0 forms)
+    const int8_t* pool_code = nullptr;
+    // forward with pool_out: record that route here (W > 0 forms; relu decides the code's relu bit)
+    int8_t* pool_code_out = nullptr;
     // 0: pool_dx (NHWC16) is not written, only its C32 (pool_dx_next) / P16 copies; the pool
     // gradient's routing still needs pool_dx non-null.  Likewise out may be null in the input
     // gradient when its consumers read the C32 (next) and P16 copies.
@@ -321,6 +348,7 @@ bool rowconv_nhwc_pref(const ConvGeom& g);
 constexpr int ROWCONV_BAR_WORDS = 2 * 19 * 32;  // grid-barrier state (both parities)
 static_assert(ROWCONV_BAR_WORDS == NITI_ROWCONV_STATE_WORDS, "header constant");
 bool rowconv_ok(const ConvGeom& g);
+bool rowconv_seg(const ConvGeom& g);  // the row-segment form (W = 0) takes g
 // the input-gradient conv of a stride-1 pad-1 3x3 layer as a forward conv (dy -> dx, ci <-> co);
 // false if the layer's input gradient cannot run on the row kernel
 bool rowconv_dgrad_geom(const ConvGeom& layer, ConvGeom* d);

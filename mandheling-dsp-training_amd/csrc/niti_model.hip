@@ -140,6 +140,11 @@ struct Layer {
     int8_t* wT = nullptr;    // IHWO16, kept in step with w by sgd_update
     int8_t* r = nullptr;     // conv (+relu) output NHWC16 [n][oh][ow][cop]
     int8_t* p = nullptr;     // pooled NHWC16
+    // the 2x2 pool's gradient route recorded by the forward (pool_code4, [n][ph][pw][cop] bytes; the
+    // pooled layers whose forward and next input gradient run on the kernels that know it)
+    int8_t* pc = nullptr;
+    bool r_written = false;  // this step wrote r (a pooled layer with a recorded route skips it
+                             // under keep_grads(0): nothing else reads it; its tap is then invalid)
     int8_t* flat = nullptr;  // flattened NHWC16 [n][1][1][c*ph*pw]
     int8_t* dy = nullptr;    // output gradient NHWC16 [n][oh][ow][cop]
     int8_t* dtmp = nullptr;  // gradient wrt the pooled / flattened output
@@ -150,7 +155,7 @@ struct Layer {
     int32_t* slab16 = nullptr;
     size_t slab16_bytes = 0;
     // the GEMM-path weight gradient's own split-K slabs when its combine is deferred the same way
-    // (grown to the plan's need on the first step that defers, ensure_wslab)
+    // (sized for the current plans at the head of run(), size_wslabs)
     int32_t* wslab = nullptr;
     size_t wslab_bytes = 0;
     SgdJob defer{};
@@ -244,6 +249,16 @@ struct Model {
     // copies (niti_model_get_tap rebuilds it from the C32 copy)
     std::vector<char> dy16_valid;
     bool rowconv_dgrad_layer(int i) const { return use_rowconv && L[i].rcd; }
+    // layer i's 2x2 pool route travels as codes (Layer::pc): its forward (the first layer's conv0
+    // kernel or a W > 0 row kernel) records it and layer i + 1's input gradient (a W > 0 row kernel,
+    // or the head's) reads it instead of the pre-pool output and the pooled one
+    bool pool_code_layer(int i) const {
+        const Layer& l = L[i];
+        if (!l.pool || l.flatten || l.pc == nullptr || i + 1 >= (int)L.size()) return false;
+        const bool fwd = (l.col && conv0_ok(l.g)) || (rowconv_layer(i) && !rowconv_seg(l.g));
+        const bool bwd = (rowconv_dgrad_layer(i + 1) && !rowconv_seg(L[i + 1].dg)) || head_dgrad_ok(i + 1);
+        return fwd && bwd;
+    }
     // the classifier head (a 1x1 conv over 1x1 maps, at most 64 outputs) on the row kernel's
     // W = 1 path: forward, and its input gradient into the previous layer's relu / 2x2 pool
     bool head_layer(int i) const {
@@ -260,6 +275,7 @@ struct Model {
     }
     // the int8 weight gradient of the last step kept for niti_model_get (which = 1)
     bool keep_grads = true;
+    bool g8_written = false;  // the last step stored the int8 weight gradients (tap(layer, 1))
     // IHWO16 weights of the layers whose input gradient ran on the row kernel (the SGD kernel
     // skips them there) -- rebuilt when the GEMM input gradient takes over again
     int refresh_wt(hipStream_t st) {
@@ -507,20 +523,35 @@ struct Model {
         return true;
     }
     size_t ws_bytes_for(int op) const { return op == PLAN_WGRAD ? slab_w_bytes : slab_bytes; }
-    // layer i's own slab buffer for a deferred GEMM weight-gradient combine, sized to the plan it runs
-    // with (false: its plan does not split K into C-shaped slabs, or no memory)
-    bool ensure_wslab(int i) {
-        Layer& l = L[i];
+    // layer i's own slab buffer for a deferred GEMM weight-gradient combine is big enough for the
+    // plan it runs with (false: its plan does not split K into C-shaped slabs, or not sized)
+    bool ensure_wslab(int i) const {
+        const Layer& l = L[i];
         const PlanChoice c = conv_plan_query(PLAN_WGRAD, l.g, false, slab_w_bytes);
         if (c.strat != 2 || c.splits < 2 || c.bm == PLAN_P16_TILE) return false;
-        const size_t need = conv_wgrad_slab_bytes(l.g, c);  // (GEMM or tap-sharing slabs)
-        if (l.wslab_bytes >= need) return true;
-        if (hipDeviceSynchronize() != hipSuccess) return false;
-        void* p = ws.alloc(need);
-        if (!p) return false;
-        l.wslab = (int32_t*)p;
-        l.wslab_bytes = need;
-        return true;
+        return l.wslab_bytes >= conv_wgrad_slab_bytes(l.g, c);  // (GEMM or tap-sharing slabs)
+    }
+    // size every layer's deferred-combine slab for the current plans, at the head of run() whenever a
+    // plan override changed since the last sizing (one device sync, the old buffer freed): no
+    // allocation or sync inside the step
+    unsigned wslab_epoch = 0;
+    int size_wslabs() {
+        if (wslab_epoch == plan_override_epoch()) return NITI_NO_ERROR;
+        bool synced = false;
+        for (Layer& l : L) {
+            const PlanChoice c = conv_plan_query(PLAN_WGRAD, l.g, false, slab_w_bytes);
+            if (c.strat != 2 || c.splits < 2 || c.bm == PLAN_P16_TILE) continue;
+            const size_t need = conv_wgrad_slab_bytes(l.g, c);
+            if (l.wslab_bytes >= need) continue;
+            if (!synced && hipDeviceSynchronize() != hipSuccess) return NITI_NO_EXECUTION;
+            synced = true;
+            void* p = ws.replace(l.wslab, need);
+            l.wslab = (int32_t*)p;
+            l.wslab_bytes = p ? need : 0;
+            if (!p) return NITI_OUT_OF_MEMORY;
+        }
+        wslab_epoch = plan_override_epoch();
+        return NITI_NO_ERROR;
     }
     int ensure_streams() {
         if (side) return NITI_NO_ERROR;
@@ -673,6 +704,10 @@ int Model::build(int arch_, int batch_, int in_hw) {
         if (l.pool) {
             l.p = (int8_t*)ws.alloc((size_t)n * l.ph * l.pw * g.cop);
             l.dtmp = (int8_t*)ws.alloc((size_t)n * l.ph * l.pw * g.cop);
+            if (!l.flatten && l.ph * 2 == g.oh && l.pw * 2 == g.ow) {
+                l.pc = (int8_t*)ws.alloc((size_t)n * l.ph * l.pw * g.cop);
+                if (!l.pc) return NITI_OUT_OF_MEMORY;
+            }
         }
         if (l.flatten) {
             const int fc = g.c_out * l.ph * l.pw;
@@ -695,18 +730,16 @@ int Model::build(int arch_, int batch_, int in_hw) {
         slab_bytes = std::max(slab_bytes, conv_fwd_workspace(g));
         slab_bytes = std::max(slab_bytes, conv_dgrad_workspace(g));
         slab_w_bytes = std::max(slab_w_bytes, conv_wgrad_workspace(g));
-        if (!l.col && g.kh == 1 && g.kw == 1 && g.h == 1 && g.w == 1 && g.c_out <= 64) {  // head_layer
-            l.bar = (uint32_t*)ws.alloc(ROWCONV_BAR_WORDS * 4);
-            if (!l.bar || hipMemset(l.bar, 0, ROWCONV_BAR_WORDS * 4) != hipSuccess) return NITI_OUT_OF_MEMORY;
-        }
+        // grid-barrier state of every layer: the row kernels' fused launches and speculation slots,
+        // the head's, or the GEMM path's fused-rescale launches (STRAT_FUSED)
+        l.bar = (uint32_t*)ws.alloc(ROWCONV_BAR_WORDS * 4);
+        if (!l.bar || hipMemset(l.bar, 0, ROWCONV_BAR_WORDS * 4) != hipSuccess) return NITI_OUT_OF_MEMORY;
         if (!l.col && rowconv_ok(g)) {
             l.rc = 1;
             l.wf = (int8_t*)ws.alloc(rowconv_wf_bytes(g.c_out, g.c_in));
             l.xc32 = (int8_t*)ws.alloc((size_t)n * round_up(g.c_in, 32) * g.h * g.w);
-            l.bar = (uint32_t*)ws.alloc(ROWCONV_BAR_WORDS * 4);
-            if (!l.wf || !l.xc32 || !l.bar) return NITI_OUT_OF_MEMORY;
-            if (hipMemset(l.bar, 0, ROWCONV_BAR_WORDS * 4) != hipSuccess ||
-                hipMemset(l.wf, 0, rowconv_wf_bytes(g.c_out, g.c_in)) != hipSuccess)
+            if (!l.wf || !l.xc32) return NITI_OUT_OF_MEMORY;
+            if (hipMemset(l.wf, 0, rowconv_wf_bytes(g.c_out, g.c_in)) != hipSuccess)
                 return NITI_NO_EXECUTION;
             rc_acc_size = std::max(rc_acc_size, rowconv_acc_bytes(g, false));
             // the input gradient too, where the previous layer's output (pooled 2x2 or not) is
@@ -835,10 +868,13 @@ int Model::fwd_layer(int i, hipStream_t st) {
     Layer& l = L[i];
     const ConvGeom& g = l.g;
     probe(i, 0, true, st);
+    l.r_written = true;
     if (l.col && conv0_ok(g) && !l.flatten) {
         // first layer on its im2col copy: range pass, [all-reduce MAX], requant + relu + pool pass
         ActOut o;
-        o.out = l.r;
+        const bool code = pool_code_layer(i);
+        l.r_written = keep_grads || !code;
+        o.out = l.r_written ? l.r : nullptr;
         o.relu = l.relu;
         o.exp_in = exp0;
         o.wscale = l.ws_dev;
@@ -850,7 +886,7 @@ int Model::fwd_layer(int i, hipStream_t st) {
         conv0_ranged = false;
         if (dp && exact) CTRY(coll->allreduce(rng(i, 0), MAX_WORDS, COLL_MAX_U32, st));
         MTRY(conv0_fwd(g, l.in, l.w, rng(i, 0), o, 1, st, next_c32 && l.pool ? L[i + 1].xc32 : nullptr,
-                       next_c32 && !l.pool ? L[i + 1].xc32 : nullptr));
+                       next_c32 && !l.pool ? L[i + 1].xc32 : nullptr, code ? l.pc : nullptr));
         if (next_c32) xc32_valid[i + 1] = 1;
         probe(i, 0, false, st);
         return NITI_NO_ERROR;
@@ -891,8 +927,11 @@ int Model::fwd_layer(int i, hipStream_t st) {
         const int8_t* xin = xn ? l.in : l.xc32;
         RowConvOut o;
         o.x_nhwc = xn ? 1 : 0;
-        o.out = l.r;
+        const bool code = pool_code_layer(i);
+        l.r_written = keep_grads || !code;
+        o.out = l.r_written ? l.r : nullptr;
         o.pool_out = l.pool ? l.p : nullptr;
+        o.pool_code_out = code ? l.pc : nullptr;
         const bool feeds_next = i + 1 < (int)L.size() && rowconv_layer(i + 1) && !l.flatten &&
                                 !rowconv_nhwc_pref(L[i + 1].g);
         o.next = feeds_next ? L[i + 1].xc32 : nullptr;
@@ -935,7 +974,16 @@ int Model::fwd_layer(int i, hipStream_t st) {
         o.pool.H = g.oh;
         o.pool.W = g.ow;
     }
-    if (spec) {  // the speculative pair: one GEMM pass while the bit width holds, no int32 tensor
+    hipError_t fe = hipErrorNotSupported;
+    if (!dp && !capturing && !fuse_pool) {  // one launch with the rescale fused (plan strategy 4)
+        fe = conv_fwd_fused(g, l.in, l.w, o, FusedBar{l.bar, l.epoch + 1, rc_err}, st);
+        if (fe != hipErrorNotSupported) {
+            ++l.epoch;
+            MTRY(fe);
+        }
+    }
+    if (fe != hipErrorNotSupported) {
+    } else if (spec) {  // the speculative pair: one GEMM pass while the bit width holds, no int32 tensor
         int8_t* alt = conv_fwd_spec_alt_bytes(g) <= gspec_alt_bytes ? gspec_alt : nullptr;
         MTRY(conv_fwd_spec(g, l.in, l.w, rng(i, 0), o, l.gspec, 0, st, alt));
         if (dp && exact) CTRY(coll->allreduce(rng(i, 0), MAX_WORDS, COLL_MAX_U32, st));
@@ -1057,10 +1105,15 @@ int Model::dgrad_layer(int i, hipStream_t st) {
         // the head's input gradient on the row kernel (W = 1), into the previous layer's relu or
         // 2x2-pool gradient (+ its C32 / P16 copies)
         RowConvOut o;
+        o.dgrad_slot = 1;  // (every input-gradient launch: its own speculation hint slot)
         int8_t* next = rowconv_dgrad_layer(i - 1) && !rowconv_nhwc_pref(pv.dg) ? pv.dyc32 : nullptr;
         if (pv.pool) {
-            o.pool_x = pv.r;
-            o.pool_y = pv.p;
+            if (pool_code_layer(i - 1)) {
+                o.pool_code = pv.pc;
+            } else {
+                o.pool_x = pv.r;
+                o.pool_y = pv.p;
+            }
             o.pool_dx = pv.dy;
             o.pool_dx_next = next;
             o.pool_relu = pv.relu;
@@ -1076,7 +1129,6 @@ int Model::dgrad_layer(int i, hipStream_t st) {
         if (!dp && !capturing && rowconv_fc_ok(n, K, rows, true)) {
             MTRY(rowconv_fc(n, K, rows, l.dy, g.cop, l.wT, g.cop, o, 0, rng(i, 1), l.bar, ++l.epoch, rc_err, st));
         } else if (rowconv_spec2_on()) {
-            o.dgrad_slot = 1;
             MTRY(rowconv_fc(n, K, rows, l.dy, g.cop, l.wT, g.cop, o, RC_SPEC_A, rng(i, 1), l.bar, 0, nullptr, st));
             if (dp && exact) CTRY(coll->allreduce(rng(i, 1), MAX_WORDS, COLL_MAX_U32, st));
             MTRY(rowconv_fc(n, K, rows, l.dy, g.cop, l.wT, g.cop, o, RC_SPEC_B, rng(i, 1), l.bar, 0, nullptr, st));
@@ -1103,6 +1155,7 @@ int Model::dgrad_layer(int i, hipStream_t st) {
         }
         const int8_t* dyin = xn ? l.dy : l.dyc32;
         RowConvOut o;
+        o.dgrad_slot = 1;  // (every input-gradient launch: its own speculation hint slot)
         o.x_nhwc = xn ? 1 : 0;
         int8_t* next = rowconv_dgrad_layer(i - 1) && !rowconv_nhwc_pref(pv.dg) ? pv.dyc32 : nullptr;
         // the previous layer's P16 dy for its weight gradient, when the launch's pixels make whole
@@ -1110,8 +1163,12 @@ int Model::dgrad_layer(int i, hipStream_t st) {
         o.p16 = fuse_dp16 && wgrad_p16_splits(i - 1) > 0 && rowconv_p16_ok(l.dg, pv.pool) ? dp16[i - 1] : nullptr;
         const bool skip16 = skip_dy16(i, next, o.p16);
         if (pv.pool) {
-            o.pool_x = pv.r;
-            o.pool_y = pv.p;
+            if (pool_code_layer(i - 1)) {
+                o.pool_code = pv.pc;
+            } else {
+                o.pool_x = pv.r;
+                o.pool_y = pv.p;
+            }
             o.pool_dx = pv.dy;
             o.pool_dx_next = next;
             o.pool_relu = pv.relu;
@@ -1125,7 +1182,6 @@ int Model::dgrad_layer(int i, hipStream_t st) {
         if (!dp && !capturing && rowconv_fused_ok(d, true)) {
             MTRY(rowconv_fwd(d, dyin, l.wft, o, 0, rng(i, 1), l.bar, ++l.epoch, rc_err, st));
         } else if (rowconv_spec2_on()) {
-            o.dgrad_slot = 1;
             o.acc_store = rowconv_acc_bytes(d, true) ? rc_acc : nullptr;
             MTRY(rowconv_fwd(d, dyin, l.wft, o, RC_SPEC_A, rng(i, 1), l.bar, 0, nullptr, st));
             if (dp && exact) CTRY(coll->allreduce(rng(i, 1), MAX_WORDS, COLL_MAX_U32, st));
@@ -1175,7 +1231,16 @@ int Model::dgrad_layer(int i, hipStream_t st) {
         o.out = pv.dy;
         if (conv_dgrad_phase2_separate(g, slab_bytes)) o.out_p16 = p16_out;
     }
-    if (spec) {  // the speculative pair (no int32 tensor while the bit width holds)
+    hipError_t fe = hipErrorNotSupported;
+    if (!dp && !capturing && !fuse && o.out_p16 == nullptr && o.out != nullptr) {  // one launch, the rescale fused
+        fe = conv_dgrad_fused(g, l.dy, l.wT, o, FusedBar{l.bar, l.epoch + 1, rc_err}, st);
+        if (fe != hipErrorNotSupported) {
+            ++l.epoch;
+            MTRY(fe);
+        }
+    }
+    if (fe != hipErrorNotSupported) {
+    } else if (spec) {  // the speculative pair (no int32 tensor while the bit width holds)
         int8_t* alt = conv_dgrad_spec_alt_bytes(g) <= gspec_alt_bytes ? gspec_alt : nullptr;
         MTRY(conv_dgrad_spec(g, l.dy, l.wT, rng(i, 1), o, l.gspec + GEMM_SPEC_SLOT_WORDS, 0, st, alt));
         if (dp && exact) CTRY(coll->allreduce(rng(i, 1), MAX_WORDS, COLL_MAX_U32, st));
@@ -1320,6 +1385,8 @@ int Model::autotune(hipStream_t st, int reps) {
                         c.strat = 3;
                         cands.push_back(c);
                     }
+                    c.strat = 4;  // one launch, the rescale fused (where every tile is resident)
+                    cands.push_back(c);
                 }
                 for (int s : split_opts) {
                     if (s > steps / 2 || plan_slab_bytes(key.M, key.N, s) > wsb) break;
@@ -1365,6 +1432,10 @@ int Model::run(const int8_t* x_nchw, int exp_in, const uint8_t* images, const in
     for (auto& l : L) l.defer = SgdJob{};
     if (dp) {
         const int rc = ensure_comm_stream();
+        if (rc != NITI_NO_ERROR) return rc;
+    }
+    if (!dp && !capturing && !tuning) {
+        const int rc = size_wslabs();  // (plan changes: no allocation or sync inside the step)
         if (rc != NITI_NO_ERROR) return rc;
     }
     invalidate_xp16();  // the forward pass rewrites every layer input
@@ -1502,6 +1573,7 @@ int Model::run(const int8_t* x_nchw, int exp_in, const uint8_t* images, const in
     MTRY(sgd_update_many(many, n_many, st));  // (+ the deferred combines) also rewrites the fragment-major weight copies
     for (int i = 0; i < nl; ++i)
         if (L[i].fc_sgd) MTRY(conv_wgrad_fc_sgd(L[i].g, L[i].in, L[i].dy, rng(i, 2), jobs[i], 1, st));
+    g8_written = keep_grads;
     return NITI_NO_ERROR;
 }
 
@@ -1679,7 +1751,7 @@ int niti_model_get_tap(niti_model_t m, int layer, int which, int8_t* host, size_
     size_t need = 0;
     if (which == 0 || which == 2)
         need = (size_t)n * g.c_out * g.oh * g.ow;
-    else if (which == 1 && m->m.keep_grads)
+    else if (which == 1 && m->m.g8_written)
         need = (size_t)g.c_out * g.c_in * g.kh * g.kw;
     else
         return NITI_INVALID_VALUE;
@@ -1687,6 +1759,10 @@ int niti_model_get_tap(niti_model_t m, int layer, int which, int8_t* host, size_
     if (bytes < out_need) return NITI_INVALID_VALUE;
     if (hipMalloc(&tmp, need) != hipSuccess) return NITI_OUT_OF_MEMORY;
     hipError_t e;
+    if (which == 0 && !l.r_written) {  // (a pooled layer whose route went as codes under keep_grads(0))
+        (void)hipFree(tmp);
+        return NITI_INVALID_VALUE;
+    }
     if (which == 0)
         e = niti::nhwc16_to_nchw(l.r, n, g.c_out, g.oh * g.ow, g.cop, tmp, nullptr);
     else if (which == 2 && !m->m.dy16_valid[layer]) {  // rebuilt from the C32 copy the step wrote
@@ -1877,7 +1953,7 @@ int niti_model_plan_set(niti_model_t m, int layer, int phase, const int plan[4])
         const bool taps = plan[0] == niti::PLAN_TAPS_TILE && plan[1] == niti::PLAN_TAPS_TILE && op == niti::PLAN_WGRAD &&
                           niti::conv_wgrad_taps_ok(g);
         if ((!taps && (!tile_ok(plan[0]) || !tile_ok(plan[1]))) || plan[2] < 1 || plan[2] > 4096 || plan[3] < 0 ||
-            plan[3] > 3 || (taps && plan[3] == 1) || (plan[3] == 3 && (op == niti::PLAN_WGRAD || plan[2] != 1)))
+            plan[3] > 4 || (taps && plan[3] == 1) || (plan[3] >= 3 && (op == niti::PLAN_WGRAD || plan[2] != 1)))
             return NITI_INVALID_VALUE;
         niti::PlanChoice c;
         c.bm = plan[0];
@@ -1903,7 +1979,7 @@ int niti_model_plan_set(niti_model_t m, int layer, int phase, const int plan[4])
         const bool p16 = plan[0] == niti::PLAN_P16_TILE && plan[1] == niti::PLAN_P16_TILE &&
                          op == niti::PLAN_WGRAD && niti::conv_wgrad_p16_ok(g);
         if ((!taps && !p16 && (!tile_ok(plan[0]) || !tile_ok(plan[1]))) || plan[2] < 1 || plan[3] < 0 ||
-            plan[3] > 3 || ((taps || p16) && plan[3] == 1) || (plan[3] == 3 && (op == niti::PLAN_WGRAD || plan[2] != 1)))
+            plan[3] > 4 || ((taps || p16) && plan[3] == 1) || (plan[3] >= 3 && (op == niti::PLAN_WGRAD || plan[2] != 1)))
             return NITI_INVALID_VALUE;
         if (p16) {
             if (plan[2] > 64) return NITI_INVALID_VALUE;

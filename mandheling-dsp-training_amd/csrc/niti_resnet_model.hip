@@ -133,11 +133,14 @@ int ResNetModel::build(int batch_, int in_hw_, int classes_) {
         slab_bytes = std::max(slab_bytes, conv_fwd_workspace(g));
         slab_bytes = std::max(slab_bytes, conv_dgrad_workspace(g));
         slab_w_bytes = std::max(slab_w_bytes, conv_wgrad_workspace(g));
+        // grid-barrier state: the row kernels' fused launches and speculation slots, or the GEMM
+        // path's fused-rescale launches (STRAT_FUSED)
+        c.bar = (uint32_t*)ws.alloc(ROWCONV_BAR_WORDS * 4);
+        if (!c.bar || hipMemset(c.bar, 0, ROWCONV_BAR_WORDS * 4) != hipSuccess) return NITI_OUT_OF_MEMORY;
         if (i > 0 && rowconv_ok(g)) {
             c.rows = 1;
             c.wf = A8(rowconv_wf_bytes(g.c_out, g.c_in));
-            c.bar = (uint32_t*)ws.alloc(ROWCONV_BAR_WORDS * 4);
-            if (!c.wf || !c.bar || hipMemset(c.bar, 0, ROWCONV_BAR_WORDS * 4) != hipSuccess) return NITI_OUT_OF_MEMORY;
+            if (!c.wf) return NITI_OUT_OF_MEMORY;
             if (!rowconv_nhwc_pref(g) && !(c.xc32 = A8((size_t)n * round_up(g.c_in, 32) * g.h * g.w)))
                 return NITI_OUT_OF_MEMORY;
             rc_acc_size = std::max(rc_acc_size, rowconv_acc_bytes(g, false));
@@ -351,6 +354,16 @@ int ResNetModel::fwd_conv(int i, hipStream_t st) {
             o.pool3.OH = o.pool3.OW = ph;
             if (!keep_grads) o.out = nullptr;  // (the pre-pool output: only its tap reads it)
         }
+        stem_y_written = o.out != nullptr;
+    }
+    if (!dp && !capturing) {  // one launch with the rescale fused (plan strategy 4, every tile resident)
+        const hipError_t e = conv_fwd_fused(g, c.in, c.w, o, FusedBar{c.bar, c.epoch + 1, rc_err}, st);
+        if (e != hipErrorNotSupported) {
+            ++c.epoch;
+            RTRY(e);
+            probe(i, 0, false, st);
+            return NITI_NO_ERROR;
+        }
     }
     if (conv_fwd_spec_ok(g)) {  // the GEMM's speculative pair (plan strategy 3)
         int8_t* alt = conv_fwd_spec_alt_bytes(g) <= gspec_alt_bytes ? gspec_alt : nullptr;
@@ -410,6 +423,15 @@ int ResNetModel::dgrad_conv(int i, hipStream_t st) {
     o.wscale = c.ws_dev;
     o.exp_out = c.dx_exp;
     uint32_t* slot = c.gspec + GEMM_SPEC_SLOT_WORDS;
+    if (!dp && !capturing) {  // one launch with the rescale fused (plan strategy 4; stride 1)
+        const hipError_t e = conv_dgrad_fused(g, c.dy, c.wT, o, FusedBar{c.bar, c.epoch + 1, rc_err}, st);
+        if (e != hipErrorNotSupported) {
+            ++c.epoch;
+            RTRY(e);
+            probe(i, 1, false, st);
+            return NITI_NO_ERROR;
+        }
+    }
     if (conv_dgrad_spec_ok(g)) {
         int8_t* alt = conv_dgrad_spec_alt_bytes(g) <= gspec_alt_bytes ? gspec_alt : nullptr;
         RTRY(conv_dgrad_spec(g, c.dy, c.wT, rng(i, 1), o, slot, 0, st, alt));
@@ -439,20 +461,35 @@ int ResNetModel::wgrad_conv(int i, hipStream_t st) {
     return NITI_NO_ERROR;
 }
 
-// conv i's own slab buffer for a deferred weight-gradient combine, sized to the plan it runs with
-// (false: the plan does not split K into C-shaped slabs, or no memory)
+// conv i's own slab buffer for a deferred weight-gradient combine is big enough for the plan it
+// runs with (false: the plan does not split K into C-shaped slabs, or the buffer was not sized)
 bool ResNetModel::ensure_wslab(int i) {
-    RConv& c = C[i];
+    const RConv& c = C[i];
     const PlanChoice p = conv_plan_query(PLAN_WGRAD, c.g, false, slab_w_bytes);
     if (p.strat != 2 || p.splits < 2 || p.bm == PLAN_P16_TILE) return false;
-    const size_t need = conv_wgrad_slab_bytes(c.g, p);  // (GEMM or tap-sharing slabs)
-    if (c.wslab_bytes >= need) return true;
-    if (hipDeviceSynchronize() != hipSuccess) return false;
-    void* q = ws.alloc(need);
-    if (!q) return false;
-    c.wslab = (int32_t*)q;
-    c.wslab_bytes = need;
-    return true;
+    return c.wslab_bytes >= conv_wgrad_slab_bytes(c.g, p);  // (GEMM or tap-sharing slabs)
+}
+
+// Size every conv's deferred-combine slab for the current plans: at the head of run(), before
+// anything is enqueued, whenever a plan override changed since the last sizing (one device sync,
+// the old buffer freed).  Inside the step ensure_wslab only checks.
+int ResNetModel::size_wslabs() {
+    if (wslab_epoch == plan_override_epoch()) return NITI_NO_ERROR;
+    bool synced = false;
+    for (RConv& c : C) {
+        const PlanChoice p = conv_plan_query(PLAN_WGRAD, c.g, false, slab_w_bytes);
+        if (p.strat != 2 || p.splits < 2 || p.bm == PLAN_P16_TILE) continue;
+        const size_t need = conv_wgrad_slab_bytes(c.g, p);
+        if (c.wslab_bytes >= need) continue;
+        if (!synced && hipDeviceSynchronize() != hipSuccess) return NITI_NO_EXECUTION;
+        synced = true;
+        void* q = ws.replace(c.wslab, need);
+        c.wslab = (int32_t*)q;
+        c.wslab_bytes = q ? need : 0;
+        if (!q) return NITI_OUT_OF_MEMORY;
+    }
+    wslab_epoch = plan_override_epoch();
+    return NITI_NO_ERROR;
 }
 
 // Block k's output: relu(requant(aligned y_b + shortcut)) -- range pass (the sum not stored),
@@ -568,6 +605,10 @@ int ResNetModel::run(const int8_t* x_nchw, int exp_in, const uint8_t* images, co
         ~InStep() { f = false; }
     } in_step_guard(in_step);
     for (RConv& c : C) c.defer = SgdJob{};
+    if (!dp && !capturing && !tuning) {
+        const int rc = size_wslabs();  // (plan changes: no allocation or sync inside the step)
+        if (rc != NITI_NO_ERROR) return rc;
+    }
     // the range words start each step at zero: zeroed by the input statistics launch (uint8
     // images), else here
     if (images == nullptr || amax_bytes % 16 != 0) RTRY(hipMemsetAsync(amax, 0, amax_bytes, st));
@@ -682,6 +723,7 @@ int ResNetModel::run(const int8_t* x_nchw, int exp_in, const uint8_t* images, co
         }
     }
     RTRY(sgd_update_many(jobs, nl, st));
+    g8_written = keep_grads;
     return NITI_NO_ERROR;
 }
 
@@ -808,6 +850,8 @@ int ResNetModel::autotune(hipStream_t st, int reps) {
                         c.strat = 3;
                         cands.push_back(c);
                     }
+                    c.strat = 4;  // one launch, the rescale fused (where every tile is resident)
+                    cands.push_back(c);
                 }
                 for (int s : split_opts) {
                     if (s > steps / 2 || plan_slab_bytes(key.M, key.N, s) > wsb) break;
@@ -925,10 +969,10 @@ int ResNetModel::get_tap(int layer, int which, int8_t* host, size_t bytes, hipSt
     const int n = batch;
     if (hipStreamSynchronize(st) != hipSuccess) return NITI_NO_EXECUTION;
     size_t need = 0;
-    if (which == 0 && layer == 0 && stem_pooled && !keep_grads) return NITI_INVALID_VALUE;  // (never written)
+    if (which == 0 && layer == 0 && !stem_y_written) return NITI_INVALID_VALUE;  // (not written by the last step)
     if (which == 0 || which == 2)
         need = (size_t)n * g.c_out * g.oh * g.ow;
-    else if (which == 1 && keep_grads)
+    else if (which == 1 && g8_written)
         need = (size_t)g.c_out * g.c_in * g.kh * g.kw;
     else
         return NITI_INVALID_VALUE;

@@ -90,6 +90,10 @@ struct ResNetModel {
     // the stem's requantise pass also max-pooled (Pool3) this step; with keep_grads off its pre-pool
     // output is then never written (its forward tap is unavailable)
     bool stem_pooled = false;
+    // what the last step wrote for the debug taps (get_tap reads these, not the current
+    // keep_grads): the stem's pre-pool output, the int8 weight gradients
+    bool stem_y_written = false;
+    bool g8_written = false;
     int8_t* d0 = nullptr;         // the stem's output gradient
     int32_t* gsum = nullptr;      // global sum pool [n][512]
     int8_t* g8pool = nullptr;     // its requantisation (the fc input)
@@ -166,6 +170,8 @@ struct ResNetModel {
     int wgrad_conv(int i, hipStream_t st);
     bool in_step = false;  // run(): weight gradients may leave their split-K combine to the update
     bool ensure_wslab(int i);
+    int size_wslabs();
+    unsigned wslab_epoch = 0;  // plan_override_epoch() the slabs were last sized for
     int residual_fwd(int k, hipStream_t st);
     int residual_bwd(int k, hipStream_t st);
     int run(const int8_t* x_nchw, int exp_in, const uint8_t* images, const int32_t* labels, hipStream_t st);

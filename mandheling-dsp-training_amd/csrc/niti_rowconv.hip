@@ -127,6 +127,8 @@ struct RowConvArgs {
     int8_t* pool_dx;
     int8_t* pool_dx_next;
     int pool_relu;
+    const int8_t* pool_code;     // the recorded route (pool_code4) instead of pool_x / pool_y, or null
+    int8_t* pool_code_out;       // forward with pool_out: the route recorded, or null
     int pool_dx_nhwc;            // 0: the NHWC16 pool_dx is not written (its consumers read the C32 / P16 copies)
     int8_t* p16;                 // P16 [pixels/16][cop][16] copy of out / pool_dx, or null
     int64_t p16_pixels;          // pixels of that tensor
@@ -559,23 +561,19 @@ struct EpiIn {
                   // at the output's own pixels: hipcc merges the two branches' loads into one)
 };
 
-// SWAR on 4 int8 lanes of a dword; a "hi" result is meaningful in bit 7 of each byte only
-constexpr uint32_t SW_H = 0x80808080u, SW_L = 0x7F7F7F7Fu;
-__device__ __forceinline__ uint32_t sw_ge_hi(uint32_t x, uint32_t m) {  // signed x >= m
-    const uint32_t ax = x ^ SW_H, bm = m ^ SW_H;  // as unsigned
-    const uint32_t t = (ax | SW_H) - (bm & SW_L);  // bit 7: low 7 bits of ax >= those of bm
-    const uint32_t d = ax ^ bm;                    // bit 7: the top bits differ -> ax's top bit decides
-    return ((d & ax) | (~d & t)) & SW_H;
-}
-__device__ __forceinline__ uint32_t sw_pos_hi(uint32_t x) {  // signed x > 0
-    const uint32_t nz = (((x & SW_L) + SW_L) | x) & SW_H;
-    return nz & ~x;
-}
-__device__ __forceinline__ uint32_t sw_expand(uint32_t hb) { return hb | (hb - (hb >> 7)); }
+// (SWAR byte helpers sw_ge_hi / sw_pos_hi / sw_expand and the 2x2 pool codes: niti_device.hpp)
 
 template <int R, bool PX = true>
 __device__ __forceinline__ void epi_masks(const RowConvArgs& a, EpiIn<R, PX>& e) {
-    if (PX && a.pool_dx != nullptr) {
+    if (PX && a.pool_dx != nullptr && a.pool_code != nullptr) {
+        // the route the forward pass recorded: e.y holds the code bytes
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+                for (int t = 0; t < 4; ++t) e.x[PX ? r : 0][t][k] = (int)pool_code_mask((uint32_t)e.y[r][k], t);
+    } else if (PX && a.pool_dx != nullptr) {
         // NITI_CPUPoolGrad_Int8's scan: the first window element >= the pool output takes it
 #pragma unroll
         for (int r = 0; r < R; ++r)
@@ -613,13 +611,14 @@ __device__ __forceinline__ void epi_prefetch(const RowConvArgs& a, const RowUnit
     // the tensor at the output's own pixels (pool_y or relu_mask) in one branch-free load per row
     // (two branches writing e.y were merged by hipcc through a scratch array)
     const bool pool = a.pool_dx != nullptr;
-    const int8_t* ps = (pool ? a.pool_y : a.relu_mask) + z;
+    const bool code = pool && a.pool_code != nullptr;  // the recorded route: one load per row
+    const int8_t* ps = (pool ? (code ? a.pool_code : a.pool_y) : a.relu_mask) + z;
     const int8_t* px = a.pool_x + z;
     if (!pool && a.relu_mask == nullptr) return;
 #pragma unroll
     for (int r = 0; r < R; ++r)
         e.y[r] = *(const v4i*)(ps + ((img * H + U.b * R + r) * W + ox) * a.cop + cb16);
-    if (pool) {
+    if (pool && !code) {
 #pragma unroll
         for (int r = 0; r < R; ++r)
 #pragma unroll
@@ -750,9 +749,21 @@ __device__ __forceinline__ void rowconv_epilogue(const RowConvArgs& a, const Row
                 pm[i] = (int8_t)(v0 > v1 ? v0 : v1);
             }
             const v4i v = pack_cols(pm);
+            v4i code{0, 0, 0, 0};
+            if (a.pool_code_out != nullptr) {
+                // the window's elements: this lane's (top, bottom) and the odd neighbour's
+                const v4i t0 = pack_cols(q[r]), t2 = pack_cols(q[r + 1]);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const uint32_t t1 = (uint32_t)__builtin_amdgcn_mov_dpp(t0[k], 0xB1, 0xF, 0xF, false);
+                    const uint32_t t3 = (uint32_t)__builtin_amdgcn_mov_dpp(t2[k], 0xB1, 0xF, 0xF, false);
+                    code[k] = (int)pool_code4((uint32_t)t0[k], t1, (uint32_t)t2[k], t3, (uint32_t)v[k], a.relu != 0);
+                }
+            }
             if (U.img_ok && (ox & 1) == 0) {
                 const int py = (U.b * R + r) / 2, px = ox / 2;
                 *(v4i*)(a.pool_out + ((img * HO + py) * WO + px) * a.cop + cb16) = v;
+                if (a.pool_code_out != nullptr) *(v4i*)(a.pool_code_out + ((img * HO + py) * WO + px) * a.cop + cb16) = code;
                 if (a.next != nullptr)
                     *(v4i*)(a.next + (((img * a.COB + U.cob) * HO + py) * WO + px) * 32 + 16 * h) = v;
             }
@@ -1059,7 +1070,7 @@ template <int R, int MODE, bool DG, bool PX = true>
 __device__ __forceinline__ void seg_run(const RowConvArgs& a, int lane, int wid, int8_t* smem, uint32_t& m,
                                         uint32_t g) {
     constexpr int NR = R + 2, S = 4, L = NR + 3;
-    const int H = a.hw, W = a.hw, CB = a.CB;
+    const int H = a.hw, CB = a.CB;
     const int h = lane >> 5, c = lane & 31;
     const __amdgpu_buffer_rsrc_t rX = make_rsrc(a.x, a.xbytes);
     const __amdgpu_buffer_rsrc_t rW = make_rsrc(a.wf, a.wbytes);
@@ -1495,7 +1506,7 @@ bool rowconv_ok(const ConvGeom& g) {
     return true;
 }
 
-static bool rowconv_seg(const ConvGeom& g) { return g.w > 16 || g.w == 14; }
+bool rowconv_seg(const ConvGeom& g) { return g.w > 16 || g.w == 14; }
 
 // the row-segment form can read its input as NHWC16 in place (RowConvOut::x_nhwc) ...
 bool rowconv_nhwc_ok(const ConvGeom& g) { return rowconv_ok(g) && rowconv_seg(g) && g.cip % 32 == 0; }
@@ -1667,7 +1678,7 @@ static hipError_t launch_rc(int W, int R, int grid, RowConvArgs a, hipStream_t s
 // (hipOccupancyMaxActiveBlocksPerMultiprocessor over its LDS and registers), cached per (device,
 // kernel); 0 without a device.  The fused mode's grid barrier needs the whole grid resident, so a
 // smaller or partitioned device takes the two-launch form instead.
-int resident_wgs(const void* f) {
+int resident_wgs(const void* f, int threads) {
     static std::mutex mu;
     static std::map<std::pair<int, const void*>, int> cache;
     int dev = -1;
@@ -1681,7 +1692,7 @@ int resident_wgs(const void* f) {
     if (it != cache.end()) return it->second;
     int cus = 0, occ = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, f, 256, 0) != hipSuccess) {
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, f, threads, 0) != hipSuccess) {
         (void)hipGetLastError();
         return 0;
     }
@@ -1761,10 +1772,15 @@ hipError_t rowconv_fwd(const ConvGeom& g, const int8_t* x_c32, const int8_t* wf,
     const int spec2 = spec ? mode - RC_SPEC_A + 1 : 0;
     if (spec) mode = RC_REQUANT;
     // an output: NHWC16 out, the pool gradient, or (input gradient) only the C32 / P16 copies
-    if (mode != RC_RANGE && o.out == nullptr && o.pool_dx == nullptr && o.next == nullptr && o.p16 == nullptr)
+    if (mode != RC_RANGE && o.out == nullptr && o.pool_dx == nullptr && o.next == nullptr && o.p16 == nullptr &&
+        o.pool_out == nullptr)
         return hipErrorInvalidValue;
-    if (o.pool_dx != nullptr && (o.pool_x == nullptr || o.pool_y == nullptr || o.out != nullptr || o.pool_out != nullptr ||
-                                 o.relu_mask != nullptr || o.next != nullptr))
+    if (o.pool_dx != nullptr && ((o.pool_code == nullptr && (o.pool_x == nullptr || o.pool_y == nullptr)) ||
+                                 o.out != nullptr || o.pool_out != nullptr || o.relu_mask != nullptr || o.next != nullptr))
+        return hipErrorInvalidValue;
+    // the recorded pool route: the W > 0 forms (the row-segment epilogues scan the window)
+    if ((o.pool_code != nullptr && o.pool_dx == nullptr) || (o.pool_code_out != nullptr && o.pool_out == nullptr) ||
+        ((o.pool_code != nullptr || o.pool_code_out != nullptr) && rowconv_seg(g)))
         return hipErrorInvalidValue;
     RowConvArgs a{};
     const int CB = (g.c_in + 31) / 32, COB = g.cop / 32;
@@ -1837,6 +1853,8 @@ hipError_t rowconv_fwd(const ConvGeom& g, const int8_t* x_c32, const int8_t* wf,
     a.pool_dx = o.pool_dx;
     a.pool_dx_next = o.pool_dx_next;
     a.pool_relu = o.pool_relu;
+    a.pool_code = o.pool_code;
+    a.pool_code_out = o.pool_code_out;
     a.pool_dx_nhwc = o.pool_dx_nhwc;
     a.p16 = o.p16;
     a.p16_pixels = (int64_t)g.n * g.h * g.w * (o.pool_dx != nullptr ? 4 : 1);
@@ -1958,7 +1976,8 @@ hipError_t rowconv_fc(int n, int K, int rows, const int8_t* x, int xld, const in
     // an output: NHWC16 out, the pool gradient, or (input gradient) only the C32 / P16 copies
     if (mode != RC_RANGE && o.out == nullptr && o.pool_dx == nullptr && o.next == nullptr && o.p16 == nullptr)
         return hipErrorInvalidValue;
-    if (o.pool_out != nullptr || (o.pool_dx != nullptr && (o.pool_x == nullptr || o.pool_y == nullptr)))
+    if (o.pool_out != nullptr || o.pool_code_out != nullptr || (o.pool_code != nullptr && o.pool_dx == nullptr) ||
+        (o.pool_dx != nullptr && o.pool_code == nullptr && (o.pool_x == nullptr || o.pool_y == nullptr)))
         return hipErrorInvalidValue;
     const int64_t xb = (int64_t)n * xld, wb = (int64_t)rows * wld;
     if (xb > 0x7fffffff || wb > 0x7fffffff) return hipErrorInvalidValue;
@@ -1999,6 +2018,7 @@ hipError_t rowconv_fc(int n, int K, int rows, const int8_t* x, int xld, const in
     a.pool_dx = o.pool_dx;
     a.pool_dx_next = o.pool_dx_next;
     a.pool_relu = o.pool_relu;
+    a.pool_code = o.pool_code;
     a.pool_dx_nhwc = o.pool_dx_nhwc;
     a.p16 = o.p16;
     a.p16_pixels = (int64_t)n * (o.pool_dx != nullptr ? 4 : 1);

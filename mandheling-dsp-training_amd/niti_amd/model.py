@@ -158,7 +158,8 @@ class NitiModel:
 
     def plans(self):
         """{(layer, phase): (bm, bn, splits, strategy)}; phase 0 fwd / 1 input grad / 2 weight grad,
-        strategy 0 store / 1 recompute / 2 split-K / 3 the speculative pair (forward / input gradient)."""
+        strategy 0 store / 1 recompute / 2 split-K / 3 the speculative pair / 4 fused: one launch with the
+        rescale behind an in-kernel grid barrier (forward / input gradient)."""
         out = {}
         for i in range(len(self.layers)):
             for ph in (0, 1, 2):

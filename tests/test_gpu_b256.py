@@ -65,11 +65,13 @@ def case():
     return dict(layers=layers, W=W, S=S, img=img, labels=labels, x=x, ascale=ascale, newW=newW, rec=rec)
 
 
-def _step_and_compare(T, case, prepare):
+def _step_and_compare(T, case, prepare, keep_grads=True):
     import niti_amd
+    from niti_amd._lib import NitiError
     from niti_amd.model import NitiModel
     layers, rec = case["layers"], case["rec"]
     m = NitiModel(niti_amd.ARCH_VGG11, B)
+    m.keep_grads(keep_grads)
     img = T.from_numpy(case["img"]).cuda()
     lab = T.from_numpy(case["labels"]).cuda()
     for i, (w, s) in enumerate(zip(case["W"], case["S"])):
@@ -85,9 +87,14 @@ def _step_and_compare(T, case, prepare):
     logits, e = m.logits()
     assert e == rec["exp"][-1] and np.array_equal(logits, rec["logits"])
     for i in range(len(layers)):
-        assert np.array_equal(m.tap(i, 0), rec["r"][i]), ("fwd", i, plans[(i, 0)])
+        if keep_grads or not layers[i]["pool"]:
+            assert np.array_equal(m.tap(i, 0), rec["r"][i]), ("fwd", i, plans[(i, 0)])
+        else:  # the pooled layers' 2x2 route went to the input gradients as codes: no pre-pool output
+            with pytest.raises(NitiError):
+                m.tap(i, 0)
         assert np.array_equal(m.tap(i, 2), rec["dy"][i]), ("dy", i)
-        assert np.array_equal(m.tap(i, 1), rec["dw"][i]), ("dw", i, plans[(i, 2)])
+        if keep_grads:
+            assert np.array_equal(m.tap(i, 1), rec["dw"][i]), ("dw", i, plans[(i, 2)])
         assert np.array_equal(m.get_weight(i), case["newW"][i]), ("w", i)
     return plans
 
@@ -99,6 +106,20 @@ def test_vgg11_b256_autotuned_step_full_parity(T, case):
     finally:
         NitiModel.reset_plans()
     print("\nautotuned plans {(layer, phase): (bm, bn, splits, strategy)}:", plans)
+
+
+def test_vgg11_b256_bench_config_parity(T, case):
+    """The step exactly as bench.py times it: autotuned plans and keep_grads(False) -- no int8
+    weight-gradient copies, and the pooled layers' 2x2 routes recorded as codes by the forward
+    kernels (conv0's and the row kernels' epilogues) and read by the next input gradient instead of
+    the pre-pool output, which is then never written (NITI_CPUPoolGrad_Int8.cpp:21-77: the first
+    window element >= the pooled value takes the gradient).  Logits, every output gradient, every
+    unpooled forward tap and every new weight against the oracle."""
+    from niti_amd.model import NitiModel
+    try:
+        _step_and_compare(T, case, lambda m: m.autotune(), keep_grads=False)
+    finally:
+        NitiModel.reset_plans()
 
 
 @pytest.mark.parametrize("splits", [6, 8])

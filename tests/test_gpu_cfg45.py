@@ -9,8 +9,7 @@
   tile-mode tap-sharing weight gradient with 128 / 64 / 32 / 16 K splits on conv1_2 .. conv3_1, and
   split-K GEMMs on the deeper layers.  Every tap of a whole step is compared with the oracle.
 - Exact data parallelism where the row-segment speculative pair runs under the cross-rank MAX:
-  VGG-16 at 224 px, one image per rank through the C++ in-process group, and ResNet-18 at 112 px
-  through ThreadComm.  One rank gets an all-zero image, so its local bit width is 0 in every forward
+  VGG-16 at 224 px and ResNet-18 at 112 px, one image per rank through the C++ in-process group.  One rank gets an all-zero image, so its local bit width is 0 in every forward
   layer while the global one is not.  The first step has no hint, so every pair's launch B redoes
   its launch against the all-reduced max.  Every rank must equal one device stepping the whole batch.
 Reference semantics: NITI_Conv_Int8.cpp:260-307 (RangeEstimate over the whole batch, then the shift
@@ -110,13 +109,16 @@ VGG16_BENCH_PLANS = {
 }
 
 
-@pytest.mark.parametrize("plans", ["autotuned", "bench", "spec"])
+@pytest.mark.parametrize("plans", ["autotuned", "bench", "spec", "fused"])
 def test_vgg16_224_tuned_plans_step_matches_oracle(T, plans):
     """A whole VGG-16 224-px step (batch 2) under the autotuner's plans, under the bench's batch-64
-    kernel choices forced on, or with every GEMM-path forward and input gradient on the speculative
+    kernel choices forced on, with every GEMM-path forward and input gradient on the speculative
     pair (plan strategy 3: launch A requantises with the previous bit width, launch B redoes it on a
-    change -- no int32 tensor), every tap against the oracle over two steps; plans dropped after."""
+    change -- no int32 tensor), or on the fused form (plan strategy 4: one launch, the accumulators
+    kept in registers across the in-kernel grid barrier that carries the bit width), every tap
+    against the oracle over two steps; plans dropped after."""
     import niti_amd
+    from niti_amd import _lib as L
     import niti_model_ref as R
     from niti_amd.model import NitiModel
     layers = R.vgg16_layers(224)
@@ -137,12 +139,14 @@ def test_vgg16_224_tuned_plans_step_matches_oracle(T, plans):
             for layer in range(1, 5):
                 assert m.plan(layer, 2)[:2] == (32, 32), layer
         else:
+            st = 3 if plans == "spec" else 4
             for layer in range(5, len(layers)):
                 for phase in (0, 1):
-                    m.set_plan(layer, phase, (128, 128, 1, 3))
-                    assert m.plan(layer, phase)[3] == 3, (layer, phase)
+                    m.set_plan(layer, phase, (128, 128, 1, st))
+                    assert m.plan(layer, phase)[3] == st, (layer, phase)
         for i, (w, s) in enumerate(zip(W, S)):
             m.set_weight(i, w, s)
+        n0 = L.lib().niti_diag_gemm_fused_launches()
         for step in range(2):
             x = rng.integers(-127, 128, (2, 3, 224, 224)).astype(np.int8)
             labels = rng.integers(0, 1000, 2).astype(np.int32)
@@ -157,6 +161,8 @@ def test_vgg16_224_tuned_plans_step_matches_oracle(T, plans):
                 assert np.array_equal(m.get_weight(i), newW[i]), ("w", step, i)
             W = newW
         assert m.rowconv_error() == 0
+        if plans == "fused":
+            assert L.lib().niti_diag_gemm_fused_launches() > n0
     finally:
         NitiModel.reset_plans()
 
@@ -249,47 +255,57 @@ def test_vgg16_224_local_dp_row_segment_pair(T):
         assert m.rowconv_error() == 0
 
 
-def test_resnet18_112_thread_dp_row_segment_pair(T):
-    """ResNet-18 at 112 px, world 2 through ThreadComm: its 28 / 14-px stride-1 convs run the
-    row-segment speculative pair with the MAX between A and B.  One rank's images are all zero on
-    steps 0 and 2.  Every rank equals one full-batch device (logits, weight gradients, weights)."""
+def test_resnet18_112_local_dp_row_segment_pair(T):
+    """ResNet-18 at 112 px, 1000 classes, world 2 on the C++ step driver (the bench's) through the
+    in-process group (the RCCL protocol's calls, order and streams): its 28 / 14-px stride-1 convs run
+    the row-segment speculative pair with the MAX between A and B.  One rank's images are all zero on
+    steps 0 and 2.  Every rank equals one full-batch device (every tap slice, weight gradient and
+    weight), and the full-batch device equals the oracle on the first step."""
+    import niti_amd
     import niti_resnet_ref as RR
-    from niti_amd.dp import ThreadComm
-    from niti_amd.resnet import ResNet18
+    from niti_amd.model import LocalGroup, NitiModel
     world, per, hw, classes = 2, 1, 112, 1000
     convs = RR.resnet18_convs(hw, classes)
     W, S = RR.init_weights(convs, seed=113)
-    full = ResNet18(world * per, hw, classes)
-    comm = ThreadComm(world)
-    ranks = [ResNet18(per, hw, classes, comm=comm.rank(r)) for r in range(world)]
-    assert any(full.rows), "no row-kernel layer at 112 px"
+    full = NitiModel(niti_amd.ARCH_RESNET18, world * per, hw, classes)
+    ranks = [NitiModel(niti_amd.ARCH_RESNET18, per, hw, classes) for _ in range(world)]
+    group = LocalGroup(world)
+    for r, m in enumerate(ranks):
+        m.attach_local(group, r, exact=True)
     for m in [full] + ranks:
         for i, (w, s) in enumerate(zip(W, S)):
             m.set_weight(i, w, s)
-        m.record = True
+    streams = [T.cuda.Stream() for _ in range(world)]
     rng = np.random.default_rng(113)
     for step, (x, labels) in enumerate(_batches(rng, 3, world, per, (3, hw, hw), classes)):
         full.train_step(T.from_numpy(x).cuda(), -2, T.from_numpy(labels).cuda())
         T.cuda.synchronize()
+        parts = [(T.from_numpy(x[r * per:(r + 1) * per].copy()).cuda(),
+                  T.from_numpy(labels[r * per:(r + 1) * per].copy()).cuda()) for r in range(world)]
 
-        def run(r):
-            sl = slice(r * per, (r + 1) * per)
-            try:
-                ranks[r].train_step(T.from_numpy(x[sl].copy()).cuda(), -2, T.from_numpy(labels[sl].copy()).cuda())
-            except BaseException:
-                comm._bar.abort()
-                raise
+        def rank_step(r):
+            ranks[r].train_step(parts[r][0], -2, parts[r][1], stream=C.c_void_p(streams[r].cuda_stream))
+            streams[r].synchronize()
 
-        _in_threads([lambda r=r: run(r) for r in range(world)])
-        T.cuda.synchronize()
-        ft = full.taps()
-        for r, m in enumerate(ranks):
-            t = m.taps()
-            assert t["exp_logits"] == ft["exp_logits"], (step, r)
-            assert np.array_equal(t["logits"], ft["logits"][r * per:(r + 1) * per]), (step, r)
+        _in_threads([lambda r=r: rank_step(r) for r in range(world)])
+        if step == 0:  # anchor the full-batch device on the oracle
+            newW, rec = RR.train_step(convs, W, S, x, -2, labels, classes=classes)
+            lg, e = full.logits()
+            assert e == rec["exp_logits"] and np.array_equal(lg, rec["logits"])
             for i, c in enumerate(convs):
-                assert np.array_equal(t["fwd"][i], ft["fwd"][i][r * per:(r + 1) * per]), ("fwd", step, r, c["name"])
-                assert np.array_equal(t["dw"][i], ft["dw"][i]), ("dw", step, r, c["name"])
+                assert np.array_equal(full.tap(i, 2), rec["dy"][i]), ("oracle dy", c["name"])
+                assert np.array_equal(full.get_weight(i), newW[i]), ("oracle w", c["name"])
+        fl, fe = full.logits()
+        for r, m in enumerate(ranks):
+            sl = slice(r * per, (r + 1) * per)
+            lg, e = m.logits()
+            assert e == fe and np.array_equal(lg, fl[sl]), (step, r)
+            for i, c in enumerate(convs):
+                assert np.array_equal(m.tap(i, 0), full.tap(i, 0)[sl]), ("fwd", step, r, c["name"])
+                assert np.array_equal(m.tap(i, 2), full.tap(i, 2)[sl]), ("dy", step, r, c["name"])
+                assert np.array_equal(m.tap(i, 1), full.tap(i, 1)), ("dw", step, r, c["name"])
                 assert np.array_equal(m.get_weight(i), full.get_weight(i)), ("w", step, r, c["name"])
+    # the pairs ran under the exchange: the first step's launches B redid theirs (no hint yet)
+    assert sum(s[1] + s[2] + s[4] + s[5] for s in ranks[1].spec_stats()) > 0
     for m in [full] + ranks:
         assert m.rowconv_error() == 0

@@ -63,7 +63,17 @@ def _run(T, arch, layers, batch, steps=2, seed=5, graph=False, reuse_buffers=Tru
         assert e == rec["exp"][-1], (step, e, rec["exp"][-1])
         assert np.array_equal(logits, rec["logits"]), step
         for i in range(len(layers)):
-            assert np.array_equal(m.tap(i, 0), rec["r"][i]), ("fwd", step, i)
+            if not keep_grads and layers[i]["pool"] and sched[step]:
+                # keep_grads(0): a pooled layer whose 2x2 route went to the next input gradient as
+                # codes (the row kernels) does not write its pre-pool output, so that tap is invalid
+                from niti_amd._lib import NitiError
+                try:
+                    fwd = m.tap(i, 0)
+                except NitiError:
+                    fwd = None
+                assert fwd is None or np.array_equal(fwd, rec["r"][i]), ("fwd", step, i)
+            else:
+                assert np.array_equal(m.tap(i, 0), rec["r"][i]), ("fwd", step, i)
             assert np.array_equal(m.tap(i, 2), rec["dy"][i]), ("dy", step, i)
             if keep_grads:
                 assert np.array_equal(m.tap(i, 1), rec["dw"][i]), ("dw", step, i)

@@ -91,12 +91,73 @@ def test_resnet18_cpp_224_images_step_matches_oracle(T):
     assert m.rowconv_error() == 0
 
 
+def test_resnet18_cpp_224_bench_plans_without_taps(T):
+    """BASELINE config 5's timed step as bench.py runs it, at 224 px on a batch of 4: the plan set the
+    batch-128 bench autotuned (tests/golden/plans_resnet18_bench_r05.json, forced through set_plan:
+    the stem's store plan with the requantise pass max-pooling (Pool3), the 128 / 224-split weight
+    gradients, the 32x32 tap-sharing plans at 128 splits, the 2- and 8-split input gradients) and
+    keep_grads(False), from uint8 images through the device quantiser.  Two steps against the oracle:
+    the logits, every forward tap but the stem's (not written under Pool3 + keep_grads(False)), every
+    output gradient, every new weight (NITI_Conv_Int8.cpp:260-307, NITI_GradientConv_Int8.cpp:274-296,
+    NITI_SGD.hpp:20-54)."""
+    import json
+    import niti_oracle as O
+    import niti_resnet_ref as RR
+    from niti_amd._lib import NitiError
+    from niti_amd.model import NitiModel
+    O.set_threads(max(1, min(16, len(os.sched_getaffinity(0)))))
+    hw, batch, classes = 224, 4, 1000
+    convs = RR.resnet18_convs(hw, classes)
+    W, S = RR.init_weights(convs, seed=226)
+    rng = np.random.default_rng(226)
+    m = _model(batch, hw, classes, W, S)
+    m.keep_grads(False)
+    plans = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "plans_resnet18_bench_r05.json")))
+    img = T.zeros((batch, 3, hw, hw), dtype=T.uint8, device="cuda")
+    lab = T.zeros(batch, dtype=T.int32, device="cuda")
+    try:
+        m.train_step_images(img, lab)  # the bench's setup step, then its plans; the weights restored
+        for k, p in plans.items():
+            layer, phase = (int(v) for v in k.split(","))
+            m.set_plan(layer, phase, p)
+        for i, (w, s) in enumerate(zip(W, S)):
+            m.set_weight(i, w, s)
+        assert m.plan(0, 0) == (128, 64, 1, 0) and m.plan(7, 2) == (128, 64, 224, 2)
+        for step in range(2):
+            im = rng.integers(0, 256, (batch, 3, hw, hw)).astype(np.uint8)
+            lb = rng.integers(0, classes, batch).astype(np.int32)
+            img.copy_(T.from_numpy(im))
+            lab.copy_(T.from_numpy(lb))
+            m.train_step_images(img, lab)
+            x, a = O.quantize_images(im)
+            newW, rec = RR.train_step(convs, W, S, x, a, lb, classes=classes)
+            xd, ad = m.input()
+            assert ad == a and np.array_equal(xd, x), step
+            lg, e = m.logits()
+            assert e == rec["exp_logits"] and np.array_equal(lg, rec["logits"]), step
+            for i, c in enumerate(convs):
+                if i > 0:
+                    f = O.relu(rec["fwd"][i]) if m.layers[i]["relu"] else rec["fwd"][i]
+                    assert np.array_equal(m.tap(i, 0), f), ("fwd", step, c["name"])
+                assert np.array_equal(m.tap(i, 2), rec["dy"][i]), ("dy", step, c["name"])
+                assert np.array_equal(m.get_weight(i), newW[i]), ("w", step, c["name"])
+            with pytest.raises(NitiError):
+                m.tap(0, 0)  # the stem's pre-pool output was never written
+            W = newW
+        assert m.rowconv_error() == 0
+    finally:
+        NitiModel.reset_plans()
+
+
 def test_resnet18_cpp_autotuned_recompute_and_gemm_paths(T):
     """The autotuner's plans, then every GEMM-path forward forced onto the recompute form, then every
-    GEMM-path forward and input gradient onto the speculative pair (plan strategy 3), then the row
+    GEMM-path forward and input gradient onto the fused form (plan strategy 4: one launch, the
+    rescale behind the in-kernel grid barrier; 128x128 and 64x64 tiles; the strided input gradients
+    keep their sub-pixel classes), then onto the speculative pair (plan strategy 3), then the row
     kernels switched off too (every conv on the GEMM pair): two steps each against the oracle; the
     plans are dropped afterwards."""
     import niti_resnet_ref as RR
+    from niti_amd import _lib as L
     from niti_amd.model import NitiModel
     hw, batch, classes = 64, 3, 1000
     convs = RR.resnet18_convs(hw, classes)
@@ -110,10 +171,15 @@ def test_resnet18_cpp_autotuned_recompute_and_gemm_paths(T):
         m.autotune(reps=1)
         for i, (w, s) in enumerate(zip(W, S)):
             m.set_weight(i, w, s)
-        for phase in ("tuned", "recompute", "spec", "gemm"):
+        for phase in ("tuned", "recompute", "fused", "spec", "gemm"):
             if phase == "recompute":
                 for i in range(len(convs)):
                     m.set_plan(i, 0, (128, 128, 1, 1))
+            if phase == "fused":  # one launch with the rescale behind the grid barrier (strategy 4)
+                n0 = L.lib().niti_diag_gemm_fused_launches()
+                for i in range(len(convs)):
+                    for ph in (0, 1):
+                        m.set_plan(i, ph, (64, 64, 1, 4) if i % 2 else (128, 128, 1, 4))
             if phase == "spec":  # the speculative pair on every GEMM-path forward and input gradient
                 for i in range(len(convs)):
                     for ph in (0, 1):
@@ -127,6 +193,9 @@ def test_resnet18_cpp_autotuned_recompute_and_gemm_paths(T):
                 m.train_step(T.from_numpy(x).cuda(), -2, T.from_numpy(lab).cuda())
                 _check_step(m, convs, rec, newW, (phase, step))
                 W = newW
+            if phase == "fused":
+                assert L.lib().niti_diag_gemm_fused_launches() > n0
+        assert m.rowconv_error() == 0
     finally:
         NitiModel.reset_plans()
 

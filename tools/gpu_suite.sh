@@ -4,7 +4,7 @@
 set -u
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
-TAG=${TAG:-r05}
+TAG=${TAG:-r06}
 TESTS=${TESTS:-tests}
 timeout -k 10 1000 python -u -m pytest $TESTS -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/gpu_tests_$TAG.log 2>&1
 rc=$?; tail -5 gpurun_out/gpu_tests_$TAG.log; echo "pytest rc=$rc"

@@ -1,6 +1,6 @@
 """2^24-guard and float32-accumulation change counts at ImageNet size, at the bench batch, on a sampled
 layer set: VGG-16 224 px batch 64 (BASELINE cfg 4 per GPU) and ResNet-18 224 px
-batch 128 (cfg 5 per GPU).
+batch 128 (cfg 5 per GPU, its stem).
 
 One device step (uint8 images through the on-device quantiser, as bench.py) records every layer's
 input, output, output gradient and int8 weight gradient; for sampled outputs of a few layers the
@@ -134,43 +134,36 @@ def run_vgg16(args, T, threads):
 
 
 def run_resnet18(args, T, threads):
-    from niti_amd.resnet import ResNet18
+    """The stem (7x7 / 2 over 224 px, the ResNet-18 layer with the largest K and the most guard
+    passes) on the C++ step driver: its input is the quantised batch (model.input()); the other
+    layers' inputs are not exposed as taps by niti_model_get_tap."""
+    import niti_amd
+    from niti_amd.model import NitiModel
     batch = 128
-    net = ResNet18(batch, 224)
+    net = NitiModel(niti_amd.ARCH_RESNET18, batch, 224, 1000)
     rng = np.random.default_rng(11)
     W = []
-    for i in range(len(net.convs)):
+    for i in range(len(net.layers)):
         w, s = O.synth_w(rng, net.weight_shape(i))
         net.set_weight(i, w, s)
         W.append(w)
     img = T.from_numpy(rng.integers(0, 256, (batch, 3, 224, 224), dtype=np.uint8)).cuda()
     lab = T.from_numpy(rng.integers(0, 1000, batch).astype(np.int32)).cuda()
-    net.record = True
     net.train_step_images(img, lab)
     T.cuda.synchronize()
-    taps = net.taps()
-    print(f"ResNet-18 224x224, batch {batch}, one device step from uint8 images (seed 11)", flush=True)
+    print(f"ResNet-18 224x224, batch {batch}, one device step from uint8 images (seed 11), the stem", flush=True)
     srng = np.random.default_rng(2)
-    for i in (0, 1, 12, len(net.convs) - 1):
-        l = net.convs[i]
-        x = net.input_tap(i)
-        y = taps["fwd"][i]
-        dy = taps["dy"].get(i)
-        dw = taps["dw"].get(i)
-        g = O.geom(batch, l["ci"], l["h"], l["h"], l["co"], l["k"], stride=l["stride"], pad=l["pad"])
-        name = f"{l['name']} {l['ci']}->{l['co']}@{l['h']}"
-        ny = batch * l["co"] * g.oh * g.ow
-        relu = bool(net.rec["fwd"][i][1])
-        report(name, "forward", g, 0, x, W[i], y, srng.choice(ny, min(args.samples, ny), replace=False), threads,
-               relu=relu)
-        if dy is not None:
-            nw = l["co"] * l["ci"] * l["k"] * l["k"]
-            report(name, "weight gradient", g, 1, x, dy, dw, srng.choice(nw, min(args.wsamples, nw), replace=False),
-                   threads, rule="grad")
-            if i > 0 and l["stride"] == 1 and l["k"] == 3:
-                nx = batch * l["ci"] * l["h"] * l["h"]
-                report(name, "input gradient", g, 2, dy, W[i], None,
-                       srng.choice(nx, min(args.samples, nx), replace=False), threads)
+    l = net.layers[0]
+    x, _ = net.input()
+    y, dy, dw = net.tap(0, 0), net.tap(0, 2), net.tap(0, 1)
+    g = O.geom(batch, l["c_in"], l["h"], l["w"], l["c_out"], l["kh"], stride=l["stride"], pad=l["pad"])
+    name = f"stem {l['c_in']}->{l['c_out']}@{l['h']}"
+    ny = batch * l["c_out"] * g.oh * g.ow
+    report(name, "forward", g, 0, x, W[0], y, srng.choice(ny, min(args.samples, ny), replace=False), threads,
+           relu=bool(l["relu"]))
+    nw = l["c_out"] * l["c_in"] * l["kh"] * l["kw"]
+    report(name, "weight gradient", g, 1, x, dy, dw, srng.choice(nw, min(args.wsamples, nw), replace=False),
+           threads, rule="grad")
 
 
 def main():
