@@ -107,6 +107,31 @@ __device__ __forceinline__ uint32_t pool_code_mask(uint32_t code, int t) {
     return sw_expand(((code >> t) & 0x01010101u) << 7);
 }
 
+// A speculative pair's guess and its update, for slot words [0] the last bit width + 1 (0: none),
+// [5] the one before it, [6] a 2-bit chooser between "the last" and "the one before" (a layer whose
+// maximum sits at a power of two flips back and forth; as a branch predictor's chooser).  pick:
+// the guess (bw + 1); learn: called by one thread of the pair's second launch with the true bw.
+__device__ __forceinline__ uint32_t spec_pick(const uint32_t* hint) {
+    const uint32_t h = (uint32_t)__builtin_amdgcn_readfirstlane(
+        (int)__hip_atomic_load(hint, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    const uint32_t hp = (uint32_t)__builtin_amdgcn_readfirstlane(
+        (int)__hip_atomic_load(hint + 5, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    const uint32_t ch = (uint32_t)__builtin_amdgcn_readfirstlane(
+        (int)__hip_atomic_load(hint + 6, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    return ch >= 2u && hp != 0u ? hp : h;
+}
+__device__ __forceinline__ void spec_learn(uint32_t* hint, int bw) {
+    const uint32_t h = __hip_atomic_load(hint, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t hp = __hip_atomic_load(hint + 5, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t ch = __hip_atomic_load(hint + 6, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool last_ok = h == (uint32_t)bw + 1u, prev_ok = hp == (uint32_t)bw + 1u;
+    if (prev_ok && !last_ok && ch < 3u) ++ch;
+    if (last_ok && !prev_ok && ch > 0u) --ch;
+    __hip_atomic_store(hint + 6, ch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(hint + 5, h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(hint, (uint32_t)bw + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // The residual rule (niti_resnet.hip): z = hi * 2^d + (lo >> r), arithmetic shift
 __device__ __forceinline__ int32_t residual_z(int32_t hi, int32_t lo, int d, int r) {
     return hi * (1 << d) + (r >= 31 ? (lo < 0 ? -1 : 0) : lo >> r);

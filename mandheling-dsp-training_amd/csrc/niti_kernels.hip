@@ -3493,20 +3493,43 @@ __global__ void __launch_bounds__(256) residual_requant_kernel(const int8_t* __r
                                                                int64_t n16, const uint32_t* __restrict__ amax,
                                                                int8_t* __restrict__ ez, int8_t* __restrict__ exp_out,
                                                                int relu, const int8_t* __restrict__ relu_mask,
-                                                               int8_t* __restrict__ out) {
+                                                               int8_t* __restrict__ out, int spec,
+                                                               uint32_t* __restrict__ hint) {
     const int xa = *ea, xb = *eb;
     const bool a_hi = xa >= xb;
     const int diff = a_hi ? xa - xb : xb - xa;
     const int d = diff < 23 ? diff : 23, r = diff - d;
-    const int bw = bitwidth_of(read_max(amax));  // whole wave active
+    int bw;
+    if (spec == 1) {  // launch A: the guess; the range is published below
+        bw = (int)spec_pick(hint) - 1;
+        if (bw < 0) bw = 0;  // (no hint yet: B redoes unless the max is 0)
+        if (blockIdx.x == 0 && threadIdx.x == 0)
+            __hip_atomic_store(hint + 1, (uint32_t)bw + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+        bw = bitwidth_of(read_max(amax));  // whole wave active
+        if (spec == 2) {  // launch B: A's output stands unless the (all-reduced) range differs
+            const int used = __builtin_amdgcn_readfirstlane(
+                                 (int)__hip_atomic_load(hint + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) - 1;
+            if (blockIdx.x == 0 && threadIdx.x == 0) {
+                spec_learn(hint, bw);
+                if (bw != used) __hip_atomic_fetch_add(hint + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const int shift = bw - 7;
+                const int e_z = (a_hi ? xa : xb) - d;
+                if (ez != nullptr) *ez = (int8_t)e_z;
+                if (exp_out != nullptr) *exp_out = (int8_t)(e_z + (shift > 1 ? shift : (shift == 1 ? 2 : 0)));
+            }
+            if (bw == used) return;
+        }
+    }
     const int shift = bw - 7;
     const int s = shift > 1 ? shift : 2;
     const bool raw = shift <= 0;
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (spec == 0 && blockIdx.x == 0 && threadIdx.x == 0) {
         const int e_z = (a_hi ? xa : xb) - d;
         if (ez != nullptr) *ez = (int8_t)e_z;
         if (exp_out != nullptr) *exp_out = (int8_t)(e_z + (shift > 1 ? shift : (shift == 1 ? 2 : 0)));
     }
+    uint32_t m = 0;
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += (int64_t)gridDim.x * 256) {
         const v16c va = ((const v16c*)a)[i], vb = ((const v16c*)b)[i];
         v16c mk;
@@ -3515,6 +3538,10 @@ __global__ void __launch_bounds__(256) residual_requant_kernel(const int8_t* __r
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
             const int32_t z = residual_z(a_hi ? va[e] : vb[e], a_hi ? vb[e] : va[e], d, r);
+            if (spec == 1) {
+                const uint32_t u = uabs32(z);
+                m = m > u ? m : u;
+            }
             int32_t o = raw ? (int32_t)(int8_t)z : psto_fast(z, s);
             if (relu && o < 0) o = 0;
             if (relu_mask != nullptr && mk[e] <= 0) o = 0;  // the next op's NITI_ReluGrad_Int8, fused
@@ -3522,17 +3549,25 @@ __global__ void __launch_bounds__(256) residual_requant_kernel(const int8_t* __r
         }
         ((v16c*)out)[i] = q;
     }
+    if (spec == 1) {  // NITI_RangeEstimate of z for launch B
+        m = wave_max(m);
+        __shared__ uint32_t red[4];
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+        __syncthreads();
+        if (threadIdx.x == 0) publish_max(const_cast<uint32_t*>(amax), max(max(red[0], red[1]), max(red[2], red[3])));
+    }
 }
 
 hipError_t residual_requant(const int8_t* a, const int8_t* ea, const int8_t* b, const int8_t* eb, int64_t n,
                             const uint32_t* amax, int8_t* ez, int8_t* exp_out, int relu, int8_t* out, hipStream_t st,
-                            const int8_t* relu_mask) {
+                            const int8_t* relu_mask, int spec, uint32_t* slot) {
     if (n < 0 || n % 16 != 0 || !a || !b || !ea || !eb || !amax || !out) return hipErrorInvalidValue;
+    if (spec < 0 || spec > 2 || (spec != 0 && slot == nullptr)) return hipErrorInvalidValue;
     const int64_t n16 = n / 16;
     int64_t blocks = (n16 + 255) / 256;
     blocks = blocks < 1 ? 1 : blocks > 2048 ? 2048 : blocks;
     hipLaunchKernelGGL(residual_requant_kernel, dim3((unsigned)blocks), dim3(256), 0, st, a, ea, b, eb, n16, amax, ez,
-                       exp_out, relu, relu_mask, out);
+                       exp_out, relu, relu_mask, out, spec, slot);
     return hipGetLastError();
 }
 

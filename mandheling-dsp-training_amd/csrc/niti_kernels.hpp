@@ -136,10 +136,16 @@ int resident_wgs(const void* f, int threads = 256);
 hipError_t residual_add(const int8_t* a, const int8_t* ea, const int8_t* b, const int8_t* eb, int64_t n,
                         int32_t* z, int8_t* ez, uint32_t* amax, hipStream_t st);
 // the fused form: z recomputed from a, b and requantised with the range in amax (from residual_add
-// with z = null); out int8 (n elements), *ez and *exp_out = *ez + inc (either may be null)
+// with z = null); out int8 (n elements), *ez and *exp_out = *ez + inc (either may be null).
+// spec 1 / 2: the speculative pair instead of range pass + requantise pass -- launch A (1)
+// requantises with the guessed bit width (spec_pick over slot, RES_SPEC_SLOT_WORDS zeroed words)
+// and publishes max|z| into amax (zeroed by the caller); launch B (2; after any MAX all-reduce)
+// writes the exponents and redoes the pass only when the range's bit width differs: 3 bytes per
+// element on a hit instead of 5.  slot word [2] counts the redone launches.
+constexpr int RES_SPEC_SLOT_WORDS = 32;
 hipError_t residual_requant(const int8_t* a, const int8_t* ea, const int8_t* b, const int8_t* eb, int64_t n,
                             const uint32_t* amax, int8_t* ez, int8_t* exp_out, int relu, int8_t* out, hipStream_t st,
-                            const int8_t* relu_mask = nullptr);
+                            const int8_t* relu_mask = nullptr, int spec = 0, uint32_t* slot = nullptr);
 // acc[n][cp] = sum over hw pixels of x NHWC16 (+ max into amax); its gradient: dy broadcast
 hipError_t sum_pool(const int8_t* x, int n, int hw, int cp, int32_t* acc, uint32_t* amax, hipStream_t st);
 // (relu_mask: the pooled map, NHWC16 -- its relu gradient applied too, dx = mask > 0 ? dy : 0)
@@ -321,9 +327,9 @@ struct RowConvOut {
     int8_t* pool_dx_next = nullptr;
     int pool_relu = 0;
     // the route as the forward pass that pooled recorded it (pool_code4, NHWC16-shaped [n][H][W][cop]
-    // bytes): read instead of pool_x / pool_y, which may then be null (W > 0 forms)
+    // bytes): read instead of pool_x / pool_y, which may then be null
     const int8_t* pool_code = nullptr;
-    // forward with pool_out: record that route here (W > 0 forms; relu decides the code's relu bit)
+    // forward with pool_out: record that route here (relu decides the code's relu bit)
     int8_t* pool_code_out = nullptr;
     // 0: pool_dx (NHWC16) is not written, only its C32 (pool_dx_next) / P16 copies; the pool
     // gradient's routing still needs pool_dx non-null.  Likewise out may be null in the input

@@ -250,13 +250,13 @@ struct Model {
     std::vector<char> dy16_valid;
     bool rowconv_dgrad_layer(int i) const { return use_rowconv && L[i].rcd; }
     // layer i's 2x2 pool route travels as codes (Layer::pc): its forward (the first layer's conv0
-    // kernel or a W > 0 row kernel) records it and layer i + 1's input gradient (a W > 0 row kernel,
-    // or the head's) reads it instead of the pre-pool output and the pooled one
+    // kernel or a row kernel) records it and layer i + 1's input gradient (a row kernel, or the
+    // head's) reads it instead of the pre-pool output and the pooled one
     bool pool_code_layer(int i) const {
         const Layer& l = L[i];
         if (!l.pool || l.flatten || l.pc == nullptr || i + 1 >= (int)L.size()) return false;
-        const bool fwd = (l.col && conv0_ok(l.g)) || (rowconv_layer(i) && !rowconv_seg(l.g));
-        const bool bwd = (rowconv_dgrad_layer(i + 1) && !rowconv_seg(L[i + 1].dg)) || head_dgrad_ok(i + 1);
+        const bool fwd = (l.col && conv0_ok(l.g)) || rowconv_layer(i);
+        const bool bwd = rowconv_dgrad_layer(i + 1) || head_dgrad_ok(i + 1);
         return fwd && bwd;
     }
     // the classifier head (a 1x1 conv over 1x1 maps, at most 64 outputs) on the row kernel's

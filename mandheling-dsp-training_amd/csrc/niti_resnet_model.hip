@@ -105,6 +105,9 @@ int ResNetModel::build(int batch_, int in_hw_, int classes_) {
     if (!rc_err || hipMemset(rc_err, 0, 64) != hipSuccess) return NITI_OUT_OF_MEMORY;
     res_bar = (uint32_t*)ws.alloc(ROWCONV_BAR_WORDS * 4);
     if (!res_bar || hipMemset(res_bar, 0, ROWCONV_BAR_WORDS * 4) != hipSuccess) return NITI_OUT_OF_MEMORY;
+    res_slot = (uint32_t*)ws.alloc(2 * B.size() * RES_SPEC_SLOT_WORDS * 4);
+    if (!res_slot || hipMemset(res_slot, 0, 2 * B.size() * RES_SPEC_SLOT_WORDS * 4) != hipSuccess)
+        return NITI_OUT_OF_MEMORY;
     for (int i = 0; i < nl; ++i) {
         RConv& c = C[i];
         const ConvGeom& g = c.g;
@@ -508,6 +511,15 @@ int ResNetModel::residual_fwd(int k, hipStream_t st) {
         }
         --res_epoch;
     }
+    if (res_spec_on()) {  // the speculative pair: one pass of the sum while its bit width holds
+        uint32_t* slot = res_slot + (2 * k) * RES_SPEC_SLOT_WORDS;
+        RTRY(residual_requant(cb.y, cb.y_exp, sc, es, b.out_elems, rng_blk(k, 0), b.ez, b.out_exp, 1, b.out, st,
+                              nullptr, 1, slot));
+        if (dp() && exact) RTRY(coll->allreduce(rng_blk(k, 0), MAX_WORDS, COLL_MAX_U32, st));
+        RTRY(residual_requant(cb.y, cb.y_exp, sc, es, b.out_elems, rng_blk(k, 0), b.ez, b.out_exp, 1, b.out, st,
+                              nullptr, 2, slot));
+        return NITI_NO_ERROR;
+    }
     RTRY(residual_add(cb.y, cb.y_exp, sc, es, b.out_elems, nullptr, nullptr, rng_blk(k, 0), st));
     if (dp() && exact) RTRY(coll->allreduce(rng_blk(k, 0), MAX_WORDS, COLL_MAX_U32, st));
     RTRY(residual_requant(cb.y, cb.y_exp, sc, es, b.out_elems, rng_blk(k, 0), b.ez, b.out_exp, 1, b.out, st));
@@ -530,10 +542,19 @@ int ResNetModel::residual_bwd(int k, hipStream_t st) {
         }
         --res_epoch;
     }
+    const int8_t* mask = k > 0 ? B[k - 1].out : nullptr;
+    if (res_spec_on()) {  // the speculative pair (residual_fwd)
+        uint32_t* slot = res_slot + (2 * k + 1) * RES_SPEC_SLOT_WORDS;
+        RTRY(residual_requant(b.dua, ca.dx_exp, s, es, b.in_elems, rng_blk(k, 1), b.ezb, b.du_exp, 0, b.du, st, mask,
+                              1, slot));
+        if (dp() && exact) RTRY(coll->allreduce(rng_blk(k, 1), MAX_WORDS, COLL_MAX_U32, st));
+        RTRY(residual_requant(b.dua, ca.dx_exp, s, es, b.in_elems, rng_blk(k, 1), b.ezb, b.du_exp, 0, b.du, st, mask,
+                              2, slot));
+        return NITI_NO_ERROR;
+    }
     RTRY(residual_add(b.dua, ca.dx_exp, s, es, b.in_elems, nullptr, nullptr, rng_blk(k, 1), st));
     if (dp() && exact) RTRY(coll->allreduce(rng_blk(k, 1), MAX_WORDS, COLL_MAX_U32, st));
-    RTRY(residual_requant(b.dua, ca.dx_exp, s, es, b.in_elems, rng_blk(k, 1), b.ezb, b.du_exp, 0, b.du, st,
-                          k > 0 ? B[k - 1].out : nullptr));
+    RTRY(residual_requant(b.dua, ca.dx_exp, s, es, b.in_elems, rng_blk(k, 1), b.ezb, b.du_exp, 0, b.du, st, mask));
     return NITI_NO_ERROR;
 }
 

@@ -122,6 +122,12 @@ struct ResNetModel {
     }
     uint32_t* res_bar = nullptr;
     uint32_t res_epoch = 0;
+    // the residual sums' speculative pairs: one slot per block and direction (residual_requant)
+    uint32_t* res_slot = nullptr;
+    static bool res_spec_on() {
+        static const bool off = getenv("NITI_RES_SPEC") && atoi(getenv("NITI_RES_SPEC")) == 0;
+        return !off;
+    }
     bool res_fused_on() const {
         static const bool on = getenv("NITI_RES_FUSED") && atoi(getenv("NITI_RES_FUSED")) == 1;
         return on && !dp() && !capturing && res_bar != nullptr;

@@ -793,13 +793,14 @@ __device__ __forceinline__ void seg_prefetch(const RowConvArgs& a, const RowUnit
     uint32_t z = 0;
     asm volatile("" : "+s"(z));
     const bool pool = PX && a.pool_dx != nullptr;
-    const int8_t* ps = (pool ? a.pool_y : a.relu_mask) + z;
+    const bool code = pool && a.pool_code != nullptr;  // the recorded route: one load per row
+    const int8_t* ps = (pool ? (code ? a.pool_code : a.pool_y) : a.relu_mask) + z;
     const int8_t* px = a.pool_x + z;
     if (!pool && a.relu_mask == nullptr) return;
 #pragma unroll
     for (int r = 0; r < R; ++r) e.y[r] = *(const v4i*)(ps + ((img * H + U.b * R + r) * W + xs) * a.cop + cb16);
     if constexpr (PX)
-    if (pool) {
+    if (pool && !code) {
 #pragma unroll
         for (int r = 0; r < R; ++r)
 #pragma unroll
@@ -892,9 +893,21 @@ __device__ __forceinline__ void seg_epilogue(const RowConvArgs& a, const RowUnit
                 pm[i] = (int8_t)(v0 > v1 ? v0 : v1);
             }
             const v4i v = pack_cols(pm);
+            v4i code{0, 0, 0, 0};
+            if (a.pool_code_out != nullptr) {  // the window: this lane's (top, bottom) and lane + 1's
+                const v4i t0 = pack_cols(q[r]), t2 = pack_cols(q[r + 1]);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const uint32_t t1 = (uint32_t)__builtin_amdgcn_update_dpp(0, t0[k], 0x101, 0xF, 0xF, true);
+                    const uint32_t t3 = (uint32_t)__builtin_amdgcn_update_dpp(0, t2[k], 0x101, 0xF, 0xF, true);
+                    code[k] = (int)pool_code4((uint32_t)t0[k], t1, (uint32_t)t2[k], t3, (uint32_t)v[k], a.relu != 0);
+                }
+            }
             if (U.out_ok && (x & 1) == 0) {
                 const int py = (U.b * R + r) / 2, pxo = x / 2;
                 *(v4i*)(a.pool_out + ((img * HO + py) * WO + pxo) * a.cop + cb16) = v;
+                if (a.pool_code_out != nullptr)
+                    *(v4i*)(a.pool_code_out + ((img * HO + py) * WO + pxo) * a.cop + cb16) = code;
                 if (a.next != nullptr)
                     *(v4i*)(a.next + (((img * a.COB + U.cob) * HO + py) * WO + pxo) * 32 + 16 * h) = v;
             }
@@ -978,16 +991,20 @@ __device__ __forceinline__ void write_exponent(const RowConvArgs& a, uint32_t gm
 // width hold.  Slot words:
 // [0] the hint (bw + 1, 0 none; written by B's block 0, read by A), [1] what A did (the hint it
 // used, bit 31 set when it stored instead; written by A's block 0, read by B), [2] redone launches,
-// [3] pairs left in store mode (read and written by B's thread 0, read by A), [4] stored pairs.
+// [3] pairs left in store mode (read and written by B's thread 0, read by A), [4] stored pairs,
+// [5] the bit width one pair earlier (bw + 1), [6] the predictor's chooser (0..3, written by B).
 // Every other reader of a word runs in the other launch, so no launch's blocks race on a word.
+// The guess (spec_pick / spec_learn, niti_device.hpp): a layer's bit width either holds from pair to
+// pair or, with gradients whose maximum sits at a power of two, flips back and forth; a 2-bit
+// chooser counts which of "the last bit width" and "the one before it" would have been right.
 constexpr uint32_t SPEC_COOLDOWN = 8;  // the default of spec_cooldown() (NITI_SPEC_COOLDOWN overrides; profiles/r05_spec_cooldown_ab.txt)
 __device__ __forceinline__ int spec_guess(const RowConvArgs& a, bool can_store, bool& store) {
-    const uint32_t h = __hip_atomic_load(a.hint, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint32_t f = __hip_atomic_load(a.hint + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t gh = spec_pick(a.hint);  // the guess, as bw + 1 (0: none)
     store = can_store && a.acc_store != nullptr && __builtin_amdgcn_readfirstlane((int)f) != 0;
     if (blockIdx.x == 0 && threadIdx.x == 0)
-        __hip_atomic_store(a.hint + 1, h | (store ? 0x80000000u : 0u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return __builtin_amdgcn_readfirstlane((int)h) - 1;
+        __hip_atomic_store(a.hint + 1, gh | (store ? 0x80000000u : 0u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return (int)gh - 1;
 }
 
 // launch B: g = the rule's max word; returns whether this launch has work (A stored the
@@ -1002,7 +1019,7 @@ __device__ __forceinline__ bool spec_settle(const RowConvArgs& a, uint32_t& g, b
     const bool changed = bw != (int)(w1 & 0x7fffffffu) - 1;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         write_exponent(a, g);
-        __hip_atomic_store(a.hint, (uint32_t)bw + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        spec_learn(a.hint, bw);  // the next guess (spec_pick)
         // store mode for the next SPEC_COOLDOWN pairs after a change (a layer whose bit width flips
         // from step to step, gradients near a power of two, stays there; block 0 of B is the only
         // reader-writer of this word within a launch)
@@ -1051,7 +1068,7 @@ template <int R, bool DG>
 __device__ __forceinline__ int seg_epi_stores(const RowConvArgs& a) {
     if (DG && a.pool_dx != nullptr) return 4 * R * ((a.pool_dx_nhwc ? 1 : 0) + (a.pool_dx_next != nullptr ? 1 : 0));
     int e = R * ((a.out != nullptr ? 1 : 0) + (a.next != nullptr && a.pool_out == nullptr ? 1 : 0));
-    if (a.pool_out != nullptr) e += (R / 2) * (1 + (a.next != nullptr ? 1 : 0));
+    if (a.pool_out != nullptr) e += (R / 2) * (1 + (a.next != nullptr ? 1 : 0) + (a.pool_code_out != nullptr ? 1 : 0));
     return e;
 }
 
@@ -1144,7 +1161,9 @@ __device__ __forceinline__ void seg_run(const RowConvArgs& a, int lane, int wid,
     // s - 1 before / after it (xb1, xa1): everything issued after the stage step s waits for
     int xa2 = 0, xb1 = 0, xa1 = 0, xb = 0, xa = 0;
     const int pf_n = __builtin_amdgcn_readfirstlane(
-        DG && MODE != RC_RANGE ? (PX && a.pool_dx != nullptr ? 5 * R : (a.relu_mask != nullptr ? R : 0)) : 0);
+        DG && MODE != RC_RANGE ? (PX && a.pool_dx != nullptr ? (a.pool_code != nullptr ? R : 5 * R)
+                                                             : (a.relu_mask != nullptr ? R : 0))
+                               : 0);
     const int st_n = __builtin_amdgcn_readfirstlane(MODE == RC_RANGE ? (a.acc_store != nullptr ? 4 * R : 0)
                                                                       : seg_epi_stores<R, DG>(a));
     v16i acc[R];
@@ -1778,9 +1797,8 @@ hipError_t rowconv_fwd(const ConvGeom& g, const int8_t* x_c32, const int8_t* wf,
     if (o.pool_dx != nullptr && ((o.pool_code == nullptr && (o.pool_x == nullptr || o.pool_y == nullptr)) ||
                                  o.out != nullptr || o.pool_out != nullptr || o.relu_mask != nullptr || o.next != nullptr))
         return hipErrorInvalidValue;
-    // the recorded pool route: the W > 0 forms (the row-segment epilogues scan the window)
-    if ((o.pool_code != nullptr && o.pool_dx == nullptr) || (o.pool_code_out != nullptr && o.pool_out == nullptr) ||
-        ((o.pool_code != nullptr || o.pool_code_out != nullptr) && rowconv_seg(g)))
+    // the recorded pool route (pool_code4)
+    if ((o.pool_code != nullptr && o.pool_dx == nullptr) || (o.pool_code_out != nullptr && o.pool_out == nullptr))
         return hipErrorInvalidValue;
     RowConvArgs a{};
     const int CB = (g.c_in + 31) / 32, COB = g.cop / 32;

@@ -120,11 +120,17 @@ def test_vgg16_224_tuned_plans_step_matches_oracle(T, plans):
     import niti_amd
     from niti_amd import _lib as L
     import niti_model_ref as R
+    from niti_amd._lib import NitiError
     from niti_amd.model import NitiModel
     layers = R.vgg16_layers(224)
     W, S = R.init_weights(layers, seed=31)
     rng = np.random.default_rng(31)
     m = NitiModel(niti_amd.ARCH_VGG16, 2)
+    # the bench's plans also with the bench's keep_grads(False): no int8 weight-gradient copies, and
+    # the pooled layers' 2x2 routes go to the next input gradient as codes (the row-segment kernels'
+    # epilogues record them), their pre-pool outputs unwritten
+    keep = plans != "bench"
+    m.keep_grads(keep)
     try:
         for i, (w, s) in enumerate(zip(W, S)):
             m.set_weight(i, w, s)
@@ -155,9 +161,15 @@ def test_vgg16_224_tuned_plans_step_matches_oracle(T, plans):
             logits, e = m.logits()
             assert e == rec["exp"][-1] and np.array_equal(logits, rec["logits"]), step
             for i in range(len(layers)):
-                assert np.array_equal(m.tap(i, 0), rec["r"][i]), ("fwd", step, i)
+                try:
+                    fwd = m.tap(i, 0)
+                except NitiError:  # (keep_grads(False): a pooled layer whose route went as codes)
+                    assert not keep and layers[i]["pool"], ("fwd tap", step, i)
+                    fwd = rec["r"][i]
+                assert np.array_equal(fwd, rec["r"][i]), ("fwd", step, i)
                 assert np.array_equal(m.tap(i, 2), rec["dy"][i]), ("dy", step, i)
-                assert np.array_equal(m.tap(i, 1), rec["dw"][i]), ("dw", step, i)
+                if keep:
+                    assert np.array_equal(m.tap(i, 1), rec["dw"][i]), ("dw", step, i)
                 assert np.array_equal(m.get_weight(i), newW[i]), ("w", step, i)
             W = newW
         assert m.rowconv_error() == 0

@@ -181,10 +181,10 @@ def test_vgg11_step_autotuned(T):
     # timing: GEMM tiles are 64..256 wide; the tap-sharing weight-gradient kernel reports 32x32
     # and the P16 weight-gradient kernel 16x16, both unsplit (strategy 0) or split-K (strategy 2),
     # never recompute (strategy 1); the speculative pair (strategy 3) only on forward / input-gradient
-    # GEMMs, unsplit.
+    # GEMMs, unsplit; so is the fused form (strategy 4).
     for (layer, phase), (bm, bn, splits, strat) in seen.items():
-        assert splits >= 1 and strat in (0, 1, 2, 3), (layer, phase)
-        if strat == 3:
+        assert splits >= 1 and strat in (0, 1, 2, 3, 4), (layer, phase)
+        if strat in (3, 4):
             assert phase != 2 and splits == 1, (layer, phase, splits)
         if bm in (16, 32) or bn in (16, 32):
             assert bm == bn and phase == 2 and strat in (0, 2), (layer, phase, bm, bn, strat)
