@@ -326,6 +326,13 @@ void niti_diag_gemm_speculate(int bias);
 /* diagnostics: implicit-GEMM launches of this process that ran with the rescale fused behind the
  * in-kernel grid barrier (plan strategy 4) */
 unsigned long long niti_diag_gemm_fused_launches(void);
+/* diagnostics: launches of the classifier head's one-launch chain (forward, loss gradient, weight and
+ * input gradient) in this process */
+unsigned long long niti_diag_head_chain_launches(void);
+/* diagnostics: VGG-11's classifier head as one launch (forward, loss gradient, weight gradient, input
+ * gradient through the pool routes; niti_head.hip) instead of four; 0 (default, measured slower) off.
+ * Also NITI_HEAD_CHAIN=1.  Results identical either way. */
+void niti_diag_head_chain(int on);
 /* jobs per P16 input-copy launch of a model step for later steps (<= 0: the default 16); a small
  * cap sends a step down its more-than-one-launch branches.  Results are identical for every cap. */
 void niti_diag_p16_jobs_cap(int cap);

@@ -468,6 +468,8 @@ void niti_diag_rowconv_barrier(uint32_t spin_limit, uint32_t expect_extra) {
 void niti_diag_rowconv_speculate(int mode) { niti::rowconv_speculate(mode); }
 void niti_diag_gemm_speculate(int bias) { niti::gemm_speculate_bias(bias); }
 unsigned long long niti_diag_gemm_fused_launches(void) { return niti::gemm_fused_launches(); }
+unsigned long long niti_diag_head_chain_launches(void) { return niti::head_chain_launches(); }
+void niti_diag_head_chain(int on) { niti::head_chain_enable(on); }
 void niti_diag_p16_jobs_cap(int cap) { niti::model_p16_jobs_cap(cap); }
 
 int niti_conv_wgrad_p16_workspace(const niti_geom* g, int splits, size_t* bytes) {

@@ -3649,7 +3649,17 @@ __global__ void __launch_bounds__(256) conv0_kernel(Conv0 g) {
                 for (int r = 0; r < 2; ++r)
 #pragma unroll
                     for (int i = 0; i < 16; ++i) {
-                        int32_t v = raw ? (int32_t)(int8_t)acc[r][i] : psto_fast(acc[r][i], s);
+                        int32_t v;
+                        if (raw) {
+                            v = (int32_t)(int8_t)acc[r][i];
+                        } else if (g.relu) {  // PSTO of max(acc, 0): a negative value is 0 whatever its rounding
+                            const uint32_t x = (uint32_t)max(acc[r][i], 0);
+                            const uint32_t qp = __builtin_amdgcn_ubfe(x, s >> 1, s - (s >> 1));
+                            const uint32_t pr = __builtin_amdgcn_ubfe(x, 0, s >> 1) << (s & 1);
+                            v = (int32_t)min((x >> s) + (qp > pr ? 1u : 0u), 127u);
+                        } else {
+                            v = psto_fast(acc[r][i], s);
+                        }
                         if (g.relu && v < 0) v = 0;
                         q[r][i] = (int8_t)v;
                     }
@@ -4572,56 +4582,6 @@ hipError_t relu_grad_nhwc16(const int8_t* x, const int8_t* dy, int64_t n, int8_t
     return hipGetLastError();
 }
 
-__device__ __forceinline__ int64_t ipow2_64(int64_t t) { return (int64_t)pow2_x86((int)(t & 31)); }
-
-// NITI_CPULossGrad_Int8.cpp:81-200 for rows of at most 16 classes: a 16-lane group per sample,
-// one lane per class, the row's max and sums reduced across the group (int64, exact).  (The
-// first form ran a thread per sample with the class row in registers: 16 sequential 64-bit
-// divisions per thread on 4 waves, 12 us for batch 256.)
-constexpr int LOSS_MAXC = 16;
-__device__ __forceinline__ int64_t group16_reduce(int64_t v, bool is_max) {
-#pragma unroll
-    for (int o = 1; o < 16; o <<= 1) {
-        const int64_t w = __shfl_xor(v, o, 16);
-        v = is_max ? (v > w ? v : w) : v + w;
-    }
-    return v;
-}
-__device__ __forceinline__ void loss_rows16(const int8_t* __restrict__ logits, int batch, int classes, int ld,
-                                            const int8_t* __restrict__ ascale_p, const int32_t* __restrict__ labels,
-                                            int8_t* __restrict__ out, int t) {
-    const int i = t >> 4, j = t & 15;
-    const bool row = i < batch;  // whole groups stay in the shuffles
-    const bool cls = row && j < classes;
-    const int as = (int)*ascale_p;
-    const int8_t* L = logits + (int64_t)(row ? i : 0) * ld;
-    int64_t o = 0;
-    if (as > -7) {
-        int64_t sv = INT64_MIN;
-        if (cls) {
-            int64_t v = (int64_t)L[j] * 47274;
-            v = v / (1 << 15);
-            sv = as >= 0 ? v * ipow2_64(as) : v / ipow2_64(-as);
-        }
-        const int64_t mx = group16_reduce(sv, true) - 10;
-        int64_t d = cls ? sv - mx : 0;
-        d = d > 0 ? d : 0;
-        o = cls ? ipow2_64(d) - 1 : 0;
-    } else {
-        const int64_t base = ipow2_64(1 - 2 * (int64_t)as);
-        const int64_t sb = ipow2_64(1 - (int64_t)as);
-        const int64_t v = cls ? L[j] : 0;
-        o = cls ? base + v * sb + v * v : 0;
-    }
-    const int64_t sum = group16_reduce(o, false);
-    o = cls ? (o * (1 << 11)) / sum : 0;
-    const int64_t gs = group16_reduce(o, false);
-    if (!row) return;
-    const int32_t gf = (int32_t)(j == labels[i] ? o - gs : o);
-    int8_t* O = out + (int64_t)i * ld;
-    if (j < ld) O[j] = cls ? (int8_t)psto_any(gf, 4) : (int8_t)0;
-    for (int jj = j + 16; jj < ld; jj += 16) O[jj] = 0;
-}
 __global__ void __launch_bounds__(256) loss_grad_kernel(const int8_t* __restrict__ logits, int batch, int classes,
                                                         int ld, const int8_t* __restrict__ ascale_p,
                                                         const int32_t* __restrict__ labels, int8_t* __restrict__ out) {

@@ -397,6 +397,37 @@ hipError_t rowconv_fwd(const ConvGeom& g, const int8_t* x_c32, const int8_t* wf,
 // A 1x1 layer over 1x1 maps (the classifier head) on the same kernel: rows output channels of
 // Σ_k x[n][k] w[row][k] (x [n][xld], w [rows][wld], row-major), with the same epilogues (the
 // pool-gradient one routes into 2x2 windows: the head's input is a 1x1 pooled map)
+// The classifier head's step chain in one launch (niti_head.hip): forward with the rescale, the loss
+// gradient, the int32 weight gradient (+ range) and the input gradient routed through the previous
+// layer's 2x2 max pool by its recorded codes; no grid barrier (every head workgroup recomputes the
+// tiny forward and the input gradient's range).  n % 4 == 0, n <= 512,
+// K % 32 == 0, c_out <= 16, cop == 16.
+struct HeadChain {
+    const int8_t* x = nullptr;  // [n][xld] the head's input (the previous layer's pooled output)
+    int xld = 0;
+    const int8_t* w = nullptr;   // [c_out][K] (OHWI16 of the 1x1 head)
+    const int8_t* wT = nullptr;  // [K][cop] (IHWO16)
+    int n = 0, K = 0, c_out = 0, cop = 0, relu = 0;
+    const int8_t* exp_in = nullptr;
+    const int8_t* wscale = nullptr;
+    int8_t* exp_out = nullptr;
+    int8_t* logits = nullptr;  // [n][cop]
+    const int32_t* labels = nullptr;
+    int8_t* dy = nullptr;  // [n][cop]
+    int32_t* dw = nullptr;  // [c_out][K]
+    uint32_t* dw_amax = nullptr;
+    const int8_t* code = nullptr;   // [n][K] the previous layer's pool routes (pool_code4)
+    int8_t* pool_dx = nullptr;      // [n][2][2][K] NHWC16, or null
+    int8_t* pool_dx_c32 = nullptr;  // [n][K/32][2][2][32], or null
+    int8_t* p16 = nullptr;          // [4n/16][K][16], or null
+    int G = 0;                      // (set by head_chain: K / 32 head workgroups)
+    int stamps = 0;                 // (diagnostics)
+};
+bool head_chain_ok(int n, int K, int c_out, int cop);
+hipError_t head_chain(const HeadChain& h, hipStream_t st);
+unsigned long long head_chain_launches();  // (diagnostics)
+bool head_chain_enabled();  // NITI_HEAD_CHAIN=1 / niti_diag_head_chain(1); off by default
+void head_chain_enable(int on);
 bool rowconv_fc_ok(int n, int K, int rows, bool fused);
 // its weight gradient: dw [c_out][cip] int32 = Σ_p dy[p][co] x[p][ci] (c_out <= 32, cip % 32 == 0),
 // max|dw| published into amax (may be null)

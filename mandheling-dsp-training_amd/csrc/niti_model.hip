@@ -505,6 +505,16 @@ struct Model {
     // the input gradient of layer i need not write L[i - 1].dy in NHWC16: its weight gradient reads
     // the P16 copy (p16) and its input gradient the C32 copy (next) this same launch writes (layer 0's
     // GEMM weight gradient reads NHWC16).  NITI_DY16=1 keeps the copy (A/B diagnostics).
+    // the classifier head's whole chain (forward, loss gradient, weight and input gradient into the
+    // previous layer's pool routes) as one launch (niti_head.hip): single device, the head on the
+    // row kernel's W = 1 path after a pooled layer whose routes travel as codes (VGG-11)
+    bool head_chain_on() const {
+        const int h = (int)L.size() - 1;
+        if (!head_chain_enabled() || h < 1 || dp() || tuning || probe_layer == h) return false;
+        const Layer& l = L[h];
+        return head_layer(h) && head_dgrad_ok(h) && L[h - 1].pool && pool_code_layer(h - 1) &&
+               head_chain_ok(batch, l.g.cip, l.g.c_out, l.g.cop) && L[h - 1].g.cop == l.g.cip && l.g.kh * l.g.kw == 1;
+    }
     bool skip_dy16(int i, const int8_t* next, const int8_t* p16) const {
         static const bool keep = getenv("NITI_DY16") != nullptr && getenv("NITI_DY16")[0] == '1';
         return !keep && i - 1 >= 1 && next != nullptr && p16 != nullptr && wgrad_p16_splits(i - 1) > 0;
@@ -1490,7 +1500,8 @@ int Model::run(const int8_t* x_nchw, int exp_in, const uint8_t* images, const in
             MTRY(image_quantize(images, n, in_c, in_h * in_w, round_up(in_c, 16), qstats, count, x0, exp0, true, st));
     }
     if (L[0].col && !fused_in) MTRY(im2col32(L[0].og, x0, L[0].xcol, st));
-    for (int i = 0; i < nl; ++i) {
+    const bool hc = head_chain_on();  // (then the head's forward runs in the chain launch below)
+    for (int i = 0; i < nl - (hc ? 1 : 0); ++i) {
         const int rc = fwd_layer(i, st);
         if (rc != NITI_NO_ERROR) return rc;
     }
@@ -1501,7 +1512,49 @@ int Model::run(const int8_t* x_nchw, int exp_in, const uint8_t* images, const in
         Layer& t = L[nl - 1];
         P16Conv jobs[P16_MAX_JOBS];
         int nj = 0;
-        if (!ov && p16_input_jobs(jobs, &nj) && nj > 0) {
+        if (hc) {
+            // the head's forward, loss gradient, weight gradient and input gradient (through the
+            // last pool's recorded routes, + its C32 / P16 copies) in one launch; then, on one
+            // stream, every P16 input copy in one more
+            const bool with_jobs = !ov && p16_input_jobs(jobs, &nj);
+            if (!with_jobs) nj = 0;
+            Layer& pv = L[nl - 2];
+            HeadChain h;
+            h.x = t.in;
+            h.xld = t.g.cip;
+            h.w = t.w;
+            h.wT = t.wT;
+            h.n = n;
+            h.K = t.g.cip;
+            h.c_out = t.g.c_out;
+            h.cop = t.g.cop;
+            h.relu = t.relu;
+            h.exp_in = pv.exp;
+            h.wscale = t.ws_dev;
+            h.exp_out = t.exp;
+            h.logits = t.r;
+            h.labels = labels;
+            h.dy = t.dy;
+            h.dw = t.dwacc;
+            h.dw_amax = rng(nl - 1, 2);
+            h.code = pv.pc;
+            int8_t* next = rowconv_dgrad_layer(nl - 2) && !rowconv_nhwc_pref(pv.dg) ? pv.dyc32 : nullptr;
+            h.p16 = fuse_dp16 && wgrad_p16_splits(nl - 2) > 0 ? dp16[nl - 2] : nullptr;
+            h.pool_dx = skip_dy16(nl - 1, next, h.p16) ? nullptr : pv.dy;
+            h.pool_dx_c32 = next;
+            MTRY(head_chain(h, st));
+            if (with_jobs && nj > 0) {  // (a launch of its own: see niti_head.hip)
+                MTRY(nhwc16_to_p16_many(jobs, nj, st));
+                for (int j = 0; j < nl; ++j)
+                    if (wgrad_p16_splits(j)) xp16_valid[j] = 1;
+                p16_done = true;
+            }
+            t.r_written = true;
+            dy16_valid[nl - 1] = 1;
+            dy16_valid[nl - 2] = h.pool_dx != nullptr;
+            dp16_valid[nl - 2] = h.p16 != nullptr ? 1 : 0;
+            dyc32_valid[nl - 2] = next != nullptr ? 1 : 0;
+        } else if (!ov && p16_input_jobs(jobs, &nj) && nj > 0) {
             // one stream: the loss gradient and every P16 input copy in one launch (the copies read
             // forward activations only); A/B on one box, 8 alternating 200-step runs: median step
             // 0.395 vs 0.400 ms (profiles/r03_lossp16_ab.txt)
@@ -1532,10 +1585,11 @@ int Model::run(const int8_t* x_nchw, int exp_in, const uint8_t* images, const in
         }
         Layer& l = L[i];
         const ConvGeom& g = l.g;
-        int rc = wgrad_layer(i, wst);
+        const bool in_chain = hc && i == nl - 1;  // (the head chain launch did both)
+        int rc = in_chain ? NITI_NO_ERROR : wgrad_layer(i, wst);
         // data parallel: a completed gradient bucket goes to the comm stream right away
         if (rc == NITI_NO_ERROR && dp && closes_bucket[i]) rc = sum_bucket(i, wst);
-        if (rc == NITI_NO_ERROR && i > 0) rc = dgrad_layer(i, st);
+        if (rc == NITI_NO_ERROR && i > 0 && !in_chain) rc = dgrad_layer(i, st);
         if (rc != NITI_NO_ERROR) return rc;
         // NITI_SGD (NITI_SGD.hpp:20-54) for this layer is deferred: every layer's update runs in one
         // launch after the backward pass (the input gradients above read the old weights); the IHWO16

@@ -137,4 +137,136 @@ __device__ __forceinline__ void sgd_tile(const SgdJob& J, int bw, int ci0, int c
     sgd_tile_finish(J, bw, ci0, co0, k, in, T);
 }
 
+// NITI_LOSS_Grad rows (niti_kernels.hip loss_grad*, niti_head.hip): see loss_grad in niti_kernels.hpp
+__device__ __forceinline__ int64_t ipow2_64(int64_t t) { return (int64_t)pow2_x86((int)(t & 31)); }
+// v / ipow2_64(k) (C division, truncation toward zero) by shifts: the divisor is 2^(k & 31) as an
+// int32, so -2^31 when k & 31 == 31 (no 64-bit division)
+__device__ __forceinline__ int64_t div_pow2_x86(int64_t v, int64_t k) {
+    const int e = (int)(k & 31);
+    const int64_t q = v >= 0 ? (v >> e) : -((-v) >> e);
+    return e == 31 ? -q : q;
+}
+
+// NITI_CPULossGrad_Int8.cpp:81-200 for rows of at most 16 classes: a 16-lane group per sample,
+// one lane per class, the row's max and sums reduced across the group (int64, exact).  (The
+// first form ran a thread per sample with the class row in registers: 16 sequential 64-bit
+// divisions per thread on 4 waves, 12 us for batch 256.)
+constexpr int LOSS_MAXC = 16;
+// max / sum over each 16-lane group, every lane receiving it, with DPP moves (no LDS round trips):
+// lane ^ 1 and lane ^ 2 inside each quad, then rotations of the 16-lane row by 4 and 8
+template <int CTRL>
+__device__ __forceinline__ int64_t dpp64(int64_t v) {
+    const int lo = __builtin_amdgcn_mov_dpp((int)(uint32_t)v, CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(uint32_t)((uint64_t)v >> 32), CTRL, 0xF, 0xF, false);
+    return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+__device__ __forceinline__ int64_t group16_reduce(int64_t v, bool is_max) {
+    auto op = [&](int64_t w) { v = is_max ? (v > w ? v : w) : v + w; };
+    op(dpp64<0xB1>(v));   // quad_perm [1,0,3,2]
+    op(dpp64<0x4E>(v));   // quad_perm [2,3,0,1]
+    op(dpp64<0x124>(v));  // row_ror:4
+    op(dpp64<0x128>(v));  // row_ror:8
+    return v;
+}
+// a / b with C semantics (truncation toward zero) for |a|, |b| < 2^52, b != 0: the correctly rounded
+// double quotient is within one of the integer one; the remainder's sign and size fix it (no 64-bit
+// integer division)
+__device__ __forceinline__ int64_t div_trunc52(int64_t a, int64_t b) {
+    int64_t q = (int64_t)__builtin_trunc((double)a / (double)b);
+    const int64_t r = a - q * b;
+    const bool same = (a >= 0) == (b > 0);
+    if (r != 0 && (r > 0) != (a > 0))
+        q += same ? -1 : 1;
+    else if ((r >= 0 ? r : -r) >= (b >= 0 ? b : -b))
+        q += same ? 1 : -1;
+    return q;
+}
+__device__ __forceinline__ void loss_rows16(const int8_t* __restrict__ logits, int batch, int classes, int ld,
+                                            const int8_t* __restrict__ ascale_p, const int32_t* __restrict__ labels,
+                                            int8_t* __restrict__ out, int t) {
+    const int i = t >> 4, j = t & 15;
+    const bool row = i < batch;  // whole groups stay in the shuffles
+    const bool cls = row && j < classes;
+    const int as = (int)*ascale_p;
+    const int8_t* L = logits + (int64_t)(row ? i : 0) * ld;
+    int64_t o = 0;
+    if (as > -7) {
+        int64_t sv = INT64_MIN;
+        if (cls) {
+            int64_t v = (int64_t)L[j] * 47274;
+            v = v / (1 << 15);
+            sv = as >= 0 ? v * ipow2_64(as) : div_pow2_x86(v, -as);
+        }
+        const int64_t mx = group16_reduce(sv, true) - 10;
+        int64_t d = cls ? sv - mx : 0;
+        d = d > 0 ? d : 0;
+        o = cls ? ipow2_64(d) - 1 : 0;
+    } else {
+        const int64_t base = ipow2_64(1 - 2 * (int64_t)as);
+        const int64_t sb = ipow2_64(1 - (int64_t)as);
+        const int64_t v = cls ? L[j] : 0;
+        o = cls ? base + v * sb + v * v : 0;
+    }
+    const int64_t sum = group16_reduce(o, false);
+    // |o| < 2^39 and |sum| < 2^43 (o = 2^d - 1 with d <= 31, or base + v sb + v^2 with base, sb <=
+    // 2^31 and |v| <= 128), so o * 2^11 and sum stay inside div_trunc52's range
+    o = cls ? (sum != 0 ? div_trunc52(o * (1 << 11), sum) : 0) : 0;
+    const int64_t gs = group16_reduce(o, false);
+    if (!row) return;
+    const int32_t gf = (int32_t)(j == labels[i] ? o - gs : o);
+    int8_t* O = out + (int64_t)i * ld;
+    if (j < ld) O[j] = cls ? (int8_t)psto_any(gf, 4) : (int8_t)0;
+    for (int jj = j + 16; jj < ld; jj += 16) O[jj] = 0;
+}
+// The same row with one thread per sample (the head chain: one workgroup takes every row, so a
+// 16-lane group per row would take n / 16 dependent passes): the classes in a loop, the one division
+// per class on the double path (div_trunc52).  Identical results to loss_rows16.
+__device__ __forceinline__ void loss_row_serial(const int8_t* __restrict__ L, int classes, int as, int label,
+                                                int8_t* __restrict__ out, int ld) {
+    int64_t o[LOSS_MAXC];
+    if (as > -7) {
+        int64_t sv[LOSS_MAXC];
+        int64_t mx = INT64_MIN;
+#pragma unroll
+        for (int j = 0; j < LOSS_MAXC; ++j) {
+            sv[j] = INT64_MIN;
+            if (j < classes) {
+                int64_t v = (int64_t)L[j] * 47274;
+                v = v / (1 << 15);
+                sv[j] = as >= 0 ? v * ipow2_64(as) : div_pow2_x86(v, -as);
+                mx = mx > sv[j] ? mx : sv[j];
+            }
+        }
+        mx -= 10;
+#pragma unroll
+        for (int j = 0; j < LOSS_MAXC; ++j) {
+            int64_t d = j < classes ? sv[j] - mx : 0;
+            d = d > 0 ? d : 0;
+            o[j] = j < classes ? ipow2_64(d) - 1 : 0;
+        }
+    } else {
+        const int64_t base = ipow2_64(1 - 2 * (int64_t)as);
+        const int64_t sb = ipow2_64(1 - (int64_t)as);
+#pragma unroll
+        for (int j = 0; j < LOSS_MAXC; ++j) {
+            const int64_t v = j < classes ? L[j] : 0;
+            o[j] = j < classes ? base + v * sb + v * v : 0;
+        }
+    }
+    int64_t sum = 0;
+#pragma unroll
+    for (int j = 0; j < LOSS_MAXC; ++j) sum += o[j];
+    int64_t gs = 0;
+#pragma unroll
+    for (int j = 0; j < LOSS_MAXC; ++j) {
+        o[j] = j < classes ? (sum != 0 ? div_trunc52(o[j] * (1 << 11), sum) : 0) : 0;
+        gs += o[j];
+    }
+#pragma unroll
+    for (int j = 0; j < LOSS_MAXC; ++j) {
+        const int32_t gf = (int32_t)(j == label ? o[j] - gs : o[j]);
+        if (j < ld) out[j] = j < classes ? (int8_t)psto_any(gf, 4) : (int8_t)0;
+    }
+    for (int j = LOSS_MAXC; j < ld; ++j) out[j] = 0;
+}
 }  // namespace niti

@@ -110,6 +110,8 @@ def lib():
         "niti_diag_rowconv_speculate": (None, [C.c_int]),
         "niti_diag_gemm_speculate": (None, [C.c_int]),
         "niti_diag_gemm_fused_launches": (C.c_ulonglong, []),
+        "niti_diag_head_chain_launches": (C.c_ulonglong, []),
+        "niti_diag_head_chain": (None, [C.c_int]),
         "niti_diag_p16_jobs_cap": (None, [C.c_int]),
         "niti_tensor_convert": (ci, [tp, tp, vp]),
         "niti_geom_finalize": (ci, [C.POINTER(Geom)]),

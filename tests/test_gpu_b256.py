@@ -65,13 +65,14 @@ def case():
     return dict(layers=layers, W=W, S=S, img=img, labels=labels, x=x, ascale=ascale, newW=newW, rec=rec)
 
 
-def _step_and_compare(T, case, prepare, keep_grads=True):
+def _step_and_compare(T, case, prepare, keep_grads=True, overlap=True):
     import niti_amd
     from niti_amd._lib import NitiError
     from niti_amd.model import NitiModel
     layers, rec = case["layers"], case["rec"]
     m = NitiModel(niti_amd.ARCH_VGG11, B)
     m.keep_grads(keep_grads)
+    m.set_overlap(overlap)
     img = T.from_numpy(case["img"]).cuda()
     lab = T.from_numpy(case["labels"]).cuda()
     for i, (w, s) in enumerate(zip(case["W"], case["S"])):
@@ -108,18 +109,27 @@ def test_vgg11_b256_autotuned_step_full_parity(T, case):
     print("\nautotuned plans {(layer, phase): (bm, bn, splits, strategy)}:", plans)
 
 
-def test_vgg11_b256_bench_config_parity(T, case):
-    """The step exactly as bench.py times it: autotuned plans and keep_grads(False) -- no int8
-    weight-gradient copies, and the pooled layers' 2x2 routes recorded as codes by the forward
+@pytest.mark.parametrize("head_chain", [0, 1])
+def test_vgg11_b256_bench_config_parity(T, case, head_chain):
+    """The step exactly as bench.py times it: one stream, autotuned plans and keep_grads(False) -- no
+    int8 weight-gradient copies, and the pooled layers' 2x2 routes recorded as codes by the forward
     kernels (conv0's and the row kernels' epilogues) and read by the next input gradient instead of
     the pre-pool output, which is then never written (NITI_CPUPoolGrad_Int8.cpp:21-77: the first
-    window element >= the pooled value takes the gradient).  Logits, every output gradient, every
-    unpooled forward tap and every new weight against the oracle."""
+    window element >= the pooled value takes the gradient); the head's forward, loss gradient,
+    weight and input gradients in the one head-chain launch
+    (niti_head.hip, off by default; both ways).  Logits, every output gradient, every unpooled forward
+    tap and every new weight against the oracle."""
+    from niti_amd import _lib as L
     from niti_amd.model import NitiModel
+    n0 = L.lib().niti_diag_head_chain_launches()
+    L.lib().niti_diag_head_chain(head_chain)
     try:
-        _step_and_compare(T, case, lambda m: m.autotune(), keep_grads=False)
+        _step_and_compare(T, case, lambda m: m.autotune(), keep_grads=False, overlap=False)
     finally:
+        L.lib().niti_diag_head_chain(0)
         NitiModel.reset_plans()
+    ran = L.lib().niti_diag_head_chain_launches() - n0
+    assert (ran > 0) == bool(head_chain)
 
 
 @pytest.mark.parametrize("splits", [6, 8])

@@ -298,3 +298,23 @@ def test_vgg11_step_p16_copies_over_several_launches(T, cap):
         _run(T, niti_amd.ARCH_VGG11, R.vgg11_layers(), batch=32, steps=2, seed=41 + cap)
     finally:
         lib.niti_diag_p16_jobs_cap(0)
+
+
+@pytest.mark.parametrize("batch,graph,keep", [(8, False, True), (36, False, False), (100, True, True)])
+def test_vgg11_step_head_chain(T, batch, graph, keep):
+    """VGG-11's classifier head as one launch (niti_head.hip: forward with the rescale, the loss
+    gradient, the weight gradient and the input gradient routed through conv7's pool codes; off by
+    default) at batches that leave a row tile partly empty (8, 36, 100), under graph replay too: two
+    steps against the oracle, and the launch must have run."""
+    import niti_amd
+    import niti_model_ref as R
+    from niti_amd import _lib as L
+    lib = L.lib()
+    n0 = lib.niti_diag_head_chain_launches()
+    lib.niti_diag_head_chain(1)
+    try:
+        _run(T, niti_amd.ARCH_VGG11, R.vgg11_layers(), batch=batch, steps=2, seed=61 + batch, graph=graph,
+             overlap=False, keep_grads=keep)
+    finally:
+        lib.niti_diag_head_chain(0)
+    assert lib.niti_diag_head_chain_launches() > n0
