@@ -211,6 +211,9 @@ def main():
                     help="weight gradients on a second stream beside the input-gradient chain (measured within 1 %% "
                          "of the single-stream step on MI355X, and it slows the overlapped kernels by sharing the CUs)")
     ap.add_argument("--no-overlap", action="store_true", help="(default) weight gradients on the step stream")
+    ap.add_argument("--probe-every", type=int, default=1,
+                    help="time the probed launch in one timed step of every K (its begin / end events hold the "
+                         "dispatches either side of it back; 0: in none, an A/B diagnostic)")
     ap.add_argument("--probe-plan", default="", help="bm,bn,splits,strategy forced on the probed GEMM after "
                                                      "autotuning (PMC passes re-use the timed run's plan)")
     ap.add_argument("--dp-path", action="store_true", help="diagnostic: run the data-parallel step on one GPU (a "
@@ -329,7 +332,9 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
+        if args.probe_every != 1:
+            model.probe_pause(args.probe_every <= 0 or i % args.probe_every != args.probe_every - 1)
         step()
     torch.cuda.synchronize()
     if dist:
@@ -346,6 +351,7 @@ def main():
     # launches B redid, and pairs the row kernels ran in store mode or the GEMM pair settled from an
     # alternate, per layer over warmup + timed steps (fwd redone, fwd stored/alt, dgrad redone, dgrad
     # stored/alt)
+    model.probe_pause(False)
     spec = [(s[1], s[2], s[4], s[5]) for s in model.spec_stats()]
     spec = {"redone": sum(a + c for a, _, c, _ in spec), "stored_or_alternate": sum(b + d for _, b, _, d in spec),
             "per_layer": [list(v) for v in spec if any(v)]}

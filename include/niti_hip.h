@@ -258,8 +258,9 @@ int niti_conv_dgrad_phase2(const niti_geom* g, const int8_t* dy_nhwc16, const in
  * if max|y|'s bit width differs from that guess -- the results are modes 1 + 2's, at one GEMM pass
  * when the bit width holds from step to step. */
 #define NITI_ROWCONV_STATE_WORDS 1216
-/* the speculative pair's slot of a state (dgrad 0 forward, 1 input gradient): u32 [0] the hint (bit
- * width + 1, 0 none), [1] the guess the last mode-3 call used, [2] the mode-4 calls that redid */
+/* the speculative pair's slot of a state (dgrad 0 forward, 1 input gradient): u32 [0] the hint (the
+ * bit width on the input's scale: bw + 1 + exp_in + wscale + 512, 0 none), [1] the guess (bw + 1) the
+ * last mode-3 call used, [2] the mode-4 calls that redid */
 uint32_t* niti_rows_spec_slot(uint32_t* state, int dgrad);
 int niti_conv_rows_ok(const niti_geom* g);
 int niti_nhwc16_to_c32(const int8_t* in_nhwc16, int n, int hw, int cp, int c, int8_t* out_c32, void* stream);
@@ -483,6 +484,9 @@ int niti_model_rowconv_error(niti_model_t m);
  * width + 1), forward launches redone, forward pairs in store mode, then the same for the input
  * gradient (niti_rows_spec_slot; synchronises) */
 int niti_model_spec_stats(niti_model_t m, uint32_t* out, int max_layers);
+/* diagnostics: the 32 words of one row-kernel layer's speculative slot (niti_rows_spec_slot), with
+ * the last 24 pairs' record (bw, input scale, guess) in words 8.. (synchronises) */
+int niti_model_spec_slot(niti_model_t m, int layer, int dgrad, uint32_t* out32);
 /* Replay the step as a hipGraph (single device only -- with a communicator attached the step
  * always runs as direct launches).  Default 0 (direct launches: measured faster on ROCm 7.2). */
 int niti_model_set_graph(niti_model_t m, int enable);
@@ -517,6 +521,9 @@ void niti_plan_reset(void);
  * duration and the number of launches timed, then resets the count. */
 int niti_model_set_probe(niti_model_t m, int layer, int phase, int max_launches);
 int niti_model_probe_read(niti_model_t m, double* total_ms, int* count);
+/* paused != 0: the armed probe skips the next launches (no events, no span slot) until resumed;
+ * a host flag, so a timed loop can time the probed launch in some of its steps only */
+int niti_model_probe_pause(niti_model_t m, int paused);
 /* Weight-gradient probes (phase 2) also time the launch from inside: the kernel min-es its
  * blocks' start and max-es their end on the device wall clock (s_memrealtime); this returns the
  * summed first-block-start -> last-block-end spans and their count, then re-arms. */

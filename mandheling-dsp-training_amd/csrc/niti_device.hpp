@@ -107,29 +107,80 @@ __device__ __forceinline__ uint32_t pool_code_mask(uint32_t code, int t) {
     return sw_expand(((code >> t) & 0x01010101u) << 7);
 }
 
-// A speculative pair's guess and its update, for slot words [0] the last bit width + 1 (0: none),
-// [5] the one before it, [6] a 2-bit chooser between "the last" and "the one before" (a layer whose
-// maximum sits at a power of two flips back and forth; as a branch predictor's chooser).  pick:
-// the guess (bw + 1); learn: called by one thread of the pair's second launch with the true bw.
-__device__ __forceinline__ uint32_t spec_pick(const uint32_t* hint) {
+// The residual rule, 4 sums per operand dword with bit-field extracts: the compiler's form of
+// residual_z + psto_fast ran ~18.5 VALU per element and the pass VALU-bound (15.7 us against 12 us
+// of memory for layer1's 77 MB, tools/probes/exit_probe.hip).  Per byte e: hi = sbfe(hw, 8e, 8),
+// lo >> r = sbfe(lw, 8e + min(r, 7), 8 - min(r, 7)) (lo's sign once r >= 7), z = (hi << d) + that
+// (d <= 23), then PSTO (psto_fast): q = u >> s, qp = ubfe(u, h, s - h) (= (u mod 2^s) >> h),
+// pr = ubfe(u, 0, h) << (s & 1), q + (qp > pr), clip 127, the sign restored; relu: u = max(z, 0).
+// The range (launch A) as a running max and min of z.  Not used for the raw cast (shift <= 0).
+// (Packed 16-bit VALU, two sums per lane, measured 2.4x slower on gfx950: 37 vs 15.7 us.)
+struct ResRule {
+    uint32_t d, loff, lw, s, h, hs, odd;
+};
+__device__ __forceinline__ ResRule res_rule(int d, int r, int s) {
+    const int rr = r < 7 ? r : 7;
+    return ResRule{(uint32_t)d, (uint32_t)rr, (uint32_t)(8 - rr), (uint32_t)s, (uint32_t)(s >> 1),
+                   (uint32_t)(s - (s >> 1)), (uint32_t)(s & 1)};
+}
+template <bool RELU>
+__device__ __forceinline__ uint32_t res_rule4(uint32_t hw, uint32_t lw, const ResRule& k, int& mx, int& mn, bool range) {
+    uint32_t o[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const int hi = __builtin_amdgcn_sbfe((int)hw, 8 * e, 8);
+        const int lo = __builtin_amdgcn_sbfe((int)lw, 8 * e + (int)k.loff, (int)k.lw);
+        const int z = (int)(((uint32_t)hi << k.d) + (uint32_t)lo);
+        if (range) {
+            mx = max(mx, z);
+            mn = min(mn, z);
+        }
+        const uint32_t u = RELU ? (uint32_t)max(z, 0) : (uint32_t)max(z, -z);
+        const uint32_t q = u >> k.s;
+        const uint32_t qp = __builtin_amdgcn_ubfe(u, k.h, k.hs);
+        const uint32_t pr = __builtin_amdgcn_ubfe(u, 0, k.h) << k.odd;
+        uint32_t v = min(q + (qp > pr ? 1u : 0u), 127u);
+        if (!RELU) v = z < 0 ? 0u - v : v;
+        o[e] = v & 0xffu;
+    }
+    return o[0] | (o[1] << 8) | (o[2] << 16) | (o[3] << 24);
+}
+
+// A speculative pair's guess and its update, for slot words [0] the last bit width, [5] the one
+// before it, [6] a 2-bit chooser between "the last" and "the one before" (a layer whose maximum
+// sits at a power of two flips back and forth; as a branch predictor's chooser).  The bit widths
+// are kept on the scale of the layer's input: K = bw + escale, escale = the input's exponent (+ the
+// weight's), encoded as K + 1 + SPEC_K0 (0: none).  The int8 rule keeps every tensor's maximum in
+// [64, 127], so when an upstream layer's bit width crosses a power of two its output exponent moves
+// by one and its int8 values halve or double -- and every downstream layer's accumulator bit width
+// moves by one with them while K holds: the guess bw = K - escale follows the flip (a hint kept as
+// the bare bw missed in every layer below the one that flipped, ~50 % of the ResNet-18 pairs in
+// profiles/r06_resnet18_bench.json).  pick: the guess (bw + 1, 0: none); learn: called by one thread
+// of the pair's second launch with the true bw.
+constexpr int SPEC_K0 = 512;
+__device__ __forceinline__ uint32_t spec_pick(const uint32_t* hint, int escale) {
     const uint32_t h = (uint32_t)__builtin_amdgcn_readfirstlane(
         (int)__hip_atomic_load(hint, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     const uint32_t hp = (uint32_t)__builtin_amdgcn_readfirstlane(
         (int)__hip_atomic_load(hint + 5, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     const uint32_t ch = (uint32_t)__builtin_amdgcn_readfirstlane(
         (int)__hip_atomic_load(hint + 6, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    return ch >= 2u && hp != 0u ? hp : h;
+    const uint32_t k = ch >= 2u && hp != 0u ? hp : h;
+    if (k == 0u) return 0u;
+    const int g = (int)k - SPEC_K0 - escale;  // bw + 1
+    return (uint32_t)(g < 1 ? 1 : g > 32 ? 32 : g);
 }
-__device__ __forceinline__ void spec_learn(uint32_t* hint, int bw) {
+__device__ __forceinline__ void spec_learn(uint32_t* hint, int bw, int escale) {
+    const uint32_t kv = (uint32_t)(bw + 1 + escale + SPEC_K0);
     const uint32_t h = __hip_atomic_load(hint, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint32_t hp = __hip_atomic_load(hint + 5, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     uint32_t ch = __hip_atomic_load(hint + 6, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const bool last_ok = h == (uint32_t)bw + 1u, prev_ok = hp == (uint32_t)bw + 1u;
+    const bool last_ok = h == kv, prev_ok = hp == kv;
     if (prev_ok && !last_ok && ch < 3u) ++ch;
     if (last_ok && !prev_ok && ch > 0u) --ch;
     __hip_atomic_store(hint + 6, ch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(hint + 5, h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(hint, (uint32_t)bw + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(hint, kv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // The residual rule (niti_resnet.hip): z = hi * 2^d + (lo >> r), arithmetic shift

@@ -222,13 +222,15 @@ struct Epi {
     int8_t* exp_out = nullptr;
     unsigned long long* span = nullptr;  // kernel-span probe slot (probe_span_arm)
     // the speculative pair (plan strategy STRAT_SPEC, EPI_REQUANT only): spec 1 = launch A --
-    // requantise with the bit width in hint[0] (the layer's previous one, bw + 1; 0 none) and publish
+    // requantise with the bit width hint[0] gives (the layer's previous one on its input's scale,
+    // spec_pick; 0 none) and publish
     // max|C| into amax; spec 2 = launch B -- every block exits at once unless the max's bit width
     // differs from the one A used (hint[1]), and otherwise requantises with it.  Slot words as the
     // row kernels' (niti_rowconv.hip spec_guess / spec_settle): [0] hint (written by B), [1] the guess
     // A used (written by A), [2] launches B redid.
     int spec = 0;
     uint32_t* hint = nullptr;
+    int hint_scale = 0;  // the hint on the input's scale (forward) or bare (input gradient)
     // launch A also writes the output requantised one bit width below and above its guess into
     // alt[0 .. M*ldo) / alt[M*ldo .. 2*M*ldo) (may be null): launch B then settles a +-1 change --
     // the common miss, a max near a power of two -- by copying instead of redoing the GEMM
@@ -252,6 +254,12 @@ struct Epi {
     uint32_t spin_limit = 0;
 };
 
+// the input's scale for the pair's hint (spec_pick, niti_device.hpp): exponent in + weight scale
+__device__ __forceinline__ int gemm_spec_escale(const Epi& epi) {
+    if (!epi.hint_scale) return 0;
+    return __builtin_amdgcn_readfirstlane((epi.exp_in ? (int)*epi.exp_in : 0) + (epi.wscale ? (int)*epi.wscale : 0));
+}
+
 // launch B of the pair: the rule's bit width of the (all-reduced) max against the one A used
 // (hint[1] = bw + 1); block 0 writes the exponent and the next hint.  Returns 0 when A's output
 // stands (every block of B then exits), 1 / 2 when A's alternate one bit width below / above holds
@@ -264,6 +272,7 @@ __device__ __forceinline__ int gemm_spec_settle(const Epi& epi) {
         (int)__hip_atomic_load(epi.hint + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     const int used = (int)(h1 & 0x7fffffffu) - 1;
     const bool alts = (h1 >> 31) != 0u;  // A wrote the alternates
+    const int esc = gemm_spec_escale(epi);  // (before the exponent write: exp_out may alias exp_in)
     const int act = bw == used ? 0 : !alts ? -1 : (bw == used - 1 && used >= 1) ? 1 : bw == used + 1 ? 2 : -1;
     if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
         if (act >= 0 && epi.exp_out != nullptr) {  // (a redo writes it in its epilogue)
@@ -271,7 +280,7 @@ __device__ __forceinline__ int gemm_spec_settle(const Epi& epi) {
             const int inc = shift > 1 ? shift : (shift == 1 ? 2 : 0);
             *epi.exp_out = (int8_t)((epi.exp_in ? (int)*epi.exp_in : 0) + (epi.wscale ? (int)*epi.wscale : 0) + inc);
         }
-        __hip_atomic_store(epi.hint, (uint32_t)bw + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        spec_learn(epi.hint, bw, esc);
         if (act < 0) __hip_atomic_fetch_add(epi.hint + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (act > 0) __hip_atomic_fetch_add(epi.hint + 3, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         // the alternates' window: a miss opens it for the next GEMM_SPEC_ALT_PAIRS pairs, a hit
@@ -344,8 +353,8 @@ __device__ __forceinline__ void gemm_epilogue(v16i (&acc)[TM][TN], int r0, int c
         if (fused) {
             bw = fused_bw;
         } else if (spec_a) {
-            const uint32_t h = __hip_atomic_load(epi.hint, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            bw = __builtin_amdgcn_readfirstlane((int)h) - 1;  // no hint yet: 0 (B redoes unless the max is 0)
+            const uint32_t h = spec_pick(epi.hint, gemm_spec_escale(epi));  // bw + 1 on the input's scale
+            bw = (int)h - 1;  // no hint yet: 0 (B redoes unless the max is 0)
             if (h != 0u) bw += epi.spec_bias;
             if (bw < 0) bw = 0;
             abw = bw;
@@ -2101,6 +2110,7 @@ static hipError_t act_spec(int op, const LA& la, const LB& lb, int M, int N, int
     e.exp_out = o.exp_out;
     e.spec = pass == 0 ? 1 : 2;
     e.hint = hint;
+    e.hint_scale = op == PLAN_FWD ? 1 : 0;
     e.alt = alt;
     e.spec_bias = g_gemm_spec_bias;
     return launch_mode<LA, LB, EPI_REQUANT, false>(p, la, lb, M, N, kc_total, e, st);
@@ -3494,14 +3504,14 @@ __global__ void __launch_bounds__(256) residual_requant_kernel(const int8_t* __r
                                                                int8_t* __restrict__ ez, int8_t* __restrict__ exp_out,
                                                                int relu, const int8_t* __restrict__ relu_mask,
                                                                int8_t* __restrict__ out, int spec,
-                                                               uint32_t* __restrict__ hint) {
+                                                               uint32_t* __restrict__ hint, int pk) {
     const int xa = *ea, xb = *eb;
     const bool a_hi = xa >= xb;
     const int diff = a_hi ? xa - xb : xb - xa;
     const int d = diff < 23 ? diff : 23, r = diff - d;
     int bw;
     if (spec == 1) {  // launch A: the guess; the range is published below
-        bw = (int)spec_pick(hint) - 1;
+        bw = (int)spec_pick(hint, relu ? (a_hi ? xa : xb) - d : 0) - 1;  // forward: on z's scale
         if (bw < 0) bw = 0;  // (no hint yet: B redoes unless the max is 0)
         if (blockIdx.x == 0 && threadIdx.x == 0)
             __hip_atomic_store(hint + 1, (uint32_t)bw + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -3511,7 +3521,7 @@ __global__ void __launch_bounds__(256) residual_requant_kernel(const int8_t* __r
             const int used = __builtin_amdgcn_readfirstlane(
                                  (int)__hip_atomic_load(hint + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) - 1;
             if (blockIdx.x == 0 && threadIdx.x == 0) {
-                spec_learn(hint, bw);
+                spec_learn(hint, bw, relu ? (a_hi ? xa : xb) - d : 0);
                 if (bw != used) __hip_atomic_fetch_add(hint + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 const int shift = bw - 7;
                 const int e_z = (a_hi ? xa : xb) - d;
@@ -3530,6 +3540,27 @@ __global__ void __launch_bounds__(256) residual_requant_kernel(const int8_t* __r
         if (exp_out != nullptr) *exp_out = (int8_t)(e_z + (shift > 1 ? shift : (shift == 1 ? 2 : 0)));
     }
     uint32_t m = 0;
+    if (pk && !raw) {  // the bit-field form (res_rule4)
+        const ResRule k = res_rule(d, r, s);
+        const int8_t* hi = a_hi ? a : b;
+        const int8_t* lo = a_hi ? b : a;
+        int mx = 0, mn = 0;
+        for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += (int64_t)gridDim.x * 256) {
+            const v4i vh = ((const v4i*)hi)[i], vl = ((const v4i*)lo)[i];
+            v4i mk;
+            if (relu_mask != nullptr) mk = ((const v4i*)relu_mask)[i];
+            v4i q;
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                uint32_t o = relu ? res_rule4<true>((uint32_t)vh[w], (uint32_t)vl[w], k, mx, mn, spec == 1)
+                                  : res_rule4<false>((uint32_t)vh[w], (uint32_t)vl[w], k, mx, mn, spec == 1);
+                if (relu_mask != nullptr) o &= sw_expand(sw_pos_hi((uint32_t)mk[w]));
+                q[w] = (int)o;
+            }
+            ((v4i*)out)[i] = q;
+        }
+        m = max(uabs32(mx), uabs32(mn));
+    } else {
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += (int64_t)gridDim.x * 256) {
         const v16c va = ((const v16c*)a)[i], vb = ((const v16c*)b)[i];
         v16c mk;
@@ -3549,6 +3580,7 @@ __global__ void __launch_bounds__(256) residual_requant_kernel(const int8_t* __r
         }
         ((v16c*)out)[i] = q;
     }
+    }
     if (spec == 1) {  // NITI_RangeEstimate of z for launch B
         m = wave_max(m);
         __shared__ uint32_t red[4];
@@ -3566,8 +3598,10 @@ hipError_t residual_requant(const int8_t* a, const int8_t* ea, const int8_t* b, 
     const int64_t n16 = n / 16;
     int64_t blocks = (n16 + 255) / 256;
     blocks = blocks < 1 ? 1 : blocks > 2048 ? 2048 : blocks;
+    // NITI_RES_PK=0: the 32-bit loop only (an A/B switch for the packed form)
+    static const int pk = getenv("NITI_RES_PK") ? atoi(getenv("NITI_RES_PK")) : 1;
     hipLaunchKernelGGL(residual_requant_kernel, dim3((unsigned)blocks), dim3(256), 0, st, a, ea, b, eb, n16, amax, ez,
-                       exp_out, relu, relu_mask, out, spec, slot);
+                       exp_out, relu, relu_mask, out, spec, slot, pk);
     return hipGetLastError();
 }
 

@@ -338,7 +338,7 @@ struct Model {
     void probe_launch(int layer, int phase, hipEvent_t* b, hipEvent_t* e, unsigned long long** sp) {
         *b = *e = nullptr;
         *sp = nullptr;
-        if (layer != probe_layer || phase != probe_phase || tuning || capturing) return;
+        if (layer != probe_layer || phase != probe_phase || probe_paused || tuning || capturing) return;
         if (probe_count < (int)ev0.size()) {
             *b = ev0[probe_count];
             *e = ev1[probe_count];
@@ -454,13 +454,13 @@ struct Model {
     unsigned long long* span = nullptr;
     int span_cap = 0, span_count = 0;
     void arm_kernel_events(int layer, int phase) {
-        if (layer != probe_layer || phase != probe_phase || tuning || capturing || probe_count >= (int)ev0.size())
+        if (layer != probe_layer || phase != probe_phase || probe_paused || tuning || capturing || probe_count >= (int)ev0.size())
             return;
         probe_events_arm(ev0[probe_count], ev1[probe_count]);
         ++probe_count;
     }
     void arm_span(int layer, int phase) {
-        if (layer != probe_layer || phase != probe_phase || tuning || capturing || span == nullptr ||
+        if (layer != probe_layer || phase != probe_phase || probe_paused || tuning || capturing || span == nullptr ||
             span_count >= span_cap)
             return;
         probe_span_arm(span + 2 * SPAN_MAX_BLOCKS * span_count++);
@@ -471,6 +471,7 @@ struct Model {
             seg_cut(st);
             return;
         }
+        if (probe_paused) return;
         if (probe_count >= (int)ev0.size()) return;
         if (begin) {
             (void)hipEventRecord(ev0[probe_count], st);
@@ -481,7 +482,7 @@ struct Model {
     }
     // the end event of a probe that the callee records itself (right after the GEMM launch)
     hipEvent_t probe_end_event(int layer, int phase) {
-        if (layer != probe_layer || phase != probe_phase || capturing || tuning || probe_count >= (int)ev0.size())
+        if (layer != probe_layer || phase != probe_phase || probe_paused || capturing || tuning || probe_count >= (int)ev0.size())
             return nullptr;
         return ev1[probe_count++];
     }
@@ -499,6 +500,7 @@ struct Model {
 
     int build(int arch_, int batch_, int in_hw = 0);
     bool tuning = false;  // autotune in progress: no collectives, no probe
+    bool probe_paused = false;  // niti_model_probe_pause: the armed probe skips these launches
     int fwd_layer(int i, hipStream_t st);
     int wgrad_layer(int i, hipStream_t st);
     int dgrad_layer(int i, hipStream_t st);
@@ -859,7 +861,7 @@ int Model::step(const int8_t* x_nchw, int exp_in, const uint8_t* images, const i
     }
     MTRY(hipEventRecord(gin, st));
     MTRY(hipStreamWaitEvent(gstream, gin, 0));
-    const bool probing = segs.size() == 3 && probe_count < (int)ev0.size();
+    const bool probing = segs.size() == 3 && !probe_paused && probe_count < (int)ev0.size();
     for (size_t j = 0; j < segs.size(); ++j) {
         if (probing && j == 1) MTRY(hipEventRecord(ev0[probe_count], gstream));
         if (probing && j == 2) MTRY(hipEventRecord(ev1[probe_count++], gstream));
@@ -1897,6 +1899,25 @@ int niti_model_set_rowconv(niti_model_t m, int enable) {
     return NITI_NO_ERROR;
 }
 
+int niti_model_spec_slot(niti_model_t m, int layer, int dgrad, uint32_t* out32) {
+    if (!m || !out32 || layer < 0) return NITI_INVALID_VALUE;
+    const uint32_t* bar = nullptr;
+    if (m->r) {
+        if (layer >= (int)m->r->C.size()) return NITI_INVALID_VALUE;
+        bar = m->r->C[layer].bar;
+    } else {
+        if (layer >= (int)m->m.L.size()) return NITI_INVALID_VALUE;
+        bar = m->m.L[layer].bar;
+    }
+    std::fill(out32, out32 + 32, 0u);
+    if (bar == nullptr) return NITI_NO_ERROR;
+    if (hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpy(out32, niti::rowconv_spec_slot(const_cast<uint32_t*>(bar), dgrad != 0), 32 * 4,
+                  hipMemcpyDeviceToHost) != hipSuccess)
+        return NITI_NO_EXECUTION;
+    return NITI_NO_ERROR;
+}
+
 int niti_model_spec_stats(niti_model_t m, uint32_t* out, int max_layers) {
     if (m && m->r) return out && max_layers >= 0 ? m->r->spec_stats(out, max_layers) : NITI_INVALID_VALUE;
     if (!m || !out || max_layers < 0) return NITI_INVALID_VALUE;
@@ -2131,6 +2152,15 @@ int niti_model_probe_read_span(niti_model_t m, double* total_ms, int* count) {
     // re-arm the slots for the next measurement
     if (hipMemset(m->m.span, 0, h.size() * 8) != hipSuccess) return NITI_NO_EXECUTION;
     m->m.span_count = 0;
+    return NITI_NO_ERROR;
+}
+
+int niti_model_probe_pause(niti_model_t m, int paused) {
+    if (!m) return NITI_INVALID_VALUE;
+    if (m->r)
+        m->r->probe_paused = paused != 0;
+    else
+        m->m.probe_paused = paused != 0;
     return NITI_NO_ERROR;
 }
 

@@ -290,7 +290,7 @@ void ResNetModel::clear_probe() {
 }
 
 void ResNetModel::probe(int layer, int phase, bool begin, hipStream_t st) {
-    if (layer != probe_layer || phase != probe_phase || tuning || capturing || probe_count >= (int)ev0.size()) return;
+    if (layer != probe_layer || phase != probe_phase || probe_paused || tuning || capturing || probe_count >= (int)ev0.size()) return;
     if (begin) {
         (void)hipEventRecord(ev0[probe_count], st);
     } else {

@@ -143,6 +143,7 @@ struct ResNetModel {
     bool keep_grads = true;
     bool use_rowconv = true;
     bool tuning = false;
+    bool probe_paused = false;  // niti_model_probe_pause
     bool capturing = false;
     // data parallel: ranges on the step stream (coll), gradient-bucket SUMs on cst (coll_grad)
     std::unique_ptr<Collective> coll, coll_grad;

@@ -112,6 +112,7 @@ struct RowConvArgs {
     const int8_t* wscale;
     int8_t* exp_out;
     int relu;
+    int hint_scale;   // the pair's hint on the input's scale (forward slot) or bare (input gradient)
     uint32_t* amax;   // RANGE: published; REQUANT: read
     uint32_t* bar;    // FUSED: barrier state
     uint32_t epoch;
@@ -997,10 +998,18 @@ __device__ __forceinline__ void write_exponent(const RowConvArgs& a, uint32_t gm
 // The guess (spec_pick / spec_learn, niti_device.hpp): a layer's bit width either holds from pair to
 // pair or, with gradients whose maximum sits at a power of two, flips back and forth; a 2-bit
 // chooser counts which of "the last bit width" and "the one before it" would have been right.
+// the input's scale for the hint (spec_pick): exponent in + weight scale, both settled before A;
+// forward slots only -- an input gradient's bit width follows its own value better than dy's scale
+// (tools/spec_trace.py, profiles/r06_spec_trace_resnet18.txt: K = bw + escale drifts down steadily
+// over the steps while bw stays within 14-16)
+__device__ __forceinline__ int spec_escale(const RowConvArgs& a) {
+    if (!a.hint_scale) return 0;
+    return __builtin_amdgcn_readfirstlane((a.exp_in ? (int)*a.exp_in : 0) + (a.wscale ? (int)*a.wscale : 0));
+}
 constexpr uint32_t SPEC_COOLDOWN = 8;  // the default of spec_cooldown() (NITI_SPEC_COOLDOWN overrides; profiles/r05_spec_cooldown_ab.txt)
 __device__ __forceinline__ int spec_guess(const RowConvArgs& a, bool can_store, bool& store) {
     const uint32_t f = __hip_atomic_load(a.hint + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint32_t gh = spec_pick(a.hint);  // the guess, as bw + 1 (0: none)
+    const uint32_t gh = spec_pick(a.hint, spec_escale(a));  // the guess, as bw + 1 (0: none)
     store = can_store && a.acc_store != nullptr && __builtin_amdgcn_readfirstlane((int)f) != 0;
     if (blockIdx.x == 0 && threadIdx.x == 0)
         __hip_atomic_store(a.hint + 1, gh | (store ? 0x80000000u : 0u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1013,19 +1022,27 @@ __device__ __forceinline__ int spec_guess(const RowConvArgs& a, bool can_store, 
 __device__ __forceinline__ bool spec_settle(const RowConvArgs& a, uint32_t& g, bool& stored) {
     g = read_max(a.amax);
     const int bw = bitwidth_rc(g);
+    const int esc = spec_escale(a);  // before write_exponent (exp_out may alias a later exp_in)
     const uint32_t w1 = (uint32_t)__builtin_amdgcn_readfirstlane(
         (int)__hip_atomic_load(a.hint + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     stored = (w1 >> 31) != 0;
     const bool changed = bw != (int)(w1 & 0x7fffffffu) - 1;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         write_exponent(a, g);
-        spec_learn(a.hint, bw);  // the next guess (spec_pick)
+        spec_learn(a.hint, bw, esc);  // the next guess (spec_pick)
         // store mode for the next SPEC_COOLDOWN pairs after a change (a layer whose bit width flips
         // from step to step, gradients near a power of two, stays there; block 0 of B is the only
         // reader-writer of this word within a launch)
         const uint32_t cd = __hip_atomic_load(a.hint + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(a.hint + 3, changed ? a.spec_cooldown : (cd > 0u ? cd - 1u : 0u), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
+        // the last 24 pairs' record (niti_model_spec_slot): word 7 counts, 8 + (count mod 24) holds
+        // bw | (escale + 256) << 8 | the guess A used (bw + 1) << 20
+        const uint32_t hn = __hip_atomic_load(a.hint + 7, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(a.hint + 8 + hn % 24u,
+                           (uint32_t)bw | ((uint32_t)(esc + 256) << 8) | ((w1 & 0xfffu) << 20), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(a.hint + 7, hn + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (stored) __hip_atomic_fetch_add(a.hint + 4, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         else if (changed) __hip_atomic_fetch_add(a.hint + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -1882,6 +1899,7 @@ hipError_t rowconv_fwd(const ConvGeom& g, const int8_t* x_c32, const int8_t* wf,
     // the hint slot (the speculative pair's, and the fused mode's speculative epilogue): forward or
     // input gradient, by the operands or the caller's dgrad_slot, so the two directions never share it
     a.hint = (spec || mode == RC_FUSED) && bar != nullptr ? bar + (16 + (dg || o.dgrad_slot ? 1 : 0)) * BAR_LINE : nullptr;
+    a.hint_scale = dg || o.dgrad_slot ? 0 : 1;
     if (o.p16 != nullptr && (!dg || !rowconv_p16_ok(g, o.pool_dx != nullptr))) return hipErrorInvalidValue;
     if (o.pool_out != nullptr && (R % 2 != 0 || g.h % 2 != 0)) return hipErrorInvalidValue;
     if (mode == RC_FUSED) {
@@ -2046,6 +2064,7 @@ hipError_t rowconv_fc(int n, int K, int rows, const int8_t* x, int xld, const in
     // the hint slot (the speculative pair's, and the fused mode's speculative epilogue): forward or
     // input gradient, by the operands or the caller's dgrad_slot, so the two directions never share it
     a.hint = (spec || mode == RC_FUSED) && bar != nullptr ? bar + (16 + (dg || o.dgrad_slot ? 1 : 0)) * BAR_LINE : nullptr;
+    a.hint_scale = dg || o.dgrad_slot ? 0 : 1;
     if (o.p16 != nullptr && (o.pool_dx == nullptr || a.p16_pixels % 16 != 0)) return hipErrorInvalidValue;
     if (o.next != nullptr && a.cop % 32 != 0) return hipErrorInvalidValue;
     if (mode == RC_FUSED) {

@@ -188,6 +188,8 @@ def lib():
         "niti_plan_reset": (None, []),
         "niti_model_set_probe": (ci, [vp, ci, ci, ci]),
         "niti_model_probe_read": (ci, [vp, C.POINTER(C.c_double), C.POINTER(ci)]),
+        "niti_model_probe_pause": (ci, [vp, ci]),
+        "niti_model_spec_slot": (ci, [vp, ci, ci, C.POINTER(C.c_uint32)]),
         "niti_model_run_phase": (ci, [vp, ci, ci, vp]),
         "niti_model_probe_read_span": (ci, [vp, C.POINTER(C.c_double), C.POINTER(ci)]),
         "niti_dp_get_unique_id": (ci, [C.c_char_p]),

@@ -212,6 +212,16 @@ class NitiModel:
     def set_probe(self, layer: int, phase: int, max_launches: int = 256):
         check(self._lib.niti_model_set_probe(self._h, layer, phase, max_launches), "set_probe")
 
+    def spec_slot(self, layer: int, dgrad: int):
+        """The 32 words of one row-kernel layer's speculative slot (diagnostics)."""
+        out = (C.c_uint32 * 32)()
+        check(self._lib.niti_model_spec_slot(self._h, int(layer), int(dgrad), out), "spec_slot")
+        return list(out)
+
+    def probe_pause(self, paused: bool):
+        """Skip (True) or time again (False) the armed probe's launches; host-side only."""
+        check(self._lib.niti_model_probe_pause(self._h, 1 if paused else 0), "probe_pause")
+
     def probe_read(self):
         t = C.c_double()
         n = C.c_int()
