@@ -146,41 +146,80 @@ __device__ __forceinline__ uint32_t res_rule4(uint32_t hw, uint32_t lw, const Re
     return o[0] | (o[1] << 8) | (o[2] << 16) | (o[3] << 24);
 }
 
-// A speculative pair's guess and its update, for slot words [0] the last bit width, [5] the one
-// before it, [6] a 2-bit chooser between "the last" and "the one before" (a layer whose maximum
-// sits at a power of two flips back and forth; as a branch predictor's chooser).  The bit widths
-// are kept on the scale of the layer's input: K = bw + escale, escale = the input's exponent (+ the
-// weight's), encoded as K + 1 + SPEC_K0 (0: none).  The int8 rule keeps every tensor's maximum in
-// [64, 127], so when an upstream layer's bit width crosses a power of two its output exponent moves
-// by one and its int8 values halve or double -- and every downstream layer's accumulator bit width
-// moves by one with them while K holds: the guess bw = K - escale follows the flip (a hint kept as
-// the bare bw missed in every layer below the one that flipped, ~50 % of the ResNet-18 pairs in
-// profiles/r06_resnet18_bench.json).  pick: the guess (bw + 1, 0: none); learn: called by one thread
-// of the pair's second launch with the true bw.
+// A speculative pair's guess and its update.  Slot words: [0] / [24] the guess for the next pair in
+// two forms (below), [5] a 2-bit chooser between them, [6] bit widths recorded, [8, 16) / [16, 24)
+// the last SPEC_HIST bit widths in the two forms (rings).  The forms: on the scale of the layer's
+// input, K = bw + escale with escale = the input's exponent + the weight's, and bare; every value
+// stored as value + 1 + SPEC_K0 (0: none).  The int8 rule keeps every tensor's maximum in [64, 127],
+// so when an upstream layer's bit width crosses a power of two its output exponent moves by one and
+// its int8 values halve or double: a layer whose accumulators follow its input keeps K while its bw
+// moves (ResNet-18 layer1.1.a's forward).  Where the layer's own maximum moves instead, the bare bw
+// holds while K moves (the deeper forwards, and the input gradients, where K drifts over the steps:
+// profiles/r06_spec_trace_resnet18.txt).  Each form's guess is the most frequent of its recorded
+// values, ties to the most recent (on the bench's steps many layers' bit widths scatter over two or
+// three values at random rather than hold or alternate, and "the last value" hits less often than
+// the mode); the chooser counts which form would have been right (a tournament predictor's chooser).
+// learn (one thread of the pair's second launch, with the true bw) keeps the rings and leaves both
+// forms' next guesses in [0] / [24], so pick (every wave of launch A) reads three words in one round
+// trip: the guess as bw + 1, 0 none.
 constexpr int SPEC_K0 = 512;
-__device__ __forceinline__ uint32_t spec_pick(const uint32_t* hint, int escale) {
-    const uint32_t h = (uint32_t)__builtin_amdgcn_readfirstlane(
-        (int)__hip_atomic_load(hint, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    const uint32_t hp = (uint32_t)__builtin_amdgcn_readfirstlane(
-        (int)__hip_atomic_load(hint + 5, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    const uint32_t ch = (uint32_t)__builtin_amdgcn_readfirstlane(
-        (int)__hip_atomic_load(hint + 6, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    const uint32_t k = ch >= 2u && hp != 0u ? hp : h;
-    if (k == 0u) return 0u;
-    const int g = (int)k - SPEC_K0 - escale;  // bw + 1
+constexpr int SPEC_HIST = 8;
+// the most frequent of a ring's values, ties to the most recent (0: none); n values recorded
+__device__ __forceinline__ uint32_t spec_mode(const uint32_t (&hv)[SPEC_HIST], uint32_t n) {
+    uint32_t best = 0u, best_score = 0u;
+#pragma unroll
+    for (int j = 0; j < SPEC_HIST; ++j) {
+        uint32_t c = 0u;
+#pragma unroll
+        for (int k = 0; k < SPEC_HIST; ++k) c += hv[k] == hv[j] ? 1u : 0u;
+        const uint32_t age = (n - 1u - (uint32_t)j) % (uint32_t)SPEC_HIST;  // 0: the most recent
+        const uint32_t score = hv[j] != 0u ? c * 16u + (15u - age) : 0u;
+        if (score > best_score) {
+            best_score = score;
+            best = hv[j];
+        }
+    }
+    return best;
+}
+// a recorded value back to a guess (bw + 1) at this pair's input scale
+__device__ __forceinline__ uint32_t spec_unscale(uint32_t v, int escale) {
+    if (v == 0u) return 0u;
+    const int g = (int)v - SPEC_K0 - escale;
     return (uint32_t)(g < 1 ? 1 : g > 32 ? 32 : g);
 }
+__device__ __forceinline__ uint32_t spec_ld(const uint32_t* p) {
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ uint32_t spec_pick(const uint32_t* hint, int escale) {
+    const uint32_t ch = spec_ld(hint + 5), vb = spec_ld(hint), vs = spec_ld(hint + 24);
+    return ch >= 2u ? spec_unscale(vs, escale) : spec_unscale(vb, 0);
+}
 __device__ __forceinline__ void spec_learn(uint32_t* hint, int bw, int escale) {
-    const uint32_t kv = (uint32_t)(bw + 1 + escale + SPEC_K0);
-    const uint32_t h = __hip_atomic_load(hint, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint32_t hp = __hip_atomic_load(hint + 5, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    uint32_t ch = __hip_atomic_load(hint + 6, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const bool last_ok = h == kv, prev_ok = hp == kv;
-    if (prev_ok && !last_ok && ch < 3u) ++ch;
-    if (last_ok && !prev_ok && ch > 0u) --ch;
-    __hip_atomic_store(hint + 6, ch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(hint + 5, h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(hint, kv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t n = spec_ld(hint + 6), vb = spec_ld(hint), vs = spec_ld(hint + 24);
+    uint32_t ch = spec_ld(hint + 5);
+    uint32_t rs[SPEC_HIST], rb[SPEC_HIST];
+#pragma unroll
+    for (int j = 0; j < SPEC_HIST; ++j) {
+        rs[j] = spec_ld(hint + 8 + j);
+        rb[j] = spec_ld(hint + 16 + j);
+    }
+    // which form's guess would have been right (the guesses launch A chose between)
+    const bool hs = spec_unscale(vs, escale) == (uint32_t)bw + 1u, hb = spec_unscale(vb, 0) == (uint32_t)bw + 1u;
+    if (hs && !hb && ch < 3u) ++ch;
+    if (hb && !hs && ch > 0u) --ch;
+    const uint32_t kb = (uint32_t)(bw + 1 + SPEC_K0), ks = kb + (uint32_t)escale;
+    const uint32_t slot = n % (uint32_t)SPEC_HIST;
+#pragma unroll
+    for (int j = 0; j < SPEC_HIST; ++j) {
+        rs[j] = (uint32_t)j == slot ? ks : rs[j];
+        rb[j] = (uint32_t)j == slot ? kb : rb[j];
+    }
+    __hip_atomic_store(hint + 8 + slot, ks, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(hint + 16 + slot, kb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(hint + 5, ch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(hint + 6, n + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(hint, spec_mode(rb, n + 1u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(hint + 24, spec_mode(rs, n + 1u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // The residual rule (niti_resnet.hip): z = hi * 2^d + (lo >> r), arithmetic shift

@@ -993,11 +993,11 @@ __device__ __forceinline__ void write_exponent(const RowConvArgs& a, uint32_t gm
 // [0] the hint (bw + 1, 0 none; written by B's block 0, read by A), [1] what A did (the hint it
 // used, bit 31 set when it stored instead; written by A's block 0, read by B), [2] redone launches,
 // [3] pairs left in store mode (read and written by B's thread 0, read by A), [4] stored pairs,
-// [5] the bit width one pair earlier (bw + 1), [6] the predictor's chooser (0..3, written by B).
+// [0], [5], [6], [8, 25) the predictor's state (spec_learn, written by B's thread 0), [7] / [25, 32)
+// the diagnostic record of the last 7 pairs (niti_model_spec_slot).
 // Every other reader of a word runs in the other launch, so no launch's blocks race on a word.
-// The guess (spec_pick / spec_learn, niti_device.hpp): a layer's bit width either holds from pair to
-// pair or, with gradients whose maximum sits at a power of two, flips back and forth; a 2-bit
-// chooser counts which of "the last bit width" and "the one before it" would have been right.
+// The guess (spec_pick / spec_learn, niti_device.hpp): the most frequent of the layer's last 8 bit
+// widths, bare or on its input's scale (forward slots), whichever has been right more often.
 // the input's scale for the hint (spec_pick): exponent in + weight scale, both settled before A;
 // forward slots only -- an input gradient's bit width follows its own value better than dy's scale
 // (tools/spec_trace.py, profiles/r06_spec_trace_resnet18.txt: K = bw + escale drifts down steadily
@@ -1036,10 +1036,10 @@ __device__ __forceinline__ bool spec_settle(const RowConvArgs& a, uint32_t& g, b
         const uint32_t cd = __hip_atomic_load(a.hint + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(a.hint + 3, changed ? a.spec_cooldown : (cd > 0u ? cd - 1u : 0u), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
-        // the last 24 pairs' record (niti_model_spec_slot): word 7 counts, 8 + (count mod 24) holds
+        // the last 7 pairs' record (niti_model_spec_slot): word 7 counts, 25 + (count mod 7) holds
         // bw | (escale + 256) << 8 | the guess A used (bw + 1) << 20
         const uint32_t hn = __hip_atomic_load(a.hint + 7, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(a.hint + 8 + hn % 24u,
+        __hip_atomic_store(a.hint + 25 + hn % 7u,
                            (uint32_t)bw | ((uint32_t)(esc + 256) << 8) | ((w1 & 0xfffu) << 20), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(a.hint + 7, hn + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

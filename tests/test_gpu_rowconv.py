@@ -76,9 +76,11 @@ def _spec_pairs(T, st, dgrad, amax, eo, launch, check):
     (launch 4 redoes); every pair's outputs are the rule's, and the slot counts the two misses."""
     off = st.spec_offset(dgrad)
     for rep in range(3):
-        if rep == 2:
-            hint = int(st.state[off].item())
-            st.state[off] = hint + 1 if hint < 20 else hint - 1
+        if rep == 2:  # both forms' next guesses one bit wide (spec_pick: words 0 / 24)
+            for j in (0, 24):
+                hint = int(st.state[off + j].item())
+                if hint != 0:
+                    st.state[off + j] = hint + 1
         amax.zero_()
         if eo is not None:
             eo.zero_()

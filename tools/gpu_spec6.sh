@@ -14,3 +14,6 @@ for net in resnet18 vgg16; do
   echo "$net $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/spec6_${net}_$TAG.log) $(grep -o '"rowconv_spec": {[^}]*}' gpurun_out/spec6_${net}_$TAG.log)"
 done
 timeout -k 10 300 python3 tools/spec_trace.py --arch resnet18 --load-plans tools/probes/plans_resnet18_r06.json > gpurun_out/spec_trace_r18_$TAG.txt 2>&1 || exit $?
+timeout -k 10 300 python3 bench.py --dp-path --cpu-sample 0 > gpurun_out/spec6_dppath_$TAG.log 2>&1 || exit $?
+echo "vgg11 dp-path $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/spec6_dppath_$TAG.log) $(grep -o '"rowconv_spec": {"redone": [0-9]*, "stored_or_alternate": [0-9]*' gpurun_out/spec6_dppath_$TAG.log)"
+timeout -k 10 300 python3 tools/spec_trace.py --arch vgg16 --load-plans tools/probes/plans_vgg16_r06.json > gpurun_out/spec_trace_v16_$TAG.txt 2>&1 || exit $?
