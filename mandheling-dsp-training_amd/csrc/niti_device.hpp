@@ -159,28 +159,11 @@ __device__ __forceinline__ uint32_t res_rule4(uint32_t hw, uint32_t lw, const Re
 // values, ties to the most recent (on the bench's steps many layers' bit widths scatter over two or
 // three values at random rather than hold or alternate, and "the last value" hits less often than
 // the mode); the chooser counts which form would have been right (a tournament predictor's chooser).
-// learn (one thread of the pair's second launch, with the true bw) keeps the rings and leaves both
+// learn (one wave of the pair's second launch, with the true bw) keeps the rings and leaves both
 // forms' next guesses in [0] / [24], so pick (every wave of launch A) reads three words in one round
 // trip: the guess as bw + 1, 0 none.
 constexpr int SPEC_K0 = 512;
 constexpr int SPEC_HIST = 8;
-// the most frequent of a ring's values, ties to the most recent (0: none); n values recorded
-__device__ __forceinline__ uint32_t spec_mode(const uint32_t (&hv)[SPEC_HIST], uint32_t n) {
-    uint32_t best = 0u, best_score = 0u;
-#pragma unroll
-    for (int j = 0; j < SPEC_HIST; ++j) {
-        uint32_t c = 0u;
-#pragma unroll
-        for (int k = 0; k < SPEC_HIST; ++k) c += hv[k] == hv[j] ? 1u : 0u;
-        const uint32_t age = (n - 1u - (uint32_t)j) % (uint32_t)SPEC_HIST;  // 0: the most recent
-        const uint32_t score = hv[j] != 0u ? c * 16u + (15u - age) : 0u;
-        if (score > best_score) {
-            best_score = score;
-            best = hv[j];
-        }
-    }
-    return best;
-}
 // a recorded value back to a guess (bw + 1) at this pair's input scale
 __device__ __forceinline__ uint32_t spec_unscale(uint32_t v, int escale) {
     if (v == 0u) return 0u;
@@ -194,32 +177,59 @@ __device__ __forceinline__ uint32_t spec_pick(const uint32_t* hint, int escale) 
     const uint32_t ch = spec_ld(hint + 5), vb = spec_ld(hint), vs = spec_ld(hint + 24);
     return ch >= 2u ? spec_unscale(vs, escale) : spec_unscale(vb, 0);
 }
-__device__ __forceinline__ void spec_learn(uint32_t* hint, int bw, int escale) {
+// the same with the input's scale read here (exponent in + weight scale, when on): every load is
+// issued before any is used -- one memory round trip at the head of launch A, not two; *f gets
+// slot word [3] (the row kernels' store flag) from the same trip
+__device__ __forceinline__ uint32_t spec_pick_e(const uint32_t* hint, const int8_t* e_in, const int8_t* ws, bool on,
+                                                uint32_t* f) {
+    const uint32_t ch = __hip_atomic_load(hint + 5, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t vb = __hip_atomic_load(hint, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t vs = __hip_atomic_load(hint + 24, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t w3 = __hip_atomic_load(hint + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int8_t zero = 0;
+    const int ei = *(on && e_in ? e_in : &zero), wv = *(on && ws ? ws : &zero);
+    *f = (uint32_t)__builtin_amdgcn_readfirstlane((int)w3);
+    const int esc = __builtin_amdgcn_readfirstlane(ei + wv);
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)ch) >= 2u
+               ? spec_unscale((uint32_t)__builtin_amdgcn_readfirstlane((int)vs), esc)
+               : spec_unscale((uint32_t)__builtin_amdgcn_readfirstlane((int)vb), 0);
+}
+// learn, by one whole wave (the first of the second launch's first block): lane j < SPEC_HIST
+// takes ring entry j, the counts and the mode's pick are lane-parallel (a thread-serial form
+// counted 64 pairs per ring and sat on that block's path, ~1 us per launch B)
+__device__ __forceinline__ uint32_t spec_mode_wave(uint32_t v, uint32_t n, int lane) {
+    uint32_t c = 0u;
+#pragma unroll
+    for (int k = 0; k < SPEC_HIST; ++k) c += (uint32_t)__builtin_amdgcn_readlane((int)v, k) == v ? 1u : 0u;
+    const uint32_t age = (n - 1u - (uint32_t)lane) % (uint32_t)SPEC_HIST;  // 0: the most recent
+    const uint32_t score = lane < SPEC_HIST && v != 0u ? ((c * 16u + (15u - age)) << 16) | (v & 0xffffu) : 0u;
+    return wave_max(score) & 0xffffu;
+}
+__device__ __forceinline__ void spec_learn(uint32_t* hint, int bw, int escale, int lane) {
     const uint32_t n = spec_ld(hint + 6), vb = spec_ld(hint), vs = spec_ld(hint + 24);
     uint32_t ch = spec_ld(hint + 5);
-    uint32_t rs[SPEC_HIST], rb[SPEC_HIST];
-#pragma unroll
-    for (int j = 0; j < SPEC_HIST; ++j) {
-        rs[j] = spec_ld(hint + 8 + j);
-        rb[j] = spec_ld(hint + 16 + j);
-    }
+    const bool in = lane < SPEC_HIST;
+    uint32_t rs = in ? __hip_atomic_load(hint + 8 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+    uint32_t rb = in ? __hip_atomic_load(hint + 16 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
     // which form's guess would have been right (the guesses launch A chose between)
     const bool hs = spec_unscale(vs, escale) == (uint32_t)bw + 1u, hb = spec_unscale(vb, 0) == (uint32_t)bw + 1u;
     if (hs && !hb && ch < 3u) ++ch;
     if (hb && !hs && ch > 0u) --ch;
     const uint32_t kb = (uint32_t)(bw + 1 + SPEC_K0), ks = kb + (uint32_t)escale;
     const uint32_t slot = n % (uint32_t)SPEC_HIST;
-#pragma unroll
-    for (int j = 0; j < SPEC_HIST; ++j) {
-        rs[j] = (uint32_t)j == slot ? ks : rs[j];
-        rb[j] = (uint32_t)j == slot ? kb : rb[j];
+    if ((uint32_t)lane == slot) {
+        rs = ks;
+        rb = kb;
     }
-    __hip_atomic_store(hint + 8 + slot, ks, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(hint + 16 + slot, kb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(hint + 5, ch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(hint + 6, n + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(hint, spec_mode(rb, n + 1u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(hint + 24, spec_mode(rs, n + 1u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t ms = spec_mode_wave(rs, n + 1u, lane), mb = spec_mode_wave(rb, n + 1u, lane);
+    if (lane == 0) {
+        __hip_atomic_store(hint + 8 + slot, ks, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(hint + 16 + slot, kb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(hint + 5, ch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(hint + 6, n + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(hint, mb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(hint + 24, ms, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
 }
 
 // The residual rule (niti_resnet.hip): z = hi * 2^d + (lo >> r), arithmetic shift

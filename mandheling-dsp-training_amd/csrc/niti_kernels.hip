@@ -274,13 +274,13 @@ __device__ __forceinline__ int gemm_spec_settle(const Epi& epi) {
     const bool alts = (h1 >> 31) != 0u;  // A wrote the alternates
     const int esc = gemm_spec_escale(epi);  // (before the exponent write: exp_out may alias exp_in)
     const int act = bw == used ? 0 : !alts ? -1 : (bw == used - 1 && used >= 1) ? 1 : bw == used + 1 ? 2 : -1;
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 64) spec_learn(epi.hint, bw, esc, threadIdx.x);
     if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
         if (act >= 0 && epi.exp_out != nullptr) {  // (a redo writes it in its epilogue)
             const int shift = bw - 7;
             const int inc = shift > 1 ? shift : (shift == 1 ? 2 : 0);
             *epi.exp_out = (int8_t)((epi.exp_in ? (int)*epi.exp_in : 0) + (epi.wscale ? (int)*epi.wscale : 0) + inc);
         }
-        spec_learn(epi.hint, bw, esc);
         if (act < 0) __hip_atomic_fetch_add(epi.hint + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (act > 0) __hip_atomic_fetch_add(epi.hint + 3, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         // the alternates' window: a miss opens it for the next GEMM_SPEC_ALT_PAIRS pairs, a hit
@@ -353,7 +353,8 @@ __device__ __forceinline__ void gemm_epilogue(v16i (&acc)[TM][TN], int r0, int c
         if (fused) {
             bw = fused_bw;
         } else if (spec_a) {
-            const uint32_t h = spec_pick(epi.hint, gemm_spec_escale(epi));  // bw + 1 on the input's scale
+            uint32_t f = 0;
+            const uint32_t h = spec_pick_e(epi.hint, epi.exp_in, epi.wscale, epi.hint_scale != 0, &f);  // bw + 1
             bw = (int)h - 1;  // no hint yet: 0 (B redoes unless the max is 0)
             if (h != 0u) bw += epi.spec_bias;
             if (bw < 0) bw = 0;
@@ -3520,8 +3521,8 @@ __global__ void __launch_bounds__(256) residual_requant_kernel(const int8_t* __r
         if (spec == 2) {  // launch B: A's output stands unless the (all-reduced) range differs
             const int used = __builtin_amdgcn_readfirstlane(
                                  (int)__hip_atomic_load(hint + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) - 1;
+            if (blockIdx.x == 0 && threadIdx.x < 64) spec_learn(hint, bw, relu ? (a_hi ? xa : xb) - d : 0, threadIdx.x);
             if (blockIdx.x == 0 && threadIdx.x == 0) {
-                spec_learn(hint, bw, relu ? (a_hi ? xa : xb) - d : 0);
                 if (bw != used) __hip_atomic_fetch_add(hint + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 const int shift = bw - 7;
                 const int e_z = (a_hi ? xa : xb) - d;

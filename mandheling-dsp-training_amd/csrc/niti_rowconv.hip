@@ -993,7 +993,7 @@ __device__ __forceinline__ void write_exponent(const RowConvArgs& a, uint32_t gm
 // [0] the hint (bw + 1, 0 none; written by B's block 0, read by A), [1] what A did (the hint it
 // used, bit 31 set when it stored instead; written by A's block 0, read by B), [2] redone launches,
 // [3] pairs left in store mode (read and written by B's thread 0, read by A), [4] stored pairs,
-// [0], [5], [6], [8, 25) the predictor's state (spec_learn, written by B's thread 0), [7] / [25, 32)
+// [0], [5], [6], [8, 25) the predictor's state (spec_learn, written by B's first wave), [7] / [25, 32)
 // the diagnostic record of the last 7 pairs (niti_model_spec_slot).
 // Every other reader of a word runs in the other launch, so no launch's blocks race on a word.
 // The guess (spec_pick / spec_learn, niti_device.hpp): the most frequent of the layer's last 8 bit
@@ -1008,45 +1008,59 @@ __device__ __forceinline__ int spec_escale(const RowConvArgs& a) {
 }
 constexpr uint32_t SPEC_COOLDOWN = 8;  // the default of spec_cooldown() (NITI_SPEC_COOLDOWN overrides; profiles/r05_spec_cooldown_ab.txt)
 __device__ __forceinline__ int spec_guess(const RowConvArgs& a, bool can_store, bool& store) {
-    const uint32_t f = __hip_atomic_load(a.hint + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint32_t gh = spec_pick(a.hint, spec_escale(a));  // the guess, as bw + 1 (0: none)
-    store = can_store && a.acc_store != nullptr && __builtin_amdgcn_readfirstlane((int)f) != 0;
+    uint32_t f = 0;
+    const uint32_t gh = spec_pick_e(a.hint, a.exp_in, a.wscale, a.hint_scale != 0, &f);  // the guess, bw + 1 (0: none)
+    store = can_store && a.acc_store != nullptr && f != 0;
     if (blockIdx.x == 0 && threadIdx.x == 0)
         __hip_atomic_store(a.hint + 1, gh | (store ? 0x80000000u : 0u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return (int)gh - 1;
 }
 
 // launch B: g = the rule's max word; returns whether this launch has work (A stored the
-// accumulators -- `stored` -- or guessed a different bit width), else every block returns; block 0
-// writes the exponent, the next hint and store flag, and the counts
-__device__ __forceinline__ bool spec_settle(const RowConvArgs& a, uint32_t& g, bool& stored) {
+// accumulators -- `stored` -- or guessed a different bit width), else every block returns.  The
+// bookkeeping (exponent, the next guess, store flag, counts) is spec_book's, by one block after its
+// work: done up front it held the first block's work back by its memory round trips.
+struct SpecBook {
+    uint32_t g, w1;
+    int bw, esc;
+    bool stored, changed;
+};
+__device__ __forceinline__ bool spec_settle(const RowConvArgs& a, uint32_t& g, bool& stored, SpecBook& bk) {
     g = read_max(a.amax);
-    const int bw = bitwidth_rc(g);
-    const int esc = spec_escale(a);  // before write_exponent (exp_out may alias a later exp_in)
-    const uint32_t w1 = (uint32_t)__builtin_amdgcn_readfirstlane(
+    bk.g = g;
+    bk.bw = bitwidth_rc(g);
+    bk.esc = spec_escale(a);  // before the exponent write (exp_out may alias a later exp_in)
+    bk.w1 = (uint32_t)__builtin_amdgcn_readfirstlane(
         (int)__hip_atomic_load(a.hint + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    stored = (w1 >> 31) != 0;
-    const bool changed = bw != (int)(w1 & 0x7fffffffu) - 1;
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        write_exponent(a, g);
-        spec_learn(a.hint, bw, esc);  // the next guess (spec_pick)
+    stored = (bk.w1 >> 31) != 0;
+    bk.stored = stored;
+    bk.changed = bk.bw != (int)(bk.w1 & 0x7fffffffu) - 1;
+    return stored || bk.changed;
+}
+// called by every thread of every block of launch B once its work is done (or at once on a hit):
+// the last block (a persistent grid's fewest units) writes the exponent, the next guess, the store
+// flag and the counts
+__device__ __forceinline__ void spec_book(const RowConvArgs& a, const SpecBook& bk) {
+    if (blockIdx.x != gridDim.x - 1) return;
+    if (threadIdx.x < 64) spec_learn(a.hint, bk.bw, bk.esc, threadIdx.x);  // the next guess (spec_pick)
+    if (threadIdx.x == 0) {
+        write_exponent(a, bk.g);
         // store mode for the next SPEC_COOLDOWN pairs after a change (a layer whose bit width flips
-        // from step to step, gradients near a power of two, stays there; block 0 of B is the only
+        // from step to step, gradients near a power of two, stays there; this block of B is the only
         // reader-writer of this word within a launch)
         const uint32_t cd = __hip_atomic_load(a.hint + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(a.hint + 3, changed ? a.spec_cooldown : (cd > 0u ? cd - 1u : 0u), __ATOMIC_RELAXED,
+        const uint32_t hn = __hip_atomic_load(a.hint + 7, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(a.hint + 3, bk.changed ? a.spec_cooldown : (cd > 0u ? cd - 1u : 0u), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
         // the last 7 pairs' record (niti_model_spec_slot): word 7 counts, 25 + (count mod 7) holds
         // bw | (escale + 256) << 8 | the guess A used (bw + 1) << 20
-        const uint32_t hn = __hip_atomic_load(a.hint + 7, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(a.hint + 25 + hn % 7u,
-                           (uint32_t)bw | ((uint32_t)(esc + 256) << 8) | ((w1 & 0xfffu) << 20), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+                           (uint32_t)bk.bw | ((uint32_t)(bk.esc + 256) << 8) | ((bk.w1 & 0xfffu) << 20),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(a.hint + 7, hn + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (stored) __hip_atomic_fetch_add(a.hint + 4, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        else if (changed) __hip_atomic_fetch_add(a.hint + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (bk.stored) __hip_atomic_fetch_add(a.hint + 4, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else if (bk.changed) __hip_atomic_fetch_add(a.hint + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    return stored || changed;
 }
 
 
@@ -1345,11 +1359,15 @@ __global__ void __launch_bounds__(256, (RC_EXP & 16) ? 2 : 1) rowconv_fwd_kernel
     } else if constexpr (MODE == RC_REQUANT && W == 0) {
         uint32_t g = 0;
         bool store = false;
+        SpecBook bk{};
         if (a.spec2 == 1) {  // (the row-segment form stores no accumulators: always the guess)
             const int guess = spec_guess(a, false, store);
             g = guess <= 0 ? 0u : 1u << guess;
         } else if (a.spec2 == 2) {
-            if (!spec_settle(a, g, store)) return;
+            if (!spec_settle(a, g, store, bk)) {
+                spec_book(a, bk);
+                return;
+            }
         } else {
             g = read_max(a.amax);
             if (blockIdx.x == 0 && threadIdx.x == 0) write_exponent(a, g);
@@ -1363,6 +1381,7 @@ __global__ void __launch_bounds__(256, (RC_EXP & 16) ? 2 : 1) rowconv_fwd_kernel
             __syncthreads();
             if (threadIdx.x == 0) publish_max(a.amax, max(max(red[0], red[1]), max(red[2], red[3])));
         }
+        if (a.spec2 == 2) spec_book(a, bk);
     } else if constexpr (MODE == RC_RANGE) {
         uint32_t m = 0;
         for (int b = blockIdx.x; b < a.wgs; b += gridDim.x) {
@@ -1384,12 +1403,16 @@ __global__ void __launch_bounds__(256, (RC_EXP & 16) ? 2 : 1) rowconv_fwd_kernel
         // load: the accumulators come from acc_store (the range launch's, or a storing launch A's);
         // store: this launch A stores them instead of requantising (spec_guess)
         bool load = a.acc_store != nullptr, store = false;
+        SpecBook bk{};
         if (a.spec2 == 1) {
             const int guess = spec_guess(a, true, store);
             g = guess <= 0 ? 0u : 1u << guess;
             load = false;
         } else if (a.spec2 == 2) {
-            if (!spec_settle(a, g, load)) return;
+            if (!spec_settle(a, g, load, bk)) {
+                spec_book(a, bk);
+                return;
+            }
         } else {
             g = read_max(a.amax);
             if (blockIdx.x == 0 && threadIdx.x == 0) write_exponent(a, g);
@@ -1423,6 +1446,7 @@ __global__ void __launch_bounds__(256, (RC_EXP & 16) ? 2 : 1) rowconv_fwd_kernel
             __syncthreads();
             if (threadIdx.x == 0) publish_max(a.amax, max(max(red[0], red[1]), max(red[2], red[3])));
         }
+        if (a.spec2 == 2) spec_book(a, bk);
     }
 }
 
