@@ -485,7 +485,7 @@ int niti_model_rowconv_error(niti_model_t m);
  * gradient (niti_rows_spec_slot; synchronises) */
 int niti_model_spec_stats(niti_model_t m, uint32_t* out, int max_layers);
 /* diagnostics: the 32 words of one row-kernel layer's speculative slot (niti_rows_spec_slot), with
- * the last 7 pairs' record (bw, input scale, guess) in words 25.. (synchronises) */
+ * the last 6 pairs' record (bw, input scale, guess) in words 26.. (synchronises) */
 int niti_model_spec_slot(niti_model_t m, int layer, int dgrad, uint32_t* out32);
 /* Replay the step as a hipGraph (single device only -- with a communicator attached the step
  * always runs as direct launches).  Default 0 (direct launches: measured faster on ROCm 7.2). */

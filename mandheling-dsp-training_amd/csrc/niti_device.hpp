@@ -146,22 +146,24 @@ __device__ __forceinline__ uint32_t res_rule4(uint32_t hw, uint32_t lw, const Re
     return o[0] | (o[1] << 8) | (o[2] << 16) | (o[3] << 24);
 }
 
-// A speculative pair's guess and its update.  Slot words: [0] / [24] the guess for the next pair in
-// two forms (below), [5] a 2-bit chooser between them, [6] bit widths recorded, [8, 16) / [16, 24)
-// the last SPEC_HIST bit widths in the two forms (rings).  The forms: on the scale of the layer's
+// A speculative pair's guess and its update.  Slot words: [0] / [24] / [25] the next pair's guess
+// by three predictors (below), [5] their hit counters (3 x 4 bits), [6] bit widths recorded,
+// [8, 16) / [16, 24) the last SPEC_HIST bit widths in two forms (rings): on the scale of the layer's
 // input, K = bw + escale with escale = the input's exponent + the weight's, and bare; every value
-// stored as value + 1 + SPEC_K0 (0: none).  The int8 rule keeps every tensor's maximum in [64, 127],
-// so when an upstream layer's bit width crosses a power of two its output exponent moves by one and
-// its int8 values halve or double: a layer whose accumulators follow its input keeps K while its bw
-// moves (ResNet-18 layer1.1.a's forward).  Where the layer's own maximum moves instead, the bare bw
-// holds while K moves (the deeper forwards, and the input gradients, where K drifts over the steps:
-// profiles/r06_spec_trace_resnet18.txt).  Each form's guess is the most frequent of its recorded
-// values, ties to the most recent (on the bench's steps many layers' bit widths scatter over two or
-// three values at random rather than hold or alternate, and "the last value" hits less often than
-// the mode); the chooser counts which form would have been right (a tournament predictor's chooser).
-// learn (one wave of the pair's second launch, with the true bw) keeps the rings and leaves both
-// forms' next guesses in [0] / [24], so pick (every wave of launch A) reads three words in one round
-// trip: the guess as bw + 1, 0 none.
+// stored as value + 1 + SPEC_K0 (0: none).  The predictors:
+// - mode (bare, [0]): the most frequent of the last 8 bit widths, ties to the most recent.  On the
+//   bench's steps many layers' bit widths scatter over two or three values at random rather than
+//   hold, and "the last value" then hits less often than the mode;
+// - mode on the input's scale ([24]): the int8 rule keeps every tensor's maximum in [64, 127], so
+//   when an upstream layer's bit width crosses a power of two its output exponent moves by one and
+//   its int8 values halve or double; a layer whose accumulators follow its input keeps K while its bw
+//   moves (ResNet-18 layer1.1.a's forward; the input gradients' K drifts instead: the input-gradient
+//   slots record escale 0, profiles/r06_spec_trace_resnet18.txt);
+// - alternation ([25]): the bit width two pairs back, for a layer that flips back and forth.
+// Each predictor's counter moves +1 / -1 (0..7) on its hit / miss; pick follows the highest (ties:
+// bare mode, alternation, scaled mode).  learn (one wave of the pair's second launch, with the true
+// bw) keeps the rings and leaves the three guesses in their words, so pick (every wave of launch A)
+// reads four words in one memory round trip.  The guess is bw + 1, 0 none.
 constexpr int SPEC_K0 = 512;
 constexpr int SPEC_HIST = 8;
 // a recorded value back to a guess (bw + 1) at this pair's input scale
@@ -173,30 +175,37 @@ __device__ __forceinline__ uint32_t spec_unscale(uint32_t v, int escale) {
 __device__ __forceinline__ uint32_t spec_ld(const uint32_t* p) {
     return (uint32_t)__builtin_amdgcn_readfirstlane((int)__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
+__device__ __forceinline__ uint32_t spec_choose(uint32_t cnt, uint32_t gb, uint32_t gs, uint32_t ga) {
+    const uint32_t cb = cnt & 15u, cs = (cnt >> 4) & 15u, ca = (cnt >> 8) & 15u;
+    if (cb >= cs && cb >= ca) return gb;
+    return ca >= cs ? ga : gs;
+}
 __device__ __forceinline__ uint32_t spec_pick(const uint32_t* hint, int escale) {
-    const uint32_t ch = spec_ld(hint + 5), vb = spec_ld(hint), vs = spec_ld(hint + 24);
-    return ch >= 2u ? spec_unscale(vs, escale) : spec_unscale(vb, 0);
+    const uint32_t cnt = spec_ld(hint + 5), vb = spec_ld(hint), vs = spec_ld(hint + 24), va = spec_ld(hint + 25);
+    return spec_choose(cnt, spec_unscale(vb, 0), spec_unscale(vs, escale), spec_unscale(va, 0));
 }
 // the same with the input's scale read here (exponent in + weight scale, when on): every load is
 // issued before any is used -- one memory round trip at the head of launch A, not two; *f gets
 // slot word [3] (the row kernels' store flag) from the same trip
 __device__ __forceinline__ uint32_t spec_pick_e(const uint32_t* hint, const int8_t* e_in, const int8_t* ws, bool on,
                                                 uint32_t* f) {
-    const uint32_t ch = __hip_atomic_load(hint + 5, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t cnt = __hip_atomic_load(hint + 5, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint32_t vb = __hip_atomic_load(hint, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint32_t vs = __hip_atomic_load(hint + 24, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t va = __hip_atomic_load(hint + 25, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint32_t w3 = __hip_atomic_load(hint + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int8_t zero = 0;
     const int ei = *(on && e_in ? e_in : &zero), wv = *(on && ws ? ws : &zero);
     *f = (uint32_t)__builtin_amdgcn_readfirstlane((int)w3);
     const int esc = __builtin_amdgcn_readfirstlane(ei + wv);
-    return (uint32_t)__builtin_amdgcn_readfirstlane((int)ch) >= 2u
-               ? spec_unscale((uint32_t)__builtin_amdgcn_readfirstlane((int)vs), esc)
-               : spec_unscale((uint32_t)__builtin_amdgcn_readfirstlane((int)vb), 0);
+    return spec_choose((uint32_t)__builtin_amdgcn_readfirstlane((int)cnt),
+                       spec_unscale((uint32_t)__builtin_amdgcn_readfirstlane((int)vb), 0),
+                       spec_unscale((uint32_t)__builtin_amdgcn_readfirstlane((int)vs), esc),
+                       spec_unscale((uint32_t)__builtin_amdgcn_readfirstlane((int)va), 0));
 }
-// learn, by one whole wave (the first of the second launch's first block): lane j < SPEC_HIST
-// takes ring entry j, the counts and the mode's pick are lane-parallel (a thread-serial form
-// counted 64 pairs per ring and sat on that block's path, ~1 us per launch B)
+// learn, by one whole wave (the second launch's bookkeeping block): lane j < SPEC_HIST takes ring
+// entry j, the counts and the mode's pick are lane-parallel (a thread-serial form counted 64 pairs
+// per ring on the launch's path)
 __device__ __forceinline__ uint32_t spec_mode_wave(uint32_t v, uint32_t n, int lane) {
     uint32_t c = 0u;
 #pragma unroll
@@ -205,18 +214,23 @@ __device__ __forceinline__ uint32_t spec_mode_wave(uint32_t v, uint32_t n, int l
     const uint32_t score = lane < SPEC_HIST && v != 0u ? ((c * 16u + (15u - age)) << 16) | (v & 0xffffu) : 0u;
     return wave_max(score) & 0xffffu;
 }
+__device__ __forceinline__ uint32_t spec_count(uint32_t c, bool hit) {
+    return hit ? (c < 7u ? c + 1u : 7u) : (c > 0u ? c - 1u : 0u);
+}
 __device__ __forceinline__ void spec_learn(uint32_t* hint, int bw, int escale, int lane) {
-    const uint32_t n = spec_ld(hint + 6), vb = spec_ld(hint), vs = spec_ld(hint + 24);
-    uint32_t ch = spec_ld(hint + 5);
+    const uint32_t n = spec_ld(hint + 6), vb = spec_ld(hint), vs = spec_ld(hint + 24), va = spec_ld(hint + 25);
+    const uint32_t cnt = spec_ld(hint + 5);
     const bool in = lane < SPEC_HIST;
     uint32_t rs = in ? __hip_atomic_load(hint + 8 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
     uint32_t rb = in ? __hip_atomic_load(hint + 16 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-    // which form's guess would have been right (the guesses launch A chose between)
-    const bool hs = spec_unscale(vs, escale) == (uint32_t)bw + 1u, hb = spec_unscale(vb, 0) == (uint32_t)bw + 1u;
-    if (hs && !hb && ch < 3u) ++ch;
-    if (hb && !hs && ch > 0u) --ch;
+    const uint32_t t = (uint32_t)bw + 1u;
+    const uint32_t cnt2 = spec_count(cnt & 15u, spec_unscale(vb, 0) == t) |
+                          (spec_count((cnt >> 4) & 15u, spec_unscale(vs, escale) == t) << 4) |
+                          (spec_count((cnt >> 8) & 15u, spec_unscale(va, 0) == t) << 8);
     const uint32_t kb = (uint32_t)(bw + 1 + SPEC_K0), ks = kb + (uint32_t)escale;
     const uint32_t slot = n % (uint32_t)SPEC_HIST;
+    // the alternation guess for the next pair: this pair's predecessor (two pairs back from it)
+    const uint32_t prev = n > 0u ? (uint32_t)__builtin_amdgcn_readlane((int)rb, (int)((n - 1u) % (uint32_t)SPEC_HIST)) : 0u;
     if ((uint32_t)lane == slot) {
         rs = ks;
         rb = kb;
@@ -225,10 +239,11 @@ __device__ __forceinline__ void spec_learn(uint32_t* hint, int bw, int escale, i
     if (lane == 0) {
         __hip_atomic_store(hint + 8 + slot, ks, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(hint + 16 + slot, kb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(hint + 5, ch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(hint + 5, cnt2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(hint + 6, n + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(hint, mb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(hint + 24, ms, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(hint + 25, prev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 

@@ -993,11 +993,12 @@ __device__ __forceinline__ void write_exponent(const RowConvArgs& a, uint32_t gm
 // [0] the hint (bw + 1, 0 none; written by B's block 0, read by A), [1] what A did (the hint it
 // used, bit 31 set when it stored instead; written by A's block 0, read by B), [2] redone launches,
 // [3] pairs left in store mode (read and written by B's thread 0, read by A), [4] stored pairs,
-// [0], [5], [6], [8, 25) the predictor's state (spec_learn, written by B's first wave), [7] / [25, 32)
-// the diagnostic record of the last 7 pairs (niti_model_spec_slot).
+// [0], [5], [6], [8, 26) the predictor's state (spec_learn, written by B's bookkeeping wave), [7] /
+// [26, 32) the diagnostic record of the last 6 pairs (niti_model_spec_slot).
 // Every other reader of a word runs in the other launch, so no launch's blocks race on a word.
-// The guess (spec_pick / spec_learn, niti_device.hpp): the most frequent of the layer's last 8 bit
-// widths, bare or on its input's scale (forward slots), whichever has been right more often.
+// The guess (spec_pick / spec_learn, niti_device.hpp): of three predictors -- the most frequent of
+// the layer's last 8 bit widths, the same on its input's scale (forward slots), the bit width two
+// pairs back -- the one that has been right most often lately.
 // the input's scale for the hint (spec_pick): exponent in + weight scale, both settled before A;
 // forward slots only -- an input gradient's bit width follows its own value better than dy's scale
 // (tools/spec_trace.py, profiles/r06_spec_trace_resnet18.txt: K = bw + escale drifts down steadily
@@ -1022,14 +1023,15 @@ __device__ __forceinline__ int spec_guess(const RowConvArgs& a, bool can_store, 
 // work: done up front it held the first block's work back by its memory round trips.
 struct SpecBook {
     uint32_t g, w1;
-    int bw, esc;
+    int bw, esc, eiw;  // eiw: exponent in + weight scale (the exponent's base)
     bool stored, changed;
 };
 __device__ __forceinline__ bool spec_settle(const RowConvArgs& a, uint32_t& g, bool& stored, SpecBook& bk) {
     g = read_max(a.amax);
     bk.g = g;
     bk.bw = bitwidth_rc(g);
-    bk.esc = spec_escale(a);  // before the exponent write (exp_out may alias a later exp_in)
+    bk.eiw = __builtin_amdgcn_readfirstlane((a.exp_in ? (int)*a.exp_in : 0) + (a.wscale ? (int)*a.wscale : 0));
+    bk.esc = a.hint_scale ? bk.eiw : 0;  // read before the exponent write (exp_out may alias a later exp_in)
     bk.w1 = (uint32_t)__builtin_amdgcn_readfirstlane(
         (int)__hip_atomic_load(a.hint + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     stored = (bk.w1 >> 31) != 0;
@@ -1041,20 +1043,24 @@ __device__ __forceinline__ bool spec_settle(const RowConvArgs& a, uint32_t& g, b
 // the last block (a persistent grid's fewest units) writes the exponent, the next guess, the store
 // flag and the counts
 __device__ __forceinline__ void spec_book(const RowConvArgs& a, const SpecBook& bk) {
-    if (blockIdx.x != gridDim.x - 1) return;
-    if (threadIdx.x < 64) spec_learn(a.hint, bk.bw, bk.esc, threadIdx.x);  // the next guess (spec_pick)
+    if (blockIdx.x != gridDim.x - 1 || threadIdx.x >= 64) return;
+    // (these loads issue with spec_learn's: one memory round trip for the whole bookkeeping)
+    const uint32_t cd = __hip_atomic_load(a.hint + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t hn = __hip_atomic_load(a.hint + 7, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    spec_learn(a.hint, bk.bw, bk.esc, threadIdx.x);  // the next guess (spec_pick)
     if (threadIdx.x == 0) {
-        write_exponent(a, bk.g);
+        if (a.exp_out != nullptr) {  // write_exponent on the base read up front
+            const int shift = bitwidth_rc(bk.g) - 7;
+            *a.exp_out = (int8_t)(bk.eiw + (shift > 1 ? shift : (shift == 1 ? 2 : 0)));
+        }
         // store mode for the next SPEC_COOLDOWN pairs after a change (a layer whose bit width flips
         // from step to step, gradients near a power of two, stays there; this block of B is the only
         // reader-writer of this word within a launch)
-        const uint32_t cd = __hip_atomic_load(a.hint + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint32_t hn = __hip_atomic_load(a.hint + 7, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(a.hint + 3, bk.changed ? a.spec_cooldown : (cd > 0u ? cd - 1u : 0u), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
-        // the last 7 pairs' record (niti_model_spec_slot): word 7 counts, 25 + (count mod 7) holds
+        // the last 6 pairs' record (niti_model_spec_slot): word 7 counts, 26 + (count mod 6) holds
         // bw | (escale + 256) << 8 | the guess A used (bw + 1) << 20
-        __hip_atomic_store(a.hint + 25 + hn % 7u,
+        __hip_atomic_store(a.hint + 26 + hn % 6u,
                            (uint32_t)bk.bw | ((uint32_t)(bk.esc + 256) << 8) | ((bk.w1 & 0xfffu) << 20),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(a.hint + 7, hn + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1800,6 +1806,11 @@ void rowconv_speculate(int mode) { g_rc_spec = mode; }
 uint32_t* rowconv_spec_slot(uint32_t* bar, bool dg) { return bar + (16 + (dg ? 1 : 0)) * BAR_LINE; }
 // pairs a layer stays in store mode after its bit width changed (A/B knob NITI_SPEC_COOLDOWN; 0 never
 // stores: a miss then redoes the GEMM instead of reading back stored accumulators)
+// NITI_SPEC_SCALE=0: the forward slots' guesses bare too (an A/B switch for the scaled form)
+static bool spec_scale_on() {
+    static const bool v = getenv("NITI_SPEC_SCALE") ? atoi(getenv("NITI_SPEC_SCALE")) != 0 : true;
+    return v;
+}
 static uint32_t spec_cooldown() {
     static const int v = getenv("NITI_SPEC_COOLDOWN") ? atoi(getenv("NITI_SPEC_COOLDOWN")) : (int)SPEC_COOLDOWN;
     return v < 0 ? 0u : (uint32_t)v;
@@ -1923,7 +1934,7 @@ hipError_t rowconv_fwd(const ConvGeom& g, const int8_t* x_c32, const int8_t* wf,
     // the hint slot (the speculative pair's, and the fused mode's speculative epilogue): forward or
     // input gradient, by the operands or the caller's dgrad_slot, so the two directions never share it
     a.hint = (spec || mode == RC_FUSED) && bar != nullptr ? bar + (16 + (dg || o.dgrad_slot ? 1 : 0)) * BAR_LINE : nullptr;
-    a.hint_scale = dg || o.dgrad_slot ? 0 : 1;
+    a.hint_scale = dg || o.dgrad_slot || !spec_scale_on() ? 0 : 1;
     if (o.p16 != nullptr && (!dg || !rowconv_p16_ok(g, o.pool_dx != nullptr))) return hipErrorInvalidValue;
     if (o.pool_out != nullptr && (R % 2 != 0 || g.h % 2 != 0)) return hipErrorInvalidValue;
     if (mode == RC_FUSED) {
@@ -2088,7 +2099,7 @@ hipError_t rowconv_fc(int n, int K, int rows, const int8_t* x, int xld, const in
     // the hint slot (the speculative pair's, and the fused mode's speculative epilogue): forward or
     // input gradient, by the operands or the caller's dgrad_slot, so the two directions never share it
     a.hint = (spec || mode == RC_FUSED) && bar != nullptr ? bar + (16 + (dg || o.dgrad_slot ? 1 : 0)) * BAR_LINE : nullptr;
-    a.hint_scale = dg || o.dgrad_slot ? 0 : 1;
+    a.hint_scale = dg || o.dgrad_slot || !spec_scale_on() ? 0 : 1;
     if (o.p16 != nullptr && (o.pool_dx == nullptr || a.p16_pixels % 16 != 0)) return hipErrorInvalidValue;
     if (o.next != nullptr && a.cop % 32 != 0) return hipErrorInvalidValue;
     if (mode == RC_FUSED) {

@@ -76,8 +76,8 @@ def _spec_pairs(T, st, dgrad, amax, eo, launch, check):
     (launch 4 redoes); every pair's outputs are the rule's, and the slot counts the two misses."""
     off = st.spec_offset(dgrad)
     for rep in range(3):
-        if rep == 2:  # both forms' next guesses one bit wide (spec_pick: words 0 / 24)
-            for j in (0, 24):
+        if rep == 2:  # every predictor's next guess one bit wide (spec_pick: words 0 / 24 / 25)
+            for j in (0, 24, 25):
                 hint = int(st.state[off + j].item())
                 if hint != 0:
                     st.state[off + j] = hint + 1

@@ -2,7 +2,7 @@
 
 Builds the bench's model (synthetic weights seed 17, one fixed batch of random uint8 images and
 labels, keep_grads(0), the given plan set), runs --steps steps and prints, per layer and direction,
-the last 7 pairs' (bit width, input scale = exponent in + weight scale, guess A used) from the slot
+the last 6 pairs' (bit width, input scale = exponent in + weight scale, guess A used) from the slot
 record (niti_model_spec_slot) -- what the hint predictor sees.
 
   python tools/spec_trace.py --arch resnet18 --load-plans tools/probes/plans_resnet18_r06.json
@@ -62,12 +62,12 @@ def main():
             n = w[7]
             if n == 0:
                 continue
-            recs = [w[25 + (j % 7)] for j in range(max(0, n - 7), n)]
+            recs = [w[26 + (j % 6)] for j in range(max(0, n - 6), n)]
             bws = [r & 0xFF for r in recs]
             esc = [((r >> 8) & 0xFFF) - 256 for r in recs]
             used = [(r >> 20) - 1 for r in recs]
             miss = sum(1 for b, u in zip(bws, used) if b != u)
-            print(f"layer {i:2d} {'dgrad' if d else 'fwd  '} pairs {n:3d} redone {w[2]:3d} last7 miss {miss:2d}")
+            print(f"layer {i:2d} {'dgrad' if d else 'fwd  '} pairs {n:3d} redone {w[2]:3d} last6 miss {miss:2d}")
             print("   bw    ", " ".join(f"{b:3d}" for b in bws))
             print("   escale", " ".join(f"{e:3d}" for e in esc))
             print("   K      ", " ".join(f"{b + e:3d}" for b, e in zip(bws, esc)))
