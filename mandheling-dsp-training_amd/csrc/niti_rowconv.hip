@@ -1019,8 +1019,8 @@ __device__ __forceinline__ int spec_guess(const RowConvArgs& a, bool can_store, 
 
 // launch B: g = the rule's max word; returns whether this launch has work (A stored the
 // accumulators -- `stored` -- or guessed a different bit width), else every block returns.  The
-// bookkeeping (exponent, the next guess, store flag, counts) is spec_book's, by one block after its
-// work: done up front it held the first block's work back by its memory round trips.
+// bookkeeping (exponent, the next guess, store flag, counts) is spec_book's, by one block, up front
+// (after its work it delayed the launch's end by its memory round trips and stores).
 struct SpecBook {
     uint32_t g, w1;
     int bw, esc, eiw;  // eiw: exponent in + weight scale (the exponent's base)
@@ -1039,9 +1039,8 @@ __device__ __forceinline__ bool spec_settle(const RowConvArgs& a, uint32_t& g, b
     bk.changed = bk.bw != (int)(bk.w1 & 0x7fffffffu) - 1;
     return stored || bk.changed;
 }
-// called by every thread of every block of launch B once its work is done (or at once on a hit):
-// the last block (a persistent grid's fewest units) writes the exponent, the next guess, the store
-// flag and the counts
+// called by every thread of every block of launch B after spec_settle: the last block (a persistent
+// grid's fewest units) writes the exponent, the next guess, the store flag and the counts
 __device__ __forceinline__ void spec_book(const RowConvArgs& a, const SpecBook& bk) {
     if (blockIdx.x != gridDim.x - 1 || threadIdx.x >= 64) return;
     // (these loads issue with spec_learn's: one memory round trip for the whole bookkeeping)
@@ -1370,10 +1369,9 @@ __global__ void __launch_bounds__(256, (RC_EXP & 16) ? 2 : 1) rowconv_fwd_kernel
             const int guess = spec_guess(a, false, store);
             g = guess <= 0 ? 0u : 1u << guess;
         } else if (a.spec2 == 2) {
-            if (!spec_settle(a, g, store, bk)) {
-                spec_book(a, bk);
-                return;
-            }
+            const bool work = spec_settle(a, g, store, bk);
+            spec_book(a, bk);
+            if (!work) return;
         } else {
             g = read_max(a.amax);
             if (blockIdx.x == 0 && threadIdx.x == 0) write_exponent(a, g);
@@ -1387,7 +1385,6 @@ __global__ void __launch_bounds__(256, (RC_EXP & 16) ? 2 : 1) rowconv_fwd_kernel
             __syncthreads();
             if (threadIdx.x == 0) publish_max(a.amax, max(max(red[0], red[1]), max(red[2], red[3])));
         }
-        if (a.spec2 == 2) spec_book(a, bk);
     } else if constexpr (MODE == RC_RANGE) {
         uint32_t m = 0;
         for (int b = blockIdx.x; b < a.wgs; b += gridDim.x) {
@@ -1415,10 +1412,9 @@ __global__ void __launch_bounds__(256, (RC_EXP & 16) ? 2 : 1) rowconv_fwd_kernel
             g = guess <= 0 ? 0u : 1u << guess;
             load = false;
         } else if (a.spec2 == 2) {
-            if (!spec_settle(a, g, load, bk)) {
-                spec_book(a, bk);
-                return;
-            }
+            const bool work = spec_settle(a, g, load, bk);
+            spec_book(a, bk);
+            if (!work) return;
         } else {
             g = read_max(a.amax);
             if (blockIdx.x == 0 && threadIdx.x == 0) write_exponent(a, g);
@@ -1452,7 +1448,6 @@ __global__ void __launch_bounds__(256, (RC_EXP & 16) ? 2 : 1) rowconv_fwd_kernel
             __syncthreads();
             if (threadIdx.x == 0) publish_max(a.amax, max(max(red[0], red[1]), max(red[2], red[3])));
         }
-        if (a.spec2 == 2) spec_book(a, bk);
     }
 }
 
